@@ -1,0 +1,372 @@
+"""Column storage for the row-sharded DataFrame.
+
+Each rank holds only its local rows ("partition").  Numeric and vector data live on
+the session device (HBM on MI355X) as torch tensors; strings and token arrays live on
+the host (object arrays) and are moved to the device only as offsets+bytes by the ops
+that need them (HashingTF).  Untouched columns are shared between DataFrames
+(``withColumn``/``select`` never copy), which replaces Spark's lazy lineage for the
+purposes of the widgets (SURVEY §7.2 decision 2).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import types as T
+
+
+class Column:
+    dtype: T.DataType
+
+    def __len__(self) -> int:
+        raise NotImplementedError
+
+    @property
+    def n(self) -> int:
+        return len(self)
+
+    def take(self, idx: torch.Tensor) -> "Column":
+        raise NotImplementedError
+
+    def slice(self, start: int, end: int) -> "Column":
+        return self.take(torch.arange(start, end, dtype=torch.int64))
+
+    def mask_select(self, mask: torch.Tensor) -> "Column":
+        return self.take(torch.nonzero(mask.cpu() if isinstance(self, HostColumn) else mask).reshape(-1))
+
+    def to_pylist(self) -> list:
+        raise NotImplementedError
+
+    def to_numpy(self):
+        raise NotImplementedError
+
+    def nbytes(self) -> int:
+        return 0
+
+    @staticmethod
+    def concat(cols: list["Column"]) -> "Column":
+        return type(cols[0]).concat(cols)
+
+
+# --------------------------------------------------------------------------- numeric
+class NumericColumn(Column):
+    """1-D numeric data; ``valid`` (bool) marks non-null rows (None = all valid)."""
+
+    def __init__(self, data: torch.Tensor, valid: torch.Tensor | None = None, dtype: T.DataType | None = None):
+        if data.dim() != 1:
+            raise ValueError("numeric column must be 1-D")
+        self.data = data
+        self.valid = valid
+        self.dtype = dtype or T.from_torch_dtype(data.dtype)
+
+    def __len__(self):
+        return int(self.data.shape[0])
+
+    def take(self, idx):
+        idx = idx.to(self.data.device)
+        return NumericColumn(self.data[idx], None if self.valid is None else self.valid[idx], self.dtype)
+
+    def mask_select(self, mask):
+        mask = mask.to(self.data.device)
+        return NumericColumn(self.data[mask], None if self.valid is None else self.valid[mask], self.dtype)
+
+    def slice(self, start, end):
+        return NumericColumn(self.data[start:end], None if self.valid is None else self.valid[start:end], self.dtype)
+
+    def null_mask(self) -> torch.Tensor:
+        """True where the value is null or NaN (Spark fillna semantics for numerics)."""
+        m = torch.zeros_like(self.data, dtype=torch.bool) if self.valid is None else ~self.valid
+        if self.data.is_floating_point():
+            m = m | torch.isnan(self.data)
+        return m
+
+    def cast(self, dt: T.DataType) -> Column:
+        dt = T.parse_type(dt)
+        if isinstance(dt, T.StringType):
+            vals = self.to_pylist()
+            return StringColumn(np.array([None if v is None else _fmt_num(v) for v in vals], dtype=object))
+        if not isinstance(dt, T.NumericType):
+            raise TypeError(f"cannot cast {self.dtype.simpleString()} to {dt.simpleString()}")
+        d = self.data
+        if d.is_floating_point() and not dt.torch_dtype.is_floating_point and dt.torch_dtype != torch.bool:
+            bad = torch.isnan(d) | torch.isinf(d)
+            out = torch.where(bad, torch.zeros_like(d), d).trunc().to(dt.torch_dtype)
+            valid = ~bad if self.valid is None else (self.valid & ~bad)
+            return NumericColumn(out, valid if bool((~valid).any()) else None, dt)
+        return NumericColumn(d.to(dt.torch_dtype), self.valid, dt)
+
+    def to_numpy(self):
+        a = self.data.detach().cpu()
+        if a.dtype == torch.bfloat16:
+            a = a.float()
+        a = a.numpy()
+        if self.valid is not None:
+            v = self.valid.cpu().numpy()
+            if not v.all():
+                if a.dtype.kind == "f":
+                    a = a.copy()
+                    a[~v] = np.nan
+                else:
+                    a = a.astype(object)
+                    a[~v] = None
+        return a
+
+    def to_pylist(self):
+        a = self.to_numpy()
+        out = a.tolist()
+        if self.valid is not None:
+            v = self.valid.cpu().numpy()
+            out = [x if ok else None for x, ok in zip(out, v)]
+        return out
+
+    def nbytes(self):
+        return self.data.element_size() * self.data.numel()
+
+    @staticmethod
+    def concat(cols):
+        data = torch.cat([c.data.to(cols[0].data.device) for c in cols])
+        if all(c.valid is None for c in cols):
+            valid = None
+        else:
+            valid = torch.cat([c.valid if c.valid is not None else torch.ones_like(c.data, dtype=torch.bool)
+                               for c in cols])
+        return NumericColumn(data, valid, cols[0].dtype)
+
+
+def _fmt_num(v):
+    if isinstance(v, float) and v.is_integer():
+        return repr(v)
+    return str(v)
+
+
+# --------------------------------------------------------------------------- vectors
+class VectorColumn(Column):
+    """Dense ML vectors: a [n, ld] device matrix, logical width ``size`` <= ld.
+
+    bf16 matrices are stored with ld padded to a multiple of 8 (16-B rows chunks for
+    the streaming kernels) and zero-filled padding.
+    """
+
+    dtype = T.VectorUDT()
+
+    def __init__(self, data: torch.Tensor, size: int | None = None):
+        if data.dim() != 2:
+            raise ValueError("vector column must be 2-D")
+        self.data = data
+        self.size = int(data.shape[1] if size is None else size)
+
+    def __len__(self):
+        return int(self.data.shape[0])
+
+    @property
+    def ld(self):
+        return int(self.data.shape[1])
+
+    def dense(self) -> torch.Tensor:
+        return self.data if self.size == self.ld else self.data[:, : self.size]
+
+    def take(self, idx):
+        return VectorColumn(self.data[idx.to(self.data.device)], self.size)
+
+    def mask_select(self, mask):
+        return VectorColumn(self.data[mask.to(self.data.device)], self.size)
+
+    def slice(self, start, end):
+        return VectorColumn(self.data[start:end], self.size)
+
+    def to_numpy(self):
+        a = self.dense().detach().cpu()
+        if a.dtype in (torch.bfloat16, torch.float16):
+            a = a.float()
+        return a.numpy().astype(np.float64)
+
+    def to_pylist(self):
+        from ..ml.linalg import DenseVector
+        return [DenseVector(r) for r in self.to_numpy()]
+
+    def nbytes(self):
+        return self.data.element_size() * self.data.numel()
+
+    @staticmethod
+    def concat(cols):
+        return VectorColumn(torch.cat([c.data.to(cols[0].data.device) for c in cols]), cols[0].size)
+
+
+class SparseVectorColumn(Column):
+    """CSR sparse ML vectors (HashingTF / CountVectorizer output)."""
+
+    dtype = T.VectorUDT()
+
+    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, values: torch.Tensor, size: int):
+        self.indptr, self.indices, self.values, self.size = indptr, indices, values, int(size)
+
+    def __len__(self):
+        return int(self.indptr.shape[0] - 1)
+
+    def to_dense(self, dtype=torch.float32) -> torch.Tensor:
+        n = len(self)
+        out = torch.zeros((n, self.size), dtype=dtype, device=self.values.device)
+        if self.values.numel():
+            counts = (self.indptr[1:] - self.indptr[:-1]).to(self.values.device)
+            rows = torch.repeat_interleave(torch.arange(n, device=self.values.device), counts)
+            out.index_put_((rows, self.indices.to(self.values.device).long()), self.values.to(dtype), accumulate=True)
+        return out
+
+    def take(self, idx):
+        idx = idx.to(self.indptr.device).long()
+        starts = self.indptr[idx]
+        lens = self.indptr[idx + 1] - starts
+        new_ptr = torch.zeros(idx.numel() + 1, dtype=torch.int64, device=self.indptr.device)
+        new_ptr[1:] = torch.cumsum(lens, 0)
+        total = int(new_ptr[-1].item()) if idx.numel() else 0
+        if total:
+            seg = torch.repeat_interleave(torch.arange(idx.numel(), device=self.indptr.device), lens)
+            pos = torch.arange(total, device=self.indptr.device) - new_ptr[:-1][seg] + starts[seg]
+            ind, val = self.indices[pos.to(self.indices.device)], self.values[pos.to(self.values.device)]
+        else:
+            ind, val = self.indices[:0], self.values[:0]
+        return SparseVectorColumn(new_ptr, ind, val, self.size)
+
+    def mask_select(self, mask):
+        return self.take(torch.nonzero(mask.to(self.indptr.device)).reshape(-1))
+
+    def to_numpy(self):
+        return self.to_dense(torch.float64).cpu().numpy()
+
+    def to_pylist(self):
+        from ..ml.linalg import SparseVector
+        ptr = self.indptr.cpu().numpy()
+        ind = self.indices.cpu().numpy()
+        val = self.values.double().cpu().numpy()
+        return [SparseVector(self.size, ind[ptr[i]:ptr[i + 1]], val[ptr[i]:ptr[i + 1]]) for i in range(len(self))]
+
+    def nbytes(self):
+        return sum(t.element_size() * t.numel() for t in (self.indptr, self.indices, self.values))
+
+    @staticmethod
+    def concat(cols):
+        ptrs, off = [], 0
+        for i, c in enumerate(cols):
+            p = c.indptr if i == 0 else c.indptr[1:]
+            ptrs.append(p + off)
+            off += int(c.indptr[-1].item())
+        return SparseVectorColumn(torch.cat(ptrs), torch.cat([c.indices for c in cols]),
+                                  torch.cat([c.values for c in cols]), cols[0].size)
+
+
+# --------------------------------------------------------------------------- host data
+class HostColumn(Column):
+    def __init__(self, values: np.ndarray):
+        if not isinstance(values, np.ndarray) or values.dtype != object:
+            arr = np.empty(len(values), dtype=object)
+            arr[:] = list(values)
+            values = arr
+        self.values = values
+
+    def __len__(self):
+        return len(self.values)
+
+    def take(self, idx):
+        return type(self)(self.values[idx.cpu().numpy()])
+
+    def mask_select(self, mask):
+        return type(self)(self.values[mask.cpu().numpy().astype(bool)])
+
+    def slice(self, start, end):
+        return type(self)(self.values[start:end])
+
+    def to_numpy(self):
+        return self.values
+
+    def to_pylist(self):
+        return self.values.tolist()
+
+    def null_mask(self) -> torch.Tensor:
+        return torch.from_numpy(np.array([v is None for v in self.values], dtype=bool))
+
+    def nbytes(self):
+        return int(sum(len(v) if isinstance(v, (str, list)) else 8 for v in self.values if v is not None))
+
+    @classmethod
+    def concat(cls, cols):
+        return cls(np.concatenate([c.values for c in cols]) if cols else np.empty(0, dtype=object))
+
+
+class StringColumn(HostColumn):
+    dtype = T.StringType()
+
+    def cast(self, dt: T.DataType) -> Column:
+        dt = T.parse_type(dt)
+        if isinstance(dt, T.StringType):
+            return self
+        if not isinstance(dt, T.NumericType):
+            raise TypeError(f"cannot cast string to {dt.simpleString()}")
+        n = len(self.values)
+        out = np.zeros(n, dtype=np.float64)
+        valid = np.zeros(n, dtype=bool)
+        for i, v in enumerate(self.values):
+            if v is None:
+                continue
+            s = str(v).strip()
+            if isinstance(dt, T.BooleanType):
+                if s.lower() in ("true", "false"):
+                    out[i], valid[i] = float(s.lower() == "true"), True
+                continue
+            try:
+                out[i], valid[i] = float(s), True
+            except ValueError:
+                pass
+        t = torch.from_numpy(out)
+        if not dt.torch_dtype.is_floating_point:
+            t = t.trunc()
+        return NumericColumn(t.to(dt.torch_dtype), None if valid.all() else torch.from_numpy(valid), dt)
+
+
+class ArrayColumn(HostColumn):
+    def __init__(self, values, elementType: T.DataType | None = None):
+        super().__init__(values)
+        self.dtype = T.ArrayType(elementType or T.StringType())
+
+    def take(self, idx):
+        return ArrayColumn(self.values[idx.cpu().numpy()], self.dtype.elementType)
+
+    def mask_select(self, mask):
+        return ArrayColumn(self.values[mask.cpu().numpy().astype(bool)], self.dtype.elementType)
+
+    def slice(self, start, end):
+        return ArrayColumn(self.values[start:end], self.dtype.elementType)
+
+    @classmethod
+    def concat(cls, cols):
+        return ArrayColumn(np.concatenate([c.values for c in cols]), cols[0].dtype.elementType)
+
+
+def from_numpy(arr: np.ndarray, device) -> Column:
+    """Column from a host numpy array (numeric -> device tensor; other -> host strings)."""
+    arr = np.asarray(arr)
+    if arr.dtype.kind in "fiub":
+        if arr.dtype.kind == "u":
+            arr = arr.astype(np.int64)
+        if arr.ndim == 2:
+            return VectorColumn(torch.from_numpy(np.ascontiguousarray(arr)).to(device))
+        return NumericColumn(torch.from_numpy(np.ascontiguousarray(arr)).to(device))
+    vals = arr.astype(object)
+    if len(vals) and all(isinstance(v, (list, tuple, np.ndarray)) or v is None for v in vals):
+        first = next((v for v in vals if v is not None), None)
+        if first is not None and len(first) and isinstance(first[0], str):
+            return ArrayColumn([None if v is None else list(v) for v in vals])
+        if first is not None:
+            mat = np.array([np.asarray(v, dtype=np.float64) for v in vals])
+            return VectorColumn(torch.from_numpy(mat).to(device))
+    out = np.empty(len(vals), dtype=object)
+    for i, v in enumerate(vals):
+        if v is None or (isinstance(v, float) and np.isnan(v)):
+            out[i] = None
+        elif hasattr(v, "toArray"):
+            out[i] = v
+        else:
+            out[i] = v if isinstance(v, str) else str(v)
+    if len(out) and any(hasattr(v, "toArray") for v in out if v is not None):
+        mat = np.array([np.asarray(v.toArray(), dtype=np.float64) for v in out])
+        return VectorColumn(torch.from_numpy(mat).to(device))
+    return StringColumn(out)

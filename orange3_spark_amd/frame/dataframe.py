@@ -1,0 +1,764 @@
+"""Row-sharded columnar DataFrame (replaces ``pyspark.sql.DataFrame``).
+
+Every rank of the session holds a contiguous block of the global rows (its
+*partition*); numeric/vector columns live in HBM.  Operations are eager; column
+buffers are shared between DataFrames until modified.  Global operations (count,
+collect/toPandas, sort, groupBy) use the session communicator (RCCL over xGMI on a
+GPU node, gloo on CPU).
+
+Reference call sites this type serves (orangecontrib/spark/...):
+  * ``df.fillna(value, subset)``      widgets/data/spark_fill.py:63
+  * ``df.sample(withReplacement, fraction, seed)``  widgets/data/spark_sample.py:70
+  * ``df.cache()``                    widgets/data/spark_df_cache.py:39, base/spark_ml_transformer.py:134
+  * ``df.withColumn('label', df[c].cast('double'))``  widgets/ml/spark_ml_dataset.py:578
+  * ``df.columns``                    base/spark_ml_transformer.py:105, widgets/ml/spark_ml_dataset.py:422
+  * ``df.toPandas()``                 widgets/data/spark_to_pandas.py:25, spark_to_orange.py:31
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+from typing import Iterable
+
+import numpy as np
+import torch
+
+from . import column as C
+from . import expr as E
+from . import types as T
+
+
+class Row(tuple):
+    """Immutable named row (``pyspark.sql.Row``-like)."""
+
+    def __new__(cls, *args, **kwargs):
+        if kwargs:
+            names = list(kwargs.keys())
+            r = tuple.__new__(cls, list(kwargs.values()))
+            r.__fields__ = names
+            return r
+        r = tuple.__new__(cls, args)
+        r.__fields__ = None
+        return r
+
+    @classmethod
+    def _make(cls, names, values):
+        r = tuple.__new__(cls, values)
+        r.__fields__ = list(names)
+        return r
+
+    def asDict(self):
+        return dict(zip(self.__fields__ or [], self))
+
+    def __getattr__(self, item):
+        if item.startswith("__"):
+            raise AttributeError(item)
+        try:
+            return self[self.__fields__.index(item)]
+        except (ValueError, AttributeError):
+            raise AttributeError(item)
+
+    def __getitem__(self, k):
+        if isinstance(k, str):
+            return tuple.__getitem__(self, self.__fields__.index(k))
+        return tuple.__getitem__(self, k)
+
+    def __repr__(self):
+        if self.__fields__:
+            return "Row(" + ", ".join(f"{k}={v!r}" for k, v in zip(self.__fields__, self)) + ")"
+        return "Row" + tuple.__repr__(self)
+
+    def __reduce__(self):
+        return (Row._make, (self.__fields__, tuple(self)))
+
+
+class StorageLevel:
+    NONE = "NONE"
+    MEMORY_ONLY = "MEMORY_ONLY"
+    MEMORY_AND_DISK = "MEMORY_AND_DISK"
+
+
+class DataFrame:
+    def __init__(self, session, cols: "OrderedDict[str, C.Column]", nrows: int | None = None):
+        self.session = session
+        self._cols: OrderedDict = OrderedDict(cols)
+        if nrows is None:
+            nrows = len(next(iter(self._cols.values()))) if self._cols else 0
+        self._n = int(nrows)
+        for k, c in self._cols.items():
+            if len(c) != self._n:
+                raise ValueError(f"column {k!r} has {len(c)} rows, expected {self._n}")
+        self._cached = False
+        self._offset = None
+        self.lineage = None  # optional SyntheticLineage (rows recomputable in-kernel)
+
+    # ------------------------------------------------------------------ basics
+    @property
+    def comm(self):
+        return self.session.comm
+
+    @property
+    def device(self):
+        return self.session.device
+
+    def __len__(self):
+        return self._n
+
+    @property
+    def columns(self) -> list[str]:
+        return list(self._cols.keys())
+
+    @property
+    def dtypes(self) -> list[tuple[str, str]]:
+        return [(k, c.dtype.simpleString()) for k, c in self._cols.items()]
+
+    @property
+    def schema(self) -> T.StructType:
+        st = T.StructType()
+        for k, c in self._cols.items():
+            md = {}
+            if isinstance(c, (C.VectorColumn, C.SparseVectorColumn)):
+                md = {"ml_attr": {"num_attrs": c.size}}
+            st.add(k, c.dtype, True, md)
+        return st
+
+    def printSchema(self):
+        print("root")
+        for k, c in self._cols.items():
+            print(f" |-- {k}: {c.dtype.simpleString()} (nullable = true)")
+
+    def _col(self, name: str) -> C.Column:
+        try:
+            return self._cols[name]
+        except KeyError:
+            for k in self._cols:
+                if k.lower() == name.lower():
+                    return self._cols[k]
+            raise KeyError(f"cannot resolve column '{name}' among {self.columns}")
+
+    def column_data(self, name: str) -> C.Column:
+        return self._col(name)
+
+    def __getitem__(self, item):
+        if isinstance(item, str):
+            self._col(item)
+            return E.col(item)
+        if isinstance(item, int):
+            return E.col(self.columns[item])
+        if isinstance(item, (list, tuple)):
+            return self.select(*item)
+        if isinstance(item, E.Expr):
+            return self.filter(item)
+        raise TypeError(item)
+
+    def __getattr__(self, name):
+        if name.startswith("_") or name in ("session", "lineage"):
+            raise AttributeError(name)
+        cols = self.__dict__.get("_cols", {})
+        if name in cols:
+            return E.col(name)
+        raise AttributeError(name)
+
+    def _new(self, cols, n=None) -> "DataFrame":
+        return DataFrame(self.session, cols, self._n if n is None else n)
+
+    def _resolve(self, c) -> tuple[str, C.Column]:
+        if isinstance(c, str):
+            if c == "*":
+                raise ValueError("'*' handled by caller")
+            return c, self._col(c)
+        if isinstance(c, E.Expr):
+            return c.name, c.eval(self)
+        raise TypeError(f"unsupported column spec {c!r}")
+
+    # ------------------------------------------------------------------ counts/offsets
+    def count(self) -> int:
+        return int(self.comm.sum_scalar(int(self._n)))
+
+    def row_offset(self) -> int:
+        """Global index of this partition's first row."""
+        if self._offset is None:
+            sizes = self.comm.all_gather_object(int(self._n))
+            self._offset = int(sum(sizes[: self.comm.rank]))
+        return self._offset
+
+    def partition_sizes(self) -> list[int]:
+        return self.comm.all_gather_object(int(self._n))
+
+    # ------------------------------------------------------------------ projection
+    def select(self, *cols) -> "DataFrame":
+        if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
+            cols = tuple(cols[0])
+        out = OrderedDict()
+        for c in cols:
+            if isinstance(c, str) and c == "*":
+                out.update(self._cols)
+                continue
+            name, data = self._resolve(c)
+            out[name] = data
+        return self._new(out)
+
+    def selectExpr(self, *exprs) -> "DataFrame":
+        from ..sql.parser import parse_expression
+        return self.select(*[parse_expression(e) for e in exprs])
+
+    def withColumn(self, name: str, e) -> "DataFrame":
+        data = e.eval(self) if isinstance(e, E.Expr) else E.lit(e).eval(self)
+        out = OrderedDict(self._cols)
+        out[name] = data
+        return self._new(out)
+
+    def withColumns(self, mapping: dict) -> "DataFrame":
+        df = self
+        for k, v in mapping.items():
+            df = df.withColumn(k, v)
+        return df
+
+    def withColumnData(self, name: str, data: C.Column) -> "DataFrame":
+        """Attach an already-computed column (used by ML transformers)."""
+        if len(data) != self._n:
+            raise ValueError("row count mismatch")
+        out = OrderedDict(self._cols)
+        out[name] = data
+        df = self._new(out)
+        df.lineage = self.lineage
+        return df
+
+    def withColumnRenamed(self, existing: str, new: str) -> "DataFrame":
+        out = OrderedDict((new if k == existing else k, v) for k, v in self._cols.items())
+        return self._new(out)
+
+    def drop(self, *names) -> "DataFrame":
+        names = {n.name if isinstance(n, E.Expr) else n for n in names}
+        return self._new(OrderedDict((k, v) for k, v in self._cols.items() if k not in names))
+
+    def alias(self, name) -> "DataFrame":
+        return self
+
+    # ------------------------------------------------------------------ row selection
+    def _take(self, idx: torch.Tensor) -> "DataFrame":
+        idx = idx.to(torch.int64)
+        out = OrderedDict()
+        for k, c in self._cols.items():
+            out[k] = c.take(idx.cpu() if isinstance(c, C.HostColumn) else idx.to(_col_device(c, self.device)))
+        return self._new(out, int(idx.numel()))
+
+    def _mask(self, mask: torch.Tensor) -> "DataFrame":
+        out = OrderedDict()
+        n = int(mask.sum().item())
+        for k, c in self._cols.items():
+            out[k] = c.mask_select(mask.cpu() if isinstance(c, C.HostColumn) else mask.to(_col_device(c, self.device)))
+        return self._new(out, n)
+
+    def filter(self, condition) -> "DataFrame":
+        if isinstance(condition, str):
+            from ..sql.parser import parse_expression
+            condition = parse_expression(condition)
+        c = condition.eval(self)
+        m = c.data.bool()
+        if c.valid is not None:
+            m = m & c.valid
+        return self._mask(m)
+
+    where = filter
+
+    def limit(self, num: int) -> "DataFrame":
+        sizes = self.partition_sizes()
+        off = sum(sizes[: self.comm.rank])
+        keep = max(0, min(self._n, num - off))
+        return self._take(torch.arange(keep, dtype=torch.int64))
+
+    # ------------------------------------------------------------------ missing values
+    def fillna(self, value, subset=None) -> "DataFrame":
+        """Replace null/NaN (Spark ``DataFrame.fillna`` semantics: numeric value fills
+        numeric columns, string value fills string columns, dict maps column->value)."""
+        if isinstance(subset, str):
+            subset = [subset]
+        if isinstance(value, dict):
+            items = value.items()
+        else:
+            items = [(k, value) for k in (subset or self.columns)]
+        out = OrderedDict(self._cols)
+        for k, v in items:
+            if k not in out:
+                if subset is not None or isinstance(value, dict):
+                    raise KeyError(f"cannot resolve column '{k}'")
+                continue
+            c = out[k]
+            if isinstance(c, C.NumericColumn) and isinstance(v, (int, float)) and not isinstance(v, bool):
+                if isinstance(c.dtype, T.BooleanType):
+                    continue
+                m = c.null_mask()
+                fill = torch.tensor(v, dtype=c.data.dtype, device=c.data.device) if c.data.is_floating_point() \
+                    else torch.tensor(int(v), dtype=c.data.dtype, device=c.data.device)
+                out[k] = C.NumericColumn(torch.where(m, fill, c.data), None, c.dtype)
+            elif isinstance(c, C.NumericColumn) and isinstance(v, bool) and isinstance(c.dtype, T.BooleanType):
+                m = c.null_mask()
+                out[k] = C.NumericColumn(torch.where(m, torch.tensor(v, device=c.data.device), c.data), None, c.dtype)
+            elif isinstance(c, C.StringColumn) and isinstance(v, str):
+                vals = c.values.copy()
+                for i, x in enumerate(vals):
+                    if x is None:
+                        vals[i] = v
+                out[k] = C.StringColumn(vals)
+        return self._new(out)
+
+    def dropna(self, how: str = "any", thresh: int | None = None, subset=None) -> "DataFrame":
+        names = [subset] if isinstance(subset, str) else (subset or self.columns)
+        nulls = []
+        for k in names:
+            c = self._col(k)
+            if isinstance(c, (C.NumericColumn, C.HostColumn)):
+                nulls.append(c.null_mask().to(self.device))
+        if not nulls:
+            return self
+        nn = torch.stack([~m for m in nulls]).sum(0)
+        if thresh is not None:
+            keep = nn >= thresh
+        elif how == "all":
+            keep = nn > 0
+        else:
+            keep = nn == len(nulls)
+        return self._mask(keep)
+
+    @property
+    def na(self):
+        return _NaFunctions(self)
+
+    # ------------------------------------------------------------------ sampling
+    def _global_rows(self) -> torch.Tensor:
+        off = self.row_offset()
+        return torch.arange(off, off + self._n, dtype=torch.int64, device=self.device)
+
+    def sample(self, withReplacement=None, fraction=None, seed=None) -> "DataFrame":
+        """Bernoulli (or Poisson when withReplacement) sampling keyed on (seed, global
+        row), so the sample is independent of how rows are partitioned over GPUs."""
+        if isinstance(withReplacement, float) and fraction is None:
+            withReplacement, fraction = False, withReplacement
+        if isinstance(fraction, int) and seed is None and isinstance(withReplacement, float):
+            withReplacement, fraction, seed = False, withReplacement, fraction
+        withReplacement = bool(withReplacement)
+        fraction = float(0.5 if fraction is None else fraction)
+        if fraction < 0:
+            raise ValueError("fraction must be nonnegative")
+        seed = int(self.session.conf.seed() if seed is None else seed)
+        from ..ops import sampling
+        rows = self._global_rows()
+        if withReplacement:
+            counts = sampling.poisson_counts(rows, seed, fraction)
+            idx = torch.repeat_interleave(torch.arange(self._n, device=self.device), counts)
+            return self._take(idx)
+        if fraction > 1:
+            raise ValueError("fraction must be <= 1 without replacement")
+        return self._mask(sampling.bernoulli_mask(rows, seed, fraction))
+
+    def randomSplit(self, weights, seed=None) -> list["DataFrame"]:
+        w = np.asarray(weights, dtype=np.float64)
+        if (w < 0).any() or w.sum() <= 0:
+            raise ValueError("weights must be nonnegative with positive sum")
+        cum = np.concatenate([[0.0], np.cumsum(w / w.sum())])
+        seed = int(self.session.conf.seed() if seed is None else seed)
+        from ..ops import sampling
+        u = sampling.uniform(self._global_rows(), seed)
+        outs = []
+        for i in range(len(w)):
+            hi = 1.0 + 1e-12 if i == len(w) - 1 else cum[i + 1]
+            outs.append(self._mask((u >= cum[i]) & (u < hi)))
+        return outs
+
+    # ------------------------------------------------------------------ caching
+    def cache(self) -> "DataFrame":
+        """Materialise and pin the partition in HBM (everything is already eager; this
+        also resolves any pending synthetic lineage into device memory within the
+        session's cache budget)."""
+        if self.lineage is not None:
+            self.lineage.materialise(self)
+        self._cached = True
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return self
+
+    def persist(self, storageLevel=None) -> "DataFrame":
+        return self.cache()
+
+    def unpersist(self, blocking=False) -> "DataFrame":
+        self._cached = False
+        return self
+
+    @property
+    def is_cached(self) -> bool:
+        return self._cached
+
+    @property
+    def storageLevel(self):
+        return StorageLevel.MEMORY_ONLY if self._cached else StorageLevel.NONE
+
+    # ------------------------------------------------------------------ gathering
+    def _gather_column(self, c: C.Column) -> C.Column:
+        comm = self.comm
+        if comm.world_size == 1:
+            return c
+        if isinstance(c, C.NumericColumn):
+            data = comm.all_gather_v(c.data)
+            valid = None
+            anynull = comm.all_gather_object(c.valid is not None)
+            if any(anynull):
+                v = c.valid if c.valid is not None else torch.ones_like(c.data, dtype=torch.bool)
+                valid = comm.all_gather_v(v.to(torch.uint8)).bool()
+            return C.NumericColumn(data, valid, c.dtype)
+        if isinstance(c, C.VectorColumn):
+            return C.VectorColumn(comm.all_gather_v(c.data), c.size)
+        parts = comm.all_gather_object(c)
+        return C.Column.concat(parts)
+
+    def _gathered(self) -> "OrderedDict[str, C.Column]":
+        return OrderedDict((k, self._gather_column(c)) for k, c in self._cols.items())
+
+    def collect(self) -> list[Row]:
+        cols = self._gathered()
+        names = list(cols.keys())
+        if not names:
+            return []
+        lists = [c.to_pylist() for c in cols.values()]
+        return [Row._make(names, vals) for vals in zip(*lists)]
+
+    def take(self, num: int) -> list[Row]:
+        return self.limit(num).collect()
+
+    def head(self, n: int | None = None):
+        if n is None:
+            rows = self.take(1)
+            return rows[0] if rows else None
+        return self.take(n)
+
+    def first(self):
+        return self.head()
+
+    def toPandas(self):
+        import pandas as pd
+        cols = self._gathered()
+        data = OrderedDict()
+        for k, c in cols.items():
+            if isinstance(c, (C.VectorColumn, C.SparseVectorColumn)):
+                data[k] = c.to_pylist()
+            else:
+                data[k] = c.to_numpy()
+        return pd.DataFrame(data, columns=list(cols.keys()))
+
+    def toArrow(self):
+        import pyarrow as pa
+        cols = self._gathered()
+        arrays, names = [], []
+        for k, c in cols.items():
+            names.append(k)
+            if isinstance(c, C.NumericColumn):
+                a = c.data.detach().cpu()
+                if a.dtype == torch.bfloat16:
+                    a = a.float()
+                mask = None if c.valid is None else ~c.valid.cpu().numpy()
+                arrays.append(pa.array(a.numpy(), mask=mask))
+            elif isinstance(c, (C.VectorColumn, C.SparseVectorColumn)):
+                arrays.append(pa.array([list(r) for r in c.to_numpy()], type=pa.list_(pa.float64())))
+            else:
+                arrays.append(pa.array(c.to_pylist()))
+        return pa.table(arrays, names=names)
+
+    def show(self, n: int = 20, truncate: bool = True):
+        rows = self.take(n)
+        names = self.columns
+
+        def fmt(v):
+            s = "null" if v is None else str(v)
+            return s[:17] + "..." if truncate and len(s) > 20 else s
+        table = [[fmt(v) for v in r] for r in rows]
+        widths = [max([len(h)] + [len(r[i]) for r in table]) for i, h in enumerate(names)]
+        sep = "+" + "+".join("-" * w for w in widths) + "+"
+        print(sep)
+        print("|" + "|".join(h.rjust(w) for h, w in zip(names, widths)) + "|")
+        print(sep)
+        for r in table:
+            print("|" + "|".join(v.rjust(w) for v, w in zip(r, widths)) + "|")
+        print(sep)
+
+    # ------------------------------------------------------------------ redistribution
+    def _from_full(self, cols: "OrderedDict[str, C.Column]") -> "DataFrame":
+        """Keep this rank's even slice of a replicated full-column set."""
+        n = len(next(iter(cols.values()))) if cols else 0
+        r, w = self.comm.rank, self.comm.world_size
+        lo, hi = (n * r) // w, (n * (r + 1)) // w
+        out = OrderedDict()
+        for k, c in cols.items():
+            c = c.slice(lo, hi)
+            if isinstance(c, C.NumericColumn):
+                c = C.NumericColumn(c.data.to(self.device), None if c.valid is None else c.valid.to(self.device), c.dtype)
+            elif isinstance(c, C.VectorColumn):
+                c = C.VectorColumn(c.data.to(self.device), c.size)
+            out[k] = c
+        return DataFrame(self.session, out, hi - lo)
+
+    def repartition(self, *args) -> "DataFrame":
+        return self._from_full(self._gathered())
+
+    coalesce = repartition
+
+    def orderBy(self, *cols, ascending=True) -> "DataFrame":
+        if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
+            cols = tuple(cols[0])
+        full = DataFrame(self.session.local_view(), self._gathered())
+        asc = ascending if isinstance(ascending, (list, tuple)) else [ascending] * len(cols)
+        order = np.arange(len(full))
+        for c, a in reversed(list(zip(cols, asc))):
+            e = E.col(c) if isinstance(c, str) else c
+            if getattr(e, "_desc", False):
+                a = False
+            vals = e.eval(full)
+            if isinstance(vals, C.NumericColumn):
+                key = vals.to_numpy()[order]
+                if key.dtype == object:
+                    key = np.array([np.inf if v is None else v for v in key], dtype=np.float64)
+                idx = np.argsort(key if a else -key.astype(np.float64), kind="stable")
+            else:
+                key = vals.to_numpy()[order]
+                idx = np.array(sorted(range(len(key)), key=lambda i: (key[i] is None, key[i] if key[i] is not None else ""),
+                                      reverse=not a), dtype=np.int64)
+            order = order[idx]
+        sorted_full = full._take(torch.from_numpy(order.astype(np.int64)))
+        return self._from_full(sorted_full._cols)
+
+    sort = orderBy
+
+    def union(self, other: "DataFrame") -> "DataFrame":
+        if len(other.columns) != len(self.columns):
+            raise ValueError("union requires the same number of columns")
+        out = OrderedDict()
+        for (k, a), b in zip(self._cols.items(), other._cols.values()):
+            out[k] = C.Column.concat([a, b])
+        return self._new(out, self._n + len(other))
+
+    unionAll = union
+
+    def unionByName(self, other: "DataFrame") -> "DataFrame":
+        return self.union(other.select(*self.columns))
+
+    def distinct(self) -> "DataFrame":
+        full = self._gathered()
+        rows = list(zip(*[c.to_pylist() for c in full.values()])) if full else []
+        seen, keep = set(), []
+        for i, r in enumerate(rows):
+            key = tuple(_hashable(v) for v in r)
+            if key not in seen:
+                seen.add(key)
+                keep.append(i)
+        local = DataFrame(self.session.local_view(), full)._take(torch.tensor(keep, dtype=torch.int64))
+        return self._from_full(local._cols)
+
+    dropDuplicates = distinct
+
+    def join(self, other: "DataFrame", on=None, how: str = "inner") -> "DataFrame":
+        from .join import join as _join
+        return _join(self, other, on, how)
+
+    def crossJoin(self, other: "DataFrame") -> "DataFrame":
+        return self.join(other, None, "cross")
+
+    # ------------------------------------------------------------------ aggregation
+    def groupBy(self, *cols) -> "GroupedData":
+        if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
+            cols = tuple(cols[0])
+        return GroupedData(self, [E.col(c) if isinstance(c, str) else c for c in cols])
+
+    groupby = groupBy
+
+    def agg(self, *aggs) -> "DataFrame":
+        return GroupedData(self, []).agg(*aggs)
+
+    def describe(self, *cols) -> "DataFrame":
+        if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
+            cols = cols[0]
+        names = list(cols) or [k for k, c in self._cols.items()
+                               if isinstance(c, (C.NumericColumn, C.StringColumn))]
+        stats = ["count", "mean", "stddev", "min", "max"]
+        res = OrderedDict(summary=np.array(stats, dtype=object))
+        for k in names:
+            c = self._col(k)
+            vals = []
+            if isinstance(c, C.NumericColumn):
+                s = _numeric_stats(self.comm, c)
+                vals = [s["count"], s["mean"], s["stddev"], s["min"], s["max"]]
+            else:
+                full = self._gather_column(c).to_pylist()
+                nn = [v for v in full if v is not None]
+                vals = [len(nn), None, None, min(nn) if nn else None, max(nn) if nn else None]
+            res[k] = np.array([None if v is None else str(v) for v in vals], dtype=object)
+        local = self.session.local_view()
+        full = OrderedDict((k, C.StringColumn(v)) for k, v in res.items())
+        return self._from_full(DataFrame(local, full)._cols)
+
+    summary = describe
+
+    # ------------------------------------------------------------------ io / catalog
+    @property
+    def write(self):
+        from ..io import DataFrameWriter
+        return DataFrameWriter(self)
+
+    def createOrReplaceTempView(self, name: str) -> None:
+        self.session.catalog.registerTempView(name, self)
+
+    registerTempTable = createOrReplaceTempView
+    createTempView = createOrReplaceTempView
+
+    def __repr__(self):
+        return "DataFrame[" + ", ".join(f"{k}: {t}" for k, t in self.dtypes) + "]"
+
+
+def _col_device(c: C.Column, default):
+    if isinstance(c, (C.NumericColumn, C.VectorColumn)):
+        return c.data.device
+    if isinstance(c, C.SparseVectorColumn):
+        return c.indptr.device
+    return default
+
+
+def _hashable(v):
+    if isinstance(v, list):
+        return tuple(v)
+    if hasattr(v, "toArray"):
+        return tuple(np.asarray(v.toArray()).tolist())
+    if isinstance(v, float) and math.isnan(v):
+        return "NaN"
+    return v
+
+
+def _numeric_stats(comm, c: C.NumericColumn) -> dict:
+    d = c.data.to(torch.float64)
+    ok = ~c.null_mask()
+    v = d[ok]
+    n = float(v.numel())
+    s = float(v.sum().item()) if n else 0.0
+    ss = float((v * v).sum().item()) if n else 0.0
+    mn = float(v.min().item()) if n else math.inf
+    mx = float(v.max().item()) if n else -math.inf
+    t = torch.tensor([n, s, ss], dtype=torch.float64, device=comm.device)
+    comm.all_reduce(t)
+    n, s, ss = t.tolist()
+    mn = comm.all_gather_object(mn)
+    mx = comm.all_gather_object(mx)
+    mn, mx = min(mn), max(mx)
+    mean = s / n if n else None
+    var = (ss - n * mean * mean) / (n - 1) if n > 1 else None
+    return {"count": int(n), "mean": mean, "stddev": math.sqrt(max(var, 0.0)) if var is not None else None,
+            "min": mn if n else None, "max": mx if n else None, "sum": s}
+
+
+class _NaFunctions:
+    def __init__(self, df):
+        self.df = df
+
+    def fill(self, value, subset=None):
+        return self.df.fillna(value, subset)
+
+    def drop(self, how="any", thresh=None, subset=None):
+        return self.df.dropna(how, thresh, subset)
+
+
+class GroupedData:
+    """groupBy(...).agg(...): per-partition partial aggregates, combined across ranks."""
+
+    def __init__(self, df: DataFrame, keys: list):
+        self.df, self.keys = df, keys
+
+    def agg(self, *aggs) -> DataFrame:
+        if len(aggs) == 1 and isinstance(aggs[0], dict):
+            aggs = tuple(getattr(E, fn if fn != "mean" else "avg")(c).alias(f"{fn}({c})") for c, fn in aggs[0].items())
+        df = self.df
+        full = DataFrame(df.session.local_view(), df._gathered())
+        key_cols = [k.eval(full) for k in self.keys]
+        key_lists = [kc.to_pylist() for kc in key_cols]
+        n = len(full)
+        groups: "OrderedDict[tuple, list[int]]" = OrderedDict()
+        for i in range(n):
+            key = tuple(_hashable(kl[i]) for kl in key_lists)
+            groups.setdefault(key, []).append(i)
+        if not self.keys and not groups:
+            groups[()] = []
+        out = OrderedDict()
+        for j, k in enumerate(self.keys):
+            firsts = [key_lists[j][idx[0]] for idx in groups.values()]
+            out[k.name] = C.from_numpy(np.array(firsts, dtype=object) if isinstance(key_cols[j], C.HostColumn)
+                                       else np.array(firsts), "cpu")
+        for a in aggs:
+            vals = a.arg.eval(full) if a.arg is not None else None
+            res = []
+            for idx in groups.values():
+                res.append(_aggregate(a, vals, idx))
+            if a.fn == "count":
+                out[a.name] = C.NumericColumn(torch.tensor(res, dtype=torch.int64))
+            else:
+                arr = np.array([np.nan if r is None else r for r in res], dtype=np.float64)
+                out[a.name] = C.NumericColumn(torch.from_numpy(arr),
+                                              torch.from_numpy(~np.isnan(arr)) if np.isnan(arr).any() and a.fn not in ("avg", "sum") else None)
+        return df._from_full(out)
+
+    def count(self) -> DataFrame:
+        return self.agg(E.count().alias("count"))
+
+    def _simple(self, fn, cols):
+        if not cols:
+            cols = [k for k, c in self.df._cols.items() if isinstance(c, C.NumericColumn)
+                    and k not in {e.name for e in self.keys}]
+        return self.agg(*[getattr(E, fn)(c).alias(f"{fn}({c})") for c in cols])
+
+    def sum(self, *cols):
+        return self._simple("sum", cols)
+
+    def avg(self, *cols):
+        return self._simple("avg", cols)
+
+    mean = avg
+
+    def min(self, *cols):
+        return self._simple("min", cols)
+
+    def max(self, *cols):
+        return self._simple("max", cols)
+
+
+def _aggregate(a: E.Agg, vals, idx):
+    if a.fn == "count":
+        if vals is None:
+            return len(idx)
+        py = vals.to_pylist() if not isinstance(vals, C.HostColumn) else list(vals.values)
+        sel = [py[i] for i in idx if py[i] is not None and not (isinstance(py[i], float) and math.isnan(py[i]))]
+        return len(set(map(_hashable, sel))) if a.distinct else len(sel)
+    if isinstance(vals, C.NumericColumn):
+        d = vals.data.to(torch.float64)[torch.tensor(idx, dtype=torch.int64, device=vals.data.device)] \
+            if idx else vals.data.to(torch.float64)[:0]
+        if vals.valid is not None and idx:
+            d = d[vals.valid[torch.tensor(idx, dtype=torch.int64, device=vals.valid.device)]]
+        d = d[~torch.isnan(d)]
+        if d.numel() == 0:
+            return None
+        if a.fn == "sum":
+            return float(d.sum())
+        if a.fn == "avg":
+            return float(d.mean())
+        if a.fn == "min":
+            return float(d.min())
+        if a.fn == "max":
+            return float(d.max())
+        if a.fn == "stddev":
+            return float(d.std()) if d.numel() > 1 else None
+        if a.fn == "variance":
+            return float(d.var()) if d.numel() > 1 else None
+    py = [vals.values[i] for i in idx if vals.values[i] is not None]
+    if not py:
+        return None
+    if a.fn == "min":
+        return min(py)
+    if a.fn == "max":
+        return max(py)
+    raise TypeError(f"aggregate {a.fn} not supported on {vals.dtype.simpleString()}")
+
+
+_ = Iterable

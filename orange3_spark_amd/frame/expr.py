@@ -1,0 +1,409 @@
+"""Column expressions (the ``pyspark.sql.Column`` / ``functions`` surface the widgets use).
+
+An expression is a small tree evaluated eagerly against one partition
+(``expr.eval(df) -> column.Column``).  Used by ``withColumn(name, df[c].cast('double'))``
+(reference: orangecontrib/spark/widgets/ml/spark_ml_dataset.py:578), ``filter``,
+``select`` and the SQL engine.
+"""
+from __future__ import annotations
+
+import math
+import re
+from typing import Any, Callable
+
+import numpy as np
+import torch
+
+from . import column as C
+from . import types as T
+
+
+class Expr:
+    def __init__(self, fn: Callable, name: str, refs: tuple = ()):
+        self._fn = fn
+        self._name = name
+        self.refs = refs  # referenced source column names
+
+    # evaluation ---------------------------------------------------------------
+    def eval(self, df) -> C.Column:
+        return self._fn(df)
+
+    @property
+    def name(self) -> str:
+        return self._name
+
+    def __repr__(self):
+        return f"Column<'{self._name}'>"
+
+    def alias(self, name: str) -> "Expr":
+        return Expr(self._fn, name, self.refs)
+
+    name_ = alias
+
+    def cast(self, dataType) -> "Expr":
+        dt = T.parse_type(dataType)
+
+        def f(df):
+            c = self.eval(df)
+            if isinstance(c, (C.NumericColumn, C.StringColumn)):
+                return c.cast(dt)
+            raise TypeError(f"cannot cast {c.dtype.simpleString()} to {dt.simpleString()}")
+        return Expr(f, f"CAST({self._name} AS {dt.simpleString().upper()})", self.refs)
+
+    astype = cast
+
+    # arithmetic ---------------------------------------------------------------
+    def _bin(self, other, op: str, torch_op, bool_out=False):
+        o = other if isinstance(other, Expr) else lit(other)
+
+        def f(df):
+            a, b = self.eval(df), o.eval(df)
+            return _binary(a, b, op, torch_op, bool_out, len(df))
+        return Expr(f, f"({self._name} {op} {o._name})", self.refs + o.refs)
+
+    def __add__(self, o): return self._bin(o, "+", torch.add)
+    def __radd__(self, o): return lit(o)._bin(self, "+", torch.add)
+    def __sub__(self, o): return self._bin(o, "-", torch.sub)
+    def __rsub__(self, o): return lit(o)._bin(self, "-", torch.sub)
+    def __mul__(self, o): return self._bin(o, "*", torch.mul)
+    def __rmul__(self, o): return lit(o)._bin(self, "*", torch.mul)
+    def __truediv__(self, o): return self._bin(o, "/", _div)
+    def __rtruediv__(self, o): return lit(o)._bin(self, "/", _div)
+    def __mod__(self, o): return self._bin(o, "%", torch.remainder)
+    def __pow__(self, o): return self._bin(o, "**", _pow)
+    def __eq__(self, o): return self._bin(o, "=", torch.eq, True)  # noqa: E721
+    def __ne__(self, o): return self._bin(o, "!=", torch.ne, True)
+    def __lt__(self, o): return self._bin(o, "<", torch.lt, True)
+    def __le__(self, o): return self._bin(o, "<=", torch.le, True)
+    def __gt__(self, o): return self._bin(o, ">", torch.gt, True)
+    def __ge__(self, o): return self._bin(o, ">=", torch.ge, True)
+    def __and__(self, o): return self._bin(o, "AND", torch.logical_and, True)
+    def __or__(self, o): return self._bin(o, "OR", torch.logical_or, True)
+    __hash__ = object.__hash__
+
+    def __invert__(self):
+        def f(df):
+            c = self.eval(df)
+            return C.NumericColumn(~c.data.bool(), c.valid, T.BooleanType())
+        return Expr(f, f"(NOT {self._name})", self.refs)
+
+    def __neg__(self):
+        def f(df):
+            c = self.eval(df)
+            return C.NumericColumn(-c.data, c.valid, c.dtype)
+        return Expr(f, f"(- {self._name})", self.refs)
+
+    def __bool__(self):
+        raise ValueError("Cannot convert column into bool: use '&' for 'and', '|' for 'or', '~' for 'not'")
+
+    # predicates ---------------------------------------------------------------
+    def isNull(self):
+        def f(df):
+            c = self.eval(df)
+            if isinstance(c, C.NumericColumn):
+                m = torch.zeros_like(c.data, dtype=torch.bool) if c.valid is None else ~c.valid
+            elif isinstance(c, C.HostColumn):
+                m = c.null_mask()
+            else:
+                m = torch.zeros(len(c), dtype=torch.bool)
+            return C.NumericColumn(m, None, T.BooleanType())
+        return Expr(f, f"({self._name} IS NULL)", self.refs)
+
+    def isNotNull(self):
+        return ~self.isNull()
+
+    def isin(self, *vals):
+        vals = list(vals[0]) if len(vals) == 1 and isinstance(vals[0], (list, tuple, set)) else list(vals)
+
+        def f(df):
+            c = self.eval(df)
+            if isinstance(c, C.NumericColumn):
+                ref = torch.tensor(vals, dtype=c.data.dtype, device=c.data.device)
+                return C.NumericColumn(torch.isin(c.data, ref), c.valid, T.BooleanType())
+            s = set(vals)
+            return C.NumericColumn(torch.tensor([v in s for v in c.values], dtype=torch.bool), None, T.BooleanType())
+        return Expr(f, f"({self._name} IN {tuple(vals)})", self.refs)
+
+    def between(self, lo, hi):
+        return (self >= lo) & (self <= hi)
+
+    def like(self, pattern: str):
+        rx = re.compile("^" + re.escape(pattern).replace("%", ".*").replace("_", ".") + "$", re.S)
+
+        def f(df):
+            c = self.eval(df)
+            return C.NumericColumn(torch.tensor([v is not None and bool(rx.match(str(v))) for v in c.values],
+                                                dtype=torch.bool), None, T.BooleanType())
+        return Expr(f, f"({self._name} LIKE '{pattern}')", self.refs)
+
+    def desc(self):
+        e = Expr(self._fn, self._name, self.refs)
+        e._desc = True
+        return e
+
+    def asc(self):
+        return Expr(self._fn, self._name, self.refs)
+
+    def otherwise(self, value):
+        if not hasattr(self, "_cases"):
+            raise ValueError("otherwise() only valid after when()")
+        return _when_expr(self._cases, value)
+
+    def when(self, cond, value):
+        if not hasattr(self, "_cases"):
+            raise ValueError("when() only valid after functions.when()")
+        return _make_when(self._cases + [(cond, value)])
+
+    def getItem(self, i: int):
+        def f(df):
+            c = self.eval(df)
+            if isinstance(c, C.VectorColumn):
+                return C.NumericColumn(c.data[:, i].to(torch.float64))
+            if isinstance(c, C.SparseVectorColumn):
+                return C.NumericColumn(c.to_dense(torch.float64)[:, i])
+            if isinstance(c, C.ArrayColumn):
+                return C.StringColumn(np.array([None if v is None or i >= len(v) else v[i] for v in c.values], dtype=object))
+            raise TypeError("getItem on non-array column")
+        return Expr(f, f"{self._name}[{i}]", self.refs)
+
+    __getitem__ = getItem
+
+
+def _div(a, b):
+    return torch.div(a.to(torch.float64), b.to(torch.float64))
+
+
+def _pow(a, b):
+    return torch.pow(a.to(torch.float64), b.to(torch.float64))
+
+
+def _promote(a: torch.Tensor, b: torch.Tensor):
+    if a.dtype == b.dtype:
+        return a, b
+    dt = torch.promote_types(a.dtype, b.dtype)
+    if dt in (torch.float32, torch.float16, torch.bfloat16) and (a.dtype == torch.float64 or b.dtype == torch.float64 or
+                                                                  not a.is_floating_point() or not b.is_floating_point()):
+        dt = torch.float64
+    return a.to(dt), b.to(dt)
+
+
+def _binary(a: C.Column, b: C.Column, op, torch_op, bool_out, n):
+    if isinstance(a, C.NumericColumn) and isinstance(b, C.NumericColumn):
+        x, y = a.data, b.data.to(a.data.device)
+        if y.dim() == 0:
+            y = y.expand_as(x)
+        if x.dim() == 0:
+            x = x.expand_as(y)
+        if op in ("AND", "OR"):
+            r = torch_op(x.bool(), y.bool())
+        else:
+            x, y = _promote(x, y)
+            r = torch_op(x, y)
+        valid = _and_valid(a.valid, b.valid)
+        if op == "/":
+            valid = _and_valid(valid, y != 0)
+        dt = T.BooleanType() if bool_out else T.from_torch_dtype(r.dtype)
+        return C.NumericColumn(r, valid, dt)
+    # host (string) comparisons
+    av = _host_values(a, n)
+    bv = _host_values(b, n)
+    py = {"=": lambda p, q: p == q, "!=": lambda p, q: p != q, "<": lambda p, q: p < q,
+          "<=": lambda p, q: p <= q, ">": lambda p, q: p > q, ">=": lambda p, q: p >= q,
+          "+": lambda p, q: p + q}[op]
+    out = [None if (p is None or q is None) else py(p, q) for p, q in zip(av, bv)]
+    if bool_out:
+        valid = torch.tensor([o is not None for o in out], dtype=torch.bool)
+        return C.NumericColumn(torch.tensor([bool(o) for o in out], dtype=torch.bool),
+                               None if bool(valid.all()) else valid, T.BooleanType())
+    return C.StringColumn(np.array(out, dtype=object))
+
+
+def _host_values(c: C.Column, n: int):
+    if isinstance(c, C.NumericColumn):
+        if c.data.dim() == 0:
+            return [c.data.item()] * n
+        return c.to_pylist()
+    if isinstance(c, _Scalar):
+        return [c.value] * n
+    return list(c.values)
+
+
+def _and_valid(a, b):
+    if a is None:
+        return b
+    if b is None:
+        return a
+    return a & b.to(a.device)
+
+
+class _Scalar(C.Column):
+    """Broadcast literal (host)."""
+
+    def __init__(self, value, n):
+        self.value, self._n = value, n
+        self.dtype = T.StringType()
+        self.values = np.array([value] * n, dtype=object)
+
+    def __len__(self):
+        return self._n
+
+
+def lit(value: Any) -> Expr:
+    if isinstance(value, Expr):
+        return value
+
+    def f(df):
+        n = len(df)
+        if value is None:
+            return C.NumericColumn(torch.zeros(n, dtype=torch.float64, device=df.device),
+                                   torch.zeros(n, dtype=torch.bool, device=df.device), T.DoubleType())
+        if isinstance(value, bool):
+            return C.NumericColumn(torch.full((n,), value, dtype=torch.bool, device=df.device), None, T.BooleanType())
+        if isinstance(value, int):
+            return C.NumericColumn(torch.full((n,), value, dtype=torch.int64 if abs(value) > 2**31 - 1 else torch.int32,
+                                              device=df.device))
+        if isinstance(value, float):
+            return C.NumericColumn(torch.full((n,), value, dtype=torch.float64, device=df.device))
+        return C.StringColumn(np.array([value] * n, dtype=object))
+    name = repr(value) if isinstance(value, str) else str(value)
+    if value is None:
+        name = "NULL"
+    return Expr(f, name)
+
+
+def col(name: str) -> Expr:
+    def f(df):
+        return df._col(name)
+    return Expr(f, name, (name,))
+
+
+column = col
+
+
+def when(cond: Expr, value) -> Expr:
+    return _make_when([(cond, value)])
+
+
+def _make_when(cases):
+    e = _when_expr(cases, None)
+    e._cases = cases
+    return e
+
+
+def _when_expr(cases, default):
+    def f(df):
+        n = len(df)
+        out = lit(default).eval(df)
+        for cond, val in reversed(cases):
+            cm = cond.eval(df)
+            m = cm.data.bool() & (cm.valid if cm.valid is not None else True)
+            v = lit(val).eval(df) if not isinstance(val, Expr) else val.eval(df)
+            if isinstance(v, C.NumericColumn) and isinstance(out, C.NumericColumn):
+                x, y = _promote(v.data, out.data.to(v.data.device))
+                data = torch.where(m.to(x.device), x, y)
+                vv = v.valid if v.valid is not None else torch.ones(n, dtype=torch.bool, device=x.device)
+                ov = out.valid if out.valid is not None else torch.ones(n, dtype=torch.bool, device=x.device)
+                valid = torch.where(m.to(x.device), vv, ov)
+                out = C.NumericColumn(data, None if bool(valid.all()) else valid)
+            else:
+                a, b = _host_values(v, n), _host_values(out, n)
+                mm = m.cpu().numpy()
+                out = C.StringColumn(np.array([p if k else q for p, q, k in zip(a, b, mm)], dtype=object))
+        return out
+    return Expr(f, "CASE WHEN ... END", tuple(r for c, _ in cases for r in c.refs))
+
+
+def _unary(name, fn):
+    def mk(e):
+        e = col(e) if isinstance(e, str) else e
+
+        def f(df):
+            c = e.eval(df)
+            return C.NumericColumn(fn(c.data.to(torch.float64)), c.valid, T.DoubleType())
+        return Expr(f, f"{name}({e.name})", e.refs)
+    return mk
+
+
+sqrt = _unary("SQRT", torch.sqrt)
+log = _unary("LOG", torch.log)
+exp = _unary("EXP", torch.exp)
+log1p = _unary("LOG1P", torch.log1p)
+
+
+def abs(e):  # noqa: A001
+    e = col(e) if isinstance(e, str) else e
+
+    def f(df):
+        c = e.eval(df)
+        return C.NumericColumn(torch.abs(c.data), c.valid, c.dtype)
+    return Expr(f, f"ABS({e.name})", e.refs)
+
+
+def isnan(e):
+    e = col(e) if isinstance(e, str) else e
+
+    def f(df):
+        c = e.eval(df)
+        d = c.data
+        return C.NumericColumn(torch.isnan(d) if d.is_floating_point() else torch.zeros_like(d, dtype=torch.bool),
+                               None, T.BooleanType())
+    return Expr(f, f"isnan({e.name})", e.refs)
+
+
+def coalesce(*es):
+    es = [col(e) if isinstance(e, str) else e for e in es]
+
+    def f(df):
+        out = es[-1].eval(df)
+        for e in reversed(es[:-1]):
+            c = e.eval(df)
+            m = ~(c.null_mask())
+            x, y = _promote(c.data, out.data.to(c.data.device))
+            valid = m | (out.valid if out.valid is not None else torch.ones_like(m))
+            out = C.NumericColumn(torch.where(m, x, y), None if bool(valid.all()) else valid)
+        return out
+    return Expr(f, "coalesce(" + ",".join(e.name for e in es) + ")", tuple(r for e in es for r in e.refs))
+
+
+# ------------------------------------------------------------------ aggregate exprs
+class Agg:
+    """Aggregate expression for groupBy().agg() / DataFrame.agg() / SQL."""
+
+    def __init__(self, fn: str, arg: Expr | None, name: str | None = None, distinct=False):
+        self.fn, self.arg, self.distinct = fn, arg, distinct
+        self._name = name or (f"{fn}({arg.name if arg is not None else '1'})" if fn != "count" or arg is not None
+                              else "count(1)")
+
+    @property
+    def name(self):
+        return self._name
+
+    def alias(self, name):
+        return Agg(self.fn, self.arg, name, self.distinct)
+
+
+def _agg(fn):
+    def mk(e="*"):
+        if isinstance(e, str):
+            e = None if e == "*" else col(e)
+        return Agg(fn, e)
+    return mk
+
+
+sum = _agg("sum")  # noqa: A001
+avg = mean = _agg("avg")
+min = _agg("min")  # noqa: A001
+max = _agg("max")  # noqa: A001
+count = _agg("count")
+stddev = _agg("stddev")
+variance = _agg("variance")
+
+
+def countDistinct(e):
+    e = col(e) if isinstance(e, str) else e
+    return Agg("count", e, f"count(DISTINCT {e.name})", distinct=True)
+
+
+__all__ = ["Expr", "Agg", "col", "column", "lit", "when", "sqrt", "log", "exp", "log1p", "abs", "isnan",
+           "coalesce", "sum", "avg", "mean", "min", "max", "count", "stddev", "variance", "countDistinct"]
+_ = math

@@ -1,0 +1,341 @@
+"""DataFrame readers/writers (parquet, csv, json) with per-rank partitioning.
+
+Parquet files are written Spark-style as a directory of ``part-XXXXX`` files (one per
+rank) plus ``_SUCCESS``; each rank reads only the row groups that overlap its row
+range.  Spark's ML ``VectorUDT`` parquet struct
+(``struct<type:tinyint,size:int,indices:array<int>,values:array<double>>``) is
+recognised on read and produced on write, so model/data directories interoperate.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from .frame import column as C
+from .frame.dataframe import DataFrame
+
+VECTOR_FIELDS = ("type", "size", "indices", "values")
+
+
+def _pa():
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    return pa, pq
+
+
+def vector_arrow_type():
+    pa, _ = _pa()
+    return pa.struct([("type", pa.int8()), ("size", pa.int32()), ("indices", pa.list_(pa.int32())),
+                      ("values", pa.list_(pa.float64()))])
+
+
+def vectors_to_arrow(rows) -> "pa.Array":
+    """List of DenseVector/SparseVector/array-like -> Spark VectorUDT struct array."""
+    pa, _ = _pa()
+    from .ml.linalg import SparseVector
+    recs = []
+    for v in rows:
+        if v is None:
+            recs.append(None)
+        elif isinstance(v, SparseVector):
+            recs.append({"type": 0, "size": int(v.size), "indices": [int(i) for i in v.indices],
+                         "values": [float(x) for x in v.values]})
+        else:
+            arr = np.asarray(v.toArray() if hasattr(v, "toArray") else v, dtype=np.float64)
+            recs.append({"type": 1, "size": None, "indices": None, "values": arr.tolist()})
+    return pa.array(recs, type=vector_arrow_type())
+
+
+def _is_vector_struct(t) -> bool:
+    pa, _ = _pa()
+    return pa.types.is_struct(t) and [t.field(i).name for i in range(t.num_fields)] == list(VECTOR_FIELDS)
+
+
+def arrow_to_columns(table, session) -> "OrderedDict[str, C.Column]":
+    pa, _ = _pa()
+    out = OrderedDict()
+    dev = session.device
+    for name, arr in zip(table.column_names, table.columns):
+        arr = arr.combine_chunks() if hasattr(arr, "combine_chunks") else arr
+        t = arr.type
+        if _is_vector_struct(t):
+            out[name] = _vector_struct_to_column(arr.to_pylist(), session)
+        elif pa.types.is_list(t) and (pa.types.is_floating(t.value_type) or pa.types.is_integer(t.value_type)):
+            vals = arr.to_pylist()
+            mat = np.array([np.asarray(v, dtype=np.float64) for v in vals]) if vals else np.zeros((0, 0))
+            out[name] = C.VectorColumn(torch.from_numpy(mat).to(dev))
+        elif pa.types.is_list(t):
+            out[name] = C.ArrayColumn(arr.to_pylist())
+        elif pa.types.is_boolean(t) or pa.types.is_integer(t) or pa.types.is_floating(t):
+            mask = arr.is_null().to_numpy(zero_copy_only=False) if arr.null_count else None
+            if pa.types.is_boolean(t):
+                np_arr = np.array(arr.fill_null(False).to_pylist(), dtype=bool)
+            else:
+                np_arr = arr.fill_null(0).to_numpy(zero_copy_only=False)
+                if np_arr.dtype.kind == "u":
+                    np_arr = np_arr.astype(np.int64)
+            col = C.NumericColumn(torch.from_numpy(np.ascontiguousarray(np_arr)).to(dev),
+                                  None if mask is None else torch.from_numpy(~mask).to(dev))
+            out[name] = col
+        else:
+            out[name] = C.StringColumn(np.array([None if v is None else str(v) for v in arr.to_pylist()], dtype=object))
+    return out
+
+
+def _vector_struct_to_column(recs, session) -> C.Column:
+    dev = session.device
+    if not recs:
+        return C.VectorColumn(torch.zeros((0, 0), dtype=torch.float64, device=dev))
+    sizes = [r["size"] if r and r["type"] == 0 else (len(r["values"]) if r else 0) for r in recs]
+    d = max(sizes) if sizes else 0
+    if all(r and r["type"] == 1 for r in recs):
+        mat = np.array([r["values"] for r in recs], dtype=np.float64).reshape(len(recs), d)
+        return C.VectorColumn(torch.from_numpy(mat).to(dev))
+    ptr, ind, val = [0], [], []
+    for r in recs:
+        if r is None:
+            ptr.append(ptr[-1])
+        elif r["type"] == 0:
+            ind.extend(r["indices"])
+            val.extend(r["values"])
+            ptr.append(ptr[-1] + len(r["indices"]))
+        else:
+            nz = [(i, v) for i, v in enumerate(r["values"]) if v != 0]
+            ind.extend(i for i, _ in nz)
+            val.extend(v for _, v in nz)
+            ptr.append(ptr[-1] + len(nz))
+    return C.SparseVectorColumn(torch.tensor(ptr, dtype=torch.int64, device=dev),
+                                torch.tensor(ind, dtype=torch.int32, device=dev),
+                                torch.tensor(val, dtype=torch.float64, device=dev), d)
+
+
+def columns_to_arrow(df: DataFrame, local_only: bool = True):
+    """This rank's partition (or the gathered frame) as a pyarrow Table."""
+    pa, _ = _pa()
+    cols = df._cols if local_only else df._gathered()
+    arrays, names = [], []
+    for k, c in cols.items():
+        names.append(k)
+        if isinstance(c, C.NumericColumn):
+            a = c.data.detach().cpu()
+            if a.dtype == torch.bfloat16:
+                a = a.float()
+            mask = None if c.valid is None else ~c.valid.cpu().numpy()
+            arrays.append(pa.array(a.numpy(), mask=mask))
+        elif isinstance(c, (C.VectorColumn, C.SparseVectorColumn)):
+            arrays.append(vectors_to_arrow(c.to_pylist()))
+        elif isinstance(c, C.ArrayColumn):
+            arrays.append(pa.array(c.to_pylist(), type=pa.list_(pa.string())))
+        else:
+            arrays.append(pa.array(c.to_pylist(), type=pa.string()))
+    return pa.table(arrays, names=names)
+
+
+def _parquet_files(path: str) -> list[str]:
+    if os.path.isdir(path):
+        files = sorted(f for f in glob.glob(os.path.join(path, "**", "*.parquet"), recursive=True)
+                       if not os.path.basename(f).startswith(("_", ".")))
+        if not files:
+            files = sorted(f for f in glob.glob(os.path.join(path, "part-*")) if not f.endswith(".crc"))
+        return files
+    return sorted(glob.glob(path)) or [path]
+
+
+def read_parquet(session, path: str, columns=None) -> DataFrame:
+    """Each rank reads only the row groups overlapping its contiguous row range."""
+    pa, pq = _pa()
+    files = _parquet_files(path)
+    metas = [pq.ParquetFile(f) for f in files]
+    spans = []  # (file idx, row group idx, start, nrows)
+    total = 0
+    for fi, pf in enumerate(metas):
+        for gi in range(pf.metadata.num_row_groups):
+            nr = pf.metadata.row_group(gi).num_rows
+            spans.append((fi, gi, total, nr))
+            total += nr
+    lo, hi = session._shard_bounds(total)
+    pieces = []
+    for fi, gi, start, nr in spans:
+        s, e = max(lo, start), min(hi, start + nr)
+        if s >= e:
+            continue
+        t = metas[fi].read_row_group(gi, columns=columns)
+        pieces.append(t.slice(s - start, e - s))
+    if pieces:
+        table = pa.concat_tables(pieces, promote_options="default")
+    else:
+        schema = metas[0].schema_arrow if metas else pa.schema([])
+        if columns:
+            schema = pa.schema([schema.field(c) for c in columns])
+        table = schema.empty_table()
+    return DataFrame(session, arrow_to_columns(table, session), table.num_rows)
+
+
+def write_parquet(df: DataFrame, path: str, mode: str = "error") -> None:
+    _, pq = _pa()
+    comm = df.comm
+    if comm.rank == 0:
+        _prepare_dir(path, mode)
+    comm.barrier()
+    pq.write_table(columns_to_arrow(df), os.path.join(path, f"part-{comm.rank:05d}.snappy.parquet"))
+    comm.barrier()
+    if comm.rank == 0:
+        open(os.path.join(path, "_SUCCESS"), "w").close()
+
+
+def _prepare_dir(path, mode):
+    import shutil
+    if os.path.exists(path):
+        if mode in ("error", "errorifexists", None):
+            raise FileExistsError(f"path {path} already exists")
+        if mode == "ignore":
+            return
+        if mode == "overwrite":
+            shutil.rmtree(path) if os.path.isdir(path) else os.remove(path)
+    os.makedirs(path, exist_ok=True)
+
+
+def read_csv(session, path: str, header=True, inferSchema=True, sep=",", **kw) -> DataFrame:
+    import pandas as pd
+    files = sorted(glob.glob(os.path.join(path, "*.csv"))) if os.path.isdir(path) else [path]
+    frames = [pd.read_csv(f, sep=sep, header=0 if header else None, dtype=None if inferSchema else str) for f in files]
+    pdf = pd.concat(frames, ignore_index=True) if frames else pd.DataFrame()
+    if not header:
+        pdf.columns = [f"_c{i}" for i in range(pdf.shape[1])]
+    return session.createDataFrame(pdf)
+
+
+class DataFrameReader:
+    def __init__(self, session):
+        self.session = session
+        self._format = "parquet"
+        self._opts = {}
+
+    def format(self, source):
+        self._format = source
+        return self
+
+    def option(self, key, value):
+        self._opts[key] = value
+        return self
+
+    def options(self, **kw):
+        self._opts.update(kw)
+        return self
+
+    def schema(self, schema):
+        return self
+
+    def load(self, path=None, format=None, **kw):
+        fmt = format or self._format
+        opts = dict(self._opts, **kw)
+        if fmt == "parquet":
+            return self.parquet(path)
+        if fmt == "csv":
+            return self.csv(path, **opts)
+        if fmt == "json":
+            return self.json(path)
+        raise ValueError(f"unknown format {fmt}")
+
+    def parquet(self, *paths, columns=None):
+        if len(paths) == 1:
+            return read_parquet(self.session, paths[0], columns)
+        dfs = [read_parquet(self.session, p, columns) for p in paths]
+        out = dfs[0]
+        for d in dfs[1:]:
+            out = out.union(d)
+        return out
+
+    def csv(self, path, header=None, inferSchema=None, sep=None, **kw):
+        h = self._opts.get("header", True) if header is None else header
+        h = str(h).lower() in ("true", "1") if isinstance(h, str) else bool(h)
+        i = self._opts.get("inferSchema", True) if inferSchema is None else inferSchema
+        i = str(i).lower() in ("true", "1") if isinstance(i, str) else bool(i)
+        return read_csv(self.session, path, h, i, sep or self._opts.get("sep", ","))
+
+    def json(self, path):
+        import pandas as pd
+        pdf = pd.read_json(path, lines=True)
+        return self.session.createDataFrame(pdf)
+
+    def table(self, name):
+        return self.session.table(name)
+
+
+class DataFrameWriter:
+    def __init__(self, df: DataFrame):
+        self.df = df
+        self._mode = "error"
+        self._format = "parquet"
+
+    def mode(self, saveMode):
+        self._mode = saveMode or "error"
+        return self
+
+    def format(self, source):
+        self._format = source
+        return self
+
+    def option(self, key, value):
+        return self
+
+    def options(self, **kw):
+        return self
+
+    def partitionBy(self, *cols):
+        return self
+
+    def save(self, path, format=None, mode=None):
+        if mode:
+            self._mode = mode
+        fmt = format or self._format
+        if fmt == "parquet":
+            return self.parquet(path)
+        if fmt == "csv":
+            return self.csv(path)
+        if fmt == "json":
+            return self.json(path)
+        raise ValueError(fmt)
+
+    def parquet(self, path, mode=None):
+        write_parquet(self.df, path, mode or self._mode)
+
+    def csv(self, path, mode=None, header=True):
+        comm = self.df.comm
+        if comm.rank == 0:
+            _prepare_dir(path, mode or self._mode)
+        comm.barrier()
+        self.df.toPandas().iloc[0:0]  # schema check on every rank
+        pdf = DataFrame(self.df.session.local_view(), self.df._cols).toPandas()
+        pdf.to_csv(os.path.join(path, f"part-{comm.rank:05d}.csv"), index=False, header=header)
+        comm.barrier()
+
+    def json(self, path, mode=None):
+        comm = self.df.comm
+        if comm.rank == 0:
+            _prepare_dir(path, mode or self._mode)
+        comm.barrier()
+        rows = DataFrame(self.df.session.local_view(), self.df._cols).collect()
+        with open(os.path.join(path, f"part-{comm.rank:05d}.json"), "w") as f:
+            for r in rows:
+                f.write(json.dumps({k: _jsonable(v) for k, v in r.asDict().items()}) + "\n")
+        comm.barrier()
+
+    def saveAsTable(self, name, format=None, mode=None):
+        self.df.session.catalog.saveAsTable(self.df, name, mode or self._mode)
+
+    def insertInto(self, name, overwrite=False):
+        self.df.session.catalog.saveAsTable(self.df, name, "overwrite" if overwrite else "append")
+
+
+def _jsonable(v):
+    if hasattr(v, "toArray"):
+        return np.asarray(v.toArray()).tolist()
+    if isinstance(v, (np.floating, np.integer)):
+        return v.item()
+    return v

@@ -1,0 +1,106 @@
+"""ctypes binding of the in-tree gfx950 kernel library (``_lib/libo3s_kernels.so``).
+
+Policy ("fail loudly"): on a machine with a visible GPU every op dispatches to the HIP
+kernels; if the library is missing or does not load there, :func:`kernels` raises
+instead of silently using a PyTorch fallback.  The PyTorch reference implementations
+are only used for CPU tensors (tests, the CPU plumbing config) -- see
+``ops/__init__.py``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+from . import build as _build
+
+_LOCK = threading.Lock()
+_LIB = None
+_HOST = None
+
+c_i64, c_i32, c_u32, c_f32 = C.c_int64, C.c_int, C.c_uint32, C.c_float
+c_vp = C.c_void_p
+
+# name -> argtypes (every kernel entry point returns int: 0 = ok, <0 arg error, >0 hipError)
+_SIGS: dict[str, list] = {
+    "o3s_glm_layout": [c_i64, C.POINTER(c_i32), C.POINTER(c_i32)],
+    "o3s_glm_grad": [c_i32, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_u32, c_i64,
+                     c_vp, c_f32, c_vp, c_i32, c_vp, c_vp],
+    "o3s_synth_glm": [c_vp, c_i64, c_i64, c_vp, c_u32, c_i64, c_vp, c_f32, c_i32, c_vp],
+    "o3s_glm_margin": [c_vp, c_i64, c_i64, c_vp, c_f32, c_vp, c_i32, c_vp],
+}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib_path() -> Path:
+    return _build.KERNEL_LIB
+
+
+def _load():
+    global _LIB
+    path = lib_path()
+    if not path.exists() and os.environ.get("O3S_AUTOBUILD", "1") == "1":
+        _build.build()
+    if not path.exists():
+        raise NativeError(f"kernel library missing: {path} (run python -m orange3_spark_amd.ops.build)")
+    lib = C.CDLL(str(path), mode=C.RTLD_GLOBAL)
+    for name, argt in _SIGS.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = argt
+        fn.restype = C.c_int
+    _LIB = lib
+    return lib
+
+
+def kernels():
+    """Return the loaded kernel library (raises NativeError if it cannot be loaded)."""
+    if _LIB is not None:
+        return _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        return _load()
+
+
+def available() -> bool:
+    try:
+        kernels()
+        return True
+    except Exception:
+        return False
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise NativeError(f"{what} failed with code {rc}")
+
+
+def num_cus(device: torch.device) -> int:
+    try:
+        return torch.cuda.get_device_properties(device).multi_processor_count
+    except Exception:
+        return 256
+
+
+def grid_for(device: torch.device, work_items: int, per_block: int, blocks_per_cu: int = 8) -> int:
+    """Grid for a streaming kernel: enough blocks to fill every CU, capped (Guideline 11)."""
+    need = max(1, (work_items + per_block - 1) // per_block)
+    return int(max(1, min(need, num_cus(device) * blocks_per_cu)))

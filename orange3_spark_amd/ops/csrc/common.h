@@ -1,0 +1,99 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels of orange3_spark_amd.
+//
+// Conventions used by every kernel in this directory:
+//   * wave = 64 lanes; block sizes are multiples of 64 (256 by default = 4 waves).
+//   * bf16 data is loaded 16 B per lane (8 elements, one `global_load_dwordx4`),
+//     never element-wise (CDNA guide, Guideline 13).
+//   * cross-block reductions never use float atomics in the hot loop: each block
+//     writes one partial "slab" row and a second, tiny kernel sums the slabs in a
+//     fixed order (deterministic, Guideline 12).
+//   * every entry point is `extern "C"` taking raw device pointers + a hipStream_t,
+//     so Python drives it through ctypes with torch's current stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define O3S_API extern "C" __attribute__((visibility("default")))
+
+namespace o3s {
+
+constexpr int kWave = 64;
+
+typedef short short8 __attribute__((ext_vector_type(8)));
+typedef float float4_ __attribute__((ext_vector_type(4)));
+
+// --- bf16 <-> f32 -----------------------------------------------------------
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+// Round-to-nearest-even f32 -> bf16 bits (inputs here are finite by construction;
+// NaN is preserved as a quiet NaN).
+__host__ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t u = __float_as_uint(f);
+#else
+  uint32_t u; __builtin_memcpy(&u, &f, 4);
+#endif
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// Unpack 8 bf16 (one 16-B chunk) into f32.
+__device__ __forceinline__ void unpack8(const short8 v, float (&x)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = bf16_to_f32((uint16_t)v[j]);
+}
+
+// --- counter-based hashing (synthetic data; identical on host via torch) ----
+// murmur3 fmix32 finaliser: full avalanche, two 32-bit multiplies.
+__host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu;
+  h ^= h >> 13; h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+// Per-row key from (seed, global row index).
+__host__ __device__ __forceinline__ uint32_t row_key(uint32_t seed, int64_t row) {
+  uint32_t lo = (uint32_t)(row & 0xffffffffll);
+  uint32_t hi = (uint32_t)((uint64_t)row >> 32);
+  return fmix32(seed ^ fmix32(lo * 0x9E3779B1u + hi * 0x7FEB352Du + 0x165667B1u));
+}
+// Signed 16-bit lane of a hash -> uniform in [-1, 1) (exact in f32).
+__host__ __device__ __forceinline__ float u16_to_unit(uint32_t bits16) {
+  return (float)(int16_t)(uint16_t)bits16 * (1.0f / 32768.0f);
+}
+
+// --- wave / block reductions -------------------------------------------------
+template <int WIDTH>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int off = WIDTH / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, WIDTH);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) { return group_sum<64>(v); }
+
+// Numerically stable log(1 + exp(x)).
+__device__ __forceinline__ float log1pexp(float x) {
+  return x > 0.f ? x + log1pf(__expf(-x)) : log1pf(__expf(x));
+}
+__device__ __forceinline__ float sigmoidf(float x) {
+  return 1.0f / (1.0f + __expf(-x));
+}
+
+// Bijective XCD-aware block remap (CDNA guide §5 "XCD swizzle must be bijective"):
+// consecutive logical tiles land on the same XCD (shared L2).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+}  // namespace o3s
+
+#define O3S_CHECK_LAUNCH() \
+  do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)

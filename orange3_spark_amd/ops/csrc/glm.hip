@@ -1,0 +1,524 @@
+// Generalised-linear-model streaming kernels (gfx950).
+//
+// Replaces the per-partition gradient closure that Spark MLlib runs inside
+// `treeAggregate` for LogisticRegression / LinearSVC / LinearRegression (reached in
+// the reference through OWSparkEstimator.apply -> `fit`,
+// orangecontrib/spark/base/spark_ml_estimator.py:19-25).
+//
+// Layout: X is a row-major bf16 matrix [n, ld] (ld % 8 == 0, zero padded).  A row
+// is split over LPR lanes ("row group"); lane c of a group owns the 16-B chunks
+// c, c+LPR, ... (CPL chunks).  A wave therefore streams 64/LPR consecutive rows per
+// `global_load_dwordx4` -- for D = 256 that is two rows per wave-instruction, 1 KiB
+// contiguous -- and the gradient  X^T r  is lane-local (each lane always touches
+// the same 8*CPL columns), so only the per-row dot product needs a cross-lane sum.
+//
+// The op is a GEMV: HBM bound (512 B/row at D=256), so MFMA buys nothing here
+// (SURVEY §7.5 item 2); the budget is bytes.  VALU work per row is ~6x below the
+// HBM-bound cycle budget at 256 CUs, so the kernel runs at the streaming rate.
+//
+// Cross-block reduction: one fp32 slab row per block + `glm_finish` (fp64, fixed
+// order) -> bitwise deterministic results, no float atomics (Guideline 12).
+//
+// SRC == 1 ("synthetic lineage"): instead of loading a chunk, the lane regenerates
+// it from the counter hash used by `synth_glm_kernel`, so rows that did not fit in
+// HBM are recomputed from lineage on every pass -- the MI355X equivalent of Spark's
+// MEMORY_ONLY caching, where evicted partitions are recomputed.  Regenerated and
+// materialised rows are bit-identical.
+#include "common.h"
+
+using namespace o3s;
+
+namespace {
+
+enum { LOSS_LOGISTIC = 0, LOSS_HINGE = 1, LOSS_SQUARED = 2 };
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+// One 16-B chunk (8 features) of synthetic row `rk` (row key) at chunk index ch.
+// Values are k/32768 (k int16) rounded to bf16.
+__device__ __forceinline__ short8 synth_chunk(uint32_t rk, int ch) {
+  short8 v;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const uint32_t h = fmix32(rk + (uint32_t)(ch * 4 + p) * 0x9E3779B9u);
+    v[2 * p] = (short)f32_to_bf16(u16_to_unit(h & 0xffffu));
+    v[2 * p + 1] = (short)f32_to_bf16(u16_to_unit(h >> 16));
+  }
+  return v;
+}
+// Label draw for a synthetic row: y ~ Bernoulli(sigmoid(margin_true)).
+__device__ __forceinline__ float synth_label(uint32_t rk, float margin_true) {
+  const float u = (float)(fmix32(rk ^ 0xA511E9B3u) >> 8) * (1.0f / 16777216.0f);
+  return u < sigmoidf(margin_true) ? 1.0f : 0.0f;
+}
+
+// ---------------------------------------------------------------------------
+// "Transpose" reduction of U per-row partial sums over the LPR lanes of a row group.
+// A butterfly would cost U*log2(LPR) cross-lane ops; recursive halving costs
+// U/2 + U/4 + ... + (remaining butterfly) -- for LPR=32, U=8: 9 instead of 40 -- and
+// leaves every lane with the COMPLETE sums of NF = U >> H consecutive rows
+// (H = min(log2 U, log2 LPR)), so the per-row epilogue (sigmoid, loss) runs once per
+// row instead of once per lane-row.
+constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
+
+template <int LPR, int U>
+struct RowReduce {
+  static constexpr int LL = ilog2(LPR), LU = ilog2(U);
+  static constexpr int H = LL < LU ? LL : LU;   // halving steps
+  static constexpr int NF = U >> H;             // rows finished per lane
+  // first row index owned by group-lane c
+  __device__ static __forceinline__ int base(int c) {
+    int b = 0;
+#pragma unroll
+    for (int s = 0; s < H; ++s) b += ((c >> (LL - 1 - s)) & 1) * (U >> (s + 1));
+    return b;
+  }
+  // group-lane holding row u (lower, butterflied bits zero)
+  __host__ __device__ static constexpr int owner(int u) {
+    int c = 0;
+    for (int s = 0; s < H; ++s) c += (((u - u % NF) >> (LU - 1 - s)) & 1) << (LL - 1 - s);
+    return c;
+  }
+  // true for exactly one lane per finished row
+  __device__ static __forceinline__ bool representative(int c) {
+    return (c & ((1 << (LL - H)) - 1)) == 0;
+  }
+  __device__ static __forceinline__ void run(float (&v)[U], int c) {
+    int n = U;
+#pragma unroll
+    for (int s = 0; s < LL; ++s) {
+      const int off = LPR >> (s + 1);
+      if (s < H) {
+        const bool up = (c & off) != 0;
+        n >>= 1;
+#pragma unroll
+        for (int j = 0; j < U / 2; ++j) {
+          if (j < n) {
+            const float keep = up ? v[j + n] : v[j];
+            const float send = up ? v[j] : v[j + n];
+            v[j] = keep + __shfl_xor(send, off, kWave);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < NF; ++j) v[j] += __shfl_xor(v[j], off, kWave);
+      }
+    }
+  }
+};
+
+template <int LPR, int CPL, int UNROLL, int LOSS, int SRC>
+__global__ __launch_bounds__(kBlock) void glm_grad_kernel(
+    const uint16_t* __restrict__ X, int64_t ld, int64_t n, const float* __restrict__ y,
+    const float* __restrict__ sw, const float* __restrict__ coef, float intercept,
+    uint32_t seed, int64_t row0, const float* __restrict__ wtrue, float btrue,
+    float* __restrict__ partial, int pstride) {
+  constexpr int G = kWave / LPR;             // rows per wave-instruction
+  constexpr int RT = G * UNROLL;             // rows per wave tile
+  constexpr int DP = LPR * CPL * 8;          // padded feature count
+  using RR = RowReduce<LPR, UNROLL>;
+  constexpr int NF = RR::NF;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  const int g = lane / LPR, c = lane % LPR;
+  const int nch = (int)(ld / 8);
+  const int ubase = RR::base(c);
+  const bool rep = RR::representative(c);
+
+  float w[CPL][8], wt[CPL][8], acc[CPL][8];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = 8 * (c + k * LPR) + j;
+      w[k][j] = col < ld ? coef[col] : 0.f;
+      wt[k][j] = (SRC == 1 && col < ld) ? wtrue[col] : 0.f;
+      acc[k][j] = 0.f;
+    }
+  float acc_r = 0.f, acc_loss = 0.f, acc_w = 0.f;
+
+  const int64_t ntiles = (n + RT - 1) / RT;
+  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t base = t * RT;
+    // Loads are issued unconditionally from clamped addresses and masked in
+    // registers afterwards: a per-load `ok ? load : 0` makes hipcc branch around
+    // every load and serialise them (CDNA guide §5, "three .s-level traps" (c)).
+    short8 xv[UNROLL][CPL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t row = base + u * G + g;
+      const bool ok = row < n;
+      const int64_t rowc = ok ? row : n - 1;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int ch = c + k * LPR;
+        const bool okc = ok && ch < nch;
+        if (SRC == 0) {
+          const int chc = ch < nch ? ch : nch - 1;
+          short8 v = __builtin_nontemporal_load(reinterpret_cast<const short8*>(X + rowc * ld + 8 * chc));
+          xv[u][k] = okc ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
+        } else {
+          short8 v = synth_chunk(row_key(seed, row0 + rowc), ch);
+          xv[u][k] = okc ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+      }
+    }
+    // labels / weights of the rows this lane finishes
+    float yy[NF], ww[NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int64_t row = base + (ubase + j) * G + g;
+      const bool ok = row < n;
+      const int64_t rowc = ok ? row : n - 1;
+      if (SRC == 0) {
+        const float yv = y[rowc];
+        const float wv = sw ? sw[rowc] : 1.f;
+        yy[j] = ok ? yv : 0.f;
+        ww[j] = ok ? wv : 0.f;
+      } else {
+        ww[j] = ok ? 1.f : 0.f;
+      }
+    }
+    float dot[UNROLL], dtrue[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      float d = 0.f, dt = 0.f;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        float x[8];
+        unpack8(xv[u][k], x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          d = fmaf(x[j], w[k][j], d);
+          if (SRC == 1) dt = fmaf(x[j], wt[k][j], dt);
+        }
+      }
+      dot[u] = d;
+      dtrue[u] = dt;
+    }
+    RR::run(dot, c);
+    if (SRC == 1) {
+      RR::run(dtrue, c);
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const int64_t row = base + (ubase + j) * G + g;
+        yy[j] = synth_label(row_key(seed, row0 + row), dtrue[j] + btrue);
+      }
+    }
+    float res[NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const float m = dot[j] + intercept;
+      float r, l;
+      if (LOSS == LOSS_LOGISTIC) {
+        const float e = __expf(-fabsf(m));
+        const float inv = 1.0f / (1.0f + e);
+        const float p = m >= 0.f ? inv : e * inv;   // sigmoid(m)
+        r = (p - yy[j]) * ww[j];
+        l = ww[j] * (fmaxf(m, 0.f) + __logf(1.0f + e) - yy[j] * m);
+      } else if (LOSS == LOSS_HINGE) {
+        const float s = 2.f * yy[j] - 1.f;
+        const float mg = 1.f - s * m;
+        r = mg > 0.f ? -s * ww[j] : 0.f;
+        l = mg > 0.f ? ww[j] * mg : 0.f;
+      } else {
+        const float e = m - yy[j];
+        r = e * ww[j];
+        l = 0.5f * ww[j] * e * e;
+      }
+      res[j] = r;
+      if (rep) { acc_r += r; acc_loss += l; acc_w += ww[j]; }
+    }
+    // Re-unpack from the packed registers for X^T r instead of keeping 8*UNROLL*CPL
+    // unpacked floats live across the reduction (halves the VGPR footprint).
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) asm volatile("" : "+v"(xv[u][k]));
+    // broadcast each row's residual back to its LPR lanes, accumulate X^T r
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const float r = __shfl(res[u % NF], g * LPR + RR::owner(u), kWave);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        float x[8];
+        unpack8(xv[u][k], x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(r, x[j], acc[k][j]);
+      }
+    }
+  }
+
+  // Sum the G row groups of the wave (lanes c, c+LPR, ...), then the 4 waves via LDS.
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = acc[k][j];
+#pragma unroll
+      for (int off = LPR; off < kWave; off <<= 1) v += __shfl_xor(v, off, kWave);
+      acc[k][j] = v;
+    }
+  acc_r = wave_sum(acc_r);
+  acc_loss = wave_sum(acc_loss);
+  acc_w = wave_sum(acc_w);
+
+  __shared__ float red[kWavesPerBlock][DP + 4];
+  if (lane < LPR) {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wid][8 * (c + k * LPR) + j] = acc[k][j];
+  }
+  if (lane == 0) {
+    red[wid][DP] = acc_r;
+    red[wid][DP + 1] = acc_loss;
+    red[wid][DP + 2] = acc_w;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < DP + 3; i += kBlock) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < kWavesPerBlock; ++q) s += red[q][i];
+    partial[(int64_t)blockIdx.x * pstride + i] = s;
+  }
+}
+
+// Materialise synthetic rows [row0, row0+n) into X (bf16) and labels y.
+template <int LPR, int CPL>
+__global__ __launch_bounds__(kBlock) void synth_glm_kernel(
+    uint16_t* __restrict__ X, int64_t ld, int64_t n, float* __restrict__ y, uint32_t seed,
+    int64_t row0, const float* __restrict__ wtrue, float btrue) {
+  constexpr int G = kWave / LPR;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, c = lane % LPR;
+  float wt[CPL][8];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = 8 * (c + k * LPR) + j;
+      wt[k][j] = col < ld ? wtrue[col] : 0.f;
+    }
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  const int64_t ntiles = (n + G - 1) / G;
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    const int64_t row = t * G + g;
+    const bool ok = row < n;
+    const uint32_t rk = row_key(seed, row0 + row);
+    float dt = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      const int ch = c + k * LPR;
+      if (8 * ch < ld) {
+        short8 v = synth_chunk(rk, ch);
+        float x[8];
+        unpack8(v, x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dt = fmaf(x[j], wt[k][j], dt);
+        if (ok) *reinterpret_cast<short8*>(X + row * ld + 8 * ch) = v;
+      }
+    }
+    dt = group_sum<LPR>(dt);
+    if (ok && c == 0) y[row] = synth_label(rk, dt + btrue);
+  }
+}
+
+// margins[i] = x_i . coef + intercept (model.transform / predict path).
+template <int LPR, int CPL>
+__global__ __launch_bounds__(kBlock) void glm_margin_kernel(
+    const uint16_t* __restrict__ X, int64_t ld, int64_t n, const float* __restrict__ coef,
+    float intercept, float* __restrict__ out) {
+  constexpr int G = kWave / LPR;
+  constexpr int UNROLL = CPL >= 8 ? 1 : 8 / CPL;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int g = lane / LPR, c = lane % LPR;
+  const int nch = (int)(ld / 8);
+  float w[CPL][8];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = 8 * (c + k * LPR) + j;
+      w[k][j] = col < ld ? coef[col] : 0.f;
+    }
+  const int64_t gw = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kWave;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) / kWave;
+  const int64_t RT = (int64_t)G * UNROLL;
+  const int64_t ntiles = (n + RT - 1) / RT;
+  for (int64_t t = gw; t < ntiles; t += nw) {
+    short8 xv[UNROLL][CPL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t row = t * RT + u * G + g;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int ch = c + k * LPR;
+        xv[u][k] = (row < n && ch < nch)
+                       ? *reinterpret_cast<const short8*>(X + row * ld + 8 * ch)
+                       : short8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t row = t * RT + u * G + g;
+      float d = 0.f;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        float x[8];
+        unpack8(xv[u][k], x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d = fmaf(x[j], w[k][j], d);
+      }
+      d = group_sum<LPR>(d);
+      if (row < n && c == 0) out[row] = d + intercept;
+    }
+  }
+}
+
+// out[i] = sum_b partial[b][i] in fp64, fixed order (deterministic).
+__global__ void glm_finish_kernel(const float* __restrict__ partial, int nblocks, int pstride,
+                                  int ncols, double* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ncols) return;
+  double s = 0.0;
+  for (int b = 0; b < nblocks; ++b) s += (double)partial[(int64_t)b * pstride + i];
+  out[i] = s;
+}
+
+int pick_lpr(int nch) {
+  int l = 4;
+  while (l < nch && l < 64) l <<= 1;
+  return l;
+}
+int pick_cpl(int nch) {
+  if (nch <= 64) return 1;
+  const int need = (nch + 63) / 64;
+  int c = 2;
+  while (c < need) c <<= 1;
+  return c;  // 2,4,8,16 (caller checks <= 16)
+}
+
+template <int LPR, int CPL, int LOSS, int SRC>
+void launch_grad(int grid, hipStream_t st, const uint16_t* X, int64_t ld, int64_t n,
+                 const float* y, const float* sw, const float* coef, float b, uint32_t seed,
+                 int64_t row0, const float* wt, float bt, float* partial, int pstride) {
+  // rows in flight per lane: 8 loads for the streaming pass; the lineage pass keeps
+  // fewer chunks live (its hash work, not memory latency, is the limiter)
+  constexpr int UNROLL = SRC == 1 ? (CPL >= 4 ? 1 : 4 / CPL) : (CPL == 1 ? 8 : (CPL == 2 ? 2 : 1));
+  hipLaunchKernelGGL((glm_grad_kernel<LPR, CPL, UNROLL, LOSS, SRC>), dim3(grid), dim3(kBlock), 0,
+                     st, X, ld, n, y, sw, coef, b, seed, row0, wt, bt, partial, pstride);
+}
+
+template <int LOSS, int SRC>
+int dispatch_grad(int lpr, int cpl, int grid, hipStream_t st, const uint16_t* X, int64_t ld,
+                  int64_t n, const float* y, const float* sw, const float* coef, float b,
+                  uint32_t seed, int64_t row0, const float* wt, float bt, float* partial,
+                  int pstride) {
+#define O3S_G(L, C)                                                                         \
+  if (lpr == L && cpl == C) {                                                               \
+    launch_grad<L, C, LOSS, SRC>(grid, st, X, ld, n, y, sw, coef, b, seed, row0, wt, bt,   \
+                                 partial, pstride);                                         \
+    return 0;                                                                               \
+  }
+  O3S_G(4, 1) O3S_G(8, 1) O3S_G(16, 1) O3S_G(32, 1) O3S_G(64, 1)
+  O3S_G(64, 2) O3S_G(64, 4) O3S_G(64, 8) O3S_G(64, 16)
+#undef O3S_G
+  return -1;
+}
+
+}  // namespace
+
+// Number of fp32 slots per partial-slab row and the padded width for `ld`.
+O3S_API int o3s_glm_layout(int64_t ld, int* dpad, int* pstride) {
+  const int nch = (int)(ld / 8);
+  const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
+  if (ld % 8 != 0 || cpl > 16) return -1;
+  *dpad = lpr * cpl * 8;
+  *pstride = *dpad + 4;
+  return 0;
+}
+
+// Gradient/loss pass.  out (fp64, dpad+3): [grad (dpad) | sum r | loss | weight sum].
+// partial must hold grid * pstride floats.  src: 0 = X in memory, 1 = synthetic lineage.
+O3S_API int o3s_glm_grad(int loss, int src, const void* X, int64_t ld, int64_t n, const float* y,
+                         const float* sw, const float* coef, float intercept, uint32_t seed,
+                         int64_t row0, const float* wtrue, float btrue, float* partial,
+                         int grid, double* out, hipStream_t st) {
+  const int nch = (int)(ld / 8);
+  const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
+  if (ld % 8 != 0 || cpl > 16 || grid <= 0) return -1;
+  const int dpad = lpr * cpl * 8, pstride = dpad + 4;
+  const uint16_t* Xh = (const uint16_t*)X;
+  int rc = -1;
+  if (n > 0) {
+    if (src == 0) {
+      if (loss == LOSS_LOGISTIC)
+        rc = dispatch_grad<LOSS_LOGISTIC, 0>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+      else if (loss == LOSS_HINGE)
+        rc = dispatch_grad<LOSS_HINGE, 0>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+      else
+        rc = dispatch_grad<LOSS_SQUARED, 0>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+    } else {
+      if (loss == LOSS_LOGISTIC)
+        rc = dispatch_grad<LOSS_LOGISTIC, 1>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+      else if (loss == LOSS_HINGE)
+        rc = dispatch_grad<LOSS_HINGE, 1>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+      else
+        rc = dispatch_grad<LOSS_SQUARED, 1>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+    }
+    if (rc != 0) return rc;
+  } else {
+    hipMemsetAsync(partial, 0, sizeof(float) * pstride * (size_t)grid, st);
+  }
+  O3S_CHECK_LAUNCH();
+  const int ncols = dpad + 3;
+  hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 255) / 256), dim3(256), 0, st, partial, grid,
+                     pstride, ncols, out);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+O3S_API int o3s_synth_glm(void* X, int64_t ld, int64_t n, float* y, uint32_t seed, int64_t row0,
+                          const float* wtrue, float btrue, int grid, hipStream_t st) {
+  const int nch = (int)(ld / 8);
+  const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
+  if (ld % 8 != 0 || cpl > 16) return -1;
+  if (n <= 0) return 0;
+  uint16_t* Xh = (uint16_t*)X;
+#define O3S_S(L, C)                                                                           \
+  if (lpr == L && cpl == C) {                                                                 \
+    hipLaunchKernelGGL((synth_glm_kernel<L, C>), dim3(grid), dim3(kBlock), 0, st, Xh, ld, n, y, \
+                       seed, row0, wtrue, btrue);                                             \
+    O3S_CHECK_LAUNCH();                                                                       \
+    return 0;                                                                                 \
+  }
+  O3S_S(4, 1) O3S_S(8, 1) O3S_S(16, 1) O3S_S(32, 1) O3S_S(64, 1)
+  O3S_S(64, 2) O3S_S(64, 4) O3S_S(64, 8) O3S_S(64, 16)
+#undef O3S_S
+  return -1;
+}
+
+O3S_API int o3s_glm_margin(const void* X, int64_t ld, int64_t n, const float* coef,
+                           float intercept, float* out, int grid, hipStream_t st) {
+  const int nch = (int)(ld / 8);
+  const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
+  if (ld % 8 != 0 || cpl > 16) return -1;
+  if (n <= 0) return 0;
+  const uint16_t* Xh = (const uint16_t*)X;
+#define O3S_M(L, C)                                                                            \
+  if (lpr == L && cpl == C) {                                                                  \
+    hipLaunchKernelGGL((glm_margin_kernel<L, C>), dim3(grid), dim3(kBlock), 0, st, Xh, ld, n,   \
+                       coef, intercept, out);                                                  \
+    O3S_CHECK_LAUNCH();                                                                        \
+    return 0;                                                                                  \
+  }
+  O3S_M(4, 1) O3S_M(8, 1) O3S_M(16, 1) O3S_M(32, 1) O3S_M(64, 1)
+  O3S_M(64, 2) O3S_M(64, 4) O3S_M(64, 8) O3S_M(64, 16)
+#undef O3S_M
+  return -1;
+}

@@ -1,0 +1,241 @@
+"""GLM streaming ops: fused gradient/loss pass, margins, synthetic row generation.
+
+GPU tensors dispatch to ``csrc/glm.hip``; CPU tensors use the PyTorch reference
+implementations below (fp64 math), which also serve as the numerics oracle in the
+tests (kernel vs plain fp32/fp64 PyTorch of the same op).
+
+Loss ids match the kernel: 0 logistic (y in {0,1}), 1 hinge (y in {0,1}, LinearSVC),
+2 squared (LinearRegression).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+LOSS_LOGISTIC, LOSS_HINGE, LOSS_SQUARED = 0, 1, 2
+_MASK = 0xFFFFFFFF
+
+
+def padded_width(d: int) -> int:
+    """Row stride (elements) used for bf16 feature matrices: multiple of 8 (16 B)."""
+    return max(8, (d + 7) // 8 * 8)
+
+
+def layout(ld: int) -> tuple[int, int]:
+    """(dpad, pstride) of the gradient kernel for row stride ``ld`` (mirrors o3s_glm_layout)."""
+    nch = ld // 8
+    lpr = 4
+    while lpr < nch and lpr < 64:
+        lpr <<= 1
+    cpl = 1
+    if nch > 64:
+        need = (nch + 63) // 64
+        cpl = 2
+        while cpl < need:
+            cpl <<= 1
+    if cpl > 16:
+        raise ValueError(f"feature dimension {ld} too large for the fused GLM kernel")
+    dpad = lpr * cpl * 8
+    return dpad, dpad + 4
+
+
+# --------------------------------------------------------------------------- hashing
+def _fmix32(h: torch.Tensor) -> torch.Tensor:
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & _MASK
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & _MASK
+    return h ^ (h >> 16)
+
+
+def row_keys(seed: int, rows: torch.Tensor) -> torch.Tensor:
+    lo = rows & _MASK
+    hi = rows >> 32
+    inner = (lo * 0x9E3779B1 + hi * 0x7FEB352D + 0x165667B1) & _MASK
+    return _fmix32((seed & _MASK) ^ _fmix32(inner))
+
+
+def _u16_unit(bits: torch.Tensor) -> torch.Tensor:
+    v = bits & 0xFFFF
+    v = torch.where(v >= 0x8000, v - 0x10000, v)
+    return v.to(torch.float32) * (1.0 / 32768.0)
+
+
+def synth_features_torch(rk: torch.Tensor, ld: int, d: int) -> torch.Tensor:
+    """bf16 [n, ld] features for row keys ``rk`` (int64 [n]).
+
+    All ``ld`` columns are generated (synthetic widths are rounded up to a multiple of 8;
+    the ground-truth weights of columns >= d are zero, so those are pure noise features).
+    """
+    n = rk.shape[0]
+    pairs = torch.arange(ld // 2, dtype=torch.int64, device=rk.device)  # (ch*4+p) == col//2
+    h = _fmix32((rk[:, None] + pairs[None, :] * 0x9E3779B9) & _MASK)
+    lo = _u16_unit(h)
+    hi = _u16_unit(h >> 16)
+    return torch.stack([lo, hi], dim=-1).reshape(n, ld).to(torch.bfloat16)
+
+
+def synth_labels_torch(rk: torch.Tensor, margin_true: torch.Tensor) -> torch.Tensor:
+    u = (_fmix32(rk ^ 0xA511E9B3) >> 8).to(torch.float32) * (1.0 / 16777216.0)
+    return (u < torch.sigmoid(margin_true.to(torch.float32))).to(torch.float32)
+
+
+def synth_truth(seed: int, d: int, ld: int | None = None) -> tuple[torch.Tensor, float]:
+    """Ground-truth separating hyperplane for synthetic classification data."""
+    ld = ld or padded_width(d)
+    rng = np.random.default_rng(seed ^ 0x5EED)
+    w = np.zeros(ld, dtype=np.float32)
+    # features are U[-1,1) (var 1/3): scale so the true margin has std ~2
+    w[:d] = rng.standard_normal(d).astype(np.float32) * np.float32(np.sqrt(12.0 / max(d, 1)))
+    b = float(rng.standard_normal() * 0.25)
+    return torch.from_numpy(w), b
+
+
+def synth_glm(n: int, d: int, seed: int, row0: int = 0, device="cpu", ld: int | None = None,
+              wtrue: torch.Tensor | None = None, btrue: float | None = None):
+    """Materialise synthetic rows [row0, row0+n): (X bf16 [n, ld], y f32 [n])."""
+    ld = ld or padded_width(d)
+    if wtrue is None:
+        wtrue, btrue = synth_truth(seed, d, ld)
+    device = torch.device(device)
+    X = torch.empty((n, ld), dtype=torch.bfloat16, device=device)
+    y = torch.empty((n,), dtype=torch.float32, device=device)
+    if n == 0:
+        return X, y
+    if device.type == "cuda":
+        lib = N.kernels()
+        wt = wtrue.to(device=device, dtype=torch.float32).contiguous()
+        grid = N.grid_for(device, n, 256)
+        N.check(lib.o3s_synth_glm(X.data_ptr(), ld, n, y.data_ptr(), seed & _MASK, row0,
+                                  wt.data_ptr(), float(btrue), grid, N.stream_of(X)), "synth_glm")
+        return X, y
+    step = 1 << 16
+    for s in range(0, n, step):
+        e = min(n, s + step)
+        rk = row_keys(seed, torch.arange(row0 + s, row0 + e, dtype=torch.int64))
+        xs = synth_features_torch(rk, ld, d)
+        X[s:e] = xs
+        y[s:e] = synth_labels_torch(rk, xs.float() @ wtrue.float() + btrue)
+    return X, y
+
+
+# --------------------------------------------------------------------------- gradient
+def _loss_terms(m: torch.Tensor, y: torch.Tensor, w: torch.Tensor, loss: int):
+    if loss == LOSS_LOGISTIC:
+        r = (torch.sigmoid(m) - y) * w
+        l = w * (torch.nn.functional.softplus(m) - y * m)
+    elif loss == LOSS_HINGE:
+        s = 2.0 * y - 1.0
+        mg = 1.0 - s * m
+        act = (mg > 0).to(m.dtype)
+        r = -s * w * act
+        l = w * mg * act
+    else:
+        e = m - y
+        r = e * w
+        l = 0.5 * w * e * e
+    return r, l
+
+
+def glm_grad_torch(X, y, sw, coef, intercept, loss: int) -> torch.Tensor:
+    """fp64 reference: [grad (ld) | sum r | loss | weight sum]."""
+    Xd = X.to(torch.float64)
+    m = Xd @ coef.to(torch.float64)[: X.shape[1]] + float(intercept)
+    yd = y.to(torch.float64)
+    w = torch.ones_like(yd) if sw is None else sw.to(torch.float64)
+    r, l = _loss_terms(m, yd, w, loss)
+    g = Xd.T @ r
+    return torch.cat([g, torch.stack([r.sum(), l.sum(), w.sum()])])
+
+
+class GlmWorkspace:
+    """Per-device scratch for the gradient pass (partial slabs + fp64 result)."""
+
+    def __init__(self, device: torch.device, ld: int, grid: int | None = None):
+        self.device = torch.device(device)
+        self.ld = ld
+        self.dpad, self.pstride = layout(ld)
+        self.grid = grid or (N.num_cus(self.device) * 8 if self.device.type == "cuda" else 1)
+        self.partial = torch.empty(self.grid * self.pstride, dtype=torch.float32, device=self.device)
+        self.out = torch.empty(self.dpad + 3, dtype=torch.float64, device=self.device)
+
+
+def glm_grad(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, coef: torch.Tensor,
+             intercept: float, loss: int, ws: GlmWorkspace | None = None) -> torch.Tensor:
+    """Fused margin -> loss -> X^T r pass.  Returns fp64 [grad (dpad) | sum r | loss | wsum].
+
+    ``coef`` is fp32 with at least ``ld`` entries (padded columns ignored).  The returned
+    tensor aliases the workspace buffer when one is given.
+    """
+    ld = X.shape[1]
+    if X.is_cuda:
+        if X.dtype != torch.bfloat16 or not X.is_contiguous():
+            raise TypeError("GPU GLM pass expects a contiguous bf16 feature matrix")
+        ws = ws or GlmWorkspace(X.device, ld)
+        cf = _coef_buf(coef, ws.dpad, X.device)
+        lib = N.kernels()
+        N.check(lib.o3s_glm_grad(loss, 0, X.data_ptr(), ld, X.shape[0], y.data_ptr(),
+                                 N.ptr(sw), cf.data_ptr(), float(intercept), 0, 0, None, 0.0,
+                                 ws.partial.data_ptr(), ws.grid, ws.out.data_ptr(),
+                                 N.stream_of(X)), "glm_grad")
+        return ws.out
+    dpad, _ = layout(ld)
+    ref = glm_grad_torch(X, y, sw, coef.to(torch.float64)[:ld], intercept, loss)
+    out = torch.zeros(dpad + 3, dtype=torch.float64)
+    out[:ld] = ref[:ld]
+    out[dpad:] = ref[ld:]
+    return out
+
+
+def glm_grad_synth(n: int, ld: int, d: int, seed: int, row0: int, wtrue: torch.Tensor,
+                   btrue: float, coef: torch.Tensor, intercept: float, loss: int,
+                   ws: GlmWorkspace) -> torch.Tensor:
+    """Gradient over synthetic rows regenerated in-kernel (lineage recompute)."""
+    if ws.device.type == "cuda":
+        cf = _coef_buf(coef, ws.dpad, ws.device)
+        wt = _coef_buf(wtrue, ws.dpad, ws.device, slot=1)
+        lib = N.kernels()
+        N.check(lib.o3s_glm_grad(loss, 1, None, ld, n, None, None, cf.data_ptr(), float(intercept),
+                                 seed & _MASK, row0, wt.data_ptr(), float(btrue),
+                                 ws.partial.data_ptr(), ws.grid, ws.out.data_ptr(),
+                                 torch.cuda.current_stream(ws.device).cuda_stream), "glm_grad_synth")
+        return ws.out
+    X, y = synth_glm(n, d, seed, row0, "cpu", ld, wtrue, btrue)
+    return glm_grad(X, y, None, coef, intercept, loss)
+
+
+_COEF_CACHE: dict = {}
+
+
+def _coef_buf(coef: torch.Tensor, dpad: int, device, slot: int = 0) -> torch.Tensor:
+    """fp32 coefficient vector zero-padded to dpad on ``device`` (reused buffer)."""
+    key = (str(device), dpad, slot)
+    buf = _COEF_CACHE.get(key)
+    if buf is None:
+        buf = torch.zeros(dpad, dtype=torch.float32, device=device)
+        _COEF_CACHE[key] = buf
+    k = min(coef.shape[0], dpad)
+    buf[:k].copy_(coef[:k], non_blocking=True)
+    if k < dpad:
+        buf[k:].zero_()
+    return buf
+
+
+def glm_margin(X: torch.Tensor, coef: torch.Tensor, intercept: float) -> torch.Tensor:
+    """margins = X . coef + intercept (fp32 [n])."""
+    ld = X.shape[1]
+    if X.is_cuda and X.dtype == torch.bfloat16 and X.is_contiguous():
+        dpad, _ = layout(ld)
+        cf = torch.zeros(dpad, dtype=torch.float32, device=X.device)
+        k = min(coef.shape[0], dpad)
+        cf[:k] = coef[:k].to(X.device, torch.float32)
+        out = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
+        lib = N.kernels()
+        grid = N.grid_for(X.device, X.shape[0], 64)
+        N.check(lib.o3s_glm_margin(X.data_ptr(), ld, X.shape[0], cf.data_ptr(), float(intercept),
+                                   out.data_ptr(), grid, N.stream_of(X)), "glm_margin")
+        return out
+    c = coef.to(X.device, torch.float64)[:ld]
+    return (X.to(torch.float64) @ c + float(intercept)).to(torch.float32)

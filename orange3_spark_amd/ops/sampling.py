@@ -1,0 +1,51 @@
+"""Counter-based row sampling (``df.sample`` / ``randomSplit`` / SGD minibatches).
+
+Spark samples per partition with a per-partition seeded RNG, so results change with
+the partitioning.  Here the draw for a row is a pure function of (seed, global row
+index) via the same fmix32 hash as the synthetic generators: a sample is identical on
+1, 2, 4 or 8 GPUs.  Elementwise on device tensors (trivially HBM bound; torch ops are
+adequate here, SURVEY §2.8 row `df.sample`).
+"""
+from __future__ import annotations
+
+import torch
+
+from .glm import _fmix32, row_keys
+
+_MASK = 0xFFFFFFFF
+
+
+def uniform(rows: torch.Tensor, seed: int, stream: int = 0) -> torch.Tensor:
+    """U[0,1) float64 per global row index."""
+    k = row_keys((seed * 0x2545F491 + stream * 0x9E3779B9) & _MASK, rows)
+    k2 = _fmix32(k ^ 0x68E31DA4)
+    hi = (k >> 5).to(torch.float64)          # 27 bits
+    lo = (k2 >> 6).to(torch.float64)         # 26 bits
+    return (hi * 67108864.0 + lo) * (1.0 / 9007199254740992.0)
+
+
+def bernoulli_mask(rows: torch.Tensor, seed: int, fraction: float) -> torch.Tensor:
+    if fraction >= 1.0:
+        return torch.ones_like(rows, dtype=torch.bool)
+    if fraction <= 0.0:
+        return torch.zeros_like(rows, dtype=torch.bool)
+    return uniform(rows, seed) < fraction
+
+
+def poisson_counts(rows: torch.Tensor, seed: int, lam: float) -> torch.Tensor:
+    """Poisson(lam) draw per row by inversion of the CDF (lam is small for sampling)."""
+    if lam <= 0:
+        return torch.zeros_like(rows)
+    u = uniform(rows, seed, stream=1)
+    k = torch.zeros_like(rows)
+    p = torch.exp(torch.tensor(-lam, dtype=torch.float64, device=rows.device)).expand_as(u).clone()
+    cdf = p.clone()
+    kmax = int(lam + 12 * (lam ** 0.5) + 12)
+    for i in range(1, kmax + 1):
+        more = u > cdf
+        if not bool(more.any()):
+            break
+        k = k + more.to(k.dtype)
+        p = p * (lam / i)
+        cdf = cdf + p
+    return k

@@ -1,0 +1,263 @@
+"""Collective communication for row-sharded (data-parallel) training.
+
+Replaces Spark's ``treeAggregate`` / broadcast / shuffle between YARN executors
+(SURVEY §2.9).  Design, MI355X-first:
+
+* one process per GPU (``torchrun``-style env: RANK / LOCAL_RANK / WORLD_SIZE);
+* ``torch.distributed`` with backend ``"nccl"`` -- on ROCm that *is* RCCL running over
+  the xGMI point-to-point links -- for device tensors, ``gloo`` for CPU tensors and
+  the multi-process CPU tests;
+* estimators aggregate **one flat buffer per step** (gradient + loss + weight sum in a
+  single fp64 vector, KMeans sums+counts, histogram slabs): xGMI rings are per-link
+  bound and small messages are latency bound, so fewer larger collectives win
+  (:meth:`Comm.all_reduce_coalesced` packs several tensors into one launch);
+* :class:`LocalComm` is the world_size==1 fast path (all collectives are identity).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+import pickle
+from typing import Any, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+class Comm:
+    """Interface.  All methods are collective: every rank must call them in order."""
+
+    rank: int = 0
+    world_size: int = 1
+    device: torch.device = torch.device("cpu")
+    backend: str = "local"
+
+    # -- tensor collectives (in place unless stated) --------------------------------
+    def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        raise NotImplementedError
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate equally-sized shards along dim 0 (rank order)."""
+        raise NotImplementedError
+
+    def all_gather_v(self, t: torch.Tensor) -> torch.Tensor:
+        """Concatenate variable-length shards along dim 0 (rank order)."""
+        raise NotImplementedError
+
+    def reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
+        raise NotImplementedError
+
+    def all_to_all_v(self, send: torch.Tensor, send_counts: Sequence[int]) -> tuple[torch.Tensor, list[int]]:
+        """Exchange row blocks: rows [sum(c[:r]), sum(c[:r+1])) go to rank r."""
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        raise NotImplementedError
+
+    # -- python objects ---------------------------------------------------------
+    def all_gather_object(self, obj: Any) -> list:
+        raise NotImplementedError
+
+    def broadcast_object(self, obj: Any, src: int = 0) -> Any:
+        raise NotImplementedError
+
+    # -- helpers ----------------------------------------------------------------
+    def all_reduce_coalesced(self, tensors: Sequence[torch.Tensor], op: str = "sum") -> list[torch.Tensor]:
+        """Pack tensors of one dtype/device into a single buffer -> one collective."""
+        if self.world_size == 1 or not tensors:
+            return list(tensors)
+        flat = torch.cat([t.reshape(-1) for t in tensors])
+        self.all_reduce(flat, op)
+        out, off = [], 0
+        for t in tensors:
+            k = t.numel()
+            t.copy_(flat[off:off + k].view_as(t))
+            out.append(t)
+            off += k
+        return out
+
+    def sum_scalar(self, x: float | int) -> float | int:
+        if self.world_size == 1:
+            return x
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
+        self.all_reduce(t)
+        v = t.item()
+        return int(round(v)) if isinstance(x, int) else v
+
+    def max_scalar(self, x: float) -> float:
+        if self.world_size == 1:
+            return x
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
+        self.all_reduce(t, "max")
+        return t.item()
+
+    @property
+    def is_driver(self) -> bool:
+        return self.rank == 0
+
+
+class LocalComm(Comm):
+    """Single process, single device: every collective is the identity."""
+
+    def __init__(self, device: torch.device | str = "cpu"):
+        self.device = torch.device(device)
+        self.rank, self.world_size, self.backend = 0, 1, "local"
+
+    def all_reduce(self, t, op="sum"):
+        return t
+
+    def all_gather(self, t):
+        return t
+
+    def all_gather_v(self, t):
+        return t
+
+    def reduce_scatter(self, t):
+        return t
+
+    def broadcast(self, t, src=0):
+        return t
+
+    def all_to_all_v(self, send, send_counts):
+        return send, [int(send.shape[0])]
+
+    def barrier(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def all_gather_object(self, obj):
+        return [obj]
+
+    def broadcast_object(self, obj, src=0):
+        return obj
+
+
+_OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN,
+        "prod": dist.ReduceOp.PRODUCT}
+
+
+class TorchComm(Comm):
+    """torch.distributed process group: RCCL (backend "nccl") on GPU, gloo on CPU.
+
+    On a GPU node a second gloo group is created for CPU-side object traffic so python
+    object collectives never allocate device memory.
+    """
+
+    def __init__(self, device: torch.device, backend: str | None = None, group=None):
+        self.device = torch.device(device)
+        if not dist.is_initialized():
+            init_process_group(self.device, backend)
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world_size = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+        self._cpu_group = None
+        if self.backend != "gloo":
+            self._cpu_group = dist.new_group(backend="gloo")
+
+    def all_reduce(self, t, op="sum"):
+        if self.world_size > 1:
+            dist.all_reduce(t, op=_OPS[op], group=self.group)
+        return t
+
+    def all_gather(self, t):
+        if self.world_size == 1:
+            return t
+        t = t.contiguous()
+        out = torch.empty((self.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t, group=self.group)
+        return out
+
+    def all_gather_v(self, t):
+        if self.world_size == 1:
+            return t
+        sizes = self.all_gather_object(int(t.shape[0]))
+        m = max(sizes)
+        pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[: t.shape[0]] = t
+        full = self.all_gather(pad)
+        parts = [full[r * m: r * m + s] for r, s in enumerate(sizes)]
+        return torch.cat(parts) if parts else t
+
+    def reduce_scatter(self, t):
+        if self.world_size == 1:
+            return t
+        k = t.shape[0] // self.world_size
+        out = torch.empty((k,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
+        return out
+
+    def broadcast(self, t, src=0):
+        if self.world_size > 1:
+            dist.broadcast(t, src=src, group=self.group)
+        return t
+
+    def all_to_all_v(self, send, send_counts):
+        if self.world_size == 1:
+            return send, [int(send.shape[0])]
+        counts = torch.tensor(list(send_counts), dtype=torch.int64)
+        all_counts = self.all_gather_object(counts.tolist())
+        recv_counts = [all_counts[r][self.rank] for r in range(self.world_size)]
+        out = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
+        dist.all_to_all_single(out, send.contiguous(), output_split_sizes=recv_counts,
+                               input_split_sizes=list(map(int, send_counts)), group=self.group)
+        return out, recv_counts
+
+    def barrier(self):
+        if self.world_size > 1:
+            if self.device.type == "cuda":
+                dist.barrier(group=self.group, device_ids=[self.device.index])
+            else:
+                dist.barrier(group=self.group)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def all_gather_object(self, obj):
+        if self.world_size == 1:
+            return [obj]
+        out = [None] * self.world_size
+        dist.all_gather_object(out, obj, group=self._cpu_group or self.group)
+        return out
+
+    def broadcast_object(self, obj, src=0):
+        if self.world_size == 1:
+            return obj
+        buf = [obj]
+        dist.broadcast_object_list(buf, src=src, group=self._cpu_group or self.group)
+        return buf[0]
+
+
+def env_world() -> tuple[int, int, int]:
+    """(rank, local_rank, world_size) from torchrun-style environment variables."""
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    return rank, local, world
+
+
+def init_process_group(device: torch.device, backend: str | None = None, timeout_s: int = 1800) -> None:
+    if dist.is_initialized():
+        return
+    rank, _, world = env_world()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    if backend is None:
+        backend = "nccl" if device.type == "cuda" else "gloo"
+    kw = dict(backend=backend, rank=rank, world_size=world,
+              timeout=datetime.timedelta(seconds=timeout_s))
+    if device.type == "cuda":
+        kw["device_id"] = device
+    dist.init_process_group(**kw)
+
+
+def make_comm(device: torch.device | str, world_size: int | None = None) -> Comm:
+    device = torch.device(device)
+    _, _, world = env_world()
+    if world_size is not None:
+        world = world_size
+    if world <= 1 and not dist.is_initialized():
+        return LocalComm(device)
+    return TorchComm(device)

@@ -1,0 +1,300 @@
+"""Session: the engine entry point (replaces SparkContext + HiveContext/SparkSession).
+
+In the reference a single process-global pair ``sc``/``hc`` is created by the Context
+widget (orangecontrib/spark/widgets/data/spark_context.py:68-78) and shared through
+class attributes (orangecontrib/spark/base/shared_spark_context.py:9-27).  Here:
+
+* a Session owns the device of this process (``cuda:LOCAL_RANK`` on MI355X, else CPU),
+  the communicator (RCCL via torch.distributed when WORLD_SIZE > 1), the catalog
+  ("Hive" tables in a parquet warehouse) and the SQL engine;
+* one process per GPU: under ``torchrun --nproc-per-node 8`` every rank creates the
+  same Session and holds 1/8 of every DataFrame's rows (SPMD, like Spark executors but
+  with the driver program replicated);
+* ``Session.getOrCreate()`` / ``Session.active()`` give the process-global instance
+  the widgets share (``SharedSession`` mixin in the add-on).
+"""
+from __future__ import annotations
+
+import logging
+import threading
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from .conf import SessionConf
+from .frame import column as C
+from .frame.dataframe import DataFrame, Row
+from .parallel.comm import LocalComm, env_world, make_comm
+
+log = logging.getLogger("orange3_spark_amd")
+
+__version__ = "0.1.0"
+
+
+class Session:
+    _active: "Session | None" = None
+    _lock = threading.Lock()
+
+    def __init__(self, conf: SessionConf | None = None, comm=None, device=None):
+        self.conf = conf.copy() if conf is not None else SessionConf()
+        self.device = torch.device(device) if device is not None else self._pick_device()
+        if comm is None:
+            master = self.conf.master().lower()
+            rank, local, world = env_world()
+            comm = make_comm(self.device) if (world > 1 or master == "spmd") else LocalComm(self.device)
+        self.comm = comm
+        if self.conf.get("spark.master", "").lower() == "spmd":
+            want = int(self.conf.get("spark.executor.instances", str(self.comm.world_size)))
+            if want not in (1, self.comm.world_size):
+                log.warning("spark.executor.instances=%s but WORLD_SIZE=%s", want, self.comm.world_size)
+        from .catalog import Catalog
+        self.catalog = Catalog(self)
+        self._stopped = False
+        self.version = __version__
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+
+    # ------------------------------------------------------------------ lifecycle
+    def _pick_device(self) -> torch.device:
+        pref = self.conf.device_pref()
+        if pref == "cpu":
+            return torch.device("cpu")
+        if torch.cuda.is_available():
+            _, local, _ = env_world()
+            return torch.device("cuda", local % max(1, torch.cuda.device_count()))
+        if pref == "cuda":
+            raise RuntimeError("o3s.device=cuda but no GPU is visible")
+        return torch.device("cpu")
+
+    @classmethod
+    def getOrCreate(cls, conf: SessionConf | None = None) -> "Session":
+        with cls._lock:
+            if cls._active is None or cls._active._stopped:
+                cls._active = Session(conf)
+            elif conf is not None:
+                for k, v in conf.getAll():
+                    cls._active.conf.set(k, v)
+            return cls._active
+
+    @classmethod
+    def active(cls) -> "Session | None":
+        return cls._active if cls._active is not None and not cls._active._stopped else None
+
+    getActiveSession = active
+
+    def stop(self) -> None:
+        self._stopped = True
+        if Session._active is self:
+            Session._active = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.stop()
+
+    @property
+    def rank(self) -> int:
+        return self.comm.rank
+
+    @property
+    def world_size(self) -> int:
+        return self.comm.world_size
+
+    @property
+    def defaultParallelism(self) -> int:
+        return self.comm.world_size
+
+    @property
+    def sparkContext(self):
+        return self
+
+    @property
+    def appName(self):
+        return self.conf.get("spark.app.name")
+
+    def local_view(self) -> "Session":
+        """A view of this session whose collectives are local (replicated compute)."""
+        v = object.__new__(Session)
+        v.__dict__.update(self.__dict__)
+        v.comm = LocalComm(self.device)
+        return v
+
+    # ------------------------------------------------------------------ dtype policy
+    def vector_dtype(self) -> torch.dtype:
+        pref = self.conf.vector_dtype()
+        if pref == "auto":
+            return torch.bfloat16 if self.device.type == "cuda" else torch.float64
+        return {"bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float32": torch.float32,
+                "float": torch.float32, "float64": torch.float64, "double": torch.float64}[pref]
+
+    # ------------------------------------------------------------------ creation
+    def _shard_bounds(self, n: int) -> tuple[int, int]:
+        r, w = self.comm.rank, self.comm.world_size
+        return (n * r) // w, (n * (r + 1)) // w
+
+    def createDataFrame(self, data, schema=None, samplingRatio=None, verifySchema=True) -> DataFrame:
+        """Create a row-sharded DataFrame from host data.
+
+        Accepts a pandas DataFrame, a pyarrow Table, a list of Rows/tuples/dicts, a
+        2-D numpy array, a dict of column arrays, or an Orange-style Table (anything
+        with ``domain``/``X``).  Every rank is given the same host data (SPMD) and
+        keeps its contiguous slice.
+        """
+        from .io import arrow_to_columns
+        from .utils import data_utils
+        import pandas as pd
+        try:
+            import pyarrow as pa
+        except ImportError:  # pragma: no cover
+            pa = None
+        names = _schema_names(schema)
+        if hasattr(data, "domain") and hasattr(data, "X"):
+            data = data_utils.orange_to_pandas(data)
+        if pa is not None and isinstance(data, pa.Table):
+            n = data.num_rows
+            lo, hi = self._shard_bounds(n)
+            cols = arrow_to_columns(data.slice(lo, hi - lo), self)
+            return DataFrame(self, cols, hi - lo)
+        if isinstance(data, dict):
+            data = pd.DataFrame(data)
+        if isinstance(data, np.ndarray):
+            if data.ndim == 1:
+                data = data[:, None]
+            data = pd.DataFrame(data, columns=names or [f"_{i + 1}" for i in range(data.shape[1])])
+            names = None
+        if isinstance(data, (list, tuple)):
+            data = _rows_to_pandas(list(data), names)
+            names = None
+        if not isinstance(data, pd.DataFrame):
+            raise TypeError(f"cannot create a DataFrame from {type(data).__name__}")
+        if names:
+            data = data.copy()
+            data.columns = names
+        n = len(data)
+        lo, hi = self._shard_bounds(n)
+        part = data.iloc[lo:hi]
+        cols = OrderedDict()
+        for k in part.columns:
+            cols[str(k)] = C.from_numpy(part[k].to_numpy(), self.device)
+        df = DataFrame(self, cols, hi - lo)
+        if schema is not None and not isinstance(schema, (list, tuple)) and hasattr(schema, "fields"):
+            for f in schema.fields:
+                from .frame.types import NumericType
+                if f.name in df.columns and isinstance(f.dataType, NumericType):
+                    df = df.withColumn(f.name, df[f.name].cast(f.dataType))
+        return df
+
+    def range(self, start: int, end: int | None = None, step: int = 1, numPartitions=None) -> DataFrame:
+        if end is None:
+            start, end = 0, start
+        n = max(0, (end - start + step - 1) // step) if step > 0 else max(0, (start - end - step - 1) // (-step))
+        lo, hi = self._shard_bounds(n)
+        ids = torch.arange(lo, hi, dtype=torch.int64, device=self.device) * step + start
+        return DataFrame(self, OrderedDict(id=C.NumericColumn(ids)), hi - lo)
+
+    def emptyDataFrame(self) -> DataFrame:
+        return DataFrame(self, OrderedDict(), 0)
+
+    # ------------------------------------------------------------------ catalog / sql
+    def table(self, name: str) -> DataFrame:
+        return self.catalog.table(name)
+
+    def sql(self, query: str) -> DataFrame:
+        from .sql.engine import execute
+        return execute(self, query)
+
+    def tableNames(self, dbName: str | None = None) -> list[str]:
+        return self.catalog.tableNames(dbName)
+
+    def tables(self, dbName: str | None = None) -> DataFrame:
+        names = self.tableNames(dbName)
+        db = dbName or self.catalog.currentDatabase()
+        return self.createDataFrame({"database": [db] * len(names), "tableName": names,
+                                     "isTemporary": [n in self.catalog._temp for n in names]})
+
+    @property
+    def read(self):
+        from .io import DataFrameReader
+        return DataFrameReader(self)
+
+    @property
+    def synthetic(self):
+        from .synthetic import SyntheticData
+        return SyntheticData(self)
+
+    def __repr__(self):
+        return (f"Session(app={self.appName!r}, device={self.device}, rank={self.rank}/"
+                f"{self.world_size}, backend={self.comm.backend})")
+
+
+SparkSession = Session
+
+
+class _Builder:
+    def __init__(self):
+        self._conf = SessionConf()
+
+    def config(self, key=None, value=None, conf=None):
+        if conf is not None:
+            for k, v in conf.getAll():
+                self._conf.set(k, v)
+        if key is not None:
+            self._conf.set(key, value)
+        return self
+
+    def appName(self, name):
+        return self.config("spark.app.name", name)
+
+    def master(self, m):
+        return self.config("spark.master", m)
+
+    def enableHiveSupport(self):
+        return self
+
+    def getOrCreate(self) -> Session:
+        return Session.getOrCreate(self._conf)
+
+
+class _BuilderDescriptor:
+    def __get__(self, obj, owner):
+        return _Builder()
+
+
+Session.builder = _BuilderDescriptor()
+
+
+def _schema_names(schema):
+    if schema is None:
+        return None
+    if isinstance(schema, (list, tuple)):
+        return [s if isinstance(s, str) else s.name for s in schema]
+    if hasattr(schema, "names"):
+        return list(schema.names)
+    if isinstance(schema, str):
+        return [p.strip().split(" ")[0].split(":")[0] for p in schema.split(",")]
+    return None
+
+
+def _rows_to_pandas(rows: list, names):
+    import pandas as pd
+    if not rows:
+        return pd.DataFrame(columns=names or [])
+    first = rows[0]
+    if isinstance(first, Row) and first.__fields__:
+        return pd.DataFrame([tuple(r) for r in rows], columns=names or first.__fields__)
+    if isinstance(first, dict):
+        return pd.DataFrame(rows, columns=names)
+    if not isinstance(first, (list, tuple)):
+        rows = [(r,) for r in rows]
+        first = rows[0]
+    names = names or [f"_{i + 1}" for i in range(len(first))]
+    cols = list(zip(*rows))
+    data = OrderedDict()
+    for k, vals in zip(names, cols):
+        if any(hasattr(v, "toArray") for v in vals):
+            data[k] = pd.Series(list(vals), dtype=object)
+        else:
+            data[k] = list(vals)
+    return pd.DataFrame(data)
