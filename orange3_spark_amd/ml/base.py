@@ -1,0 +1,217 @@
+"""Estimator / Transformer / Model / Evaluator / Pipeline (``pyspark.ml`` base API).
+
+The reference's generic widgets call exactly these entry points:
+``method().fit(in_df, params=paramMap)`` (orangecontrib/spark/base/spark_ml_estimator.py:19-25),
+``method_instance.transform(in_df, params=paramMap)`` (base/spark_ml_transformer.py:129-139),
+``model.transform(df)`` (widgets/ml/spark_ml_model.py:53) and an Evaluator's
+``evaluate`` (widgets/ml/spark_ml_evaluation.py:42-78).  ``Pipeline``/``PipelineModel``
+are beyond-ref (BASELINE north star).
+"""
+from __future__ import annotations
+
+import os
+from abc import ABC, abstractmethod
+
+import torch
+
+from .param import Param, Params, TypeConverters, keyword_only, shared
+from .util import (MLReadable, MLWritable, MLWriter, apply_metadata, load_metadata, py_class, register,
+                   save_metadata)
+
+
+def _is_param_map(p) -> bool:
+    return isinstance(p, dict)
+
+
+class Transformer(Params, ABC):
+    """Abstract: transforms one DataFrame into another."""
+
+    def transform(self, dataset, params=None):
+        if params is None:
+            params = {}
+        if not _is_param_map(params):
+            raise TypeError(f"Params must be a param map but got {type(params)}.")
+        if params:
+            return self.copy(params)._transform(dataset)
+        return self._transform(dataset)
+
+    @abstractmethod
+    def _transform(self, dataset):
+        raise NotImplementedError
+
+
+class Estimator(Params, ABC):
+    """Abstract: fits a Model to a DataFrame."""
+
+    def fit(self, dataset, params=None):
+        if params is None:
+            params = {}
+        if isinstance(params, (list, tuple)):
+            return [self.fit(dataset, p) for p in params]
+        if not _is_param_map(params):
+            raise TypeError(f"Params must be either a param map or a list/tuple of param maps, but got {type(params)}.")
+        if params:
+            return self.copy(params)._fit(dataset)
+        return self._fit(dataset)
+
+    def fitMultiple(self, dataset, paramMaps):
+        for i, pm in enumerate(paramMaps):
+            yield i, self.fit(dataset, pm)
+
+    @abstractmethod
+    def _fit(self, dataset):
+        raise NotImplementedError
+
+
+class Model(Transformer, ABC):
+    """A fitted Transformer produced by an Estimator."""
+
+    parent = None
+
+    def _with_parent(self, est):
+        self.parent = est
+        # models inherit the estimator's param values (Spark copyValues)
+        est._copyValues(self)
+        return self
+
+
+class Evaluator(Params, ABC):
+    def evaluate(self, dataset, params=None):
+        if params is None:
+            params = {}
+        if params:
+            return self.copy(params)._evaluate(dataset)
+        return self._evaluate(dataset)
+
+    @abstractmethod
+    def _evaluate(self, dataset):
+        raise NotImplementedError
+
+    def isLargerBetter(self) -> bool:
+        return True
+
+
+class UnaryTransformer(Transformer, ABC):
+    """Applies a per-column function inputCol -> outputCol."""
+
+
+# ------------------------------------------------------------------ pipelines
+class _PipelineWriter(MLWriter):
+    def saveImpl(self, path):
+        inst = self.instance
+        stages = inst.getStages()
+        save_metadata(inst, path, paramMap={"stageUids": [s.uid for s in stages]})
+        digits = len(str(len(stages)))
+        for i, s in enumerate(stages):
+            sp = os.path.join(path, "stages", f"{i:0{digits}d}_{s.uid}")
+            s.write().saveImpl(sp) if hasattr(s, "write") else None
+
+
+def _load_stages(path, meta):
+    uids = meta["paramMap"]["stageUids"]
+    digits = len(str(len(uids)))
+    stages = []
+    for i, uid in enumerate(uids):
+        sp = os.path.join(path, "stages", f"{i:0{digits}d}_{uid}")
+        m = load_metadata(sp)
+        cls = py_class(m["class"])
+        if hasattr(cls, "_load_impl"):
+            stages.append(cls._load_impl(sp, m))
+        else:
+            inst = cls()
+            apply_metadata(inst, m)
+            stages.append(inst)
+    return stages
+
+
+@register("org.apache.spark.ml.Pipeline")
+class Pipeline(Estimator, MLWritable, MLReadable):
+    """A simple pipeline: a sequence of Estimator and Transformer stages."""
+
+    stages = shared("stages", "a list of pipeline stages")
+
+    @keyword_only
+    def __init__(self, *, stages=None):
+        super().__init__()
+        self._set(**self._input_kwargs)
+
+    def setStages(self, value):
+        return self._set(stages=value)
+
+    def getStages(self):
+        return list(self.getOrDefault(self.stages)) if self.isDefined(self.stages) else []
+
+    @keyword_only
+    def setParams(self, *, stages=None):
+        return self._set(**self._input_kwargs)
+
+    def _fit(self, dataset):
+        stages = self.getStages()
+        for s in stages:
+            if not isinstance(s, (Estimator, Transformer)):
+                raise TypeError(f"Cannot recognize a pipeline stage of type {type(s)}.")
+        last_est = max([i for i, s in enumerate(stages) if isinstance(s, Estimator)], default=-1)
+        models = []
+        df = dataset
+        for i, s in enumerate(stages):
+            if i <= last_est:
+                if isinstance(s, Transformer):
+                    models.append(s)
+                    df = s.transform(df)
+                else:
+                    m = s.fit(df)
+                    models.append(m)
+                    if i < last_est:
+                        df = m.transform(df)
+            else:
+                models.append(s)
+        return PipelineModel(models)._with_uid(self.uid)
+
+    def copy(self, extra=None):
+        that = super().copy(extra)
+        that._set(stages=[s.copy(extra) for s in self.getStages()])
+        return that
+
+    def write(self):
+        return _PipelineWriter(self)
+
+    @classmethod
+    def _load_impl(cls, path, meta):
+        p = Pipeline(stages=_load_stages(path, meta))
+        p.uid = meta["uid"]
+        return p
+
+
+@register("org.apache.spark.ml.PipelineModel")
+class PipelineModel(Model, MLWritable, MLReadable):
+    def __init__(self, stages=None):
+        super().__init__()
+        self.stages = list(stages or [])
+
+    def _with_uid(self, uid):
+        self.uid = uid
+        return self
+
+    def _transform(self, dataset):
+        df = dataset
+        for s in self.stages:
+            df = s.transform(df)
+        return df
+
+    def copy(self, extra=None):
+        return PipelineModel([s.copy(extra) for s in self.stages])._with_uid(self.uid)
+
+    def getStages(self):
+        return list(self.stages)
+
+    def write(self):
+        w = _PipelineWriter(self)
+        return w
+
+    @classmethod
+    def _load_impl(cls, path, meta):
+        return PipelineModel(_load_stages(path, meta))._with_uid(meta["uid"])
+
+
+# PipelineModel writer needs getStages + uid like Pipeline
+_ = TypeConverters, Param, torch

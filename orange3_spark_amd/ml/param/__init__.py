@@ -321,8 +321,8 @@ def _setter(pname):
 
 def add_accessors(cls):
     """Generate getX/setX for every Param declared on ``cls`` (if missing)."""
-    for n in list(vars(cls)):
-        if isinstance(vars(cls)[n], Param):
+    for n in list(dir(cls)):
+        if isinstance(getattr(cls, n, None), Param):
             cap = n[0].upper() + n[1:]
             if not hasattr(cls, "get" + cap):
                 setattr(cls, "get" + cap, _getter(n))

@@ -1,0 +1,291 @@
+"""Spark-ML-compatible persistence (``MLWritable`` / ``MLReadable``).
+
+Directory layout written by Spark's ``DefaultParamsWriter`` and model writers, which we
+reproduce so saved models interoperate with Spark tooling (beyond-ref: the reference
+has no model persistence at all, SURVEY §5 "Checkpoint / resume"):
+
+    <path>/metadata/part-00000     one-line JSON: class, timestamp, sparkVersion, uid,
+                                   paramMap, defaultParamMap
+    <path>/metadata/_SUCCESS
+    <path>/data/part-00000-*.parquet   model data (coefficients, centres, trees, ...)
+
+Model ``data`` schemas follow Spark's (e.g. LogisticRegressionModel: numClasses int,
+numFeatures int, interceptVector vector, coefficientMatrix matrix, isMultinomial
+boolean).  Vectors/matrices use Spark's VectorUDT/MatrixUDT parquet structs.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import time
+import uuid
+from typing import Any
+
+import numpy as np
+
+SPARK_VERSION = "3.5.1"
+
+# python class -> JVM class name and back (filled by register())
+_PY2JVM: dict[type, str] = {}
+_JVM2PY: dict[str, type] = {}
+
+
+def register(jvm_name: str):
+    def deco(cls):
+        _PY2JVM[cls] = jvm_name
+        _JVM2PY[jvm_name] = cls
+        cls._java_class = jvm_name
+        return cls
+    return deco
+
+
+def jvm_name(obj_or_cls) -> str:
+    cls = obj_or_cls if isinstance(obj_or_cls, type) else type(obj_or_cls)
+    return _PY2JVM.get(cls) or f"orange3_spark_amd.{cls.__module__.split('.')[-1]}.{cls.__name__}"
+
+
+def py_class(jvm: str) -> type:
+    if jvm in _JVM2PY:
+        return _JVM2PY[jvm]
+    # accept our own fallback names
+    for cls in _PY2JVM:
+        if jvm.endswith("." + cls.__name__):
+            return cls
+    raise ValueError(f"unknown saved class {jvm}")
+
+
+def _jsonable(v: Any):
+    from .linalg import DenseMatrix, Vector
+    if isinstance(v, Vector):
+        return {"type": 1, "values": np.asarray(v.toArray()).tolist()}
+    if isinstance(v, DenseMatrix):
+        return {"numRows": v.numRows, "numCols": v.numCols, "values": v.values.tolist()}
+    if isinstance(v, (np.floating,)):
+        return float(v)
+    if isinstance(v, (np.integer,)):
+        return int(v)
+    if isinstance(v, np.ndarray):
+        return v.tolist()
+    if isinstance(v, (list, tuple)):
+        return [_jsonable(x) for x in v]
+    if isinstance(v, (str, int, float, bool)) or v is None:
+        return v
+    if hasattr(v, "uid"):
+        return v.uid
+    return str(v)
+
+
+def _is_rank0() -> bool:
+    from ..session import Session
+    s = Session.active()
+    return s is None or s.comm.rank == 0
+
+
+def _barrier():
+    from ..session import Session
+    s = Session.active()
+    if s is not None and s.comm.world_size > 1:
+        s.comm.barrier()
+
+
+def prepare_path(path: str, overwrite: bool) -> None:
+    if _is_rank0():
+        if os.path.exists(path):
+            if not overwrite:
+                raise FileExistsError(f"Path {path} already exists. To overwrite it, please use write.overwrite().save(path)")
+            shutil.rmtree(path)
+        os.makedirs(path, exist_ok=True)
+    _barrier()
+
+
+def save_metadata(instance, path: str, extraMetadata: dict | None = None, paramMap: dict | None = None) -> None:
+    if not _is_rank0():
+        return
+    meta = {
+        "class": jvm_name(instance),
+        "timestamp": int(round(time.time() * 1000)),
+        "sparkVersion": SPARK_VERSION,
+        "uid": instance.uid,
+        "paramMap": paramMap if paramMap is not None else
+        {p.name: _jsonable(v) for p, v in instance._paramMap.items()},
+        "defaultParamMap": {p.name: _jsonable(v) for p, v in instance._defaultParamMap.items() if v is not None},
+    }
+    if extraMetadata:
+        meta.update(extraMetadata)
+    d = os.path.join(path, "metadata")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "part-00000"), "w") as f:
+        f.write(json.dumps(meta, separators=(",", ":")) + "\n")
+    open(os.path.join(d, "_SUCCESS"), "w").close()
+
+
+def load_metadata(path: str, expected_class: str | None = None) -> dict:
+    d = os.path.join(path, "metadata")
+    files = sorted(f for f in os.listdir(d) if f.startswith("part-"))
+    with open(os.path.join(d, files[0])) as f:
+        meta = json.loads(f.readline())
+    if expected_class and meta["class"] != expected_class:
+        raise ValueError(f"Error loading metadata: Expected class name {expected_class} but found class name {meta['class']}")
+    return meta
+
+
+def apply_metadata(instance, meta: dict) -> None:
+    """Restore uid + param values (skipping params this implementation lacks)."""
+    instance.uid = meta["uid"]
+    for p in instance.params:
+        p.parent = instance.uid
+    instance._params = None
+    for name, v in meta.get("defaultParamMap", {}).items():
+        if instance.hasParam(name):
+            instance._defaultParamMap[instance.getParam(name)] = _from_json(instance, name, v)
+    for name, v in meta.get("paramMap", {}).items():
+        if instance.hasParam(name):
+            instance._set(**{name: _from_json(instance, name, v)})
+
+
+def _from_json(instance, name, v):
+    from .linalg import DenseMatrix, DenseVector
+    if isinstance(v, dict) and "values" in v and "type" in v:
+        return DenseVector(v["values"])
+    if isinstance(v, dict) and "numRows" in v:
+        return DenseMatrix(v["numRows"], v["numCols"], v["values"])
+    return v
+
+
+def write_data(path: str, columns: dict, subdir: str = "data") -> None:
+    """Write one row-set of model data as a Spark-style parquet part file."""
+    if not _is_rank0():
+        return
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    d = os.path.join(path, subdir)
+    os.makedirs(d, exist_ok=True)
+    table = pa.table(columns) if not isinstance(columns, pa.Table) else columns
+    pq.write_table(table, os.path.join(d, f"part-00000-{uuid.uuid4()}-c000.snappy.parquet"), compression="snappy")
+    open(os.path.join(d, "_SUCCESS"), "w").close()
+
+
+def read_data(path: str, subdir: str = "data"):
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    d = os.path.join(path, subdir)
+    files = sorted(f for f in os.listdir(d) if f.endswith(".parquet"))
+    return pa.concat_tables([pq.read_table(os.path.join(d, f)) for f in files])
+
+
+# ------------------------------------------------------------ VectorUDT / MatrixUDT
+def vector_struct(v) -> dict:
+    from .linalg import SparseVector
+    if isinstance(v, SparseVector):
+        return {"type": 0, "size": v.size, "indices": v.indices.tolist(), "values": v.values.tolist()}
+    arr = np.asarray(v.toArray() if hasattr(v, "toArray") else v, dtype=np.float64)
+    return {"type": 1, "size": None, "indices": None, "values": arr.tolist()}
+
+
+def vector_from_struct(s):
+    from .linalg import DenseVector, SparseVector
+    if s["type"] == 0:
+        return SparseVector(s["size"], s["indices"], s["values"])
+    return DenseVector(s["values"])
+
+
+def matrix_arrow_type():
+    import pyarrow as pa
+    return pa.struct([("type", pa.int8()), ("numRows", pa.int32()), ("numCols", pa.int32()),
+                      ("colPtrs", pa.list_(pa.int32())), ("rowIndices", pa.list_(pa.int32())),
+                      ("values", pa.list_(pa.float64())), ("isTransposed", pa.bool_())])
+
+
+def matrix_struct(m) -> dict:
+    """Dense matrix in Spark MatrixUDT form (type 1 = dense, column-major values)."""
+    from .linalg import DenseMatrix
+    if not isinstance(m, DenseMatrix):
+        m = DenseMatrix.from_array(np.asarray(m))
+    return {"type": 1, "numRows": m.numRows, "numCols": m.numCols, "colPtrs": None, "rowIndices": None,
+            "values": m.values.tolist(), "isTransposed": m.isTransposed}
+
+
+def matrix_from_struct(s):
+    from .linalg import DenseMatrix
+    return DenseMatrix(s["numRows"], s["numCols"], s["values"], s["isTransposed"])
+
+
+def vec_col(vectors):
+    import pyarrow as pa
+    from ..io import vector_arrow_type
+    return pa.array([vector_struct(v) for v in vectors], type=vector_arrow_type())
+
+
+def mat_col(mats):
+    import pyarrow as pa
+    return pa.array([matrix_struct(m) for m in mats], type=matrix_arrow_type())
+
+
+# --------------------------------------------------------------------- writer API
+class MLWriter:
+    def __init__(self, instance):
+        self.instance = instance
+        self.shouldOverwrite = False
+
+    def overwrite(self):
+        self.shouldOverwrite = True
+        return self
+
+    def session(self, s):
+        return self
+
+    def option(self, k, v):
+        return self
+
+    def save(self, path: str):
+        prepare_path(path, self.shouldOverwrite)
+        self.saveImpl(path)
+        _barrier()
+
+    def saveImpl(self, path: str):
+        inst = self.instance
+        save_metadata(inst, path, getattr(inst, "_extra_metadata", lambda: None)())
+        if hasattr(inst, "_save_data"):
+            inst._save_data(path)
+
+
+class MLReader:
+    def __init__(self, cls):
+        self.cls = cls
+
+    def session(self, s):
+        return self
+
+    def load(self, path: str):
+        meta = load_metadata(path)
+        cls = py_class(meta["class"])
+        if not issubclass(cls, self.cls) and not issubclass(self.cls, cls):
+            raise ValueError(f"{path} holds a {meta['class']}, not a {self.cls.__name__}")
+        if hasattr(cls, "_load_impl"):
+            return cls._load_impl(path, meta)
+        inst = cls()
+        apply_metadata(inst, meta)
+        return inst
+
+
+class MLWritable:
+    def write(self) -> MLWriter:
+        return MLWriter(self)
+
+    def save(self, path: str) -> None:
+        self.write().save(path)
+
+
+class MLReadable:
+    @classmethod
+    def read(cls) -> MLReader:
+        return MLReader(cls)
+
+    @classmethod
+    def load(cls, path: str):
+        return cls.read().load(path)
+
+
+DefaultParamsWritable = MLWritable
+DefaultParamsReadable = MLReadable

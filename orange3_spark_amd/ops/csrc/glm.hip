@@ -380,6 +380,92 @@ __global__ __launch_bounds__(kBlock) void glm_margin_kernel(
   }
 }
 
+// Weighted column moments (Spark's MultivariateOnlineSummarizer subset used by the
+// GLM solvers for standardization): per column sum(w*x), sum(w*x^2), plus sum(w).
+// Same lane layout as the gradient pass; one slab row per block, fp64 finish.
+template <int LPR, int CPL, int SRC>
+__global__ __launch_bounds__(kBlock) void glm_colstats_kernel(
+    const uint16_t* __restrict__ X, int64_t ld, int64_t n, const float* __restrict__ sw,
+    uint32_t seed, int64_t row0, float* __restrict__ partial, int pstride) {
+  constexpr int G = kWave / LPR;
+  constexpr int UNROLL = CPL >= 4 ? 1 : 4 / CPL;
+  constexpr int DP = LPR * CPL * 8;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  const int g = lane / LPR, c = lane % LPR;
+  const int nch = (int)(ld / 8);
+  float s1[CPL][8], s2[CPL][8];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s1[k][j] = s2[k][j] = 0.f;
+  float sw_acc = 0.f;
+  const int64_t RT = (int64_t)G * UNROLL;
+  const int64_t ntiles = (n + RT - 1) / RT;
+  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
+  for (int64_t t = gw; t < ntiles; t += nw) {
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t row = t * RT + u * G + g;
+      const bool ok = row < n;
+      const int64_t rowc = ok ? row : n - 1;
+      const float wv = sw ? sw[rowc] : 1.f;
+      const float w = ok ? wv : 0.f;
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int ch = c + k * LPR;
+        const int chc = ch < nch ? ch : nch - 1;
+        short8 v = SRC == 0 ? __builtin_nontemporal_load(reinterpret_cast<const short8*>(X + rowc * ld + 8 * chc))
+                            : synth_chunk(row_key(seed, row0 + rowc), chc);
+        const float wk = ch < nch ? w : 0.f;
+        float x[8];
+        unpack8(v, x);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float wx = wk * x[j];
+          s1[k][j] += wx;
+          s2[k][j] = fmaf(wx, x[j], s2[k][j]);
+        }
+      }
+      if (c == 0) sw_acc += w;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float a = s1[k][j], b = s2[k][j];
+#pragma unroll
+      for (int off = LPR; off < kWave; off <<= 1) {
+        a += __shfl_xor(a, off, kWave);
+        b += __shfl_xor(b, off, kWave);
+      }
+      s1[k][j] = a;
+      s2[k][j] = b;
+    }
+  sw_acc = wave_sum(sw_acc);
+  // waves add into one LDS row in turn (fixed order -> deterministic)
+  __shared__ float red[2 * DP + 2];
+  for (int q = 0; q < kWavesPerBlock; ++q) {
+    if (wid == q) {
+      if (lane < LPR) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int i1 = 8 * (c + k * LPR) + j;
+            red[i1] = (q == 0 ? 0.f : red[i1]) + s1[k][j];
+            red[DP + i1] = (q == 0 ? 0.f : red[DP + i1]) + s2[k][j];
+          }
+      }
+      if (lane == 0) red[2 * DP] = (q == 0 ? 0.f : red[2 * DP]) + sw_acc;
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < 2 * DP + 1; i += kBlock) partial[(int64_t)blockIdx.x * pstride + i] = red[i];
+}
+
 // out[i] = sum_b partial[b][i] in fp64, fixed order (deterministic).
 __global__ void glm_finish_kernel(const float* __restrict__ partial, int nblocks, int pstride,
                                   int ncols, double* __restrict__ out) {
@@ -521,4 +607,41 @@ O3S_API int o3s_glm_margin(const void* X, int64_t ld, int64_t n, const float* co
   O3S_M(64, 2) O3S_M(64, 4) O3S_M(64, 8) O3S_M(64, 16)
 #undef O3S_M
   return -1;
+}
+
+// Column moments: out (fp64, 2*dpad+1) = [sum w x | sum w x^2 | sum w].  partial must hold
+// grid * (2*dpad+2) floats.
+O3S_API int o3s_glm_colstats(int src, const void* X, int64_t ld, int64_t n, const float* sw,
+                             uint32_t seed, int64_t row0, float* partial, int grid, double* out,
+                             hipStream_t st) {
+  const int nch = (int)(ld / 8);
+  const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
+  if (ld % 8 != 0 || cpl > 16 || grid <= 0) return -1;
+  const int dpad = lpr * cpl * 8, pstride = 2 * dpad + 2;
+  const uint16_t* Xh = (const uint16_t*)X;
+  if (n > 0) {
+    bool done = false;
+#define O3S_C(L, C)                                                                            \
+  if (!done && lpr == L && cpl == C) {                                                         \
+    if (src == 0)                                                                              \
+      hipLaunchKernelGGL((glm_colstats_kernel<L, C, 0>), dim3(grid), dim3(kBlock), 0, st, Xh,   \
+                         ld, n, sw, seed, row0, partial, pstride);                             \
+    else                                                                                       \
+      hipLaunchKernelGGL((glm_colstats_kernel<L, C, 1>), dim3(grid), dim3(kBlock), 0, st, Xh,   \
+                         ld, n, sw, seed, row0, partial, pstride);                             \
+    done = true;                                                                               \
+  }
+    O3S_C(4, 1) O3S_C(8, 1) O3S_C(16, 1) O3S_C(32, 1) O3S_C(64, 1)
+    O3S_C(64, 2) O3S_C(64, 4) O3S_C(64, 8) O3S_C(64, 16)
+#undef O3S_C
+    if (!done) return -1;
+  } else {
+    hipMemsetAsync(partial, 0, sizeof(float) * pstride * (size_t)grid, st);
+  }
+  O3S_CHECK_LAUNCH();
+  const int ncols = 2 * dpad + 1;
+  hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 255) / 256), dim3(256), 0, st, partial, grid,
+                     pstride, ncols, out);
+  O3S_CHECK_LAUNCH();
+  return 0;
 }

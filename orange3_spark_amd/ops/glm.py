@@ -239,3 +239,39 @@ def glm_margin(X: torch.Tensor, coef: torch.Tensor, intercept: float) -> torch.T
         return out
     c = coef.to(X.device, torch.float64)[:ld]
     return (X.to(torch.float64) @ c + float(intercept)).to(torch.float32)
+
+
+# --------------------------------------------------------------------------- moments
+def _colstats_out(ld: int, device, grid: int):
+    dpad, _ = layout(ld)
+    partial = torch.empty(grid * (2 * dpad + 2), dtype=torch.float32, device=device)
+    out = torch.empty(2 * dpad + 1, dtype=torch.float64, device=device)
+    return dpad, partial, out
+
+
+def glm_colstats(X: torch.Tensor, sw: torch.Tensor | None = None) -> torch.Tensor:
+    """fp64 [sum w x (ld) | sum w x^2 (ld) | sum w] over the rows of X."""
+    ld = X.shape[1]
+    if X.is_cuda and X.dtype == torch.bfloat16 and X.is_contiguous():
+        grid = N.num_cus(X.device) * 4
+        dpad, partial, out = _colstats_out(ld, X.device, grid)
+        N.check(N.kernels().o3s_glm_colstats(0, X.data_ptr(), ld, X.shape[0], N.ptr(sw), 0, 0,
+                                             partial.data_ptr(), grid, out.data_ptr(), N.stream_of(X)),
+                "glm_colstats")
+        return torch.cat([out[:ld], out[dpad:dpad + ld], out[2 * dpad:]])
+    Xd = X.to(torch.float64)
+    w = torch.ones(X.shape[0], dtype=torch.float64, device=X.device) if sw is None else sw.to(torch.float64)
+    return torch.cat([w @ Xd, w @ (Xd * Xd), w.sum().reshape(1)])
+
+
+def glm_colstats_synth(n: int, ld: int, d: int, seed: int, row0: int, device) -> torch.Tensor:
+    device = torch.device(device)
+    if device.type == "cuda":
+        grid = N.num_cus(device) * 4
+        dpad, partial, out = _colstats_out(ld, device, grid)
+        N.check(N.kernels().o3s_glm_colstats(1, None, ld, n, None, seed & _MASK, row0, partial.data_ptr(), grid,
+                                             out.data_ptr(), torch.cuda.current_stream(device).cuda_stream),
+                "glm_colstats_synth")
+        return torch.cat([out[:ld], out[dpad:dpad + ld], out[2 * dpad:]])
+    X, _ = synth_glm(n, d, seed, row0, "cpu", ld, torch.zeros(ld), 0.0)
+    return glm_colstats(X)
