@@ -134,6 +134,10 @@ class Params:
 
     _counters = {}
 
+    def __init_subclass__(cls, **kw):
+        super().__init_subclass__(**kw)
+        add_accessors(cls)   # getX/setX for every Param, like pyspark's generated accessors
+
     def __init__(self):
         self._paramMap: dict[Param, Any] = {}
         self._defaultParamMap: dict[Param, Any] = {}

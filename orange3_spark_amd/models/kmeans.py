@@ -1,0 +1,168 @@
+"""KMeans engine: k-means|| initialisation + Lloyd iterations over row-sharded data.
+
+Per Lloyd iteration on each rank: ``kmeans_assign`` (MFMA GEMM + fused argmin) ->
+``kmeans_update`` (sorted segmented sums into block slabs) -> ONE all-reduce of a
+single fp64 buffer [sums (K*D) | counts (K) | cost] over RCCL.  Spark semantics
+(mllib KMeans): empty clusters keep their previous centre; converged when every centre
+moved less than ``tol`` (euclidean); cost = sum of squared distances.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..ops import kmeans as K
+from ..ops import sampling
+
+
+@dataclass
+class KMeansResult:
+    centers: torch.Tensor          # [k, D] fp64 (host)
+    cost: float
+    iterations: int
+    sizes: list
+    history: list = field(default_factory=list)
+    seconds: float = 0.0
+
+
+def _global_rows(comm, n_local, device):
+    sizes = comm.all_gather_object(int(n_local))
+    off = sum(sizes[: comm.rank])
+    return torch.arange(off, off + n_local, dtype=torch.int64, device=device), sum(sizes)
+
+
+def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -> torch.Tensor:
+    """k-means|| (Bahmani et al.): oversample ~2k candidates per round, then weighted
+    k-means++ on the (small) candidate set, replicated on every rank."""
+    dev = X.device
+    rows, n = _global_rows(comm, X.shape[0], dev)
+    # first centre: one uniformly random global row
+    rng = np.random.default_rng(seed)
+    pick = int(rng.integers(0, max(n, 1)))
+    mine = (rows == pick).nonzero()
+    c0 = X[mine[0, 0]].to(torch.float64) if mine.numel() else torch.zeros(X.shape[1], dtype=torch.float64, device=dev)
+    c0 = c0.contiguous()
+    comm.all_reduce(c0)
+    centers = c0[None, :]
+    for step in range(steps):
+        _, d = K.assign(X, centers.float())
+        cost = d.to(torch.float64).sum()
+        comm.all_reduce(cost)
+        if float(cost) <= 0:
+            break
+        p = (2.0 * k * d.to(torch.float64) / float(cost)).clamp(max=1.0)
+        u = sampling.uniform(rows, seed + 1 + step, stream=7)
+        new = X[u < p].to(torch.float64)
+        new = comm.all_gather_v(new) if comm.world_size > 1 else new
+        centers = torch.cat([centers, new.to(dev)])
+    # weights = number of points closest to each candidate
+    a, _ = K.assign(X, centers.float())
+    wts = torch.zeros(centers.shape[0], dtype=torch.float64, device=dev).index_add_(
+        0, a.long(), torch.ones(a.shape[0], dtype=torch.float64, device=dev))
+    comm.all_reduce(wts)
+    return _local_kmeanspp(centers, wts, k, seed)
+
+
+def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: int = 30) -> torch.Tensor:
+    """Weighted k-means++ + Lloyd on candidates (Spark LocalKMeans), fp64 on device."""
+    m = P.shape[0]
+    if m <= k:
+        extra = k - m
+        return torch.cat([P, P[:1].expand(extra, -1)]) if extra else P
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    first = int(torch.multinomial(w.cpu().double(), 1, generator=g))
+    C = [P[first]]
+    d2 = ((P - P[first]) ** 2).sum(1)
+    for _ in range(1, k):
+        prob = (w * d2).cpu()
+        if float(prob.sum()) <= 0:
+            idx = int(torch.randint(0, m, (1,), generator=g))
+        else:
+            idx = int(torch.multinomial(prob, 1, generator=g))
+        C.append(P[idx])
+        d2 = torch.minimum(d2, ((P - P[idx]) ** 2).sum(1))
+    C = torch.stack(C)
+    for _ in range(iters):
+        dist = (P * P).sum(1, keepdim=True) - 2 * P @ C.T + (C * C).sum(1)[None, :]
+        a = dist.argmin(1)
+        sums = torch.zeros_like(C).index_add_(0, a, P * w[:, None])
+        cnt = torch.zeros(k, dtype=P.dtype, device=P.device).index_add_(0, a, w)
+        newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp_min(1e-300)[:, None], C)
+        if torch.allclose(newC, C):
+            break
+        C = newC
+    return C
+
+
+def random_init(comm, X, k, seed):
+    rows, n = _global_rows(comm, X.shape[0], X.device)
+    rng = np.random.default_rng(seed)
+    picks = torch.from_numpy(rng.choice(max(n, 1), size=min(k, n), replace=False)).to(X.device)
+    C = torch.zeros((k, X.shape[1]), dtype=torch.float64, device=X.device)
+    hit = torch.isin(rows, picks)
+    for r_, x in zip(rows[hit].tolist(), X[hit].to(torch.float64)):
+        C[(picks == r_).nonzero()[0, 0]] = x
+    comm.all_reduce(C)
+    return C
+
+
+def fit_kmeans(comm, X: torch.Tensor, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int = 0,
+               init: str = "k-means||", init_steps: int = 2, initial: torch.Tensor | None = None,
+               weights: torch.Tensor | None = None, cosine: bool = False) -> KMeansResult:
+    t0 = time.time()
+    if cosine:
+        X = X / X.norm(dim=1, keepdim=True).clamp_min(1e-300)
+    if initial is not None:
+        C = initial.to(X.device, torch.float64)
+    elif init == "random":
+        C = random_init(comm, X, k, seed)
+    else:
+        C = kmeans_parallel_init(comm, X, k, init_steps, seed)
+    D = X.shape[1]
+    ws = K.UpdateWorkspace(X.device, ((k + 31) // 32) * 32, D) if K.kernel_ok(X) and weights is None else None
+    hist = []
+    it = 0
+    sizes = None
+    cost = float("nan")
+    for it in range(1, max_iter + 1):
+        prep = K.prepare_centers(C.float()) if K.kernel_ok(X) else None
+        a, d = K.assign(X, C.float(), prep)
+        if ws is not None:
+            sums, cnt = K.update(X, a, ws.K, ws)
+            sums, cnt = sums[:k], cnt[:k]
+        else:
+            sums, cnt = K.update_torch(X, a, k, weights)
+        dd = d.to(torch.float64) if weights is None else d.to(torch.float64) * weights.to(torch.float64)
+        buf = torch.cat([sums.reshape(-1), cnt, dd.sum().reshape(1)])
+        comm.all_reduce(buf)
+        sums, cnt, cost = buf[: k * D].reshape(k, D), buf[k * D: k * D + k], float(buf[-1])
+        hist.append(cost)
+        newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp_min(1e-300)[:, None], C)
+        if cosine:
+            newC = newC / newC.norm(dim=1, keepdim=True).clamp_min(1e-300)
+        moved = ((newC - C) ** 2).sum(1).max().item()
+        C = newC
+        sizes = cnt
+        if moved <= tol * tol:
+            break
+    # final cost/sizes w.r.t. the returned centres (Spark reports the last assignment's)
+    a, d = K.assign(X, C.float())
+    cnt = torch.zeros(k, dtype=torch.float64, device=X.device).index_add_(
+        0, a.long(), torch.ones(a.shape[0], dtype=torch.float64, device=X.device))
+    buf = torch.cat([cnt, d.to(torch.float64).sum().reshape(1)])
+    comm.all_reduce(buf)
+    return KMeansResult(C.cpu(), float(buf[-1]), it, [int(x) for x in buf[:k].tolist()], hist, time.time() - t0)
+
+
+def predict(X: torch.Tensor, C: torch.Tensor, cosine=False) -> torch.Tensor:
+    if cosine:
+        X = X / X.norm(dim=1, keepdim=True).clamp_min(1e-300)
+    a, _ = K.assign(X.float() if X.is_cuda else X, C.to(X.device).float() if X.is_cuda else C.to(X.device))
+    return a
+
+
+_ = math

@@ -466,14 +466,25 @@ __global__ __launch_bounds__(kBlock) void glm_colstats_kernel(
   for (int i = threadIdx.x; i < 2 * DP + 1; i += kBlock) partial[(int64_t)blockIdx.x * pstride + i] = red[i];
 }
 
-// out[i] = sum_b partial[b][i] in fp64, fixed order (deterministic).
-__global__ void glm_finish_kernel(const float* __restrict__ partial, int nblocks, int pstride,
-                                  int ncols, double* __restrict__ out) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= ncols) return;
+// out[i] = sum_b partial[b][i] in fp64, fixed order (deterministic).  Block = 32
+// columns x 32 strided partial-row groups; each thread sums nblocks/32 rows, then the
+// 32 group sums of a column are combined in LDS in a fixed order.
+__global__ __launch_bounds__(1024) void glm_finish_kernel(const float* __restrict__ partial, int nblocks,
+                                                          int pstride, int ncols, double* __restrict__ out) {
+  __shared__ double red[32][33];
+  const int cx = threadIdx.x & 31, gy = threadIdx.x >> 5;
+  const int i = blockIdx.x * 32 + cx;
   double s = 0.0;
-  for (int b = 0; b < nblocks; ++b) s += (double)partial[(int64_t)b * pstride + i];
-  out[i] = s;
+  if (i < ncols)
+    for (int b = gy; b < nblocks; b += 32) s += (double)partial[(int64_t)b * pstride + i];
+  red[gy][cx] = s;
+  __syncthreads();
+  if (gy == 0 && i < ncols) {
+    double t = 0.0;
+#pragma unroll 8
+    for (int q = 0; q < 32; ++q) t += red[q][cx];
+    out[i] = t;
+  }
 }
 
 int pick_lpr(int nch) {
@@ -563,7 +574,7 @@ O3S_API int o3s_glm_grad(int loss, int src, const void* X, int64_t ld, int64_t n
   }
   O3S_CHECK_LAUNCH();
   const int ncols = dpad + 3;
-  hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 255) / 256), dim3(256), 0, st, partial, grid,
+  hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 31) / 32), dim3(1024), 0, st, partial, grid,
                      pstride, ncols, out);
   O3S_CHECK_LAUNCH();
   return 0;
@@ -640,7 +651,7 @@ O3S_API int o3s_glm_colstats(int src, const void* X, int64_t ld, int64_t n, cons
   }
   O3S_CHECK_LAUNCH();
   const int ncols = 2 * dpad + 1;
-  hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 255) / 256), dim3(256), 0, st, partial, grid,
+  hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 31) / 32), dim3(1024), 0, st, partial, grid,
                      pstride, ncols, out);
   O3S_CHECK_LAUNCH();
   return 0;

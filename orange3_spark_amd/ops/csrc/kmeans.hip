@@ -1,0 +1,357 @@
+// KMeans assign + update (gfx950).  Replaces the per-partition closest-centre search
+// and per-cluster sums that Spark's KMeans runs per iteration (reached through the
+// Clustering widget -> fit, orangecontrib/spark/widgets/ml/spark_ml_clustering.py:14).
+//
+// ---------------------------------------------------------------------------------
+// kmeans_assign: argmin_c ||x - c||^2 = argmin_c (||c||^2 - 2 x.c) as an MFMA GEMM
+// with a fused arg-min epilogue -- the N x K distance matrix is never materialised.
+//
+//  * D' = C . X^T with v_mfma_f32_32x32x16_bf16: A = a 32-centroid chunk (from LDS),
+//    B = X^T of a 32-row tile (registers).  In this orientation each lane's 16
+//    accumulators belong to ONE data row (its column) and 16 centroids, so the running
+//    (min, argmin) is lane-local: no cross-lane work until one final half-wave merge.
+//  * split precision: x = xh + xl, c = ch + cl (bf16 hi/lo); x.c ~ xh.ch + xl.ch + xh.cl
+//    (3 bf16 MFMAs, ~2^-16 relative error, i.e. fp32-level distance accuracy at the
+//    bf16 MFMA rate; a 1-pass bf16 product would mis-assign near ties).  The -2 factor
+//    is folded into the centre split on the host.
+//  * each wave owns one 32-row tile (X fragments hi/lo: 64 VGPRs at D=128, held for the
+//    whole centroid sweep); 8 waves share each centroid chunk through LDS, staged by
+//    LDS-DMA (global_load_lds_dwordx4) double-buffered so chunk j+1 lands under chunk
+//    j's MFMAs; the 16-B slot XOR-swizzle (slot ^= row & 15, applied to the DMA SOURCE
+//    address since the DMA image is lane-linear) makes the 32-row ds_read_b128
+//    fragment reads bank-conflict free (CDNA guide §5.5 T2, §5.4 rule 21).
+//
+// kmeans_update: per-cluster sums without float atomics.  Each block takes chunks of
+// R rows, counting-sorts their indices by cluster in LDS (bucket order made
+// deterministic by an in-bucket insertion sort), then each wave owns a contiguous
+// cluster range and streams its rows (coalesced 512-B row reads) accumulating in
+// registers; a cluster's sum is flushed once per chunk into the block's private slab.
+// Slabs are summed by kmeans_reduce in a fixed order (bitwise deterministic).
+#include "common.h"
+
+using namespace o3s;
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kAssignWaves = 8;   // 8 waves x one 32-row tile share each centroid chunk
+constexpr int kAssignThreads = kAssignWaves * kWave;
+
+__device__ __forceinline__ void split_bf16(float v, short& hi, short& lo) {
+  const uint16_t h = f32_to_bf16(v);
+  hi = (short)h;
+  lo = (short)f32_to_bf16(v - bf16_to_f32(h));
+}
+
+// KS = D / 16 k-steps, TT = 32-row tiles per wave.  Cpad: centroids padded to 32
+// (padding rows carry cn = +inf).
+template <int KS, int TT>
+__global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
+    const float* __restrict__ X, int64_t n, int64_t ldx, const uint16_t* __restrict__ Chi,
+    const uint16_t* __restrict__ Clo, const float* __restrict__ cn, int Cpad,
+    int32_t* __restrict__ assign, float* __restrict__ mind, int Dx) {
+  constexpr int D = KS * 16;
+  constexpr int SLOTS = D / 8;                 // 16-B slots per centroid row
+  constexpr int CH_ELEMS = 32 * D;             // bf16 per chunk (hi or lo)
+  constexpr int PIECES = 2 * 32 * SLOTS;       // 16-B pieces per chunk (hi + lo)
+  constexpr int PER_THREAD = (PIECES + kAssignThreads - 1) / kAssignThreads;
+  static_assert(PIECES % kWave == 0, "whole waves per DMA instruction");
+  constexpr int ROWS_PER_WAVE = 32 * TT;
+  constexpr int ROWS_PER_BLOCK = kAssignWaves * ROWS_PER_WAVE;
+  // ONE __shared__ array (guide §5 item 4a): [buf][hi|lo][32][D] bf16, slot-swizzled rows
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * CH_ELEMS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t row_base = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wid * ROWS_PER_WAVE;
+
+  // ---- X^T fragments (B operand) for the wave's rows, split hi/lo, + ||x||^2
+  bf16x8 bh[TT][KS], bl[TT][KS];
+  float xn[TT];
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+    const int64_t row = row_base + t * 32 + r;
+    const int64_t rowc = row < n ? row : n - 1;
+    const float* xp = X + rowc * ldx;
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c0 = ks * 16 + 8 * h;          // Dx % 4 == 0: whole float4s are in or out
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 a = c0 < Dx ? *reinterpret_cast<const float4*>(xp + c0) : z;
+      const float4 b = c0 + 4 < Dx ? *reinterpret_cast<const float4*>(xp + c0 + 4) : z;
+      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        short hi, lo;
+        split_bf16(v[j], hi, lo);
+        bh[t][ks][j] = hi;
+        bl[t][ks][j] = lo;
+        s = fmaf(v[j], v[j], s);
+      }
+    }
+    xn[t] = s + __shfl_xor(s, 32, 64);
+  }
+
+  // ---- chunk staging by LDS-DMA (global_load_lds_dwordx4): the LDS image is lane-linear,
+  // so the XOR swizzle is applied to the SOURCE slot (guide §5.4 rule 21).
+  const int nchunks = Cpad / 32;
+  auto stage = [&](int chunk, int buf) {
+#pragma unroll
+    for (int k = 0; k < PER_THREAD; ++k) {
+      const int P = threadIdx.x + k * kAssignThreads;      // linear 16-B piece index
+      if (PIECES % kAssignThreads != 0 && P >= PIECES) break;   // wave-uniform
+      const int which = P / (32 * SLOTS);
+      const int rem = P % (32 * SLOTS);
+      const int cr = rem / SLOTS, sw = rem % SLOTS;
+      const int sl = sw ^ (cr & 15 & (SLOTS - 1));
+      const uint16_t* src = (which ? Clo : Chi) + ((int64_t)(chunk * 32 + cr)) * D + sl * 8;
+      uint16_t* dst = lds + buf * 2 * CH_ELEMS + (wid * kWave + k * kAssignThreads) * 8;   // wave-uniform
+      __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+    }
+  };
+
+  float bestv[TT], xnv[TT];
+  int besti[TT];
+#pragma unroll
+  for (int t = 0; t < TT; ++t) { bestv[t] = INFINITY; besti[t] = 0; xnv[t] = xn[t]; }
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ch = 0; ch < nchunks; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < nchunks) stage(ch + 1, buf ^ 1);       // DMA in flight under the MFMAs
+    const uint16_t* Lh = lds + buf * 2 * CH_ELEMS;
+    const uint16_t* Ll = Lh + CH_ELEMS;
+    f32x16 acc[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int sl = ks * 2 + h;
+      const int sw = sl ^ (r & 15 & (SLOTS - 1));
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Lh + r * D + sw * 8);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(Ll + r * D + sw * 8);
+#pragma unroll
+      for (int t = 0; t < TT; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t][ks], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t][ks], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t][ks], acc[t], 0, 0, 0);
+      }
+    }
+    // epilogue: centroid of acc reg i = ch*32 + (i&3) + 8*(i>>2) + 4*h
+    const int cbase = ch * 32 + 4 * h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 c4 = *reinterpret_cast<const float4*>(cn + cbase + 8 * q);
+      const float cv[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int idx = cbase + 8 * q + j;
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+          const float dv = acc[t][4 * q + j] + cv[j];
+          const bool better = dv < bestv[t];
+          bestv[t] = better ? dv : bestv[t];
+          besti[t] = better ? idx : besti[t];
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // next chunk landed
+    __syncthreads();                                   // ... for every wave; buf free again
+  }
+  // merge the two half-waves (different centroid subsets of the same row)
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+    const float ov = __shfl_xor(bestv[t], 32, 64);
+    const int oi = __shfl_xor(besti[t], 32, 64);
+    if (ov < bestv[t] || (ov == bestv[t] && oi < besti[t])) { bestv[t] = ov; besti[t] = oi; }
+    const int64_t row = row_base + t * 32 + r;
+    if (h == 0 && row < n) {
+      assign[row] = besti[t];
+      if (mind) mind[row] = fmaxf(bestv[t] + xnv[t], 0.f);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+constexpr int kUpdThreads = 512;
+constexpr int kUpdWaves = kUpdThreads / kWave;
+constexpr int kUpdRows = 8192;
+
+// One block: chunks of kUpdRows rows; slab (block-private) = [Kp][D] sums + [Kp] counts.
+template <int DV>  // floats per lane per row (D = 64 * DV)
+__global__ __launch_bounds__(kUpdThreads) void kmeans_update_kernel(
+    const float* __restrict__ X, int64_t n, int64_t ldx, int D, const int32_t* __restrict__ assign,
+    int Kp, float* __restrict__ slab, float* __restrict__ cnt_slab) {
+  extern __shared__ __attribute__((aligned(16))) int smem[];
+  int* hist = smem;                  // [Kp]  bucket sizes
+  int* start = hist + Kp;            // [Kp+1] bucket starts
+  int* cursor = start + Kp + 1;      // [Kp]
+  int* sorted = cursor + Kp;         // [kUpdRows]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* myslab = slab + (int64_t)blockIdx.x * Kp * D;
+  float* mycnt = cnt_slab + (int64_t)blockIdx.x * Kp;
+  const int64_t nch = (n + kUpdRows - 1) / kUpdRows;
+  for (int64_t cidx = blockIdx.x; cidx < nch; cidx += gridDim.x) {
+    const int64_t r0 = cidx * kUpdRows;
+    const int rows = (int)min((int64_t)kUpdRows, n - r0);
+    for (int i = threadIdx.x; i < Kp; i += kUpdThreads) hist[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < rows; i += kUpdThreads) atomicAdd(&hist[assign[r0 + i]], 1);
+    __syncthreads();
+    if (wid == 0) {   // exclusive scan by one wave (Kp <= a few thousand)
+      int carry = 0;
+      for (int b = 0; b < Kp; b += 64) {
+        const int v = (b + lane < Kp) ? hist[b + lane] : 0;
+        int x = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const int y = __shfl_up(x, off, 64);
+          if (lane >= off) x += y;
+        }
+        if (b + lane < Kp) { start[b + lane] = carry + x - v; cursor[b + lane] = carry + x - v; }
+        carry += __shfl(x, 63, 64);
+      }
+      if (lane == 0) start[Kp] = carry;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < rows; i += kUpdThreads) {
+      const int pos = atomicAdd(&cursor[assign[r0 + i]], 1);
+      sorted[pos] = i;
+    }
+    __syncthreads();
+    // deterministic bucket order: insertion-sort each (small) bucket by row index
+    for (int b = threadIdx.x; b < Kp; b += kUpdThreads) {
+      const int s0 = start[b], s1 = start[b + 1];
+      for (int i = s0 + 1; i < s1; ++i) {
+        const int v = sorted[i];
+        int j = i - 1;
+        while (j >= s0 && sorted[j] > v) { sorted[j + 1] = sorted[j]; --j; }
+        sorted[j + 1] = v;
+      }
+    }
+    __syncthreads();
+    // wave w owns clusters [c0, c1): its rows are the contiguous sorted range
+    const int c0 = (int)((int64_t)Kp * wid / kUpdWaves), c1 = (int)((int64_t)Kp * (wid + 1) / kUpdWaves);
+    for (int c = c0; c < c1; ++c) {
+      const int s0 = start[c], s1 = start[c + 1];
+      if (s0 == s1) continue;
+      float acc[DV];
+#pragma unroll
+      for (int v = 0; v < DV; ++v) acc[v] = 0.f;
+      int i = s0;
+      for (; i + 4 <= s1; i += 4) {       // 4 rows in flight
+        float x[4][DV];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float* xp = X + (r0 + sorted[i + u]) * ldx;
+#pragma unroll
+          for (int v = 0; v < DV; ++v) {
+            const int col = lane + 64 * v;
+            x[u][v] = col < D ? xp[col] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int v = 0; v < DV; ++v) acc[v] += x[u][v];
+      }
+      for (; i < s1; ++i) {
+        const float* xp = X + (r0 + sorted[i]) * ldx;
+#pragma unroll
+        for (int v = 0; v < DV; ++v) {
+          const int col = lane + 64 * v;
+          acc[v] += col < D ? xp[col] : 0.f;
+        }
+      }
+      float* dst = myslab + (int64_t)c * D;
+#pragma unroll
+      for (int v = 0; v < DV; ++v) {
+        const int col = lane + 64 * v;
+        if (col < D) dst[col] += acc[v];
+      }
+      if (lane == 0) mycnt[c] += (float)(s1 - s0);
+    }
+    __syncthreads();
+  }
+}
+
+// sums[k][d] = sum_g slab[g][k][d] (fixed order), counts likewise.
+__global__ void kmeans_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ cnt_slab,
+                                     int G, int64_t KD, int Kp, double* __restrict__ sums,
+                                     double* __restrict__ counts) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < KD) {
+    double s = 0.0;
+    for (int g = 0; g < G; ++g) s += (double)slab[(int64_t)g * KD + i];
+    sums[i] = s;
+  }
+  if (i < Kp) {
+    double s = 0.0;
+    for (int g = 0; g < G; ++g) s += (double)cnt_slab[(int64_t)g * Kp + i];
+    counts[i] = s;
+  }
+}
+
+}  // namespace
+
+// D must be a multiple of 16 (<= 256), X rows 16-B aligned (ldx % 4 == 0); Cpad % 32 == 0.
+// Dx: true feature count (% 4 == 0); Chi/Clo are [Cpad][Dp] with Dp = roundup(Dx, 32).
+O3S_API int o3s_kmeans_assign(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi,
+                              const void* Clo, const float* cn, int Cpad, int32_t* assign, float* mind,
+                              hipStream_t st) {
+  if (n <= 0) return 0;
+  const int D = (Dx + 31) / 32 * 32;
+  if (Dx % 4 != 0 || D > 256 || ldx % 4 != 0 || Cpad % 32 != 0) return -1;
+  const int rows_per_block = kAssignWaves * 32;
+  const int grid = (int)((n + rows_per_block - 1) / rows_per_block);
+  const uint16_t* hi = (const uint16_t*)Chi;
+  const uint16_t* lo = (const uint16_t*)Clo;
+#define O3S_KA(KS)                                                                                   \
+  case KS:                                                                                           \
+    hipLaunchKernelGGL((kmeans_assign_kernel<KS, 1>), dim3(grid), dim3(kAssignThreads), 0, st, X, n, ldx, \
+                       hi, lo, cn, Cpad, assign, mind, Dx);                                          \
+    break;
+  switch (D / 16) {
+    O3S_KA(2) O3S_KA(4) O3S_KA(6) O3S_KA(8) O3S_KA(10) O3S_KA(12) O3S_KA(14) O3S_KA(16)
+    default: return -2;
+  }
+#undef O3S_KA
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+O3S_API int o3s_kmeans_update_ws(int Kp, int D, int grid, int64_t* slab_floats, int64_t* cnt_floats,
+                                 int* lds_bytes) {
+  *slab_floats = (int64_t)grid * Kp * D;
+  *cnt_floats = (int64_t)grid * Kp;
+  *lds_bytes = (int)(sizeof(int) * (3 * Kp + 1 + kUpdRows));
+  return 0;
+}
+
+// slab/cnt_slab must be zeroed by the caller (hipMemsetAsync) before each call.
+O3S_API int o3s_kmeans_update(const float* X, int64_t n, int64_t ldx, int D, const int32_t* assign, int Kp,
+                              float* slab, float* cnt_slab, int grid, double* sums, double* counts,
+                              hipStream_t st) {
+  if (D > 256 || n < 0) return -1;
+  const int lds = (int)(sizeof(int) * (3 * Kp + 1 + kUpdRows));
+  if (lds > 160 * 1024) return -3;
+  if (n > 0) {
+#define O3S_KU(DV)                                                                                    \
+  hipLaunchKernelGGL((kmeans_update_kernel<DV>), dim3(grid), dim3(kUpdThreads), lds, st, X, n, ldx, D, \
+                     assign, Kp, slab, cnt_slab);
+    if (D <= 64) { O3S_KU(1) } else if (D <= 128) { O3S_KU(2) } else if (D <= 192) { O3S_KU(3) } else { O3S_KU(4) }
+#undef O3S_KU
+    O3S_CHECK_LAUNCH();
+  }
+  const int64_t KD = (int64_t)Kp * D;
+  const int64_t work = KD > Kp ? KD : Kp;
+  hipLaunchKernelGGL(kmeans_reduce_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st, slab, cnt_slab,
+                     grid, KD, Kp, sums, counts);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}

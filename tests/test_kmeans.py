@@ -1,0 +1,82 @@
+"""KMeans: CPU path vs scikit-learn, GPU kernels vs fp64 PyTorch references."""
+import numpy as np
+import pytest
+import torch
+
+from orange3_spark_amd import Session, SessionConf
+from orange3_spark_amd.ml.clustering import KMeans, KMeansModel
+from orange3_spark_amd.ops import kmeans as K
+
+
+@pytest.fixture(scope="module")
+def cpu():
+    return Session(SessionConf().set("o3s.device", "cpu"))
+
+
+def test_kmeans_cpu_recovers_blobs(cpu):
+    df = cpu.synthetic.blobs(3000, 8, k=5, seed=1, spread=0.3)
+    m = KMeans(k=5, seed=3, maxIter=50).fit(df)
+    C = np.array(m.clusterCenters())
+    true = df.true_centers.double().numpy()
+    d = ((C[:, None] - true[None]) ** 2).sum(-1)
+    assert d.min(0).max() < 0.05
+    assert m.summary.trainingCost < 3000 * 8 * 0.3 ** 2 * 1.5
+    out = m.transform(df)
+    assert out.select("prediction").count() == 3000
+
+
+def test_kmeans_cost_close_to_sklearn(cpu):
+    from sklearn.cluster import KMeans as SK
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(2000, 6))
+    import pandas as pd
+    df = cpu.createDataFrame(pd.DataFrame({"features": list(X)}))
+    m = KMeans(k=8, seed=1, maxIter=100, tol=1e-8).fit(df)
+    sk = SK(n_clusters=8, n_init=5, random_state=0).fit(X)
+    assert m.summary.trainingCost < sk.inertia_ * 1.05
+
+
+def test_kmeans_save_load(cpu, tmp_path):
+    df = cpu.synthetic.blobs(500, 4, k=3, seed=2)
+    m = KMeans(k=3, seed=0).fit(df)
+    m.save(str(tmp_path / "km"))
+    m2 = KMeansModel.load(str(tmp_path / "km"))
+    assert np.allclose(np.array(m.clusterCenters()), np.array(m2.clusterCenters()))
+    assert m2.getK() == 3 and m2.uid == m.uid
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,Kc", [(128, 1024), (64, 100), (32, 7), (100, 33), (160, 64)])
+def test_gpu_assign_matches_fp64(gpu, D, Kc):
+    g = torch.Generator(device="cpu").manual_seed(D + Kc)
+    X = (torch.randn(20011, D, generator=g) * 3).to(gpu)
+    C = (torch.randn(Kc, D, generator=g) * 3).to(gpu)
+    a, d = K.assign(X, C)
+    ra, rd = K.assign_torch(X, C)
+    # exact agreement except for near-ties: check the chosen centre is optimal to 1e-4 rel
+    Xd, Cd = X.double(), C.double()
+    dist_sel = ((Xd - Cd[a.long()]) ** 2).sum(1)
+    assert torch.all(dist_sel <= rd.double() * (1 + 1e-4) + 1e-3)
+    assert (a == ra).float().mean() > 0.999
+    assert torch.allclose(d.double(), rd.double(), rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.gpu
+def test_gpu_update_matches_index_add(gpu):
+    g = torch.Generator(device="cpu").manual_seed(5)
+    X = torch.randn(100003, 128, generator=g).to(gpu)
+    a = torch.randint(0, 1000, (100003,), generator=g, dtype=torch.int32).to(gpu)
+    s, c = K.update(X, a, 1024)
+    rs, rc = K.update_torch(X, a, 1024)
+    assert torch.allclose(s, rs, atol=1e-3)
+    assert torch.equal(c, rc)
+    s2, _ = K.update(X, a, 1024)
+    assert torch.equal(s.clone(), s2)   # deterministic
+
+
+@pytest.mark.gpu
+def test_gpu_kmeans_fit(gpu):
+    s = Session(SessionConf().set("o3s.device", "cuda"))
+    df = s.synthetic.blobs(200_000, 128, k=64, seed=4, spread=0.5)
+    m = KMeans(k=64, seed=1, maxIter=30).fit(df)
+    assert m.summary.trainingCost / 200_000 < 128 * 0.25 * 1.3

@@ -1,0 +1,77 @@
+"""BASELINE config 2: KMeans k=1024 on 100M x 128 fp32, 1 MI355X.
+
+Times Lloyd iterations (assign MFMA kernel + slab update kernel + all-reduce + centre
+update) after a fixed initialisation; prints one JSON line (samples/s per iteration).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from orange3_spark_amd import Session  # noqa: E402
+from orange3_spark_amd.ops import kmeans as K  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--d", type=int, default=128)
+    ap.add_argument("--k", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--torch-baseline", action="store_true", help="also time a torch (rocBLAS GEMM) assign")
+    a = ap.parse_args()
+    s = Session.getOrCreate()
+    df = s.synthetic.blobs(a.rows, a.d, k=a.k, seed=3, spread=1.0)
+    X = df.column_data("features").data
+    C = df.true_centers.float() + 0.5
+    comm = s.comm
+    ws = K.UpdateWorkspace(X.device, (a.k + 31) // 32 * 32, a.d)
+    torch.cuda.synchronize()
+
+    def it(C):
+        prep = K.prepare_centers(C)
+        asg, d = K.assign(X, C, prep)
+        sums, cnt = K.update(X, asg, ws.K, ws)
+        buf = torch.cat([sums[: a.k].reshape(-1), cnt[: a.k], d.double().sum().reshape(1)])
+        comm.all_reduce(buf)
+        cnt = buf[a.k * a.d: a.k * a.d + a.k]
+        sums = buf[: a.k * a.d].reshape(a.k, a.d)
+        return torch.where(cnt[:, None] > 0, sums / cnt.clamp_min(1)[:, None], C.double()).float(), float(buf[-1])
+
+    C, _ = it(C)
+    torch.cuda.synchronize()
+    t_assign = time.perf_counter()
+    prep = K.prepare_centers(C)
+    for _ in range(a.iters):
+        asg, d = K.assign(X, C, prep)
+    torch.cuda.synchronize()
+    t_assign = (time.perf_counter() - t_assign) / a.iters
+    t_upd = time.perf_counter()
+    for _ in range(a.iters):
+        K.update(X, asg, ws.K, ws)
+    torch.cuda.synchronize()
+    t_upd = (time.perf_counter() - t_upd) / a.iters
+    t0 = time.perf_counter()
+    cost = None
+    for _ in range(a.iters):
+        C, cost = it(C)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.iters
+    flop = 2.0 * a.rows * a.k * a.d
+    out = {"metric": "KMeans Lloyd iteration samples/s (k=1024, 100M x 128 fp32)", "value": a.rows / dt,
+           "unit": "samples/s", "ms_per_iter": dt * 1e3, "assign_ms": t_assign * 1e3, "update_ms": t_upd * 1e3,
+           "assign_tflops_fp32_equiv": flop / t_assign / 1e12, "rows": a.rows, "d": a.d, "k": a.k, "cost": cost}
+    if a.torch_baseline:
+        t1 = time.perf_counter()
+        K.assign_torch(X[: 10_000_000], C, chunk=1 << 20)
+        torch.cuda.synchronize()
+        out["torch_fp64_assign_ms_per_10M"] = (time.perf_counter() - t1) * 1e3
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
