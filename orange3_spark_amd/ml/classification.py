@@ -335,3 +335,7 @@ class LinearSVCModel(U.ProbabilisticClassifierMixin, Model, _LinearSVCParams, ML
 
 
 _ = Vectors
+
+
+from ._tree import (DecisionTreeClassificationModel, DecisionTreeClassifier, GBTClassificationModel,  # noqa: E402,F401
+                    GBTClassifier, RandomForestClassificationModel, RandomForestClassifier)

@@ -77,14 +77,19 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
     first = int(torch.multinomial(w.cpu().double(), 1, generator=g))
     C = [P[first]]
     d2 = ((P - P[first]) ** 2).sum(1)
+    trials = 2 + int(math.log(k))          # greedy k-means++: best of several seeds per step
     for _ in range(1, k):
         prob = (w * d2).cpu()
         if float(prob.sum()) <= 0:
-            idx = int(torch.randint(0, m, (1,), generator=g))
+            cand = torch.randint(0, m, (trials,), generator=g)
         else:
-            idx = int(torch.multinomial(prob, 1, generator=g))
+            cand = torch.multinomial(prob, trials, replacement=True, generator=g)
+        cd = ((P[None, :, :] - P[cand.to(P.device)][:, None, :]) ** 2).sum(-1)   # [trials, m]
+        pot = (w[None, :] * torch.minimum(d2[None, :], cd)).sum(1)
+        best = int(pot.argmin())
+        idx = int(cand[best])
         C.append(P[idx])
-        d2 = torch.minimum(d2, ((P - P[idx]) ** 2).sum(1))
+        d2 = torch.minimum(d2, cd[best])
     C = torch.stack(C)
     for _ in range(iters):
         dist = (P * P).sum(1, keepdim=True) - 2 * P @ C.T + (C * C).sum(1)[None, :]

@@ -1,0 +1,370 @@
+"""Decision-tree engine (DecisionTree / RandomForest / GBT), level-wise, row-sharded.
+
+Replaces MLlib's RandomForest.run / GradientBoostedTrees.boost (reached through the
+Classification/Regression widgets, orangecontrib/spark/base/spark_ml_estimator.py:22).
+
+Pipeline per tree, per level (every rank):
+  1. ``ops.trees.node_hist``: LDS-privatised histogram kernel over this rank's rows,
+     which are kept grouped by node in a permutation (``order``), one slab row per work
+     item, summed per node in a fixed order;
+  2. ONE all-reduce of the level's [nodes, F, bins, stats] histogram (<= 3 MB at depth 8,
+     64 features, 32 bins) over RCCL;
+  3. best split per node on device (replicated; Spark impurity/gain semantics, bins
+     from approximate quantiles, ``minInstancesPerNode``, ``minInfoGain``, per-node
+     feature subsets for forests);
+  4. stable re-partition of ``order`` into the children (cumsum ranks, no sort).
+Node numbering follows Spark (root = 1, children 2i / 2i+1).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..ops import sampling
+from ..ops import trees as T
+
+
+# ----------------------------------------------------------------------------- binning
+def find_splits(comm, X: torch.Tensor, max_bins: int, seed: int = 0, sample: int | None = None) -> list:
+    """Per-feature candidate thresholds from a global sample (Spark findSplitsBySorting:
+    few distinct values -> midpoints, else approximate quantiles)."""
+    n_local = X.shape[0]
+    n = comm.sum_scalar(int(n_local))
+    want = sample or max(max_bins * max_bins, 10000)
+    frac = min(1.0, want / max(n, 1))
+    sizes = comm.all_gather_object(int(n_local))
+    off = sum(sizes[: comm.rank])
+    rows = torch.arange(off, off + n_local, dtype=torch.int64, device=X.device)
+    m = sampling.bernoulli_mask(rows, seed + 17, frac)
+    S = X[m].to(torch.float64)
+    S = comm.all_gather_v(S) if comm.world_size > 1 else S
+    S = S.cpu().numpy()
+    splits = []
+    for f in range(X.shape[1]):
+        v = S[:, f]
+        v = v[~np.isnan(v)]
+        u = np.unique(v)
+        if len(u) <= 1:
+            splits.append(np.zeros(0))
+        elif len(u) <= max_bins - 1:
+            splits.append((u[:-1] + u[1:]) / 2.0)
+        else:
+            qs = np.quantile(v, np.linspace(0, 1, max_bins + 1)[1:-1], method="linear")
+            splits.append(np.unique(qs))
+    return splits
+
+
+def bin_features(X: torch.Tensor, splits: list) -> torch.Tensor:
+    """uint8 [n, F]: bin = #thresholds < value (value <= t_0 -> bin 0)."""
+    n, F = X.shape
+    out = torch.empty((n, F), dtype=torch.uint8, device=X.device)
+    step = 1 << 22
+    for f in range(F):
+        t = torch.as_tensor(splits[f], dtype=X.dtype if X.is_floating_point() else torch.float64, device=X.device)
+        for a in range(0, n, step):
+            col = X[a:a + step, f]
+            out[a:a + step, f] = torch.bucketize(col.to(t.dtype), t, right=False).to(torch.uint8) if t.numel() \
+                else torch.zeros_like(col, dtype=torch.uint8)
+    return out
+
+
+# ----------------------------------------------------------------------------- impurity
+def _impurity(stats: torch.Tensor, kind: str) -> tuple[torch.Tensor, torch.Tensor]:
+    """stats [..., S] -> (impurity, weight)."""
+    if kind == "variance":
+        w = stats[..., 0]
+        mean = stats[..., 1] / w.clamp_min(1e-300)
+        imp = (stats[..., 2] / w.clamp_min(1e-300) - mean * mean).clamp_min(0.0)
+        return torch.where(w > 0, imp, torch.zeros_like(imp)), w
+    w = stats.sum(-1)
+    p = stats / w.clamp_min(1e-300)[..., None]
+    if kind == "gini":
+        imp = 1.0 - (p * p).sum(-1)
+    elif kind == "entropy":
+        imp = -(torch.where(p > 0, p * torch.log2(p.clamp_min(1e-300)), torch.zeros_like(p))).sum(-1)
+    else:
+        raise ValueError(kind)
+    return torch.where(w > 0, imp, torch.zeros_like(imp)), w
+
+
+@dataclass
+class Tree:
+    """Flat tree: arrays indexed by Spark node id (1-based; 0 unused)."""
+    feature: np.ndarray          # split feature (-1 = leaf)
+    threshold: np.ndarray        # split threshold (value <= thr -> left)
+    split_bin: np.ndarray
+    value: np.ndarray            # [nodes, V]: mean (regression) or class distribution
+    impurity: np.ndarray
+    gain: np.ndarray
+    count: np.ndarray            # weighted instance count
+    num_features: int = 0
+
+    @property
+    def depth(self) -> int:
+        ids = np.nonzero(self.count > 0)[0]
+        return int(math.floor(math.log2(ids.max()))) if ids.size else 0
+
+    @property
+    def numNodes(self) -> int:
+        return int(np.sum(self.count > 0))
+
+    def leaf_of(self, X: torch.Tensor) -> torch.Tensor:
+        """Spark node id of the leaf for each row of raw features X (device traversal)."""
+        dev = X.device
+        feat = torch.from_numpy(self.feature).to(dev)
+        thr = torch.from_numpy(self.threshold).to(dev, torch.float64)
+        node = torch.ones(X.shape[0], dtype=torch.int64, device=dev)
+        for _ in range(self.depth + 1):
+            f = feat[node]
+            leaf = f < 0
+            if bool(leaf.all()):
+                break
+            xv = X.gather(1, f.clamp_min(0)[:, None]).squeeze(1).to(torch.float64)
+            nxt = torch.where(xv <= thr[node], 2 * node, 2 * node + 1)
+            node = torch.where(leaf, node, nxt)
+        return node
+
+    def predict_value(self, X: torch.Tensor) -> torch.Tensor:
+        v = torch.from_numpy(self.value).to(X.device)
+        return v[self.leaf_of(X)]
+
+    def feature_importance(self) -> np.ndarray:
+        imp = np.zeros(self.num_features)
+        for i in np.nonzero(self.feature >= 0)[0]:
+            imp[self.feature[i]] += self.gain[i] * self.count[i]
+        s = imp.sum()
+        return imp / s if s > 0 else imp
+
+
+class TreeBuilder:
+    """Grows one tree over this rank's binned rows (collectives keep ranks in lockstep)."""
+
+    def __init__(self, comm, bins: torch.Tensor, splits: list, y: torch.Tensor, w: torch.Tensor | None,
+                 impurity: str, num_classes: int, max_depth: int = 5, min_instances: float = 1.0,
+                 min_info_gain: float = 0.0, feature_fraction: float = 1.0, seed: int = 0,
+                 max_bins: int = 32):
+        self.comm, self.bins, self.splits = comm, bins, splits
+        self.y, self.w = y, w
+        self.kind = impurity
+        self.cls = impurity in ("gini", "entropy")
+        self.S = num_classes if self.cls else 3
+        self.B = max(2, max(len(s) for s in splits) + 1) if splits else 2
+        self.max_depth, self.min_inst, self.min_gain = max_depth, min_instances, min_info_gain
+        self.ffrac, self.seed = feature_fraction, seed
+        self.F = bins.shape[1]
+
+    def build(self):
+        dev = self.bins.device
+        n = self.bins.shape[0]
+        F, B, S = self.F, self.B, self.S
+        max_nodes = 2 ** (self.max_depth + 1)
+        feature = -np.ones(max_nodes, dtype=np.int64)
+        threshold = np.zeros(max_nodes)
+        split_bin = np.zeros(max_nodes, dtype=np.int64)
+        value = np.zeros((max_nodes, S if self.cls else 1))
+        impurity = np.zeros(max_nodes)
+        gain = np.zeros(max_nodes)
+        count = np.zeros(max_nodes)
+        order = torch.arange(n, dtype=torch.int32, device=dev)
+        seg_lo = torch.zeros(1, dtype=torch.int64, device=dev)
+        seg_hi = torch.full((1,), n, dtype=torch.int64, device=dev)
+        seg_node = torch.ones(1, dtype=torch.int64, device=dev)
+        leaf_segments = []
+        rng = np.random.default_rng(self.seed)
+        for depth in range(self.max_depth + 1):
+            nodes = seg_node.tolist()
+            if not nodes:
+                break
+            k = len(nodes)
+            local = torch.arange(k, device=dev)
+            H = T.node_hist(self.bins, order, self.y, self.w, seg_lo, seg_hi, local, k, B, S, self.cls)
+            H = H.to(torch.float64).contiguous()
+            self.comm.all_reduce(H)                               # [k, F, B, S]
+            tot = H[:, 0].sum(1)                                   # [k, S] node stats (feature 0 bins)
+            imp_p, w_p = _impurity(tot, self.kind)
+            vals = (tot / w_p.clamp_min(1e-300)[:, None]) if self.cls else \
+                (tot[:, 1] / w_p.clamp_min(1e-300))[:, None]
+            # split search: cumulative stats over bins (left = bins <= j)
+            cum = H.cumsum(2)                                      # [k, F, B, S]
+            left = cum[:, :, :-1]
+            right = tot[:, None, None, :] - left
+            iL, wL = _impurity(left, self.kind)
+            iR, wR = _impurity(right, self.kind)
+            W = w_p[:, None, None].clamp_min(1e-300)
+            g = imp_p[:, None, None] - (wL / W) * iL - (wR / W) * iR
+            ok = (wL >= self.min_inst) & (wR >= self.min_inst)
+            nb = torch.tensor([len(s) for s in self.splits], device=dev)
+            ok &= torch.arange(B - 1, device=dev)[None, None, :] < nb[None, :, None]
+            if self.ffrac < 1.0:
+                m = max(1, int(math.ceil(self.ffrac * F)))
+                fmask = torch.zeros((k, F), dtype=torch.bool, device=dev)
+                for i in range(k):
+                    fmask[i, torch.from_numpy(rng.choice(F, m, replace=False)).to(dev)] = True
+                ok &= fmask[:, :, None]
+            g = torch.where(ok, g, torch.full_like(g, -math.inf))
+            best = g.reshape(k, -1).max(1)
+            bf = (best.indices // (B - 1)).cpu().numpy()
+            bb = (best.indices % (B - 1)).cpu().numpy()
+            bg = best.values.cpu().numpy()
+            node_ids = np.array(nodes)
+            vals_np, imp_np, w_np = vals.cpu().numpy(), imp_p.cpu().numpy(), w_p.cpu().numpy()
+            value[node_ids] = vals_np
+            impurity[node_ids] = imp_np
+            count[node_ids] = w_np
+            do_split = (bg > self.min_gain) & (bg > 0) & np.isfinite(bg) & (depth < self.max_depth)
+            if not do_split.any():
+                leaf_segments.append((seg_lo, seg_hi, seg_node))
+                break
+            for i, nid in enumerate(node_ids):
+                if do_split[i]:
+                    feature[nid] = bf[i]
+                    split_bin[nid] = bb[i]
+                    threshold[nid] = float(self.splits[bf[i]][bb[i]])
+                    gain[nid] = bg[i]
+            # --- partition the splitting segments
+            spl = torch.from_numpy(do_split).to(dev)
+            leaf_segments.append((seg_lo[~spl], seg_hi[~spl], seg_node[~spl]))
+            s_lo, s_hi, s_node = seg_lo[spl], seg_hi[spl], seg_node[spl]
+            s_feat = torch.from_numpy(bf[do_split]).to(dev)
+            s_bin = torch.from_numpy(bb[do_split]).to(dev)
+            lens = s_hi - s_lo
+            total = int(lens.sum())
+            sid = torch.repeat_interleave(torch.arange(s_lo.numel(), device=dev), lens)
+            first = torch.cumsum(lens, 0) - lens
+            pos = s_lo[sid] + (torch.arange(total, device=dev) - first[sid])
+            rows = order[pos].long()
+            bvals = self.bins.view(-1)[rows * F + s_feat[sid]]
+            go_left = bvals.to(torch.int64) <= s_bin[sid]
+            gl = go_left.to(torch.int64)
+            cl = torch.cumsum(gl, 0)
+            cl_before = cl[first] - gl[first]                      # exclusive prefix at segment starts
+            nleft = torch.zeros(s_lo.numel(), dtype=torch.int64, device=dev).index_add_(0, sid, gl)
+            lrank = cl - cl_before[sid]                            # inclusive rank among lefts
+            rel = torch.arange(total, device=dev) - first[sid]
+            rrank = rel + 1 - lrank
+            newpos = torch.where(go_left, s_lo[sid] + lrank - 1, s_lo[sid] + nleft[sid] + rrank - 1)
+            new_order = order.clone()
+            new_order[newpos] = order[pos]
+            order = new_order
+            mid = s_lo + nleft
+            seg_lo = torch.stack([s_lo, mid], 1).reshape(-1)
+            seg_hi = torch.stack([mid, s_hi], 1).reshape(-1)
+            seg_node = torch.stack([2 * s_node, 2 * s_node + 1], 1).reshape(-1)
+            # empty local segments still participate (other ranks may have rows there)
+        tree = Tree(feature, threshold, split_bin, value, impurity, gain, count, F)
+        # per-row leaf ids of the training rows (for boosting updates), no traversal needed
+        leaf_row = torch.empty(n, dtype=torch.int64, device=dev)
+        for lo, hi, nd in leaf_segments:
+            if lo.numel() == 0:
+                continue
+            lens = (hi - lo)
+            tot_ = int(lens.sum())
+            if tot_ == 0:
+                continue
+            sid = torch.repeat_interleave(torch.arange(lo.numel(), device=dev), lens)
+            first = torch.cumsum(lens, 0) - lens
+            pos = lo[sid] + (torch.arange(tot_, device=dev) - first[sid])
+            leaf_row[order[pos].long()] = nd[sid]
+        return tree, leaf_row
+
+
+# ----------------------------------------------------------------------------- ensembles
+@dataclass
+class Ensemble:
+    trees: list
+    weights: list
+    kind: str                         # "gbt" | "rf" | "dt"
+    num_classes: int = 0
+    losses: list = field(default_factory=list)
+
+
+def subsample_weights(n_local, rows: torch.Tensor, rate: float, seed: int, bootstrap: bool) -> torch.Tensor | None:
+    if bootstrap:
+        return sampling.poisson_counts(rows, seed, rate).to(torch.float32)
+    if rate < 1.0:
+        return sampling.bernoulli_mask(rows, seed, rate).to(torch.float32)
+    return None
+
+
+def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_iter: int = 20,
+            step: float = 0.1, max_depth: int = 5, min_instances: float = 1.0, min_info_gain: float = 0.0,
+            subsampling_rate: float = 1.0, seed: int = 0, feature_fraction: float = 1.0, rows=None,
+            classification: bool = True) -> Ensemble:
+    """Spark GradientBoostedTrees.boost: tree 0 fit on (scaled) labels with weight 1, then
+    trees on pseudo-residuals with weight ``step``."""
+    dev = bins.device
+    yy = y.to(torch.float64)
+    if classification:
+        yy = 2.0 * yy - 1.0
+    Fm = torch.zeros_like(yy)
+    trees, weights, losses = [], [], []
+    for m in range(max_iter):
+        if m == 0:
+            target = yy
+        elif loss == "logistic":
+            target = 4.0 * yy / (1.0 + torch.exp(2.0 * yy * Fm))
+        elif loss == "squared":
+            target = 2.0 * (yy - Fm)
+        else:  # absolute
+            target = torch.sign(yy - Fm)
+        sw = w
+        if subsampling_rate < 1.0 and rows is not None:
+            sub = subsample_weights(None, rows, subsampling_rate, seed + m, False)
+            sw = sub if w is None else w * sub
+        tb = TreeBuilder(comm, bins, splits, target.float(), sw, "variance", 1, max_depth, min_instances,
+                         min_info_gain, feature_fraction, seed + m)
+        tree, leaf_row = tb.build()
+        wt = 1.0 if m == 0 else step
+        Fm = Fm + wt * torch.from_numpy(tree.value[:, 0]).to(dev)[leaf_row]
+        trees.append(tree)
+        weights.append(wt)
+        if loss == "logistic":
+            l = torch.log1p(torch.exp(-2.0 * yy * Fm)).sum() * 2.0
+        elif loss == "squared":
+            l = ((yy - Fm) ** 2).sum()
+        else:
+            l = (yy - Fm).abs().sum()
+        cnt = torch.tensor([float(yy.numel())], dtype=torch.float64, device=dev)
+        buf = torch.cat([l.reshape(1), cnt])
+        comm.all_reduce(buf)
+        losses.append(float(buf[0] / buf[1]))
+    return Ensemble(trees, weights, "gbt", 2 if classification else 0, losses)
+
+
+def fit_forest(comm, bins, splits, y, w, num_trees: int, impurity: str, num_classes: int, max_depth: int,
+               min_instances: float, min_info_gain: float, subsampling_rate: float, feature_fraction: float,
+               seed: int, rows: torch.Tensor, bootstrap: bool) -> Ensemble:
+    trees = []
+    for t in range(num_trees):
+        sw = subsample_weights(None, rows, subsampling_rate, seed * 7919 + t, bootstrap)
+        if w is not None:
+            sw = w if sw is None else w * sw
+        tb = TreeBuilder(comm, bins, splits, y, sw, impurity, num_classes, max_depth, min_instances,
+                         min_info_gain, feature_fraction, seed + 31 * t)
+        tree, _ = tb.build()
+        trees.append(tree)
+    return Ensemble(trees, [1.0] * num_trees, "rf", num_classes)
+
+
+def feature_fraction_for(strategy: str, F: int, classification: bool, num_trees: int) -> float:
+    s = str(strategy).lower()
+    if s == "auto":
+        s = "all" if num_trees == 1 else ("sqrt" if classification else "onethird")
+    if s == "all":
+        return 1.0
+    if s == "sqrt":
+        return math.ceil(math.sqrt(F)) / F
+    if s == "log2":
+        return max(1, math.ceil(math.log2(F))) / F
+    if s == "onethird":
+        return math.ceil(F / 3.0) / F
+    try:
+        v = float(s)
+    except ValueError:
+        raise ValueError(f"invalid featureSubsetStrategy {strategy}")
+    if v >= 1.0 and float(v).is_integer() and "." not in s:
+        return min(1.0, v / F)
+    return v
