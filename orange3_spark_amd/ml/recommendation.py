@@ -1,0 +1,217 @@
+"""Recommendation (``pyspark.ml.recommendation`` surface): ALS / ALSModel.
+
+Reached in the reference through the Recommendation widget
+(orangecontrib/spark/widgets/ml/spark_ml_recommendation.py:15).
+"""
+from __future__ import annotations
+
+import os
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from ..frame import column as C
+from ..frame.dataframe import DataFrame, Row
+from ..models import als as ALSE
+from . import common as U
+from .base import Estimator, Model
+from .param import (HasBlockSize, HasCheckpointInterval, HasMaxIter, HasPredictionCol, HasRegParam, HasSeed,
+                    TypeConverters, keyword_only, shared)
+from .util import MLReadable, MLWritable, apply_metadata, register, save_metadata
+
+
+class _ALSModelParams(HasPredictionCol, HasBlockSize):
+    userCol = shared("userCol", "column name for user ids. Ids must be within the integer value range.",
+                     TypeConverters.toString)
+    itemCol = shared("itemCol", "column name for item ids. Ids must be within the integer value range.",
+                     TypeConverters.toString)
+    coldStartStrategy = shared("coldStartStrategy", "strategy for dealing with unknown or new users/items at "
+                               "prediction time. This may be useful in cross-validation or production scenarios, "
+                               "for handling user/item ids the model has not seen in the training data. Supported "
+                               "values: 'nan', 'drop'.", TypeConverters.toString)
+
+    def __init__(self):
+        super().__init__()
+        self._setDefault(userCol="user", itemCol="item", coldStartStrategy="nan", blockSize=4096)
+
+
+class _ALSParams(_ALSModelParams, HasMaxIter, HasRegParam, HasCheckpointInterval, HasSeed):
+    rank = shared("rank", "rank of the factorization", TypeConverters.toInt)
+    numUserBlocks = shared("numUserBlocks", "number of user blocks", TypeConverters.toInt)
+    numItemBlocks = shared("numItemBlocks", "number of item blocks", TypeConverters.toInt)
+    implicitPrefs = shared("implicitPrefs", "whether to use implicit preference", TypeConverters.toBoolean)
+    alpha = shared("alpha", "alpha for implicit preference", TypeConverters.toFloat)
+    ratingCol = shared("ratingCol", "column name for ratings", TypeConverters.toString)
+    nonnegative = shared("nonnegative", "whether to use nonnegative constraint for least squares",
+                         TypeConverters.toBoolean)
+    intermediateStorageLevel = shared("intermediateStorageLevel", "StorageLevel for intermediate datasets. "
+                                      "Cannot be 'NONE'.", TypeConverters.toString)
+    finalStorageLevel = shared("finalStorageLevel", "StorageLevel for ALS model factors.", TypeConverters.toString)
+    cgIters = shared("cgIters", "conjugate-gradient steps per half-iteration for large problems (warm-started; "
+                                "small problems are solved exactly).", TypeConverters.toInt)
+
+    def __init__(self):
+        super().__init__()
+        self._setDefault(rank=10, maxIter=10, regParam=0.1, numUserBlocks=10, numItemBlocks=10,
+                         implicitPrefs=False, alpha=1.0, ratingCol="rating", nonnegative=False,
+                         checkpointInterval=10, intermediateStorageLevel="MEMORY_AND_DISK",
+                         finalStorageLevel="MEMORY_AND_DISK", cgIters=3, seed=0)
+
+
+@register("org.apache.spark.ml.recommendation.ALS")
+class ALS(Estimator, _ALSParams, MLWritable, MLReadable):
+    """Alternating Least Squares matrix factorization (explicit or implicit feedback).
+    Ratings are exchanged with all-to-all into user and item blocks; the other side's
+    factors are all-gathered each half-iteration; per-row systems are solved with
+    kernel-driven conjugate gradient (exact dense solve for small problems)."""
+
+    @keyword_only
+    def __init__(self, *, rank=10, maxIter=10, regParam=0.1, numUserBlocks=10, numItemBlocks=10,
+                 implicitPrefs=False, alpha=1.0, userCol="user", itemCol="item", seed=None, ratingCol="rating",
+                 nonnegative=False, checkpointInterval=10, intermediateStorageLevel="MEMORY_AND_DISK",
+                 finalStorageLevel="MEMORY_AND_DISK", coldStartStrategy="nan", blockSize=4096, cgIters=3):
+        super().__init__()
+        self._set(**self._input_kwargs)
+
+    def _fit(self, df):
+        g = self.getOrDefault
+        users = U.numeric_column(df, g(self.userCol), torch.int64)
+        items = U.numeric_column(df, g(self.itemCol), torch.int64)
+        r = U.numeric_column(df, g(self.ratingCol), torch.float32)
+        res = ALSE.fit_als(df.comm, users, items, r, g(self.rank), g(self.maxIter), g(self.regParam),
+                           g(self.implicitPrefs), g(self.alpha), g(self.seed), g(self.nonnegative), g(self.cgIters))
+        m = ALSModel._from(res.user_ids, res.U, res.item_ids, res.V, g(self.rank))
+        m.iterationSeconds = res.iter_seconds
+        return m._with_parent(self)
+
+
+@register("org.apache.spark.ml.recommendation.ALSModel")
+class ALSModel(Model, _ALSModelParams, MLWritable, MLReadable):
+    def __init__(self):
+        super().__init__()
+        self.rank = 0
+        self._uid_t = self._U = self._iid_t = self._V = None
+
+    @classmethod
+    def _from(cls, uid, U_, iid, V, rank):
+        m = cls()
+        m._uid_t, m._U, m._iid_t, m._V, m.rank = uid, U_, iid, V, int(rank)
+        return m
+
+    def _factors_df(self, ids, F):
+        from ..session import Session
+        s = Session.active() or Session.getOrCreate()
+        full = OrderedDict(id=C.NumericColumn(ids.to(torch.int32)), features=C.VectorColumn(F.float()))
+        return DataFrame(s.local_view(), full)._from_full(full) if s.comm.world_size > 1 else \
+            DataFrame(s, OrderedDict((k, _to(v, s.device)) for k, v in full.items()))
+
+    @property
+    def userFactors(self):
+        return self._factors_df(self._uid_t, self._U)
+
+    @property
+    def itemFactors(self):
+        return self._factors_df(self._iid_t, self._V)
+
+    def _lookup(self, ids_t, table, q):
+        q = q.to(ids_t.device, torch.int64)
+        pos = torch.searchsorted(ids_t, q).clamp_max(max(ids_t.numel() - 1, 0))
+        hit = ids_t[pos] == q if ids_t.numel() else torch.zeros_like(q, dtype=torch.bool)
+        return pos, hit
+
+    def _transform(self, df):
+        g = self.getOrDefault
+        u = U.numeric_column(df, g(self.userCol), torch.int64)
+        i = U.numeric_column(df, g(self.itemCol), torch.int64)
+        pu, hu = self._lookup(self._uid_t, self._U, u)
+        pi, hi = self._lookup(self._iid_t, self._V, i)
+        pred = (self._U[pu].to(torch.float64) * self._V[pi].to(torch.float64)).sum(1)
+        ok = hu & hi
+        pred = torch.where(ok, pred, torch.full_like(pred, float("nan")))
+        out = df.withColumnData(g(self.predictionCol), C.NumericColumn(pred.float()))
+        if g(self.coldStartStrategy) == "drop":
+            out = out._mask(ok.to(df.device))
+        return out
+
+    def _recommend(self, Q, ids_q, T, ids_t, k, qname, tname):
+        from ..session import Session
+        s = Session.active() or Session.getOrCreate()
+        k = min(k, T.shape[0])
+        recs = []
+        for a in range(0, Q.shape[0], 1 << 14):
+            sc = Q[a:a + 1 << 14] @ T.T
+            v, ix = torch.topk(sc, k, dim=1)
+            for row_i, (vv, ii) in enumerate(zip(v.cpu().tolist(), ix.cpu().tolist())):
+                recs.append([Row._make([tname, "rating"], [int(ids_t[j]), float(x)]) for j, x in zip(ii, vv)])
+        cols = OrderedDict()
+        cols[qname] = C.NumericColumn(ids_q.to(torch.int32).to(s.device))
+        arr = np.empty(len(recs), dtype=object)
+        arr[:] = recs
+        cols["recommendations"] = C.ArrayColumn(arr)
+        return DataFrame(s, cols, len(recs))
+
+    def recommendForAllUsers(self, numItems):
+        return self._recommend(self._U, self._uid_t, self._V, self._iid_t.cpu().numpy(), numItems,
+                               self.getOrDefault(self.userCol), self.getOrDefault(self.itemCol))
+
+    def recommendForAllItems(self, numUsers):
+        return self._recommend(self._V, self._iid_t, self._U, self._uid_t.cpu().numpy(), numUsers,
+                               self.getOrDefault(self.itemCol), self.getOrDefault(self.userCol))
+
+    def recommendForUserSubset(self, dataset, numItems):
+        q = U.numeric_column(dataset, self.getOrDefault(self.userCol), torch.int64)
+        pos, hit = self._lookup(self._uid_t, self._U, torch.unique(q))
+        return self._recommend(self._U[pos[hit]], self._uid_t[pos[hit]], self._V, self._iid_t.cpu().numpy(),
+                               numItems, self.getOrDefault(self.userCol), self.getOrDefault(self.itemCol))
+
+    def recommendForItemSubset(self, dataset, numUsers):
+        q = U.numeric_column(dataset, self.getOrDefault(self.itemCol), torch.int64)
+        pos, hit = self._lookup(self._iid_t, self._V, torch.unique(q))
+        return self._recommend(self._V[pos[hit]], self._iid_t[pos[hit]], self._U, self._uid_t.cpu().numpy(),
+                               numUsers, self.getOrDefault(self.itemCol), self.getOrDefault(self.userCol))
+
+    # Spark layout: metadata (+rank), userFactors/ and itemFactors/ parquet (id:int, features:array<float>)
+    def _extra_metadata(self):
+        return {"rank": self.rank}
+
+    def write(self):
+        from .util import MLWriter
+
+        class _W(MLWriter):
+            def saveImpl(w, path):
+                save_metadata(self, path, self._extra_metadata())
+                from .util import _is_rank0
+                if _is_rank0():
+                    import pyarrow as pa
+                    import pyarrow.parquet as pq
+                    for name, ids, F in (("userFactors", self._uid_t, self._U), ("itemFactors", self._iid_t, self._V)):
+                        d = os.path.join(path, name)
+                        os.makedirs(d, exist_ok=True)
+                        t = pa.table({"id": pa.array(ids.cpu().numpy().astype(np.int32)),
+                                      "features": pa.array(F.float().cpu().numpy().tolist(),
+                                                           type=pa.list_(pa.float32()))})
+                        pq.write_table(t, os.path.join(d, "part-00000.snappy.parquet"))
+        return _W(self)
+
+    @classmethod
+    def _load_impl(cls, path, meta):
+        import pyarrow.parquet as pq
+        from ..session import Session
+        dev = (Session.active() or Session.getOrCreate()).device
+        parts = []
+        for name in ("userFactors", "itemFactors"):
+            t = pq.read_table(os.path.join(path, name)).to_pydict()
+            ids = torch.tensor(t["id"], dtype=torch.int64)
+            o = torch.argsort(ids)
+            F = torch.tensor(t["features"], dtype=torch.float32)[o]
+            parts += [ids[o].to(dev), F.to(dev)]
+        m = cls._from(parts[0], parts[1], parts[2], parts[3], meta.get("rank", parts[1].shape[1]))
+        apply_metadata(m, meta)
+        return m
+
+
+def _to(c, dev):
+    if isinstance(c, C.NumericColumn):
+        return C.NumericColumn(c.data.to(dev))
+    return C.VectorColumn(c.data.to(dev))

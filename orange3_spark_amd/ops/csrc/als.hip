@@ -1,0 +1,98 @@
+// ALS ratings passes (gfx950).  Replaces the per-block normal-equation assembly of
+// Spark's ALS (reached through the Recommendation widget -> fit,
+// orangecontrib/spark/widgets/ml/spark_ml_recommendation.py:15).
+//
+// The solver is conjugate gradient on each user's (item's) normal equations, so the
+// rank x rank systems are never formed: every CG step needs only
+//     out[u] = sum_{j in row u} w_j * (F[col_j] . V[u]) * F[col_j]          (MATVEC)
+// and once per half-iteration the right-hand side
+//     out[u] = sum_{j in row u} b_j * F[col_j]                              (RHS)
+// over the CSR ratings of this rank (rows = users for the user half, items for the item
+// half; F = the all-gathered factor table of the other side).  The dense parts
+// (implicit Y^T Y . v, lambda * n_u * v) are batched GEMMs done by the caller.
+//
+// One wave per CSR row: lane l holds dims l, l+64, ... (R/64 per lane) of V[u] and of
+// the accumulator in registers; F rows are streamed 16 B... per lane-pair coalesced
+// (R*4 bytes contiguous per rating); the per-rating dot product is one wave
+// reduction.  4 ratings are kept in flight per wave to hide gather latency.
+#include "common.h"
+
+using namespace o3s;
+
+namespace {
+
+constexpr int kAlsWaves = 4;
+
+template <int RV, int MODE>   // RV = dims per lane (R = 64*RV); MODE 0 = MATVEC, 1 = RHS
+__global__ __launch_bounds__(kAlsWaves * 64) void als_pass_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ coef,
+    int64_t nrows, const float* __restrict__ F, int R, const float* __restrict__ V, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t u = (int64_t)blockIdx.x * kAlsWaves + (threadIdx.x >> 6);
+  if (u >= nrows) return;
+  float v[RV], acc[RV];
+#pragma unroll
+  for (int k = 0; k < RV; ++k) {
+    const int d = lane + 64 * k;
+    v[k] = (MODE == 0 && d < R) ? V[u * R + d] : 0.f;
+    acc[k] = 0.f;
+  }
+  const int64_t s0 = indptr[u], s1 = indptr[u + 1];
+  constexpr int U = 4;
+  for (int64_t j0 = s0; j0 < s1; j0 += U) {
+    float f[U][RV], cj[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int64_t j = j0 + q;
+      const bool ok = j < s1;
+      const int64_t jc = ok ? j : s0;
+      const int64_t c = cols[jc];
+      cj[q] = ok ? coef[jc] : 0.f;
+#pragma unroll
+      for (int k = 0; k < RV; ++k) {
+        const int d = lane + 64 * k;
+        f[q][k] = d < R ? F[c * R + d] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      float s = cj[q];
+      if (MODE == 0) {
+        float dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < RV; ++k) dot = fmaf(f[q][k], v[k], dot);
+        s *= wave_sum(dot);
+      }
+#pragma unroll
+      for (int k = 0; k < RV; ++k) acc[k] = fmaf(s, f[q][k], acc[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < RV; ++k) {
+    const int d = lane + 64 * k;
+    if (d < R) out[u * R + d] = acc[k];
+  }
+}
+
+}  // namespace
+
+O3S_API int o3s_als_pass(int mode, const int64_t* indptr, const int32_t* cols, const float* coef, int64_t nrows,
+                         const float* F, int R, const float* V, float* out, hipStream_t st) {
+  if (nrows <= 0) return 0;
+  if (R <= 0 || R > 512) return -1;
+  const int rv = (R + 63) / 64;
+  const unsigned grid = (unsigned)((nrows + kAlsWaves - 1) / kAlsWaves);
+#define O3S_AL(RVV)                                                                                      \
+  if (rv == RVV) {                                                                                       \
+    if (mode == 0)                                                                                       \
+      hipLaunchKernelGGL((als_pass_kernel<RVV, 0>), dim3(grid), dim3(kAlsWaves * 64), 0, st, indptr, cols, \
+                         coef, nrows, F, R, V, out);                                                     \
+    else                                                                                                 \
+      hipLaunchKernelGGL((als_pass_kernel<RVV, 1>), dim3(grid), dim3(kAlsWaves * 64), 0, st, indptr, cols, \
+                         coef, nrows, F, R, V, out);                                                     \
+  }
+  O3S_AL(1) O3S_AL(2) O3S_AL(3) O3S_AL(4) O3S_AL(5) O3S_AL(6) O3S_AL(7) O3S_AL(8)
+#undef O3S_AL
+  O3S_CHECK_LAUNCH();
+  return 0;
+}

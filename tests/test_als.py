@@ -1,0 +1,122 @@
+"""ALS: explicit/implicit on CPU vs a numpy reference; GPU kernel vs torch; CG vs exact."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from orange3_spark_amd import Session, SessionConf
+from orange3_spark_amd.ml.evaluation import RegressionEvaluator
+from orange3_spark_amd.ml.recommendation import ALS, ALSModel
+from orange3_spark_amd.models import als as AE
+
+
+@pytest.fixture(scope="module")
+def cpu():
+    return Session(SessionConf().set("o3s.device", "cpu"))
+
+
+def _ratings(n_u=60, n_i=40, rank=3, density=0.5, seed=0):
+    rng = np.random.default_rng(seed)
+    U = rng.normal(size=(n_u, rank))
+    V = rng.normal(size=(n_i, rank))
+    mask = rng.uniform(size=(n_u, n_i)) < density
+    u, i = np.nonzero(mask)
+    r = (U @ V.T)[u, i] + 0.01 * rng.normal(size=u.size)
+    return pd.DataFrame({"user": u * 3 + 7, "item": i * 5 + 1, "rating": r})
+
+
+def _numpy_als(pdf, rank, iters, reg, implicit, alpha, X, Y):
+    users = np.unique(pdf.user.values)
+    items = np.unique(pdf.item.values)
+    ui = np.searchsorted(users, pdf.user.values)
+    ii = np.searchsorted(items, pdf.item.values)
+    r = pdf.rating.values
+    X, Y = X.copy(), Y.copy()
+
+    def solve(nrows, rows, cols, F, Fother_tf):
+        out = np.zeros((nrows, rank))
+        for u in range(nrows):
+            sel = rows == u
+            Fg = F[cols[sel]]
+            rr = r[sel]
+            if implicit:
+                c1 = alpha * np.abs(rr)
+                A = Fother_tf + (Fg * c1[:, None]).T @ Fg + reg * (rr > 0).sum() * np.eye(rank)
+                b = ((1 + c1) * (rr > 0)) @ Fg
+            else:
+                A = Fg.T @ Fg + reg * sel.sum() * np.eye(rank)
+                b = rr @ Fg
+            out[u] = np.linalg.solve(A, b)
+        return out
+    for _ in range(iters):
+        X = solve(len(users), ui, ii, Y, Y.T @ Y)
+        Y = solve(len(items), ii, ui, X, X.T @ X)
+    return X, Y
+
+
+@pytest.mark.parametrize("implicit", [False, True])
+def test_als_matches_numpy_reference(cpu, implicit):
+    pdf = _ratings(seed=1)
+    df = cpu.createDataFrame(pdf)
+    m = ALS(rank=3, maxIter=5, regParam=0.05, implicitPrefs=implicit, alpha=2.0, seed=3).fit(df)
+    # rebuild the same initial factors the engine used
+    users, items = np.unique(pdf.user), np.unique(pdf.item)
+    X0 = AE.init_factors(0, len(users), 3, 3, "cpu", False).double().numpy()
+    Y0 = AE.init_factors(0, len(items), 3, 3 ^ 0x5A5A, "cpu", False).double().numpy()
+    X, Y = _numpy_als(pdf, 3, 5, 0.05, implicit, 2.0, X0, Y0)
+    assert np.allclose(m._U.double().numpy(), X, atol=1e-4)
+    assert np.allclose(m._V.double().numpy(), Y, atol=1e-4)
+
+
+def test_als_explicit_fits_low_rank(cpu):
+    pdf = _ratings(n_u=80, n_i=50, seed=2, density=0.6)
+    df = cpu.createDataFrame(pdf)
+    m = ALS(rank=3, maxIter=15, regParam=0.01, seed=1).fit(df)
+    rmse = RegressionEvaluator(labelCol="rating", metricName="rmse").evaluate(m.transform(df))
+    assert rmse < 0.1
+    recs = m.recommendForAllUsers(3).collect()
+    assert len(recs) == 80 and len(recs[0].recommendations) == 3
+
+
+def test_als_cold_start_and_save(cpu, tmp_path):
+    pdf = _ratings(seed=3)
+    df = cpu.createDataFrame(pdf)
+    m = ALS(rank=2, maxIter=3, seed=0, coldStartStrategy="drop").fit(df)
+    test = cpu.createDataFrame(pd.DataFrame({"user": [7, 99999], "item": [1, 1]}))
+    assert m.transform(test).count() == 1
+    m.save(str(tmp_path / "als"))
+    m2 = ALSModel.load(str(tmp_path / "als"))
+    assert torch.allclose(m2._U, m._U) and m2.rank == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [10, 64, 128])
+def test_gpu_als_pass_matches_torch(gpu, R):
+    from orange3_spark_amd.ops import als as A
+    g = torch.Generator(device="cpu").manual_seed(R)
+    n, m, nnz = 3000, 2000, 60000
+    rows = torch.sort(torch.randint(0, n, (nnz,), generator=g)).values
+    indptr = torch.zeros(n + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(torch.bincount(rows, minlength=n), 0)
+    cols = torch.randint(0, m, (nnz,), generator=g, dtype=torch.int32)
+    coef = torch.rand(nnz, generator=g)
+    F = torch.randn(m, R, generator=g)
+    V = torch.randn(n, R, generator=g)
+    for mode in (0, 1):
+        a = A.pass_(mode, indptr.to(gpu), cols.to(gpu), coef.to(gpu), F.to(gpu), V.to(gpu) if mode == 0 else None)
+        b = A.pass_torch(mode, indptr, cols, coef, F, V)
+        assert torch.allclose(a.cpu(), b, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_gpu_als_cg_close_to_exact():
+    s = Session(SessionConf().set("o3s.device", "cuda"))
+    df = s.synthetic.ratings(20000, 3000, 400000, rank=8, seed=1, implicit=True)
+    ex = ALS(rank=16, maxIter=4, implicitPrefs=True, alpha=1.0, seed=1).fit(df)
+    users = df.column_data("user").data.long()
+    items = df.column_data("item").data.long()
+    r = df.column_data("rating").data
+    res = AE.fit_als(s.comm, users, items, r, 16, 4, 0.1, True, 1.0, 1, cg_iters=8, exact=False)
+    pe = (ex._U @ ex._V.T)
+    pc = (res.U @ res.V.T)
+    assert ((pe - pc).norm() / pe.norm()).item() < 0.05
