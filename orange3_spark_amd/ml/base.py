@@ -177,8 +177,9 @@ class Pipeline(Estimator, MLWritable, MLReadable):
 
     @classmethod
     def _load_impl(cls, path, meta):
+        from .util import set_uid
         p = Pipeline(stages=_load_stages(path, meta))
-        p.uid = meta["uid"]
+        set_uid(p, meta["uid"])
         return p
 
 
@@ -189,7 +190,8 @@ class PipelineModel(Model, MLWritable, MLReadable):
         self.stages = list(stages or [])
 
     def _with_uid(self, uid):
-        self.uid = uid
+        from .util import set_uid
+        set_uid(self, uid)
         return self
 
     def _transform(self, dataset):

@@ -132,16 +132,24 @@ def load_metadata(path: str, expected_class: str | None = None) -> dict:
 
 def apply_metadata(instance, meta: dict) -> None:
     """Restore uid + param values (skipping params this implementation lacks)."""
-    instance.uid = meta["uid"]
-    for p in instance.params:
-        p.parent = instance.uid
-    instance._params = None
+    set_uid(instance, meta["uid"])
     for name, v in meta.get("defaultParamMap", {}).items():
         if instance.hasParam(name):
             instance._defaultParamMap[instance.getParam(name)] = _from_json(instance, name, v)
     for name, v in meta.get("paramMap", {}).items():
         if instance.hasParam(name):
             instance._set(**{name: _from_json(instance, name, v)})
+
+
+def set_uid(instance, uid: str) -> None:
+    """Re-key an instance's params to a new uid (Param hashing depends on the parent uid)."""
+    defaults = {p.name: v for p, v in instance._defaultParamMap.items()}
+    values = {p.name: v for p, v in instance._paramMap.items()}
+    instance.uid = uid
+    instance._params = None
+    instance._copy_params()
+    instance._defaultParamMap = {instance.getParam(k): v for k, v in defaults.items()}
+    instance._paramMap = {instance.getParam(k): v for k, v in values.items()}
 
 
 def _from_json(instance, name, v):

@@ -34,6 +34,7 @@ _SIGS: dict[str, list] = {
     "o3s_glm_colstats": [c_i32, c_vp, c_i64, c_i64, c_vp, c_u32, c_i64, c_vp, c_i32, c_vp, c_vp],
     "o3s_kmeans_assign": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
     "o3s_kmeans_update_ws": [c_i32, c_i32, c_i32, C.POINTER(c_i64), C.POINTER(c_i64), C.POINTER(c_i32)],
+    "o3s_murmur3_terms": [c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp, c_vp],
     "o3s_als_pass": [c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp],
     "o3s_tree_hist_lds": [c_i32, c_i32, c_i32],
     "o3s_tree_hist": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],
@@ -75,6 +76,31 @@ def kernels():
         if _LIB is not None:
             return _LIB
         return _load()
+
+
+_HOST_SIGS: dict[str, list] = {
+    "o3s_host_murmur3": [c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp],
+    "o3s_host_tokenize": [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp],
+}
+
+
+def host():
+    """Host C++ runtime library (text hashing/tokenizing); built with the kernels."""
+    global _HOST
+    if _HOST is not None:
+        return _HOST
+    with _LOCK:
+        if _HOST is None:
+            path = _build.HOST_LIB
+            if not path.exists():
+                _build.build()
+            lib = C.CDLL(str(path))
+            for name, argt in _HOST_SIGS.items():
+                fn = getattr(lib, name)
+                fn.argtypes = argt
+                fn.restype = C.c_int64 if name == "o3s_host_tokenize" else None
+            _HOST = lib
+    return _HOST
 
 
 def available() -> bool:

@@ -1,0 +1,121 @@
+"""Feature transformers/estimators on the CPU path vs numpy / scikit-learn / Spark-doc values."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from orange3_spark_amd import Session, SessionConf
+from orange3_spark_amd.ml import feature as F
+from orange3_spark_amd.ml.base import Pipeline, PipelineModel
+from orange3_spark_amd.ml.classification import LogisticRegression
+
+
+@pytest.fixture(scope="module")
+def s():
+    return Session(SessionConf().set("o3s.device", "cpu"))
+
+
+def test_hashing_tf_matches_spark_doc_example(s):
+    df = s.createDataFrame(pd.DataFrame({"words": [["a", "b", "c"]]}))
+    out = F.HashingTF(numFeatures=10, inputCol="words", outputCol="features").transform(df)
+    v = out.collect()[0].features
+    assert list(v.indices) == [5, 7, 8] and list(v.values) == [1.0, 1.0, 1.0]
+
+
+def test_tokenizer_stopwords_ngram_countvectorizer_idf(s):
+    df = s.createDataFrame(pd.DataFrame({"text": ["Hello world of Spark", "the quick brown fox", "hello hello"]}))
+    tok = F.Tokenizer(inputCol="text", outputCol="words").transform(df)
+    assert tok.collect()[0].words == ["hello", "world", "of", "spark"]
+    sw = F.StopWordsRemover(inputCol="words", outputCol="clean").transform(tok)
+    assert sw.collect()[1].clean == ["quick", "brown", "fox"]
+    ng = F.NGram(n=2, inputCol="words", outputCol="ng").transform(tok)
+    assert ng.collect()[2].ng == ["hello hello"]
+    cvm = F.CountVectorizer(inputCol="words", outputCol="tf").fit(tok)
+    assert cvm.vocabulary[0] == "hello"
+    tf = cvm.transform(tok)
+    idf = F.IDF(inputCol="tf", outputCol="tfidf").fit(tf)
+    out = idf.transform(tf).collect()
+    assert np.isclose(idf.idf.toArray()[0], np.log(4 / 3))
+    assert out[2].tfidf.values[0] == pytest.approx(2 * np.log(4 / 3))
+    rt = F.RegexTokenizer(inputCol="text", outputCol="w2", pattern="\\W+").transform(df)
+    assert rt.collect()[0].w2 == ["hello", "world", "of", "spark"]
+
+
+def test_scalers_match_sklearn(s):
+    from sklearn.preprocessing import MaxAbsScaler, MinMaxScaler, StandardScaler
+    rng = np.random.default_rng(0)
+    X = rng.normal(size=(200, 4)) * [1, 2, 3, 4] + [0, 1, 2, 3]
+    df = s.createDataFrame(pd.DataFrame({"f": list(X)}))
+    ss = F.StandardScaler(inputCol="f", outputCol="o", withMean=True).fit(df).transform(df)
+    got = np.stack([r.o.toArray() for r in ss.collect()])
+    ref = (X - X.mean(0)) / X.std(0, ddof=1)
+    assert np.allclose(got, ref)
+    mm = F.MinMaxScaler(inputCol="f", outputCol="o").fit(df).transform(df)
+    assert np.allclose(np.stack([r.o.toArray() for r in mm.collect()]), MinMaxScaler().fit_transform(X))
+    ma = F.MaxAbsScaler(inputCol="f", outputCol="o").fit(df).transform(df)
+    assert np.allclose(np.stack([r.o.toArray() for r in ma.collect()]), MaxAbsScaler().fit_transform(X))
+
+
+def test_string_indexer_onehot_index_to_string(s):
+    df = s.createDataFrame(pd.DataFrame({"c": ["a", "b", "a", "c", "a", "c"]}))
+    m = F.StringIndexer(inputCol="c", outputCol="ci").fit(df)
+    assert m.labels == ["a", "c", "b"]
+    out = m.transform(df)
+    assert [r.ci for r in out.collect()] == [0.0, 2.0, 0.0, 1.0, 0.0, 1.0]
+    oh = F.OneHotEncoder(inputCols=["ci"], outputCols=["oh"]).fit(out).transform(out)
+    v = oh.collect()[1].oh
+    assert v.size == 2 and v.toArray().tolist() == [0.0, 0.0]
+    back = F.IndexToString(inputCol="ci", outputCol="orig", labels=m.labels).transform(out)
+    assert [r.orig for r in back.collect()] == ["a", "b", "a", "c", "a", "c"]
+
+
+def test_pca_matches_numpy(s):
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(300, 5)) @ rng.normal(size=(5, 5))
+    df = s.createDataFrame(pd.DataFrame({"f": list(X)}))
+    m = F.PCA(k=2, inputCol="f", outputCol="p").fit(df)
+    w, v = np.linalg.eigh(np.cov(X.T))
+    top = v[:, np.argsort(w)[::-1][:2]]
+    assert np.allclose(np.abs(m.pc.toArray()), np.abs(top), atol=1e-8)
+
+
+def test_misc_transformers(s):
+    df = s.createDataFrame(pd.DataFrame({"x": [0.1, 0.6, 1.5], "v": [np.array([1.0, 2.0])] * 3}))
+    assert [r.b for r in F.Binarizer(threshold=0.5, inputCol="x", outputCol="b").transform(df).collect()] == [0, 1, 1]
+    bz = F.Bucketizer(splits=[-np.inf, 0.5, 1.0, np.inf], inputCol="x", outputCol="b").transform(df)
+    assert [r.b for r in bz.collect()] == [0.0, 1.0, 2.0]
+    pe = F.PolynomialExpansion(degree=2, inputCol="v", outputCol="p").transform(df).collect()[0].p.toArray()
+    assert pe.tolist() == [1.0, 1.0, 2.0, 2.0, 4.0]     # Spark order: x, x^2, y, xy, y^2
+    nz = F.Normalizer(p=1.0, inputCol="v", outputCol="n").transform(df).collect()[0].n.toArray()
+    assert np.allclose(nz, [1 / 3, 2 / 3])
+    ew = F.ElementwiseProduct(scalingVec=[2.0, 3.0], inputCol="v", outputCol="e").transform(df)
+    assert ew.collect()[0].e.toArray().tolist() == [2.0, 6.0]
+    dct = F.DCT(inputCol="v", outputCol="d").transform(df).collect()[0].d.toArray()
+    from scipy.fft import dct as sdct
+    assert np.allclose(dct, sdct(np.array([1.0, 2.0]), norm="ortho"))
+    imp = F.Imputer(inputCols=["x"], outputCols=["xi"], strategy="median").fit(df)
+    assert imp.surrogates["x"] == 0.6
+
+
+def test_pipeline_fit_save_load(s, tmp_path):
+    rng = np.random.default_rng(2)
+    X = rng.normal(size=(400, 3))
+    y = (X @ [1, -2, 0.5] > 0).astype(float)
+    df = s.createDataFrame(pd.DataFrame({"a": X[:, 0], "b": X[:, 1], "c": X[:, 2], "label": y}))
+    pipe = Pipeline(stages=[F.VectorAssembler(inputCols=["a", "b", "c"], outputCol="raw"),
+                            F.StandardScaler(inputCol="raw", outputCol="features"),
+                            LogisticRegression(maxIter=50)])
+    pm = pipe.fit(df)
+    acc = (pm.transform(df).toPandas()["prediction"].values == y).mean()
+    assert acc > 0.95
+    pm.save(str(tmp_path / "pm"))
+    pm2 = PipelineModel.load(str(tmp_path / "pm"))
+    p1 = pm.transform(df).toPandas()["prediction"].values
+    p2 = pm2.transform(df).toPandas()["prediction"].values
+    assert np.array_equal(p1, p2)
+    import json
+    meta = json.loads(open(tmp_path / "pm" / "metadata" / "part-00000").read())
+    assert meta["class"] == "org.apache.spark.ml.PipelineModel" and len(meta["paramMap"]["stageUids"]) == 3
+    pipe.save(str(tmp_path / "p"))
+    p3 = Pipeline.load(str(tmp_path / "p"))
+    assert [type(x).__name__ for x in p3.getStages()] == ["VectorAssembler", "StandardScaler", "LogisticRegression"]
