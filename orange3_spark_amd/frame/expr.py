@@ -260,7 +260,7 @@ def lit(value: Any) -> Expr:
         if isinstance(value, bool):
             return C.NumericColumn(torch.full((n,), value, dtype=torch.bool, device=df.device), None, T.BooleanType())
         if isinstance(value, int):
-            return C.NumericColumn(torch.full((n,), value, dtype=torch.int64 if abs(value) > 2**31 - 1 else torch.int32,
+            return C.NumericColumn(torch.full((n,), value, dtype=torch.int64 if (value > 2**31 - 1 or value < -2**31) else torch.int32,
                                               device=df.device))
         if isinstance(value, float):
             return C.NumericColumn(torch.full((n,), value, dtype=torch.float64, device=df.device))

@@ -1,0 +1,177 @@
+"""SQL execution over catalog tables / temp views (``session.sql``)."""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+
+from ..frame import column as C
+from ..frame import expr as E
+from ..frame.dataframe import DataFrame
+from .parser import AggCall, Select, _AggExpr, _as_agg_expr, parse
+
+
+def _strings_df(session, data: dict) -> DataFrame:
+    cols = OrderedDict((k, C.StringColumn(np.array(v, dtype=object)) if not isinstance(v, C.Column) else v)
+                       for k, v in data.items())
+    local = DataFrame(session.local_view(), cols)
+    return DataFrame(session, OrderedDict(), 0)._from_full(local._cols) if session.comm.world_size > 1 else \
+        DataFrame(session, cols)
+
+
+def execute(session, query: str) -> DataFrame:
+    stmt = parse(query)
+    kind = stmt[0]
+    cat = session.catalog
+    if kind == "show_databases":
+        return _strings_df(session, {"databaseName": cat.databaseNames()})
+    if kind == "show_tables":
+        db = stmt[1] or cat.currentDatabase()
+        names = cat.tableNames(db)
+        return _strings_df(session, {"namespace": [db] * len(names), "tableName": names,
+                                     "isTemporary": ["true" if n in cat._temp else "false" for n in names]})
+    if kind == "use":
+        cat.setCurrentDatabase(stmt[1])
+        return session.emptyDataFrame()
+    if kind == "create_database":
+        cat.createDatabase(stmt[1], ifNotExists=True)
+        return session.emptyDataFrame()
+    if kind == "drop_table":
+        if cat.tableExists(stmt[1]) or not stmt[2]:
+            if stmt[1] in cat._temp:
+                cat.dropTempView(stmt[1])
+            else:
+                cat.dropTable(stmt[1])
+        return session.emptyDataFrame()
+    if kind == "drop_database":
+        cat.dropDatabase(stmt[1])
+        return session.emptyDataFrame()
+    if kind == "describe":
+        df = cat.table(stmt[1])
+        return _strings_df(session, {"col_name": df.columns, "data_type": [t for _, t in df.dtypes],
+                                     "comment": [None] * len(df.columns)})
+    if kind == "ctas":
+        df = run_select(session, stmt[2])
+        cat.saveAsTable(df, stmt[1], "error")
+        return session.emptyDataFrame()
+    return run_select(session, stmt[1])
+
+
+def run_select(session, s: Select) -> DataFrame:
+    if s.subquery is not None:
+        df = run_select(session, s.subquery)
+    elif s.table is not None:
+        df = session.catalog.table(s.table)
+    else:
+        df = DataFrame(session, OrderedDict(_dummy=C.NumericColumn(_zeros(session))), 1 if session.rank == 0 else 0)
+    for j in s.joins:
+        right = session.catalog.table(j.table)
+        df = _sql_join(df, right, j)
+    if s.where is not None:
+        df = df.filter(s.where)
+    has_agg = any(isinstance(it.expr, (AggCall, _AggExpr)) for it in s.items) or s.group_by
+    if has_agg:
+        df = _aggregate(df, s)
+    else:
+        sel = []
+        for it in s.items:
+            if isinstance(it.expr, str) and it.expr == "*":
+                sel += [c for c in df.columns if c != "_dummy"]
+            else:
+                sel.append(it.expr.alias(it.alias) if it.alias else it.expr)
+        order_exprs = s.order_by
+        if order_exprs:
+            # order by may reference columns not selected: sort first
+            df = df.orderBy(*[e for e, _ in order_exprs], ascending=[a for _, a in order_exprs])
+            order_exprs = []
+        df = df.select(*sel)
+        if s.distinct:
+            df = df.distinct()
+    if s.order_by and has_agg:
+        keys = []
+        for e, a in s.order_by:
+            if isinstance(e, (AggCall, _AggExpr)):
+                keys.append((E.col(_as_agg_expr(e).text), a))
+            else:
+                keys.append((e, a))
+        df = df.orderBy(*[k for k, _ in keys], ascending=[a for _, a in keys])
+    if s.limit is not None:
+        df = df.limit(s.limit)
+    if s.union is not None:
+        other = run_select(session, s.union)
+        df = df.union(other)
+        if not s.union_all:
+            df = df.distinct()
+    return df
+
+
+def _zeros(session):
+    import torch
+    return torch.zeros(1 if session.rank == 0 else 0, dtype=torch.int32, device=session.device)
+
+
+def _sql_join(left: DataFrame, right: DataFrame, j) -> DataFrame:
+    if j.how == "cross" or j.on is None:
+        return left.join(right, None, "cross")
+    # support equi-joins "a.x = b.y" (and conjunctions of them)
+    keys = _equi_keys(j.on)
+    if keys is None:
+        raise NotImplementedError("only equi-join ON conditions are supported")
+    lk, rk = zip(*keys)
+    if list(lk) == list(rk):
+        return left.join(right, list(lk), j.how)
+    r2 = right
+    for a, b in keys:
+        if a != b:
+            r2 = r2.withColumnRenamed(b, a)
+    return left.join(r2, list(lk), j.how)
+
+
+def _equi_keys(cond):
+    name = getattr(cond, "name", "")
+    import re
+    parts = [p.strip("() ") for p in re.split(r"\bAND\b", name)]
+    out = []
+    for p in parts:
+        m = re.fullmatch(r"\(?\s*([\w.]+)\s*=\s*([\w.]+)\s*\)?", p)
+        if not m:
+            return None
+        out.append((m.group(1).split(".")[-1], m.group(2).split(".")[-1]))
+    return out
+
+
+def _aggregate(df: DataFrame, s: Select) -> DataFrame:
+    keys = list(s.group_by)
+    aggs: "OrderedDict[str, AggCall]" = OrderedDict()
+    post = []
+    for it in s.items:
+        if isinstance(it.expr, str) and it.expr == "*":
+            raise ValueError("SELECT * with GROUP BY is not supported")
+        ae = _as_agg_expr(it.expr) if isinstance(it.expr, (AggCall, _AggExpr)) else None
+        if ae is not None:
+            for a in ae.aggs:
+                aggs[a.text] = a
+            post.append((ae, it.alias or ae.text))
+        else:
+            post.append((it.expr, it.alias or it.expr.name))
+    if s.having is not None:
+        for a in _as_agg_expr(s.having).aggs:
+            aggs[a.text] = a
+    for e, _ in s.order_by:
+        if isinstance(e, (AggCall, _AggExpr)):
+            for a in _as_agg_expr(e).aggs:
+                aggs[a.text] = a
+    agg_objs = [E.Agg(a.fn, a.arg, a.text, a.distinct) for a in aggs.values()]
+    g = df.groupBy(*keys).agg(*agg_objs)
+    names = {k: k for k in aggs}
+    if s.having is not None:
+        g = g.filter(_as_agg_expr(s.having).build(names))
+    sel = []
+    for e, alias in post:
+        if isinstance(e, _AggExpr):
+            sel.append(e.build(names).alias(alias))
+        else:
+            sel.append(E.col(e.name).alias(alias) if e.name in g.columns else e.alias(alias))
+    extra = [k for k in aggs if k not in {a for _, a in post}]
+    out = g.select(*sel, *[E.col(k) for k in extra if s.order_by])
+    return out

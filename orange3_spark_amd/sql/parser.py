@@ -1,0 +1,522 @@
+"""Hand-written SQL tokenizer + recursive-descent parser (the SparkSQL subset the "Data
+Frame" widget needs; reference: orangecontrib/spark/widgets/data/spark_sql_dataframe.py:83-94
+runs ``hc.sql(query)``; Hive Table uses ``show databases``, spark_table.py:41).
+
+Produces plain tuples (the AST) consumed by ``sql.engine``; scalar expressions compile
+to ``frame.expr.Expr`` so evaluation is the same vectorised device code as the
+DataFrame API.
+"""
+from __future__ import annotations
+
+import re
+from dataclasses import dataclass, field
+
+from ..frame import expr as E
+
+_TOKEN = re.compile(r"""
+    (?P<ws>\s+|--[^\n]*)
+  | (?P<num>\d+\.\d*(?:[eE][-+]?\d+)?|\.\d+(?:[eE][-+]?\d+)?|\d+(?:[eE][-+]?\d+)?)
+  | (?P<str>'(?:[^']|'')*')
+  | (?P<qid>`[^`]+`|"[^"]+")
+  | (?P<op><=|>=|<>|!=|==|\|\||[-+*/%(),.;=<>])
+  | (?P<id>[A-Za-z_][A-Za-z0-9_]*)
+""", re.X)
+
+KEYWORDS = {"select", "from", "where", "group", "by", "order", "having", "limit", "as", "and", "or", "not",
+            "null", "is", "in", "like", "between", "distinct", "asc", "desc", "true", "false", "case", "when",
+            "then", "else", "end", "cast", "join", "inner", "left", "right", "outer", "full", "cross", "on",
+            "union", "all", "show", "databases", "tables", "use", "create", "database", "drop", "table", "if",
+            "exists", "describe", "desc", "with"}
+
+
+@dataclass
+class Tok:
+    kind: str
+    val: str
+
+
+def tokenize(sql: str) -> list[Tok]:
+    out, pos = [], 0
+    while pos < len(sql):
+        m = _TOKEN.match(sql, pos)
+        if not m:
+            raise SyntaxError(f"unexpected character at {pos}: {sql[pos:pos + 20]!r}")
+        pos = m.end()
+        kind = m.lastgroup
+        v = m.group(kind)
+        if kind == "ws":
+            continue
+        if kind == "qid":
+            out.append(Tok("id", v[1:-1]))
+        elif kind == "id" and v.lower() in KEYWORDS:
+            out.append(Tok("kw", v.lower()))
+        else:
+            out.append(Tok(kind, v))
+    out.append(Tok("eof", ""))
+    return out
+
+
+@dataclass
+class SelectItem:
+    expr: object            # Expr | AggCall | "*"
+    alias: str | None = None
+
+
+@dataclass
+class AggCall:
+    fn: str
+    arg: object             # Expr or None (count(*))
+    distinct: bool = False
+    text: str = ""
+
+
+@dataclass
+class Join:
+    table: str
+    alias: str | None
+    how: str
+    on: object
+
+
+@dataclass
+class Select:
+    items: list
+    table: str | None = None
+    alias: str | None = None
+    subquery: object = None
+    joins: list = field(default_factory=list)
+    where: object = None
+    group_by: list = field(default_factory=list)
+    having: object = None
+    order_by: list = field(default_factory=list)
+    limit: int | None = None
+    distinct: bool = False
+    union: object = None
+    union_all: bool = False
+
+
+class Parser:
+    def __init__(self, sql: str):
+        self.toks = tokenize(sql)
+        self.i = 0
+        self.src = sql
+
+    # -- helpers ---------------------------------------------------------------
+    def peek(self, k=0) -> Tok:
+        return self.toks[min(self.i + k, len(self.toks) - 1)]
+
+    def next(self) -> Tok:
+        t = self.toks[self.i]
+        self.i += 1
+        return t
+
+    def accept(self, kind, val=None) -> Tok | None:
+        t = self.peek()
+        if t.kind == kind and (val is None or t.val == val):
+            self.i += 1
+            return t
+        return None
+
+    def expect(self, kind, val=None) -> Tok:
+        t = self.accept(kind, val)
+        if t is None:
+            p = self.peek()
+            raise SyntaxError(f"expected {val or kind} but found {p.val!r}")
+        return t
+
+    def kw(self, *words) -> bool:
+        for k, w in enumerate(words):
+            t = self.peek(k)
+            if not (t.kind == "kw" and t.val == w):
+                return False
+        self.i += len(words)
+        return True
+
+    def ident(self) -> str:
+        t = self.next()
+        if t.kind not in ("id", "kw"):
+            raise SyntaxError(f"expected identifier, found {t.val!r}")
+        return t.val
+
+    def qualified(self) -> str:
+        name = self.ident()
+        while self.accept("op", "."):
+            name += "." + self.ident()
+        return name
+
+    # -- statements --------------------------------------------------------------
+    def statement(self):
+        if self.kw("show", "databases"):
+            return ("show_databases",)
+        if self.kw("show", "tables"):
+            db = None
+            if self.kw("in") or self.kw("from"):
+                db = self.ident()
+            return ("show_tables", db)
+        if self.kw("use"):
+            return ("use", self.ident())
+        if self.kw("create", "database"):
+            ine = self.kw("if", "not", "exists")
+            return ("create_database", self.ident(), ine)
+        if self.kw("drop", "table"):
+            ie = self.kw("if", "exists")
+            return ("drop_table", self.qualified(), ie)
+        if self.kw("drop", "database"):
+            ie = self.kw("if", "exists")
+            return ("drop_database", self.ident(), ie)
+        if self.kw("describe") or self.kw("desc"):
+            self.kw("table")
+            return ("describe", self.qualified())
+        if self.kw("create", "table"):
+            name = self.qualified()
+            self.expect("kw", "as")
+            return ("ctas", name, self.select())
+        sel = self.select()
+        self.accept("op", ";")
+        if self.peek().kind != "eof":
+            raise SyntaxError(f"unexpected trailing input: {self.peek().val!r}")
+        return ("select", sel)
+
+    def select(self) -> Select:
+        self.expect("kw", "select")
+        distinct = bool(self.kw("distinct"))
+        items = [self.select_item()]
+        while self.accept("op", ","):
+            items.append(self.select_item())
+        s = Select(items, distinct=distinct)
+        if self.kw("from"):
+            if self.accept("op", "("):
+                s.subquery = self.select()
+                self.expect("op", ")")
+            else:
+                s.table = self.qualified()
+            s.alias = self._alias()
+            while True:
+                how = None
+                if self.kw("join") or self.kw("inner", "join"):
+                    how = "inner"
+                elif self.kw("left", "outer", "join") or self.kw("left", "join"):
+                    how = "left"
+                elif self.kw("right", "outer", "join") or self.kw("right", "join"):
+                    how = "right"
+                elif self.kw("full", "outer", "join") or self.kw("full", "join"):
+                    how = "outer"
+                elif self.kw("cross", "join"):
+                    how = "cross"
+                if how is None:
+                    break
+                t = self.qualified()
+                al = self._alias()
+                on = None
+                if how != "cross":
+                    self.expect("kw", "on")
+                    on = self.expr()
+                s.joins.append(Join(t, al, how, on))
+        if self.kw("where"):
+            s.where = self.expr()
+        if self.kw("group", "by"):
+            s.group_by = [self.expr()]
+            while self.accept("op", ","):
+                s.group_by.append(self.expr())
+        if self.kw("having"):
+            s.having = self.expr(allow_agg=True)
+        if self.kw("order", "by"):
+            s.order_by = [self.order_item()]
+            while self.accept("op", ","):
+                s.order_by.append(self.order_item())
+        if self.kw("limit"):
+            s.limit = int(float(self.expect("num").val))
+        if self.kw("union"):
+            s.union_all = bool(self.kw("all"))
+            s.union = self.select()
+        return s
+
+    def _alias(self):
+        if self.kw("as"):
+            return self.ident()
+        t = self.peek()
+        if t.kind == "id":
+            self.i += 1
+            return t.val
+        return None
+
+    def select_item(self) -> SelectItem:
+        if self.accept("op", "*"):
+            return SelectItem("*")
+        if self.peek().kind == "id" and self.peek(1).val == "." and self.peek(2).val == "*":
+            self.i += 3
+            return SelectItem("*")
+        e = self.expr(allow_agg=True)
+        return SelectItem(e, self._alias())
+
+    def order_item(self):
+        e = self.expr(allow_agg=True)
+        asc = True
+        if self.kw("desc"):
+            asc = False
+        else:
+            self.kw("asc")
+        return (e, asc)
+
+    # -- expressions -------------------------------------------------------------
+    def expr(self, allow_agg=False):
+        self._allow_agg = allow_agg
+        return self.or_expr()
+
+    def or_expr(self):
+        e = self.and_expr()
+        while self.kw("or"):
+            e = _combine(e, self.and_expr(), lambda a, b: a | b)
+        return e
+
+    def and_expr(self):
+        e = self.not_expr()
+        while self.kw("and"):
+            e = _combine(e, self.not_expr(), lambda a, b: a & b)
+        return e
+
+    def not_expr(self):
+        if self.kw("not"):
+            return _unary_map(self.not_expr(), lambda a: ~a)
+        return self.cmp_expr()
+
+    def cmp_expr(self):
+        e = self.add_expr()
+        t = self.peek()
+        if t.kind == "op" and t.val in ("=", "==", "!=", "<>", "<", "<=", ">", ">="):
+            self.i += 1
+            r = self.add_expr()
+            op = {"=": "__eq__", "==": "__eq__", "!=": "__ne__", "<>": "__ne__", "<": "__lt__", "<=": "__le__",
+                  ">": "__gt__", ">=": "__ge__"}[t.val]
+            return _combine(e, r, lambda a, b: getattr(a, op)(b))
+        if self.kw("is"):
+            neg = self.kw("not")
+            self.expect("kw", "null")
+            return _unary_map(e, (lambda a: a.isNotNull()) if neg else (lambda a: a.isNull()))
+        neg = False
+        if self.peek().kind == "kw" and self.peek().val == "not" and self.peek(1).val in ("in", "like", "between"):
+            self.i += 1
+            neg = True
+        if self.kw("in"):
+            self.expect("op", "(")
+            vals = [self.literal_value()]
+            while self.accept("op", ","):
+                vals.append(self.literal_value())
+            self.expect("op", ")")
+            r = _unary_map(e, lambda a: a.isin(vals))
+            return _unary_map(r, lambda a: ~a) if neg else r
+        if self.kw("like"):
+            pat = self.expect("str").val[1:-1].replace("''", "'")
+            r = _unary_map(e, lambda a: a.like(pat))
+            return _unary_map(r, lambda a: ~a) if neg else r
+        if self.kw("between"):
+            lo = self.add_expr()
+            self.expect("kw", "and")
+            hi = self.add_expr()
+            r = _combine(_combine(e, lo, lambda a, b: a >= b), _combine(e, hi, lambda a, b: a <= b),
+                         lambda a, b: a & b)
+            return _unary_map(r, lambda a: ~a) if neg else r
+        return e
+
+    def literal_value(self):
+        t = self.next()
+        if t.kind == "num":
+            return float(t.val) if any(c in t.val for c in ".eE") else int(t.val)
+        if t.kind == "str":
+            return t.val[1:-1].replace("''", "'")
+        if t.kind == "op" and t.val == "-":
+            v = self.literal_value()
+            return -v
+        if t.kind == "kw" and t.val in ("true", "false"):
+            return t.val == "true"
+        raise SyntaxError(f"expected literal, found {t.val!r}")
+
+    def add_expr(self):
+        e = self.mul_expr()
+        while self.peek().kind == "op" and self.peek().val in ("+", "-", "||"):
+            op = self.next().val
+            r = self.mul_expr()
+            e = _combine(e, r, (lambda a, b: a + b) if op in ("+", "||") else (lambda a, b: a - b))
+        return e
+
+    def mul_expr(self):
+        e = self.unary()
+        while self.peek().kind == "op" and self.peek().val in ("*", "/", "%"):
+            op = self.next().val
+            r = self.unary()
+            e = _combine(e, r, {"*": lambda a, b: a * b, "/": lambda a, b: a / b, "%": lambda a, b: a % b}[op])
+        return e
+
+    def unary(self):
+        if self.accept("op", "-"):
+            return _unary_map(self.unary(), lambda a: -a)
+        if self.accept("op", "+"):
+            return self.unary()
+        return self.primary()
+
+    def primary(self):
+        t = self.peek()
+        if t.kind == "num":
+            self.i += 1
+            v = float(t.val) if any(c in t.val for c in ".eE") else int(t.val)
+            return E.lit(v)
+        if t.kind == "str":
+            self.i += 1
+            return E.lit(t.val[1:-1].replace("''", "'"))
+        if t.kind == "kw" and t.val in ("null", "true", "false"):
+            self.i += 1
+            return E.lit(None if t.val == "null" else t.val == "true")
+        if self.accept("op", "("):
+            e = self.or_expr()
+            self.expect("op", ")")
+            return e
+        if self.kw("cast"):
+            self.expect("op", "(")
+            e = self.or_expr()
+            self.expect("kw", "as")
+            ty = self.ident()
+            if self.accept("op", "("):
+                while not self.accept("op", ")"):
+                    self.next()
+            self.expect("op", ")")
+            return _unary_map(e, lambda a: a.cast(ty))
+        if self.kw("case"):
+            cases = []
+            while self.kw("when"):
+                c = self.or_expr()
+                self.expect("kw", "then")
+                v = self.or_expr()
+                cases.append((c, v))
+            default = None
+            if self.kw("else"):
+                default = self.or_expr()
+            self.expect("kw", "end")
+            w = E.when(cases[0][0], cases[0][1])
+            for c, v in cases[1:]:
+                w = w.when(c, v)
+            return w.otherwise(default) if default is not None else w.otherwise(None)
+        if t.kind in ("id", "kw"):
+            name = self.ident()
+            if self.accept("op", "("):
+                return self.func_call(name)
+            while self.peek().val == "." and self.peek(1).kind in ("id", "kw"):
+                self.i += 1
+                name = self.ident()        # qualified column: keep the column part
+            return E.col(name)
+        raise SyntaxError(f"unexpected token {t.val!r}")
+
+    def func_call(self, name):
+        fn = name.lower()
+        if fn in ("count", "sum", "avg", "mean", "min", "max", "stddev", "stddev_samp", "variance", "var_samp"):
+            distinct = bool(self.kw("distinct"))
+            if self.accept("op", "*"):
+                arg = None
+            else:
+                arg = self.or_expr()
+            self.expect("op", ")")
+            canon = {"mean": "avg", "stddev_samp": "stddev", "var_samp": "variance"}.get(fn, fn)
+            text = f"{canon}({'DISTINCT ' if distinct else ''}{'1' if arg is None else arg.name})"
+            if canon == "count" and arg is None:
+                text = "count(1)"
+            return AggCall(canon, arg, distinct, text)
+        args = []
+        if not self.accept("op", ")"):
+            args.append(self.or_expr())
+            while self.accept("op", ","):
+                args.append(self.or_expr())
+            self.expect("op", ")")
+        f = {"sqrt": E.sqrt, "log": E.log, "ln": E.log, "exp": E.exp, "abs": E.abs, "isnan": E.isnan,
+             "coalesce": E.coalesce, "log1p": E.log1p}.get(fn)
+        if f is None:
+            if fn in ("lower", "upper", "length", "trim"):
+                return _string_fn(fn, args[0])
+            if fn in ("round", "floor", "ceil"):
+                return _math_fn(fn, args)
+            raise SyntaxError(f"unknown function {name}")
+        return f(*args)
+
+
+def _is_agg(x):
+    return isinstance(x, AggCall) or isinstance(x, _AggExpr)
+
+
+class _AggExpr:
+    """Expression over aggregate results (e.g. ``sum(x) / count(*)``), resolved after grouping."""
+
+    def __init__(self, aggs: list, build, text: str):
+        self.aggs, self.build, self.text = aggs, build, text
+
+    @property
+    def name(self):
+        return self.text
+
+
+def _as_agg_expr(x):
+    if isinstance(x, _AggExpr):
+        return x
+    if isinstance(x, AggCall):
+        return _AggExpr([x], lambda m: E.col(m[x.text]), x.text)
+    return _AggExpr([], lambda m: x, x.name if hasattr(x, "name") else str(x))
+
+
+def _combine(a, b, f):
+    if _is_agg(a) or _is_agg(b):
+        A, B = _as_agg_expr(a), _as_agg_expr(b)
+        return _AggExpr(A.aggs + B.aggs, lambda m: f(A.build(m), B.build(m)), f"({A.text} ? {B.text})")
+    return f(a, b)
+
+
+def _unary_map(a, f):
+    if _is_agg(a):
+        A = _as_agg_expr(a)
+        return _AggExpr(A.aggs, lambda m: f(A.build(m)), A.text)
+    return f(a)
+
+
+def _string_fn(fn, e):
+    import numpy as np
+    from ..frame import column as C
+
+    def run(df):
+        c = e.eval(df)
+        vals = c.to_pylist()
+        if fn == "length":
+            import torch
+            return C.NumericColumn(torch.tensor([len(v) if v is not None else 0 for v in vals], dtype=torch.int32))
+        op = {"lower": str.lower, "upper": str.upper, "trim": str.strip}[fn]
+        return C.StringColumn(np.array([None if v is None else op(str(v)) for v in vals], dtype=object))
+    return E.Expr(run, f"{fn}({e.name})", e.refs)
+
+
+def _math_fn(fn, args):
+    import torch
+    from ..frame import column as C
+    e = args[0]
+    nd = 0
+    if len(args) > 1:
+        nd = int(args[1]._fn.__closure__ and 0 or 0)
+
+    def run(df):
+        c = e.eval(df)
+        d = c.data.to(torch.float64)
+        if fn == "floor":
+            d = torch.floor(d)
+        elif fn == "ceil":
+            d = torch.ceil(d)
+        else:
+            d = torch.round(d, decimals=nd)
+        return C.NumericColumn(d, c.valid)
+    return E.Expr(run, f"{fn}({e.name})", e.refs)
+
+
+def parse(sql: str):
+    return Parser(sql).statement()
+
+
+def parse_expression(text: str):
+    p = Parser(text)
+    e = p.expr(allow_agg=False)
+    alias = p._alias()
+    if p.peek().kind != "eof":
+        raise SyntaxError(f"unexpected trailing input in expression: {p.peek().val!r}")
+    return e.alias(alias) if alias else e

