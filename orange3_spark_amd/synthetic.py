@@ -188,13 +188,20 @@ class SyntheticData:
         n = hi - lo
         X = torch.empty((n, numFeatures), dtype=dtype, device=dev)
         lab = torch.empty(n, dtype=torch.int32, device=dev)
-        step = 1 << 24
+        step = 1 << 20
+        cols = torch.arange(numFeatures, dtype=torch.int64, device=dev)
         for a in range(0, n, step):
             b = min(n, a + step)
             rows = torch.arange(lo + a, lo + b, dtype=torch.int64, device=dev)
             cid = (G.row_keys(seed, rows) % k).to(torch.int64)
-            g = torch.Generator(device=dev).manual_seed(seed * 1000003 + lo + a)
-            X[a:b] = centers[cid] + spread * torch.randn((b - a, numFeatures), generator=g, device=dev, dtype=dtype)
+            # Box-Muller noise keyed on (row, column): identical for any partitioning
+            key = rows[:, None] * numFeatures + cols[None, :]
+            h1 = G.row_keys(seed ^ 0x3C6EF372, key.reshape(-1))
+            h2 = G._fmix32(h1 ^ 0x1B873593)
+            u1 = ((h1 >> 8).to(torch.float32) + 0.5) * (1.0 / 16777216.0)
+            u2 = (h2 >> 8).to(torch.float32) * (1.0 / 16777216.0)
+            z = torch.sqrt(-2.0 * torch.log(u1)) * torch.cos(6.283185307179586 * u2)
+            X[a:b] = centers[cid] + spread * z.reshape(b - a, numFeatures).to(dtype)
             lab[a:b] = cid.to(torch.int32)
         df = DataFrame(s, OrderedDict(features=C.VectorColumn(X), cluster=C.NumericColumn(lab)), n)
         df.true_centers = centers

@@ -1,0 +1,84 @@
+"""Multi-process (gloo, world_size=2) runs of the distributed code paths; results must
+match the single-process run (row sharding must not change the answer)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _work(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import pandas as pd
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.ml.classification import GBTClassifier, LogisticRegression
+    from orange3_spark_amd.ml.clustering import KMeans
+    from orange3_spark_amd.ml.evaluation import BinaryClassificationEvaluator, MulticlassClassificationEvaluator
+    from orange3_spark_amd.ml.recommendation import ALS
+    conf = SessionConf().set("o3s.device", "cpu").set("spark.master", "spmd" if world > 1 else "local")
+    s = Session(conf)
+    res = {}
+    df = s.synthetic.classification(3001, 12, seed=5)
+    res["count"] = df.count()
+    m = LogisticRegression(maxIter=30, regParam=0.01).fit(df)
+    res["lr_coef"] = m.coefficients.toArray()
+    out = m.transform(df)
+    res["auc"] = BinaryClassificationEvaluator().evaluate(out)
+    res["acc"] = MulticlassClassificationEvaluator(metricName="accuracy").evaluate(out)
+    km = KMeans(k=4, seed=2, maxIter=10).fit(s.synthetic.blobs(2000, 5, k=4, seed=1))
+    res["km_cost"] = km.summary.trainingCost
+    res["sample_n"] = df.sample(False, 0.3, seed=9).count()
+    g = GBTClassifier(maxIter=3, maxDepth=3, seed=1).fit(s.synthetic.trees(2000, 6, seed=2))
+    res["gbt_loss"] = g.trainingLossHistory
+    rng = np.random.default_rng(0)
+    u = rng.integers(0, 50, 600)
+    i = rng.integers(0, 30, 600)
+    r = rng.normal(size=600)
+    rows = np.stack([u, i, r], 1)
+    lo, hi = (600 * rank) // world, (600 * (rank + 1)) // world
+    pdf = pd.DataFrame({"user": u, "item": i, "rating": r})
+    als = ALS(rank=3, maxIter=3, seed=1).fit(s.createDataFrame(pdf))
+    res["als_U"] = als._U.numpy()
+    res["groupby"] = sorted((row.g, row.n) for row in s.createDataFrame(
+        pd.DataFrame({"g": list("abcab" * 20)})).groupBy("g").count().withColumnRenamed("count", "n").collect())
+    if rank == 0:
+        torch.save(res, os.path.join(out_dir, f"w{world}.pt"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+    del rows, lo, hi
+
+
+@pytest.mark.timeout(600)
+def test_world2_matches_world1(tmp_path):
+    _work(0, 1, _free_port(), str(tmp_path))
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_work, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(600)
+        assert p.exitcode == 0
+    a = torch.load(tmp_path / "w1.pt", weights_only=False)
+    b = torch.load(tmp_path / "w2.pt", weights_only=False)
+    assert a["count"] == b["count"] == 3001
+    assert np.allclose(a["lr_coef"], b["lr_coef"], atol=1e-6)
+    assert abs(a["auc"] - b["auc"]) < 1e-9 and abs(a["acc"] - b["acc"]) < 1e-9
+    assert a["km_cost"] == pytest.approx(b["km_cost"], rel=1e-9)
+    assert a["sample_n"] == b["sample_n"]
+    assert np.allclose(a["gbt_loss"], b["gbt_loss"], rtol=1e-6)
+    assert np.allclose(a["als_U"], b["als_U"], atol=1e-4)
+    assert a["groupby"] == b["groupby"]
