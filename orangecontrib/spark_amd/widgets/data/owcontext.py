@@ -1,0 +1,51 @@
+"""Context widget: create the shared Session (reference: widgets/data/spark_context.py:13-78)."""
+from collections import OrderedDict
+
+from orange3_spark_amd.conf import DEFAULTS, SessionConf
+
+from ...utils.gui_param import GuiParam
+from ..base import SharedSession
+from ..compat import Setting, Widget
+
+
+class OWSessionContext(SharedSession, Widget):
+    priority = 0
+    name = "Context"
+    description = "Create the shared MI355X session (replaces the Spark/Hive contexts)"
+    icon = "../icons/context.svg"
+    inputs, outputs = [], []
+    saved_gui_params = Setting(OrderedDict())
+
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self.conf = SessionConf()
+        params = OrderedDict(DEFAULTS)
+        for k, v in self.saved_gui_params.items():
+            params[k] = v
+        self.gui_parameters = OrderedDict((k, GuiParam(label=k, default_value=str(v))) for k, v in params.items())
+
+    def set_param(self, key, value):
+        if key not in self.gui_parameters:
+            self.gui_parameters[key] = GuiParam(label=key, default_value=str(value))
+        else:
+            self.gui_parameters[key].set_value(value)
+        return self
+
+    def create_context(self):
+        from orange3_spark_amd import Session
+        if self.session is not None:
+            self.session.stop()
+        conf = SessionConf(loadDefaults=False)
+        for key, p in self.gui_parameters.items():
+            conf.set(key, p.get_value())
+            self.saved_gui_params[key] = p.get_value()
+        self.session = Session.getOrCreate(conf) if Session.active() is None else Session(conf)
+        Session._active = self.session
+        self.info(repr(self.session))
+        self.hide()
+        return self.session
+
+    def onDeleteWidget(self):
+        if self.session is not None:
+            self.session.stop()
+            self.session = None

@@ -1,0 +1,34 @@
+"""Orange to Pandas conversion widget (reference widgets/data/: spark_from_orange.py, spark_from_pandas.py,
+spark_to_orange.py, spark_to_pandas.py, pandas_to_orange.py, orange_to_pandas.py; the
+duplicate class/display names of the reference are made unique, quirk Q13)."""
+import pandas as pd
+
+from orange3_spark_amd.frame.dataframe import DataFrame
+from orange3_spark_amd.utils.data_utils import orange_to_pandas, pandas_to_orange
+
+from ..base import SharedSession
+from ..compat import Widget
+
+
+class OWOrangeToPandas(SharedSession, Widget):
+    priority = 12
+    name = "Orange to Pandas"
+    description = "Convert Table -> Pandas"
+    icon = "../icons/convert.svg"
+    inputs = [("Table", object, "get_input")]
+    outputs = [("Pandas", pd.DataFrame)]
+
+    def get_input(self, obj):
+        if obj is None:
+            self.send("Pandas", None)
+            return None
+        session = self.session
+        if session is None and "session" in "orange_to_pandas(obj)":
+            from orange3_spark_amd import Session
+            session = Session.getOrCreate()
+        out = orange_to_pandas(obj)
+        self.send("Pandas", out)
+        return out
+
+
+_ = (pd, DataFrame, orange_to_pandas, pandas_to_orange)

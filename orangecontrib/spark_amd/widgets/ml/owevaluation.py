@@ -1,0 +1,47 @@
+"""Evaluation: compute EVERY metric an evaluator supports and show a Metric|Value table
+(reference widgets/ml/spark_ml_evaluation.py:13-78: metric names parsed from the
+metricName doc ``(a|b|c)`` at :43; its apply called undefined methods and showed random
+numbers without input -- quirk Q3 -- here it evaluates for real and shows nothing
+without input)."""
+from orange3_spark_amd.ml import evaluation
+
+from ...utils.ml_api_utils import get_evaluators
+from ..base import OWTransformerBase
+
+
+class OWEvaluation(OWTransformerBase):
+    priority = 9
+    name = "Evaluation"
+    description = "Evaluate predictions with every metric of the chosen evaluator"
+    icon = "../icons/evaluate.svg"
+    outputs = []
+    module = evaluation
+    get_modules = staticmethod(get_evaluators)
+
+    def __init__(self, **kw):
+        self.values = {}
+        super().__init__(**kw)
+
+    def metric_names(self):
+        doc = self.gui_parameters["metricName"].doc_text
+        return doc.split("(")[-1].replace(")", "").split("|")
+
+    def apply(self):
+        self.values = {}
+        if self.in_df is None:
+            self.info("no input DataFrame")
+            return self.values
+        self.error()
+        ev = self.method()
+        pm = self.build_param_map(ev)
+        for metric in self.metric_names():
+            try:
+                self.values[metric] = ev.evaluate(self.in_df, {**{k: v for k, v in pm.items()},
+                                                               ev.getParam("metricName"): metric})
+            except Exception as e:  # noqa: BLE001  (e.g. logLoss without a probability column)
+                self.values[metric] = f"n/a ({type(e).__name__})"
+        self.update_saved_gui_parameters()
+        return self.values
+
+    def table(self):
+        return [("Metric", "Value")] + [(k, v) for k, v in self.values.items()]
