@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from ..frame import column as C
+from ..ops import _native as N
 from ..ops import glm as G
 from ..synthetic import LineageVectorColumn
 from . import optim
@@ -99,21 +100,27 @@ class GlmData:
         return mean[:self.d], var[:self.d], W, ymean, yvar
 
     # ---------------------------------------------------------------- one pass
-    def pass_device(self, coef_eff: torch.Tensor, intercept: float, loss: int) -> torch.Tensor:
-        """Local pass; returns device fp64 [grad (dpad) | sum r | loss | wsum] (not reduced)."""
+    def pass_device(self, coef_eff: torch.Tensor, intercept: float | None, loss: int) -> torch.Tensor:
+        """Local pass; returns device fp64 [grad (dpad) | sum r | loss | wsum] (not reduced).
+
+        Resident and lineage rows accumulate into the workspace's result buffer (valid
+        until the next pass).  ``intercept=None``: ``coef_eff`` is the fp32 [dpad + 1]
+        device operand (coefficients + intercept).
+        """
         ws = self.ws
-        out = None
+        filled = False
         if self.X.shape[0]:
-            out = G.glm_grad(self.X, self.y, self.sw, coef_eff, intercept, loss, ws).clone()
+            G.glm_grad(self.X, self.y, self.sw, coef_eff, intercept, loss, ws)
+            filled = True
         if self.lineage:
             spec, r0, nl = self.lineage
-            o2 = G.glm_grad_synth(nl, self.ld, spec.d, spec.seed, r0, spec.wtrue, spec.btrue, coef_eff,
-                                  intercept, loss, ws)
-            out = o2.clone() if out is None else out + o2
-        if out is None:
-            out = torch.zeros(ws.dpad + 3, dtype=torch.float64, device=self.device)
+            G.glm_grad_synth(nl, self.ld, spec.d, spec.seed, r0, spec.wtrue, spec.btrue, coef_eff,
+                             intercept, loss, ws, accumulate=filled)
+            filled = True
+        if not filled:
+            ws.out.zero_()
         self.passes += 1
-        return out
+        return ws.out
 
     def pass_torch(self, coef_eff: torch.Tensor, intercept: float, loss: int) -> torch.Tensor:
         dpad = self.ld
@@ -263,41 +270,49 @@ class DeviceSGD:
         self.l2v = (float(reg) * self.inv_std ** 2) if not standardization else None
         self.bt = torch.zeros(dpad, dtype=torch.float64, device=dev)      # standardised coefficients
         self.b = torch.zeros(1, dtype=torch.float64, device=dev)
-        self.coef_eff = torch.zeros(dpad, dtype=torch.float32, device=dev)
+        # kernel operand: effective fp32 coefficients followed by the intercept
+        self.coef_eff = torch.zeros(dpad + 1, dtype=torch.float32, device=dev)
         self.fi = fit_intercept
         self.step_size = float(step_size)
         self.t = 0
-        self.losses: list[torch.Tensor] = []
+        self.loss_hist = torch.zeros(1024, dtype=torch.float64, device=dev)
         self.W = float(data.comm.sum_scalar(float(data.n_local if data.sw is None else float(data.sw.sum()))))
 
     def step(self):
+        """One step, entirely stream-ordered on the device: pass -> all-reduce -> update."""
         self.t += 1
         d = self.data
         out = self._pass()
         d.comm.all_reduce(out)
-        W = out[self.dpad + 2]
         eta = self.step_size / math.sqrt(self.t)
+        if self.t > self.loss_hist.shape[0]:
+            self.loss_hist = torch.cat([self.loss_hist, torch.zeros_like(self.loss_hist)])
+        slot = self.loss_hist[self.t - 1:self.t]
+        if d.kernel:
+            lib = N.kernels()
+            N.check(lib.o3s_glm_sgd_update(out.data_ptr(), self.dpad, self.bt.data_ptr(), self.b.data_ptr(),
+                                           self.inv_std.data_ptr(), N.ptr(self.l2v), self.l2, eta, int(self.fi),
+                                           self.coef_eff.data_ptr(), slot.data_ptr(),
+                                           torch.cuda.current_stream(d.device).cuda_stream), "glm_sgd_update")
+            return
+        W = out[self.dpad + 2]
         g = out[: self.dpad] * self.inv_std / W
-        if self.l2v is not None:
-            g = g + self.l2v * self.bt
-        elif self.l2:
-            g = g + self.l2 * self.bt
+        g = g + (self.l2v if self.l2v is not None else self.l2) * self.bt
         self.bt -= eta * g
         if self.fi:
             self.b -= eta * out[self.dpad] / W
-        self.coef_eff.copy_((self.bt * self.inv_std).to(torch.float32))
-        self.losses.append(out[self.dpad + 1] / W)
+        self.coef_eff[: self.dpad].copy_((self.bt * self.inv_std).to(torch.float32))
+        self.coef_eff[self.dpad:].copy_(self.b.to(torch.float32))
+        slot.copy_(out[self.dpad + 1:self.dpad + 2] / W)
 
     def _pass(self):
-        # intercept is read on the host only once per step via a device scalar -> pass as float
-        b = float(self.b.item()) if self.fi else 0.0
         if self.data.kernel:
-            return self.data.pass_device(self.coef_eff, b, self.loss)
-        return self.data.pass_torch(self.coef_eff, b, self.loss)
+            return self.data.pass_device(self.coef_eff, None, self.loss)
+        return self.data.pass_torch(self.coef_eff[: self.dpad], float(self.b.item()), self.loss)
 
     def result(self) -> GlmResult:
         coef = (self.bt * self.inv_std)[: self.data.d].cpu().numpy()
-        hist = [float(x) for x in torch.stack(self.losses).cpu()] if self.losses else []
+        hist = [float(x) for x in self.loss_hist[: self.t].cpu()]
         return GlmResult(coef, float(self.b.item()), hist, self.t, False, 0.0, self.data.passes)
 
 

@@ -21,14 +21,15 @@ _LOCK = threading.Lock()
 _LIB = None
 _HOST = None
 
-c_i64, c_i32, c_u32, c_f32 = C.c_int64, C.c_int, C.c_uint32, C.c_float
+c_i64, c_i32, c_u32, c_f32, c_f64 = C.c_int64, C.c_int, C.c_uint32, C.c_float, C.c_double
 c_vp = C.c_void_p
 
 # name -> argtypes (every kernel entry point returns int: 0 = ok, <0 arg error, >0 hipError)
 _SIGS: dict[str, list] = {
     "o3s_glm_layout": [c_i64, C.POINTER(c_i32), C.POINTER(c_i32)],
-    "o3s_glm_grad": [c_i32, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_f32, c_u32, c_i64,
-                     c_vp, c_f32, c_vp, c_i32, c_vp, c_vp],
+    "o3s_glm_grad": [c_i32, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_u32, c_i64,
+                     c_vp, c_f32, c_vp, c_i32, c_vp, c_i32, c_vp],
+    "o3s_glm_sgd_update": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_f64, c_f64, c_i32, c_vp, c_vp, c_vp],
     "o3s_synth_glm": [c_vp, c_i64, c_i64, c_vp, c_u32, c_i64, c_vp, c_f32, c_i32, c_vp],
     "o3s_glm_margin": [c_vp, c_i64, c_i64, c_vp, c_f32, c_vp, c_i32, c_vp],
     "o3s_glm_colstats": [c_i32, c_vp, c_i64, c_i64, c_vp, c_u32, c_i64, c_vp, c_i32, c_vp, c_vp],

@@ -59,11 +59,6 @@ __host__ __device__ __forceinline__ uint32_t row_key(uint32_t seed, int64_t row)
   uint32_t hi = (uint32_t)((uint64_t)row >> 32);
   return fmix32(seed ^ fmix32(lo * 0x9E3779B1u + hi * 0x7FEB352Du + 0x165667B1u));
 }
-// Signed 16-bit lane of a hash -> uniform in [-1, 1) (exact in f32).
-__host__ __device__ __forceinline__ float u16_to_unit(uint32_t bits16) {
-  return (float)(int16_t)(uint16_t)bits16 * (1.0f / 32768.0f);
-}
-
 // --- wave / block reductions -------------------------------------------------
 template <int WIDTH>
 __device__ __forceinline__ float group_sum(float v) {

@@ -35,15 +35,28 @@ enum { LOSS_LOGISTIC = 0, LOSS_HINGE = 1, LOSS_SQUARED = 2 };
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
-// One 16-B chunk (8 features) of synthetic row `rk` (row key) at chunk index ch.
-// Values are k/32768 (k int16) rounded to bf16.
+// Synthetic features: hash word i = fmix32(rk + i * golden) of row key rk supplies the
+// four features 4i..4i+3, one per byte b: x = (2b - 255) / 256, i.e. 256 symmetric
+// levels in (-1, 1) (mean 0, var ~1/3), every one EXACT in bf16 (<= 8 significant
+// bits).  Exactness lets the lineage pass skip the bf16 round trip: it decodes a byte
+// with one v_cvt_f32_ubyteN and folds the affine map into the weights (see
+// glm_grad_kernel), two hashes per 16-B chunk instead of four.
+__device__ __forceinline__ uint32_t synth_word(uint32_t rk, int i) {
+  return fmix32(rk + (uint32_t)i * 0x9E3779B9u);
+}
+__device__ __forceinline__ float synth_byte(uint32_t h, int q) {
+  return (float)((h >> (8 * q)) & 0xffu);     // -> v_cvt_f32_ubyte{q}
+}
+constexpr float kSynthScale = 1.0f / 128.0f, kSynthShift = -255.0f / 256.0f;
+// One 16-B chunk (8 features) of synthetic row `rk` at chunk index ch, as bf16.
 __device__ __forceinline__ short8 synth_chunk(uint32_t rk, int ch) {
   short8 v;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const uint32_t h = fmix32(rk + (uint32_t)(ch * 4 + p) * 0x9E3779B9u);
-    v[2 * p] = (short)f32_to_bf16(u16_to_unit(h & 0xffffu));
-    v[2 * p + 1] = (short)f32_to_bf16(u16_to_unit(h >> 16));
+  for (int p = 0; p < 2; ++p) {
+    const uint32_t h = synth_word(rk, 2 * ch + p);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[4 * p + q] = (short)f32_to_bf16(fmaf(synth_byte(h, q), kSynthScale, kSynthShift));
   }
   return v;
 }
@@ -111,7 +124,7 @@ struct RowReduce {
 template <int LPR, int CPL, int UNROLL, int LOSS, int SRC>
 __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
     const uint16_t* __restrict__ X, int64_t ld, int64_t n, const float* __restrict__ y,
-    const float* __restrict__ sw, const float* __restrict__ coef, float intercept,
+    const float* __restrict__ sw, const float* __restrict__ coef, const float* __restrict__ bptr,
     uint32_t seed, int64_t row0, const float* __restrict__ wtrue, float btrue,
     float* __restrict__ partial, int pstride) {
   constexpr int G = kWave / LPR;             // rows per wave-instruction
@@ -125,17 +138,30 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
   const int nch = (int)(ld / 8);
   const int ubase = RR::base(c);
   const bool rep = RR::representative(c);
+  // read from device memory so a device-side optimizer step never syncs the host
+  const float intercept = *bptr;
 
+  // SRC == 1 works on raw bytes b (x = b*kSynthScale + kSynthShift): the weights are
+  // pre-scaled by kSynthScale and each lane's dot products start from the shift term
+  // kSynthShift * sum(w over its columns); X^T r accumulates r*b/128 plus a per-lane
+  // residual sum rs, corrected once at the end.
   float w[CPL][8], wt[CPL][8], acc[CPL][8];
+  float wshift = 0.f, wtshift = 0.f, rs = 0.f;
 #pragma unroll
   for (int k = 0; k < CPL; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int col = 8 * (c + k * LPR) + j;
-      w[k][j] = col < ld ? coef[col] : 0.f;
-      wt[k][j] = (SRC == 1 && col < ld) ? wtrue[col] : 0.f;
+      const float wv = col < ld ? coef[col] : 0.f;
+      const float wtv = (SRC == 1 && col < ld) ? wtrue[col] : 0.f;
+      w[k][j] = SRC == 1 ? wv * kSynthScale : wv;
+      wt[k][j] = wtv * kSynthScale;
+      wshift += wv;
+      wtshift += wtv;
       acc[k][j] = 0.f;
     }
+  wshift *= kSynthShift;
+  wtshift *= kSynthShift;
   float acc_r = 0.f, acc_loss = 0.f, acc_w = 0.f;
 
   const int64_t ntiles = (n + RT - 1) / RT;
@@ -146,23 +172,27 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
     // Loads are issued unconditionally from clamped addresses and masked in
     // registers afterwards: a per-load `ok ? load : 0` makes hipcc branch around
     // every load and serialise them (CDNA guide §5, "three .s-level traps" (c)).
+    // SRC == 1: rows past n are harmless (their residual is masked to 0) and columns
+    // past ld meet zero weights and are never written out, so no masking is needed.
     short8 xv[UNROLL][CPL];
+    uint32_t hv[UNROLL][CPL][2];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const int64_t row = base + u * G + g;
       const bool ok = row < n;
       const int64_t rowc = ok ? row : n - 1;
+      const uint32_t rk = SRC == 1 ? row_key(seed, row0 + row) : 0u;
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int ch = c + k * LPR;
-        const bool okc = ok && ch < nch;
         if (SRC == 0) {
+          const bool okc = ok && ch < nch;
           const int chc = ch < nch ? ch : nch - 1;
           short8 v = __builtin_nontemporal_load(reinterpret_cast<const short8*>(X + rowc * ld + 8 * chc));
           xv[u][k] = okc ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
         } else {
-          short8 v = synth_chunk(row_key(seed, row0 + rowc), ch);
-          xv[u][k] = okc ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
+          hv[u][k][0] = synth_word(rk, 2 * ch);
+          hv[u][k][1] = synth_word(rk, 2 * ch + 1);
         }
       }
     }
@@ -185,11 +215,16 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
     float dot[UNROLL], dtrue[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      float d = 0.f, dt = 0.f;
+      float d = SRC == 1 ? wshift : 0.f, dt = wtshift;
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         float x[8];
-        unpack8(xv[u][k], x);
+        if (SRC == 0) {
+          unpack8(xv[u][k], x);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = synth_byte(hv[u][k][j >> 2], j & 3);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           d = fmaf(x[j], w[k][j], d);
@@ -215,7 +250,7 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
       float r, l;
       if (LOSS == LOSS_LOGISTIC) {
         const float e = __expf(-fabsf(m));
-        const float inv = 1.0f / (1.0f + e);
+        const float inv = __builtin_amdgcn_rcpf(1.0f + e);
         const float p = m >= 0.f ? inv : e * inv;   // sigmoid(m)
         r = (p - yy[j]) * ww[j];
         l = ww[j] * (fmaxf(m, 0.f) + __logf(1.0f + e) - yy[j] * m);
@@ -237,21 +272,36 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u)
 #pragma unroll
-      for (int k = 0; k < CPL; ++k) asm volatile("" : "+v"(xv[u][k]));
+      for (int k = 0; k < CPL; ++k) {
+        if (SRC == 0) asm volatile("" : "+v"(xv[u][k]));
+        else asm volatile("" : "+v"(hv[u][k][0]), "+v"(hv[u][k][1]));
+      }
     // broadcast each row's residual back to its LPR lanes, accumulate X^T r
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
-      const float r = __shfl(res[u % NF], g * LPR + RR::owner(u), kWave);
+      float r = __shfl(res[u % NF], g * LPR + RR::owner(u), kWave);
+      if (SRC == 1) { rs += r; r *= kSynthScale; }
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         float x[8];
-        unpack8(xv[u][k], x);
+        if (SRC == 0) {
+          unpack8(xv[u][k], x);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) x[j] = synth_byte(hv[u][k][j >> 2], j & 3);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(r, x[j], acc[k][j]);
       }
     }
   }
 
+  if (SRC == 1) {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(rs, kSynthShift, acc[k][j]);
+  }
   // Sum the G row groups of the wave (lanes c, c+LPR, ...), then the 4 waves via LDS.
 #pragma unroll
   for (int k = 0; k < CPL; ++k)
@@ -470,7 +520,8 @@ __global__ __launch_bounds__(kBlock) void glm_colstats_kernel(
 // columns x 32 strided partial-row groups; each thread sums nblocks/32 rows, then the
 // 32 group sums of a column are combined in LDS in a fixed order.
 __global__ __launch_bounds__(1024) void glm_finish_kernel(const float* __restrict__ partial, int nblocks,
-                                                          int pstride, int ncols, double* __restrict__ out) {
+                                                          int pstride, int ncols, double* __restrict__ out,
+                                                          int accumulate) {
   __shared__ double red[32][33];
   const int cx = threadIdx.x & 31, gy = threadIdx.x >> 5;
   const int i = blockIdx.x * 32 + cx;
@@ -483,7 +534,33 @@ __global__ __launch_bounds__(1024) void glm_finish_kernel(const float* __restric
     double t = 0.0;
 #pragma unroll 8
     for (int q = 0; q < 32; ++q) t += red[q][cx];
-    out[i] = t;
+    out[i] = accumulate ? out[i] + t : t;
+  }
+}
+
+// One device-side gradient-descent step on the all-reduced pass result `out`
+// (DeviceSGD): standardised coefficients bt <- bt - eta*(g/W + l2*bt), intercept
+// b <- b - eta * sum(r)/W, then refresh the fp32 kernel operand coef_eff (dpad
+// coefficients + intercept) and record the loss -- no host round trip per step.
+__global__ __launch_bounds__(256) void glm_sgd_update_kernel(
+    const double* __restrict__ out, int dpad, double* __restrict__ bt, double* __restrict__ b,
+    const double* __restrict__ inv_std, const double* __restrict__ l2v, double l2, double eta,
+    int fit_intercept, float* __restrict__ coef_eff, double* __restrict__ loss_slot) {
+  const double W = out[dpad + 2];
+  const double invW = W > 0.0 ? 1.0 / W : 0.0;
+  for (int i = threadIdx.x; i < dpad; i += blockDim.x) {
+    const double inv = inv_std[i];
+    const double reg = l2v ? l2v[i] : l2;
+    const double v = bt[i] - eta * (out[i] * inv * invW + reg * bt[i]);
+    bt[i] = v;
+    coef_eff[i] = (float)(v * inv);
+  }
+  if (threadIdx.x == 0) {
+    double bv = b[0];
+    if (fit_intercept) bv -= eta * out[dpad] * invW;
+    b[0] = bv;
+    coef_eff[dpad] = (float)bv;
+    if (loss_slot) loss_slot[0] = out[dpad + 1] * invW;
   }
 }
 
@@ -502,7 +579,7 @@ int pick_cpl(int nch) {
 
 template <int LPR, int CPL, int LOSS, int SRC>
 void launch_grad(int grid, hipStream_t st, const uint16_t* X, int64_t ld, int64_t n,
-                 const float* y, const float* sw, const float* coef, float b, uint32_t seed,
+                 const float* y, const float* sw, const float* coef, const float* b, uint32_t seed,
                  int64_t row0, const float* wt, float bt, float* partial, int pstride) {
   // rows in flight per lane: 8 loads for the streaming pass; the lineage pass keeps
   // fewer chunks live (its hash work, not memory latency, is the limiter)
@@ -513,7 +590,7 @@ void launch_grad(int grid, hipStream_t st, const uint16_t* X, int64_t ld, int64_
 
 template <int LOSS, int SRC>
 int dispatch_grad(int lpr, int cpl, int grid, hipStream_t st, const uint16_t* X, int64_t ld,
-                  int64_t n, const float* y, const float* sw, const float* coef, float b,
+                  int64_t n, const float* y, const float* sw, const float* coef, const float* b,
                   uint32_t seed, int64_t row0, const float* wt, float bt, float* partial,
                   int pstride) {
 #define O3S_G(L, C)                                                                         \
@@ -522,8 +599,13 @@ int dispatch_grad(int lpr, int cpl, int grid, hipStream_t st, const uint16_t* X,
                                  partial, pstride);                                         \
     return 0;                                                                               \
   }
-  O3S_G(4, 1) O3S_G(8, 1) O3S_G(16, 1) O3S_G(32, 1) O3S_G(64, 1)
-  O3S_G(64, 2) O3S_G(64, 4) O3S_G(64, 8) O3S_G(64, 16)
+  if constexpr (SRC == 0) {
+    O3S_G(4, 1) O3S_G(8, 1) O3S_G(16, 1) O3S_G(32, 1) O3S_G(64, 1)
+    O3S_G(64, 2) O3S_G(64, 4) O3S_G(64, 8) O3S_G(64, 16)
+  } else {
+    O3S_G(4, 1) O3S_G(8, 1) O3S_G(4, 4) O3S_G(8, 4) O3S_G(16, 4) O3S_G(32, 4)
+    O3S_G(64, 4) O3S_G(64, 8) O3S_G(64, 16)
+  }
 #undef O3S_G
   return -1;
 }
@@ -540,42 +622,51 @@ O3S_API int o3s_glm_layout(int64_t ld, int* dpad, int* pstride) {
   return 0;
 }
 
-// Gradient/loss pass.  out (fp64, dpad+3): [grad (dpad) | sum r | loss | weight sum].
-// partial must hold grid * pstride floats.  src: 0 = X in memory, 1 = synthetic lineage.
+// Gradient/loss pass.  out (fp64, dpad+3): [grad (dpad) | sum r | loss | weight sum],
+// overwritten (accumulate == 0) or added to.  coef holds dpad+1 floats: the padded
+// coefficients followed by the intercept.  partial must hold grid * pstride floats.
+// src: 0 = X in memory, 1 = synthetic lineage.
 O3S_API int o3s_glm_grad(int loss, int src, const void* X, int64_t ld, int64_t n, const float* y,
-                         const float* sw, const float* coef, float intercept, uint32_t seed,
+                         const float* sw, const float* coef, uint32_t seed,
                          int64_t row0, const float* wtrue, float btrue, float* partial,
-                         int grid, double* out, hipStream_t st) {
+                         int grid, double* out, int accumulate, hipStream_t st) {
   const int nch = (int)(ld / 8);
   const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
   if (ld % 8 != 0 || cpl > 16 || grid <= 0) return -1;
   const int dpad = lpr * cpl * 8, pstride = dpad + 4;
   const uint16_t* Xh = (const uint16_t*)X;
   int rc = -1;
+  // The lineage pass is VALU bound and its per-row work (row key, cross-lane dot
+  // reduction, label draw, residual broadcast) is replicated on every lane of a row,
+  // so it uses 4x fewer lanes per row with 4x more columns each (same padded width).
+  int lpr_s = lpr, cpl_s = cpl;
+  if (cpl == 1 && lpr >= 16) { lpr_s = lpr / 4; cpl_s = 4; }
+  else if (cpl == 2) { lpr_s = 32; cpl_s = 4; }
   if (n > 0) {
     if (src == 0) {
       if (loss == LOSS_LOGISTIC)
-        rc = dispatch_grad<LOSS_LOGISTIC, 0>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+        rc = dispatch_grad<LOSS_LOGISTIC, 0>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, coef + dpad, seed, row0, wtrue, btrue, partial, pstride);
       else if (loss == LOSS_HINGE)
-        rc = dispatch_grad<LOSS_HINGE, 0>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+        rc = dispatch_grad<LOSS_HINGE, 0>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, coef + dpad, seed, row0, wtrue, btrue, partial, pstride);
       else
-        rc = dispatch_grad<LOSS_SQUARED, 0>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+        rc = dispatch_grad<LOSS_SQUARED, 0>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, coef + dpad, seed, row0, wtrue, btrue, partial, pstride);
     } else {
       if (loss == LOSS_LOGISTIC)
-        rc = dispatch_grad<LOSS_LOGISTIC, 1>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+        rc = dispatch_grad<LOSS_LOGISTIC, 1>(lpr_s, cpl_s, grid, st, Xh, ld, n, y, sw, coef, coef + dpad, seed, row0, wtrue, btrue, partial, pstride);
       else if (loss == LOSS_HINGE)
-        rc = dispatch_grad<LOSS_HINGE, 1>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+        rc = dispatch_grad<LOSS_HINGE, 1>(lpr_s, cpl_s, grid, st, Xh, ld, n, y, sw, coef, coef + dpad, seed, row0, wtrue, btrue, partial, pstride);
       else
-        rc = dispatch_grad<LOSS_SQUARED, 1>(lpr, cpl, grid, st, Xh, ld, n, y, sw, coef, intercept, seed, row0, wtrue, btrue, partial, pstride);
+        rc = dispatch_grad<LOSS_SQUARED, 1>(lpr_s, cpl_s, grid, st, Xh, ld, n, y, sw, coef, coef + dpad, seed, row0, wtrue, btrue, partial, pstride);
     }
     if (rc != 0) return rc;
   } else {
+    if (accumulate) return 0;
     hipMemsetAsync(partial, 0, sizeof(float) * pstride * (size_t)grid, st);
   }
   O3S_CHECK_LAUNCH();
   const int ncols = dpad + 3;
   hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 31) / 32), dim3(1024), 0, st, partial, grid,
-                     pstride, ncols, out);
+                     pstride, ncols, out, accumulate);
   O3S_CHECK_LAUNCH();
   return 0;
 }
@@ -652,7 +743,16 @@ O3S_API int o3s_glm_colstats(int src, const void* X, int64_t ld, int64_t n, cons
   O3S_CHECK_LAUNCH();
   const int ncols = 2 * dpad + 1;
   hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 31) / 32), dim3(1024), 0, st, partial, grid,
-                     pstride, ncols, out);
+                     pstride, ncols, out, 0);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+O3S_API int o3s_glm_sgd_update(const double* out, int dpad, double* bt, double* b, const double* inv_std,
+                               const double* l2v, double l2, double eta, int fit_intercept, float* coef_eff,
+                               double* loss_slot, hipStream_t st) {
+  hipLaunchKernelGGL(glm_sgd_update_kernel, dim3(1), dim3(256), 0, st, out, dpad, bt, b, inv_std, l2v, l2,
+                     eta, fit_intercept, coef_eff, loss_slot);
   O3S_CHECK_LAUNCH();
   return 0;
 }

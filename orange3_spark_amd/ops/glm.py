@@ -57,24 +57,21 @@ def row_keys(seed: int, rows: torch.Tensor) -> torch.Tensor:
     return _fmix32((seed & _MASK) ^ _fmix32(inner))
 
 
-def _u16_unit(bits: torch.Tensor) -> torch.Tensor:
-    v = bits & 0xFFFF
-    v = torch.where(v >= 0x8000, v - 0x10000, v)
-    return v.to(torch.float32) * (1.0 / 32768.0)
-
-
 def synth_features_torch(rk: torch.Tensor, ld: int, d: int) -> torch.Tensor:
     """bf16 [n, ld] features for row keys ``rk`` (int64 [n]).
 
-    All ``ld`` columns are generated (synthetic widths are rounded up to a multiple of 8;
-    the ground-truth weights of columns >= d are zero, so those are pure noise features).
+    Word i = fmix32(rk + i*golden) gives features 4i..4i+3 (byte q -> column 4i+q) as
+    (2b - 255)/256: 256 symmetric levels in (-1, 1), exact in bf16 (csrc/glm.hip
+    ``synth_chunk``).  All ``ld`` columns are generated (synthetic widths are rounded up to
+    a multiple of 8; the ground-truth weights of columns >= d are zero, so those are pure
+    noise features).
     """
     n = rk.shape[0]
-    pairs = torch.arange(ld // 2, dtype=torch.int64, device=rk.device)  # (ch*4+p) == col//2
-    h = _fmix32((rk[:, None] + pairs[None, :] * 0x9E3779B9) & _MASK)
-    lo = _u16_unit(h)
-    hi = _u16_unit(h >> 16)
-    return torch.stack([lo, hi], dim=-1).reshape(n, ld).to(torch.bfloat16)
+    words = torch.arange(ld // 4, dtype=torch.int64, device=rk.device)
+    h = _fmix32((rk[:, None] + words[None, :] * 0x9E3779B9) & _MASK)
+    shifts = torch.arange(4, dtype=torch.int64, device=rk.device) * 8
+    b = (h[:, :, None] >> shifts) & 0xFF
+    return ((2 * b - 255).to(torch.float32) * (1.0 / 256.0)).reshape(n, ld).to(torch.bfloat16)
 
 
 def synth_labels_torch(rk: torch.Tensor, margin_true: torch.Tensor) -> torch.Tensor:
@@ -163,24 +160,30 @@ class GlmWorkspace:
 
 
 def glm_grad(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, coef: torch.Tensor,
-             intercept: float, loss: int, ws: GlmWorkspace | None = None) -> torch.Tensor:
+             intercept: float | None, loss: int, ws: GlmWorkspace | None = None,
+             accumulate: bool = False) -> torch.Tensor:
     """Fused margin -> loss -> X^T r pass.  Returns fp64 [grad (dpad) | sum r | loss | wsum].
 
-    ``coef`` is fp32 with at least ``ld`` entries (padded columns ignored).  The returned
-    tensor aliases the workspace buffer when one is given.
+    ``coef`` is fp32 with at least ``ld`` entries (padded columns ignored).  With
+    ``intercept=None`` it must be the device operand itself: dpad coefficients followed
+    by the intercept (what DeviceSGD keeps on the GPU, so no host sync is needed).  The
+    returned tensor aliases the workspace buffer when one is given; ``accumulate`` adds
+    into it instead of overwriting.
     """
     ld = X.shape[1]
     if X.is_cuda:
         if X.dtype != torch.bfloat16 or not X.is_contiguous():
             raise TypeError("GPU GLM pass expects a contiguous bf16 feature matrix")
         ws = ws or GlmWorkspace(X.device, ld)
-        cf = _coef_buf(coef, ws.dpad, X.device)
+        cf = _coef_buf(coef, ws.dpad, X.device, intercept=intercept)
         lib = N.kernels()
         N.check(lib.o3s_glm_grad(loss, 0, X.data_ptr(), ld, X.shape[0], y.data_ptr(),
-                                 N.ptr(sw), cf.data_ptr(), float(intercept), 0, 0, None, 0.0,
-                                 ws.partial.data_ptr(), ws.grid, ws.out.data_ptr(),
+                                 N.ptr(sw), cf.data_ptr(), 0, 0, None, 0.0,
+                                 ws.partial.data_ptr(), ws.grid, ws.out.data_ptr(), int(accumulate),
                                  N.stream_of(X)), "glm_grad")
         return ws.out
+    if intercept is None:
+        intercept = float(coef[-1])
     dpad, _ = layout(ld)
     ref = glm_grad_torch(X, y, sw, coef.to(torch.float64)[:ld], intercept, loss)
     out = torch.zeros(dpad + 3, dtype=torch.float64)
@@ -190,36 +193,49 @@ def glm_grad(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, coef: to
 
 
 def glm_grad_synth(n: int, ld: int, d: int, seed: int, row0: int, wtrue: torch.Tensor,
-                   btrue: float, coef: torch.Tensor, intercept: float, loss: int,
-                   ws: GlmWorkspace) -> torch.Tensor:
+                   btrue: float, coef: torch.Tensor, intercept: float | None, loss: int,
+                   ws: GlmWorkspace, accumulate: bool = False) -> torch.Tensor:
     """Gradient over synthetic rows regenerated in-kernel (lineage recompute)."""
     if ws.device.type == "cuda":
-        cf = _coef_buf(coef, ws.dpad, ws.device)
-        wt = _coef_buf(wtrue, ws.dpad, ws.device, slot=1)
+        cf = _coef_buf(coef, ws.dpad, ws.device, intercept=intercept)
+        wt = _coef_buf(wtrue, ws.dpad, ws.device, slot=1, intercept=0.0)
         lib = N.kernels()
-        N.check(lib.o3s_glm_grad(loss, 1, None, ld, n, None, None, cf.data_ptr(), float(intercept),
+        N.check(lib.o3s_glm_grad(loss, 1, None, ld, n, None, None, cf.data_ptr(),
                                  seed & _MASK, row0, wt.data_ptr(), float(btrue),
-                                 ws.partial.data_ptr(), ws.grid, ws.out.data_ptr(),
+                                 ws.partial.data_ptr(), ws.grid, ws.out.data_ptr(), int(accumulate),
                                  torch.cuda.current_stream(ws.device).cuda_stream), "glm_grad_synth")
         return ws.out
     X, y = synth_glm(n, d, seed, row0, "cpu", ld, wtrue, btrue)
-    return glm_grad(X, y, None, coef, intercept, loss)
+    out = glm_grad(X, y, None, coef, intercept, loss)
+    if accumulate and ws is not None and getattr(ws, "out", None) is not None:
+        ws.out += out
+        return ws.out
+    return out
 
 
 _COEF_CACHE: dict = {}
 
 
-def _coef_buf(coef: torch.Tensor, dpad: int, device, slot: int = 0) -> torch.Tensor:
-    """fp32 coefficient vector zero-padded to dpad on ``device`` (reused buffer)."""
+def _coef_buf(coef: torch.Tensor, dpad: int, device, slot: int = 0,
+              intercept: float | None = 0.0) -> torch.Tensor:
+    """Kernel operand: fp32 [dpad coefficients (zero padded) | intercept] on ``device``.
+
+    ``intercept=None`` means ``coef`` already is such an operand and is used as is.
+    """
+    if intercept is None:
+        if coef.shape[0] != dpad + 1 or coef.dtype != torch.float32 or coef.device != torch.device(device):
+            raise ValueError("coef operand must be fp32 [dpad + 1] on the pass device")
+        return coef
     key = (str(device), dpad, slot)
     buf = _COEF_CACHE.get(key)
     if buf is None:
-        buf = torch.zeros(dpad, dtype=torch.float32, device=device)
+        buf = torch.zeros(dpad + 1, dtype=torch.float32, device=device)
         _COEF_CACHE[key] = buf
     k = min(coef.shape[0], dpad)
     buf[:k].copy_(coef[:k], non_blocking=True)
     if k < dpad:
-        buf[k:].zero_()
+        buf[k:dpad].zero_()
+    buf[dpad] = float(intercept)
     return buf
 
 

@@ -38,6 +38,9 @@ def main():
         bytes_ = a.rows * (X.shape[1] * 2 + 4)
         res[name] = {"ms": dt * 1e3, "rows_per_s": a.rows / dt,
                      "GBps": bytes_ / dt / 1e9 if name == "mem" else None}
+    gm = G.glm_grad(X, y, None, coef, 0.0, 0, ws).clone()
+    gs = G.glm_grad_synth(a.rows, X.shape[1], a.d, 1, 0, *G.synth_truth(1, a.d), coef, 0.0, 0, ws).clone()
+    res["mem_vs_synth_max_rel"] = float(((gm - gs).abs() / gm.abs().clamp_min(1e-3 * a.rows)).max())
     print(json.dumps(res))
 
 
