@@ -208,7 +208,7 @@ class TorchComm(Comm):
 
     def barrier(self):
         if self.world_size > 1:
-            if self.device.type == "cuda":
+            if self.device.type == "cuda" and self.backend == "nccl":
                 dist.barrier(group=self.group, device_ids=[self.device.index])
             else:
                 dist.barrier(group=self.group)
@@ -245,10 +245,12 @@ def init_process_group(device: torch.device, backend: str | None = None, timeout
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     if backend is None:
-        backend = "nccl" if device.type == "cuda" else "gloo"
+        # O3S_DIST_BACKEND=gloo rehearses multi-rank runs with several ranks on one GPU
+        # (RCCL refuses two ranks per device); production GPU runs use RCCL ("nccl").
+        backend = os.environ.get("O3S_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
     kw = dict(backend=backend, rank=rank, world_size=world,
               timeout=datetime.timedelta(seconds=timeout_s))
-    if device.type == "cuda":
+    if device.type == "cuda" and backend == "nccl":
         kw["device_id"] = device
     dist.init_process_group(**kw)
 
