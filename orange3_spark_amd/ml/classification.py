@@ -339,3 +339,7 @@ _ = Vectors
 
 from ._tree import (DecisionTreeClassificationModel, DecisionTreeClassifier, GBTClassificationModel,  # noqa: E402,F401
                     GBTClassifier, RandomForestClassificationModel, RandomForestClassifier)
+from ._fm import FMClassificationModel, FMClassifier  # noqa: E402,F401
+from ._mlp import MultilayerPerceptronClassificationModel, MultilayerPerceptronClassifier  # noqa: E402,F401
+from ._nb import NaiveBayes, NaiveBayesModel  # noqa: E402,F401
+from ._ovr import OneVsRest, OneVsRestModel  # noqa: E402,F401

@@ -166,3 +166,8 @@ class LinearRegressionModel(U.PredictionModelMixin, Model, _LinearRegressionPara
         m = cls._from(vector_from_struct(t["coefficients"]).toArray(), t["intercept"])
         apply_metadata(m, meta)
         return m
+from ._fm import FMRegressionModel, FMRegressor  # noqa: E402,F401
+from ._regression_extra import (AFTSurvivalRegression, AFTSurvivalRegressionModel,  # noqa: E402,F401
+                                GeneralizedLinearRegression, GeneralizedLinearRegressionModel,
+                                GeneralizedLinearRegressionTrainingSummary, IsotonicRegression,
+                                IsotonicRegressionModel)

@@ -82,11 +82,13 @@ def kernels():
 _HOST_SIGS: dict[str, list] = {
     "o3s_host_murmur3": [c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp],
     "o3s_host_tokenize": [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp],
+    "o3s_host_pav": [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp],
 }
+_HOST_RET = {"o3s_host_tokenize": C.c_int64, "o3s_host_pav": C.c_int64}
 
 
 def host():
-    """Host C++ runtime library (text hashing/tokenizing); built with the kernels."""
+    """Host C++ runtime library (text hashing/tokenizing, PAV); built with the kernels."""
     global _HOST
     if _HOST is not None:
         return _HOST
@@ -99,7 +101,7 @@ def host():
             for name, argt in _HOST_SIGS.items():
                 fn = getattr(lib, name)
                 fn.argtypes = argt
-                fn.restype = C.c_int64 if name == "o3s_host_tokenize" else None
+                fn.restype = _HOST_RET.get(name)
             _HOST = lib
     return _HOST
 

@@ -50,6 +50,17 @@ def _work(rank, world, port, out_dir):
     pdf = pd.DataFrame({"user": u, "item": i, "rating": r})
     als = ALS(rank=3, maxIter=3, seed=1).fit(s.createDataFrame(pdf))
     res["als_U"] = als._U.numpy()
+    from orange3_spark_amd.ml.classification import NaiveBayes
+    from orange3_spark_amd.ml.feature import VectorAssembler
+    from orange3_spark_amd.ml.regression import GeneralizedLinearRegression, IsotonicRegression
+    xi = np.round(rng.uniform(0, 10, 400), 1)
+    yi = xi + rng.normal(0, 1, 400)
+    dfi = VectorAssembler(inputCols=["x"], outputCol="features").transform(
+        s.createDataFrame(pd.DataFrame({"x": xi, "label": yi})))
+    iso = IsotonicRegression().fit(dfi)
+    res["iso"] = np.concatenate([iso.boundaries.toArray(), iso.predictions.toArray()])
+    res["nb_theta"] = NaiveBayes(modelType="gaussian").fit(df).theta.toArray()
+    res["glr"] = GeneralizedLinearRegression(family="binomial").fit(df).coefficients.toArray()
     res["groupby"] = sorted((row.g, row.n) for row in s.createDataFrame(
         pd.DataFrame({"g": list("abcab" * 20)})).groupBy("g").count().withColumnRenamed("count", "n").collect())
     if rank == 0:
@@ -82,3 +93,6 @@ def test_world2_matches_world1(tmp_path):
     assert np.allclose(a["gbt_loss"], b["gbt_loss"], rtol=1e-6)
     assert np.allclose(a["als_U"], b["als_U"], atol=1e-4)
     assert a["groupby"] == b["groupby"]
+    assert a["iso"].shape == b["iso"].shape and np.allclose(a["iso"], b["iso"], atol=1e-9)
+    assert np.allclose(a["nb_theta"], b["nb_theta"], atol=1e-9)
+    assert np.allclose(a["glr"], b["glr"], atol=1e-8)
