@@ -128,3 +128,7 @@ class KMeansModel(Model, _KMeansParams, MLWritable, MLReadable):
         m = cls._from(np.array([vector_from_struct(r["clusterCenter"]).toArray() for r in rows]))
         apply_metadata(m, meta)
         return m
+
+
+from ._clustering_extra import (LDA, BisectingKMeans, BisectingKMeansModel, GaussianMixture,  # noqa: E402,F401
+                                GaussianMixtureModel, LDAModel, LocalLDAModel, PowerIterationClustering)

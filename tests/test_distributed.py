@@ -61,6 +61,10 @@ def _work(rank, world, port, out_dir):
     res["iso"] = np.concatenate([iso.boundaries.toArray(), iso.predictions.toArray()])
     res["nb_theta"] = NaiveBayes(modelType="gaussian").fit(df).theta.toArray()
     res["glr"] = GeneralizedLinearRegression(family="binomial").fit(df).coefficients.toArray()
+    from orange3_spark_amd.ml.clustering import BisectingKMeans, GaussianMixture
+    blobs = s.synthetic.blobs(1200, 4, k=3, seed=4)
+    res["bkm_cost"] = BisectingKMeans(k=3, seed=1).fit(blobs).summary.trainingCost
+    res["gmm_ll"] = GaussianMixture(k=3, seed=1, maxIter=20).fit(blobs).summary.logLikelihood
     res["groupby"] = sorted((row.g, row.n) for row in s.createDataFrame(
         pd.DataFrame({"g": list("abcab" * 20)})).groupBy("g").count().withColumnRenamed("count", "n").collect())
     if rank == 0:
@@ -96,3 +100,5 @@ def test_world2_matches_world1(tmp_path):
     assert a["iso"].shape == b["iso"].shape and np.allclose(a["iso"], b["iso"], atol=1e-9)
     assert np.allclose(a["nb_theta"], b["nb_theta"], atol=1e-9)
     assert np.allclose(a["glr"], b["glr"], atol=1e-8)
+    assert a["bkm_cost"] == pytest.approx(b["bkm_cost"], rel=1e-9)
+    assert a["gmm_ll"] == pytest.approx(b["gmm_ll"], rel=1e-9)
