@@ -355,6 +355,8 @@ def from_numpy(arr: np.ndarray, device) -> Column:
         first = next((v for v in vals if v is not None), None)
         if first is not None and len(first) and isinstance(first[0], str):
             return ArrayColumn([None if v is None else list(v) for v in vals])
+        if len({len(v) for v in vals if v is not None}) > 1 or any(v is None for v in vals):
+            return ArrayColumn([None if v is None else [float(x) for x in v] for v in vals])   # array<double>
         if first is not None:
             mat = np.array([np.asarray(v, dtype=np.float64) for v in vals])
             return VectorColumn(torch.from_numpy(mat).to(device))

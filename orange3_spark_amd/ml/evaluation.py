@@ -351,3 +351,5 @@ class ClusteringEvaluator(Evaluator, HasFeaturesCol, HasPredictionCol, HasWeight
 
 
 _ = HasFeaturesCol
+
+from ._evaluation_extra import MultilabelClassificationEvaluator, RankingEvaluator  # noqa: E402,F401

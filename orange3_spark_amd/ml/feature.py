@@ -58,6 +58,9 @@ def _as_matrix(col: C.Column, n: int, device) -> torch.Tensor:
     raise TypeError(f"Data type {col.dtype.simpleString()} of column is not supported.")
 
 
+from ._selector import _SelectorModel  # noqa: E402
+
+
 def _vec(df, name) -> torch.Tensor:
     return U.dense_features(df, name, torch.float64)
 
@@ -1371,28 +1374,6 @@ class PCAModel(Model, _InOut, MLWritable, MLReadable):
         return m
 
 
-class _SelectorModel(Model, HasFeaturesCol, HasOutputCol, MLWritable, MLReadable):
-    def __init__(self):
-        super().__init__()
-        self.selectedFeatures = []
-
-    def _transform(self, df):
-        X = _vec(df, self.getOrDefault(self.featuresCol))
-        idx = torch.tensor(self.selectedFeatures, dtype=torch.int64, device=X.device)
-        return df.withColumnData(self.getOrDefault(self.outputCol), C.VectorColumn(X[:, idx]))
-
-    def _save_data(self, path):
-        import pyarrow as pa
-        write_data(path, {"selectedFeatures": pa.array([self.selectedFeatures], pa.list_(pa.int32()))})
-
-    @classmethod
-    def _load_impl(cls, path, meta):
-        m = cls()
-        m.selectedFeatures = read_data(path).to_pylist()[0]["selectedFeatures"]
-        apply_metadata(m, meta)
-        return m
-
-
 @register("org.apache.spark.ml.feature.VarianceThresholdSelector")
 class VarianceThresholdSelector(Estimator, HasFeaturesCol, HasOutputCol, MLWritable, MLReadable):
     """Feature selector that removes all low-variance features."""
@@ -1589,6 +1570,10 @@ class MinHashLSHModel(_LSHModel):
         return 1 - inter / union.clamp_min(1)
 
 
+from ._feature_extra import (RFormula, RFormulaModel, UnivariateFeatureSelector,  # noqa: E402,F401
+                             UnivariateFeatureSelectorModel, Word2Vec, Word2VecModel)
+
 __all__ = [n for n, v in list(globals().items()) if isinstance(v, type) and issubclass(v, (Transformer, Estimator))
            and not n.startswith("_")] + ["to_vector_column"]
 _ = (HasMaxIter, HasStepSize, HasTol, HasWeightCol)
+

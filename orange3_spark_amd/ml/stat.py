@@ -159,3 +159,40 @@ class KolmogorovSmirnovTest:
         x = dataset.comm.all_gather_v(x) if dataset.comm.world_size > 1 else x
         r = stats.kstest(x.cpu().numpy(), distName, args=params)
         return dataset.session.createDataFrame([(float(r.pvalue), float(r.statistic))], ["pValue", "statistic"])
+
+
+def _test_frame(dataset, p, dof, stat, flatten):
+    s_ = dataset.session
+    if flatten:
+        import pandas as pd
+        return s_.createDataFrame(pd.DataFrame({"featureIndex": np.arange(len(p)), "pValue": p,
+                                                "degreesOfFreedom": np.asarray(dof, dtype=np.int64),
+                                                "fValue": stat}))
+    cols = OrderedDict(pValues=C.VectorColumn(torch.from_numpy(np.asarray(p, dtype=np.float64))[None, :]),
+                       degreesOfFreedom=C.ArrayColumn([[int(v) for v in dof]]),
+                       fValues=C.VectorColumn(torch.from_numpy(np.asarray(stat, dtype=np.float64))[None, :]))
+    return DataFrame(s_.local_view(), cols)
+
+
+class ANOVATest:
+    """ANOVA F-test of continuous features against a categorical label (Spark >= 3.1)."""
+
+    @staticmethod
+    def test(dataset, featuresCol, labelCol, flatten=False):
+        from ._feature_extra import anova_f
+        X = U.dense_features(dataset, featuresCol, torch.float64)
+        y = U.numeric_column(dataset, labelCol)
+        F, p, dof = anova_f(dataset.comm, X, y)
+        return _test_frame(dataset, p, dof, F, flatten)
+
+
+class FValueTest:
+    """F-value regression test of continuous features against a continuous label."""
+
+    @staticmethod
+    def test(dataset, featuresCol, labelCol, flatten=False):
+        from ._feature_extra import f_regression
+        X = U.dense_features(dataset, featuresCol, torch.float64)
+        y = U.numeric_column(dataset, labelCol)
+        F, p, dof = f_regression(dataset.comm, X, y)
+        return _test_frame(dataset, p, dof, F, flatten)
