@@ -65,7 +65,7 @@ def bin_features(X: torch.Tensor, splits: list) -> torch.Tensor:
     for f in range(F):
         t = torch.as_tensor(splits[f], dtype=X.dtype if X.is_floating_point() else torch.float64, device=X.device)
         for a in range(0, n, step):
-            col = X[a:a + step, f]
+            col = X[a:a + step, f].contiguous()
             out[a:a + step, f] = torch.bucketize(col.to(t.dtype), t, right=False).to(torch.uint8) if t.numel() \
                 else torch.zeros_like(col, dtype=torch.uint8)
     return out
