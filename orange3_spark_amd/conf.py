@@ -42,6 +42,9 @@ DEFAULTS = OrderedDict([
     ("o3s.vector.dtype", "auto"),
     ("o3s.memory.fraction", "0.85"),
     ("o3s.seed", "42"),
+    ("o3s.trace", "false"),                 # runtime/tracing.py phase tracer + roctx ranges
+    ("o3s.checkpoint.interval", "0"),       # iterations between checkpoints (needs spark.checkpoint.dir)
+    ("o3s.comm.timeout", "1800"),           # seconds before a hung collective raises
 ])
 
 

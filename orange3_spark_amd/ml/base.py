@@ -14,6 +14,7 @@ from abc import ABC, abstractmethod
 
 import torch
 
+from ..runtime.tracing import trace
 from .param import Param, Params, TypeConverters, keyword_only, shared
 from .util import (MLReadable, MLWritable, MLWriter, apply_metadata, load_metadata, py_class, register,
                    save_metadata)
@@ -31,9 +32,10 @@ class Transformer(Params, ABC):
             params = {}
         if not _is_param_map(params):
             raise TypeError(f"Params must be a param map but got {type(params)}.")
-        if params:
-            return self.copy(params)._transform(dataset)
-        return self._transform(dataset)
+        with trace(f"{type(self).__name__}.transform"):
+            if params:
+                return self.copy(params)._transform(dataset)
+            return self._transform(dataset)
 
     @abstractmethod
     def _transform(self, dataset):
@@ -50,9 +52,10 @@ class Estimator(Params, ABC):
             return [self.fit(dataset, p) for p in params]
         if not _is_param_map(params):
             raise TypeError(f"Params must be either a param map or a list/tuple of param maps, but got {type(params)}.")
-        if params:
-            return self.copy(params)._fit(dataset)
-        return self._fit(dataset)
+        with trace(f"{type(self).__name__}.fit"):
+            if params:
+                return self.copy(params)._fit(dataset)
+            return self._fit(dataset)
 
     def fitMultiple(self, dataset, paramMaps):
         for i, pm in enumerate(paramMaps):
@@ -79,9 +82,10 @@ class Evaluator(Params, ABC):
     def evaluate(self, dataset, params=None):
         if params is None:
             params = {}
-        if params:
-            return self.copy(params)._evaluate(dataset)
-        return self._evaluate(dataset)
+        with trace(f"{type(self).__name__}.evaluate"):
+            if params:
+                return self.copy(params)._evaluate(dataset)
+            return self._evaluate(dataset)
 
     @abstractmethod
     def _evaluate(self, dataset):

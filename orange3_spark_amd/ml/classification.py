@@ -20,6 +20,7 @@ from .param import (HasAggregationDepth, HasElasticNetParam, HasFeaturesCol, Has
                     HasMaxBlockSizeInMB, HasMaxIter, HasPredictionCol, HasProbabilityCol, HasRawPredictionCol,
                     HasRegParam, HasStandardization, HasStepSize, HasThreshold, HasThresholds, HasTol,
                     HasWeightCol, TypeConverters, add_accessors, keyword_only, shared)
+from ..runtime.checkpoint import for_estimator
 from .util import MLReadable, MLWritable, apply_metadata, mat_col, read_data, register, vec_col, write_data
 
 
@@ -100,7 +101,8 @@ class LogisticRegression(Estimator, _LogisticRegressionParams, MLWritable, MLRea
         solver = g(self.solver).lower()
         res = GLM.fit_glm(data, "logistic", g(self.regParam), g(self.elasticNetParam), g(self.fitIntercept),
                           g(self.standardization), g(self.maxIter), g(self.tol),
-                          "sgd" if solver == "sgd" else "auto", g(self.stepSize), g(self.miniBatchFraction))
+                          "sgd" if solver == "sgd" else "auto", g(self.stepSize), g(self.miniBatchFraction),
+                          ckpt=for_estimator(self, df))
         m = LogisticRegressionModel._from(res.coef[None, :], np.array([res.intercept]), False, 2)
         m.summary = _Summary(res.history, res.iterations, res.seconds, res.passes)
         return m._with_parent(self)
@@ -265,7 +267,7 @@ class LinearSVC(Estimator, _LinearSVCParams, MLWritable, MLReadable):
         data = GLM.GlmData(comm, U.features_column(df, g(self.featuresCol)), y, U.weights_or_none(df, self))
         res = GLM.fit_glm(data, "hinge", g(self.regParam), 0.0, g(self.fitIntercept), g(self.standardization),
                           g(self.maxIter), g(self.tol), "sgd" if g(self.solver) == "sgd" else "auto",
-                          g(self.stepSize), init_intercept=0.0)
+                          g(self.stepSize), init_intercept=0.0, ckpt=for_estimator(self, df))
         m = LinearSVCModel._from(res.coef, res.intercept)
         m.summary = _Summary(res.history, res.iterations, res.seconds, res.passes)
         return m._with_parent(self)

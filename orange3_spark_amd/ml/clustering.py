@@ -68,8 +68,10 @@ class KMeans(Estimator, _KMeansParams, MLWritable, MLReadable):
         X = U.dense_features(df, g(self.featuresCol))
         X = X.float().contiguous() if X.is_cuda else X.to(torch.float64)
         w = U.weights_or_none(df, self)
+        from ..runtime.checkpoint import for_estimator
         res = KM.fit_kmeans(df.comm, X, g(self.k), g(self.maxIter), g(self.tol), g(self.seed), g(self.initMode),
-                            g(self.initSteps), weights=w, cosine=g(self.distanceMeasure) == "cosine")
+                            g(self.initSteps), weights=w, cosine=g(self.distanceMeasure) == "cosine",
+                            ckpt=for_estimator(self, df))
         m = KMeansModel._from(res.centers.numpy())
         m.summary = _ClusteringSummary(g(self.k), res.sizes, res.cost, res.iterations)
         m.trainingSeconds = res.seconds

@@ -79,8 +79,10 @@ class ALS(Estimator, _ALSParams, MLWritable, MLReadable):
         users = U.numeric_column(df, g(self.userCol), torch.int64)
         items = U.numeric_column(df, g(self.itemCol), torch.int64)
         r = U.numeric_column(df, g(self.ratingCol), torch.float32)
+        from ..runtime.checkpoint import for_estimator
         res = ALSE.fit_als(df.comm, users, items, r, g(self.rank), g(self.maxIter), g(self.regParam),
-                           g(self.implicitPrefs), g(self.alpha), g(self.seed), g(self.nonnegative), g(self.cgIters))
+                           g(self.implicitPrefs), g(self.alpha), g(self.seed), g(self.nonnegative), g(self.cgIters),
+                           ckpt=for_estimator(self, df, sharded=True))
         m = ALSModel._from(res.user_ids, res.U, res.item_ids, res.V, g(self.rank))
         m.iterationSeconds = res.iter_seconds
         return m._with_parent(self)

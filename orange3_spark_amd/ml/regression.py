@@ -19,6 +19,7 @@ from .linalg import DenseVector
 from .param import (HasAggregationDepth, HasElasticNetParam, HasFeaturesCol, HasFitIntercept, HasLabelCol,
                     HasMaxBlockSizeInMB, HasMaxIter, HasPredictionCol, HasRegParam, HasStandardization, HasTol,
                     HasWeightCol, TypeConverters, keyword_only, shared)
+from ..runtime.checkpoint import for_estimator
 from .util import MLReadable, MLWritable, apply_metadata, read_data, register, vec_col, write_data
 
 
@@ -73,7 +74,7 @@ class LinearRegression(Estimator, _LinearRegressionParams, MLWritable, MLReadabl
             return m._with_parent(self)
         data = GLM.GlmData(comm, feat, y, w)
         res = GLM.fit_glm(data, "squared", g(self.regParam), alpha, g(self.fitIntercept), g(self.standardization),
-                          g(self.maxIter), g(self.tol))
+                          g(self.maxIter), g(self.tol), ckpt=for_estimator(self, df))
         m = LinearRegressionModel._from(res.coef, res.intercept)
         m.summary = _Summary(objectiveHistory=res.history, totalIterations=res.iterations)
         return m._with_parent(self)

@@ -26,6 +26,7 @@ import torch
 
 from ..ops import als as A
 from ..ops import sampling
+from ..runtime.tracing import trace
 
 
 @dataclass
@@ -148,7 +149,8 @@ class AlsResult:
 
 def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tensor, rank: int = 10,
             max_iter: int = 10, reg: float = 0.1, implicit: bool = False, alpha: float = 1.0, seed: int = 0,
-            nonneg: bool = False, cg_iters: int = 3, exact: bool | None = None, keep_full: bool = True) -> AlsResult:
+            nonneg: bool = False, cg_iters: int = 3, exact: bool | None = None, keep_full: bool = True,
+            ckpt=None) -> AlsResult:
     t0 = time.time()
     dev = ratings.device
     uid = global_ids(comm, users)
@@ -161,27 +163,36 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
     X = init_factors(by_user.row_lo, by_user.nrows, rank, seed, dev, nonneg)
     Y = init_factors(by_item.row_lo, by_item.nrows, rank, seed ^ 0x5A5A, dev, nonneg)
     its = []
-    for _ in range(max_iter):
-        ti = time.time()
-        Yf = comm.all_gather_v(Y) if comm.world_size > 1 else Y
-        YtY = None
-        if implicit:
-            YtY = (Y.T.to(torch.float64) @ Y.to(torch.float64)).contiguous()
-            comm.all_reduce(YtY)
-            YtY = YtY.float()
-        X = solve_side(by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact)
-        del Yf
-        Xf = comm.all_gather_v(X) if comm.world_size > 1 else X
-        XtX = None
-        if implicit:
-            XtX = (X.T.to(torch.float64) @ X.to(torch.float64)).contiguous()
-            comm.all_reduce(XtX)
-            XtX = XtX.float()
-        Y = solve_side(by_item, Xf, Y, reg, implicit, alpha, XtX, cg_iters, nonneg, exact)
-        del Xf
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        its.append(time.time() - ti)
+    start = 0
+    last = ckpt.latest() if ckpt is not None else None
+    if last is not None:                 # resume: this rank's factor shards (runtime/checkpoint.py)
+        start, st, _ = last
+        X = torch.from_numpy(st["X"]).to(dev, X.dtype)
+        Y = torch.from_numpy(st["Y"]).to(dev, Y.dtype)
+    for it in range(start, max_iter):
+        with trace("als.iter"):
+            ti = time.time()
+            Yf = comm.all_gather_v(Y) if comm.world_size > 1 else Y
+            YtY = None
+            if implicit:
+                YtY = (Y.T.to(torch.float64) @ Y.to(torch.float64)).contiguous()
+                comm.all_reduce(YtY)
+                YtY = YtY.float()
+            X = solve_side(by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact)
+            del Yf
+            Xf = comm.all_gather_v(X) if comm.world_size > 1 else X
+            XtX = None
+            if implicit:
+                XtX = (X.T.to(torch.float64) @ X.to(torch.float64)).contiguous()
+                comm.all_reduce(XtX)
+                XtX = XtX.float()
+            Y = solve_side(by_item, Xf, Y, reg, implicit, alpha, XtX, cg_iters, nonneg, exact)
+            del Xf
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            its.append(time.time() - ti)
+            if ckpt is not None and ckpt.due(it + 1):
+                ckpt.save(it + 1, {"X": X.cpu().numpy(), "Y": Y.cpu().numpy()})
     Uf = comm.all_gather_v(X) if (keep_full and comm.world_size > 1) else X
     Vf = comm.all_gather_v(Y) if (keep_full and comm.world_size > 1) else Y
     return AlsResult(uid, iid, Uf, Vf, time.time() - t0, its)

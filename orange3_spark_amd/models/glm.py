@@ -27,6 +27,7 @@ import torch
 from ..frame import column as C
 from ..ops import _native as N
 from ..ops import glm as G
+from ..runtime.tracing import traced
 from ..synthetic import LineageVectorColumn
 from . import optim
 
@@ -136,6 +137,7 @@ class GlmData:
         self.passes += 1
         return acc
 
+    @traced("glm.pass")
     def loss_grad(self, coef_eff: np.ndarray, intercept: float, loss: int):
         """Global (loss_sum, grad (d), grad_intercept, weight_sum) as fp64 numpy."""
         ct = torch.from_numpy(np.ascontiguousarray(coef_eff, dtype=np.float64))
@@ -204,7 +206,7 @@ class GlmObjective:
 
 def fit_glm(data: GlmData, loss: str, reg=0.0, alpha=0.0, fit_intercept=True, standardization=True,
             max_iter=100, tol=1e-6, solver="auto", step_size=1.0, mini_batch_fraction=1.0, seed=0,
-            init_intercept=None) -> GlmResult:
+            init_intercept=None, ckpt=None) -> GlmResult:
     t0 = time.time()
     mean, var, W, ymean, yvar = data.moments()
     std = np.sqrt(var)
@@ -218,15 +220,24 @@ def fit_glm(data: GlmData, loss: str, reg=0.0, alpha=0.0, fit_intercept=True, st
             x0[-1] = math.log(ymean / (1 - ymean))
         elif loss == "squared":
             x0[-1] = ymean
+    done = 0
+    last = ckpt.latest() if ckpt is not None else None
+    if last is not None and last[1]["x"].shape == x0.shape:
+        done, x0 = last[0], last[1]["x"]            # warm restart from the checkpointed iterate
+
+    def save(it, x, f):
+        if ckpt is not None and ckpt.due(done + it):
+            ckpt.save(done + it, {"x": np.asarray(x)})
+    left = max(max_iter - done, 0)
     if solver in ("sgd", "gd"):
-        res = _sgd(obj, x0, max_iter, step_size, mini_batch_fraction, seed, tol)
+        res = _sgd(obj, x0, left, step_size, mini_batch_fraction, seed, tol)
     elif reg * alpha > 0:
         l1 = np.concatenate([obj.pen1, [0.0]]) if fit_intercept else obj.pen1
-        r = optim.owlqn(obj.smooth, x0, l1, max_iter=max_iter, tol=tol)
-        res = GlmResult(r.x, 0.0, r.history, r.iterations, r.converged)
+        r = optim.owlqn(obj.smooth, x0, l1, max_iter=left, tol=tol, callback=save)
+        res = GlmResult(r.x, 0.0, r.history, done + r.iterations, r.converged)
     else:
-        r = optim.lbfgs(obj.smooth, x0, max_iter=max_iter, tol=tol)
-        res = GlmResult(r.x, 0.0, r.history, r.iterations, r.converged)
+        r = optim.lbfgs(obj.smooth, x0, max_iter=left, tol=tol, callback=save)
+        res = GlmResult(r.x, 0.0, r.history, done + r.iterations, r.converged)
     bt, b = obj.split(res.coef)
     res.coef = bt * obj.inv_std
     res.intercept = float(b)
@@ -278,6 +289,7 @@ class DeviceSGD:
         self.loss_hist = torch.zeros(1024, dtype=torch.float64, device=dev)
         self.W = float(data.comm.sum_scalar(float(data.n_local if data.sw is None else float(data.sw.sum()))))
 
+    @traced("sgd.step")
     def step(self):
         """One step, entirely stream-ordered on the device: pass -> all-reduce -> update."""
         self.t += 1

@@ -17,6 +17,7 @@ import torch
 
 from ..ops import kmeans as K
 from ..ops import sampling
+from ..runtime.tracing import trace
 
 
 @dataclass
@@ -117,11 +118,14 @@ def random_init(comm, X, k, seed):
 
 def fit_kmeans(comm, X: torch.Tensor, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int = 0,
                init: str = "k-means||", init_steps: int = 2, initial: torch.Tensor | None = None,
-               weights: torch.Tensor | None = None, cosine: bool = False) -> KMeansResult:
+               weights: torch.Tensor | None = None, cosine: bool = False, ckpt=None) -> KMeansResult:
     t0 = time.time()
     if cosine:
         X = X / X.norm(dim=1, keepdim=True).clamp_min(1e-300)
-    if initial is not None:
+    last = ckpt.latest() if ckpt is not None else None
+    if last is not None:
+        C = None                         # resumed below; skip the initialisation passes
+    elif initial is not None:
         C = initial.to(X.device, torch.float64)
     elif init == "random":
         C = random_init(comm, X, k, seed)
@@ -130,30 +134,37 @@ def fit_kmeans(comm, X: torch.Tensor, k: int, max_iter: int = 20, tol: float = 1
     D = X.shape[1]
     ws = K.UpdateWorkspace(X.device, ((k + 31) // 32) * 32, D) if K.kernel_ok(X) and weights is None else None
     hist = []
-    it = 0
+    it = start = 0
+    if last is not None:                 # resume from the last saved centres
+        start, st, _ = last
+        C = torch.from_numpy(st["C"]).to(X.device, torch.float64)
+        hist = [float(v) for v in st["hist"]]
     sizes = None
     cost = float("nan")
-    for it in range(1, max_iter + 1):
-        prep = K.prepare_centers(C.float()) if K.kernel_ok(X) else None
-        a, d = K.assign(X, C.float(), prep)
-        if ws is not None:
-            sums, cnt = K.update(X, a, ws.K, ws)
-            sums, cnt = sums[:k], cnt[:k]
-        else:
-            sums, cnt = K.update_torch(X, a, k, weights)
-        dd = d.to(torch.float64) if weights is None else d.to(torch.float64) * weights.to(torch.float64)
-        buf = torch.cat([sums.reshape(-1), cnt, dd.sum().reshape(1)])
-        comm.all_reduce(buf)
-        sums, cnt, cost = buf[: k * D].reshape(k, D), buf[k * D: k * D + k], float(buf[-1])
-        hist.append(cost)
-        newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp_min(1e-300)[:, None], C)
-        if cosine:
-            newC = newC / newC.norm(dim=1, keepdim=True).clamp_min(1e-300)
-        moved = ((newC - C) ** 2).sum(1).max().item()
-        C = newC
-        sizes = cnt
-        if moved <= tol * tol:
-            break
+    for it in range(start + 1, max_iter + 1):
+        with trace("kmeans.iter"):
+            prep = K.prepare_centers(C.float()) if K.kernel_ok(X) else None
+            a, d = K.assign(X, C.float(), prep)
+            if ws is not None:
+                sums, cnt = K.update(X, a, ws.K, ws)
+                sums, cnt = sums[:k], cnt[:k]
+            else:
+                sums, cnt = K.update_torch(X, a, k, weights)
+            dd = d.to(torch.float64) if weights is None else d.to(torch.float64) * weights.to(torch.float64)
+            buf = torch.cat([sums.reshape(-1), cnt, dd.sum().reshape(1)])
+            comm.all_reduce(buf)
+            sums, cnt, cost = buf[: k * D].reshape(k, D), buf[k * D: k * D + k], float(buf[-1])
+            hist.append(cost)
+            newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp_min(1e-300)[:, None], C)
+            if cosine:
+                newC = newC / newC.norm(dim=1, keepdim=True).clamp_min(1e-300)
+            moved = ((newC - C) ** 2).sum(1).max().item()
+            C = newC
+            sizes = cnt
+            if ckpt is not None and ckpt.due(it):
+                ckpt.save(it, {"C": C.cpu().numpy(), "hist": np.asarray(hist)})
+            if moved <= tol * tol:
+                break
     # final cost/sizes w.r.t. the returned centres (Spark reports the last assignment's)
     a, d = K.assign(X, C.float())
     cnt = torch.zeros(k, dtype=torch.float64, device=X.device).index_add_(

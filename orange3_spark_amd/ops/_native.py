@@ -15,6 +15,7 @@ from pathlib import Path
 
 import torch
 
+from ..runtime.faults import O3SError
 from . import build as _build
 
 _LOCK = threading.Lock()
@@ -43,8 +44,8 @@ _SIGS: dict[str, list] = {
 }
 
 
-class NativeError(RuntimeError):
-    pass
+class NativeError(O3SError):
+    """A native kernel launch was rejected (bad shape/arguments) or failed."""
 
 
 def lib_path() -> Path:
@@ -125,8 +126,16 @@ def stream_of(t: torch.Tensor) -> int:
 
 
 def check(rc: int, what: str) -> None:
+    """Validate a native launch's return code (+ fault injection / launch-blocking mode)."""
+    from ..runtime import faults
+    faults.INJECTOR.hit("kernel")
     if rc != 0:
         raise NativeError(f"{what} failed with code {rc}")
+    if faults.launch_blocking() and torch.cuda.is_available():
+        try:
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 - surfaces async HIP faults at the launching call
+            raise faults.DeviceError(what, e) from e
 
 
 def num_cus(device: torch.device) -> int:

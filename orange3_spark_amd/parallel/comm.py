@@ -146,10 +146,10 @@ class TorchComm(Comm):
     object collectives never allocate device memory.
     """
 
-    def __init__(self, device: torch.device, backend: str | None = None, group=None):
+    def __init__(self, device: torch.device, backend: str | None = None, group=None, timeout_s: int = 1800):
         self.device = torch.device(device)
         if not dist.is_initialized():
-            init_process_group(self.device, backend)
+            init_process_group(self.device, backend, timeout_s)
         self.group = group
         self.rank = dist.get_rank(group)
         self.world_size = dist.get_world_size(group)
@@ -255,11 +255,38 @@ def init_process_group(device: torch.device, backend: str | None = None, timeout
     dist.init_process_group(**kw)
 
 
-def make_comm(device: torch.device | str, world_size: int | None = None) -> Comm:
+def make_comm(device: torch.device | str, world_size: int | None = None, timeout_s: int = 1800) -> Comm:
     device = torch.device(device)
     _, _, world = env_world()
     if world_size is not None:
         world = world_size
     if world <= 1 and not dist.is_initialized():
         return LocalComm(device)
-    return TorchComm(device)
+    return TorchComm(device, timeout_s=timeout_s)
+
+
+# ------------------------------------------------------------ tracing + failure wrapping
+def _guard(name, fn):
+    """Trace a collective, apply fault injection, and turn backend exceptions into
+    CommError carrying op/rank/world (runtime/faults.py)."""
+    from ..runtime.faults import INJECTOR, CommError, O3SError
+    from ..runtime.tracing import trace
+    op = "comm." + name
+
+    def wrapper(self, *a, **k):
+        INJECTOR.hit(op)
+        with trace(op):
+            try:
+                return fn(self, *a, **k)
+            except O3SError:
+                raise
+            except Exception as e:  # noqa: BLE001 - RCCL/gloo raise RuntimeError/DistBackendError/...
+                raise CommError(name, self.rank, self.world_size, self.backend, e) from e
+    wrapper.__name__, wrapper.__doc__, wrapper.__wrapped__ = fn.__name__, fn.__doc__, fn
+    return wrapper
+
+
+for _n in ("all_reduce", "all_gather", "all_gather_v", "reduce_scatter", "broadcast", "all_to_all_v", "barrier",
+           "all_gather_object", "broadcast_object"):
+    setattr(TorchComm, _n, _guard(_n, TorchComm.__dict__[_n]))
+LocalComm.all_reduce = _guard("all_reduce", LocalComm.__dict__["all_reduce"])

@@ -42,7 +42,8 @@ class Session:
         if comm is None:
             master = self.conf.master().lower()
             rank, local, world = env_world()
-            comm = make_comm(self.device) if (world > 1 or master == "spmd") else LocalComm(self.device)
+            comm = make_comm(self.device, timeout_s=int(float(self.conf.get("o3s.comm.timeout", "1800")))) \
+                if (world > 1 or master == "spmd") else LocalComm(self.device)
         self.comm = comm
         if self.conf.get("spark.master", "").lower() == "spmd":
             want = int(self.conf.get("spark.executor.instances", str(self.comm.world_size)))
@@ -54,6 +55,9 @@ class Session:
         self.version = __version__
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+        if str(self.conf.get("o3s.trace", "false")).lower() in ("1", "true", "yes"):
+            from .runtime.tracing import TRACER
+            TRACER.enable(sync=str(self.conf.get("o3s.trace.sync", "false")).lower() in ("1", "true"))
 
     # ------------------------------------------------------------------ lifecycle
     def _pick_device(self) -> torch.device:
@@ -113,6 +117,26 @@ class Session:
     @property
     def appName(self):
         return self.conf.get("spark.app.name")
+
+    # ------------------------------------------------------------------ runtime services
+    def setCheckpointDir(self, dirName: str) -> None:
+        """Enable iteration checkpoints / resume for iterative estimators
+        (runtime/checkpoint.py; SparkContext.setCheckpointDir)."""
+        self.conf.set("spark.checkpoint.dir", str(dirName))
+
+    def getCheckpointDir(self):
+        return self.conf.get("spark.checkpoint.dir", None)
+
+    def health_check(self, timeout_s: float = 30.0) -> dict:
+        """Probe every rank (runtime/faults.py)."""
+        from .runtime.faults import health_check
+        return health_check(self.comm, timeout_s)
+
+    @property
+    def tracer(self):
+        """Process tracer (runtime/tracing.py): ``session.tracer.enable()``, ``.table()``."""
+        from .runtime.tracing import TRACER
+        return TRACER
 
     def local_view(self) -> "Session":
         """A view of this session whose collectives are local (replicated compute)."""
