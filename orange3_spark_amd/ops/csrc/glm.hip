@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
     // SRC == 1: rows past n are harmless (their residual is masked to 0) and columns
     // past ld meet zero weights and are never written out, so no masking is needed.
     short8 xv[UNROLL][CPL];
-    uint32_t hv[UNROLL][CPL][2];
+    float xf[UNROLL][CPL][8];          // SRC == 1: decoded once, reused by dot and X^T r
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const int64_t row = base + u * G + g;
@@ -191,8 +191,12 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
           short8 v = __builtin_nontemporal_load(reinterpret_cast<const short8*>(X + rowc * ld + 8 * chc));
           xv[u][k] = okc ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
         } else {
-          hv[u][k][0] = synth_word(rk, 2 * ch);
-          hv[u][k][1] = synth_word(rk, 2 * ch + 1);
+          const uint32_t h0 = synth_word(rk, 2 * ch), h1 = synth_word(rk, 2 * ch + 1);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            xf[u][k][j] = synth_byte(h0, j);
+            xf[u][k][4 + j] = synth_byte(h1, j);
+          }
         }
       }
     }
@@ -223,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
           unpack8(xv[u][k], x);
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = synth_byte(hv[u][k][j >> 2], j & 3);
+          for (int j = 0; j < 8; ++j) x[j] = xf[u][k][j];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -274,7 +278,10 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         if (SRC == 0) asm volatile("" : "+v"(xv[u][k]));
-        else asm volatile("" : "+v"(hv[u][k][0]), "+v"(hv[u][k][1]));
+        else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(xf[u][k][j]));
+        }
       }
     // broadcast each row's residual back to its LPR lanes, accumulate X^T r
 #pragma unroll
@@ -288,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
           unpack8(xv[u][k], x);
         } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) x[j] = synth_byte(hv[u][k][j >> 2], j & 3);
+          for (int j = 0; j < 8; ++j) x[j] = xf[u][k][j];
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(r, x[j], acc[k][j]);
