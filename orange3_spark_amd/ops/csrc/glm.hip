@@ -590,7 +590,7 @@ void launch_grad(int grid, hipStream_t st, const uint16_t* X, int64_t ld, int64_
                  int64_t row0, const float* wt, float bt, float* partial, int pstride) {
   // rows in flight per lane: 8 loads for the streaming pass; the lineage pass keeps
   // fewer chunks live (its hash work, not memory latency, is the limiter)
-  constexpr int UNROLL = SRC == 1 ? (CPL >= 4 ? 1 : 4 / CPL) : (CPL == 1 ? 8 : (CPL == 2 ? 2 : 1));
+  constexpr int UNROLL = SRC == 1 ? (CPL >= 8 ? 1 : 8 / CPL) : (CPL == 1 ? 8 : (CPL == 2 ? 2 : 1));
   hipLaunchKernelGGL((glm_grad_kernel<LPR, CPL, UNROLL, LOSS, SRC>), dim3(grid), dim3(kBlock), 0,
                      st, X, ld, n, y, sw, coef, b, seed, row0, wt, bt, partial, pstride);
 }
