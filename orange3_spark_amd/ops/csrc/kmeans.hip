@@ -56,58 +56,104 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
   constexpr int SLOTS = D / 8;                 // 16-B slots per centroid row
   constexpr int CH_ELEMS = 32 * D;             // bf16 per chunk (hi or lo)
   constexpr int PIECES = 2 * 32 * SLOTS;       // 16-B pieces per chunk (hi + lo)
-  constexpr int PER_THREAD = (PIECES + kAssignThreads - 1) / kAssignThreads;
+  // G centroid chunks per LDS stage (one barrier per G chunks), double-buffered
+  constexpr int G = D <= 128 ? 4 : 2;
+  constexpr int PER_THREAD = (G * PIECES + kAssignThreads - 1) / kAssignThreads;
   static_assert(PIECES % kWave == 0, "whole waves per DMA instruction");
   constexpr int ROWS_PER_WAVE = 32 * TT;
   constexpr int ROWS_PER_BLOCK = kAssignWaves * ROWS_PER_WAVE;
   // ONE __shared__ array (guide §5 item 4a): [buf][hi|lo][32][D] bf16, slot-swizzled rows
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * 2 * CH_ELEMS];
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * G * 2 * CH_ELEMS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int64_t row_base = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wid * ROWS_PER_WAVE;
 
-  // ---- X^T fragments (B operand) for the wave's rows, split hi/lo, + ||x||^2
+  // ---- X^T fragments (B operand) for the wave's rows, split hi/lo, + ||x||^2.
+  // The fragment layout wants 32 rows per load instruction (lane r <- row r), which
+  // touches 32 rows x 32 B per wave-instruction; instead the wave streams its 32-row
+  // tile row-contiguously (1 KiB per instruction) into its slice of the (not yet used)
+  // centroid LDS buffer and reads the fragments back transposed.  16-B slots are
+  // XOR-swizzled by row so the 32-row column reads are conflict free.
+  // (D > 128: the tile does not fit the stage buffer; load the fragments directly.)
+  constexpr int XS = D / 4;                    // 16-B slots per staged row
+  constexpr bool kStageX = kAssignWaves * ROWS_PER_WAVE * D * 4 <= (int)sizeof(lds);
+  float* xt = reinterpret_cast<float*>(lds) + wid * ROWS_PER_WAVE * D;
   bf16x8 bh[TT][KS], bl[TT][KS];
   float xn[TT];
+  if constexpr (kStageX) {
+    constexpr int PIECES_X = ROWS_PER_WAVE * XS;
+#pragma unroll 4
+    for (int P = lane; P < PIECES_X; P += kWave) {
+      const int rr = P / XS, sl = P % XS;
+      const int64_t row = row_base + rr;
+      const int64_t rowc = row < n ? row : n - 1;
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 v = 4 * sl < Dx ? *reinterpret_cast<const float4*>(X + rowc * ldx + 4 * sl) : z;
+      *reinterpret_cast<float4*>(xt + rr * D + 4 * (sl ^ (rr & (XS - 1) & 31))) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave reads back only its own slice
+  }
 #pragma unroll
   for (int t = 0; t < TT; ++t) {
-    const int64_t row = row_base + t * 32 + r;
-    const int64_t rowc = row < n ? row : n - 1;
-    const float* xp = X + rowc * ldx;
+    const int rr = t * 32 + r;
     float s = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const int c0 = ks * 16 + 8 * h;          // Dx % 4 == 0: whole float4s are in or out
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 a = c0 < Dx ? *reinterpret_cast<const float4*>(xp + c0) : z;
-      const float4 b = c0 + 4 < Dx ? *reinterpret_cast<const float4*>(xp + c0 + 4) : z;
-      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        short hi, lo;
-        split_bf16(v[j], hi, lo);
-        bh[t][ks][j] = hi;
-        bl[t][ks][j] = lo;
-        s = fmaf(v[j], v[j], s);
+      float4 a, b;
+      if constexpr (kStageX) {
+        const int s0 = (ks * 16 + 8 * h) / 4;
+        const int sw = rr & (XS - 1) & 31;
+        a = *reinterpret_cast<const float4*>(xt + rr * D + 4 * (s0 ^ sw));
+        b = *reinterpret_cast<const float4*>(xt + rr * D + 4 * ((s0 + 1) ^ sw));
+      } else {
+        const int64_t row = row_base + rr;
+        const float* xp = X + (row < n ? row : n - 1) * ldx;
+        const int c0 = ks * 16 + 8 * h;        // Dx % 4 == 0: whole float4s are in or out
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        a = c0 < Dx ? *reinterpret_cast<const float4*>(xp + c0) : z;
+        b = c0 + 4 < Dx ? *reinterpret_cast<const float4*>(xp + c0 + 4) : z;
       }
+      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      // pack pairs into dwords explicitly and pin the packed registers: left as 16 separate
+      // shorts, hipcc keeps one bf16 per VGPR and re-packs every fragment (4 v_perm) for
+      // every chunk of the centroid sweep
+      uint32_t ph[4], pl[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        short h0, l0, h1, l1;
+        split_bf16(v[2 * j], h0, l0);
+        split_bf16(v[2 * j + 1], h1, l1);
+        ph[j] = (uint32_t)(uint16_t)h0 | ((uint32_t)(uint16_t)h1 << 16);
+        pl[j] = (uint32_t)(uint16_t)l0 | ((uint32_t)(uint16_t)l1 << 16);
+        s = fmaf(v[2 * j], v[2 * j], s);
+        s = fmaf(v[2 * j + 1], v[2 * j + 1], s);
+      }
+      bh[t][ks] = __builtin_bit_cast(bf16x8, ph);
+      bl[t][ks] = __builtin_bit_cast(bf16x8, pl);
+      asm volatile("" : "+v"(bh[t][ks]), "+v"(bl[t][ks]));
     }
     xn[t] = s + __shfl_xor(s, 32, 64);
   }
+  __syncthreads();                             // every wave done with the staging area
 
   // ---- chunk staging by LDS-DMA (global_load_lds_dwordx4): the LDS image is lane-linear,
   // so the XOR swizzle is applied to the SOURCE slot (guide §5.4 rule 21).
   const int nchunks = Cpad / 32;
-  auto stage = [&](int chunk, int buf) {
+  const int nchunks_ = Cpad / 32;
+  auto stage = [&](int stg, int buf) {
 #pragma unroll
     for (int k = 0; k < PER_THREAD; ++k) {
-      const int P = threadIdx.x + k * kAssignThreads;      // linear 16-B piece index
-      if (PIECES % kAssignThreads != 0 && P >= PIECES) break;   // wave-uniform
-      const int which = P / (32 * SLOTS);
-      const int rem = P % (32 * SLOTS);
+      const int P = threadIdx.x + k * kAssignThreads;      // linear 16-B piece index in the stage
+      const int g = P / PIECES;                            // wave-uniform (PIECES % 64 == 0)
+      const int chunk = stg * G + g;
+      if (P >= G * PIECES || chunk >= nchunks_) continue;  // the DMA image stays lane-linear
+      const int Q = P % PIECES;
+      const int which = Q / (32 * SLOTS);
+      const int rem = Q % (32 * SLOTS);
       const int cr = rem / SLOTS, sw = rem % SLOTS;
       const int sl = sw ^ (cr & 15 & (SLOTS - 1));
       const uint16_t* src = (which ? Clo : Chi) + ((int64_t)(chunk * 32 + cr)) * D + sl * 8;
-      uint16_t* dst = lds + buf * 2 * CH_ELEMS + (wid * kWave + k * kAssignThreads) * 8;   // wave-uniform
+      uint16_t* dst = lds + buf * G * 2 * CH_ELEMS + (wid * kWave + k * kAssignThreads) * 8;   // wave-uniform
       __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
     }
   };
@@ -119,31 +165,12 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
   stage(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int ch = 0; ch < nchunks; ++ch) {
-    const int buf = ch & 1;
-    if (ch + 1 < nchunks) stage(ch + 1, buf ^ 1);       // DMA in flight under the MFMAs
-    const uint16_t* Lh = lds + buf * 2 * CH_ELEMS;
-    const uint16_t* Ll = Lh + CH_ELEMS;
-    f32x16 acc[TT];
-#pragma unroll
-    for (int t = 0; t < TT; ++t)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int sl = ks * 2 + h;
-      const int sw = sl ^ (r & 15 & (SLOTS - 1));
-      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Lh + r * D + sw * 8);
-      const bf16x8 al = *reinterpret_cast<const bf16x8*>(Ll + r * D + sw * 8);
-#pragma unroll
-      for (int t = 0; t < TT; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t][ks], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t][ks], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t][ks], acc[t], 0, 0, 0);
-      }
-    }
-    // epilogue: centroid of acc reg i = ch*32 + (i&3) + 8*(i>>2) + 4*h
-    const int cbase = ch * 32 + 4 * h;
+  // Software pipeline: the MFMAs of chunk ch are issued, then the arg-min epilogue of
+  // chunk ch-1 (independent VALU work) fills the MFMA issue gaps instead of running in
+  // a separate phase after every barrier.
+  f32x16 accp[TT];
+  auto epilogue = [&](const f32x16 (&a)[TT], int chp) {
+    const int cbase = chp * 32 + 4 * h;      // acc reg i -> centroid cbase + (i&3) + 8*(i>>2)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float4 c4 = *reinterpret_cast<const float4*>(cn + cbase + 8 * q);
@@ -153,16 +180,54 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
         const int idx = cbase + 8 * q + j;
 #pragma unroll
         for (int t = 0; t < TT; ++t) {
-          const float dv = acc[t][4 * q + j] + cv[j];
+          const float dv = a[t][4 * q + j] + cv[j];
           const bool better = dv < bestv[t];
           bestv[t] = better ? dv : bestv[t];
           besti[t] = better ? idx : besti[t];
         }
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // next chunk landed
-    __syncthreads();                                   // ... for every wave; buf free again
+  };
+  const int nstages = (nchunks + G - 1) / G;
+  for (int stg = 0; stg < nstages; ++stg) {
+   const int buf = stg & 1;
+   if (stg + 1 < nstages) stage(stg + 1, buf ^ 1);      // DMA in flight under the MFMAs
+   for (int g = 0; g < G; ++g) {
+    const int ch = stg * G + g;
+    if (ch >= nchunks) break;
+    const uint16_t* Lh = lds + (buf * G + g) * 2 * CH_ELEMS;
+    const uint16_t* Ll = Lh + CH_ELEMS;
+    f32x16 acc[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    // A fragments are read one k-step ahead of the MFMAs that consume them, so the LDS
+    // latency hides under the previous step's three MFMAs
+    auto afrag = [&](const uint16_t* L, int ks) {
+      const int sw = (ks * 2 + h) ^ (r & 15 & (SLOTS - 1));
+      return *reinterpret_cast<const bf16x8*>(L + r * D + sw * 8);
+    };
+    bf16x8 nh = afrag(Lh, 0), nl = afrag(Ll, 0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 ah = nh, al = nl;
+      if (ks + 1 < KS) { nh = afrag(Lh, ks + 1); nl = afrag(Ll, ks + 1); }
+#pragma unroll
+      for (int t = 0; t < TT; ++t) {
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t][ks], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t][ks], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t][ks], acc[t], 0, 0, 0);
+      }
+    }
+    if (ch > 0) epilogue(accp, ch - 1);
+#pragma unroll
+    for (int t = 0; t < TT; ++t) accp[t] = acc[t];
+   }
+   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // next stage landed
+   __syncthreads();                                    // ... for every wave; buf free again
   }
+  if (nchunks > 0) epilogue(accp, nchunks - 1);
   // merge the two half-waves (different centroid subsets of the same row)
 #pragma unroll
   for (int t = 0; t < TT; ++t) {
