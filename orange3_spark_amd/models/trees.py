@@ -25,6 +25,7 @@ import torch
 
 from ..ops import sampling
 from ..ops import trees as T
+from ..runtime.tracing import trace
 
 
 # ----------------------------------------------------------------------------- binning
@@ -180,9 +181,12 @@ class TreeBuilder:
                 break
             k = len(nodes)
             local = torch.arange(k, device=dev)
-            H = T.node_hist(self.bins, order, self.y, self.w, seg_lo, seg_hi, local, k, B, S, self.cls)
-            H = H.to(torch.float64).contiguous()
+            with trace("tree.hist"):
+                H = T.node_hist(self.bins, order, self.y, self.w, seg_lo, seg_hi, local, k, B, S, self.cls)
+                H = H.to(torch.float64).contiguous()
             self.comm.all_reduce(H)                               # [k, F, B, S]
+            tsplit = trace("tree.split")
+            tsplit.__enter__()
             tot = H[:, 0].sum(1)                                   # [k, S] node stats (feature 0 bins)
             imp_p, w_p = _impurity(tot, self.kind)
             vals = (tot / w_p.clamp_min(1e-300)[:, None]) if self.cls else \
@@ -191,10 +195,17 @@ class TreeBuilder:
             cum = H.cumsum(2)                                      # [k, F, B, S]
             left = cum[:, :, :-1]
             right = tot[:, None, None, :] - left
-            iL, wL = _impurity(left, self.kind)
-            iR, wR = _impurity(right, self.kind)
             W = w_p[:, None, None].clamp_min(1e-300)
-            g = imp_p[:, None, None] - (wL / W) * iL - (wR / W) * iR
+            if self.cls:
+                iL, wL = _impurity(left, self.kind)
+                iR, wR = _impurity(right, self.kind)
+                g = imp_p[:, None, None] - (wL / W) * iL - (wR / W) * iR
+            else:
+                # variance gain from (w, w*y) only: (SyL^2/wL + SyR^2/wR - Sy^2/W) / W
+                wL, wR = left[..., 0], right[..., 0]
+                sL, sR = left[..., 1], right[..., 1]
+                sP = tot[:, 1][:, None, None]
+                g = (sL * sL / wL.clamp_min(1e-300) + sR * sR / wR.clamp_min(1e-300) - sP * sP / W) / W
             ok = (wL >= self.min_inst) & (wR >= self.min_inst)
             nb = torch.tensor([len(s) for s in self.splits], device=dev)
             ok &= torch.arange(B - 1, device=dev)[None, None, :] < nb[None, :, None]
@@ -215,9 +226,12 @@ class TreeBuilder:
             impurity[node_ids] = imp_np
             count[node_ids] = w_np
             do_split = (bg > self.min_gain) & (bg > 0) & np.isfinite(bg) & (depth < self.max_depth)
+            tsplit.__exit__(None, None, None)
             if not do_split.any():
                 leaf_segments.append((seg_lo, seg_hi, seg_node))
                 break
+            tpart = trace("tree.partition")
+            tpart.__enter__()
             for i, nid in enumerate(node_ids):
                 if do_split[i]:
                     feature[nid] = bf[i]
@@ -230,29 +244,12 @@ class TreeBuilder:
             s_lo, s_hi, s_node = seg_lo[spl], seg_hi[spl], seg_node[spl]
             s_feat = torch.from_numpy(bf[do_split]).to(dev)
             s_bin = torch.from_numpy(bb[do_split]).to(dev)
-            lens = s_hi - s_lo
-            total = int(lens.sum())
-            sid = torch.repeat_interleave(torch.arange(s_lo.numel(), device=dev), lens)
-            first = torch.cumsum(lens, 0) - lens
-            pos = s_lo[sid] + (torch.arange(total, device=dev) - first[sid])
-            rows = order[pos].long()
-            bvals = self.bins.view(-1)[rows * F + s_feat[sid]]
-            go_left = bvals.to(torch.int64) <= s_bin[sid]
-            gl = go_left.to(torch.int64)
-            cl = torch.cumsum(gl, 0)
-            cl_before = cl[first] - gl[first]                      # exclusive prefix at segment starts
-            nleft = torch.zeros(s_lo.numel(), dtype=torch.int64, device=dev).index_add_(0, sid, gl)
-            lrank = cl - cl_before[sid]                            # inclusive rank among lefts
-            rel = torch.arange(total, device=dev) - first[sid]
-            rrank = rel + 1 - lrank
-            newpos = torch.where(go_left, s_lo[sid] + lrank - 1, s_lo[sid] + nleft[sid] + rrank - 1)
-            new_order = order.clone()
-            new_order[newpos] = order[pos]
-            order = new_order
+            order, nleft = T.partition(self.bins, order, s_lo, s_hi, s_feat, s_bin)
             mid = s_lo + nleft
             seg_lo = torch.stack([s_lo, mid], 1).reshape(-1)
             seg_hi = torch.stack([mid, s_hi], 1).reshape(-1)
             seg_node = torch.stack([2 * s_node, 2 * s_node + 1], 1).reshape(-1)
+            tpart.__exit__(None, None, None)
             # empty local segments still participate (other ranks may have rows there)
         tree = Tree(feature, threshold, split_bin, value, impurity, gain, count, F)
         # per-row leaf ids of the training rows (for boosting updates), no traversal needed

@@ -72,6 +72,11 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 __device__ __forceinline__ float wave_sum(float v) { return group_sum<64>(v); }
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
 
 // Numerically stable log(1 + exp(x)).
 __device__ __forceinline__ float log1pexp(float x) {

@@ -23,7 +23,14 @@ using namespace o3s;
 
 namespace {
 
-constexpr int kHistWaves = 4;
+// A wave's private image is 64*B*SL floats whatever FP is (SL = LDS stats: classes for
+// CLS, 2 for REG -- the regression image holds w and w*y; the split gain needs only
+// those, and the node's sum of w*y^2 is accumulated in registers by the lanes of
+// feature 0).  At B = 32 that is 16 KB per wave, so 2-wave blocks fit 5 per CU.
+// Each lane gathers U rows (order -> row -> bins/y) per batch and the next batch's
+// gathers are issued before the current batch's LDS updates, so the dependent HBM
+// latency overlaps the read-modify-writes.
+constexpr int kHistWaves = 2;
 constexpr int kHistThreads = kHistWaves * kWave;
 
 // FP: features per row-slot (power of 2, <= 64); RS = 64 / FP row-slots per wave.
@@ -33,10 +40,13 @@ __global__ __launch_bounds__(kHistThreads) void tree_hist_kernel(
     const float* __restrict__ y, const float* __restrict__ w, const int64_t* __restrict__ item_lo,
     const int64_t* __restrict__ item_hi, float* __restrict__ slab, int64_t slab_stride) {
   constexpr int RS = kWave / FP;
-  extern __shared__ __attribute__((aligned(16))) float hist[];   // [wave][rs][B][S][FP] (+pad)
+  constexpr int U = 8;
+  const int SL = CLS ? S : 2;                                     // stats kept in LDS
+  extern __shared__ __attribute__((aligned(16))) float hist[];   // [wave][rs][B][SL][FP] (+pad)
+  __shared__ float y2part[kHistWaves * RS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int rs = lane / FP, f = lane % FP;
-  const int region = B * S * FP + 16;                             // +16: rs-regions on distinct banks
+  const int region = B * SL * FP + 16;                            // +16: rs-regions on distinct banks
   const int per_wave = RS * region;
   float* my = hist + wid * per_wave + rs * region;
   for (int i = threadIdx.x; i < kHistWaves * per_wave; i += kHistThreads) hist[i] = 0.f;
@@ -44,38 +54,63 @@ __global__ __launch_bounds__(kHistThreads) void tree_hist_kernel(
   const int fcol = fg0 + f;
   const bool fok = fcol < F;
   const int64_t lo = item_lo[blockIdx.x], hi = item_hi[blockIdx.x];
-  // rows of the item are dealt round-robin to (wave, row-slot) pairs, 4 rows in flight
-  constexpr int U = 4;
-  const int64_t stride = (int64_t)kHistWaves * RS;
-  for (int64_t p0 = lo + wid * RS + rs; p0 < hi; p0 += stride * U) {
-    int b[U];
-    float yy[U], ww[U];
-    bool ok[U];
+  const int64_t stride = (int64_t)kHistWaves * RS;                // rows dealt round-robin to row-slots
+  float wy2 = 0.f;                                                // REG: sum of w*y^2 (lanes f == 0)
+  // Three-stage software pipeline over batches of U rows per lane: the order[] indices
+  // of batch k+2 and the bins/y/w gathers of batch k+1 are in flight while batch k is
+  // accumulated.  Loads are unconditional (clamped to the item; masked rows contribute
+  // weight 0 at use time), so the compiler emits counted vmcnt waits instead of
+  // draining every load at a branch merge.
+  const int64_t step = stride * U;
+  auto ld_rows = [&](int64_t q0, int32_t (&r)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t p = p0 + u * stride;
-      ok[u] = p < hi;
-      const int64_t pc = ok[u] ? p : lo;
-      const int64_t row = order[pc];
-      b[u] = fok ? bins[row * F + fcol] : 0;
-      yy[u] = y[row];
-      ww[u] = w ? w[row] : 1.f;
+      const int64_t q = q0 + u * stride;
+      r[u] = order[q < hi ? q : hi - 1];
     }
+  };
+  auto ld_data = [&](const int32_t (&r)[U], int (&bo)[U], float (&yo)[U], float (&wo)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (!(ok[u] && fok)) continue;
-      float* cell = my + b[u] * S * FP + f;
+      const int64_t row = r[u];
+      bo[u] = bins[row * F + (fok ? fcol : 0)];
+      yo[u] = y[row];
+      wo[u] = w ? w[row] : 1.f;
+    }
+  };
+  int32_t r1[U], r2[U];
+  int b0[U], b1[U];
+  float y0[U], y1[U], w0[U], w1[U];
+  int64_t p0 = lo + wid * RS + rs;
+  if (p0 < hi) {
+    ld_rows(p0, r1);
+    ld_data(r1, b0, y0, w0);
+    ld_rows(p0 + step, r1);
+  }
+  for (; p0 < hi; p0 += step) {
+    ld_rows(p0 + 2 * step, r2);
+    ld_data(r1, b1, y1, w1);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = fok && (p0 + u * stride < hi);
+      const float wv = ok ? w0[u] : 0.f;
+      float* cell = my + b0[u] * SL * FP + f;
       if (CLS) {
-        cell[(int)yy[u] * FP] += ww[u];
+        cell[(int)y0[u] * FP] += wv;
       } else {
-        cell[0] += ww[u];
-        cell[FP] += ww[u] * yy[u];
-        cell[2 * FP] += ww[u] * yy[u] * yy[u];
+        const float wy = wv * y0[u];
+        cell[0] += wv;
+        cell[FP] += wy;
+        wy2 = fmaf(wy, y0[u], wy2);
       }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) { b0[u] = b1[u]; y0[u] = y1[u]; w0[u] = w1[u]; r1[u] = r2[u]; }
   }
+  if (!CLS && f == 0) y2part[wid * RS + rs] = wy2;
   __syncthreads();
-  // fixed-order block reduction -> slab[item][f][b][s] (features of this group only)
+  // fixed-order block reduction -> slab[item][f][b][s] (features of this group only);
+  // REG stat 2 (w*y^2) is a node total: stored in (feature 0, bin 0), zero elsewhere
   float* out = slab + (int64_t)blockIdx.x * slab_stride;
   const int cells = FP * B * S;
   for (int i = threadIdx.x; i < cells; i += kHistThreads) {
@@ -83,18 +118,115 @@ __global__ __launch_bounds__(kHistThreads) void tree_hist_kernel(
     const int bb = rem / S, ss = rem % S;
     if (fg0 + ff >= F) continue;
     float acc = 0.f;
-    for (int q = 0; q < kHistWaves; ++q)
-      for (int r = 0; r < RS; ++r) acc += hist[q * per_wave + r * region + (bb * S + ss) * FP + ff];
+    if (CLS || ss < 2) {
+      for (int q = 0; q < kHistWaves; ++q)
+        for (int r = 0; r < RS; ++r) acc += hist[q * per_wave + r * region + (bb * SL + ss) * FP + ff];
+    } else if (fg0 + ff == 0 && bb == 0) {
+      for (int q = 0; q < kHistWaves * RS; ++q) acc += y2part[q];
+    }
     out[((int64_t)(fg0 + ff) * B + bb) * S + ss] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// Level partition: every splitting segment of `order` is stably split into the rows
+// going left (bins[row][feat] <= bin) followed by the rows going right.  Work items are
+// the histogram items (contiguous runs inside one segment); pass 1 counts each item's
+// left rows, the engine turns the counts into per-item destinations (tiny scans), pass 2
+// writes each row to its destination.  Ranks inside an item come from wave ballots +
+// a block scan, so the split is stable and deterministic.
+constexpr int kPartThreads = 256;
+constexpr int kPartWaves = kPartThreads / kWave;
+
+__device__ __forceinline__ bool goes_left(const uint8_t* __restrict__ bins, int F, int32_t row, int feat,
+                                          int bin) {
+  return (int)bins[(int64_t)row * F + feat] <= bin;
+}
+
+__global__ __launch_bounds__(kPartThreads) void tree_part_count_kernel(
+    const uint8_t* __restrict__ bins, int F, const int32_t* __restrict__ order, const int64_t* __restrict__ it_lo,
+    const int64_t* __restrict__ it_hi, const int32_t* __restrict__ it_feat, const int32_t* __restrict__ it_bin,
+    int64_t* __restrict__ it_left, uint8_t* __restrict__ flags) {
+  __shared__ int wsum[kPartWaves];
+  const int64_t lo = it_lo[blockIdx.x], hi = it_hi[blockIdx.x];
+  const int feat = it_feat[blockIdx.x], bin = it_bin[blockIdx.x];
+  int cnt = 0;
+  for (int64_t p = lo + threadIdx.x; p < hi; p += kPartThreads) {
+    const bool l = goes_left(bins, F, order[p], feat, bin);     // the one random gather per row
+    flags[p] = l;                                               // pass 2 reads this sequentially
+    cnt += l;
+  }
+  cnt = wave_sum_i(cnt);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) wsum[wid] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int i = 0; i < kPartWaves; ++i) t += wsum[i];
+    it_left[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kPartThreads) void tree_part_scatter_kernel(
+    const uint8_t* __restrict__ bins, int F, const int32_t* __restrict__ order, int32_t* __restrict__ out,
+    const int64_t* __restrict__ it_lo, const int64_t* __restrict__ it_hi, const int32_t* __restrict__ it_feat,
+    const int32_t* __restrict__ it_bin, const int64_t* __restrict__ dst_left, const int64_t* __restrict__ dst_right,
+    const uint8_t* __restrict__ flags) {
+  __shared__ int wl[kPartWaves];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t lo = it_lo[blockIdx.x], hi = it_hi[blockIdx.x];
+  const int feat = it_feat[blockIdx.x], bin = it_bin[blockIdx.x];
+  int64_t nl = dst_left[blockIdx.x], nr = dst_right[blockIdx.x];
+  const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (int64_t base = lo; base < hi; base += kPartThreads) {
+    const int64_t p = base + threadIdx.x;
+    const bool ok = p < hi;
+    const int32_t row = ok ? order[p] : 0;
+    const bool left = ok && flags[p];
+    const uint64_t m = __ballot(left);
+    if (lane == 0) wl[wid] = __popcll(m);
+    __syncthreads();
+    int before = 0, total = 0;
+#pragma unroll
+    for (int i = 0; i < kPartWaves; ++i) {
+      before += i < wid ? wl[i] : 0;
+      total += wl[i];
+    }
+    const int rank_l = before + __popcll(m & below);             // lefts before me in this round
+    const int64_t round_base = p - threadIdx.x;
+    const int valid = (int)((hi - round_base) < kPartThreads ? (hi - round_base) : kPartThreads);
+    if (ok) {
+      if (left) out[nl + rank_l] = row;
+      else out[nr + ((int)threadIdx.x - rank_l)] = row;           // rights before me = idx - lefts before
+    }
+    nl += total;
+    nr += valid - total;
+    __syncthreads();                                              // wl reused next round
   }
 }
 
 }  // namespace
 
+O3S_API int o3s_tree_partition(const uint8_t* bins, int F, const int32_t* order, int32_t* out,
+                               const int64_t* it_lo, const int64_t* it_hi, const int32_t* it_feat,
+                               const int32_t* it_bin, int64_t* it_left, const int64_t* dst_left,
+                               const int64_t* dst_right, uint8_t* flags, int n_items, int pass, hipStream_t st) {
+  if (n_items <= 0) return 0;
+  if (pass == 0)
+    hipLaunchKernelGGL(tree_part_count_kernel, dim3(n_items), dim3(kPartThreads), 0, st, bins, F, order, it_lo,
+                       it_hi, it_feat, it_bin, it_left, flags);
+  else
+    hipLaunchKernelGGL(tree_part_scatter_kernel, dim3(n_items), dim3(kPartThreads), 0, st, bins, F, order, out,
+                       it_lo, it_hi, it_feat, it_bin, dst_left, dst_right, flags);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
 // Shared-memory bytes needed for (F-group width fp, B bins, S stats); 0 if it cannot fit.
-O3S_API int o3s_tree_hist_lds(int fp, int B, int S) {
+O3S_API int o3s_tree_hist_lds(int fp, int B, int S, int cls) {
   const int RS = 64 / fp;
-  const int64_t bytes = (int64_t)kHistWaves * RS * (B * S * fp + 16) * 4;
+  const int SL = cls ? S : 2;
+  const int64_t bytes = (int64_t)kHistWaves * RS * (B * SL * fp + 16) * 4;
   return bytes <= 160 * 1024 ? (int)bytes : 0;
 }
 
@@ -108,7 +240,7 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
   int fp = 1;
   while (fp < F && fp < 64) fp <<= 1;
   if (fp < 4) fp = 4;
-  const int lds = o3s_tree_hist_lds(fp, B, S);
+  const int lds = o3s_tree_hist_lds(fp, B, S, cls);
   if (lds == 0) return -2;
   const int64_t stride = (int64_t)F * B * S;
   for (int fg0 = 0; fg0 < F; fg0 += fp) {

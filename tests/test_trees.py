@@ -93,3 +93,21 @@ def test_gpu_gbt_fit():
     m = GBTClassifier(maxIter=5, maxDepth=5).fit(df)
     auc = BinaryClassificationEvaluator().evaluate(m.transform(df))
     assert auc > 0.8
+
+
+@pytest.mark.gpu
+def test_gpu_partition_matches_torch(gpu):
+    from orange3_spark_amd.ops import trees as T
+    g = torch.Generator().manual_seed(0)
+    n, F = 200_003, 13
+    bins = torch.randint(0, 32, (n, F), generator=g, dtype=torch.uint8)
+    order = torch.randperm(n, generator=g).to(torch.int32)
+    cuts = torch.tensor([0, 5, 70_000, 70_001, 150_000, n])           # includes 1-row and empty-ish segments
+    s_lo, s_hi = cuts[:-1].clone(), cuts[1:].clone()
+    s_feat = torch.randint(0, F, (s_lo.numel(),), generator=g)
+    s_bin = torch.randint(0, 32, (s_lo.numel(),), generator=g)
+    ref_o, ref_n = T.partition_torch(bins, order, s_lo, s_hi, s_feat, s_bin)
+    got_o, got_n = T.partition(bins.to(gpu), order.to(gpu), s_lo.to(gpu), s_hi.to(gpu), s_feat.to(gpu),
+                               s_bin.to(gpu), chunk=4096)
+    assert torch.equal(got_n.cpu(), ref_n)
+    assert torch.equal(got_o.cpu(), ref_o)                             # stable -> identical permutation

@@ -35,13 +35,18 @@ def main():
     rows = df._global_rows()
     TR.fit_gbt(s.comm, bins, splits, y, None, "logistic", 1, 0.1, a.depth, rows=rows)   # warmup
     torch.cuda.synchronize()
+    from orange3_spark_amd.runtime.tracing import TRACER
+    TRACER.reset()
     t1 = time.perf_counter()
     ens = TR.fit_gbt(s.comm, bins, splits, y, None, "logistic", a.trees, 0.1, a.depth, rows=rows)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t1) / a.trees
+    from orange3_spark_amd.runtime.tracing import TRACER
+    phases = {k: round(v["total_s"] / a.trees, 4) for k, v in TRACER.summary().items()} if TRACER.enabled else None
     print(json.dumps({"metric": "GBTClassifier seconds per tree (depth 8, 64 features)", "value": dt,
                       "unit": "s/tree", "rows_per_gpu": a.rows, "n_gpus": s.comm.world_size,
-                      "binning_s": t_bin, "loss": ens.losses, "nodes": [t.numNodes for t in ens.trees]}))
+                      "binning_s": t_bin, "loss": ens.losses, "nodes": [t.numNodes for t in ens.trees],
+                      "phase_s_per_tree": phases}))
 
 
 if __name__ == "__main__":
