@@ -99,11 +99,11 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
     rows = torch.repeat_interleave(torch.arange(n, device=dev), csr.indptr[1:] - csr.indptr[:-1])
     nu = torch.zeros(n, dtype=torch.float32, device=dev).index_add_(0, rows, pos.float())
     lam = (reg * nu).to(torch.float32)
-    rhs = A.pass_(1, csr.indptr, csr.cols, b, Ffull, None)
     nnz = int(csr.cols.numel())
     if exact is None:
         exact = nnz * R * R <= (1 << 26)
     if exact:
+        rhs = A.pass_(1, csr.indptr, csr.cols, b, Ffull, None)
         Fg = Ffull[csr.cols.long()].to(torch.float64)
         outer = Fg[:, :, None] * Fg[:, None, :] * w.to(torch.float64)[:, None, None]
         M = torch.zeros((n, R, R), dtype=torch.float64, device=dev).index_add_(0, rows, outer)
@@ -121,7 +121,11 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
         return out + lam[:, None] * v
 
     x = X0.clone()
-    r = rhs - Amul(x)
+    # first residual: the rhs and A x0 gather the same factor rows -> one fused pass
+    ax, rhs = A.pass_both(csr.indptr, csr.cols, w, Ffull, x, b)
+    if implicit and FtF is not None:
+        ax = ax + x @ FtF
+    r = rhs - (ax + lam[:, None] * x)
     p = r.clone()
     rs = (r * r).sum(1)
     for _ in range(cg_iters):
@@ -135,6 +139,19 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
         p = r + beta[:, None] * p
         rs = rs_new
     return x.clamp_min(0) if nonneg else x
+
+
+def gram(F: torch.Tensor, chunk: int = 1 << 20) -> torch.Tensor:
+    """F^T F (fp64 [R, R]) as chunked fp32 GEMMs (hipBLASLt) accumulated in fp64.
+
+    One fp64 GEMM over millions of rows runs on the fp64 matrix path (~180 ms for
+    6.25M x 128 on MI355X); fp32 tiles of 1M rows keep the long sum in fp64 at ~1 ms."""
+    R = F.shape[1]
+    out = torch.zeros((R, R), dtype=torch.float64, device=F.device)
+    for a in range(0, F.shape[0], chunk):
+        Fc = F[a:a + chunk].float()
+        out += (Fc.T @ Fc).double()
+    return out
 
 
 @dataclass
@@ -175,7 +192,7 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
             Yf = comm.all_gather_v(Y) if comm.world_size > 1 else Y
             YtY = None
             if implicit:
-                YtY = (Y.T.to(torch.float64) @ Y.to(torch.float64)).contiguous()
+                YtY = gram(Y)
                 comm.all_reduce(YtY)
                 YtY = YtY.float()
             X = solve_side(by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact)
@@ -183,7 +200,7 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
             Xf = comm.all_gather_v(X) if comm.world_size > 1 else X
             XtX = None
             if implicit:
-                XtX = (X.T.to(torch.float64) @ X.to(torch.float64)).contiguous()
+                XtX = gram(X)
                 comm.all_reduce(XtX)
                 XtX = XtX.float()
             Y = solve_side(by_item, Xf, Y, reg, implicit, alpha, XtX, cg_iters, nonneg, exact)

@@ -23,24 +23,28 @@ namespace {
 
 constexpr int kAlsWaves = 4;
 
-template <int RV, int MODE>   // RV = dims per lane (R = 64*RV); MODE 0 = MATVEC, 1 = RHS
+// MODE 0 = MATVEC, 1 = RHS, 2 = both in one gather pass (out = matvec, out2 = rhs with
+// coefficients coef2): CG's first residual needs rhs - A x0, and both sum the same rows.
+template <int RV, int MODE>   // RV = dims per lane (R = 64*RV)
 __global__ __launch_bounds__(kAlsWaves * 64) void als_pass_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ coef,
-    int64_t nrows, const float* __restrict__ F, int R, const float* __restrict__ V, float* __restrict__ out) {
+    int64_t nrows, const float* __restrict__ F, int R, const float* __restrict__ V, float* __restrict__ out,
+    const float* __restrict__ coef2, float* __restrict__ out2) {
   const int lane = threadIdx.x & 63;
   const int64_t u = (int64_t)blockIdx.x * kAlsWaves + (threadIdx.x >> 6);
   if (u >= nrows) return;
-  float v[RV], acc[RV];
+  float v[RV], acc[RV], acc2[RV];
 #pragma unroll
   for (int k = 0; k < RV; ++k) {
     const int d = lane + 64 * k;
-    v[k] = (MODE == 0 && d < R) ? V[u * R + d] : 0.f;
+    v[k] = (MODE != 1 && d < R) ? V[u * R + d] : 0.f;
     acc[k] = 0.f;
+    acc2[k] = 0.f;
   }
   const int64_t s0 = indptr[u], s1 = indptr[u + 1];
   constexpr int U = 4;
   for (int64_t j0 = s0; j0 < s1; j0 += U) {
-    float f[U][RV], cj[U];
+    float f[U][RV], cj[U], cj2[U];
 #pragma unroll
     for (int q = 0; q < U; ++q) {
       const int64_t j = j0 + q;
@@ -48,6 +52,7 @@ __global__ __launch_bounds__(kAlsWaves * 64) void als_pass_kernel(
       const int64_t jc = ok ? j : s0;
       const int64_t c = cols[jc];
       cj[q] = ok ? coef[jc] : 0.f;
+      cj2[q] = (MODE == 2 && ok) ? coef2[jc] : 0.f;
 #pragma unroll
       for (int k = 0; k < RV; ++k) {
         const int d = lane + 64 * k;
@@ -57,7 +62,7 @@ __global__ __launch_bounds__(kAlsWaves * 64) void als_pass_kernel(
 #pragma unroll
     for (int q = 0; q < U; ++q) {
       float s = cj[q];
-      if (MODE == 0) {
+      if (MODE != 1) {
         float dot = 0.f;
 #pragma unroll
         for (int k = 0; k < RV; ++k) dot = fmaf(f[q][k], v[k], dot);
@@ -65,19 +70,25 @@ __global__ __launch_bounds__(kAlsWaves * 64) void als_pass_kernel(
       }
 #pragma unroll
       for (int k = 0; k < RV; ++k) acc[k] = fmaf(s, f[q][k], acc[k]);
+      if (MODE == 2) {
+#pragma unroll
+        for (int k = 0; k < RV; ++k) acc2[k] = fmaf(cj2[q], f[q][k], acc2[k]);
+      }
     }
   }
 #pragma unroll
   for (int k = 0; k < RV; ++k) {
     const int d = lane + 64 * k;
     if (d < R) out[u * R + d] = acc[k];
+    if (MODE == 2 && d < R) out2[u * R + d] = acc2[k];
   }
 }
 
 }  // namespace
 
 O3S_API int o3s_als_pass(int mode, const int64_t* indptr, const int32_t* cols, const float* coef, int64_t nrows,
-                         const float* F, int R, const float* V, float* out, hipStream_t st) {
+                         const float* F, int R, const float* V, float* out, const float* coef2, float* out2,
+                         hipStream_t st) {
   if (nrows <= 0) return 0;
   if (R <= 0 || R > 512) return -1;
   const int rv = (R + 63) / 64;
@@ -86,10 +97,13 @@ O3S_API int o3s_als_pass(int mode, const int64_t* indptr, const int32_t* cols, c
   if (rv == RVV) {                                                                                       \
     if (mode == 0)                                                                                       \
       hipLaunchKernelGGL((als_pass_kernel<RVV, 0>), dim3(grid), dim3(kAlsWaves * 64), 0, st, indptr, cols, \
-                         coef, nrows, F, R, V, out);                                                     \
-    else                                                                                                 \
+                         coef, nrows, F, R, V, out, coef2, out2);                                        \
+    else if (mode == 1)                                                                                  \
       hipLaunchKernelGGL((als_pass_kernel<RVV, 1>), dim3(grid), dim3(kAlsWaves * 64), 0, st, indptr, cols, \
-                         coef, nrows, F, R, V, out);                                                     \
+                         coef, nrows, F, R, V, out, coef2, out2);                                        \
+    else                                                                                                 \
+      hipLaunchKernelGGL((als_pass_kernel<RVV, 2>), dim3(grid), dim3(kAlsWaves * 64), 0, st, indptr, cols, \
+                         coef, nrows, F, R, V, out, coef2, out2);                                        \
   }
   O3S_AL(1) O3S_AL(2) O3S_AL(3) O3S_AL(4) O3S_AL(5) O3S_AL(6) O3S_AL(7) O3S_AL(8)
 #undef O3S_AL

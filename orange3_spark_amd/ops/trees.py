@@ -27,7 +27,7 @@ def _items(seg_lo: torch.Tensor, seg_hi: torch.Tensor, chunk: int):
     k = torch.arange(seg_id.numel(), device=dev) - first[seg_id]
     it_lo = (seg_lo[seg_id] + k * chunk).to(torch.int64).contiguous()
     it_hi = torch.minimum(it_lo + chunk, seg_hi[seg_id].to(torch.int64)).contiguous()
-    return it_lo, it_hi, seg_id
+    return it_lo, it_hi, seg_id, first
 
 
 def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi: torch.Tensor,
@@ -42,7 +42,7 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     dev = bins.device
     F = bins.shape[1]
     nseg = s_lo.numel()
-    it_lo, it_hi, it_seg = _items(s_lo, s_hi, chunk)
+    it_lo, it_hi, it_seg, first_item = _items(s_lo, s_hi, chunk)
     n_items = int(it_lo.numel())
     new_order = order.clone()
     if n_items == 0:
@@ -60,9 +60,7 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     nleft = torch.zeros(nseg, dtype=torch.int64, device=dev).index_add_(0, it_seg, it_left)
     cl = torch.cumsum(it_left, 0) - it_left                    # global exclusive prefixes
     cr = torch.cumsum(it_right, 0) - it_right
-    first_item = torch.zeros(nseg, dtype=torch.int64, device=dev)
-    first_item.index_reduce_(0, it_seg, torch.arange(n_items, device=dev), "amin", include_self=False)
-    f = first_item[it_seg]
+    f = first_item[it_seg]                                     # first item of each item's segment
     dst_left = (s_lo[it_seg] + cl - cl[f]).contiguous()
     dst_right = (s_lo[it_seg] + nleft[it_seg] + cr - cr[f]).contiguous()
     N.check(lib.o3s_tree_partition(bins.data_ptr(), F, order.data_ptr(), new_order.data_ptr(), it_lo.data_ptr(),
@@ -114,7 +112,7 @@ def node_hist(bins: torch.Tensor, order: torch.Tensor, y: torch.Tensor, w: torch
     out = torch.zeros((n_nodes, F * B * S), dtype=torch.float32, device=dev)
     if seg_lo.numel() == 0:
         return out.view(n_nodes, F, B, S)
-    it_lo, it_hi, seg_id = _items(seg_lo, seg_hi, chunk)
+    it_lo, it_hi, seg_id, _ = _items(seg_lo, seg_hi, chunk)
     it_node = seg_node[seg_id].to(torch.int64)
     n_items = int(it_lo.numel())
     if n_items == 0:

@@ -86,7 +86,7 @@ def test_als_cold_start_and_save(cpu, tmp_path):
     assert m.transform(test).count() == 1
     m.save(str(tmp_path / "als"))
     m2 = ALSModel.load(str(tmp_path / "als"))
-    assert torch.allclose(m2._U, m._U) and m2.rank == 2
+    assert torch.allclose(m2._U.cpu(), m._U.cpu()) and m2.rank == 2
 
 
 @pytest.mark.gpu
@@ -106,6 +106,10 @@ def test_gpu_als_pass_matches_torch(gpu, R):
         a = A.pass_(mode, indptr.to(gpu), cols.to(gpu), coef.to(gpu), F.to(gpu), V.to(gpu) if mode == 0 else None)
         b = A.pass_torch(mode, indptr, cols, coef, F, V)
         assert torch.allclose(a.cpu(), b, rtol=1e-4, atol=1e-3)
+    coef2 = torch.rand(nnz, generator=g)
+    mv, rhs = A.pass_both(indptr.to(gpu), cols.to(gpu), coef.to(gpu), F.to(gpu), V.to(gpu), coef2.to(gpu))
+    assert torch.allclose(mv.cpu(), A.pass_torch(0, indptr, cols, coef, F, V), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(rhs.cpu(), A.pass_torch(1, indptr, cols, coef2, F, None), rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.gpu
