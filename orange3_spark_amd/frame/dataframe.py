@@ -669,36 +669,11 @@ class GroupedData:
         self.df, self.keys = df, keys
 
     def agg(self, *aggs) -> DataFrame:
+        """Device-side partial aggregation per rank + merge by key (frame/groupby.py)."""
+        from .groupby import aggregate
         if len(aggs) == 1 and isinstance(aggs[0], dict):
             aggs = tuple(getattr(E, fn if fn != "mean" else "avg")(c).alias(f"{fn}({c})") for c, fn in aggs[0].items())
-        df = self.df
-        full = DataFrame(df.session.local_view(), df._gathered())
-        key_cols = [k.eval(full) for k in self.keys]
-        key_lists = [kc.to_pylist() for kc in key_cols]
-        n = len(full)
-        groups: "OrderedDict[tuple, list[int]]" = OrderedDict()
-        for i in range(n):
-            key = tuple(_hashable(kl[i]) for kl in key_lists)
-            groups.setdefault(key, []).append(i)
-        if not self.keys and not groups:
-            groups[()] = []
-        out = OrderedDict()
-        for j, k in enumerate(self.keys):
-            firsts = [key_lists[j][idx[0]] for idx in groups.values()]
-            out[k.name] = C.from_numpy(np.array(firsts, dtype=object) if isinstance(key_cols[j], C.HostColumn)
-                                       else np.array(firsts), "cpu")
-        for a in aggs:
-            vals = a.arg.eval(full) if a.arg is not None else None
-            res = []
-            for idx in groups.values():
-                res.append(_aggregate(a, vals, idx))
-            if a.fn == "count":
-                out[a.name] = C.NumericColumn(torch.tensor(res, dtype=torch.int64))
-            else:
-                arr = np.array([np.nan if r is None else r for r in res], dtype=np.float64)
-                out[a.name] = C.NumericColumn(torch.from_numpy(arr),
-                                              torch.from_numpy(~np.isnan(arr)) if np.isnan(arr).any() and a.fn not in ("avg", "sum") else None)
-        return df._from_full(out)
+        return self.df._from_full(aggregate(self.df, self.keys, list(aggs)))
 
     def count(self) -> DataFrame:
         return self.agg(E.count().alias("count"))
