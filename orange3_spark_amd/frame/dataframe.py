@@ -189,6 +189,9 @@ class DataFrame:
     def select(self, *cols) -> "DataFrame":
         if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
             cols = tuple(cols[0])
+        gens = [c for c in cols if getattr(c, "_generator", None)]
+        if len(gens) > 1:
+            raise ValueError("Only one generator (explode) allowed per select clause")
         out = OrderedDict()
         for c in cols:
             if isinstance(c, str) and c == "*":
@@ -196,7 +199,33 @@ class DataFrame:
                 continue
             name, data = self._resolve(c)
             out[name] = data
+        if gens:
+            return self._explode(out, gens[0])
         return self._new(out)
+
+    def _explode(self, out: "OrderedDict[str, C.Column]", g) -> "DataFrame":
+        """Row expansion for explode/posexplode: one row per array element (rows with
+        empty or null arrays disappear, as in Spark)."""
+        name = g.name
+        arr = out[name]
+        lists = [v if v is not None else [] for v in (arr.values if isinstance(arr, C.HostColumn)
+                                                        else arr.to_pylist())]
+        lens = np.array([len(v) for v in lists], dtype=np.int64)
+        idx = torch.from_numpy(np.repeat(np.arange(len(lists)), lens))
+        flat = [x for v in lists for x in v]
+        res = OrderedDict()
+        for k, c in out.items():
+            if k == name:
+                if g._generator == "posexplode":
+                    res["pos"] = C.NumericColumn(torch.from_numpy(np.concatenate(
+                        [np.arange(n_) for n_ in lens]) if len(lens) else np.zeros(0, dtype=np.int64)).to(self.device),
+                        None, T.IntegerType())
+                res[k] = C.from_numpy(np.array(flat, dtype=object) if flat and isinstance(flat[0], str)
+                                      else np.array(flat), self.device) if flat else C.StringColumn(
+                                          np.array([], dtype=object))
+            else:
+                res[k] = c.take(idx.to(c.data.device) if isinstance(c, C.NumericColumn) else idx)
+        return self._new(res, len(flat))
 
     def selectExpr(self, *exprs) -> "DataFrame":
         from ..sql.parser import parse_expression

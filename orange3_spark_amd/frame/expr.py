@@ -36,7 +36,10 @@ class Expr:
         return f"Column<'{self._name}'>"
 
     def alias(self, name: str) -> "Expr":
-        return Expr(self._fn, name, self.refs)
+        out = Expr(self._fn, name, self.refs)
+        if getattr(self, "_generator", None):
+            out._generator = self._generator
+        return out
 
     name_ = alias
 

@@ -79,6 +79,8 @@ def arrow_to_columns(table, session) -> "OrderedDict[str, C.Column]":
                 np_arr = arr.fill_null(0).to_numpy(zero_copy_only=False)
                 if np_arr.dtype.kind == "u":
                     np_arr = np_arr.astype(np.int64)
+                elif not np_arr.flags.writeable:
+                    np_arr = np_arr.copy()               # arrow buffers are read-only
             col = C.NumericColumn(torch.from_numpy(np.ascontiguousarray(np_arr)).to(dev),
                                   None if mask is None else torch.from_numpy(~mask).to(dev))
             out[name] = col

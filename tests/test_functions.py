@@ -1,0 +1,91 @@
+"""pyspark.sql.functions surface, explode, new aggregates (CPU)."""
+import math
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from orange3_spark_amd import Session, SessionConf
+from orange3_spark_amd.sql import functions as F
+
+
+@pytest.fixture(scope="module")
+def s():
+    return Session(SessionConf().set("o3s.device", "cpu"))
+
+
+@pytest.fixture(scope="module")
+def df(s):
+    return s.createDataFrame(pd.DataFrame({
+        "name": ["  Alice ", "bob", "Carol", None], "x": [1.5, -2.25, 3.0, 4.0], "k": [1, 2, 1, 2],
+        "d": ["2024-01-31", "2024-02-29", "2023-12-25", None], "tags": ["a,b", "c", "", "d,e,f"]}))
+
+
+def test_string_functions(df):
+    r = df.select(F.upper(F.trim("name")).alias("u"), F.length("name").alias("n"),
+                  F.substring("name", 3, 2).alias("sub"), F.concat_ws("-", "name", "k").alias("cw"),
+                  F.regexp_replace("name", "[aeiou]", "_").alias("rr"),
+                  F.regexp_extract("d", r"(\d+)-(\d+)", 2).alias("re")).toPandas()
+    assert r.u.tolist() == ["ALICE", "BOB", "CAROL", None]
+    assert r.n.tolist()[:3] == [8, 3, 5] and (r.n.isna().iloc[3] or r.n.iloc[3] is None)
+    assert r["sub"].tolist()[1:3] == ["b", "ro"]
+    assert r.cw.tolist() == ["  Alice -1", "bob-2", "Carol-1", "2"]
+    assert r.rr.tolist()[1] == "b_b"
+    assert r["re"].tolist()[:3] == ["01", "02", "12"]
+
+
+def test_math_and_null_functions(df):
+    r = df.select(F.round("x", 1).alias("r"), F.bround(F.lit(2.5)).alias("b"), F.floor("x").alias("f"),
+                  F.pow("x", 2).alias("p"), F.greatest("x", "k").alias("g"), F.isnull("name").alias("nn"),
+                  F.signum("x").alias("sg")).toPandas()
+    assert r.r.tolist() == [1.5, -2.3, 3.0, 4.0]            # HALF_UP away from zero
+    assert r.b.tolist()[0] == 2.0                             # HALF_EVEN
+    assert r.f.tolist() == [1.0, -3.0, 3.0, 4.0]
+    assert r.p.tolist()[1] == pytest.approx(5.0625)
+    assert r.g.tolist() == [1.5, 2.0, 3.0, 4.0]
+    assert r.nn.tolist() == [False, False, False, True]
+
+
+def test_dates(df):
+    r = df.select(F.year("d").alias("y"), F.month("d").alias("m"), F.dayofmonth("d").alias("dd"),
+                  F.date_add("d", 1).alias("n"), F.datediff("d", F.lit("2024-01-01")).alias("dd2")).toPandas()
+    assert r.y.tolist()[:3] == [2024, 2024, 2023]
+    assert r.n.tolist()[:2] == ["2024-02-01", "2024-03-01"]
+    assert r.dd2.tolist()[:3] == [30, 59, -7]
+
+
+def test_arrays_and_explode(df):
+    arr = df.select("k", F.split("tags", ",").alias("t"))
+    r = arr.select("k", F.size("t").alias("n"), F.array_contains("t", "c").alias("hasc")).toPandas()
+    assert r.n.tolist() == [2, 1, 1, 3] and r.hasc.tolist() == [False, True, False, False]
+    ex = arr.select("k", F.explode("t").alias("tag")).toPandas()
+    assert ex.tag.tolist() == ["a", "b", "c", "", "d", "e", "f"]
+    assert ex.k.tolist() == [1, 1, 2, 1, 2, 2, 2]
+    pe = arr.select(F.posexplode("t")).toPandas()
+    assert pe["pos"].tolist() == [0, 1, 0, 0, 0, 1, 2]
+
+
+def test_new_aggregates_and_expr(df):
+    g = df.groupBy("k").agg(F.first("name").alias("f"), F.last("x").alias("l"),
+                            F.collect_list("x").alias("cl"), F.sumDistinct("k").alias("sd")).toPandas()
+    g = g.set_index("k")
+    assert g.loc[1, "f"] == "  Alice " and g.loc[2, "l"] == 4.0
+    assert g.loc[1, "cl"] == [1.5, 3.0] and g.loc[2, "sd"] == 2
+    r = df.select(F.expr("x * 2 + k").alias("e")).toPandas()
+    assert r.e.tolist() == [4.0, -2.5, 7.0, 10.0]
+
+
+def test_rand_and_ids_are_deterministic(df):
+    a = df.select(F.rand(7).alias("r"), F.randn(7).alias("z"), F.monotonically_increasing_id().alias("i")).toPandas()
+    b = df.select(F.rand(7).alias("r"), F.randn(7).alias("z")).toPandas()
+    assert a.r.tolist() == b.r.tolist() and all(0 <= v < 1 for v in a.r)
+    assert a.i.tolist() == [0, 1, 2, 3] and all(math.isfinite(v) for v in a.z)
+
+
+def test_udf(df):
+    plus = F.udf(lambda v, k: v * 10 + k, "double")
+    r = df.select(plus("x", "k").alias("u")).toPandas()
+    assert r.u.tolist() == [16.0, -20.5, 31.0, 42.0]
+    up = F.udf(lambda s: s.upper())
+    assert df.select(up("name").alias("n")).toPandas().n.tolist()[1] == "BOB"
+    _ = np
