@@ -5,7 +5,8 @@ tuples, ``Setting``, ``self.send(channel, obj)``, ``info/warning/error``).
 Orange3 and Qt are not installed here, so every widget's logic is written
 against this module and is fully testable headlessly; :mod:`.workflow` wires widgets into
 a signal graph (the canvas) and replays ``.ows`` files.  When Orange *is* importable,
-``HAVE_ORANGE`` is True and the Qt views in ``views.py`` subclass the real OWWidget.
+``HAVE_ORANGE`` is True and :mod:`.views` wraps every headless widget in a generated
+Qt ``OWWidget`` subclass (``<Class>View``) that Orange's widget discovery finds.
 """
 from __future__ import annotations
 

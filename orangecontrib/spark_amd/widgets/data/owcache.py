@@ -17,3 +17,8 @@ class OWCacheDataFrame(Widget):
         if df is not None:
             df = df.cache()
         self.send("DataFrame", df)
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

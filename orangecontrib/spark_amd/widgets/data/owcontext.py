@@ -49,3 +49,8 @@ class OWSessionContext(SharedSession, Widget):
         if self.session is not None:
             self.session.stop()
             self.session = None
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

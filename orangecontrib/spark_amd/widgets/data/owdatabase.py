@@ -57,3 +57,8 @@ class OWDatabase(Widget):
         self.send("Pandas", pdf)
         self.info(f"{len(pdf)} rows")
         return pdf
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

@@ -33,3 +33,8 @@ class OWFillNa(Widget):
         out = self.in_df.fillna(v, sub)
         self.send("DataFrame", out)
         return out
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

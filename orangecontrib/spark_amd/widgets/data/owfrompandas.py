@@ -32,3 +32,8 @@ class OWFromPandas(SharedSession, Widget):
 
 
 _ = (pd, DataFrame, orange_to_pandas, pandas_to_orange)
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

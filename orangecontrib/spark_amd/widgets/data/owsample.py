@@ -31,3 +31,8 @@ class OWSample(Widget):
                                 int(coerce(self.seed)))
         self.send("DataFrame", out)
         return out
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

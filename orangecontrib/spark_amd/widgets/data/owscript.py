@@ -70,3 +70,8 @@ class OWScript(SharedSession, Widget):
         self.out_object = ns.get("out_object")
         self.send("out_object", self.out_object)
         return self.out_object
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

@@ -35,3 +35,8 @@ class OWSQLDataFrame(SharedSession, Widget):
         self.info(f"{len(df.columns)} columns")
         self.send("DataFrame", df)
         return df
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

@@ -41,3 +41,8 @@ class OWCatalogTable(SharedSession, Widget):
         self.send("DataFrame", df)
         self.hide()
         return df
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

@@ -12,3 +12,8 @@ class OWClassification(OWEstimatorBase):
     icon = "../icons/classify.svg"
     module = classification
     box_text = "Classification"
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

@@ -12,3 +12,8 @@ class OWClustering(OWEstimatorBase):
     icon = "../icons/kmeans.svg"
     module = clustering
     box_text = "Clustering"
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

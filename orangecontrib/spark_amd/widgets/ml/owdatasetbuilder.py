@@ -82,3 +82,8 @@ class OWDatasetBuilder(Widget):
             self.available_attrs = []
         self.used_attrs, self.class_attrs, self.meta_attrs = [], [], []
         self.update_domain_role_hints()
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

@@ -45,3 +45,8 @@ class OWEvaluation(OWTransformerBase):
 
     def table(self):
         return [("Metric", "Value")] + [(k, v) for k, v in self.values.items()]
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

@@ -12,3 +12,8 @@ class OWFeature(OWTransformerBase):
     icon = "../icons/feature.svg"
     module = feature
     box_text = "Feature"
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

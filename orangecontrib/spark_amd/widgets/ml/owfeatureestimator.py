@@ -12,3 +12,8 @@ class OWFeatureEstimator(OWEstimatorBase):
     icon = "../icons/feature.svg"
     module = feature
     box_text = "Feature Estimator"
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

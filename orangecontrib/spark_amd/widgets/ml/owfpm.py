@@ -12,3 +12,8 @@ class OWFrequentPatterns(OWEstimatorBase):
     icon = "../icons/feature.svg"
     module = fpm
     box_text = "Frequent Patterns"
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

@@ -39,3 +39,8 @@ class OWModelIO(Widget):
         self.path = path
         self.send("Model", self.model)
         return self.model
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

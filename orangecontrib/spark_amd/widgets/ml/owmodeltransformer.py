@@ -40,3 +40,8 @@ class OWModelTransformer(Widget):
 
 
 _ = Model
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

@@ -44,3 +44,8 @@ class OWPipeline(Widget):
             return None
         self.send("Model", model)
         return model
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

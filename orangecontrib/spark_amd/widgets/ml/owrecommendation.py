@@ -12,3 +12,8 @@ class OWRecommendation(OWEstimatorBase):
     icon = "../icons/recommend.svg"
     module = recommendation
     box_text = "Recommendation"
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

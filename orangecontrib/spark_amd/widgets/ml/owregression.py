@@ -12,3 +12,8 @@ class OWRegression(OWEstimatorBase):
     icon = "../icons/regression.svg"
     module = regression
     box_text = "Regression"
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())

@@ -53,3 +53,8 @@ class OWTuning(Widget):
         self.metrics = getattr(m, "avgMetrics", None) or getattr(m, "validationMetrics", [])
         self.send("Model", m)
         return m
+
+
+from ..views import export_views  # noqa: E402
+
+export_views(globals())
