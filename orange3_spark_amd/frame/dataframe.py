@@ -26,6 +26,7 @@ import torch
 from . import column as C
 from . import expr as E
 from . import types as T
+from .extras import DataFrameExtras
 
 
 class Row(tuple):
@@ -78,7 +79,7 @@ class StorageLevel:
     MEMORY_AND_DISK = "MEMORY_AND_DISK"
 
 
-class DataFrame:
+class DataFrame(DataFrameExtras):
     def __init__(self, session, cols: "OrderedDict[str, C.Column]", nrows: int | None = None):
         self.session = session
         self._cols: OrderedDict = OrderedDict(cols)
@@ -525,34 +526,23 @@ class DataFrame:
             out[k] = c
         return DataFrame(self.session, out, hi - lo)
 
-    def repartition(self, *args) -> "DataFrame":
-        return self._from_full(self._gathered())
-
-    coalesce = repartition
-
     def orderBy(self, *cols, ascending=True) -> "DataFrame":
+        """Distributed sample sort (frame/shuffle.py): range exchange on the leading key,
+        stable local lexicographic sort.  ``col.desc()`` / ``asc_nulls_last()`` etc. honoured;
+        Spark's null order (first when ascending, last when descending) by default."""
+        from .shuffle import sort
         if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
             cols = tuple(cols[0])
-        full = DataFrame(self.session.local_view(), self._gathered())
-        asc = ascending if isinstance(ascending, (list, tuple)) else [ascending] * len(cols)
-        order = np.arange(len(full))
-        for c, a in reversed(list(zip(cols, asc))):
+        asc = list(ascending) if isinstance(ascending, (list, tuple)) else [ascending] * len(cols)
+        exprs, dirs, nulls = [], [], []
+        for c, a in zip(cols, asc):
             e = E.col(c) if isinstance(c, str) else c
-            if getattr(e, "_desc", False):
-                a = False
-            vals = e.eval(full)
-            if isinstance(vals, C.NumericColumn):
-                key = vals.to_numpy()[order]
-                if key.dtype == object:
-                    key = np.array([np.inf if v is None else v for v in key], dtype=np.float64)
-                idx = np.argsort(key if a else -key.astype(np.float64), kind="stable")
-            else:
-                key = vals.to_numpy()[order]
-                idx = np.array(sorted(range(len(key)), key=lambda i: (key[i] is None, key[i] if key[i] is not None else ""),
-                                      reverse=not a), dtype=np.int64)
-            order = order[idx]
-        sorted_full = full._take(torch.from_numpy(order.astype(np.int64)))
-        return self._from_full(sorted_full._cols)
+            a = bool(a) and not getattr(e, "_desc", False)
+            nf = getattr(e, "_nulls_first", None)
+            exprs.append(e)
+            dirs.append(a)
+            nulls.append(a if nf is None else nf)
+        return sort(self, exprs, dirs, nulls)
 
     sort = orderBy
 
@@ -570,18 +560,17 @@ class DataFrame:
         return self.union(other.select(*self.columns))
 
     def distinct(self) -> "DataFrame":
-        full = self._gathered()
-        rows = list(zip(*[c.to_pylist() for c in full.values()])) if full else []
-        seen, keep = set(), []
-        for i, r in enumerate(rows):
-            key = tuple(_hashable(v) for v in r)
-            if key not in seen:
-                seen.add(key)
-                keep.append(i)
-        local = DataFrame(self.session.local_view(), full)._take(torch.tensor(keep, dtype=torch.int64))
-        return self._from_full(local._cols)
+        return self.dropDuplicates()
 
-    dropDuplicates = distinct
+    def dropDuplicates(self, subset=None) -> "DataFrame":
+        """First occurrence (global row order) of each distinct row / ``subset`` key:
+        128-bit row keys hash-exchanged to owner ranks, survivors masked in place."""
+        from .shuffle import keep_mask
+        if isinstance(subset, str):
+            subset = [subset]
+        return self._mask(keep_mask(self, subset, "distinct"))
+
+    drop_duplicates = dropDuplicates
 
     def join(self, other: "DataFrame", on=None, how: str = "inner") -> "DataFrame":
         from .join import join as _join
@@ -690,6 +679,9 @@ class _NaFunctions:
     def drop(self, how="any", thresh=None, subset=None):
         return self.df.dropna(how, thresh, subset)
 
+    def replace(self, to_replace, value=None, subset=None):
+        return self.df.replace(to_replace, value, subset)
+
 
 class GroupedData:
     """groupBy(...).agg(...): per-partition partial aggregates, combined across ranks."""
@@ -727,42 +719,52 @@ class GroupedData:
     def max(self, *cols):
         return self._simple("max", cols)
 
+    def pivot(self, pivot_col, values=None) -> "PivotedData":
+        return PivotedData(self.df, self.keys, E.col(pivot_col) if isinstance(pivot_col, str) else pivot_col, values)
 
-def _aggregate(a: E.Agg, vals, idx):
-    if a.fn == "count":
-        if vals is None:
-            return len(idx)
-        py = vals.to_pylist() if not isinstance(vals, C.HostColumn) else list(vals.values)
-        sel = [py[i] for i in idx if py[i] is not None and not (isinstance(py[i], float) and math.isnan(py[i]))]
-        return len(set(map(_hashable, sel))) if a.distinct else len(sel)
-    if isinstance(vals, C.NumericColumn):
-        d = vals.data.to(torch.float64)[torch.tensor(idx, dtype=torch.int64, device=vals.data.device)] \
-            if idx else vals.data.to(torch.float64)[:0]
-        if vals.valid is not None and idx:
-            d = d[vals.valid[torch.tensor(idx, dtype=torch.int64, device=vals.valid.device)]]
-        d = d[~torch.isnan(d)]
-        if d.numel() == 0:
-            return None
-        if a.fn == "sum":
-            return float(d.sum())
-        if a.fn == "avg":
-            return float(d.mean())
-        if a.fn == "min":
-            return float(d.min())
-        if a.fn == "max":
-            return float(d.max())
-        if a.fn == "stddev":
-            return float(d.std()) if d.numel() > 1 else None
-        if a.fn == "variance":
-            return float(d.var()) if d.numel() > 1 else None
-    py = [vals.values[i] for i in idx if vals.values[i] is not None]
-    if not py:
-        return None
-    if a.fn == "min":
-        return min(py)
-    if a.fn == "max":
-        return max(py)
-    raise TypeError(f"aggregate {a.fn} not supported on {vals.dtype.simpleString()}")
+    def applyInPandas(self, func, schema) -> DataFrame:
+        """``func(pandas.DataFrame of one group) -> pandas.DataFrame``: rows are
+        hash-exchanged by the grouping keys so every group lives on one rank, then each
+        rank runs its groups (Spark's FlatMapGroupsInPandas)."""
+        import pandas as pd
+        from .extras import _frame_from_pandas
+        names = [k.name for k in self.keys]
+        local = self.df.repartition(*names).toPandas_local()
+        parts = [func(g) for _, g in local.groupby(names, sort=False, dropna=False)] if len(local) else []
+        return _frame_from_pandas(self.df, pd.concat(parts, ignore_index=True) if parts else pd.DataFrame(), schema)
 
 
-_ = Iterable
+class PivotedData(GroupedData):
+    """``groupBy(keys).pivot(col[, values]).agg(...)``: one output column per (pivot value,
+    aggregate).  One device aggregation over keys + pivot column, reshaped on the host
+    (the aggregated table is small).  Pivot values default to the sorted distinct values."""
+
+    def __init__(self, df, keys, pivot, values):
+        super().__init__(df, keys)
+        self.pivot_expr, self.values = pivot, values
+
+    def agg(self, *aggs) -> DataFrame:
+        from .groupby import aggregate
+        if len(aggs) == 1 and isinstance(aggs[0], dict):
+            aggs = tuple(getattr(E, fn if fn != "mean" else "avg")(c).alias(f"{fn}({c})") for c, fn in aggs[0].items())
+        local = self.df.session.local_view()
+        keyed = DataFrame(local, aggregate(self.df, self.keys + [self.pivot_expr], list(aggs))).collect()
+        groups = DataFrame(local, aggregate(self.df, self.keys, [E.count().alias("__n")])).collect()
+        nk = len(self.keys)
+        values = self.values
+        if values is None:
+            seen = {_hashable(r[nk]): r[nk] for r in keyed}
+            values = sorted(seen.values(), key=lambda v: (v is None, v if v is not None else 0))
+        table = {(tuple(_hashable(x) for x in r[:nk]), _hashable(r[nk])): r[nk + 1:] for r in keyed}
+        out = OrderedDict()
+        for i, k in enumerate(self.keys):
+            out[k.name] = C.from_numpy(np.array([g[i] for g in groups], dtype=object), "cpu")
+        for v in values:
+            for j, a in enumerate(aggs):
+                name = str(v) if len(aggs) == 1 else f"{v}_{a.name}"
+                col = []
+                for g in groups:
+                    hit = table.get((tuple(_hashable(x) for x in g[:nk]), _hashable(v)))
+                    col.append(None if hit is None else hit[j])
+                out[name] = C.from_numpy(np.array(col, dtype=object), "cpu")
+        return self.df._from_full(out)

@@ -139,13 +139,30 @@ class Expr:
                                                 dtype=torch.bool), None, T.BooleanType())
         return Expr(f, f"({self._name} LIKE '{pattern}')", self.refs)
 
-    def desc(self):
+    def _ordered(self, desc: bool, nulls_first=None):
         e = Expr(self._fn, self._name, self.refs)
-        e._desc = True
+        e._desc = desc
+        if nulls_first is not None:
+            e._nulls_first = nulls_first
         return e
 
+    def desc(self):
+        return self._ordered(True)
+
     def asc(self):
-        return Expr(self._fn, self._name, self.refs)
+        return self._ordered(False)
+
+    def asc_nulls_first(self):
+        return self._ordered(False, True)
+
+    def asc_nulls_last(self):
+        return self._ordered(False, False)
+
+    def desc_nulls_first(self):
+        return self._ordered(True, True)
+
+    def desc_nulls_last(self):
+        return self._ordered(True, False)
 
     def otherwise(self, value):
         if not hasattr(self, "_cases"):

@@ -64,6 +64,24 @@ class Comm:
     def broadcast_object(self, obj: Any, src: int = 0) -> Any:
         raise NotImplementedError
 
+    def all_to_all_object(self, objs: Sequence[Any]) -> list:
+        """``objs[r]`` goes to rank r; returns the objects received, in source-rank order.
+        Pickled into one byte buffer on the comm device -> a single all_to_all_v (the
+        objects are this job's own data, never files)."""
+        if self.world_size == 1:
+            return [objs[0]]
+        import pickle
+        blobs = [pickle.dumps(o, protocol=pickle.HIGHEST_PROTOCOL) for o in objs]
+        flat = torch.frombuffer(bytearray(b"".join(blobs)), dtype=torch.uint8) if any(blobs) \
+            else torch.zeros(0, dtype=torch.uint8)
+        recv, counts = self.all_to_all_v(flat.to(self.device), [len(b) for b in blobs])
+        raw = recv.cpu().numpy().tobytes()
+        out, off = [], 0
+        for c in counts:
+            out.append(pickle.loads(raw[off:off + c]))
+            off += c
+        return out
+
     # -- helpers ----------------------------------------------------------------
     def all_reduce_coalesced(self, tensors: Sequence[torch.Tensor], op: str = "sum") -> list[torch.Tensor]:
         """Pack tensors of one dtype/device into a single buffer -> one collective."""
