@@ -21,6 +21,7 @@ from .param import (HasFeaturesCol, HasFitIntercept, HasLabelCol, HasMaxIter, Ha
                     HasProbabilityCol, HasRawPredictionCol, HasRegParam, HasSeed, HasSolver, HasStepSize,
                     HasThresholds, HasTol, HasWeightCol, TypeConverters, keyword_only, shared)
 from .util import MLReadable, MLWritable, apply_metadata, mat_col, read_data, register, vec_col, write_data
+from . import _summary as S
 
 
 class _FMParams(HasFeaturesCol, HasLabelCol, HasPredictionCol, HasMaxIter, HasStepSize, HasTol, HasSolver,
@@ -147,10 +148,22 @@ class _FMModelBase(Model, _FMParams, MLWritable, MLReadable):
         return m
 
 
-class _Summary:
-    def __init__(self, history, iterations):
-        self.objectiveHistory = list(history)
-        self.totalIterations = int(iterations)
+class FMClassificationTrainingSummary(S.BinaryClassificationSummary, S.TrainingSummaryMixin):
+    """Spark FMClassificationTrainingSummary: binary metrics over the training predictions."""
+
+    def __init__(self, model, df, res):
+        g = model.getOrDefault
+        super().__init__(lambda: model.transform(df), scoreCol=g(model.probabilityCol), labelCol=g(model.labelCol),
+                         predictionCol=g(model.predictionCol))
+        self._init_training(res.history, res.iterations)
+
+
+class FMRegressionTrainingSummary(S.LinearRegressionSummary, S.TrainingSummaryMixin):
+    def __init__(self, model, df, res):
+        g = model.getOrDefault
+        super().__init__(lambda: model.transform(df), labelCol=g(model.labelCol), predictionCol=g(model.predictionCol),
+                         featuresCol=g(model.featuresCol), fitIntercept=g(model.fitIntercept))
+        self._init_training(res.history, res.iterations)
 
 
 class _FMClassifierParams(_FMParams, HasProbabilityCol, HasRawPredictionCol, HasThresholds):
@@ -171,9 +184,9 @@ class FMClassifier(Estimator, _FMClassifierParams, MLWritable, MLReadable):
 
     def _fit(self, df):
         V, w, b, res = _fit_fm(self, df, True)
-        m = FMClassificationModel._from(V, w, b)
-        m.summary = _Summary(res.history, res.iterations)
-        return m._with_parent(self)
+        m = FMClassificationModel._from(V, w, b)._with_parent(self)
+        m.summary = FMClassificationTrainingSummary(m, df, res)
+        return m
 
 
 @register("org.apache.spark.ml.classification.FMClassificationModel")
@@ -204,9 +217,9 @@ class FMRegressor(Estimator, _FMParams, MLWritable, MLReadable):
 
     def _fit(self, df):
         V, w, b, res = _fit_fm(self, df, False)
-        m = FMRegressionModel._from(V, w, b)
-        m.summary = _Summary(res.history, res.iterations)
-        return m._with_parent(self)
+        m = FMRegressionModel._from(V, w, b)._with_parent(self)
+        m.summary = FMRegressionTrainingSummary(m, df, res)
+        return m
 
 
 @register("org.apache.spark.ml.regression.FMRegressionModel")

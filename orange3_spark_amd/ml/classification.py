@@ -24,14 +24,31 @@ from ..runtime.checkpoint import for_estimator
 from .util import MLReadable, MLWritable, apply_metadata, mat_col, read_data, register, vec_col, write_data
 
 
-class _Summary:
-    """Training summary (subset of Spark's LogisticRegressionTrainingSummary)."""
+from . import _summary as S  # noqa: E402
 
-    def __init__(self, history, iterations, seconds=0.0, passes=0):
-        self.objectiveHistory = list(history)
-        self.totalIterations = int(iterations)
-        self.trainingSeconds = float(seconds)
-        self.dataPasses = int(passes)
+
+def _lr_summary(model, df, training, res=None):
+    """Spark (Binary)LogisticRegression(Training)Summary over ``model.transform(df)``."""
+    g = model.getOrDefault
+    kw = dict(labelCol=g(model.labelCol), predictionCol=g(model.predictionCol),
+              probabilityCol=g(model.probabilityCol), featuresCol=g(model.featuresCol),
+              weightCol=g(model.weightCol) if model.isDefined(model.weightCol) and g(model.weightCol) else None)
+    pred = (lambda: model.transform(df))
+    binary = not model._multinomial
+    if training:
+        cls = S.BinaryLogisticRegressionTrainingSummary if binary else S.LogisticRegressionTrainingSummary
+        return cls(pred, res.history, res.iterations, getattr(res, "seconds", 0.0), getattr(res, "passes", 0), **kw)
+    return (S.BinaryLogisticRegressionSummary if binary else S.LogisticRegressionSummary)(pred, **kw)
+
+
+def _svc_summary(model, df, res=None):
+    g = model.getOrDefault
+    kw = dict(labelCol=g(model.labelCol), predictionCol=g(model.predictionCol),
+              weightCol=g(model.weightCol) if model.isDefined(model.weightCol) and g(model.weightCol) else None)
+    pred = (lambda: model.transform(df))
+    if res is None:
+        return S.LinearSVCSummary(pred, **kw)
+    return S.LinearSVCTrainingSummary(pred, res.history, res.iterations, res.seconds, res.passes, **kw)
 
 
 # ====================================================================== Logistic
@@ -94,18 +111,18 @@ class LogisticRegression(Estimator, _LogisticRegressionParams, MLWritable, MLRea
             X = U.dense_features(df, g(self.featuresCol))
             B, b, r = GLM.fit_multinomial(comm, X, y, sw, max(k, 2), g(self.regParam), g(self.elasticNetParam),
                                           g(self.fitIntercept), g(self.standardization), g(self.maxIter), g(self.tol))
-            m = LogisticRegressionModel._from(B, b, True, max(k, 2))
-            m.summary = _Summary(r.history, r.iterations)
-            return m._with_parent(self)
+            m = LogisticRegressionModel._from(B, b, True, max(k, 2))._with_parent(self)
+            m.summary = _lr_summary(m, df, True, r)
+            return m
         data = GLM.GlmData(comm, feat, y, sw)
         solver = g(self.solver).lower()
         res = GLM.fit_glm(data, "logistic", g(self.regParam), g(self.elasticNetParam), g(self.fitIntercept),
                           g(self.standardization), g(self.maxIter), g(self.tol),
                           "sgd" if solver == "sgd" else "auto", g(self.stepSize), g(self.miniBatchFraction),
                           ckpt=for_estimator(self, df))
-        m = LogisticRegressionModel._from(res.coef[None, :], np.array([res.intercept]), False, 2)
-        m.summary = _Summary(res.history, res.iterations, res.seconds, res.passes)
-        return m._with_parent(self)
+        m = LogisticRegressionModel._from(res.coef[None, :], np.array([res.intercept]), False, 2)._with_parent(self)
+        m.summary = _lr_summary(m, df, True, res)
+        return m
 
     def trainer(self, df):
         """Device-resident SGD stepper for this estimator's params (used by bench.py)."""
@@ -197,9 +214,8 @@ class LogisticRegressionModel(U.ProbabilisticClassifierMixin, Model, _LogisticRe
         return torch.softmax(raw, dim=1)
 
     def evaluate(self, df):
-        from .evaluation import BinaryClassificationEvaluator
-        out = self.transform(df)
-        return {"areaUnderROC": BinaryClassificationEvaluator(labelCol=self.getOrDefault(self.labelCol)).evaluate(out)}
+        """Evaluate on ``df``: a (Binary)LogisticRegressionSummary (metrics computed lazily)."""
+        return _lr_summary(self, df, False)
 
     # persistence (Spark >= 2.1 LogisticRegressionModel data schema)
     def _save_data(self, path):
@@ -268,9 +284,9 @@ class LinearSVC(Estimator, _LinearSVCParams, MLWritable, MLReadable):
         res = GLM.fit_glm(data, "hinge", g(self.regParam), 0.0, g(self.fitIntercept), g(self.standardization),
                           g(self.maxIter), g(self.tol), "sgd" if g(self.solver) == "sgd" else "auto",
                           g(self.stepSize), init_intercept=0.0, ckpt=for_estimator(self, df))
-        m = LinearSVCModel._from(res.coef, res.intercept)
-        m.summary = _Summary(res.history, res.iterations, res.seconds, res.passes)
-        return m._with_parent(self)
+        m = LinearSVCModel._from(res.coef, res.intercept)._with_parent(self)
+        m.summary = _svc_summary(m, df, res)
+        return m
 
 
 @register("org.apache.spark.ml.classification.LinearSVCModel")
@@ -287,6 +303,10 @@ class LinearSVCModel(U.ProbabilisticClassifierMixin, Model, _LinearSVCParams, ML
         m = cls()
         m._w, m._b = np.asarray(w, dtype=np.float64), float(b)
         return m
+
+    def evaluate(self, df):
+        """Evaluate on ``df``: a LinearSVCSummary (binary metrics on rawPrediction)."""
+        return _svc_summary(self, df)
 
     @property
     def coefficients(self):

@@ -27,71 +27,77 @@ HIST_BINS = 1 << 20
 
 
 def _num(df, name, dtype=torch.float64):
+    """Column tensor; ``dtype=None`` keeps the stored dtype (the kernels convert in registers)."""
     c = df.column_data(name)
-    if isinstance(c, C.NumericColumn):
-        return c.data.to(dtype)
-    if isinstance(c, C.VectorColumn):
-        return c.data.to(dtype)
+    if isinstance(c, (C.NumericColumn, C.VectorColumn)):
+        return c.data if dtype is None else c.data.to(dtype)
     raise TypeError(f"column {name} is not numeric")
 
 
-def _weights(df, ev, n, device):
+def _weights(df, ev, n, device, required=True):
+    """Weight column, or unit weights (``None`` when not ``required``: kernels skip the read)."""
     if ev.isDefined(ev.weightCol) and ev.getOrDefault(ev.weightCol):
         return _num(df, ev.getOrDefault(ev.weightCol)).to(device)
-    return torch.ones(n, dtype=torch.float64, device=device)
+    return torch.ones(n, dtype=torch.float64, device=device) if required else None
 
 
-def _binary_curve_metrics(score: np.ndarray, label: np.ndarray, w: np.ndarray):
-    """Spark BinaryClassificationMetrics (no down-sampling): ROC AUC and PR AUC."""
+def _exact_curve(score: np.ndarray, label: np.ndarray, w: np.ndarray):
+    """(thresholds desc, cum TP, cum FP, P, N) at every distinct score (Spark
+    BinaryClassificationMetrics without down-sampling)."""
     order = np.argsort(-score, kind="stable")
     s, l, w = score[order], label[order], w[order]
     pos_w = w * (l > 0.5)
     neg_w = w * (l <= 0.5)
-    # group by distinct threshold
     bounds = np.nonzero(np.diff(s))[0]
-    ends = np.concatenate([bounds, [len(s) - 1]]) if len(s) else np.array([], dtype=int)
+    ends = np.concatenate([bounds, [len(s) - 1]]).astype(np.int64) if len(s) else np.array([], dtype=np.int64)
     tp = np.cumsum(pos_w)[ends] if len(s) else np.array([])
     fp = np.cumsum(neg_w)[ends] if len(s) else np.array([])
-    P, N = pos_w.sum(), neg_w.sum()
-    tpr = np.concatenate([[0.0], tp / P if P > 0 else np.zeros_like(tp), [1.0]])
-    fpr = np.concatenate([[0.0], fp / N if N > 0 else np.zeros_like(fp), [1.0]])
-    roc = float(np.trapezoid(tpr, fpr)) if hasattr(np, "trapezoid") else float(np.trapz(tpr, fpr))
-    recall = tp / P if P > 0 else np.zeros_like(tp)
-    precision = np.where(tp + fp > 0, tp / np.maximum(tp + fp, 1e-300), 1.0)
-    if len(precision):
-        rec = np.concatenate([[0.0], recall])
-        prec = np.concatenate([[precision[0]], precision])
-        pr = float(np.sum((rec[1:] - rec[:-1]) * (prec[1:] + prec[:-1]) / 2))
+    return s[ends] if len(s) else np.array([]), tp, fp, pos_w.sum(), neg_w.sum()
+
+
+def _hist_curve(comm, score: torch.Tensor, label: torch.Tensor, w):
+    """Large-data path: 2^20-bin score histograms per class (one fused pass, ops/evaluation.py
+    score_hist kernel on the GPU), one all-reduce (16 MB fp64).  Thresholds are bin edges."""
+    from ..ops import evaluation as EV
+    if score.numel():
+        mn, mx = torch.aminmax(score)
+        lohi = torch.tensor([float(mn), -float(mx)], dtype=torch.float64, device=comm.device)
     else:
-        pr = 0.0
-    return roc, pr
-
-
-def _hist_curve_metrics(comm, score: torch.Tensor, label: torch.Tensor, w: torch.Tensor):
-    """Large-data path: 2^20-bin score histograms per class, one all-reduce (16 MB fp64)."""
-    lo = comm.all_gather_object(float(score.min().item()) if score.numel() else math.inf)
-    hi = comm.all_gather_object(float(score.max().item()) if score.numel() else -math.inf)
-    lo, hi = min(lo), max(hi)
+        lohi = torch.tensor([math.inf, math.inf], dtype=torch.float64, device=comm.device)
+    comm.all_reduce(lohi, "min")
+    lo, hi = float(lohi[0]), -float(lohi[1])
     span = max(hi - lo, 1e-12)
-    b = ((score - lo) / span * (HIST_BINS - 1)).clamp(0, HIST_BINS - 1).long()
-    pos = label > 0.5
-    hp = torch.zeros(HIST_BINS, dtype=torch.float64, device=score.device).index_add_(0, b[pos], w[pos])
-    hn = torch.zeros(HIST_BINS, dtype=torch.float64, device=score.device).index_add_(0, b[~pos], w[~pos])
-    h = torch.stack([hp, hn])
+    h = EV.score_hist(score, label, lo, span, HIST_BINS, w)
     comm.all_reduce(h)
     hp, hn = h[0].flip(0).cpu().numpy(), h[1].flip(0).cpu().numpy()
     keep = (hp + hn) > 0
-    tp, fp = np.cumsum(hp)[keep], np.cumsum(hn)[keep]
-    P, N = hp.sum(), hn.sum()
-    tpr = np.concatenate([[0.0], tp / max(P, 1e-300), [1.0]])
-    fpr = np.concatenate([[0.0], fp / max(N, 1e-300), [1.0]])
+    edges = lo + (np.arange(HIST_BINS, dtype=np.float64)[::-1]) * (span / (HIST_BINS - 1))
+    return edges[keep], np.cumsum(hp)[keep], np.cumsum(hn)[keep], hp.sum(), hn.sum()
+
+
+def binary_curve(comm, score: torch.Tensor, label: torch.Tensor, w):
+    """Global (thresholds, tp, fp, P, N): exact when the row count is small, else histogram."""
+    n = comm.sum_scalar(int(score.shape[0]))
+    if n <= EXACT_AUC_MAX_ROWS:
+        if w is None:
+            w = torch.ones(score.shape[0], dtype=torch.float64, device=score.device)
+        s, y, ww = (comm.all_gather_v(t.to(torch.float64).contiguous()) for t in (score, label, w))
+        return _exact_curve(s.cpu().numpy(), y.cpu().numpy(), ww.cpu().numpy())
+    return _hist_curve(comm, score, label, w)
+
+
+def curve_areas(tp, fp, P, N):
+    """(areaUnderROC, areaUnderPR) by the trapezoid rule over the curve points."""
+    tpr = np.concatenate([[0.0], tp / P if P > 0 else np.zeros_like(tp), [1.0]])
+    fpr = np.concatenate([[0.0], fp / N if N > 0 else np.zeros_like(fp), [1.0]])
     roc = float(np.sum((fpr[1:] - fpr[:-1]) * (tpr[1:] + tpr[:-1]) / 2))
-    recall = tp / max(P, 1e-300)
+    if not len(tp):
+        return roc, 0.0
+    recall = tp / P if P > 0 else np.zeros_like(tp)
     precision = np.where(tp + fp > 0, tp / np.maximum(tp + fp, 1e-300), 1.0)
     rec = np.concatenate([[0.0], recall])
-    prec = np.concatenate([[precision[0] if len(precision) else 1.0], precision])
-    pr = float(np.sum((rec[1:] - rec[:-1]) * (prec[1:] + prec[:-1]) / 2))
-    return roc, pr
+    prec = np.concatenate([[precision[0]], precision])
+    return roc, float(np.sum((rec[1:] - rec[:-1]) * (prec[1:] + prec[:-1]) / 2))
 
 
 @add_accessors
@@ -119,25 +125,20 @@ class BinaryClassificationEvaluator(Evaluator, HasLabelCol, HasRawPredictionCol,
         return self._set(**self._input_kwargs)
 
     def _scores(self, df):
+        """(score view, label, weight or None) in their stored dtypes -- no copies."""
         raw = df.column_data(self.getOrDefault(self.rawPredictionCol))
         if isinstance(raw, C.VectorColumn):
             s = raw.data[:, 1] if raw.data.shape[1] > 1 else raw.data[:, 0]
         else:
             s = raw.data
-        s = s.to(torch.float64)
-        y = _num(df, self.getOrDefault(self.labelCol)).to(s.device)
-        w = _weights(df, self, s.shape[0], s.device)
+        y = _num(df, self.getOrDefault(self.labelCol), None).to(s.device)
+        w = _weights(df, self, s.shape[0], s.device, required=False)
         return s, y, w
 
     def _evaluate(self, df):
         s, y, w = self._scores(df)
-        comm = df.comm
-        n = comm.sum_scalar(int(s.shape[0]))
-        if n <= EXACT_AUC_MAX_ROWS:
-            s, y, w = (comm.all_gather_v(t) for t in (s, y, w))
-            roc, pr = _binary_curve_metrics(s.cpu().numpy(), y.cpu().numpy(), w.cpu().numpy())
-        else:
-            roc, pr = _hist_curve_metrics(comm, s, y, w)
+        _, tp, fp, P, N = binary_curve(df.comm, s, y, w)
+        roc, pr = curve_areas(tp, fp, P, N)
         return roc if self.getOrDefault(self.metricName) == "areaUnderROC" else pr
 
     def isLargerBetter(self):
@@ -181,19 +182,19 @@ class MulticlassClassificationEvaluator(Evaluator, HasLabelCol, HasPredictionCol
         g = self.getOrDefault
         comm = df.comm
         metric = g(self.metricName)
-        y = _num(df, g(self.labelCol))
-        w = _weights(df, self, y.shape[0], y.device)
+        y = _num(df, g(self.labelCol), None)
         if metric == "logLoss":
+            w = _weights(df, self, y.shape[0], y.device)
             prob = df.column_data(g(self.probabilityCol)).data.to(torch.float64)
             p = prob.gather(1, y.long()[:, None]).squeeze(1).clamp(g(self.eps), 1 - g(self.eps))
             t = torch.stack([(-torch.log(p) * w).sum(), w.sum()])
             comm.all_reduce(t)
             return float(t[0] / t[1])
-        pred = _num(df, g(self.predictionCol)).to(y.device)
+        from ..ops import evaluation as EV
+        pred = _num(df, g(self.predictionCol), None).to(y.device)
         k = int(comm.max_scalar(float(max(y.max().item() if y.numel() else 0, pred.max().item() if pred.numel() else 0)))) + 1
         k = max(k, int(g(self.metricLabel)) + 1)
-        idx = y.long() * k + pred.long()
-        cm = torch.zeros(k * k, dtype=torch.float64, device=y.device).index_add_(0, idx, w)
+        cm = EV.confusion(y, pred, k, _weights(df, self, y.shape[0], y.device, required=False)).reshape(-1)
         comm.all_reduce(cm)
         cm = cm.reshape(k, k).cpu().numpy()       # rows = label, cols = prediction
         return _multiclass_metric(cm, metric, int(g(self.metricLabel)), g(self.beta))
@@ -272,12 +273,10 @@ class RegressionEvaluator(Evaluator, HasLabelCol, HasPredictionCol, HasWeightCol
 
     def _evaluate(self, df):
         g = self.getOrDefault
-        y = _num(df, g(self.labelCol))
-        p = _num(df, g(self.predictionCol)).to(y.device)
-        w = _weights(df, self, y.shape[0], y.device)
-        e = p - y
-        st = torch.stack([w.sum(), (w * e * e).sum(), (w * e.abs()).sum(), (w * y).sum(), (w * y * y).sum(),
-                          (w * p).sum(), (w * p * p).sum()])
+        from ..ops import evaluation as EV
+        y = _num(df, g(self.labelCol), None)
+        p = _num(df, g(self.predictionCol), None).to(y.device)
+        st = EV.regression_stats(y, p, _weights(df, self, y.shape[0], y.device, required=False))
         df.comm.all_reduce(st)
         W, se, ae, sy, syy, sp, spp = st.tolist()
         mse = se / W

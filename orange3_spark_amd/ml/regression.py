@@ -23,9 +23,19 @@ from ..runtime.checkpoint import for_estimator
 from .util import MLReadable, MLWritable, apply_metadata, read_data, register, vec_col, write_data
 
 
-class _Summary:
-    def __init__(self, **kw):
-        self.__dict__.update(kw)
+from . import _summary as S  # noqa: E402
+
+
+def _linreg_summary(model, df, res_history=None, iterations=0):
+    g = model.getOrDefault
+    kw = dict(labelCol=g(model.labelCol), predictionCol=g(model.predictionCol), featuresCol=g(model.featuresCol),
+              weightCol=g(model.weightCol) if model.isDefined(model.weightCol) and g(model.weightCol) else None,
+              coefficients=model._w, intercept=model._b, fitIntercept=g(model.fitIntercept),
+              regParam=g(model.regParam))
+    pred = (lambda: model.transform(df))
+    if res_history is None:
+        return S.LinearRegressionSummary(pred, **kw)
+    return S.LinearRegressionTrainingSummary(pred, res_history, iterations, **kw)
 
 
 class _LinearRegressionParams(HasFeaturesCol, HasLabelCol, HasPredictionCol, HasMaxIter, HasRegParam,
@@ -69,15 +79,15 @@ class LinearRegression(Estimator, _LinearRegressionParams, MLWritable, MLReadabl
         if solver == "normal" or (solver == "auto" and alpha == 0.0 and feat.size <= 4096):
             coef, b, hist = _normal_equations(comm, U.dense_features(df, g(self.featuresCol)), y, w, g(self.regParam),
                                               g(self.fitIntercept), g(self.standardization))
-            m = LinearRegressionModel._from(coef, b)
-            m.summary = _Summary(objectiveHistory=hist, totalIterations=0)
-            return m._with_parent(self)
+            m = LinearRegressionModel._from(coef, b)._with_parent(self)
+            m.summary = _linreg_summary(m, df, hist, 0)
+            return m
         data = GLM.GlmData(comm, feat, y, w)
         res = GLM.fit_glm(data, "squared", g(self.regParam), alpha, g(self.fitIntercept), g(self.standardization),
                           g(self.maxIter), g(self.tol), ckpt=for_estimator(self, df))
-        m = LinearRegressionModel._from(res.coef, res.intercept)
-        m.summary = _Summary(objectiveHistory=res.history, totalIterations=res.iterations)
-        return m._with_parent(self)
+        m = LinearRegressionModel._from(res.coef, res.intercept)._with_parent(self)
+        m.summary = _linreg_summary(m, df, res.history, res.iterations)
+        return m
 
 
 def _normal_equations(comm, X, y, w, reg, fit_intercept, standardization):
@@ -147,13 +157,8 @@ class LinearRegressionModel(U.PredictionModelMixin, Model, _LinearRegressionPara
         return X.to(torch.float64)[:, : len(self._w)] @ torch.from_numpy(self._w).to(X.device) + self._b
 
     def evaluate(self, df):
-        from .evaluation import RegressionEvaluator
-        out = self.transform(df)
-        ev = RegressionEvaluator(labelCol=self.getOrDefault(self.labelCol))
-        return _Summary(rootMeanSquaredError=ev.evaluate(out, {ev.metricName: "rmse"}),
-                        meanSquaredError=ev.evaluate(out, {ev.metricName: "mse"}),
-                        r2=ev.evaluate(out, {ev.metricName: "r2"}),
-                        meanAbsoluteError=ev.evaluate(out, {ev.metricName: "mae"}), predictions=out)
+        """Evaluate on ``df``: a LinearRegressionSummary (metrics computed lazily)."""
+        return _linreg_summary(self, df)
 
     def _save_data(self, path):
         import pyarrow as pa

@@ -170,4 +170,4 @@ def test_frame_ops_gpu_match_cpu(s):
         elif k == "quant":
             assert np.allclose(a[k], b[k], rtol=1e-12), k
         else:
-            assert a[k] == b[k], k
+            assert repr(a[k]) == repr(b[k]), k            # NaN-aware
