@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import logging
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -62,6 +63,19 @@ class GlmData:
         self.chunk = chunk_rows
         self.ws = G.GlmWorkspace(self.device, self.ld) if self.kernel else None
         self.passes = 0
+        # Resident rows stream HBM (memory bound) while lineage rows are regenerated
+        # in-kernel (VALU bound).  The two run concurrently on two HIP streams (lineage
+        # at one block per CU).  Measured on MI355X (profiles/glm_overlap.json): resident
+        # 41.2 ms + lineage 24.8 ms alone, 63.8 ms overlapped vs 67.2 ms back to back --
+        # the resident kernel's own VALU work (bf16 unpack + 2 FMA per element) competes
+        # for issue slots, so the overlap only hides ~5%.
+        self.overlap = None
+        if self.kernel and self.lineage and self.X.shape[0] and os.environ.get("O3S_GLM_OVERLAP", "1") == "1":
+            cus = N.num_cus(self.device)
+            res_grid = int(os.environ.get("O3S_GLM_GRID_RES", str(cus * 8)))
+            lin_grid = int(os.environ.get("O3S_GLM_GRID_LIN", str(cus)))
+            self.ws = G.GlmWorkspace(self.device, self.ld, grid=res_grid)
+            self.overlap = (torch.cuda.Stream(self.device), G.GlmWorkspace(self.device, self.ld, grid=lin_grid))
 
     # ---------------------------------------------------------------- moments
     def moments(self):
@@ -109,6 +123,8 @@ class GlmData:
         device operand (coefficients + intercept).
         """
         ws = self.ws
+        if self.overlap is not None:
+            return self._pass_overlapped(coef_eff, intercept, loss)
         filled = False
         if self.X.shape[0]:
             G.glm_grad(self.X, self.y, self.sw, coef_eff, intercept, loss, ws)
@@ -120,6 +136,21 @@ class GlmData:
             filled = True
         if not filled:
             ws.out.zero_()
+        self.passes += 1
+        return ws.out
+
+    def _pass_overlapped(self, coef_eff, intercept, loss):
+        side, ws_l = self.overlap
+        ws = self.ws
+        main = torch.cuda.current_stream(self.device)
+        cf = G._coef_buf(coef_eff, ws.dpad, self.device, intercept=intercept)   # operand ready on main
+        side.wait_stream(main)
+        spec, r0, nl = self.lineage
+        with torch.cuda.stream(side):
+            G.glm_grad_synth(nl, self.ld, spec.d, spec.seed, r0, spec.wtrue, spec.btrue, cf, None, loss, ws_l)
+        G.glm_grad(self.X, self.y, self.sw, cf, None, loss, ws)
+        main.wait_stream(side)
+        ws.out += ws_l.out
         self.passes += 1
         return ws.out
 
