@@ -187,9 +187,20 @@ class DataFrame(DataFrameExtras):
         return self.comm.all_gather_object(int(self._n))
 
     # ------------------------------------------------------------------ projection
+    def _with_windows(self, exprs):
+        """Frame with the hidden window columns ``exprs`` need (sql/window.py), or None."""
+        from ..sql.window import apply, window_refs
+        keys = [k for k in window_refs(exprs) if k not in self._cols]
+        return apply(self, keys) if keys else None
+
     def select(self, *cols) -> "DataFrame":
         if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
             cols = tuple(cols[0])
+        win = self._with_windows([c for c in cols if isinstance(c, E.Expr)])
+        if win is not None:
+            return win.select(*[c if not (isinstance(c, str) and c == "*") else E.col(k)
+                                for c in cols for k in ([c] if not (isinstance(c, str) and c == "*")
+                                                        else list(self.columns))])
         gens = [c for c in cols if getattr(c, "_generator", None)]
         if len(gens) > 1:
             raise ValueError("Only one generator (explode) allowed per select clause")
@@ -233,6 +244,11 @@ class DataFrame(DataFrameExtras):
         return self.select(*[parse_expression(e) for e in exprs])
 
     def withColumn(self, name: str, e) -> "DataFrame":
+        if isinstance(e, E.Expr):
+            win = self._with_windows([e])
+            if win is not None:
+                res = win.withColumn(name, e)
+                return res.select(*[k for k in res.columns if not k.startswith("__win:")])
         data = e.eval(self) if isinstance(e, E.Expr) else E.lit(e).eval(self)
         out = OrderedDict(self._cols)
         out[name] = data

@@ -94,7 +94,16 @@ class Expr:
         def f(df):
             c = self.eval(df)
             return C.NumericColumn(-c.data, c.valid, c.dtype)
-        return Expr(f, f"(- {self._name})", self.refs)
+        out = Expr(f, f"(- {self._name})", self.refs)
+        if isinstance(getattr(self, "_literal", None), (int, float)):
+            out._literal = -self._literal
+        return out
+
+    def eval_literal(self):
+        """Python value of a literal expression (SQL function arguments such as ntile(4))."""
+        if not hasattr(self, "_literal"):
+            raise SyntaxError(f"expected a literal, found {self._name}")
+        return self._literal
 
     def __bool__(self):
         raise ValueError("Cannot convert column into bool: use '&' for 'and', '|' for 'or', '~' for 'not'")
@@ -288,7 +297,9 @@ def lit(value: Any) -> Expr:
     name = repr(value) if isinstance(value, str) else str(value)
     if value is None:
         name = "NULL"
-    return Expr(f, name)
+    e = Expr(f, name)
+    e._literal = value
+    return e
 
 
 def col(name: str) -> Expr:
@@ -400,6 +411,11 @@ class Agg:
 
     def alias(self, name):
         return Agg(self.fn, self.arg, name, self.distinct)
+
+    def over(self, window):
+        """Aggregate over a window frame (``sum("x").over(Window.partitionBy(...))``)."""
+        from ..sql.window import WindowExpr
+        return WindowExpr(self, window, f"{self._name} OVER (...)")
 
 
 def _agg(fn):

@@ -80,11 +80,18 @@ def run_select(session, s: Select) -> DataFrame:
             else:
                 sel.append(it.expr.alias(it.alias) if it.alias else it.expr)
         order_exprs = s.order_by
+        from .window import window_refs
+        if order_exprs and window_refs([e for e in sel if isinstance(e, E.Expr)]):
+            # ORDER BY applies after the window functions (which re-partition rows)
+            df = df.select(*sel)
+            df = df.orderBy(*[e for e, _ in order_exprs], ascending=[a for _, a in order_exprs])
+            sel, order_exprs = None, []
         if order_exprs:
             # order by may reference columns not selected: sort first
             df = df.orderBy(*[e for e, _ in order_exprs], ascending=[a for _, a in order_exprs])
             order_exprs = []
-        df = df.select(*sel)
+        if sel is not None:
+            df = df.select(*sel)
         if s.distinct:
             df = df.distinct()
     if s.order_by and has_agg:

@@ -423,5 +423,9 @@ def udf(f=None, returnType=None):
     return wrap
 
 
+# window functions (sql/window.py)
+from .window import (Window, cume_dist, dense_rank, lag, lead, nth_value, ntile, percent_rank,  # noqa: E402,F401
+                     rank, row_number)
+
 __all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations", "hashlib", "math", "re", "np",
                                                                      "torch", "C", "E", "T")]

@@ -405,8 +405,84 @@ class Parser:
             return E.col(name)
         raise SyntaxError(f"unexpected token {t.val!r}")
 
+    def word(self, *words) -> bool:
+        """Case-insensitive match of non-reserved words (OVER, PARTITION, ROWS, ...)."""
+        for k, w in enumerate(words):
+            t = self.peek(k)
+            if not (t.kind in ("id", "kw") and t.val.lower() == w):
+                return False
+        self.i += len(words)
+        return True
+
     def func_call(self, name):
+        f = self._func_call(name)
+        if self.word("over"):
+            return self.window_spec(f)
+        return f
+
+    def _frame_bound(self):
+        from .window import currentRow, unboundedFollowing, unboundedPreceding
+        if self.word("unbounded", "preceding"):
+            return unboundedPreceding
+        if self.word("unbounded", "following"):
+            return unboundedFollowing
+        if self.word("current", "row"):
+            return currentRow
+        n = int(float(self.expect("num").val))
+        if self.word("preceding"):
+            return -n
+        if self.word("following"):
+            return n
+        raise SyntaxError("expected PRECEDING or FOLLOWING")
+
+    def window_spec(self, f):
+        """``<function> OVER ([PARTITION BY e, ...] [ORDER BY e [ASC|DESC], ...]
+        [ROWS|RANGE BETWEEN <bound> AND <bound>])``."""
+        from .window import WindowExpr, WindowFunction, WindowSpec
+        self.expect("op", "(")
+        spec = WindowSpec()
+        if self.word("partition", "by"):
+            parts = [self.or_expr()]
+            while self.accept("op", ","):
+                parts.append(self.or_expr())
+            spec = spec.partitionBy(*parts)
+        if self.kw("order", "by"):
+            items = [self.order_item()]
+            while self.accept("op", ","):
+                items.append(self.order_item())
+            spec = spec.orderBy(*[e if a else e.desc() for e, a in items])
+        for kind in ("rows", "range"):
+            if self.word(kind):
+                self.kw("between")
+                lo = self._frame_bound()
+                self.kw("and")
+                hi = self._frame_bound()
+                spec = spec.rowsBetween(lo, hi) if kind == "rows" else spec.rangeBetween(lo, hi)
+        self.expect("op", ")")
+        if isinstance(f, AggCall):
+            f = E.Agg(f.fn, f.arg, f.text, f.distinct)
+        if not isinstance(f, (E.Agg, WindowFunction)):
+            raise SyntaxError("OVER applies to aggregate or window functions")
+        return WindowExpr(f, spec, f"{f.name} OVER (...)")
+
+    def _func_call(self, name):
+        from . import window as W
         fn = name.lower()
+        if fn in ("row_number", "rank", "dense_rank", "percent_rank", "cume_dist"):
+            self.expect("op", ")")
+            return getattr(W, fn)()
+        if fn in ("ntile", "lag", "lead", "first_value", "last_value"):
+            args = [self.or_expr()]
+            while self.accept("op", ","):
+                args.append(self.or_expr())
+            self.expect("op", ")")
+            if fn == "ntile":
+                return W.ntile(int(args[0].eval_literal()))
+            if fn in ("first_value", "last_value"):
+                return E.Agg("first" if fn == "first_value" else "last", args[0], f"{fn}({args[0].name})")
+            off = int(args[1].eval_literal()) if len(args) > 1 else 1
+            default = args[2].eval_literal() if len(args) > 2 else None
+            return (W.lag if fn == "lag" else W.lead)(args[0], off, default)
         if fn in ("count", "sum", "avg", "mean", "min", "max", "stddev", "stddev_samp", "variance", "var_samp"):
             distinct = bool(self.kw("distinct"))
             if self.accept("op", "*"):

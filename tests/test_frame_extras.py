@@ -50,6 +50,12 @@ def _frame_ops(s):
     r["crosstab"] = [tuple(map(str, x)) for x in df.crosstab("k", "b").collect()]
     r["apply"] = sorted(tuple(x) for x in df.groupBy("k").applyInPandas(
         lambda g: pd.DataFrame({"k": [g.k.iloc[0]], "n": [len(g)]}), "k long, n long").collect())
+    from orange3_spark_amd.sql import Window
+    w = Window.partitionBy("k").orderBy("c")
+    r["window"] = sorted((int(x.k), round(x.c, 12), int(x.rn), float(x.run)) for x in df.select(
+        "k", "c", F.row_number().over(w).alias("rn"), F.sum("c").over(w).alias("run")).collect())
+    r["window_global"] = [int(x.rn) for x in df.select(
+        F.rank().over(Window.orderBy("a")).alias("rn")).collect()]
     return r
 
 
@@ -156,6 +162,9 @@ def test_frame_ops_world2_match_world1(tmp_path):
     for k in a:
         if isinstance(a[k], float):                    # partial sums combine in a different order
             assert a[k] == pytest.approx(b[k], rel=1e-12), k
+        elif k == "window":
+            assert [t[:3] for t in a[k]] == [t[:3] for t in b[k]]
+            assert np.allclose([t[3] for t in a[k]], [t[3] for t in b[k]], rtol=1e-12)
         else:
             assert a[k] == b[k], k
 

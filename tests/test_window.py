@@ -1,0 +1,109 @@
+"""Window functions (DataFrame API and SQL OVER) against pandas oracles."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from orange3_spark_amd import Session, SessionConf
+from orange3_spark_amd.sql import Window
+from orange3_spark_amd.sql import functions as F
+
+
+@pytest.fixture(scope="module")
+def s():
+    return Session(SessionConf().set("o3s.device", "cpu"))
+
+
+def _pdf(n=300, seed=0):
+    rng = np.random.default_rng(seed)
+    return pd.DataFrame({"g": rng.choice(["a", "b", "c"], n), "v": rng.integers(0, 15, n).astype(float),
+                         "id": np.arange(n)})
+
+
+def _window_frame(df):
+    w = Window.partitionBy("g").orderBy("v", "id")
+    wt = Window.partitionBy("g").orderBy("v")                    # ties -> RANGE frame peers
+    return df.select(
+        "g", "v", "id",
+        F.row_number().over(w).alias("rn"), F.rank().over(wt).alias("rk"), F.dense_rank().over(wt).alias("dr"),
+        F.percent_rank().over(wt).alias("pr"), F.cume_dist().over(wt).alias("cd"), F.ntile(4).over(w).alias("nt"),
+        F.lag("v", 2).over(w).alias("lag2"), F.lead("v", 1, -1.0).over(w).alias("lead1"),
+        F.sum("v").over(wt).alias("run_range"), F.sum("v").over(w.rowsBetween(-2, 0)).alias("sum3"),
+        F.max("v").over(w.rowsBetween(-3, 1)).alias("mx"), F.min("v").over(w.rowsBetween(Window.unboundedPreceding,
+                                                                                         Window.currentRow)).alias("cmin"),
+        F.avg("v").over(Window.partitionBy("g")).alias("gavg"), F.count("v").over(w).alias("cnt"))
+
+
+def test_window_functions_match_pandas(s):
+    p = _pdf()
+    r = _window_frame(s.createDataFrame(p)).toPandas().sort_values("id").reset_index(drop=True)
+    q = p.sort_values(["g", "v", "id"])
+    grp = q.groupby("g")
+    q = q.assign(rn=grp.cumcount() + 1,
+                 rk=grp.v.rank(method="min").astype(int), dr=grp.v.rank(method="dense").astype(int),
+                 lag2=grp.v.shift(2), lead1=grp.v.shift(-1).fillna(-1.0),
+                 sum3=grp.v.rolling(3, min_periods=1).sum().reset_index(level=0, drop=True),
+                 mx=grp.v.apply(lambda x: x[::-1].rolling(2, min_periods=1).max()[::-1]).reset_index(level=0, drop=True),
+                 cmin=grp.v.cummin(), gavg=grp.v.transform("mean"), cnt=grp.cumcount() + 1)
+    n = grp.v.transform("size")
+    q["pr"] = (q.rk - 1) / (n - 1)
+    q["cd"] = grp.v.rank(method="max") / n
+    q["run_range"] = _range_sum(q)
+    q["nt"] = _ntile(q, 4)
+    q = q.sort_values("id").reset_index(drop=True)
+    for c in ("rn", "rk", "dr", "nt", "cnt"):
+        assert r[c].astype(int).tolist() == q[c].astype(int).tolist(), c
+    for c in ("pr", "cd", "lead1", "sum3", "cmin", "gavg", "run_range"):
+        assert np.allclose(r[c].astype(float), q[c].astype(float)), c
+    lag = r["lag2"].astype(float)
+    assert np.allclose(lag.fillna(-99), q["lag2"].fillna(-99))
+    # max over ROWS BETWEEN 3 PRECEDING AND 1 FOLLOWING
+    exp_mx = []
+    for _, d in p.sort_values(["g", "v", "id"]).groupby("g"):
+        vals = d.v.values
+        for i in range(len(vals)):
+            exp_mx.append((d.id.values[i], vals[max(0, i - 3): i + 2].max()))
+    exp_mx = dict(exp_mx)
+    assert np.allclose(r.mx.values, [exp_mx[i] for i in r.id.values])
+
+
+def _range_sum(q):
+    out = []
+    for _, d in q.groupby("g", sort=False):
+        tot = d.groupby("v").v.sum().cumsum()
+        out.append(pd.Series(tot.reindex(d.v).values, index=d.index))
+    return pd.concat(out).reindex(q.index)
+
+
+def _ntile(q, k):
+    out = []
+    for _, d in q.groupby("g", sort=False):
+        n = len(d)
+        base, extra = divmod(n, k)
+        tiles = []
+        for t in range(k):
+            tiles += [t + 1] * (base + (1 if t < extra else 0))
+        out.append(pd.Series(tiles, index=d.index))
+    return pd.concat(out).reindex(q.index)
+
+
+def test_sql_over_clause(s):
+    p = _pdf(60, seed=3)
+    s.createDataFrame(p).createOrReplaceTempView("wt")
+    r = s.sql("SELECT id, g, ROW_NUMBER() OVER (PARTITION BY g ORDER BY v DESC, id) AS rn, "
+              "SUM(v) OVER (PARTITION BY g) AS tot, LAG(v, 1, 0) OVER (PARTITION BY g ORDER BY id) AS prev, "
+              "AVG(v) OVER (ORDER BY id ROWS BETWEEN 2 PRECEDING AND CURRENT ROW) AS ma FROM wt ORDER BY id").toPandas()
+    assert r.id.tolist() == list(range(60))
+    q = p.sort_values(["g", "v", "id"], ascending=[True, False, True])
+    q["rn"] = q.groupby("g").cumcount() + 1
+    q = q.sort_values("id")
+    assert r.rn.tolist() == q.rn.tolist()
+    assert np.allclose(r.tot, p.groupby("g").v.transform("sum"))
+    assert np.allclose(r.prev.astype(float), p.groupby("g").v.shift(1).fillna(0))
+    assert np.allclose(r.ma, p.v.rolling(3, min_periods=1).mean())
+
+
+def test_window_with_column_and_global_order(s):
+    df = s.createDataFrame(pd.DataFrame({"x": [5.0, 1.0, 3.0, 3.0]}))
+    out = df.withColumn("r", F.dense_rank().over(Window.orderBy(F.col("x").desc()))).toPandas()
+    assert out.x.tolist() == [5.0, 3.0, 3.0, 1.0] and out.r.tolist() == [1, 2, 2, 3]
+    assert not any(c.startswith("__win") for c in out.columns)
