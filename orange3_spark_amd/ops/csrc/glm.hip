@@ -344,6 +344,245 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Mixed pass: resident rows (HBM stream, memory bound) and lineage rows (regenerated
+// in-kernel, VALU bound) in ONE launch.  Two back-to-back or two-stream launches leave
+// one resource idle (the first grid fills every CU slot, so the second kernel only
+// starts as the first drains: profiles/glm_overlap.json, 63.8 ms vs 41 + 25 ms alone).
+// Here every wave walks one interleaved sequence of S = Tr + Tl row tiles in which
+// lineage tiles are spread evenly (Bresenham: tile s is lineage iff
+// floor((s+1) Tl / S) > floor(s Tl / S)), so at any moment each CU holds a mix of
+// load-bound and ALU-bound waves and both roles finish together.  Both roles use the
+// same lane->column mapping (the lineage one), so they share w / acc registers.
+template <int LOSS>
+__device__ __forceinline__ void loss_terms(float m, float yv, float wv, float& r, float& l) {
+  if (LOSS == LOSS_LOGISTIC) {
+    const float e = __expf(-fabsf(m));
+    const float inv = __builtin_amdgcn_rcpf(1.0f + e);
+    const float p = m >= 0.f ? inv : e * inv;
+    r = (p - yv) * wv;
+    l = wv * (fmaxf(m, 0.f) + __logf(1.0f + e) - yv * m);
+  } else if (LOSS == LOSS_HINGE) {
+    const float s = 2.f * yv - 1.f;
+    const float mg = 1.f - s * m;
+    r = mg > 0.f ? -s * wv : 0.f;
+    l = mg > 0.f ? wv * mg : 0.f;
+  } else {
+    const float e = m - yv;
+    r = e * wv;
+    l = 0.5f * wv * e * e;
+  }
+}
+
+template <int LPR, int CPL, int UNROLL, int LOSS, int SRC>
+__device__ __forceinline__ void mixed_tile(
+    int64_t base, int64_t n, const uint16_t* __restrict__ X, int64_t ld, int nch,
+    const float* __restrict__ y, const float* __restrict__ sw, uint32_t seed, int64_t row0,
+    const float (&w)[CPL][8], const float (&wt)[CPL][8], float wshift, float wtshift,
+    float btrue, float intercept, int g, int c, int ubase, bool rep, float (&acc)[CPL][8],
+    float& rs, float& acc_r, float& acc_loss, float& acc_w) {
+  constexpr int G = kWave / LPR;
+  using RR = RowReduce<LPR, UNROLL>;
+  constexpr int NF = RR::NF;
+  short8 xv[UNROLL][CPL];
+  float xf[UNROLL][CPL][8];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    const int64_t row = base + u * G + g;
+    const bool ok = row < n;
+    const int64_t rowc = ok ? row : n - 1;
+    if (SRC == 0) {
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int ch = c + k * LPR;
+        const int chc = ch < nch ? ch : nch - 1;
+        short8 v = __builtin_nontemporal_load(reinterpret_cast<const short8*>(X + rowc * ld + 8 * chc));
+        xv[u][k] = (ok && ch < nch) ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    } else {
+      const uint32_t rk = row_key(seed, row0 + row);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int ch = c + k * LPR;
+        const uint32_t h0 = synth_word(rk, 2 * ch), h1 = synth_word(rk, 2 * ch + 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          xf[u][k][j] = synth_byte(h0, j);
+          xf[u][k][4 + j] = synth_byte(h1, j);
+        }
+      }
+    }
+  }
+  float yy[NF], ww[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int64_t row = base + (ubase + j) * G + g;
+    const bool ok = row < n;
+    const int64_t rowc = ok ? row : n - 1;
+    if (SRC == 0) {
+      const float yv = y[rowc];
+      const float wv = sw ? sw[rowc] : 1.f;
+      yy[j] = ok ? yv : 0.f;
+      ww[j] = ok ? wv : 0.f;
+    } else {
+      ww[j] = ok ? 1.f : 0.f;
+    }
+  }
+  float dot[UNROLL], dtrue[UNROLL];
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    float d = 0.f, dt = 0.f;
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      float x[8];
+      if (SRC == 0) unpack8(xv[u][k], x);
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = xf[u][k][j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        d = fmaf(x[j], w[k][j], d);
+        if (SRC == 1) dt = fmaf(x[j], wt[k][j], dt);
+      }
+    }
+    dot[u] = SRC == 1 ? fmaf(d, kSynthScale, wshift) : d;
+    dtrue[u] = fmaf(dt, kSynthScale, wtshift);
+  }
+  RR::run(dot, c);
+  if (SRC == 1) {
+    RR::run(dtrue, c);
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int64_t row = base + (ubase + j) * G + g;
+      yy[j] = synth_label(row_key(seed, row0 + row), dtrue[j] + btrue);
+    }
+  }
+  float res[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    float r, l;
+    loss_terms<LOSS>(dot[j] + intercept, yy[j], ww[j], r, l);
+    res[j] = r;
+    if (rep) { acc_r += r; acc_loss += l; acc_w += ww[j]; }
+  }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      if (SRC == 0) asm volatile("" : "+v"(xv[u][k]));
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(xf[u][k][j]));
+      }
+    }
+#pragma unroll
+  for (int u = 0; u < UNROLL; ++u) {
+    float r = __shfl(res[u % NF], g * LPR + RR::owner(u), kWave);
+    if (SRC == 1) { rs += r; r *= kSynthScale; }
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      float x[8];
+      if (SRC == 0) unpack8(xv[u][k], x);
+      else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = xf[u][k][j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[k][j] = fmaf(r, x[j], acc[k][j]);
+    }
+  }
+}
+
+template <int LPR, int CPL, int UNROLL, int LOSS>
+__global__ __launch_bounds__(kBlock) void glm_grad_mixed_kernel(
+    const uint16_t* __restrict__ X, int64_t ld, int64_t n_res, const float* __restrict__ y,
+    const float* __restrict__ sw, const float* __restrict__ coef, const float* __restrict__ bptr,
+    uint32_t seed, int64_t row0, int64_t n_lin, const float* __restrict__ wtrue, float btrue,
+    float* __restrict__ partial, int pstride) {
+  constexpr int G = kWave / LPR;
+  constexpr int RT = G * UNROLL;
+  constexpr int DP = LPR * CPL * 8;
+  using RR = RowReduce<LPR, UNROLL>;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  const int g = lane / LPR, c = lane % LPR;
+  const int nch = (int)(ld / 8);
+  const int ubase = RR::base(c);
+  const bool rep = RR::representative(c);
+  const float intercept = *bptr;
+
+  float w[CPL][8], wt[CPL][8], acc[CPL][8];
+  float wshift = 0.f, wtshift = 0.f, rs = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = 8 * (c + k * LPR) + j;
+      w[k][j] = col < ld ? coef[col] : 0.f;
+      wt[k][j] = col < ld ? wtrue[col] : 0.f;
+      wshift += w[k][j];
+      wtshift += wt[k][j];
+      acc[k][j] = 0.f;
+    }
+  wshift *= kSynthShift;
+  wtshift *= kSynthShift;
+  float acc_r = 0.f, acc_loss = 0.f, acc_w = 0.f;
+
+  const int64_t Tr = (n_res + RT - 1) / RT, Tl = (n_lin + RT - 1) / RT, S = Tr + Tl;
+  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
+  if (gw < S) {
+    // lineage tiles before unit s: L = floor(s Tl / S), rem = s Tl mod S (s Tl < 2^62)
+    int64_t L = gw * Tl / S, rem = gw * Tl - L * S;
+    const int64_t q0 = nw * Tl / S, r0 = nw * Tl - q0 * S;
+    for (int64_t s = gw; s < S; s += nw) {
+      if (rem + Tl >= S)
+        mixed_tile<LPR, CPL, UNROLL, LOSS, 1>(L * RT, n_lin, X, ld, nch, y, sw, seed, row0, w, wt, wshift,
+                                              wtshift, btrue, intercept, g, c, ubase, rep, acc, rs, acc_r,
+                                              acc_loss, acc_w);
+      else
+        mixed_tile<LPR, CPL, UNROLL, LOSS, 0>((s - L) * RT, n_res, X, ld, nch, y, sw, seed, row0, w, wt,
+                                              wshift, wtshift, btrue, intercept, g, c, ubase, rep, acc, rs,
+                                              acc_r, acc_loss, acc_w);
+      rem += r0;
+      L += q0;
+      if (rem >= S) { rem -= S; ++L; }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = fmaf(rs, kSynthShift, acc[k][j]);
+#pragma unroll
+      for (int off = LPR; off < kWave; off <<= 1) v += __shfl_xor(v, off, kWave);
+      acc[k][j] = v;
+    }
+  acc_r = wave_sum(acc_r);
+  acc_loss = wave_sum(acc_loss);
+  acc_w = wave_sum(acc_w);
+  __shared__ float red[kWavesPerBlock][DP + 4];
+  if (lane < LPR) {
+#pragma unroll
+    for (int k = 0; k < CPL; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wid][8 * (c + k * LPR) + j] = acc[k][j];
+  }
+  if (lane == 0) {
+    red[wid][DP] = acc_r;
+    red[wid][DP + 1] = acc_loss;
+    red[wid][DP + 2] = acc_w;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < DP + 3; i += kBlock) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < kWavesPerBlock; ++q) s += red[q][i];
+    partial[(int64_t)blockIdx.x * pstride + i] = s;
+  }
+}
+
 // Materialise synthetic rows [row0, row0+n) into X (bf16) and labels y.
 template <int LPR, int CPL>
 __global__ __launch_bounds__(kBlock) void synth_glm_kernel(
