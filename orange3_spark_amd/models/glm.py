@@ -64,13 +64,22 @@ class GlmData:
         self.ws = G.GlmWorkspace(self.device, self.ld) if self.kernel else None
         self.passes = 0
         # Resident rows stream HBM (memory bound) while lineage rows are regenerated
-        # in-kernel (VALU bound).  The two run concurrently on two HIP streams (lineage
-        # at one block per CU).  Measured on MI355X (profiles/glm_overlap.json): resident
-        # 41.2 ms + lineage 24.8 ms alone, 63.8 ms overlapped vs 67.2 ms back to back --
-        # the resident kernel's own VALU work (bf16 unpack + 2 FMA per element) competes
-        # for issue slots, so the overlap only hides ~5%.
+        # in-kernel (VALU bound).  Two kernels on two HIP streams barely overlap (the
+        # first grid fills every CU slot; profiles/glm_overlap.json: 63.8 ms vs 67.2 ms
+        # back to back at 1B x 256 on one GPU), so by default (O3S_GLM_MIXED=1) ONE
+        # launch interleaves resident and lineage tiles inside every wave
+        # (ops.glm.glm_grad_mixed): 46-47 ms for the same pass
+        # (profiles/glm_mixed_sweep.json).  The grid is 32 blocks per CU: the dispatcher
+        # then balances CUs that stream at different speeds (a persistent one-wave-set
+        # grid was 8-10 % slower).
         self.overlap = None
-        if self.kernel and self.lineage and self.X.shape[0] and os.environ.get("O3S_GLM_OVERLAP", "1") == "1":
+        self.mixed = (self.kernel and self.lineage is not None and self.X.shape[0] > 0
+                      and os.environ.get("O3S_GLM_MIXED", "1") == "1")
+        if self.mixed:
+            cus = N.num_cus(self.device)
+            self.ws = G.GlmWorkspace(self.device, self.ld,
+                                     grid=int(os.environ.get("O3S_GLM_GRID_MIX", str(cus * 32))))
+        elif self.kernel and self.lineage and self.X.shape[0] and os.environ.get("O3S_GLM_OVERLAP", "1") == "1":
             cus = N.num_cus(self.device)
             res_grid = int(os.environ.get("O3S_GLM_GRID_RES", str(cus * 8)))
             lin_grid = int(os.environ.get("O3S_GLM_GRID_LIN", str(cus)))
@@ -123,6 +132,12 @@ class GlmData:
         device operand (coefficients + intercept).
         """
         ws = self.ws
+        if self.mixed:
+            spec, r0, nl = self.lineage
+            G.glm_grad_mixed(self.X, self.y, self.sw, nl, spec.d, spec.seed, r0, coef_eff, intercept,
+                             loss, ws)
+            self.passes += 1
+            return ws.out
         if self.overlap is not None:
             return self._pass_overlapped(coef_eff, intercept, loss)
         filled = False

@@ -21,6 +21,7 @@ constexpr int kWave = 64;
 
 typedef short short8 __attribute__((ext_vector_type(8)));
 typedef float float4_ __attribute__((ext_vector_type(4)));
+typedef float float2_ __attribute__((ext_vector_type(2)));
 
 // --- bf16 <-> f32 -----------------------------------------------------------
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) {

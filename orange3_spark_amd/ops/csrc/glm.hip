@@ -35,25 +35,51 @@ enum { LOSS_LOGISTIC = 0, LOSS_HINGE = 1, LOSS_SQUARED = 2 };
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
-// Synthetic features: hash word i = fmix32(rk + i * golden) of row key rk supplies the
-// four features 4i..4i+3, one per byte b: x = (2b - 255) / 256, i.e. 256 symmetric
-// levels in (-1, 1) (mean 0, var ~1/3), every one EXACT in bf16 (<= 8 significant
-// bits).  Exactness lets the lineage pass skip the bf16 round trip: it decodes a byte
-// with one v_cvt_f32_ubyteN and folds the affine map into the weights (see
-// glm_grad_kernel), two hashes per 16-B chunk instead of four.
-__device__ __forceinline__ uint32_t synth_word(uint32_t rk, int i) {
-  return fmix32(rk + (uint32_t)i * 0x9E3779B9u);
+// Synthetic features: word i = mix24(fk + i * 0x9E3779) of the row's feature key fk
+// supplies the four features 4i..4i+3, one per byte b: x = (2b - 255) / 256, i.e. 256
+// symmetric levels in (-1, 1) (mean 0, var ~1/3), every one EXACT in bf16 (<= 8
+// significant bits).  Exactness lets the lineage pass skip the bf16 round trip: it
+// decodes a byte with one v_cvt_f32_ubyteN and folds the affine map into the weights
+// (see glm_grad_kernel), two hashes per 16-B chunk.
+//
+// mix24 is a bijective 32-bit mixer built from full-rate VALU ops only: two
+// v_mad_u32_u24 steps h <- (h mod 2^24) * C + h (a bijection for even C: the low 24 bits
+// are multiplied by the odd C + 1, the top byte is recovered from the carry) between
+// xorshifts -- 5 issue cycles per word, vs 13 for murmur's fmix32 whose two
+// v_mul_lo_u32 are quarter rate.  On byte-uniformity (chi^2), cross-column correlation
+// and word-uniqueness tests it matches fmix32 (see ops/glm.py::_mix24, the torch twin).
+__host__ __device__ __forceinline__ uint32_t umad24(uint32_t a, uint32_t c, uint32_t add) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul24(a, c) + add;
+#else
+  return (a & 0xFFFFFFu) * c + add;
+#endif
+}
+__host__ __device__ __forceinline__ uint32_t mix24(uint32_t h) {
+  h ^= h >> 16;
+  h = umad24(h, 0xED5AD4u, h);
+  h ^= h >> 15;
+  return umad24(h, 0x2C1B3Cu, h);
+}
+// Feature key of global row `row` (labels use the murmur row_key of common.h).
+__device__ __forceinline__ uint32_t feat_key(uint32_t seed, int64_t row) {
+  const uint32_t lo = (uint32_t)(row & 0xffffffffll);
+  const uint32_t hi = (uint32_t)((uint64_t)row >> 32);
+  return mix24(mix24(lo + seed * 0x9E3779B1u) ^ umad24(hi, 0x7FEB35u, 0x165667u));
+}
+__device__ __forceinline__ uint32_t synth_word(uint32_t fk, int i) {
+  return mix24(umad24((uint32_t)i, 0x9E3779u, fk));
 }
 __device__ __forceinline__ float synth_byte(uint32_t h, int q) {
   return (float)((h >> (8 * q)) & 0xffu);     // -> v_cvt_f32_ubyte{q}
 }
 constexpr float kSynthScale = 1.0f / 128.0f, kSynthShift = -255.0f / 256.0f;
 // One 16-B chunk (8 features) of synthetic row `rk` at chunk index ch, as bf16.
-__device__ __forceinline__ short8 synth_chunk(uint32_t rk, int ch) {
+__device__ __forceinline__ short8 synth_chunk(uint32_t fk, int ch) {
   short8 v;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    const uint32_t h = synth_word(rk, 2 * ch + p);
+    const uint32_t h = synth_word(fk, 2 * ch + p);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       v[4 * p + q] = (short)f32_to_bf16(fmaf(synth_byte(h, q), kSynthScale, kSynthShift));
@@ -181,7 +207,7 @@ __global__ __launch_bounds__(kBlock) void glm_grad_kernel(
       const int64_t row = base + u * G + g;
       const bool ok = row < n;
       const int64_t rowc = ok ? row : n - 1;
-      const uint32_t rk = SRC == 1 ? row_key(seed, row0 + row) : 0u;
+      const uint32_t rk = SRC == 1 ? feat_key(seed, row0 + row) : 0u;
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int ch = c + k * LPR;
@@ -374,16 +400,21 @@ __device__ __forceinline__ void loss_terms(float m, float yv, float wv, float& r
   }
 }
 
+// One tile of RT rows.  SRC 0: rows of X (bf16 in HBM); SRC 1: rows regenerated from
+// their lineage (raw bytes b, x = b*kSynthScale + kSynthShift, the affine map folded into
+// the dot product and a per-lane residual sum rs).  Labels / weights of both roles come
+// from the materialised label column (y, sw already offset to the role's first row).
 template <int LPR, int CPL, int UNROLL, int LOSS, int SRC>
 __device__ __forceinline__ void mixed_tile(
     int64_t base, int64_t n, const uint16_t* __restrict__ X, int64_t ld, int nch,
     const float* __restrict__ y, const float* __restrict__ sw, uint32_t seed, int64_t row0,
-    const float (&w)[CPL][8], const float (&wt)[CPL][8], float wshift, float wtshift,
-    float btrue, float intercept, int g, int c, int ubase, bool rep, float (&acc)[CPL][8],
-    float& rs, float& acc_r, float& acc_loss, float& acc_w) {
+    const float (&w)[CPL][8], float wshift, float intercept, int g, int c,
+    float (&acc)[CPL][8], float& rs, float& acc_r, float& acc_loss, float& acc_w) {
   constexpr int G = kWave / LPR;
   using RR = RowReduce<LPR, UNROLL>;
   constexpr int NF = RR::NF;
+  const int ubase = RR::base(c);
+  const bool rep = RR::representative(c);
   short8 xv[UNROLL][CPL];
   float xf[UNROLL][CPL][8];
 #pragma unroll
@@ -400,7 +431,7 @@ __device__ __forceinline__ void mixed_tile(
         xv[u][k] = (ok && ch < nch) ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
       }
     } else {
-      const uint32_t rk = row_key(seed, row0 + row);
+      const uint32_t rk = feat_key(seed, row0 + row);
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
         const int ch = c + k * LPR;
@@ -419,19 +450,16 @@ __device__ __forceinline__ void mixed_tile(
     const int64_t row = base + (ubase + j) * G + g;
     const bool ok = row < n;
     const int64_t rowc = ok ? row : n - 1;
-    if (SRC == 0) {
-      const float yv = y[rowc];
-      const float wv = sw ? sw[rowc] : 1.f;
-      yy[j] = ok ? yv : 0.f;
-      ww[j] = ok ? wv : 0.f;
-    } else {
-      ww[j] = ok ? 1.f : 0.f;
-    }
+    const float yv = y[rowc];
+    const float wv = sw ? sw[rowc] : 1.f;
+    yy[j] = ok ? yv : 0.f;
+    ww[j] = ok ? wv : 0.f;
   }
-  float dot[UNROLL], dtrue[UNROLL];
+  float dot[UNROLL];
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
-    float d = 0.f, dt = 0.f;
+    // two interleaved partial sums -> v_pk_fma_f32 (one issue per two features)
+    float2_ d2 = {0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
       float x[8];
@@ -441,23 +469,15 @@ __device__ __forceinline__ void mixed_tile(
         for (int j = 0; j < 8; ++j) x[j] = xf[u][k][j];
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        d = fmaf(x[j], w[k][j], d);
-        if (SRC == 1) dt = fmaf(x[j], wt[k][j], dt);
+      for (int j = 0; j < 8; j += 2) {
+        const float2_ xx = {x[j], x[j + 1]}, ww2 = {w[k][j], w[k][j + 1]};
+        d2 = __builtin_elementwise_fma(xx, ww2, d2);
       }
     }
+    const float d = d2.x + d2.y;
     dot[u] = SRC == 1 ? fmaf(d, kSynthScale, wshift) : d;
-    dtrue[u] = fmaf(dt, kSynthScale, wtshift);
   }
   RR::run(dot, c);
-  if (SRC == 1) {
-    RR::run(dtrue, c);
-#pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const int64_t row = base + (ubase + j) * G + g;
-      yy[j] = synth_label(row_key(seed, row0 + row), dtrue[j] + btrue);
-    }
-  }
   float res[NF];
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
@@ -494,12 +514,18 @@ __device__ __forceinline__ void mixed_tile(
   }
 }
 
-template <int LPR, int CPL, int UNROLL, int LOSS>
-__global__ __launch_bounds__(kBlock) void glm_grad_mixed_kernel(
+// y / sw hold n_res + n_lin entries: the resident rows' labels, then the lineage rows'.
+// MW: minimum waves per SIMD the register allocator must allow (2 = no constraint at
+// D = 256, 174 VGPRs; 3 = 168 VGPRs with a 4-register spill outside the tile loop).
+// LW = 0: every wave walks the interleaved tile sequence (both roles per wave).
+// LW > 0: fixed roles -- waves 0..LW-1 of each block regenerate lineage tiles, the
+// other 4 - LW stream resident tiles with UR rows per lane in flight, so the load
+// pipeline never pauses for hash work (each role strides over its own tiles).
+template <int LPR, int CPL, int UNROLL, int LOSS, int MW, int LW, int UR>
+__global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
     const uint16_t* __restrict__ X, int64_t ld, int64_t n_res, const float* __restrict__ y,
     const float* __restrict__ sw, const float* __restrict__ coef, const float* __restrict__ bptr,
-    uint32_t seed, int64_t row0, int64_t n_lin, const float* __restrict__ wtrue, float btrue,
-    float* __restrict__ partial, int pstride) {
+    uint32_t seed, int64_t row0, int64_t n_lin, float* __restrict__ partial, int pstride) {
   constexpr int G = kWave / LPR;
   constexpr int RT = G * UNROLL;
   constexpr int DP = LPR * CPL * 8;
@@ -508,46 +534,58 @@ __global__ __launch_bounds__(kBlock) void glm_grad_mixed_kernel(
   const int wid = threadIdx.x / kWave;
   const int g = lane / LPR, c = lane % LPR;
   const int nch = (int)(ld / 8);
-  const int ubase = RR::base(c);
-  const bool rep = RR::representative(c);
   const float intercept = *bptr;
+  const float* y_lin = y + n_res;
+  const float* sw_lin = sw ? sw + n_res : nullptr;
 
-  float w[CPL][8], wt[CPL][8], acc[CPL][8];
-  float wshift = 0.f, wtshift = 0.f, rs = 0.f;
+  float w[CPL][8], acc[CPL][8];
+  float wshift = 0.f, rs = 0.f;
 #pragma unroll
   for (int k = 0; k < CPL; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int col = 8 * (c + k * LPR) + j;
       w[k][j] = col < ld ? coef[col] : 0.f;
-      wt[k][j] = col < ld ? wtrue[col] : 0.f;
       wshift += w[k][j];
-      wtshift += wt[k][j];
       acc[k][j] = 0.f;
     }
   wshift *= kSynthShift;
-  wtshift *= kSynthShift;
   float acc_r = 0.f, acc_loss = 0.f, acc_w = 0.f;
 
-  const int64_t Tr = (n_res + RT - 1) / RT, Tl = (n_lin + RT - 1) / RT, S = Tr + Tl;
-  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wid;
-  const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
-  if (gw < S) {
-    // lineage tiles before unit s: L = floor(s Tl / S), rem = s Tl mod S (s Tl < 2^62)
-    int64_t L = gw * Tl / S, rem = gw * Tl - L * S;
-    const int64_t q0 = nw * Tl / S, r0 = nw * Tl - q0 * S;
-    for (int64_t s = gw; s < S; s += nw) {
-      if (rem + Tl >= S)
-        mixed_tile<LPR, CPL, UNROLL, LOSS, 1>(L * RT, n_lin, X, ld, nch, y, sw, seed, row0, w, wt, wshift,
-                                              wtshift, btrue, intercept, g, c, ubase, rep, acc, rs, acc_r,
-                                              acc_loss, acc_w);
-      else
-        mixed_tile<LPR, CPL, UNROLL, LOSS, 0>((s - L) * RT, n_res, X, ld, nch, y, sw, seed, row0, w, wt,
-                                              wshift, wtshift, btrue, intercept, g, c, ubase, rep, acc, rs,
-                                              acc_r, acc_loss, acc_w);
-      rem += r0;
-      L += q0;
-      if (rem >= S) { rem -= S; ++L; }
+  if constexpr (LW == 0) {
+    const int64_t Tr = (n_res + RT - 1) / RT, Tl = (n_lin + RT - 1) / RT, S = Tr + Tl;
+    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+    const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
+    if (gw < S) {
+      // lineage tiles before unit s: L = floor(s Tl / S), rem = s Tl mod S (s Tl < 2^62)
+      int64_t L = gw * Tl / S, rem = gw * Tl - L * S;
+      const int64_t q0 = nw * Tl / S, r0 = nw * Tl - q0 * S;
+      for (int64_t s = gw; s < S; s += nw) {
+        if (rem + Tl >= S)
+          mixed_tile<LPR, CPL, UNROLL, LOSS, 1>(L * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
+                                                wshift, intercept, g, c, acc, rs, acc_r, acc_loss, acc_w);
+        else
+          mixed_tile<LPR, CPL, UNROLL, LOSS, 0>((s - L) * RT, n_res, X, ld, nch, y, sw, seed, row0, w,
+                                                wshift, intercept, g, c, acc, rs, acc_r, acc_loss, acc_w);
+        rem += r0;
+        L += q0;
+        if (rem >= S) { rem -= S; ++L; }
+      }
+    }
+  } else {
+    if (wid < LW) {
+      const int64_t Tl = (n_lin + RT - 1) / RT;
+      const int64_t nlw = (int64_t)gridDim.x * LW;
+      for (int64_t t = (int64_t)blockIdx.x * LW + wid; t < Tl; t += nlw)
+        mixed_tile<LPR, CPL, UNROLL, LOSS, 1>(t * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
+                                              wshift, intercept, g, c, acc, rs, acc_r, acc_loss, acc_w);
+    } else {
+      constexpr int RTR = G * UR;
+      const int64_t Tr = (n_res + RTR - 1) / RTR;
+      const int64_t nrw = (int64_t)gridDim.x * (kWavesPerBlock - LW);
+      for (int64_t t = (int64_t)blockIdx.x * (kWavesPerBlock - LW) + (wid - LW); t < Tr; t += nrw)
+        mixed_tile<LPR, CPL, UR, LOSS, 0>(t * RTR, n_res, X, ld, nch, y, sw, seed, row0, w, wshift,
+                                          intercept, g, c, acc, rs, acc_r, acc_loss, acc_w);
     }
   }
 #pragma unroll
@@ -605,13 +643,13 @@ __global__ __launch_bounds__(kBlock) void synth_glm_kernel(
   for (int64_t t = gw; t < ntiles; t += nw) {
     const int64_t row = t * G + g;
     const bool ok = row < n;
-    const uint32_t rk = row_key(seed, row0 + row);
+    const uint32_t rk = row_key(seed, row0 + row), fk = feat_key(seed, row0 + row);
     float dt = 0.f;
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
       const int ch = c + k * LPR;
       if (8 * ch < ld) {
-        short8 v = synth_chunk(rk, ch);
+        short8 v = synth_chunk(fk, ch);
         float x[8];
         unpack8(v, x);
 #pragma unroll
@@ -713,7 +751,7 @@ __global__ __launch_bounds__(kBlock) void glm_colstats_kernel(
         const int ch = c + k * LPR;
         const int chc = ch < nch ? ch : nch - 1;
         short8 v = SRC == 0 ? __builtin_nontemporal_load(reinterpret_cast<const short8*>(X + rowc * ld + 8 * chc))
-                            : synth_chunk(row_key(seed, row0 + rowc), chc);
+                            : synth_chunk(feat_key(seed, row0 + rowc), chc);
         const float wk = ch < nch ? w : 0.f;
         float x[8];
         unpack8(v, x);
@@ -913,6 +951,82 @@ O3S_API int o3s_glm_grad(int loss, int src, const void* X, int64_t ld, int64_t n
   const int ncols = dpad + 3;
   hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 31) / 32), dim3(1024), 0, st, partial, grid,
                      pstride, ncols, out, accumulate);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int L, int C, int MW, int LW, int UR>
+static void launch_mixed(int loss, int grid, hipStream_t st, const uint16_t* X, int64_t ld, int64_t n_res,
+                         const float* y, const float* sw, const float* coef, const float* b, uint32_t seed,
+                         int64_t row0, int64_t n_lin, float* partial, int pstride) {
+  constexpr int U = C >= 8 ? 1 : 8 / C;
+  constexpr int UR2 = UR > 0 ? UR : U;
+  if (loss == LOSS_LOGISTIC)
+    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_LOGISTIC, MW, LW, UR2>), dim3(grid), dim3(kBlock), 0,
+                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride);
+  else if (loss == LOSS_HINGE)
+    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_HINGE, MW, LW, UR2>), dim3(grid), dim3(kBlock), 0,
+                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride);
+  else
+    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_SQUARED, MW, LW, UR2>), dim3(grid), dim3(kBlock), 0,
+                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride);
+}
+
+// Mixed resident + lineage pass in one launch (see glm_grad_mixed_kernel): n_res rows
+// of X plus n_lin synthetic rows starting at global row row0; y / sw cover all
+// n_res + n_lin rows.  Same out / coef / partial
+// contract as o3s_glm_grad (out is overwritten).  waves: 3 asks the register allocator
+// for 3 waves/SIMD (see glm_grad_mixed_kernel), anything else 2.  mode: 0 = interleaved
+// roles; 1..3 = that many lineage waves per block (fixed roles); 10 + LW = fixed roles
+// with 4 resident rows in flight per lane.
+O3S_API int o3s_glm_grad_mixed(int loss, const void* X, int64_t ld, int64_t n_res, const float* y,
+                               const float* sw, const float* coef, uint32_t seed, int64_t row0,
+                               int64_t n_lin, float* partial, int grid, double* out, int waves,
+                               int mode, hipStream_t st) {
+  const int nch = (int)(ld / 8);
+  const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
+  if (ld % 8 != 0 || cpl > 16 || grid <= 0 || n_res < 0 || n_lin < 0) return -1;
+  const int dpad = lpr * cpl * 8, pstride = dpad + 4;
+  int lpr_s = lpr, cpl_s = cpl;
+  if (cpl == 1 && lpr >= 16) { lpr_s = lpr / 4; cpl_s = 4; }
+  else if (cpl == 2) { lpr_s = 32; cpl_s = 4; }
+  const uint16_t* Xh = (const uint16_t*)X;
+  const float* b = coef + dpad;
+  bool done = false;
+#define O3S_MX(L, C)                                                                                  \
+  if (!done && lpr_s == L && cpl_s == C) {                                                            \
+    done = true;                                                                                      \
+    if (mode == 0 && waves == 3)                                                                      \
+      launch_mixed<L, C, 3, 0, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
+                                  partial, pstride);                                                 \
+    else if (mode == 0)                                                                               \
+      launch_mixed<L, C, 2, 0, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
+                                  partial, pstride);                                                 \
+    else if (mode == 1)                                                                               \
+      launch_mixed<L, C, 3, 1, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
+                                  partial, pstride);                                                 \
+    else if (mode == 2)                                                                               \
+      launch_mixed<L, C, 3, 2, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
+                                  partial, pstride);                                                 \
+    else if (mode == 3)                                                                               \
+      launch_mixed<L, C, 3, 3, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
+                                  partial, pstride);                                                 \
+    else if (mode == 12)                                                                              \
+      launch_mixed<L, C, 3, 2, 4>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
+                                  partial, pstride);                                                 \
+    else if (mode == 11)                                                                              \
+      launch_mixed<L, C, 3, 1, 4>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
+                                  partial, pstride);                                                 \
+    else done = false;                                                                                \
+  }
+  O3S_MX(4, 1) O3S_MX(8, 1) O3S_MX(4, 4) O3S_MX(8, 4) O3S_MX(16, 4) O3S_MX(32, 4)
+  O3S_MX(64, 4) O3S_MX(64, 8) O3S_MX(64, 16)
+#undef O3S_MX
+  if (!done) return -1;
+  O3S_CHECK_LAUNCH();
+  const int ncols = dpad + 3;
+  hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 31) / 32), dim3(1024), 0, st, partial, grid,
+                     pstride, ncols, out, 0);
   O3S_CHECK_LAUNCH();
   return 0;
 }

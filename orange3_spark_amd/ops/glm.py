@@ -9,6 +9,8 @@ Loss ids match the kernel: 0 logistic (y in {0,1}), 1 hinge (y in {0,1}, LinearS
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -57,19 +59,35 @@ def row_keys(seed: int, rows: torch.Tensor) -> torch.Tensor:
     return _fmix32((seed & _MASK) ^ _fmix32(inner))
 
 
-def synth_features_torch(rk: torch.Tensor, ld: int, d: int) -> torch.Tensor:
-    """bf16 [n, ld] features for row keys ``rk`` (int64 [n]).
+def _mix24(h: torch.Tensor) -> torch.Tensor:
+    """Torch twin of csrc/glm.hip ``mix24`` (bijective; v_mad_u32_u24 steps + xorshifts)."""
+    h = h ^ (h >> 16)
+    h = ((h & 0xFFFFFF) * 0xED5AD4 + h) & _MASK
+    h = h ^ (h >> 15)
+    return ((h & 0xFFFFFF) * 0x2C1B3C + h) & _MASK
 
-    Word i = fmix32(rk + i*golden) gives features 4i..4i+3 (byte q -> column 4i+q) as
+
+def feat_keys(seed: int, rows: torch.Tensor) -> torch.Tensor:
+    """Per-row feature keys (csrc/glm.hip ``feat_key``); labels use :func:`row_keys`."""
+    lo = rows & _MASK
+    hi = rows >> 32
+    k = _mix24((lo + ((seed * 0x9E3779B1) & _MASK)) & _MASK)
+    return _mix24(k ^ (((hi & 0xFFFFFF) * 0x7FEB35 + 0x165667) & _MASK))
+
+
+def synth_features_torch(fk: torch.Tensor, ld: int, d: int) -> torch.Tensor:
+    """bf16 [n, ld] features for feature keys ``fk`` (int64 [n], :func:`feat_keys`).
+
+    Word i = mix24(fk + i*0x9E3779) gives features 4i..4i+3 (byte q -> column 4i+q) as
     (2b - 255)/256: 256 symmetric levels in (-1, 1), exact in bf16 (csrc/glm.hip
     ``synth_chunk``).  All ``ld`` columns are generated (synthetic widths are rounded up to
     a multiple of 8; the ground-truth weights of columns >= d are zero, so those are pure
     noise features).
     """
-    n = rk.shape[0]
-    words = torch.arange(ld // 4, dtype=torch.int64, device=rk.device)
-    h = _fmix32((rk[:, None] + words[None, :] * 0x9E3779B9) & _MASK)
-    shifts = torch.arange(4, dtype=torch.int64, device=rk.device) * 8
+    n = fk.shape[0]
+    words = torch.arange(ld // 4, dtype=torch.int64, device=fk.device)
+    h = _mix24((fk[:, None] + words[None, :] * 0x9E3779) & _MASK)
+    shifts = torch.arange(4, dtype=torch.int64, device=fk.device) * 8
     b = (h[:, :, None] >> shifts) & 0xFF
     return ((2 * b - 255).to(torch.float32) * (1.0 / 256.0)).reshape(n, ld).to(torch.bfloat16)
 
@@ -111,8 +129,9 @@ def synth_glm(n: int, d: int, seed: int, row0: int = 0, device="cpu", ld: int | 
     step = 1 << 16
     for s in range(0, n, step):
         e = min(n, s + step)
-        rk = row_keys(seed, torch.arange(row0 + s, row0 + e, dtype=torch.int64))
-        xs = synth_features_torch(rk, ld, d)
+        rows = torch.arange(row0 + s, row0 + e, dtype=torch.int64)
+        rk = row_keys(seed, rows)
+        xs = synth_features_torch(feat_keys(seed, rows), ld, d)
         X[s:e] = xs
         y[s:e] = synth_labels_torch(rk, xs.float() @ wtrue.float() + btrue)
     return X, y
@@ -211,6 +230,38 @@ def glm_grad_synth(n: int, ld: int, d: int, seed: int, row0: int, wtrue: torch.T
         ws.out += out
         return ws.out
     return out
+
+
+# waves/SIMD the mixed kernel is register-allocated for (2 or 3; tools/sweep_glm_mixed.sh)
+MIX_WAVES = int(os.environ.get("O3S_GLM_MIX_WAVES", "3"))
+# 0 = every wave interleaves both roles; 1..3 = lineage waves per 4-wave block (fixed
+# roles); 11/12 = fixed roles with 4 resident rows in flight per lane
+MIX_MODE = int(os.environ.get("O3S_GLM_MIX_MODE", "0"))
+
+
+def glm_grad_mixed(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, n_lin: int, d: int,
+                   seed: int, row0: int, coef: torch.Tensor, intercept: float | None, loss: int,
+                   ws: GlmWorkspace) -> torch.Tensor:
+    """Resident rows of ``X`` plus ``n_lin`` lineage rows (global rows ``row0..``) in ONE
+    launch (csrc/glm.hip ``glm_grad_mixed_kernel``): memory-bound and VALU-bound tiles
+    are interleaved inside every wave so both resources stay busy.  ``y``/``sw`` are the
+    materialised label/weight columns of all ``X.shape[0] + n_lin`` rows.  Overwrites
+    ``ws.out``."""
+    ld = X.shape[1]
+    nr = X.shape[0]
+    if y.shape[0] != nr + n_lin or (sw is not None and sw.shape[0] != nr + n_lin):
+        raise ValueError("label / weight columns must cover the resident and lineage rows")
+    if ws.device.type != "cuda":
+        Xl, _ = synth_glm(n_lin, d, seed, row0, "cpu", ld, torch.zeros(ld), 0.0)
+        return glm_grad(torch.cat([X, Xl]), y, sw, coef, intercept, loss)
+    if X.dtype != torch.bfloat16 or not X.is_contiguous() or not y.is_contiguous():
+        raise TypeError("GPU GLM pass expects a contiguous bf16 feature matrix")
+    cf = _coef_buf(coef, ws.dpad, ws.device, intercept=intercept)
+    N.check(N.kernels().o3s_glm_grad_mixed(loss, X.data_ptr(), ld, nr, y.data_ptr(), N.ptr(sw),
+                                           cf.data_ptr(), seed & _MASK, row0, n_lin, ws.partial.data_ptr(),
+                                           ws.grid, ws.out.data_ptr(), MIX_WAVES, MIX_MODE, N.stream_of(X)),
+            "glm_grad_mixed")
+    return ws.out
 
 
 _COEF_CACHE: dict = {}

@@ -74,8 +74,8 @@ class LineageVectorColumn(C.VectorColumn):
         if self.lineage_rows == 0:
             return C.VectorColumn(self.data[idx.to(self.data.device)], self.size)
         idx = idx.to(torch.int64)
-        rk = G.row_keys(self.spec.seed, idx.to(self.data.device) + self.row0)
-        return C.VectorColumn(G.synth_features_torch(rk, self.ld, self.spec.d), self.size)
+        fk = G.feat_keys(self.spec.seed, idx.to(self.data.device) + self.row0)
+        return C.VectorColumn(G.synth_features_torch(fk, self.ld, self.spec.d), self.size)
 
     def mask_select(self, mask):
         return self.take(torch.nonzero(mask.to(self.data.device)).reshape(-1))

@@ -91,3 +91,38 @@ def test_gpu_grad_deterministic(gpu):
     a = G.glm_grad(X, y, None, coef, 0.0, 0).clone()
     b = G.glm_grad(X, y, None, coef, 0.0, 0).clone()
     assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,loss", [(256, 0), (256, 1), (256, 2), (20, 0), (100, 0), (600, 0)])
+def test_gpu_grad_mixed_matches_fp64(gpu, d, loss):
+    """One-launch resident + lineage pass == fp64 torch over the materialised rows."""
+    n_res, n_lin, seed = 30011, 20007, 13
+    ld = G.padded_width(d)
+    wt, bt = G.synth_truth(seed, d, ld)
+    # resident rows: arbitrary data (rows 0..n_res); lineage: global rows n_res..
+    Xr, yr = G.synth_glm(n_res, d, seed + 1, device=gpu, ld=ld)
+    Xl, yl = G.synth_glm(n_lin, d, seed, row0=n_res, device=gpu, ld=ld, wtrue=wt, btrue=bt)
+    coef = torch.randn(ld, generator=torch.Generator().manual_seed(4)).to(gpu) * 0.05
+    ws = G.GlmWorkspace(gpu, ld, grid=96)
+    yall = torch.cat([yr, 1.0 - yl])           # lineage labels come from the label column
+    out = G.glm_grad_mixed(Xr, yall, None, n_lin, d, seed, n_res, coef, 0.1, loss, ws).clone()
+    ref = G.glm_grad_torch(torch.cat([Xr, Xl]), yall, None, coef.double(), 0.1, loss)
+    dpad = ws.dpad
+    assert torch.allclose(out[:ld], ref[:ld], rtol=1e-3, atol=0.05), (out[:ld] - ref[:ld]).abs().max()
+    assert torch.allclose(out[dpad:], ref[ld:], rtol=1e-3, atol=0.5)
+    again = G.glm_grad_mixed(Xr, yall, None, n_lin, d, seed, n_res, coef, 0.1, loss, ws).clone()
+    assert torch.equal(out, again)                      # deterministic slab reduction
+
+
+def test_cpu_grad_mixed_matches_split():
+    d, seed = 24, 3
+    ld = G.padded_width(d)
+    wt, bt = G.synth_truth(seed, d, ld)
+    Xr, yr = G.synth_glm(500, d, seed + 1, ld=ld)
+    Xl, yl = G.synth_glm(300, d, seed, row0=500, ld=ld, wtrue=wt, btrue=bt)
+    coef = torch.linspace(-0.1, 0.1, ld)
+    ws = G.GlmWorkspace("cpu", ld)
+    out = G.glm_grad_mixed(Xr, torch.cat([yr, yl]), None, 300, d, seed, 500, coef, 0.2, 0, ws)
+    ref = G.glm_grad(torch.cat([Xr, Xl]), torch.cat([yr, yl]), None, coef, 0.2, 0)
+    assert torch.allclose(out, ref, rtol=1e-10, atol=1e-9)
