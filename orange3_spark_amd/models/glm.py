@@ -73,8 +73,10 @@ class GlmData:
         # then balances CUs that stream at different speeds (a persistent one-wave-set
         # grid was 8-10 % slower).
         self.overlap = None
-        self.mixed = (self.kernel and self.lineage is not None and self.X.shape[0] > 0
-                      and os.environ.get("O3S_GLM_MIXED", "1") == "1")
+        # (also without lineage rows: its LPR = 8 lane mapping streams 6.7 TB/s vs 6.4 TB/s
+        # for glm_grad's, tools/bench_glm_roles.py)
+        self.mixed = self.kernel and os.environ.get("O3S_GLM_MIXED", "1") == "1" \
+            and (self.sw is None or self.sw.shape[0] == self.y.shape[0])
         if self.mixed:
             cus = N.num_cus(self.device)
             self.ws = G.GlmWorkspace(self.device, self.ld,
@@ -133,9 +135,9 @@ class GlmData:
         """
         ws = self.ws
         if self.mixed:
-            spec, r0, nl = self.lineage
-            G.glm_grad_mixed(self.X, self.y, self.sw, nl, spec.d, spec.seed, r0, coef_eff, intercept,
-                             loss, ws)
+            spec, r0, nl = self.lineage if self.lineage else (None, 0, 0)
+            G.glm_grad_mixed(self.X, self.y, self.sw, nl, spec.d if spec else self.d,
+                             spec.seed if spec else 0, r0, coef_eff, intercept, loss, ws)
             self.passes += 1
             return ws.out
         if self.overlap is not None:
