@@ -126,3 +126,19 @@ def test_cpu_grad_mixed_matches_split():
     out = G.glm_grad_mixed(Xr, torch.cat([yr, yl]), None, 300, d, seed, 500, coef, 0.2, 0, ws)
     ref = G.glm_grad(torch.cat([Xr, Xl]), torch.cat([yr, yl]), None, coef, 0.2, 0)
     assert torch.allclose(out, ref, rtol=1e-10, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 11, 12])
+def test_gpu_grad_mixed_modes_agree(gpu, mode, monkeypatch):
+    """Every role layout of the mixed kernel computes the same pass (up to sum order)."""
+    n_res, n_lin, d, seed = 40009, 30011, 256, 21
+    Xr, yr = G.synth_glm(n_res, d, seed + 1, device=gpu)
+    yall = torch.cat([yr, (torch.arange(n_lin, device=gpu) % 3 == 0).float()])
+    coef = torch.randn(d, generator=torch.Generator().manual_seed(2)).to(gpu) * 0.05
+    ws = G.GlmWorkspace(gpu, d, grid=512)
+    monkeypatch.setattr(G, "MIX_MODE", 0)
+    ref = G.glm_grad_mixed(Xr, yall, None, n_lin, d, seed, n_res, coef, -0.2, 0, ws).clone()
+    monkeypatch.setattr(G, "MIX_MODE", mode)
+    out = G.glm_grad_mixed(Xr, yall, None, n_lin, d, seed, n_res, coef, -0.2, 0, ws).clone()
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-3)

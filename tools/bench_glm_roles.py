@@ -32,9 +32,11 @@ def main():
     ap.add_argument("--d", type=int, default=256)
     ap.add_argument("--grid", type=int, default=8192)
     ap.add_argument("--waves", type=int, default=3)
+    ap.add_argument("--mode", type=int, default=0)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     G.MIX_WAVES = a.waves
+    G.MIX_MODE = a.mode
     n, d, seed = a.rows, a.d, 5
     wt, bt = G.synth_truth(seed, d)
     X, y = G.synth_glm(n, d, seed, device=dev, wtrue=wt, btrue=bt)
@@ -43,10 +45,13 @@ def main():
     ws = G.GlmWorkspace(dev, d, grid=a.grid)
     ws8 = G.GlmWorkspace(dev, d)
     empty = X[:0]
-    r = {"rows": n, "d": d, "grid": a.grid, "waves": a.waves}
+    r = {"rows": n, "d": d, "grid": a.grid, "waves": a.waves, "mode": a.mode}
     r["mixed_res_only_ms"] = timed(lambda: G.glm_grad_mixed(X, y, None, 0, d, seed, n, coef, 0.0, 0, ws))
     r["mixed_lin_only_ms"] = timed(lambda: G.glm_grad_mixed(empty, y, None, n, d, seed, 0, coef, 0.0, 0, ws))
     r["mixed_both_ms"] = timed(lambda: G.glm_grad_mixed(X, y2, None, n, d, seed, n, coef, 0.0, 0, ws))
+    if a.mode != 0:
+        print(json.dumps(r, indent=1))
+        return
     r["res_kernel_ms"] = timed(lambda: G.glm_grad(X, y, None, coef, 0.0, 0, ws8))
     r["lin_kernel_ms"] = timed(lambda: G.glm_grad_synth(n, d, d, seed, 0, wt, bt, coef, 0.0, 0, ws8))
     gb = n * d * 2 / 1e9
