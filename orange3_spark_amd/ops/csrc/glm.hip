@@ -400,6 +400,28 @@ __device__ __forceinline__ void loss_terms(float m, float yv, float wv, float& r
   }
 }
 
+// Cross-lane sums for the LPR = 8, two-rows-per-lane layout without LDS traffic: the
+// quad butterflies use quad_perm DPP, the cross-quad halving row_half_mirror (lane i <->
+// 7 - i: after the quad sums every lane of a quad holds the same value, so the mirror
+// partner serves as lane i ^ 4).  Leaves lanes c < 4 with row 0's sum and lanes c >= 4
+// with row 1's -- the RowReduce<8, 2> layout (base(c) = c >> 2) -- in v[0].  Replaces
+// three ds_bpermute round trips (and their lgkmcnt waits) per tile by five DPP adds.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
+                                                               false));
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141;
+__device__ __forceinline__ void row_reduce_8x2(float (&v)[2], int c) {
+  v[0] += dpp_f<kDppXor1>(v[0]);
+  v[1] += dpp_f<kDppXor1>(v[1]);
+  v[0] += dpp_f<kDppXor2>(v[0]);
+  v[1] += dpp_f<kDppXor2>(v[1]);
+  const bool up = (c & 4) != 0;
+  const float keep = up ? v[1] : v[0], send = up ? v[0] : v[1];
+  v[0] = keep + dpp_f<kDppHalfMirror>(send);
+}
+
 // One tile of RT rows.  SRC 0: rows of X (bf16 in HBM); SRC 1: rows regenerated from
 // their lineage (raw bytes b, x = b*kSynthScale + kSynthShift, the affine map folded into
 // the dot product and a per-lane residual sum rs).  Labels / weights of both roles come
@@ -477,7 +499,9 @@ __device__ __forceinline__ void mixed_tile(
     const float d = d2.x + d2.y;
     dot[u] = SRC == 1 ? fmaf(d, kSynthScale, wshift) : d;
   }
-  RR::run(dot, c);
+  constexpr bool kDpp = LPR == 8 && UNROLL == 2;
+  if constexpr (kDpp) row_reduce_8x2(dot, c);
+  else RR::run(dot, c);
   float res[NF];
 #pragma unroll
   for (int j = 0; j < NF; ++j) {
@@ -496,9 +520,13 @@ __device__ __forceinline__ void mixed_tile(
         for (int j = 0; j < 8; ++j) asm volatile("" : "+v"(xf[u][k][j]));
       }
     }
+  float other = 0.f;
+  if constexpr (kDpp) other = dpp_f<kDppHalfMirror>(res[0]);   // the other row's residual
 #pragma unroll
   for (int u = 0; u < UNROLL; ++u) {
-    float r = __shfl(res[u % NF], g * LPR + RR::owner(u), kWave);
+    float r;
+    if constexpr (kDpp) r = ((c & 4) != 0) == (u == 0) ? other : res[0];
+    else r = __shfl(res[u % NF], g * LPR + RR::owner(u), kWave);
     if (SRC == 1) { rs += r; r *= kSynthScale; }
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
