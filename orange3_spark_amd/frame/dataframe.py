@@ -102,6 +102,22 @@ class DataFrame(DataFrameExtras):
     def device(self):
         return self.session.device
 
+    @property
+    def rdd(self):
+        """RDD of Rows: one partition per rank holding that rank's shard (rdd.py)."""
+        from ..rdd import RDD
+        df = self
+        cache = {}
+
+        def rows(p):
+            if "rows" not in cache:
+                names = list(df._cols)
+                lists = [c.to_pylist() for c in df._cols.values()]
+                cache["rows"] = [Row._make(names, vals) for vals in zip(*lists)]
+            return cache["rows"]
+        ctx = self.session.sparkContext
+        return RDD(ctx, self.comm.world_size, rows, owner=lambda p: p)
+
     def __len__(self):
         return self._n
 

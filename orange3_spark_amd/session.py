@@ -112,7 +112,15 @@ class Session:
 
     @property
     def sparkContext(self):
-        return self
+        """The SparkContext view (RDDs, broadcast, accumulators; rdd.py)."""
+        ctx = self.__dict__.get("_sc_view")
+        if ctx is None:
+            from .rdd import Context
+            ctx = self.__dict__["_sc_view"] = Context(self)
+        return ctx
+
+    def parallelize(self, c, numSlices=None):
+        return self.sparkContext.parallelize(c, numSlices)
 
     @property
     def appName(self):
@@ -173,6 +181,9 @@ class Session:
             import pyarrow as pa
         except ImportError:  # pragma: no cover
             pa = None
+        from .rdd import RDD
+        if isinstance(data, RDD):
+            return data.toDF(schema)
         names = _schema_names(schema)
         if hasattr(data, "domain") and hasattr(data, "X"):
             data = data_utils.orange_to_pandas(data)

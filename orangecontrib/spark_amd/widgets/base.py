@@ -42,7 +42,15 @@ class SharedSession:
         SharedSession._session = val
 
     # reference-compatible aliases (sc = SparkContext, hc = HiveContext)
-    sc = session
+    @property
+    def sc(self):
+        s = self.session
+        return s.sparkContext if s is not None else None
+
+    @sc.setter
+    def sc(self, val):
+        self.session = getattr(val, "session", val)
+
     hc = session
 
 

@@ -56,7 +56,7 @@ class OWScript(SharedSession, Widget):
 
     def commit(self):
         ns = self.namespace
-        ns.update(session=self.session, spark=self.session, sc=self.session, hc=self.session,
+        ns.update(session=self.session, spark=self.session, sc=self.sc, hc=self.session,
                   in_object=self.in_object, out_object=self.out_object)
         buf = io.StringIO()
         self.error()
