@@ -89,3 +89,24 @@ def test_udf(df):
     up = F.udf(lambda s: s.upper())
     assert df.select(up("name").alias("n")).toPandas().n.tolist()[1] == "BOB"
     _ = np
+
+
+def test_ml_functions_vector_array_roundtrip():
+    import numpy as np
+    import pandas as pd
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.ml.feature import HashingTF, VectorAssembler
+    from orange3_spark_amd.ml.functions import array_to_vector, predict_batch_udf, vector_to_array
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    df = VectorAssembler(inputCols=["a", "b"], outputCol="v").transform(
+        s.createDataFrame(pd.DataFrame({"a": [1.0, 2.0, -1.5], "b": [3.0, 4.0, 0.25]})))
+    arr = df.withColumn("arr", vector_to_array("v"))
+    assert [r.arr for r in arr.select("arr").collect()] == [[1.0, 3.0], [2.0, 4.0], [-1.5, 0.25]]
+    back = arr.withColumn("v2", array_to_vector("arr")).select("v2").collect()
+    assert np.allclose([r.v2.toArray() for r in back], [[1, 3], [2, 4], [-1.5, 0.25]])
+    tf = HashingTF(inputCol="w", outputCol="tf", numFeatures=16).transform(
+        s.createDataFrame(pd.DataFrame({"w": [["a", "b", "a"], ["c"]]})))
+    dense = [r.x for r in tf.select(vector_to_array("tf").alias("x")).collect()]
+    assert len(dense[0]) == 16 and sum(dense[0]) == 3.0 and sum(dense[1]) == 1.0
+    pred = predict_batch_udf(lambda: (lambda x: x.sum(axis=1)), return_type="double", batch_size=2)
+    assert [r.p for r in df.select(pred("v").alias("p")).collect()] == [4.0, 6.0, -1.25]
