@@ -119,6 +119,12 @@ class Session:
             ctx = self.__dict__["_sc_view"] = Context(self)
         return ctx
 
+    @property
+    def udf(self):
+        """``spark.udf.register(name, f, returnType)`` -> callable from SQL (sql/udf.py)."""
+        from .sql.udf import UDFRegistration
+        return UDFRegistration()
+
     def parallelize(self, c, numSlices=None):
         return self.sparkContext.parallelize(c, numSlices)
 

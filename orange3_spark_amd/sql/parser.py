@@ -506,10 +506,44 @@ class Parser:
         if f is None:
             if fn in ("lower", "upper", "length", "trim"):
                 return _string_fn(fn, args[0])
-            if fn in ("round", "floor", "ceil"):
+            if fn in ("floor", "ceil"):
                 return _math_fn(fn, args)
-            raise SyntaxError(f"unknown function {name}")
+            return _resolve_function(name, fn, args)
         return f(*args)
+
+
+_SCALAR_ANN = {"int", "str", "bool", "float", "int | None", "str | None"}
+_SCALAR_NAMES = {"value", "format", "sep", "pattern", "replacement", "idx", "pos", "length_", "n", "pad", "d",
+                 "numBits", "scale", "days", "limit", "substr", "asc", "i", "seed"}
+
+
+def _resolve_function(name, fn, args):
+    """Registered UDFs (spark.udf.register), then any ``sql.functions`` function by name.
+    Literal arguments bound to scalar parameters (``substring(s, 1, 3)``) are passed as
+    Python values, column arguments as expressions."""
+    import inspect
+    from . import functions as F
+    from .udf import lookup
+    u = lookup(fn)
+    if u is not None:
+        return u(*args)
+    g = getattr(F, fn, None)
+    if fn.startswith("_") or not callable(g) or isinstance(g, type):
+        raise SyntaxError(f"unknown function {name}")
+    try:
+        params = list(inspect.signature(g).parameters.values())
+    except (TypeError, ValueError):
+        params = []
+    call = []
+    for i, a in enumerate(args):
+        p = params[i] if i < len(params) else (params[-1] if params else None)
+        scalar = p is not None and p.kind is not inspect.Parameter.VAR_POSITIONAL and (
+            str(p.annotation) in _SCALAR_ANN or p.name in _SCALAR_NAMES)
+        if scalar and hasattr(a, "_literal"):
+            call.append(a.eval_literal())
+        else:
+            call.append(a)
+    return g(*call)
 
 
 def _is_agg(x):

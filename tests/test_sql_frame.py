@@ -96,3 +96,22 @@ def test_orange_conversions(s):
     assert back["k"].tolist() == ["1", "2"] * 10 and back["s"].tolist() == list("xy" * 10)
     df = s.createDataFrame(t)
     assert df.count() == 20
+
+
+def test_sql_resolves_function_library_and_registered_udfs():
+    import pandas as pd
+    from orange3_spark_amd import Session, SessionConf
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    df = s.createDataFrame(pd.DataFrame({"name": ["Ann", "bob"], "x": [1.25, -2.0]}))
+    df.createOrReplaceTempView("udf_t")
+    s.udf.register("plus1", lambda v: v + 1, "double")
+    rows = s.sql("SELECT upper(name) AS u, substring(name, 1, 2) AS s2, concat(name, '_', name) AS c, "
+                 "plus1(x) AS p, round(x, 1) AS r, regexp_replace(name, 'b', 'B') AS rr, "
+                 "PLUS1(plus1(x)) AS pp FROM udf_t").collect()
+    assert rows[0].u == "ANN" and rows[0].s2 == "An" and rows[0].c == "Ann_Ann"
+    assert rows[0].p == 2.25 and rows[1].pp == 0.0
+    assert rows[0].r == 1.3 and rows[1].r == -2.0            # HALF_UP like Spark
+    assert rows[1].rr == "BoB"
+    import pytest
+    with pytest.raises(SyntaxError):
+        s.sql("SELECT no_such_fn(x) FROM udf_t")
