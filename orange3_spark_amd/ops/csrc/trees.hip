@@ -34,7 +34,9 @@ constexpr int kHistWaves = 2;
 constexpr int kHistThreads = kHistWaves * kWave;
 
 // FP: features per row-slot (power of 2, <= 64); RS = 64 / FP row-slots per wave.
-template <int FP, bool CLS>
+// HW: per-row weights present (a compile-time switch: a runtime null test per row
+// became a branch around every weight load and split the counted vmcnt waits).
+template <int FP, bool CLS, bool HW>
 __global__ __launch_bounds__(kHistThreads) void tree_hist_kernel(
     const uint8_t* __restrict__ bins, int F, int fg0, int B, int S, const int32_t* __restrict__ order,
     const float* __restrict__ y, const float* __restrict__ w, const int64_t* __restrict__ item_lo,
@@ -61,12 +63,16 @@ __global__ __launch_bounds__(kHistThreads) void tree_hist_kernel(
   // accumulated.  Loads are unconditional (clamped to the item; masked rows contribute
   // weight 0 at use time), so the compiler emits counted vmcnt waits instead of
   // draining every load at a branch merge.
-  const int64_t step = stride * U;
-  auto ld_rows = [&](int64_t q0, int32_t (&r)[U]) {
+  // Positions are 32-bit offsets inside the item (items hold <= 2^31 rows): the row loop's
+  // index math and clamps stay single SALU ops (the CU's scalar unit is shared by its waves).
+  const int32_t* __restrict__ ord = order + lo;
+  const int32_t nl = (int32_t)(hi - lo);
+  const int32_t s32 = (int32_t)stride, step = s32 * U;
+  auto ld_rows = [&](int32_t j0, int32_t (&r)[U]) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t q = q0 + u * stride;
-      r[u] = order[q < hi ? q : hi - 1];
+      const int32_t j = j0 + u * s32;
+      r[u] = ord[j < nl ? j : nl - 1];
     }
   };
   auto ld_data = [&](const int32_t (&r)[U], int (&bo)[U], float (&yo)[U], float (&wo)[U]) {
@@ -75,24 +81,24 @@ __global__ __launch_bounds__(kHistThreads) void tree_hist_kernel(
       const int64_t row = r[u];
       bo[u] = bins[row * F + (fok ? fcol : 0)];
       yo[u] = y[row];
-      wo[u] = w ? w[row] : 1.f;
+      wo[u] = HW ? w[row] : 1.f;
     }
   };
   int32_t r1[U], r2[U];
   int b0[U], b1[U];
   float y0[U], y1[U], w0[U], w1[U];
-  int64_t p0 = lo + wid * RS + rs;
-  if (p0 < hi) {
-    ld_rows(p0, r1);
+  int32_t j0 = wid * RS + rs;
+  if (j0 < nl) {
+    ld_rows(j0, r1);
     ld_data(r1, b0, y0, w0);
-    ld_rows(p0 + step, r1);
+    ld_rows(j0 + step, r1);
   }
-  for (; p0 < hi; p0 += step) {
-    ld_rows(p0 + 2 * step, r2);
+  for (; j0 < nl; j0 += step) {
+    ld_rows(j0 + 2 * step, r2);
     ld_data(r1, b1, y1, w1);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool ok = fok && (p0 + u * stride < hi);
+      const bool ok = fok && (j0 + u * s32 < nl);
       const float wv = ok ? w0[u] : 0.f;
       float* cell = my + b0[u] * SL * FP + f;
       if (CLS) {
@@ -244,17 +250,19 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
   if (lds == 0) return -2;
   const int64_t stride = (int64_t)F * B * S;
   for (int fg0 = 0; fg0 < F; fg0 += fp) {
+#define O3S_TH1(FPV, C, W)                                                                              \
+  hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W>), dim3(n_items), dim3(kHistThreads), lds, st, bins, F, fg0, \
+                     B, S, order, y, w, item_lo, item_hi, slab, stride);
 #define O3S_TH(FPV)                                                                                     \
   if (fp == FPV) {                                                                                      \
-    if (cls)                                                                                            \
-      hipLaunchKernelGGL((tree_hist_kernel<FPV, true>), dim3(n_items), dim3(kHistThreads), lds, st, bins, \
-                         F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);                    \
-    else                                                                                                \
-      hipLaunchKernelGGL((tree_hist_kernel<FPV, false>), dim3(n_items), dim3(kHistThreads), lds, st, bins, \
-                         F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);                    \
+    if (cls && w) { O3S_TH1(FPV, true, true) }                                                          \
+    else if (cls) { O3S_TH1(FPV, true, false) }                                                         \
+    else if (w) { O3S_TH1(FPV, false, true) }                                                           \
+    else { O3S_TH1(FPV, false, false) }                                                                 \
   }
     O3S_TH(4) O3S_TH(8) O3S_TH(16) O3S_TH(32) O3S_TH(64)
 #undef O3S_TH
+#undef O3S_TH1
     O3S_CHECK_LAUNCH();
   }
   (void)n;
