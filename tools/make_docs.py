@@ -114,6 +114,24 @@ def api_page(modname: str) -> str:
     return "\n".join(lines)
 
 
+def class_methods_page(title: str, classes) -> str:
+    """Method reference of non-ML classes (RDD / SparkContext view / ml.functions)."""
+    lines = [f"# {title}", ""]
+    for cls in classes:
+        if inspect.isfunction(cls):
+            lines += [f"## `{cls.__name__}{inspect.signature(cls)}`", "", (inspect.getdoc(cls) or "").strip(), ""]
+            continue
+        lines += [f"## {cls.__name__}", "", (inspect.getdoc(cls) or "").split("\n\n")[0], ""]
+        for name, fn in sorted(vars(cls).items()):
+            if name.startswith("_") or not (inspect.isfunction(fn) or isinstance(fn, property)):
+                continue
+            doc = (inspect.getdoc(fn) or "").split("\n")[0]
+            sig = "" if isinstance(fn, property) else str(inspect.signature(fn)).replace("(self, ", "(").replace("(self)", "()")
+            lines.append(f"- `{name}{sig}`" + (f" — {doc}" if doc else ""))
+        lines.append("")
+    return "\n".join(lines)
+
+
 def main():
     os.makedirs(os.path.join(DOC, "widgets"), exist_ok=True)
     os.makedirs(os.path.join(DOC, "api"), exist_ok=True)
@@ -135,6 +153,15 @@ def main():
         with open(os.path.join(DOC, "api", f"{m}.md"), "w") as f:
             f.write(api_page(m) + "\n")
         index.append(f"- [`ml.{m}`](api/{m}.md)")
+    from orange3_spark_amd import rdd as R
+    from orange3_spark_amd.ml import functions as MF
+    with open(os.path.join(DOC, "api", "rdd.md"), "w") as f:
+        f.write(class_methods_page("RDD API (`orange3_spark_amd.rdd`)",
+                                   [R.Context, R.RDD, R.Broadcast, R.Accumulator, R.StatCounter]) + "\n")
+    with open(os.path.join(DOC, "api", "ml_functions.md"), "w") as f:
+        f.write(class_methods_page("`orange3_spark_amd.ml.functions`",
+                                   [MF.vector_to_array, MF.array_to_vector, MF.predict_batch_udf]) + "\n")
+    index += ["- [RDD / SparkContext](api/rdd.md)", "- [`ml.functions`](api/ml_functions.md)"]
     with open(os.path.join(DOC, "index.md"), "w") as f:
         f.write("\n".join(index) + "\n")
     print("wrote", DOC)
