@@ -35,6 +35,7 @@ class Catalog:
     def __init__(self, session):
         self.session = session
         self._temp: dict[str, DataFrame] = {}
+        self._cached: dict[str, DataFrame] = {}
         self._current = "default"
 
     # ------------------------------------------------------------------ paths
@@ -116,6 +117,8 @@ class Catalog:
     def table(self, name: str) -> DataFrame:
         if name in self._temp:
             return self._temp[name]
+        if name in self._cached:
+            return self._cached[name]
         p = self._table_path(name)
         if not os.path.isdir(p):
             raise KeyError(f"Table or view not found: {name}")
@@ -146,4 +149,73 @@ class Catalog:
         return self._temp.pop(name, None) is not None
 
     def cacheTable(self, name: str) -> None:
-        self.table(name).cache()
+        """Materialise the table in device memory; later ``table(name)`` calls reuse it."""
+        df = self.table(name).cache()
+        self._cached[name] = df
+
+    def isCached(self, name: str) -> bool:
+        return name in self._cached or (name in self._temp and getattr(self._temp[name], "is_cached", False))
+
+    def uncacheTable(self, name: str) -> None:
+        self._cached.pop(name, None)
+
+    def clearCache(self) -> None:
+        self._cached.clear()
+
+    def refreshTable(self, name: str) -> None:
+        """Drop any cached copy so the next read sees the files on disk."""
+        self._cached.pop(name, None)
+
+    def databaseExists(self, dbName: str) -> bool:
+        return dbName in self.databaseNames()
+
+    def getDatabase(self, dbName: str) -> Database:
+        if not self.databaseExists(dbName):
+            raise KeyError(f"Database not found: {dbName}")
+        return Database(dbName, locationUri=self._db_path(dbName))
+
+    def getTable(self, tableName: str) -> Table:
+        if tableName in self._temp:
+            return Table(tableName, None, True)
+        if not self.tableExists(tableName):
+            raise KeyError(f"Table or view not found: {tableName}")
+        db, t = self._split(tableName)
+        return Table(t, db, False)
+
+    def listColumns(self, tableName: str, dbName: str | None = None) -> list:
+        """Column(name, description, dataType, nullable, isPartition, isBucket) entries."""
+        from collections import namedtuple
+        Column = namedtuple("Column", "name description dataType nullable isPartition isBucket")
+        df = self.table(f"{dbName}.{tableName}" if dbName else tableName)
+        return [Column(f.name, None, f.dataType.simpleString(), True, False, False) for f in df.schema.fields]
+
+    def listFunctions(self, dbName: str | None = None) -> list:
+        """Built-in SQL functions (sql/functions.py) and registered UDFs (spark.udf)."""
+        import inspect
+        from collections import namedtuple
+        from .sql import functions as F
+        from .sql import udf as U
+        Function = namedtuple("Function", "name description className isTemporary")
+        names = sorted(n for n, v in vars(F).items() if callable(v) and not n.startswith("_")
+                       and not inspect.isclass(v) and getattr(v, "__module__", "").startswith("orange3_spark_amd"))
+        out = [Function(n, None, "builtin", False) for n in names]
+        out += [Function(n, None, "python_udf", True) for n in sorted(U._REGISTRY)]
+        return out
+
+    def functionExists(self, functionName: str, dbName: str | None = None) -> bool:
+        return any(f.name.lower() == functionName.lower() for f in self.listFunctions())
+
+    def createTable(self, tableName: str, path: str | None = None, source: str | None = None, schema=None,
+                    **options):
+        """Register files at ``path`` (parquet / csv / json) as a catalog table, or create an
+        empty table from ``schema``; returns it as a DataFrame."""
+        if path is not None:
+            df = self.session.read.load(path, format=source or "parquet", **options)
+        else:
+            names = [f.name for f in getattr(schema, "fields", [])]
+            import pandas as pd
+            df = self.session.createDataFrame(pd.DataFrame({n: pd.Series([], dtype=float) for n in names}))
+        self.saveAsTable(df, tableName, "overwrite")
+        return self.table(tableName)
+
+    createExternalTable = createTable

@@ -242,6 +242,11 @@ class DataFrameReader:
             return self.csv(path, **opts)
         if fmt == "json":
             return self.json(path)
+        if fmt == "text":
+            return self.text(path)
+        if fmt == "jdbc":
+            return self.jdbc(opts.get("url"), opts.get("dbtable") or opts.get("query"),
+                             properties={k: v for k, v in opts.items() if k not in ("url", "dbtable", "query")})
         raise ValueError(f"unknown format {fmt}")
 
     def parquet(self, *paths, columns=None):
@@ -267,6 +272,62 @@ class DataFrameReader:
 
     def table(self, name):
         return self.session.table(name)
+
+    def text(self, paths, wholetext: bool = False, lineSep=None):
+        """Lines of text files -> one string column ``value`` (``wholetext``: one row per file)."""
+        import glob
+        import pandas as pd
+        files = []
+        for p in ([paths] if isinstance(paths, str) else list(paths)):
+            if os.path.isdir(p):
+                files += sorted(os.path.join(p, f) for f in os.listdir(p) if not f.startswith(("_", ".")))
+            else:
+                files += sorted(glob.glob(p)) or [p]
+        vals = []
+        for f in files:
+            with open(f, "r", encoding="utf-8", errors="replace") as fh:
+                txt = fh.read()
+            if wholetext:
+                vals.append(txt)
+            else:
+                parts = txt.split(lineSep) if lineSep else txt.splitlines()
+                vals.extend(parts)
+        return self.session.createDataFrame(pd.DataFrame({"value": pd.Series(vals, dtype=object)}))
+
+    def jdbc(self, url, table, column=None, lowerBound=None, upperBound=None, numPartitions=None,
+             predicates=None, properties=None):
+        """Read a database table or ``(SELECT ...) alias`` subquery through a DB-API driver
+        (the reference reaches databases through its ODBC widget,
+        orangecontrib/spark/widgets/data/odbc_table.py:141-161).  ``jdbc:sqlite:<path>`` uses
+        the stdlib sqlite3; ``jdbc:odbc:<connection string>`` uses pyodbc when importable.
+        ``predicates`` become OR-ed WHERE clauses.  Every rank runs the query and keeps its
+        row slice (SPMD)."""
+        import pandas as pd
+        conn = _dbapi_connect(url, properties or {})
+        try:
+            src = table if str(table).lstrip().startswith("(") or " " not in str(table).strip() else f"({table}) q"
+            sql = f"SELECT * FROM {src}"
+            if predicates:
+                sql += " WHERE " + " OR ".join(f"({p})" for p in predicates)
+            pdf = pd.read_sql_query(sql, conn)
+        finally:
+            conn.close()
+        return self.session.createDataFrame(pdf)
+
+
+def _dbapi_connect(url, props):
+    url = str(url or "")
+    if url.startswith("jdbc:"):
+        url = url[len("jdbc:"):]
+    if url.startswith("odbc:"):
+        import pyodbc                                      # optional dependency
+        return pyodbc.connect(url[len("odbc:"):])
+    if url.startswith("sqlite:"):
+        url = url[len("sqlite:"):]
+        if url.startswith("//"):
+            url = url[2:]
+    import sqlite3
+    return sqlite3.connect(url or ":memory:")
 
 
 class DataFrameWriter:
@@ -328,11 +389,57 @@ class DataFrameWriter:
                 f.write(json.dumps({k: _jsonable(v) for k, v in r.asDict().items()}) + "\n")
         comm.barrier()
 
+    def text(self, path, compression=None, lineSep=None):
+        """One string column -> ``part-NNNNN.txt`` per rank (Spark's text sink)."""
+        if len(self.df.columns) != 1:
+            raise ValueError("text sink supports a single string column")
+        comm = self.df.comm
+        if comm.rank == 0:
+            _prepare_dir(path, self._mode)
+        comm.barrier()
+        vals = DataFrame(self.df.session.local_view(), self.df._cols).toPandas().iloc[:, 0]
+        with open(os.path.join(path, f"part-{comm.rank:05d}.txt"), "w") as f:
+            for v in vals:
+                f.write(("" if v is None else str(v)) + (lineSep or "\n"))
+        comm.barrier()
+
+    def jdbc(self, url, table, mode=None, properties=None):
+        """Write the DataFrame to a database table through a DB-API driver (rank 0 writes
+        the gathered rows; modes error / append / overwrite / ignore)."""
+        mode = (mode or self._mode or "error").lower()
+        pdf = self.df.toPandas()
+        if self.df.comm.rank == 0:
+            conn = _dbapi_connect(url, properties or {})
+            try:
+                exists = pd_table_exists(conn, table)
+                if exists and mode in ("error", "errorifexists"):
+                    raise ValueError(f"table {table} already exists")
+                if not (exists and mode == "ignore"):
+                    for c in pdf.columns:             # vectors / arrays -> JSON text cells
+                        if pdf[c].dtype == object:
+                            pdf[c] = pdf[c].map(lambda v: json.dumps(_jsonable(v)) if hasattr(v, "toArray")
+                                                or isinstance(v, (list, tuple)) else v)
+                    pdf.to_sql(table, conn, index=False, if_exists="replace" if mode == "overwrite" else "append")
+                conn.commit()
+            finally:
+                conn.close()
+        self.df.comm.barrier()
+
     def saveAsTable(self, name, format=None, mode=None):
         self.df.session.catalog.saveAsTable(self.df, name, mode or self._mode)
 
     def insertInto(self, name, overwrite=False):
         self.df.session.catalog.saveAsTable(self.df, name, "overwrite" if overwrite else "append")
+
+
+def pd_table_exists(conn, table) -> bool:
+    try:
+        cur = conn.cursor()
+        cur.execute(f"SELECT 1 FROM {table} LIMIT 1")
+        cur.fetchall()
+        return True
+    except Exception:  # noqa: BLE001 - driver-specific "no such table"
+        return False
 
 
 def _jsonable(v):

@@ -115,3 +115,42 @@ def test_sql_resolves_function_library_and_registered_udfs():
     import pytest
     with pytest.raises(SyntaxError):
         s.sql("SELECT no_such_fn(x) FROM udf_t")
+
+
+def test_jdbc_and_text_sources(tmp_path):
+    import pandas as pd
+    from orange3_spark_amd import Session, SessionConf
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    df = s.createDataFrame(pd.DataFrame({"a": [1, 2, 3], "b": ["x", "y", "z"]}))
+    url = f"jdbc:sqlite:{tmp_path / 'db.sqlite'}"
+    df.write.jdbc(url, "tab", mode="overwrite")
+    assert [r.a for r in s.read.jdbc(url, "tab", predicates=["a >= 2"]).collect()] == [2, 3]
+    q = s.read.format("jdbc").option("url", url).option("dbtable", "(SELECT a * 10 AS a10 FROM tab) q").load()
+    assert [r.a10 for r in q.collect()] == [10, 20, 30]
+    df.write.jdbc(url, "tab", mode="append")
+    assert s.read.jdbc(url, "tab").count() == 6
+    import pytest
+    with pytest.raises(ValueError):
+        df.write.jdbc(url, "tab")                         # default mode: error if it exists
+    df.select("b").write.text(str(tmp_path / "txt"))
+    assert [r.value for r in s.read.text(str(tmp_path / "txt")).collect()] == ["x", "y", "z"]
+    assert s.read.text(str(tmp_path / "txt"), wholetext=True).count() == 1
+
+
+def test_catalog_extras(tmp_path):
+    import pandas as pd
+    from orange3_spark_amd import Session, SessionConf
+    s = Session(SessionConf().set("o3s.device", "cpu").set("spark.sql.warehouse.dir", str(tmp_path / "wh")))
+    s.createDataFrame(pd.DataFrame({"a": [1, 2], "b": ["x", "y"]})).write.saveAsTable("t1")
+    c = s.catalog
+    assert [col.name for col in c.listColumns("t1")] == ["a", "b"]
+    c.cacheTable("t1")
+    assert c.isCached("t1") and c.table("t1").count() == 2
+    c.uncacheTable("t1")
+    assert not c.isCached("t1")
+    assert c.getTable("t1").database == "default" and c.databaseExists("default")
+    assert c.functionExists("regexp_replace") and not c.functionExists("nope")
+    s.udf.register("twice", lambda v: 2 * v, "double")
+    assert c.functionExists("twice")
+    s.createDataFrame(pd.DataFrame({"z": [1.0]})).write.parquet(str(tmp_path / "pq"))
+    assert c.createTable("t2", path=str(tmp_path / "pq")).columns == ["z"]
