@@ -79,8 +79,13 @@ class GlmData:
             and (self.sw is None or self.sw.shape[0] == self.y.shape[0])
         if self.mixed:
             cus = N.num_cus(self.device)
+            # 16-row tiles, 4 waves per block: never more blocks than one tile per wave
+            # (a small table would otherwise launch 8K mostly-idle blocks and make the
+            # finish kernel sum 8K slab rows -- ~100 us per step on a 4K-row table)
+            tiles = -(-int(self.X.shape[0]) // 16) + -(-int(self.lineage[2] if self.lineage else 0) // 16)
+            grid = max(1, min(cus * 32, -(-tiles // 4)))
             self.ws = G.GlmWorkspace(self.device, self.ld,
-                                     grid=int(os.environ.get("O3S_GLM_GRID_MIX", str(cus * 32))))
+                                     grid=int(os.environ.get("O3S_GLM_GRID_MIX", str(grid))))
         elif self.kernel and self.lineage and self.X.shape[0] and os.environ.get("O3S_GLM_OVERLAP", "1") == "1":
             cus = N.num_cus(self.device)
             res_grid = int(os.environ.get("O3S_GLM_GRID_RES", str(cus * 8)))
@@ -335,26 +340,41 @@ class DeviceSGD:
         self.step_size = float(step_size)
         self.t = 0
         self.loss_hist = torch.zeros(1024, dtype=torch.float64, device=dev)
+        self.t_dev = torch.zeros(1, dtype=torch.int64, device=dev)      # device step counter
+        self._graph = None
+        self._graph_failed = False
+        self._eager_steps = 0
         self.W = float(data.comm.sum_scalar(float(data.n_local if data.sw is None else float(data.sw.sum()))))
 
     @traced("sgd.step")
     def step(self):
-        """One step, entirely stream-ordered on the device: pass -> all-reduce -> update."""
+        """One step, entirely stream-ordered on the device: pass -> all-reduce -> update.
+
+        GPU: after two eager steps the step is captured into a HIP graph (torch.cuda.CUDAGraph
+        over the raw kernel launches; the step counter, step size and loss slot live on the
+        device, so the captured step has no host arguments) and later steps replay it -- the
+        launch sequence of a step costs one graph launch instead of ~4 kernel launches plus
+        Python.  O3S_SGD_GRAPH=0 disables it; with several ranks it is opt-in
+        (O3S_SGD_GRAPH=all: the RCCL all-reduce is captured too)."""
         self.t += 1
         d = self.data
-        out = self._pass()
-        d.comm.all_reduce(out)
+        if d.kernel:
+            if self._graph is not None and self.t <= self.loss_hist.shape[0]:
+                self._graph.replay()
+                return
+            if self.t > self.loss_hist.shape[0]:
+                self.loss_hist = torch.cat([self.loss_hist, torch.zeros_like(self.loss_hist)])
+                self._graph = None
+            self._kernel_step()
+            self._eager_steps += 1
+            self._maybe_capture()
+            return
         eta = self.step_size / math.sqrt(self.t)
         if self.t > self.loss_hist.shape[0]:
             self.loss_hist = torch.cat([self.loss_hist, torch.zeros_like(self.loss_hist)])
         slot = self.loss_hist[self.t - 1:self.t]
-        if d.kernel:
-            lib = N.kernels()
-            N.check(lib.o3s_glm_sgd_update(out.data_ptr(), self.dpad, self.bt.data_ptr(), self.b.data_ptr(),
-                                           self.inv_std.data_ptr(), N.ptr(self.l2v), self.l2, eta, int(self.fi),
-                                           self.coef_eff.data_ptr(), slot.data_ptr(),
-                                           torch.cuda.current_stream(d.device).cuda_stream), "glm_sgd_update")
-            return
+        out = self._pass()
+        d.comm.all_reduce(out)
         W = out[self.dpad + 2]
         g = out[: self.dpad] * self.inv_std / W
         g = g + (self.l2v if self.l2v is not None else self.l2) * self.bt
@@ -364,6 +384,34 @@ class DeviceSGD:
         self.coef_eff[: self.dpad].copy_((self.bt * self.inv_std).to(torch.float32))
         self.coef_eff[self.dpad:].copy_(self.b.to(torch.float32))
         slot.copy_(out[self.dpad + 1:self.dpad + 2] / W)
+
+    def _kernel_step(self):
+        d = self.data
+        out = self._pass()
+        d.comm.all_reduce(out)
+        N.check(N.kernels().o3s_glm_sgd_update_dev(
+            out.data_ptr(), self.dpad, self.bt.data_ptr(), self.b.data_ptr(), self.inv_std.data_ptr(),
+            N.ptr(self.l2v), self.l2, self.step_size, int(self.fi), self.coef_eff.data_ptr(),
+            self.loss_hist.data_ptr(), int(self.loss_hist.shape[0]), self.t_dev.data_ptr(),
+            torch.cuda.current_stream(d.device).cuda_stream), "glm_sgd_update")
+
+    def _maybe_capture(self):
+        from ..runtime import faults
+        mode = os.environ.get("O3S_SGD_GRAPH", "1")
+        if self._graph is not None or self._graph_failed or mode == "0" or self._eager_steps < 2:
+            return
+        if self.data.comm.world_size > 1 and mode != "all":
+            return
+        if faults.launch_blocking():
+            return
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._kernel_step()
+            self._graph = g
+        except Exception as e:  # noqa: BLE001 - fall back to eager launches
+            log.warning("SGD step graph capture failed (%s); continuing eagerly", e)
+            self._graph_failed = True
 
     def _pass(self):
         if self.data.kernel:

@@ -876,6 +876,36 @@ __global__ __launch_bounds__(256) void glm_sgd_update_kernel(
   }
 }
 
+// Graph-capturable variant: the step counter lives on the device (t <- t + 1, eta =
+// step_size / sqrt(t), loss recorded at loss_hist[t - 1] while t <= cap), so a captured
+// step has no per-step host arguments and can be replayed from a HIP graph.
+__global__ __launch_bounds__(256) void glm_sgd_update_dev_kernel(
+    const double* __restrict__ out, int dpad, double* __restrict__ bt, double* __restrict__ b,
+    const double* __restrict__ inv_std, const double* __restrict__ l2v, double l2, double step_size,
+    int fit_intercept, float* __restrict__ coef_eff, double* __restrict__ loss_hist, int64_t cap,
+    int64_t* __restrict__ t_dev) {
+  const int64_t t = t_dev[0] + 1;
+  const double eta = step_size / sqrt((double)t);
+  const double W = out[dpad + 2];
+  const double invW = W > 0.0 ? 1.0 / W : 0.0;
+  for (int i = threadIdx.x; i < dpad; i += blockDim.x) {
+    const double inv = inv_std[i];
+    const double reg = l2v ? l2v[i] : l2;
+    const double v = bt[i] - eta * (out[i] * inv * invW + reg * bt[i]);
+    bt[i] = v;
+    coef_eff[i] = (float)(v * inv);
+  }
+  __syncthreads();                       // every lane has read t_dev before it moves
+  if (threadIdx.x == 0) {
+    double bv = b[0];
+    if (fit_intercept) bv -= eta * out[dpad] * invW;
+    b[0] = bv;
+    coef_eff[dpad] = (float)bv;
+    if (t <= cap) loss_hist[t - 1] = out[dpad + 1] * invW;
+    t_dev[0] = t;
+  }
+}
+
 int pick_lpr(int nch) {
   int l = 4;
   while (l < nch && l < 64) l <<= 1;
@@ -1141,6 +1171,16 @@ O3S_API int o3s_glm_sgd_update(const double* out, int dpad, double* bt, double* 
                                double* loss_slot, hipStream_t st) {
   hipLaunchKernelGGL(glm_sgd_update_kernel, dim3(1), dim3(256), 0, st, out, dpad, bt, b, inv_std, l2v, l2,
                      eta, fit_intercept, coef_eff, loss_slot);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+O3S_API int o3s_glm_sgd_update_dev(const double* out, int dpad, double* bt, double* b, const double* inv_std,
+                                   const double* l2v, double l2, double step_size, int fit_intercept,
+                                   float* coef_eff, double* loss_hist, int64_t cap, int64_t* t_dev,
+                                   hipStream_t st) {
+  hipLaunchKernelGGL(glm_sgd_update_dev_kernel, dim3(1), dim3(256), 0, st, out, dpad, bt, b, inv_std, l2v, l2,
+                     step_size, fit_intercept, coef_eff, loss_hist, cap, t_dev);
   O3S_CHECK_LAUNCH();
   return 0;
 }
