@@ -9,9 +9,15 @@ Reference behaviour (orangecontrib/spark/utils/data_utils.py):
     quirk Q1); here it is a direct columnar conversion of X / Y / metas.
   * ``format_sql`` (:17-18) used sqlparse (absent here): an in-house keyword upper-caser
     and clause re-indenter with the same intent.
+  * ``save_csv_IO`` (:55-74) wrote an Orange table into an in-memory CSV with an empty
+    delimiter (TypeError) and handed it over un-rewound; ``load_csvIO`` (:77-114) built its
+    rows lazily and returned nothing (quirk Q2).  Both are fixed here: comma-separated,
+    header row of variable names, buffer rewound / rows materialised.
 """
 from __future__ import annotations
 
+import csv
+import io
 import re
 from collections import OrderedDict
 
@@ -77,6 +83,36 @@ def orange_to_pandas(table) -> pd.DataFrame:
     for j, v in enumerate(dom.metas):
         put(v, M[:, j])
     return pd.DataFrame(data)
+
+
+def save_csv_IO(data) -> io.StringIO:
+    """Orange Table or pandas DataFrame -> rewound in-memory CSV (header = column names)."""
+    pdf = data if isinstance(data, pd.DataFrame) else orange_to_pandas(data)
+    buf = io.StringIO()
+    w = csv.writer(buf, delimiter=",", lineterminator="\n")
+    w.writerow([str(c) for c in pdf.columns])
+    for row in pdf.itertuples(index=False):
+        w.writerow(["" if v is None or (isinstance(v, float) and np.isnan(v)) else v for v in row])
+    buf.seek(0)
+    return buf
+
+
+def load_csvIO(buf, delimiter: str = ","):
+    """In-memory CSV -> (header, rows); numeric cells parsed as float, empty cells None."""
+    if hasattr(buf, "seek"):
+        buf.seek(0)
+    rows = list(csv.reader(buf, delimiter=delimiter))
+    if not rows:
+        return [], []
+
+    def cell(v):
+        if v == "":
+            return None
+        try:
+            return float(v)
+        except ValueError:
+            return v
+    return rows[0], [[cell(v) for v in r] for r in rows[1:]]
 
 
 _KEYWORDS = ["select", "from", "where", "group by", "order by", "having", "limit", "join", "left join",
