@@ -396,6 +396,12 @@ class LDA(Estimator, _LDAParams, MLWritable, MLReadable):
                 allg = comm.all_gather_v(G_) if comm.world_size > 1 else G_
                 state.alpha = CE.update_alpha(state.alpha, allg, rho)
             state.iterations = it
+        if em:
+            m = DistributedLDAModel._from(state.lam.cpu().numpy(), state.alpha.cpu().numpy(), eta, V)
+            m._with_parent(self)
+            m._train_ll, _ = m._doc_bound(df)
+            m._log_prior = float(CE.topic_bound(m._state(dev)))
+            return m
         m = LDAModel._from(state.lam.cpu().numpy(), state.alpha.cpu().numpy(), eta, V)
         return m._with_parent(self)
 
@@ -506,6 +512,40 @@ class LDAModel(Model, _LDAParams, MLWritable, MLReadable):
 
 
 LocalLDAModel = LDAModel
+
+
+@register("org.apache.spark.ml.clustering.DistributedLDAModel")
+class DistributedLDAModel(LDAModel):
+    """Model of ``LDA(optimizer="em")`` (Spark's DistributedLDAModel).  The topics matrix is
+    small (k x vocabSize) and replicated on every rank, so "distributed" only records how it
+    was trained; the extra EM diagnostics are kept and ``toLocal()`` drops them."""
+
+    def __init__(self):
+        super().__init__()
+        self._train_ll = float("nan")
+        self._log_prior = float("nan")
+
+    def isDistributed(self):
+        return True
+
+    def trainingLogLikelihood(self) -> float:
+        """Variational bound on the training corpus at the final iteration."""
+        return self._train_ll
+
+    def logPrior(self) -> float:
+        """log p(topics | topicConcentration) + log p(docConcentration) terms of the bound."""
+        return self._log_prior
+
+    def toLocal(self) -> LDAModel:
+        m = LDAModel._from(self._lam, self._alpha, self._eta, self._V)
+        m._paramMap.update(self._paramMap)
+        return m
+
+    def getCheckpointFiles(self):
+        return []
+
+    def deleteCheckpointFiles(self):
+        pass
 
 
 # ===================================================== PowerIterationClustering

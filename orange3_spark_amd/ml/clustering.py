@@ -133,4 +133,5 @@ class KMeansModel(Model, _KMeansParams, MLWritable, MLReadable):
 
 
 from ._clustering_extra import (LDA, BisectingKMeans, BisectingKMeansModel, GaussianMixture,  # noqa: E402,F401
-                                GaussianMixtureModel, LDAModel, LocalLDAModel, PowerIterationClustering)
+                                GaussianMixtureModel, LDAModel, LocalLDAModel, DistributedLDAModel,
+                                PowerIterationClustering)

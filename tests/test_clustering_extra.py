@@ -69,6 +69,16 @@ def test_lda_separates_topics(session, tmp_path):
     m.save(str(tmp_path / "lda"))
     m2 = CL.LocalLDAModel.load(str(tmp_path / "lda"))
     np.testing.assert_allclose(m2.topicsMatrix().toArray(), m.topicsMatrix().toArray())
+    assert not m.isDistributed()
+    # optimizer="em": a DistributedLDAModel with the EM diagnostics; toLocal() keeps the topics
+    me = CL.LDA(k=2, maxIter=15, seed=1, optimizer="em").fit(dd)
+    assert isinstance(me, CL.DistributedLDAModel) and me.isDistributed()
+    assert me.trainingLogLikelihood() < 0 and np.isfinite(me.logPrior())
+    loc = me.toLocal()
+    assert not loc.isDistributed()
+    np.testing.assert_allclose(loc.topicsMatrix().toArray(), me.topicsMatrix().toArray())
+    me.save(str(tmp_path / "lda_em"))
+    assert isinstance(CL.DistributedLDAModel.load(str(tmp_path / "lda_em")), CL.DistributedLDAModel)
 
 
 def test_power_iteration_clustering(session):
