@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kAlsWaves * 64) void als_pass_kernel(
         float dot = 0.f;
 #pragma unroll
         for (int k = 0; k < RV; ++k) dot = fmaf(f[q][k], v[k], dot);
-        s *= wave_sum(dot);
+        s *= wave_sum_dpp(dot);             // DPP: no LDS round trips in the per-rating chain
       }
 #pragma unroll
       for (int k = 0; k < RV; ++k) acc[k] = fmaf(s, f[q][k], acc[k]);

@@ -79,6 +79,25 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   return v;
 }
 
+// Full-wave sum through DPP (no LDS round trips): quad butterflies, half-row and row
+// mirrors, then row_bcast:15 / row_bcast:31 fold the four 16-lane rows into lane 63, read
+// back as a wave-uniform scalar.  All 64 lanes must be active.  ~6 VALU ops of latency
+// instead of six dependent ds_bpermute round trips (__shfl_xor).
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK,
+                                                                   0xF, false));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v = dpp_add<0xB1>(v);          // quad_perm [1,0,3,2]
+  v = dpp_add<0x4E>(v);          // quad_perm [2,3,0,1]
+  v = dpp_add<0x141>(v);         // row_half_mirror
+  v = dpp_add<0x140>(v);         // row_mirror
+  v = dpp_add<0x142, 0xA>(v);    // row_bcast:15 -> rows 1, 3
+  v = dpp_add<0x143, 0xC>(v);    // row_bcast:31 -> rows 2, 3 (lane 63 = total)
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
 // Numerically stable log(1 + exp(x)).
 __device__ __forceinline__ float log1pexp(float x) {
   return x > 0.f ? x + log1pf(__expf(-x)) : log1pf(__expf(x));

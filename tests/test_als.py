@@ -90,7 +90,7 @@ def test_als_cold_start_and_save(cpu, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("R", [10, 64, 128])
+@pytest.mark.parametrize("R", [10, 64, 100, 128, 129, 200, 255])
 def test_gpu_als_pass_matches_torch(gpu, R):
     from orange3_spark_amd.ops import als as A
     g = torch.Generator(device="cpu").manual_seed(R)
