@@ -48,8 +48,19 @@ class Row(tuple):
         r.__fields__ = list(names)
         return r
 
-    def asDict(self):
-        return dict(zip(self.__fields__ or [], self))
+    def asDict(self, recursive: bool = False):
+        d = dict(zip(self.__fields__ or [], self))
+        if recursive:
+            def conv(v):
+                if isinstance(v, Row):
+                    return v.asDict(True)
+                if isinstance(v, list):
+                    return [conv(x) for x in v]
+                if isinstance(v, dict):
+                    return {k: conv(x) for k, x in v.items()}
+                return v
+            d = {k: conv(v) for k, v in d.items()}
+        return d
 
     def __getattr__(self, item):
         if item.startswith("__"):
@@ -236,21 +247,23 @@ class DataFrame(DataFrameExtras):
         empty or null arrays disappear, as in Spark)."""
         name = g.name
         arr = out[name]
-        lists = [v if v is not None else [] for v in (arr.values if isinstance(arr, C.HostColumn)
-                                                        else arr.to_pylist())]
+        outer = g._generator.endswith("_outer")          # explode_outer: empty / null -> one null row
+        lists = [(list(v) if v is not None and len(v) else ([None] if outer else []))
+                 for v in (arr.values if isinstance(arr, C.HostColumn) else arr.to_pylist())]
         lens = np.array([len(v) for v in lists], dtype=np.int64)
         idx = torch.from_numpy(np.repeat(np.arange(len(lists)), lens))
         flat = [x for v in lists for x in v]
         res = OrderedDict()
         for k, c in out.items():
             if k == name:
-                if g._generator == "posexplode":
+                if g._generator.startswith("posexplode"):
                     res["pos"] = C.NumericColumn(torch.from_numpy(np.concatenate(
                         [np.arange(n_) for n_ in lens]) if len(lens) else np.zeros(0, dtype=np.int64)).to(self.device),
                         None, T.IntegerType())
-                res[k] = C.from_numpy(np.array(flat, dtype=object) if flat and isinstance(flat[0], str)
-                                      else np.array(flat), self.device) if flat else C.StringColumn(
-                                          np.array([], dtype=object))
+                has_none = any(x is None for x in flat)
+                res[k] = C.from_numpy(np.array(flat, dtype=object) if flat and (has_none or isinstance(
+                    next((x for x in flat if x is not None), ""), str)) else np.array(flat), self.device) \
+                    if flat else C.StringColumn(np.array([], dtype=object))
             else:
                 res[k] = c.take(idx.to(c.data.device) if isinstance(c, C.NumericColumn) else idx)
         return self._new(res, len(flat))

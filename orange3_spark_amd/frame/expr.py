@@ -410,7 +410,11 @@ class Agg:
         return self._name
 
     def alias(self, name):
-        return Agg(self.fn, self.arg, name, self.distinct)
+        out = Agg(self.fn, self.arg, name, self.distinct)
+        for extra in ("arg2", "param"):            # second column / parameter of corr, percentile, ...
+            if hasattr(self, extra):
+                setattr(out, extra, getattr(self, extra))
+        return out
 
     def over(self, window):
         """Aggregate over a window frame (``sum("x").over(Window.partitionBy(...))``)."""

@@ -160,7 +160,18 @@ def aggregate(df, keys: list, aggs: list):
             host_parts[tag] = [(g_, 0, x_) for g_, x_ in zip(gg, vv)]
             host_tags.add(tag)
             continue
-        if a.distinct or a.fn in ("collect_list", "collect_set", "first", "last") or \
+        if a.fn in ("corr", "covar_pop", "covar_samp") and isinstance(vals, C.NumericColumn):
+            # co-moments of the rows where both columns are valid: n, Sx, Sy, Sxx, Syy, Sxy
+            x, okx = _values_valid(vals, dev)
+            yv, oky = _values_valid(a.arg2.eval(df), dev)
+            ok = okx & oky
+            x, yv = torch.where(ok, x, torch.zeros_like(x)), torch.where(ok, yv, torch.zeros_like(yv))
+            z = lambda v: torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, v)  # noqa: E731
+            parts[tag + "n"] = z(ok.double())
+            for sfx, v in (("s", x), ("t", yv), ("q", x * x), ("r", yv * yv), ("p", x * yv)):
+                parts[tag + sfx] = z(v)
+            continue
+        if a.distinct or a.fn in ("collect_list", "collect_set", "first", "last", "percentile") or \
                 not isinstance(vals, C.NumericColumn):
             # host path: (group, value) pairs or per-group python reductions
             py = vals.to_pylist() if not isinstance(vals, C.HostColumn) else list(vals.values)
@@ -172,10 +183,14 @@ def aggregate(df, keys: list, aggs: list):
         x, ok = _values_valid(vals, dev)
         cnt = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, ok.double())
         parts[tag + "n"] = cnt
-        if a.fn in ("sum", "avg", "stddev", "variance"):
+        moments = ("stddev", "variance", "stddev_pop", "var_pop", "skewness", "kurtosis")
+        if a.fn in ("sum", "avg") + moments:
             parts[tag + "s"] = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, x)
-        if a.fn in ("stddev", "variance"):
+        if a.fn in moments:
             parts[tag + "q"] = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, x * x)
+        if a.fn in ("skewness", "kurtosis"):
+            parts[tag + "c"] = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, x * x * x)
+            parts[tag + "f"] = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, x * x * x * x)
         if a.fn in ("min", "max"):
             fill = math.inf if a.fn == "min" else -math.inf
             src = torch.where(ok, x, torch.full_like(x, fill))
@@ -265,6 +280,29 @@ def _final(a, tag, m):
         mean = m[tag + "s"] / cnt
         var = max((m[tag + "q"] - cnt * mean * mean) / (cnt - 1), 0.0)
         return math.sqrt(var) if a.fn == "stddev" else var
+    if a.fn in ("stddev_pop", "var_pop"):
+        mean = m[tag + "s"] / cnt
+        var = max(m[tag + "q"] / cnt - mean * mean, 0.0)
+        return math.sqrt(var) if a.fn == "stddev_pop" else var
+    if a.fn in ("skewness", "kurtosis"):
+        mu = m[tag + "s"] / cnt
+        m2 = max(m[tag + "q"] / cnt - mu * mu, 0.0)
+        if m2 == 0.0:
+            return None
+        if a.fn == "skewness":
+            m3 = m[tag + "c"] / cnt - 3 * mu * m[tag + "q"] / cnt + 2 * mu ** 3
+            return m3 / m2 ** 1.5
+        m4 = (m[tag + "f"] / cnt - 4 * mu * m[tag + "c"] / cnt + 6 * mu * mu * m[tag + "q"] / cnt - 3 * mu ** 4)
+        return m4 / (m2 * m2) - 3.0                       # excess kurtosis, like Spark
+    if a.fn in ("corr", "covar_pop", "covar_samp"):
+        sx, sy = m[tag + "s"], m[tag + "t"]
+        cxy = m[tag + "p"] - sx * sy / cnt
+        if a.fn == "covar_pop":
+            return cxy / cnt
+        if a.fn == "covar_samp":
+            return cxy / (cnt - 1) if cnt > 1 else None
+        cxx, cyy = m[tag + "q"] - sx * sx / cnt, m[tag + "r"] - sy * sy / cnt
+        return cxy / math.sqrt(cxx * cyy) if cxx > 0 and cyy > 0 else None
     raise TypeError(f"unsupported aggregate {a.fn}")
 
 
@@ -290,6 +328,11 @@ def _host_final(a, pairs):
         return out
     if not nn:
         return None
+    if a.fn == "percentile":
+        vs = sorted(nn)
+        ps = a.param if isinstance(a.param, (list, tuple)) else [a.param]
+        res = [vs[min(len(vs) - 1, max(0, math.ceil(p * len(vs)) - 1))] for p in ps]
+        return res if isinstance(a.param, (list, tuple)) else res[0]
     if a.distinct:
         nn = list({_hashable(v): v for v in nn}.values())
     if a.fn == "min":
@@ -306,9 +349,10 @@ def _host_final(a, pairs):
 def _result_column(a, res):
     if a.fn == "count":
         return C.NumericColumn(torch.tensor(res, dtype=torch.int64))
-    if a.fn in ("collect_list", "collect_set"):
+    if a.fn in ("collect_list", "collect_set") or (a.fn == "percentile" and isinstance(a.param, (list, tuple))):
         arr = np.empty(len(res), dtype=object)
-        arr[:] = res
+        for i, r in enumerate(res):        # element-wise: equal-length lists must not broadcast
+            arr[i] = r
         return C.ArrayColumn(arr)
     if all(r is None or isinstance(r, (int, float, bool)) for r in res):
         arr = np.array([np.nan if r is None else r for r in res], dtype=np.float64)

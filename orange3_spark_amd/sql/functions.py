@@ -262,7 +262,11 @@ def spark_partition_id():
 # ----------------------------------------------------------------------------- dates
 def _dates(vals):
     import pandas as pd
-    return pd.to_datetime(pd.Series(vals, dtype=object), errors="coerce")
+    ser = pd.Series(vals, dtype=object)
+    try:                                    # rows may mix dates and timestamps
+        return pd.to_datetime(ser, errors="coerce", format="mixed")
+    except (TypeError, ValueError):
+        return pd.to_datetime(ser, errors="coerce")
 
 
 def _date_map(name, fn, c, kind="int"):
@@ -335,7 +339,8 @@ def array(*cols):
         n = len(df)
         vals = [_host(e.eval(df), n) for e in es]
         arr = np.empty(n, dtype=object)
-        arr[:] = [list(r) for r in zip(*vals)]
+        for i, r in enumerate(zip(*vals) if vals else ((),) * n):
+            arr[i] = list(r)
         return C.ArrayColumn(arr)
     return Expr(f, f"array({', '.join(e.name for e in es)})", _refs(*es))
 
@@ -429,3 +434,536 @@ from .window import (Window, cume_dist, dense_rank, lag, lead, nth_value, ntile,
 
 __all__ = [n for n in dir() if not n.startswith("_") and n not in ("annotations", "hashlib", "math", "re", "np",
                                                                      "torch", "C", "E", "T")]
+
+
+# ============================================================================ more of the
+# pyspark.sql.functions surface (strings / dates / JSON / arrays / maps / math / nulls /
+# statistical aggregates).  Host functions run over the rank's slice; the moment and
+# co-moment aggregates run as device partial sums merged across ranks (frame/groupby.py).
+import base64 as _b64  # noqa: E402
+import binascii as _binascii  # noqa: E402
+import json as _json  # noqa: E402
+import zlib as _zlib  # noqa: E402
+
+
+def _nn(v):
+    return v is not None and not (isinstance(v, float) and math.isnan(v))
+
+
+# ---- strings
+def substring_index(c, delim: str, count: int):
+    def f(s):
+        parts = str(s).split(delim)
+        if count > 0:
+            return delim.join(parts[:count])
+        if count < 0:
+            return delim.join(parts[count:])
+        return ""
+    return _host_map("substring_index", f, c)
+
+
+def format_string(format: str, *cols):  # noqa: A002
+    py = re.sub(r"%(\d+)\$", r"%", format)                   # Java positional args unsupported -> sequential
+    return _host_map("format_string", lambda *v: py % tuple(v), *cols)
+
+
+def translate(c, matching: str, replace: str):
+    table = {ord(m): (replace[i] if i < len(replace) else None) for i, m in enumerate(matching)}
+    return _host_map("translate", lambda s: str(s).translate(table), c)
+
+
+def levenshtein(left, right):
+    def lev(a, b):
+        a, b = str(a), str(b)
+        prev = list(range(len(b) + 1))
+        for i, ca in enumerate(a, 1):
+            cur = [i]
+            for j, cb in enumerate(b, 1):
+                cur.append(builtins.min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (ca != cb)))
+            prev = cur
+        return prev[-1]
+    return _host_map("levenshtein", lev, left, right, kind="int")
+
+
+def soundex(c):
+    codes = {**dict.fromkeys("BFPV", "1"), **dict.fromkeys("CGJKQSXZ", "2"), **dict.fromkeys("DT", "3"),
+             "L": "4", **dict.fromkeys("MN", "5"), "R": "6"}
+
+    def sx(s):
+        s = "".join(ch for ch in str(s).upper() if ch.isalpha())
+        if not s:
+            return ""
+        out, last = s[0], codes.get(s[0], "")
+        for ch in s[1:]:
+            d = codes.get(ch, "")
+            if d and d != last:
+                out += d
+            if ch not in "HW":
+                last = d
+        return (out + "000")[:4]
+    return _host_map("soundex", sx, c)
+
+
+def ascii(c):  # noqa: A001
+    return _host_map("ascii", lambda s: ord(str(s)[0]) if str(s) else 0, c, kind="int")
+
+
+def base64(c):
+    return _host_map("base64", lambda s: _b64.b64encode(s if isinstance(s, bytes) else str(s).encode()).decode(), c)
+
+
+def unbase64(c):
+    return _host_map("unbase64", lambda s: _b64.b64decode(str(s)).decode("utf-8", "replace"), c)
+
+
+def hex(c):  # noqa: A001
+    def h(v):
+        if isinstance(v, (int, float)) and not isinstance(v, bool) and float(v).is_integer():
+            return format(int(v) & 0xFFFFFFFFFFFFFFFF, "X") if int(v) < 0 else format(int(v), "X")
+        return _binascii.hexlify(str(v).encode()).decode().upper()
+    return _host_map("hex", h, c)
+
+
+def unhex(c):
+    return _host_map("unhex", lambda s: _binascii.unhexlify(str(s)).decode("utf-8", "replace"), c)
+
+
+def conv(c, fromBase: int, toBase: int):
+    digits = "0123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ"
+
+    def cv(s):
+        n = int(str(s).strip(), fromBase)
+        if n == 0:
+            return "0"
+        neg, n, out = n < 0, builtins.abs(n), ""
+        while n:
+            n, r = divmod(n, builtins.abs(toBase))
+            out = digits[r] + out
+        return ("-" if neg else "") + out
+    return _host_map("conv", cv, c)
+
+
+def bin(c):  # noqa: A001
+    return _host_map("bin", lambda v: format(int(v) & 0xFFFFFFFFFFFFFFFF if int(v) < 0 else int(v), "b"), c)
+
+
+def crc32(c):
+    return _host_map("crc32", lambda s: _zlib.crc32(s if isinstance(s, bytes) else str(s).encode()), c, kind="int")
+
+
+def xxhash64(*cols):
+    """64-bit xxHash of the values' UTF-8 text (seed 42 like Spark; parity with Spark's binary
+    encoding of non-string types is not pinned)."""
+    import xxhash as _xx
+
+    def h(*v):
+        x = _xx.xxh64(seed=42)
+        for a in v:
+            x.update(str(a).encode())
+        u = x.intdigest()
+        return u - (1 << 64) if u >= (1 << 63) else u
+    return _host_map("xxhash64", h, *cols, kind="int")
+
+
+def locate(substr: str, c, pos: int = 1):
+    return _host_map("locate", lambda s: str(s).find(substr, builtins.max(pos - 1, 0)) + 1, c, kind="int")
+
+
+# ---- nulls
+def nvl(c1, c2):
+    return coalesce(_e(c1), _e(c2))
+
+
+ifnull = nvl
+
+
+def nullif(c1, c2):
+    a, b = _e(c1), _e(c2)
+
+    def f(df):
+        n = len(df)
+        x, y = _host(a.eval(df), n), _host(b.eval(df), n)
+        out = [None if (u is not None and v is not None and u == v) else u for u, v in zip(x, y)]
+        if all(v is None or isinstance(v, (int, float)) for v in out):
+            return _num_out(out, torch.float64, df.device)
+        return _str_out(out)
+    return Expr(f, f"nullif({a.name}, {b.name})", _refs(a, b))
+
+
+# ---- math
+def expm1(c): return _num_map("EXPM1", torch.expm1, c)
+def factorial(c): return _host_map("factorial", lambda v: math.factorial(int(v)) if 0 <= int(v) <= 20 else None,
+                                   c, kind="int")
+def shiftleft(c, numBits: int): return _host_map("shiftleft", lambda v: int(v) << numBits, c, kind="int")
+def shiftright(c, numBits: int): return _host_map("shiftright", lambda v: int(v) >> numBits, c, kind="int")
+def bitwise_not(c): return _host_map("bitwise_not", lambda v: ~int(v), c, kind="int")
+
+
+bitwiseNOT = bitwise_not
+shiftLeft, shiftRight = shiftleft, shiftright
+
+
+# ---- dates / timestamps
+def _java_fmt(fmt: str) -> str:
+    return (fmt.replace("yyyy", "%Y").replace("yy", "%y").replace("MM", "%m").replace("dd", "%d")
+            .replace("HH", "%H").replace("mm", "%M").replace("ss", "%S"))
+
+
+def to_timestamp(c, format=None):  # noqa: A002
+    e = _e(c)
+
+    def f(df):
+        import pandas as pd
+        vals = pd.Series(_host(e.eval(df), len(df)), dtype=object)
+        s = pd.to_datetime(vals, format=_java_fmt(format) if format else None, errors="coerce")
+        return _str_out([None if pd.isna(v) else v.strftime("%Y-%m-%d %H:%M:%S") for v in s])
+    return Expr(f, f"to_timestamp({e.name})", e.refs)
+
+
+def unix_timestamp(c=None, format: str = "yyyy-MM-dd HH:mm:ss"):  # noqa: A002
+    if c is None:
+        import time as _t
+        now = int(_t.time())
+        return Expr(lambda df: _num_out([now] * len(df), torch.int64, df.device), "unix_timestamp()")
+    e = _e(c)
+
+    def f(df):
+        import pandas as pd
+        s = pd.to_datetime(pd.Series(_host(e.eval(df), len(df)), dtype=object), format=_java_fmt(format),
+                           errors="coerce")
+        return _num_out([None if pd.isna(v) else int(v.timestamp()) for v in s], torch.int64, df.device)
+    return Expr(f, f"unix_timestamp({e.name})", e.refs)
+
+
+def from_unixtime(c, format: str = "yyyy-MM-dd HH:mm:ss"):  # noqa: A002
+    import datetime as _dt
+    py = _java_fmt(format)
+    return _host_map("from_unixtime", lambda v: _dt.datetime.utcfromtimestamp(int(v)).strftime(py), c)
+
+
+def date_trunc(format: str, c):  # noqa: A002
+    unit = format.lower()
+    freq = {"year": "YS", "yyyy": "YS", "yy": "YS", "month": "MS", "mon": "MS", "mm": "MS", "day": "D", "dd": "D",
+            "hour": "h", "minute": "min", "second": "s", "week": "W-MON", "quarter": "QS"}.get(unit, "D")
+
+    def trunc_(s):
+        if freq in ("YS", "MS", "QS"):
+            p = {"YS": "Y", "MS": "M", "QS": "Q"}[freq]
+            return s.dt.to_period(p).dt.start_time
+        if freq == "W-MON":
+            return (s - __import__("pandas").to_timedelta(s.dt.dayofweek, unit="D")).dt.normalize()
+        return s.dt.floor(freq)
+    return _date_map("date_trunc", lambda s: trunc_(s).dt.strftime("%Y-%m-%d %H:%M:%S").where(s.notna(), None), c,
+                     kind="str")
+
+
+def trunc(c, format: str):  # noqa: A002
+    return _date_map("trunc", lambda s: date_trunc_series(s, format).dt.strftime("%Y-%m-%d").where(s.notna(), None),
+                     c, kind="str")
+
+
+def date_trunc_series(s, format):  # noqa: A002
+    p = {"year": "Y", "yyyy": "Y", "yy": "Y", "month": "M", "mon": "M", "mm": "M", "quarter": "Q"}.get(
+        format.lower(), "M")
+    return s.dt.to_period(p).dt.start_time
+
+
+def weekofyear(c): return _date_map("weekofyear", lambda s: s.dt.isocalendar().week.astype("float"), c)
+def quarter(c): return _date_map("quarter", lambda s: s.dt.quarter.astype("float"), c)
+
+
+def last_day(c):
+    return _date_map("last_day", lambda s: (s + __import__("pandas").offsets.MonthEnd(0)).dt.strftime("%Y-%m-%d")
+                     .where(s.notna(), None), c, kind="str")
+
+
+def next_day(c, dayOfWeek: str):
+    import pandas as pd
+    names = ["mo", "tu", "we", "th", "fr", "sa", "su"]
+    target = names.index(dayOfWeek.lower()[:2])
+    return _date_map("next_day", lambda s: (s + pd.to_timedelta(((target - s.dt.dayofweek - 1) % 7) + 1, unit="D"))
+                     .dt.strftime("%Y-%m-%d").where(s.notna(), None), c, kind="str")
+
+
+def add_months(c, months: int):
+    import pandas as pd
+    return _date_map("add_months", lambda s: (s + pd.DateOffset(months=months)).dt.strftime("%Y-%m-%d")
+                     .where(s.notna(), None), c, kind="str")
+
+
+def months_between(date1, date2, roundOff: bool = True):
+    a, b = _e(date1), _e(date2)
+
+    def f(df):
+        n = len(df)
+        x, y = _dates(_host(a.eval(df), n)), _dates(_host(b.eval(df), n))
+        out = []
+        for u, v in zip(x, y):
+            if u is None or v is None or str(u) == "NaT" or str(v) == "NaT":
+                out.append(None)
+                continue
+            m = (u.year - v.year) * 12 + (u.month - v.month)
+            if not (u.day == v.day or (u.is_month_end and v.is_month_end)):
+                m += (u.day - v.day) / 31.0 + ((u.hour * 3600 + u.minute * 60 + u.second) -
+                                             (v.hour * 3600 + v.minute * 60 + v.second)) / (31.0 * 86400)
+            out.append(round(m, 8) if roundOff else m)
+        return _num_out(out, torch.float64, df.device)
+    return Expr(f, f"months_between({a.name}, {b.name})", _refs(a, b))
+
+
+def current_timestamp():
+    import datetime
+    t = datetime.datetime.now().strftime("%Y-%m-%d %H:%M:%S")
+    return Expr(lambda df: _str_out([t] * len(df)), "current_timestamp()")
+
+
+now = current_timestamp
+
+
+def input_file_name():
+    """Files are not tracked per row by this engine's readers: always the empty string."""
+    return Expr(lambda df: _str_out([""] * len(df)), "input_file_name()")
+
+
+# ---- JSON
+def to_json(c, options=None):
+    def tj(v):
+        if hasattr(v, "asDict"):
+            v = v.asDict(recursive=True)
+        if hasattr(v, "toArray"):
+            v = np.asarray(v.toArray()).tolist()
+        return _json.dumps(v, separators=(",", ":"), default=str)
+    return _host_map("to_json", tj, c)
+
+
+def from_json(c, schema, options=None):
+    """JSON text -> struct (a Row of the schema's fields) or, without field info, a dict."""
+    from ..frame.dataframe import Row
+    try:
+        st = T.parse_type(schema) if isinstance(schema, str) else schema
+        names = [f.name for f in st.fields]
+    except Exception:  # noqa: BLE001 - schema forms the type parser does not know: keep dicts
+        names = None
+
+    def fj(s):
+        try:
+            d = _json.loads(str(s))
+        except ValueError:
+            return None
+        if names and isinstance(d, dict):
+            return Row._make(names, [d.get(n) for n in names])
+        return d
+    return _host_map("from_json", fj, c, kind="array")
+
+
+def get_json_object(c, path: str):
+    """JSONPath subset: ``$.a.b``, ``$.a[0]``, ``$['a']``."""
+    toks = re.findall(r"\.([A-Za-z_][\w]*)|\[(\d+)\]|\['([^']+)'\]", path)
+
+    def g(s):
+        try:
+            v = _json.loads(str(s))
+        except ValueError:
+            return None
+        for name, idx, qname in toks:
+            if name or qname:
+                if not isinstance(v, dict) or (name or qname) not in v:
+                    return None
+                v = v[name or qname]
+            else:
+                if not isinstance(v, list) or int(idx) >= len(v):
+                    return None
+                v = v[int(idx)]
+        return v if isinstance(v, str) else _json.dumps(v, separators=(",", ":"))
+    return _host_map("get_json_object", g, c)
+
+
+# ---- structs and maps
+def struct(*cols):
+    from ..frame.dataframe import Row
+    es = [_e(a) for a in (cols[0] if len(cols) == 1 and isinstance(cols[0], (list, tuple)) else cols)]
+
+    def f(df):
+        n = len(df)
+        vals = [_host(e.eval(df), n) for e in es]
+        names = [e.name for e in es]
+        arr = np.empty(n, dtype=object)
+        arr[:] = [Row._make(names, list(r)) for r in zip(*vals)]
+        return C.ArrayColumn(arr)
+    return Expr(f, f"struct({', '.join(e.name for e in es)})", _refs(*es))
+
+
+def create_map(*cols):
+    es = [_e(a) for a in (cols[0] if len(cols) == 1 and isinstance(cols[0], (list, tuple)) else cols)]
+
+    def f(df):
+        n = len(df)
+        vals = [_host(e.eval(df), n) for e in es]
+        arr = np.empty(n, dtype=object)
+        arr[:] = [{r[i]: r[i + 1] for i in range(0, len(r) - 1, 2)} for r in zip(*vals)]
+        return C.ArrayColumn(arr)
+    return Expr(f, f"map({', '.join(e.name for e in es)})", _refs(*es))
+
+
+def map_keys(c): return _host_map("map_keys", lambda m: list(m.keys()), c, kind="array")
+def map_values(c): return _host_map("map_values", lambda m: list(m.values()), c, kind="array")
+
+
+# ---- arrays
+def array_join(c, delimiter: str, null_replacement=None):
+    return _host_map("array_join", lambda v: delimiter.join(
+        str(x) if x is not None else null_replacement for x in v if x is not None or null_replacement is not None), c)
+
+
+def array_position(c, value):
+    return _host_map("array_position", lambda v: (list(v).index(value) + 1) if value in v else 0, c, kind="int")
+
+
+def array_remove(c, element):
+    return _host_map("array_remove", lambda v: [x for x in v if x != element], c, kind="array")
+
+
+def arrays_zip(*cols):
+    return _host_map("arrays_zip", lambda *vs: [list(t) for t in __import__("itertools").zip_longest(*vs)], *cols,
+                     kind="array")
+
+
+def flatten(c):
+    return _host_map("flatten", lambda v: [x for sub in v if sub is not None for x in sub], c, kind="array")
+
+
+def slice(x, start: int, length: int):  # noqa: A001
+    def sl(v):
+        v = list(v)
+        b = start - 1 if start > 0 else len(v) + start
+        return v[builtins.max(b, 0):builtins.max(b, 0) + length]
+    return _host_map("slice", sl, x, kind="array")
+
+
+def sequence(start, stop, step=None):
+    es = [_e(start), _e(stop)] + ([_e(step)] if step is not None else [])
+
+    def seq(a, b, s=None):
+        a, b = int(a), int(b)
+        s = int(s) if s is not None else (1 if b >= a else -1)
+        return list(range(a, b + (1 if s > 0 else -1), s))
+    return _host_map("sequence", seq, *es, kind="array")
+
+
+def array_union(a, b):
+    return _host_map("array_union", lambda x, y: list(dict.fromkeys(list(x) + list(y))), a, b, kind="array")
+
+
+def array_intersect(a, b):
+    return _host_map("array_intersect", lambda x, y: [v for v in dict.fromkeys(x) if v in set(y)], a, b,
+                     kind="array")
+
+
+def array_except(a, b):
+    return _host_map("array_except", lambda x, y: [v for v in dict.fromkeys(x) if v not in set(y)], a, b,
+                     kind="array")
+
+
+def array_max(c):
+    return _host_map("array_max", lambda v: builtins.max((x for x in v if x is not None), default=None), c,
+                     kind="float")
+
+
+def array_min(c):
+    return _host_map("array_min", lambda v: builtins.min((x for x in v if x is not None), default=None), c,
+                     kind="float")
+
+
+def array_sort(c):
+    return _host_map("array_sort", lambda v: sorted((x for x in v if x is not None)) + [x for x in v if x is None],
+                     c, kind="array")
+
+
+def explode_outer(c):
+    """explode that keeps rows whose array is empty or null (one null element)."""
+    e = _e(c)
+    out = Expr(lambda df: e.eval(df), "col", e.refs)
+    out._generator = "explode_outer"
+    return out
+
+
+def posexplode_outer(c):
+    e = _e(c)
+    out = Expr(lambda df: e.eval(df), "col", e.refs)
+    out._generator = "posexplode_outer"
+    return out
+
+
+# ---- sorting helpers
+def asc_nulls_first(c): return _e(c).asc_nulls_first()
+def asc_nulls_last(c): return _e(c).asc_nulls_last()
+def desc_nulls_first(c): return _e(c).desc_nulls_first()
+def desc_nulls_last(c): return _e(c).desc_nulls_last()
+
+
+# ---- statistical aggregates (device partial moments, merged across ranks)
+def stddev_pop(c): return Agg("stddev_pop", _e(c), f"stddev_pop({_e(c).name})")
+def var_pop(c): return Agg("var_pop", _e(c), f"var_pop({_e(c).name})")
+def skewness(c): return Agg("skewness", _e(c), f"skewness({_e(c).name})")
+def kurtosis(c): return Agg("kurtosis", _e(c), f"kurtosis({_e(c).name})")
+
+
+def _agg2(fn, a, b):
+    x, y = _e(a), _e(b)
+    out = Agg(fn, x, f"{fn}({x.name}, {y.name})")
+    out.arg2 = y
+    return out
+
+
+def corr(col1, col2): return _agg2("corr", col1, col2)
+def covar_pop(col1, col2): return _agg2("covar_pop", col1, col2)
+def covar_samp(col1, col2): return _agg2("covar_samp", col1, col2)
+
+
+def approx_count_distinct(c, rsd: float = 0.05):
+    """Exact distinct count (device dedupe) -- within any ``rsd``."""
+    return Agg("count", _e(c), f"approx_count_distinct({_e(c).name})", distinct=True)
+
+
+approxCountDistinct = approx_count_distinct
+
+
+def percentile_approx(c, percentage, accuracy: int = 10000):
+    """Exact percentile(s): the smallest value v with at least ``p`` of the group <= v (Spark's
+    definition of its approximation target)."""
+    out = Agg("percentile", _e(c), f"percentile_approx({_e(c).name}, {percentage}, {accuracy})")
+    out.param = percentage
+    return out
+
+
+approx_percentile = percentile_approx
+
+
+def pandas_udf(f=None, returnType=None, functionType=None):
+    """Vectorised UDF: ``f(pandas.Series, ...) -> pandas.Series`` applied to the rank's whole
+    slice at once (scalar pandas UDF)."""
+    def wrap(fn):
+        rt = T.parse_type(returnType) if returnType is not None else T.DoubleType()
+
+        def call(*cols):
+            es = [_e(a) for a in cols]
+
+            def ev(df):
+                import pandas as pd
+                n = len(df)
+                series = [pd.Series(_host(e.eval(df), n)) for e in es]
+                res = pd.Series(fn(*series)).tolist()
+                if isinstance(rt, T.NumericType):
+                    return _num_out([None if not _nn(v) else v for v in res],
+                                    torch.int64 if isinstance(rt, (T.IntegerType, T.LongType)) else torch.float64,
+                                    df.device)
+                return _str_out(res)
+            return Expr(ev, f"{getattr(fn, '__name__', 'pandas_udf')}({', '.join(e.name for e in es)})",
+                        _refs(*es))
+        call.func, call.returnType = fn, rt
+        return call
+    if f is not None and callable(f):
+        return wrap(f)
+    if f is not None and returnType is None:
+        returnType = f
+    return wrap

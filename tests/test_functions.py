@@ -110,3 +110,64 @@ def test_ml_functions_vector_array_roundtrip():
     assert len(dense[0]) == 16 and sum(dense[0]) == 3.0 and sum(dense[1]) == 1.0
     pred = predict_batch_udf(lambda: (lambda x: x.sum(axis=1)), return_type="double", batch_size=2)
     assert [r.p for r in df.select(pred("v").alias("p")).collect()] == [4.0, 6.0, -1.25]
+
+
+def test_extended_function_surface():
+    import json as _json
+    import math
+    import numpy as np
+    import pandas as pd
+    from scipy import stats
+    from orange3_spark_amd import Session, SessionConf
+    import orange3_spark_amd.sql.functions as F
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    df = s.createDataFrame(pd.DataFrame({
+        "s": ["a.b.c", "Robert", "hello"], "d": ["2024-01-31", "2024-02-15 10:30:00", "2023-12-01"],
+        "j": ['{"a": {"b": [1, 2]}, "c": "x"}', '{"a": {"b": [3]}}', "not json"],
+        "n": [5, -3, 10], "t": ["x", "x", "y"]}))
+    r = df.select(
+        F.substring_index("s", ".", 2).alias("si"), F.soundex("s").alias("sx"), F.levenshtein("s", "t").alias("lv"),
+        F.ascii("s").alias("asc"), F.base64("t").alias("b64"), F.hex("n").alias("hx"), F.conv("n", 10, 2).alias("cv"),
+        F.crc32("t").alias("crc"), F.translate("s", "abc", "xy").alias("tr"), F.locate("l", "s").alias("lc"),
+        F.format_string("%s-%d", "t", "n").alias("fs"), F.get_json_object("j", "$.a.b[0]").alias("gj"),
+        F.get_json_object("j", "$.c").alias("gc"), F.weekofyear("d").alias("wk"), F.quarter("d").alias("q"),
+        F.last_day("d").alias("ld"), F.add_months("d", 1).alias("am"), F.date_trunc("month", "d").alias("dt"),
+        F.unix_timestamp("d", "yyyy-MM-dd").alias("ut"), F.nvl(F.lit(None), "n").alias("nv"),
+        F.nullif("t", F.lit("x")).alias("ni"), F.factorial(F.lit(5)).alias("fa"), F.shiftleft("n", 2).alias("sl"),
+        F.xxhash64("t").alias("xx")).toPandas()
+    assert list(r.si) == ["a.b", "Robert", "hello"] and r.sx[1] == "R163" and r.lv[2] == 5
+    assert r.asc[0] == 97 and r.b64[0] == "eA==" and r.hx[0] == "5" and r.cv[0] == "101"
+    assert r.tr[0] == "x.y." and r.lc[2] == 3 and r.fs[0] == "x-5"
+    assert r.gj[0] == "1" and r.gj[1] == "3" and r.gj[2] is None and r.gc[0] == "x"
+    assert r.wk[0] == 5 and r.q[1] == 1 and r.ld[1] == "2024-02-29" and r.am[0] == "2024-02-29"
+    assert r.dt[1] == "2024-02-01 00:00:00" and r.nv[0] == 5 and r.ni[2] == "y" and (pd.isna(r.ni[0]) or r.ni[0] is None)
+    assert r.fa[0] == 120 and r.sl[0] == 20 and r.xx[0] == r.xx[1] != r.xx[2]
+    a = s.createDataFrame(pd.DataFrame({"k": [1, 2]})).select(
+        F.sequence(F.lit(1), F.lit(4)).alias("seq"), F.array(F.lit(3), F.lit(1), F.lit(3)).alias("arr"))
+    a = a.select("seq", "arr", F.array_join("arr", "|").alias("aj"), F.array_position("arr", 1).alias("ap"),
+                 F.array_remove("arr", 3).alias("ar"), F.slice("seq", 2, 2).alias("sc"),
+                 F.array_union("arr", "seq").alias("au"), F.array_intersect("arr", "seq").alias("ai"),
+                 F.array_except("seq", "arr").alias("ae"), F.array_max("seq").alias("mx"),
+                 F.array_sort("arr").alias("so"), F.arrays_zip("seq", "arr").alias("z"),
+                 F.to_json(F.struct("seq")).alias("tj"), F.map_keys(F.create_map(F.lit("a"), F.lit(1))).alias("mk"))
+    row = a.collect()[0]
+    assert row.seq == [1, 2, 3, 4] and row.aj == "3|1|3" and row.ap == 2 and row.ar == [1] and row.sc == [2, 3]
+    assert row.au == [3, 1, 2, 4] and row.ai == [3, 1] and row.ae == [2, 4] and row.mx == 4.0 and row.so == [1, 3, 3]
+    assert row.z[0] == [1, 3] and _json.loads(row.tj) == {"seq": [1, 2, 3, 4]} and row.mk == ["a"]
+    e = s.createDataFrame(pd.DataFrame({"id": [1, 2]})).withColumn(
+        "v", F.when(F.col("id") == 1, F.array(F.lit(7), F.lit(8))).otherwise(F.array()))
+    assert e.select("id", F.explode_outer("v").alias("x")).count() == 3
+    rng = np.random.default_rng(1)
+    pdf = pd.DataFrame({"x": rng.normal(size=400), "y": rng.normal(size=400)})
+    st = s.createDataFrame(pdf).agg(F.skewness("x").alias("sk"), F.kurtosis("x").alias("ku"),
+                                    F.corr("x", "y").alias("c"), F.covar_samp("x", "y").alias("cs"),
+                                    F.percentile_approx("x", [0.25, 0.75]).alias("q")).collect()[0]
+    assert math.isclose(st.sk, stats.skew(pdf.x), rel_tol=1e-9)
+    assert math.isclose(st.ku, stats.kurtosis(pdf.x), rel_tol=1e-9)
+    assert math.isclose(st.c, np.corrcoef(pdf.x, pdf.y)[0, 1], rel_tol=1e-9)
+    assert math.isclose(st.cs, np.cov(pdf.x, pdf.y)[0, 1], rel_tol=1e-9)
+    xs = np.sort(pdf.x.to_numpy())
+    assert st.q == [xs[99], xs[299]]
+    pu = F.pandas_udf(lambda v: v * 2, "double")
+    assert [r.p for r in s.createDataFrame(pd.DataFrame({"v": [1.0, 2.5]})).select(pu("v").alias("p")).collect()] \
+        == [2.0, 5.0]

@@ -161,7 +161,15 @@ def main():
     with open(os.path.join(DOC, "api", "ml_functions.md"), "w") as f:
         f.write(class_methods_page("`orange3_spark_amd.ml.functions`",
                                    [MF.vector_to_array, MF.array_to_vector, MF.predict_batch_udf]) + "\n")
-    index += ["- [RDD / SparkContext](api/rdd.md)", "- [`ml.functions`](api/ml_functions.md)"]
+    from orange3_spark_amd.sql import functions as SF
+    fns = sorted(n for n, f in vars(SF).items() if inspect.isfunction(f) and not n.startswith("_")
+                 and f.__module__ == SF.__name__)
+    with open(os.path.join(DOC, "api", "sql_functions.md"), "w") as f:
+        f.write("\n".join([f"# `orange3_spark_amd.sql.functions` ({len(fns)} functions)", "",
+                           "Column functions with `pyspark.sql.functions` names and semantics.", ""]
+                          + [f"- `{n}{inspect.signature(getattr(SF, n))}`" for n in fns]) + "\n")
+    index += ["- [RDD / SparkContext](api/rdd.md)", "- [`ml.functions`](api/ml_functions.md)",
+              "- [`sql.functions`](api/sql_functions.md)"]
     with open(os.path.join(DOC, "index.md"), "w") as f:
         f.write("\n".join(index) + "\n")
     print("wrote", DOC)
