@@ -115,6 +115,11 @@ class Catalog:
         return name in self._temp or os.path.isdir(self._table_path(name))
 
     def table(self, name: str) -> DataFrame:
+        if name.startswith("global_temp."):
+            from .frame.extras import _GLOBAL_TEMP
+            if name[12:] in _GLOBAL_TEMP:
+                return _GLOBAL_TEMP[name[12:]]
+            raise KeyError(f"Table or view not found: {name}")
         if name in self._temp:
             return self._temp[name]
         if name in self._cached:
@@ -144,6 +149,10 @@ class Catalog:
 
     def registerTempView(self, name: str, df: DataFrame) -> None:
         self._temp[name] = df
+
+    def dropGlobalTempView(self, name: str) -> bool:
+        from .frame.extras import _GLOBAL_TEMP
+        return _GLOBAL_TEMP.pop(name, None) is not None
 
     def dropTempView(self, name: str) -> bool:
         return self._temp.pop(name, None) is not None

@@ -26,7 +26,7 @@ import torch
 from . import column as C
 from . import expr as E
 from . import types as T
-from .extras import DataFrameExtras
+from .extras import DataFrameExtras, DataFrameExtras2
 
 
 class Row(tuple):
@@ -90,7 +90,7 @@ class StorageLevel:
     MEMORY_AND_DISK = "MEMORY_AND_DISK"
 
 
-class DataFrame(DataFrameExtras):
+class DataFrame(DataFrameExtras, DataFrameExtras2):
     def __init__(self, session, cols: "OrderedDict[str, C.Column]", nrows: int | None = None):
         self.session = session
         self._cols: OrderedDict = OrderedDict(cols)
@@ -228,6 +228,8 @@ class DataFrame(DataFrameExtras):
             return win.select(*[c if not (isinstance(c, str) and c == "*") else E.col(k)
                                 for c in cols for k in ([c] if not (isinstance(c, str) and c == "*")
                                                         else list(self.columns))])
+        if any(getattr(c, "_expand", False) for c in cols):           # colRegex results
+            cols = tuple(x for c in cols for x in (c if getattr(c, "_expand", False) else [c]))
         gens = [c for c in cols if getattr(c, "_generator", None)]
         if len(gens) > 1:
             raise ValueError("Only one generator (explode) allowed per select clause")

@@ -411,3 +411,190 @@ class DataFrameStatFunctions:
 
     def sampleBy(self, col, fractions, seed=None):
         return self.df.sampleBy(col, fractions, seed)
+
+
+class Observation:
+    """``pyspark.sql.Observation``: named metrics collected by ``df.observe``.  Frames are
+    materialised eagerly here, so the metrics are available as soon as ``observe``
+    returns (Spark fills them at the first action)."""
+
+    def __init__(self, name: str | None = None):
+        self.name = name or f"observation_{id(self):x}"
+        self._metrics = None
+
+    @property
+    def get(self) -> dict:
+        if self._metrics is None:
+            raise RuntimeError("observation has not been attached to a DataFrame")
+        return self._metrics
+
+
+_GLOBAL_TEMP: dict = {}     # ``global_temp`` database: views shared by every session of the process
+
+
+class DataFrameExtras2:
+    """Remaining pyspark ``DataFrame`` methods: grouping sets, regex column selection,
+    offset, observations, global temp views, schema coercion, Arrow batches and the
+    streaming no-ops of a batch engine."""
+
+    # ------------------------------------------------------------------ grouping sets
+    def rollup(self, *cols):
+        """Hierarchical subtotals: grouping sets (k1..kn), (k1..kn-1), ..., () ."""
+        from .grouping_sets import GroupingSets, rollup_sets
+        keys = _key_exprs(cols)
+        return GroupingSets(self, keys, rollup_sets(len(keys)))
+
+    def cube(self, *cols):
+        """All 2**n grouping sets of the keys."""
+        from .grouping_sets import GroupingSets, cube_sets
+        keys = _key_exprs(cols)
+        return GroupingSets(self, keys, cube_sets(len(keys)))
+
+    # ------------------------------------------------------------------ selection
+    def colRegex(self, colName: str):
+        """Columns whose name fully matches the (optionally back-quoted) regex; expands
+        in ``select``."""
+        import re
+        pat = colName[1:-1] if colName.startswith("`") and colName.endswith("`") else colName
+        rx = re.compile(pat)
+        names = [k for k in self.columns if rx.fullmatch(k)]
+        return _ColumnList(names)
+
+    def offset(self, num: int):
+        """Skip the first ``num`` rows of the global row order."""
+        off = self.row_offset()
+        start = max(0, min(self._n, num - off))
+        return self._take(torch.arange(start, self._n, dtype=torch.int64))
+
+    def observe(self, observation, *exprs):
+        """Compute the aggregate ``exprs`` over this frame into ``observation`` (an
+        :class:`Observation` or a name) and return the frame unchanged."""
+        if isinstance(observation, str):
+            observation = Observation(observation)
+        row = self.agg(*exprs).collect()[0]
+        observation._metrics = row.asDict()
+        self._observations = getattr(self, "_observations", {})
+        self._observations[observation.name] = observation
+        return self
+
+    # ------------------------------------------------------------------ views / session
+    @property
+    def sparkSession(self):
+        return self.session
+
+    @property
+    def isStreaming(self) -> bool:
+        return False
+
+    def createGlobalTempView(self, name: str):
+        if name in _GLOBAL_TEMP:
+            raise ValueError(f"Temporary view '{name}' already exists")
+        _GLOBAL_TEMP[name] = self
+
+    def createOrReplaceGlobalTempView(self, name: str):
+        _GLOBAL_TEMP[name] = self
+
+    def inputFiles(self) -> list:
+        """Files this frame was read from (empty for frames built in memory)."""
+        return list(getattr(self, "_input_files", []))
+
+    def sameSemantics(self, other) -> bool:
+        """True when both frames hold the same column objects in the same layout (frames
+        are materialised, so identical storage is identical semantics)."""
+        return self.semanticHash() == other.semanticHash()
+
+    def semanticHash(self) -> int:
+        return hash(tuple((k, id(c), len(c)) for k, c in self._cols.items()))
+
+    def withMetadata(self, columnName: str, metadata: dict):
+        out = self._new(OrderedDict(self._cols))
+        out._metadata = dict(getattr(self, "_metadata", {}))
+        out._metadata[columnName] = dict(metadata)
+        return out
+
+    def to(self, schema):
+        """Reorder / cast columns to ``schema`` (StructType or DDL string): columns are
+        matched by name, missing nullable columns raise like Spark."""
+        st = T.parse_schema(schema) if isinstance(schema, str) else schema
+        cols = []
+        for f in st.fields:
+            if f.name not in self._cols:
+                raise KeyError(f"column '{f.name}' not found")
+            cols.append(E.col(f.name).cast(f.dataType).alias(f.name))
+        return self.select(*cols)
+
+    # ------------------------------------------------------------------ arrow / streaming no-ops
+    def mapInArrow(self, func, schema):
+        """``func(iterator of pyarrow.RecordBatch) -> iterator of RecordBatch`` per rank."""
+        import pyarrow as pa
+        batch = pa.RecordBatch.from_pandas(self.toPandas_local(), preserve_index=False)
+        out = list(func(iter([batch])))
+        pdf = pa.Table.from_batches(out).to_pandas() if out else __import__("pandas").DataFrame()
+        return _frame_from_pandas(self, pdf, schema)
+
+    def withWatermark(self, eventTime: str, delayThreshold: str):
+        """Batch frames are complete: a watermark drops nothing."""
+        if eventTime not in self._cols:
+            raise KeyError(eventTime)
+        return self
+
+    def dropDuplicatesWithinWatermark(self, subset=None):
+        return self.dropDuplicates(subset)
+
+    def writeTo(self, table: str):
+        return DataFrameWriterV2(self, table)
+
+
+class DataFrameWriterV2:
+    """``df.writeTo(table)``: create / replace / append / overwrite a warehouse table."""
+
+    def __init__(self, df, table: str):
+        self.df, self.table = df, table
+        self._props: dict = {}
+
+    def using(self, provider):
+        return self
+
+    def option(self, key, value):
+        self._props[key] = value
+        return self
+
+    def options(self, **kw):
+        self._props.update(kw)
+        return self
+
+    def tableProperty(self, key, value):
+        return self.option(key, value)
+
+    def partitionedBy(self, *cols):
+        return self
+
+    def create(self):
+        self.df.session.catalog.saveAsTable(self.df, self.table, "error")
+
+    def replace(self):
+        if not self.df.session.catalog.tableExists(self.table):
+            raise KeyError(f"table {self.table} does not exist")
+        self.df.session.catalog.saveAsTable(self.df, self.table, "overwrite")
+
+    def createOrReplace(self):
+        self.df.session.catalog.saveAsTable(self.df, self.table, "overwrite")
+
+    def append(self):
+        self.df.session.catalog.saveAsTable(self.df, self.table, "append")
+
+    def overwrite(self, condition=None):
+        self.df.session.catalog.saveAsTable(self.df, self.table, "overwrite")
+
+    overwritePartitions = overwrite
+
+
+class _ColumnList(list):
+    """Result of ``colRegex``: a list of column names that ``select`` expands in place."""
+    _expand = True
+
+
+def _key_exprs(cols):
+    if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
+        cols = tuple(cols[0])
+    return [E.col(c) if isinstance(c, str) else c for c in cols]

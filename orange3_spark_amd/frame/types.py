@@ -155,6 +155,27 @@ def parse_type(t) -> DataType:
     raise ValueError(f"unknown data type {t!r}")
 
 
+def parse_schema(ddl: str) -> StructType:
+    """DDL schema string (``"a INT, b string"`` or ``"a: int, b: string"``) -> StructType."""
+    st = StructType()
+    depth, cur, parts = 0, "", []
+    for ch in ddl:                      # split on top-level commas (array<...> may nest)
+        depth += (ch == "<") - (ch == ">")
+        if ch == "," and depth == 0:
+            parts.append(cur)
+            cur = ""
+        else:
+            cur += ch
+    parts.append(cur)
+    for p in parts:
+        p = p.strip()
+        if not p:
+            continue
+        name, _, typ = p.replace(":", " ", 1).partition(" ")
+        st.add(name.strip().strip("`"), parse_type(typ.strip()))
+    return st
+
+
 def from_torch_dtype(dt: torch.dtype) -> DataType:
     return {
         torch.float64: DoubleType(), torch.float32: FloatType(), torch.float16: FloatType(),

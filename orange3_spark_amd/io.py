@@ -231,7 +231,25 @@ class DataFrameReader:
         return self
 
     def schema(self, schema):
+        """User schema: applied positionally (names + casts) to what the source yields."""
+        from .frame import types as T
+        self._schema = T.parse_schema(schema) if isinstance(schema, str) else schema
         return self
+
+    def _finish(self, df, paths):
+        import glob
+        files = []
+        for p in ([paths] if isinstance(paths, str) else list(paths or [])):
+            if os.path.isdir(p):
+                files += sorted(os.path.abspath(os.path.join(r, f)) for r, _, fs in os.walk(p) for f in fs
+                                if not f.startswith(("_", ".")))
+            else:
+                files += sorted(os.path.abspath(g) for g in glob.glob(p)) or [os.path.abspath(p)]
+        st = getattr(self, "_schema", None)
+        if st is not None and len(st.fields) == len(df.columns):
+            df = df.toDF(*st.names).to(st)
+        df._input_files = files
+        return df
 
     def load(self, path=None, format=None, **kw):
         fmt = format or self._format
@@ -251,24 +269,24 @@ class DataFrameReader:
 
     def parquet(self, *paths, columns=None):
         if len(paths) == 1:
-            return read_parquet(self.session, paths[0], columns)
+            return self._finish(read_parquet(self.session, paths[0], columns), paths)
         dfs = [read_parquet(self.session, p, columns) for p in paths]
         out = dfs[0]
         for d in dfs[1:]:
             out = out.union(d)
-        return out
+        return self._finish(out, paths)
 
     def csv(self, path, header=None, inferSchema=None, sep=None, **kw):
         h = self._opts.get("header", True) if header is None else header
         h = str(h).lower() in ("true", "1") if isinstance(h, str) else bool(h)
         i = self._opts.get("inferSchema", True) if inferSchema is None else inferSchema
         i = str(i).lower() in ("true", "1") if isinstance(i, str) else bool(i)
-        return read_csv(self.session, path, h, i, sep or self._opts.get("sep", ","))
+        return self._finish(read_csv(self.session, path, h, i, sep or self._opts.get("sep", ",")), path)
 
     def json(self, path):
         import pandas as pd
         pdf = pd.read_json(path, lines=True)
-        return self.session.createDataFrame(pdf)
+        return self._finish(self.session.createDataFrame(pdf), path)
 
     def table(self, name):
         return self.session.table(name)
@@ -292,7 +310,8 @@ class DataFrameReader:
             else:
                 parts = txt.split(lineSep) if lineSep else txt.splitlines()
                 vals.extend(parts)
-        return self.session.createDataFrame(pd.DataFrame({"value": pd.Series(vals, dtype=object)}))
+        return self._finish(self.session.createDataFrame(pd.DataFrame({"value": pd.Series(vals, dtype=object)})),
+                            files)
 
     def jdbc(self, url, table, column=None, lowerBound=None, upperBound=None, numPartitions=None,
              predicates=None, properties=None):

@@ -102,6 +102,8 @@ def run_select(session, s: Select) -> DataFrame:
             else:
                 keys.append((e, a))
         df = df.orderBy(*[k for k, _ in keys], ascending=[a for _, a in keys])
+    if s.offset is not None:
+        df = df.offset(s.offset)
     if s.limit is not None:
         df = df.limit(s.limit)
     if s.union is not None:
@@ -168,8 +170,17 @@ def _aggregate(df: DataFrame, s: Select) -> DataFrame:
         if isinstance(e, (AggCall, _AggExpr)):
             for a in _as_agg_expr(e).aggs:
                 aggs[a.text] = a
-    agg_objs = [E.Agg(a.fn, a.arg, a.text, a.distinct) for a in aggs.values()]
-    g = df.groupBy(*keys).agg(*agg_objs)
+    agg_objs = [a.built.alias(a.text) if a.built is not None else E.Agg(a.fn, a.arg, a.text, a.distinct)
+                for a in aggs.values()]
+    if s.grouping == "rollup":
+        g = df.rollup(*keys).agg(*agg_objs)
+    elif s.grouping == "cube":
+        g = df.cube(*keys).agg(*agg_objs)
+    elif s.grouping == "sets":
+        from ..frame.grouping_sets import GroupingSets
+        g = GroupingSets(df, keys, s.grouping_sets).agg(*agg_objs)
+    else:
+        g = df.groupBy(*keys).agg(*agg_objs)
     names = {k: k for k in aggs}
     if s.having is not None:
         g = g.filter(_as_agg_expr(s.having).build(names))

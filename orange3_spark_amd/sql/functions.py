@@ -376,6 +376,19 @@ def posexplode(c):
 def first(c, ignorenulls: bool = False): return Agg("first", _e(c), f"first({_e(c).name})")
 def last(c, ignorenulls: bool = False): return Agg("last", _e(c), f"last({_e(c).name})")
 def collect_list(c): return Agg("collect_list", _e(c), f"collect_list({_e(c).name})")
+
+
+def grouping(c):
+    """1 if ``c`` is aggregated away in this grouping set of a rollup / cube, else 0."""
+    return Agg("grouping", _e(c), f"grouping({_e(c).name})")
+
+
+def grouping_id(*cols):
+    """Bit vector of :func:`grouping` over ``cols`` (default: all grouping keys), first
+    column most significant."""
+    a = Agg("grouping_id", None, f"grouping_id({', '.join(_e(x).name for x in cols)})")
+    a.param = [_e(x).name for x in cols] or None
+    return a
 def collect_set(c): return Agg("collect_set", _e(c), f"collect_set({_e(c).name})")
 def stddev_samp(c): return stddev(c)
 def var_samp(c): return variance(c)

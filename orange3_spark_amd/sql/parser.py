@@ -68,6 +68,14 @@ class AggCall:
     arg: object             # Expr or None (count(*))
     distinct: bool = False
     text: str = ""
+    built: object = None    # prebuilt frame Agg (statistical / two-argument aggregates)
+
+
+# SQL aggregates built through sql.functions (arguments after the first are literals)
+_EXTRA_AGGS = {"first", "last", "collect_list", "collect_set", "stddev_pop", "var_pop", "skewness",
+               "kurtosis", "approx_count_distinct", "corr", "covar_pop", "covar_samp", "percentile_approx",
+               "percentile", "grouping", "grouping_id"}
+_TWO_COLUMN_AGGS = {"corr", "covar_pop", "covar_samp"}
 
 
 @dataclass
@@ -90,6 +98,9 @@ class Select:
     having: object = None
     order_by: list = field(default_factory=list)
     limit: int | None = None
+    offset: int | None = None
+    grouping: str | None = None          # "rollup" | "cube" | "sets"
+    grouping_sets: list | None = None    # index tuples into group_by (GROUPING SETS)
     distinct: bool = False
     union: object = None
     union_all: bool = False
@@ -123,6 +134,25 @@ class Parser:
             p = self.peek()
             raise SyntaxError(f"expected {val or kind} but found {p.val!r}")
         return t
+
+    def idw(self, *words) -> bool:
+        """Non-reserved words (ROLLUP, CUBE, SETS, OFFSET, ...) arrive as identifiers."""
+        for k, w in enumerate(words):
+            t = self.peek(k)
+            if not (t.kind == "id" and t.val.lower() == w):
+                return False
+        self.i += len(words)
+        return True
+
+    def _expr_list(self) -> list:
+        self.expect("op", "(")
+        out = []
+        if not self.accept("op", ")"):
+            out.append(self.expr())
+            while self.accept("op", ","):
+                out.append(self.expr())
+            self.expect("op", ")")
+        return out
 
     def kw(self, *words) -> bool:
         for k, w in enumerate(words):
@@ -215,9 +245,33 @@ class Parser:
         if self.kw("where"):
             s.where = self.expr()
         if self.kw("group", "by"):
-            s.group_by = [self.expr()]
-            while self.accept("op", ","):
-                s.group_by.append(self.expr())
+            if self.idw("rollup") or self.idw("cube"):
+                s.grouping = self.toks[self.i - 1].val.lower()
+                s.group_by = self._expr_list()
+            elif self.idw("grouping", "sets"):
+                self.expect("op", "(")
+                sets = []
+                while True:
+                    sets.append(self._expr_list() if self.peek().val == "(" else [self.expr()])
+                    if not self.accept("op", ","):
+                        break
+                self.expect("op", ")")
+                names: dict = {}
+                for st in sets:
+                    for e in st:
+                        names.setdefault(e.name, e)
+                order = list(names)
+                s.group_by = list(names.values())
+                s.grouping = "sets"
+                s.grouping_sets = [tuple(sorted(order.index(e.name) for e in st)) for st in sets]
+            else:
+                s.group_by = [self.expr()]
+                while self.accept("op", ","):
+                    s.group_by.append(self.expr())
+                if self.peek().kind == "kw" and self.peek().val == "with" and \
+                        self.peek(1).kind == "id" and self.peek(1).val.lower() in ("rollup", "cube"):
+                    self.i += 2
+                    s.grouping = self.toks[self.i - 1].val.lower()
         if self.kw("having"):
             s.having = self.expr(allow_agg=True)
         if self.kw("order", "by"):
@@ -226,6 +280,8 @@ class Parser:
                 s.order_by.append(self.order_item())
         if self.kw("limit"):
             s.limit = int(float(self.expect("num").val))
+        if self.idw("offset"):
+            s.offset = int(float(self.expect("num").val))
         if self.kw("union"):
             s.union_all = bool(self.kw("all"))
             s.union = self.select()
@@ -501,6 +557,12 @@ class Parser:
             while self.accept("op", ","):
                 args.append(self.or_expr())
             self.expect("op", ")")
+        if fn in _EXTRA_AGGS:
+            from . import functions as F
+            ncol = 2 if fn in _TWO_COLUMN_AGGS else (len(args) if fn == "grouping_id" else min(1, len(args)))
+            lits = [a.eval_literal() for a in args[ncol:]]
+            text = f"{fn}({', '.join(a.name for a in args)})"
+            return AggCall(fn, args[0] if args else None, False, text, getattr(F, fn)(*args[:ncol], *lits))
         f = {"sqrt": E.sqrt, "log": E.log, "ln": E.log, "exp": E.exp, "abs": E.abs, "isnan": E.isnan,
              "coalesce": E.coalesce, "log1p": E.log1p}.get(fn)
         if f is None:

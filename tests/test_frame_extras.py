@@ -183,3 +183,49 @@ def test_frame_ops_gpu_match_cpu(s):
             assert np.allclose([t[3] for t in a[k]], [t[3] for t in b[k]], rtol=1e-12)
         else:
             assert repr(a[k]) == repr(b[k]), k            # NaN-aware
+
+
+def test_rollup_cube_grouping_id_and_misc_surface(tmp_path):
+    import pandas as pd
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.sql import functions as F, Observation
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    pdf = pd.DataFrame({"a": ["x", "x", "y", "y", "y"], "b": [1, 2, 1, 1, 2], "v": [1.0, 2.0, 3.0, 4.0, 5.0]})
+    df = s.createDataFrame(pdf)
+    r = df.rollup("a", "b").agg(F.sum("v").alias("sv"), F.grouping_id().alias("g")).toPandas()
+    assert len(r) == 4 + 2 + 1
+    tot = r[r.g == 3]
+    assert len(tot) == 1 and tot.sv.iloc[0] == 15.0 and tot.a.iloc[0] is None
+    sub = r[r.g == 1].set_index("a").sv.to_dict()
+    assert sub == {"x": 3.0, "y": 12.0}
+    c = df.cube("a", "b").agg(F.count("v").alias("n"), F.grouping("a").alias("ga")).toPandas()
+    assert len(c) == 4 + 2 + 2 + 1
+    byb = c[(c.ga == 1) & c.b.notna()].set_index("b").n.to_dict()
+    assert byb == {1: 3, 2: 2}
+    # pandas reference for the full rollup
+    ref = pdf.groupby(["a", "b"]).v.sum().to_dict()
+    got = {(a, int(b)): v for a, b, v, g in zip(r.a, r.b, r.sv, r.g) if g == 0}
+    assert got == ref
+    # colRegex, offset, observe, to(schema), global temp views, writeTo, inputFiles
+    assert df.select(df.colRegex("`[ab]`")).columns == ["a", "b"]
+    assert [x.v for x in df.offset(3).collect()] == [4.0, 5.0]
+    ob = Observation("m")
+    assert df.observe(ob, F.max("v").alias("mx"), F.count("v").alias("n")) is df
+    assert ob.get == {"mx": 5.0, "n": 5}
+    t = df.to("v double, b bigint")
+    assert t.columns == ["v", "b"] and t.dtypes[1][1] in ("bigint", "long")
+    df.createOrReplaceGlobalTempView("gv")
+    assert s.table("global_temp.gv").count() == 5
+    assert s.catalog.dropGlobalTempView("gv")
+    s.conf.set("o3s.warehouse", str(tmp_path / "wh")) if hasattr(s.conf, "set") else None
+    df.write.parquet(str(tmp_path / "p"))
+    rd = s.read.parquet(str(tmp_path / "p"))
+    assert rd.inputFiles() and all(f.endswith(".parquet") for f in rd.inputFiles())
+    rs = s.read.schema("x string, y long, z double").parquet(str(tmp_path / "p"))
+    assert rs.columns == ["x", "y", "z"]
+    assert df.sparkSession is s and not df.isStreaming and df.sameSemantics(df)
+    assert df.withWatermark("b", "1 minute") is df
+    import pyarrow as pa
+    m = df.mapInArrow(lambda it: (pa.RecordBatch.from_pydict({"w": [x * 2 for x in b.column("v").to_pylist()]})
+                                  for b in it), "w double")
+    assert [r_.w for r_ in m.collect()] == [2.0, 4.0, 6.0, 8.0, 10.0]
