@@ -257,6 +257,13 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
         flat = [x for v in lists for x in v]
         res = OrderedDict()
         for k, c in out.items():
+            if k == name and getattr(g, "_inline", False):          # inline: struct fields -> columns
+                fields = list(next((x for x in flat if x is not None), Row()).__fields__)
+                for j, fname in enumerate(fields):
+                    vals = [None if x is None else x[j] for x in flat]
+                    obj = any(v is None or isinstance(v, (str, list, dict)) for v in vals)
+                    res[fname] = C.from_numpy(np.array(vals, dtype=object) if obj else np.array(vals), self.device)
+                continue
             if k == name:
                 if g._generator.startswith("posexplode"):
                     res["pos"] = C.NumericColumn(torch.from_numpy(np.concatenate(

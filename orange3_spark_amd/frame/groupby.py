@@ -171,7 +171,8 @@ def aggregate(df, keys: list, aggs: list):
             for sfx, v in (("s", x), ("t", yv), ("q", x * x), ("r", yv * yv), ("p", x * yv)):
                 parts[tag + sfx] = z(v)
             continue
-        if a.distinct or a.fn in ("collect_list", "collect_set", "first", "last", "percentile") or \
+        if a.distinct or a.fn in ("collect_list", "collect_set", "first", "last", "percentile", "median", "mode",
+                                  "product", "bool_and", "bool_or", "max_by", "min_by") or \
                 not isinstance(vals, C.NumericColumn):
             # host path: (group, value) pairs or per-group python reductions
             py = vals.to_pylist() if not isinstance(vals, C.HostColumn) else list(vals.values)
@@ -326,8 +327,37 @@ def _host_final(a, pairs):
                 seen.add(h)
                 out.append(v)
         return out
+    if a.fn in ("max_by", "min_by"):
+        # values are [ordering, value] pairs; rows with a null ordering are skipped
+        cand = [v for v in vals if v is not None and v[0] is not None
+                and not (isinstance(v[0], float) and math.isnan(v[0]))]
+        if not cand:
+            return None
+        pick = max if a.fn == "max_by" else min
+        return pick(cand, key=lambda v: v[0])[1]
     if not nn:
         return None
+    if a.fn == "median":
+        vs = sorted(float(v) for v in nn)
+        pos = 0.5 * (len(vs) - 1)
+        lo = int(math.floor(pos))
+        hi = min(lo + 1, len(vs) - 1)
+        return vs[lo] + (vs[hi] - vs[lo]) * (pos - lo)
+    if a.fn == "mode":
+        counts: dict = {}
+        for v in nn:
+            counts[_hashable(v)] = counts.get(_hashable(v), 0) + 1
+        best = max(counts.values())
+        return next(v for v in nn if counts[_hashable(v)] == best)      # first-seen among ties
+    if a.fn == "product":
+        out = 1.0
+        for v in nn:
+            out *= float(v)
+        return out
+    if a.fn == "bool_and":
+        return all(bool(v) for v in nn)
+    if a.fn == "bool_or":
+        return any(bool(v) for v in nn)
     if a.fn == "percentile":
         vs = sorted(nn)
         ps = a.param if isinstance(a.param, (list, tuple)) else [a.param]
@@ -354,6 +384,9 @@ def _result_column(a, res):
         for i, r in enumerate(res):        # element-wise: equal-length lists must not broadcast
             arr[i] = r
         return C.ArrayColumn(arr)
+    if a.fn in ("bool_and", "bool_or"):
+        valid = torch.tensor([r is not None for r in res]) if any(r is None for r in res) else None
+        return C.NumericColumn(torch.tensor([bool(r) for r in res], dtype=torch.bool), valid)
     if all(r is None or isinstance(r, (int, float, bool)) for r in res):
         arr = np.array([np.nan if r is None else r for r in res], dtype=np.float64)
         valid = torch.from_numpy(np.array([r is not None for r in res])) if any(r is None for r in res) else None

@@ -10,6 +10,7 @@ so results do not depend on the number of GPUs.
 from __future__ import annotations
 
 import builtins
+from collections import OrderedDict
 import hashlib
 import math
 import re
@@ -980,3 +981,524 @@ def pandas_udf(f=None, returnType=None, functionType=None):
     if f is not None and returnType is None:
         returnType = f
     return wrap
+
+
+# ============================================================================ round-out batch
+# hyperbolic / trig / rounding
+def sinh(c): return _num_map("SINH", torch.sinh, c)
+def cosh(c): return _num_map("COSH", torch.cosh, c)
+def tanh(c): return _num_map("TANH", torch.tanh, c)
+def asinh(c): return _num_map("ASINH", torch.asinh, c)
+def acosh(c): return _num_map("ACOSH", torch.acosh, c)
+def atanh(c): return _num_map("ATANH", torch.atanh, c)
+def cot(c): return _num_map("COT", lambda x: 1.0 / torch.tan(x), c)
+def sec(c): return _num_map("SEC", lambda x: 1.0 / torch.cos(x), c)
+def csc(c): return _num_map("CSC", lambda x: 1.0 / torch.sin(x), c)
+def rint(c): return _num_map("rint", torch.round, c)       # torch.round is half-to-even, like Math.rint
+def ln(c): return log(c)
+def power(a, b): return pow(a, b)
+def sign(c): return signum(c)
+def positive(c): return _e(c)
+def negative(c): return _num_map("negative", torch.neg, c)
+def e(): return lit(math.e)
+def pi(): return lit(math.pi)
+
+
+def pmod(a, b):
+    """Positive modulus (result has the divisor's sign convention of Spark: always >= 0 for b > 0)."""
+    return _num_map("pmod", lambda x, y: torch.remainder(x, y) + 0.0, a, b)     # no -0.0
+
+
+def mod(a, b):
+    return _num_map("mod", lambda x, y: torch.fmod(x, y), a, b)
+
+
+def try_divide(a, b):
+    """a / b, null where b == 0 (instead of an error)."""
+    ea, eb = _e(a), _e(b)
+
+    def f(df):
+        x, y = ea.eval(df), eb.eval(df)
+        xd, yd = x.data.to(torch.float64), y.data.to(torch.float64).to(x.data.device)
+        ok = yd != 0
+        for c in (x, y):
+            if getattr(c, "valid", None) is not None:
+                ok = ok & c.valid.to(ok.device)
+        return C.NumericColumn(torch.where(ok, xd / torch.where(ok, yd, torch.ones_like(yd)), torch.zeros_like(xd)),
+                               ok, T.DoubleType())
+    return Expr(f, f"try_divide({ea.name}, {eb.name})", _refs(ea, eb))
+
+
+def try_add(a, b): return _e(a) + _e(b)
+
+
+def width_bucket(v, min_, max_, numBucket):
+    """Bucket 1..numBucket of v in [min, max); 0 below, numBucket+1 at/above max."""
+    def wb(x, lo, hi, nb):
+        if x < lo:
+            return 0
+        if x >= hi:
+            return int(nb) + 1
+        return int((x - lo) / (hi - lo) * nb) + 1
+    return _host_map("width_bucket", wb, v, min_, max_, numBucket, kind="int")
+
+
+# strings
+def left(c, n): return _host_map("left", lambda s, k: str(s)[:builtins.max(int(k), 0)], c, n)
+def right(c, n): return _host_map("right", lambda s, k: str(s)[-int(k):] if int(k) > 0 else "", c, n)
+def char_length(c): return length(c)
+def character_length(c): return length(c)
+def ucase(c): return upper(c)
+def lcase(c): return lower(c)
+def bit_length(c): return _host_map("bit_length", lambda s: 8 * len(str(s).encode()), c, kind="int")
+def octet_length(c): return _host_map("octet_length", lambda s: len(str(s).encode()), c, kind="int")
+def startswith(c, p): return _host_map("startswith", lambda s, q: str(s).startswith(str(q)), c, p, kind="bool")
+def endswith(c, p): return _host_map("endswith", lambda s, q: str(s).endswith(str(q)), c, p, kind="bool")
+def contains(c, p): return _host_map("contains", lambda s, q: str(q) in str(s), c, p, kind="bool")
+
+
+def _sql_like(pattern: str, flags=0):
+    rx = "".join(".*" if ch == "%" else "." if ch == "_" else re.escape(ch) for ch in pattern)
+    return re.compile(rx, flags | re.S)
+
+
+def like(c, pattern):
+    rx = _sql_like(pattern if isinstance(pattern, str) else pattern.eval_literal())
+    return _host_map("like", lambda s: rx.fullmatch(str(s)) is not None, c, kind="bool")
+
+
+def ilike(c, pattern):
+    rx = _sql_like(pattern if isinstance(pattern, str) else pattern.eval_literal(), re.I)
+    return _host_map("ilike", lambda s: rx.fullmatch(str(s)) is not None, c, kind="bool")
+
+
+def rlike(c, pattern):
+    rx = re.compile(pattern if isinstance(pattern, str) else pattern.eval_literal())
+    return _host_map("rlike", lambda s: rx.search(str(s)) is not None, c, kind="bool")
+
+
+regexp_like = rlike
+regexp = rlike
+
+
+def regexp_extract_all(c, pattern, idx=1):
+    rx = re.compile(pattern if isinstance(pattern, str) else pattern.eval_literal())
+    return _host_map("regexp_extract_all", lambda s: [m.group(idx) if rx.groups else m.group(0)
+                                                      for m in rx.finditer(str(s))], c, kind="array")
+
+
+def split_part(c, delimiter, partNum):
+    def sp(s, d, k):
+        parts = str(s).split(str(d))
+        k = int(k)
+        if k == 0:
+            raise ValueError("split_part index must not be 0")
+        return parts[k - 1] if 0 < k <= len(parts) else (parts[k] if -len(parts) <= k < 0 else "")
+    return _host_map("split_part", sp, c, delimiter, partNum)
+
+
+def overlay(src, replace, pos, len=-1):  # noqa: A002
+    def ov(s, r, p, n):
+        s, r, p, n = str(s), str(r), int(p), int(n)
+        n = builtins.len(r) if n < 0 else n
+        return s[:p - 1] + r + s[p - 1 + n:]
+    return _host_map("overlay", ov, src, replace, pos, len)
+
+
+def encode(c, charset):
+    return _host_map("encode", lambda s: str(s).encode(charset.replace("-", "").lower()
+                                                        .replace("utf8", "utf-8")), c, kind="str")
+
+
+def decode(c, charset):
+    return _host_map("decode", lambda b: (b if isinstance(b, (bytes, bytearray)) else str(b).encode())
+                     .decode(charset.replace("-", "").lower().replace("utf8", "utf-8")), c)
+
+
+# nulls / misc
+def nvl2(c, v_if_not_null, v_if_null):
+    return when(_e(c).isNotNull(), _e(v_if_not_null)).otherwise(_e(v_if_null))
+
+
+def equal_null(a, b):
+    ea, eb = _e(a), _e(b)
+
+    def f(df):
+        n = len(df)
+        x, y = _host(ea.eval(df), n), _host(eb.eval(df), n)
+        return _num_out([(u is None and v is None) or (u is not None and v is not None and u == v)
+                         for u, v in zip(x, y)], torch.bool, df.device)
+    return Expr(f, f"equal_null({ea.name}, {eb.name})", _refs(ea, eb))
+
+
+def raise_error(msg):
+    def f(df):
+        if len(df):
+            raise RuntimeError(str(msg))
+        return _num_out([], torch.float64, df.device)
+    return Expr(f, "raise_error()", ())
+
+
+def curdate(): return current_date()
+
+
+def timestamp_seconds(c):
+    import datetime as _dt
+    return _host_map("timestamp_seconds", lambda v: _dt.datetime.utcfromtimestamp(float(v))
+                     .strftime("%Y-%m-%d %H:%M:%S"), c)
+
+
+def make_date(y, m, d):
+    import datetime as _dt
+    return _host_map("make_date", lambda a, b, c_: _dt.date(int(a), int(b), int(c_)).isoformat(), y, m, d)
+
+
+def from_utc_timestamp(c, tz):
+    import pandas as pd
+
+    def cv(v, z):
+        t = pd.Timestamp(str(v))
+        t = t.tz_localize("UTC") if t.tzinfo is None else t
+        return t.tz_convert(str(z)).tz_localize(None).strftime("%Y-%m-%d %H:%M:%S")
+    return _host_map("from_utc_timestamp", cv, c, tz)
+
+
+def to_utc_timestamp(c, tz):
+    import pandas as pd
+
+    def cv(v, z):
+        t = pd.Timestamp(str(v))
+        t = t.tz_localize(str(z)) if t.tzinfo is None else t
+        return t.tz_convert("UTC").tz_localize(None).strftime("%Y-%m-%d %H:%M:%S")
+    return _host_map("to_utc_timestamp", cv, c, tz)
+
+
+def window(timeColumn, windowDuration: str, slideDuration=None, startTime=None):
+    """Tumbling time window: struct(start, end) of the fixed-size window holding each
+    timestamp (sliding windows with slide < duration are not expressible as one row)."""
+    import pandas as pd
+    dur = pd.Timedelta(windowDuration).total_seconds()
+    off = pd.Timedelta(startTime).total_seconds() if startTime else 0.0
+    if slideDuration and pd.Timedelta(slideDuration).total_seconds() != dur:
+        raise NotImplementedError("sliding windows (slideDuration != windowDuration)")
+    from ..frame.dataframe import Row
+
+    def w(v):
+        t = pd.Timestamp(str(v)).timestamp()
+        s0 = math.floor((t - off) / dur) * dur + off
+        fmt = lambda x: pd.Timestamp(x, unit="s").strftime("%Y-%m-%d %H:%M:%S")  # noqa: E731
+        return Row._make(["start", "end"], [fmt(s0), fmt(s0 + dur)])
+    return _host_map("window", w, timeColumn, kind="array")
+
+
+def inline(c):
+    """Generator over an array of structs: one row per struct (DataFrame.select expands
+    it to the struct's fields)."""
+    out = explode(c)
+    out._inline = True
+    return out
+
+
+def json_tuple(c, *fields):
+    import json as _json
+
+    def jt(s):
+        try:
+            d = _json.loads(str(s))
+        except ValueError:
+            return [None] * len(fields)
+        return [None if d.get(k) is None else (v if isinstance(v := d.get(k), str) else _json.dumps(v))
+                for k in fields]
+    return _host_map("json_tuple", jt, c, kind="array")
+
+
+def schema_of_json(js):
+    import json as _json
+    s = js if isinstance(js, str) else js.eval_literal()
+
+    def ty(v):
+        if isinstance(v, bool):
+            return "BOOLEAN"
+        if isinstance(v, int):
+            return "BIGINT"
+        if isinstance(v, float):
+            return "DOUBLE"
+        if isinstance(v, list):
+            return f"ARRAY<{ty(v[0]) if v else 'STRING'}>"
+        if isinstance(v, dict):
+            return "STRUCT<" + ", ".join(f"{k}: {ty(x)}" for k, x in sorted(v.items())) + ">"
+        return "STRING"
+    return lit(ty(_json.loads(s)))
+
+
+# arrays / maps
+def array_repeat(c, count): return _host_map("array_repeat", lambda v, k: [v] * int(k), c, count, kind="array")
+def array_append(c, v): return _host_map("array_append", lambda a, x: list(a) + [x], c, v, kind="array")
+def array_prepend(c, v): return _host_map("array_prepend", lambda a, x: [x] + list(a), c, v, kind="array")
+def array_compact(c): return _host_map("array_compact", lambda a: [x for x in a if x is not None], c, kind="array")
+def array_size(c): return size(c)
+def cardinality(c): return size(c)
+
+
+def array_insert(c, pos, value):
+    def ins(a, p, x):
+        a, p = list(a), int(p)
+        if p == 0:
+            raise ValueError("array_insert position must not be 0")
+        i = p - 1 if p > 0 else len(a) + p + 1
+        if i > len(a):
+            a += [None] * (i - len(a))
+        a.insert(builtins.max(i, 0), x)
+        return a
+    return _host_map("array_insert", ins, c, pos, value, kind="array")
+
+
+def arrays_overlap(a, b):
+    def ov(x, y):
+        sx, sy = {v for v in x if v is not None}, {v for v in y if v is not None}
+        if sx & sy:
+            return True
+        return None if (len(x) and len(y) and (None in x or None in y)) else False
+    return _host_map("arrays_overlap", ov, a, b, kind="bool")
+
+
+def shuffle(c, seed=None):
+    import random as _random
+    rng = _random.Random(seed)
+    return _host_map("shuffle", lambda a: rng.sample(list(a), len(a)), c, kind="array")
+
+
+def try_element_at(c, i):
+    def ta(a, k):
+        k = int(k)
+        if isinstance(a, dict):
+            return a.get(k)
+        return (a[k - 1] if k > 0 else a[k]) if k != 0 and len(a) >= builtins.abs(k) else None
+    return _host_map("try_element_at", ta, c, i, kind="str")
+
+
+def map_concat(*cols):
+    def mc(*ms):
+        out = {}
+        for m in ms:
+            out.update(m)
+        return out
+    return _host_map("map_concat", mc, *cols, kind="array")
+
+
+def map_entries(c):
+    from ..frame.dataframe import Row
+    return _host_map("map_entries", lambda m: [Row._make(["key", "value"], [k, v]) for k, v in m.items()], c,
+                     kind="array")
+
+
+def map_from_arrays(k, v): return _host_map("map_from_arrays", lambda a, b: dict(zip(a, b)), k, v, kind="array")
+
+
+def map_from_entries(c):
+    return _host_map("map_from_entries", lambda a: {(r[0]): r[1] for r in a}, c, kind="array")
+
+
+# ---- higher-order functions: the lambda is evaluated ONCE per rank over the flattened
+# elements (a local frame of all array elements), so its body runs as vectorised column
+# code (device ops for numeric bodies), not per element in Python.
+def _lambda_params(f):
+    import inspect
+    return [p for p in inspect.signature(f).parameters]
+
+
+def _run_lambda(df, f, params: dict, owner: np.ndarray, outer_refs):
+    """Evaluate ``f(*cols)`` over a local frame whose columns are the flattened lambda
+    parameters; columns of ``df`` the body references are repeated per element."""
+    import pandas as pd
+    from ..frame.dataframe import DataFrame
+    n_el = len(owner)
+    data = {f"__lp{i}": pd.Series(v, dtype=object) if any(isinstance(x, (list, dict, str)) or x is None
+                                                            for x in v) else pd.Series(v)
+            for i, v in enumerate(params.values())}
+    local = df.session.local_view()
+    body = f(*[col(f"__lp{i}") for i in range(len(params))])
+    body = _e(body)
+    extra = [r for r in body.refs if not r.startswith("__lp") and r in df.columns]
+    if n_el == 0:
+        return []
+    frame = local.createDataFrame(pd.DataFrame(data)) if data else None
+    if extra:
+        idx = torch.from_numpy(owner.astype(np.int64))
+        cols = OrderedDict(frame._cols)
+        for r in extra:
+            cols[r] = df._col(r).take(idx.to(_dev_of(df._col(r), df.device)))
+        frame = DataFrame(local, cols, n_el)
+    return _host(body.eval(frame), n_el)
+
+
+def _dev_of(c, default):
+    d = getattr(getattr(c, "data", None), "device", None)
+    return d if d is not None else ("cpu" if isinstance(c, C.HostColumn) else default)
+
+
+def _hof(name, c, f, combine, kind="array", map_input=False):
+    ec = _e(c)
+
+    def ev(df):
+        n = len(df)
+        vals = _host(ec.eval(df), n)
+        nargs = len(_lambda_params(f))
+        owner, flat_a, flat_b = [], [], []
+        for r, v in enumerate(vals):
+            if v is None:
+                continue
+            items = list(v.items()) if map_input else list(enumerate(v))
+            for i, x in items:
+                owner.append(r)
+                if map_input:
+                    flat_a.append(i)
+                    flat_b.append(x)
+                else:
+                    flat_a.append(x)
+                    flat_b.append(i)
+        owner = np.asarray(owner, dtype=np.int64)
+        params = {"a": flat_a} if nargs == 1 else {"a": flat_a, "b": flat_b}
+        res = _run_lambda(df, f, params, owner, ())
+        per = [[] for _ in range(n)]
+        for o, a_, b_, y in zip(owner.tolist(), flat_a, flat_b, res):
+            per[o].append((a_, b_, y))
+        out = [None if vals[r] is None else combine(per[r]) for r in range(n)]
+        if kind == "array":
+            arr = np.empty(n, dtype=object)
+            for i, x in enumerate(out):
+                arr[i] = x
+            return C.ArrayColumn(arr)
+        return _num_out(out, torch.bool, df.device)
+    return Expr(ev, f"{name}({ec.name}, lambdafunction)", ec.refs)
+
+
+def transform(c, f):
+    """``transform(arr, x -> f(x))`` / ``(x, i) -> f(x, i)``."""
+    return _hof("transform", c, f, lambda items: [y for _, _, y in items])
+
+
+def filter(c, f):  # noqa: A001
+    return _hof("filter", c, f, lambda items: [a for a, _, y in items if y])
+
+
+def exists(c, f):
+    return _hof("exists", c, f, lambda items: builtins.any(bool(y) for _, _, y in items if y is not None),
+                kind="bool")
+
+
+def forall(c, f):
+    return _hof("forall", c, f, lambda items: builtins.all(bool(y) for _, _, y in items if y is not None),
+                kind="bool")
+
+
+def transform_values(c, f):
+    return _hof("transform_values", c, f, lambda items: {k: y for k, _, y in items}, map_input=True)
+
+
+def transform_keys(c, f):
+    return _hof("transform_keys", c, f, lambda items: {y: v for _, v, y in items}, map_input=True)
+
+
+def map_filter(c, f):
+    return _hof("map_filter", c, f, lambda items: {k: v for k, v, y in items if y}, map_input=True)
+
+
+def zip_with(left_, right_, f):
+    el, er = _e(left_), _e(right_)
+
+    def ev(df):
+        n = len(df)
+        a, b = _host(el.eval(df), n), _host(er.eval(df), n)
+        owner, fa, fb = [], [], []
+        for r, (x, y) in enumerate(zip(a, b)):
+            if x is None or y is None:
+                continue
+            m = builtins.max(len(x), len(y))
+            for i in range(m):
+                owner.append(r)
+                fa.append(x[i] if i < len(x) else None)
+                fb.append(y[i] if i < len(y) else None)
+        owner = np.asarray(owner, dtype=np.int64)
+        res = _run_lambda(df, f, {"a": fa, "b": fb}, owner, ())
+        per = [[] for _ in range(n)]
+        for o, y in zip(owner.tolist(), res):
+            per[o].append(y)
+        arr = np.empty(n, dtype=object)
+        for r in range(n):
+            arr[r] = None if a[r] is None or b[r] is None else per[r]
+        return C.ArrayColumn(arr)
+    return Expr(ev, f"zip_with({el.name}, {er.name}, lambdafunction)", _refs(el, er))
+
+
+def aggregate(c, initialValue, merge, finish=None):
+    """Left fold of each array: vectorised across rows one element position at a time
+    (``max(len)`` evaluations of ``merge`` over the rows that still have elements)."""
+    ec, ei = _e(c), _e(initialValue)
+
+    def ev(df):
+        n = len(df)
+        vals = _host(ec.eval(df), n)
+        acc = list(_host(ei.eval(df), n))
+        lens = [0 if v is None else len(v) for v in vals]
+        for j in range(builtins.max(lens, default=0)):
+            rows = [r for r in range(n) if lens[r] > j]
+            res = _run_lambda(df, merge, {"acc": [acc[r] for r in rows], "x": [vals[r][j] for r in rows]},
+                              np.asarray(rows, dtype=np.int64), ())
+            for r, y in zip(rows, res):
+                acc[r] = y
+        if finish is not None and n:
+            acc = _run_lambda(df, finish, {"acc": acc}, np.arange(n, dtype=np.int64), ())
+        out = [None if vals[r] is None else acc[r] for r in range(n)]
+        if builtins.all(isinstance(v, (int, float, bool)) or v is None for v in out):
+            return _num_out(out, torch.float64 if builtins.any(isinstance(v, float) for v in out) else torch.int64,
+                            df.device)
+        return _str_out(out)
+    return Expr(ev, f"aggregate({ec.name}, ...)", _refs(ec, ei))
+
+
+reduce = aggregate
+
+
+# ---- aggregates
+def median(c):
+    """Exact median (Spark ``median`` = ``percentile(c, 0.5)``, linear interpolation)."""
+    out = Agg("median", _e(c), f"median({_e(c).name})")
+    return out
+
+
+def mode(c):
+    return Agg("mode", _e(c), f"mode({_e(c).name})")
+
+
+def product(c):
+    return Agg("product", _e(c), f"product({_e(c).name})")
+
+
+def count_if(c):
+    return Agg("count", when(_e(c), lit(1)), f"count_if({_e(c).name})")
+
+
+def bool_and(c): return Agg("bool_and", _e(c), f"bool_and({_e(c).name})")
+def bool_or(c): return Agg("bool_or", _e(c), f"bool_or({_e(c).name})")
+
+
+every = bool_and
+some = bool_or
+
+
+def any_value(c, ignoreNulls=False):
+    return Agg("first", _e(c), f"any_value({_e(c).name})")
+
+
+def max_by(c, ord_):
+    out = Agg("max_by", array(_e(ord_), _e(c)), f"max_by({_e(c).name}, {_e(ord_).name})")
+    return out
+
+
+def min_by(c, ord_):
+    return Agg("min_by", array(_e(ord_), _e(c)), f"min_by({_e(c).name}, {_e(ord_).name})")
+
+
+def first_value(c, ignoreNulls=False): return first(c, ignoreNulls)
+def last_value(c, ignoreNulls=False): return last(c, ignoreNulls)

@@ -171,3 +171,49 @@ def test_extended_function_surface():
     pu = F.pandas_udf(lambda v: v * 2, "double")
     assert [r.p for r in s.createDataFrame(pd.DataFrame({"v": [1.0, 2.5]})).select(pu("v").alias("p")).collect()] \
         == [2.0, 5.0]
+
+
+def test_higher_order_and_round_out_functions():
+    import pandas as pd
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.sql import functions as F
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    df = s.createDataFrame(pd.DataFrame({"id": [1, 2, 3], "t": ["ab cd", "x", "Hello"], "v": [1.0, 2.0, 4.0]}))
+    a = df.withColumn("arr", F.array(F.col("v"), F.col("v") * 2, F.lit(5.0)))
+    r = a.select(F.transform("arr", lambda x: x * 10).alias("tr"), F.transform("arr", lambda x, i: x + i).alias("ti"),
+                 F.filter("arr", lambda x: x > 3).alias("fi"), F.exists("arr", lambda x: x > 7).alias("ex"),
+                 F.forall("arr", lambda x: x > 0).alias("fa"),
+                 F.aggregate("arr", F.lit(0.0), lambda acc, x: acc + x, lambda acc: acc * 2).alias("ag"),
+                 F.zip_with("arr", "arr", lambda x, y: x * y).alias("zw"),
+                 F.transform("arr", lambda x: x + F.col("id")).alias("outer")).collect()
+    assert r[0].tr == [10.0, 20.0, 50.0] and r[0].ti == [1.0, 3.0, 7.0] and r[1].fi == [4.0, 5.0]
+    assert [x.ex for x in r] == [False, False, True] and all(x.fa for x in r)
+    assert [x.ag for x in r] == [16.0, 22.0, 34.0] and r[2].zw == [16.0, 64.0, 25.0] and r[2].outer == [7.0, 11.0, 8.0]
+    m = df.select(F.create_map(F.lit("a"), F.col("v"), F.lit("b"), F.col("v") * 3).alias("m")).select(
+        F.transform_values("m", lambda k, v: v + 1).alias("tv"), F.map_filter("m", lambda k, v: v > 3).alias("mf"),
+        F.transform_keys("m", lambda k, v: F.upper(k)).alias("tk")).collect()
+    assert m[1].tv == {"a": 3.0, "b": 7.0} and m[1].mf == {"b": 6.0} and m[0].tk == {"A": 1.0, "B": 3.0}
+    g = s.createDataFrame(pd.DataFrame({"k": ["a", "a", "b", "b", "b"], "x": [1.0, 3.0, 2.0, 2.0, 5.0],
+                                        "y": [5, 1, 2, 9, 3], "b": [True, False, True, True, True]}))
+    got = {row.k: row for row in g.groupBy("k").agg(
+        F.median("x").alias("md"), F.mode("x").alias("mo"), F.product("x").alias("p"),
+        F.count_if(F.col("x") > 1.5).alias("ci"), F.bool_and("b").alias("ba"), F.bool_or("b").alias("bo"),
+        F.max_by("x", "y").alias("mb"), F.min_by("x", "y").alias("nb")).collect()}
+    assert (got["a"].md, got["a"].mo, got["a"].p, got["a"].ci, got["a"].ba, got["a"].mb, got["a"].nb) == \
+        (2.0, 1.0, 3.0, 1, False, 1.0, 3.0)
+    assert (got["b"].md, got["b"].mo, got["b"].p, got["b"].ci, got["b"].ba, got["b"].bo) == (2.0, 2.0, 20.0, 3, True, True)
+    g.createOrReplaceTempView("hof")
+    q = s.sql("SELECT k, median(x) AS md, max_by(x, y) AS mb, count_if(x > 1.5) AS ci FROM hof GROUP BY k").collect()
+    assert {row.k: (row.md, row.mb, row.ci) for row in q} == {"a": (2.0, 1.0, 1), "b": (2.0, 2.0, 3)}
+    row = df.select(F.like("t", "a%").alias("l"), F.ilike("t", "h%").alias("il"), F.left("t", F.lit(2)).alias("le"),
+                    F.split_part("t", F.lit(" "), F.lit(2)).alias("sp"), F.overlay("t", F.lit("ZZ"), F.lit(1)).alias("ov"),
+                    F.width_bucket("v", F.lit(0.0), F.lit(4.0), F.lit(4)).alias("wb"),
+                    F.try_divide("v", F.col("v") - 1).alias("td"), F.pmod(F.col("v") - 3, F.lit(2.0)).alias("pm"),
+                    F.nvl2("t", F.lit(1), F.lit(0)).alias("n2"),
+                    F.array_insert(F.array(F.col("v")), F.lit(1), F.lit(9.0)).alias("ai")).collect()
+    assert [x.l for x in row] == [True, False, False] and row[2].il and row[0].le == "ab" and row[0].sp == "cd"
+    assert row[0].ov == "ZZ cd" and [x.wb for x in row] == [2, 3, 5] and row[0].td is None and row[1].td == 2.0
+    assert row[0].pm == 0.0 and row[0].n2 == 1 and row[1].ai == [9.0, 2.0]
+    st = s.createDataFrame(pd.DataFrame({"id": [1, 2]}))
+    st = st.select("id", F.array(F.struct(F.col("id").alias("a"), (F.col("id") * 2).alias("b"))).alias("s"))
+    assert st.select("id", F.inline("s")).collect()[1].b == 4
