@@ -143,11 +143,14 @@ class Tree:
 class TreeBuilder:
     """Grows one tree over this rank's binned rows (collectives keep ranks in lockstep)."""
 
+    hist_subtraction = True         # False: scan every node at every level (reference path)
+
     def __init__(self, comm, bins: torch.Tensor, splits: list, y: torch.Tensor, w: torch.Tensor | None,
                  impurity: str, num_classes: int, max_depth: int = 5, min_instances: float = 1.0,
                  min_info_gain: float = 0.0, feature_fraction: float = 1.0, seed: int = 0,
-                 max_bins: int = 32):
+                 max_bins: int = 32, bins_t: torch.Tensor | None = None):
         self.comm, self.bins, self.splits = comm, bins, splits
+        self.bins_t = bins_t if bins_t is not None else T.feature_major(bins)
         self.y, self.w = y, w
         self.kind = impurity
         self.cls = impurity in ("gini", "entropy")
@@ -175,16 +178,32 @@ class TreeBuilder:
         seg_node = torch.ones(1, dtype=torch.int64, device=dev)
         leaf_segments = []
         rng = np.random.default_rng(self.seed)
+        # histogram subtraction: below the root only the globally smaller child of each
+        # split is scanned; its sibling is parent - smaller (histograms are additive), which
+        # at least halves the rows the hist kernel touches per level and the all-reduce size
+        parent_H = None                                           # [P, F, B, S] fp64, global
+        small_right = None                                        # [P] bool: right child smaller
         for depth in range(self.max_depth + 1):
             nodes = seg_node.tolist()
             if not nodes:
                 break
             k = len(nodes)
-            local = torch.arange(k, device=dev)
             with trace("tree.hist"):
-                H = T.node_hist(self.bins, order, self.y, self.w, seg_lo, seg_hi, local, k, B, S, self.cls)
-                H = H.to(torch.float64).contiguous()
-            self.comm.all_reduce(H)                               # [k, F, B, S]
+                if parent_H is None or not self.hist_subtraction:
+                    H = T.node_hist(self.bins, order, self.y, self.w, seg_lo, seg_hi,
+                                    torch.arange(k, device=dev), k, B, S, self.cls)
+                    H = H.to(torch.float64).contiguous()
+                    self.comm.all_reduce(H)                       # [k, F, B, S]
+                else:
+                    P = k // 2                                    # segments come as (left, right) pairs
+                    pick = 2 * torch.arange(P, device=dev) + small_right.to(torch.int64)
+                    Hs = T.node_hist(self.bins, order, self.y, self.w, seg_lo[pick], seg_hi[pick],
+                                     torch.arange(P, device=dev), P, B, S, self.cls)
+                    Hs = Hs.to(torch.float64).contiguous()
+                    self.comm.all_reduce(Hs)
+                    H = torch.empty((k, F, B, S), dtype=torch.float64, device=dev)
+                    H[pick] = Hs
+                    H[pick ^ 1] = parent_H - Hs
             tsplit = trace("tree.split")
             tsplit.__enter__()
             tot = H[:, 0].sum(1)                                   # [k, S] node stats (feature 0 bins)
@@ -226,6 +245,9 @@ class TreeBuilder:
             impurity[node_ids] = imp_np
             count[node_ids] = w_np
             do_split = (bg > self.min_gain) & (bg > 0) & np.isfinite(bg) & (depth < self.max_depth)
+            # global child weights at the chosen split decide which child the next level scans
+            wl_best = wL.reshape(k, -1).gather(1, best.indices[:, None])[:, 0]
+            wr_best = wR.reshape(k, -1).gather(1, best.indices[:, None])[:, 0]
             tsplit.__exit__(None, None, None)
             if not do_split.any():
                 leaf_segments.append((seg_lo, seg_hi, seg_node))
@@ -244,7 +266,9 @@ class TreeBuilder:
             s_lo, s_hi, s_node = seg_lo[spl], seg_hi[spl], seg_node[spl]
             s_feat = torch.from_numpy(bf[do_split]).to(dev)
             s_bin = torch.from_numpy(bb[do_split]).to(dev)
-            order, nleft = T.partition(self.bins, order, s_lo, s_hi, s_feat, s_bin)
+            parent_H = H[spl]
+            small_right = (wr_best < wl_best)[spl]
+            order, nleft = T.partition(self.bins, order, s_lo, s_hi, s_feat, s_bin, bins_t=self.bins_t)
             mid = s_lo + nleft
             seg_lo = torch.stack([s_lo, mid], 1).reshape(-1)
             seg_hi = torch.stack([mid, s_hi], 1).reshape(-1)
@@ -293,6 +317,7 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
     """Spark GradientBoostedTrees.boost: tree 0 fit on (scaled) labels with weight 1, then
     trees on pseudo-residuals with weight ``step``."""
     dev = bins.device
+    bins_t = T.feature_major(bins)                    # shared by every tree of the ensemble
     yy = y.to(torch.float64)
     if classification:
         yy = 2.0 * yy - 1.0
@@ -312,7 +337,7 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
             sub = subsample_weights(None, rows, subsampling_rate, seed + m, False)
             sw = sub if w is None else w * sub
         tb = TreeBuilder(comm, bins, splits, target.float(), sw, "variance", 1, max_depth, min_instances,
-                         min_info_gain, feature_fraction, seed + m)
+                         min_info_gain, feature_fraction, seed + m, bins_t=bins_t)
         tree, leaf_row = tb.build()
         wt = 1.0 if m == 0 else step
         Fm = Fm + wt * torch.from_numpy(tree.value[:, 0]).to(dev)[leaf_row]
@@ -335,12 +360,13 @@ def fit_forest(comm, bins, splits, y, w, num_trees: int, impurity: str, num_clas
                min_instances: float, min_info_gain: float, subsampling_rate: float, feature_fraction: float,
                seed: int, rows: torch.Tensor, bootstrap: bool) -> Ensemble:
     trees = []
+    bins_t = T.feature_major(bins)
     for t in range(num_trees):
         sw = subsample_weights(None, rows, subsampling_rate, seed * 7919 + t, bootstrap)
         if w is not None:
             sw = w if sw is None else w * sw
         tb = TreeBuilder(comm, bins, splits, y, sw, impurity, num_classes, max_depth, min_instances,
-                         min_info_gain, feature_fraction, seed + 31 * t)
+                         min_info_gain, feature_fraction, seed + 31 * t, bins_t=bins_t)
         tree, _ = tb.build()
         trees.append(tree)
     return Ensemble(trees, [1.0] * num_trees, "rf", num_classes)

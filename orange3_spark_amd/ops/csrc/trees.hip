@@ -144,13 +144,17 @@ __global__ __launch_bounds__(kHistThreads) void tree_hist_kernel(
 constexpr int kPartThreads = 256;
 constexpr int kPartWaves = kPartThreads / kWave;
 
-__device__ __forceinline__ bool goes_left(const uint8_t* __restrict__ bins, int F, int32_t row, int feat,
-                                          int bin) {
-  return (int)bins[(int64_t)row * F + feat] <= bin;
+// bins element (row, feat) at row * rs + feat * cs: the partition reads a feature-major
+// copy (rs = 1, cs = n), so within a segment (rows in ascending order after every stable
+// split) neighbouring lanes hit neighbouring bytes of one feature column instead of one
+// byte per 64-B row.
+__device__ __forceinline__ bool goes_left(const uint8_t* __restrict__ bins, int64_t rs, int64_t cs, int32_t row,
+                                          int feat, int bin) {
+  return (int)bins[(int64_t)row * rs + (int64_t)feat * cs] <= bin;
 }
 
 __global__ __launch_bounds__(kPartThreads) void tree_part_count_kernel(
-    const uint8_t* __restrict__ bins, int F, const int32_t* __restrict__ order, const int64_t* __restrict__ it_lo,
+    const uint8_t* __restrict__ bins, int64_t rs, int64_t cs, const int32_t* __restrict__ order, const int64_t* __restrict__ it_lo,
     const int64_t* __restrict__ it_hi, const int32_t* __restrict__ it_feat, const int32_t* __restrict__ it_bin,
     int64_t* __restrict__ it_left, uint8_t* __restrict__ flags) {
   __shared__ int wsum[kPartWaves];
@@ -158,7 +162,7 @@ __global__ __launch_bounds__(kPartThreads) void tree_part_count_kernel(
   const int feat = it_feat[blockIdx.x], bin = it_bin[blockIdx.x];
   int cnt = 0;
   for (int64_t p = lo + threadIdx.x; p < hi; p += kPartThreads) {
-    const bool l = goes_left(bins, F, order[p], feat, bin);     // the one random gather per row
+    const bool l = goes_left(bins, rs, cs, order[p], feat, bin);     // the one random gather per row
     flags[p] = l;                                               // pass 2 reads this sequentially
     cnt += l;
   }
@@ -174,7 +178,7 @@ __global__ __launch_bounds__(kPartThreads) void tree_part_count_kernel(
 }
 
 __global__ __launch_bounds__(kPartThreads) void tree_part_scatter_kernel(
-    const uint8_t* __restrict__ bins, int F, const int32_t* __restrict__ order, int32_t* __restrict__ out,
+    const int32_t* __restrict__ order, int32_t* __restrict__ out,
     const int64_t* __restrict__ it_lo, const int64_t* __restrict__ it_hi, const int32_t* __restrict__ it_feat,
     const int32_t* __restrict__ it_bin, const int64_t* __restrict__ dst_left, const int64_t* __restrict__ dst_right,
     const uint8_t* __restrict__ flags) {
@@ -211,18 +215,66 @@ __global__ __launch_bounds__(kPartThreads) void tree_part_scatter_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Feature-major copy of the binned matrix ([n][F] -> [F][n], uint8) for the partition.
+// One block = 256 rows x <= 64 features staged through LDS: 4-byte coalesced row reads
+// (F % 4 == 0), 4-byte coalesced column writes; rows are padded by 4 bytes so the byte
+// scatter into the [feature][row] tile spreads over banks.
+constexpr int kTrRows = 256;
+__global__ __launch_bounds__(256) void u8_transpose_kernel(const uint8_t* __restrict__ in, int64_t n, int F,
+                                                           uint8_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[64][kTrRows + 4];
+  const int64_t r0 = (int64_t)blockIdx.x * kTrRows;
+  const int f0 = blockIdx.y * 64;
+  const int fw = F - f0 < 64 ? F - f0 : 64;                 // % 4 == 0
+  const int rows = n - r0 < kTrRows ? (int)(n - r0) : kTrRows;
+  const int wq = fw / 4;                                    // 4-byte words per tile row
+  for (int w = threadIdx.x; w < kTrRows * wq; w += 256) {
+    const int r = w / wq, q = w % wq;
+    if (r < rows) {
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(in + (r0 + r) * F + f0 + 4 * q);
+      tile[4 * q + 0][r] = (uint8_t)v;
+      tile[4 * q + 1][r] = (uint8_t)(v >> 8);
+      tile[4 * q + 2][r] = (uint8_t)(v >> 16);
+      tile[4 * q + 3][r] = (uint8_t)(v >> 24);
+    }
+  }
+  __syncthreads();
+  const bool full = rows == kTrRows && (n & 3) == 0;
+  for (int w = threadIdx.x; w < fw * (kTrRows / 4); w += 256) {
+    const int f = w / (kTrRows / 4), q = w % (kTrRows / 4);
+    uint8_t* dst = out + (int64_t)(f0 + f) * n + r0 + 4 * q;
+    if (full) {
+      *reinterpret_cast<uint32_t*>(dst) = *reinterpret_cast<const uint32_t*>(&tile[f][4 * q]);
+    } else {
+      for (int j = 0; j < 4; ++j)
+        if (4 * q + j < rows) dst[j] = tile[f][4 * q + j];
+    }
+  }
+}
+
 }  // namespace
 
-O3S_API int o3s_tree_partition(const uint8_t* bins, int F, const int32_t* order, int32_t* out,
+// in: [n][F] uint8 with F % 4 == 0; out: [F][n].
+O3S_API int o3s_u8_transpose(const uint8_t* in, int64_t n, int F, uint8_t* out, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (F % 4 != 0 || F <= 0) return -1;
+  const dim3 grid((unsigned)((n + kTrRows - 1) / kTrRows), (unsigned)((F + 63) / 64));
+  hipLaunchKernelGGL(u8_transpose_kernel, grid, dim3(256), 0, st, in, n, F, out);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+O3S_API int o3s_tree_partition(const uint8_t* bins, int64_t rs, int64_t cs, const int32_t* order, int32_t* out,
                                const int64_t* it_lo, const int64_t* it_hi, const int32_t* it_feat,
                                const int32_t* it_bin, int64_t* it_left, const int64_t* dst_left,
                                const int64_t* dst_right, uint8_t* flags, int n_items, int pass, hipStream_t st) {
   if (n_items <= 0) return 0;
   if (pass == 0)
-    hipLaunchKernelGGL(tree_part_count_kernel, dim3(n_items), dim3(kPartThreads), 0, st, bins, F, order, it_lo,
+    hipLaunchKernelGGL(tree_part_count_kernel, dim3(n_items), dim3(kPartThreads), 0, st, bins, rs, cs, order, it_lo,
                        it_hi, it_feat, it_bin, it_left, flags);
   else
-    hipLaunchKernelGGL(tree_part_scatter_kernel, dim3(n_items), dim3(kPartThreads), 0, st, bins, F, order, out,
+    hipLaunchKernelGGL(tree_part_scatter_kernel, dim3(n_items), dim3(kPartThreads), 0, st, order, out,
                        it_lo, it_hi, it_feat, it_bin, dst_left, dst_right, flags);
   O3S_CHECK_LAUNCH();
   return 0;

@@ -30,8 +30,21 @@ def _items(seg_lo: torch.Tensor, seg_hi: torch.Tensor, chunk: int):
     return it_lo, it_hi, seg_id, first
 
 
+def feature_major(bins: torch.Tensor) -> torch.Tensor | None:
+    """[F, n] copy of the binned matrix for the partition's per-row feature reads (GPU;
+    LDS-tiled ``u8_transpose_kernel``, F % 4 == 0, else torch's strided copy)."""
+    if not bins.is_cuda:
+        return None
+    n, F = bins.shape
+    if F % 4 != 0 or not bins.is_contiguous():
+        return bins.t().contiguous()
+    out = torch.empty((F, n), dtype=torch.uint8, device=bins.device)
+    N.check(N.kernels().o3s_u8_transpose(bins.data_ptr(), n, F, out.data_ptr(), N.stream_of(bins)), "u8_transpose")
+    return out
+
+
 def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi: torch.Tensor,
-              s_feat: torch.Tensor, s_bin: torch.Tensor, chunk: int = 1 << 14):
+              s_feat: torch.Tensor, s_bin: torch.Tensor, chunk: int = 1 << 14, bins_t: torch.Tensor | None = None):
     """Stable split of every segment [s_lo, s_hi) of ``order`` into rows with
     bins[row, feat] <= bin (first) and the rest.  Returns (new_order, nleft per segment).
 
@@ -53,7 +66,8 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     flags = torch.empty(order.shape[0], dtype=torch.uint8, device=dev)
     lib = N.kernels()
     st = N.stream_of(bins)
-    N.check(lib.o3s_tree_partition(bins.data_ptr(), F, order.data_ptr(), None, it_lo.data_ptr(), it_hi.data_ptr(),
+    src, rs, cs = (bins_t, 1, bins.shape[0]) if bins_t is not None else (bins, F, 1)
+    N.check(lib.o3s_tree_partition(src.data_ptr(), rs, cs, order.data_ptr(), None, it_lo.data_ptr(), it_hi.data_ptr(),
                                    it_feat.data_ptr(), it_bin.data_ptr(), it_left.data_ptr(), None, None,
                                    flags.data_ptr(), n_items, 0, st), "tree_part_count")
     it_right = (it_hi - it_lo) - it_left
@@ -63,7 +77,7 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     f = first_item[it_seg]                                     # first item of each item's segment
     dst_left = (s_lo[it_seg] + cl - cl[f]).contiguous()
     dst_right = (s_lo[it_seg] + nleft[it_seg] + cr - cr[f]).contiguous()
-    N.check(lib.o3s_tree_partition(bins.data_ptr(), F, order.data_ptr(), new_order.data_ptr(), it_lo.data_ptr(),
+    N.check(lib.o3s_tree_partition(src.data_ptr(), rs, cs, order.data_ptr(), new_order.data_ptr(), it_lo.data_ptr(),
                                    it_hi.data_ptr(), it_feat.data_ptr(), it_bin.data_ptr(), None,
                                    dst_left.data_ptr(), dst_right.data_ptr(), flags.data_ptr(), n_items, 1, st),
             "tree_part_scatter")

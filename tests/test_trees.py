@@ -96,7 +96,8 @@ def test_gpu_gbt_fit():
 
 
 @pytest.mark.gpu
-def test_gpu_partition_matches_torch(gpu):
+@pytest.mark.parametrize("feature_major", [False, True])
+def test_gpu_partition_matches_torch(gpu, feature_major):
     from orange3_spark_amd.ops import trees as T
     g = torch.Generator().manual_seed(0)
     n, F = 200_003, 13
@@ -107,7 +108,40 @@ def test_gpu_partition_matches_torch(gpu):
     s_feat = torch.randint(0, F, (s_lo.numel(),), generator=g)
     s_bin = torch.randint(0, 32, (s_lo.numel(),), generator=g)
     ref_o, ref_n = T.partition_torch(bins, order, s_lo, s_hi, s_feat, s_bin)
-    got_o, got_n = T.partition(bins.to(gpu), order.to(gpu), s_lo.to(gpu), s_hi.to(gpu), s_feat.to(gpu),
-                               s_bin.to(gpu), chunk=4096)
+    bg = bins.to(gpu)
+    got_o, got_n = T.partition(bg, order.to(gpu), s_lo.to(gpu), s_hi.to(gpu), s_feat.to(gpu),
+                               s_bin.to(gpu), chunk=4096, bins_t=T.feature_major(bg) if feature_major else None)
     assert torch.equal(got_n.cpu(), ref_n)
     assert torch.equal(got_o.cpu(), ref_o)                             # stable -> identical permutation
+
+
+@pytest.mark.parametrize("cls_model", ["dt_cls", "gbt_reg", "rf_cls"])
+def test_hist_subtraction_matches_full_scan(cpu, cls_model):
+    """Scanning only the smaller child per split (sibling = parent - child) grows the same
+    trees as scanning every node."""
+    from orange3_spark_amd.models.trees import TreeBuilder
+    rng = np.random.default_rng(5)
+    X = rng.uniform(-1, 1, size=(3000, 6))
+    y = ((X[:, 0] > 0.1) ^ (X[:, 2] > -0.3)).astype(float)
+    yr = np.round(X[:, 0] * 4 + X[:, 3] * 2 + rng.normal(size=3000))
+    df = cpu.createDataFrame(pd.DataFrame({"features": list(X), "label": yr if cls_model == "gbt_reg" else y}))
+    mk = {"dt_cls": lambda: DecisionTreeClassifier(maxDepth=6),
+          "gbt_reg": lambda: GBTRegressor(maxDepth=5, maxIter=3),
+          "rf_cls": lambda: RandomForestClassifier(numTrees=3, maxDepth=5, seed=2)}[cls_model]
+    outs = []
+    for flag in (True, False):
+        TreeBuilder.hist_subtraction = flag
+        try:
+            outs.append(mk().fit(df).transform(df).toPandas()["prediction"].to_numpy())
+        finally:
+            TreeBuilder.hist_subtraction = True
+    # same splits; GBT leaf values (real-valued residual sums) agree to rounding
+    np.testing.assert_allclose(outs[0], outs[1], rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,F", [(1_000_003, 64), (4099, 12), (256, 68), (5, 4)])
+def test_gpu_u8_transpose(gpu, n, F):
+    from orange3_spark_amd.ops import trees as T
+    b = torch.randint(0, 255, (n, F), dtype=torch.uint8, generator=torch.Generator().manual_seed(n)).to(gpu)
+    assert torch.equal(T.feature_major(b).cpu(), b.cpu().t().contiguous())

@@ -22,7 +22,9 @@ def main():
     ap.add_argument("--features", type=int, default=64)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--trees", type=int, default=3)
+    ap.add_argument("--no-subtraction", action="store_true", help="scan every node at every level")
     a = ap.parse_args()
+    TR.TreeBuilder.hist_subtraction = not a.no_subtraction
     s = Session.getOrCreate()
     df = s.synthetic.trees(a.rows, a.features, seed=5)
     X = df.column_data("features").data
@@ -45,7 +47,7 @@ def main():
     phases = {k: round(v["total_s"] / a.trees, 4) for k, v in TRACER.summary().items()} if TRACER.enabled else None
     print(json.dumps({"metric": "GBTClassifier seconds per tree (depth 8, 64 features)", "value": dt,
                       "unit": "s/tree", "rows_per_gpu": a.rows, "n_gpus": s.comm.world_size,
-                      "binning_s": t_bin, "loss": ens.losses, "nodes": [t.numNodes for t in ens.trees],
+                      "binning_s": t_bin, "hist_subtraction": TR.TreeBuilder.hist_subtraction, "loss": ens.losses, "nodes": [t.numNodes for t in ens.trees],
                       "phase_s_per_tree": phases}))
 
 
