@@ -23,6 +23,7 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
+from ..ops import _native as N
 from ..ops import sampling
 from ..ops import trees as T
 from ..runtime.tracing import trace
@@ -59,8 +60,23 @@ def find_splits(comm, X: torch.Tensor, max_bins: int, seed: int = 0, sample: int
 
 
 def bin_features(X: torch.Tensor, splits: list) -> torch.Tensor:
-    """uint8 [n, F]: bin = #thresholds < value (value <= t_0 -> bin 0)."""
+    """uint8 [n, F]: bin = #thresholds < value (value <= t_0 -> bin 0).
+
+    GPU fp32: one pass of ``bin_features_kernel`` (all thresholds in LDS, branchless
+    search per element); otherwise per-feature ``torch.bucketize``."""
     n, F = X.shape
+    if X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and X.stride(1) == 1 and n > 0:
+        T_ = max((len(s) for s in splits), default=0) + 1
+        Tp = 1 << max(0, (T_ - 1).bit_length())
+        if Tp <= 256 and 4 * F * (Tp + 1) <= 160 * 1024:
+            th = np.full((F, Tp), np.inf, dtype=np.float32)
+            for f, s in enumerate(splits):
+                th[f, :len(s)] = np.asarray(s, dtype=np.float32)
+            tht = torch.from_numpy(th).to(X.device)
+            out = torch.empty((n, F), dtype=torch.uint8, device=X.device)
+            N.check(N.kernels().o3s_bin_features(X.data_ptr(), n, X.stride(0), F, tht.data_ptr(), Tp,
+                                                 out.data_ptr(), N.stream_of(X)), "bin_features")
+            return out
     out = torch.empty((n, F), dtype=torch.uint8, device=X.device)
     step = 1 << 22
     for f in range(F):

@@ -253,7 +253,53 @@ __global__ __launch_bounds__(256) void u8_transpose_kernel(const uint8_t* __rest
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Quantile binning: bin = #thresholds < x (torch.bucketize(right=False) semantics) for
+// every element of X [n][F] fp32.  All features' thresholds sit in LDS ([F][Tp+1] with
+// +inf padding to a power of two Tp; the +1 row pad puts consecutive features of one
+// wave on different banks); each element is a branchless log2(Tp)-step search.  One
+// streaming pass: X read once, bins written once (row-major, coalesced bytes).
+constexpr int kBinRows = 64;
+__global__ __launch_bounds__(256) void bin_features_kernel(const float* __restrict__ X, int64_t n, int64_t ldx,
+                                                           int F, const float* __restrict__ th, int Tp,
+                                                           uint8_t* __restrict__ out) {
+  extern __shared__ float sth[];
+  const int TS = Tp + 1;
+  for (int i = threadIdx.x; i < F * Tp; i += 256) sth[(i / Tp) * TS + i % Tp] = th[i];
+  __syncthreads();
+  const int per = kBinRows * F;
+  const int64_t nchunks = (n + kBinRows - 1) / kBinRows;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t r0 = c * kBinRows;
+    const int rows = n - r0 < kBinRows ? (int)(n - r0) : kBinRows;
+    for (int li = threadIdx.x; li < rows * F; li += 256) {
+      const int lr = li / F, f = li - lr * F;
+      const float x = X[(r0 + lr) * ldx + f];
+      const float* a = sth + f * TS;
+      int b = 0;
+      for (int st = Tp >> 1; st > 0; st >>= 1) b += (a[b + st - 1] < x) ? st : 0;
+      out[(r0 + lr) * F + f] = (uint8_t)b;
+    }
+    (void)per;
+  }
+}
+
 }  // namespace
+
+// X: [n][F] fp32 (row stride ldx); th: [F][Tp] fp32 sorted, +inf padded, Tp a power of
+// two <= 256 with at least one pad per feature; out: [n][F] uint8.
+O3S_API int o3s_bin_features(const float* X, int64_t n, int64_t ldx, int F, const float* th, int Tp, uint8_t* out,
+                             hipStream_t st) {
+  if (n <= 0) return 0;
+  if (Tp < 1 || Tp > 256 || (Tp & (Tp - 1)) || F <= 0) return -1;
+  const size_t lds = sizeof(float) * (size_t)F * (Tp + 1);
+  if (lds > 160 * 1024) return -2;
+  const int64_t nchunks = (n + kBinRows - 1) / kBinRows;
+  const unsigned grid = (unsigned)(nchunks < 8192 ? nchunks : 8192);
+  hipLaunchKernelGGL(bin_features_kernel, dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, Tp, out);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
 
 // in: [n][F] uint8 with F % 4 == 0; out: [F][n].
 O3S_API int o3s_u8_transpose(const uint8_t* in, int64_t n, int F, uint8_t* out, hipStream_t st) {

@@ -145,3 +145,19 @@ def test_gpu_u8_transpose(gpu, n, F):
     from orange3_spark_amd.ops import trees as T
     b = torch.randint(0, 255, (n, F), dtype=torch.uint8, generator=torch.Generator().manual_seed(n)).to(gpu)
     assert torch.equal(T.feature_major(b).cpu(), b.cpu().t().contiguous())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,F,nb", [(100_003, 64, 32), (5000, 7, 2), (777, 130, 255), (3, 1, 32)])
+def test_gpu_bin_features_matches_bucketize(gpu, n, F, nb):
+    from orange3_spark_amd.models import trees as TR
+    g = torch.Generator().manual_seed(F)
+    X = torch.randn(n, F, generator=g)
+    X[:, 0] = torch.round(X[:, 0] * 2) / 2                          # ties on thresholds
+    splits = TR.find_splits(Session(SessionConf().set("o3s.device", "cpu")).comm, X, nb, 0)
+    ref = torch.empty((n, F), dtype=torch.uint8)
+    for f in range(F):
+        t = torch.as_tensor(splits[f], dtype=torch.float32)
+        ref[:, f] = torch.bucketize(X[:, f], t).to(torch.uint8) if t.numel() else 0
+    got = TR.bin_features(X.to(gpu), splits).cpu()
+    assert torch.equal(got, ref)
