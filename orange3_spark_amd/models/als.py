@@ -36,6 +36,7 @@ class Csr:
     vals: torch.Tensor        # float32 ratings
     row_lo: int               # first dense row index owned by this rank
     nrows: int
+    cache: dict = field(default_factory=dict)   # per-(implicit, alpha, reg) solve constants
 
 
 def global_ids(comm, ids: torch.Tensor) -> torch.Tensor:
@@ -91,18 +92,27 @@ def _weights(vals: torch.Tensor, implicit: bool, alpha: float):
     return torch.ones_like(vals).float().contiguous(), vals.float().contiguous(), torch.ones_like(vals, dtype=torch.bool)
 
 
+FUSED_CG = True        # False: CG bookkeeping as separate torch ops (reference path)
+
+
 def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, implicit: bool, alpha: float,
                FtF: torch.Tensor | None, cg_iters: int, nonneg: bool, exact: bool | None = None) -> torch.Tensor:
     n, R = csr.nrows, Ffull.shape[1]
     dev = Ffull.device
-    w, b, pos = _weights(csr.vals, implicit, alpha)
-    rows = torch.repeat_interleave(torch.arange(n, device=dev), csr.indptr[1:] - csr.indptr[:-1])
-    nu = torch.zeros(n, dtype=torch.float32, device=dev).index_add_(0, rows, pos.float())
-    lam = (reg * nu).to(torch.float32)
+    key = (implicit, float(alpha), float(reg))
+    if key not in csr.cache:          # the ratings do not change between iterations
+        w, b, pos = _weights(csr.vals, implicit, alpha)
+        rows = torch.repeat_interleave(torch.arange(n, device=dev), csr.indptr[1:] - csr.indptr[:-1])
+        nu = torch.zeros(n, dtype=torch.float32, device=dev).index_add_(0, rows, pos.float())
+        csr.cache.clear()
+        csr.cache[key] = (w, b, (reg * nu).to(torch.float32).contiguous())
+        del rows, pos
+    w, b, lam = csr.cache[key]
     nnz = int(csr.cols.numel())
     if exact is None:
         exact = nnz * R * R <= (1 << 26)
     if exact:
+        rows = torch.repeat_interleave(torch.arange(n, device=dev), csr.indptr[1:] - csr.indptr[:-1])
         rhs = A.pass_(1, csr.indptr, csr.cols, b, Ffull, None)
         Fg = Ffull[csr.cols.long()].to(torch.float64)
         outer = Fg[:, :, None] * Fg[:, None, :] * w.to(torch.float64)[:, None, None]
@@ -123,6 +133,16 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
     x = X0.clone()
     # first residual: the rhs and A x0 gather the same factor rows -> one fused pass
     ax, rhs = A.pass_both(csr.indptr, csr.cols, w, Ffull, x, b)
+    if FUSED_CG and A.cg_kernel_ok(Ffull) and x.is_contiguous() and x.dtype == torch.float32:
+        # device path: every CG vector update is one fused row-wise kernel (als_cg_kernel)
+        use_g = implicit and FtF is not None
+        lam_c = lam.contiguous()
+        r, p, rs = A.cg_init(x, ax, (x @ FtF) if use_g else None, rhs, lam_c)
+        del ax, rhs
+        for _ in range(cg_iters):
+            ap = A.pass_(0, csr.indptr, csr.cols, w, Ffull, p)
+            A.cg_step(x, r, p, ap, (p @ FtF) if use_g else None, lam_c, rs)
+        return x.clamp_min(0) if nonneg else x
     if implicit and FtF is not None:
         ax = ax + x @ FtF
     r = rhs - (ax + lam[:, None] * x)

@@ -49,3 +49,26 @@ def pass_both(indptr, cols, coef, F, V, coef2):
                                          out2.data_ptr(), N.stream_of(Fc)), "als_pass2")
         return out, out2
     return pass_torch(0, indptr, cols, coef, F, V), pass_torch(1, indptr, cols, coef2, F, None)
+
+
+def cg_kernel_ok(F: torch.Tensor) -> bool:
+    return F.is_cuda and F.dtype == torch.float32 and F.shape[1] <= 512
+
+
+def cg_init(x, ax, pf, rhs, lam):
+    """Fused CG start (als_cg_kernel mode 0): returns (r, p, rs) for
+    r = rhs - (ax + pf + lam*x)."""
+    n, R = x.shape
+    r = torch.empty_like(x)
+    p = torch.empty_like(x)
+    rs = torch.empty(n, dtype=torch.float32, device=x.device)
+    N.check(N.kernels().o3s_als_cg(0, n, R, x.data_ptr(), r.data_ptr(), p.data_ptr(), ax.data_ptr(), N.ptr(pf),
+                                   rhs.data_ptr(), lam.data_ptr(), rs.data_ptr(), N.stream_of(x)), "als_cg_init")
+    return r, p, rs
+
+
+def cg_step(x, r, p, ap, pf, lam, rs):
+    """Fused CG step (als_cg_kernel mode 1): updates x, r, p, rs in place."""
+    n, R = x.shape
+    N.check(N.kernels().o3s_als_cg(1, n, R, x.data_ptr(), r.data_ptr(), p.data_ptr(), ap.data_ptr(), N.ptr(pf),
+                                   None, lam.data_ptr(), rs.data_ptr(), N.stream_of(x)), "als_cg_step")

@@ -124,3 +124,24 @@ def test_gpu_als_cg_close_to_exact():
     pe = (ex._U @ ex._V.T)
     pc = (res.U @ res.V.T)
     assert ((pe - pc).norm() / pe.norm()).item() < 0.05
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("implicit,R", [(True, 128), (False, 40), (True, 200)])
+def test_gpu_fused_cg_matches_torch_cg(implicit, R):
+    """als_cg_kernel (fused CG vector updates) vs the same CG as separate torch ops."""
+    s = Session(SessionConf().set("o3s.device", "cuda"))
+    df = s.synthetic.ratings(30000, 4000, 500000, rank=8, seed=2, implicit=implicit)
+    users = df.column_data("user").data.long()
+    items = df.column_data("item").data.long()
+    r = df.column_data("rating").data
+    out = []
+    for fused in (True, False):
+        AE.FUSED_CG = fused
+        try:
+            res = AE.fit_als(s.comm, users, items, r, R, 2, 0.1, implicit, 1.0, 3, cg_iters=3, exact=False)
+        finally:
+            AE.FUSED_CG = True
+        out.append((res.U.clone(), res.V.clone()))
+    for a, b in zip(out[0], out[1]):
+        assert ((a - b).norm() / b.norm()).item() < 1e-4
