@@ -137,6 +137,13 @@ class MultilayerPerceptronClassificationModel(U.ProbabilisticClassifierMixin, Mo
                                               MLReadable):
     """Model fitted by MultilayerPerceptronClassifier."""
 
+    def evaluate(self, df):
+        """Multiclass metrics of this model's predictions on ``df`` (Spark >= 3.1)."""
+        from . import _summary as S
+        g = self.getOrDefault
+        return S.ClassificationSummary(lambda: self.transform(df), labelCol=g(self.labelCol),
+                                       predictionCol=g(self.predictionCol))
+
     def __init__(self):
         super().__init__()
         self._layers = []

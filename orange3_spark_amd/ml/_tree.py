@@ -123,6 +123,14 @@ class _TreeModelMixin:
     def treeWeights(self):
         return list(self._ens.weights)
 
+    def predictLeaf(self, value):
+        """Leaf node id of ``value`` (a feature vector) in every tree, as a DenseVector
+        (node ids are heap-numbered: root 1, children 2i / 2i+1; Spark's own leaf
+        numbering is an implementation detail -- parity unpinned)."""
+        x = np.asarray(value.toArray() if hasattr(value, "toArray") else value, dtype=np.float64)[None, :]
+        X = torch.from_numpy(x)
+        return DenseVector([float(t.leaf_of(X)[0]) for t in self._ens.trees])
+
     @property
     def getNumTrees(self):
         return len(self._ens.trees)
@@ -294,6 +302,18 @@ class _TreeClassifierModel(_TreeModelMixin, U.ProbabilisticClassifierMixin, Mode
         if ens.kind == "dt":
             return probs[0] * 1.0
         return torch.stack(probs).sum(0)
+
+    def evaluate(self, df):
+        """Spark >= 3.1 tree-classifier summary on ``df``: binary (ROC / PR curves, AUC)
+        for two classes, multiclass metrics otherwise."""
+        from . import _summary as S
+        g = self.getOrDefault
+        kw = dict(labelCol=g(self.labelCol), predictionCol=g(self.predictionCol),
+                  weightCol=g(self.weightCol) if self.isDefined(self.weightCol) and g(self.weightCol) else None)
+        pred = (lambda: self.transform(df))
+        if self.numClasses == 2:
+            return S.BinaryClassificationSummary(pred, scoreCol=g(self.probabilityCol), **kw)
+        return S.ClassificationSummary(pred, **kw)
 
     def _raw2prob(self, raw):
         if self._ens.kind == "gbt":

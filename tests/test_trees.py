@@ -161,3 +161,15 @@ def test_gpu_bin_features_matches_bucketize(gpu, n, F, nb):
         ref[:, f] = torch.bucketize(X[:, f], t).to(torch.uint8) if t.numel() else 0
     got = TR.bin_features(X.to(gpu), splits).cpu()
     assert torch.equal(got, ref)
+
+
+def test_tree_models_predict_leaf_and_evaluate(cpu):
+    df, X, y = _xor_data(cpu, n=1500, seed=3)
+    rf = RandomForestClassifier(numTrees=4, maxDepth=4, seed=3).fit(df)
+    leaves = rf.predictLeaf(X[0]).toArray()
+    assert leaves.shape == (4,)
+    for t, leaf in zip(rf._ens.trees, leaves):          # a leaf: reached node that was not split
+        assert t.feature[int(leaf)] < 0 and t.count[int(leaf)] > 0
+    sm = rf.evaluate(df)
+    pred = rf.transform(df).toPandas()["prediction"].to_numpy()
+    assert abs(sm.accuracy - (pred == y).mean()) < 1e-12 and 0.5 < sm.areaUnderROC <= 1.0
