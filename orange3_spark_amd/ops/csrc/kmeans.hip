@@ -22,10 +22,10 @@
 //    fragment reads bank-conflict free (CDNA guide §5.5 T2, §5.4 rule 21).
 //
 // kmeans_update: per-cluster sums without float atomics.  Each block takes chunks of
-// R rows, counting-sorts their indices by cluster in LDS (bucket order made
-// deterministic by an in-bucket insertion sort), then each wave owns a contiguous
+// R rows, counting-sorts their indices by cluster in LDS, then each wave owns a contiguous
 // cluster range and streams its rows (coalesced 512-B row reads) accumulating in
 // registers; a cluster's sum is flushed once per chunk into the block's private slab.
+// (The bucket order is row order, produced by a stable ballot-ranked scatter.)
 // Slabs are summed by kmeans_reduce in a fixed order (bitwise deterministic).
 #include "common.h"
 
@@ -245,71 +245,113 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
 // ---------------------------------------------------------------------------------
 constexpr int kUpdThreads = 512;
 constexpr int kUpdWaves = kUpdThreads / kWave;
-constexpr int kUpdRows = 8192;
 
-// One block: chunks of kUpdRows rows; slab (block-private) = [Kp][D] sums + [Kp] counts.
+// Rows per chunk R (host-chosen, <= 65536 so sorted indices fit uint16): the largest of
+// 16384..1024 whose LDS image fits.  Bigger chunks amortise the per-chunk slab
+// read-modify-write (Kp x D floats) over more X bytes.
+__host__ __device__ inline int upd_lds_bytes(int Kp, int R) {
+  // start[Kp+1] int + per-(wave, cluster) uint16 counts + sorted[R] uint16
+  return (int)(sizeof(int) * (Kp + 1) + sizeof(uint16_t) * (kUpdWaves * Kp + R));
+}
+inline int upd_rows(int Kp) {
+  for (int R = 16384; R >= 8192; R >>= 1)              // 2 blocks per CU
+    if (upd_lds_bytes(Kp, R) <= 80 * 1024) return R;
+  for (int R = 16384; R >= 256; R >>= 1)               // 1 block per CU
+    if (upd_lds_bytes(Kp, R) <= 160 * 1024) return R;
+  return 0;
+}
+
+// One block: chunks of R rows; slab (block-private) = [Kp][D] sums + [Kp] counts.
+// Counting sort by cluster that is STABLE without any sort pass: wave w owns rows
+// [w R/8, (w+1) R/8) of the chunk; per-(wave, cluster) counts give each wave its base
+// inside every bucket, and inside a wave the 64-row groups are scattered in row order
+// with ballot ranking (peel one key per step: rank = popcount of same-key lanes below).
+// Bucket order is therefore row order -> bitwise-deterministic sums for any k (the old
+// in-bucket insertion sort was O(bucket^2) per thread, i.e. quadratic at small k).
 template <int DV>  // floats per lane per row (D = 64 * DV)
 __global__ __launch_bounds__(kUpdThreads) void kmeans_update_kernel(
     const float* __restrict__ X, int64_t n, int64_t ldx, int D, const int32_t* __restrict__ assign,
-    int Kp, float* __restrict__ slab, float* __restrict__ cnt_slab) {
+    int Kp, int R, float* __restrict__ slab, float* __restrict__ cnt_slab) {
   extern __shared__ __attribute__((aligned(16))) int smem[];
-  int* hist = smem;                  // [Kp]  bucket sizes
-  int* start = hist + Kp;            // [Kp+1] bucket starts
-  int* cursor = start + Kp + 1;      // [Kp]
-  int* sorted = cursor + Kp;         // [kUpdRows]
+  int* start = smem;                                    // [Kp+1] bucket starts
+  // [waves][Kp] uint16 counts -> per-wave bases (seg <= 2048 rows per wave fits 16 bits).
+  // Counted as 32-bit LDS atomics on the word shared by waves 2j / 2j+1 (halves never carry).
+  uint16_t* cntw = reinterpret_cast<uint16_t*>(start + Kp + 1);
+  uint32_t* cnt32 = reinterpret_cast<uint32_t*>(cntw);  // [waves/2][Kp] words
+  uint16_t* sorted = cntw + kUpdWaves * Kp;             // [R]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int seg = R / kUpdWaves;                        // rows per wave segment (multiple of 64)
+  uint16_t* mycw = cntw + (wid >> 1) * 2 * Kp;          // element (key) at mycw[2*key + (wid&1)]
+  const int half = wid & 1;
   float* myslab = slab + (int64_t)blockIdx.x * Kp * D;
   float* mycnt = cnt_slab + (int64_t)blockIdx.x * Kp;
-  const int64_t nch = (n + kUpdRows - 1) / kUpdRows;
+  const int64_t nch = (n + R - 1) / R;
   for (int64_t cidx = blockIdx.x; cidx < nch; cidx += gridDim.x) {
-    const int64_t r0 = cidx * kUpdRows;
-    const int rows = (int)min((int64_t)kUpdRows, n - r0);
-    for (int i = threadIdx.x; i < Kp; i += kUpdThreads) hist[i] = 0;
+    const int64_t r0 = cidx * R;
+    const int rows = (int)min((int64_t)R, n - r0);
+    for (int i = threadIdx.x; i < kUpdWaves / 2 * Kp; i += kUpdThreads) cnt32[i] = 0u;
     __syncthreads();
-    for (int i = threadIdx.x; i < rows; i += kUpdThreads) atomicAdd(&hist[assign[r0 + i]], 1);
+    const int s0 = wid * seg, s1 = min(rows, s0 + seg);
+    for (int i = s0 + lane; i < s1; i += kWave)
+      atomicAdd(&cnt32[(wid >> 1) * Kp + assign[r0 + i]], 1u << (16 * half));
     __syncthreads();
-    if (wid == 0) {   // exclusive scan by one wave (Kp <= a few thousand)
+    // per cluster: exclusive prefix over waves (in place), total -> start[]
+    for (int c = threadIdx.x; c < Kp; c += kUpdThreads) {
+      int run = 0;
+#pragma unroll
+      for (int j = 0; j < kUpdWaves / 2; ++j) {
+        const uint32_t v = cnt32[j * Kp + c];
+        const int lo = (int)(v & 0xffffu), hi = (int)(v >> 16);
+        cnt32[j * Kp + c] = (uint32_t)run | ((uint32_t)(run + lo) << 16);
+        run += lo + hi;
+      }
+      start[c] = run;
+    }
+    __syncthreads();
+    if (wid == 0) {   // exclusive scan of bucket sizes by one wave
       int carry = 0;
       for (int b = 0; b < Kp; b += 64) {
-        const int v = (b + lane < Kp) ? hist[b + lane] : 0;
+        const int v = (b + lane < Kp) ? start[b + lane] : 0;
         int x = v;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
           const int y = __shfl_up(x, off, 64);
           if (lane >= off) x += y;
         }
-        if (b + lane < Kp) { start[b + lane] = carry + x - v; cursor[b + lane] = carry + x - v; }
+        if (b + lane < Kp) start[b + lane] = carry + x - v;
         carry += __shfl(x, 63, 64);
       }
       if (lane == 0) start[Kp] = carry;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < rows; i += kUpdThreads) {
-      const int pos = atomicAdd(&cursor[assign[r0 + i]], 1);
-      sorted[pos] = i;
-    }
-    __syncthreads();
-    // deterministic bucket order: insertion-sort each (small) bucket by row index
-    for (int b = threadIdx.x; b < Kp; b += kUpdThreads) {
-      const int s0 = start[b], s1 = start[b + 1];
-      for (int i = s0 + 1; i < s1; ++i) {
-        const int v = sorted[i];
-        int j = i - 1;
-        while (j >= s0 && sorted[j] > v) { sorted[j + 1] = sorted[j]; --j; }
-        sorted[j + 1] = v;
+    // stable scatter: this wave's groups in row order; mycw[k] is the running base
+    for (int g = s0; g < s1; g += kWave) {
+      const int i = g + lane;
+      const int key = i < s1 ? assign[r0 + i] : -1;
+      uint64_t todo = __ballot(i < s1);
+      while (todo) {
+        const int leader = __ffsll((unsigned long long)todo) - 1;
+        const int k = __shfl(key, leader, 64);
+        const uint64_t m = __ballot(key == k);
+        if (key == k) {
+          const int rank = __popcll(m & ((1ull << lane) - 1ull));
+          sorted[start[k] + mycw[2 * k + half] + rank] = (uint16_t)i;
+        }
+        if (lane == leader) mycw[2 * k + half] = (uint16_t)(mycw[2 * k + half] + __popcll(m));
+        todo &= ~m;
       }
     }
     __syncthreads();
     // wave w owns clusters [c0, c1): its rows are the contiguous sorted range
     const int c0 = (int)((int64_t)Kp * wid / kUpdWaves), c1 = (int)((int64_t)Kp * (wid + 1) / kUpdWaves);
     for (int c = c0; c < c1; ++c) {
-      const int s0 = start[c], s1 = start[c + 1];
-      if (s0 == s1) continue;
+      const int b0 = start[c], b1 = start[c + 1];
+      if (b0 == b1) continue;
       float acc[DV];
 #pragma unroll
       for (int v = 0; v < DV; ++v) acc[v] = 0.f;
-      int i = s0;
-      for (; i + 4 <= s1; i += 4) {       // 4 rows in flight
+      int i = b0;
+      for (; i + 4 <= b1; i += 4) {       // 4 rows in flight
         float x[4][DV];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -325,7 +367,7 @@ __global__ __launch_bounds__(kUpdThreads) void kmeans_update_kernel(
 #pragma unroll
           for (int v = 0; v < DV; ++v) acc[v] += x[u][v];
       }
-      for (; i < s1; ++i) {
+      for (; i < b1; ++i) {
         const float* xp = X + (r0 + sorted[i]) * ldx;
 #pragma unroll
         for (int v = 0; v < DV; ++v) {
@@ -339,7 +381,7 @@ __global__ __launch_bounds__(kUpdThreads) void kmeans_update_kernel(
         const int col = lane + 64 * v;
         if (col < D) dst[col] += acc[v];
       }
-      if (lane == 0) mycnt[c] += (float)(s1 - s0);
+      if (lane == 0) mycnt[c] += (float)(b1 - b0);
     }
     __syncthreads();
   }
@@ -392,10 +434,11 @@ O3S_API int o3s_kmeans_assign(const float* X, int64_t n, int64_t ldx, int Dx, co
 
 O3S_API int o3s_kmeans_update_ws(int Kp, int D, int grid, int64_t* slab_floats, int64_t* cnt_floats,
                                  int* lds_bytes) {
+  const int R = upd_rows(Kp);
   *slab_floats = (int64_t)grid * Kp * D;
   *cnt_floats = (int64_t)grid * Kp;
-  *lds_bytes = (int)(sizeof(int) * (3 * Kp + 1 + kUpdRows));
-  return 0;
+  *lds_bytes = R ? upd_lds_bytes(Kp, R) : -1;   // -1: Kp too large for the LDS sort
+  return R ? 0 : -3;
 }
 
 // slab/cnt_slab must be zeroed by the caller (hipMemsetAsync) before each call.
@@ -403,12 +446,13 @@ O3S_API int o3s_kmeans_update(const float* X, int64_t n, int64_t ldx, int D, con
                               float* slab, float* cnt_slab, int grid, double* sums, double* counts,
                               hipStream_t st) {
   if (D > 256 || n < 0) return -1;
-  const int lds = (int)(sizeof(int) * (3 * Kp + 1 + kUpdRows));
-  if (lds > 160 * 1024) return -3;
+  const int R = upd_rows(Kp);
+  if (!R) return -3;
+  const int lds = upd_lds_bytes(Kp, R);
   if (n > 0) {
 #define O3S_KU(DV)                                                                                    \
   hipLaunchKernelGGL((kmeans_update_kernel<DV>), dim3(grid), dim3(kUpdThreads), lds, st, X, n, ldx, D, \
-                     assign, Kp, slab, cnt_slab);
+                     assign, Kp, R, slab, cnt_slab);
     if (D <= 64) { O3S_KU(1) } else if (D <= 128) { O3S_KU(2) } else if (D <= 192) { O3S_KU(3) } else { O3S_KU(4) }
 #undef O3S_KU
     O3S_CHECK_LAUNCH();

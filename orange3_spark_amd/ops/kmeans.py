@@ -33,6 +33,13 @@ def kernel_ok(X: torch.Tensor) -> bool:
             and X.shape[1] <= MAX_KERNEL_D and X.stride(1) == 1 and X.stride(0) % 4 == 0)
 
 
+def update_kernel_ok(X: torch.Tensor) -> bool:
+    """The slab-update kernel streams whole rows (D <= 256), independent of the assign
+    kernel's register-bound D limit."""
+    return (X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and X.shape[1] <= 256
+            and X.stride(1) == 1)
+
+
 def assign_torch(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 16):
     n = X.shape[0]
     a = torch.empty(n, dtype=torch.int32, device=X.device)
@@ -66,7 +73,10 @@ class UpdateWorkspace:
         self.K, self.D = K, D
         self.grid = grid or N.num_cus(device) * 2
         sf, cf, lb = Ct.c_int64(), Ct.c_int64(), Ct.c_int()
-        N.kernels().o3s_kmeans_update_ws(K, D, self.grid, Ct.byref(sf), Ct.byref(cf), Ct.byref(lb))
+        # -3: K too large for the in-LDS counting sort -> update() takes the torch path
+        self.ok = N.kernels().o3s_kmeans_update_ws(K, D, self.grid, Ct.byref(sf), Ct.byref(cf), Ct.byref(lb)) == 0
+        if not self.ok:
+            sf.value = cf.value = 0
         self.slab = torch.empty(sf.value, dtype=torch.float32, device=device)
         self.cnt = torch.empty(cf.value, dtype=torch.float32, device=device)
         self.sums = torch.empty((K, D), dtype=torch.float64, device=device)
@@ -84,9 +94,11 @@ def update_torch(X, a, K: int, w=None):
 
 
 def update(X, a, K: int, ws: UpdateWorkspace | None = None, w=None):
-    if not kernel_ok(X) or w is not None or X.shape[1] > 256:
+    if not update_kernel_ok(X) or w is not None:
         return update_torch(X, a, K, w)
     ws = ws or UpdateWorkspace(X.device, K, X.shape[1])
+    if not ws.ok:
+        return update_torch(X, a, K, w)
     ws.slab.zero_()
     ws.cnt.zero_()
     N.check(N.kernels().o3s_kmeans_update(X.data_ptr(), X.shape[0], X.stride(0), X.shape[1], a.data_ptr(), K,

@@ -75,6 +75,29 @@ def test_gpu_update_matches_index_add(gpu):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k,D", [(2, 128), (7, 64), (300, 200), (4099, 32)])
+def test_gpu_update_small_and_odd_k(gpu, k, D):
+    """Small k gives huge buckets (the stable ballot scatter must stay linear); K=4099 runs
+    with a smaller per-chunk row count; ties to the fp64 index_add reference."""
+    g = torch.Generator(device="cpu").manual_seed(k)
+    n = 300_001
+    X = torch.randn(n, D, generator=g).to(gpu)
+    a = torch.randint(0, k, (n,), generator=g, dtype=torch.int32).to(gpu)
+    a[:70_000] = 0                          # one very large bucket
+    s, c = K_update(X, a, k)
+    rs, rc = K.update_torch(X, a, k)
+    assert torch.allclose(s, rs, atol=5e-3)
+    assert torch.equal(c, rc)
+    s2, _ = K_update(X, a, k)
+    assert torch.equal(s, s2)
+
+
+def K_update(X, a, K_):
+    s, c = K.update(X, a, K_)
+    return s.clone(), c.clone()
+
+
+@pytest.mark.gpu
 def test_gpu_kmeans_fit(gpu):
     s = Session(SessionConf().set("o3s.device", "cuda"))
     df = s.synthetic.blobs(200_000, 128, k=64, seed=4, spread=0.5)
