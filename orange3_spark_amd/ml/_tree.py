@@ -90,14 +90,17 @@ class _GBTParams(_EnsembleParams, HasMaxIter, HasStepSize):
 
 
 # ----------------------------------------------------------------------------- training
-def _prepare(df, est, classification: bool):
+def _prepare(df, est, classification: bool, split_rows: torch.Tensor | None = None):
+    """split_rows: optional bool mask of the rows the split candidates come from (GBT with
+    a validation indicator: the training rows only, as Spark splits the dataset first)."""
     g = est.getOrDefault
     X = U.dense_features(df, g(est.featuresCol))
     X = X.float() if X.is_cuda else X.to(torch.float64)
     y = U.numeric_column(df, g(est.labelCol), torch.float64)
     w = U.weights_or_none(df, est)
     comm = df.comm
-    splits = TR.find_splits(comm, X, g(est.maxBins), g(est.seed))
+    Xs = X if split_rows is None else X[split_rows.to(X.device)]
+    splits = TR.find_splits(comm, Xs, g(est.maxBins), g(est.seed))
     bins = TR.bin_features(X, splits)
     k = U.num_classes(comm, y) if classification else 0
     rows = df._global_rows()
@@ -106,6 +109,23 @@ def _prepare(df, est, classification: bool):
 
 def _min_inst(est, df, w):
     return float(est.getOrDefault(est.minInstancesPerNode))
+
+
+def _min_wfrac(est) -> float:
+    v = float(est.getOrDefault(est.minWeightFractionPerNode))
+    if not 0.0 <= v < 0.5:
+        raise ValueError(f"minWeightFractionPerNode must be in [0.0, 0.5), got {v}")
+    return v
+
+
+def _validation_mask(est, df):
+    """Spark validationIndicatorCol (GBT): True rows validate, False rows train."""
+    if not est.isDefined(est.validationIndicatorCol):
+        return None
+    vc = est.getOrDefault(est.validationIndicatorCol)
+    if not vc:
+        return None
+    return U.numeric_column(df, vc, torch.float64) != 0
 
 
 # ----------------------------------------------------------------------------- models
@@ -124,12 +144,20 @@ class _TreeModelMixin:
         return list(self._ens.weights)
 
     def predictLeaf(self, value):
-        """Leaf node id of ``value`` (a feature vector) in every tree, as a DenseVector
-        (node ids are heap-numbered: root 1, children 2i / 2i+1; Spark's own leaf
-        numbering is an implementation detail -- parity unpinned)."""
+        """Leaf index of ``value`` (a feature vector) in every tree, as a DenseVector.
+        Leaves are numbered 0..numLeaves-1 in preorder (left to right), Spark's
+        ``Node.predictLeaf`` / ``leafCol`` numbering."""
         x = np.asarray(value.toArray() if hasattr(value, "toArray") else value, dtype=np.float64)[None, :]
         X = torch.from_numpy(x)
-        return DenseVector([float(t.leaf_of(X)[0]) for t in self._ens.trees])
+        return DenseVector([float(t.leaf_index(X)[0]) for t in self._ens.trees])
+
+    def _transform(self, df):
+        out = super()._transform(df)
+        lc = self.getOrDefault(self.leafCol) if self.hasParam("leafCol") and self.isDefined(self.leafCol) else ""
+        if lc:                                  # Spark leafCol: per-tree preorder leaf indices
+            X = self._X(df)
+            out = out.withColumnData(lc, U.vec_out(torch.stack([t.leaf_index(X) for t in self._ens.trees], 1)))
+        return out
 
     @property
     def getNumTrees(self):
@@ -357,7 +385,8 @@ class DecisionTreeClassifier(Estimator, _DecisionTreeParams, HasProbabilityCol, 
         g = self.getOrDefault
         X, y, w, bins, splits, k, rows = _prepare(df, self, True)
         tb = TR.TreeBuilder(df.comm, bins, splits, y, w, g(self.impurity).lower(), max(k, 2), g(self.maxDepth),
-                            _min_inst(self, df, w), g(self.minInfoGain), 1.0, g(self.seed))
+                            _min_inst(self, df, w), g(self.minInfoGain), 1.0, g(self.seed),
+                            min_weight_fraction=_min_wfrac(self))
         tree, _ = tb.build()
         m = DecisionTreeClassificationModel._of_tree(tree, max(k, 2))
         return m._with_parent(self)
@@ -404,7 +433,8 @@ class RandomForestClassifier(Estimator, _RFParams, HasProbabilityCol, HasRawPred
         ff = TR.feature_fraction_for(g(self.featureSubsetStrategy), X.shape[1], True, g(self.numTrees))
         ens = TR.fit_forest(df.comm, bins, splits, y, w, g(self.numTrees), g(self.impurity).lower(), max(k, 2),
                             g(self.maxDepth), _min_inst(self, df, w), g(self.minInfoGain), g(self.subsamplingRate),
-                            ff, g(self.seed), rows, g(self.bootstrap))
+                            ff, g(self.seed), rows, g(self.bootstrap),
+                            min_weight_fraction=_min_wfrac(self))
         m = RandomForestClassificationModel()
         m._ens, m.numClasses, m.numFeatures = ens, max(k, 2), X.shape[1]
         return m._with_parent(self)
@@ -438,13 +468,15 @@ class GBTClassifier(Estimator, _GBTParams, HasProbabilityCol, HasRawPredictionCo
 
     def _fit(self, df):
         g = self.getOrDefault
-        X, y, w, bins, splits, k, rows = _prepare(df, self, True)
+        val = _validation_mask(self, df)
+        X, y, w, bins, splits, k, rows = _prepare(df, self, True, None if val is None else ~val)
         if k > 2:
             raise ValueError(f"GBTClassifier currently only supports binary classification, got {k} classes")
         ff = TR.feature_fraction_for(g(self.featureSubsetStrategy), X.shape[1], True, 1)
         ens = TR.fit_gbt(df.comm, bins, splits, y, w, "logistic", g(self.maxIter), g(self.stepSize),
                          g(self.maxDepth), _min_inst(self, df, w), g(self.minInfoGain), g(self.subsamplingRate),
-                         g(self.seed), ff, rows, True)
+                         g(self.seed), ff, rows, True, validation=val,
+                         validation_tol=g(self.validationTol), min_weight_fraction=_min_wfrac(self))
         m = GBTClassificationModel()
         m._ens, m.numClasses, m.numFeatures = ens, 2, X.shape[1]
         m.trainingLossHistory = ens.losses
@@ -482,7 +514,7 @@ class DecisionTreeRegressor(Estimator, _DecisionTreeParams, MLWritable, MLReadab
         g = self.getOrDefault
         X, y, w, bins, splits, _, rows = _prepare(df, self, False)
         tb = TR.TreeBuilder(df.comm, bins, splits, y, w, "variance", 1, g(self.maxDepth), _min_inst(self, df, w),
-                            g(self.minInfoGain), 1.0, g(self.seed))
+                            g(self.minInfoGain), 1.0, g(self.seed), min_weight_fraction=_min_wfrac(self))
         tree, _ = tb.build()
         return DecisionTreeRegressionModel._of_tree(tree)._with_parent(self)
 
@@ -525,7 +557,7 @@ class RandomForestRegressor(Estimator, _RFParams, MLWritable, MLReadable):
         ff = TR.feature_fraction_for(g(self.featureSubsetStrategy), X.shape[1], False, g(self.numTrees))
         ens = TR.fit_forest(df.comm, bins, splits, y, w, g(self.numTrees), "variance", 1, g(self.maxDepth),
                             _min_inst(self, df, w), g(self.minInfoGain), g(self.subsamplingRate), ff, g(self.seed),
-                            rows, g(self.bootstrap))
+                            rows, g(self.bootstrap), min_weight_fraction=_min_wfrac(self))
         ens.num_classes = 0
         m = RandomForestRegressionModel()
         m._ens, m.numFeatures = ens, X.shape[1]
@@ -556,11 +588,13 @@ class GBTRegressor(Estimator, _GBTParams, MLWritable, MLReadable):
 
     def _fit(self, df):
         g = self.getOrDefault
-        X, y, w, bins, splits, _, rows = _prepare(df, self, False)
+        val = _validation_mask(self, df)
+        X, y, w, bins, splits, _, rows = _prepare(df, self, False, None if val is None else ~val)
         ff = TR.feature_fraction_for(g(self.featureSubsetStrategy), X.shape[1], False, 1)
         ens = TR.fit_gbt(df.comm, bins, splits, y, w, g(self.lossType).lower(), g(self.maxIter), g(self.stepSize),
                          g(self.maxDepth), _min_inst(self, df, w), g(self.minInfoGain), g(self.subsamplingRate),
-                         g(self.seed), ff, rows, False)
+                         g(self.seed), ff, rows, False, validation=val,
+                         validation_tol=g(self.validationTol), min_weight_fraction=_min_wfrac(self))
         m = GBTRegressionModel()
         m._ens, m.numFeatures = ens, X.shape[1]
         m.trainingLossHistory = ens.losses

@@ -202,8 +202,9 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
     its = []
     start = 0
     last = ckpt.latest() if ckpt is not None else None
-    if last is not None:                 # resume: this rank's factor shards (runtime/checkpoint.py)
-        start, st, _ = last
+    if last is not None and tuple(last[1]["X"].shape) == tuple(X.shape) \
+            and tuple(last[1]["Y"].shape) == tuple(Y.shape):
+        start, st, _ = last              # resume: this rank's factor shards (runtime/checkpoint.py)
         X = torch.from_numpy(st["X"]).to(dev, X.dtype)
         Y = torch.from_numpy(st["Y"]).to(dev, Y.dtype)
     for it in range(start, max_iter):
@@ -230,6 +231,8 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
             its.append(time.time() - ti)
             if ckpt is not None and ckpt.due(it + 1):
                 ckpt.save(it + 1, {"X": X.cpu().numpy(), "Y": Y.cpu().numpy()})
+    if ckpt is not None:
+        ckpt.clear()                     # finished: a later fit must not resume from this run
     Uf = comm.all_gather_v(X) if (keep_full and comm.world_size > 1) else X
     Vf = comm.all_gather_v(Y) if (keep_full and comm.world_size > 1) else Y
     return AlsResult(uid, iid, Uf, Vf, time.time() - t0, its)

@@ -291,6 +291,8 @@ def fit_glm(data: GlmData, loss: str, reg=0.0, alpha=0.0, fit_intercept=True, st
     else:
         r = optim.lbfgs(obj.smooth, x0, max_iter=left, tol=tol, callback=save)
         res = GlmResult(r.x, 0.0, r.history, done + r.iterations, r.converged)
+    if ckpt is not None:
+        ckpt.clear()                     # finished: a later fit must not resume from this run
     bt, b = obj.split(res.coef)
     res.coef = bt * obj.inv_std
     res.intercept = float(b)

@@ -123,6 +123,8 @@ def fit_kmeans(comm, X: torch.Tensor, k: int, max_iter: int = 20, tol: float = 1
     if cosine:
         X = X / X.norm(dim=1, keepdim=True).clamp_min(1e-300)
     last = ckpt.latest() if ckpt is not None else None
+    if last is not None and tuple(last[1]["C"].shape) != (k, X.shape[1]):
+        last = None                      # incompatible state: start afresh
     if last is not None:
         C = None                         # resumed below; skip the initialisation passes
     elif initial is not None:
@@ -132,7 +134,9 @@ def fit_kmeans(comm, X: torch.Tensor, k: int, max_iter: int = 20, tol: float = 1
     else:
         C = kmeans_parallel_init(comm, X, k, init_steps, seed)
     D = X.shape[1]
-    ws = K.UpdateWorkspace(X.device, ((k + 31) // 32) * 32, D) if K.kernel_ok(X) and weights is None else None
+    # the update kernel has its own gate (D <= 256, any D % 4) -- wider than the assign
+    # kernel's register-bound one, so e.g. D = 200 still gets the slab update
+    ws = K.UpdateWorkspace(X.device, ((k + 31) // 32) * 32, D) if K.update_kernel_ok(X) and weights is None else None
     hist = []
     it = start = 0
     if last is not None:                 # resume from the last saved centres
@@ -165,6 +169,8 @@ def fit_kmeans(comm, X: torch.Tensor, k: int, max_iter: int = 20, tol: float = 1
                 ckpt.save(it, {"C": C.cpu().numpy(), "hist": np.asarray(hist)})
             if moved <= tol * tol:
                 break
+    if ckpt is not None:
+        ckpt.clear()                     # finished: a later fit must not resume from this run
     # final cost/sizes w.r.t. the returned centres (Spark reports the last assignment's)
     a, d = K.assign(X, C.float())
     cnt = torch.zeros(k, dtype=torch.float64, device=X.device).index_add_(

@@ -89,6 +89,24 @@ def bin_features(X: torch.Tensor, splits: list) -> torch.Tensor:
 
 
 # ----------------------------------------------------------------------------- impurity
+def _sibling(parent: torch.Tensor, child: torch.Tensor, cls: bool) -> torch.Tensor:
+    """Histogram of the scanned child's sibling, parent - child ([P, F, B, S] fp64).
+
+    Both operands are exact ordered fp64 sums, but with fractional weights the
+    difference can still leave rounding residue in bins the sibling does not populate;
+    it is cleaned so such a bin reads as empty: weights / class counts are clamped at 0
+    and REG bins whose weight is not positive get zero w*y.  The REG node total of w*y^2
+    (feature 0, bin 0, stat 2) is only clamped at 0."""
+    sib = parent - child
+    if cls:
+        return sib.clamp_min_(0.0)
+    y2 = sib[:, 0, 0, 2].clamp_min(0.0)
+    empty = sib[..., 0] <= 0.0
+    sib[..., :2] = torch.where(empty[..., None], torch.zeros_like(sib[..., :2]), sib[..., :2])
+    sib[:, 0, 0, 2] = y2
+    return sib
+
+
 def _impurity(stats: torch.Tensor, kind: str) -> tuple[torch.Tensor, torch.Tensor]:
     """stats [..., S] -> (impurity, weight)."""
     if kind == "variance":
@@ -144,6 +162,26 @@ class Tree:
             node = torch.where(leaf, node, nxt)
         return node
 
+    def is_leaf(self, nid: int) -> bool:
+        return bool(self.feature[nid] < 0 or 2 * nid >= len(self.feature) or self.count[2 * nid] == 0)
+
+    def leaf_index_map(self) -> np.ndarray:
+        """heap node id -> Spark leaf index (leaves numbered 0..numLeaves-1 in preorder,
+        i.e. left to right, as ``leafCol`` / ``predictLeaf`` report them); -1 elsewhere."""
+        out = -np.ones(len(self.feature), dtype=np.int64)
+        nxt, stack = 0, [1]
+        while stack:
+            nid = stack.pop()
+            if self.is_leaf(nid):
+                out[nid], nxt = nxt, nxt + 1
+            else:
+                stack += [2 * nid + 1, 2 * nid]                 # left subtree first
+        return out
+
+    def leaf_index(self, X: torch.Tensor) -> torch.Tensor:
+        """Preorder leaf index of each row (int64, device of X)."""
+        return torch.from_numpy(self.leaf_index_map()).to(X.device)[self.leaf_of(X)]
+
     def predict_value(self, X: torch.Tensor) -> torch.Tensor:
         v = torch.from_numpy(self.value).to(X.device)
         return v[self.leaf_of(X)]
@@ -164,8 +202,9 @@ class TreeBuilder:
     def __init__(self, comm, bins: torch.Tensor, splits: list, y: torch.Tensor, w: torch.Tensor | None,
                  impurity: str, num_classes: int, max_depth: int = 5, min_instances: float = 1.0,
                  min_info_gain: float = 0.0, feature_fraction: float = 1.0, seed: int = 0,
-                 max_bins: int = 32, bins_t: torch.Tensor | None = None):
+                 max_bins: int = 32, bins_t: torch.Tensor | None = None, min_weight_fraction: float = 0.0):
         self.comm, self.bins, self.splits = comm, bins, splits
+        self.min_wfrac = float(min_weight_fraction)      # Spark minWeightFractionPerNode
         self.bins_t = bins_t if bins_t is not None else T.feature_major(bins)
         self.y, self.w = y, w
         self.kind = impurity
@@ -219,7 +258,7 @@ class TreeBuilder:
                     self.comm.all_reduce(Hs)
                     H = torch.empty((k, F, B, S), dtype=torch.float64, device=dev)
                     H[pick] = Hs
-                    H[pick ^ 1] = parent_H - Hs
+                    H[pick ^ 1] = _sibling(parent_H, Hs, self.cls)
             tsplit = trace("tree.split")
             tsplit.__enter__()
             tot = H[:, 0].sum(1)                                   # [k, S] node stats (feature 0 bins)
@@ -242,6 +281,10 @@ class TreeBuilder:
                 sP = tot[:, 1][:, None, None]
                 g = (sL * sL / wL.clamp_min(1e-300) + sR * sR / wR.clamp_min(1e-300) - sP * sP / W) / W
             ok = (wL >= self.min_inst) & (wR >= self.min_inst)
+            if self.min_wfrac > 0.0:
+                if depth == 0:
+                    self.min_w = self.min_wfrac * float(w_p[0])   # fraction of the root's total weight
+                ok &= (wL >= self.min_w) & (wR >= self.min_w)
             nb = torch.tensor([len(s) for s in self.splits], device=dev)
             ok &= torch.arange(B - 1, device=dev)[None, None, :] < nb[None, :, None]
             if self.ffrac < 1.0:
@@ -326,19 +369,41 @@ def subsample_weights(n_local, rows: torch.Tensor, rate: float, seed: int, boots
     return None
 
 
+def _gbt_point_loss(loss: str, yy: torch.Tensor, Fm: torch.Tensor) -> torch.Tensor:
+    if loss == "logistic":
+        return 2.0 * torch.log1p(torch.exp(-2.0 * yy * Fm))
+    if loss == "squared":
+        return (yy - Fm) ** 2
+    return (yy - Fm).abs()
+
+
 def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_iter: int = 20,
             step: float = 0.1, max_depth: int = 5, min_instances: float = 1.0, min_info_gain: float = 0.0,
             subsampling_rate: float = 1.0, seed: int = 0, feature_fraction: float = 1.0, rows=None,
-            classification: bool = True) -> Ensemble:
+            classification: bool = True, validation: torch.Tensor | None = None, validation_tol: float = 0.01,
+            min_weight_fraction: float = 0.0) -> Ensemble:
     """Spark GradientBoostedTrees.boost: tree 0 fit on (scaled) labels with weight 1, then
-    trees on pseudo-residuals with weight ``step``."""
+    trees on pseudo-residuals with weight ``step``.
+
+    ``validation`` (bool per local row, Spark's ``validationIndicatorCol``): those rows get
+    weight 0 in every tree and, after each tree, the weighted mean validation loss is
+    all-reduced; boosting stops once it improves by less than
+    ``validation_tol * max(error, 0.01)`` and the ensemble is cut back to the best
+    iteration (Spark runWithValidation semantics)."""
     dev = bins.device
     bins_t = T.feature_major(bins)                    # shared by every tree of the ensemble
     yy = y.to(torch.float64)
     if classification:
         yy = 2.0 * yy - 1.0
+    wd = torch.ones_like(yy) if w is None else w.to(torch.float64)
+    if validation is not None:
+        vmask = validation.to(dev, torch.bool)
+        w_val = torch.where(vmask, wd, torch.zeros_like(wd))
+        wd = torch.where(vmask, torch.zeros_like(wd), wd)
+        w = wd.float()
     Fm = torch.zeros_like(yy)
     trees, weights, losses = [], [], []
+    best_err, best_m = math.inf, 0
     for m in range(max_iter):
         if m == 0:
             target = yy
@@ -353,28 +418,36 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
             sub = subsample_weights(None, rows, subsampling_rate, seed + m, False)
             sw = sub if w is None else w * sub
         tb = TreeBuilder(comm, bins, splits, target.float(), sw, "variance", 1, max_depth, min_instances,
-                         min_info_gain, feature_fraction, seed + m, bins_t=bins_t)
+                         min_info_gain, feature_fraction, seed + m, bins_t=bins_t,
+                         min_weight_fraction=min_weight_fraction)
         tree, leaf_row = tb.build()
         wt = 1.0 if m == 0 else step
         Fm = Fm + wt * torch.from_numpy(tree.value[:, 0]).to(dev)[leaf_row]
         trees.append(tree)
         weights.append(wt)
-        if loss == "logistic":
-            l = torch.log1p(torch.exp(-2.0 * yy * Fm)).sum() * 2.0
-        elif loss == "squared":
-            l = ((yy - Fm) ** 2).sum()
-        else:
-            l = (yy - Fm).abs().sum()
-        cnt = torch.tensor([float(yy.numel())], dtype=torch.float64, device=dev)
-        buf = torch.cat([l.reshape(1), cnt])
+        pl = _gbt_point_loss(loss, yy, Fm)
+        parts = [(pl * wd).sum().reshape(1), wd.sum().reshape(1)]
+        if validation is not None:
+            parts += [(pl * w_val).sum().reshape(1), w_val.sum().reshape(1)]
+        buf = torch.cat(parts)
         comm.all_reduce(buf)
-        losses.append(float(buf[0] / buf[1]))
+        losses.append(float(buf[0] / buf[1].clamp_min(1e-300)))
+        if validation is not None:
+            err = float(buf[2] / buf[3].clamp_min(1e-300))
+            if m == 0:
+                best_err, best_m = err, 1
+            elif best_err - err < validation_tol * max(err, 0.01):
+                break
+            elif err < best_err:
+                best_err, best_m = err, m + 1
+    if validation is not None:
+        trees, weights, losses = trees[:best_m], weights[:best_m], losses[:best_m]
     return Ensemble(trees, weights, "gbt", 2 if classification else 0, losses)
 
 
 def fit_forest(comm, bins, splits, y, w, num_trees: int, impurity: str, num_classes: int, max_depth: int,
                min_instances: float, min_info_gain: float, subsampling_rate: float, feature_fraction: float,
-               seed: int, rows: torch.Tensor, bootstrap: bool) -> Ensemble:
+               seed: int, rows: torch.Tensor, bootstrap: bool, min_weight_fraction: float = 0.0) -> Ensemble:
     trees = []
     bins_t = T.feature_major(bins)
     for t in range(num_trees):
@@ -382,7 +455,8 @@ def fit_forest(comm, bins, splits, y, w, num_trees: int, impurity: str, num_clas
         if w is not None:
             sw = w if sw is None else w * sw
         tb = TreeBuilder(comm, bins, splits, y, sw, impurity, num_classes, max_depth, min_instances,
-                         min_info_gain, feature_fraction, seed + 31 * t, bins_t=bins_t)
+                         min_info_gain, feature_fraction, seed + 31 * t, bins_t=bins_t,
+                         min_weight_fraction=min_weight_fraction)
         tree, _ = tb.build()
         trees.append(tree)
     return Ensemble(trees, [1.0] * num_trees, "rf", num_classes)

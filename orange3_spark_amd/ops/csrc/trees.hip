@@ -284,7 +284,48 @@ __global__ __launch_bounds__(256) void bin_features_kernel(const float* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Deterministic fp64 range sums of slab rows: out[j][c] = sum_{r in [lo_j, lo_j+cnt_j)} in[r][c],
+// rows added in ascending order (the engine calls it twice: fp32 item slabs -> fp64
+// partials over fixed runs of <= 64 items, then partials -> one row per segment), so a
+// node's histogram is bitwise reproducible and never rounds bin weights past 2^24.
+// One thread per column (lanes read consecutive columns: coalesced), 4 rows in flight.
+template <typename T>
+__global__ __launch_bounds__(256) void slab_range_sum_kernel(const T* __restrict__ in, int64_t C,
+                                                             const int64_t* __restrict__ lo,
+                                                             const int64_t* __restrict__ cnt,
+                                                             double* __restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int64_t r0 = lo[blockIdx.y], n = cnt[blockIdx.y];
+  const T* p = in + r0 * C + c;
+  double acc = 0.0;
+  int64_t r = 0;
+  for (; r + 4 <= n; r += 4) {
+    const double a = (double)p[(r + 0) * C], b = (double)p[(r + 1) * C];
+    const double d = (double)p[(r + 2) * C], e = (double)p[(r + 3) * C];
+    acc += a; acc += b; acc += d; acc += e;                // ascending order, no reassociation
+  }
+  for (; r < n; ++r) acc += (double)p[r * C];
+  out[(int64_t)blockIdx.y * C + c] = acc;
+}
+
 }  // namespace
+
+// out[j] = ordered fp64 sum of rows [lo[j], lo[j] + cnt[j]) of in ([*][C], fp32 if
+// in_f64 == 0 else fp64); n_out <= 65535 ranges per launch.
+O3S_API int o3s_slab_range_sum(const void* in, int in_f64, int64_t C, const int64_t* lo, const int64_t* cnt,
+                               int n_out, double* out, hipStream_t st) {
+  if (n_out <= 0 || C <= 0) return 0;
+  if (n_out > 65535) return -1;
+  const dim3 grid((unsigned)((C + 255) / 256), (unsigned)n_out);
+  if (in_f64)
+    hipLaunchKernelGGL(slab_range_sum_kernel<double>, grid, dim3(256), 0, st, (const double*)in, C, lo, cnt, out);
+  else
+    hipLaunchKernelGGL(slab_range_sum_kernel<float>, grid, dim3(256), 0, st, (const float*)in, C, lo, cnt, out);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
 
 // X: [n][F] fp32 (row stride ldx); th: [F][Tp] fp32 sorted, +inf padded, Tp a power of
 // two <= 256 with at least one pad per feature; out: [n][F] uint8.

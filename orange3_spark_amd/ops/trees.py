@@ -113,36 +113,74 @@ def partition_torch(bins, order, s_lo, s_hi, s_feat, s_bin):
 def node_hist(bins: torch.Tensor, order: torch.Tensor, y: torch.Tensor, w: torch.Tensor | None,
               seg_lo: torch.Tensor, seg_hi: torch.Tensor, seg_node: torch.Tensor, n_nodes: int, B: int, S: int,
               cls: bool, chunk: int = 1 << 13) -> torch.Tensor:
-    """Histograms [n_nodes, F, B, S] (fp32) of rows order[lo:hi] for each segment -> node.
+    """Histograms [n_nodes, F, B, S] (fp64) of rows order[lo:hi] for each segment -> node.
 
     Classification: per-bin weighted class counts.  Regression (S = 3): per-bin sums of
     w and w*y; the node's sum of w*y^2 sits in (feature 0, bin 0, stat 2) -- variance
     split gains need only the first two, the node impurity the third.
 
-    Segments are split into work items of <= ``chunk`` rows; the kernel writes one slab row
-    per item and the rows are summed per node in item order (deterministic)."""
+    Segments are split into work items of <= ``chunk`` rows; the kernel writes one fp32
+    slab row per item (exact for integer weights: <= 8192 rows per item) and the slab rows
+    of each segment are summed in fp64, in item order, by ``slab_range_sum_kernel``
+    (two fixed-shape stages), so the result is bitwise reproducible and bins past 2^24
+    weight keep full precision -- which histogram subtraction (sibling = parent - child)
+    relies on."""
     F = bins.shape[1]
     dev = bins.device
-    out = torch.zeros((n_nodes, F * B * S), dtype=torch.float32, device=dev)
+    out = torch.zeros((n_nodes, F * B * S), dtype=torch.float64, device=dev)
     if seg_lo.numel() == 0:
         return out.view(n_nodes, F, B, S)
-    it_lo, it_hi, seg_id, _ = _items(seg_lo, seg_hi, chunk)
-    it_node = seg_node[seg_id].to(torch.int64)
+    it_lo, it_hi, seg_id, first = _items(seg_lo, seg_hi, chunk)
     n_items = int(it_lo.numel())
     if n_items == 0:
         return out.view(n_nodes, F, B, S)
     if hist_kernel_ok(bins, B, S, cls):
-        slab = torch.empty((n_items, F * B * S), dtype=torch.float32, device=dev)
+        C = F * B * S
+        slab = torch.empty((n_items, C), dtype=torch.float32, device=dev)
         yf = y.to(torch.float32).contiguous()
         wf = None if w is None else w.to(torch.float32).contiguous()
-        N.check(N.kernels().o3s_tree_hist(bins.data_ptr(), bins.shape[0], F, B, S, int(cls),
-                                          order.data_ptr(), yf.data_ptr(), N.ptr(wf), it_lo.data_ptr(),
-                                          it_hi.data_ptr(), n_items, slab.data_ptr(), N.stream_of(bins)),
-                "tree_hist")
-        out.index_add_(0, it_node, slab)
+        lib = N.kernels()
+        st = N.stream_of(bins)
+        N.check(lib.o3s_tree_hist(bins.data_ptr(), bins.shape[0], F, B, S, int(cls),
+                                  order.data_ptr(), yf.data_ptr(), N.ptr(wf), it_lo.data_ptr(),
+                                  it_hi.data_ptr(), n_items, slab.data_ptr(), st), "tree_hist")
+        seg_sum = _ordered_segment_sums(lib, st, slab, seg_lo, seg_hi, first, chunk)
+        out.index_add_(0, seg_node.to(torch.int64), seg_sum)    # one segment per node in the engine
         return out.view(n_nodes, F, B, S)
     # reference path (CPU / oversize bins): direct scatter-add per segment
     return hist_torch(bins, order, y, w, seg_lo, seg_hi, seg_node, n_nodes, B, S, cls)
+
+
+_RUN = 64      # slab rows per first-stage partial
+
+
+def _ordered_segment_sums(lib, st, slab, seg_lo, seg_hi, first, chunk):
+    """[nseg, C] fp64: sum of each segment's slab rows (items of a segment are contiguous
+    from ``first[s]``) in a fixed order -- runs of <= 64 items, then the runs in order."""
+    dev = slab.device
+    C = slab.shape[1]
+    nseg = seg_lo.numel()
+    lens = (seg_hi - seg_lo).clamp_min(0)
+    n_it = torch.where(lens > 0, (lens + chunk - 1) // chunk, torch.zeros_like(lens)).to(torch.int64)
+    n_run = (n_it + _RUN - 1) // _RUN
+    run_seg = torch.repeat_interleave(torch.arange(nseg, device=dev), n_run)
+    run_first = torch.cumsum(n_run, 0) - n_run
+    k = torch.arange(run_seg.numel(), device=dev) - run_first[run_seg]
+    r_lo = (first.to(torch.int64)[run_seg] + k * _RUN).contiguous()
+    r_cnt = torch.minimum(torch.full_like(r_lo, _RUN), first.to(torch.int64)[run_seg] + n_it[run_seg] - r_lo).contiguous()
+    runs = torch.empty((run_seg.numel(), C), dtype=torch.float64, device=dev)
+    out = torch.zeros((nseg, C), dtype=torch.float64, device=dev)
+    for a in range(0, runs.shape[0], 65535):
+        b = min(a + 65535, runs.shape[0])
+        N.check(lib.o3s_slab_range_sum(slab.data_ptr(), 0, C, r_lo[a:b].data_ptr(), r_cnt[a:b].data_ptr(), b - a,
+                                       runs[a:].data_ptr(), st), "slab_range_sum")
+    run_first = run_first.contiguous()
+    n_run = n_run.contiguous()
+    for a in range(0, nseg, 65535):
+        b = min(a + 65535, nseg)
+        N.check(lib.o3s_slab_range_sum(runs.data_ptr(), 1, C, run_first[a:b].data_ptr(), n_run[a:b].data_ptr(), b - a,
+                                       out[a:].data_ptr(), st), "slab_range_sum")
+    return out
 
 
 def hist_torch(bins, order, y, w, seg_lo, seg_hi, seg_node, n_nodes, B, S, cls):
@@ -151,7 +189,7 @@ def hist_torch(bins, order, y, w, seg_lo, seg_hi, seg_node, n_nodes, B, S, cls):
     out = torch.zeros(n_nodes * F * B * S, dtype=torch.float64, device=dev)
     lens = (seg_hi - seg_lo).clamp_min(0)
     if int(lens.sum()) == 0:
-        return out.view(n_nodes, F, B, S).float()
+        return out.view(n_nodes, F, B, S)
     pos = torch.cat([torch.arange(int(a), int(b), device=dev) for a, b in zip(seg_lo.tolist(), seg_hi.tolist())])
     node = torch.repeat_interleave(seg_node.to(dev), lens)
     rows = order[pos].long()
@@ -175,4 +213,4 @@ def hist_torch(bins, order, y, w, seg_lo, seg_hi, seg_node, n_nodes, B, S, cls):
                                                              torch.zeros_like(ends, dtype=cs.dtype))
         seg_tot = torch.where(lens > 0, seg_tot, torch.zeros_like(seg_tot))
         out.index_add_(0, seg_node.to(dev).long() * F * B * S + 2, seg_tot)
-    return out.view(n_nodes, F, B, S).float()
+    return out.view(n_nodes, F, B, S)

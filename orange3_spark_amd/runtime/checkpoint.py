@@ -10,8 +10,9 @@ the last checkpoint instead of iteration 0 -- e.g. after a crashed or interrupte
 Format (no pickle): ``<dir>/<key>/step-<n>/rank-<r>.npz`` (numpy arrays, loaded with
 ``allow_pickle=False``) + ``meta.json``; rank-sharded state (ALS factors) writes one file
 per rank, replicated state is written by rank 0 only.  The key hashes the estimator
-class, its params and a data fingerprint, so a changed configuration never resumes from
-a stale state.
+class, its params and a digest of every input column's rows (all ranks, in rank order),
+so a changed configuration or changed data never resumes from a stale state, and a
+completed fit clears its checkpoints.
 """
 from __future__ import annotations
 
@@ -110,13 +111,109 @@ class Checkpointer:
         return None
 
     def clear(self) -> None:
-        if self.enabled and (self.comm is None or self.comm.rank == 0):
+        """Drop every checkpoint of this key: called once a fit has COMPLETED, so a later
+        fit never resumes from a finished run's state."""
+        if not self.enabled:
+            return
+        if self.comm is not None:
+            self.comm.barrier()
+        if self.comm is None or self.comm.rank == 0:
             shutil.rmtree(self.root, ignore_errors=True)
+        if self.comm is not None:
+            self.comm.barrier()
+
+
+# --------------------------------------------------------------------------- data fingerprint
+_FP_CHUNK = 1 << 26          # int32 words per device reduction chunk (int64 temporaries: 512 MB)
+
+
+def _tensor_digest(t) -> tuple:
+    """Order-sensitive digest of a tensor's bytes, computed where the tensor lives.
+
+    The bytes are read as int32 words w_i and folded into two wrapping int64 sums,
+    sum(w_i) and sum(w_i * m_i) with m_i an odd multiplicative hash of the word position,
+    so a changed value or a permutation of rows changes the digest.  One streaming pass
+    (chunked so the int64 temporaries stay bounded); only runs when checkpointing is on.
+    """
+    import torch
+    if t is None:
+        return ("none",)
+    t = t.detach()
+    if not t.is_contiguous():
+        t = t.contiguous()
+    b = t.reshape(-1).view(torch.uint8) if t.numel() else t.new_empty(0, dtype=torch.uint8)
+    nw = b.numel() // 4
+    words = b[: nw * 4].view(torch.int32)
+    s0 = torch.zeros((), dtype=torch.int64, device=t.device)
+    s1 = torch.zeros((), dtype=torch.int64, device=t.device)
+    for lo in range(0, nw, _FP_CHUNK):
+        w = words[lo: lo + _FP_CHUNK].to(torch.int64)
+        pos = torch.arange(lo, lo + w.numel(), dtype=torch.int64, device=t.device)
+        m = ((pos * 0x9E3779B1) & 0x7FFFFFFF) | 1
+        s0 += w.sum()
+        s1 += (w * m).sum()
+    tail = bytes(b[nw * 4:].cpu().tolist())
+    return (str(t.dtype), tuple(t.shape), int(s0), int(s1), tail)
+
+
+def column_digest(col) -> tuple:
+    """Digest of one column's local rows (device columns on device, host columns on host)."""
+    from ..frame import column as C
+    try:
+        from ..synthetic import LineageVectorColumn
+    except ImportError:          # pragma: no cover
+        LineageVectorColumn = ()
+    if LineageVectorColumn and isinstance(col, LineageVectorColumn):
+        # rows past the resident prefix are a pure function of (seed, global row)
+        sp = col.spec
+        return ("lineage", sp.seed, sp.d, sp.ld, len(col), col.row0, float(sp.btrue),
+                _tensor_digest(sp.wtrue), _tensor_digest(col.data))
+    if isinstance(col, C.NumericColumn):
+        return ("num", _tensor_digest(col.data), _tensor_digest(col.valid))
+    if isinstance(col, C.VectorColumn):
+        return ("vec", col.size, _tensor_digest(col.data))
+    if isinstance(col, C.SparseVectorColumn):
+        return ("csr", col.size, _tensor_digest(col.indptr), _tensor_digest(col.indices),
+                _tensor_digest(col.values))
+    if isinstance(col, C.HostColumn):
+        h = hashlib.sha1()
+        for v in col.values:
+            h.update(repr(v).encode())
+            h.update(b"\x00")
+        return ("host", len(col), h.hexdigest())
+    return (type(col).__name__, len(col))
+
+
+def _input_columns(est, df) -> list[str]:
+    """Columns the estimator reads: every ``*Col`` / ``*Cols`` param naming a column of df."""
+    names = []
+    for p in est.params:
+        if not (p.name.endswith("Col") or p.name.endswith("Cols")) or not est.isDefined(p):
+            continue
+        v = est.getOrDefault(p)
+        for c in (v if isinstance(v, (list, tuple)) else [v]):
+            if isinstance(c, str) and c in df.columns and c not in names:
+                names.append(c)
+    return names
+
+
+def data_fingerprint(est, df) -> str:
+    """Fingerprint of the rows ``est`` would train on, identical on every rank: the global
+    row count plus the rank-ordered digests of every input column's local rows."""
+    local = fingerprint(len(df), [(c, column_digest(df.column_data(c))) for c in _input_columns(est, df)])
+    comm = df.comm
+    parts = comm.all_gather_object(local) if comm is not None and comm.world_size > 1 else [local]
+    return fingerprint(parts)
 
 
 def for_estimator(est, df, sharded: bool = False, extra=()) -> Checkpointer:
     """Checkpointer for ``est.fit(df)``: enabled when the session has a checkpoint dir and
-    the estimator's ``checkpointInterval`` (or conf ``o3s.checkpoint.interval``) is > 0."""
+    the estimator's ``checkpointInterval`` (or conf ``o3s.checkpoint.interval``) is > 0.
+
+    The key hashes the estimator class, its params, a digest of the training data
+    (:func:`data_fingerprint`) and ``extra`` (e.g. ALS user/item counts), so only a fit of
+    the same configuration on the same data resumes; solvers call ``clear()`` once a fit
+    completes."""
     session = getattr(df, "session", None)
     root = checkpoint_dir(session)
     interval = 0
@@ -125,8 +222,10 @@ def for_estimator(est, df, sharded: bool = False, extra=()) -> Checkpointer:
             interval = int(est.getOrDefault(est.getParam("checkpointInterval")))
         else:
             interval = int(session.conf.get("o3s.checkpoint.interval", "0") or 0)
+    if not root or interval <= 0:
+        return Checkpointer(None, "", 0, df.comm, sharded=sharded)
     params = sorted((p.name, repr(v)) for p, v in est.extractParamMap().items()
                     if p.name not in ("checkpointInterval",))
-    n = df.comm.sum_scalar(len(df)) if root else 0
-    key = f"{type(est).__name__}-{fingerprint(type(est).__name__, params, n, extra)}"
+    data = data_fingerprint(est, df)
+    key = f"{type(est).__name__}-{fingerprint(type(est).__name__, params, data, extra)}"
     return Checkpointer(root, key, interval, df.comm, sharded=sharded)

@@ -103,3 +103,25 @@ def test_gpu_kmeans_fit(gpu):
     df = s.synthetic.blobs(200_000, 128, k=64, seed=4, spread=0.5)
     m = KMeans(k=64, seed=1, maxIter=30).fit(df)
     assert m.summary.trainingCost / 200_000 < 128 * 0.25 * 1.3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [200, 130])
+def test_gpu_kmeans_fit_wide_d_uses_update_kernel(gpu, D, monkeypatch):
+    """D in (160, 256] or D % 4 != 0: the assign kernel falls back to torch, but the fit
+    still takes the slab update kernel (its own D <= 256 gate) and agrees with
+    an all-torch fit."""
+    calls = {"n": 0}
+    real = K.update
+
+    def spy(*a, **kw):
+        calls["n"] += 1
+        return real(*a, **kw)
+    s = Session(SessionConf().set("o3s.device", "cuda"))
+    df = s.synthetic.blobs(50_000, D, k=8, seed=2, spread=0.5)
+    monkeypatch.setattr(K, "update", spy)
+    m = KMeans(k=8, seed=1, maxIter=10, tol=0.0).fit(df)
+    assert calls["n"] >= 1
+    monkeypatch.setattr(K, "update_kernel_ok", lambda X: False)
+    ref = KMeans(k=8, seed=1, maxIter=10, tol=0.0).fit(df)
+    np.testing.assert_allclose(np.array(m.clusterCenters()), np.array(ref.clusterCenters()), rtol=1e-4, atol=1e-4)

@@ -113,3 +113,35 @@ def test_lr_and_als_resume(tmp_path):
     _crash_after_first_checkpoint(lambda: est2.fit(rd))
     a1 = est2.fit(rd)
     np.testing.assert_allclose(a1._U.numpy(), a0._U.numpy(), atol=1e-6)
+
+
+def test_checkpoint_key_tracks_data_and_completed_fits_clear(tmp_path):
+    """A same-size fit on DIFFERENT data must not resume from the first fit's state, and a
+    completed fit leaves no checkpoint behind (stale-resume bug)."""
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    s.setCheckpointDir(str(tmp_path / "ck"))
+    def ratings(seed):
+        r = np.random.default_rng(seed)
+        return s.createDataFrame(pd.DataFrame({"user": r.integers(0, 40, 800), "item": r.integers(0, 30, 800),
+                                               "rating": r.normal(size=800)}))
+    a, b = ratings(1), ratings(2)
+    ALS(rank=3, maxIter=4, seed=1, checkpointInterval=2).fit(a)
+    assert not list((tmp_path / "ck").glob("ALS-*/step-*"))          # cleared on completion
+    # leave a stale mid-fit checkpoint of A behind, then fit B (same row count)
+    _crash_after_first_checkpoint(lambda: ALS(rank=3, maxIter=4, seed=1, checkpointInterval=2).fit(a))
+    assert list((tmp_path / "ck").glob("ALS-*/step-*"))
+    got = ALS(rank=3, maxIter=4, seed=1, checkpointInterval=2).fit(b)
+    s.conf.set("spark.checkpoint.dir", "")
+    fresh = ALS(rank=3, maxIter=4, seed=1, checkpointInterval=2).fit(b)
+    np.testing.assert_allclose(got._U.numpy(), fresh._U.numpy(), atol=1e-9)
+    np.testing.assert_allclose(got._V.numpy(), fresh._V.numpy(), atol=1e-9)
+
+    s.setCheckpointDir(str(tmp_path / "ck2"))
+    s.conf.set("o3s.checkpoint.interval", "2")
+    x1 = s.synthetic.blobs(2000, 4, k=3, seed=5)
+    x2 = s.synthetic.blobs(2000, 4, k=3, seed=6)
+    _crash_after_first_checkpoint(lambda: KMeans(k=3, seed=1, maxIter=6, tol=0.0).fit(x1))
+    got = KMeans(k=3, seed=1, maxIter=6, tol=0.0).fit(x2)
+    s.conf.set("spark.checkpoint.dir", "")
+    fresh = KMeans(k=3, seed=1, maxIter=6, tol=0.0).fit(x2)
+    np.testing.assert_allclose(np.array(got.clusterCenters()), np.array(fresh.clusterCenters()), atol=1e-12)

@@ -140,6 +140,42 @@ def test_hist_subtraction_matches_full_scan(cpu, cls_model):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cls", [False, True])
+def test_gpu_hist_subtraction_exact_with_heavy_fractional_weights(gpu, cls):
+    """Sibling = parent - child equals a direct scan of the sibling when weights are
+    fractional and a bin's weight is past 2^24 (fp64 ordered slab sums), and
+    the histogram is bitwise reproducible across launches."""
+    from orange3_spark_amd.models.trees import _sibling
+    from orange3_spark_amd.ops import trees as T
+    g = torch.Generator().manual_seed(11)
+    n, F, B = 400_003, 8, 16
+    S = 3 if not cls else 2
+    bins = torch.randint(0, B, (n, F), generator=g, dtype=torch.uint8)
+    bins[: n // 2, 0] = 3                                           # one heavy bin in feature 0 ...
+    bins[n // 2:, 0] %= 3                                           # ... that only the child populates
+    y = (torch.randint(0, 2, (n,), generator=g).float() if cls else torch.randn(n, generator=g))
+    w = 700.0 + torch.rand(n, generator=g) * 0.37                    # bin 3: ~1.4e8 > 2^24
+    bins, y, w = bins.to(gpu), y.to(gpu), w.to(gpu)
+    order = torch.arange(n, dtype=torch.int32, device=gpu)
+    split = 8192 * 30                                               # item-aligned: child items = parent's first 30
+    lo_p, hi_p = torch.tensor([0], device=gpu), torch.tensor([n], device=gpu)
+    nd = torch.tensor([0], device=gpu)
+    parent = T.node_hist(bins, order, y, w, lo_p, hi_p, nd, 1, B, S, cls)
+    again = T.node_hist(bins, order, y, w, lo_p, hi_p, nd, 1, B, S, cls)
+    assert parent.dtype == torch.float64 and torch.equal(parent, again)          # deterministic
+    assert float(parent[0, 0, 3, :2].sum()) > 2 ** 24
+    child = T.node_hist(bins, order, y, w, torch.tensor([0], device=gpu), torch.tensor([split], device=gpu),
+                        nd, 1, B, S, cls)
+    direct = T.node_hist(bins, order, y, w, torch.tensor([split], device=gpu), hi_p, nd, 1, B, S, cls)
+    sib = _sibling(parent, child, cls)
+    ref = T.hist_torch(bins, order, y, w, torch.tensor([split], device=gpu), hi_p, nd, 1, B, S, cls)
+    torch.testing.assert_close(direct, ref, rtol=1e-6, atol=1.0)   # fp32 per-item partials, fp64 sums
+    torch.testing.assert_close(sib, ref, rtol=1e-6, atol=1.0)
+    assert bool((sib[0, 0, 3] == 0).all())                          # empty in the sibling: exactly empty
+    assert bool((sib[..., 0] >= 0).all())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,F", [(1_000_003, 64), (4099, 12), (256, 68), (5, 4)])
 def test_gpu_u8_transpose(gpu, n, F):
     from orange3_spark_amd.ops import trees as T
@@ -168,8 +204,59 @@ def test_tree_models_predict_leaf_and_evaluate(cpu):
     rf = RandomForestClassifier(numTrees=4, maxDepth=4, seed=3).fit(df)
     leaves = rf.predictLeaf(X[0]).toArray()
     assert leaves.shape == (4,)
-    for t, leaf in zip(rf._ens.trees, leaves):          # a leaf: reached node that was not split
-        assert t.feature[int(leaf)] < 0 and t.count[int(leaf)] > 0
+    for t, leaf in zip(rf._ens.trees, leaves):          # preorder leaf index in [0, numLeaves)
+        m = t.leaf_index_map()
+        n_leaves = int((m >= 0).sum())
+        assert 0 <= leaf < n_leaves
+        heap = int(t.leaf_of(torch.from_numpy(X[:1]))[0])
+        assert m[heap] == leaf and t.feature[heap] < 0
+    # leafCol: one preorder index per tree, matching predictLeaf row by row
+    out = rf.copy({rf.leafCol: "leaf"}).transform(df).toPandas()
+    got = np.stack(out["leaf"].map(lambda v: v.toArray()))
+    np.testing.assert_array_equal(got[:5], np.stack([rf.predictLeaf(x).toArray() for x in X[:5]]))
     sm = rf.evaluate(df)
     pred = rf.transform(df).toPandas()["prediction"].to_numpy()
     assert abs(sm.accuracy - (pred == y).mean()) < 1e-12 and 0.5 < sm.areaUnderROC <= 1.0
+
+
+def test_leaf_index_is_preorder():
+    from orange3_spark_amd.models.trees import Tree
+    # root 1 splits; 2 is a leaf; 3 splits into leaves 6, 7  -> preorder leaves 2, 6, 7
+    size = 8
+    feat = -np.ones(size, dtype=np.int64)
+    feat[1], feat[3] = 0, 0
+    cnt = np.zeros(size)
+    cnt[[1, 2, 3, 6, 7]] = 1
+    t = Tree(feat, np.zeros(size), np.zeros(size, dtype=np.int64), np.zeros((size, 1)), np.zeros(size),
+             np.zeros(size), cnt, 1)
+    m = t.leaf_index_map()
+    assert (m[2], m[6], m[7]) == (0, 1, 2) and m[1] == -1 and m[3] == -1
+
+
+def test_gbt_validation_indicator_stops_early(cpu):
+    rng = np.random.default_rng(9)
+    X = rng.uniform(-1, 1, size=(3000, 4))
+    y = (X[:, 0] + 0.3 * rng.normal(size=3000) > 0).astype(float)
+    val = rng.uniform(size=3000) < 0.3
+    df = cpu.createDataFrame(pd.DataFrame({"features": list(X), "label": y, "isVal": val}))
+    full = GBTClassifier(maxIter=40, maxDepth=3, stepSize=0.5).fit(df)
+    es = GBTClassifier(maxIter=40, maxDepth=3, stepSize=0.5, validationIndicatorCol="isVal",
+                       validationTol=0.01).fit(df)
+    assert len(full.trees) == 40
+    assert 1 <= len(es.trees) < 40                      # noisy label: validation loss plateaus early
+    # training rows only: a fit on the train split alone grows the same first tree
+    tr = cpu.createDataFrame(pd.DataFrame({"features": list(X[~val]), "label": y[~val]}))
+    one = GBTClassifier(maxIter=1, maxDepth=3).fit(tr)
+    np.testing.assert_allclose(es._ens.trees[0].value[:, 0], one._ens.trees[0].value[:, 0], atol=1e-9)
+
+
+def test_min_weight_fraction_per_node(cpu):
+    df, X, y = _xor_data(cpu, n=2000, seed=8)
+    deep = DecisionTreeClassifier(maxDepth=8).fit(df)
+    frac = DecisionTreeClassifier(maxDepth=8, minWeightFractionPerNode=0.2).fit(df)
+    t = frac._ens.trees[0]
+    leaves = [i for i in range(1, len(t.feature)) if t.count[i] > 0 and t.is_leaf(i)]
+    assert min(t.count[i] for i in leaves) >= 0.2 * 2000 - 1e-9
+    assert frac.numNodes < deep.numNodes
+    with pytest.raises(ValueError):
+        DecisionTreeClassifier(minWeightFractionPerNode=0.6).fit(df)
