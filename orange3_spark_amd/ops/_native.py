@@ -43,7 +43,9 @@ _SIGS: dict[str, list] = {
     "o3s_synth_glm": [c_vp, c_i64, c_i64, c_vp, c_u32, c_i64, c_vp, c_f32, c_i32, c_vp],
     "o3s_glm_margin": [c_vp, c_i64, c_i64, c_vp, c_f32, c_vp, c_i32, c_vp],
     "o3s_glm_colstats": [c_i32, c_vp, c_i64, c_i64, c_vp, c_u32, c_i64, c_vp, c_i32, c_vp, c_vp],
-    "o3s_kmeans_assign": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
+    "o3s_kmeans_assign": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp],
+    "o3s_kmeans_screen": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, C.c_float, c_vp, c_vp, c_vp,
+                          c_vp, c_i32, c_vp],
     "o3s_kmeans_update_ws": [c_i32, c_i32, c_i32, C.POINTER(c_i64), C.POINTER(c_i64), C.POINTER(c_i32)],
     "o3s_murmur3_terms": [c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp, c_vp],
     "o3s_als_cg": [c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],

@@ -51,7 +51,7 @@ template <int KS, int TT>
 __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
     const float* __restrict__ X, int64_t n, int64_t ldx, const uint16_t* __restrict__ Chi,
     const uint16_t* __restrict__ Clo, const float* __restrict__ cn, int Cpad,
-    int32_t* __restrict__ assign, float* __restrict__ mind, int Dx) {
+    int32_t* __restrict__ assign, float* __restrict__ mind, int Dx, const int32_t* __restrict__ rowlist) {
   constexpr int D = KS * 16;
   constexpr int SLOTS = D / 8;                 // 16-B slots per centroid row
   constexpr int CH_ELEMS = 32 * D;             // bf16 per chunk (hi or lo)
@@ -86,7 +86,8 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
     for (int P = lane; P < PIECES_X; P += kWave) {
       const int rr = P / XS, sl = P % XS;
       const int64_t row = row_base + rr;
-      const int64_t rowc = row < n ? row : n - 1;
+      int64_t rowc = row < n ? row : n - 1;
+      if (rowlist) rowc = rowlist[rowc];        // recheck pass: rows gathered by index
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 v = 4 * sl < Dx ? *reinterpret_cast<const float4*>(X + rowc * ldx + 4 * sl) : z;
       *reinterpret_cast<float4*>(xt + rr * D + 4 * (sl ^ (rr & (XS - 1) & 31))) = v;
@@ -107,7 +108,9 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
         b = *reinterpret_cast<const float4*>(xt + rr * D + 4 * ((s0 + 1) ^ sw));
       } else {
         const int64_t row = row_base + rr;
-        const float* xp = X + (row < n ? row : n - 1) * ldx;
+        int64_t rowc = row < n ? row : n - 1;
+        if (rowlist) rowc = rowlist[rowc];
+        const float* xp = X + rowc * ldx;
         const int c0 = ks * 16 + 8 * h;        // Dx % 4 == 0: whole float4s are in or out
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         a = c0 < Dx ? *reinterpret_cast<const float4*>(xp + c0) : z;
@@ -236,8 +239,265 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
     if (ov < bestv[t] || (ov == bestv[t] && oi < besti[t])) { bestv[t] = ov; besti[t] = oi; }
     const int64_t row = row_base + t * 32 + r;
     if (h == 0 && row < n) {
-      assign[row] = besti[t];
-      if (mind) mind[row] = fmaxf(bestv[t] + xnv[t], 0.f);
+      const int64_t orow = rowlist ? (int64_t)rowlist[row] : row;
+      assign[orow] = besti[t];
+      if (mind) mind[orow] = fmaxf(bestv[t] + xnv[t], 0.f);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// kmeans_screen: ONE bf16 MFMA per k-step plus a rigorous error bound.
+//
+// With xh = bf16(x), ch = bf16(c) the screened distance d~_c = ||c||^2 + (-2 ch).xh
+// differs from cn_c - 2 x.c by at most 2 (|xl.c| + |xh.cl|) + fp32 accumulation
+// <= 2^-6 ||x|| ||c|| (|xl_i| <= 2^-8 |x_i|, Cauchy-Schwarz); E = 2^-5 ||x|| max||c||
+// keeps a 2x margin.  Each lane tracks best, index and SECOND best (one v_med3: the new
+// second is med3(old best, v, old second)); a row whose margin (second - best) exceeds
+// 2E has provably the same arg-min as the exact product and is finished here: its
+// squared distance is recomputed exactly in fp32 from the register-resident split x and
+// the fp32 centre row.  Other rows (near-ties) are appended to a compacted list (one
+// atomic per wave) and re-solved by the split-precision kernel above.  This is 1/3 of
+// the MFMAs of the split kernel; the ||c||^2 bias is folded into the accumulator init
+// (read from LDS), so the epilogue is 4 VALU per distance (cmp, cndmask, min, med3).
+//
+// 4 waves (one per SIMD) x TT 32-row tiles per block, 2 blocks per CU: one block's X
+// staging and DMA prologue overlaps the other's MFMA sweep.
+constexpr int kScrWaves = 4;
+constexpr int kScrThreads = kScrWaves * kWave;
+
+template <int KS>
+struct ScrLds {
+  static constexpr int D = KS * 16;
+  static constexpr int G = D <= 128 ? 4 : 2;                    // centroid chunks per stage
+  static constexpr int CHUNK_BYTES = 2 * 32 * D;                // hi only
+  static constexpr int STAGE_BYTES = 2 * G * CHUNK_BYTES;       // double buffered
+  static constexpr int X_BYTES = kScrWaves * 32 * D * 4;        // one 32-row tile per wave
+  static constexpr int BYTES = STAGE_BYTES > X_BYTES ? STAGE_BYTES : X_BYTES;
+};
+
+template <int KS, int TT>
+__global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
+    const float* __restrict__ X, int64_t n, int64_t ldx, const uint16_t* __restrict__ Chi,
+    const float* __restrict__ cn, const float* __restrict__ C32, int ldc, int Cpad, float eps_cmax,
+    int32_t* __restrict__ assign, float* __restrict__ mind, int32_t* __restrict__ flag_cnt,
+    int32_t* __restrict__ flag_rows, int Dx) {
+  using L = ScrLds<KS>;
+  constexpr int D = L::D;
+  constexpr int G = L::G;
+  constexpr int SLOTS = D / 8;
+  constexpr int CH_ELEMS = 32 * D;
+  constexpr int PIECES = 32 * SLOTS;
+  constexpr int PER_THREAD = (G * PIECES + kScrThreads - 1) / kScrThreads;
+  static_assert(PIECES % kWave == 0, "whole waves per DMA instruction");
+  static_assert(G % 2 == 0, "chunks are processed in ping-pong pairs");
+  constexpr int XS = D / 4;
+  constexpr int XL = 32 * XS / kWave;          // float4 loads per lane per 32-row tile
+  __shared__ __attribute__((aligned(16))) uint16_t lds[L::BYTES / 2];
+  extern __shared__ __attribute__((aligned(16))) float scn[];  // [Cpad] ||c||^2
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int64_t row_base = (int64_t)blockIdx.x * (kScrWaves * 32 * TT) + (int64_t)wid * 32 * TT;
+
+  for (int i = threadIdx.x; i < Cpad; i += kScrThreads) scn[i] = cn[i];
+  // ---- X tiles -> split bf16 fragments (B operand) + ||x||^2.  All XL loads of a tile
+  // are issued before any is consumed (one HBM round trip per tile), then staged
+  // row-contiguously through this wave's LDS slice (slot XOR swizzle: conflict-free
+  // transposed reads).
+  float* xt = reinterpret_cast<float*>(lds) + wid * 32 * D;
+  bf16x8 bh[TT][KS], bl[TT][KS];
+  float xn[TT];
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+    float4 xv[XL];
+#pragma unroll
+    for (int q = 0; q < XL; ++q) {
+      const int P = lane + q * kWave;
+      const int rr = P / XS, sl = P % XS;
+      const int64_t row = row_base + t * 32 + rr;
+      const int64_t rowc = row < n ? row : n - 1;
+      const int slc = 4 * sl < Dx ? sl : 0;
+      xv[q] = *reinterpret_cast<const float4*>(X + rowc * ldx + 4 * slc);
+      if (4 * sl >= Dx) xv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < XL; ++q) {
+      const int P = lane + q * kWave;
+      const int rr = P / XS, sl = P % XS;
+      *reinterpret_cast<float4*>(xt + rr * D + 4 * (sl ^ (rr & (XS - 1) & 31))) = xv[q];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int s0 = (ks * 16 + 8 * h) / 4;
+      const int sw = r & (XS - 1) & 31;
+      const float4 a = *reinterpret_cast<const float4*>(xt + r * D + 4 * (s0 ^ sw));
+      const float4 b = *reinterpret_cast<const float4*>(xt + r * D + 4 * ((s0 + 1) ^ sw));
+      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      uint32_t ph[4], pl[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        short h0, l0, h1, l1;
+        split_bf16(v[2 * j], h0, l0);
+        split_bf16(v[2 * j + 1], h1, l1);
+        ph[j] = (uint32_t)(uint16_t)h0 | ((uint32_t)(uint16_t)h1 << 16);
+        pl[j] = (uint32_t)(uint16_t)l0 | ((uint32_t)(uint16_t)l1 << 16);
+        s = fmaf(v[2 * j], v[2 * j], s);
+        s = fmaf(v[2 * j + 1], v[2 * j + 1], s);
+      }
+      bh[t][ks] = __builtin_bit_cast(bf16x8, ph);
+      bl[t][ks] = __builtin_bit_cast(bf16x8, pl);
+      asm volatile("" : "+v"(bh[t][ks]), "+v"(bl[t][ks]));
+    }
+    xn[t] = s + __shfl_xor(s, 32, 64);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slice reads done before the next tile
+  }
+  __syncthreads();                                         // staging area free; scn visible
+
+  const int nchunks = Cpad / 32;
+  auto stage = [&](int stg, int buf) {
+#pragma unroll
+    for (int k = 0; k < PER_THREAD; ++k) {
+      const int P = threadIdx.x + k * kScrThreads;
+      const int g = P / PIECES;
+      const int chunk = stg * G + g;
+      if (P >= G * PIECES || chunk >= nchunks) continue;
+      const int Q = P % PIECES;
+      const int cr = Q / SLOTS, sw = Q % SLOTS;
+      const int sl = sw ^ (cr & 15 & (SLOTS - 1));
+      const uint16_t* src = Chi + ((int64_t)(chunk * 32 + cr)) * D + sl * 8;
+      uint16_t* dst = lds + buf * G * CH_ELEMS + (wid * kWave + k * kScrThreads) * 8;   // wave-uniform
+      __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+    }
+  };
+  // Running (best, second, index) per row.  The index is kept RELATIVE to the current
+  // chunk base (ch*32 + 4h): candidates are then the inline constants (i&3) + 8*(i>>2)
+  // and a new chunk costs one subtract -- 4 VALU per distance (cmp, 2 cndmask, med3).
+  float best[TT], second[TT];
+  int bidx[TT];
+#pragma unroll
+  for (int t = 0; t < TT; ++t) { best[t] = INFINITY; second[t] = INFINITY; bidx[t] = 0; }
+  auto epilogue = [&](const f32x16 (&a)[TT]) {
+#pragma unroll
+    for (int t = 0; t < TT; ++t) bidx[t] -= 32;          // re-base onto this chunk
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int k = (i & 3) + 8 * (i >> 2);
+#pragma unroll
+      for (int t = 0; t < TT; ++t) {
+        const float dv = a[t][i];
+        const bool better = dv < best[t];
+        second[t] = __builtin_amdgcn_fmed3f(best[t], dv, second[t]);
+        bidx[t] = better ? k : bidx[t];
+        best[t] = better ? dv : best[t];
+      }
+    }
+  };
+  // one chunk's MFMAs: accumulators start at ||c||^2 (bias folded into the first MFMA's C)
+  auto sweep = [&](const uint16_t* Lh, int ch, f32x16 (&acc)[TT]) {
+    const int cbase = ch * 32 + 4 * h;
+    f32x16 c0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 c4 = *reinterpret_cast<const float4*>(scn + cbase + 8 * q);
+      c0[4 * q + 0] = c4.x; c0[4 * q + 1] = c4.y; c0[4 * q + 2] = c4.z; c0[4 * q + 3] = c4.w;
+    }
+    auto afrag = [&](int ks) {
+      const int sw = (ks * 2 + h) ^ (r & 15 & (SLOTS - 1));
+      return *reinterpret_cast<const bf16x8*>(Lh + r * D + sw * 8);
+    };
+    bf16x8 nh = afrag(0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 ah = nh;
+      if (ks + 1 < KS) nh = afrag(ks + 1);
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t][ks], ks == 0 ? c0 : acc[t], 0, 0, 0);
+    }
+  };
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // ping-pong accumulators: the epilogue of one chunk runs beside the next chunk's MFMAs
+  f32x16 accA[TT], accB[TT];
+  const int nstages = (nchunks + G - 1) / G;
+  bool pendA = false, pendB = false;
+  for (int stg = 0; stg < nstages; ++stg) {
+    const int buf = stg & 1;
+    if (stg + 1 < nstages) stage(stg + 1, buf ^ 1);
+#pragma unroll
+    for (int g = 0; g < G; g += 2) {
+      const int ch = stg * G + g;
+      if (ch < nchunks) {
+        sweep(lds + (buf * G + g) * CH_ELEMS, ch, accA);
+        if (pendB) epilogue(accB);
+        pendA = true; pendB = false;
+      }
+      if (ch + 1 < nchunks) {
+        sweep(lds + (buf * G + g + 1) * CH_ELEMS, ch + 1, accB);
+        if (pendA) epilogue(accA);
+        pendB = true; pendA = false;
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (pendA) epilogue(accA);
+  if (pendB) epilogue(accB);
+  const int last_base = (nchunks - 1) * 32 + 4 * h;
+
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+    // absolute index, then merge the half-waves (disjoint centroid subsets of one row)
+    const int myi = bidx[t] + last_base;
+    const float ob = __shfl_xor(best[t], 32, 64), os = __shfl_xor(second[t], 32, 64);
+    const int oi = __shfl_xor(myi, 32, 64);
+    const float sec = fminf(fmaxf(best[t], ob), fminf(second[t], os));
+    const bool take = ob < best[t] || (ob == best[t] && oi < myi);
+    const int idx = take ? oi : myi;
+    const float bv = fminf(best[t], ob);
+    // exact fp32 squared distance to the chosen centre from x = xh + xl (branch-free:
+    // padded columns hold x = 0 and read c = 0)
+    const float* cp = C32 + (int64_t)idx * ldc;
+    float s = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c0 = ks * 16 + 8 * h;
+      const bool v0 = c0 < Dx, v1 = c0 + 4 < Dx;
+      float4 u = *reinterpret_cast<const float4*>(cp + (v0 ? c0 : 0));
+      float4 w = *reinterpret_cast<const float4*>(cp + (v1 ? c0 + 4 : 0));
+      if (!v0) u = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!v1) w = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float cv[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+      const uint32_t* ph = reinterpret_cast<const uint32_t*>(&bh[t][ks]);
+      const uint32_t* pl = reinterpret_cast<const uint32_t*>(&bl[t][ks]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t hw = ph[j >> 1], lw = pl[j >> 1];
+        const float xh = __uint_as_float((j & 1) ? (hw & 0xffff0000u) : (hw << 16));
+        const float xl = __uint_as_float((j & 1) ? (lw & 0xffff0000u) : (lw << 16));
+        const float df = (xh + xl) - cv[j];
+        s = fmaf(df, df, s);
+      }
+    }
+    s += __shfl_xor(s, 32, 64);
+    const int64_t row = row_base + t * 32 + r;
+    const float bound = 2.f * eps_cmax * sqrtf(xn[t]);
+    const bool ok = row < n && h == 0;
+    const bool fl = ok && !(sec - bv > bound);             // near-tie (or NaN): exact re-solve
+    if (ok) {
+      assign[row] = idx;
+      if (mind) mind[row] = s;
+    }
+    const uint64_t m = __ballot(fl);
+    if (m) {
+      const int leader = __ffsll((unsigned long long)m) - 1;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(flag_cnt, (int)__popcll(m));
+      base = __shfl(base, leader, 64);
+      if (fl) flag_rows[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)row;
     }
   }
 }
@@ -408,9 +668,10 @@ __global__ void kmeans_reduce_kernel(const float* __restrict__ slab, const float
 
 // D must be a multiple of 16 (<= 256), X rows 16-B aligned (ldx % 4 == 0); Cpad % 32 == 0.
 // Dx: true feature count (% 4 == 0); Chi/Clo are [Cpad][Dp] with Dp = roundup(Dx, 32).
+// rowlist (optional): process rows rowlist[0..n) of X (the screen pass's near-ties).
 O3S_API int o3s_kmeans_assign(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi,
                               const void* Clo, const float* cn, int Cpad, int32_t* assign, float* mind,
-                              hipStream_t st) {
+                              const int32_t* rowlist, hipStream_t st) {
   if (n <= 0) return 0;
   const int D = (Dx + 31) / 32 * 32;
   if (Dx % 4 != 0 || D > 256 || ldx % 4 != 0 || Cpad % 32 != 0) return -1;
@@ -421,13 +682,46 @@ O3S_API int o3s_kmeans_assign(const float* X, int64_t n, int64_t ldx, int Dx, co
 #define O3S_KA(KS)                                                                                   \
   case KS:                                                                                           \
     hipLaunchKernelGGL((kmeans_assign_kernel<KS, 1>), dim3(grid), dim3(kAssignThreads), 0, st, X, n, ldx, \
-                       hi, lo, cn, Cpad, assign, mind, Dx);                                          \
+                       hi, lo, cn, Cpad, assign, mind, Dx, rowlist);                                 \
     break;
   switch (D / 16) {
     O3S_KA(2) O3S_KA(4) O3S_KA(6) O3S_KA(8) O3S_KA(10) O3S_KA(12) O3S_KA(14) O3S_KA(16)
     default: return -2;
   }
 #undef O3S_KA
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+// Screen pass (see kmeans_screen_kernel).  C32: fp32 centres [K][ldc] (ldc % 4 == 0);
+// eps_cmax = 2^-5 * max ||c||; flag_cnt (zeroed by the caller) / flag_rows [n]: near-tie
+// rows for o3s_kmeans_assign(rowlist).  tt: 32-row tiles per wave (1 or 2).
+O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
+                              const float* C32, int ldc, int Cpad, float eps_cmax, int32_t* assign, float* mind,
+                              int32_t* flag_cnt, int32_t* flag_rows, int tt, hipStream_t st) {
+  if (n <= 0) return 0;
+  const int D = (Dx + 31) / 32 * 32;
+  if (Dx % 4 != 0 || D > 160 || ldx % 4 != 0 || ldc % 4 != 0 || Cpad % 32 != 0 || n > 0x7fffffffll) return -1;
+  if (tt != 1 && tt != 2) return -1;
+  const size_t dyn = sizeof(float) * (size_t)Cpad;
+  const uint16_t* hi = (const uint16_t*)Chi;
+#define O3S_KS(KS, TT)                                                                                     \
+  {                                                                                                        \
+    const int rows_per_block = kScrWaves * 32 * TT;                                                        \
+    const int64_t grid = (n + rows_per_block - 1) / rows_per_block;                                        \
+    if (ScrLds<KS>::BYTES + dyn > 160 * 1024) return -3;                                                   \
+    hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, X, n, \
+                       ldx, hi, cn, C32, ldc, Cpad, eps_cmax, assign, mind, flag_cnt, flag_rows, Dx);       \
+  }
+  switch (D / 16) {
+    case 2: if (tt == 2) O3S_KS(2, 2) else O3S_KS(2, 1) break;
+    case 4: if (tt == 2) O3S_KS(4, 2) else O3S_KS(4, 1) break;
+    case 6: if (tt == 2) O3S_KS(6, 2) else O3S_KS(6, 1) break;
+    case 8: if (tt == 2) O3S_KS(8, 2) else O3S_KS(8, 1) break;
+    case 10: O3S_KS(10, 1) break;
+    default: return -2;
+  }
+#undef O3S_KS
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -14,8 +14,21 @@ from . import _native as N
 MAX_KERNEL_D = 160
 
 
-def prepare_centers(C: torch.Tensor):
-    """Split -2*C into bf16 hi/lo [Kp, Dp] (zero padded) and ||c||^2 [Kp] (+inf padded)."""
+class Prepared:
+    """Centre-side operands of the assign kernels, built once per Lloyd iteration:
+    bf16 hi/lo split of -2*C [Kp, Dp] (zero padded), ||c||^2 [Kp] (+inf padded), the fp32
+    centres [K, D] (exact distance of screened rows) and max ||c|| (screen bound)."""
+
+    __slots__ = ("hi", "lo", "cn", "c32", "cmax")
+
+    def __init__(self, hi, lo, cn, c32, cmax):
+        self.hi, self.lo, self.cn, self.c32, self.cmax = hi, lo, cn, c32, cmax
+
+    def __iter__(self):                         # legacy (hi, lo, cn) unpacking
+        return iter((self.hi, self.lo, self.cn))
+
+
+def prepare_centers(C: torch.Tensor) -> Prepared:
     K, D = C.shape
     Kp, Dp = (K + 31) // 32 * 32, (D + 31) // 32 * 32
     Cd = C.to(torch.float64)
@@ -24,8 +37,10 @@ def prepare_centers(C: torch.Tensor):
     hi = m2.to(torch.bfloat16)
     lo = (m2 - hi.float()).to(torch.bfloat16)
     cn = torch.full((Kp,), float("inf"), dtype=torch.float32, device=C.device)
-    cn[:K] = (Cd * Cd).sum(1).float()
-    return hi.contiguous(), lo.contiguous(), cn
+    norms = (Cd * Cd).sum(1)
+    cn[:K] = norms.float()
+    cmax = float(norms.max().sqrt()) if K else 0.0
+    return Prepared(hi.contiguous(), lo.contiguous(), cn, C.float().contiguous(), cmax)
 
 
 def kernel_ok(X: torch.Tensor) -> bool:
@@ -55,16 +70,78 @@ def assign_torch(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 16):
     return a, d
 
 
-def assign(X: torch.Tensor, C: torch.Tensor, prepared=None):
+# screen-pass bound factor: E = SCREEN_EPS * ||x|| * max||c|| bounds the error of a one-pass
+# bf16 distance (2^-6 derived in csrc/kmeans.hip; 2x margin)
+SCREEN_EPS = 2.0 ** -5
+# fall back to the split-precision kernel for every row once the screen flags this share
+SCREEN_MAX_FLAG_FRACTION = 0.3
+SCREEN_TT = 0                 # 32-row tiles per wave in the screen kernel (0: by D)
+_screen_state: dict = {}      # (data_ptr, shape) -> last flagged fraction
+
+
+class _ScreenWs:
+    """Per-device near-tie buffers: a counter and a row list (grown on demand)."""
+
+    def __init__(self):
+        self.cnt = None
+        self.rows = None
+
+    def get(self, n: int, dev):
+        if self.cnt is None or self.cnt.device != dev:
+            self.cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.rows = None
+        if self.rows is None or self.rows.numel() < n:
+            self.rows = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        return self.cnt, self.rows
+
+
+_SWS = _ScreenWs()
+
+
+def screen_ok(X: torch.Tensor) -> bool:
+    return kernel_ok(X) and X.shape[0] < 2 ** 31
+
+
+def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", stats: dict | None = None):
+    """(cluster int32 [n], squared distance f32 [n]) of every row of X.
+
+    GPU: ``mode='screen'`` runs the one-MFMA screen kernel and re-solves only its near-tie
+    rows with the split-precision kernel; ``'split'`` runs the split kernel on every row;
+    ``'auto'`` screens unless the previous call on this X flagged more than
+    ``SCREEN_MAX_FLAG_FRACTION`` of the rows (then it splits directly)."""
     if not kernel_ok(X):
         return assign_torch(X, C)
-    hi, lo, cn = prepared or prepare_centers(C)
+    P = prepared if isinstance(prepared, Prepared) else prepare_centers(C)
     n = X.shape[0]
     a = torch.empty(n, dtype=torch.int32, device=X.device)
     d = torch.empty(n, dtype=torch.float32, device=X.device)
-    N.check(N.kernels().o3s_kmeans_assign(X.data_ptr(), n, X.stride(0), X.shape[1], hi.data_ptr(), lo.data_ptr(),
-                                          cn.data_ptr(), hi.shape[0], a.data_ptr(), d.data_ptr(), N.stream_of(X)),
+    lib = N.kernels()
+    st = N.stream_of(X)
+    key = (X.data_ptr(), tuple(X.shape))
+    if mode == "auto":
+        mode = "split" if _screen_state.get(key, 0.0) > SCREEN_MAX_FLAG_FRACTION or not screen_ok(X) else "screen"
+    if mode == "screen" and screen_ok(X):
+        cnt, rows = _SWS.get(n, X.device)
+        cnt.zero_()
+        tt = SCREEN_TT or (2 if X.shape[1] <= 128 else 1)
+        N.check(lib.o3s_kmeans_screen(X.data_ptr(), n, X.stride(0), X.shape[1], P.hi.data_ptr(), P.cn.data_ptr(),
+                                      P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0],
+                                      Ct.c_float(SCREEN_EPS * P.cmax), a.data_ptr(), d.data_ptr(),
+                                      cnt.data_ptr(), rows.data_ptr(), tt, st), "kmeans_screen")
+        m = int(cnt.item())                      # the near-tie count sizes the re-solve grid
+        _screen_state[key] = m / max(n, 1)
+        if stats is not None:
+            stats["flagged"] = m
+        if m:
+            N.check(lib.o3s_kmeans_assign(X.data_ptr(), m, X.stride(0), X.shape[1], P.hi.data_ptr(),
+                                          P.lo.data_ptr(), P.cn.data_ptr(), P.hi.shape[0], a.data_ptr(),
+                                          d.data_ptr(), rows.data_ptr(), st), "kmeans_assign(recheck)")
+        return a, d
+    N.check(lib.o3s_kmeans_assign(X.data_ptr(), n, X.stride(0), X.shape[1], P.hi.data_ptr(), P.lo.data_ptr(),
+                                  P.cn.data_ptr(), P.hi.shape[0], a.data_ptr(), d.data_ptr(), None, st),
             "kmeans_assign")
+    if stats is not None:
+        stats["flagged"] = n
     return a, d
 
 

@@ -125,3 +125,49 @@ def test_gpu_kmeans_fit_wide_d_uses_update_kernel(gpu, D, monkeypatch):
     monkeypatch.setattr(K, "update_kernel_ok", lambda X: False)
     ref = KMeans(k=8, seed=1, maxIter=10, tol=0.0).fit(df)
     np.testing.assert_allclose(np.array(m.clusterCenters()), np.array(ref.clusterCenters()), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,Kc,kind", [(128, 1024, "blobs"), (128, 1024, "uniform"), (64, 100, "uniform"),
+                                       (160, 64, "blobs"), (32, 7, "uniform"), (100, 33, "blobs")])
+def test_gpu_screen_assign_matches_split_and_fp64(gpu, D, Kc, kind):
+    """One-MFMA screen + exact re-solve of near-ties == the split-precision kernel's
+    answer (and the fp64 reference), on easy (blobs) and tie-heavy (uniform) data."""
+    g = torch.Generator(device="cpu").manual_seed(D * 7 + Kc)
+    n = 40_003
+    if kind == "blobs":
+        C = torch.rand(Kc, D, generator=g) * 20 - 10
+        X = C[torch.randint(0, Kc, (n,), generator=g)] + torch.randn(n, D, generator=g)
+        C = C + 0.3 * torch.randn(Kc, D, generator=g)
+    else:
+        X = torch.rand(n, D, generator=g)
+        C = torch.rand(Kc, D, generator=g)
+    X, C = X.to(gpu), C.to(gpu)
+    P = K.prepare_centers(C)
+    st = {}
+    a1, d1 = K.assign(X, C, P, mode="screen", stats=st)
+    a3, d3 = K.assign(X, C, P, mode="split")
+    ra, rd = K.assign_torch(X, C)
+    if kind == "blobs":
+        assert st["flagged"] < n // 100                 # easy data: almost every row screened
+    assert (a1 == a3).float().mean() > 0.9999
+    assert (a1 == ra).float().mean() > 0.999
+    torch.testing.assert_close(d1.double(), rd.double(), rtol=1e-4, atol=1e-2)
+    # a row whose centre is duplicated is an exact tie: it must be flagged and re-solved
+    C2 = torch.cat([C, C[:1]])
+    a2, _ = K.assign(X[:4096], C2, mode="screen", stats=st)
+    ref2, _ = K.assign(X[:4096], C2, mode="split")
+    assert torch.equal(a2, ref2)
+
+
+@pytest.mark.gpu
+def test_gpu_screen_auto_falls_back_when_most_rows_tie(gpu):
+    g = torch.Generator(device="cpu").manual_seed(3)
+    X = torch.rand(20_000, 64, generator=g).to(gpu) * 1e-3      # all rows nearly equidistant
+    C = torch.rand(256, 64, generator=g).to(gpu)
+    st = {}
+    K.assign(X, C, mode="auto", stats=st)
+    if st["flagged"] > 0.3 * X.shape[0]:
+        st2 = {}
+        K.assign(X, C, mode="auto", stats=st2)
+        assert st2["flagged"] == X.shape[0]             # split path taken directly

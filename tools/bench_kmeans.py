@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--k", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--torch-baseline", action="store_true", help="also time a torch (rocBLAS GEMM) assign")
+    ap.add_argument("--mode", default="auto", choices=["auto", "screen", "split"],
+                    help="assign path: one-MFMA screen + near-tie re-solve, or split precision everywhere")
     a = ap.parse_args()
     s = Session.getOrCreate()
     df = s.synthetic.blobs(a.rows, a.d, k=a.k, seed=3, spread=1.0)
@@ -34,7 +36,7 @@ def main():
 
     def it(C):
         prep = K.prepare_centers(C)
-        asg, d = K.assign(X, C, prep)
+        asg, d = K.assign(X, C, prep, mode=a.mode)
         sums, cnt = K.update(X, asg, ws.K, ws)
         buf = torch.cat([sums[: a.k].reshape(-1), cnt[: a.k], d.double().sum().reshape(1)])
         comm.all_reduce(buf)
@@ -46,8 +48,9 @@ def main():
     torch.cuda.synchronize()
     t_assign = time.perf_counter()
     prep = K.prepare_centers(C)
+    st = {}
     for _ in range(a.iters):
-        asg, d = K.assign(X, C, prep)
+        asg, d = K.assign(X, C, prep, mode=a.mode, stats=st)
     torch.cuda.synchronize()
     t_assign = (time.perf_counter() - t_assign) / a.iters
     t_upd = time.perf_counter()
@@ -64,7 +67,8 @@ def main():
     flop = 2.0 * a.rows * a.k * a.d
     out = {"metric": "KMeans Lloyd iteration samples/s (k=1024, 100M x 128 fp32)", "value": a.rows / dt,
            "unit": "samples/s", "ms_per_iter": dt * 1e3, "assign_ms": t_assign * 1e3, "update_ms": t_upd * 1e3,
-           "assign_tflops_fp32_equiv": flop / t_assign / 1e12, "rows": a.rows, "d": a.d, "k": a.k, "cost": cost}
+           "assign_tflops_fp32_equiv": flop / t_assign / 1e12, "rows": a.rows, "d": a.d, "k": a.k, "cost": cost,
+           "assign_mode": a.mode, "near_tie_rows_resolved": st.get("flagged")}
     if a.torch_baseline:
         t1 = time.perf_counter()
         K.assign_torch(X[: 10_000_000], C, chunk=1 << 20)

@@ -14,13 +14,21 @@ ap.add_argument("--rows", type=int, default=20_000_000)
 ap.add_argument("--d", type=int, default=128)
 ap.add_argument("--k", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=3)
+ap.add_argument("--mode", default="auto", choices=["auto", "screen", "split"])
+ap.add_argument("--tt", type=int, default=0, help="screen kernel tiles per wave (0 = default)")
 a = ap.parse_args()
 s = Session.getOrCreate()
 df = s.synthetic.blobs(a.rows, a.d, k=a.k, seed=3, spread=1.0)
 X = df.column_data("features").data
 C = df.true_centers.float() + 0.5
 prep = K.prepare_centers(C)
-for _ in range(a.iters):
-    K.assign(X, C, prep)
+if a.tt:
+    K.SCREEN_TT = a.tt
+import time  # noqa: E402
+K.assign(X, C, prep, mode=a.mode)
 torch.cuda.synchronize()
-print("done")
+t = time.perf_counter()
+for _ in range(a.iters):
+    K.assign(X, C, prep, mode=a.mode)
+torch.cuda.synchronize()
+print(f"done {a.mode} tt={a.tt} rows={a.rows} ms/assign={(time.perf_counter() - t) / a.iters * 1e3:.2f}")
