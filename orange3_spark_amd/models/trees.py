@@ -215,7 +215,14 @@ class TreeBuilder:
         self.ffrac, self.seed = feature_fraction, seed
         self.F = bins.shape[1]
 
-    def build(self):
+    def build(self, leaf_acc: torch.Tensor | None = None, leaf_scale: float = 1.0):
+        """Grow the tree.  Returns (tree, leaf_row): leaf_row = per-row leaf node ids.
+
+        ``leaf_acc`` (fp64 [n], boosting): instead of materialising leaf_row, every segment
+        adds ``leaf_scale * value(leaf)`` to leaf_acc[row] of its rows the moment it becomes
+        a leaf (``tree_leaf_apply_kernel``), and the row permutation ping-pongs between two
+        buffers (rows of finished leaves are never needed again, so no full copy per
+        level); leaf_row is then None."""
         dev = self.bins.device
         n = self.bins.shape[0]
         F, B, S = self.F, self.B, self.S
@@ -228,34 +235,41 @@ class TreeBuilder:
         gain = np.zeros(max_nodes)
         count = np.zeros(max_nodes)
         order = torch.arange(n, dtype=torch.int32, device=dev)
-        seg_lo = torch.zeros(1, dtype=torch.int64, device=dev)
-        seg_hi = torch.full((1,), n, dtype=torch.int64, device=dev)
-        seg_node = torch.ones(1, dtype=torch.int64, device=dev)
+        spare = torch.empty_like(order) if (leaf_acc is not None and order.is_cuda) else None
+        # segment bounds live on the HOST (a few hundred int64s): per level there are two
+        # device->host copies (the split decisions, then the left counts of the partition)
+        # and the work-item plans are uploaded right after them, while the GPU is idle
+        seg_lo = np.zeros(1, dtype=np.int64)
+        seg_hi = np.full(1, n, dtype=np.int64)
+        seg_node = np.ones(1, dtype=np.int64)
         leaf_segments = []
         rng = np.random.default_rng(self.seed)
+        nb = torch.tensor([len(s_) for s_ in self.splits], device=dev)
+        bin_ids = torch.arange(B - 1, device=dev)
+        V = S if self.cls else 1
         # histogram subtraction: below the root only the globally smaller child of each
         # split is scanned; its sibling is parent - smaller (histograms are additive), which
         # at least halves the rows the hist kernel touches per level and the all-reduce size
         parent_H = None                                           # [P, F, B, S] fp64, global
-        small_right = None                                        # [P] bool: right child smaller
+        small_right = None                                        # [P] bool (host): right child smaller
         for depth in range(self.max_depth + 1):
-            nodes = seg_node.tolist()
-            if not nodes:
+            k = len(seg_node)
+            if k == 0:
                 break
-            k = len(nodes)
+            node_ids = seg_node
             with trace("tree.hist"):
                 if parent_H is None or not self.hist_subtraction:
-                    H = T.node_hist(self.bins, order, self.y, self.w, seg_lo, seg_hi,
-                                    torch.arange(k, device=dev), k, B, S, self.cls)
+                    H = T.node_hist(self.bins, order, self.y, self.w, seg_lo, seg_hi, np.arange(k), k, B, S, self.cls)
                     H = H.to(torch.float64).contiguous()
                     self.comm.all_reduce(H)                       # [k, F, B, S]
                 else:
                     P = k // 2                                    # segments come as (left, right) pairs
-                    pick = 2 * torch.arange(P, device=dev) + small_right.to(torch.int64)
-                    Hs = T.node_hist(self.bins, order, self.y, self.w, seg_lo[pick], seg_hi[pick],
-                                     torch.arange(P, device=dev), P, B, S, self.cls)
+                    pick_h = 2 * np.arange(P) + small_right.astype(np.int64)
+                    Hs = T.node_hist(self.bins, order, self.y, self.w, seg_lo[pick_h], seg_hi[pick_h],
+                                     np.arange(P), P, B, S, self.cls)
                     Hs = Hs.to(torch.float64).contiguous()
                     self.comm.all_reduce(Hs)
+                    pick = torch.from_numpy(pick_h).to(dev)
                     H = torch.empty((k, F, B, S), dtype=torch.float64, device=dev)
                     H[pick] = Hs
                     H[pick ^ 1] = _sibling(parent_H, Hs, self.cls)
@@ -285,31 +299,35 @@ class TreeBuilder:
                 if depth == 0:
                     self.min_w = self.min_wfrac * float(w_p[0])   # fraction of the root's total weight
                 ok &= (wL >= self.min_w) & (wR >= self.min_w)
-            nb = torch.tensor([len(s) for s in self.splits], device=dev)
-            ok &= torch.arange(B - 1, device=dev)[None, None, :] < nb[None, :, None]
+            ok &= bin_ids[None, None, :] < nb[None, :, None]
             if self.ffrac < 1.0:
                 m = max(1, int(math.ceil(self.ffrac * F)))
-                fmask = torch.zeros((k, F), dtype=torch.bool, device=dev)
+                fm = np.zeros((k, F), dtype=bool)
                 for i in range(k):
-                    fmask[i, torch.from_numpy(rng.choice(F, m, replace=False)).to(dev)] = True
-                ok &= fmask[:, :, None]
+                    fm[i, rng.choice(F, m, replace=False)] = True
+                ok &= torch.from_numpy(fm).to(dev)[:, :, None]
             g = torch.where(ok, g, torch.full_like(g, -math.inf))
             best = g.reshape(k, -1).max(1)
-            bf = (best.indices // (B - 1)).cpu().numpy()
-            bb = (best.indices % (B - 1)).cpu().numpy()
-            bg = best.values.cpu().numpy()
-            node_ids = np.array(nodes)
-            vals_np, imp_np, w_np = vals.cpu().numpy(), imp_p.cpu().numpy(), w_p.cpu().numpy()
+            # global child weights at the chosen split decide which child the next level scans
+            wl_best = wL.reshape(k, -1).gather(1, best.indices[:, None])[:, 0]
+            wr_best = wR.reshape(k, -1).gather(1, best.indices[:, None])[:, 0]
+            # ONE device->host copy of every per-node decision input
+            bundle = torch.cat([best.indices.to(torch.float64), best.values, imp_p, w_p, wl_best, wr_best,
+                                vals.reshape(-1)]).cpu().numpy()
+            bi = bundle[:k].astype(np.int64)
+            bg, imp_np, w_np, wl_np, wr_np = (bundle[q * k:(q + 1) * k] for q in range(1, 6))
+            vals_np = bundle[6 * k:].reshape(k, V)
+            bf, bb = bi // (B - 1), bi % (B - 1)
             value[node_ids] = vals_np
             impurity[node_ids] = imp_np
             count[node_ids] = w_np
             do_split = (bg > self.min_gain) & (bg > 0) & np.isfinite(bg) & (depth < self.max_depth)
-            # global child weights at the chosen split decide which child the next level scans
-            wl_best = wL.reshape(k, -1).gather(1, best.indices[:, None])[:, 0]
-            wr_best = wR.reshape(k, -1).gather(1, best.indices[:, None])[:, 0]
             tsplit.__exit__(None, None, None)
             if not do_split.any():
                 leaf_segments.append((seg_lo, seg_hi, seg_node))
+                if leaf_acc is not None:
+                    with trace("tree.leaf_apply"):
+                        T.leaf_apply(order, seg_lo, seg_hi, value[node_ids, 0] * leaf_scale, leaf_acc)
                 break
             tpart = trace("tree.partition")
             tpart.__enter__()
@@ -320,26 +338,43 @@ class TreeBuilder:
                     threshold[nid] = float(self.splits[bf[i]][bb[i]])
                     gain[nid] = bg[i]
             # --- partition the splitting segments
-            spl = torch.from_numpy(do_split).to(dev)
-            leaf_segments.append((seg_lo[~spl], seg_hi[~spl], seg_node[~spl]))
-            s_lo, s_hi, s_node = seg_lo[spl], seg_hi[spl], seg_node[spl]
-            s_feat = torch.from_numpy(bf[do_split]).to(dev)
-            s_bin = torch.from_numpy(bb[do_split]).to(dev)
-            parent_H = H[spl]
-            small_right = (wr_best < wl_best)[spl]
-            order, nleft = T.partition(self.bins, order, s_lo, s_hi, s_feat, s_bin, bins_t=self.bins_t)
-            mid = s_lo + nleft
-            seg_lo = torch.stack([s_lo, mid], 1).reshape(-1)
-            seg_hi = torch.stack([mid, s_hi], 1).reshape(-1)
-            seg_node = torch.stack([2 * s_node, 2 * s_node + 1], 1).reshape(-1)
+            leaf_segments.append((seg_lo[~do_split], seg_hi[~do_split], seg_node[~do_split]))
+            if leaf_acc is not None and not do_split.all():
+                with trace("tree.leaf_apply"):
+                    T.leaf_apply(order, seg_lo[~do_split], seg_hi[~do_split],
+                                 value[node_ids[~do_split], 0] * leaf_scale, leaf_acc)
+            s_lo, s_hi, s_node = seg_lo[do_split], seg_hi[do_split], seg_node[do_split]
+            parent_H = H[torch.from_numpy(do_split).to(dev)]
+            small_right = (wr_np < wl_np)[do_split]
+            if spare is not None:                                 # ping-pong: no full copy
+                new_order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
+                                               bins_t=self.bins_t, out=spare)
+                spare, order = order, new_order
+            else:
+                order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
+                                           bins_t=self.bins_t)
+            mid = s_lo + nleft.cpu().numpy().astype(np.int64)
+            seg_lo = np.stack([s_lo, mid], 1).reshape(-1)
+            seg_hi = np.stack([mid, s_hi], 1).reshape(-1)
+            seg_node = np.stack([2 * s_node, 2 * s_node + 1], 1).reshape(-1)
             tpart.__exit__(None, None, None)
             # empty local segments still participate (other ranks may have rows there)
         tree = Tree(feature, threshold, split_bin, value, impurity, gain, count, F)
-        # per-row leaf ids of the training rows (for boosting updates), no traversal needed
+        if leaf_acc is not None:
+            return tree, None
+        with trace("tree.leaf_rows"):
+            leaf_row = self._leaf_rows(n, order, leaf_segments)
+        return tree, leaf_row
+
+    @staticmethod
+    def _leaf_rows(n, order, leaf_segments):
+        """per-row leaf ids of the training rows (for boosting updates), no traversal needed"""
+        dev = order.device
         leaf_row = torch.empty(n, dtype=torch.int64, device=dev)
         for lo, hi, nd in leaf_segments:
-            if lo.numel() == 0:
+            if len(lo) == 0:
                 continue
+            lo, hi, nd = (torch.from_numpy(np.asarray(a, dtype=np.int64)).to(dev) for a in (lo, hi, nd))
             lens = (hi - lo)
             tot_ = int(lens.sum())
             if tot_ == 0:
@@ -348,7 +383,7 @@ class TreeBuilder:
             first = torch.cumsum(lens, 0) - lens
             pos = lo[sid] + (torch.arange(tot_, device=dev) - first[sid])
             leaf_row[order[pos].long()] = nd[sid]
-        return tree, leaf_row
+        return leaf_row
 
 
 # ----------------------------------------------------------------------------- ensembles
@@ -405,6 +440,8 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
     trees, weights, losses = [], [], []
     best_err, best_m = math.inf, 0
     for m in range(max_iter):
+        tg = trace("gbt.grad")
+        tg.__enter__()
         if m == 0:
             target = yy
         elif loss == "logistic":
@@ -413,6 +450,7 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
             target = 2.0 * (yy - Fm)
         else:  # absolute
             target = torch.sign(yy - Fm)
+        tg.__exit__(None, None, None)
         sw = w
         if subsampling_rate < 1.0 and rows is not None:
             sub = subsample_weights(None, rows, subsampling_rate, seed + m, False)
@@ -420,9 +458,10 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
         tb = TreeBuilder(comm, bins, splits, target.float(), sw, "variance", 1, max_depth, min_instances,
                          min_info_gain, feature_fraction, seed + m, bins_t=bins_t,
                          min_weight_fraction=min_weight_fraction)
-        tree, leaf_row = tb.build()
         wt = 1.0 if m == 0 else step
-        Fm = Fm + wt * torch.from_numpy(tree.value[:, 0]).to(dev)[leaf_row]
+        tree, _ = tb.build(leaf_acc=Fm, leaf_scale=wt)          # Fm += wt * leaf value, per row
+        tu = trace("gbt.update")
+        tu.__enter__()
         trees.append(tree)
         weights.append(wt)
         pl = _gbt_point_loss(loss, yy, Fm)
@@ -432,6 +471,7 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
         buf = torch.cat(parts)
         comm.all_reduce(buf)
         losses.append(float(buf[0] / buf[1].clamp_min(1e-300)))
+        tu.__exit__(None, None, None)
         if validation is not None:
             err = float(buf[2] / buf[3].clamp_min(1e-300))
             if m == 0:

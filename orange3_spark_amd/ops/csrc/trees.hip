@@ -9,11 +9,12 @@
 // after every level), so a work item = one contiguous run of rows of ONE node.
 //
 // LDS-privatised histograms with NO atomics and NO bank conflicts: lane (rs, f) of a
-// wave owns feature f of row-slot rs, so each lane writes only its own columns of an LDS
+// wave owns feature f of row-slot rs, so each lane updates only its own columns of an LDS
 // image laid out [rs][bin][stat][f] (f fastest: 64 lanes -> 64 banks), and every wave
-// has its own image.  At the end the block sums its waves' images in a fixed order
-// and writes ONE fp32 slab row per work item; the engine sums slab rows per node in a
-// fixed order (deterministic).
+// has its own image (plain read-modify-writes: LDS float atomics -- ds_add_f32 --
+// measured 7x slower here, profiles/gbt_hist_lds_atomic_experiment.json).  At the end
+// the block sums its waves' images in a fixed order and writes ONE fp32 slab row per
+// work item; the engine sums slab rows per node in a fixed order (deterministic).
 //
 // Stat modes: REG (S = 3: w, w*y, w*y^2 -- variance impurity, GBT residual trees) and
 // CLS (S = #classes: weighted class counts -- gini/entropy).
@@ -285,6 +286,24 @@ __global__ __launch_bounds__(256) void bin_features_kernel(const float* __restri
 }
 
 // ---------------------------------------------------------------------------------
+// Leaf apply (boosting): when a segment of `order` becomes a leaf, every row in it gets
+// the leaf's (weighted) value added to its running prediction: acc[order[p]] += val.
+// Items are contiguous runs inside one leaf segment, so each row is touched once per
+// tree -- this replaces building a per-row leaf-id column and gathering from it.
+__global__ __launch_bounds__(256) void tree_leaf_apply_kernel(const int32_t* __restrict__ order,
+                                                              const int64_t* __restrict__ it_lo,
+                                                              const int64_t* __restrict__ it_hi,
+                                                              const double* __restrict__ it_val,
+                                                              double* __restrict__ acc) {
+  const int64_t lo = it_lo[blockIdx.x], hi = it_hi[blockIdx.x];
+  const double v = it_val[blockIdx.x];
+  for (int64_t p = lo + threadIdx.x; p < hi; p += 256) {
+    const int32_t row = order[p];
+    acc[row] += v;
+  }
+}
+
+// ---------------------------------------------------------------------------------
 // Deterministic fp64 range sums of slab rows: out[j][c] = sum_{r in [lo_j, lo_j+cnt_j)} in[r][c],
 // rows added in ascending order (the engine calls it twice: fp32 item slabs -> fp64
 // partials over fixed runs of <= 64 items, then partials -> one row per segment), so a
@@ -311,6 +330,15 @@ __global__ __launch_bounds__(256) void slab_range_sum_kernel(const T* __restrict
 }
 
 }  // namespace
+
+// acc[order[p]] += it_val[i] for p in [it_lo[i], it_hi[i]) (items of leaf segments).
+O3S_API int o3s_tree_leaf_apply(const int32_t* order, const int64_t* it_lo, const int64_t* it_hi,
+                                const double* it_val, int n_items, double* acc, hipStream_t st) {
+  if (n_items <= 0) return 0;
+  hipLaunchKernelGGL(tree_leaf_apply_kernel, dim3(n_items), dim3(256), 0, st, order, it_lo, it_hi, it_val, acc);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
 
 // out[j] = ordered fp64 sum of rows [lo[j], lo[j] + cnt[j]) of in ([*][C], fp32 if
 // in_f64 == 0 else fp64); n_out <= 65535 ranges per launch.

@@ -6,6 +6,18 @@ import torch
 from . import _native as N
 
 
+def _host(x):
+    """int64 numpy view of a small index array given as numpy or a (device) tensor."""
+    import numpy as np
+    if isinstance(x, torch.Tensor):
+        return x.detach().to("cpu", torch.int64).numpy()
+    return np.asarray(x, dtype=np.int64)
+
+
+def _dev(x, dev):
+    return x.to(dev) if isinstance(x, torch.Tensor) else torch.from_numpy(_host(x)).to(dev)
+
+
 def hist_kernel_ok(bins: torch.Tensor, B: int, S: int, cls: bool) -> bool:
     if not bins.is_cuda or bins.dtype != torch.uint8:
         return False
@@ -14,20 +26,6 @@ def hist_kernel_ok(bins: torch.Tensor, B: int, S: int, cls: bool) -> bool:
     while fp < F and fp < 64:
         fp <<= 1
     return N.kernels().o3s_tree_hist_lds(fp, B, S, int(cls)) > 0
-
-
-def _items(seg_lo: torch.Tensor, seg_hi: torch.Tensor, chunk: int):
-    """Split segments into work items of <= chunk rows: (it_lo, it_hi, it_seg)."""
-    dev = seg_lo.device
-    lens = (seg_hi - seg_lo).clamp_min(0)
-    nchunks = (lens + chunk - 1) // chunk
-    nchunks = torch.where(lens > 0, nchunks, torch.zeros_like(nchunks))
-    seg_id = torch.repeat_interleave(torch.arange(seg_lo.numel(), device=dev), nchunks)
-    first = torch.cumsum(nchunks, 0) - nchunks
-    k = torch.arange(seg_id.numel(), device=dev) - first[seg_id]
-    it_lo = (seg_lo[seg_id] + k * chunk).to(torch.int64).contiguous()
-    it_hi = torch.minimum(it_lo + chunk, seg_hi[seg_id].to(torch.int64)).contiguous()
-    return it_lo, it_hi, seg_id, first
 
 
 def feature_major(bins: torch.Tensor) -> torch.Tensor | None:
@@ -44,24 +42,40 @@ def feature_major(bins: torch.Tensor) -> torch.Tensor | None:
 
 
 def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi: torch.Tensor,
-              s_feat: torch.Tensor, s_bin: torch.Tensor, chunk: int = 1 << 14, bins_t: torch.Tensor | None = None):
+              s_feat: torch.Tensor, s_bin: torch.Tensor, chunk: int = 1 << 14, bins_t: torch.Tensor | None = None,
+              out: torch.Tensor | None = None):
     """Stable split of every segment [s_lo, s_hi) of ``order`` into rows with
     bins[row, feat] <= bin (first) and the rest.  Returns (new_order, nleft per segment).
+
+    ``out`` (GPU): write the split segments into this buffer and leave every other
+    position of it untouched (ping-pong buffers of a caller that no longer needs the
+    rows outside the split segments); default: a full copy of ``order`` first.
 
     GPU: two passes of ``tree_part_*_kernel`` over work items (count, then scatter to
     destinations computed by small scans here); CPU: the PyTorch reference."""
     if not (bins.is_cuda and order.dtype == torch.int32):
-        return partition_torch(bins, order, s_lo, s_hi, s_feat, s_bin)
+        dv = bins.device
+        return partition_torch(bins, order, _dev(s_lo, dv), _dev(s_hi, dv), _dev(s_feat, dv), _dev(s_bin, dv))
+    import numpy as np
     dev = bins.device
     F = bins.shape[1]
-    nseg = s_lo.numel()
-    it_lo, it_hi, it_seg, first_item = _items(s_lo, s_hi, chunk)
-    n_items = int(it_lo.numel())
-    new_order = order.clone()
+    # work items planned on the host (segment bounds are tiny) and uploaded in one copy
+    lo, hi = _host(s_lo), _host(s_hi)
+    nseg = len(lo)
+    n_it = (np.maximum(hi - lo, 0) + chunk - 1) // chunk
+    first = np.cumsum(n_it) - n_it
+    n_items = int(n_it.sum())
+    new_order = order.clone() if out is None else out
     if n_items == 0:
         return new_order, torch.zeros(nseg, dtype=torch.int64, device=dev)
-    it_feat = s_feat[it_seg].to(torch.int32).contiguous()
-    it_bin = s_bin[it_seg].to(torch.int32).contiguous()
+    seg_of = np.repeat(np.arange(nseg), n_it)
+    it_lo_h = lo[seg_of] + (np.arange(n_items) - first[seg_of]) * chunk
+    it_hi_h = np.minimum(it_lo_h + chunk, hi[seg_of])
+    i64 = torch.from_numpy(np.concatenate([it_lo_h, it_hi_h, seg_of, first[seg_of], lo[seg_of]])).to(dev)
+    it_lo, it_hi, it_seg, f, seg_lo_it = (i64[k * n_items:(k + 1) * n_items] for k in range(5))
+    fb = np.concatenate([_host(s_feat).astype(np.int32)[seg_of], _host(s_bin).astype(np.int32)[seg_of]])
+    i32 = torch.from_numpy(fb).to(dev)
+    it_feat, it_bin = i32[:n_items], i32[n_items:]
     it_left = torch.empty(n_items, dtype=torch.int64, device=dev)
     flags = torch.empty(order.shape[0], dtype=torch.uint8, device=dev)
     lib = N.kernels()
@@ -74,14 +88,48 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     nleft = torch.zeros(nseg, dtype=torch.int64, device=dev).index_add_(0, it_seg, it_left)
     cl = torch.cumsum(it_left, 0) - it_left                    # global exclusive prefixes
     cr = torch.cumsum(it_right, 0) - it_right
-    f = first_item[it_seg]                                     # first item of each item's segment
-    dst_left = (s_lo[it_seg] + cl - cl[f]).contiguous()
-    dst_right = (s_lo[it_seg] + nleft[it_seg] + cr - cr[f]).contiguous()
+    dst_left = (seg_lo_it + cl - cl[f]).contiguous()           # f: first item of each item's segment
+    dst_right = (seg_lo_it + nleft[it_seg] + cr - cr[f]).contiguous()
     N.check(lib.o3s_tree_partition(src.data_ptr(), rs, cs, order.data_ptr(), new_order.data_ptr(), it_lo.data_ptr(),
                                    it_hi.data_ptr(), it_feat.data_ptr(), it_bin.data_ptr(), None,
                                    dst_left.data_ptr(), dst_right.data_ptr(), flags.data_ptr(), n_items, 1, st),
             "tree_part_scatter")
     return new_order, nleft
+
+
+def leaf_apply(order: torch.Tensor, seg_lo: torch.Tensor, seg_hi: torch.Tensor, seg_val: torch.Tensor,
+               acc: torch.Tensor, chunk: int = 1 << 14) -> None:
+    """acc[order[p]] += seg_val[s] for every position p of segment s (fp64 acc).
+
+    GPU: ``tree_leaf_apply_kernel`` over <= chunk-row items planned on the host; CPU: torch."""
+    import numpy as np
+    if len(seg_lo) == 0:
+        return
+    dev = acc.device
+    lo, hi = _host(seg_lo), _host(seg_hi)
+    val = seg_val.detach().to("cpu", torch.float64).numpy() if isinstance(seg_val, torch.Tensor) \
+        else np.asarray(seg_val, dtype=np.float64)
+    lens = np.maximum(hi - lo, 0)
+    if not (acc.is_cuda and order.dtype == torch.int32 and acc.dtype == torch.float64):
+        if lens.sum() == 0:
+            return
+        pos = torch.from_numpy(np.concatenate([np.arange(a, b) for a, b in zip(lo, hi)])).to(order.device)
+        v = torch.from_numpy(np.repeat(val, lens)).to(acc.device, acc.dtype)
+        acc.index_add_(0, order[pos].long().to(acc.device), v)
+        return
+    n_it = (lens + chunk - 1) // chunk
+    first = np.cumsum(n_it) - n_it
+    n_items = int(n_it.sum())
+    if n_items == 0:
+        return
+    seg_of = np.repeat(np.arange(len(lo)), n_it)
+    it_lo = lo[seg_of] + (np.arange(n_items) - first[seg_of]) * chunk
+    it_hi = np.minimum(it_lo + chunk, hi[seg_of])
+    i64 = torch.from_numpy(np.concatenate([it_lo, it_hi])).to(dev)
+    fv = torch.from_numpy(np.ascontiguousarray(val[seg_of])).to(dev)
+    N.check(N.kernels().o3s_tree_leaf_apply(order.data_ptr(), i64[:n_items].data_ptr(), i64[n_items:].data_ptr(),
+                                            fv.data_ptr(), n_items, acc.data_ptr(), N.stream_of(acc)),
+            "tree_leaf_apply")
 
 
 def partition_torch(bins, order, s_lo, s_hi, s_feat, s_bin):
@@ -128,59 +176,74 @@ def node_hist(bins: torch.Tensor, order: torch.Tensor, y: torch.Tensor, w: torch
     F = bins.shape[1]
     dev = bins.device
     out = torch.zeros((n_nodes, F * B * S), dtype=torch.float64, device=dev)
-    if seg_lo.numel() == 0:
+    if len(seg_lo) == 0:
         return out.view(n_nodes, F, B, S)
-    it_lo, it_hi, seg_id, first = _items(seg_lo, seg_hi, chunk)
-    n_items = int(it_lo.numel())
-    if n_items == 0:
+    if not hist_kernel_ok(bins, B, S, cls):
+        # reference path (CPU / oversize bins): direct scatter-add per segment
+        return hist_torch(bins, order, y, w, _dev(seg_lo, dev), _dev(seg_hi, dev), _dev(seg_node, dev), n_nodes,
+                          B, S, cls)
+    plan = _HistPlan(seg_lo, seg_hi, seg_node, chunk, dev)
+    if plan.n_items == 0:
         return out.view(n_nodes, F, B, S)
-    if hist_kernel_ok(bins, B, S, cls):
-        C = F * B * S
-        slab = torch.empty((n_items, C), dtype=torch.float32, device=dev)
-        yf = y.to(torch.float32).contiguous()
-        wf = None if w is None else w.to(torch.float32).contiguous()
-        lib = N.kernels()
-        st = N.stream_of(bins)
-        N.check(lib.o3s_tree_hist(bins.data_ptr(), bins.shape[0], F, B, S, int(cls),
-                                  order.data_ptr(), yf.data_ptr(), N.ptr(wf), it_lo.data_ptr(),
-                                  it_hi.data_ptr(), n_items, slab.data_ptr(), st), "tree_hist")
-        seg_sum = _ordered_segment_sums(lib, st, slab, seg_lo, seg_hi, first, chunk)
-        out.index_add_(0, seg_node.to(torch.int64), seg_sum)    # one segment per node in the engine
-        return out.view(n_nodes, F, B, S)
-    # reference path (CPU / oversize bins): direct scatter-add per segment
-    return hist_torch(bins, order, y, w, seg_lo, seg_hi, seg_node, n_nodes, B, S, cls)
+    C = F * B * S
+    slab = torch.empty((plan.n_items, C), dtype=torch.float32, device=dev)
+    yf = y.to(torch.float32).contiguous()
+    wf = None if w is None else w.to(torch.float32).contiguous()
+    lib = N.kernels()
+    st = N.stream_of(bins)
+    N.check(lib.o3s_tree_hist(bins.data_ptr(), bins.shape[0], F, B, S, int(cls), order.data_ptr(), yf.data_ptr(),
+                              N.ptr(wf), plan.it_lo.data_ptr(), plan.it_hi.data_ptr(), plan.n_items,
+                              slab.data_ptr(), st), "tree_hist")
+    # ordered fp64 sums: runs of <= 64 item rows, then each segment's runs in order
+    runs = torch.empty((plan.n_runs, C), dtype=torch.float64, device=dev)
+    for a in range(0, plan.n_runs, 65535):
+        b = min(a + 65535, plan.n_runs)
+        N.check(lib.o3s_slab_range_sum(slab.data_ptr(), 0, C, plan.r_lo[a:].data_ptr(), plan.r_cnt[a:].data_ptr(),
+                                       b - a, runs[a:].data_ptr(), st), "slab_range_sum")
+    nseg = plan.nseg
+    seg_sum = torch.empty((nseg, C), dtype=torch.float64, device=dev)
+    for a in range(0, nseg, 65535):
+        b = min(a + 65535, nseg)
+        N.check(lib.o3s_slab_range_sum(runs.data_ptr(), 1, C, plan.s_run0[a:].data_ptr(), plan.s_nrun[a:].data_ptr(),
+                                       b - a, seg_sum[a:].data_ptr(), st), "slab_range_sum")
+    out.index_add_(0, plan.seg_node, seg_sum)             # one segment per node in the engine
+    return out.view(n_nodes, F, B, S)
 
 
 _RUN = 64      # slab rows per first-stage partial
 
 
-def _ordered_segment_sums(lib, st, slab, seg_lo, seg_hi, first, chunk):
-    """[nseg, C] fp64: sum of each segment's slab rows (items of a segment are contiguous
-    from ``first[s]``) in a fixed order -- runs of <= 64 items, then the runs in order."""
-    dev = slab.device
-    C = slab.shape[1]
-    nseg = seg_lo.numel()
-    lens = (seg_hi - seg_lo).clamp_min(0)
-    n_it = torch.where(lens > 0, (lens + chunk - 1) // chunk, torch.zeros_like(lens)).to(torch.int64)
-    n_run = (n_it + _RUN - 1) // _RUN
-    run_seg = torch.repeat_interleave(torch.arange(nseg, device=dev), n_run)
-    run_first = torch.cumsum(n_run, 0) - n_run
-    k = torch.arange(run_seg.numel(), device=dev) - run_first[run_seg]
-    r_lo = (first.to(torch.int64)[run_seg] + k * _RUN).contiguous()
-    r_cnt = torch.minimum(torch.full_like(r_lo, _RUN), first.to(torch.int64)[run_seg] + n_it[run_seg] - r_lo).contiguous()
-    runs = torch.empty((run_seg.numel(), C), dtype=torch.float64, device=dev)
-    out = torch.zeros((nseg, C), dtype=torch.float64, device=dev)
-    for a in range(0, runs.shape[0], 65535):
-        b = min(a + 65535, runs.shape[0])
-        N.check(lib.o3s_slab_range_sum(slab.data_ptr(), 0, C, r_lo[a:b].data_ptr(), r_cnt[a:b].data_ptr(), b - a,
-                                       runs[a:].data_ptr(), st), "slab_range_sum")
-    run_first = run_first.contiguous()
-    n_run = n_run.contiguous()
-    for a in range(0, nseg, 65535):
-        b = min(a + 65535, nseg)
-        N.check(lib.o3s_slab_range_sum(runs.data_ptr(), 1, C, run_first[a:b].data_ptr(), n_run[a:b].data_ptr(), b - a,
-                                       out[a:].data_ptr(), st), "slab_range_sum")
-    return out
+class _HistPlan:
+    """Work items (<= chunk rows of one segment) and their fixed-order reduction runs,
+    planned on the host from the (small) segment bounds and uploaded in ONE copy --
+    instead of a dozen tiny device ops and syncs per tree level."""
+
+    def __init__(self, seg_lo, seg_hi, seg_node, chunk: int, dev):
+        import numpy as np
+        lo, hi, nd = _host(seg_lo), _host(seg_hi), _host(seg_node)
+        lens = np.maximum(hi - lo, 0)
+        n_it = (lens + chunk - 1) // chunk
+        first = np.cumsum(n_it) - n_it
+        self.nseg = len(lo)
+        self.n_items = int(n_it.sum())
+        seg_of = np.repeat(np.arange(self.nseg), n_it)
+        k = np.arange(self.n_items) - first[seg_of]
+        it_lo = lo[seg_of] + k * chunk
+        it_hi = np.minimum(it_lo + chunk, hi[seg_of])
+        n_run = (n_it + _RUN - 1) // _RUN
+        run0 = np.cumsum(n_run) - n_run
+        self.n_runs = int(n_run.sum())
+        rseg = np.repeat(np.arange(self.nseg), n_run)
+        kr = np.arange(self.n_runs) - run0[rseg]
+        r_lo = first[rseg] + kr * _RUN
+        r_cnt = np.minimum(_RUN, first[rseg] + n_it[rseg] - r_lo)
+        parts = [it_lo, it_hi, r_lo, r_cnt, run0, n_run, nd]
+        buf = torch.from_numpy(np.concatenate(parts).astype(np.int64)).to(dev, non_blocking=False)
+        views, off = [], 0
+        for p in parts:
+            views.append(buf[off: off + len(p)])
+            off += len(p)
+        self.it_lo, self.it_hi, self.r_lo, self.r_cnt, self.s_run0, self.s_nrun, self.seg_node = views
 
 
 def hist_torch(bins, order, y, w, seg_lo, seg_hi, seg_node, n_nodes, B, S, cls):
