@@ -1,0 +1,53 @@
+"""bench.py driver contract: one JSON line with the required keys, and the multi-rank
+(torchrun, gloo on CPU, world_size 4) run reports the same losses as one rank -- the
+row-sharded DP step must not change the optimisation (strong scaling, same data)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def _env():
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    return env
+
+
+@pytest.mark.timeout(300)
+def test_bench_single_and_four_ranks_agree():
+    args = ["--steps", "3", "--warmup", "1", "--rows", "24000", "--features", "32"]
+    one = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                         timeout=240)
+    assert one.returncode == 0, one.stderr[-2000:]
+    r1 = _json_line(one.stdout)
+    assert KEYS <= set(r1) and r1["n_gpus"] == 1 and r1["steps"] == 3 and r1["warmup"] == 1
+    assert r1["higher_is_better"] is True and r1["config"]["global_batch"] == 24000 and r1["value"] > 0
+    four = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "4",
+                           *args], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=240)
+    assert four.returncode == 0, four.stderr[-3000:]
+    r4 = _json_line(four.stdout)
+    assert r4["n_gpus"] == 4 and r4["config"]["parallelism"] == "dp4" and r4["config"]["global_batch"] == 24000
+    assert abs(r4["first_loss"] - r1["first_loss"]) < 1e-9
+    assert abs(r4["final_loss"] - r1["final_loss"]) < 1e-7 * abs(r1["final_loss"])
