@@ -528,7 +528,9 @@ inline int upd_rows(int Kp) {
 // with ballot ranking (peel one key per step: rank = popcount of same-key lanes below).
 // Bucket order is therefore row order -> bitwise-deterministic sums for any k (the old
 // in-bucket insertion sort was O(bucket^2) per thread, i.e. quadratic at small k).
-template <int DV>  // floats per lane per row (D = 64 * DV)
+// DV: floats per lane per row (scalar path, D <= 64 * DV); LPR > 0: vector path, LPR
+// lanes x float4 per row (D <= 4 * LPR, D % 4 == 0, 16-B rows), 64 / LPR rows per load.
+template <int DV, int LPR>
 __global__ __launch_bounds__(kUpdThreads) void kmeans_update_kernel(
     const float* __restrict__ X, int64_t n, int64_t ldx, int D, const int32_t* __restrict__ assign,
     int Kp, int R, float* __restrict__ slab, float* __restrict__ cnt_slab) {
@@ -588,17 +590,47 @@ __global__ __launch_bounds__(kUpdThreads) void kmeans_update_kernel(
     for (int g = s0; g < s1; g += kWave) {
       const int i = g + lane;
       const int key = i < s1 ? assign[r0 + i] : -1;
-      uint64_t todo = __ballot(i < s1);
-      while (todo) {
-        const int leader = __ffsll((unsigned long long)todo) - 1;
-        const int k = __shfl(key, leader, 64);
-        const uint64_t m = __ballot(key == k);
-        if (key == k) {
-          const int rank = __popcll(m & ((1ull << lane) - 1ull));
-          sorted[start[k] + mycw[2 * k + half] + rank] = (uint16_t)i;
+      if (Kp <= 32) {
+        // few clusters: peel one key per step (<= 32 steps, usually a handful)
+        uint64_t todo = __ballot(i < s1);
+        while (todo) {
+          const int leader = __ffsll((unsigned long long)todo) - 1;
+          const int k = __shfl(key, leader, 64);
+          const uint64_t m = __ballot(key == k);
+          if (key == k) {
+            const int rank = __popcll(m & ((1ull << lane) - 1ull));
+            sorted[start[k] + mycw[2 * k + half] + rank] = (uint16_t)i;
+          }
+          if (lane == leader) mycw[2 * k + half] = (uint16_t)(mycw[2 * k + half] + __popcll(m));
+          todo &= ~m;
         }
-        if (lane == leader) mycw[2 * k + half] = (uint16_t)(mycw[2 * k + half] + __popcll(m));
-        todo &= ~m;
+      } else {
+        // many clusters (up to 64 distinct keys per group): bitonic-sort the 64
+        // (key, lane) pairs in registers (21 compare-exchange steps), then every lane's
+        // rank inside its key run comes from one ballot of the run heads -- the same
+        // stable order as the peeling loop at a fraction of its ~64 iterations
+        uint32_t v = ((uint32_t)(key < 0 ? 0xFFFF : key) << 6) | (uint32_t)lane;
+#pragma unroll
+        for (int kk = 2; kk <= 64; kk <<= 1) {
+#pragma unroll
+          for (int j = kk >> 1; j > 0; j >>= 1) {
+            const uint32_t o = (uint32_t)__shfl_xor((int)v, j, 64);
+            const bool keep_min = ((lane & kk) == 0) == ((lane & j) == 0);
+            v = keep_min ? (v < o ? v : o) : (v > o ? v : o);
+          }
+        }
+        const int k = (int)(v >> 6);
+        const bool valid = k != 0xFFFF;
+        const int prev = __shfl_up((int)v, 1, 64) >> 6;
+        const int next = __shfl_down((int)v, 1, 64) >> 6;
+        const uint64_t heads = __ballot(valid && (lane == 0 || prev != k));
+        const uint64_t upto = ~0ull >> (63 - lane);                  // bits 0..lane
+        const int run0 = 63 - __clzll((long long)(heads & upto));
+        const int rank = lane - run0;
+        if (valid) {
+          sorted[start[k] + mycw[2 * k + half] + rank] = (uint16_t)(g + (int)(v & 63u));
+          if (lane == 63 || next != k) mycw[2 * k + half] = (uint16_t)(mycw[2 * k + half] + rank + 1);
+        }
       }
     }
     __syncthreads();
@@ -607,6 +639,39 @@ __global__ __launch_bounds__(kUpdThreads) void kmeans_update_kernel(
     for (int c = c0; c < c1; ++c) {
       const int b0 = start[c], b1 = start[c + 1];
       if (b0 == b1) continue;
+      if constexpr (LPR > 0) {
+        // 16-B loads: each lane owns 4 columns of one of RPI row slots; the slots'
+        // partial sums are folded by xor-shuffles before the slab update
+        constexpr int RPI = kWave / LPR;
+        const int slot = lane / LPR, col = 4 * (lane % LPR);
+        const bool cok = col < D;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        auto ld = [&](int i) {
+          const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (!cok || i >= b1) return z;
+          return *reinterpret_cast<const float4*>(X + (r0 + sorted[i]) * ldx + col);
+        };
+        for (int i = b0 + slot; i < b1; i += 4 * RPI) {      // 4 row loads in flight per lane
+          const float4 x0 = ld(i), x1 = ld(i + RPI), x2 = ld(i + 2 * RPI), x3 = ld(i + 3 * RPI);
+          acc.x += x0.x; acc.y += x0.y; acc.z += x0.z; acc.w += x0.w;
+          acc.x += x1.x; acc.y += x1.y; acc.z += x1.z; acc.w += x1.w;
+          acc.x += x2.x; acc.y += x2.y; acc.z += x2.z; acc.w += x2.w;
+          acc.x += x3.x; acc.y += x3.y; acc.z += x3.z; acc.w += x3.w;
+        }
+#pragma unroll
+        for (int off = LPR; off < kWave; off <<= 1) {
+          acc.x += __shfl_xor(acc.x, off, 64);
+          acc.y += __shfl_xor(acc.y, off, 64);
+          acc.z += __shfl_xor(acc.z, off, 64);
+          acc.w += __shfl_xor(acc.w, off, 64);
+        }
+        if (slot == 0 && cok) {
+          float4* dst = reinterpret_cast<float4*>(myslab + (int64_t)c * D + col);
+          float4 d4 = *dst;
+          d4.x += acc.x; d4.y += acc.y; d4.z += acc.z; d4.w += acc.w;
+          *dst = d4;
+        }
+      } else {
       float acc[DV];
 #pragma unroll
       for (int v = 0; v < DV; ++v) acc[v] = 0.f;
@@ -640,6 +705,7 @@ __global__ __launch_bounds__(kUpdThreads) void kmeans_update_kernel(
       for (int v = 0; v < DV; ++v) {
         const int col = lane + 64 * v;
         if (col < D) dst[col] += acc[v];
+      }
       }
       if (lane == 0) mycnt[c] += (float)(b1 - b0);
     }
@@ -744,10 +810,17 @@ O3S_API int o3s_kmeans_update(const float* X, int64_t n, int64_t ldx, int D, con
   if (!R) return -3;
   const int lds = upd_lds_bytes(Kp, R);
   if (n > 0) {
-#define O3S_KU(DV)                                                                                    \
-  hipLaunchKernelGGL((kmeans_update_kernel<DV>), dim3(grid), dim3(kUpdThreads), lds, st, X, n, ldx, D, \
+#define O3S_KU(DV, LPR)                                                                               \
+  hipLaunchKernelGGL((kmeans_update_kernel<DV, LPR>), dim3(grid), dim3(kUpdThreads), lds, st, X, n, ldx, D, \
                      assign, Kp, R, slab, cnt_slab);
-    if (D <= 64) { O3S_KU(1) } else if (D <= 128) { O3S_KU(2) } else if (D <= 192) { O3S_KU(3) } else { O3S_KU(4) }
+    const bool vec = D % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)X & 15) == 0;
+    if (vec) {
+      if (D <= 32) { O3S_KU(1, 8) } else if (D <= 64) { O3S_KU(1, 16) } else if (D <= 128) { O3S_KU(2, 32) }
+      else { O3S_KU(4, 64) }
+    } else {
+      if (D <= 64) { O3S_KU(1, 0) } else if (D <= 128) { O3S_KU(2, 0) } else if (D <= 192) { O3S_KU(3, 0) }
+      else { O3S_KU(4, 0) }
+    }
 #undef O3S_KU
     O3S_CHECK_LAUNCH();
   }
