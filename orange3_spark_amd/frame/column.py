@@ -341,6 +341,47 @@ class ArrayColumn(HostColumn):
         return ArrayColumn(np.concatenate([c.values for c in cols]), cols[0].dtype.elementType)
 
 
+class DeviceTokensColumn(ArrayColumn):
+    """array<string> produced by the device Tokenizer and kept on the GPU: token t of the
+    column is bytes[tok_start[t]:tok_end[t]] (a span of the lower-cased UTF-8 buffer), the
+    tokens of row r are t in [doc_offs[r], doc_offs[r+1]); ``valid`` marks non-null rows.
+    HashingTF hashes the spans in place; every other consumer sees the usual host
+    ``values`` (python lists), decoded lazily on first access."""
+
+    def __init__(self, doc_offs: torch.Tensor, tok_start: torch.Tensor, tok_end: torch.Tensor, data: torch.Tensor,
+                 valid: torch.Tensor | None = None):
+        self.doc_offs, self.tok_start, self.tok_end, self.data, self.valid = doc_offs, tok_start, tok_end, data, valid
+        self.dtype = T.ArrayType(T.StringType())
+        self._host = None
+
+    def __len__(self):
+        return int(self.doc_offs.numel() - 1)
+
+    @property
+    def values(self) -> np.ndarray:
+        if self._host is None:
+            offs = self.doc_offs.cpu().numpy()
+            ts, te = self.tok_start.cpu().numpy(), self.tok_end.cpu().numpy()
+            raw = self.data.cpu().numpy().tobytes()
+            valid = None if self.valid is None else self.valid.cpu().numpy()
+            out = np.empty(len(self), dtype=object)
+            for r in range(len(self)):
+                if valid is not None and not valid[r]:
+                    out[r] = None
+                    continue
+                a, b = offs[r], offs[r + 1]
+                out[r] = [raw[ts[t]:te[t]].decode("utf-8", "replace") for t in range(a, b)]
+            self._host = out
+        return self._host
+
+    @values.setter
+    def values(self, v):
+        self._host = v
+
+    def nbytes(self):
+        return sum(t.element_size() * t.numel() for t in (self.doc_offs, self.tok_start, self.tok_end, self.data))
+
+
 def from_numpy(arr: np.ndarray, device) -> Column:
     """Column from a host numpy array (numeric -> device tensor; other -> host strings)."""
     arr = np.asarray(arr)

@@ -363,7 +363,9 @@ class Tokenizer(_Simple):
         self._set(**self._input_kwargs)
 
     def _apply(self, df, name):
-        return C.ArrayColumn(TX.tokenize_lower_ws(_strings(df, name)))
+        vals = _strings(df, name)
+        dev = TX.device_tokenize(np.asarray(vals, dtype=object), df.device) if df.device.type == "cuda" else None
+        return dev if dev is not None else C.ArrayColumn(TX.tokenize_lower_ws(vals))
 
 
 @register("org.apache.spark.ml.feature.RegexTokenizer")
@@ -464,8 +466,15 @@ def _terms_to_csr(rows_terms: list, num_features: int, device, binary: bool) -> 
     n = len(rows_terms)
     dev = torch.device(device)
     _, bucket = TX.murmur3_buckets(flat, num_features, dev)
-    row = torch.repeat_interleave(torch.arange(n, device=dev), torch.tensor(counts, device=dev))
-    key = row * num_features + bucket.to(dev)
+    return _buckets_to_csr(bucket.to(dev), torch.tensor(counts, device=dev), n, num_features, binary)
+
+
+def _buckets_to_csr(bucket: torch.Tensor, counts: torch.Tensor, n: int, num_features: int,
+                    binary: bool) -> C.SparseVectorColumn:
+    """Per-row term buckets (row-major, ``counts`` per row) -> CSR term frequencies."""
+    dev = bucket.device
+    row = torch.repeat_interleave(torch.arange(n, device=dev), counts.to(dev))
+    key = row * num_features + bucket
     uk, cnt = torch.unique(key, return_counts=True)         # sorted by (row, bucket)
     r = uk // num_features
     indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
@@ -495,9 +504,16 @@ class HashingTF(_Simple, HasNumFeatures):
         return int(b[0])
 
     def _apply(self, df, name):
-        vals = df.column_data(name).values
+        col = df.column_data(name)
+        nf = self.getOrDefault(self.numFeatures)
+        if isinstance(col, C.DeviceTokensColumn) and col.data.is_cuda:
+            # device tokens: hash the spans in place (murmur3_span_kernel) -> CSR on device
+            bucket = TX.murmur3_span_buckets(col, nf)
+            counts = col.doc_offs[1:] - col.doc_offs[:-1]
+            return _buckets_to_csr(bucket, counts, len(col), nf, self.getOrDefault(self.binary))
+        vals = col.values
         return _terms_to_csr([None if v is None else [str(t) for t in v] for v in vals],
-                             self.getOrDefault(self.numFeatures), df.device, self.getOrDefault(self.binary))
+                             nf, df.device, self.getOrDefault(self.binary))
 
 
 @register("org.apache.spark.ml.feature.FeatureHasher")

@@ -7,6 +7,7 @@ and runs MurmurHash3_x86_32 either on the GPU (csrc/text.hip) or in the host C++
 from __future__ import annotations
 
 import ctypes as Ct
+import re
 
 import numpy as np
 import torch
@@ -47,25 +48,40 @@ def murmur3_buckets(strings, num_buckets: int, device=None, seed: int = SPARK_SE
     return torch.from_numpy(h), torch.from_numpy(k)
 
 
+_WS = re.compile(r"[ \t\n\x0b\f\r]")
+
+
+def spark_split(s: str) -> list:
+    """Java ``s.split("\\s")``: every single whitespace char separates (runs give empty
+    tokens), trailing empty tokens dropped, "" -> [""] (Spark Tokenizer after lower-case)."""
+    if s == "":
+        return [""]
+    parts = _WS.split(s)
+    while parts and parts[-1] == "":
+        parts.pop()
+    return parts
+
+
 def tokenize_lower_ws(strings) -> list:
-    """Spark Tokenizer semantics: lower-case then split on whitespace (native fast path)."""
+    """Spark Tokenizer semantics (lower-case, then ``split("\\s")``; native fast path for
+    ASCII columns, Python for non-ASCII text where Unicode lower-casing is needed)."""
     vals = ["" if s is None else s for s in strings]
     offs, data = pack(vals)
     n = len(vals)
     if n == 0:
         return []
     if data.size and int(data.max()) >= 128:        # non-ASCII: Java/Python Unicode lower()
-        return [None if s is None else s.lower().split() for s in strings]
+        return [None if s is None else spark_split(s.lower()) for s in strings]
     buf = data if data.size else np.zeros(1, np.uint8)
     out = np.empty_like(buf)
-    cap = int(data.size // 2 + n + 1)
+    cap = int(data.size + n + 1)                     # <= one token per byte + one per string
     ts = np.empty(cap, dtype=np.int64)
     te = np.empty(cap, dtype=np.int64)
     counts = np.empty(n, dtype=np.int64)
     k = N.host().o3s_host_tokenize(offs.ctypes.data, buf.ctypes.data, n, out.ctypes.data, ts.ctypes.data,
                                    te.ctypes.data, cap, counts.ctypes.data)
     if k < 0:
-        return [s.lower().split() for s in vals]
+        return [None if s is None else spark_split(s.lower()) for s in strings]
     raw = out.tobytes()
     res, j = [], 0
     for i in range(n):
@@ -78,4 +94,63 @@ def tokenize_lower_ws(strings) -> list:
     return res
 
 
-_ = Ct
+def arrow_strings(values):
+    """(offsets int64 [n+1], UTF-8 bytes uint8, valid bool [n] | None) of an object array of
+    str/None, converted in C by pyarrow (no per-string Python work)."""
+    import pyarrow as pa
+    arr = pa.array(values, type=pa.large_string(), from_pandas=True)
+    validity, obuf, dbuf = arr.buffers()
+    n = len(arr)
+    offs = np.frombuffer(obuf, dtype=np.int64, count=n + 1, offset=8 * arr.offset)
+    base = int(offs[0])
+    data = np.frombuffer(dbuf, dtype=np.uint8) if dbuf is not None else np.zeros(0, np.uint8)
+    data = data[base: int(offs[-1])]
+    valid = None
+    if arr.null_count:
+        valid = ~np.asarray(arr.is_null().to_numpy(zero_copy_only=False), dtype=bool)
+    return offs - base, data, valid
+
+
+def device_tokenize(values, device, min_rows: int = 1):
+    """Spark Tokenizer on the GPU for an ASCII string column: returns a
+    :class:`~orange3_spark_amd.frame.column.DeviceTokensColumn` (tokens stay on the device
+    as spans of the lower-cased byte buffer), or None when the column needs the host path
+    (non-ASCII text, CPU device, or fewer than ``min_rows`` rows)."""
+    from ..frame.column import DeviceTokensColumn
+    dev = torch.device(device)
+    if dev.type != "cuda" or len(values) < min_rows:
+        return None
+    offs, data, valid = arrow_strings(values)
+    if data.size and int(data.max()) >= 128:
+        return None
+    n = len(offs) - 1
+    o = torch.from_numpy(np.ascontiguousarray(offs)).to(dev)
+    b = torch.from_numpy(data.copy() if data.size else np.zeros(1, np.uint8)).to(dev)
+    lib = N.kernels()
+    st = N.stream_of(o)
+    counts = torch.empty(n, dtype=torch.int64, device=dev)
+    N.check(lib.o3s_tokenize(0, o.data_ptr(), b.data_ptr(), n, counts.data_ptr(), None, None, None, None, st),
+            "tokenize_count")
+    if valid is not None:
+        counts.masked_fill_(torch.from_numpy(~valid).to(dev), 0)
+    doc_offs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(counts, 0, out=doc_offs[1:])
+    ntok = int(doc_offs[-1])
+    low = torch.empty_like(b)
+    ts = torch.empty(max(ntok, 1), dtype=torch.int64, device=dev)
+    te = torch.empty(max(ntok, 1), dtype=torch.int64, device=dev)
+    # null rows hold "" in the Arrow buffers; their masked count of 0 makes emit skip them
+    N.check(lib.o3s_tokenize(1, o.data_ptr(), b.data_ptr(), n, None, doc_offs.data_ptr(), low.data_ptr(),
+                             ts.data_ptr(), te.data_ptr(), st), "tokenize_emit")
+    vt = None if valid is None else torch.from_numpy(valid).to(dev)
+    return DeviceTokensColumn(doc_offs, ts[:ntok], te[:ntok], low, vt)
+
+
+def murmur3_span_buckets(tok, num_buckets: int, seed: int = SPARK_SEED) -> torch.Tensor:
+    """Bucket (int64) of every token of a DeviceTokensColumn (Spark HashingTF hash)."""
+    ntok = int(tok.tok_start.numel())
+    out = torch.empty(ntok, dtype=torch.int64, device=tok.data.device)
+    N.check(N.kernels().o3s_murmur3_spans(tok.tok_start.data_ptr(), tok.tok_end.data_ptr(), tok.data.data_ptr(),
+                                          ntok, seed, num_buckets, out.data_ptr(), N.stream_of(out)),
+            "murmur3_spans")
+    return out

@@ -119,3 +119,59 @@ def test_pipeline_fit_save_load(s, tmp_path):
     pipe.save(str(tmp_path / "p"))
     p3 = Pipeline.load(str(tmp_path / "p"))
     assert [type(x).__name__ for x in p3.getStages()] == ["VectorAssembler", "StandardScaler", "LogisticRegression"]
+
+
+def test_tokenizer_spark_split_semantics(s):
+    """Spark Tokenizer = toLowerCase + split("\\\\s"): whitespace runs give empty tokens,
+    trailing empties dropped, "" -> [""], all-whitespace -> []."""
+    from orange3_spark_amd.ops.text import spark_split, tokenize_lower_ws
+    cases = ["a  b", " a", "a ", "   ", "", "Tab\tSep\nLine", "x\x0by\x0cz\rw", "MiXeD  Case  "]
+    want = [["a", "", "b"], ["", "a"], ["a"], [], [""], ["tab", "sep", "line"], ["x", "y", "z", "w"],
+            ["mixed", "", "case"]]
+    assert [spark_split(c.lower()) for c in cases] == want
+    assert tokenize_lower_ws(cases + [None]) == want + [None]
+    assert tokenize_lower_ws(["Ünïcode  Straße"]) == [["ünïcode", "", "straße"]]
+
+
+def _corpus(n, seed):
+    rng = np.random.default_rng(seed)
+    words = ["Spark", "GPU", "mi355x", "HashingTF", "the", "a", "", "x" * 40, "Tok3n", "UPPER"]
+    seps = [" ", "  ", "\t", "\n", " \r ", "\x0b"]
+    out = []
+    for i in range(n):
+        k = int(rng.integers(0, 12))
+        parts = [words[int(j)] for j in rng.integers(0, len(words), k)]
+        txt = ""
+        for p in parts:
+            txt += p + seps[int(rng.integers(0, len(seps)))]
+        if rng.uniform() < 0.2:
+            txt = seps[int(rng.integers(0, len(seps)))] + txt
+        if rng.uniform() < 0.3:
+            txt = txt.rstrip()
+        out.append(None if i % 97 == 5 else txt)
+    return out
+
+
+@pytest.mark.gpu
+def test_gpu_tokenizer_and_hashingtf_match_host():
+    """Device Tokenizer (tokenize kernels) + HashingTF over the device token spans ==
+    the host path, token for token and CSR entry for entry."""
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.frame import column as C
+    from orange3_spark_amd.ops.text import tokenize_lower_ws
+    gs = Session(SessionConf().set("o3s.device", "cuda"))
+    texts = _corpus(20_011, 3)
+    df = gs.createDataFrame(pd.DataFrame({"text": texts}))
+    tok = F.Tokenizer(inputCol="text", outputCol="words").transform(df)
+    col = tok.column_data("words")
+    assert isinstance(col, C.DeviceTokensColumn)
+    assert list(col.values) == tokenize_lower_ws(texts)
+    tf = F.HashingTF(numFeatures=1 << 12, inputCol="words", outputCol="tf").transform(tok).column_data("tf")
+    host = F._terms_to_csr([None if v is None else v for v in tokenize_lower_ws(texts)], 1 << 12,
+                           torch.device("cpu"), False)
+    assert torch.equal(tf.indptr.cpu(), host.indptr.cpu())
+    assert torch.equal(tf.indices.cpu(), host.indices.cpu())
+    assert torch.equal(tf.values.cpu(), host.values.cpu())
+    # downstream host consumers still work on the lazily decoded lists
+    sw = F.StopWordsRemover(inputCol="words", outputCol="clean").transform(tok)
+    assert sw.count() == len(texts)
