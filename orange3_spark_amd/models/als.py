@@ -93,6 +93,12 @@ def _weights(vals: torch.Tensor, implicit: bool, alpha: float):
 
 
 FUSED_CG = True        # False: CG bookkeeping as separate torch ops (reference path)
+# rows averaging at least this many ratings are solved exactly (MFMA Gram + batched
+# Cholesky, Spark's per-row solve) instead of by warm-started CG; 0 disables.  Off by
+# default: on the rank-128 item side of the ALS config it measured 0.58 s/iteration vs
+# 0.154 s with CG (the batched rocSOLVER Cholesky and the gather-latency-bound Gram cost
+# more than the 4 CG gather passes; profiles/als_dense_solve_experiment.json).
+DENSE_MIN_AVG = 0
 
 
 def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, implicit: bool, alpha: float,
@@ -111,6 +117,10 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
     nnz = int(csr.cols.numel())
     if exact is None:
         exact = nnz * R * R <= (1 << 26)
+    if not exact and not nonneg and DENSE_MIN_AVG and A.gram_ok(Ffull) and nnz >= DENSE_MIN_AVG * max(n, 1):
+        # many ratings per row (the item side): exact solves, Gram on MFMA + batched Cholesky
+        with trace("als.dense_solve"):
+            return A.dense_solve(csr.indptr, csr.cols, w, b, Ffull, FtF if implicit else None, lam)
     if exact:
         rows = torch.repeat_interleave(torch.arange(n, device=dev), csr.indptr[1:] - csr.indptr[:-1])
         rhs = A.pass_(1, csr.indptr, csr.cols, b, Ffull, None)

@@ -72,3 +72,39 @@ def cg_step(x, r, p, ap, pf, lam, rs):
     n, R = x.shape
     N.check(N.kernels().o3s_als_cg(1, n, R, x.data_ptr(), r.data_ptr(), p.data_ptr(), ap.data_ptr(), N.ptr(pf),
                                    None, lam.data_ptr(), rs.data_ptr(), N.stream_of(x)), "als_cg_step")
+
+
+def gram_ok(F: torch.Tensor) -> bool:
+    R = F.shape[1]
+    return F.is_cuda and F.dtype == torch.float32 and R % 32 == 0 and 32 <= R <= 128
+
+
+def dense_solve(indptr, cols, w, b, F, FtF, lam, batch_bytes: int = 1 << 30) -> torch.Tensor:
+    """Exact per-row normal-equation solves: ``als_gram_kernel`` (MFMA) forms
+    A_u = FtF + sum w y y^T + lam_u I and b_u for a batch of rows, a batched Cholesky
+    (rocSOLVER via torch.linalg.cholesky_ex) solves them; rows whose fp32 factorisation
+    fails are re-solved in fp64."""
+    n = indptr.numel() - 1
+    R = F.shape[1]
+    dev = F.device
+    x = torch.empty((n, R), dtype=torch.float32, device=dev)
+    bs = max(1, min(n, batch_bytes // (R * R * 4)))
+    Fc = F.contiguous()
+    Gc = None if FtF is None else FtF.contiguous().float()
+    lib = N.kernels()
+    A = torch.empty((bs, R, R), dtype=torch.float32, device=dev)
+    bv = torch.empty((bs, R), dtype=torch.float32, device=dev)
+    for r0 in range(0, n, bs):
+        m = min(bs, n - r0)
+        N.check(lib.o3s_als_gram(indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), Fc.data_ptr(), R,
+                                 N.ptr(Gc), lam.data_ptr(), r0, m, A.data_ptr(), bv.data_ptr(), N.stream_of(Fc)),
+                "als_gram")
+        L, info = torch.linalg.cholesky_ex(A[:m])
+        xs = torch.cholesky_solve(bv[:m, :, None], L)[:, :, 0]
+        bad = info != 0
+        if bool(bad.any()):
+            Ad = A[:m][bad].double()
+            Ad = Ad + 1e-12 * torch.eye(R, dtype=torch.float64, device=dev)[None]
+            xs[bad] = torch.linalg.solve(Ad, bv[:m][bad].double()[:, :, None])[:, :, 0].float()
+        x[r0:r0 + m] = xs
+    return x

@@ -161,6 +161,132 @@ __global__ __launch_bounds__(kAlsWaves * 64) void als_cg_kernel(int64_t nrows, i
   if (lane == 0) rs[u] = rs1;
 }
 
+
+// ---------------------------------------------------------------------------------
+// Exact normal equations on MFMA (rows with many ratings, e.g. the item side):
+//     A_u = FtF[implicit] + sum_j w_j y_j y_j^T + lam_u I,      b_u = sum_j b_j y_j
+// for a batch of CSR rows, written densely (A: [batch][R][R] fp32, b: [batch][R]) for a
+// batched Cholesky solve -- Spark's exact per-row solve instead of warm-started CG.
+// One 256-thread workgroup per row.  Each 16-rating k-step the block gathers the 16
+// factor rows (R fp32 each), scales them by sqrt(w_j) (w >= 0: alpha|r| or 1), splits
+// them into bf16 hi + lo and stores them TRANSPOSED ([R][16], rating index fastest) in
+// LDS, so an MFMA fragment (8 consecutive ratings of one factor component) is one 16-B
+// read.  Wave I (< R/32) owns output rows [32I, 32I+32) and all R/32 column tiles:
+// 3 v_mfma_f32_32x32x16_bf16 per tile (hi.hi + lo.hi + hi.lo: ~2^-16 relative, fp32-level
+// Gram entries).  The gathers of step s+1 are in flight while step s's MFMAs run
+// (double-buffered LDS, one barrier per step).  The rhs is accumulated in fp32 by the
+// staging threads and reduced through LDS at the end.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kGramKS = 16;                 // ratings per k-step
+constexpr int kGramLd = kGramKS + 8;        // LDS row stride (bf16): 48 B, spreads banks
+
+template <int RT>   // R = 32 * RT
+__global__ __launch_bounds__(256) void als_gram_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
+    const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ FtF,
+    const float* __restrict__ lam, int64_t row0, float* __restrict__ Aout, float* __restrict__ bout) {
+  constexpr int R = 32 * RT;
+  constexpr int EPT = R / 16;               // elements per staging thread (16 threads per rating)
+  __shared__ __attribute__((aligned(16))) uint16_t T[2][2][R * kGramLd];   // [buf][hi|lo][r][k]
+  __shared__ float rpart[kGramKS][R];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int64_t u = row0 + blockIdx.x;
+  const int64_t j0 = indptr[u], j1 = indptr[u + 1];
+  const int sk = tid >> 4, sseg = tid & 15;         // staging: rating sk of the step, elements sseg*EPT..
+  float rhs[EPT];
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) rhs[e] = 0.f;
+  float yv[EPT], wv = 0.f, bv = 0.f;
+  auto load = [&](int64_t jb) {                     // gather this thread's slice of rating jb + sk
+    const int64_t j = jb + sk;
+    const bool ok = j < j1;
+    const int64_t c = ok ? (int64_t)cols[j] : 0;
+    wv = ok ? w[j] : 0.f;
+    bv = ok ? b[j] : 0.f;
+    const float* fp = F + c * R + sseg * EPT;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) yv[e] = ok ? fp[e] : 0.f;
+  };
+  auto store = [&](int buf) {
+    const float sw = sqrtf(fmaxf(wv, 0.f));
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      rhs[e] = fmaf(bv, yv[e], rhs[e]);
+      const float z = sw * yv[e];
+      const uint16_t hi = f32_to_bf16(z);
+      const uint16_t lo = f32_to_bf16(z - bf16_to_f32(hi));
+      const int r = sseg * EPT + e;
+      T[buf][0][r * kGramLd + sk] = hi;
+      T[buf][1][r * kGramLd + sk] = lo;
+    }
+  };
+  f32x16 acc[RT];
+#pragma unroll
+  for (int J = 0; J < RT; ++J)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[J][i] = 0.f;
+  const int r = lane & 31, h = lane >> 5;
+  const int nsteps = (int)((j1 - j0 + kGramKS - 1) / kGramKS);
+  if (nsteps > 0) {
+    load(j0);
+    store(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (more) load(j0 + (int64_t)(s + 1) * kGramKS);          // next step's gathers in flight
+    if (wid < RT) {
+      const uint16_t* Th = T[buf][0];
+      const uint16_t* Tl = T[buf][1];
+      const bf16x8 ah = *reinterpret_cast<const bf16x8*>(Th + (32 * wid + r) * kGramLd + 8 * h);
+      const bf16x8 al = *reinterpret_cast<const bf16x8*>(Tl + (32 * wid + r) * kGramLd + 8 * h);
+#pragma unroll
+      for (int J = 0; J < RT; ++J) {
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(Th + (32 * J + r) * kGramLd + 8 * h);
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(Tl + (32 * J + r) * kGramLd + 8 * h);
+        acc[J] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[J], 0, 0, 0);
+        acc[J] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[J], 0, 0, 0);
+        acc[J] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[J], 0, 0, 0);
+      }
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+  // A_u = acc + FtF + lam I, written straight from the accumulators (lanes -> columns)
+  float* Ab = Aout + (int64_t)blockIdx.x * R * R;
+  if (wid < RT) {
+    const float lu = lam[u];
+#pragma unroll
+    for (int J = 0; J < RT; ++J) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int m = 32 * wid + 4 * h + (i & 3) + 8 * (i >> 2);
+        const int nn = 32 * J + r;
+        float v = acc[J][i];
+        if (FtF) v += FtF[m * R + nn];
+        if (m == nn) v += lu;
+        Ab[m * R + nn] = v;
+      }
+    }
+  }
+  // rhs: the 16 staging threads of each element slice hold partial sums over their ratings
+  if (nsteps == 0) {
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) rhs[e] = 0.f;
+  }
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) rpart[sk][sseg * EPT + e] = rhs[e];
+  __syncthreads();
+  for (int c = tid; c < R; c += 256) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < kGramKS; ++k) t += rpart[k][c];
+    bout[(int64_t)blockIdx.x * R + c] = t;
+  }
+}
+
 }  // namespace
 
 // mode 0: CG init (x, av = A-part of A x, rhs -> r, p, rs); mode 1: CG step (p, av = A-part of A p).
@@ -207,6 +333,27 @@ O3S_API int o3s_als_pass(int mode, const int64_t* indptr, const int32_t* cols, c
   }
   O3S_AL(1) O3S_AL(2) O3S_AL(3) O3S_AL(4) O3S_AL(5) O3S_AL(6) O3S_AL(7) O3S_AL(8)
 #undef O3S_AL
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+// Dense normal equations for CSR rows [row0, row0 + nrows) (R = 32, 64, 96 or 128):
+// A: [nrows][R][R], b: [nrows][R] fp32.  FtF may be null (explicit feedback).
+O3S_API int o3s_als_gram(const int64_t* indptr, const int32_t* cols, const float* w, const float* b, const float* F,
+                         int R, const float* FtF, const float* lam, int64_t row0, int64_t nrows, float* A,
+                         float* bout, hipStream_t st) {
+  if (nrows <= 0) return 0;
+  if (R % 32 != 0 || R < 32 || R > 128 || nrows > 0x7fffffff) return -1;
+#define O3S_G(RTV)                                                                                        \
+  case RTV:                                                                                               \
+    hipLaunchKernelGGL((als_gram_kernel<RTV>), dim3((unsigned)nrows), dim3(256), 0, st, indptr, cols, w, b, F, \
+                       FtF, lam, row0, A, bout);                                                          \
+    break;
+  switch (R / 32) {
+    O3S_G(1) O3S_G(2) O3S_G(3) O3S_G(4)
+    default: return -1;
+  }
+#undef O3S_G
   O3S_CHECK_LAUNCH();
   return 0;
 }

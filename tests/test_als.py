@@ -145,3 +145,28 @@ def test_gpu_fused_cg_matches_torch_cg(implicit, R):
         out.append((res.U.clone(), res.V.clone()))
     for a, b in zip(out[0], out[1]):
         assert ((a - b).norm() / b.norm()).item() < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("implicit,R", [(True, 128), (False, 64), (True, 32), (False, 96)])
+def test_gpu_dense_gram_cholesky_matches_exact_fp64(implicit, R, monkeypatch):
+    """MFMA Gram (als_gram_kernel) + batched Cholesky == the fp64 dense reference solve of
+    the same normal equations (the item side: many ratings per row)."""
+    from orange3_spark_amd.ops import als as A
+    monkeypatch.setattr(AE, "DENSE_MIN_AVG", 64)
+    s = Session(SessionConf().set("o3s.device", "cuda"))
+    df = s.synthetic.ratings(20000, 1500, 300000, rank=8, seed=4, implicit=implicit)
+    users = df.column_data("user").data.long()
+    items = df.column_data("item").data.long()
+    r = df.column_data("rating").data.float()
+    uid, iid = AE.global_ids(s.comm, users), AE.global_ids(s.comm, items)
+    uix, iix = torch.searchsorted(uid, users), torch.searchsorted(iid, items)
+    by_item = AE.partition(s.comm, iix, uix, r, iid.numel())
+    X = AE.init_factors(0, uid.numel(), R, 5, users.device, False)
+    Y0 = AE.init_factors(0, iid.numel(), R, 6, users.device, False)
+    G = (X.double().T @ X.double()).float() if implicit else None
+    assert A.gram_ok(X) and by_item.cols.numel() >= AE.DENSE_MIN_AVG * by_item.nrows
+    dense = AE.solve_side(by_item, X, Y0, 0.1, implicit, 2.0, G, 3, False, exact=None)
+    ref = AE.solve_side(by_item, X, Y0, 0.1, implicit, 2.0, G, 3, False, exact=True)
+    err = ((dense.double() - ref.double()).norm() / ref.double().norm()).item()
+    assert err < 2e-4, err

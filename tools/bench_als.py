@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--rank", type=int, default=128)
     ap.add_argument("--iters", type=int, default=2)
     ap.add_argument("--cg", type=int, default=3)
+    ap.add_argument("--dense-min-avg", type=int, default=None,
+                    help="rows averaging >= this many ratings take the exact MFMA Gram + Cholesky solve (0 = CG only)")
     a = ap.parse_args()
     s = Session.getOrCreate()
     df = s.synthetic.ratings(a.users, a.items, a.ratings, rank=8, seed=1, implicit=True)
@@ -33,6 +35,8 @@ def main():
     r = df.column_data("rating").data
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if a.dense_min_avg is not None:
+        AE.DENSE_MIN_AVG = a.dense_min_avg
     res = AE.fit_als(s.comm, u, i, r, a.rank, a.iters, 0.1, True, 1.0, 0, cg_iters=a.cg, exact=False,
                      keep_full=False)
     torch.cuda.synchronize()
