@@ -114,7 +114,7 @@ class LogisticRegression(Estimator, _LogisticRegressionParams, MLWritable, MLRea
             m = LogisticRegressionModel._from(B, b, True, max(k, 2))._with_parent(self)
             m.summary = _lr_summary(m, df, True, r)
             return m
-        data = GLM.GlmData(comm, feat, y, sw)
+        data = GLM.make_glm_data(comm, feat, y, sw)
         solver = g(self.solver).lower()
         res = GLM.fit_glm(data, "logistic", g(self.regParam), g(self.elasticNetParam), g(self.fitIntercept),
                           g(self.standardization), g(self.maxIter), g(self.tol),
@@ -193,15 +193,16 @@ class LogisticRegressionModel(U.ProbabilisticClassifierMixin, Model, _LogisticRe
         if isinstance(c, C.VectorColumn) and c.data.is_cuda and c.data.dtype == torch.bfloat16 \
                 and not self._multinomial and not isinstance(c, LineageVectorColumn):
             return c.data            # padded bf16 -> margin kernel
+        if isinstance(c, C.SparseVectorColumn) and not self._multinomial:
+            return U.linear_features(df, name)     # CSR rows -> sparse margin kernel
         return U.dense_features(df, name)
 
     def _raw(self, X):
         if not self._multinomial:
-            if X.is_cuda and X.dtype == torch.bfloat16:
+            if isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.bfloat16:
                 m = G.glm_margin(X, torch.from_numpy(self._B[0]).float().to(X.device), float(self._b[0])).double()
             else:
-                w = torch.from_numpy(self._B[0]).to(X.device, torch.float64)
-                m = X.to(torch.float64)[:, : w.shape[0]] @ w + float(self._b[0])
+                m = U.linear_margin(X, self._B[0], float(self._b[0]))
             return torch.stack([-m, m], dim=1)
         W = torch.from_numpy(self._B.T).to(X.device, torch.float32 if X.is_cuda else torch.float64)
         b = torch.from_numpy(self._b).to(X.device, W.dtype)
@@ -280,7 +281,7 @@ class LinearSVC(Estimator, _LinearSVCParams, MLWritable, MLReadable):
         k = U.num_classes(comm, y)
         if k > 2:
             raise ValueError(f"LinearSVC only supports binary classification. {k} classes detected in labelCol")
-        data = GLM.GlmData(comm, U.features_column(df, g(self.featuresCol)), y, U.weights_or_none(df, self))
+        data = GLM.make_glm_data(comm, U.features_column(df, g(self.featuresCol)), y, U.weights_or_none(df, self))
         res = GLM.fit_glm(data, "hinge", g(self.regParam), 0.0, g(self.fitIntercept), g(self.standardization),
                           g(self.maxIter), g(self.tol), "sgd" if g(self.solver) == "sgd" else "auto",
                           g(self.stepSize), init_intercept=0.0, ckpt=for_estimator(self, df))
@@ -320,11 +321,14 @@ class LinearSVCModel(U.ProbabilisticClassifierMixin, Model, _LinearSVCParams, ML
     def numFeatures(self):
         return int(self._w.shape[0])
 
+    def _features_for_predict(self, df, name):
+        return U.linear_features(df, name)        # sparse rows stay CSR
+
     def _raw(self, X):
-        if X.is_cuda and X.dtype == torch.bfloat16:
+        if isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.bfloat16:
             m = G.glm_margin(X, torch.from_numpy(self._w).float().to(X.device), self._b).double()
         else:
-            m = X.to(torch.float64)[:, : self._w.shape[0]] @ torch.from_numpy(self._w).to(X.device) + self._b
+            m = U.linear_margin(X, self._w, self._b)
         return torch.stack([-m, m], dim=1)
 
     def _raw2prob(self, raw):

@@ -30,6 +30,26 @@ def dense_features(df, name: str, dtype=None) -> torch.Tensor:
     return t if dtype is None else t.to(dtype)
 
 
+def linear_features(df, name: str):
+    """Operand of a linear model's margin: CSR rows (ops.sparse.SparseRows, never
+    densified) for sparse vector columns, else the dense tensor."""
+    c = features_column(df, name)
+    if isinstance(c, C.SparseVectorColumn):
+        from ..ops.sparse import SparseRows
+        return SparseRows(c.indptr, c.indices, c.values, c.size)
+    return dense_features(df, name)
+
+
+def linear_margin(X, w: np.ndarray, b: float) -> torch.Tensor:
+    """fp64 margins X.w + b for a dense tensor or SparseRows operand."""
+    from ..ops.sparse import SparseRows
+    if isinstance(X, SparseRows):
+        wt = torch.from_numpy(np.asarray(w, dtype=np.float64))
+        return X.margins(wt, float(b)).to(torch.float64) if X.kernel else X._margins_f64(wt, float(b))
+    wt = torch.from_numpy(np.asarray(w, dtype=np.float64)).to(X.device)
+    return X.to(torch.float64)[:, : wt.shape[0]] @ wt + float(b)
+
+
 def numeric_column(df, name: str, dtype=torch.float64) -> torch.Tensor:
     c = df.column_data(name)
     if isinstance(c, C.NumericColumn):
@@ -70,8 +90,11 @@ class PredictionModelMixin:
     def _predict_tensor(self, X: torch.Tensor) -> torch.Tensor:
         raise NotImplementedError
 
+    def _features_for_predict(self, df, name):
+        return dense_features(df, name)
+
     def _transform(self, df):
-        X = dense_features(df, self.getOrDefault(self.featuresCol))
+        X = self._features_for_predict(df, self.getOrDefault(self.featuresCol))
         pred = self._predict_tensor(X)
         pc = self.getOrDefault(self.predictionCol)
         return df.withColumnData(pc, num_out(pred)) if pc else df

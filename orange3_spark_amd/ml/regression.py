@@ -82,7 +82,7 @@ class LinearRegression(Estimator, _LinearRegressionParams, MLWritable, MLReadabl
             m = LinearRegressionModel._from(coef, b)._with_parent(self)
             m.summary = _linreg_summary(m, df, hist, 0)
             return m
-        data = GLM.GlmData(comm, feat, y, w)
+        data = GLM.make_glm_data(comm, feat, y, w)
         res = GLM.fit_glm(data, "squared", g(self.regParam), alpha, g(self.fitIntercept), g(self.standardization),
                           g(self.maxIter), g(self.tol), ckpt=for_estimator(self, df))
         m = LinearRegressionModel._from(res.coef, res.intercept)._with_parent(self)
@@ -153,8 +153,11 @@ class LinearRegressionModel(U.PredictionModelMixin, Model, _LinearRegressionPara
     def scale(self):
         return 1.0
 
+    def _features_for_predict(self, df, name):
+        return U.linear_features(df, name)        # sparse rows stay CSR
+
     def _predict_tensor(self, X):
-        return X.to(torch.float64)[:, : len(self._w)] @ torch.from_numpy(self._w).to(X.device) + self._b
+        return U.linear_margin(X, self._w, self._b)
 
     def evaluate(self, df):
         """Evaluate on ``df``: a LinearRegressionSummary (metrics computed lazily)."""

@@ -209,6 +209,63 @@ class GlmData:
         return float(o[dpad + 1]), o[: self.d].copy(), float(o[dpad]), float(o[dpad + 2])
 
 
+class SparseGlmData:
+    """This rank's CSR rows for the GLM solvers (HashingTF / CountVectorizer features):
+    margins and X^T r by the sparse kernels (ops/sparse.py), never densified.  Spark's
+    standardization is a per-column scale without centering, so sparsity is kept.
+    Provides the interface GlmObjective / fit_glm use (d, comm, moments, loss_grad)."""
+
+    kernel = False           # no device-resident SGD trainer for sparse rows
+    lineage = None
+
+    def __init__(self, comm, feat: C.SparseVectorColumn, y: torch.Tensor, sw: torch.Tensor | None = None):
+        from ..ops.sparse import SparseRows
+        self.comm = comm
+        self.rows = SparseRows(feat.indptr, feat.indices, feat.values, feat.size)
+        self.device = self.rows.device
+        self.d = int(feat.size)
+        self.y = y.to(self.device)
+        self.sw = None if sw is None else sw.to(self.device)
+        self.n_local = self.rows.n
+        self.n = int(comm.sum_scalar(self.n_local))
+        self.passes = 0
+
+    def moments(self):
+        w = None if self.sw is None else self.sw.to(torch.float32)
+        s1 = self.rows.colsum(w)
+        s2 = self.rows.colsum(w, square=True)
+        wd = torch.ones(self.n_local, dtype=torch.float64, device=self.device) if self.sw is None \
+            else self.sw.to(torch.float64)
+        yd = self.y.to(torch.float64)
+        full = torch.cat([s1, s2, torch.stack([wd.sum(), (wd * yd).sum(), (wd * yd * yd).sum()])]).contiguous()
+        self.comm.all_reduce(full)
+        full = full.cpu().numpy()
+        d = self.d
+        s1, s2, W, ys1, ys2 = full[:d], full[d:2 * d], full[2 * d], full[2 * d + 1], full[2 * d + 2]
+        mean = s1 / max(W, 1e-300)
+        var = np.maximum((s2 - W * mean * mean) / max(W - 1.0, 1e-300), 0.0)
+        ymean = ys1 / max(W, 1e-300)
+        yvar = max((ys2 - W * ymean * ymean) / max(W - 1.0, 1e-300), 0.0)
+        return mean, var, W, ymean, yvar
+
+    @traced("glm.pass")
+    def loss_grad(self, coef_eff: np.ndarray, intercept: float, loss: int):
+        ct = torch.from_numpy(np.ascontiguousarray(coef_eff, dtype=np.float64))
+        out = self.rows.loss_grad(ct, intercept, loss, self.y, self.sw)
+        self.comm.all_reduce(out)
+        self.passes += 1
+        o = out.cpu().numpy()
+        d = self.d
+        return float(o[d + 1]), o[:d].copy(), float(o[d]), float(o[d + 2])
+
+
+def make_glm_data(comm, feat: C.Column, y: torch.Tensor, sw: torch.Tensor | None = None):
+    """GlmData for dense / lineage features, SparseGlmData for CSR features."""
+    if isinstance(feat, C.SparseVectorColumn):
+        return SparseGlmData(comm, feat, y, sw)
+    return GlmData(comm, feat, y, sw)
+
+
 @dataclass
 class GlmResult:
     coef: np.ndarray

@@ -37,6 +37,9 @@ _SIGS: dict[str, list] = {
     "o3s_slab_range_sum": [c_vp, c_i32, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp],
     "o3s_tree_leaf_apply": [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],
     "o3s_als_gram": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp],
+    "o3s_csr_glm": [c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp],
+    "o3s_csc_colsum": [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
+    "o3s_csc_piece": [],
     "o3s_tokenize": [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_murmur3_spans": [c_vp, c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp],
     "o3s_tree_partition": [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,

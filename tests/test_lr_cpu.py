@@ -1,5 +1,6 @@
 """LogisticRegression / LinearSVC on the CPU path vs scikit-learn (BASELINE config #1 plumbing)."""
 import numpy as np
+import pandas as pd
 import pytest
 import torch
 
@@ -107,3 +108,37 @@ def test_weight_col(session):
     from sklearn.linear_model import LogisticRegression as SK
     sk = SK(penalty=None, max_iter=5000, tol=1e-12).fit(X, y, sample_weight=w)
     assert np.allclose(m.coefficients.toArray(), sk.coef_[0], rtol=3e-3, atol=3e-3)
+
+
+def _sparse_vs_dense(s, loss_model):
+    from orange3_spark_amd.frame import column as C
+    from orange3_spark_amd.frame.dataframe import DataFrame
+    rng = np.random.default_rng(3)
+    n, d = 1200, 40
+    X = rng.normal(size=(n, d)) * (rng.uniform(size=(n, d)) < 0.15)            # ~15% dense
+    X = X.astype(np.float32).astype(np.float64)          # CSR values are fp32: same data both ways
+    y = (X @ rng.normal(size=d) + 0.2 * rng.normal(size=n) > 0).astype(float)
+    dense = s.createDataFrame(pd.DataFrame({"features": list(X), "label": y}))
+    nz = [np.nonzero(r)[0] for r in X]
+    indptr = torch.tensor(np.concatenate([[0], np.cumsum([len(z) for z in nz])]), dtype=torch.int64)
+    idx = torch.tensor(np.concatenate(nz), dtype=torch.int32)
+    val = torch.tensor(np.concatenate([X[i, z] for i, z in enumerate(nz)]), dtype=torch.float32)
+    sp = dense.withColumnData("features", C.SparseVectorColumn(indptr, idx, val, d))
+    a = loss_model().fit(dense)
+    b = loss_model().fit(sp)
+    np.testing.assert_allclose(b.coefficients.toArray(), a.coefficients.toArray(), rtol=1e-6, atol=1e-7)
+    pa = a.transform(dense).toPandas()["prediction"].to_numpy()
+    pb = b.transform(sp).toPandas()["prediction"].to_numpy()
+    np.testing.assert_allclose(pb, pa, rtol=1e-6, atol=1e-7)
+    return sp, DataFrame
+
+
+def test_sparse_features_match_dense_lr_svc_linreg(session):
+    """CSR features take the sparse GLM path (never densified) and fit the same model."""
+    from orange3_spark_amd.ml.classification import LinearSVC
+    from orange3_spark_amd.ml.regression import LinearRegression
+    from orange3_spark_amd.models.glm import SparseGlmData, make_glm_data
+    sp, _ = _sparse_vs_dense(session, lambda: LogisticRegression(maxIter=100, regParam=0.01, tol=1e-10))
+    assert isinstance(make_glm_data(sp.comm, sp.column_data("features"), torch.zeros(len(sp))), SparseGlmData)
+    _sparse_vs_dense(session, lambda: LinearSVC(maxIter=100, regParam=0.01, tol=1e-10))
+    _sparse_vs_dense(session, lambda: LinearRegression(maxIter=100, regParam=0.01, tol=1e-10))
