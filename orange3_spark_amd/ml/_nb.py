@@ -16,6 +16,7 @@ import math
 import numpy as np
 import torch
 
+from ..frame import column as C
 from . import common as U
 from .base import Estimator, Model
 from .linalg import DenseMatrix, DenseVector
@@ -66,6 +67,19 @@ def class_sums(comm, X: torch.Tensor, y: torch.Tensor, w: torch.Tensor | None, K
     return S, S2, buf[-K:]
 
 
+def sparse_class_sums(comm, rows, y: torch.Tensor, w: torch.Tensor | None, K: int):
+    """All-reduced (S [K,D], None, weight per class [K]) fp64 for CSR rows (ops.sparse):
+    one CSC column-sum pass per class with r = w * [y == k]."""
+    dev = rows.device
+    yd = y.to(dev)
+    wd = torch.ones_like(yd, dtype=torch.float32) if w is None else w.to(dev, torch.float32)
+    S = torch.stack([rows.colsum(torch.where(yd == k, wd, torch.zeros_like(wd))) for k in range(K)])
+    cnt = torch.zeros(K, dtype=torch.float64, device=dev).index_add_(0, yd.long(), wd.to(torch.float64))
+    buf = torch.cat([S.reshape(-1), cnt])
+    comm.all_reduce(buf)
+    return buf[: K * rows.d].reshape(K, rows.d), None, buf[-K:]
+
+
 @register("org.apache.spark.ml.classification.NaiveBayes")
 class NaiveBayes(Estimator, _NaiveBayesParams, MLWritable, MLReadable):
     """Naive Bayes Classifiers. It supports both Multinomial and Bernoulli NB. Multinomial
@@ -93,19 +107,29 @@ class NaiveBayes(Estimator, _NaiveBayesParams, MLWritable, MLReadable):
             raise ValueError(f"Invalid modelType: {mt}. Supported: {', '.join(_TYPES)}")
         lam = float(g(self.smoothing))
         comm = df.comm
-        X = U.dense_features(df, g(self.featuresCol))
         y = U.numeric_column(df, g(self.labelCol))
         w = U.weights_or_none(df, self)
         K = U.num_classes(comm, y)
-        if mt in ("multinomial", "complement") and X.numel():
-            lo = -comm.max_scalar(float(-X.float().min()))
+        col = U.features_column(df, g(self.featuresCol))
+        if isinstance(col, C.SparseVectorColumn) and mt != "gaussian":
+            # term counts stay CSR: per-class column sums by the CSC piece kernels
+            X = U.linear_features(df, g(self.featuresCol))
+            vals = X.val
+        else:
+            X = U.dense_features(df, g(self.featuresCol))
+            vals = X
+        if mt in ("multinomial", "complement") and vals.numel():
+            lo = -comm.max_scalar(float(-vals.float().min()))
             if lo < 0:
                 raise ValueError(f"Naive Bayes requires nonnegative feature values but found {lo}.")
-        if mt == "bernoulli" and X.numel():
-            Xf = X.float()
+        if mt == "bernoulli" and vals.numel():
+            Xf = vals.float()
             if not bool(((Xf == 0) | (Xf == 1)).all()):
                 raise ValueError("Bernoulli naive Bayes requires 0 or 1 feature values.")
-        S, S2, cnt = class_sums(comm, X, y, w, K, squares=mt == "gaussian")
+        if isinstance(X, torch.Tensor):
+            S, S2, cnt = class_sums(comm, X, y, w, K, squares=mt == "gaussian")
+        else:
+            S, S2, cnt = sparse_class_sums(comm, X, y, w, K)
         S, cnt = S.cpu().numpy(), cnt.cpu().numpy()
         D = S.shape[1]
         N = cnt.sum()
@@ -169,7 +193,15 @@ class NaiveBayesModel(U.ProbabilisticClassifierMixin, Model, _NaiveBayesParams, 
     def numFeatures(self) -> int:
         return int(self._theta.shape[1])
 
+    def _features_for_predict(self, df, name):
+        mt = self.getOrDefault(self.modelType) if self.isDefined(self.modelType) else self._type
+        if mt != "gaussian":
+            return U.linear_features(df, name)      # CSR rows for sparse counts
+        return U.dense_features(df, name)
+
     def _raw(self, X):
+        if not isinstance(X, torch.Tensor):         # CSR rows: one sparse margin pass per class
+            return self._raw_sparse(X)
         dt = torch.float32 if X.is_cuda else torch.float64
         Xf = X.to(dt)[:, : self.numFeatures]
         th = torch.from_numpy(self._theta).to(X.device, dt)
@@ -189,6 +221,20 @@ class NaiveBayesModel(U.ProbabilisticClassifierMixin, Model, _NaiveBayesParams, 
             quad = (Xf * Xf) @ iv.T - 2.0 * Xf @ (th * iv).T + (th * th * iv).sum(1)
             raw = pi - 0.5 * torch.log(2 * math.pi * var).sum(1) - 0.5 * quad
         return raw.to(torch.float64)
+
+    def _raw_sparse(self, X):
+        mt = self.getOrDefault(self.modelType) if self.isDefined(self.modelType) else self._type
+        th, pi = self._theta, self._pi
+        K = th.shape[0]
+        if mt == "multinomial":
+            cols = [U.linear_margin(X, th[k], pi[k]) for k in range(K)]
+        elif mt == "bernoulli":
+            neg = np.log1p(-np.exp(th))
+            cols = [U.linear_margin(X, th[k] - neg[k], pi[k] + neg[k].sum()) for k in range(K)]
+        else:  # complement
+            s = torch.stack([U.linear_margin(X, th[k], 0.0) for k in range(K)], 1)
+            return s - torch.logsumexp(s, dim=1, keepdim=True)
+        return torch.stack(cols, 1)
 
     def _raw2prob(self, raw):
         return torch.softmax(raw, dim=1)

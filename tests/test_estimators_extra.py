@@ -4,7 +4,7 @@ import numpy as np
 import pandas as pd
 import pytest
 
-from orange3_spark_amd import Session
+from orange3_spark_amd import Session, SessionConf
 from orange3_spark_amd.ml import classification as CL
 from orange3_spark_amd.ml import regression as RG
 from orange3_spark_amd.ml.feature import VectorAssembler
@@ -167,3 +167,31 @@ def test_aft_matches_scipy(session):
     assert abs(a.scale - np.exp(r.x[4])) < 1e-4
     q = column(a.transform(df), "q")
     assert q.shape == (400, 9) and np.all(np.diff(q, axis=1) > 0)
+
+
+@pytest.mark.parametrize("mt", ["multinomial", "bernoulli", "complement"])
+def test_naive_bayes_sparse_counts_match_dense(mt):
+    """Term-count (CSR) features fit and predict without densifying, same model as dense."""
+    import torch
+    from orange3_spark_amd.frame import column as C
+    from orange3_spark_amd.ml.classification import NaiveBayes
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    rng = np.random.default_rng(7)
+    n, d = 600, 30
+    X = rng.poisson(0.4, size=(n, d)).astype(float)
+    if mt == "bernoulli":
+        X = (X > 0).astype(float)
+    y = (X[:, :5].sum(1) > X[:, 5:10].sum(1)).astype(float)
+    dense = s.createDataFrame(pd.DataFrame({"features": list(X), "label": y}))
+    nz = [np.nonzero(r)[0] for r in X]
+    indptr = torch.tensor(np.concatenate([[0], np.cumsum([len(z) for z in nz])]), dtype=torch.int64)
+    sp = dense.withColumnData("features", C.SparseVectorColumn(
+        indptr, torch.tensor(np.concatenate(nz), dtype=torch.int32),
+        torch.tensor(np.concatenate([X[i, z] for i, z in enumerate(nz)]), dtype=torch.float32), d))
+    a = NaiveBayes(modelType=mt).fit(dense)
+    b = NaiveBayes(modelType=mt).fit(sp)
+    np.testing.assert_allclose(b.theta.toArray(), a.theta.toArray(), rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(b.pi.toArray(), a.pi.toArray(), rtol=1e-12)
+    pa = np.stack(a.transform(dense).toPandas()["probability"].map(lambda v: v.toArray()))
+    pb = np.stack(b.transform(sp).toPandas()["probability"].map(lambda v: v.toArray()))
+    np.testing.assert_allclose(pb, pa, rtol=1e-9, atol=1e-12)
