@@ -163,3 +163,30 @@ def test_gpu_text_pipeline_tokenizer_hashingtf_lr_stays_sparse():
     model = pipe.fit(df)
     auc = BinaryClassificationEvaluator().evaluate(model.transform(df))
     assert auc > 0.99, auc
+
+
+@pytest.mark.gpu
+def test_gpu_naive_bayes_sparse_counts():
+    """Multinomial NB on CSR term counts on the GPU == the CPU fp64 fit."""
+    import pandas as pd
+    from orange3_spark_amd.frame import column as C
+    from orange3_spark_amd.ml.classification import NaiveBayes
+    rng = np.random.default_rng(2)
+    n, d = 20_000, 3000
+    X = rng.poisson(0.02, size=(n, d)).astype(np.float32)
+    y = (X[:, :50].sum(1) > X[:, 50:100].sum(1)).astype(float)
+    nz = [np.nonzero(r)[0] for r in X]
+    indptr = torch.tensor(np.concatenate([[0], np.cumsum([len(z) for z in nz])]), dtype=torch.int64)
+    idx = torch.tensor(np.concatenate(nz), dtype=torch.int32)
+    val = torch.tensor(np.concatenate([X[i, z] for i, z in enumerate(nz)]), dtype=torch.float32)
+    out = []
+    for dev in ("cpu", "cuda"):
+        s = Session(SessionConf().set("o3s.device", dev))
+        df = s.createDataFrame(pd.DataFrame({"label": y}))
+        df = df.withColumnData("features", C.SparseVectorColumn(indptr.to(s.device), idx.to(s.device),
+                                                                val.to(s.device), d))
+        m = NaiveBayes().fit(df)
+        prob = np.stack(m.transform(df).toPandas()["probability"].map(lambda v: v.toArray()))
+        out.append((m.theta.toArray(), prob))
+    np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-6, atol=1e-8)
+    np.testing.assert_allclose(out[1][1], out[0][1], rtol=1e-3, atol=5e-5)   # fp32 sparse margins
