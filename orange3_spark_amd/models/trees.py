@@ -125,6 +125,43 @@ def _impurity(stats: torch.Tensor, kind: str) -> tuple[torch.Tensor, torch.Tenso
     return torch.where(w > 0, imp, torch.zeros_like(imp)), w
 
 
+def _split_bundle_torch(H, kind, cls, nb, bin_ids, fm, min_inst, min_w, min_wfrac):
+    """Reference of ``tree_split_kernel``: the per-node decision bundle (fp64
+    [idx | gain | impurity | weight | wL | wR | values]) from histograms [k, F, B, S]."""
+    k = H.shape[0]
+    dev = H.device
+    tot = H[:, 0].sum(1)                                   # [k, S] node stats (feature 0 bins)
+    imp_p, w_p = _impurity(tot, kind)
+    vals = (tot / w_p.clamp_min(1e-300)[:, None]) if cls else (tot[:, 1] / w_p.clamp_min(1e-300))[:, None]
+    # split search: cumulative stats over bins (left = bins <= j)
+    cum = H.cumsum(2)                                      # [k, F, B, S]
+    left = cum[:, :, :-1]
+    right = tot[:, None, None, :] - left
+    W = w_p[:, None, None].clamp_min(1e-300)
+    if cls:
+        iL, wL = _impurity(left, kind)
+        iR, wR = _impurity(right, kind)
+        g = imp_p[:, None, None] - (wL / W) * iL - (wR / W) * iR
+    else:
+        # variance gain from (w, w*y) only: (SyL^2/wL + SyR^2/wR - Sy^2/W) / W
+        wL, wR = left[..., 0], right[..., 0]
+        sL, sR = left[..., 1], right[..., 1]
+        sP = tot[:, 1][:, None, None]
+        g = (sL * sL / wL.clamp_min(1e-300) + sR * sR / wR.clamp_min(1e-300) - sP * sP / W) / W
+    ok = (wL >= min_inst) & (wR >= min_inst)
+    mw = (min_wfrac * w_p)[:, None, None] if min_wfrac > 0.0 else torch.full_like(W, min_w)
+    ok &= (mw <= 0.0) | ((wL >= mw) & (wR >= mw))
+    ok &= bin_ids[None, None, :] < nb[None, :, None]
+    if fm is not None:
+        ok &= torch.from_numpy(fm).to(dev)[:, :, None]
+    g = torch.where(ok, g, torch.full_like(g, -math.inf))
+    best = g.reshape(k, -1).max(1)
+    # global child weights at the chosen split decide which child the next level scans
+    wl_best = wL.reshape(k, -1).gather(1, best.indices[:, None])[:, 0]
+    wr_best = wR.reshape(k, -1).gather(1, best.indices[:, None])[:, 0]
+    return torch.cat([best.indices.to(torch.float64), best.values, imp_p, w_p, wl_best, wr_best, vals.reshape(-1)])
+
+
 @dataclass
 class Tree:
     """Flat tree: arrays indexed by Spark node id (1-based; 0 unused)."""
@@ -236,6 +273,13 @@ class TreeBuilder:
         count = np.zeros(max_nodes)
         order = torch.arange(n, dtype=torch.int32, device=dev)
         spare = torch.empty_like(order) if (leaf_acc is not None and order.is_cuda) else None
+        # labels / weights travel with the rows in POSITION order (yp[p] belongs to row
+        # order[p]): the histogram kernel streams them instead of gathering a cache line
+        # per row; order starts as the identity, so the initial copies are plain clones
+        yp = self.y.to(torch.float32).contiguous().clone()
+        wp = None if self.w is None else self.w.to(torch.float32).contiguous().clone()
+        y_sp = torch.empty_like(yp) if spare is not None else None
+        w_sp = torch.empty_like(wp) if (spare is not None and wp is not None) else None
         # segment bounds live on the HOST (a few hundred int64s): per level there are two
         # device->host copies (the split decisions, then the left counts of the partition)
         # and the work-item plans are uploaded right after them, while the GPU is idle
@@ -259,14 +303,15 @@ class TreeBuilder:
             node_ids = seg_node
             with trace("tree.hist"):
                 if parent_H is None or not self.hist_subtraction:
-                    H = T.node_hist(self.bins, order, self.y, self.w, seg_lo, seg_hi, np.arange(k), k, B, S, self.cls)
+                    H = T.node_hist(self.bins, order, yp, wp, seg_lo, seg_hi, np.arange(k), k, B, S, self.cls,
+                                    ypos=True)
                     H = H.to(torch.float64).contiguous()
                     self.comm.all_reduce(H)                       # [k, F, B, S]
                 else:
                     P = k // 2                                    # segments come as (left, right) pairs
                     pick_h = 2 * np.arange(P) + small_right.astype(np.int64)
-                    Hs = T.node_hist(self.bins, order, self.y, self.w, seg_lo[pick_h], seg_hi[pick_h],
-                                     np.arange(P), P, B, S, self.cls)
+                    Hs = T.node_hist(self.bins, order, yp, wp, seg_lo[pick_h], seg_hi[pick_h],
+                                     np.arange(P), P, B, S, self.cls, ypos=True)
                     Hs = Hs.to(torch.float64).contiguous()
                     self.comm.all_reduce(Hs)
                     pick = torch.from_numpy(pick_h).to(dev)
@@ -275,48 +320,28 @@ class TreeBuilder:
                     H[pick ^ 1] = _sibling(parent_H, Hs, self.cls)
             tsplit = trace("tree.split")
             tsplit.__enter__()
-            tot = H[:, 0].sum(1)                                   # [k, S] node stats (feature 0 bins)
-            imp_p, w_p = _impurity(tot, self.kind)
-            vals = (tot / w_p.clamp_min(1e-300)[:, None]) if self.cls else \
-                (tot[:, 1] / w_p.clamp_min(1e-300))[:, None]
-            # split search: cumulative stats over bins (left = bins <= j)
-            cum = H.cumsum(2)                                      # [k, F, B, S]
-            left = cum[:, :, :-1]
-            right = tot[:, None, None, :] - left
-            W = w_p[:, None, None].clamp_min(1e-300)
-            if self.cls:
-                iL, wL = _impurity(left, self.kind)
-                iR, wR = _impurity(right, self.kind)
-                g = imp_p[:, None, None] - (wL / W) * iL - (wR / W) * iR
-            else:
-                # variance gain from (w, w*y) only: (SyL^2/wL + SyR^2/wR - Sy^2/W) / W
-                wL, wR = left[..., 0], right[..., 0]
-                sL, sR = left[..., 1], right[..., 1]
-                sP = tot[:, 1][:, None, None]
-                g = (sL * sL / wL.clamp_min(1e-300) + sR * sR / wR.clamp_min(1e-300) - sP * sP / W) / W
-            ok = (wL >= self.min_inst) & (wR >= self.min_inst)
-            if self.min_wfrac > 0.0:
-                if depth == 0:
-                    self.min_w = self.min_wfrac * float(w_p[0])   # fraction of the root's total weight
-                ok &= (wL >= self.min_w) & (wR >= self.min_w)
-            ok &= bin_ids[None, None, :] < nb[None, :, None]
+            fm = None
             if self.ffrac < 1.0:
                 m = max(1, int(math.ceil(self.ffrac * F)))
                 fm = np.zeros((k, F), dtype=bool)
                 for i in range(k):
                     fm[i, rng.choice(F, m, replace=False)] = True
-                ok &= torch.from_numpy(fm).to(dev)[:, :, None]
-            g = torch.where(ok, g, torch.full_like(g, -math.inf))
-            best = g.reshape(k, -1).max(1)
-            # global child weights at the chosen split decide which child the next level scans
-            wl_best = wL.reshape(k, -1).gather(1, best.indices[:, None])[:, 0]
-            wr_best = wR.reshape(k, -1).gather(1, best.indices[:, None])[:, 0]
+            # min child weight: at the root a fraction of its total weight (Spark
+            # minWeightFractionPerNode), below it the absolute value that gave
+            mw_frac = self.min_wfrac if depth == 0 else 0.0
+            mw_abs = getattr(self, "min_w", 0.0)
+            if H.is_cuda:
+                bundle_t = T.best_splits(H, nb, fm, self.kind, self.min_inst, mw_abs, mw_frac)
+            else:
+                bundle_t = _split_bundle_torch(H, self.kind, self.cls, nb, bin_ids, fm, self.min_inst, mw_abs,
+                                               mw_frac)
             # ONE device->host copy of every per-node decision input
-            bundle = torch.cat([best.indices.to(torch.float64), best.values, imp_p, w_p, wl_best, wr_best,
-                                vals.reshape(-1)]).cpu().numpy()
+            bundle = bundle_t.cpu().numpy()
             bi = bundle[:k].astype(np.int64)
             bg, imp_np, w_np, wl_np, wr_np = (bundle[q * k:(q + 1) * k] for q in range(1, 6))
             vals_np = bundle[6 * k:].reshape(k, V)
+            if depth == 0 and self.min_wfrac > 0.0:
+                self.min_w = self.min_wfrac * float(w_np[0])      # fraction of the root's total weight
             bf, bb = bi // (B - 1), bi % (B - 1)
             value[node_ids] = vals_np
             impurity[node_ids] = imp_np
@@ -346,13 +371,19 @@ class TreeBuilder:
             s_lo, s_hi, s_node = seg_lo[do_split], seg_hi[do_split], seg_node[do_split]
             parent_H = H[torch.from_numpy(do_split).to(dev)]
             small_right = (wr_np < wl_np)[do_split]
+            pay = (yp,) if wp is None else (yp, wp)
             if spare is not None:                                 # ping-pong: no full copy
+                pout = (y_sp,) if wp is None else (y_sp, w_sp)
                 new_order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
-                                               bins_t=self.bins_t, out=spare)
+                                               bins_t=self.bins_t, out=spare, payload=pay, payload_out=pout)
                 spare, order = order, new_order
+                y_sp, yp = yp, y_sp
+                w_sp, wp = wp, w_sp
             else:
+                pout = tuple(t.clone() for t in pay)
                 order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
-                                           bins_t=self.bins_t)
+                                           bins_t=self.bins_t, payload=pay, payload_out=pout)
+                yp, wp = pout[0], (pout[1] if len(pout) > 1 else None)
             mid = s_lo + nleft.cpu().numpy().astype(np.int64)
             seg_lo = np.stack([s_lo, mid], 1).reshape(-1)
             seg_hi = np.stack([mid, s_hi], 1).reshape(-1)

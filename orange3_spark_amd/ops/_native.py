@@ -43,7 +43,7 @@ _SIGS: dict[str, list] = {
     "o3s_tokenize": [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_murmur3_spans": [c_vp, c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp],
     "o3s_tree_partition": [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
-                           c_vp],
+                           c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_glm_sgd_update": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_f64, c_f64, c_i32, c_vp, c_vp, c_vp],
     "o3s_glm_sgd_update_dev": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_f64, c_f64, c_i32, c_vp, c_vp, c_i64, c_vp,
                                c_vp],
@@ -58,7 +58,9 @@ _SIGS: dict[str, list] = {
     "o3s_als_cg": [c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_als_pass": [c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_tree_hist_lds": [c_i32, c_i32, c_i32, c_i32],
-    "o3s_tree_hist": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],
+    "o3s_tree_split": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_f64, c_f64, c_f64, c_vp, c_vp],
+    "o3s_tree_hist": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32,
+                      c_vp],
     "o3s_eval_grid": [c_i64],
     "o3s_regression_stats": [c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp],
     "o3s_confusion": [c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp],

@@ -20,6 +20,7 @@
 // CLS (S = #classes: weighted class counts -- gini/entropy).
 #include "common.h"
 
+
 using namespace o3s;
 
 namespace {
@@ -37,17 +38,20 @@ constexpr int kHistThreads = kHistWaves * kWave;
 // FP: features per row-slot (power of 2, <= 64); RS = 64 / FP row-slots per wave.
 // HW: per-row weights present (a compile-time switch: a runtime null test per row
 // became a branch around every weight load and split the counted vmcnt waits).
-template <int FP, bool CLS, bool HW>
-__global__ __launch_bounds__(kHistThreads) void tree_hist_kernel(
+// YP: y / w are stored in POSITION order (y[p] belongs to row order[p]; the partition
+// moves them with the rows), so they stream contiguously instead of costing one random
+// cache-line gather each per row -- only the 64-B bins row is gathered.
+template <int FP, bool CLS, bool HW, bool YP, int U>
+__global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
     const uint8_t* __restrict__ bins, int F, int fg0, int B, int S, const int32_t* __restrict__ order,
     const float* __restrict__ y, const float* __restrict__ w, const int64_t* __restrict__ item_lo,
     const int64_t* __restrict__ item_hi, float* __restrict__ slab, int64_t slab_stride) {
   constexpr int RS = kWave / FP;
-  constexpr int U = 8;
   const int SL = CLS ? S : 2;                                     // stats kept in LDS
   extern __shared__ __attribute__((aligned(16))) float hist[];   // [wave][rs][B][SL][FP] (+pad)
   __shared__ float y2part[kHistWaves * RS];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
   const int rs = lane / FP, f = lane % FP;
   const int region = B * SL * FP + 16;                            // +16: rs-regions on distinct banks
   const int per_wave = RS * region;
@@ -57,62 +61,150 @@ __global__ __launch_bounds__(kHistThreads) void tree_hist_kernel(
   const int fcol = fg0 + f;
   const bool fok = fcol < F;
   const int64_t lo = item_lo[blockIdx.x], hi = item_hi[blockIdx.x];
-  const int64_t stride = (int64_t)kHistWaves * RS;                // rows dealt round-robin to row-slots
   float wy2 = 0.f;                                                // REG: sum of w*y^2 (lanes f == 0)
-  // Three-stage software pipeline over batches of U rows per lane: the order[] indices
-  // of batch k+2 and the bins/y/w gathers of batch k+1 are in flight while batch k is
-  // accumulated.  Loads are unconditional (clamped to the item; masked rows contribute
-  // weight 0 at use time), so the compiler emits counted vmcnt waits instead of
-  // draining every load at a branch merge.
-  // Positions are 32-bit offsets inside the item (items hold <= 2^31 rows): the row loop's
-  // index math and clamps stay single SALU ops (the CU's scalar unit is shared by its waves).
+  // Positions are 32-bit offsets inside the item (items hold <= 2^31 rows); loads are
+  // unconditional (clamped to the item; rows past it get weight 0), so the compiler
+  // emits counted vmcnt waits instead of draining every load at a branch merge.
   const int32_t* __restrict__ ord = order + lo;
   const int32_t nl = (int32_t)(hi - lo);
-  const int32_t s32 = (int32_t)stride, step = s32 * U;
-  auto ld_rows = [&](int32_t j0, int32_t (&r)[U]) {
+  const float* __restrict__ yl = YP ? y + lo : y;
+  const float* __restrict__ wl = (YP && HW) ? w + lo : w;
+  if constexpr (RS == 1) {
+    // One row per wave-instruction (lane = feature).  The per-row metadata comes in
+    // 32-row chunks -- lane l loads order[] / y / w of position l of the chunk, ONE
+    // vector load each per 32 rows -- and is broadcast per row with v_readlane, so a row
+    // costs one 64-B gather, one LDS read + write and a few VALU (the first version
+    // issued three uniform vector loads per row and ran at half this rate:
+    // tools/bench_hist.py 62.5M rows 6.2 -> 2.8 ms).  Chunks of a wave: wid,
+    // wid + kHistWaves, ...; two chunk buffers swap roles: while chunk c is accumulated,
+    // chunk c+1's 32 gathers and chunk c+2's order[] entries are in flight.
+    constexpr int32_t CH = 32;                     // < 63 loads in flight: vmcnt stays countable
+    constexpr int32_t cstep = kHistWaves * CH;
+    const int32_t j0w = wid * CH;
+    const int fc = fok ? fcol : 0;
+    auto ld_ord = [&](int32_t jb, int32_t& ov) {
+      const int32_t j = jb + j0w + (lane & (CH - 1));
+      ov = ord[j < nl ? j : nl - 1];
+    };
+    auto ld_chunk = [&](int32_t jb, int32_t ov, int (&bo)[CH], float& yv, float& wv) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int32_t j = j0 + u * s32;
-      r[u] = ord[j < nl ? j : nl - 1];
-    }
-  };
-  auto ld_data = [&](const int32_t (&r)[U], int (&bo)[U], float (&yo)[U], float (&wo)[U]) {
+      for (int q = 0; q < CH; ++q) {
+        const int32_t row = __builtin_amdgcn_readlane(ov, q);
+        bo[q] = (bins + (int64_t)row * F)[fc];
+      }
+      const int32_t j = jb + j0w + (lane & (CH - 1));
+      const int32_t jc = j < nl ? j : nl - 1;
+      yv = YP ? yl[jc] : y[ov];
+      wv = HW ? (YP ? wl[jc] : w[ov]) : 1.f;
+      wv = j < nl ? wv : 0.f;
+    };
+    auto acc_chunk = [&](const int (&bo)[CH], float yv, float wv) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t row = r[u];
-      bo[u] = bins[row * F + (fok ? fcol : 0)];
-      yo[u] = y[row];
-      wo[u] = HW ? w[row] : 1.f;
-    }
-  };
-  int32_t r1[U], r2[U];
-  int b0[U], b1[U];
-  float y0[U], y1[U], w0[U], w1[U];
-  int32_t j0 = wid * RS + rs;
-  if (j0 < nl) {
-    ld_rows(j0, r1);
-    ld_data(r1, b0, y0, w0);
-    ld_rows(j0 + step, r1);
-  }
-  for (; j0 < nl; j0 += step) {
-    ld_rows(j0 + 2 * step, r2);
-    ld_data(r1, b1, y1, w1);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool ok = fok && (j0 + u * s32 < nl);
-      const float wv = ok ? w0[u] : 0.f;
-      float* cell = my + b0[u] * SL * FP + f;
-      if (CLS) {
-        cell[(int)y0[u] * FP] += wv;
-      } else {
-        const float wy = wv * y0[u];
-        cell[0] += wv;
-        cell[FP] += wy;
-        wy2 = fmaf(wy, y0[u], wy2);
+      for (int q = 0; q < CH; ++q) {
+        const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), q));
+        const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), q));
+        float* cell = my + bo[q] * SL * FP + f;
+        if (CLS) {
+          cell[(int)yq * FP] += wq;
+        } else {
+          const float wy = wq * yq;
+          cell[0] += wq;
+          cell[FP] += wy;
+          wy2 = fmaf(wy, yq, wy2);
+        }
+      }
+    };
+    if (j0w < nl) {
+      // per step: gathers of chunk c+1 (its order[] arrived during the previous step),
+      // order[] of chunk c+2, then the LDS updates of chunk c.  sched_barrier keeps the
+      // phases in this order (the scheduler would pull loads next to their consumers).
+      int bA[CH], bB[CH];
+      int32_t ov;
+      float yA, yB, wA, wB;
+      ld_ord(0, ov);
+      ld_chunk(0, ov, bA, yA, wA);
+      ld_ord(cstep, ov);
+      for (int32_t jb = 0;; jb += 2 * cstep) {
+        __builtin_amdgcn_sched_barrier(0);
+        ld_chunk(jb + cstep, ov, bB, yB, wB);
+        __builtin_amdgcn_sched_barrier(0);
+        ld_ord(jb + 2 * cstep, ov);
+        __builtin_amdgcn_sched_barrier(0);
+        acc_chunk(bA, yA, wA);
+        if (jb + cstep + j0w >= nl) break;
+        __builtin_amdgcn_sched_barrier(0);
+        ld_chunk(jb + 2 * cstep, ov, bA, yA, wA);
+        __builtin_amdgcn_sched_barrier(0);
+        ld_ord(jb + 3 * cstep, ov);
+        __builtin_amdgcn_sched_barrier(0);
+        acc_chunk(bB, yB, wB);
+        if (jb + 2 * cstep + j0w >= nl) break;
       }
     }
+  } else {
+    // Several row-slots per wave (FP < 64): lanes gather their own rows.  Batch k of a
+    // wave = U*RS consecutive positions k*step + wid*U*RS + u*RS + rs; the two batch
+    // buffers swap roles (a register rotation would force the compiler to drain every
+    // in-flight load): batch k+1's gathers and batch k+2's order[] reads fly while batch
+    // k is accumulated.
+    constexpr int32_t step = kHistWaves * U * RS;
+    const int32_t jw = wid * (U * RS) + rs;
+    auto ld_rows = [&](int32_t jb, int32_t (&r)[U]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) { b0[u] = b1[u]; y0[u] = y1[u]; w0[u] = w1[u]; r1[u] = r2[u]; }
+      for (int u = 0; u < U; ++u) {
+        const int32_t j = jb + jw + u * RS;
+        r[u] = ord[j < nl ? j : nl - 1];
+      }
+    };
+    auto ld_data = [&](int32_t jb, const int32_t (&r)[U], int (&bo)[U], float (&yo)[U], float (&wo)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = r[u];
+        bo[u] = bins[row * F + (fok ? fcol : 0)];
+        if (YP) {
+          const int32_t j = jb + jw + u * RS;
+          const int32_t jc = j < nl ? j : nl - 1;
+          yo[u] = yl[jc];
+          wo[u] = HW ? wl[jc] : 1.f;
+        } else {
+          yo[u] = y[row];
+          wo[u] = HW ? w[row] : 1.f;
+        }
+      }
+    };
+    auto accumulate = [&](int32_t jb, const int (&bo)[U], const float (&yo)[U], const float (&wo)[U]) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool ok = fok && (jb + jw + u * RS < nl);
+        const float wv = ok ? wo[u] : 0.f;
+        float* cell = my + bo[u] * SL * FP + f;
+        if (CLS) {
+          cell[(int)yo[u] * FP] += wv;
+        } else {
+          const float wy = wv * yo[u];
+          cell[0] += wv;
+          cell[FP] += wy;
+          wy2 = fmaf(wy, yo[u], wy2);
+        }
+      }
+    };
+    int32_t rA[U], rB[U];
+    int bA[U], bB[U];
+    float yA[U], yB[U], wA[U], wB[U];
+    if (jw < nl) {
+      ld_rows(0, rA);
+      ld_data(0, rA, bA, yA, wA);
+      ld_rows(step, rB);
+      for (int32_t j0 = 0; j0 < nl; j0 += 2 * step) {
+        ld_data(j0 + step, rB, bB, yB, wB);
+        ld_rows(j0 + 2 * step, rA);
+        accumulate(j0, bA, yA, wA);
+        if (j0 + step >= nl) break;
+        ld_data(j0 + 2 * step, rA, bA, yA, wA);
+        ld_rows(j0 + 3 * step, rB);
+        accumulate(j0 + step, bB, yB, wB);
+      }
+    }
   }
   if (!CLS && f == 0) y2part[wid * RS + rs] = wy2;
   __syncthreads();
@@ -182,7 +274,8 @@ __global__ __launch_bounds__(kPartThreads) void tree_part_scatter_kernel(
     const int32_t* __restrict__ order, int32_t* __restrict__ out,
     const int64_t* __restrict__ it_lo, const int64_t* __restrict__ it_hi, const int32_t* __restrict__ it_feat,
     const int32_t* __restrict__ it_bin, const int64_t* __restrict__ dst_left, const int64_t* __restrict__ dst_right,
-    const uint8_t* __restrict__ flags) {
+    const uint8_t* __restrict__ flags, const float* __restrict__ py, float* __restrict__ py_out,
+    const float* __restrict__ pw, float* __restrict__ pw_out) {
   __shared__ int wl[kPartWaves];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t lo = it_lo[blockIdx.x], hi = it_hi[blockIdx.x];
@@ -207,8 +300,11 @@ __global__ __launch_bounds__(kPartThreads) void tree_part_scatter_kernel(
     const int64_t round_base = p - threadIdx.x;
     const int valid = (int)((hi - round_base) < kPartThreads ? (hi - round_base) : kPartThreads);
     if (ok) {
-      if (left) out[nl + rank_l] = row;
-      else out[nr + ((int)threadIdx.x - rank_l)] = row;           // rights before me = idx - lefts before
+      // rights before me = idx - lefts before; position-ordered payloads move with the row
+      const int64_t d = left ? nl + rank_l : nr + ((int)threadIdx.x - rank_l);
+      out[d] = row;
+      if (py) py_out[d] = py[p];
+      if (pw) pw_out[d] = pw[p];
     }
     nl += total;
     nr += valid - total;
@@ -329,6 +425,125 @@ __global__ __launch_bounds__(256) void slab_range_sum_kernel(const T* __restrict
   out[(int64_t)blockIdx.y * C + c] = acc;
 }
 
+// ---------------------------------------------------------------------------------
+// Best split per node, fused (replaces ~40 small device ops per tree level).  One block
+// per node: thread f scans feature f's bins once in ascending order, keeping the
+// cumulative left stats (right = node total - left), and evaluates every threshold's
+// gain with Spark's impurity definitions (variance from (w, w*y) sums; gini / entropy
+// from class counts); the block then keeps the largest gain (ties -> lowest candidate
+// index f*(B-1)+b, deterministic).  The node total comes from feature 0 (REG: stat 2,
+// the sum of w*y^2, is stored in feature 0's bin 0 only).
+// out (fp64, k nodes): [best idx | best gain | impurity | weight | wL(best) | wR(best) |
+// values k x V] -- the exact bundle the engine copies to the host once per level.
+constexpr int kSplitThreads = 256;
+constexpr int kSplitMaxS = 64;
+
+// SM: compile-time bound on S (register-resident stats for S <= 8)
+template <int SM>
+__device__ __forceinline__ double split_imp(const double* st, int S, int kind, double& wsum) {
+  // kind 1 = gini, 2 = entropy (classification stats: class weights)
+  double w = 0.0;
+#pragma unroll
+  for (int s = 0; s < SM; ++s)
+    if (s < S) w += st[s];
+  wsum = w;
+  if (!(w > 0.0)) return 0.0;
+  const double inv = 1.0 / (w > 1e-300 ? w : 1e-300);
+  double acc = 0.0;
+#pragma unroll
+  for (int s = 0; s < SM; ++s) {
+    if (s >= S) continue;
+    const double p = st[s] * inv;
+    if (kind == 1) acc += p * p;
+    else if (p > 0.0) acc -= p * log2(p);
+  }
+  return kind == 1 ? 1.0 - acc : acc;
+}
+
+template <bool CLS, int SM>
+__global__ __launch_bounds__(kSplitThreads) void tree_split_kernel(
+    const double* __restrict__ H, int k, int F, int B, int S, int kind, const int32_t* __restrict__ nb,
+    const uint8_t* __restrict__ fmask, double min_inst, double min_w, double min_wfrac, double* __restrict__ out) {
+  __shared__ double tot[kSplitMaxS];
+  __shared__ double rg[kSplitThreads], rwl[kSplitThreads], rwr[kSplitThreads];
+  __shared__ int ri[kSplitThreads];
+  const int node = blockIdx.x;
+  const double* Hn = H + (int64_t)node * F * B * S;
+  for (int s = threadIdx.x; s < S; s += kSplitThreads) {
+    double a = 0.0;
+    for (int b = 0; b < B; ++b) a += Hn[b * S + s];
+    tot[s] = a;
+  }
+  __syncthreads();
+  double imp_p, w_p;
+  if (CLS) {
+    imp_p = split_imp<kSplitMaxS>(tot, S, kind, w_p);
+  } else {
+    w_p = tot[0];
+    const double wc = w_p > 1e-300 ? w_p : 1e-300;
+    const double mean = tot[1] / wc;
+    const double v = tot[2] / wc - mean * mean;
+    imp_p = w_p > 0.0 ? (v > 0.0 ? v : 0.0) : 0.0;
+  }
+  const double W = w_p > 1e-300 ? w_p : 1e-300;
+  const double mw = min_wfrac > 0.0 ? min_wfrac * w_p : min_w;   // depth 0: fraction of the root weight
+  double bg = -INFINITY, bwl = 0.0, bwr = 0.0;
+  int bi = 0x7fffffff;
+  double left[SM], right[SM];
+  for (int f = threadIdx.x; f < F; f += kSplitThreads) {
+    const double* Hf = Hn + (int64_t)f * B * S;
+    const bool fon = fmask == nullptr || fmask[(int64_t)node * F + f];
+    const int nbf = nb[f];
+#pragma unroll
+    for (int s = 0; s < SM; ++s) left[s] = 0.0;
+    for (int b = 0; b < B - 1; ++b) {
+#pragma unroll
+      for (int s = 0; s < SM; ++s)
+        if (s < S) left[s] += Hf[b * S + s];
+      double g, wL, wR;
+      if (CLS) {
+#pragma unroll
+        for (int s = 0; s < SM; ++s) right[s] = s < S ? tot[s] - left[s] : 0.0;
+        const double iL = split_imp<SM>(left, S, kind, wL);
+        const double iR = split_imp<SM>(right, S, kind, wR);
+        g = imp_p - (wL / W) * iL - (wR / W) * iR;
+      } else {
+        wL = left[0];
+        wR = tot[0] - left[0];
+        const double sL = left[1], sR = tot[1] - left[1], sP = tot[1];
+        g = (sL * sL / (wL > 1e-300 ? wL : 1e-300) + sR * sR / (wR > 1e-300 ? wR : 1e-300) - sP * sP / W) / W;
+      }
+      bool ok = wL >= min_inst && wR >= min_inst && b < nbf && fon;
+      if (mw > 0.0) ok = ok && wL >= mw && wR >= mw;
+      const int idx = f * (B - 1) + b;
+      if (ok && (g > bg || (g == bg && idx < bi))) { bg = g; bi = idx; bwl = wL; bwr = wR; }
+    }
+  }
+  rg[threadIdx.x] = bg; ri[threadIdx.x] = bi; rwl[threadIdx.x] = bwl; rwr[threadIdx.x] = bwr;
+  __syncthreads();
+  for (int h = kSplitThreads / 2; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      const int o = threadIdx.x + h;
+      if (rg[o] > rg[threadIdx.x] || (rg[o] == rg[threadIdx.x] && ri[o] < ri[threadIdx.x])) {
+        rg[threadIdx.x] = rg[o]; ri[threadIdx.x] = ri[o]; rwl[threadIdx.x] = rwl[o]; rwr[threadIdx.x] = rwr[o];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int best = ri[0] == 0x7fffffff ? 0 : ri[0];
+    out[node] = (double)best;
+    out[k + node] = rg[0];
+    out[2 * k + node] = imp_p;
+    out[3 * k + node] = w_p;
+    out[4 * k + node] = rwl[0];
+    out[5 * k + node] = rwr[0];
+  }
+  const int V = CLS ? S : 1;
+  for (int v = threadIdx.x; v < V; v += kSplitThreads)
+    out[6 * k + (int64_t)node * V + v] = CLS ? tot[v] / W : tot[1] / W;
+}
+
 }  // namespace
 
 // acc[order[p]] += it_val[i] for p in [it_lo[i], it_hi[i]) (items of leaf segments).
@@ -383,14 +598,16 @@ O3S_API int o3s_u8_transpose(const uint8_t* in, int64_t n, int F, uint8_t* out, 
 O3S_API int o3s_tree_partition(const uint8_t* bins, int64_t rs, int64_t cs, const int32_t* order, int32_t* out,
                                const int64_t* it_lo, const int64_t* it_hi, const int32_t* it_feat,
                                const int32_t* it_bin, int64_t* it_left, const int64_t* dst_left,
-                               const int64_t* dst_right, uint8_t* flags, int n_items, int pass, hipStream_t st) {
+                               const int64_t* dst_right, uint8_t* flags, int n_items, int pass, const float* py,
+                               float* py_out, const float* pw, float* pw_out, hipStream_t st) {
+  if ((py != nullptr) != (py_out != nullptr) || (pw != nullptr) != (pw_out != nullptr)) return -1;
   if (n_items <= 0) return 0;
   if (pass == 0)
     hipLaunchKernelGGL(tree_part_count_kernel, dim3(n_items), dim3(kPartThreads), 0, st, bins, rs, cs, order, it_lo,
                        it_hi, it_feat, it_bin, it_left, flags);
   else
     hipLaunchKernelGGL(tree_part_scatter_kernel, dim3(n_items), dim3(kPartThreads), 0, st, order, out,
-                       it_lo, it_hi, it_feat, it_bin, dst_left, dst_right, flags);
+                       it_lo, it_hi, it_feat, it_bin, dst_left, dst_right, flags, py, py_out, pw, pw_out);
   O3S_CHECK_LAUNCH();
   return 0;
 }
@@ -407,7 +624,7 @@ O3S_API int o3s_tree_hist_lds(int fp, int B, int S, int cls) {
 // slab: [n_items][F*B*S] fp32 (every cell written).  cls: 0 = REG (S must be 3), 1 = CLS.
 O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, int cls, const int32_t* order,
                           const float* y, const float* w, const int64_t* item_lo, const int64_t* item_hi,
-                          int n_items, float* slab, hipStream_t st) {
+                          int n_items, float* slab, int ypos, hipStream_t st) {
   if (n_items <= 0) return 0;
   if (!cls && S != 3) return -1;
   int fp = 1;
@@ -417,9 +634,12 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
   if (lds == 0) return -2;
   const int64_t stride = (int64_t)F * B * S;
   for (int fg0 = 0; fg0 < F; fg0 += fp) {
+#define O3S_TH3(FPV, C, W, P, UU)                                                                       \
+  hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, UU>), dim3(n_items), dim3(kHistThreads), lds, st, bins,  \
+                     F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
+#define O3S_TH2(FPV, C, W, P) O3S_TH3(FPV, C, W, P, 8)
 #define O3S_TH1(FPV, C, W)                                                                              \
-  hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W>), dim3(n_items), dim3(kHistThreads), lds, st, bins, F, fg0, \
-                     B, S, order, y, w, item_lo, item_hi, slab, stride);
+  if (ypos) { O3S_TH2(FPV, C, W, true) } else { O3S_TH2(FPV, C, W, false) }
 #define O3S_TH(FPV)                                                                                     \
   if (fp == FPV) {                                                                                      \
     if (cls && w) { O3S_TH1(FPV, true, true) }                                                          \
@@ -430,8 +650,33 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
     O3S_TH(4) O3S_TH(8) O3S_TH(16) O3S_TH(32) O3S_TH(64)
 #undef O3S_TH
 #undef O3S_TH1
+#undef O3S_TH2
+#undef O3S_TH3
     O3S_CHECK_LAUNCH();
   }
   (void)n;
+  return 0;
+}
+
+// H: [k][F][B][S] fp64 node histograms; nb[F]: valid thresholds per feature; fmask
+// [k][F] (uint8, null = all features); kind 0 = variance (S == 3), 1 = gini, 2 = entropy.
+// min_wfrac > 0 (root level): the minimum child weight is that fraction of the node's
+// weight, else min_w.  out: fp64 [6k + k*V] (see tree_split_kernel).
+O3S_API int o3s_tree_split(const double* H, int k, int F, int B, int S, int kind, const int32_t* nb,
+                           const uint8_t* fmask, double min_inst, double min_w, double min_wfrac, double* out,
+                           hipStream_t st) {
+  if (k <= 0) return 0;
+  if (F <= 0 || B < 2 || S <= 0 || S > kSplitMaxS || kind < 0 || kind > 2) return -1;
+  if (kind == 0 && S != 3) return -1;
+  if (kind == 0)
+    hipLaunchKernelGGL((tree_split_kernel<false, 3>), dim3(k), dim3(kSplitThreads), 0, st, H, k, F, B, S, kind, nb,
+                       fmask, min_inst, min_w, min_wfrac, out);
+  else if (S <= 8)
+    hipLaunchKernelGGL((tree_split_kernel<true, 8>), dim3(k), dim3(kSplitThreads), 0, st, H, k, F, B, S, kind, nb,
+                       fmask, min_inst, min_w, min_wfrac, out);
+  else
+    hipLaunchKernelGGL((tree_split_kernel<true, kSplitMaxS>), dim3(k), dim3(kSplitThreads), 0, st, H, k, F, B, S,
+                       kind, nb, fmask, min_inst, min_w, min_wfrac, out);
+  O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -1,6 +1,7 @@
 """Tree histogram op: gfx950 kernel (csrc/trees.hip) with a PyTorch reference."""
 from __future__ import annotations
 
+import numpy as np
 import torch
 
 from . import _native as N
@@ -43,7 +44,7 @@ def feature_major(bins: torch.Tensor) -> torch.Tensor | None:
 
 def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi: torch.Tensor,
               s_feat: torch.Tensor, s_bin: torch.Tensor, chunk: int = 1 << 14, bins_t: torch.Tensor | None = None,
-              out: torch.Tensor | None = None):
+              out: torch.Tensor | None = None, payload=(), payload_out=()):
     """Stable split of every segment [s_lo, s_hi) of ``order`` into rows with
     bins[row, feat] <= bin (first) and the rest.  Returns (new_order, nleft per segment).
 
@@ -51,11 +52,19 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     position of it untouched (ping-pong buffers of a caller that no longer needs the
     rows outside the split segments); default: a full copy of ``order`` first.
 
+    ``payload`` (<= 2 fp32 arrays in POSITION order, e.g. y and w): moved with the rows
+    into the matching ``payload_out`` buffers (same rule as ``out``: positions outside
+    the split segments are not written).
+
     GPU: two passes of ``tree_part_*_kernel`` over work items (count, then scatter to
     destinations computed by small scans here); CPU: the PyTorch reference."""
+    payload, payload_out = tuple(payload), tuple(payload_out)
+    if len(payload) != len(payload_out) or len(payload) > 2:
+        raise ValueError("payload / payload_out mismatch")
     if not (bins.is_cuda and order.dtype == torch.int32):
         dv = bins.device
-        return partition_torch(bins, order, _dev(s_lo, dv), _dev(s_hi, dv), _dev(s_feat, dv), _dev(s_bin, dv))
+        return partition_torch(bins, order, _dev(s_lo, dv), _dev(s_hi, dv), _dev(s_feat, dv), _dev(s_bin, dv),
+                               out=out, payload=payload, payload_out=payload_out)
     import numpy as np
     dev = bins.device
     F = bins.shape[1]
@@ -83,16 +92,22 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     src, rs, cs = (bins_t, 1, bins.shape[0]) if bins_t is not None else (bins, F, 1)
     N.check(lib.o3s_tree_partition(src.data_ptr(), rs, cs, order.data_ptr(), None, it_lo.data_ptr(), it_hi.data_ptr(),
                                    it_feat.data_ptr(), it_bin.data_ptr(), it_left.data_ptr(), None, None,
-                                   flags.data_ptr(), n_items, 0, st), "tree_part_count")
+                                   flags.data_ptr(), n_items, 0, None, None, None, None, st), "tree_part_count")
     it_right = (it_hi - it_lo) - it_left
     nleft = torch.zeros(nseg, dtype=torch.int64, device=dev).index_add_(0, it_seg, it_left)
     cl = torch.cumsum(it_left, 0) - it_left                    # global exclusive prefixes
     cr = torch.cumsum(it_right, 0) - it_right
     dst_left = (seg_lo_it + cl - cl[f]).contiguous()           # f: first item of each item's segment
     dst_right = (seg_lo_it + nleft[it_seg] + cr - cr[f]).contiguous()
+    pl = [None] * 4
+    for q, (a, b) in enumerate(zip(payload, payload_out)):
+        if a.dtype != torch.float32 or b.dtype != torch.float32 or a.numel() != order.numel() \
+                or b.numel() != order.numel() or not (a.is_contiguous() and b.is_contiguous()):
+            raise ValueError("payloads must be contiguous fp32 arrays of the order's length")
+        pl[2 * q], pl[2 * q + 1] = a.data_ptr(), b.data_ptr()
     N.check(lib.o3s_tree_partition(src.data_ptr(), rs, cs, order.data_ptr(), new_order.data_ptr(), it_lo.data_ptr(),
                                    it_hi.data_ptr(), it_feat.data_ptr(), it_bin.data_ptr(), None,
-                                   dst_left.data_ptr(), dst_right.data_ptr(), flags.data_ptr(), n_items, 1, st),
+                                   dst_left.data_ptr(), dst_right.data_ptr(), flags.data_ptr(), n_items, 1, *pl, st),
             "tree_part_scatter")
     return new_order, nleft
 
@@ -132,7 +147,32 @@ def leaf_apply(order: torch.Tensor, seg_lo: torch.Tensor, seg_hi: torch.Tensor, 
             "tree_leaf_apply")
 
 
-def partition_torch(bins, order, s_lo, s_hi, s_feat, s_bin):
+_KINDS = {"variance": 0, "gini": 1, "entropy": 2}
+
+
+def best_splits(H: torch.Tensor, nb: torch.Tensor, fmask, kind: str, min_inst: float, min_w: float,
+                min_wfrac: float) -> torch.Tensor:
+    """Per-node best split of histograms H [k, F, B, S] (fp64, GPU) in ONE launch of
+    ``tree_split_kernel``.  Returns the fp64 bundle [idx | gain | impurity | weight |
+    wL | wR | values (k x V)] (V = S for classification, 1 for variance).
+
+    ``fmask`` (numpy bool [k, F] or None): features each node may split on (forests);
+    ``min_wfrac`` > 0: the minimum child weight is that fraction of the node's weight
+    (the root level), else ``min_w``."""
+    k, F, B, S = H.shape
+    dev = H.device
+    Hc = H.to(torch.float64).contiguous()
+    nb32 = nb.to(dev, torch.int32).contiguous()
+    fm = None if fmask is None else torch.from_numpy(np.ascontiguousarray(fmask, dtype=np.uint8)).to(dev)
+    V = 1 if kind == "variance" else S
+    out = torch.empty(6 * k + k * V, dtype=torch.float64, device=dev)
+    N.check(N.kernels().o3s_tree_split(Hc.data_ptr(), k, F, B, S, _KINDS[kind], nb32.data_ptr(), N.ptr(fm),
+                                       float(min_inst), float(min_w), float(min_wfrac), out.data_ptr(),
+                                       N.stream_of(Hc)), "tree_split")
+    return out
+
+
+def partition_torch(bins, order, s_lo, s_hi, s_feat, s_bin, out=None, payload=(), payload_out=()):
     dev = bins.device
     F = bins.shape[1]
     lens = s_hi - s_lo
@@ -146,22 +186,27 @@ def partition_torch(bins, order, s_lo, s_hi, s_feat, s_bin):
     gl = go_left.to(torch.int64)
     cl = torch.cumsum(gl, 0)
     nleft = torch.zeros(s_lo.numel(), dtype=torch.int64, device=dev).index_add_(0, sid, gl)
+    new_order = order.clone() if out is None else out
     if total == 0:
-        return order.clone(), nleft
+        return new_order, nleft
     cl_before = cl[first.clamp_max(total - 1)] - gl[first.clamp_max(total - 1)]
     lrank = cl - cl_before[sid]                            # inclusive rank among lefts
     rel = torch.arange(total, device=dev) - first[sid]
     rrank = rel + 1 - lrank
     newpos = torch.where(go_left, s_lo[sid] + lrank - 1, s_lo[sid] + nleft[sid] + rrank - 1)
-    new_order = order.clone()
     new_order[newpos] = order[pos]
+    for a, b in zip(payload, payload_out):
+        b[newpos] = a[pos]
     return new_order, nleft
 
 
 def node_hist(bins: torch.Tensor, order: torch.Tensor, y: torch.Tensor, w: torch.Tensor | None,
               seg_lo: torch.Tensor, seg_hi: torch.Tensor, seg_node: torch.Tensor, n_nodes: int, B: int, S: int,
-              cls: bool, chunk: int = 1 << 13) -> torch.Tensor:
+              cls: bool, chunk: int = 1 << 13, ypos: bool = False) -> torch.Tensor:
     """Histograms [n_nodes, F, B, S] (fp64) of rows order[lo:hi] for each segment -> node.
+
+    ``ypos``: y / w are in position order (y[p] is the label of row order[p], kept so
+    by moving them through ``partition(payload=...)``): they stream contiguously.
 
     Classification: per-bin weighted class counts.  Regression (S = 3): per-bin sums of
     w and w*y; the node's sum of w*y^2 sits in (feature 0, bin 0, stat 2) -- variance
@@ -181,7 +226,7 @@ def node_hist(bins: torch.Tensor, order: torch.Tensor, y: torch.Tensor, w: torch
     if not hist_kernel_ok(bins, B, S, cls):
         # reference path (CPU / oversize bins): direct scatter-add per segment
         return hist_torch(bins, order, y, w, _dev(seg_lo, dev), _dev(seg_hi, dev), _dev(seg_node, dev), n_nodes,
-                          B, S, cls)
+                          B, S, cls, ypos=ypos)
     plan = _HistPlan(seg_lo, seg_hi, seg_node, chunk, dev)
     if plan.n_items == 0:
         return out.view(n_nodes, F, B, S)
@@ -193,7 +238,7 @@ def node_hist(bins: torch.Tensor, order: torch.Tensor, y: torch.Tensor, w: torch
     st = N.stream_of(bins)
     N.check(lib.o3s_tree_hist(bins.data_ptr(), bins.shape[0], F, B, S, int(cls), order.data_ptr(), yf.data_ptr(),
                               N.ptr(wf), plan.it_lo.data_ptr(), plan.it_hi.data_ptr(), plan.n_items,
-                              slab.data_ptr(), st), "tree_hist")
+                              slab.data_ptr(), int(bool(ypos)), st), "tree_hist")
     # ordered fp64 sums: runs of <= 64 item rows, then each segment's runs in order
     runs = torch.empty((plan.n_runs, C), dtype=torch.float64, device=dev)
     for a in range(0, plan.n_runs, 65535):
@@ -246,7 +291,7 @@ class _HistPlan:
         self.it_lo, self.it_hi, self.r_lo, self.r_cnt, self.s_run0, self.s_nrun, self.seg_node = views
 
 
-def hist_torch(bins, order, y, w, seg_lo, seg_hi, seg_node, n_nodes, B, S, cls):
+def hist_torch(bins, order, y, w, seg_lo, seg_hi, seg_node, n_nodes, B, S, cls, ypos=False):
     F = bins.shape[1]
     dev = bins.device
     out = torch.zeros(n_nodes * F * B * S, dtype=torch.float64, device=dev)
@@ -257,8 +302,9 @@ def hist_torch(bins, order, y, w, seg_lo, seg_hi, seg_node, n_nodes, B, S, cls):
     node = torch.repeat_interleave(seg_node.to(dev), lens)
     rows = order[pos].long()
     bb = bins[rows].long()                                  # [m, F]
-    yy = y[rows].to(torch.float64)
-    ww = torch.ones_like(yy) if w is None else w[rows].to(torch.float64)
+    at = pos if ypos else rows
+    yy = y[at].to(torch.float64)
+    ww = torch.ones_like(yy) if w is None else w[at].to(torch.float64)
     fidx = torch.arange(F, device=dev)[None, :]
     base = ((node[:, None] * F + fidx) * B + bb) * S        # [m, F]
     if cls:

@@ -84,6 +84,13 @@ def test_gpu_hist_matches_torch(gpu, F, B, S, cls):
     a = T.node_hist(bins, order, y, w, lo, hi, nd, 3, B, S, cls, chunk=50_000)
     b = T.hist_torch(bins, order, y, w, lo, hi, nd, 3, B, S, cls)
     assert torch.allclose(a, b, rtol=1e-4, atol=1e-2)
+    # position-ordered labels / weights (ypos): same histogram
+    for ww in (w, None):
+        ol = order.long()
+        c = T.node_hist(bins, order, y[ol].contiguous(), None if ww is None else ww[ol].contiguous(), lo, hi, nd, 3,
+                        B, S, cls, chunk=50_000, ypos=True)
+        d = T.node_hist(bins, order, y, ww, lo, hi, nd, 3, B, S, cls, chunk=50_000)
+        assert torch.equal(c, d)
 
 
 @pytest.mark.gpu
@@ -113,6 +120,22 @@ def test_gpu_partition_matches_torch(gpu, feature_major):
                                s_bin.to(gpu), chunk=4096, bins_t=T.feature_major(bg) if feature_major else None)
     assert torch.equal(got_n.cpu(), ref_n)
     assert torch.equal(got_o.cpu(), ref_o)                             # stable -> identical permutation
+    # payloads in position order move with their rows; positions outside the split
+    # segments of the output buffers are left alone
+    yv = torch.randn(n, generator=g)
+    wv = torch.rand(n, generator=g)
+    yp, wp = yv[order.long()].contiguous(), wv[order.long()].contiguous()
+    outs = [torch.full((n,), -7.0, device=gpu) for _ in range(2)]
+    o2 = torch.full((n,), -1, dtype=torch.int32, device=gpu)
+    sub = slice(1, 4)                                                  # split only segments 1..3
+    T.partition(bg, order.to(gpu), s_lo[sub].to(gpu), s_hi[sub].to(gpu), s_feat[sub].to(gpu), s_bin[sub].to(gpu),
+                chunk=4096, out=o2, payload=(yp.to(gpu), wp.to(gpu)), payload_out=outs)
+    o2c = o2.cpu()
+    inside = torch.zeros(n, dtype=torch.bool)
+    inside[int(s_lo[1]):int(s_hi[3])] = True
+    assert bool((o2c[~inside] == -1).all()) and bool((outs[0].cpu()[~inside] == -7.0).all())
+    rows = o2c[inside].long()
+    assert torch.equal(outs[0].cpu()[inside], yv[rows]) and torch.equal(outs[1].cpu()[inside], wv[rows])
 
 
 @pytest.mark.parametrize("cls_model", ["dt_cls", "gbt_reg", "rf_cls"])
@@ -260,3 +283,51 @@ def test_min_weight_fraction_per_node(cpu):
     assert frac.numNodes < deep.numNodes
     with pytest.raises(ValueError):
         DecisionTreeClassifier(minWeightFractionPerNode=0.6).fit(df)
+
+
+def test_partition_payload_torch():
+    """CPU reference: payloads (position order) follow their rows through a partition."""
+    from orange3_spark_amd.ops import trees as T
+    g = torch.Generator().manual_seed(3)
+    n, F = 1000, 5
+    bins = torch.randint(0, 8, (n, F), generator=g, dtype=torch.uint8)
+    order = torch.randperm(n, generator=g).to(torch.int32)
+    yv = torch.randn(n, generator=g)
+    yp = yv[order.long()].contiguous()
+    lo, hi = torch.tensor([0, 400]), torch.tensor([400, n])
+    out_y = yp.clone()
+    new, _ = T.partition(bins, order, lo, hi, torch.tensor([1, 3]), torch.tensor([2, 5]), payload=(yp,),
+                         payload_out=(out_y,))
+    assert torch.equal(out_y, yv[new.long()])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,S", [("variance", 3), ("gini", 2), ("entropy", 5), ("gini", 12)])
+def test_gpu_split_kernel_matches_torch(gpu, kind, S):
+    """tree_split_kernel (one fused launch per level) == the torch split search."""
+    from orange3_spark_amd.models.trees import _split_bundle_torch
+    from orange3_spark_amd.ops import trees as T
+    g = torch.Generator().manual_seed(S)
+    k, F, B = 37, 20, 16
+    H = torch.rand((k, F, B, S), generator=g, dtype=torch.float64) * 50
+    if kind == "variance":
+        H[..., 1] = torch.randn((k, F, B), generator=g, dtype=torch.float64) * 20
+        H[..., 2] = 0.0
+        H[:, 0, 0, 2] = 1e4
+        H[:, 1:, :, :2] = H[:, :1, :, :2].expand(-1, F - 1, -1, -1)[:, :, torch.randperm(B, generator=g)]
+    else:                                                             # every feature sees the node's rows
+        H[:, 1:] = H[:, :1].expand(-1, F - 1, -1, -1)[:, :, torch.randperm(B, generator=g)]
+    H[3] = 0.0                                                        # an empty node
+    nb = torch.randint(1, B, (F,), generator=g)
+    fm = (torch.rand((k, F), generator=g) < 0.5).numpy()
+    bin_ids = torch.arange(B - 1)
+    for fmask, mi, mw, mwf in ((None, 1.0, 0.0, 0.0), (fm, 30.0, 0.0, 0.0), (fm, 1.0, 0.0, 0.2), (None, 1.0, 90.0, 0.0)):
+        ref = _split_bundle_torch(H, kind, kind != "variance", nb, bin_ids, fmask, mi, mw, mwf)
+        got = T.best_splits(H.to(gpu), nb.to(gpu), fmask, kind, mi, mw, mwf).cpu()
+        fin = torch.isfinite(ref[k:2 * k])
+        assert torch.equal(fin, torch.isfinite(got[k:2 * k]))
+        assert torch.equal(ref[:k][fin], got[:k][fin])                # same split (no exact ties here)
+        torch.testing.assert_close(got[k:2 * k][fin], ref[k:2 * k][fin], rtol=1e-9, atol=1e-12)
+        torch.testing.assert_close(got[2 * k:4 * k], ref[2 * k:4 * k], rtol=1e-12, atol=1e-12)
+        torch.testing.assert_close(got[4 * k:6 * k][fin.repeat(2)], ref[4 * k:6 * k][fin.repeat(2)])
+        torch.testing.assert_close(got[6 * k:], ref[6 * k:], rtol=1e-12, atol=1e-12)
