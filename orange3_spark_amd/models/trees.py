@@ -239,11 +239,13 @@ class TreeBuilder:
     def __init__(self, comm, bins: torch.Tensor, splits: list, y: torch.Tensor, w: torch.Tensor | None,
                  impurity: str, num_classes: int, max_depth: int = 5, min_instances: float = 1.0,
                  min_info_gain: float = 0.0, feature_fraction: float = 1.0, seed: int = 0,
-                 max_bins: int = 32, bins_t: torch.Tensor | None = None, min_weight_fraction: float = 0.0):
+                 max_bins: int = 32, bins_t: torch.Tensor | None = None, min_weight_fraction: float = 0.0,
+                 own_y: bool = False):
         self.comm, self.bins, self.splits = comm, bins, splits
         self.min_wfrac = float(min_weight_fraction)      # Spark minWeightFractionPerNode
         self.bins_t = bins_t if bins_t is not None else T.feature_major(bins)
         self.y, self.w = y, w
+        self.own_y = own_y               # y is a scratch fp32 buffer the build may overwrite
         self.kind = impurity
         self.cls = impurity in ("gini", "entropy")
         self.S = num_classes if self.cls else 3
@@ -276,7 +278,9 @@ class TreeBuilder:
         # labels / weights travel with the rows in POSITION order (yp[p] belongs to row
         # order[p]): the histogram kernel streams them instead of gathering a cache line
         # per row; order starts as the identity, so the initial copies are plain clones
-        yp = self.y.to(torch.float32).contiguous().clone()
+        yp = self.y.to(torch.float32).contiguous()
+        if not (self.own_y and yp is self.y):
+            yp = yp.clone()
         wp = None if self.w is None else self.w.to(torch.float32).contiguous().clone()
         y_sp = torch.empty_like(yp) if spare is not None else None
         w_sp = torch.empty_like(wp) if (spare is not None and wp is not None) else None
@@ -435,14 +439,6 @@ def subsample_weights(n_local, rows: torch.Tensor, rate: float, seed: int, boots
     return None
 
 
-def _gbt_point_loss(loss: str, yy: torch.Tensor, Fm: torch.Tensor) -> torch.Tensor:
-    if loss == "logistic":
-        return 2.0 * torch.log1p(torch.exp(-2.0 * yy * Fm))
-    if loss == "squared":
-        return (yy - Fm) ** 2
-    return (yy - Fm).abs()
-
-
 def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_iter: int = 20,
             step: float = 0.1, max_depth: int = 5, min_instances: float = 1.0, min_info_gain: float = 0.0,
             subsampling_rate: float = 1.0, seed: int = 0, feature_fraction: float = 1.0, rows=None,
@@ -461,50 +457,41 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
     yy = y.to(torch.float64)
     if classification:
         yy = 2.0 * yy - 1.0
-    wd = torch.ones_like(yy) if w is None else w.to(torch.float64)
+    wd = None if w is None else w.to(torch.float64)           # None: unit training weights
+    w_val = None
     if validation is not None:
         vmask = validation.to(dev, torch.bool)
-        w_val = torch.where(vmask, wd, torch.zeros_like(wd))
-        wd = torch.where(vmask, torch.zeros_like(wd), wd)
+        wd0 = torch.ones_like(yy) if wd is None else wd
+        w_val = torch.where(vmask, wd0, torch.zeros_like(wd0))
+        wd = torch.where(vmask, torch.zeros_like(wd0), wd0)
         w = wd.float()
     Fm = torch.zeros_like(yy)
     trees, weights, losses = [], [], []
     best_err, best_m = math.inf, 0
+    target = yy.to(torch.float32)                            # tree 0 fits the (scaled) labels
     for m in range(max_iter):
-        tg = trace("gbt.grad")
-        tg.__enter__()
-        if m == 0:
-            target = yy
-        elif loss == "logistic":
-            target = 4.0 * yy / (1.0 + torch.exp(2.0 * yy * Fm))
-        elif loss == "squared":
-            target = 2.0 * (yy - Fm)
-        else:  # absolute
-            target = torch.sign(yy - Fm)
-        tg.__exit__(None, None, None)
         sw = w
         if subsampling_rate < 1.0 and rows is not None:
             sub = subsample_weights(None, rows, subsampling_rate, seed + m, False)
             sw = sub if w is None else w * sub
-        tb = TreeBuilder(comm, bins, splits, target.float(), sw, "variance", 1, max_depth, min_instances,
+        tb = TreeBuilder(comm, bins, splits, target, sw, "variance", 1, max_depth, min_instances,
                          min_info_gain, feature_fraction, seed + m, bins_t=bins_t,
-                         min_weight_fraction=min_weight_fraction)
+                         min_weight_fraction=min_weight_fraction, own_y=True)
         wt = 1.0 if m == 0 else step
         tree, _ = tb.build(leaf_acc=Fm, leaf_scale=wt)          # Fm += wt * leaf value, per row
         tu = trace("gbt.update")
         tu.__enter__()
         trees.append(tree)
         weights.append(wt)
-        pl = _gbt_point_loss(loss, yy, Fm)
-        parts = [(pl * wd).sum().reshape(1), wd.sum().reshape(1)]
-        if validation is not None:
-            parts += [(pl * w_val).sum().reshape(1), w_val.sum().reshape(1)]
-        buf = torch.cat(parts)
+        # one fused pass: this iteration's (validation) loss and the next tree's residuals
+        target = torch.empty_like(target) if m + 1 < max_iter else None
+        buf = T.gbt_grad_loss(loss, yy, Fm, wd, w_val, target)
         comm.all_reduce(buf)
-        losses.append(float(buf[0] / buf[1].clamp_min(1e-300)))
+        sums = buf.cpu().numpy()
+        losses.append(float(sums[0] / max(sums[1], 1e-300)))
         tu.__exit__(None, None, None)
         if validation is not None:
-            err = float(buf[2] / buf[3].clamp_min(1e-300))
+            err = float(sums[2] / max(sums[3], 1e-300))
             if m == 0:
                 best_err, best_m = err, 1
             elif best_err - err < validation_tol * max(err, 0.01):

@@ -20,6 +20,8 @@
 // CLS (S = #classes: weighted class counts -- gini/entropy).
 #include "common.h"
 
+#include <cstdlib>
+
 
 using namespace o3s;
 
@@ -41,7 +43,7 @@ constexpr int kHistThreads = kHistWaves * kWave;
 // YP: y / w are stored in POSITION order (y[p] belongs to row order[p]; the partition
 // moves them with the rows), so they stream contiguously instead of costing one random
 // cache-line gather each per row -- only the 64-B bins row is gathered.
-template <int FP, bool CLS, bool HW, bool YP, int U>
+template <int FP, bool CLS, bool HW, bool YP, int U, int GRP>
 __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
     const uint8_t* __restrict__ bins, int F, int fg0, int B, int S, const int32_t* __restrict__ order,
     const float* __restrict__ y, const float* __restrict__ w, const int64_t* __restrict__ item_lo,
@@ -53,7 +55,8 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
   const int rs = lane / FP, f = lane % FP;
-  const int region = B * SL * FP + 16;                            // +16: rs-regions on distinct banks
+  // B + 1 bin rows: row B is the trash row of the grouped updates (FP = 64 path)
+  const int region = (B + 1) * SL * FP + 16;                      // +16: rs-regions on distinct banks
   const int per_wave = RS * region;
   float* my = hist + wid * per_wave + rs * region;
   for (int i = threadIdx.x; i < kHistWaves * per_wave; i += kHistThreads) hist[i] = 0.f;
@@ -98,19 +101,53 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
       wv = HW ? (YP ? wl[jc] : w[ov]) : 1.f;
       wv = j < nl ? wv : 0.f;
     };
+    // Rows are accumulated in groups of GRP: a lane's cells for the rows of a group are
+    // made distinct first (a row whose cell repeats an earlier one's adds its stats into
+    // that row's and is redirected to the trash bin row B with zero stats), so the GRP
+    // read-modify-writes are independent: GRP LDS reads in flight, one wait, GRP writes,
+    // instead of one LDS round trip per row.
+    const int trash = B * SL * FP;
     auto acc_chunk = [&](const int (&bo)[CH], float yv, float wv) {
 #pragma unroll
-      for (int q = 0; q < CH; ++q) {
-        const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), q));
-        const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), q));
-        float* cell = my + bo[q] * SL * FP + f;
-        if (CLS) {
-          cell[(int)yq * FP] += wq;
-        } else {
-          const float wy = wq * yq;
-          cell[0] += wq;
-          cell[FP] += wy;
-          wy2 = fmaf(wy, yq, wy2);
+      for (int q0 = 0; q0 < CH; q0 += GRP) {
+        int off[GRP];
+        float a0[GRP], a1[GRP];
+#pragma unroll
+        for (int g = 0; g < GRP; ++g) {
+          const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), q0 + g));
+          const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), q0 + g));
+          a0[g] = wq;
+          if (CLS) {
+            off[g] = (bo[q0 + g] * SL + (int)yq) * FP;
+            a1[g] = 0.f;
+          } else {
+            off[g] = bo[q0 + g] * SL * FP;
+            a1[g] = wq * yq;
+            wy2 = fmaf(a1[g], yq, wy2);
+          }
+        }
+#pragma unroll
+        for (int g = 1; g < GRP; ++g) {
+#pragma unroll
+          for (int p = 0; p < g; ++p) {
+            const bool m = off[g] == off[p];
+            a0[p] += m ? a0[g] : 0.f;
+            if (!CLS) a1[p] += m ? a1[g] : 0.f;
+            off[g] = m ? trash : off[g];
+            a0[g] = m ? 0.f : a0[g];
+            if (!CLS) a1[g] = m ? 0.f : a1[g];
+          }
+        }
+        float v0[GRP], v1[GRP];
+#pragma unroll
+        for (int g = 0; g < GRP; ++g) {
+          v0[g] = my[off[g] + f];
+          if (!CLS) v1[g] = my[off[g] + FP + f];
+        }
+#pragma unroll
+        for (int g = 0; g < GRP; ++g) {
+          my[off[g] + f] = v0[g] + a0[g];
+          if (!CLS) my[off[g] + FP + f] = v1[g] + a1[g];
         }
       }
     };
@@ -544,6 +581,58 @@ __global__ __launch_bounds__(kSplitThreads) void tree_split_kernel(
     out[6 * k + (int64_t)node * V + v] = CLS ? tot[v] / W : tot[1] / W;
 }
 
+// ---------------------------------------------------------------------------------
+// Boosting step epilogue, fused (Spark GradientBoostedTrees: after tree m the training
+// (and validation) loss of F_m, and the pseudo-residuals of tree m+1): ONE pass over
+// (y, F, w) instead of ~15 elementwise / reduction launches.  loss 0 = logistic
+// (y in {-1, +1}: loss 2*log(1 + e^{-2yF}), computed stably; residual 4y / (1 + e^{2yF})),
+// 1 = squared ((y-F)^2; 2(y-F)), 2 = absolute (|y-F|; sign(y-F)).  Per-block partial
+// sums [sum loss*w, sum w, sum loss*wv, sum wv] (fp64; fixed grid and fixed-order block
+// reduction, so reproducible); target (fp32, may be null) gets the residuals.
+constexpr int kGbtThreads = 256;
+__global__ __launch_bounds__(kGbtThreads) void gbt_grad_loss_kernel(
+    const double* __restrict__ y, const double* __restrict__ F, const double* __restrict__ w,
+    const double* __restrict__ wv, int64_t n, int loss, float* __restrict__ target, double* __restrict__ partial) {
+  __shared__ double red[4][kGbtThreads / kWave];
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * kGbtThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kGbtThreads + threadIdx.x; i < n; i += stride) {
+    const double yi = y[i], fi = F[i];
+    double l, g;
+    if (loss == 0) {
+      const double z = -2.0 * yi * fi;                             // log(1 + e^z), stably
+      l = 2.0 * (z > 0.0 ? z + log1p(exp(-z)) : log1p(exp(z)));
+      g = 4.0 * yi / (1.0 + exp(-z));
+    } else if (loss == 1) {
+      const double d = yi - fi;
+      l = d * d;
+      g = 2.0 * d;
+    } else {
+      const double d = yi - fi;
+      l = fabs(d);
+      g = (double)((d > 0.0) - (d < 0.0));
+    }
+    const double wi = w ? w[i] : 1.0;
+    s0 += l * wi;
+    s1 += wi;
+    if (wv) {
+      const double vi = wv[i];
+      s2 += l * vi;
+      s3 += vi;
+    }
+    if (target) target[i] = (float)g;
+  }
+  s0 = wave_sum_d(s0); s1 = wave_sum_d(s1); s2 = wave_sum_d(s2); s3 = wave_sum_d(s3);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { red[0][wid] = s0; red[1][wid] = s1; red[2][wid] = s2; red[3][wid] = s3; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double a = 0.0;
+    for (int q = 0; q < kGbtThreads / kWave; ++q) a += red[threadIdx.x][q];
+    partial[(int64_t)blockIdx.x * 4 + threadIdx.x] = a;
+  }
+}
+
 }  // namespace
 
 // acc[order[p]] += it_val[i] for p in [it_lo[i], it_hi[i]) (items of leaf segments).
@@ -616,7 +705,7 @@ O3S_API int o3s_tree_partition(const uint8_t* bins, int64_t rs, int64_t cs, cons
 O3S_API int o3s_tree_hist_lds(int fp, int B, int S, int cls) {
   const int RS = 64 / fp;
   const int SL = cls ? S : 2;
-  const int64_t bytes = (int64_t)kHistWaves * RS * (B * SL * fp + 16) * 4;
+  const int64_t bytes = (int64_t)kHistWaves * RS * ((B + 1) * SL * fp + 16) * 4;
   return bytes <= 160 * 1024 ? (int)bytes : 0;
 }
 
@@ -633,10 +722,14 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
   const int lds = o3s_tree_hist_lds(fp, B, S, cls);
   if (lds == 0) return -2;
   const int64_t stride = (int64_t)F * B * S;
+  static const int hist_g = getenv("O3S_HIST_G") ? atoi(getenv("O3S_HIST_G")) : 1;
   for (int fg0 = 0; fg0 < F; fg0 += fp) {
+#define O3S_TH4(FPV, C, W, P, UU, GG)                                                                   \
+  hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, UU, GG>), dim3(n_items), dim3(kHistThreads), lds, st,    \
+                     bins, F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
 #define O3S_TH3(FPV, C, W, P, UU)                                                                       \
-  hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, UU>), dim3(n_items), dim3(kHistThreads), lds, st, bins,  \
-                     F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
+  if (hist_g == 4) { O3S_TH4(FPV, C, W, P, UU, 4) } else if (hist_g == 2) { O3S_TH4(FPV, C, W, P, UU, 2) } \
+  else { O3S_TH4(FPV, C, W, P, UU, 1) }
 #define O3S_TH2(FPV, C, W, P) O3S_TH3(FPV, C, W, P, 8)
 #define O3S_TH1(FPV, C, W)                                                                              \
   if (ypos) { O3S_TH2(FPV, C, W, true) } else { O3S_TH2(FPV, C, W, false) }
@@ -652,6 +745,7 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
 #undef O3S_TH1
 #undef O3S_TH2
 #undef O3S_TH3
+#undef O3S_TH4
     O3S_CHECK_LAUNCH();
   }
   (void)n;
@@ -677,6 +771,18 @@ O3S_API int o3s_tree_split(const double* H, int k, int F, int B, int S, int kind
   else
     hipLaunchKernelGGL((tree_split_kernel<true, kSplitMaxS>), dim3(k), dim3(kSplitThreads), 0, st, H, k, F, B, S,
                        kind, nb, fmask, min_inst, min_w, min_wfrac, out);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+// y, F, w, wv: fp64 [n] (w / wv may be null: unit training weights / no validation);
+// target: fp32 [n] or null; partial: fp64 [n_blocks][4].
+O3S_API int o3s_gbt_grad_loss(const double* y, const double* F, const double* w, const double* wv, int64_t n,
+                              int loss, float* target, double* partial, int n_blocks, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (loss < 0 || loss > 2 || n_blocks <= 0) return -1;
+  hipLaunchKernelGGL(gbt_grad_loss_kernel, dim3(n_blocks), dim3(kGbtThreads), 0, st, y, F, w, wv, n, loss, target,
+                     partial);
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -148,6 +148,55 @@ def leaf_apply(order: torch.Tensor, seg_lo: torch.Tensor, seg_hi: torch.Tensor, 
 
 
 _KINDS = {"variance": 0, "gini": 1, "entropy": 2}
+_GBT_LOSS = {"logistic": 0, "squared": 1, "absolute": 2}
+
+
+def gbt_point_loss(loss: str, yy: torch.Tensor, Fm: torch.Tensor) -> torch.Tensor:
+    """Spark GBT per-row loss (logistic: 2*log(1 + e^{-2yF}), evaluated stably)."""
+    if loss == "logistic":
+        z = -2.0 * yy * Fm
+        return 2.0 * torch.where(z > 0, z + torch.log1p(torch.exp(-z)), torch.log1p(torch.exp(z)))
+    if loss == "squared":
+        return (yy - Fm) ** 2
+    return (yy - Fm).abs()
+
+
+def gbt_residual(loss: str, yy: torch.Tensor, Fm: torch.Tensor) -> torch.Tensor:
+    """Pseudo-residuals (negative loss gradients) the next tree is fit to."""
+    if loss == "logistic":
+        return 4.0 * yy / (1.0 + torch.exp(2.0 * yy * Fm))
+    if loss == "squared":
+        return 2.0 * (yy - Fm)
+    return torch.sign(yy - Fm)
+
+
+def gbt_grad_loss(loss: str, yy: torch.Tensor, Fm: torch.Tensor, w: torch.Tensor | None, w_val: torch.Tensor | None,
+                  target: torch.Tensor | None = None) -> torch.Tensor:
+    """One boosting epilogue pass: returns fp64 [sum loss*w, sum w, sum loss*w_val,
+    sum w_val] over the local rows and (``target`` given, fp32) writes the residuals of
+    the next tree into it.  GPU: ``gbt_grad_loss_kernel`` (one fused pass, fixed-grid
+    partial sums); CPU: the torch reference."""
+    n = yy.shape[0]
+    dev = yy.device
+    if yy.is_cuda and n > 0:
+        f64 = [None if t is None else t.to(torch.float64).contiguous() for t in (yy, Fm, w, w_val)]
+        nb = int(min(2048, max(1, (n + 255) // 256)))
+        part = torch.empty((nb, 4), dtype=torch.float64, device=dev)
+        if target is not None and (target.dtype != torch.float32 or target.numel() != n or not target.is_contiguous()):
+            raise ValueError("target must be a contiguous fp32 [n] tensor")
+        N.check(N.kernels().o3s_gbt_grad_loss(*(N.ptr(t) for t in f64), n, _GBT_LOSS[loss], N.ptr(target),
+                                              part.data_ptr(), nb, N.stream_of(yy)), "gbt_grad_loss")
+        return part.sum(0)
+    pl = gbt_point_loss(loss, yy.double(), Fm.double())
+    wt = torch.ones_like(pl) if w is None else w.double()
+    out = [(pl * wt).sum(), wt.sum()]
+    if w_val is not None:
+        out += [(pl * w_val.double()).sum(), w_val.double().sum()]
+    else:
+        out += [torch.zeros((), dtype=torch.float64, device=dev)] * 2
+    if target is not None:
+        target.copy_(gbt_residual(loss, yy.double(), Fm.double()))
+    return torch.stack(out)
 
 
 def best_splits(H: torch.Tensor, nb: torch.Tensor, fmask, kind: str, min_inst: float, min_w: float,

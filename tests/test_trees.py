@@ -331,3 +331,26 @@ def test_gpu_split_kernel_matches_torch(gpu, kind, S):
         torch.testing.assert_close(got[2 * k:4 * k], ref[2 * k:4 * k], rtol=1e-12, atol=1e-12)
         torch.testing.assert_close(got[4 * k:6 * k][fin.repeat(2)], ref[4 * k:6 * k][fin.repeat(2)])
         torch.testing.assert_close(got[6 * k:], ref[6 * k:], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("loss", ["logistic", "squared", "absolute"])
+def test_gpu_gbt_grad_loss_matches_torch(gpu, loss):
+    """gbt_grad_loss_kernel (fused loss sums + residuals) == the torch reference."""
+    from orange3_spark_amd.ops import trees as T
+    g = torch.Generator().manual_seed(7)
+    n = 1_000_003
+    yy = (torch.randint(0, 2, (n,), generator=g).double() * 2 - 1) if loss == "logistic" else \
+        torch.randn(n, generator=g, dtype=torch.float64)
+    Fm = torch.randn(n, generator=g, dtype=torch.float64) * 30            # large margins: stable loss needed
+    w = torch.rand(n, generator=g, dtype=torch.float64)
+    wv = torch.where(torch.rand(n, generator=g) < 0.2, w, torch.zeros_like(w))
+    for ww, vv in ((None, None), (w, wv)):
+        t_ref = torch.empty(n, dtype=torch.float32)
+        ref = T.gbt_grad_loss(loss, yy, Fm, ww, vv, t_ref)
+        t_got = torch.empty(n, dtype=torch.float32, device=gpu)
+        got = T.gbt_grad_loss(loss, yy.to(gpu), Fm.to(gpu), None if ww is None else ww.to(gpu),
+                              None if vv is None else vv.to(gpu), t_got).cpu()
+        assert torch.isfinite(got).all()
+        torch.testing.assert_close(got, ref, rtol=1e-10, atol=1e-8)
+        torch.testing.assert_close(t_got.cpu(), t_ref, rtol=1e-6, atol=1e-6)
