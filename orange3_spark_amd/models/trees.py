@@ -318,7 +318,7 @@ class TreeBuilder:
                                      np.arange(P), P, B, S, self.cls, ypos=True)
                     Hs = Hs.to(torch.float64).contiguous()
                     self.comm.all_reduce(Hs)
-                    pick = torch.from_numpy(pick_h).to(dev)
+                    pick = N.upload(pick_h, dev)
                     H = torch.empty((k, F, B, S), dtype=torch.float64, device=dev)
                     H[pick] = Hs
                     H[pick ^ 1] = _sibling(parent_H, Hs, self.cls)
@@ -373,7 +373,7 @@ class TreeBuilder:
                     T.leaf_apply(order, seg_lo[~do_split], seg_hi[~do_split],
                                  value[node_ids[~do_split], 0] * leaf_scale, leaf_acc)
             s_lo, s_hi, s_node = seg_lo[do_split], seg_hi[do_split], seg_node[do_split]
-            parent_H = H[torch.from_numpy(do_split).to(dev)]
+            parent_H = H[N.upload(do_split, dev)]
             small_right = (wr_np < wl_np)[do_split]
             pay = (yp,) if wp is None else (yp, wp)
             if spare is not None:                                 # ping-pong: no full copy

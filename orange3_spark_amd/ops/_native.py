@@ -147,6 +147,22 @@ def ptr(t: torch.Tensor | None) -> int | None:
     return t.data_ptr()
 
 
+def upload(arr, dev) -> torch.Tensor:
+    """Host array -> device tensor WITHOUT stalling the host: staged through (cached)
+    pinned memory and copied non_blocking on the current stream.  A pageable copy
+    blocks the host until the stream has drained, so every small plan upload of a
+    launch-bound loop (tree levels) would leave the GPU idle while Python catches up;
+    PyTorch's caching host allocator keeps the pinned block alive until the copy ran."""
+    import numpy as np
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    dev = torch.device(dev)
+    if dev.type != "cuda":
+        return t.to(dev)
+    p = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    p.copy_(t)
+    return p.to(dev, non_blocking=True)
+
+
 def stream_of(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 

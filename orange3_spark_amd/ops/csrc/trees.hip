@@ -20,8 +20,6 @@
 // CLS (S = #classes: weighted class counts -- gini/entropy).
 #include "common.h"
 
-#include <cstdlib>
-
 
 using namespace o3s;
 
@@ -43,7 +41,7 @@ constexpr int kHistThreads = kHistWaves * kWave;
 // YP: y / w are stored in POSITION order (y[p] belongs to row order[p]; the partition
 // moves them with the rows), so they stream contiguously instead of costing one random
 // cache-line gather each per row -- only the 64-B bins row is gathered.
-template <int FP, bool CLS, bool HW, bool YP, int U, int GRP>
+template <int FP, bool CLS, bool HW, bool YP, int U>
 __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
     const uint8_t* __restrict__ bins, int F, int fg0, int B, int S, const int32_t* __restrict__ order,
     const float* __restrict__ y, const float* __restrict__ w, const int64_t* __restrict__ item_lo,
@@ -55,8 +53,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
   const int rs = lane / FP, f = lane % FP;
-  // B + 1 bin rows: row B is the trash row of the grouped updates (FP = 64 path)
-  const int region = (B + 1) * SL * FP + 16;                      // +16: rs-regions on distinct banks
+  const int region = B * SL * FP + 16;                            // +16: rs-regions on distinct banks
   const int per_wave = RS * region;
   float* my = hist + wid * per_wave + rs * region;
   for (int i = threadIdx.x; i < kHistWaves * per_wave; i += kHistThreads) hist[i] = 0.f;
@@ -101,53 +98,21 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
       wv = HW ? (YP ? wl[jc] : w[ov]) : 1.f;
       wv = j < nl ? wv : 0.f;
     };
-    // Rows are accumulated in groups of GRP: a lane's cells for the rows of a group are
-    // made distinct first (a row whose cell repeats an earlier one's adds its stats into
-    // that row's and is redirected to the trash bin row B with zero stats), so the GRP
-    // read-modify-writes are independent: GRP LDS reads in flight, one wait, GRP writes,
-    // instead of one LDS round trip per row.
-    const int trash = B * SL * FP;
+    // (Grouping rows so several LDS read-modify-writes share one wait -- duplicates
+    // merged first -- measured slower: the extra VALU outweighs the LDS round trips.)
     auto acc_chunk = [&](const int (&bo)[CH], float yv, float wv) {
 #pragma unroll
-      for (int q0 = 0; q0 < CH; q0 += GRP) {
-        int off[GRP];
-        float a0[GRP], a1[GRP];
-#pragma unroll
-        for (int g = 0; g < GRP; ++g) {
-          const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), q0 + g));
-          const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), q0 + g));
-          a0[g] = wq;
-          if (CLS) {
-            off[g] = (bo[q0 + g] * SL + (int)yq) * FP;
-            a1[g] = 0.f;
-          } else {
-            off[g] = bo[q0 + g] * SL * FP;
-            a1[g] = wq * yq;
-            wy2 = fmaf(a1[g], yq, wy2);
-          }
-        }
-#pragma unroll
-        for (int g = 1; g < GRP; ++g) {
-#pragma unroll
-          for (int p = 0; p < g; ++p) {
-            const bool m = off[g] == off[p];
-            a0[p] += m ? a0[g] : 0.f;
-            if (!CLS) a1[p] += m ? a1[g] : 0.f;
-            off[g] = m ? trash : off[g];
-            a0[g] = m ? 0.f : a0[g];
-            if (!CLS) a1[g] = m ? 0.f : a1[g];
-          }
-        }
-        float v0[GRP], v1[GRP];
-#pragma unroll
-        for (int g = 0; g < GRP; ++g) {
-          v0[g] = my[off[g] + f];
-          if (!CLS) v1[g] = my[off[g] + FP + f];
-        }
-#pragma unroll
-        for (int g = 0; g < GRP; ++g) {
-          my[off[g] + f] = v0[g] + a0[g];
-          if (!CLS) my[off[g] + FP + f] = v1[g] + a1[g];
+      for (int q = 0; q < CH; ++q) {
+        const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), q));
+        const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), q));
+        float* cell = my + bo[q] * SL * FP + f;
+        if (CLS) {
+          cell[(int)yq * FP] += wq;
+        } else {
+          const float wy = wq * yq;
+          cell[0] += wq;
+          cell[FP] += wy;
+          wy2 = fmaf(wy, yq, wy2);
         }
       }
     };
@@ -705,7 +670,7 @@ O3S_API int o3s_tree_partition(const uint8_t* bins, int64_t rs, int64_t cs, cons
 O3S_API int o3s_tree_hist_lds(int fp, int B, int S, int cls) {
   const int RS = 64 / fp;
   const int SL = cls ? S : 2;
-  const int64_t bytes = (int64_t)kHistWaves * RS * ((B + 1) * SL * fp + 16) * 4;
+  const int64_t bytes = (int64_t)kHistWaves * RS * (B * SL * fp + 16) * 4;
   return bytes <= 160 * 1024 ? (int)bytes : 0;
 }
 
@@ -722,15 +687,10 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
   const int lds = o3s_tree_hist_lds(fp, B, S, cls);
   if (lds == 0) return -2;
   const int64_t stride = (int64_t)F * B * S;
-  static const int hist_g = getenv("O3S_HIST_G") ? atoi(getenv("O3S_HIST_G")) : 1;
   for (int fg0 = 0; fg0 < F; fg0 += fp) {
-#define O3S_TH4(FPV, C, W, P, UU, GG)                                                                   \
-  hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, UU, GG>), dim3(n_items), dim3(kHistThreads), lds, st,    \
-                     bins, F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
-#define O3S_TH3(FPV, C, W, P, UU)                                                                       \
-  if (hist_g == 4) { O3S_TH4(FPV, C, W, P, UU, 4) } else if (hist_g == 2) { O3S_TH4(FPV, C, W, P, UU, 2) } \
-  else { O3S_TH4(FPV, C, W, P, UU, 1) }
-#define O3S_TH2(FPV, C, W, P) O3S_TH3(FPV, C, W, P, 8)
+#define O3S_TH2(FPV, C, W, P)                                                                           \
+  hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, 8>), dim3(n_items), dim3(kHistThreads), lds, st, bins,   \
+                     F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
 #define O3S_TH1(FPV, C, W)                                                                              \
   if (ypos) { O3S_TH2(FPV, C, W, true) } else { O3S_TH2(FPV, C, W, false) }
 #define O3S_TH(FPV)                                                                                     \
@@ -744,8 +704,6 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
 #undef O3S_TH
 #undef O3S_TH1
 #undef O3S_TH2
-#undef O3S_TH3
-#undef O3S_TH4
     O3S_CHECK_LAUNCH();
   }
   (void)n;

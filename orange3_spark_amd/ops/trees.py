@@ -16,7 +16,7 @@ def _host(x):
 
 
 def _dev(x, dev):
-    return x.to(dev) if isinstance(x, torch.Tensor) else torch.from_numpy(_host(x)).to(dev)
+    return x.to(dev) if isinstance(x, torch.Tensor) else N.upload(_host(x), dev)
 
 
 def hist_kernel_ok(bins: torch.Tensor, B: int, S: int, cls: bool) -> bool:
@@ -80,10 +80,10 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     seg_of = np.repeat(np.arange(nseg), n_it)
     it_lo_h = lo[seg_of] + (np.arange(n_items) - first[seg_of]) * chunk
     it_hi_h = np.minimum(it_lo_h + chunk, hi[seg_of])
-    i64 = torch.from_numpy(np.concatenate([it_lo_h, it_hi_h, seg_of, first[seg_of], lo[seg_of]])).to(dev)
+    i64 = N.upload(np.concatenate([it_lo_h, it_hi_h, seg_of, first[seg_of], lo[seg_of]]), dev)
     it_lo, it_hi, it_seg, f, seg_lo_it = (i64[k * n_items:(k + 1) * n_items] for k in range(5))
     fb = np.concatenate([_host(s_feat).astype(np.int32)[seg_of], _host(s_bin).astype(np.int32)[seg_of]])
-    i32 = torch.from_numpy(fb).to(dev)
+    i32 = N.upload(fb, dev)
     it_feat, it_bin = i32[:n_items], i32[n_items:]
     it_left = torch.empty(n_items, dtype=torch.int64, device=dev)
     flags = torch.empty(order.shape[0], dtype=torch.uint8, device=dev)
@@ -140,8 +140,8 @@ def leaf_apply(order: torch.Tensor, seg_lo: torch.Tensor, seg_hi: torch.Tensor, 
     seg_of = np.repeat(np.arange(len(lo)), n_it)
     it_lo = lo[seg_of] + (np.arange(n_items) - first[seg_of]) * chunk
     it_hi = np.minimum(it_lo + chunk, hi[seg_of])
-    i64 = torch.from_numpy(np.concatenate([it_lo, it_hi])).to(dev)
-    fv = torch.from_numpy(np.ascontiguousarray(val[seg_of])).to(dev)
+    i64 = N.upload(np.concatenate([it_lo, it_hi]), dev)
+    fv = N.upload(val[seg_of], dev)
     N.check(N.kernels().o3s_tree_leaf_apply(order.data_ptr(), i64[:n_items].data_ptr(), i64[n_items:].data_ptr(),
                                             fv.data_ptr(), n_items, acc.data_ptr(), N.stream_of(acc)),
             "tree_leaf_apply")
@@ -212,7 +212,7 @@ def best_splits(H: torch.Tensor, nb: torch.Tensor, fmask, kind: str, min_inst: f
     dev = H.device
     Hc = H.to(torch.float64).contiguous()
     nb32 = nb.to(dev, torch.int32).contiguous()
-    fm = None if fmask is None else torch.from_numpy(np.ascontiguousarray(fmask, dtype=np.uint8)).to(dev)
+    fm = None if fmask is None else N.upload(np.asarray(fmask, dtype=np.uint8), dev)
     V = 1 if kind == "variance" else S
     out = torch.empty(6 * k + k * V, dtype=torch.float64, device=dev)
     N.check(N.kernels().o3s_tree_split(Hc.data_ptr(), k, F, B, S, _KINDS[kind], nb32.data_ptr(), N.ptr(fm),
@@ -332,7 +332,7 @@ class _HistPlan:
         r_lo = first[rseg] + kr * _RUN
         r_cnt = np.minimum(_RUN, first[rseg] + n_it[rseg] - r_lo)
         parts = [it_lo, it_hi, r_lo, r_cnt, run0, n_run, nd]
-        buf = torch.from_numpy(np.concatenate(parts).astype(np.int64)).to(dev, non_blocking=False)
+        buf = N.upload(np.concatenate(parts).astype(np.int64), dev)
         views, off = [], 0
         for p in parts:
             views.append(buf[off: off + len(p)])
