@@ -125,7 +125,7 @@ def _impurity(stats: torch.Tensor, kind: str) -> tuple[torch.Tensor, torch.Tenso
     return torch.where(w > 0, imp, torch.zeros_like(imp)), w
 
 
-def _split_bundle_torch(H, kind, cls, nb, bin_ids, fm, min_inst, min_w, min_wfrac):
+def _split_bundle_torch(H, kind, cls, nb, bin_ids, fm, min_inst, min_w, min_wfrac, min_w_node=None):
     """Reference of ``tree_split_kernel``: the per-node decision bundle (fp64
     [idx | gain | impurity | weight | wL | wR | values]) from histograms [k, F, B, S]."""
     k = H.shape[0]
@@ -149,7 +149,10 @@ def _split_bundle_torch(H, kind, cls, nb, bin_ids, fm, min_inst, min_w, min_wfra
         sP = tot[:, 1][:, None, None]
         g = (sL * sL / wL.clamp_min(1e-300) + sR * sR / wR.clamp_min(1e-300) - sP * sP / W) / W
     ok = (wL >= min_inst) & (wR >= min_inst)
-    mw = (min_wfrac * w_p)[:, None, None] if min_wfrac > 0.0 else torch.full_like(W, min_w)
+    if min_w_node is not None:
+        mw = torch.as_tensor(np.asarray(min_w_node, dtype=np.float64), device=dev)[:, None, None]
+    else:
+        mw = (min_wfrac * w_p)[:, None, None] if min_wfrac > 0.0 else torch.full_like(W, min_w)
     ok &= (mw <= 0.0) | ((wL >= mw) & (wR >= mw))
     ok &= bin_ids[None, None, :] < nb[None, :, None]
     if fm is not None:
@@ -232,79 +235,123 @@ class Tree:
 
 
 class TreeBuilder:
-    """Grows one tree over this rank's binned rows (collectives keep ranks in lockstep)."""
+    """Grows trees over this rank's binned rows (collectives keep ranks in lockstep).
+
+    Several trees grow TOGETHER (random forests: one tree per entry of ``w`` when it is a
+    list of per-tree weight vectors, e.g. bootstrap counts): every tree owns a block of
+    the position space ([t*n, (t+1)*n) of one row permutation, with its labels and
+    weights moved alongside), so each level is ONE histogram launch, ONE all-reduce, ONE
+    split launch and ONE partition for all trees -- Spark's "several trees per pass"
+    (RandomForest.run groups nodes of all trees into one aggregation), without the
+    per-tree launch and synchronisation overhead."""
 
     hist_subtraction = True         # False: scan every node at every level (reference path)
+    batch_trees = True              # False: forests grow one tree at a time (reference path)
 
-    def __init__(self, comm, bins: torch.Tensor, splits: list, y: torch.Tensor, w: torch.Tensor | None,
+    def __init__(self, comm, bins: torch.Tensor, splits: list, y: torch.Tensor, w,
                  impurity: str, num_classes: int, max_depth: int = 5, min_instances: float = 1.0,
-                 min_info_gain: float = 0.0, feature_fraction: float = 1.0, seed: int = 0,
+                 min_info_gain: float = 0.0, feature_fraction: float = 1.0, seed=0,
                  max_bins: int = 32, bins_t: torch.Tensor | None = None, min_weight_fraction: float = 0.0,
                  own_y: bool = False):
         self.comm, self.bins, self.splits = comm, bins, splits
         self.min_wfrac = float(min_weight_fraction)      # Spark minWeightFractionPerNode
         self.bins_t = bins_t if bins_t is not None else T.feature_major(bins)
-        self.y, self.w = y, w
+        self.y = y
+        self.ws = list(w) if isinstance(w, (list, tuple)) else [w]
+        self.seeds = list(seed) if isinstance(seed, (list, tuple)) else [seed] * len(self.ws)
+        if len(self.seeds) != len(self.ws):
+            raise ValueError("one seed per tree")
         self.own_y = own_y               # y is a scratch fp32 buffer the build may overwrite
         self.kind = impurity
         self.cls = impurity in ("gini", "entropy")
         self.S = num_classes if self.cls else 3
         self.B = max(2, max(len(s) for s in splits) + 1) if splits else 2
         self.max_depth, self.min_inst, self.min_gain = max_depth, min_instances, min_info_gain
-        self.ffrac, self.seed = feature_fraction, seed
+        self.ffrac = feature_fraction
         self.F = bins.shape[1]
 
     def build(self, leaf_acc: torch.Tensor | None = None, leaf_scale: float = 1.0):
-        """Grow the tree.  Returns (tree, leaf_row): leaf_row = per-row leaf node ids.
+        """Grow the (single) tree.  Returns (tree, None).
 
-        ``leaf_acc`` (fp64 [n], boosting): instead of materialising leaf_row, every segment
-        adds ``leaf_scale * value(leaf)`` to leaf_acc[row] of its rows the moment it becomes
-        a leaf (``tree_leaf_apply_kernel``), and the row permutation ping-pongs between two
-        buffers (rows of finished leaves are never needed again, so no full copy per
-        level); leaf_row is then None."""
+        ``leaf_acc`` (fp64 [n], boosting): every segment adds ``leaf_scale * value(leaf)``
+        to leaf_acc[row] of its rows the moment it becomes a leaf
+        (``tree_leaf_apply_kernel``)."""
+        if len(self.ws) != 1:
+            raise ValueError("build() grows one tree; use build_many()")
+        return self._grow(leaf_acc, leaf_scale)[0], None
+
+    def build_many(self) -> list:
+        """Grow one tree per weight vector, in batches that keep positions in int32 and
+        the per-batch row permutations within a quarter of free device memory."""
+        n = max(1, self.bins.shape[0])
+        tb = max(1, min(len(self.ws), (2 ** 31 - 1) // n))
+        if self.bins.is_cuda:
+            free, _ = torch.cuda.mem_get_info(self.bins.device)
+            tb = max(1, min(tb, int(0.25 * free) // (26 * n)))
+        trees, ws, seeds = [], self.ws, self.seeds
+        for a in range(0, len(ws), tb):
+            self.ws, self.seeds = ws[a:a + tb], seeds[a:a + tb]
+            try:
+                trees += self._grow(None, 1.0)
+            finally:
+                self.ws, self.seeds = ws, seeds
+        return trees
+
+    def _grow(self, leaf_acc, leaf_scale):
         dev = self.bins.device
         n = self.bins.shape[0]
+        Tn = len(self.ws)
         F, B, S = self.F, self.B, self.S
+        V = S if self.cls else 1
         max_nodes = 2 ** (self.max_depth + 1)
-        feature = -np.ones(max_nodes, dtype=np.int64)
-        threshold = np.zeros(max_nodes)
-        split_bin = np.zeros(max_nodes, dtype=np.int64)
-        value = np.zeros((max_nodes, S if self.cls else 1))
-        impurity = np.zeros(max_nodes)
-        gain = np.zeros(max_nodes)
-        count = np.zeros(max_nodes)
+        feature = -np.ones((Tn, max_nodes), dtype=np.int64)
+        threshold = np.zeros((Tn, max_nodes))
+        split_bin = np.zeros((Tn, max_nodes), dtype=np.int64)
+        value = np.zeros((Tn, max_nodes, V))
+        impurity = np.zeros((Tn, max_nodes))
+        gain = np.zeros((Tn, max_nodes))
+        count = np.zeros((Tn, max_nodes))
+        # one row permutation per tree, tree t at positions [t*n, (t+1)*n); labels and
+        # weights travel with the rows in POSITION order (yp[p] belongs to row order[p]),
+        # so the histogram kernel streams them instead of gathering a line per row
         order = torch.arange(n, dtype=torch.int32, device=dev)
-        spare = torch.empty_like(order) if (leaf_acc is not None and order.is_cuda) else None
-        # labels / weights travel with the rows in POSITION order (yp[p] belongs to row
-        # order[p]): the histogram kernel streams them instead of gathering a cache line
-        # per row; order starts as the identity, so the initial copies are plain clones
+        if Tn > 1:
+            order = order.repeat(Tn)
         yp = self.y.to(torch.float32).contiguous()
-        if not (self.own_y and yp is self.y):
+        if Tn > 1:
+            yp = yp.repeat(Tn)
+        elif not (self.own_y and yp is self.y):
             yp = yp.clone()
-        wp = None if self.w is None else self.w.to(torch.float32).contiguous().clone()
-        y_sp = torch.empty_like(yp) if spare is not None else None
-        w_sp = torch.empty_like(wp) if (spare is not None and wp is not None) else None
+        if all(w_ is None for w_ in self.ws):
+            wp = None
+        else:
+            wp = torch.cat([torch.ones(n, dtype=torch.float32, device=dev) if w_ is None
+                            else w_.to(dev, torch.float32).reshape(-1) for w_ in self.ws]).contiguous()
+        # ping-pong buffers on the GPU: rows of finished leaves are never read again, so a
+        # partition writes only the split segments into the spare buffers (no full copy)
+        pingpong = order.is_cuda
+        spare = torch.empty_like(order) if pingpong else None
+        y_sp = torch.empty_like(yp) if pingpong else None
+        w_sp = torch.empty_like(wp) if (pingpong and wp is not None) else None
         # segment bounds live on the HOST (a few hundred int64s): per level there are two
         # device->host copies (the split decisions, then the left counts of the partition)
-        # and the work-item plans are uploaded right after them, while the GPU is idle
-        seg_lo = np.zeros(1, dtype=np.int64)
-        seg_hi = np.full(1, n, dtype=np.int64)
-        seg_node = np.ones(1, dtype=np.int64)
-        leaf_segments = []
-        rng = np.random.default_rng(self.seed)
+        seg_lo = np.arange(Tn, dtype=np.int64) * n
+        seg_hi = seg_lo + n
+        seg_tree = np.arange(Tn, dtype=np.int64)
+        seg_nid = np.ones(Tn, dtype=np.int64)
+        rngs = [np.random.default_rng(sd) for sd in self.seeds]
         nb = torch.tensor([len(s_) for s_ in self.splits], device=dev)
         bin_ids = torch.arange(B - 1, device=dev)
-        V = S if self.cls else 1
+        root_w = np.zeros(Tn)
         # histogram subtraction: below the root only the globally smaller child of each
         # split is scanned; its sibling is parent - smaller (histograms are additive), which
         # at least halves the rows the hist kernel touches per level and the all-reduce size
         parent_H = None                                           # [P, F, B, S] fp64, global
         small_right = None                                        # [P] bool (host): right child smaller
         for depth in range(self.max_depth + 1):
-            k = len(seg_node)
+            k = len(seg_nid)
             if k == 0:
                 break
-            node_ids = seg_node
             with trace("tree.hist"):
                 if parent_H is None or not self.hist_subtraction:
                     H = T.node_hist(self.bins, order, yp, wp, seg_lo, seg_hi, np.arange(k), k, B, S, self.cls,
@@ -328,55 +375,50 @@ class TreeBuilder:
             if self.ffrac < 1.0:
                 m = max(1, int(math.ceil(self.ffrac * F)))
                 fm = np.zeros((k, F), dtype=bool)
-                for i in range(k):
-                    fm[i, rng.choice(F, m, replace=False)] = True
+                for i in range(k):                                # each tree draws from its own stream
+                    fm[i, rngs[seg_tree[i]].choice(F, m, replace=False)] = True
             # min child weight: at the root a fraction of its total weight (Spark
-            # minWeightFractionPerNode), below it the absolute value that gave
+            # minWeightFractionPerNode), below it the absolute value that gave, per tree
             mw_frac = self.min_wfrac if depth == 0 else 0.0
-            mw_abs = getattr(self, "min_w", 0.0)
+            mw_node = (self.min_wfrac * root_w[seg_tree]) if (depth > 0 and self.min_wfrac > 0.0) else None
             if H.is_cuda:
-                bundle_t = T.best_splits(H, nb, fm, self.kind, self.min_inst, mw_abs, mw_frac)
+                bundle_t = T.best_splits(H, nb, fm, self.kind, self.min_inst, 0.0, mw_frac, mw_node)
             else:
-                bundle_t = _split_bundle_torch(H, self.kind, self.cls, nb, bin_ids, fm, self.min_inst, mw_abs,
-                                               mw_frac)
+                bundle_t = _split_bundle_torch(H, self.kind, self.cls, nb, bin_ids, fm, self.min_inst, 0.0,
+                                               mw_frac, mw_node)
             # ONE device->host copy of every per-node decision input
             bundle = bundle_t.cpu().numpy()
             bi = bundle[:k].astype(np.int64)
             bg, imp_np, w_np, wl_np, wr_np = (bundle[q * k:(q + 1) * k] for q in range(1, 6))
             vals_np = bundle[6 * k:].reshape(k, V)
-            if depth == 0 and self.min_wfrac > 0.0:
-                self.min_w = self.min_wfrac * float(w_np[0])      # fraction of the root's total weight
+            if depth == 0:
+                root_w = w_np.copy()
             bf, bb = bi // (B - 1), bi % (B - 1)
-            value[node_ids] = vals_np
-            impurity[node_ids] = imp_np
-            count[node_ids] = w_np
+            value[seg_tree, seg_nid] = vals_np
+            impurity[seg_tree, seg_nid] = imp_np
+            count[seg_tree, seg_nid] = w_np
             do_split = (bg > self.min_gain) & (bg > 0) & np.isfinite(bg) & (depth < self.max_depth)
             tsplit.__exit__(None, None, None)
+            if leaf_acc is not None and not do_split.all():
+                with trace("tree.leaf_apply"):
+                    lf = ~do_split
+                    T.leaf_apply(order, seg_lo[lf], seg_hi[lf], value[seg_tree[lf], seg_nid[lf], 0] * leaf_scale,
+                                 leaf_acc)
             if not do_split.any():
-                leaf_segments.append((seg_lo, seg_hi, seg_node))
-                if leaf_acc is not None:
-                    with trace("tree.leaf_apply"):
-                        T.leaf_apply(order, seg_lo, seg_hi, value[node_ids, 0] * leaf_scale, leaf_acc)
                 break
             tpart = trace("tree.partition")
             tpart.__enter__()
-            for i, nid in enumerate(node_ids):
-                if do_split[i]:
-                    feature[nid] = bf[i]
-                    split_bin[nid] = bb[i]
-                    threshold[nid] = float(self.splits[bf[i]][bb[i]])
-                    gain[nid] = bg[i]
+            st, sn = seg_tree[do_split], seg_nid[do_split]
+            feature[st, sn] = bf[do_split]
+            split_bin[st, sn] = bb[do_split]
+            threshold[st, sn] = [float(self.splits[f_][b_]) for f_, b_ in zip(bf[do_split], bb[do_split])]
+            gain[st, sn] = bg[do_split]
             # --- partition the splitting segments
-            leaf_segments.append((seg_lo[~do_split], seg_hi[~do_split], seg_node[~do_split]))
-            if leaf_acc is not None and not do_split.all():
-                with trace("tree.leaf_apply"):
-                    T.leaf_apply(order, seg_lo[~do_split], seg_hi[~do_split],
-                                 value[node_ids[~do_split], 0] * leaf_scale, leaf_acc)
-            s_lo, s_hi, s_node = seg_lo[do_split], seg_hi[do_split], seg_node[do_split]
+            s_lo, s_hi = seg_lo[do_split], seg_hi[do_split]
             parent_H = H[N.upload(do_split, dev)]
             small_right = (wr_np < wl_np)[do_split]
             pay = (yp,) if wp is None else (yp, wp)
-            if spare is not None:                                 # ping-pong: no full copy
+            if pingpong:
                 pout = (y_sp,) if wp is None else (y_sp, w_sp)
                 new_order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
                                                bins_t=self.bins_t, out=spare, payload=pay, payload_out=pout)
@@ -391,34 +433,12 @@ class TreeBuilder:
             mid = s_lo + nleft.cpu().numpy().astype(np.int64)
             seg_lo = np.stack([s_lo, mid], 1).reshape(-1)
             seg_hi = np.stack([mid, s_hi], 1).reshape(-1)
-            seg_node = np.stack([2 * s_node, 2 * s_node + 1], 1).reshape(-1)
+            seg_tree = np.repeat(st, 2)
+            seg_nid = np.stack([2 * sn, 2 * sn + 1], 1).reshape(-1)
             tpart.__exit__(None, None, None)
             # empty local segments still participate (other ranks may have rows there)
-        tree = Tree(feature, threshold, split_bin, value, impurity, gain, count, F)
-        if leaf_acc is not None:
-            return tree, None
-        with trace("tree.leaf_rows"):
-            leaf_row = self._leaf_rows(n, order, leaf_segments)
-        return tree, leaf_row
-
-    @staticmethod
-    def _leaf_rows(n, order, leaf_segments):
-        """per-row leaf ids of the training rows (for boosting updates), no traversal needed"""
-        dev = order.device
-        leaf_row = torch.empty(n, dtype=torch.int64, device=dev)
-        for lo, hi, nd in leaf_segments:
-            if len(lo) == 0:
-                continue
-            lo, hi, nd = (torch.from_numpy(np.asarray(a, dtype=np.int64)).to(dev) for a in (lo, hi, nd))
-            lens = (hi - lo)
-            tot_ = int(lens.sum())
-            if tot_ == 0:
-                continue
-            sid = torch.repeat_interleave(torch.arange(lo.numel(), device=dev), lens)
-            first = torch.cumsum(lens, 0) - lens
-            pos = lo[sid] + (torch.arange(tot_, device=dev) - first[sid])
-            leaf_row[order[pos].long()] = nd[sid]
-        return leaf_row
+        return [Tree(feature[t], threshold[t], split_bin[t], value[t], impurity[t], gain[t], count[t], F)
+                for t in range(Tn)]
 
 
 # ----------------------------------------------------------------------------- ensembles
@@ -506,17 +526,21 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
 def fit_forest(comm, bins, splits, y, w, num_trees: int, impurity: str, num_classes: int, max_depth: int,
                min_instances: float, min_info_gain: float, subsampling_rate: float, feature_fraction: float,
                seed: int, rows: torch.Tensor, bootstrap: bool, min_weight_fraction: float = 0.0) -> Ensemble:
-    trees = []
-    bins_t = T.feature_major(bins)
+    """Random forest: every tree's bootstrap (Poisson) or subsample weights, then all
+    trees grown together level by level (``TreeBuilder.build_many``)."""
+    ws = []
     for t in range(num_trees):
         sw = subsample_weights(None, rows, subsampling_rate, seed * 7919 + t, bootstrap)
         if w is not None:
             sw = w if sw is None else w * sw
-        tb = TreeBuilder(comm, bins, splits, y, sw, impurity, num_classes, max_depth, min_instances,
-                         min_info_gain, feature_fraction, seed + 31 * t, bins_t=bins_t,
-                         min_weight_fraction=min_weight_fraction)
-        tree, _ = tb.build()
-        trees.append(tree)
+        ws.append(sw)
+    tb = TreeBuilder(comm, bins, splits, y, ws, impurity, num_classes, max_depth, min_instances,
+                     min_info_gain, feature_fraction, [seed + 31 * t for t in range(num_trees)],
+                     bins_t=T.feature_major(bins), min_weight_fraction=min_weight_fraction)
+    trees = tb.build_many() if TreeBuilder.batch_trees else \
+        [TreeBuilder(comm, bins, splits, y, ws[t], impurity, num_classes, max_depth, min_instances,
+                     min_info_gain, feature_fraction, seed + 31 * t, bins_t=tb.bins_t,
+                     min_weight_fraction=min_weight_fraction).build()[0] for t in range(num_trees)]
     return Ensemble(trees, [1.0] * num_trees, "rf", num_classes)
 
 

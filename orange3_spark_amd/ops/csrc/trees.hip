@@ -465,7 +465,8 @@ __device__ __forceinline__ double split_imp(const double* st, int S, int kind, d
 template <bool CLS, int SM>
 __global__ __launch_bounds__(kSplitThreads) void tree_split_kernel(
     const double* __restrict__ H, int k, int F, int B, int S, int kind, const int32_t* __restrict__ nb,
-    const uint8_t* __restrict__ fmask, double min_inst, double min_w, double min_wfrac, double* __restrict__ out) {
+    const uint8_t* __restrict__ fmask, double min_inst, double min_w, double min_wfrac,
+    const double* __restrict__ mw_node, double* __restrict__ out) {
   __shared__ double tot[kSplitMaxS];
   __shared__ double rg[kSplitThreads], rwl[kSplitThreads], rwr[kSplitThreads];
   __shared__ int ri[kSplitThreads];
@@ -488,7 +489,9 @@ __global__ __launch_bounds__(kSplitThreads) void tree_split_kernel(
     imp_p = w_p > 0.0 ? (v > 0.0 ? v : 0.0) : 0.0;
   }
   const double W = w_p > 1e-300 ? w_p : 1e-300;
-  const double mw = min_wfrac > 0.0 ? min_wfrac * w_p : min_w;   // depth 0: fraction of the root weight
+  // minimum child weight: per node (forests: each tree's own root fraction), else a
+  // fraction of this node's weight (the root level), else one value
+  const double mw = mw_node ? mw_node[node] : (min_wfrac > 0.0 ? min_wfrac * w_p : min_w);
   double bg = -INFINITY, bwl = 0.0, bwr = 0.0;
   int bi = 0x7fffffff;
   double left[SM], right[SM];
@@ -712,23 +715,23 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
 
 // H: [k][F][B][S] fp64 node histograms; nb[F]: valid thresholds per feature; fmask
 // [k][F] (uint8, null = all features); kind 0 = variance (S == 3), 1 = gini, 2 = entropy.
-// min_wfrac > 0 (root level): the minimum child weight is that fraction of the node's
-// weight, else min_w.  out: fp64 [6k + k*V] (see tree_split_kernel).
+// mw_node (fp64 [k], nullable): per-node minimum child weight; else min_wfrac > 0 (root
+// level): that fraction of the node's weight; else min_w.  out: fp64 [6k + k*V] (see tree_split_kernel).
 O3S_API int o3s_tree_split(const double* H, int k, int F, int B, int S, int kind, const int32_t* nb,
-                           const uint8_t* fmask, double min_inst, double min_w, double min_wfrac, double* out,
-                           hipStream_t st) {
+                           const uint8_t* fmask, double min_inst, double min_w, double min_wfrac,
+                           const double* mw_node, double* out, hipStream_t st) {
   if (k <= 0) return 0;
   if (F <= 0 || B < 2 || S <= 0 || S > kSplitMaxS || kind < 0 || kind > 2) return -1;
   if (kind == 0 && S != 3) return -1;
   if (kind == 0)
     hipLaunchKernelGGL((tree_split_kernel<false, 3>), dim3(k), dim3(kSplitThreads), 0, st, H, k, F, B, S, kind, nb,
-                       fmask, min_inst, min_w, min_wfrac, out);
+                       fmask, min_inst, min_w, min_wfrac, mw_node, out);
   else if (S <= 8)
     hipLaunchKernelGGL((tree_split_kernel<true, 8>), dim3(k), dim3(kSplitThreads), 0, st, H, k, F, B, S, kind, nb,
-                       fmask, min_inst, min_w, min_wfrac, out);
+                       fmask, min_inst, min_w, min_wfrac, mw_node, out);
   else
     hipLaunchKernelGGL((tree_split_kernel<true, kSplitMaxS>), dim3(k), dim3(kSplitThreads), 0, st, H, k, F, B, S,
-                       kind, nb, fmask, min_inst, min_w, min_wfrac, out);
+                       kind, nb, fmask, min_inst, min_w, min_wfrac, mw_node, out);
   O3S_CHECK_LAUNCH();
   return 0;
 }

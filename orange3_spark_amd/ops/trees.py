@@ -200,23 +200,25 @@ def gbt_grad_loss(loss: str, yy: torch.Tensor, Fm: torch.Tensor, w: torch.Tensor
 
 
 def best_splits(H: torch.Tensor, nb: torch.Tensor, fmask, kind: str, min_inst: float, min_w: float,
-                min_wfrac: float) -> torch.Tensor:
+                min_wfrac: float, min_w_node=None) -> torch.Tensor:
     """Per-node best split of histograms H [k, F, B, S] (fp64, GPU) in ONE launch of
     ``tree_split_kernel``.  Returns the fp64 bundle [idx | gain | impurity | weight |
     wL | wR | values (k x V)] (V = S for classification, 1 for variance).
 
     ``fmask`` (numpy bool [k, F] or None): features each node may split on (forests);
     ``min_wfrac`` > 0: the minimum child weight is that fraction of the node's weight
-    (the root level), else ``min_w``."""
+    (the root level), else ``min_w``; ``min_w_node`` (numpy [k]) overrides both per node."""
     k, F, B, S = H.shape
     dev = H.device
     Hc = H.to(torch.float64).contiguous()
     nb32 = nb.to(dev, torch.int32).contiguous()
     fm = None if fmask is None else N.upload(np.asarray(fmask, dtype=np.uint8), dev)
     V = 1 if kind == "variance" else S
+    mwn = None if min_w_node is None else N.upload(np.asarray(min_w_node, dtype=np.float64), dev)
     out = torch.empty(6 * k + k * V, dtype=torch.float64, device=dev)
     N.check(N.kernels().o3s_tree_split(Hc.data_ptr(), k, F, B, S, _KINDS[kind], nb32.data_ptr(), N.ptr(fm),
-                                       float(min_inst), float(min_w), float(min_wfrac), out.data_ptr(),
+                                       float(min_inst), float(min_w), float(min_wfrac),
+                                       N.ptr(mwn), out.data_ptr(),
                                        N.stream_of(Hc)), "tree_split")
     return out
 

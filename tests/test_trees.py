@@ -354,3 +354,35 @@ def test_gpu_gbt_grad_loss_matches_torch(gpu, loss):
         assert torch.isfinite(got).all()
         torch.testing.assert_close(got, ref, rtol=1e-10, atol=1e-8)
         torch.testing.assert_close(t_got.cpu(), t_ref, rtol=1e-6, atol=1e-6)
+
+
+def _forest_batched_vs_sequential(session, dev_name):
+    from orange3_spark_amd.models.trees import TreeBuilder
+    rng = np.random.default_rng(9)
+    X = rng.uniform(-1, 1, size=(4000, 7))
+    y = ((X[:, 0] > 0.2) ^ (X[:, 3] > -0.1)).astype(float) + (X[:, 5] > 0.6)
+    df = session.createDataFrame(pd.DataFrame({"features": list(X), "label": y}))
+    outs = []
+    for flag in (True, False):
+        TreeBuilder.batch_trees = flag
+        try:
+            m = RandomForestClassifier(numTrees=6, maxDepth=5, seed=3, subsamplingRate=0.8,
+                                       minWeightFractionPerNode=0.01).fit(df)
+            outs.append((m.transform(df).toPandas()["probability"].map(lambda v: v.toArray()).tolist(),
+                         [t.numNodes for t in m.trees]))
+        finally:
+            TreeBuilder.batch_trees = True
+    np.testing.assert_allclose(np.array(outs[0][0]), np.array(outs[1][0]), rtol=1e-9, atol=1e-12)
+    assert outs[0][1] == outs[1][1]
+
+
+def test_forest_batched_equals_sequential(cpu):
+    """Growing all trees of a forest together (one launch per level) builds the same
+    trees as growing them one at a time (bootstrap, feature subsets, min weight fraction)."""
+    _forest_batched_vs_sequential(cpu, "cpu")
+
+
+@pytest.mark.gpu
+def test_gpu_forest_batched_equals_sequential():
+    s = Session(SessionConf().set("o3s.device", "cuda"))
+    _forest_batched_vs_sequential(s, "cuda")
