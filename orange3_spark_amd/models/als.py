@@ -74,12 +74,15 @@ def partition(comm, rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, 
 
 def init_factors(n_lo: int, n: int, rank: int, seed: int, device, nonneg: bool) -> torch.Tensor:
     """Unit-norm gaussian rows keyed on (seed, global index): partition invariant."""
-    idx = torch.arange(n_lo, n_lo + n, dtype=torch.int64, device=device)
     out = torch.empty((n, rank), dtype=torch.float32, device=device)
-    for k in range(rank):
-        u1 = sampling.uniform(idx, seed, stream=2 * k + 11).clamp_min(1e-12)
-        u2 = sampling.uniform(idx, seed, stream=2 * k + 12)
-        out[:, k] = (torch.sqrt(-2 * torch.log(u1)) * torch.cos(2 * math.pi * u2)).float()
+    s1 = [2 * k + 11 for k in range(rank)]
+    s2 = [2 * k + 12 for k in range(rank)]
+    step = max(1, (1 << 25) // max(rank, 1))                 # bounded int64 temporaries
+    for a in range(0, n, step):
+        idx = torch.arange(n_lo + a, n_lo + min(n, a + step), dtype=torch.int64, device=device)
+        u1 = sampling.uniform_streams(idx, seed, s1).clamp_min(1e-12)
+        u2 = sampling.uniform_streams(idx, seed, s2)
+        out[a:a + idx.numel()] = (torch.sqrt(-2 * torch.log(u1)) * torch.cos(2 * math.pi * u2)).float()
     out /= out.norm(dim=1, keepdim=True).clamp_min(1e-12)
     return out.abs() if nonneg else out
 

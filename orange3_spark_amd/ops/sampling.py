@@ -24,6 +24,19 @@ def uniform(rows: torch.Tensor, seed: int, stream: int = 0) -> torch.Tensor:
     return (hi * 67108864.0 + lo) * (1.0 / 9007199254740992.0)
 
 
+def uniform_streams(rows: torch.Tensor, seed: int, streams) -> torch.Tensor:
+    """[n, k] U[0,1) float64: column j equals ``uniform(rows, seed, streams[j])`` bitwise,
+    computed in one broadcast pass (the per-row half of the key is hashed once)."""
+    st = torch.as_tensor(list(streams), dtype=torch.int64, device=rows.device)
+    seeds = ((seed * 0x2545F491 + st * 0x9E3779B9) & _MASK)[None, :]
+    lo = rows & _MASK
+    hi = rows >> 32
+    inner = _fmix32((lo * 0x9E3779B1 + hi * 0x7FEB352D + 0x165667B1) & _MASK)[:, None]
+    k = _fmix32(seeds ^ inner)
+    k2 = _fmix32(k ^ 0x68E31DA4)
+    return ((k >> 5).to(torch.float64) * 67108864.0 + (k2 >> 6).to(torch.float64)) * (1.0 / 9007199254740992.0)
+
+
 def bernoulli_mask(rows: torch.Tensor, seed: int, fraction: float) -> torch.Tensor:
     if fraction >= 1.0:
         return torch.ones_like(rows, dtype=torch.bool)
