@@ -314,6 +314,57 @@ __global__ __launch_bounds__(kPartThreads) void tree_part_scatter_kernel(
   }
 }
 
+// Destinations of the level partition's scatter: per segment (one block each), the
+// exclusive prefix of its items' left counts gives each item's first left slot and the
+// prefix of the right counts (after the segment's nleft lefts) its first right slot.
+// Replaces a dozen small device ops per level (cumsums, gathers, index_add).
+__device__ __forceinline__ int64_t block_incl_scan_i64(int64_t v, int64_t* wtot, int64_t& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t t = __shfl_up(v, off, 64);
+    if (lane >= off) v += t;
+  }
+  if (lane == 63) wtot[wid] = v;
+  __syncthreads();
+  int64_t before = 0;
+  total = 0;
+#pragma unroll
+  for (int q = 0; q < kPartWaves; ++q) {
+    before += q < wid ? wtot[q] : 0;
+    total += wtot[q];
+  }
+  __syncthreads();                                               // wtot reused by the next call
+  return v + before;
+}
+
+__global__ __launch_bounds__(kPartThreads) void tree_part_dest_kernel(
+    const int64_t* __restrict__ it_lo, const int64_t* __restrict__ it_hi, const int64_t* __restrict__ it_left,
+    const int64_t* __restrict__ seg_first, const int64_t* __restrict__ seg_lo, int64_t* __restrict__ dst_left,
+    int64_t* __restrict__ dst_right, int64_t* __restrict__ nleft) {
+  __shared__ int64_t wtot[kPartWaves];
+  const int s = blockIdx.x;
+  const int64_t a = seg_first[s], b = seg_first[s + 1], base = seg_lo[s];
+  int64_t carry = 0, tot;
+  for (int64_t c = a; c < b; c += kPartThreads) {
+    const int64_t i = c + threadIdx.x;
+    const int64_t v = i < b ? it_left[i] : 0;
+    const int64_t inc = block_incl_scan_i64(v, wtot, tot);
+    if (i < b) dst_left[i] = base + carry + inc - v;
+    carry += tot;
+  }
+  const int64_t L = carry;
+  if (threadIdx.x == 0) nleft[s] = L;
+  carry = 0;
+  for (int64_t c = a; c < b; c += kPartThreads) {
+    const int64_t i = c + threadIdx.x;
+    const int64_t v = i < b ? (it_hi[i] - it_lo[i]) - it_left[i] : 0;
+    const int64_t inc = block_incl_scan_i64(v, wtot, tot);
+    if (i < b) dst_right[i] = base + L + carry + inc - v;
+    carry += tot;
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // Feature-major copy of the binned matrix ([n][F] -> [F][n], uint8) for the partition.
 // One block = 256 rows x <= 64 features staged through LDS: 4-byte coalesced row reads
@@ -665,6 +716,18 @@ O3S_API int o3s_tree_partition(const uint8_t* bins, int64_t rs, int64_t cs, cons
   else
     hipLaunchKernelGGL(tree_part_scatter_kernel, dim3(n_items), dim3(kPartThreads), 0, st, order, out,
                        it_lo, it_hi, it_feat, it_bin, dst_left, dst_right, flags, py, py_out, pw, pw_out);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+// Items of segment s are [seg_first[s], seg_first[s+1]) (nseg + 1 entries); writes the
+// scatter destinations of every item and nleft[s].
+O3S_API int o3s_tree_part_dest(const int64_t* it_lo, const int64_t* it_hi, const int64_t* it_left,
+                               const int64_t* seg_first, const int64_t* seg_lo, int nseg, int64_t* dst_left,
+                               int64_t* dst_right, int64_t* nleft, hipStream_t st) {
+  if (nseg <= 0) return 0;
+  hipLaunchKernelGGL(tree_part_dest_kernel, dim3(nseg), dim3(kPartThreads), 0, st, it_lo, it_hi, it_left, seg_first,
+                     seg_lo, dst_left, dst_right, nleft);
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -57,7 +57,7 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     the split segments are not written).
 
     GPU: two passes of ``tree_part_*_kernel`` over work items (count, then scatter to
-    destinations computed by small scans here); CPU: the PyTorch reference."""
+    destinations from ``tree_part_dest_kernel``); CPU: the PyTorch reference."""
     payload, payload_out = tuple(payload), tuple(payload_out)
     if len(payload) != len(payload_out) or len(payload) > 2:
         raise ValueError("payload / payload_out mismatch")
@@ -80,12 +80,16 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     seg_of = np.repeat(np.arange(nseg), n_it)
     it_lo_h = lo[seg_of] + (np.arange(n_items) - first[seg_of]) * chunk
     it_hi_h = np.minimum(it_lo_h + chunk, hi[seg_of])
-    i64 = N.upload(np.concatenate([it_lo_h, it_hi_h, seg_of, first[seg_of], lo[seg_of]]), dev)
-    it_lo, it_hi, it_seg, f, seg_lo_it = (i64[k * n_items:(k + 1) * n_items] for k in range(5))
+    seg_first = np.append(first, n_items)
+    i64 = N.upload(np.concatenate([it_lo_h, it_hi_h, seg_first, lo]), dev)
+    it_lo, it_hi = i64[:n_items], i64[n_items:2 * n_items]
+    seg_first_d, seg_lo_d = i64[2 * n_items:2 * n_items + nseg + 1], i64[2 * n_items + nseg + 1:]
     fb = np.concatenate([_host(s_feat).astype(np.int32)[seg_of], _host(s_bin).astype(np.int32)[seg_of]])
     i32 = N.upload(fb, dev)
     it_feat, it_bin = i32[:n_items], i32[n_items:]
-    it_left = torch.empty(n_items, dtype=torch.int64, device=dev)
+    work = torch.empty(3 * n_items + nseg, dtype=torch.int64, device=dev)
+    it_left, dst_left, dst_right = work[:n_items], work[n_items:2 * n_items], work[2 * n_items:3 * n_items]
+    nleft = work[3 * n_items:]
     flags = torch.empty(order.shape[0], dtype=torch.uint8, device=dev)
     lib = N.kernels()
     st = N.stream_of(bins)
@@ -93,12 +97,9 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     N.check(lib.o3s_tree_partition(src.data_ptr(), rs, cs, order.data_ptr(), None, it_lo.data_ptr(), it_hi.data_ptr(),
                                    it_feat.data_ptr(), it_bin.data_ptr(), it_left.data_ptr(), None, None,
                                    flags.data_ptr(), n_items, 0, None, None, None, None, st), "tree_part_count")
-    it_right = (it_hi - it_lo) - it_left
-    nleft = torch.zeros(nseg, dtype=torch.int64, device=dev).index_add_(0, it_seg, it_left)
-    cl = torch.cumsum(it_left, 0) - it_left                    # global exclusive prefixes
-    cr = torch.cumsum(it_right, 0) - it_right
-    dst_left = (seg_lo_it + cl - cl[f]).contiguous()           # f: first item of each item's segment
-    dst_right = (seg_lo_it + nleft[it_seg] + cr - cr[f]).contiguous()
+    N.check(lib.o3s_tree_part_dest(it_lo.data_ptr(), it_hi.data_ptr(), it_left.data_ptr(), seg_first_d.data_ptr(),
+                                   seg_lo_d.data_ptr(), nseg, dst_left.data_ptr(), dst_right.data_ptr(),
+                                   nleft.data_ptr(), st), "tree_part_dest")
     pl = [None] * 4
     for q, (a, b) in enumerate(zip(payload, payload_out)):
         if a.dtype != torch.float32 or b.dtype != torch.float32 or a.numel() != order.numel() \
