@@ -365,10 +365,7 @@ class TreeBuilder:
                                      np.arange(P), P, B, S, self.cls, ypos=True)
                     Hs = Hs.to(torch.float64).contiguous()
                     self.comm.all_reduce(Hs)
-                    pick = N.upload(pick_h, dev)
-                    H = torch.empty((k, F, B, S), dtype=torch.float64, device=dev)
-                    H[pick] = Hs
-                    H[pick ^ 1] = _sibling(parent_H, Hs, self.cls)
+                    H = T.sibling_hists(Hs, parent_H, small_right, self.cls)
             tsplit = trace("tree.split")
             tsplit.__enter__()
             fm = None

@@ -652,6 +652,42 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_grad_loss_kernel(
   }
 }
 
+// Histogram subtraction for a whole level: node 2p + sr[p] is the scanned smaller child
+// Hs[p], node 2p + 1 - sr[p] its sibling parent[p] - Hs[p], cleaned of the rounding
+// residue fractional weights leave in bins the sibling does not populate (CLS: counts
+// clamped at 0; REG: (w, w*y) zeroed where w <= 0, the node's w*y^2 -- stat 2 of
+// feature 0 bin 0 -- clamped at 0).  One thread per (node pair, feature x bin) cell.
+__global__ __launch_bounds__(256) void tree_sibling_kernel(const double* __restrict__ Hs,
+                                                           const double* __restrict__ parent,
+                                                           const uint8_t* __restrict__ sr, int64_t P, int FB, int S,
+                                                           int cls, double* __restrict__ H) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (g >= P * FB) return;
+  const int64_t p = g / FB;
+  const int fb = (int)(g % FB);
+  const int64_t C = (int64_t)FB * S;
+  const double* hs = Hs + p * C + (int64_t)fb * S;
+  const double* pa = parent + p * C + (int64_t)fb * S;
+  const int s_small = sr[p] ? 1 : 0;
+  double* hsm = H + (2 * p + s_small) * C + (int64_t)fb * S;
+  double* hsb = H + (2 * p + 1 - s_small) * C + (int64_t)fb * S;
+  if (cls) {
+    for (int s = 0; s < S; ++s) {
+      const double a = hs[s];
+      const double d = pa[s] - a;
+      hsm[s] = a;
+      hsb[s] = d > 0.0 ? d : 0.0;
+    }
+    return;
+  }
+  const double w = pa[0] - hs[0], wy = pa[1] - hs[1], y2 = pa[2] - hs[2];
+  const bool empty = !(w > 0.0);
+  hsm[0] = hs[0]; hsm[1] = hs[1]; hsm[2] = hs[2];
+  hsb[0] = empty ? 0.0 : w;
+  hsb[1] = empty ? 0.0 : wy;
+  hsb[2] = fb == 0 ? (y2 > 0.0 ? y2 : 0.0) : y2;
+}
+
 }  // namespace
 
 // acc[order[p]] += it_val[i] for p in [it_lo[i], it_hi[i]) (items of leaf segments).
@@ -807,6 +843,18 @@ O3S_API int o3s_gbt_grad_loss(const double* y, const double* F, const double* w,
   if (loss < 0 || loss > 2 || n_blocks <= 0) return -1;
   hipLaunchKernelGGL(gbt_grad_loss_kernel, dim3(n_blocks), dim3(kGbtThreads), 0, st, y, F, w, wv, n, loss, target,
                      partial);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+// Hs, parent: fp64 [P][FB*S]; sr: uint8 [P]; H: fp64 [2P][FB*S]; cls: 0 = REG (S == 3).
+O3S_API int o3s_tree_sibling(const double* Hs, const double* parent, const uint8_t* sr, int64_t P, int FB, int S,
+                             int cls, double* H, hipStream_t st) {
+  if (P <= 0) return 0;
+  if (FB <= 0 || S <= 0 || (!cls && S != 3)) return -1;
+  const int64_t n = P * FB;
+  hipLaunchKernelGGL(tree_sibling_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, Hs, parent, sr, P, FB,
+                     S, cls, H);
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -272,16 +272,15 @@ def node_hist(bins: torch.Tensor, order: torch.Tensor, y: torch.Tensor, w: torch
     relies on."""
     F = bins.shape[1]
     dev = bins.device
-    out = torch.zeros((n_nodes, F * B * S), dtype=torch.float64, device=dev)
     if len(seg_lo) == 0:
-        return out.view(n_nodes, F, B, S)
+        return torch.zeros((n_nodes, F, B, S), dtype=torch.float64, device=dev)
     if not hist_kernel_ok(bins, B, S, cls):
         # reference path (CPU / oversize bins): direct scatter-add per segment
         return hist_torch(bins, order, y, w, _dev(seg_lo, dev), _dev(seg_hi, dev), _dev(seg_node, dev), n_nodes,
                           B, S, cls, ypos=ypos)
     plan = _HistPlan(seg_lo, seg_hi, seg_node, chunk, dev)
     if plan.n_items == 0:
-        return out.view(n_nodes, F, B, S)
+        return torch.zeros((n_nodes, F, B, S), dtype=torch.float64, device=dev)
     C = F * B * S
     slab = torch.empty((plan.n_items, C), dtype=torch.float32, device=dev)
     yf = y.to(torch.float32).contiguous()
@@ -303,8 +302,43 @@ def node_hist(bins: torch.Tensor, order: torch.Tensor, y: torch.Tensor, w: torch
         b = min(a + 65535, nseg)
         N.check(lib.o3s_slab_range_sum(runs.data_ptr(), 1, C, plan.s_run0[a:].data_ptr(), plan.s_nrun[a:].data_ptr(),
                                        b - a, seg_sum[a:].data_ptr(), st), "slab_range_sum")
-    out.index_add_(0, plan.seg_node, seg_sum)             # one segment per node in the engine
+    if plan.identity and nseg == n_nodes:                 # the engine: segment i is node i
+        return seg_sum.view(n_nodes, F, B, S)
+    out = torch.zeros((n_nodes, C), dtype=torch.float64, device=dev)
+    out.index_add_(0, plan.seg_node, seg_sum)
     return out.view(n_nodes, F, B, S)
+
+
+def sibling_hists(Hs: torch.Tensor, parent: torch.Tensor, small_right, cls: bool) -> torch.Tensor:
+    """Level histograms [2P, F, B, S] from the scanned smaller children Hs [P] and the
+    parents [P]: node 2p + small_right[p] is Hs[p], its sibling parent[p] - Hs[p] with
+    the rounding residue of fractional weights cleaned (class counts / weights clamped
+    at 0, REG w*y zeroed where w <= 0, the node's w*y^2 clamped at 0).
+
+    GPU: ``tree_sibling_kernel`` (one pass); CPU: torch."""
+    P = Hs.shape[0]
+    sr = np.asarray(small_right, dtype=np.uint8)
+    if Hs.is_cuda and P > 0:
+        Hs_c, par = Hs.contiguous(), parent.contiguous()
+        H = torch.empty((2 * P,) + tuple(Hs.shape[1:]), dtype=torch.float64, device=Hs.device)
+        srd = N.upload(sr, Hs.device)
+        _, F, B, S = Hs.shape
+        N.check(N.kernels().o3s_tree_sibling(Hs_c.data_ptr(), par.data_ptr(), srd.data_ptr(), P, F * B, S, int(cls),
+                                             H.data_ptr(), N.stream_of(Hs)), "tree_sibling")
+        return H
+    sib = parent - Hs
+    if cls:
+        sib.clamp_min_(0.0)
+    else:
+        y2 = sib[:, 0, 0, 2].clamp_min(0.0)
+        empty = sib[..., 0] <= 0.0
+        sib[..., :2] = torch.where(empty[..., None], torch.zeros_like(sib[..., :2]), sib[..., :2])
+        sib[:, 0, 0, 2] = y2
+    H = torch.empty((2 * P,) + tuple(Hs.shape[1:]), dtype=torch.float64, device=Hs.device)
+    pick = torch.from_numpy(2 * np.arange(P) + sr.astype(np.int64)).to(Hs.device)
+    H[pick] = Hs
+    H[pick ^ 1] = sib
+    return H
 
 
 _RUN = 64      # slab rows per first-stage partial
@@ -341,6 +375,7 @@ class _HistPlan:
             views.append(buf[off: off + len(p)])
             off += len(p)
         self.it_lo, self.it_hi, self.r_lo, self.r_cnt, self.s_run0, self.s_nrun, self.seg_node = views
+        self.identity = bool(np.array_equal(nd, np.arange(self.nseg)))
 
 
 def hist_torch(bins, order, y, w, seg_lo, seg_hi, seg_node, n_nodes, B, S, cls, ypos=False):

@@ -386,3 +386,23 @@ def test_forest_batched_equals_sequential(cpu):
 def test_gpu_forest_batched_equals_sequential():
     s = Session(SessionConf().set("o3s.device", "cuda"))
     _forest_batched_vs_sequential(s, "cuda")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cls", [False, True])
+def test_gpu_sibling_kernel_matches_torch(gpu, cls):
+    """tree_sibling_kernel (level histogram assembly + residue cleaning) == torch path."""
+    from orange3_spark_amd.ops import trees as T
+    g = torch.Generator().manual_seed(4)
+    P, F, B = 19, 9, 16
+    S = 4 if cls else 3
+    parent = torch.rand((P, F, B, S), generator=g, dtype=torch.float64) * 10
+    Hs = parent * torch.rand((P, F, B, S), generator=g, dtype=torch.float64)
+    Hs[0, 1, 2] = parent[0, 1, 2] + 1e-9                     # residue: sibling slightly negative
+    if not cls:
+        parent[:, 1:, :, 2] = 0.0
+        Hs[:, 1:, :, 2] = 0.0
+    sr = (torch.rand(P, generator=g) < 0.5).numpy()
+    ref = T.sibling_hists(Hs, parent, sr, cls)
+    got = T.sibling_hists(Hs.to(gpu), parent.to(gpu), sr, cls).cpu()
+    assert torch.equal(got, ref)
