@@ -41,6 +41,10 @@ def _work(rank, world, port, out_dir):
     res["sample_n"] = df.sample(False, 0.3, seed=9).count()
     g = GBTClassifier(maxIter=3, maxDepth=3, seed=1).fit(s.synthetic.trees(2000, 6, seed=2))
     res["gbt_loss"] = g.trainingLossHistory
+    from orange3_spark_amd.ml.classification import RandomForestClassifier
+    rf = RandomForestClassifier(numTrees=4, maxDepth=4, seed=3).fit(s.synthetic.trees(2000, 6, seed=2))
+    res["rf_nodes"] = [t.numNodes for t in rf.trees]
+    res["rf_imp"] = rf.featureImportances.toArray()
     rng = np.random.default_rng(0)
     u = rng.integers(0, 50, 600)
     i = rng.integers(0, 30, 600)
@@ -95,6 +99,7 @@ def test_world2_matches_world1(tmp_path):
     assert a["km_cost"] == pytest.approx(b["km_cost"], rel=1e-9)
     assert a["sample_n"] == b["sample_n"]
     assert np.allclose(a["gbt_loss"], b["gbt_loss"], rtol=1e-6)
+    assert a["rf_nodes"] == b["rf_nodes"] and np.allclose(a["rf_imp"], b["rf_imp"], atol=1e-9)
     assert np.allclose(a["als_U"], b["als_U"], atol=1e-4)
     assert a["groupby"] == b["groupby"]
     assert a["iso"].shape == b["iso"].shape and np.allclose(a["iso"], b["iso"], atol=1e-9)
