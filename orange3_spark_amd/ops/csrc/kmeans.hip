@@ -636,42 +636,73 @@ __global__ __launch_bounds__(kUpdThreads) void kmeans_update_kernel(
     __syncthreads();
     // wave w owns clusters [c0, c1): its rows are the contiguous sorted range
     const int c0 = (int)((int64_t)Kp * wid / kUpdWaves), c1 = (int)((int64_t)Kp * (wid + 1) / kUpdWaves);
+    if constexpr (LPR > 0) {
+      // Streaming form: the wave's sorted range is cut at cluster boundaries into RPI
+      // contiguous pieces, one per row slot (LPR lanes x float4 = one row); each slot
+      // streams its rows with U loads in flight and flushes its register sum to the
+      // block slab whenever the cluster changes.  No cluster spans two slots (cut points
+      // are bucket starts), so every cluster is summed by one slot in row order
+      // (deterministic) and loads stay in flight across cluster boundaries -- the old
+      // per-cluster loop waited one HBM round trip per (small) cluster.
+      constexpr int RPI = kWave / LPR;
+      constexpr int U = 8;
+      const int slot = lane / LPR, col = 4 * (lane % LPR);
+      const bool cok = col < D;
+      const int b0 = start[c0], b1 = start[c1];
+      auto cut = [&](int sl) {                    // first cluster of piece sl
+        if (sl <= 0) return c0;
+        if (sl >= RPI) return c1;
+        const int t = b0 + (int)((int64_t)(b1 - b0) * sl / RPI);
+        int lo = c0, hi = c1;                     // smallest c in [c0, c1] with start[c] >= t
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (start[mid] >= t) hi = mid; else lo = mid + 1;
+        }
+        return lo;
+      };
+      int c = cut(slot);
+      const int pe = start[cut(slot + 1)];
+      const int pb = start[c];
+      int cend = c < c1 ? start[c + 1] : pb;      // (empty piece at the last cluster: no rows)
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      auto flush = [&](int cc) {
+        if (!cok) return;
+        float4* dst = reinterpret_cast<float4*>(myslab + (int64_t)cc * D + col);
+        float4 d4 = *dst;
+        d4.x += acc.x; d4.y += acc.y; d4.z += acc.z; d4.w += acc.w;
+        *dst = d4;
+      };
+      for (int t = pb; __ballot(t < pe) != 0ull; t += U) {
+        float4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int pos = t + u;
+          x[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (cok && pos < pe) x[u] = *reinterpret_cast<const float4*>(X + (r0 + sorted[pos]) * ldx + col);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int pos = t + u;
+          if (pos < pe) {
+            while (pos >= cend) {                 // leave cluster c (flush it if it had rows)
+              if (cend > start[c]) flush(c);
+              acc = make_float4(0.f, 0.f, 0.f, 0.f);
+              ++c;
+              cend = start[c + 1];
+            }
+            acc.x += x[u].x; acc.y += x[u].y; acc.z += x[u].z; acc.w += x[u].w;
+          }
+        }
+      }
+      if (pe > pb) flush(c);
+      for (int cc = c0 + lane; cc < c1; cc += kWave) {
+        const int sz = start[cc + 1] - start[cc];
+        if (sz) mycnt[cc] += (float)sz;
+      }
+    } else {
     for (int c = c0; c < c1; ++c) {
       const int b0 = start[c], b1 = start[c + 1];
       if (b0 == b1) continue;
-      if constexpr (LPR > 0) {
-        // 16-B loads: each lane owns 4 columns of one of RPI row slots; the slots'
-        // partial sums are folded by xor-shuffles before the slab update
-        constexpr int RPI = kWave / LPR;
-        const int slot = lane / LPR, col = 4 * (lane % LPR);
-        const bool cok = col < D;
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        auto ld = [&](int i) {
-          const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (!cok || i >= b1) return z;
-          return *reinterpret_cast<const float4*>(X + (r0 + sorted[i]) * ldx + col);
-        };
-        for (int i = b0 + slot; i < b1; i += 4 * RPI) {      // 4 row loads in flight per lane
-          const float4 x0 = ld(i), x1 = ld(i + RPI), x2 = ld(i + 2 * RPI), x3 = ld(i + 3 * RPI);
-          acc.x += x0.x; acc.y += x0.y; acc.z += x0.z; acc.w += x0.w;
-          acc.x += x1.x; acc.y += x1.y; acc.z += x1.z; acc.w += x1.w;
-          acc.x += x2.x; acc.y += x2.y; acc.z += x2.z; acc.w += x2.w;
-          acc.x += x3.x; acc.y += x3.y; acc.z += x3.z; acc.w += x3.w;
-        }
-#pragma unroll
-        for (int off = LPR; off < kWave; off <<= 1) {
-          acc.x += __shfl_xor(acc.x, off, 64);
-          acc.y += __shfl_xor(acc.y, off, 64);
-          acc.z += __shfl_xor(acc.z, off, 64);
-          acc.w += __shfl_xor(acc.w, off, 64);
-        }
-        if (slot == 0 && cok) {
-          float4* dst = reinterpret_cast<float4*>(myslab + (int64_t)c * D + col);
-          float4 d4 = *dst;
-          d4.x += acc.x; d4.y += acc.y; d4.z += acc.z; d4.w += acc.w;
-          *dst = d4;
-        }
-      } else {
       float acc[DV];
 #pragma unroll
       for (int v = 0; v < DV; ++v) acc[v] = 0.f;
@@ -706,8 +737,8 @@ __global__ __launch_bounds__(kUpdThreads) void kmeans_update_kernel(
         const int col = lane + 64 * v;
         if (col < D) dst[col] += acc[v];
       }
-      }
       if (lane == 0) mycnt[c] += (float)(b1 - b0);
+    }
     }
     __syncthreads();
   }
