@@ -1,0 +1,79 @@
+"""Two ranks on ONE MI355X (gloo process group, both on cuda:0): the GPU kernels of the
+sharded estimators (GLM gradient, KMeans screen/update, tree histograms + partition,
+batched forests, ALS passes) must give the single-rank answer.  RCCL needs one GPU per
+rank, so the 8-GPU RCCL run itself is the round driver's; this rehearses every
+collective call site of those estimators on device tensors."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _work(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), O3S_DIST_BACKEND="gloo")
+    import pandas as pd
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.ml.classification import GBTClassifier, LogisticRegression, RandomForestClassifier
+    from orange3_spark_amd.ml.clustering import KMeans
+    from orange3_spark_amd.ml.recommendation import ALS
+    conf = SessionConf().set("o3s.device", "cuda").set("spark.master", "spmd" if world > 1 else "local")
+    s = Session(conf)
+    res = {}
+    df = s.synthetic.classification(20_001, 16, seed=5)
+    res["lr"] = LogisticRegression(maxIter=20, regParam=0.01).fit(df).coefficients.toArray()
+    km = KMeans(k=8, seed=2, maxIter=8).fit(s.synthetic.blobs(40_000, 32, k=8, seed=1))
+    res["km_cost"] = km.summary.trainingCost
+    res["km_centers"] = np.stack([np.asarray(c) for c in km.clusterCenters()])
+    tdf = s.synthetic.trees(30_000, 12, seed=2)
+    g = GBTClassifier(maxIter=4, maxDepth=4, seed=1).fit(tdf)
+    res["gbt_loss"] = np.array(g.trainingLossHistory)
+    rf = RandomForestClassifier(numTrees=5, maxDepth=5, seed=3).fit(tdf)
+    res["rf_nodes"] = [t.numNodes for t in rf.trees]
+    res["rf_imp"] = rf.featureImportances.toArray()
+    rng = np.random.default_rng(0)
+    pdf = pd.DataFrame({"user": rng.integers(0, 300, 5000), "item": rng.integers(0, 120, 5000),
+                        "rating": rng.normal(size=5000)})
+    res["als_U"] = ALS(rank=8, maxIter=3, seed=1).fit(s.createDataFrame(pdf))._U.cpu().numpy()
+    if rank == 0:
+        torch.save(res, os.path.join(out_dir, f"g{world}.pt"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_gpu_world2_matches_world1(tmp_path):
+    ctx = mp.get_context("spawn")
+    for world in (1, 2):
+        port = _free_port()
+        procs = [ctx.Process(target=_work, args=(r, world, port, str(tmp_path))) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(300)
+            assert p.exitcode == 0
+    a = torch.load(tmp_path / "g1.pt", weights_only=False)
+    b = torch.load(tmp_path / "g2.pt", weights_only=False)
+    assert np.allclose(a["lr"], b["lr"], atol=1e-5)
+    # per-block fp32 slab partials are summed over different row blocks per shard layout
+    assert a["km_cost"] == pytest.approx(b["km_cost"], rel=1e-4)
+    assert np.allclose(a["km_centers"], b["km_centers"], atol=1e-3)
+    assert np.allclose(a["gbt_loss"], b["gbt_loss"], rtol=1e-5)
+    assert a["rf_nodes"] == b["rf_nodes"]
+    assert np.allclose(a["rf_imp"], b["rf_imp"], atol=1e-6)
+    assert np.allclose(a["als_U"], b["als_U"], atol=1e-3)
