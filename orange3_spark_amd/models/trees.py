@@ -372,8 +372,12 @@ class TreeBuilder:
             if self.ffrac < 1.0:
                 m = max(1, int(math.ceil(self.ffrac * F)))
                 fm = np.zeros((k, F), dtype=bool)
-                for i in range(k):                                # each tree draws from its own stream
-                    fm[i, rngs[seg_tree[i]].choice(F, m, replace=False)] = True
+                for t in np.unique(seg_tree):                     # each tree draws from its own stream:
+                    rows_t = np.nonzero(seg_tree == t)[0]         # m of F features per node, uniformly
+                    keys = rngs[t].random((len(rows_t), F))
+                    pick = np.argpartition(keys, m - 1, axis=1)[:, :m] if m < F else \
+                        np.broadcast_to(np.arange(F), (len(rows_t), F))
+                    fm[rows_t[:, None], pick] = True
             # min child weight: at the root a fraction of its total weight (Spark
             # minWeightFractionPerNode), below it the absolute value that gave, per tree
             mw_frac = self.min_wfrac if depth == 0 else 0.0
