@@ -416,7 +416,8 @@ class TreeBuilder:
             gain[st, sn] = bg[do_split]
             # --- partition the splitting segments
             s_lo, s_hi = seg_lo[do_split], seg_hi[do_split]
-            parent_H = H[N.upload(do_split, dev)]
+            # integer gather (a boolean mask index would sync on the device-side nonzero)
+            parent_H = H.index_select(0, N.upload(np.nonzero(do_split)[0], dev))
             small_right = (wr_np < wl_np)[do_split]
             pay = (yp,) if wp is None else (yp, wp)
             if pingpong:

@@ -619,9 +619,11 @@ __global__ __launch_bounds__(kGbtThreads) void gbt_grad_loss_kernel(
     const double yi = y[i], fi = F[i];
     double l, g;
     if (loss == 0) {
-      const double z = -2.0 * yi * fi;                             // log(1 + e^z), stably
-      l = 2.0 * (z > 0.0 ? z + log1p(exp(-z)) : log1p(exp(z)));
-      g = 4.0 * yi / (1.0 + exp(-z));
+      // z = -2yF; loss 2 log(1 + e^z) and residual 4y sigmoid(z) from ONE exp: e = e^{-|z|}
+      const double z = -2.0 * yi * fi;
+      const double e = exp(-fabs(z));
+      l = 2.0 * (fmax(z, 0.0) + log1p(e));
+      g = 4.0 * yi * (z >= 0.0 ? 1.0 / (1.0 + e) : e / (1.0 + e));
     } else if (loss == 1) {
       const double d = yi - fi;
       l = d * d;
