@@ -50,48 +50,67 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
     comm.all_reduce(c0)
     centers = c0[None, :]
     for step in range(steps):
+        tr = trace("kmeans.init.round")
+        tr.__enter__()
         _, d = K.assign(X, centers.float())
         cost = d.to(torch.float64).sum()
         comm.all_reduce(cost)
         if float(cost) <= 0:
+            tr.__exit__(None, None, None)
             break
         p = (2.0 * k * d.to(torch.float64) / float(cost)).clamp(max=1.0)
         u = sampling.uniform(rows, seed + 1 + step, stream=7)
         new = X[u < p].to(torch.float64)
         new = comm.all_gather_v(new) if comm.world_size > 1 else new
         centers = torch.cat([centers, new.to(dev)])
+        tr.__exit__(None, None, None)
     # weights = number of points closest to each candidate
-    a, _ = K.assign(X, centers.float())
-    wts = torch.zeros(centers.shape[0], dtype=torch.float64, device=dev).index_add_(
-        0, a.long(), torch.ones(a.shape[0], dtype=torch.float64, device=dev))
-    comm.all_reduce(wts)
-    return _local_kmeanspp(centers, wts, k, seed)
+    with trace("kmeans.init.weights"):
+        a, _ = K.assign(X, centers.float())
+        wts = torch.zeros(centers.shape[0], dtype=torch.float64, device=dev).index_add_(
+            0, a.long(), torch.ones(a.shape[0], dtype=torch.float64, device=dev))
+        comm.all_reduce(wts)
+    with trace("kmeans.init.local"):
+        return _local_kmeanspp(centers, wts, k, seed)
 
 
 def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: int = 30) -> torch.Tensor:
-    """Weighted k-means++ + Lloyd on candidates (Spark LocalKMeans), fp64 on device."""
+    """Weighted k-means++ + Lloyd on candidates (Spark LocalKMeans), fp64 on device.
+
+    Greedy k-means++ (best of ``2 + ln k`` weighted draws per step).  The whole seeding
+    loop stays on the device -- draws are counter-hash uniforms keyed on (seed, step,
+    trial) inverted through the cumulative weights by ``searchsorted`` -- so its k
+    sequential steps issue kernels without a single host round trip (the host-side
+    multinomial per step cost two syncs each: ~2 s of a 3 s fit at k = 1024)."""
     m = P.shape[0]
+    dev = P.device
     if m <= k:
         extra = k - m
         return torch.cat([P, P[:1].expand(extra, -1)]) if extra else P
-    g = torch.Generator(device="cpu").manual_seed(seed)
-    first = int(torch.multinomial(w.cpu().double(), 1, generator=g))
-    C = [P[first]]
-    d2 = ((P - P[first]) ** 2).sum(1)
     trials = 2 + int(math.log(k))          # greedy k-means++: best of several seeds per step
-    for _ in range(1, k):
-        prob = (w * d2).cpu()
-        if float(prob.sum()) <= 0:
-            cand = torch.randint(0, m, (trials,), generator=g)
-        else:
-            cand = torch.multinomial(prob, trials, replacement=True, generator=g)
-        cd = ((P[None, :, :] - P[cand.to(P.device)][:, None, :]) ** 2).sum(-1)   # [trials, m]
+    keys = torch.arange(k * (trials + 1), dtype=torch.int64, device=dev).view(k, trials + 1)
+    U = sampling.uniform(keys.reshape(-1), seed, stream=31).view(k, trials + 1)
+
+    def draw(t, prob, n):
+        cs = torch.cumsum(prob, 0)
+        tot = cs[-1]
+        u = U[t, :n] * tot
+        idx = torch.searchsorted(cs, u, right=True).clamp_max(m - 1)
+        rnd = (U[t, :n] * m).long().clamp_max(m - 1)
+        return torch.where(tot > 0, idx, rnd)
+
+    first = draw(0, w, 1)[0]
+    picks = torch.empty(k, dtype=torch.int64, device=dev)
+    picks[0] = first
+    d2 = ((P - P[first]) ** 2).sum(1)
+    for t in range(1, k):
+        cand = draw(t, w * d2, trials)
+        cd = ((P[None, :, :] - P[cand][:, None, :]) ** 2).sum(-1)                  # [trials, m]
         pot = (w[None, :] * torch.minimum(d2[None, :], cd)).sum(1)
-        best = int(pot.argmin())
-        idx = int(cand[best])
-        C.append(P[idx])
+        best = pot.argmin()
+        picks[t] = cand[best]
         d2 = torch.minimum(d2, cd[best])
-    C = torch.stack(C)
+    C = P[picks]
     for _ in range(iters):
         dist = (P * P).sum(1, keepdim=True) - 2 * P @ C.T + (C * C).sum(1)[None, :]
         a = dist.argmin(1)
