@@ -103,9 +103,12 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
     picks = torch.empty(k, dtype=torch.int64, device=dev)
     picks[0] = first
     d2 = ((P - P[first]) ** 2).sum(1)
+    pn = (P * P).sum(1)
     for t in range(1, k):
         cand = draw(t, w * d2, trials)
-        cd = ((P[None, :, :] - P[cand][:, None, :]) ** 2).sum(-1)                  # [trials, m]
+        # [trials, m] squared distances as |p|^2 + |c|^2 - 2 c.p: one small fp64 GEMM
+        # instead of a [trials, m, D] difference tensor per step
+        cd = (pn[None, :] + pn[cand][:, None] - 2.0 * (P[cand] @ P.T)).clamp_min_(0.0)
         pot = (w[None, :] * torch.minimum(d2[None, :], cd)).sum(1)
         best = pot.argmin()
         picks[t] = cand[best]

@@ -76,7 +76,7 @@ SCREEN_EPS = 2.0 ** -5
 # fall back to the split-precision kernel for every row once the screen flags this share
 SCREEN_MAX_FLAG_FRACTION = 0.3
 SCREEN_TT = 0                 # 32-row tiles per wave in the screen kernel (0: by D)
-_screen_state: dict = {}      # (data_ptr, shape) -> last flagged fraction
+_screen_state: dict = {}      # (data_ptr, shape, Cpad) -> last flagged fraction (decays)
 
 
 class _ScreenWs:
@@ -117,9 +117,15 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
     d = torch.empty(n, dtype=torch.float32, device=X.device)
     lib = N.kernels()
     st = N.stream_of(X)
-    key = (X.data_ptr(), tuple(X.shape))
+    # near-tie rates depend on the centre set: keyed by the padded centre count too, so
+    # k-means|| candidate passes (thousands of close candidates: mostly near ties) do not
+    # push the later Lloyd iterations (k centres) onto the split path
+    key = (X.data_ptr(), tuple(X.shape), P.hi.shape[0])
     if mode == "auto":
-        mode = "split" if _screen_state.get(key, 0.0) > SCREEN_MAX_FLAG_FRACTION or not screen_ok(X) else "screen"
+        frac = _screen_state.get(key, 0.0)
+        mode = "split" if frac > SCREEN_MAX_FLAG_FRACTION or not screen_ok(X) else "screen"
+        if mode == "split" and frac > 0.0:
+            _screen_state[key] = 0.5 * frac       # re-probe the screen after a few split calls
     if mode == "screen" and screen_ok(X):
         cnt, rows = _SWS.get(n, X.device)
         cnt.zero_()
