@@ -73,8 +73,15 @@ def partition(comm, rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, 
 
 
 def init_factors(n_lo: int, n: int, rank: int, seed: int, device, nonneg: bool) -> torch.Tensor:
-    """Unit-norm gaussian rows keyed on (seed, global index): partition invariant."""
+    """Unit-norm gaussian rows keyed on (seed, global index): partition invariant.
+
+    GPU: ``als_init_kernel`` (one wave per row); CPU: the same draws in torch."""
     out = torch.empty((n, rank), dtype=torch.float32, device=device)
+    if out.is_cuda and 0 < rank <= 512:
+        from ..ops import _native as N
+        N.check(N.kernels().o3s_als_init(int(n_lo), int(n), int(rank), int(seed) & 0xFFFFFFFF, int(bool(nonneg)),
+                                         out.data_ptr(), N.stream_of(out)), "als_init")
+        return out
     s1 = [2 * k + 11 for k in range(rank)]
     s2 = [2 * k + 12 for k in range(rank)]
     step = max(1, (1 << 25) // max(rank, 1))                 # bounded int64 temporaries
@@ -203,15 +210,18 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
             ckpt=None) -> AlsResult:
     t0 = time.time()
     dev = ratings.device
-    uid = global_ids(comm, users)
-    iid = global_ids(comm, items)
-    uix = torch.searchsorted(uid, users.to(torch.int64))
-    iix = torch.searchsorted(iid, items.to(torch.int64))
-    nU, nI = uid.numel(), iid.numel()
-    by_user = partition(comm, uix, iix, ratings.float(), nU)
-    by_item = partition(comm, iix, uix, ratings.float(), nI)
-    X = init_factors(by_user.row_lo, by_user.nrows, rank, seed, dev, nonneg)
-    Y = init_factors(by_item.row_lo, by_item.nrows, rank, seed ^ 0x5A5A, dev, nonneg)
+    with trace("als.setup.ids"):
+        uid = global_ids(comm, users)
+        iid = global_ids(comm, items)
+        uix = torch.searchsorted(uid, users.to(torch.int64))
+        iix = torch.searchsorted(iid, items.to(torch.int64))
+        nU, nI = uid.numel(), iid.numel()
+    with trace("als.setup.partition"):
+        by_user = partition(comm, uix, iix, ratings.float(), nU)
+        by_item = partition(comm, iix, uix, ratings.float(), nI)
+    with trace("als.setup.init"):
+        X = init_factors(by_user.row_lo, by_user.nrows, rank, seed, dev, nonneg)
+        Y = init_factors(by_item.row_lo, by_item.nrows, rank, seed ^ 0x5A5A, dev, nonneg)
     its = []
     start = 0
     last = ckpt.latest() if ckpt is not None else None

@@ -55,6 +55,7 @@ _SIGS: dict[str, list] = {
                           c_vp, c_i32, c_vp],
     "o3s_kmeans_update_ws": [c_i32, c_i32, c_i32, C.POINTER(c_i64), C.POINTER(c_i64), C.POINTER(c_i32)],
     "o3s_murmur3_terms": [c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp, c_vp],
+    "o3s_als_init": [c_i64, c_i64, c_i32, c_u32, c_i32, c_vp, c_vp],
     "o3s_als_cg": [c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_als_pass": [c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_tree_hist_lds": [c_i32, c_i32, c_i32, c_i32],

@@ -287,6 +287,51 @@ __global__ __launch_bounds__(256) void als_gram_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Factor initialisation (unit-norm gaussian rows keyed on (seed, global row), so the
+// result does not depend on the sharding): element (u, k) = Box-Muller of two
+// counter-hash uniforms of streams 2k+11 / 2k+12 -- the same draws as
+// ops/sampling.py::uniform, in fp64 -- then each row scaled to unit norm.  One wave
+// per row; replaces ~15 torch passes over int64 [rows, rank] temporaries.
+__device__ __forceinline__ double hash_uniform(uint32_t seed, uint32_t stream, int64_t row) {
+  const uint32_t sv = seed * 0x2545F491u + stream * 0x9E3779B9u;
+  const uint32_t k = row_key(sv, row);
+  const uint32_t k2 = fmix32(k ^ 0x68E31DA4u);
+  return ((double)(k >> 5) * 67108864.0 + (double)(k2 >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+template <int RV>
+__global__ __launch_bounds__(256) void als_init_kernel(int64_t row0, int64_t n, int R, uint32_t seed, int nonneg,
+                                                      float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= n) return;
+  float v[RV];
+  float ss = 0.f;
+#pragma unroll
+  for (int q = 0; q < RV; ++q) {
+    const int k = lane + 64 * q;
+    v[q] = 0.f;
+    if (k < R) {
+      double u1 = hash_uniform(seed, 2u * k + 11u, row0 + u);
+      u1 = u1 > 1e-12 ? u1 : 1e-12;
+      const double u2 = hash_uniform(seed, 2u * k + 12u, row0 + u);
+      v[q] = (float)(sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2));
+      ss = fmaf(v[q], v[q], ss);
+    }
+  }
+  ss = wave_sum_dpp(ss);
+  const float inv = 1.f / fmaxf(sqrtf(ss), 1e-12f);
+#pragma unroll
+  for (int q = 0; q < RV; ++q) {
+    const int k = lane + 64 * q;
+    if (k < R) {
+      const float x = v[q] * inv;
+      out[u * R + k] = nonneg ? fabsf(x) : x;
+    }
+  }
+}
+
 }  // namespace
 
 // mode 0: CG init (x, av = A-part of A x, rhs -> r, p, rs); mode 1: CG step (p, av = A-part of A p).
@@ -354,6 +399,20 @@ O3S_API int o3s_als_gram(const int64_t* indptr, const int32_t* cols, const float
     default: return -1;
   }
 #undef O3S_G
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+// out: fp32 [n][R] rows row0 .. row0+n-1 of the factor table (R <= 512).
+O3S_API int o3s_als_init(int64_t row0, int64_t n, int R, uint32_t seed, int nonneg, float* out, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (R <= 0 || R > 512) return -1;
+  const int rv = (R + 63) / 64;
+  const unsigned grid = (unsigned)((n + 3) / 4);
+#define O3S_AI(RVV) \
+  if (rv == RVV) hipLaunchKernelGGL((als_init_kernel<RVV>), dim3(grid), dim3(256), 0, st, row0, n, R, seed, nonneg, out);
+  O3S_AI(1) O3S_AI(2) O3S_AI(3) O3S_AI(4) O3S_AI(5) O3S_AI(6) O3S_AI(7) O3S_AI(8)
+#undef O3S_AI
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -170,3 +170,13 @@ def test_gpu_dense_gram_cholesky_matches_exact_fp64(implicit, R, monkeypatch):
     ref = AE.solve_side(by_item, X, Y0, 0.1, implicit, 2.0, G, 3, False, exact=True)
     err = ((dense.double() - ref.double()).norm() / ref.double().norm()).item()
     assert err < 2e-4, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rank,nonneg", [(128, False), (10, True), (200, False)])
+def test_gpu_init_factors_kernel_matches_torch(rank, nonneg):
+    """als_init_kernel draws the same unit-norm gaussian rows as the torch path."""
+    from orange3_spark_amd.models import als as AE
+    ref = AE.init_factors(1000, 3001, rank, 12345 ^ 0x5A5A, torch.device("cpu"), nonneg)
+    got = AE.init_factors(1000, 3001, rank, 12345 ^ 0x5A5A, torch.device("cuda"), nonneg).cpu()
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)

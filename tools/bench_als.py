@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--dense-min-avg", type=int, default=None,
                     help="rows averaging >= this many ratings take the exact MFMA Gram + Cholesky solve (0 = CG only)")
     a = ap.parse_args()
+    from orange3_spark_amd.runtime.tracing import TRACER
     s = Session.getOrCreate()
     df = s.synthetic.ratings(a.users, a.items, a.ratings, rank=8, seed=1, implicit=True)
     u = df.column_data("user").data.long()
@@ -43,7 +44,9 @@ def main():
     print(json.dumps({"metric": "ALS implicit seconds per iteration (rank 128)", "value": min(res.iter_seconds),
                       "unit": "s/iter", "iter_seconds": res.iter_seconds, "total_s": time.perf_counter() - t0,
                       "users": a.users, "items": a.items, "ratings": a.ratings, "n_gpus": s.comm.world_size,
-                      "cg_iters": a.cg}))
+                      "cg_iters": a.cg,
+                      "phases_s": ({k: round(v["total_s"], 4) for k, v in TRACER.summary().items()}
+                                   if TRACER.enabled else None)}))
 
 
 if __name__ == "__main__":
