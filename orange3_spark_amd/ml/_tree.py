@@ -5,6 +5,8 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from ..runtime.tracing import trace
+
 from ..frame import column as C
 from ..models import trees as TR
 from . import common as U
@@ -100,8 +102,10 @@ def _prepare(df, est, classification: bool, split_rows: torch.Tensor | None = No
     w = U.weights_or_none(df, est)
     comm = df.comm
     Xs = X if split_rows is None else X[split_rows.to(X.device)]
-    splits = TR.find_splits(comm, Xs, g(est.maxBins), g(est.seed))
-    bins = TR.bin_features(X, splits)
+    with trace("tree.find_splits"):
+        splits = TR.find_splits(comm, Xs, g(est.maxBins), g(est.seed))
+    with trace("tree.bin_features"):
+        bins = TR.bin_features(X, splits)
     k = U.num_classes(comm, y) if classification else 0
     rows = df._global_rows()
     return X, y.float(), None if w is None else w.float(), bins, splits, k, rows

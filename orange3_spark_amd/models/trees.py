@@ -531,11 +531,26 @@ def fit_forest(comm, bins, splits, y, w, num_trees: int, impurity: str, num_clas
     """Random forest: every tree's bootstrap (Poisson) or subsample weights, then all
     trees grown together level by level (``TreeBuilder.build_many``)."""
     ws = []
-    for t in range(num_trees):
-        sw = subsample_weights(None, rows, subsampling_rate, seed * 7919 + t, bootstrap)
-        if w is not None:
-            sw = w if sw is None else w * sw
-        ws.append(sw)
+    with trace("forest.weights"):
+        if rows.is_cuda and (bootstrap or subsampling_rate < 1.0):
+            # every tree's bootstrap / subsample weights in one kernel (same draws)
+            seeds = np.array([(seed * 7919 + t) & 0xFFFFFFFF for t in range(num_trees)], dtype=np.uint32)
+            table = sampling.poisson_table(subsampling_rate, rows.device) if bootstrap else None
+            wf = None if w is None else w.to(rows.device, torch.float32).contiguous()
+            out = torch.empty((num_trees, rows.shape[0]), dtype=torch.float32, device=rows.device)
+            r64 = rows.to(torch.int64).contiguous()
+            N.check(N.kernels().o3s_forest_weights(r64.data_ptr(), r64.shape[0],
+                                                   N.upload(seeds.view(np.int32), rows.device).data_ptr(),
+                                                   num_trees, N.ptr(table), 0 if table is None else table.numel(),
+                                                   float(subsampling_rate), N.ptr(wf), out.data_ptr(),
+                                                   N.stream_of(out)), "forest_weights")
+            ws = list(out)
+        else:
+            for t in range(num_trees):
+                sw = subsample_weights(None, rows, subsampling_rate, seed * 7919 + t, bootstrap)
+                if w is not None:
+                    sw = w if sw is None else w * sw
+                ws.append(sw)
     tb = TreeBuilder(comm, bins, splits, y, ws, impurity, num_classes, max_depth, min_instances,
                      min_info_gain, feature_fraction, [seed + 31 * t for t in range(num_trees)],
                      bins_t=T.feature_major(bins), min_weight_fraction=min_weight_fraction)

@@ -293,13 +293,6 @@ __global__ __launch_bounds__(256) void als_gram_kernel(
 // counter-hash uniforms of streams 2k+11 / 2k+12 -- the same draws as
 // ops/sampling.py::uniform, in fp64 -- then each row scaled to unit norm.  One wave
 // per row; replaces ~15 torch passes over int64 [rows, rank] temporaries.
-__device__ __forceinline__ double hash_uniform(uint32_t seed, uint32_t stream, int64_t row) {
-  const uint32_t sv = seed * 0x2545F491u + stream * 0x9E3779B9u;
-  const uint32_t k = row_key(sv, row);
-  const uint32_t k2 = fmix32(k ^ 0x68E31DA4u);
-  return ((double)(k >> 5) * 67108864.0 + (double)(k2 >> 6)) * (1.0 / 9007199254740992.0);
-}
-
 template <int RV>
 __global__ __launch_bounds__(256) void als_init_kernel(int64_t row0, int64_t n, int R, uint32_t seed, int nonneg,
                                                       float* __restrict__ out) {

@@ -60,6 +60,14 @@ __host__ __device__ __forceinline__ uint32_t row_key(uint32_t seed, int64_t row)
   uint32_t hi = (uint32_t)((uint64_t)row >> 32);
   return fmix32(seed ^ fmix32(lo * 0x9E3779B1u + hi * 0x7FEB352Du + 0x165667B1u));
 }
+// U[0,1) fp64 keyed on (seed, stream, global row): bitwise the draw of
+// ops/sampling.py::uniform (53 bits from two hashes).
+__host__ __device__ __forceinline__ double hash_uniform(uint32_t seed, uint32_t stream, int64_t row) {
+  const uint32_t sv = seed * 0x2545F491u + stream * 0x9E3779B9u;
+  const uint32_t k = row_key(sv, row);
+  const uint32_t k2 = fmix32(k ^ 0x68E31DA4u);
+  return ((double)(k >> 5) * 67108864.0 + (double)(k2 >> 6)) * (1.0 / 9007199254740992.0);
+}
 // --- wave / block reductions -------------------------------------------------
 template <int WIDTH>
 __device__ __forceinline__ float group_sum(float v) {

@@ -690,6 +690,31 @@ __global__ __launch_bounds__(256) void tree_sibling_kernel(const double* __restr
   hsb[2] = fb == 0 ? (y2 > 0.0 ? y2 : 0.0) : y2;
 }
 
+// Per-tree row weights of a forest in one pass: out[t][i] = w[i] * draw(seed_t, rows[i])
+// with draw = Poisson(lam) by CDF inversion over `table` (cdf_0 .. cdf_{kmax-1}, fp64,
+// built by the caller exactly as ops/sampling.py does) or Bernoulli(rate) -- the same
+// draws as sampling.poisson_counts / bernoulli_mask (stream 1 / stream 0).
+__global__ __launch_bounds__(256) void forest_weights_kernel(const int64_t* __restrict__ rows, int64_t n,
+                                                             const uint32_t* __restrict__ seeds,
+                                                             const double* __restrict__ table, int kmax,
+                                                             float rate, const float* __restrict__ w,
+                                                             float* __restrict__ out) {
+  const int t = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t r = rows[i];
+  float v;
+  if (table) {
+    const double u = hash_uniform(seeds[t], 1u, r);
+    int k = 0;
+    for (int j = 0; j < kmax; ++j) k += table[j] < u;
+    v = (float)k;
+  } else {
+    v = hash_uniform(seeds[t], 0u, r) < (double)rate ? 1.f : 0.f;
+  }
+  out[(int64_t)t * n + i] = w ? w[i] * v : v;
+}
+
 }  // namespace
 
 // acc[order[p]] += it_val[i] for p in [it_lo[i], it_hi[i]) (items of leaf segments).
@@ -857,6 +882,18 @@ O3S_API int o3s_tree_sibling(const double* Hs, const double* parent, const uint8
   const int64_t n = P * FB;
   hipLaunchKernelGGL(tree_sibling_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, Hs, parent, sr, P, FB,
                      S, cls, H);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+// rows: int64 [n] global row ids; seeds: uint32 [T]; table: fp64 [kmax] (Poisson) or null
+// (Bernoulli with `rate`); w: fp32 [n] or null; out: fp32 [T][n].
+O3S_API int o3s_forest_weights(const int64_t* rows, int64_t n, const uint32_t* seeds, int T, const double* table,
+                               int kmax, float rate, const float* w, float* out, hipStream_t st) {
+  if (n <= 0 || T <= 0) return 0;
+  if (T > 65535 || (table && kmax <= 0)) return -1;
+  hipLaunchKernelGGL(forest_weights_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)T), dim3(256), 0, st, rows, n,
+                     seeds, table, kmax, rate, w, out);
   O3S_CHECK_LAUNCH();
   return 0;
 }

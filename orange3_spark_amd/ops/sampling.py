@@ -45,20 +45,24 @@ def bernoulli_mask(rows: torch.Tensor, seed: int, fraction: float) -> torch.Tens
     return uniform(rows, seed) < fraction
 
 
+def poisson_table(lam: float, device) -> torch.Tensor:
+    """fp64 CDF table cdf_0..cdf_{kmax-1} of Poisson(lam), accumulated on ``device``."""
+    kmax = int(lam + 12 * (lam ** 0.5) + 12)
+    p = torch.exp(torch.tensor(-lam, dtype=torch.float64, device=device))
+    cdf = [p]
+    for i in range(1, kmax):
+        p = p * (lam / i)
+        cdf.append(cdf[-1] + p)
+    return torch.stack(cdf).contiguous()
+
+
 def poisson_counts(rows: torch.Tensor, seed: int, lam: float) -> torch.Tensor:
-    """Poisson(lam) draw per row by inversion of the CDF (lam is small for sampling)."""
+    """Poisson(lam) draw per row by inversion of the CDF (lam is small for sampling).
+
+    k = #{j : cdf_j < u} over the CDF table cdf_0..cdf_{kmax-1} (the same fp64 partial
+    sums, accumulated in the same order on the same device, as a per-row loop would
+    build) -- one searchsorted instead of a loop with a device sync per term."""
     if lam <= 0:
         return torch.zeros_like(rows)
     u = uniform(rows, seed, stream=1)
-    k = torch.zeros_like(rows)
-    p = torch.exp(torch.tensor(-lam, dtype=torch.float64, device=rows.device)).expand_as(u).clone()
-    cdf = p.clone()
-    kmax = int(lam + 12 * (lam ** 0.5) + 12)
-    for i in range(1, kmax + 1):
-        more = u > cdf
-        if not bool(more.any()):
-            break
-        k = k + more.to(k.dtype)
-        p = p * (lam / i)
-        cdf = cdf + p
-    return k
+    return torch.searchsorted(poisson_table(lam, rows.device), u, right=False).to(rows.dtype)

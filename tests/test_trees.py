@@ -406,3 +406,30 @@ def test_gpu_sibling_kernel_matches_torch(gpu, cls):
     ref = T.sibling_hists(Hs, parent, sr, cls)
     got = T.sibling_hists(Hs.to(gpu), parent.to(gpu), sr, cls).cpu()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bootstrap,rate", [(True, 1.0), (True, 0.7), (False, 0.6)])
+def test_gpu_forest_weights_kernel_matches_sampling(gpu, bootstrap, rate, monkeypatch):
+    """forest_weights_kernel draws bitwise the per-tree weights of the torch sampling path."""
+    from orange3_spark_amd.models import trees as TR
+    n = 100_003
+    rows = torch.arange(5_000, 5_000 + n, dtype=torch.int64)
+    w = torch.rand(n, generator=torch.Generator().manual_seed(1))
+    ref = [TR.subsample_weights(None, rows, rate, 11 * 7919 + t, bootstrap) * w for t in range(3)]
+    seen = {}
+
+    class _Stop(Exception):
+        pass
+
+    def grab(self):
+        seen["ws"] = [x.cpu() for x in self.ws]
+        raise _Stop
+
+    monkeypatch.setattr(TR.TreeBuilder, "build_many", grab)
+    bins = torch.zeros((n, 2), dtype=torch.uint8, device=gpu)
+    with pytest.raises(_Stop):
+        TR.fit_forest(None, bins, [np.zeros(0), np.zeros(0)], torch.zeros(n, device=gpu), w.to(gpu), 3, "gini", 2,
+                      3, 1.0, 0.0, rate, 1.0, 11, rows.to(gpu), bootstrap)
+    for a, b in zip(seen["ws"], ref):
+        assert torch.equal(a, b.float())
