@@ -167,6 +167,27 @@ def upload(arr, dev) -> torch.Tensor:
     return p.to(dev, non_blocking=True)
 
 
+def upload_many(dev, *arrays) -> list:
+    """Several small host arrays -> device tensors through ONE staged copy: the arrays
+    are packed (8-byte aligned) into one pinned buffer and the device tensors are typed
+    views into its device copy."""
+    import numpy as np
+    arrs = [np.ascontiguousarray(a) for a in arrays]
+    offs, total = [], 0
+    for a in arrs:
+        offs.append(total)
+        total += (a.nbytes + 7) // 8 * 8
+    buf = np.zeros(max(total, 8), dtype=np.uint8)
+    for a, o in zip(arrs, offs):
+        buf[o:o + a.nbytes] = a.view(np.uint8).reshape(-1)
+    d = upload(buf, dev)
+    out = []
+    for a, o in zip(arrs, offs):
+        dt = torch.from_numpy(np.zeros(0, dtype=a.dtype)).dtype
+        out.append(d[o:o + a.nbytes].view(dt).view(a.shape))
+    return out
+
+
 def stream_of(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 

@@ -81,11 +81,10 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     it_lo_h = lo[seg_of] + (np.arange(n_items) - first[seg_of]) * chunk
     it_hi_h = np.minimum(it_lo_h + chunk, hi[seg_of])
     seg_first = np.append(first, n_items)
-    i64 = N.upload(np.concatenate([it_lo_h, it_hi_h, seg_first, lo]), dev)
+    fb = np.concatenate([_host(s_feat).astype(np.int32)[seg_of], _host(s_bin).astype(np.int32)[seg_of]])
+    i64, i32 = N.upload_many(dev, np.concatenate([it_lo_h, it_hi_h, seg_first, lo]).astype(np.int64), fb)
     it_lo, it_hi = i64[:n_items], i64[n_items:2 * n_items]
     seg_first_d, seg_lo_d = i64[2 * n_items:2 * n_items + nseg + 1], i64[2 * n_items + nseg + 1:]
-    fb = np.concatenate([_host(s_feat).astype(np.int32)[seg_of], _host(s_bin).astype(np.int32)[seg_of]])
-    i32 = N.upload(fb, dev)
     it_feat, it_bin = i32[:n_items], i32[n_items:]
     work = torch.empty(3 * n_items + nseg, dtype=torch.int64, device=dev)
     it_left, dst_left, dst_right = work[:n_items], work[n_items:2 * n_items], work[2 * n_items:3 * n_items]
@@ -141,8 +140,8 @@ def leaf_apply(order: torch.Tensor, seg_lo: torch.Tensor, seg_hi: torch.Tensor, 
     seg_of = np.repeat(np.arange(len(lo)), n_it)
     it_lo = lo[seg_of] + (np.arange(n_items) - first[seg_of]) * chunk
     it_hi = np.minimum(it_lo + chunk, hi[seg_of])
-    i64 = N.upload(np.concatenate([it_lo, it_hi]), dev)
-    fv = N.upload(val[seg_of], dev)
+    i64, fv = N.upload_many(dev, np.concatenate([it_lo, it_hi]).astype(np.int64),
+                            np.ascontiguousarray(val[seg_of], dtype=np.float64))
     N.check(N.kernels().o3s_tree_leaf_apply(order.data_ptr(), i64[:n_items].data_ptr(), i64[n_items:].data_ptr(),
                                             fv.data_ptr(), n_items, acc.data_ptr(), N.stream_of(acc)),
             "tree_leaf_apply")
