@@ -52,10 +52,14 @@ class Estimator(Params, ABC):
             return [self.fit(dataset, p) for p in params]
         if not _is_param_map(params):
             raise TypeError(f"Params must be either a param map or a list/tuple of param maps, but got {type(params)}.")
+        import time
+        from ..parallel.comm import COMM_STATS
+        c0 = {k: tuple(v) for k, v in COMM_STATS.items()}
+        t0 = time.perf_counter()
         with trace(f"{type(self).__name__}.fit"):
-            if params:
-                return self.copy(params)._fit(dataset)
-            return self._fit(dataset)
+            model = self.copy(params)._fit(dataset) if params else self._fit(dataset)
+        _attach_fit_stats(model, dataset, time.perf_counter() - t0, c0, COMM_STATS)
+        return model
 
     def fitMultiple(self, dataset, paramMaps):
         for i, pm in enumerate(paramMaps):
@@ -64,6 +68,28 @@ class Estimator(Params, ABC):
     @abstractmethod
     def _fit(self, dataset):
         raise NotImplementedError
+
+
+def _attach_fit_stats(model, dataset, seconds, c0, c1):
+    """``model.fitStats``: this rank's wall time of the fit, its local rows and the
+    collectives it issued (calls / bytes per op) -- the per-fit observability summary
+    (iterations and loss curves live on ``model.summary`` as in Spark).  Cheap: no
+    device sync and no collective of its own."""
+    try:
+        n_local = int(len(dataset)) if hasattr(dataset, "__len__") else None
+    except Exception:  # noqa: BLE001 - a dataset without a cheap local length
+        n_local = None
+    comm = {}
+    for op, (calls, nbytes) in c1.items():
+        a, b = c0.get(op, (0, 0))
+        if calls - a:
+            comm[op] = {"calls": calls - a, "bytes": nbytes - b}
+    stats = {"seconds": seconds, "rows_local": n_local,
+             "rows_per_s_local": (n_local / seconds) if (n_local and seconds > 0) else None, "collectives": comm}
+    try:
+        model.fitStats = stats
+    except Exception:  # noqa: BLE001 - models that forbid new attributes
+        pass
 
 
 class Model(Transformer, ABC):

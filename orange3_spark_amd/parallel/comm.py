@@ -284,6 +284,7 @@ def make_comm(device: torch.device | str, world_size: int | None = None, timeout
 
 
 # ------------------------------------------------------------ tracing + failure wrapping
+COMM_STATS: dict = {}        # op -> [calls, bytes of the first tensor argument], process-wide
 def _guard(name, fn):
     """Trace a collective, apply fault injection, and turn backend exceptions into
     CommError carrying op/rank/world (runtime/faults.py)."""
@@ -293,6 +294,10 @@ def _guard(name, fn):
 
     def wrapper(self, *a, **k):
         INJECTOR.hit(op)
+        st = COMM_STATS.setdefault(name, [0, 0])          # always-on: calls, tensor bytes (no sync)
+        st[0] += 1
+        if a and isinstance(a[0], torch.Tensor):
+            st[1] += a[0].numel() * a[0].element_size()
         with trace(op):
             try:
                 return fn(self, *a, **k)

@@ -145,3 +145,14 @@ def test_checkpoint_key_tracks_data_and_completed_fits_clear(tmp_path):
     s.conf.set("spark.checkpoint.dir", "")
     fresh = KMeans(k=3, seed=1, maxIter=6, tol=0.0).fit(x2)
     np.testing.assert_allclose(np.array(got.clusterCenters()), np.array(fresh.clusterCenters()), atol=1e-12)
+
+
+def test_fit_stats_attached():
+    """Every fitted model carries fitStats: wall seconds, local rows, collectives issued."""
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.ml.classification import LogisticRegression
+    df = Session(SessionConf().set("o3s.device", "cpu")).synthetic.classification(500, 4, seed=1)
+    m = LogisticRegression(maxIter=5).fit(df)
+    st = m.fitStats
+    assert st["seconds"] > 0 and st["rows_local"] == 500 and st["rows_per_s_local"] > 0
+    assert isinstance(st["collectives"], dict)
