@@ -253,7 +253,7 @@ def partition_torch(bins, order, s_lo, s_hi, s_feat, s_bin, out=None, payload=()
 
 def node_hist(bins: torch.Tensor, order: torch.Tensor, y: torch.Tensor, w: torch.Tensor | None,
               seg_lo: torch.Tensor, seg_hi: torch.Tensor, seg_node: torch.Tensor, n_nodes: int, B: int, S: int,
-              cls: bool, chunk: int = 1 << 13, ypos: bool = False) -> torch.Tensor:
+              cls: bool, chunk: int | None = None, ypos: bool = False) -> torch.Tensor:
     """Histograms [n_nodes, F, B, S] (fp64) of rows order[lo:hi] for each segment -> node.
 
     ``ypos``: y / w are in position order (y[p] is the label of row order[p], kept so
@@ -271,6 +271,7 @@ def node_hist(bins: torch.Tensor, order: torch.Tensor, y: torch.Tensor, w: torch
     relies on."""
     F = bins.shape[1]
     dev = bins.device
+    chunk = chunk or HIST_CHUNK
     if len(seg_lo) == 0:
         return torch.zeros((n_nodes, F, B, S), dtype=torch.float64, device=dev)
     if not hist_kernel_ok(bins, B, S, cls):
@@ -341,6 +342,7 @@ def sibling_hists(Hs: torch.Tensor, parent: torch.Tensor, small_right, cls: bool
 
 
 _RUN = 64      # slab rows per first-stage partial
+HIST_CHUNK = 1 << 13  # rows per histogram work item (4096: same speed, 16384: +5% per tree)
 
 
 class _HistPlan:
