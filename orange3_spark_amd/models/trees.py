@@ -395,43 +395,49 @@ class TreeBuilder:
             if depth == 0:
                 root_w = w_np.copy()
             bf, bb = bi // (B - 1), bi % (B - 1)
+            do_split = (bg > self.min_gain) & (bg > 0) & np.isfinite(bg) & (depth < self.max_depth)
+            tsplit.__exit__(None, None, None)
+            old_order = order
+            if do_split.any():
+                # the partition is launched first: the tree bookkeeping and the leaf
+                # updates below run on the host while it executes
+                tpart = trace("tree.partition")
+                tpart.__enter__()
+                st, sn = seg_tree[do_split], seg_nid[do_split]
+                s_lo, s_hi = seg_lo[do_split], seg_hi[do_split]
+                pay = (yp,) if wp is None else (yp, wp)
+                if pingpong:
+                    pout = (y_sp,) if wp is None else (y_sp, w_sp)
+                    new_order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
+                                                   bins_t=self.bins_t, out=spare, payload=pay, payload_out=pout)
+                    spare, order = order, new_order
+                    y_sp, yp = yp, y_sp
+                    w_sp, wp = wp, w_sp
+                else:
+                    pout = tuple(t.clone() for t in pay)
+                    order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
+                                               bins_t=self.bins_t, payload=pay, payload_out=pout)
+                    yp, wp = pout[0], (pout[1] if len(pout) > 1 else None)
+                # integer gather (a boolean mask index would sync on the device-side nonzero)
+                parent_H = H.index_select(0, N.upload(np.nonzero(do_split)[0], dev))
+                small_right = (wr_np < wl_np)[do_split]
+                tpart.__exit__(None, None, None)
             value[seg_tree, seg_nid] = vals_np
             impurity[seg_tree, seg_nid] = imp_np
             count[seg_tree, seg_nid] = w_np
-            do_split = (bg > self.min_gain) & (bg > 0) & np.isfinite(bg) & (depth < self.max_depth)
-            tsplit.__exit__(None, None, None)
             if leaf_acc is not None and not do_split.all():
-                with trace("tree.leaf_apply"):
+                with trace("tree.leaf_apply"):          # finished segments: rows in the pre-split order
                     lf = ~do_split
-                    T.leaf_apply(order, seg_lo[lf], seg_hi[lf], value[seg_tree[lf], seg_nid[lf], 0] * leaf_scale,
+                    T.leaf_apply(old_order, seg_lo[lf], seg_hi[lf], value[seg_tree[lf], seg_nid[lf], 0] * leaf_scale,
                                  leaf_acc)
             if not do_split.any():
                 break
             tpart = trace("tree.partition")
             tpart.__enter__()
-            st, sn = seg_tree[do_split], seg_nid[do_split]
             feature[st, sn] = bf[do_split]
             split_bin[st, sn] = bb[do_split]
             threshold[st, sn] = [float(self.splits[f_][b_]) for f_, b_ in zip(bf[do_split], bb[do_split])]
             gain[st, sn] = bg[do_split]
-            # --- partition the splitting segments
-            s_lo, s_hi = seg_lo[do_split], seg_hi[do_split]
-            # integer gather (a boolean mask index would sync on the device-side nonzero)
-            parent_H = H.index_select(0, N.upload(np.nonzero(do_split)[0], dev))
-            small_right = (wr_np < wl_np)[do_split]
-            pay = (yp,) if wp is None else (yp, wp)
-            if pingpong:
-                pout = (y_sp,) if wp is None else (y_sp, w_sp)
-                new_order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
-                                               bins_t=self.bins_t, out=spare, payload=pay, payload_out=pout)
-                spare, order = order, new_order
-                y_sp, yp = yp, y_sp
-                w_sp, wp = wp, w_sp
-            else:
-                pout = tuple(t.clone() for t in pay)
-                order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
-                                           bins_t=self.bins_t, payload=pay, payload_out=pout)
-                yp, wp = pout[0], (pout[1] if len(pout) > 1 else None)
             mid = s_lo + nleft.cpu().numpy().astype(np.int64)
             seg_lo = np.stack([s_lo, mid], 1).reshape(-1)
             seg_hi = np.stack([mid, s_hi], 1).reshape(-1)
