@@ -247,6 +247,7 @@ class TreeBuilder:
 
     hist_subtraction = True         # False: scan every node at every level (reference path)
     batch_trees = True              # False: forests grow one tree at a time (reference path)
+    final_from_parent = True        # False: the last level is histogrammed like any other (reference path)
 
     def __init__(self, comm, bins: torch.Tensor, splits: list, y: torch.Tensor, w,
                  impurity: str, num_classes: int, max_depth: int = 5, min_instances: float = 1.0,
@@ -398,6 +399,17 @@ class TreeBuilder:
             do_split = (bg > self.min_gain) & (bg > 0) & np.isfinite(bg) & (depth < self.max_depth)
             tsplit.__exit__(None, None, None)
             old_order = order
+            is_leaf = ~do_split                                # segments that end here
+            if do_split.any() and depth == self.max_depth - 1 and self.final_from_parent:
+                # children are at maxDepth, i.e. leaves: their stats come from the parent's
+                # histogram (left = bins <= split bin of the split feature, right = rest) and
+                # one routing pass applies the leaf values / sums the REG w*y^2 -- no
+                # partition, no histogram and no split search for the last level
+                with trace("tree.final_level"):
+                    self._final_level(H, do_split, bf, bb, bg, seg_lo, seg_hi, seg_tree, seg_nid, order, yp, wp,
+                                      leaf_acc, leaf_scale, value, impurity, count, feature, split_bin, threshold,
+                                      gain)
+                do_split = np.zeros_like(do_split)            # nothing left to grow
             if do_split.any():
                 # the partition is launched first: the tree bookkeeping and the leaf
                 # updates below run on the host while it executes
@@ -425,9 +437,9 @@ class TreeBuilder:
             value[seg_tree, seg_nid] = vals_np
             impurity[seg_tree, seg_nid] = imp_np
             count[seg_tree, seg_nid] = w_np
-            if leaf_acc is not None and not do_split.all():
+            if leaf_acc is not None and is_leaf.any():
                 with trace("tree.leaf_apply"):          # finished segments: rows in the pre-split order
-                    lf = ~do_split
+                    lf = is_leaf
                     T.leaf_apply(old_order, seg_lo[lf], seg_hi[lf], value[seg_tree[lf], seg_nid[lf], 0] * leaf_scale,
                                  leaf_acc)
             if not do_split.any():
@@ -447,6 +459,46 @@ class TreeBuilder:
             # empty local segments still participate (other ranks may have rows there)
         return [Tree(feature[t], threshold[t], split_bin[t], value[t], impurity[t], gain[t], count[t], F)
                 for t in range(Tn)]
+
+    def _final_level(self, H, do_split, bf, bb, bg, seg_lo, seg_hi, seg_tree, seg_nid, order, yp, wp, leaf_acc,
+                     leaf_scale, value, impurity, count, feature, split_bin, threshold, gain):
+        dev = H.device
+        idx = np.nonzero(do_split)[0]
+        P = len(idx)
+        st, sn = seg_tree[idx], seg_nid[idx]
+        feature[st, sn] = bf[idx]
+        split_bin[st, sn] = bb[idx]
+        threshold[st, sn] = [float(self.splits[f_][b_]) for f_, b_ in zip(bf[idx], bb[idx])]
+        gain[st, sn] = bg[idx]
+        idx_d, bf_d, bb_d = (N.upload(a.astype(np.int64), dev) for a in (idx, bf[idx], bb[idx]))
+        Hp = H.index_select(0, idx_d)                                        # [P, F, B, S]
+        ar = torch.arange(P, device=dev)
+        left = Hp[ar, bf_d].cumsum(1)[ar, bb_d]                               # [P, S]
+        tot = Hp[:, 0].sum(1)                                                 # node totals (feature 0)
+        child = torch.stack([left, tot - left], 1).cpu().numpy()              # [P, 2, S]
+        w_ch = child[..., :].sum(-1) if self.cls else child[..., 0]
+        V = self.S if self.cls else 1
+        if self.cls:
+            vals = child / np.maximum(w_ch, 1e-300)[..., None]
+        else:
+            vals = (child[..., 1] / np.maximum(w_ch, 1e-300))[..., None]
+        s_lo, s_hi = seg_lo[idx], seg_hi[idx]
+        y2 = T.final_level(self.bins, order, s_lo, s_hi, bf[idx], bb[idx], vals[:, 0, 0] * leaf_scale,
+                           vals[:, 1, 0] * leaf_scale, yp, wp, leaf_acc, need_y2=not self.cls,
+                           bins_t=self.bins_t) if (leaf_acc is not None or not self.cls) else None
+        if self.cls:
+            imp, _ = _impurity(torch.from_numpy(child), self.kind)
+        else:
+            y2 = y2.contiguous()
+            self.comm.all_reduce(y2)
+            stats = np.concatenate([child[..., :2], y2.cpu().numpy()[..., None]], -1)   # [P, 2, 3]
+            imp, _ = _impurity(torch.from_numpy(stats), self.kind)
+        imp = imp.numpy()
+        for side in (0, 1):
+            nid = 2 * sn + side
+            value[st, nid] = vals[:, side].reshape(P, V)
+            impurity[st, nid] = imp[:, side]
+            count[st, nid] = w_ch[:, side]
 
 
 # ----------------------------------------------------------------------------- ensembles

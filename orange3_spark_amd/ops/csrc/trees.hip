@@ -272,6 +272,47 @@ __global__ __launch_bounds__(kPartThreads) void tree_part_count_kernel(
   }
 }
 
+// Last split level of a tree (children at maxDepth are leaves): instead of partitioning
+// the rows and histogramming the children, one pass over every splitting segment
+// routes each row by its split (bins[row][feat] <= bin) and
+//   * (boosting, acc != null) adds the child's leaf value to the row's prediction,
+//   * accumulates the child's sum of w*y^2 (REG impurity; the children's w and w*y come
+//     from the parent's histogram) as one fp32 partial per (item, side).
+// Rows are read in position order (y / w are position-ordered payloads).
+__global__ __launch_bounds__(kPartThreads) void tree_final_level_kernel(
+    const uint8_t* __restrict__ bins, int64_t rs, int64_t cs, const int32_t* __restrict__ order,
+    const int64_t* __restrict__ it_lo, const int64_t* __restrict__ it_hi, const int32_t* __restrict__ it_feat,
+    const int32_t* __restrict__ it_bin, const double* __restrict__ it_vl, const double* __restrict__ it_vr,
+    const float* __restrict__ y, const float* __restrict__ w, double* __restrict__ acc, float* __restrict__ part) {
+  __shared__ float red[2][kPartWaves];
+  const int64_t lo = it_lo[blockIdx.x], hi = it_hi[blockIdx.x];
+  const int feat = it_feat[blockIdx.x], bin = it_bin[blockIdx.x];
+  const double vl = acc ? it_vl[blockIdx.x] : 0.0, vr = acc ? it_vr[blockIdx.x] : 0.0;
+  float sl = 0.f, sr = 0.f;
+  for (int64_t p = lo + threadIdx.x; p < hi; p += kPartThreads) {
+    const int32_t row = order[p];
+    const bool l = goes_left(bins, rs, cs, row, feat, bin);
+    if (acc) acc[row] += l ? vl : vr;
+    if (part) {
+      const float yy = y[p], ww = w ? w[p] : 1.f;
+      const float v = ww * yy * yy;
+      sl += l ? v : 0.f;
+      sr += l ? 0.f : v;
+    }
+  }
+  if (!part) return;
+  sl = wave_sum(sl);
+  sr = wave_sum(sr);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) { red[0][wid] = sl; red[1][wid] = sr; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    float a = 0.f;
+    for (int q = 0; q < kPartWaves; ++q) a += red[threadIdx.x][q];
+    part[(int64_t)blockIdx.x * 2 + threadIdx.x] = a;
+  }
+}
+
 __global__ __launch_bounds__(kPartThreads) void tree_part_scatter_kernel(
     const int32_t* __restrict__ order, int32_t* __restrict__ out,
     const int64_t* __restrict__ it_lo, const int64_t* __restrict__ it_hi, const int32_t* __restrict__ it_feat,
@@ -894,6 +935,20 @@ O3S_API int o3s_forest_weights(const int64_t* rows, int64_t n, const uint32_t* s
   if (T > 65535 || (table && kmax <= 0)) return -1;
   hipLaunchKernelGGL(forest_weights_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)T), dim3(256), 0, st, rows, n,
                      seeds, table, kmax, rate, w, out);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+// Items as in o3s_tree_partition (it_vl / it_vr: leaf values of the item's left / right
+// child); acc (fp64 [n_rows]) and part (fp32 [n_items][2]) may each be null.
+O3S_API int o3s_tree_final_level(const uint8_t* bins, int64_t rs, int64_t cs, const int32_t* order,
+                                 const int64_t* it_lo, const int64_t* it_hi, const int32_t* it_feat,
+                                 const int32_t* it_bin, const double* it_vl, const double* it_vr, const float* y,
+                                 const float* w, double* acc, float* part, int n_items, hipStream_t st) {
+  if (n_items <= 0) return 0;
+  if (part && !y) return -1;
+  hipLaunchKernelGGL(tree_final_level_kernel, dim3(n_items), dim3(kPartThreads), 0, st, bins, rs, cs, order, it_lo,
+                     it_hi, it_feat, it_bin, it_vl, it_vr, y, w, acc, part);
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -112,6 +112,76 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     return new_order, nleft
 
 
+def final_level(bins: torch.Tensor, order: torch.Tensor, s_lo, s_hi, s_feat, s_bin, vl, vr, y: torch.Tensor,
+                w: torch.Tensor | None, acc: torch.Tensor | None, need_y2: bool,
+                bins_t: torch.Tensor | None = None, chunk: int = 1 << 14):
+    """Last split level of a tree: rows of every splitting segment are routed by its
+    split; ``acc`` (fp64 [n], boosting) gets the left / right child's leaf value per row
+    (``vl`` / ``vr`` per segment) and, with ``need_y2``, the children's sums of w*y^2
+    (fp64 [nseg, 2]: left, right; y / w in position order) are returned, else None.
+
+    GPU: ``tree_final_level_kernel`` + ordered fp64 range sums; CPU: torch."""
+    lo, hi = _host(s_lo), _host(s_hi)
+    nseg = len(lo)
+    dev = bins.device
+    vl = np.asarray(vl, dtype=np.float64)
+    vr = np.asarray(vr, dtype=np.float64)
+    if nseg == 0:
+        return torch.zeros((0, 2), dtype=torch.float64, device=dev) if need_y2 else None
+    if not (bins.is_cuda and order.dtype == torch.int32):
+        F = bins.shape[1]
+        lens = np.maximum(hi - lo, 0)
+        sid = np.repeat(np.arange(nseg), lens)
+        pos = torch.from_numpy(np.concatenate([np.arange(a, b) for a, b in zip(lo, hi)]) if lens.sum()
+                               else np.zeros(0, dtype=np.int64)).to(dev)
+        rows = order[pos].long()
+        fe = torch.from_numpy(_host(s_feat)[sid]).to(dev)
+        bb = torch.from_numpy(_host(s_bin)[sid]).to(dev)
+        left = bins.view(-1)[rows * F + fe].to(torch.int64) <= bb
+        sid_t = torch.from_numpy(sid).to(dev)
+        if acc is not None:
+            v = torch.where(left, torch.from_numpy(vl[sid]).to(dev), torch.from_numpy(vr[sid]).to(dev))
+            acc.index_add_(0, rows.to(acc.device), v.to(acc.dtype))
+        if not need_y2:
+            return None
+        yy = y[pos].to(torch.float64)
+        ww = torch.ones_like(yy) if w is None else w[pos].to(torch.float64)
+        out = torch.zeros((nseg, 2), dtype=torch.float64, device=dev)
+        out.view(-1).index_add_(0, sid_t * 2 + (~left).long(), ww * yy * yy)
+        return out
+    n_it = (np.maximum(hi - lo, 0) + chunk - 1) // chunk
+    first = np.cumsum(n_it) - n_it
+    n_items = int(n_it.sum())
+    if n_items == 0:
+        return torch.zeros((nseg, 2), dtype=torch.float64, device=dev) if need_y2 else None
+    seg_of = np.repeat(np.arange(nseg), n_it)
+    it_lo = lo[seg_of] + (np.arange(n_items) - first[seg_of]) * chunk
+    it_hi = np.minimum(it_lo + chunk, hi[seg_of])
+    fb = np.concatenate([_host(s_feat).astype(np.int32)[seg_of], _host(s_bin).astype(np.int32)[seg_of]])
+    r_lo, r_cnt = first, n_it
+    i64, i32, f64 = N.upload_many(dev, np.concatenate([it_lo, it_hi, r_lo, r_cnt]).astype(np.int64), fb,
+                                  np.concatenate([vl[seg_of], vr[seg_of]]))
+    part = torch.empty((n_items, 2), dtype=torch.float32, device=dev) if need_y2 else None
+    yf = y.to(torch.float32).contiguous() if need_y2 else None
+    wf = None if (w is None or not need_y2) else w.to(torch.float32).contiguous()
+    src, rs, cs = (bins_t, 1, bins.shape[0]) if bins_t is not None else (bins, bins.shape[1], 1)
+    lib = N.kernels()
+    st = N.stream_of(bins)
+    N.check(lib.o3s_tree_final_level(src.data_ptr(), rs, cs, order.data_ptr(), i64[:n_items].data_ptr(),
+                                     i64[n_items:2 * n_items].data_ptr(), i32[:n_items].data_ptr(),
+                                     i32[n_items:].data_ptr(), f64[:n_items].data_ptr(), f64[n_items:].data_ptr(),
+                                     N.ptr(yf), N.ptr(wf), N.ptr(acc), N.ptr(part), n_items, st), "tree_final_level")
+    if not need_y2:
+        return None
+    out = torch.empty((nseg, 2), dtype=torch.float64, device=dev)
+    rl, rc = i64[2 * n_items:2 * n_items + nseg], i64[2 * n_items + nseg:]
+    for a in range(0, nseg, 65535):                           # item partials summed per segment, in order
+        b = min(a + 65535, nseg)
+        N.check(lib.o3s_slab_range_sum(part.data_ptr(), 0, 2, rl[a:].data_ptr(), rc[a:].data_ptr(), b - a,
+                                       out[a:].data_ptr(), st), "slab_range_sum")
+    return out
+
+
 def leaf_apply(order: torch.Tensor, seg_lo: torch.Tensor, seg_hi: torch.Tensor, seg_val: torch.Tensor,
                acc: torch.Tensor, chunk: int = 1 << 14) -> None:
     """acc[order[p]] += seg_val[s] for every position p of segment s (fp64 acc).

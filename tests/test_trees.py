@@ -433,3 +433,48 @@ def test_gpu_forest_weights_kernel_matches_sampling(gpu, bootstrap, rate, monkey
                       3, 1.0, 0.0, rate, 1.0, 11, rows.to(gpu), bootstrap)
     for a, b in zip(seen["ws"], ref):
         assert torch.equal(a, b.float())
+
+
+def _final_level_parity(session):
+    from orange3_spark_amd.models.trees import TreeBuilder
+    rng = np.random.default_rng(12)
+    X = rng.uniform(-1, 1, size=(5000, 6))
+    yc = ((X[:, 0] > 0.1) ^ (X[:, 2] > -0.3)).astype(float) + (X[:, 4] > 0.5)
+    yr = np.sin(3 * X[:, 0]) + X[:, 1] * X[:, 3] + 0.1 * rng.normal(size=5000)
+    w = rng.uniform(0.5, 2.0, size=5000)
+    dfc = session.createDataFrame(pd.DataFrame({"features": list(X), "label": yc, "w": w}))
+    dfr = session.createDataFrame(pd.DataFrame({"features": list(X), "label": yr, "w": w}))
+    makers = [(dfr, lambda: GBTRegressor(maxDepth=4, maxIter=4, weightCol="w")),
+              (dfc, lambda: DecisionTreeClassifier(maxDepth=5, impurity="entropy")),
+              (dfc, lambda: RandomForestClassifier(numTrees=3, maxDepth=4, seed=2)),
+              (dfr, lambda: RandomForestRegressor(numTrees=3, maxDepth=5, seed=4, weightCol="w"))]
+    for df, mk in makers:
+        outs = []
+        for flag in (True, False):
+            TreeBuilder.final_from_parent = flag
+            try:
+                m = mk().fit(df)
+            finally:
+                TreeBuilder.final_from_parent = True
+            ts = getattr(m, "_ens", None)
+            trees = ts.trees if ts is not None else [m._tree]
+            outs.append((m.transform(df).toPandas()["prediction"].to_numpy(),
+                         [(t.feature.copy(), t.value.copy(), t.impurity.copy(), t.count.copy()) for t in trees]))
+        # GPU: fp32 per-item slab partials grouped differently (per bin of the parent vs per
+        # child row block) -> leaf sums agree to ~1e-7 relative, compounding over boosting
+        np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-6)
+        for a, b in zip(outs[0][1], outs[1][1]):
+            assert np.array_equal(a[0], b[0])
+            for q in (1, 2, 3):
+                np.testing.assert_allclose(a[q], b[q], rtol=1e-5, atol=1e-6)
+
+
+def test_final_level_from_parent_matches_full_level(cpu):
+    """Leaves at maxDepth from the parent's histogram + one routing pass == histogramming
+    the last level (values, impurities, counts, predictions)."""
+    _final_level_parity(cpu)
+
+
+@pytest.mark.gpu
+def test_gpu_final_level_from_parent_matches_full_level():
+    _final_level_parity(Session(SessionConf().set("o3s.device", "cuda")))
