@@ -59,6 +59,7 @@ _SIGS: dict[str, list] = {
     "o3s_als_cg": [c_i32, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_als_pass": [c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_tree_hist_lds": [c_i32, c_i32, c_i32, c_i32],
+    "o3s_hash_uniform": [c_vp, c_i64, c_i64, c_u32, c_u32, c_i32, c_f64, c_vp, c_vp, c_vp],
     "o3s_tree_final_level": [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                              c_i32, c_vp],
     "o3s_forest_weights": [c_vp, c_i64, c_vp, c_i32, c_vp, c_i32, c_f32, c_vp, c_vp, c_vp],

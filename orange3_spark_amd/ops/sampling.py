@@ -3,8 +3,8 @@
 Spark samples per partition with a per-partition seeded RNG, so results change with
 the partitioning.  Here the draw for a row is a pure function of (seed, global row
 index) via the same fmix32 hash as the synthetic generators: a sample is identical on
-1, 2, 4 or 8 GPUs.  Elementwise on device tensors (trivially HBM bound; torch ops are
-adequate here, SURVEY §2.8 row `df.sample`).
+1, 2, 4 or 8 GPUs.  Device tensors: one ``hash_uniform_kernel`` pass (csrc/sampling.hip,
+SURVEY §2.8 row `df.sample`); host tensors: the same draws as int64 torch ops.
 """
 from __future__ import annotations
 
@@ -15,8 +15,22 @@ from .glm import _fmix32, row_keys
 _MASK = 0xFFFFFFFF
 
 
+def _device_draw(rows: torch.Tensor, seed: int, stream: int, mode: int, p: float = 0.0):
+    """GPU: ``hash_uniform_kernel`` (one pass; bitwise the torch draws below)."""
+    from . import _native as N
+    r = rows.to(torch.int64).contiguous()
+    n = r.numel()
+    out = torch.empty(n, dtype=torch.float64 if mode == 0 else torch.uint8, device=r.device)
+    N.check(N.kernels().o3s_hash_uniform(r.data_ptr(), 0, n, int(seed) & _MASK, int(stream) & _MASK, mode, float(p),
+                                         out.data_ptr() if mode == 0 else None,
+                                         out.data_ptr() if mode == 1 else None, N.stream_of(r)), "hash_uniform")
+    return out.view(rows.shape) if mode == 0 else out.view(rows.shape).to(torch.bool)
+
+
 def uniform(rows: torch.Tensor, seed: int, stream: int = 0) -> torch.Tensor:
     """U[0,1) float64 per global row index."""
+    if rows.is_cuda and rows.numel():
+        return _device_draw(rows, seed, stream, 0)
     k = row_keys((seed * 0x2545F491 + stream * 0x9E3779B9) & _MASK, rows)
     k2 = _fmix32(k ^ 0x68E31DA4)
     hi = (k >> 5).to(torch.float64)          # 27 bits
@@ -42,6 +56,8 @@ def bernoulli_mask(rows: torch.Tensor, seed: int, fraction: float) -> torch.Tens
         return torch.ones_like(rows, dtype=torch.bool)
     if fraction <= 0.0:
         return torch.zeros_like(rows, dtype=torch.bool)
+    if rows.is_cuda and rows.numel():
+        return _device_draw(rows, seed, 0, 1, fraction)
     return uniform(rows, seed) < fraction
 
 

@@ -142,3 +142,15 @@ def test_leaf_index_is_preorder_on_random_trees(seed, depth):
 
 if __name__ == "__main__":
     pytest.main([__file__])
+
+
+@pytest.mark.gpu
+def test_gpu_sampling_draws_bitwise_equal_cpu():
+    """hash_uniform_kernel == the torch draws (uniform, Bernoulli mask, Poisson counts)."""
+    from orange3_spark_amd.ops import sampling
+    rows = torch.cat([torch.arange(0, 100_000), torch.arange(2 ** 33, 2 ** 33 + 1000)])
+    g = rows.to("cuda")
+    for seed, stream in ((0, 0), (12345, 7), (-3, 11), (2 ** 40 + 5, 1)):
+        assert torch.equal(sampling.uniform(g, seed, stream).cpu(), sampling.uniform(rows, seed, stream))
+    assert torch.equal(sampling.bernoulli_mask(g, 9, 0.37).cpu(), sampling.bernoulli_mask(rows, 9, 0.37))
+    assert torch.equal(sampling.poisson_counts(g, 5, 1.0).cpu(), sampling.poisson_counts(rows, 5, 1.0))
