@@ -129,13 +129,34 @@ def aggregate(df, keys: list, aggs: list):
         enc = []
         gid = torch.zeros(n, dtype=torch.int64, device=dev)
         G = 1
-    big = torch.iinfo(torch.int64).max
-    first_row = torch.full((G,), big, dtype=torch.int64, device=dev).scatter_reduce(
-        0, gid, rows, "amin", include_self=True)
-    last_row = torch.full((G,), -1, dtype=torch.int64, device=dev).scatter_reduce(
-        0, gid, rows, "amax", include_self=True)
-    parts: dict = {"__first": first_row, "__last": last_row,
-                   "__rows": torch.bincount(gid, minlength=G).to(torch.float64)}
+    # Rows are grouped once by a stable sort of the group ids; every partial aggregate is
+    # then a segmented reduction over the sorted order (torch.segment_reduce): no
+    # contended atomics (a few thousand groups over millions of rows made scatter /
+    # index_add atomics the bottleneck) and bitwise reproducible sums.
+    if n and keys:
+        perm = torch.argsort(gid, stable=True)
+        counts = torch.bincount(gid, minlength=G)
+    else:
+        perm = None
+        counts = torch.full((1,), n, dtype=torch.int64, device=dev) if G == 1 else torch.bincount(gid, minlength=G)
+    ends = torch.cumsum(counts, 0)
+    starts = ends - counts
+
+    def red(x, op):
+        """per-group reduction of a per-row fp64 tensor (op: sum / min / max)."""
+        if n == 0:
+            fill = {"sum": 0.0, "min": math.inf, "max": -math.inf}[op]
+            return torch.full((G,), fill, dtype=torch.float64, device=dev)
+        xs = x if perm is None else x[perm]
+        return torch.segment_reduce(xs.to(torch.float64), op, lengths=counts, unsafe=True)
+
+    rs = rows if perm is None else rows[perm]
+    if n:
+        first_row, last_row = rs[starts], rs[ends - 1]
+    else:
+        first_row = torch.full((G,), torch.iinfo(torch.int64).max, dtype=torch.int64, device=dev)
+        last_row = torch.full((G,), -1, dtype=torch.int64, device=dev)
+    parts: dict = {"__first": first_row, "__last": last_row, "__rows": counts.to(torch.float64)}
     host_parts: dict = {}
     host_tags: set = set()
     for j, a in enumerate(aggs):
@@ -146,7 +167,7 @@ def aggregate(df, keys: list, aggs: list):
                 parts[tag + "n"] = parts["__rows"]
             else:
                 ok = ~vals.null_mask().to(dev)
-                parts[tag + "n"] = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, ok.double())
+                parts[tag + "n"] = red(ok.double(), "sum")
             continue
         if a.distinct and isinstance(vals, C.NumericColumn) and a.fn in ("count", "sum", "avg"):
             # dedupe (group, value) on the device first; only distinct pairs go to the host
@@ -166,7 +187,7 @@ def aggregate(df, keys: list, aggs: list):
             yv, oky = _values_valid(a.arg2.eval(df), dev)
             ok = okx & oky
             x, yv = torch.where(ok, x, torch.zeros_like(x)), torch.where(ok, yv, torch.zeros_like(yv))
-            z = lambda v: torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, v)  # noqa: E731
+            z = lambda v: red(v, "sum")  # noqa: E731
             parts[tag + "n"] = z(ok.double())
             for sfx, v in (("s", x), ("t", yv), ("q", x * x), ("r", yv * yv), ("p", x * yv)):
                 parts[tag + sfx] = z(v)
@@ -182,21 +203,19 @@ def aggregate(df, keys: list, aggs: list):
             host_tags.add(tag)
             continue
         x, ok = _values_valid(vals, dev)
-        cnt = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, ok.double())
-        parts[tag + "n"] = cnt
+        parts[tag + "n"] = red(ok.double(), "sum")
         moments = ("stddev", "variance", "stddev_pop", "var_pop", "skewness", "kurtosis")
         if a.fn in ("sum", "avg") + moments:
-            parts[tag + "s"] = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, x)
+            parts[tag + "s"] = red(x, "sum")
         if a.fn in moments:
-            parts[tag + "q"] = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, x * x)
+            parts[tag + "q"] = red(x * x, "sum")
         if a.fn in ("skewness", "kurtosis"):
-            parts[tag + "c"] = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, x * x * x)
-            parts[tag + "f"] = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, x * x * x * x)
+            parts[tag + "c"] = red(x * x * x, "sum")
+            parts[tag + "f"] = red(x * x * x * x, "sum")
         if a.fn in ("min", "max"):
             fill = math.inf if a.fn == "min" else -math.inf
             src = torch.where(ok, x, torch.full_like(x, fill))
-            parts[tag + "m"] = torch.full((G,), fill, dtype=torch.float64, device=dev).scatter_reduce(
-                0, gid, src, "amin" if a.fn == "min" else "amax", include_self=True)
+            parts[tag + "m"] = red(src, a.fn)
     # ---- merge partials across ranks by key value
     local_keys = [e[1](uk[:, i].tolist()) for i, e in enumerate(enc)] if keys else []
     table = {name: t.cpu().numpy() for name, t in parts.items()}

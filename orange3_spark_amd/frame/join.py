@@ -35,12 +35,96 @@ def join(left: DataFrame, right: DataFrame, on, how: str = "inner") -> DataFrame
     return _hash_join(left, rfull, on, how)
 
 
+def _key_codes(left: DataFrame, right: DataFrame, on):
+    """Exact per-row key codes (int64 on the left's device) for both sides, or None when
+    a key column is not numeric / string: equal keys <-> equal codes; rows with a null
+    key get -1 (left) / -2 (right) so they never match; NaN equals NaN (Spark)."""
+    dev = left.device
+    per_col = []
+    for k in on:
+        a, b = left._col(k), right._col(k)
+        if isinstance(a, C.NumericColumn) and isinstance(b, C.NumericColumn):
+            fl = a.data.is_floating_point() or b.data.is_floating_point()
+            dt = torch.float64 if fl else torch.int64
+            va, vb = a.data.to(dev, dt), b.data.to(dev, dt)
+            both = torch.cat([va, vb])
+            nan = torch.isnan(both) if fl else torch.zeros_like(both, dtype=torch.bool)
+            if fl:
+                both = torch.where(nan, torch.zeros_like(both), both)
+            _, codes = torch.unique(both, return_inverse=True)
+            codes = torch.where(nan, torch.full_like(codes, int(codes.max().item()) + 1 if codes.numel() else 0),
+                                codes)
+            null = torch.cat([a.null_mask().to(dev), b.null_mask().to(dev)]) if fl or a.valid is not None \
+                or b.valid is not None else torch.zeros_like(codes, dtype=torch.bool)
+            if fl:                                   # null_mask() counts NaN as null: NaN keys stay matchable
+                null = null & ~nan
+            per_col.append((codes, null))
+        elif isinstance(a, C.HostColumn) and isinstance(b, C.HostColumn) and not isinstance(a, C.ArrayColumn) \
+                and not isinstance(b, C.ArrayColumn):
+            import pandas as pd
+            vals = np.concatenate([np.asarray(a.values, dtype=object), np.asarray(b.values, dtype=object)])
+            codes, _ = pd.factorize(pd.Series(vals, dtype=object), use_na_sentinel=True)
+            codes = torch.from_numpy(codes.astype(np.int64)).to(dev)
+            per_col.append((codes, codes < 0))
+        else:
+            return None
+    nl = len(left)
+    if len(per_col) == 1:
+        code, null = per_col[0]
+    else:
+        stacked = torch.stack([c for c, _ in per_col], 1)
+        _, code = torch.unique(stacked, dim=0, return_inverse=True)
+        null = torch.stack([m for _, m in per_col], 1).any(1)
+    code = code.to(torch.int64)
+    lc = torch.where(null[:nl], torch.full_like(code[:nl], -1), code[:nl])
+    rc = torch.where(null[nl:], torch.full_like(code[nl:], -2), code[nl:])
+    return lc, rc
+
+
+def _vector_join(lc: torch.Tensor, rc: torch.Tensor, how: str):
+    """(li, ri) pairs of an equi-join from key codes: left rows in order, each left row's
+    matches in right-row order (stable sort + searchsorted; no per-row Python)."""
+    dev = lc.device
+    nl, nr = lc.numel(), rc.numel()
+    rs, rperm = torch.sort(rc, stable=True)
+    lo = torch.searchsorted(rs, lc, right=False)
+    hi = torch.searchsorted(rs, lc, right=True)
+    cnt = hi - lo
+    if how == "left_semi":
+        return torch.nonzero(cnt > 0).squeeze(1), None
+    if how == "left_anti":
+        return torch.nonzero(cnt == 0).squeeze(1), None
+    take = cnt if how == "inner" else torch.clamp_min(cnt, 1)
+    li = torch.repeat_interleave(torch.arange(nl, device=dev), take)
+    start = torch.cumsum(take, 0) - take
+    off = torch.arange(li.numel(), device=dev) - start[li]
+    has = cnt[li] > 0
+    ri = torch.where(has, rperm[(lo[li] + off).clamp_max(max(nr - 1, 0))] if nr else torch.zeros_like(li),
+                     torch.full_like(li, -1))
+    if how == "outer":
+        ls, _ = torch.sort(lc)
+        rl = torch.searchsorted(ls, rc, right=False)
+        rh = torch.searchsorted(ls, rc, right=True)
+        unmatched = torch.nonzero(rh == rl).squeeze(1)
+        li = torch.cat([li, torch.full_like(unmatched, -1)])
+        ri = torch.cat([ri, unmatched])
+    return li, ri
+
+
 def _keys(df: DataFrame, on):
     lists = [df.column_data(k).to_pylist() for k in on]
     return [tuple(_hashable(v) for v in row) for row in zip(*lists)] if lists else []
 
 
 def _hash_join(left: DataFrame, right: DataFrame, on, how, swap=False) -> DataFrame:
+    codes = _key_codes(left, right, on)
+    if codes is not None:
+        li, ri = _vector_join(codes[0], codes[1], how)
+        li = li.cpu() if li.is_cuda else li
+        if how in ("left_semi", "left_anti"):
+            return left._take(li)
+        out = _assemble(left, right, li, ri.cpu(), on, how)
+        return _restore_order(out, left, right, on) if swap else out
     rk = _keys(right, on)
     table = {}
     for j, k in enumerate(rk):
@@ -75,19 +159,22 @@ def _hash_join(left: DataFrame, right: DataFrame, on, how, swap=False) -> DataFr
             li.append(-1)
             ri.append(int(j))
     out = _assemble(left, right, torch.tensor(li, dtype=torch.int64), torch.tensor(ri, dtype=torch.int64), on, how)
-    if swap:
-        # restore column order: left(original right) columns last
-        cols = OrderedDict()
-        for k in on:
+    return _restore_order(out, left, right, on) if swap else out
+
+
+def _restore_order(out, left, right, on):
+    """right join computed as a swapped left join: restore the column order
+    (join keys, then the original left's columns, then the original right's)."""
+    cols = OrderedDict()
+    for k in on:
+        cols[k] = out._cols[k]
+    for k in right.columns:
+        if k not in on:
             cols[k] = out._cols[k]
-        for k in right.columns:
-            if k not in on:
-                cols[k] = out._cols[k]
-        for k in left.columns:
-            if k not in on and k in out._cols:
-                cols[k] = out._cols[k]
-        return DataFrame(out.session, cols, len(out))
-    return out
+    for k in left.columns:
+        if k not in on and k in out._cols:
+            cols[k] = out._cols[k]
+    return DataFrame(out.session, cols, len(out))
 
 
 def _take_nullable(col: C.Column, idx: torch.Tensor) -> C.Column:
