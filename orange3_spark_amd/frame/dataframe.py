@@ -788,6 +788,22 @@ class GroupedData:
         return _frame_from_pandas(self.df, pd.concat(parts, ignore_index=True) if parts else pd.DataFrame(), schema)
 
 
+def _nullable_column(vals) -> C.Column:
+    """Host column from python values with None = null: numbers stay numeric (long when
+    all are integral, else double) with a validity mask; anything else goes through
+    ``from_numpy``."""
+    present = [v for v in vals if v is not None]
+    if present and all(isinstance(v, (bool, int, float, np.number)) and not isinstance(v, (bool, np.bool_))
+                       for v in present):
+        integral = all(isinstance(v, (int, np.integer)) for v in present)
+        dt = np.int64 if integral else np.float64
+        data = np.array([0 if v is None else v for v in vals], dtype=dt)
+        valid = np.array([v is not None for v in vals])
+        return C.NumericColumn(torch.from_numpy(data), None if valid.all() else torch.from_numpy(valid),
+                               T.LongType() if integral else T.DoubleType())
+    return C.from_numpy(np.array(vals, dtype=object), "cpu")
+
+
 class PivotedData(GroupedData):
     """``groupBy(keys).pivot(col[, values]).agg(...)``: one output column per (pivot value,
     aggregate).  One device aggregation over keys + pivot column, reshaped on the host
@@ -802,7 +818,9 @@ class PivotedData(GroupedData):
         if len(aggs) == 1 and isinstance(aggs[0], dict):
             aggs = tuple(getattr(E, fn if fn != "mean" else "avg")(c).alias(f"{fn}({c})") for c, fn in aggs[0].items())
         local = self.df.session.local_view()
-        keyed = DataFrame(local, aggregate(self.df, self.keys + [self.pivot_expr], list(aggs))).collect()
+        # the pivot key gets its own name: pivoting on a grouping column must not merge the two
+        keyed = DataFrame(local, aggregate(self.df, self.keys + [self.pivot_expr.alias("__pivot__")],
+                                           list(aggs))).collect()
         groups = DataFrame(local, aggregate(self.df, self.keys, [E.count().alias("__n")])).collect()
         nk = len(self.keys)
         values = self.values
@@ -820,5 +838,5 @@ class PivotedData(GroupedData):
                 for g in groups:
                     hit = table.get((tuple(_hashable(x) for x in g[:nk]), _hashable(v)))
                     col.append(None if hit is None else hit[j])
-                out[name] = C.from_numpy(np.array(col, dtype=object), "cpu")
+                out[name] = _nullable_column(col)
         return self.df._from_full(out)

@@ -139,14 +139,93 @@ class Expr:
     def between(self, lo, hi):
         return (self >= lo) & (self <= hi)
 
-    def like(self, pattern: str):
-        rx = re.compile("^" + re.escape(pattern).replace("%", ".*").replace("_", ".") + "$", re.S)
+    def _str_pred(self, fn, label: str):
+        """Boolean predicate over a string column, vectorised through pandas' string
+        methods; a null input gives a null result (Spark)."""
+        def f(df):
+            import pandas as pd
+            c = self.eval(df)
+            vals = c.values if isinstance(c, C.HostColumn) else np.asarray(c.to_pylist(), dtype=object)
+            ser = pd.Series(vals, dtype=object)
+            null = ser.isna().to_numpy()
+            res = fn(ser.astype(str)).to_numpy(dtype=bool, na_value=False) & ~null
+            return C.NumericColumn(torch.from_numpy(res), torch.from_numpy(~null) if null.any() else None,
+                                   T.BooleanType())
+        return Expr(f, label, self.refs)
 
+    @staticmethod
+    def _like_rx(pattern: str) -> str:
+        out = []
+        i = 0
+        while i < len(pattern):                  # SQL LIKE: % and _ wildcards, backslash escapes
+            ch = pattern[i]
+            if ch == "\\" and i + 1 < len(pattern):
+                out.append(re.escape(pattern[i + 1]))
+                i += 2
+                continue
+            out.append(".*" if ch == "%" else "." if ch == "_" else re.escape(ch))
+            i += 1
+        return "".join(out)
+
+    def like(self, pattern: str):
+        rx = re.compile(self._like_rx(pattern), re.S)
+        return self._str_pred(lambda s: s.str.fullmatch(rx), f"({self._name} LIKE '{pattern}')")
+
+    def ilike(self, pattern: str):
+        rx = re.compile(self._like_rx(pattern), re.S | re.I)
+        return self._str_pred(lambda s: s.str.fullmatch(rx), f"({self._name} ILIKE '{pattern}')")
+
+    def rlike(self, pattern: str):
+        rx = re.compile(pattern)
+        return self._str_pred(lambda s: s.str.contains(rx, regex=True), f"RLIKE({self._name}, {pattern})")
+
+    def contains(self, other):
+        v = other.eval_literal() if isinstance(other, Expr) else other
+        return self._str_pred(lambda s: s.str.contains(str(v), regex=False), f"contains({self._name}, {v})")
+
+    def startswith(self, other):
+        v = other.eval_literal() if isinstance(other, Expr) else other
+        return self._str_pred(lambda s: s.str.startswith(str(v)), f"startswith({self._name}, {v})")
+
+    def endswith(self, other):
+        v = other.eval_literal() if isinstance(other, Expr) else other
+        return self._str_pred(lambda s: s.str.endswith(str(v)), f"endswith({self._name}, {v})")
+
+    def substr(self, startPos, length):
+        """1-based substring (Spark ``Column.substr``)."""
         def f(df):
             c = self.eval(df)
-            return C.NumericColumn(torch.tensor([v is not None and bool(rx.match(str(v))) for v in c.values],
-                                                dtype=torch.bool), None, T.BooleanType())
-        return Expr(f, f"({self._name} LIKE '{pattern}')", self.refs)
+            vals = c.values if isinstance(c, C.HostColumn) else np.asarray(c.to_pylist(), dtype=object)
+            st = int(startPos) - 1 if int(startPos) > 0 else int(startPos)
+            out = np.array([None if v is None else
+                            (str(v)[st:st + int(length)] if st >= 0 else str(v)[len(str(v)) + st:][:int(length)])
+                            for v in vals], dtype=object)
+            return C.StringColumn(out)
+        return Expr(f, f"substring({self._name}, {startPos}, {length})", self.refs)
+
+    def eqNullSafe(self, other):
+        """``<=>``: true when both sides are null, false when exactly one is, else ==."""
+        o = other if isinstance(other, Expr) else lit(other)
+
+        def f(df):
+            a, b = self.eval(df), o.eval(df)
+            eq = (self == o).eval(df)
+            na, nb = a.null_mask(), b.null_mask()
+            if nb.numel() == 1 and na.numel() != 1:
+                nb = nb.expand_as(na)
+            d = eq.data.to(torch.bool) if isinstance(eq, C.NumericColumn) else eq
+            res = torch.where(na.to(d.device) | nb.to(d.device), na.to(d.device) & nb.to(d.device), d)
+            return C.NumericColumn(res, None, T.BooleanType())
+        return Expr(f, f"({self._name} <=> {o._name})", tuple(self.refs) + tuple(o.refs))
+
+    def bitwiseAND(self, other):
+        return self._bin(other, "&", torch.bitwise_and)
+
+    def bitwiseOR(self, other):
+        return self._bin(other, "|", torch.bitwise_or)
+
+    def bitwiseXOR(self, other):
+        return self._bin(other, "^", torch.bitwise_xor)
 
     def _ordered(self, desc: bool, nulls_first=None):
         e = Expr(self._fn, self._name, self.refs)

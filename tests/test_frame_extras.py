@@ -229,3 +229,12 @@ def test_rollup_cube_grouping_id_and_misc_surface(tmp_path):
     m = df.mapInArrow(lambda it: (pa.RecordBatch.from_pydict({"w": [x * 2 for x in b.column("v").to_pylist()]})
                                   for b in it), "w double")
     assert [r_.w for r_ in m.collect()] == [2.0, 4.0, 6.0, 8.0, 10.0]
+
+
+def test_pivot_on_grouping_column():
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    df = s.createDataFrame(pd.DataFrame({"k": [1, 2, 1, 3], "x": [1.0, 2.0, 3.0, 4.0]}))
+    r = df.groupBy("k").pivot("k").sum("x").orderBy("k").toPandas()
+    assert list(r.columns) == ["k", "1", "2", "3"]
+    assert r["1"].tolist()[0] == 4.0 and r["2"].tolist()[1] == 2.0 and r["3"].tolist()[2] == 4.0
+    assert r["1"].isna().tolist() == [False, True, True]

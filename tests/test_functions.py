@@ -217,3 +217,25 @@ def test_higher_order_and_round_out_functions():
     st = s.createDataFrame(pd.DataFrame({"id": [1, 2]}))
     st = st.select("id", F.array(F.struct(F.col("id").alias("a"), (F.col("id") * 2).alias("b"))).alias("s"))
     assert st.select("id", F.inline("s")).collect()[1].b == 4
+
+
+def test_column_string_predicates_and_null_safe_eq(s):
+    d = s.createDataFrame(pd.DataFrame({"a": ["apple", "banana", None, "cherry_pie", "a%b"],
+                                        "n": [1, 2, None, 4, 6]}))
+    r = d.select(F.col("a").startswith("a").alias("sw"), F.col("a").endswith("e").alias("ew"),
+                 F.col("a").contains("an").alias("c"), F.col("a").like("%an_na").alias("l"),
+                 F.col("a").rlike("^c.*e$").alias("r"), F.col("a").like("a\\%b").alias("esc"),
+                 F.col("a").ilike("APP%").alias("il"), F.col("a").substr(2, 3).alias("sub"),
+                 F.col("n").eqNullSafe(None).alias("ens"), F.col("n").eqNullSafe(2).alias("en2"),
+                 F.col("n").cast("long").bitwiseAND(3).alias("band")).collect()
+    assert [x.sw for x in r] == [True, False, None, False, True]
+    assert [x.ew for x in r] == [True, False, None, True, False]
+    assert [x.c for x in r] == [False, True, None, False, False]
+    assert [x.l for x in r] == [False, True, None, False, False]
+    assert [x.r for x in r] == [False, False, None, True, False]
+    assert [x.esc for x in r] == [False, False, None, False, True]   # escaped % is literal
+    assert [x.il for x in r] == [True, False, None, False, False]
+    assert [x.sub for x in r] == ["ppl", "ana", None, "her", "%b"]
+    assert [x.ens for x in r] == [False, False, True, False, False]  # null <=> null is true
+    assert [x.en2 for x in r] == [False, True, False, False, False]  # never null
+    assert [x.band for x in r][:2] == [1, 2] and r[4].band == 2

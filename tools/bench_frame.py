@@ -22,3 +22,25 @@ t("join_small", lambda: df.join(small, "k").count())
 t("distinct_k", lambda: df.select("k").distinct().count())
 t("describe", lambda: df.describe("v").collect())
 print(json.dumps(res))
+res2 = {}
+def t2(name, fn):
+    sync(); a = time.perf_counter()
+    try:
+        fn()
+        sync()
+        res2[name] = round(time.perf_counter() - a, 4)
+    except Exception as e:  # noqa: BLE001
+        res2[name] = f"error: {type(e).__name__}: {str(e)[:80]}"
+t2("withColumn_expr", lambda: df.withColumn("z", F.col("v") * 2 + F.col("k")).count())
+t2("fillna", lambda: df.fillna(0.0).count())
+t2("dropna", lambda: df.dropna().count())
+t2("union", lambda: df.union(df).count())
+t2("orderBy_full", lambda: df.orderBy("v").count())
+t2("dropDuplicates", lambda: df.dropDuplicates(["k"]).count())
+t2("pivot", lambda: df.filter(F.col("k") < 10).groupBy("k").pivot("k").count().count())
+t2("sql_groupby", lambda: (df.createOrReplaceTempView("t"), s.sql("SELECT k, COUNT(*) c, AVG(v) a FROM t GROUP BY k").count()))
+t2("toPandas_1M", lambda: df.limit(1_000_000).toPandas())
+from orange3_spark_amd.sql.window import Window
+t2("window_rank_1M", lambda: df.limit(1_000_000).withColumn("r", F.row_number().over(Window.partitionBy("k").orderBy("v"))).count())
+t2("string_ops_1M", lambda: df.limit(1_000_000).withColumn("s", F.concat(F.lit("x"), F.col("k").cast("string"))).filter(F.col("s").startswith("x1")).count())
+print(json.dumps(res2))
