@@ -51,3 +51,30 @@ def test_bench_single_and_four_ranks_agree():
     assert r4["n_gpus"] == 4 and r4["config"]["parallelism"] == "dp4" and r4["config"]["global_batch"] == 24000
     assert abs(r4["first_loss"] - r1["first_loss"]) < 1e-9
     assert abs(r4["final_loss"] - r1["final_loss"]) < 1e-7 * abs(r1["final_loss"])
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_gpu_bench_two_ranks_match_one_rank():
+    """The GPU bench path (mixed resident + lineage kernel, device SGD update, HIP graph at
+    one rank / eager at two) on one MI355X: two ranks share cuda:0 over gloo (RCCL needs a
+    GPU per rank) and must report the one-rank losses."""
+    args = ["--steps", "3", "--warmup", "1", "--rows", "6000000", "--features", "256", "--resident-fraction", "0.002"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    env.pop("WORLD_SIZE", None)
+    one = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert one.returncode == 0, one.stderr[-2000:]
+    r1 = _json_line(one.stdout)
+    assert r1["config"]["device"].startswith("cuda") and r1["config"]["lineage_rows"] > 0
+    assert r1["config"]["resident_rows"] > 0
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+                          *args], cwd=ROOT, env=dict(env, O3S_DIST_BACKEND="gloo"), capture_output=True, text=True,
+                         timeout=240)
+    assert two.returncode == 0, two.stderr[-3000:]
+    r2 = _json_line(two.stdout)
+    assert r2["n_gpus"] == 2 and r2["config"]["global_batch"] == 6000000
+    assert r2["config"]["resident_rows"] + r2["config"]["lineage_rows"] == 6000000
+    assert abs(r2["first_loss"] - r1["first_loss"]) < 1e-6
+    assert abs(r2["final_loss"] - r1["final_loss"]) < 1e-5 * abs(r1["final_loss"])
