@@ -112,7 +112,11 @@ DENSE_MIN_AVG = 0
 
 
 def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, implicit: bool, alpha: float,
-               FtF: torch.Tensor | None, cg_iters: int, nonneg: bool, exact: bool | None = None) -> torch.Tensor:
+               FtF: torch.Tensor | None, cg_iters: int, nonneg: bool, exact: bool | None = None,
+               row_range: tuple[int, int] | None = None) -> torch.Tensor:
+    """New factors of the rows of ``csr`` (all of them, or the CG solve of rows [a, b)
+    written IN PLACE into ``X0[a:b]``, which is returned -- the chunked path of
+    :func:`fit_als`, whose per-chunk results are all-gathered while later chunks solve)."""
     n, R = csr.nrows, Ffull.shape[1]
     dev = Ffull.device
     key = (implicit, float(alpha), float(reg))
@@ -127,7 +131,12 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
     nnz = int(csr.cols.numel())
     if exact is None:
         exact = nnz * R * R <= (1 << 26)
-    if not exact and not nonneg and DENSE_MIN_AVG and A.gram_ok(Ffull) and nnz >= DENSE_MIN_AVG * max(n, 1):
+    indptr = csr.indptr
+    if row_range is not None:
+        assert not exact, "row-range solves are CG only"
+        a, e = row_range
+        indptr, lam, X0, n = csr.indptr[a:e + 1], lam[a:e], X0[a:e], e - a
+    if row_range is None and not exact and not nonneg and DENSE_MIN_AVG and A.gram_ok(Ffull) and nnz >= DENSE_MIN_AVG * max(n, 1):
         # many ratings per row (the item side): exact solves, Gram on MFMA + batched Cholesky
         with trace("als.dense_solve"):
             return A.dense_solve(csr.indptr, csr.cols, w, b, Ffull, FtF if implicit else None, lam)
@@ -145,14 +154,14 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
         return x.clamp_min(0) if nonneg else x
 
     def Amul(v):
-        out = A.pass_(0, csr.indptr, csr.cols, w, Ffull, v)
+        out = A.pass_(0, indptr, csr.cols, w, Ffull, v)
         if implicit and FtF is not None:
             out = out + v @ FtF
         return out + lam[:, None] * v
 
-    x = X0.clone()
+    x = X0 if row_range is not None else X0.clone()
     # first residual: the rhs and A x0 gather the same factor rows -> one fused pass
-    ax, rhs = A.pass_both(csr.indptr, csr.cols, w, Ffull, x, b)
+    ax, rhs = A.pass_both(indptr, csr.cols, w, Ffull, x, b)
     if FUSED_CG and A.cg_kernel_ok(Ffull) and x.is_contiguous() and x.dtype == torch.float32:
         # device path: every CG vector update is one fused row-wise kernel (als_cg_kernel)
         use_g = implicit and FtF is not None
@@ -160,9 +169,9 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
         r, p, rs = A.cg_init(x, ax, (x @ FtF) if use_g else None, rhs, lam_c)
         del ax, rhs
         for _ in range(cg_iters):
-            ap = A.pass_(0, csr.indptr, csr.cols, w, Ffull, p)
+            ap = A.pass_(0, indptr, csr.cols, w, Ffull, p)
             A.cg_step(x, r, p, ap, (p @ FtF) if use_g else None, lam_c, rs)
-        return x.clamp_min(0) if nonneg else x
+        return x.clamp_(min=0) if nonneg else x
     if implicit and FtF is not None:
         ax = ax + x @ FtF
     r = rhs - (ax + lam[:, None] * x)
@@ -171,14 +180,14 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
     for _ in range(cg_iters):
         Ap = Amul(p)
         den = (p * Ap).sum(1)
-        a = torch.where(den > 0, rs / den.clamp_min(1e-30), torch.zeros_like(rs))
-        x = x + a[:, None] * p
-        r = r - a[:, None] * Ap
+        al = torch.where(den > 0, rs / den.clamp_min(1e-30), torch.zeros_like(rs))
+        x += al[:, None] * p
+        r = r - al[:, None] * Ap
         rs_new = (r * r).sum(1)
         beta = torch.where(rs > 0, rs_new / rs.clamp_min(1e-30), torch.zeros_like(rs))
         p = r + beta[:, None] * p
         rs = rs_new
-    return x.clamp_min(0) if nonneg else x
+    return x.clamp_(min=0) if nonneg else x
 
 
 def gram(F: torch.Tensor, chunk: int = 1 << 20) -> torch.Tensor:
@@ -192,6 +201,51 @@ def gram(F: torch.Tensor, chunk: int = 1 << 20) -> torch.Tensor:
         Fc = F[a:a + chunk].float()
         out += (Fc.T @ Fc).double()
     return out
+
+
+# row chunks per half-iteration on several ranks: chunk c's all-gather (RCCL, its own
+# stream) overlaps the solve of chunk c+1; only the last chunk's transfer is exposed
+GATHER_CHUNKS = 4
+
+
+def _slot_len(n: int, world: int, chunks: int) -> int:
+    blk = -(-n // world)                 # largest row block of any rank
+    return max(1, -(-blk // chunks))
+
+
+def _slot_pos(idx: torch.Tensor, n: int, world: int, L: int) -> torch.Tensor:
+    """Row of global index ``idx`` in the slot-layout table: rank r's local row o sits in
+    chunk c = o // L at c*world*L + r*L + o % L (the order all_gather_into_tensor of
+    equal L-row chunks writes)."""
+    idx = idx.to(torch.int64)
+    los = torch.tensor([block_bounds(n, world, r)[0] for r in range(world)], dtype=torch.int64, device=idx.device)
+    owner = torch.searchsorted(los, idx, right=True) - 1
+    o = idx - los[owner]
+    c = torch.div(o, L, rounding_mode="floor")
+    return c * (world * L) + owner * L + (o - c * L)
+
+
+def _gather_slots(comm, F: torch.Tensor, table: torch.Tensor, L: int, solve) -> None:
+    """For each chunk c of this rank's rows: ``solve(a, e)`` updates F[a:e] in place (if
+    given), then F[a:e] (zero-padded to L rows) is all-gathered asynchronously into the
+    table's chunk-c slots; returns after ordering the stream behind every transfer."""
+    n, W = F.shape[0], comm.world_size
+    chunks = table.shape[0] // (W * L)
+    works, keep = [], []
+    for c in range(chunks):
+        a, e = min(c * L, n), min((c + 1) * L, n)
+        if solve is not None and e > a:
+            solve(a, e)
+        src = F[a:e]
+        if e - a != L:
+            src = torch.zeros((L, F.shape[1]), dtype=F.dtype, device=F.device)
+            src[: e - a] = F[a:e]
+        keep.append(src)
+        with trace("als.gather_chunk"):
+            works.append(comm.all_gather_into(table[c * W * L:(c + 1) * W * L], src, async_op=True))
+    for w in works:
+        if w is not None:
+            w.wait()
 
 
 @dataclass
@@ -230,25 +284,45 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
         start, st, _ = last              # resume: this rank's factor shards (runtime/checkpoint.py)
         X = torch.from_numpy(st["X"]).to(dev, X.dtype)
         Y = torch.from_numpy(st["Y"]).to(dev, Y.dtype)
+    chunked = comm.world_size > 1 and not (exact if exact is not None else
+                                            max(by_user.cols.numel(), by_item.cols.numel()) * rank * rank <= (1 << 26))
+    if chunked:
+        # factor tables in "slot" layout: every all-gather lands in place (no staging copy,
+        # no concatenation) and chunk c of every rank is gathered while chunk c+1 solves
+        Ls, Li = _slot_len(nU, comm.world_size, GATHER_CHUNKS), _slot_len(nI, comm.world_size, GATHER_CHUNKS)
+        by_user.cols = _slot_pos(by_user.cols, nI, comm.world_size, Li).to(torch.int32)
+        by_item.cols = _slot_pos(by_item.cols, nU, comm.world_size, Ls).to(torch.int32)
+        Xf = torch.zeros((GATHER_CHUNKS * comm.world_size * Ls, rank), dtype=X.dtype, device=dev)
+        Yf = torch.zeros((GATHER_CHUNKS * comm.world_size * Li, rank), dtype=Y.dtype, device=dev)
+        _gather_slots(comm, Y, Yf, Li, None)
     for it in range(start, max_iter):
         with trace("als.iter"):
             ti = time.time()
-            Yf = comm.all_gather_v(Y) if comm.world_size > 1 else Y
+            if not chunked:
+                Yf = comm.all_gather_v(Y) if comm.world_size > 1 else Y
             YtY = None
             if implicit:
                 YtY = gram(Y)
                 comm.all_reduce(YtY)
                 YtY = YtY.float()
-            X = solve_side(by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact)
-            del Yf
-            Xf = comm.all_gather_v(X) if comm.world_size > 1 else X
+            if chunked:
+                _gather_slots(comm, X, Xf, Ls, lambda a, e: solve_side(
+                    by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, False, row_range=(a, e)))
+            else:
+                X = solve_side(by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact)
+                del Yf
+                Xf = comm.all_gather_v(X) if comm.world_size > 1 else X
             XtX = None
             if implicit:
                 XtX = gram(X)
                 comm.all_reduce(XtX)
                 XtX = XtX.float()
-            Y = solve_side(by_item, Xf, Y, reg, implicit, alpha, XtX, cg_iters, nonneg, exact)
-            del Xf
+            if chunked:
+                _gather_slots(comm, Y, Yf, Li, lambda a, e: solve_side(
+                    by_item, Xf, Y, reg, implicit, alpha, XtX, cg_iters, nonneg, False, row_range=(a, e)))
+            else:
+                Y = solve_side(by_item, Xf, Y, reg, implicit, alpha, XtX, cg_iters, nonneg, exact)
+                del Xf
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
             its.append(time.time() - ti)

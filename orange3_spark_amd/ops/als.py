@@ -11,8 +11,13 @@ from . import _native as N
 
 
 def pass_torch(mode, indptr, cols, coef, F, V):
+    """``indptr`` may be a row-range view of a larger CSR (absolute offsets into cols/coef,
+    as the kernel reads them)."""
     n = indptr.numel() - 1
     R = F.shape[1]
+    base, end = int(indptr[0]), int(indptr[-1])
+    if base or end != cols.numel():
+        cols, coef, indptr = cols[base:end], coef[base:end], indptr - base
     rows = torch.repeat_interleave(torch.arange(n, device=F.device), indptr[1:] - indptr[:-1])
     Fg = F[cols.long()].to(torch.float64)
     s = coef.to(torch.float64)

@@ -44,6 +44,13 @@ class Comm:
         """Concatenate variable-length shards along dim 0 (rank order)."""
         raise NotImplementedError
 
+    def all_gather_into(self, out: torch.Tensor, t: torch.Tensor, async_op: bool = False):
+        """Equal shards gathered straight into ``out`` ([world * t.shape[0], ...], rank
+        order): no staging buffer, no concatenation.  ``async_op=True`` returns a handle
+        whose ``wait()`` orders the caller's stream after the transfer (RCCL runs it on
+        its own stream, so the caller's kernels overlap it); None when already done."""
+        raise NotImplementedError
+
     def reduce_scatter(self, t: torch.Tensor) -> torch.Tensor:
         raise NotImplementedError
 
@@ -133,6 +140,10 @@ class LocalComm(Comm):
     def all_gather_v(self, t):
         return t
 
+    def all_gather_into(self, out, t, async_op=False):
+        out.copy_(t)
+        return None
+
     def reduce_scatter(self, t):
         return t
 
@@ -199,6 +210,12 @@ class TorchComm(Comm):
         full = self.all_gather(pad)
         parts = [full[r * m: r * m + s] for r, s in enumerate(sizes)]
         return torch.cat(parts) if parts else t
+
+    def all_gather_into(self, out, t, async_op=False):
+        if self.world_size == 1:
+            out.copy_(t)
+            return None
+        return dist.all_gather_into_tensor(out, t.contiguous(), group=self.group, async_op=async_op)
 
     def reduce_scatter(self, t):
         if self.world_size == 1:
@@ -309,7 +326,7 @@ def _guard(name, fn):
     return wrapper
 
 
-for _n in ("all_reduce", "all_gather", "all_gather_v", "reduce_scatter", "broadcast", "all_to_all_v", "barrier",
+for _n in ("all_reduce", "all_gather", "all_gather_v", "all_gather_into", "reduce_scatter", "broadcast", "all_to_all_v", "barrier",
            "all_gather_object", "broadcast_object"):
     setattr(TorchComm, _n, _guard(_n, TorchComm.__dict__[_n]))
 LocalComm.all_reduce = _guard("all_reduce", LocalComm.__dict__["all_reduce"])

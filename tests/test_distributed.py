@@ -54,6 +54,11 @@ def _work(rank, world, port, out_dir):
     pdf = pd.DataFrame({"user": u, "item": i, "rating": r})
     als = ALS(rank=3, maxIter=3, seed=1).fit(s.createDataFrame(pdf))
     res["als_U"] = als._U.numpy()
+    from orange3_spark_amd.models.als import fit_als     # CG path: chunked slot-layout all-gathers at 2 ranks
+    t = torch.from_numpy(rows[lo:hi])
+    cg = fit_als(s.comm, t[:, 0].long(), t[:, 1].long(), t[:, 2].float(), rank=4, max_iter=3, implicit=True,
+                 alpha=2.0, exact=False, cg_iters=3)
+    res["als_cg"] = np.concatenate([cg.U.numpy().ravel(), cg.V.numpy().ravel()])
     from orange3_spark_amd.ml.classification import NaiveBayes
     from orange3_spark_amd.ml.feature import VectorAssembler
     from orange3_spark_amd.ml.regression import GeneralizedLinearRegression, IsotonicRegression
@@ -101,6 +106,7 @@ def test_world2_matches_world1(tmp_path):
     assert np.allclose(a["gbt_loss"], b["gbt_loss"], rtol=1e-6)
     assert a["rf_nodes"] == b["rf_nodes"] and np.allclose(a["rf_imp"], b["rf_imp"], atol=1e-9)
     assert np.allclose(a["als_U"], b["als_U"], atol=1e-4)
+    assert np.allclose(a["als_cg"], b["als_cg"], atol=1e-5)
     assert a["groupby"] == b["groupby"]
     assert a["iso"].shape == b["iso"].shape and np.allclose(a["iso"], b["iso"], atol=1e-9)
     assert np.allclose(a["nb_theta"], b["nb_theta"], atol=1e-9)

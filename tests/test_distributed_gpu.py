@@ -48,6 +48,13 @@ def _work(rank, world, port, out_dir):
     pdf = pd.DataFrame({"user": rng.integers(0, 300, 5000), "item": rng.integers(0, 120, 5000),
                         "rating": rng.normal(size=5000)})
     res["als_U"] = ALS(rank=8, maxIter=3, seed=1).fit(s.createDataFrame(pdf))._U.cpu().numpy()
+    # CG path with chunked slot-layout all-gathers (async, overlapping the next chunk's solve)
+    from orange3_spark_amd.models.als import fit_als
+    lo, hi = (5000 * rank) // world, (5000 * (rank + 1)) // world
+    t = torch.tensor(pdf.to_numpy()[lo:hi], device=s.device)
+    cg = fit_als(s.comm, t[:, 0].long(), t[:, 1].long(), t[:, 2].float(), rank=32, max_iter=3, implicit=True,
+                 alpha=2.0, exact=False, cg_iters=3)
+    res["als_cg"] = np.concatenate([cg.U.cpu().numpy().ravel(), cg.V.cpu().numpy().ravel()])
     if rank == 0:
         torch.save(res, os.path.join(out_dir, f"g{world}.pt"))
     if world > 1:
@@ -77,3 +84,4 @@ def test_gpu_world2_matches_world1(tmp_path):
     assert a["rf_nodes"] == b["rf_nodes"]
     assert np.allclose(a["rf_imp"], b["rf_imp"], atol=1e-6)
     assert np.allclose(a["als_U"], b["als_U"], atol=1e-3)
+    assert np.allclose(a["als_cg"], b["als_cg"], atol=1e-4)
