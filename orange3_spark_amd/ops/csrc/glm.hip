@@ -1184,3 +1184,218 @@ O3S_API int o3s_glm_sgd_update_dev(const double* out, int dpad, double* bt, doub
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------------
+// Multinomial (softmax) logistic regression, one fused pass over bf16 rows:
+//   margins M = X W^T + b (MFMA), row log-sum-exp, residual R = w (softmax(M) - onehot(y)),
+//   gradient G = R^T X (MFMA), sum(R) per class and the weighted cross-entropy.
+// Reference: Spark's MultinomialLogisticRegression aggregator reached from the
+// Classification widget (orangecontrib/spark/widgets/ml/spark_ml_classification.py:15,
+// SURVEY §2.8 "Multinomial: X.W with C classes uses MFMA").
+//
+// Layout (v_mfma_f32_32x32x16_bf16; lane (r = lane&31, h = lane>>5)):
+//   forward  A = W split (32 classes x 16 dims, class r, dims 8h..+8), B = X (row r, the
+//            same 8 dims -- exactly the 16-B global load of the row) -> acc[v] = margin of
+//            row r, class 8(v>>2) + 4h + (v&3);
+//   backward A = R split (class r, rows 8h..+8 of a 16-row step), B = X^T (rows 8h..+8,
+//            dim r of a 32-dim block, read transposed from this wave's LDS copy of the
+//            tile) -> G[nb][v] = dG of class 8(v>>2) + 4h + (v&3), dim 32 nb + r.
+// X is exact in bf16; W is split into three bf16 terms (hi + mid + lo: margins and loss
+// at fp32 level), the residuals R (|R| <= w) into two (hi + lo: ~2^-17 relative per term
+// of the gradient sums).  The MFMA
+// work is a few % of the HBM time of a tile: the kernel streams X once per pass (the
+// next tile's rows are loaded while this tile computes).  One wave per SIMD (the
+// 128-register gradient accumulators); per-wave slab rows, summed in fp64 by
+// glm_finish_kernel in a fixed order (no float atomics).
+namespace {
+
+typedef float sm_f32x16 __attribute__((ext_vector_type(16)));
+typedef short sm_bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int kSmWaves = 4;
+constexpr int kSmThreads = kSmWaves * kWave;
+
+template <int NB>
+struct SmLds {
+  static constexpr int D = 32 * NB;
+  static constexpr int WLD = D + 8;     // +16 B per row: conflict-free 16-B fragment reads
+  static constexpr int XLD = D + 8;
+  static constexpr int RLD = 40;        // 80-B rows: the 16-B R fragment reads hit distinct banks
+  static constexpr int W_ELEMS = 3 * 32 * WLD;
+  static constexpr int WAVE_ELEMS = 32 * XLD + 2 * 32 * RLD;
+  static constexpr int ELEMS = W_ELEMS + kSmWaves * WAVE_ELEMS;
+};
+
+template <int NB>
+__global__ __launch_bounds__(kSmThreads, 1) void glm_softmax_kernel(
+    const uint16_t* __restrict__ X, int64_t n, int64_t ldx, const int32_t* __restrict__ y,
+    const float* __restrict__ sw, const uint16_t* __restrict__ Wsp, const float* __restrict__ bias, int K,
+    float* __restrict__ partial, int pstride) {
+  using L = SmLds<NB>;
+  constexpr int D = L::D, KS = 2 * NB, WLD = L::WLD, XLD = L::XLD, RLD = L::RLD;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[L::ELEMS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  uint16_t* Ws = smem;
+  uint16_t* Xs = smem + L::W_ELEMS + wid * L::WAVE_ELEMS;
+  uint16_t* Rs = Xs + 32 * XLD;
+
+  // W splits [3][32][D] -> LDS (padded rows)
+  for (int p = threadIdx.x; p < 3 * 32 * (D / 8); p += kSmThreads) {
+    const int row = p / (D / 8), k8 = p % (D / 8);
+    *reinterpret_cast<sm_bf16x8*>(Ws + row * WLD + k8 * 8) =
+        *reinterpret_cast<const sm_bf16x8*>(Wsp + (int64_t)row * D + k8 * 8);
+  }
+  float bl[16];
+  int cls[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    cls[v] = 8 * (v >> 2) + 4 * h + (v & 3);
+    bl[v] = cls[v] < K ? bias[cls[v]] : -INFINITY;
+  }
+  __syncthreads();
+
+  sm_f32x16 G[NB];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) G[b][v] = 0.f;
+  float gb[16];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) gb[v] = 0.f;
+  float lossacc = 0.f;
+
+  const int64_t ntiles = (n + 31) / 32;
+  const int64_t step = (int64_t)gridDim.x * kSmWaves;
+  int64_t tile = (int64_t)blockIdx.x * kSmWaves + wid;
+  sm_bf16x8 xb[KS], xn[KS];
+  auto load = [&](int64_t t, sm_bf16x8 (&dst)[KS]) {
+    int64_t row = t * 32 + r;
+    row = row < n ? row : n - 1;
+    const uint16_t* src = X + row * ldx;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int col = ks * 16 + 8 * h;
+      if (col < ldx) {
+        dst[ks] = *reinterpret_cast<const sm_bf16x8*>(src + col);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dst[ks][j] = 0;
+      }
+    }
+  };
+  if (tile < ntiles) load(tile, xb);
+  for (; tile < ntiles; tile += step) {
+    if (tile + step < ntiles) load(tile + step, xn);
+    const int64_t row = tile * 32 + r;
+    const bool valid = row < n;
+    const int yl = valid ? y[row] : -1;
+    const float wr = valid ? (sw ? sw[row] : 1.f) : 0.f;
+    // ---- forward: margins of row r, 16 classes per lane
+    sm_f32x16 acc;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = bl[v];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const sm_bf16x8 a = *reinterpret_cast<const sm_bf16x8*>(Ws + (s * 32 + r) * WLD + ks * 16 + 8 * h);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, xb[ks], acc, 0, 0, 0);
+      }
+      *reinterpret_cast<sm_bf16x8*>(Xs + r * XLD + ks * 16 + 8 * h) = xb[ks];   // for the X^T reads
+    }
+    // ---- row softmax (the two half-waves hold disjoint class subsets of row r)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) mx = fmaxf(mx, acc[v]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float se = 0.f;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) se += __expf(acc[v] - mx);
+    se += __shfl_xor(se, 32, 64);
+    const float lse = mx + __logf(se);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const bool hit = cls[v] == yl;
+      const float p = __expf(acc[v] - lse);
+      const float rv = wr * (p - (hit ? 1.f : 0.f));
+      gb[v] += rv;
+      if (hit) lossacc += wr * (lse - acc[v]);
+      const uint16_t a0 = f32_to_bf16(rv);
+      Rs[(0 * 32 + cls[v]) * RLD + r] = a0;
+      Rs[(1 * 32 + cls[v]) * RLD + r] = f32_to_bf16(rv - bf16_to_f32(a0));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // ---- backward: G[class][dim] += sum over the tile's rows of R[row][class] X[row][dim]
+    sm_bf16x8 ar[2][2];
+#pragma unroll
+    for (int rs = 0; rs < 2; ++rs)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        ar[rs][s] = *reinterpret_cast<const sm_bf16x8*>(Rs + (s * 32 + r) * RLD + rs * 16 + 8 * h);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+#pragma unroll
+      for (int rs = 0; rs < 2; ++rs) {
+        sm_bf16x8 bx;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) bx[q] = (short)Xs[(rs * 16 + 8 * h + q) * XLD + b * 32 + r];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) G[b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ar[rs][s], bx, G[b], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // tile's LDS reads done before it is overwritten
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) xb[ks] = xn[ks];
+  }
+  // ---- this wave's slab row: [G class-major 32 x D | sum R (32) | loss]
+  float* out = partial + ((int64_t)blockIdx.x * kSmWaves + wid) * pstride;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) out[cls[v] * D + b * 32 + r] = G[b][v];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    float s = gb[v];
+#pragma unroll
+    for (int off = 16; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);   // over the 32 rows (same h)
+    if (r == 0) out[32 * D + cls[v]] = s;
+  }
+  const float lt = wave_sum(lossacc);
+  if (lane == 0) out[32 * D + 32] = lt;
+}
+
+}  // namespace
+
+// One multinomial pass: out (fp64, [32 * D | 32 | 1]) = (gradient class-major over
+// D = 32 * ceil(d / 32) dims, per-class residual sums, weighted cross-entropy) over the n
+// rows of X (bf16, row stride ldx, ldx % 8 == 0).  y: int32 labels in [0, K); sw: fp32
+// weights or null; Wsp: bf16 [3][32][D] (hi, mid, lo splits of the class-major
+// coefficients, zero-padded); bias: fp32 [32].  partial: fp32 [grid * 4][32 D + 33].
+O3S_API int o3s_glm_softmax(const void* X, int64_t n, int64_t ldx, int d, const int32_t* y, const float* sw,
+                            const void* Wsp, const float* bias, int K, float* partial, int grid, double* out,
+                            hipStream_t st) {
+  const int nb = (d + 31) / 32;
+  if (ldx % 8 != 0 || nb < 1 || nb > 8 || K < 1 || K > 32 || grid <= 0) return -1;
+  const int D = 32 * nb, pstride = 32 * D + 33;
+  const uint16_t* Xh = (const uint16_t*)X;
+  const uint16_t* Wh = (const uint16_t*)Wsp;
+  if (n > 0) {
+    switch (nb) {
+#define O3S_SM(NBV) \
+  case NBV: hipLaunchKernelGGL((glm_softmax_kernel<NBV>), dim3(grid), dim3(kSmThreads), 0, st, Xh, n, ldx, y, sw, \
+                               Wh, bias, K, partial, pstride); break;
+      O3S_SM(1) O3S_SM(2) O3S_SM(3) O3S_SM(4) O3S_SM(5) O3S_SM(6) O3S_SM(7) O3S_SM(8)
+#undef O3S_SM
+      default: return -1;
+    }
+  } else {
+    hipMemsetAsync(partial, 0, sizeof(float) * pstride * (size_t)grid * kSmWaves, st);
+  }
+  O3S_CHECK_LAUNCH();
+  hipLaunchKernelGGL(glm_finish_kernel, dim3((pstride + 31) / 32), dim3(1024), 0, st, partial, grid * kSmWaves,
+                     pstride, pstride, out, 0);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}

@@ -308,6 +308,57 @@ def glm_margin(X: torch.Tensor, coef: torch.Tensor, intercept: float) -> torch.T
     return (X.to(torch.float64) @ c + float(intercept)).to(torch.float32)
 
 
+# --------------------------------------------------------------------------- multinomial
+def softmax_kernel_ok(X: torch.Tensor, K: int) -> bool:
+    return (X.is_cuda and X.dtype == torch.bfloat16 and X.dim() == 2 and X.stride(1) == 1
+            and X.stride(0) % 8 == 0 and 1 <= X.shape[1] <= 256 and 1 <= K <= 32)
+
+
+def softmax_pass(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, W: torch.Tensor, b: torch.Tensor):
+    """One fused multinomial pass over the rows of X (``glm_softmax_kernel``, csrc/glm.hip).
+
+    X bf16 [n, d] (row stride a multiple of 8), y int32 labels, sw fp32 weights or None,
+    W fp32 [K, d] effective coefficients, b fp32 [K].  Returns fp64 (G [K, d] = sum_i
+    w_i (p_i - onehot(y_i)) x_i^T, sum_i w_i (p_i - onehot(y_i)) [K], sum_i w_i (lse_i -
+    m_{i, y_i}))."""
+    n, d = X.shape
+    K = W.shape[0]
+    dev = X.device
+    D = 32 * (-(-d // 32))
+    Wp = torch.zeros((32, D), dtype=torch.float32, device=dev)
+    Wp[:K, :d] = W
+    hi = Wp.to(torch.bfloat16)
+    r1 = Wp - hi.float()
+    mid = r1.to(torch.bfloat16)
+    lo = (r1 - mid.float()).to(torch.bfloat16)
+    Wsp = torch.stack([hi, mid, lo]).contiguous()
+    bp = torch.zeros(32, dtype=torch.float32, device=dev)
+    bp[:K] = b
+    grid = N.num_cus(dev)
+    pstride = 32 * D + 33
+    partial = torch.empty(grid * 4 * pstride, dtype=torch.float32, device=dev)
+    out = torch.empty(pstride, dtype=torch.float64, device=dev)
+    yi = y if y.dtype == torch.int32 else y.to(torch.int32)
+    N.check(N.kernels().o3s_glm_softmax(X.data_ptr(), n, X.stride(0), d, yi.contiguous().data_ptr(),
+                                        N.ptr(None if sw is None else sw.float().contiguous()),
+                                        Wsp.data_ptr(), bp.data_ptr(), K, partial.data_ptr(), grid,
+                                        out.data_ptr(), N.stream_of(X)), "glm_softmax")
+    return out[: 32 * D].view(32, D)[:K, :d], out[32 * D:32 * D + K], out[32 * D + 32]
+
+
+def softmax_pass_torch(X, y, sw, W, b):
+    """fp64 reference of :func:`softmax_pass`."""
+    Xd = X.to(torch.float64)
+    M = Xd @ W.to(torch.float64).T + b.to(torch.float64)
+    lse = torch.logsumexp(M, 1)
+    w = torch.ones(X.shape[0], dtype=torch.float64, device=X.device) if sw is None else sw.to(torch.float64)
+    yl = y.long()
+    P = torch.exp(M - lse[:, None])
+    P[torch.arange(X.shape[0], device=X.device), yl] -= 1.0
+    R = P * w[:, None]
+    return R.T @ Xd, R.sum(0), (w * (lse - M.gather(1, yl[:, None]).squeeze(1))).sum()
+
+
 # --------------------------------------------------------------------------- moments
 def _colstats_out(ld: int, device, grid: int):
     dpad, _ = layout(ld)

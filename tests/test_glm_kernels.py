@@ -142,3 +142,45 @@ def test_gpu_grad_mixed_modes_agree(gpu, mode, monkeypatch):
     monkeypatch.setattr(G, "MIX_MODE", mode)
     out = G.glm_grad_mixed(Xr, yall, None, n_lin, d, seed, n_res, coef, -0.2, 0, ws).clone()
     assert torch.allclose(out, ref, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,K,weighted,pad", [(256, 10, False, 0), (20, 3, True, 12), (100, 32, True, 4),
+                                             (64, 2, False, 0), (200, 7, False, 56)])
+def test_gpu_softmax_pass_matches_fp64(gpu, d, K, weighted, pad):
+    """glm_softmax_kernel (MFMA margins + gradient, split-bf16 W and R) vs the fp64 torch
+    pass on the same bf16 rows; padded row strides (vector columns) and ragged tiles."""
+    g = torch.Generator().manual_seed(d + K)
+    n = 40_003
+    Xf = torch.rand((n, d + pad), generator=g) * 2 - 1
+    Xf[:, d:] = 0
+    Xb = Xf.to(torch.bfloat16).to(gpu)
+    X = Xb[:, :d]
+    y = torch.randint(0, K, (n,), generator=g).to(gpu)
+    sw = (torch.rand(n, generator=g) + 0.5).to(gpu) if weighted else None
+    W = (torch.randn((K, d), generator=g) * 0.3).to(gpu)
+    b = (torch.randn(K, generator=g) * 0.5).to(gpu)
+    assert G.softmax_kernel_ok(X, K)
+    Gk, gb, loss = G.softmax_pass(X, y, sw, W, b)
+    Gr, gbr, lr = G.softmax_pass_torch(X, y, sw, W, b)
+    scale = Gr.abs().max().item()
+    assert (Gk - Gr).abs().max().item() <= 2e-5 * scale
+    assert torch.allclose(gb, gbr, rtol=1e-5, atol=1e-6 * n)
+    assert abs(loss.item() - lr.item()) <= 1e-5 * abs(lr.item())
+
+
+@pytest.mark.gpu
+def test_gpu_multinomial_fit_kernel_matches_chunked(gpu, monkeypatch):
+    from orange3_spark_amd.models import glm as GLM
+    from orange3_spark_amd.parallel.comm import LocalComm
+    g = torch.Generator().manual_seed(5)
+    n, d, K = 50_000, 24, 4
+    X = (torch.rand((n, d), generator=g) * 2 - 1).to(torch.bfloat16).to(gpu)
+    z = X[:, 0].float() + 0.5 * X[:, 1].float()
+    y = ((z + 1.5) / 3 * K).floor().clamp(0, K - 1).double()
+    comm = LocalComm(gpu)
+    B1, b1, r1 = GLM.fit_multinomial(comm, X, y, None, K, reg=0.01, max_iter=50)
+    monkeypatch.setenv("O3S_SOFTMAX_KERNEL", "0")
+    B0, b0, r0 = GLM.fit_multinomial(comm, X, y, None, K, reg=0.01, max_iter=50)
+    assert abs(r1.f - r0.f) <= 1e-6 * abs(r0.f)
+    assert abs(B1 - B0).max() < 1e-3 and abs(b1 - b0).max() < 1e-3
