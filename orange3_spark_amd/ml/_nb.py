@@ -16,6 +16,8 @@ import math
 import numpy as np
 import torch
 
+from ..ops.gram import rows_t_matmul
+
 from ..frame import column as C
 from . import common as U
 from .base import Estimator, Model
@@ -56,9 +58,9 @@ def class_sums(comm, X: torch.Tensor, y: torch.Tensor, w: torch.Tensor | None, K
         wc = torch.ones(b - a, dtype=dt, device=dev) if w is None else w[a:b].to(dev, dt)
         oh = torch.zeros((b - a, K), dtype=dt, device=dev)
         oh.scatter_(1, yl[a:b, None], wc[:, None])
-        S += (oh.T @ Xc).double()
+        S += rows_t_matmul(oh, Xc).double()
         if squares:
-            S2 += (oh.T @ (Xc * Xc)).double()
+            S2 += rows_t_matmul(oh, Xc * Xc).double()
         cnt += oh.sum(0).double()
     buf = torch.cat([S.reshape(-1), S2.reshape(-1) if squares else S.new_zeros(0), cnt])
     comm.all_reduce(buf)

@@ -333,7 +333,8 @@ class LinearRegressionSummary:
         if self._fit_intercept:
             Xd = torch.cat([Xd, torch.ones(Xd.shape[0], 1, dtype=torch.float64, device=Xd.device)], 1)
         Xw = Xd if w is None else Xd * w[:, None]
-        G = Xw.T @ Xd
+        from ..ops.gram import rows_t_matmul
+        G = rows_t_matmul(Xw, Xd)
         df.comm.all_reduce(G)
         G = G.cpu().numpy()
         dof = self.degreesOfFreedom

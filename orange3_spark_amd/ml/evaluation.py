@@ -55,6 +55,23 @@ def _exact_curve(score: np.ndarray, label: np.ndarray, w: np.ndarray):
     return s[ends] if len(s) else np.array([]), tp, fp, pos_w.sum(), neg_w.sum()
 
 
+def _exact_curve_device(s: torch.Tensor, y: torch.Tensor, w: torch.Tensor):
+    """:func:`_exact_curve` on the device (stable radix sort, cumulative sums, distinct-score
+    boundaries) -- only the curve points cross to the host."""
+    if not s.numel():
+        z = np.array([])
+        return z, z, z, 0.0, 0.0
+    order = torch.sort(-s, stable=True).indices
+    ss, yy, ww = s[order], y[order], w[order]
+    pos_w = ww * (yy > 0.5)
+    neg_w = ww * (yy <= 0.5)
+    ends = torch.cat([torch.nonzero(ss[1:] != ss[:-1]).flatten(),
+                      torch.tensor([ss.numel() - 1], device=ss.device)])
+    tp = torch.cumsum(pos_w, 0)[ends]
+    fp = torch.cumsum(neg_w, 0)[ends]
+    return (ss[ends].cpu().numpy(), tp.cpu().numpy(), fp.cpu().numpy(), float(pos_w.sum()), float(neg_w.sum()))
+
+
 def _hist_curve(comm, score: torch.Tensor, label: torch.Tensor, w):
     """Large-data path: 2^20-bin score histograms per class (one fused pass, ops/evaluation.py
     score_hist kernel on the GPU), one all-reduce (16 MB fp64).  Thresholds are bin edges."""
@@ -82,6 +99,8 @@ def binary_curve(comm, score: torch.Tensor, label: torch.Tensor, w):
         if w is None:
             w = torch.ones(score.shape[0], dtype=torch.float64, device=score.device)
         s, y, ww = (comm.all_gather_v(t.to(torch.float64).contiguous()) for t in (score, label, w))
+        if s.is_cuda:
+            return _exact_curve_device(s, y, ww)
         return _exact_curve(s.cpu().numpy(), y.cpu().numpy(), ww.cpu().numpy())
     return _hist_curve(comm, score, label, w)
 
@@ -327,10 +346,9 @@ class ClusteringEvaluator(Evaluator, HasFeaturesCol, HasPredictionCol, HasWeight
             X = X / X.norm(dim=1, keepdim=True).clamp_min(1e-300)
         D = X.shape[1]
         sq = (X * X).sum(1)
-        Y = torch.zeros((k, D), dtype=torch.float64, device=X.device).index_add_(0, c, X * w[:, None])
-        Psi = torch.zeros(k, dtype=torch.float64, device=X.device).index_add_(0, c, sq * w)
-        N = torch.zeros(k, dtype=torch.float64, device=X.device).index_add_(0, c, w)
-        buf = torch.cat([Y.reshape(-1), Psi, N])
+        from ..ops.binsum import bin_sums
+        st = bin_sums(X, c, k, w)          # [sum w x | sum w | sum w ||x||^2] per cluster, no atomics
+        buf = torch.cat([st[:, :D].reshape(-1), st[:, D + 1], st[:, D]])
         comm.all_reduce(buf)
         Y, Psi, N = buf[: k * D].reshape(k, D), buf[k * D: k * D + k], buf[k * D + k:]
         if cosine:

@@ -81,6 +81,44 @@ def _num_str(v):
     return repr(float(v)) if isinstance(v, float) else str(v)
 
 
+def _value_counts(df, name) -> dict:
+    """{string form: count} of the non-null values of a column, without a per-row Python
+    loop: numeric columns count their distinct values on device (torch.unique) and format
+    only those; string columns use pandas' hash table."""
+    import pandas as pd
+    c = df.column_data(name)
+    if isinstance(c, C.HostColumn):
+        vc = pd.Series(c.values, dtype=object).value_counts(dropna=True)
+        return dict(zip(vc.index.tolist(), vc.values.tolist()))
+    if isinstance(c, C.NumericColumn):
+        data = c.data if c.valid is None else c.data[c.valid.to(c.data.device)]
+        vals, counts = torch.unique(data, return_counts=True)
+        out: dict = {}
+        for v, k in zip(vals.tolist(), counts.tolist()):
+            key = _num_str(v)
+            out[key] = out.get(key, 0) + int(k)
+        return out
+    return Counter(v for v in _strings(df, name) if v is not None)
+
+
+def _index_values(df, name, idx: dict):
+    """(float64 label index per row, NaN for null / unseen; first unseen value or None)."""
+    import pandas as pd
+    c = df.column_data(name)
+    if isinstance(c, C.NumericColumn):
+        uniq, inv = torch.unique(c.data, return_inverse=True)
+        lut = np.array([idx.get(_num_str(v), np.nan) for v in uniq.tolist()], dtype=np.float64)
+        res = lut[inv.cpu().numpy()]
+        if c.valid is not None:
+            res[~c.valid.cpu().numpy()] = np.nan
+        bad_u = [v for v, l in zip(uniq.tolist(), lut) if np.isnan(l)]
+        return res, (_num_str(bad_u[0]) if bad_u else None)
+    vals = c.values if isinstance(c, C.HostColumn) else np.asarray(_strings(df, name), dtype=object)
+    res = pd.Series(vals, dtype=object).map(idx).to_numpy(dtype=np.float64, na_value=np.nan)
+    bad = np.isnan(res)
+    return res, (vals[int(np.argmax(bad))] if bad.any() else None)
+
+
 class _InOut(HasInputCol, HasOutputCol):
     def __init__(self):
         super().__init__()
@@ -980,7 +1018,7 @@ class StringIndexer(Estimator, _InOut, HasInputCols, HasOutputCols, HasHandleInv
         ins, _ = self._cols()
         labels = []
         for name in ins:
-            cnt = Counter(v for v in _strings(df, name) if v is not None)
+            cnt = _value_counts(df, name)
             total = Counter()
             for part in df.comm.all_gather_object(cnt):
                 total.update(part)
@@ -1033,18 +1071,16 @@ class StringIndexerModel(Model, _InOut, HasInputCols, HasOutputCols, HasHandleIn
         cols = []
         for name, out, labels in zip(ins, outs, self.labelsArray):
             idx = {l: i for i, l in enumerate(labels)}
-            vals = _strings(df, name)
-            res = np.empty(len(vals), dtype=np.float64)
-            for i, v in enumerate(vals):
-                if v in idx:
-                    res[i] = idx[v]
-                elif hi == "keep":
-                    res[i] = len(labels)
+            res, first_bad = _index_values(df, name, idx)        # NaN = null or unseen
+            bad = np.isnan(res)
+            if bad.any():
+                if hi == "keep":
+                    res[bad] = len(labels)
                 elif hi == "skip":
-                    res[i] = np.nan
-                    keep[i] = False
+                    keep &= torch.from_numpy(~bad)
                 else:
-                    raise ValueError(f"Unseen label: {v}. To handle unseen labels, set Param handleInvalid to keep.")
+                    raise ValueError(f"Unseen label: {first_bad}. To handle unseen labels, set Param handleInvalid "
+                                     f"to keep.")
             cols.append((out, torch.from_numpy(res)))
         for out, t in cols:
             df = df.withColumnData(out, C.NumericColumn(t.to(df.device)))
@@ -1335,8 +1371,9 @@ class PCA(Estimator, _InOut, MLWritable, MLReadable):
     def _fit(self, df):
         X = _vec(df, self.getOrDefault(self.inputCol))
         d = X.shape[1]
-        st = torch.cat([(X.T @ X).reshape(-1), X.sum(0), torch.tensor([float(X.shape[0])], dtype=X.dtype,
-                                                                       device=X.device)])
+        from ..ops.gram import rows_t_matmul
+        st = torch.cat([rows_t_matmul(X, X).reshape(-1), X.sum(0), torch.tensor([float(X.shape[0])], dtype=X.dtype,
+                                                                                 device=X.device)])
         df.comm.all_reduce(st)
         G_, s, n = st[: d * d].reshape(d, d), st[d * d: d * d + d], st[-1]
         mean = s / n

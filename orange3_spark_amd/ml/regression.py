@@ -97,7 +97,8 @@ def _normal_equations(comm, X, y, w, reg, fit_intercept, standardization):
     wd = torch.ones_like(yd) if w is None else w.to(torch.float64).to(Xd.device)
     D = Xd.shape[1]
     Xw = Xd * wd[:, None]
-    st = torch.cat([(Xw.T @ Xd).reshape(-1), Xw.T @ yd, Xw.sum(0), (wd * yd).sum().reshape(1),
+    from ..ops.gram import rows_t_matmul
+    st = torch.cat([rows_t_matmul(Xw, Xd).reshape(-1), rows_t_matmul(Xw, yd), Xw.sum(0), (wd * yd).sum().reshape(1),
                     wd.sum().reshape(1), (wd * yd * yd).sum().reshape(1)])
     comm.all_reduce(st)
     st = st.cpu().numpy()

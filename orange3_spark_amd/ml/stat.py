@@ -74,7 +74,8 @@ class Correlation:
         else:
             comm_ = comm
         d = X.shape[1]
-        st = torch.cat([(X.T @ X).reshape(-1), X.sum(0), torch.tensor([float(X.shape[0])], dtype=torch.float64,
+        from ..ops.gram import rows_t_matmul
+        st = torch.cat([rows_t_matmul(X, X).reshape(-1), X.sum(0), torch.tensor([float(X.shape[0])], dtype=torch.float64,
                                                                        device=X.device)])
         if comm_ is not None:
             comm_.all_reduce(st)

@@ -15,6 +15,8 @@ from dataclasses import dataclass, field
 import numpy as np
 import torch
 
+from ..ops import binsum as BS
+from ..ops.gram import rows_t_matmul
 from ..ops import sampling
 from . import kmeans as KM
 
@@ -34,19 +36,15 @@ class BisectingResult:
 
 
 def _summaries(comm, X, lab, nodes, D):
-    """Per node in ``nodes``: (count, sum vector, sum of squared norms), all-reduced."""
+    """Per node in ``nodes``: (count, sum vector, sum of squared norms), all-reduced
+    (one ``bin_sums`` pass: per-wave LDS bins, no global atomics)."""
     dev = X.device
     m = len(nodes)
     lut = torch.full((int(max(nodes)) + 2,), -1, dtype=torch.int64, device=dev)
     lut[torch.tensor(nodes, device=dev)] = torch.arange(m, device=dev)
-    slot = lut[lab.clamp_max(lut.shape[0] - 1)]
-    ok = (slot >= 0) & (lab < lut.shape[0])
-    s = slot[ok]
-    Xo = X[ok].to(torch.float64)
-    cnt = torch.zeros(m, dtype=torch.float64, device=dev).index_add_(0, s, torch.ones_like(s, dtype=torch.float64))
-    sums = torch.zeros((m, D), dtype=torch.float64, device=dev).index_add_(0, s, Xo)
-    sq = torch.zeros(m, dtype=torch.float64, device=dev).index_add_(0, s, (Xo * Xo).sum(1))
-    buf = torch.cat([cnt, sums.reshape(-1), sq])
+    slot = torch.where(lab < lut.shape[0], lut[lab.clamp(0, lut.shape[0] - 1)], torch.full_like(lab, -1))
+    st = BS.bin_sums(X, slot, m)                              # [m, D + 2]
+    buf = torch.cat([st[:, D], st[:, :D].reshape(-1), st[:, D + 1]])
     comm.all_reduce(buf)
     cnt, sums, sq = buf[:m], buf[m:m + m * D].reshape(m, D), buf[m + m * D:]
     centers = sums / cnt.clamp_min(1)[:, None]
@@ -96,11 +94,8 @@ def fit_bisecting(comm, X: torch.Tensor, k: int, max_iter: int, seed: int, min_d
             d0 = ((Xa - Ct[sa, 0]) ** 2).sum(1)
             d1 = ((Xa - Ct[sa, 1]) ** 2).sum(1)
             side = (d1 < d0).long()
-            key = sa * 2 + side
-            cnts = torch.zeros(2 * m, dtype=torch.float64, device=dev).index_add_(
-                0, key, torch.ones_like(key, dtype=torch.float64))
-            sums = torch.zeros((2 * m, D), dtype=torch.float64, device=dev).index_add_(0, key, Xa)
-            buf = torch.cat([cnts, sums.reshape(-1)])
+            st = BS.bin_sums(Xa, sa * 2 + side, 2 * m)
+            buf = torch.cat([st[:, D], st[:, :D].reshape(-1)])
             comm.all_reduce(buf)
             cnts, sums = buf[:2 * m].cpu().numpy(), buf[2 * m:].reshape(2 * m, D).cpu().numpy()
             newC = np.where(cnts[:, None] > 0, sums / np.maximum(cnts, 1)[:, None], C2.reshape(2 * m, D))
@@ -203,9 +198,14 @@ def gmm_log_prob(X: torch.Tensor, means: torch.Tensor, covs: torch.Tensor, logw:
     """[n, K] log(w_k N(x | mu_k, Sigma_k)) via Cholesky factors."""
     n, D = X.shape
     L = torch.linalg.cholesky(covs)                                   # [K, D, D]
-    diff = X[None, :, :] - means[:, None, :]                          # [K, n, D]
-    z = torch.linalg.solve_triangular(L, diff.transpose(1, 2), upper=False)   # [K, D, n]
-    maha = (z * z).sum(1)                                             # [K, n]
+    # whiten with the explicit inverse factor (K tiny D x D solves): z = L^-1 x - L^-1 mu is
+    # one row-parallel GEMM per component; a triangular solve against [K, D, n] right-hand
+    # sides runs out of trsm workspace at millions of rows
+    eye = torch.eye(D, dtype=X.dtype, device=X.device).expand_as(L)
+    Linv = torch.linalg.solve_triangular(L, eye, upper=False)         # [K, D, D]
+    mw = (Linv @ means[:, :, None])[:, :, 0]                          # [K, D]
+    z = torch.matmul(X[None, :, :], Linv.transpose(1, 2)) - mw[:, None, :]   # [K, n, D]
+    maha = (z * z).sum(2)                                             # [K, n]
     logdet = 2 * torch.log(torch.diagonal(L, dim1=1, dim2=2)).sum(1)  # [K]
     lp = -0.5 * (maha + logdet[:, None] + D * math.log(2 * math.pi))
     return (lp + logw[:, None]).T
@@ -266,8 +266,8 @@ def fit_gmm(comm, X: torch.Tensor, k: int, max_iter: int, tol: float, seed: int,
                 lse = lse * wt[a:a + chunk]
             ll += lse.sum()
             Nk += r.sum(0)
-            Sk += r.T @ Xc
-            Qk += torch.einsum("nk,nd,ne->kde", r, Xc, Xc)
+            Sk += rows_t_matmul(r, Xc)
+            Qk += torch.stack([rows_t_matmul(Xc * r[:, j:j + 1], Xc) for j in range(k)])
         buf = torch.cat([Nk, Sk.reshape(-1), Qk.reshape(-1), ll[None]])
         comm.all_reduce(buf)
         Nk = buf[:k]

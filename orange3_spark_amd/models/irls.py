@@ -16,6 +16,8 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
+from ..ops.gram import rows_t_matmul
+
 _DEFAULT_LINK = {"gaussian": "identity", "binomial": "logit", "poisson": "log", "gamma": "inverse"}
 _EPS = 1e-16
 
@@ -196,8 +198,8 @@ def fit_irls(comm, X: torch.Tensor, y: torch.Tensor, w: torch.Tensor | None, off
             if fit_intercept:
                 Xc = torch.cat([Xc, torch.ones((b - a, 1), dtype=dt, device=dev)], dim=1)
             wc = ww[a:b]
-            A += (Xc * wc[:, None]).T @ Xc
-            bvec += Xc.T @ (wc * z[a:b])
+            A += rows_t_matmul(Xc * wc[:, None], Xc)        # block-batched: not a 1-tile GEMM
+            bvec += rows_t_matmul(Xc, wc * z[a:b])
         buf = torch.cat([A.reshape(-1), bvec, ww.sum()[None]])
         comm.all_reduce(buf)
         return buf[: P * P].reshape(P, P).cpu().numpy(), buf[P * P: P * P + P].cpu().numpy(), float(buf[-1])

@@ -67,8 +67,9 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
     # weights = number of points closest to each candidate
     with trace("kmeans.init.weights"):
         a, _ = K.assign(X, centers.float())
-        wts = torch.zeros(centers.shape[0], dtype=torch.float64, device=dev).index_add_(
-            0, a.long(), torch.ones(a.shape[0], dtype=torch.float64, device=dev))
+        # integer histogram (LDS-privatised): an fp64 index_add_ of ones into a few hundred
+        # candidates serialises on global atomics
+        wts = torch.bincount(a.long(), minlength=centers.shape[0])[: centers.shape[0]].to(torch.float64)
         comm.all_reduce(wts)
     with trace("kmeans.init.local"):
         return _local_kmeanspp(centers, wts, k, seed)
@@ -195,8 +196,7 @@ def fit_kmeans(comm, X: torch.Tensor, k: int, max_iter: int = 20, tol: float = 1
         ckpt.clear()                     # finished: a later fit must not resume from this run
     # final cost/sizes w.r.t. the returned centres (Spark reports the last assignment's)
     a, d = K.assign(X, C.float())
-    cnt = torch.zeros(k, dtype=torch.float64, device=X.device).index_add_(
-        0, a.long(), torch.ones(a.shape[0], dtype=torch.float64, device=X.device))
+    cnt = torch.bincount(a.long(), minlength=k)[:k].to(torch.float64)
     buf = torch.cat([cnt, d.to(torch.float64).sum().reshape(1)])
     comm.all_reduce(buf)
     return KMeansResult(C.cpu(), float(buf[-1]), it, [int(x) for x in buf[:k].tolist()], hist, time.time() - t0)

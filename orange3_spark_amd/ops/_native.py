@@ -50,6 +50,7 @@ _SIGS: dict[str, list] = {
     "o3s_synth_glm": [c_vp, c_i64, c_i64, c_vp, c_u32, c_i64, c_vp, c_f32, c_i32, c_vp],
     "o3s_glm_margin": [c_vp, c_i64, c_i64, c_vp, c_f32, c_vp, c_i32, c_vp],
     "o3s_glm_colstats": [c_i32, c_vp, c_i64, c_i64, c_vp, c_u32, c_i64, c_vp, c_i32, c_vp, c_vp],
+    "o3s_bin_sums": [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp],
     "o3s_glm_softmax": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp],
     "o3s_kmeans_assign": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp],
     "o3s_kmeans_screen": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, C.c_float, c_vp, c_vp, c_vp,

@@ -108,3 +108,19 @@ def test_training_summaries_match_evaluators():
     assert rs.r2 == pytest.approx(1 - resid @ resid / np.sum((y - y.mean()) ** 2), rel=1e-8)
     assert rs.rootMeanSquaredError == pytest.approx(np.sqrt(np.mean(resid ** 2)), rel=1e-8)
     assert rs.residuals.count() == 400 and lm.evaluate(rdf).meanAbsoluteError == pytest.approx(rs.meanAbsoluteError)
+
+
+@pytest.mark.gpu
+def test_gpu_exact_curve_matches_host(gpu):
+    import numpy as np
+    from orange3_spark_amd.ml import evaluation as EV
+    g = torch.Generator().manual_seed(3)
+    n = 200_000
+    s = (torch.randint(0, 5000, (n,), generator=g).double() / 5000)      # many ties
+    y = (torch.rand(n, generator=g) < 0.4).double()
+    w = torch.rand(n, generator=g).double() + 0.5
+    host = EV._exact_curve(s.numpy(), y.numpy(), w.numpy())
+    dev = EV._exact_curve_device(s.to(gpu), y.to(gpu), w.to(gpu))
+    for a, b in zip(host[:3], dev[:3]):
+        assert a.shape == b.shape and np.allclose(a, b, rtol=1e-10)
+    assert abs(host[3] - dev[3]) < 1e-6 and abs(host[4] - dev[4]) < 1e-6
