@@ -162,6 +162,9 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
             for k in self._cols:
                 if k.lower() == name.lower():
                     return self._cols[k]
+            qual, _, part = name.rpartition(".")
+            if qual and qual.split(".")[-1] in self.__dict__.get("_aliases", ()):
+                return self._col(part)           # "alias.col" after df.alias("alias")
             raise KeyError(f"cannot resolve column '{name}' among {self.columns}")
 
     def column_data(self, name: str) -> C.Column:
@@ -169,8 +172,7 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
 
     def __getitem__(self, item):
         if isinstance(item, str):
-            self._col(item)
-            return E.col(item)
+            return E.bound_col(item, self._col(item))
         if isinstance(item, int):
             return E.col(self.columns[item])
         if isinstance(item, (list, tuple)):
@@ -184,8 +186,25 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
             raise AttributeError(name)
         cols = self.__dict__.get("_cols", {})
         if name in cols:
-            return E.col(name)
+            return E.bound_col(name, cols[name])
         raise AttributeError(name)
+
+    def _col_bound(self, name: str, src) -> C.Column:
+        """Resolve ``other[name]`` on this frame: the column object itself when this frame holds
+        it, the renamed copy a condition join made of it (``_prov``), else by name."""
+        if src is not None:
+            c = self._cols.get(name)
+            if c is src:
+                return c
+            for ref, out in self.__dict__.get("_prov", ()):
+                if ref() is src and out in self._cols:
+                    return self._cols[out]
+        return self._col(name)
+
+    def _col_qualified(self, qual: str, name: str) -> C.Column:
+        """SQL ``qual.name``: after a condition join the renamed copy of that side's column."""
+        out = self.__dict__.get("_qual_map", {}).get((qual.split(".")[-1], name))
+        return self._cols[out] if out in self._cols else self._col(name)
 
     def _new(self, cols, n=None) -> "DataFrame":
         return DataFrame(self.session, cols, self._n if n is None else n)
@@ -270,6 +289,13 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
                         [np.arange(n_) for n_ in lens]) if len(lens) else np.zeros(0, dtype=np.int64)).to(self.device),
                         None, T.IntegerType())
                 has_none = any(x is None for x in flat)
+                first = next((x for x in flat if x is not None), None)
+                if isinstance(first, (tuple, list, dict)):      # structs / arrays stay one value per row
+                    vals = np.empty(len(flat), dtype=object)
+                    for j, x in enumerate(flat):
+                        vals[j] = x
+                    res[k] = C.ArrayColumn(vals)
+                    continue
                 res[k] = C.from_numpy(np.array(flat, dtype=object) if flat and (has_none or isinstance(
                     next((x for x in flat if x is not None), ""), str)) else np.array(flat), self.device) \
                     if flat else C.StringColumn(np.array([], dtype=object))
@@ -313,11 +339,29 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
         return self._new(out)
 
     def drop(self, *names) -> "DataFrame":
-        names = {n.name if isinstance(n, E.Expr) else n for n in names}
-        return self._new(OrderedDict((k, v) for k, v in self._cols.items() if k not in names))
+        drop_names = set()
+        for n in names:
+            src = getattr(n, "_src", None) if isinstance(n, E.Expr) else None
+            if src is not None:                  # df.drop(other.id) after a condition join
+                try:
+                    obj = self._col_bound(n.name, src())
+                except KeyError:
+                    continue
+                if self._cols.get(n.name) is obj:
+                    drop_names.add(n.name)
+                else:
+                    drop_names.update(k for k, v in self._cols.items() if v is obj)
+            else:
+                drop_names.add(n.name if isinstance(n, E.Expr) else n)
+        return self._new(OrderedDict((k, v) for k, v in self._cols.items() if k not in drop_names))
 
     def alias(self, name) -> "DataFrame":
-        return self
+        """Same columns (shared buffers) under a relation name: ``col("name.x")`` resolves
+        here, and a condition join uses it to pick the side of a qualified reference."""
+        out = self._new(self._cols)
+        out.lineage, out._cached = self.lineage, self._cached
+        out._aliases = frozenset([name])
+        return out
 
     # ------------------------------------------------------------------ row selection
     def _take(self, idx: torch.Tensor) -> "DataFrame":
@@ -637,6 +681,10 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
     def groupBy(self, *cols) -> "GroupedData":
         if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
             cols = tuple(cols[0])
+        gens = [c for c in cols if getattr(c, "_generator", None)]
+        if gens:                 # e.g. groupBy(window(ts, "10 minutes", "5 minutes")): expand rows first
+            g = gens[0]
+            return self.select("*", g).groupBy(*[E.col(g.name) if c is g else c for c in cols])
         return GroupedData(self, [E.col(c) if isinstance(c, str) else c for c in cols])
 
     groupby = groupBy

@@ -62,7 +62,9 @@ class Expr:
         def f(df):
             a, b = self.eval(df), o.eval(df)
             return _binary(a, b, op, torch_op, bool_out, len(df))
-        return Expr(f, f"({self._name} {op} {o._name})", self.refs + o.refs)
+        out = Expr(f, f"({self._name} {op} {o._name})", self.refs + o.refs)
+        out._tree = (op, self, o)        # kept for join planning (equi-key extraction)
+        return out
 
     def __add__(self, o): return self._bin(o, "+", torch.add)
     def __radd__(self, o): return lit(o)._bin(self, "+", torch.add)
@@ -384,7 +386,38 @@ def lit(value: Any) -> Expr:
 def col(name: str) -> Expr:
     def f(df):
         return df._col(name)
-    return Expr(f, name, (name,))
+    e = Expr(f, name, (name,))
+    e._colname = name
+    return e
+
+
+def qualified_col(qual: str, name: str) -> Expr:
+    """SQL ``t.name``: the column ``name`` of relation ``t`` (a join picks the side by it;
+    a single-relation frame resolves the bare name)."""
+    def f(df):
+        g = getattr(type(df), "_col_qualified", None)
+        return g(df, qual, name) if g is not None else df._col(name)
+    e = Expr(f, name, (name,))
+    e._colname = name
+    e._qual = qual
+    return e
+
+
+def bound_col(name: str, src) -> Expr:
+    """``df[name]`` / ``df.name``: a column reference that also remembers WHICH column object
+    it came from (Spark's attribute id), so a join condition such as
+    ``a.id == b.id`` can tell the two sides apart.  Frames without side information
+    resolve it by name like :func:`col`."""
+    import weakref
+    ref = weakref.ref(src)
+
+    def f(df):
+        g = getattr(type(df), "_col_bound", None)
+        return g(df, name, ref()) if g is not None else df._col(name)
+    e = Expr(f, name, (name,))
+    e._colname = name
+    e._src = ref
+    return e
 
 
 column = col

@@ -1,5 +1,11 @@
-"""DataFrame joins (equi / cross).  The right side is gathered to every rank (broadcast
-hash join, Spark's strategy for small dimension tables); left rows stay on their rank."""
+"""DataFrame joins (equi / cross / arbitrary condition).  The right side is gathered to every
+rank (broadcast hash join, Spark's strategy for small dimension tables); left rows stay on
+their rank.
+
+Condition joins (``a.join(b, (a.id == b.uid) & (a.t < b.t), how)``) take the equality
+conjuncts between the two sides as hash keys (vectorised sort + searchsorted) and evaluate
+the rest of the condition on the candidate pairs; with no equality conjunct the candidates
+are the cross product, walked in bounded blocks of left rows (Spark's nested-loop join)."""
 from __future__ import annotations
 
 from collections import OrderedDict
@@ -8,6 +14,7 @@ import numpy as np
 import torch
 
 from . import column as C
+from . import expr as E
 from .dataframe import DataFrame, _hashable
 
 
@@ -15,6 +22,13 @@ def join(left: DataFrame, right: DataFrame, on, how: str = "inner") -> DataFrame
     how = {"left_outer": "left", "leftouter": "left", "right_outer": "right", "rightouter": "right",
            "full": "outer", "fullouter": "outer", "full_outer": "outer", "semi": "left_semi",
            "leftsemi": "left_semi", "anti": "left_anti", "leftanti": "left_anti"}.get(how, how)
+    if isinstance(on, (list, tuple)) and on and all(isinstance(o, E.Expr) for o in on):
+        cond = on[0]
+        for o in on[1:]:
+            cond = cond & o
+        on = cond
+    if isinstance(on, E.Expr):
+        return condition_join(left, right, on, "inner" if how == "cross" else how)
     rfull = DataFrame(right.session.local_view(), right._gathered())
     if on is None or how == "cross":
         nl, nr = len(left), len(rfull)
@@ -224,3 +238,221 @@ def _assemble(left, right, li, ri, on, how) -> DataFrame:
             col = C.VectorColumn(col.data.to(left.device), col.size)
         cols[name] = col
     return DataFrame(left.session, cols, int(li.numel()))
+
+
+# --------------------------------------------------------------------------- condition joins
+_PAIR_BLOCK = 1 << 22          # candidate pairs evaluated per block (bounds the temporaries)
+
+
+class _Sides:
+    """Which side of a condition join a column reference names.  Identity first (``a.id``
+    is the very column object ``a`` holds), then the relation alias of a qualified name
+    (``col("a.id")``, SQL ``a.id``), then a name present on exactly one side; a name on
+    both sides with nothing else to go by is ambiguous, as in Spark."""
+
+    def __init__(self, left: DataFrame, right: DataFrame, ldata: DataFrame, rdata: DataFrame):
+        self.orig = (left, right)
+        self.data = (ldata, rdata)
+
+    def _has(self, s: int, name: str) -> bool:
+        try:
+            self.orig[s]._col(name)
+            return True
+        except KeyError:
+            return False
+
+    def _key(self, s: int, name: str) -> str:
+        """The column's actual key on side s (case / "alias." prefix resolved)."""
+        f = self.orig[s]
+        obj = f._col(name)
+        if f._cols.get(name) is obj:
+            return name
+        return next(k for k, v in f._cols.items() if v is obj)
+
+    def resolve(self, name: str, src=None, qual: str | None = None) -> tuple[int, str]:
+        if src is not None:
+            for s in (0, 1):
+                f = self.orig[s]
+                if f._cols.get(name) is src:
+                    return s, name
+                for k, v in f._cols.items():
+                    if v is src:
+                        return s, k
+        if qual is None and "." in name and not any(self._has(s, name) for s in (0, 1)):
+            qual, _, name = name.rpartition(".")
+        if qual:
+            q = qual.split(".")[-1]
+            for s in (0, 1):
+                f = self.orig[s]
+                if q in f.__dict__.get("_aliases", ()):
+                    out = f.__dict__.get("_qual_map", {}).get((q, name))
+                    if out is not None:
+                        return s, out
+                    if self._has(s, name):
+                        return s, self._key(s, name)
+        hits = [s for s in (0, 1) if self._has(s, name)]
+        if len(hits) == 1:
+            return hits[0], self._key(hits[0], name)
+        if not hits:
+            raise KeyError(f"cannot resolve column '{name}' on either side of the join")
+        raise ValueError(f"Reference '{name}' is ambiguous: both join sides have it "
+                         "(use df['col'] of one side or an alias)")
+
+    def side_of(self, e) -> tuple[int, str] | None:
+        """(side, column) of a bare column reference, else None."""
+        name = getattr(e, "_colname", None)
+        if name is None:
+            return None
+        ref = getattr(e, "_src", None)
+        return self.resolve(name, None if ref is None else ref(), getattr(e, "_qual", None))
+
+
+class _PairFrame(DataFrame):
+    """A condition evaluated over candidate pairs (li[k], ri[k]): each referenced column is
+    taken from its side for exactly those pairs, once."""
+
+    def __init__(self, sides: _Sides, li: torch.Tensor, ri: torch.Tensor):
+        DataFrame.__init__(self, sides.data[0].session, OrderedDict(), int(li.numel()))
+        self._sides, self._li, self._ri, self._taken = sides, li, ri, {}
+
+    def _take_side(self, side: int, name: str) -> C.Column:
+        key = (side, name)
+        if key not in self._taken:
+            self._taken[key] = self._sides.data[side]._col(name).take(self._li if side == 0 else self._ri)
+        return self._taken[key]
+
+    def _col(self, name):
+        return self._take_side(*self._sides.resolve(name))
+
+    def _col_bound(self, name, src):
+        return self._take_side(*self._sides.resolve(name, src))
+
+    def _col_qualified(self, qual, name):
+        return self._take_side(*self._sides.resolve(name, None, qual))
+
+
+def _conjuncts(e):
+    t = getattr(e, "_tree", None)
+    if t is not None and t[0] == "AND":
+        return _conjuncts(t[1]) + _conjuncts(t[2])
+    return [e]
+
+
+def _split_condition(cond, sides: _Sides):
+    """Equality conjuncts between a left and a right column -> hash keys; the rest stays a
+    residual predicate (None when every conjunct was a key)."""
+    keys, rest = [], []
+    for c in _conjuncts(cond):
+        t = getattr(c, "_tree", None)
+        if t is not None and t[0] == "=":
+            a, b = sides.side_of(t[1]), sides.side_of(t[2])
+            if a is not None and b is not None and a[0] != b[0]:
+                keys.append((a[1], b[1]) if a[0] == 0 else (b[1], a[1]))
+                continue
+        rest.append(c)
+    residual = None
+    for c in rest:
+        residual = c if residual is None else residual & c
+    return keys, residual
+
+
+def _truth(c: C.Column) -> torch.Tensor:
+    """SQL truth of a predicate column (null -> false), as a CPU bool tensor."""
+    if isinstance(c, C.NumericColumn):
+        m = c.data.bool()
+        if c.valid is not None:
+            m = m & c.valid
+        return m.cpu()
+    return torch.tensor([bool(v) if v is not None else False for v in c.to_pylist()], dtype=torch.bool)
+
+
+def _match_pairs(sides: _Sides, cond) -> tuple[torch.Tensor, torch.Tensor]:
+    ldata, rdata = sides.data
+    nl, nr = len(ldata), len(rdata)
+    keys, residual = _split_condition(cond, sides)
+    codes = None
+    if keys:
+        kl = DataFrame(ldata.session, OrderedDict((f"k{i}", ldata._col(a)) for i, (a, _) in enumerate(keys)), nl)
+        kr = DataFrame(rdata.session, OrderedDict((f"k{i}", rdata._col(b)) for i, (_, b) in enumerate(keys)), nr)
+        codes = _key_codes(kl, kr, [f"k{i}" for i in range(len(keys))])
+    if codes is not None:
+        li, ri = _vector_join(codes[0], codes[1], "inner")
+        li, ri = li.cpu(), ri.cpu()
+        if residual is None or li.numel() == 0:
+            return li, ri
+        keep = [_truth(residual.eval(_PairFrame(sides, li[s:s + _PAIR_BLOCK], ri[s:s + _PAIR_BLOCK])))
+                for s in range(0, li.numel(), _PAIR_BLOCK)]
+        m = torch.cat(keep)
+        return li[m], ri[m]
+    # nested loop: blocks of left rows against every right row
+    li_parts, ri_parts = [], []
+    step = max(1, _PAIR_BLOCK // max(nr, 1))
+    for s in range(0, nl if nr else 0, step):
+        e = min(nl, s + step)
+        bl = torch.arange(s, e).repeat_interleave(nr)
+        br = torch.arange(nr).repeat(e - s)
+        m = _truth(cond.eval(_PairFrame(sides, bl, br)))
+        li_parts.append(bl[m])
+        ri_parts.append(br[m])
+    if not li_parts:
+        return torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64)
+    return torch.cat(li_parts), torch.cat(ri_parts)
+
+
+def condition_join(left: DataFrame, right: DataFrame, cond, how: str = "inner") -> DataFrame:
+    """``left.join(right, <Column condition>, how)``: every column of both sides is kept (a
+    right-side name that clashes gets ``_r``); ``other[c]`` references made before the join
+    still find their column in the result (``joined.select(b.id)``, ``joined.drop(b.id)``)."""
+    if how not in ("inner", "left", "right", "outer", "left_semi", "left_anti"):
+        raise ValueError(f"Unsupported join type '{how}'")
+    full = how in ("right", "outer")
+    ldata = DataFrame(left.session.local_view(), left._gathered()) if full else left
+    rdata = DataFrame(right.session.local_view(), right._gathered())
+    sides = _Sides(left, right, ldata, rdata)
+    li, ri = _match_pairs(sides, cond)
+    nl, nr = len(ldata), len(rdata)
+    if how in ("left_semi", "left_anti"):
+        hit = torch.zeros(nl, dtype=torch.bool)
+        hit[li] = True
+        return left._take(torch.nonzero(hit if how == "left_semi" else ~hit).squeeze(1))
+    if how in ("left", "outer"):
+        hit = torch.zeros(nl, dtype=torch.bool)
+        hit[li] = True
+        miss = torch.nonzero(~hit).squeeze(1)
+        li = torch.cat([li, miss])
+        ri = torch.cat([ri, torch.full_like(miss, -1)])
+        order = torch.sort(li, stable=True).indices          # left row order, matches in right order
+        li, ri = li[order], ri[order]
+    if how in ("right", "outer"):
+        hit = torch.zeros(nr, dtype=torch.bool)
+        hit[ri[ri >= 0]] = True
+        miss = torch.nonzero(~hit).squeeze(1)
+        li = torch.cat([li, torch.full_like(miss, -1)])
+        ri = torch.cat([ri, miss])
+    import weakref
+    cols, prov, qmap = OrderedDict(), [], {}
+    for s, (orig, data, idx) in enumerate(((left, ldata, li), (right, rdata, ri))):
+        nullable = bool((idx < 0).any())
+        for k, c in data._cols.items():
+            name = k
+            while name in cols:
+                name += "_r"
+            t = _take_nullable(c, idx) if nullable else c.take(idx)
+            if isinstance(t, C.NumericColumn):
+                t = C.NumericColumn(t.data.to(left.device), None if t.valid is None else t.valid.to(left.device),
+                                    t.dtype)
+            elif isinstance(t, C.VectorColumn):
+                t = C.VectorColumn(t.data.to(left.device), t.size)
+            cols[name] = t
+            src = orig._cols.get(k)
+            if src is not None:
+                prov.append((weakref.ref(src), name))
+            for a in orig.__dict__.get("_aliases", ()):
+                qmap[(a, k)] = name
+    out = DataFrame(left.session, cols, int(li.numel()))
+    if full:
+        out = left._from_full(out._cols)
+    out._prov = prov
+    out._aliases = frozenset(left.__dict__.get("_aliases", ())) | frozenset(right.__dict__.get("_aliases", ()))
+    out._qual_map = qmap
+    return out

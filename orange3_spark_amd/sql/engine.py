@@ -66,7 +66,7 @@ def run_select(session, s: Select) -> DataFrame:
         df = DataFrame(session, OrderedDict(_dummy=C.NumericColumn(_zeros(session))), 1 if session.rank == 0 else 0)
     for j in s.joins:
         right = session.catalog.table(j.table)
-        df = _sql_join(df, right, j)
+        df = _sql_join(df, right, j, s.alias or (s.table or "").split(".")[-1])
     if s.where is not None:
         df = df.filter(s.where)
     has_agg = any(isinstance(it.expr, (AggCall, _AggExpr)) for it in s.items) or s.group_by
@@ -119,13 +119,16 @@ def _zeros(session):
     return torch.zeros(1 if session.rank == 0 else 0, dtype=torch.int32, device=session.device)
 
 
-def _sql_join(left: DataFrame, right: DataFrame, j) -> DataFrame:
+def _sql_join(left: DataFrame, right: DataFrame, j, left_name: str = "") -> DataFrame:
     if j.how == "cross" or j.on is None:
         return left.join(right, None, "cross")
     # support equi-joins "a.x = b.y" (and conjunctions of them)
     keys = _equi_keys(j.on)
-    if keys is None:
-        raise NotImplementedError("only equi-join ON conditions are supported")
+    if keys is None:                     # general ON condition: hash keys + residual / nested loop
+        if not left.__dict__.get("_aliases"):
+            left = left.alias(left_name)
+        right = right.alias(j.alias or j.table.split(".")[-1])
+        return left.join(right, j.on, j.how)
     lk, rk = zip(*keys)
     if list(lk) == list(rk):
         return left.join(right, list(lk), j.how)

@@ -1174,21 +1174,36 @@ def to_utc_timestamp(c, tz):
 
 
 def window(timeColumn, windowDuration: str, slideDuration=None, startTime=None):
-    """Tumbling time window: struct(start, end) of the fixed-size window holding each
-    timestamp (sliding windows with slide < duration are not expressible as one row)."""
+    """Time window struct(start, end).  Tumbling (no slide, or slide == duration): the one
+    window holding each timestamp.  Sliding (slide < duration): a generator -- each row is
+    repeated once per window [start, start + duration) that holds it, windows starting at
+    startTime + k * slide, in ascending start order (Spark's sliding-window expansion)."""
     import pandas as pd
     dur = pd.Timedelta(windowDuration).total_seconds()
     off = pd.Timedelta(startTime).total_seconds() if startTime else 0.0
-    if slideDuration and pd.Timedelta(slideDuration).total_seconds() != dur:
-        raise NotImplementedError("sliding windows (slideDuration != windowDuration)")
+    slide = pd.Timedelta(slideDuration).total_seconds() if slideDuration else dur
+    if not 0 < slide <= dur:
+        raise ValueError(f"slideDuration must be positive and <= windowDuration, got {slideDuration}")
     from ..frame.dataframe import Row
+    fmt = lambda x: pd.Timestamp(x, unit="s").strftime("%Y-%m-%d %H:%M:%S")  # noqa: E731
 
-    def w(v):
+    if slide == dur:
+        def w(v):
+            t = pd.Timestamp(str(v)).timestamp()
+            s0 = math.floor((t - off) / dur) * dur + off
+            return Row._make(["start", "end"], [fmt(s0), fmt(s0 + dur)])
+        return _host_map("window", w, timeColumn, kind="array").alias("window")
+
+    def ws(v):
         t = pd.Timestamp(str(v)).timestamp()
-        s0 = math.floor((t - off) / dur) * dur + off
-        fmt = lambda x: pd.Timestamp(x, unit="s").strftime("%Y-%m-%d %H:%M:%S")  # noqa: E731
-        return Row._make(["start", "end"], [fmt(s0), fmt(s0 + dur)])
-    return _host_map("window", w, timeColumn, kind="array")
+        last = math.floor((t - off) / slide) * slide + off          # latest start <= t
+        starts = []
+        s0 = last
+        while s0 + dur > t:
+            starts.append(s0)
+            s0 -= slide
+        return [Row._make(["start", "end"], [fmt(a), fmt(a + dur)]) for a in reversed(starts)]
+    return explode(_host_map("window", ws, timeColumn, kind="array")).alias("window")
 
 
 def inline(c):

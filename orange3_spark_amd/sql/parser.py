@@ -456,10 +456,11 @@ class Parser:
             name = self.ident()
             if self.accept("op", "("):
                 return self.func_call(name)
+            qual = None
             while self.peek().val == "." and self.peek(1).kind in ("id", "kw"):
                 self.i += 1
-                name = self.ident()        # qualified column: keep the column part
-            return E.col(name)
+                qual, name = name, self.ident()   # qualified column: relation part picks a join side
+            return E.col(name) if qual is None else E.qualified_col(qual, name)
         raise SyntaxError(f"unexpected token {t.val!r}")
 
     def word(self, *words) -> bool:

@@ -239,3 +239,29 @@ def test_column_string_predicates_and_null_safe_eq(s):
     assert [x.ens for x in r] == [False, False, True, False, False]  # null <=> null is true
     assert [x.en2 for x in r] == [False, True, False, False, False]  # never null
     assert [x.band for x in r][:2] == [1, 2] and r[4].band == 2
+
+
+def test_tumbling_and_sliding_windows(s):
+    """window(ts, dur) = the one window holding ts; window(ts, dur, slide) repeats each row
+    once per overlapping window (Spark's sliding expansion), groupBy(window(...)) included."""
+    ts = ["2024-01-01 00:01:00", "2024-01-01 00:07:30", "2024-01-01 00:12:00"]
+    d = s.createDataFrame(pd.DataFrame({"ts": ts, "v": [1.0, 2.0, 3.0]}))
+    tw = d.select("v", F.window("ts", "10 minutes")).collect()
+    assert [(r.v, r.window.start) for r in tw] == [(1.0, "2024-01-01 00:00:00"), (2.0, "2024-01-01 00:00:00"),
+                                                   (3.0, "2024-01-01 00:10:00")]
+    sw = d.select("v", F.window("ts", "10 minutes", "5 minutes")).collect()
+    got = [(r.v, r.window.start, r.window.end) for r in sw]
+    assert got == [(1.0, "2023-12-31 23:55:00", "2024-01-01 00:05:00"),
+                   (1.0, "2024-01-01 00:00:00", "2024-01-01 00:10:00"),
+                   (2.0, "2024-01-01 00:00:00", "2024-01-01 00:10:00"),
+                   (2.0, "2024-01-01 00:05:00", "2024-01-01 00:15:00"),
+                   (3.0, "2024-01-01 00:05:00", "2024-01-01 00:15:00"),
+                   (3.0, "2024-01-01 00:10:00", "2024-01-01 00:20:00")]
+    # every (row, window) pair satisfies start <= ts < end, 3 windows per row for slide = dur / 3
+    sw3 = d.select("ts", F.window("ts", "15 minutes", "5 minutes")).collect()
+    assert len(sw3) == 9 and all(r.window.start <= r.ts < r.window.end for r in sw3)
+    agg = sorted((tuple(r.window), r["sum(v)"]) for r in
+                 d.groupBy(F.window("ts", "10 minutes", "5 minutes")).agg(F.sum("v")).collect())
+    assert [a[1] for a in agg] == [1.0, 3.0, 5.0, 3.0]
+    with pytest.raises(ValueError):
+        F.window("ts", "5 minutes", "10 minutes")
