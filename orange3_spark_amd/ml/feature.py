@@ -1625,6 +1625,7 @@ class MinHashLSHModel(_LSHModel):
 
 from ._feature_extra import (RFormula, RFormulaModel, UnivariateFeatureSelector,  # noqa: E402,F401
                              UnivariateFeatureSelectorModel, Word2Vec, Word2VecModel)
+from ._target_encoder import TargetEncoder, TargetEncoderModel  # noqa: E402,F401
 
 __all__ = [n for n, v in list(globals().items()) if isinstance(v, type) and issubclass(v, (Transformer, Estimator))
            and not n.startswith("_")] + ["to_vector_column"]

@@ -109,7 +109,8 @@ def api_page(modname: str) -> str:
             for p in params:
                 d = inst.getOrDefault(p) if inst.hasDefault(p) or inst.isSet(p) else ""
                 desc = str(p.doc).replace("|", "\\|").replace("\n", " ")
-                lines.append(f"| `{p.name}` | `{d!r}` | {desc} |")
+                dv = re.sub(r"_[0-9a-f]{12}__output", "_<uid>__output", repr(d))   # uid-free, stable
+                lines.append(f"| `{p.name}` | `{dv}` | {desc} |")
             lines.append("")
     return "\n".join(lines)
 
@@ -127,6 +128,7 @@ def class_methods_page(title: str, classes) -> str:
                 continue
             doc = (inspect.getdoc(fn) or "").split("\n")[0]
             sig = "" if isinstance(fn, property) else str(inspect.signature(fn)).replace("(self, ", "(").replace("(self)", "()")
+            sig = re.sub(r"<function (\w+) at 0x[0-9a-f]+>", r"\1", sig)       # stable across runs
             lines.append(f"- `{name}{sig}`" + (f" — {doc}" if doc else ""))
         lines.append("")
     return "\n".join(lines)
