@@ -194,3 +194,16 @@ def test_condition_join_world2():
         merged = sorted(got[0][how] + got[1][how])
         assert merged == _oracle(pa, pb, lambda x, y: _eq(x, y) and x["t"] < y["t"] + 0.5, how), how
     assert sorted(got[0]["nl"] + got[1]["nl"]) == _oracle(pa, pb, lambda x, y: x["t"] < y["lo"], "outer")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("how", ["inner", "left", "right", "outer", "left_semi", "left_anti"])
+def test_gpu_condition_join_matches_oracle(how):
+    """Columns on cuda:0: hash keys, residual and nested-loop blocks == the row oracle."""
+    g = Session(SessionConf().set("o3s.device", "cuda"))
+    pa, pb = _pdf()
+    a, b = g.createDataFrame(pa), g.createDataFrame(pb)
+    assert a._col("t").data.is_cuda
+    for case in CASES:
+        cond, pred = CASES[case]
+        assert _rows(a.join(b, cond(a, b), how)) == _oracle(pa, pb, pred, how), case

@@ -109,3 +109,14 @@ def test_world2_matches_world1(s):
     for r in (0, 1):
         for c in ("a", "b"):
             assert got[r][c] == pytest.approx(want[c], abs=1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_target_encoder_matches_cpu():
+    pdf = _pdf(20000, seed=4)
+    res = []
+    for dev in ("cpu", "cuda"):
+        d = Session(SessionConf().set("o3s.device", dev)).createDataFrame(pdf)
+        m = TargetEncoder(inputCols=["a", "b"], outputCols=["a_te", "b_te"], smoothing=4.0).fit(d)
+        res.append(m.transform(d).select("a_te", "b_te").toPandas().to_numpy())
+    assert np.allclose(res[0], res[1], atol=1e-12)
