@@ -832,8 +832,68 @@ class GroupedData:
         from .extras import _frame_from_pandas
         names = [k.name for k in self.keys]
         local = self.df.repartition(*names).toPandas_local()
-        parts = [func(g) for _, g in local.groupby(names, sort=False, dropna=False)] if len(local) else []
+        with_key = _takes_key(func, 2)
+        parts = [func(_group_key(k), g) if with_key else func(g)
+                 for k, g in local.groupby(names, sort=False, dropna=False)] if len(local) else []
         return _frame_from_pandas(self.df, pd.concat(parts, ignore_index=True) if parts else pd.DataFrame(), schema)
+
+    def cogroup(self, other: "GroupedData") -> "CoGroupedData":
+        return CoGroupedData(self, other)
+
+
+def _takes_key(func, n_frames: int) -> bool:
+    """Spark passes the grouping key first when the function takes one more argument."""
+    import inspect
+    try:
+        ps = [p for p in inspect.signature(func).parameters.values()
+              if p.kind in (p.POSITIONAL_ONLY, p.POSITIONAL_OR_KEYWORD)]
+    except (TypeError, ValueError):
+        return False
+    return len(ps) == n_frames
+
+
+def _group_key(k) -> tuple:
+    """pandas group key -> Spark's key tuple (NaN -> None, numpy scalars -> python)."""
+    k = k if isinstance(k, tuple) else (k,)
+    out = []
+    for v in k:
+        if isinstance(v, float) and v != v:
+            v = None
+        out.append(v.item() if hasattr(v, "item") else v)
+    return tuple(out)
+
+
+class CoGroupedData:
+    """``df1.groupBy(k).cogroup(df2.groupBy(k)).applyInPandas(f, schema)``: both sides are
+    hash-exchanged by their keys (same keys -> same rank), then each rank calls
+    ``f(left_group, right_group)`` -- or ``f(key, left_group, right_group)`` -- once per key
+    present on either side, the missing side as an empty frame (Spark's
+    FlatMapCoGroupsInPandas).  Key columns must have the same types on both sides."""
+
+    def __init__(self, g1: GroupedData, g2: GroupedData):
+        if len(g1.keys) != len(g2.keys):
+            raise ValueError("cogroup needs the same number of grouping keys on both sides")
+        self.g1, self.g2 = g1, g2
+
+    def applyInPandas(self, func, schema) -> DataFrame:
+        import pandas as pd
+        from .extras import _frame_from_pandas
+        sides = []
+        for g in (self.g1, self.g2):
+            names = [k.name for k in g.keys]
+            local = g.df.repartition(*names).toPandas_local()
+            groups = OrderedDict((_group_key(k), p) for k, p in local.groupby(names, sort=False, dropna=False)) \
+                if len(local) else OrderedDict()
+            sides.append((local.iloc[0:0], groups))
+        (e1, g1), (e2, g2) = sides
+        keys = list(g1) + [k for k in g2 if k not in g1]
+        with_key = _takes_key(func, 3)
+        parts = []
+        for k in keys:
+            a, b = g1.get(k, e1), g2.get(k, e2)
+            parts.append(func(k, a, b) if with_key else func(a, b))
+        return _frame_from_pandas(self.g1.df, pd.concat(parts, ignore_index=True) if parts else pd.DataFrame(),
+                                  schema)
 
 
 def _nullable_column(vals) -> C.Column:

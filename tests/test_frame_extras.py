@@ -50,6 +50,13 @@ def _frame_ops(s):
     r["crosstab"] = [tuple(map(str, x)) for x in df.crosstab("k", "b").collect()]
     r["apply"] = sorted(tuple(x) for x in df.groupBy("k").applyInPandas(
         lambda g: pd.DataFrame({"k": [g.k.iloc[0]], "n": [len(g)]}), "k long, n long").collect())
+    r["apply_key"] = sorted(tuple(x) for x in df.groupBy("k").applyInPandas(
+        lambda key, g: pd.DataFrame({"k": [key[0]], "n": [len(g)]}), "k long, n long").collect())
+    # cogroup: per key the row counts of both sides (keys 0..4 on the left, 2..6 on the right)
+    o2 = s.createDataFrame(_pdf(300, seed=1).assign(k=lambda d: d.k + 2))
+    r["cogroup"] = sorted(tuple(x) for x in df.groupBy("k").cogroup(o2.groupBy("k")).applyInPandas(
+        lambda key, a, b: pd.DataFrame({"k": [key[0]], "na": [len(a)], "nb": [len(b)]}),
+        "k long, na long, nb long").collect())
     from orange3_spark_amd.sql import Window
     w = Window.partitionBy("k").orderBy("c")
     r["window"] = sorted((int(x.k), round(x.c, 12), int(x.rn), float(x.run)) for x in df.select(
@@ -62,6 +69,10 @@ def _frame_ops(s):
 def test_frame_ops_match_pandas(s):
     r = _frame_ops(s)
     p = _pdf()
+    assert r["apply_key"] == r["apply"] == sorted((int(k), int(n)) for k, n in p.k.value_counts().items())
+    o2 = _pdf(300, seed=1).k + 2
+    ca, cb = p.k.value_counts(), o2.value_counts()
+    assert r["cogroup"] == [(k, int(ca.get(k, 0)), int(cb.get(k, 0))) for k in range(7)]
     exp = p.assign(bb=p.b.fillna("￿")).sort_values(["k", "bb", "c"], ascending=[True, False, True],
                                                          kind="stable")
     # Spark: descending puts nulls last -> None after all strings
