@@ -54,21 +54,81 @@ def execute(session, query: str) -> DataFrame:
         df = run_select(session, stmt[2])
         cat.saveAsTable(df, stmt[1], "error")
         return session.emptyDataFrame()
+    if kind == "create_view":
+        # persistent views are kept as session views too (there is no metastore to hold a plan)
+        _, name, sel, glob, _replace = stmt
+        df = run_select(session, sel)
+        if glob:
+            df.createOrReplaceGlobalTempView(name)
+        else:
+            df.createOrReplaceTempView(name)
+        return session.emptyDataFrame()
+    if kind == "insert":
+        return _insert(session, *stmt[1:])
     return run_select(session, stmt[1])
 
 
+def _insert(session, name, cols, src, overwrite) -> DataFrame:
+    """INSERT INTO / OVERWRITE a catalog table, by position (or by the listed columns)."""
+    cat = session.catalog
+    if name in cat._temp:
+        raise ValueError(f"Inserting into the temporary view {name} is not allowed (it has no storage)")
+    target = cat.table(name)
+    tcols = list(cols) if cols else target.columns
+    if src[0] == "values":
+        rows = src[1]
+        if any(len(r) != len(tcols) for r in rows):
+            raise ValueError(f"INSERT VALUES rows must have {len(tcols)} values")
+        new = _values_frame(session, rows, tcols)
+    else:
+        new = run_select(session, src[1])
+        if len(new.columns) != len(tcols):
+            raise ValueError(f"INSERT source has {len(new.columns)} columns, {name} expects {len(tcols)}")
+        new = new.toDF(*tcols)
+    missing = [c for c in target.columns if c not in tcols]
+    for c in missing:                                    # unlisted columns get NULL
+        new = new.withColumn(c, E.lit(None))
+    types = dict(target.dtypes)
+    new = new.select(*[E.col(c).cast(types[c]).alias(c) if types[c] not in ("string",) else E.col(c)
+                       for c in target.columns])
+    cat.saveAsTable(new, name, "overwrite" if overwrite else "append")
+    return session.emptyDataFrame()
+
+
+def _values_frame(session, rows, names=None) -> DataFrame:
+    """Inline table (VALUES ...): built on rank 0, rows spread like createDataFrame."""
+    width = len(rows[0]) if rows else 0
+    names = list(names) if names else [f"col{i + 1}" for i in range(width)]
+    return session.createDataFrame([tuple(r) for r in rows], names)
+
+
 def run_select(session, s: Select) -> DataFrame:
-    if s.subquery is not None:
+    if s.ctes:
+        return _with_ctes(session, s)
+    if s.values is not None:
+        df = _values_frame(session, s.values, s.value_names)
+    elif s.subquery is not None:
         df = run_select(session, s.subquery)
     elif s.table is not None:
         df = session.catalog.table(s.table)
     else:
         df = DataFrame(session, OrderedDict(_dummy=C.NumericColumn(_zeros(session))), 1 if session.rank == 0 else 0)
     for j in s.joins:
-        right = session.catalog.table(j.table)
+        right = run_select(session, j.subquery) if j.subquery is not None else session.catalog.table(j.table)
         df = _sql_join(df, right, j, s.alias or (s.table or "").split(".")[-1])
+    for lv in s.laterals:
+        from . import functions as F
+        gen = lv.gen
+        if lv.outer and getattr(gen, "_generator", None) in ("explode", "posexplode"):
+            gen = (F.explode_outer if gen._generator == "explode" else F.posexplode_outer)(gen)
+        names = list(lv.names) or ["col"]
+        if getattr(gen, "_generator", "").startswith("posexplode"):
+            df = df.select("*", gen)
+            df = df.withColumnRenamed("pos", names[0]).withColumnRenamed("col", names[1] if len(names) > 1 else "col")
+        else:
+            df = df.select("*", gen.alias(names[0]))
     if s.where is not None:
-        df = df.filter(s.where)
+        df = _where(session, df, s)
     has_agg = any(isinstance(it.expr, (AggCall, _AggExpr)) for it in s.items) or s.group_by
     if has_agg:
         df = _aggregate(df, s)
@@ -108,9 +168,56 @@ def run_select(session, s: Select) -> DataFrame:
         df = df.limit(s.limit)
     if s.union is not None:
         other = run_select(session, s.union)
-        df = df.union(other)
-        if not s.union_all:
-            df = df.distinct()
+        if len(other.columns) != len(df.columns):
+            raise ValueError(f"{s.setop.upper()} needs the same number of columns on both sides")
+        other = other.toDF(*df.columns)                 # set operations match columns by position
+        if s.setop == "intersect":
+            df = df.intersectAll(other) if s.union_all else df.intersect(other)
+        elif s.setop == "except":
+            df = df.exceptAll(other) if s.union_all else df.subtract(other)
+        else:
+            df = df.union(other)
+            if not s.union_all:
+                df = df.distinct()
+    return df
+
+
+def _with_ctes(session, s: Select) -> DataFrame:
+    """WITH a AS (...), b AS (...) SELECT ...: each CTE visible (as a view) to the later ones
+    and the body only; views of the same names are restored afterwards."""
+    import dataclasses
+    cat = session.catalog
+    saved = {name: cat._temp.get(name) for name, _ in s.ctes}
+    try:
+        for name, q in s.ctes:
+            cat.registerTempView(name, run_select(session, q))
+        return run_select(session, dataclasses.replace(s, ctes=[]))
+    finally:
+        for name, df in saved.items():
+            if df is None:
+                cat.dropTempView(name)
+            else:
+                cat.registerTempView(name, df)
+
+
+def _where(session, df: DataFrame, s: Select) -> DataFrame:
+    """WHERE: [NOT] EXISTS conjuncts become left semi / anti joins with the subquery's
+    relation on the subquery's WHERE (correlated references resolve to the outer side);
+    the remaining conjuncts filter."""
+    from ..frame.join import _conjuncts
+    from .parser import ExistsExpr
+    rest = []
+    for c in _conjuncts(s.where):
+        if isinstance(c, ExistsExpr) and c.sub.where is not None and not c.sub.group_by \
+                and not c.sub.joins and c.sub.table is not None:
+            outer_name = s.alias or (s.table or "").split(".")[-1]
+            left = df if df.__dict__.get("_aliases") else df.alias(outer_name)
+            right = session.catalog.table(c.sub.table).alias(c.sub.alias or c.sub.table.split(".")[-1])
+            df = left.join(right, c.sub.where, "left_anti" if c.neg else "left_semi")
+        else:
+            rest.append(c)
+    for c in rest:
+        df = df.filter(c)
     return df
 
 
@@ -120,14 +227,21 @@ def _zeros(session):
 
 
 def _sql_join(left: DataFrame, right: DataFrame, j, left_name: str = "") -> DataFrame:
+    if j.natural or j.using:
+        cols = j.using or [c for c in left.columns if c in set(right.columns)]
+        return left.join(right, cols, j.how) if cols else left.join(right, None, "cross")
     if j.how == "cross" or j.on is None:
-        return left.join(right, None, "cross")
+        # through the condition join so that "a.k" / "b.k" in WHERE and SELECT pick their side
+        if not left.__dict__.get("_aliases"):
+            left = left.alias(left_name)
+        right = right.alias(j.alias or (j.table or "").split(".")[-1])
+        return left.join(right, E.lit(True), "inner")
     # support equi-joins "a.x = b.y" (and conjunctions of them)
     keys = _equi_keys(j.on)
     if keys is None:                     # general ON condition: hash keys + residual / nested loop
         if not left.__dict__.get("_aliases"):
             left = left.alias(left_name)
-        right = right.alias(j.alias or j.table.split(".")[-1])
+        right = right.alias(j.alias or (j.table or "").split(".")[-1])
         return left.join(right, j.on, j.how)
     lk, rk = zip(*keys)
     if list(lk) == list(rk):

@@ -29,6 +29,10 @@ KEYWORDS = {"select", "from", "where", "group", "by", "order", "having", "limit"
             "exists", "describe", "desc", "with"}
 
 
+# non-reserved words that end a relation / select item instead of naming it
+_NOT_ALIASES = {"intersect", "except", "minus", "lateral", "natural", "semi", "anti", "using", "offset", "window"}
+
+
 @dataclass
 class Tok:
     kind: str
@@ -81,10 +85,20 @@ _TWO_COLUMN_AGGS = {"corr", "covar_pop", "covar_samp", "max_by", "min_by"}
 
 @dataclass
 class Join:
-    table: str
+    table: str | None
     alias: str | None
     how: str
     on: object
+    using: list | None = None           # JOIN ... USING (a, b)
+    natural: bool = False               # NATURAL JOIN: USING every common column
+    subquery: object = None             # JOIN (SELECT ...) alias
+
+
+@dataclass
+class Lateral:
+    gen: object                         # generator Expr (explode / posexplode / inline ...)
+    names: list                         # output column names
+    outer: bool = False
 
 
 @dataclass
@@ -105,6 +119,11 @@ class Select:
     distinct: bool = False
     union: object = None
     union_all: bool = False
+    setop: str = "union"                 # union | intersect | except (with ``union`` = right side)
+    ctes: list = field(default_factory=list)        # WITH name AS (select), ...
+    values: list | None = None           # FROM VALUES (..), (..) [AS t(a, b)]
+    value_names: list | None = None
+    laterals: list = field(default_factory=list)    # LATERAL VIEW [OUTER] gen(..) t AS c
 
 
 class Parser:
@@ -202,7 +221,52 @@ class Parser:
             name = self.qualified()
             self.expect("kw", "as")
             return ("ctas", name, self.select())
+        if self.peek().kind == "kw" and self.peek().val == "create":
+            save = self.i
+            self.i += 1
+            replace = self.kw("or") and self.idw("replace")
+            glob = self.idw("global")
+            temp = self.idw("temporary") or self.idw("temp")
+            if self.idw("view"):
+                self.kw("if", "not", "exists")
+                name = self.qualified()
+                self.expect("kw", "as")
+                sel = self.select()
+                self.accept("op", ";")
+                return ("create_view", name, sel, glob, replace or not temp)
+            self.i = save
+        if self.idw("insert"):
+            overwrite = bool(self.idw("overwrite"))
+            if not overwrite:
+                if not self.idw("into"):
+                    raise SyntaxError("expected INTO or OVERWRITE after INSERT")
+            self.kw("table")
+            name = self.qualified()
+            cols = None
+            if self.peek().val == "(" and not (self.peek(1).kind == "kw" and self.peek(1).val == "select"):
+                self.expect("op", "(")
+                cols = [self.ident()]
+                while self.accept("op", ","):
+                    cols.append(self.ident())
+                self.expect("op", ")")
+            if self.idw("values"):
+                src = ("values", self._values_rows())
+            else:
+                src = ("select", self.select())
+            self.accept("op", ";")
+            return ("insert", name, cols, src, overwrite)
+        ctes = []
+        if self.kw("with"):
+            while True:
+                cname = self.ident()
+                self.expect("kw", "as")
+                self.expect("op", "(")
+                ctes.append((cname, self.select()))
+                self.expect("op", ")")
+                if not self.accept("op", ","):
+                    break
         sel = self.select()
+        sel.ctes = ctes
         self.accept("op", ";")
         if self.peek().kind != "eof":
             raise SyntaxError(f"unexpected trailing input: {self.peek().val!r}")
@@ -216,33 +280,74 @@ class Parser:
             items.append(self.select_item())
         s = Select(items, distinct=distinct)
         if self.kw("from"):
-            if self.accept("op", "("):
-                s.subquery = self.select()
-                self.expect("op", ")")
+            if self.idw("values"):
+                s.values = self._values_rows()
+                s.alias, s.value_names = self._table_alias()
             else:
-                s.table = self.qualified()
-            s.alias = self._alias()
+                if self.accept("op", "("):
+                    s.subquery = self.select()
+                    self.expect("op", ")")
+                else:
+                    s.table = self.qualified()
+                s.alias = self._alias()
             while True:
-                how = None
-                if self.kw("join") or self.kw("inner", "join"):
-                    how = "inner"
-                elif self.kw("left", "outer", "join") or self.kw("left", "join"):
-                    how = "left"
-                elif self.kw("right", "outer", "join") or self.kw("right", "join"):
-                    how = "right"
-                elif self.kw("full", "outer", "join") or self.kw("full", "join"):
-                    how = "outer"
-                elif self.kw("cross", "join"):
+                how, natural = None, False
+                if self.accept("op", ","):                 # FROM a, b  == CROSS JOIN
                     how = "cross"
+                else:
+                    natural = bool(self.idw("natural"))
+                    if self.kw("join") or self.kw("inner", "join"):
+                        how = "inner"
+                    elif self.kw("left", "outer", "join") or self.kw("left", "join"):
+                        how = "left"
+                    elif self.kw("right", "outer", "join") or self.kw("right", "join"):
+                        how = "right"
+                    elif self.kw("full", "outer", "join") or self.kw("full", "join"):
+                        how = "outer"
+                    elif self.kw("cross", "join"):
+                        how = "cross"
+                    elif self.peek().val == "left" and self.peek(1).kind == "id" and \
+                            self.peek(1).val.lower() in ("semi", "anti") and self.peek(2).val == "join":
+                        how = "left_" + self.peek(1).val.lower()
+                        self.i += 3
+                    elif self.peek().kind == "id" and self.peek().val.lower() in ("semi", "anti") and \
+                            self.peek(1).val == "join":
+                        how = "left_" + self.peek().val.lower()
+                        self.i += 2
+                    elif natural:
+                        raise SyntaxError("expected JOIN after NATURAL")
                 if how is None:
                     break
-                t = self.qualified()
+                sub = t = None
+                if self.accept("op", "("):
+                    sub = self.select()
+                    self.expect("op", ")")
+                else:
+                    t = self.qualified()
                 al = self._alias()
-                on = None
-                if how != "cross":
+                on = using = None
+                if natural:
+                    pass
+                elif how != "cross" and self.idw("using"):
+                    self.expect("op", "(")
+                    using = [self.ident()]
+                    while self.accept("op", ","):
+                        using.append(self.ident())
+                    self.expect("op", ")")
+                elif how != "cross":
                     self.expect("kw", "on")
                     on = self.expr()
-                s.joins.append(Join(t, al, how, on))
+                s.joins.append(Join(t, al, how, on, using, natural, sub))
+            while self.idw("lateral", "view"):
+                outer = bool(self.kw("outer"))
+                gen = self.primary()
+                self.ident()                                # table alias of the generator
+                names = []
+                if self.kw("as"):
+                    names.append(self.ident())
+                    while self.accept("op", ","):
+                        names.append(self.ident())
+                s.laterals.append(Lateral(gen, names, outer))
         if self.kw("where"):
             s.where = self.expr()
         if self.kw("group", "by"):
@@ -286,13 +391,50 @@ class Parser:
         if self.kw("union"):
             s.union_all = bool(self.kw("all"))
             s.union = self.select()
+        elif self.idw("intersect") or self.idw("except") or self.idw("minus"):
+            op = self.toks[self.i - 1].val.lower()
+            s.setop = "intersect" if op == "intersect" else "except"
+            s.union_all = bool(self.kw("all"))
+            self.kw("distinct")
+            s.union = self.select()
         return s
+
+    def _values_rows(self) -> list:
+        """VALUES (1, 'a'), (2, 'b')  (or bare scalars: VALUES 1, 2) -> rows of python values."""
+        rows = []
+        while True:
+            if self.accept("op", "("):
+                row = [self._value_literal()]
+                while self.accept("op", ","):
+                    row.append(self._value_literal())
+                self.expect("op", ")")
+            else:
+                row = [self._value_literal()]
+            rows.append(row)
+            if not self.accept("op", ","):
+                return rows
+
+    def _value_literal(self):
+        if self.kw("null"):
+            return None
+        return self.literal_value()
+
+    def _table_alias(self):
+        """[AS] name [(col, ...)] after an inline table."""
+        name = self._alias()
+        cols = None
+        if name is not None and self.accept("op", "("):
+            cols = [self.ident()]
+            while self.accept("op", ","):
+                cols.append(self.ident())
+            self.expect("op", ")")
+        return name, cols
 
     def _alias(self):
         if self.kw("as"):
             return self.ident()
         t = self.peek()
-        if t.kind == "id":
+        if t.kind == "id" and t.val.lower() not in _NOT_ALIASES:
             self.i += 1
             return t.val
         return None
@@ -333,6 +475,9 @@ class Parser:
         return e
 
     def not_expr(self):
+        if self.peek().kind == "kw" and self.peek().val == "not" and self.peek(1).val == "exists":
+            self.i += 2
+            return self._exists(True)
         if self.kw("not"):
             return _unary_map(self.not_expr(), lambda a: ~a)
         return self.cmp_expr()
@@ -356,6 +501,11 @@ class Parser:
             neg = True
         if self.kw("in"):
             self.expect("op", "(")
+            if self.peek().kind == "kw" and self.peek().val == "select":
+                sub = self.select()
+                self.expect("op", ")")
+                r = _unary_map(e, lambda a: _in_subquery(a, sub))
+                return _unary_map(r, lambda a: ~a) if neg else r
             vals = [self.literal_value()]
             while self.accept("op", ","):
                 vals.append(self.literal_value())
@@ -374,6 +524,14 @@ class Parser:
                          lambda a, b: a & b)
             return _unary_map(r, lambda a: ~a) if neg else r
         return e
+
+    def _exists(self, neg: bool):
+        self.expect("op", "(")
+        allow = self._allow_agg
+        sub = self.select()
+        self._allow_agg = allow
+        self.expect("op", ")")
+        return ExistsExpr(sub, neg)
 
     def literal_value(self):
         t = self.next()
@@ -424,9 +582,15 @@ class Parser:
             self.i += 1
             return E.lit(None if t.val == "null" else t.val == "true")
         if self.accept("op", "("):
+            if self.peek().kind == "kw" and self.peek().val == "select":
+                sub = self.select()
+                self.expect("op", ")")
+                return _scalar_subquery(sub)
             e = self.or_expr()
             self.expect("op", ")")
             return e
+        if self.kw("exists"):
+            return self._exists(False)
         if self.kw("cast"):
             self.expect("op", "(")
             e = self.or_expr()
@@ -681,6 +845,43 @@ def _math_fn(fn, args):
             d = torch.round(d, decimals=nd)
         return C.NumericColumn(d, c.valid)
     return E.Expr(run, f"{fn}({e.name})", e.refs)
+
+
+class ExistsExpr(E.Expr):
+    """[NOT] EXISTS (subquery).  In a WHERE conjunct the engine turns it into a left semi /
+    anti join on the subquery's WHERE (so correlated references to the outer relation work);
+    evaluated directly, it is the uncorrelated truth value."""
+
+    def __init__(self, sub, neg: bool):
+        def f(df):
+            from .engine import run_select
+            hit = len(run_select(df.session, sub).limit(1).collect()) > 0
+            return E.lit(hit != neg).eval(df)
+        super().__init__(f, f"{'NOT ' if neg else ''}EXISTS(subquery)")
+        self.sub, self.neg = sub, neg
+
+
+def _subquery_rows(df, sub) -> list:
+    from .engine import run_select
+    return run_select(df.session, sub).collect()
+
+
+def _scalar_subquery(sub):
+    """(SELECT one value): evaluated once per use; no rows -> NULL, more than one -> error."""
+    def f(df):
+        rows = _subquery_rows(df, sub)
+        if len(rows) > 1:
+            raise ValueError("more than one row returned by a subquery used as an expression")
+        return E.lit(rows[0][0] if rows else None).eval(df)
+    return E.Expr(f, "scalarsubquery()")
+
+
+def _in_subquery(a, sub):
+    """x IN (SELECT c ...): membership in the subquery's first column."""
+    def f(df):
+        vals = [r[0] for r in _subquery_rows(df, sub)]
+        return a.isin([v for v in vals if v is not None]).eval(df)
+    return E.Expr(f, f"({a.name} IN (listquery()))", a.refs)
 
 
 def parse(sql: str):

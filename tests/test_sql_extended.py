@@ -1,0 +1,127 @@
+"""SparkSQL surface beyond single SELECTs (the "Data Frame" widget runs arbitrary
+``hc.sql(query)``, reference orangecontrib/spark/widgets/data/spark_sql_dataframe.py:83-94):
+CTEs, IN / EXISTS / scalar subqueries (correlated EXISTS as semi / anti joins), INTERSECT /
+EXCEPT [ALL], comma joins with qualified WHERE, JOIN USING / NATURAL / SEMI / ANTI, joins
+on subqueries, LATERAL VIEW, inline VALUES tables, CREATE VIEW, INSERT INTO / OVERWRITE.
+Each checked against a pandas / Python oracle."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from orange3_spark_amd import Session, SessionConf
+
+
+@pytest.fixture(scope="module")
+def s(tmp_path_factory):
+    conf = SessionConf().set("o3s.device", "cpu").set("spark.sql.warehouse.dir",
+                                                       str(tmp_path_factory.mktemp("wh")))
+    sess = Session(conf)
+    sess.createDataFrame(_t()).createOrReplaceTempView("t")
+    sess.createDataFrame(_u()).createOrReplaceTempView("u")
+    return sess
+
+
+def _t():
+    rng = np.random.default_rng(5)
+    return pd.DataFrame({"k": rng.integers(0, 8, 40), "v": rng.normal(size=40).round(6),
+                         "g": rng.choice(["a", "b", "c"], 40)})
+
+
+def _u():
+    rng = np.random.default_rng(6)
+    return pd.DataFrame({"k": rng.integers(3, 12, 15), "w": rng.normal(size=15).round(6)})
+
+
+def _rows(df):
+    return sorted(tuple(r) for r in df.collect())
+
+
+def test_cte_chain(s):
+    got = _rows(s.sql("WITH a AS (SELECT k, v FROM t WHERE v > 0), b AS (SELECT k, v FROM a WHERE k > 2) "
+                      "SELECT k, v FROM b"))
+    t = _t()
+    assert got == sorted(map(tuple, t[(t.v > 0) & (t.k > 2)][["k", "v"]].itertuples(index=False)))
+    with pytest.raises(KeyError):                       # CTE names do not leak out of the statement
+        s.sql("SELECT * FROM a").collect()
+
+
+def test_in_and_scalar_subqueries(s):
+    t, u = _t(), _u()
+    got = _rows(s.sql("SELECT k, v FROM t WHERE k IN (SELECT k FROM u WHERE w > 0)"))
+    keys = set(u[u.w > 0].k)
+    assert got == sorted(map(tuple, t[t.k.isin(keys)][["k", "v"]].itertuples(index=False)))
+    got = _rows(s.sql("SELECT k FROM t WHERE k NOT IN (SELECT k FROM u)"))
+    assert got == sorted((k,) for k in t.k if k not in set(u.k))
+    got = s.sql("SELECT k, (SELECT max(w) FROM u) AS mw FROM t WHERE v > 1").collect()
+    assert all(r.mw == pytest.approx(u.w.max()) for r in got) and len(got) == int((t.v > 1).sum())
+    with pytest.raises(ValueError, match="more than one row"):
+        s.sql("SELECT (SELECT k FROM u) AS x FROM t").collect()
+
+
+def test_correlated_exists(s):
+    t, u = _t(), _u()
+    got = _rows(s.sql("SELECT k, v FROM t WHERE EXISTS (SELECT 1 FROM u WHERE u.k = t.k AND u.w > 0.2)"))
+    ok = {k for k, w in zip(u.k, u.w) if w > 0.2}
+    assert got == sorted((k, v) for k, v in zip(t.k, t.v) if k in ok)
+    got = _rows(s.sql("SELECT k, v FROM t tt WHERE v < 0 AND NOT EXISTS (SELECT 1 FROM u WHERE u.k = tt.k)"))
+    assert got == sorted((k, v) for k, v in zip(t.k, t.v) if v < 0 and k not in set(u.k))
+
+
+@pytest.mark.parametrize("op,fn", [
+    ("INTERSECT", lambda a, b: sorted(set(a) & set(b))),
+    ("EXCEPT", lambda a, b: sorted(set(a) - set(b))),
+    ("MINUS", lambda a, b: sorted(set(a) - set(b))),
+    ("INTERSECT ALL", lambda a, b: sorted((pd.Series(a).value_counts().combine(
+        pd.Series(b).value_counts(), min, 0)).pipe(lambda c: [k for k, n in c.items() for _ in range(int(n))]))),
+    ("EXCEPT ALL", lambda a, b: sorted((pd.Series(a).value_counts().sub(
+        pd.Series(b).value_counts(), fill_value=0)).pipe(lambda c: [k for k, n in c.items() for _ in range(max(int(n), 0))]))),
+])
+def test_set_operations(s, op, fn):
+    t, u = _t(), _u()
+    got = [r[0] for r in _rows(s.sql(f"SELECT k FROM t {op} SELECT k FROM u"))]
+    assert got == fn(list(t.k), list(u.k))
+
+
+def test_comma_join_using_natural_semi_anti(s):
+    t, u = _t(), _u()
+    m = t.merge(u, on="k")
+    want = sorted(zip(m.k, m.v, m.w))
+    assert _rows(s.sql("SELECT x.k, x.v, y.w FROM t x, u y WHERE x.k = y.k")) == want
+    assert _rows(s.sql("SELECT k, v, w FROM t JOIN u USING (k)")) == want
+    assert _rows(s.sql("SELECT k, v, w FROM t NATURAL JOIN u")) == want
+    semi = _rows(s.sql("SELECT * FROM t LEFT SEMI JOIN u ON t.k = u.k"))
+    assert semi == sorted(map(tuple, t[t.k.isin(set(u.k))].itertuples(index=False)))
+    anti = _rows(s.sql("SELECT * FROM t LEFT ANTI JOIN u ON t.k = u.k"))
+    assert anti == sorted(map(tuple, t[~t.k.isin(set(u.k))].itertuples(index=False)))
+    q = _rows(s.sql("SELECT t.k, q.w2 FROM t JOIN (SELECT k, w * 2 AS w2 FROM u) q ON t.k = q.k"))
+    assert q == sorted(zip(m.k, (m.w * 2)))
+
+
+def test_lateral_view_and_values(s):
+    got = _rows(s.sql("SELECT k, e FROM t LATERAL VIEW explode(array(k, k + 1)) tt AS e WHERE v > 1"))
+    t = _t()
+    assert got == sorted((k, e) for k, v in zip(t.k, t.v) if v > 1 for e in (k, k + 1))
+    vals = s.sql("SELECT x, y FROM VALUES (1, 'a'), (2, 'b'), (3, NULL) AS tab(x, y) WHERE x > 1").collect()
+    assert [tuple(r) for r in vals] == [(2, "b"), (3, None)]
+
+
+def test_views_and_inserts(s):
+    s.sql("CREATE OR REPLACE TEMP VIEW big AS SELECT k, v FROM t WHERE v > 0")
+    t = _t()
+    assert s.sql("SELECT count(*) AS n FROM big").collect()[0].n == int((t.v > 0).sum())
+    s.sql("CREATE TABLE tab_ins AS SELECT k, v, g FROM t WHERE k = 1")
+    n0 = int((t.k == 1).sum())
+    s.sql("INSERT INTO tab_ins VALUES (99, 1.5, 'z'), (98, -1.5, 'y')")
+    s.sql("INSERT INTO TABLE tab_ins SELECT k, w, 'u' FROM u WHERE k = 5")
+    n_u = int((_u().k == 5).sum())
+    got = s.sql("SELECT k, v, g FROM tab_ins").collect()
+    assert len(got) == n0 + 2 + n_u
+    assert (99, 1.5, "z") in [tuple(r) for r in got]
+    s.sql("INSERT INTO tab_ins (k, g) VALUES (77, 'n')")           # unlisted column -> NULL
+    r = [x for x in s.sql("SELECT * FROM tab_ins").collect() if x.k == 77][0]
+    assert r.g == "n" and (r.v is None or r.v != r.v)
+    s.sql("INSERT OVERWRITE TABLE tab_ins SELECT k, v, g FROM t WHERE k = 2")
+    assert s.sql("SELECT count(*) AS n FROM tab_ins").collect()[0].n == int((t.k == 2).sum())
+    with pytest.raises(ValueError, match="temporary view"):
+        s.sql("INSERT INTO t VALUES (1, 1.0, 'a')")
+    s.sql("DROP TABLE tab_ins")
