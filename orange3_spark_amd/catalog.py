@@ -167,6 +167,9 @@ class Catalog:
 
     def uncacheTable(self, name: str) -> None:
         self._cached.pop(name, None)
+        view = self._temp.get(name)
+        if view is not None and hasattr(view, "unpersist"):
+            view.unpersist()
 
     def clearCache(self) -> None:
         self._cached.clear()

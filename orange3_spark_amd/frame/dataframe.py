@@ -938,7 +938,7 @@ class PivotedData(GroupedData):
         table = {(tuple(_hashable(x) for x in r[:nk]), _hashable(r[nk])): r[nk + 1:] for r in keyed}
         out = OrderedDict()
         for i, k in enumerate(self.keys):
-            out[k.name] = C.from_numpy(np.array([g[i] for g in groups], dtype=object), "cpu")
+            out[k.name] = _nullable_column([g[i] for g in groups])     # numeric keys stay numeric
         for v in values:
             for j, a in enumerate(aggs):
                 name = str(v) if len(aggs) == 1 else f"{v}_{a.name}"

@@ -30,6 +30,28 @@ def execute(session, query: str) -> DataFrame:
         names = cat.tableNames(db)
         return _strings_df(session, {"namespace": [db] * len(names), "tableName": names,
                                      "isTemporary": ["true" if n in cat._temp else "false" for n in names]})
+    if kind == "show_columns":
+        return _strings_df(session, {"col_name": cat.table(stmt[1]).columns})
+    if kind == "show_functions":
+        from . import functions as F
+        from .parser import _SQL_ONLY
+        names = sorted({n for n in dir(F) if not n.startswith("_") and callable(getattr(F, n))
+                        and not isinstance(getattr(F, n), type)} | set(_SQL_ONLY))
+        return _strings_df(session, {"function": names})
+    if kind == "explain":
+        return _strings_df(session, {"plan": [_explain(stmt[1], stmt[2])]})
+    if kind == "cache":
+        _, name, sel, _lazy = stmt
+        if sel is not None:
+            run_select(session, sel).createOrReplaceTempView(name)
+        cat.cacheTable(name)
+        return session.emptyDataFrame()
+    if kind == "uncache":
+        cat.uncacheTable(stmt[1])
+        return session.emptyDataFrame()
+    if kind == "refresh":
+        cat.refreshTable(stmt[1])
+        return session.emptyDataFrame()
     if kind == "use":
         cat.setCurrentDatabase(stmt[1])
         return session.emptyDataFrame()
@@ -66,6 +88,39 @@ def execute(session, query: str) -> DataFrame:
     if kind == "insert":
         return _insert(session, *stmt[1:])
     return run_select(session, stmt[1])
+
+
+def _explain(stmt, text: str) -> str:
+    """Execution outline of a statement (operators are eager device ops, so the 'plan' is the
+    order in which they run)."""
+    if stmt[0] != "select":
+        return f"== Physical Plan ==\nExecute {stmt[0].upper()}: {text}"
+    s = stmt[1]
+    steps = []
+    if s.ctes:
+        steps.append("WithCTE " + ", ".join(n for n, _ in s.ctes))
+    src = s.table or ("VALUES" if s.values is not None else ("Subquery" if s.subquery is not None else "OneRow"))
+    steps.append(f"Scan {src}" + (f" TABLESAMPLE {s.sample}" if s.sample else ""))
+    for j in s.joins:
+        kind = "BroadcastHashJoin" if (j.using or j.natural or j.on is not None) else "BroadcastNestedLoopJoin"
+        steps.append(f"{kind} {j.how} {j.table or 'subquery'}" + (f" ON {j.on.name}" if j.on is not None else ""))
+    if s.pivot:
+        steps.append(f"Pivot FOR {s.pivot[1]}")
+    steps += [f"Generate {lv.gen.name}" for lv in s.laterals]
+    if s.where is not None:
+        steps.append(f"Filter {s.where.name}")
+    if s.group_by or any(isinstance(it.expr, (AggCall, _AggExpr)) for it in s.items):
+        steps.append("HashAggregate (device segmented reduction + all-reduce)")
+    if s.order_by:
+        steps.append("Sort (range exchange + local sort)")
+    steps.append("Project " + ", ".join(it.alias or (it.expr if isinstance(it.expr, str) else
+                                                      getattr(it.expr, "name", None) or getattr(it.expr, "text", "?"))
+                                          for it in s.items))
+    if s.limit is not None:
+        steps.append(f"Limit {s.limit}")
+    if s.union is not None:
+        steps.append(f"{s.setop.capitalize()}{' All' if s.union_all else ''} (second query)")
+    return "== Physical Plan ==\n" + "\n".join(("+- " if i else "") + st for i, st in enumerate(steps))
 
 
 def _insert(session, name, cols, src, overwrite) -> DataFrame:
@@ -111,11 +166,16 @@ def run_select(session, s: Select) -> DataFrame:
         df = run_select(session, s.subquery)
     elif s.table is not None:
         df = session.catalog.table(s.table)
+        if s.sample is not None:
+            unit, n = s.sample
+            df = df.sample(fraction=n / 100.0, seed=0) if unit == "percent" else df.limit(int(n))
     else:
         df = DataFrame(session, OrderedDict(_dummy=C.NumericColumn(_zeros(session))), 1 if session.rank == 0 else 0)
     for j in s.joins:
         right = run_select(session, j.subquery) if j.subquery is not None else session.catalog.table(j.table)
         df = _sql_join(df, right, j, s.alias or (s.table or "").split(".")[-1])
+    if s.pivot is not None:
+        df = _pivot(df, s.pivot)
     for lv in s.laterals:
         from . import functions as F
         gen = lv.gen
@@ -129,6 +189,7 @@ def run_select(session, s: Select) -> DataFrame:
             df = df.select("*", gen.alias(names[0]))
     if s.where is not None:
         df = _where(session, df, s)
+    s = _resolve_ordinals(s)
     has_agg = any(isinstance(it.expr, (AggCall, _AggExpr)) for it in s.items) or s.group_by
     if has_agg:
         df = _aggregate(df, s)
@@ -180,6 +241,67 @@ def run_select(session, s: Select) -> DataFrame:
             if not s.union_all:
                 df = df.distinct()
     return df
+
+
+def _resolve_ordinals(s: Select) -> Select:
+    """GROUP BY / ORDER BY <n> (1-based select position) and GROUP BY <select alias>."""
+    import dataclasses
+
+    def item(e):
+        lit = getattr(e, "_literal", None)
+        if isinstance(lit, int) and not isinstance(lit, bool):
+            if not 1 <= lit <= len(s.items) or isinstance(s.items[lit - 1].expr, str):
+                raise ValueError(f"ordinal {lit} is out of range of the select list")
+            return s.items[lit - 1]
+        return None
+
+    aliases = {it.alias: it.expr for it in s.items if it.alias and not isinstance(it.expr, str)}
+    changed = False
+    groups = []
+    for g in s.group_by:
+        it = item(g)
+        if it is not None:
+            g, changed = it.expr, True
+        elif getattr(g, "_colname", None) in aliases and not isinstance(aliases[g._colname], (AggCall, _AggExpr)):
+            g, changed = aliases[g._colname].alias(g._colname), True
+        groups.append(g)
+    orders = []
+    for e, a in s.order_by:
+        it = item(e)
+        if it is not None:
+            e, changed = (E.col(it.alias or it.expr.name) if not isinstance(it.expr, (AggCall, _AggExpr))
+                          else it.expr), True
+        orders.append((e, a))
+    return dataclasses.replace(s, group_by=groups, order_by=orders) if changed else s
+
+
+def _pivot(df: DataFrame, spec) -> DataFrame:
+    """FROM ... PIVOT (agg [AS a], ... FOR col IN (v [AS n], ...)): group by every column not
+    pivoted or aggregated; one output column per (value, aggregate)."""
+    aggs, col, vals = spec
+    used = {col}
+    built = []
+    for a, alias in aggs:
+        ae = _as_agg_expr(a)
+        for c in ae.aggs:
+            used.update(getattr(c.arg, "refs", ()) or ())
+        if len(ae.aggs) != 1 or not isinstance(a, AggCall):
+            raise ValueError("PIVOT supports plain aggregate calls")
+        c = ae.aggs[0]
+        ag = c.built if c.built is not None else E.Agg(c.fn, c.arg, c.text, c.distinct)
+        built.append((ag, alias or c.text))
+    keys = [c for c in df.columns if c not in used]
+    values = [v for v, _ in vals]
+    out = df.groupBy(*keys).pivot(col, values).agg(*[ag.alias(n) for ag, n in built])
+    ren = {}
+    for v, name in vals:
+        for ag, n in built:
+            src = str(v) if len(built) == 1 else f"{v}_{n}"
+            ren[src] = (name or str(v)) if len(built) == 1 else f"{name or v}_{n}"
+    for a, b in ren.items():
+        if a in out.columns and a != b:
+            out = out.withColumnRenamed(a, b)
+    return out
 
 
 def _with_ctes(session, s: Select) -> DataFrame:
@@ -306,7 +428,12 @@ def _aggregate(df: DataFrame, s: Select) -> DataFrame:
         if isinstance(e, _AggExpr):
             sel.append(e.build(names).alias(alias))
         else:
-            sel.append(E.col(e.name).alias(alias) if e.name in g.columns else e.alias(alias))
+            if e.name in g.columns:
+                sel.append(E.col(e.name).alias(alias))
+            elif alias in g.columns:                      # GROUP BY <select alias>
+                sel.append(E.col(alias))
+            else:
+                sel.append(e.alias(alias))
     extra = [k for k in aggs if k not in {a for _, a in post}]
     out = g.select(*sel, *[E.col(k) for k in extra if s.order_by])
     return out

@@ -18,7 +18,7 @@ _TOKEN = re.compile(r"""
   | (?P<num>\d+\.\d*(?:[eE][-+]?\d+)?|\.\d+(?:[eE][-+]?\d+)?|\d+(?:[eE][-+]?\d+)?)
   | (?P<str>'(?:[^']|'')*')
   | (?P<qid>`[^`]+`|"[^"]+")
-  | (?P<op><=|>=|<>|!=|==|\|\||[-+*/%(),.;=<>])
+  | (?P<op><=|>=|<>|!=|==|\|\||[-+*/%(),.;=<>\[\]])
   | (?P<id>[A-Za-z_][A-Za-z0-9_]*)
 """, re.X)
 
@@ -30,7 +30,8 @@ KEYWORDS = {"select", "from", "where", "group", "by", "order", "having", "limit"
 
 
 # non-reserved words that end a relation / select item instead of naming it
-_NOT_ALIASES = {"intersect", "except", "minus", "lateral", "natural", "semi", "anti", "using", "offset", "window"}
+_NOT_ALIASES = {"intersect", "except", "minus", "lateral", "natural", "semi", "anti", "using", "offset", "window",
+                "tablesample", "pivot", "nulls", "for", "filter"}
 
 
 @dataclass
@@ -124,6 +125,8 @@ class Select:
     values: list | None = None           # FROM VALUES (..), (..) [AS t(a, b)]
     value_names: list | None = None
     laterals: list = field(default_factory=list)    # LATERAL VIEW [OUTER] gen(..) t AS c
+    sample: tuple | None = None          # TABLESAMPLE (x PERCENT | n ROWS)
+    pivot: tuple | None = None           # PIVOT (aggs FOR col IN (values))
 
 
 class Parser:
@@ -205,6 +208,33 @@ class Parser:
             return ("show_tables", db)
         if self.kw("use"):
             return ("use", self.ident())
+        if self.kw("show") and self.idw("columns"):
+            if not (self.kw("in") or self.kw("from")):
+                raise SyntaxError("expected FROM / IN after SHOW COLUMNS")
+            name = self.qualified()
+            if self.kw("in") or self.kw("from"):
+                name = self.ident() + "." + name
+            return ("show_columns", name)
+        if self.peek(-1).val == "show" and self.idw("functions"):
+            return ("show_functions",)
+        if self.idw("explain"):
+            self.idw("extended") or self.idw("formatted") or self.idw("codegen")
+            start = self.i
+            inner = self.statement()
+            return ("explain", inner, " ".join(t.val for t in self.toks[start:-1]))
+        if self.idw("cache"):
+            lazy = bool(self.idw("lazy"))
+            self.kw("table")
+            name = self.qualified()
+            sel = self.select() if self.kw("as") else None
+            return ("cache", name, sel, lazy)
+        if self.idw("uncache"):
+            self.kw("table")
+            self.kw("if", "exists")
+            return ("uncache", self.qualified())
+        if self.idw("refresh"):
+            self.kw("table")
+            return ("refresh", self.qualified())
         if self.kw("create", "database"):
             ine = self.kw("if", "not", "exists")
             return ("create_database", self.ident(), ine)
@@ -289,6 +319,12 @@ class Parser:
                     self.expect("op", ")")
                 else:
                     s.table = self.qualified()
+                if self.idw("tablesample"):
+                    self.expect("op", "(")
+                    n = float(self.expect("num").val)
+                    unit = self.ident().lower()
+                    self.expect("op", ")")
+                    s.sample = ("percent" if unit == "percent" else "rows", n)
                 s.alias = self._alias()
             while True:
                 how, natural = None, False
@@ -338,6 +374,8 @@ class Parser:
                     self.expect("kw", "on")
                     on = self.expr()
                 s.joins.append(Join(t, al, how, on, using, natural, sub))
+            if self.idw("pivot"):
+                s.pivot = self._pivot_clause()
             while self.idw("lateral", "view"):
                 outer = bool(self.kw("outer"))
                 gen = self.primary()
@@ -455,7 +493,39 @@ class Parser:
             asc = False
         else:
             self.kw("asc")
+        if self.idw("nulls"):
+            first = bool(self.idw("first"))
+            if not first and not self.idw("last"):
+                raise SyntaxError("expected FIRST or LAST after NULLS")
+            if not _is_agg(e):
+                e = (e.asc_nulls_first() if first else e.asc_nulls_last()) if asc else \
+                    (e.desc_nulls_first() if first else e.desc_nulls_last())
+                asc = True                           # direction now carried by the sort expression
         return (e, asc)
+
+    def _pivot_clause(self):
+        """PIVOT (agg [AS a], ... FOR col IN (v [AS name], ...))."""
+        self.expect("op", "(")
+        aggs = []
+        while True:
+            a = self.expr(allow_agg=True)
+            aggs.append((a, self._alias()))
+            if not self.accept("op", ","):
+                break
+        if not self.idw("for"):
+            raise SyntaxError("expected FOR in PIVOT")
+        col = self.ident()
+        self.expect("kw", "in")
+        self.expect("op", "(")
+        vals = []
+        while True:
+            v = self._value_literal()
+            vals.append((v, self._alias()))
+            if not self.accept("op", ","):
+                break
+        self.expect("op", ")")
+        self.expect("op", ")")
+        return (aggs, col, vals)
 
     # -- expressions -------------------------------------------------------------
     def expr(self, allow_agg=False):
@@ -496,7 +566,8 @@ class Parser:
             self.expect("kw", "null")
             return _unary_map(e, (lambda a: a.isNotNull()) if neg else (lambda a: a.isNull()))
         neg = False
-        if self.peek().kind == "kw" and self.peek().val == "not" and self.peek(1).val in ("in", "like", "between"):
+        if self.peek().kind == "kw" and self.peek().val == "not" and \
+                self.peek(1).val.lower() in ("in", "like", "between", "rlike", "regexp", "ilike"):
             self.i += 1
             neg = True
         if self.kw("in"):
@@ -515,6 +586,11 @@ class Parser:
         if self.kw("like"):
             pat = self.expect("str").val[1:-1].replace("''", "'")
             r = _unary_map(e, lambda a: a.like(pat))
+            return _unary_map(r, lambda a: ~a) if neg else r
+        if self.peek().kind == "id" and self.peek().val.lower() in ("rlike", "regexp", "ilike"):
+            op = self.next().val.lower()
+            pat = self.expect("str").val[1:-1].replace("''", "'")
+            r = _unary_map(e, (lambda a: a.ilike(pat)) if op == "ilike" else (lambda a: a.rlike(pat)))
             return _unary_map(r, lambda a: ~a) if neg else r
         if self.kw("between"):
             lo = self.add_expr()
@@ -556,10 +632,12 @@ class Parser:
 
     def mul_expr(self):
         e = self.unary()
-        while self.peek().kind == "op" and self.peek().val in ("*", "/", "%"):
-            op = self.next().val
+        while (self.peek().kind == "op" and self.peek().val in ("*", "/", "%")) or \
+                (self.peek().kind == "id" and self.peek().val.lower() == "div"):
+            op = self.next().val.lower()
             r = self.unary()
-            e = _combine(e, r, {"*": lambda a, b: a * b, "/": lambda a, b: a / b, "%": lambda a, b: a % b}[op])
+            e = _combine(e, r, {"*": lambda a, b: a * b, "/": lambda a, b: a / b, "%": lambda a, b: a % b,
+                                "div": _int_div}[op])
         return e
 
     def unary(self):
@@ -567,7 +645,12 @@ class Parser:
             return _unary_map(self.unary(), lambda a: -a)
         if self.accept("op", "+"):
             return self.unary()
-        return self.primary()
+        e = self.primary()
+        while self.accept("op", "["):                 # arr[i] (0-based) / map[key]
+            k = self.or_expr()
+            self.expect("op", "]")
+            e = _subscript(e, k)
+        return e
 
     def primary(self):
         t = self.peek()
@@ -600,11 +683,17 @@ class Parser:
                 while not self.accept("op", ")"):
                     self.next()
             self.expect("op", ")")
+            if ty.lower() in ("date", "timestamp"):
+                from . import functions as F
+                return _unary_map(e, F.to_date if ty.lower() == "date" else F.to_timestamp)
             return _unary_map(e, lambda a: a.cast(ty))
         if self.kw("case"):
             cases = []
+            operand = None if (self.peek().kind == "kw" and self.peek().val == "when") else self.or_expr()
             while self.kw("when"):
                 c = self.or_expr()
+                if operand is not None:                  # CASE x WHEN v THEN ...
+                    c = operand == c
                 self.expect("kw", "then")
                 v = self.or_expr()
                 cases.append((c, v))
@@ -716,6 +805,13 @@ class Parser:
             text = f"{canon}({'DISTINCT ' if distinct else ''}{'1' if arg is None else arg.name})"
             if canon == "count" and arg is None:
                 text = "count(1)"
+            if self.peek().kind == "id" and self.peek().val.lower() == "filter" and self.peek(1).val == "(":
+                self.i += 2                          # agg(x) FILTER (WHERE cond): rows failing cond ignored
+                self.expect("kw", "where")
+                cond = self.or_expr()
+                self.expect("op", ")")
+                arg = E.when(cond, E.lit(1) if arg is None else arg)
+                text = f"{text} FILTER (WHERE {cond.name})"
             return AggCall(canon, arg, distinct, text)
         args = []
         if not self.accept("op", ")"):
@@ -745,6 +841,74 @@ _SCALAR_NAMES = {"value", "format", "sep", "pattern", "replacement", "idx", "pos
                  "numBits", "scale", "days", "limit", "substr", "asc", "i", "seed"}
 
 
+def _int_div(a, b):
+    """a DIV b: integral quotient truncated toward zero (Spark), NULL on division by zero."""
+    def f(df):
+        import torch
+        from ..frame import column as C
+        x, y = a.eval(df), b.eval(df)
+        xd, yd = x.data.to(torch.float64), y.data.to(torch.float64)
+        q = torch.trunc(xd / torch.where(yd == 0, torch.ones_like(yd), yd)).to(torch.int64)
+        valid = yd != 0
+        for c in (x, y):
+            if getattr(c, "valid", None) is not None:
+                valid = valid & c.valid
+        return C.NumericColumn(q, None if bool(valid.all()) else valid)
+    return E.Expr(f, f"({a.name} DIV {b.name})", a.refs + b.refs)
+
+
+def _subscript(base, key):
+    """SQL ``base[key]``: 0-based array element, map value, or vector component."""
+    def f(df):
+        from ..frame import column as C
+        from ..frame.dataframe import _nullable_column
+        c = base.eval(df)
+        k = key.eval_literal() if hasattr(key, "_literal") else None
+        if isinstance(c, (C.VectorColumn, C.SparseVectorColumn)):
+            return base.getItem(int(k)).eval(df)
+        keys = [k] * len(c) if k is not None else key.eval(df).to_pylist()
+        out = []
+        for v, kk in zip(c.to_pylist(), keys):
+            if v is None or kk is None:
+                out.append(None)
+            elif isinstance(v, dict):
+                out.append(v.get(kk))
+            else:
+                i = int(kk)
+                out.append(v[i] if 0 <= i < len(v) else None)
+        return _nullable_column(out)
+    return E.Expr(f, f"{base.name}[{key.name}]", base.refs + key.refs)
+
+
+def _typeof(e):
+    def f(df):
+        import numpy as np
+        from ..frame import column as C
+        c = e.eval(df)
+        return C.StringColumn(np.array([c.dtype.simpleString()] * len(c), dtype=object))
+    return E.Expr(f, f"typeof({e.name})", e.refs)
+
+
+def _named_struct(*args):
+    from . import functions as F
+    if len(args) % 2:
+        raise SyntaxError("named_struct expects name, value pairs")
+    return F.struct(*[v.alias(k.eval_literal()) for k, v in zip(args[::2], args[1::2])])
+
+
+# SQL-only spellings (Hive / Spark SQL built-ins without a pyspark.sql.functions twin)
+_SQL_ONLY = {
+    "if": lambda c, a, b: E.when(c, a).otherwise(b),
+    "iff": lambda c, a, b: E.when(c, a).otherwise(b),
+    "nvl": lambda a, b: E.coalesce(a, b),
+    "ifnull": lambda a, b: E.coalesce(a, b),
+    "nvl2": lambda a, b, c: E.when(a.isNotNull(), b).otherwise(c),
+    "nullif": lambda a, b: E.when(a == b, E.lit(None)).otherwise(a),
+    "typeof": _typeof,
+    "named_struct": _named_struct,
+}
+
+
 def _resolve_function(name, fn, args):
     """Registered UDFs (spark.udf.register), then any ``sql.functions`` function by name.
     Literal arguments bound to scalar parameters (``substring(s, 1, 3)``) are passed as
@@ -755,6 +919,8 @@ def _resolve_function(name, fn, args):
     u = lookup(fn)
     if u is not None:
         return u(*args)
+    if fn in _SQL_ONLY:
+        return _SQL_ONLY[fn](*args)
     g = getattr(F, fn, None)
     if fn.startswith("_") or not callable(g) or isinstance(g, type):
         raise SyntaxError(f"unknown function {name}")

@@ -125,3 +125,56 @@ def test_views_and_inserts(s):
     with pytest.raises(ValueError, match="temporary view"):
         s.sql("INSERT INTO t VALUES (1, 1.0, 'a')")
     s.sql("DROP TABLE tab_ins")
+
+
+def test_ordinals_aliases_filter_case_nulls(s):
+    t = _t()
+    got = [tuple(r) for r in s.sql("SELECT g, count(*) FROM t GROUP BY 1 ORDER BY 2 DESC, 1").collect()]
+    vc = t.g.value_counts()
+    assert got == sorted(((g, int(n)) for g, n in vc.items()), key=lambda x: (-x[1], x[0]))
+    got = _rows(s.sql("SELECT k AS key, sum(v) AS sv FROM t GROUP BY key"))
+    want = t.groupby("k").v.sum()
+    assert [r[0] for r in got] == list(want.index) and np.allclose([r[1] for r in got], want.values)
+    r = s.sql("SELECT count(*) FILTER (WHERE v > 0) AS c, sum(v) FILTER (WHERE k < 3) AS sv FROM t").collect()[0]
+    assert r.c == int((t.v > 0).sum()) and r.sv == pytest.approx(t.v[t.k < 3].sum())
+    got = [r.c for r in s.sql("SELECT CASE k WHEN 1 THEN 'one' WHEN 2 THEN 'two' ELSE 'many' END AS c FROM t")
+           .collect()]
+    assert got == [{1: "one", 2: "two"}.get(k, "many") for k in t.k]
+    s.createDataFrame(pd.DataFrame({"x": [2.0, None, 1.0, None, 3.0]})).createOrReplaceTempView("nl")
+    assert [r.x for r in s.sql("SELECT x FROM nl ORDER BY x NULLS LAST").collect()][:3] == [1.0, 2.0, 3.0]
+    assert [r.x for r in s.sql("SELECT x FROM nl ORDER BY x DESC NULLS FIRST").collect()][2:] == [3.0, 2.0, 1.0]
+
+
+def test_sql_functions_and_operators(s):
+    t = _t()
+    r = s.sql("SELECT k DIV 3 AS d, IF(v > 0, 'p', 'n') AS sgn, nvl(NULL, k) AS nk, nullif(k, 2) AS nn, "
+              "array(k, k + 1)[1] AS a1, typeof(v) AS tv FROM t").collect()
+    for row, k, v in zip(r, t.k, t.v):
+        assert row.d == k // 3 and row.sgn == ("p" if v > 0 else "n") and row.nk == k and row.a1 == k + 1
+        assert (row.nn is None) if k == 2 else row.nn == k
+        assert row.tv == "double"
+    got = _rows(s.sql("SELECT g FROM t WHERE g RLIKE '^[ab]$' AND g NOT ILIKE 'B'"))
+    assert got == sorted((g,) for g in t.g if g == "a")
+    d = s.sql("SELECT CAST('2024-03-05' AS DATE) AS d").collect()[0].d
+    assert str(d).startswith("2024-03-05")
+
+
+def test_pivot_sample_show_explain_cache(s):
+    t = _t()
+    out = s.sql("SELECT * FROM (SELECT k, g, v FROM t) PIVOT (sum(v) FOR g IN ('a', 'b' AS bee))").collect()
+    p = t.pivot_table(index="k", columns="g", values="v", aggfunc="sum")
+    for r in out:
+        assert r.a == pytest.approx(p.loc[r.k, "a"]) if not np.isnan(p.loc[r.k, "a"]) else r.a is None
+        assert r.bee == pytest.approx(p.loc[r.k, "b"]) if not np.isnan(p.loc[r.k, "b"]) else r.bee is None
+    n = s.sql("SELECT count(*) AS n FROM t TABLESAMPLE (50 PERCENT)").collect()[0].n
+    assert 0 < n < len(t)
+    assert s.sql("SELECT * FROM t TABLESAMPLE (7 ROWS)").count() == 7
+    assert [r.col_name for r in s.sql("SHOW COLUMNS FROM t").collect()] == ["k", "v", "g"]
+    fns = {r.function for r in s.sql("SHOW FUNCTIONS").collect()}
+    assert {"abs", "explode", "nvl", "if"} <= fns
+    plan = s.sql("EXPLAIN SELECT g, count(*) FROM t JOIN u ON t.k = u.k WHERE v > 0 GROUP BY g").collect()[0].plan
+    assert "BroadcastHashJoin" in plan and "Filter" in plan and "HashAggregate" in plan
+    s.sql("CACHE TABLE tc AS SELECT k FROM t WHERE k > 5")
+    assert s.catalog.isCached("tc") and s.sql("SELECT count(*) AS n FROM tc").collect()[0].n == int((t.k > 5).sum())
+    s.sql("UNCACHE TABLE tc")
+    assert not s.catalog.isCached("tc")
