@@ -193,6 +193,7 @@ def aggregate(df, keys: list, aggs: list):
                 parts[tag + sfx] = z(v)
             continue
         if a.distinct or a.fn in ("collect_list", "collect_set", "first", "last", "percentile", "median", "mode",
+                                  "percentile_exact",
                                   "product", "bool_and", "bool_or", "max_by", "min_by") or \
                 not isinstance(vals, C.NumericColumn):
             # host path: (group, value) pairs or per-group python reductions
@@ -377,6 +378,16 @@ def _host_final(a, pairs):
         return all(bool(v) for v in nn)
     if a.fn == "bool_or":
         return any(bool(v) for v in nn)
+    if a.fn == "percentile_exact":                   # Spark percentile: linear interpolation
+        vs = sorted(float(v) for v in nn)
+        ps = a.param if isinstance(a.param, (list, tuple)) else [a.param]
+        res = []
+        for p in ps:
+            pos = float(p) * (len(vs) - 1)
+            lo = int(math.floor(pos))
+            hi = min(lo + 1, len(vs) - 1)
+            res.append(vs[lo] + (vs[hi] - vs[lo]) * (pos - lo))
+        return res if isinstance(a.param, (list, tuple)) else res[0]
     if a.fn == "percentile":
         vs = sorted(nn)
         ps = a.param if isinstance(a.param, (list, tuple)) else [a.param]
@@ -398,7 +409,8 @@ def _host_final(a, pairs):
 def _result_column(a, res):
     if a.fn == "count":
         return C.NumericColumn(torch.tensor(res, dtype=torch.int64))
-    if a.fn in ("collect_list", "collect_set") or (a.fn == "percentile" and isinstance(a.param, (list, tuple))):
+    if a.fn in ("collect_list", "collect_set") or (a.fn in ("percentile", "percentile_exact")
+                                                    and isinstance(a.param, (list, tuple))):
         arr = np.empty(len(res), dtype=object)
         for i, r in enumerate(res):        # element-wise: equal-length lists must not broadcast
             arr[i] = r

@@ -191,8 +191,9 @@ def run_select(session, s: Select) -> DataFrame:
         df = _where(session, df, s)
     s = _resolve_ordinals(s)
     has_agg = any(isinstance(it.expr, (AggCall, _AggExpr)) for it in s.items) or s.group_by
+    agg_out = None
     if has_agg:
-        df = _aggregate(df, s)
+        df = agg_out = _aggregate(df, s)
     else:
         sel = []
         for it in s.items:
@@ -223,6 +224,8 @@ def run_select(session, s: Select) -> DataFrame:
             else:
                 keys.append((e, a))
         df = df.orderBy(*[k for k, _ in keys], ascending=[a for _, a in keys])
+    if has_agg and getattr(agg_out, "_sql_extra", None):
+        df = df.drop(*agg_out._sql_extra)
     if s.offset is not None:
         df = df.offset(s.offset)
     if s.limit is not None:
@@ -434,6 +437,10 @@ def _aggregate(df: DataFrame, s: Select) -> DataFrame:
                 sel.append(E.col(alias))
             else:
                 sel.append(e.alias(alias))
-    extra = [k for k in aggs if k not in {a for _, a in post}]
-    out = g.select(*sel, *[E.col(k) for k in extra if s.order_by])
+    # aggregates only ORDER BY needs ride along for the sort and are dropped after it
+    order_texts = [a.text for e, _ in s.order_by if isinstance(e, (AggCall, _AggExpr))
+                   for a in _as_agg_expr(e).aggs]
+    extra = [k for k in dict.fromkeys(order_texts) if k not in {a for _, a in post}]
+    out = g.select(*sel, *[E.col(k) for k in extra])
+    out._sql_extra = extra
     return out

@@ -953,6 +953,137 @@ def percentile_approx(c, percentage, accuracy: int = 10000):
 approx_percentile = percentile_approx
 
 
+def percentile(c, percentage, frequency=1):
+    """Exact percentile(s) with linear interpolation between the closest ranks (Spark
+    ``percentile``; ``frequency`` other than 1 is not supported)."""
+    if not (isinstance(frequency, int) and frequency == 1):
+        raise ValueError("percentile: only frequency=1 is supported")
+    out = Agg("percentile_exact", _e(c), f"percentile({_e(c).name}, {percentage})")
+    out.param = percentage
+    return out
+
+
+def ceiling(c):
+    return ceil(c)
+
+
+def btrim(c, trim=None):
+    """Strip ``trim`` characters (default spaces) from both ends."""
+    return _host_map("btrim", (lambda s: str(s).strip(" ")) if trim is None else (lambda s: str(s).strip(trim)), c)
+
+
+def typeof(c):
+    e = _e(c)
+
+    def f(df):
+        col = e.eval(df)
+        return C.StringColumn(np.array([col.dtype.simpleString()] * len(col), dtype=object))
+    return Expr(f, f"typeof({e.name})", e.refs)
+
+
+def assert_true(c, errMsg=None):
+    """NULL when every value is true, else raise (Spark ``assert_true``)."""
+    e = _e(c)
+
+    def f(df):
+        col = e.eval(df)
+        ok = col.data.bool() if isinstance(col, C.NumericColumn) else torch.tensor(
+            [bool(v) for v in col.to_pylist()])
+        if isinstance(col, C.NumericColumn) and col.valid is not None:
+            ok = ok & col.valid
+        if not bool(ok.all()):
+            raise RuntimeError(errMsg if errMsg is not None else f"'{e.name}' is not true!")
+        return C.NumericColumn(torch.zeros(len(col), dtype=torch.float64, device=df.device),
+                               torch.zeros(len(col), dtype=torch.bool, device=df.device))
+    return Expr(f, f"assert_true({e.name})", e.refs)
+
+
+def inline_outer(c):
+    """inline that keeps rows whose array is empty or null (one all-null row)."""
+    out = explode_outer(c)
+    out._inline = True
+    return out
+
+
+def stack(n, *cols):
+    """Generator: splits the k values into ``n`` rows of k/n columns (``col0``, ``col1``, ...)."""
+    n = int(n.eval_literal() if hasattr(n, "eval_literal") else n)
+    es = [_e(x) for x in cols]
+    width = -(-len(es) // n)
+    from ..frame.dataframe import Row
+    names = [f"col{i}" for i in range(width)]
+
+    def f(df):
+        m = len(df)
+        vals = [_host(e.eval(df), m) for e in es]
+        out = np.empty(m, dtype=object)
+        for r in range(m):
+            out[r] = [Row._make(names, [vals[j * width + i][r] if j * width + i < len(es) else None
+                                        for i in range(width)]) for j in range(n)]
+        return C.ArrayColumn(out)
+    g = Expr(f, f"stack({n}, {', '.join(e.name for e in es)})", _refs(*es))
+    g._generator = "explode"
+    g._inline = True
+    return g
+
+
+def sentences(string, language=None, country=None):
+    """Split text into sentences of words (array<array<string>>); punctuation dropped."""
+    def sp(s):
+        parts = [p for p in re.split(r"(?<=[.!?])\s+", str(s).strip()) if p]
+        return [[w for w in re.findall(r"[\w']+", p)] for p in parts]
+    return _host_map("sentences", sp, string, kind="array")
+
+
+def to_number(c, format):  # noqa: A002
+    """Parse strings formatted like ``format`` (digits, ',', '.', '$', sign) to doubles; an
+    unparsable value raises (use ``try_to_number`` for NULL)."""
+    return _to_number(c, format, strict=True)
+
+
+def try_to_number(c, format):  # noqa: A002
+    return _to_number(c, format, strict=False)
+
+
+def _to_number(c, fmt, strict):
+    fmt = fmt.eval_literal() if hasattr(fmt, "eval_literal") else fmt
+
+    def conv(s):
+        t = str(s).strip().replace(",", "").replace("$", "")
+        neg = t.endswith("-") or (t.startswith("<") and t.endswith(">"))
+        t = t.strip("<>-") if neg else t
+        try:
+            v = float(t)
+        except ValueError:
+            if strict:
+                raise ValueError(f"the input '{s}' does not match the format '{fmt}'")
+            return None
+        return -v if neg else v
+    return _host_map("to_number", conv, c, kind="float")
+
+
+def to_char(c, format):  # noqa: A002
+    """Format numbers with a Spark number format ('999,999.00', '$99.9', '0000'): digit
+    count after the decimal point and grouping commas are honoured."""
+    fmt = format.eval_literal() if hasattr(format, "eval_literal") else format
+    dec = len(fmt.split(".")[1]) if "." in fmt else 0
+    comma = "," in fmt
+    dollar = fmt.startswith("$")
+    width = len([ch for ch in fmt.split(".")[0] if ch in "09"])
+    zero_pad = fmt.lstrip("$").startswith("0")
+
+    def fm(x):
+        s = f"{float(x):{',' if comma else ''}.{dec}f}"
+        if zero_pad and not comma:
+            ip, _, fp = s.partition(".")
+            s = ip.zfill(width) + ("." + fp if fp else "")
+        return ("$" if dollar else "") + s
+    return _host_map("to_char", fm, c)
+
+
+to_varchar = to_char
+
+
 def pandas_udf(f=None, returnType=None, functionType=None):
     """Vectorised UDF: ``f(pandas.Series, ...) -> pandas.Series`` applied to the rank's whole
     slice at once (scalar pandas UDF)."""

@@ -265,3 +265,28 @@ def test_tumbling_and_sliding_windows(s):
     assert [a[1] for a in agg] == [1.0, 3.0, 5.0, 3.0]
     with pytest.raises(ValueError):
         F.window("ts", "5 minutes", "10 minutes")
+
+
+def test_percentile_stack_and_misc_functions(s):
+    pdf = pd.DataFrame({"g": ["a", "b", "a", "b", "a"], "v": [1.0, 2.0, 3.0, 4.0, 5.0], "k": [1, 2, 3, 4, 2],
+                        "t": ["Hi there. How are you?", "x", "y", "z", "w"]})
+    d = s.createDataFrame(pdf)
+    out = d.groupBy("g").agg(F.percentile("v", 0.5).alias("p"), F.percentile("v", [0.25, 0.75]).alias("pp"),
+                             F.median("v").alias("m")).orderBy("g").collect()
+    for r in out:
+        vs = pdf.v[pdf.g == r.g].to_numpy()
+        assert r.p == pytest.approx(np.percentile(vs, 50)) == pytest.approx(r.m)
+        assert r.pp == pytest.approx(list(np.percentile(vs, [25, 75])))
+    st = d.select("g", F.stack(2, "k", "v")).collect()
+    assert [(r.g, r.col0) for r in st] == [(g, float(x)) for g, k, v in zip(pdf.g, pdf.k, pdf.v) for x in (k, v)]
+    r = d.select(F.typeof("v").alias("tv"), F.ceiling("v").alias("c"), F.btrim(F.lit("xxaxx"), "x").alias("b"),
+                 F.sentences("t").alias("se"), F.to_char("v", "$999,999.00").alias("tc"),
+                 F.to_number(F.lit("1,234.5"), "9,999.9").alias("tn"),
+                 F.try_to_number(F.lit("abc"), "999").alias("bad")).collect()[0]
+    assert (r.tv, r.c, r.b, r.tc, r.tn, r.bad) == ("double", 1.0, "a", "$1.00", 1234.5, None)
+    assert r.se == [["Hi", "there"], ["How", "are", "you"]]
+    with pytest.raises(RuntimeError, match="not true"):
+        d.select(F.assert_true(F.col("v") > 2)).collect()
+    assert d.select(F.assert_true(F.col("v") > 0).alias("ok")).collect()[0].ok is None
+    with pytest.raises(ValueError):
+        d.select(F.to_number(F.lit("abc"), "999")).collect()
