@@ -119,9 +119,13 @@ _KEYWORDS = ["select", "from", "where", "group by", "order by", "having", "limit
              "right join", "inner join", "outer join", "full outer join", "on", "and", "or", "not", "as", "in",
              "is", "null", "distinct", "count", "sum", "avg", "min", "max", "union", "all", "case", "when",
              "then", "else", "end", "asc", "desc", "like", "between", "show", "databases", "tables", "create",
-             "table", "insert", "into", "values", "cast", "by"]
-_CLAUSES = ["select", "from", "where", "group by", "order by", "having", "limit", "union",
-            "left join", "right join", "inner join", "full outer join", "join"]
+             "table", "insert", "into", "values", "cast", "by", "with", "intersect", "except", "minus", "exists",
+             "using", "natural", "cross join", "left semi join", "left anti join", "lateral view", "pivot", "filter",
+             "over", "partition by", "rows", "range", "preceding", "following", "unbounded", "current row",
+             "tablesample", "explain", "cache", "uncache", "view", "overwrite", "nulls first", "nulls last"]
+_CLAUSES = ["select", "from", "where", "group by", "order by", "having", "limit", "union", "intersect", "except",
+            "minus", "left join", "right join", "inner join", "full outer join", "cross join", "left semi join",
+            "left anti join", "lateral view", "join"]
 
 
 def format_sql(sql: str) -> str:
@@ -137,6 +141,7 @@ def format_sql(sql: str) -> str:
             t = re.sub(rf"\b{kw}\b", kw.upper(), t, flags=re.I)
         for cl in sorted(_CLAUSES, key=len, reverse=True):
             t = re.sub(rf"\s+\b({cl.upper()})\b", r"\n\1", t)
+        t = re.sub(r"\b(LEFT|RIGHT|INNER|OUTER|CROSS|SEMI|ANTI)\n(JOIN)\b", r"\1 \2", t)   # keep "LEFT JOIN" whole
         t = re.sub(r",\s*(?![^()]*\))", ",\n       ", t) if "SELECT" in t else t
         out.append(t)
     return "".join(out).strip()
