@@ -356,14 +356,15 @@ def _split_condition(cond, sides: _Sides):
     return keys, residual
 
 
-def _truth(c: C.Column) -> torch.Tensor:
-    """SQL truth of a predicate column (null -> false), as a CPU bool tensor."""
+def _truth(c: C.Column, device) -> torch.Tensor:
+    """SQL truth of a predicate column (null -> false), as a bool tensor on ``device``."""
     if isinstance(c, C.NumericColumn):
         m = c.data.bool()
         if c.valid is not None:
             m = m & c.valid
-        return m.cpu()
-    return torch.tensor([bool(v) if v is not None else False for v in c.to_pylist()], dtype=torch.bool)
+        return m.to(device)
+    return torch.tensor([bool(v) if v is not None else False for v in c.to_pylist()], dtype=torch.bool,
+                        device=device)
 
 
 def _match_pairs(sides: _Sides, cond) -> tuple[torch.Tensor, torch.Tensor]:
@@ -375,28 +376,29 @@ def _match_pairs(sides: _Sides, cond) -> tuple[torch.Tensor, torch.Tensor]:
         kl = DataFrame(ldata.session, OrderedDict((f"k{i}", ldata._col(a)) for i, (a, _) in enumerate(keys)), nl)
         kr = DataFrame(rdata.session, OrderedDict((f"k{i}", rdata._col(b)) for i, (_, b) in enumerate(keys)), nr)
         codes = _key_codes(kl, kr, [f"k{i}" for i in range(len(keys))])
+    dev = ldata.device                  # pair indices and masks stay on the device until the end
     if codes is not None:
         li, ri = _vector_join(codes[0], codes[1], "inner")
-        li, ri = li.cpu(), ri.cpu()
         if residual is None or li.numel() == 0:
-            return li, ri
-        keep = [_truth(residual.eval(_PairFrame(sides, li[s:s + _PAIR_BLOCK], ri[s:s + _PAIR_BLOCK])))
+            return li.cpu(), ri.cpu()
+        li, ri = li.to(dev), ri.to(dev)
+        keep = [_truth(residual.eval(_PairFrame(sides, li[s:s + _PAIR_BLOCK], ri[s:s + _PAIR_BLOCK])), dev)
                 for s in range(0, li.numel(), _PAIR_BLOCK)]
         m = torch.cat(keep)
-        return li[m], ri[m]
+        return li[m].cpu(), ri[m].cpu()
     # nested loop: blocks of left rows against every right row
     li_parts, ri_parts = [], []
     step = max(1, _PAIR_BLOCK // max(nr, 1))
     for s in range(0, nl if nr else 0, step):
         e = min(nl, s + step)
-        bl = torch.arange(s, e).repeat_interleave(nr)
-        br = torch.arange(nr).repeat(e - s)
-        m = _truth(cond.eval(_PairFrame(sides, bl, br)))
+        bl = torch.arange(s, e, device=dev).repeat_interleave(nr)
+        br = torch.arange(nr, device=dev).repeat(e - s)
+        m = _truth(cond.eval(_PairFrame(sides, bl, br)), dev)
         li_parts.append(bl[m])
         ri_parts.append(br[m])
     if not li_parts:
         return torch.zeros(0, dtype=torch.int64), torch.zeros(0, dtype=torch.int64)
-    return torch.cat(li_parts), torch.cat(ri_parts)
+    return torch.cat(li_parts).cpu(), torch.cat(ri_parts).cpu()
 
 
 def condition_join(left: DataFrame, right: DataFrame, cond, how: str = "inner") -> DataFrame:

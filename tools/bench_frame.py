@@ -44,3 +44,21 @@ from orange3_spark_amd.sql.window import Window
 t2("window_rank_1M", lambda: df.limit(1_000_000).withColumn("r", F.row_number().over(Window.partitionBy("k").orderBy("v"))).count())
 t2("string_ops_1M", lambda: df.limit(1_000_000).withColumn("s", F.concat(F.lit("x"), F.col("k").cast("string"))).filter(F.col("s").startswith("x1")).count())
 print(json.dumps(res2))
+# condition joins / SQL subqueries (this round)
+res3 = {}
+def t3(name, fn):
+    sync(); a = time.perf_counter()
+    try:
+        fn(); sync()
+        res3[name] = round(time.perf_counter() - a, 4)
+    except Exception as e:  # noqa: BLE001
+        res3[name] = f"error: {type(e).__name__}: {str(e)[:80]}"
+dims = s.range(1000).withColumn("uid", F.col("id")).withColumn("lo", F.col("id") / 1000.0).withColumn("hi", F.col("id") / 1000.0 + 0.0005)
+t3("cond_join_equi_20Mx1K", lambda: df.join(dims, df.k == dims.uid).count())
+t3("cond_join_equi_residual_20Mx1K", lambda: df.join(dims, (df.k == dims.uid) & (df.v > dims.lo)).count())
+part = df.limit(1_000_000)
+t3("band_join_nested_loop_1Mx1K", lambda: part.join(dims, (part.v >= dims.lo) & (part.v < dims.hi)).count())
+dims.createOrReplaceTempView("dims")
+t3("sql_exists_20M", lambda: s.sql("SELECT count(*) FROM t WHERE EXISTS (SELECT 1 FROM dims WHERE dims.uid = t.k AND dims.lo < 0.5)").collect())
+t3("sql_in_subquery_20M", lambda: s.sql("SELECT count(*) FROM t WHERE k IN (SELECT uid FROM dims WHERE lo < 0.5)").collect())
+print(json.dumps(res3))
