@@ -18,7 +18,7 @@ _TOKEN = re.compile(r"""
   | (?P<num>\d+\.\d*(?:[eE][-+]?\d+)?|\.\d+(?:[eE][-+]?\d+)?|\d+(?:[eE][-+]?\d+)?)
   | (?P<str>'(?:[^']|'')*')
   | (?P<qid>`[^`]+`|"[^"]+")
-  | (?P<op><=|>=|<>|!=|==|\|\||[-+*/%(),.;=<>\[\]])
+  | (?P<op><=>|<=|>=|<>|!=|==|\|\||[-+*/%(),.;=<>\[\]&|^~])
   | (?P<id>[A-Za-z_][A-Za-z0-9_]*)
 """, re.X)
 
@@ -552,12 +552,38 @@ class Parser:
             return _unary_map(self.not_expr(), lambda a: ~a)
         return self.cmp_expr()
 
-    def cmp_expr(self):
+    def bit_or(self):
+        """a | b  <  a ^ b  <  a & b  <  + -   (Spark's bitwise operator precedence)."""
+        e = self.bit_xor()
+        while self.peek().kind == "op" and self.peek().val == "|":
+            self.i += 1
+            e = _combine(e, self.bit_xor(), lambda a, b: a.bitwiseOR(b))
+        return e
+
+    def bit_xor(self):
+        e = self.bit_and()
+        while self.peek().kind == "op" and self.peek().val == "^":
+            self.i += 1
+            e = _combine(e, self.bit_and(), lambda a, b: a.bitwiseXOR(b))
+        return e
+
+    def bit_and(self):
         e = self.add_expr()
+        while self.peek().kind == "op" and self.peek().val == "&":
+            self.i += 1
+            e = _combine(e, self.add_expr(), lambda a, b: a.bitwiseAND(b))
+        return e
+
+    def cmp_expr(self):
+        e = self.bit_or()
         t = self.peek()
+        if t.kind == "op" and t.val == "<=>":                 # null-safe equality
+            self.i += 1
+            r = self.bit_or()
+            return _combine(e, r, lambda a, b: a.eqNullSafe(b))
         if t.kind == "op" and t.val in ("=", "==", "!=", "<>", "<", "<=", ">", ">="):
             self.i += 1
-            r = self.add_expr()
+            r = self.bit_or()
             op = {"=": "__eq__", "==": "__eq__", "!=": "__ne__", "<>": "__ne__", "<": "__lt__", "<=": "__le__",
                   ">": "__gt__", ">=": "__ge__"}[t.val]
             return _combine(e, r, lambda a, b: getattr(a, op)(b))
@@ -643,6 +669,9 @@ class Parser:
     def unary(self):
         if self.accept("op", "-"):
             return _unary_map(self.unary(), lambda a: -a)
+        if self.accept("op", "~"):
+            from . import functions as F
+            return _unary_map(self.unary(), F.bitwise_not)
         if self.accept("op", "+"):
             return self.unary()
         e = self.primary()

@@ -178,3 +178,9 @@ def test_pivot_sample_show_explain_cache(s):
     assert s.catalog.isCached("tc") and s.sql("SELECT count(*) AS n FROM tc").collect()[0].n == int((t.k > 5).sum())
     s.sql("UNCACHE TABLE tc")
     assert not s.catalog.isCached("tc")
+
+
+def test_bitwise_and_null_safe_operators(s):
+    s.createDataFrame(pd.DataFrame({"a": [5, 6, 12], "b": [3.0, None, 10.0]})).createOrReplaceTempView("bt")
+    got = [tuple(r) for r in s.sql("SELECT a & 3, a | 1, a ^ 1, ~a, a + 1 & 6, b <=> NULL FROM bt").collect()]
+    assert got == [(a & 3, a | 1, a ^ 1, ~a, (a + 1) & 6, b is None) for a, b in ((5, 3.0), (6, None), (12, 10.0))]
