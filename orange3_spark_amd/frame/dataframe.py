@@ -165,6 +165,12 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
             qual, _, part = name.rpartition(".")
             if qual and qual.split(".")[-1] in self.__dict__.get("_aliases", ()):
                 return self._col(part)           # "alias.col" after df.alias("alias")
+            head, _, rest = name.partition(".")
+            if rest and head in self._cols and isinstance(self._cols[head], C.HostColumn):
+                c = self._cols[head]             # "struct.field[.field]" (e.g. window.start)
+                for fld in rest.split("."):
+                    c = E.struct_field(c, fld)
+                return c
             raise KeyError(f"cannot resolve column '{name}' among {self.columns}")
 
     def column_data(self, name: str) -> C.Column:
@@ -204,7 +210,13 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
     def _col_qualified(self, qual: str, name: str) -> C.Column:
         """SQL ``qual.name``: after a condition join the renamed copy of that side's column."""
         out = self.__dict__.get("_qual_map", {}).get((qual.split(".")[-1], name))
-        return self._cols[out] if out in self._cols else self._col(name)
+        if out in self._cols:
+            return self._cols[out]
+        head = qual.split(".")[0]
+        if head in self._cols and isinstance(self._cols[head], C.HostColumn) and \
+                head not in self.__dict__.get("_aliases", ()):
+            return self._col(f"{qual}.{name}")          # SQL struct.field
+        return self._col(name)
 
     def _new(self, cols, n=None) -> "DataFrame":
         return DataFrame(self.session, cols, self._n if n is None else n)
@@ -213,7 +225,10 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
         if isinstance(c, str):
             if c == "*":
                 raise ValueError("'*' handled by caller")
-            return c, self._col(c)
+            col = self._col(c)
+            if "." in c and c not in self._cols and c.split(".")[0] in self._cols:
+                return c.rsplit(".", 1)[1], col  # struct field: Spark names the column by the field
+            return c, col
         if isinstance(c, E.Expr):
             return c.name, c.eval(self)
         raise TypeError(f"unsupported column spec {c!r}")

@@ -278,6 +278,30 @@ class Expr:
 
     __getitem__ = getItem
 
+    def getField(self, name: str):
+        """Field of a struct column (``Row`` / dict values), e.g. ``window.start``."""
+        def f(df):
+            return struct_field(self.eval(df), name)
+        return Expr(f, f"{self._name}.{name}", self.refs)
+
+
+def struct_field(c: C.Column, name: str) -> C.Column:
+    """Values of field ``name`` of a host column of structs (Rows or dicts); null structs -> null."""
+    from .dataframe import _nullable_column
+    if not isinstance(c, C.HostColumn):
+        raise TypeError(f"field access '{name}' needs a struct column, got {c.dtype.simpleString()}")
+    out = []
+    for v in c.values:
+        if v is None:
+            out.append(None)
+        elif isinstance(v, dict):
+            out.append(v.get(name))
+        elif hasattr(v, "__fields__") and name in v.__fields__:
+            out.append(v[v.__fields__.index(name)])
+        else:
+            raise KeyError(f"no struct field '{name}'")
+    return _nullable_column(out)
+
 
 def _div(a, b):
     return torch.div(a.to(torch.float64), b.to(torch.float64))

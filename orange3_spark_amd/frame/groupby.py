@@ -53,7 +53,9 @@ def _encode_key(c: C.Column, dev):
     try:
         import pandas as pd
         codes, uniques = pd.factorize(pd.Series(values, dtype=object), use_na_sentinel=False)
-        uvals = list(uniques)
+        # decode to each key's first original object (pandas turns Row structs into plain tuples)
+        _, first = np.unique(codes, return_index=True)
+        uvals = [values[i] for i in first] if len(first) == len(uniques) else list(uniques)
         return (torch.from_numpy(codes.astype(np.int64)).to(dev),
                 (lambda cs: [None if (isinstance(uvals[k], float) and math.isnan(uvals[k])) else uvals[k]
                              for k in cs]), "host")
@@ -264,7 +266,10 @@ def aggregate(df, keys: list, aggs: list):
                 valid = torch.tensor([v is not None for v in vals])
             out[k.name] = C.NumericColumn(torch.from_numpy(arr), valid, dt)
         else:
-            out[k.name] = C.from_numpy(np.array(vals, dtype=object), "cpu")
+            arr = np.empty(len(vals), dtype=object)       # element-wise: equal-length structs must not
+            for j, v in enumerate(vals):                    # become a 2-D array
+                arr[j] = v
+            out[k.name] = C.ArrayColumn(arr) if isinstance(src, C.ArrayColumn) else C.from_numpy(arr, "cpu")
     for j, a in enumerate(aggs):
         tag = f"a{j}"
         res = []

@@ -290,3 +290,20 @@ def test_percentile_stack_and_misc_functions(s):
     assert d.select(F.assert_true(F.col("v") > 0).alias("ok")).collect()[0].ok is None
     with pytest.raises(ValueError):
         d.select(F.to_number(F.lit("abc"), "999")).collect()
+
+
+def test_struct_fields_and_window_group_keys(s):
+    """groupBy(window(...)) keeps Row keys; window.start / getField / SQL w.start read fields."""
+    ts = ["2024-01-01 00:01:00", "2024-01-01 00:07:30", "2024-01-01 00:12:00"]
+    d = s.createDataFrame(pd.DataFrame({"ts": ts, "v": [1.0, 2.0, 3.0]}))
+    g = d.groupBy(F.window("ts", "10 minutes")).agg(F.sum("v").alias("s")).orderBy("window.start")
+    rows = g.collect()
+    assert [(r.window.start, r.window.end, r.s) for r in rows] == [
+        ("2024-01-01 00:00:00", "2024-01-01 00:10:00", 3.0), ("2024-01-01 00:10:00", "2024-01-01 00:20:00", 3.0)]
+    assert g.select("window.start", "s").columns == ["start", "s"]
+    assert [r[0] for r in g.select(F.col("window").getField("end")).collect()] == [
+        "2024-01-01 00:10:00", "2024-01-01 00:20:00"]
+    d.createOrReplaceTempView("tw_struct")
+    got = sorted(tuple(r) for r in s.sql("SELECT w.start AS st, sum(v) AS sv FROM (SELECT window(ts, '10 minutes') "
+                                         "AS w, v FROM tw_struct) GROUP BY w.start").collect())
+    assert got == [("2024-01-01 00:00:00", 3.0), ("2024-01-01 00:10:00", 3.0)]
