@@ -30,6 +30,41 @@ def execute(session, query: str) -> DataFrame:
         names = cat.tableNames(db)
         return _strings_df(session, {"namespace": [db] * len(names), "tableName": names,
                                      "isTemporary": ["true" if n in cat._temp else "false" for n in names]})
+    if kind == "set":
+        _, key, val = stmt
+        if key is None:
+            pairs = sorted(session.conf.getAll())
+            return _strings_df(session, {"key": [k for k, _ in pairs], "value": [str(v) for _, v in pairs]})
+        if val is not None:
+            session.conf.set(key, val)
+        return _strings_df(session, {"key": [key], "value": [str(session.conf.get(key, "<undefined>"))]})
+    if kind == "reset":
+        if stmt[1] is not None:
+            session.conf.remove(stmt[1])
+        return session.emptyDataFrame()
+    if kind == "truncate":
+        name = stmt[1]
+        if name in cat._temp:
+            raise ValueError(f"TRUNCATE TABLE cannot be used on the temporary view {name}")
+        cat.saveAsTable(cat.table(name).limit(0), name, "overwrite")
+        return session.emptyDataFrame()
+    if kind == "rename":
+        _, old, new = stmt
+        if old in cat._temp:
+            cat.registerTempView(new, cat._temp[old])
+            cat.dropTempView(old)
+        else:
+            df = cat.table(old)
+            cat.saveAsTable(df, new, "error")
+            cat.dropTable(old)
+        return session.emptyDataFrame()
+    if kind == "drop_view":
+        _, name, if_exists = stmt
+        dropped = cat.dropTempView(name) or (name.startswith("global_temp.")
+                                             and cat.dropGlobalTempView(name.split(".", 1)[1]))
+        if not dropped and not if_exists:
+            raise KeyError(f"Table or view not found: {name}")
+        return session.emptyDataFrame()
     if kind == "show_columns":
         return _strings_df(session, {"col_name": cat.table(stmt[1]).columns})
     if kind == "show_functions":

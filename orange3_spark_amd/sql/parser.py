@@ -208,6 +208,36 @@ class Parser:
             return ("show_tables", db)
         if self.kw("use"):
             return ("use", self.ident())
+        if self.idw("set"):                          # SET / SET key / SET key = value
+            if self.peek().kind == "eof":
+                return ("set", None, None)
+            start = self.i
+            while self.peek().kind != "eof" and not (self.peek().kind == "op" and self.peek().val == "="):
+                self.i += 1
+            key = "".join(t.val for t in self.toks[start:self.i])
+            if self.accept("op", "="):
+                raw = self.src.split("=", 1)[1].strip().rstrip(";").strip()
+                self.i = len(self.toks) - 1
+                return ("set", key, raw.strip("'\""))
+            return ("set", key, None)
+        if self.idw("reset"):
+            key = "".join(t.val for t in self.toks[self.i:-1]) or None
+            self.i = len(self.toks) - 1
+            return ("reset", key)
+        if self.idw("truncate"):
+            self.kw("table")
+            return ("truncate", self.qualified())
+        if self.idw("alter"):
+            self.kw("table") or self.idw("view")
+            name = self.qualified()
+            if not (self.idw("rename") and self.idw("to")):
+                raise SyntaxError("only ALTER TABLE ... RENAME TO ... is supported")
+            return ("rename", name, self.qualified())
+        if self.peek().kind == "kw" and self.peek().val == "drop" and self.peek(1).kind == "id" and \
+                self.peek(1).val.lower() == "view":
+            self.i += 2
+            ie = self.kw("if", "exists")
+            return ("drop_view", self.qualified(), ie)
         if self.kw("show") and self.idw("columns"):
             if not (self.kw("in") or self.kw("from")):
                 raise SyntaxError("expected FROM / IN after SHOW COLUMNS")

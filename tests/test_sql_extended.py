@@ -184,3 +184,26 @@ def test_bitwise_and_null_safe_operators(s):
     s.createDataFrame(pd.DataFrame({"a": [5, 6, 12], "b": [3.0, None, 10.0]})).createOrReplaceTempView("bt")
     got = [tuple(r) for r in s.sql("SELECT a & 3, a | 1, a ^ 1, ~a, a + 1 & 6, b <=> NULL FROM bt").collect()]
     assert got == [(a & 3, a | 1, a ^ 1, ~a, (a + 1) & 6, b is None) for a, b in ((5, 3.0), (6, None), (12, 10.0))]
+
+
+def test_set_truncate_rename_drop_view(s):
+    s.sql("SET spark.sql.shuffle.partitions=16")
+    assert s.conf.get("spark.sql.shuffle.partitions") == "16"
+    assert s.sql("SET spark.sql.shuffle.partitions").collect()[0].value == "16"
+    assert any(r.key == "spark.sql.shuffle.partitions" for r in s.sql("SET").collect())
+    s.sql("RESET spark.sql.shuffle.partitions")
+    assert s.conf.get("spark.sql.shuffle.partitions") is None
+    s.sql("CREATE TABLE tr1 AS SELECT k, v FROM t WHERE k < 4")
+    s.sql("ALTER TABLE tr1 RENAME TO tr2")
+    assert s.catalog.tableExists("tr2") and not s.catalog.tableExists("tr1")
+    s.sql("TRUNCATE TABLE tr2")
+    assert s.sql("SELECT count(*) AS n FROM tr2").collect()[0].n == 0
+    assert s.table("tr2").columns == ["k", "v"]
+    s.sql("DROP TABLE tr2")
+    s.sql("CREATE TEMP VIEW tv1 AS SELECT 1 AS one")
+    s.sql("ALTER VIEW tv1 RENAME TO tv2")
+    assert s.sql("SELECT one FROM tv2").collect()[0].one == 1
+    s.sql("DROP VIEW tv2")
+    s.sql("DROP VIEW IF EXISTS tv2")
+    with pytest.raises(KeyError):
+        s.sql("DROP VIEW tv2")
