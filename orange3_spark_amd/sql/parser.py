@@ -13,6 +13,43 @@ from dataclasses import dataclass, field
 
 from ..frame import expr as E
 
+GRAMMAR = """\
+statement :=
+    [WITH name AS (select) [, ...]] select
+  | CREATE TABLE name AS select
+  | CREATE [OR REPLACE] [GLOBAL] [TEMP|TEMPORARY] VIEW [IF NOT EXISTS] name AS select
+  | INSERT {INTO | OVERWRITE} [TABLE] name [(col, ...)] {VALUES (v, ...), ... | select}
+  | CACHE [LAZY] TABLE name [AS select] | UNCACHE TABLE [IF EXISTS] name | REFRESH TABLE name
+  | TRUNCATE TABLE name | ALTER {TABLE|VIEW} name RENAME TO name
+  | DROP TABLE [IF EXISTS] name | DROP VIEW [IF EXISTS] name | DROP DATABASE [IF EXISTS] name
+  | CREATE DATABASE [IF NOT EXISTS] name | USE name
+  | SHOW DATABASES | SHOW TABLES [IN db] | SHOW COLUMNS {FROM|IN} name | SHOW FUNCTIONS
+  | DESCRIBE [TABLE] name | EXPLAIN [EXTENDED] statement
+  | SET [key [= value]] | RESET [key]
+
+select :=
+    SELECT [DISTINCT] item [, ...]
+    [FROM source [TABLESAMPLE (x PERCENT | n ROWS)] [[AS] alias]
+        {[NATURAL] [INNER|LEFT [OUTER]|RIGHT [OUTER]|FULL [OUTER]|CROSS|LEFT SEMI|LEFT ANTI] JOIN source [alias]
+            [ON condition | USING (col, ...)] | , source [alias]} ...
+        [PIVOT (agg [AS a], ... FOR col IN (v [AS a], ...))]
+        [LATERAL VIEW [OUTER] generator(...) t AS col [, ...]] ...]
+    [WHERE condition]            -- incl. [NOT] EXISTS (correlated: semi / anti join), IN (select)
+    [GROUP BY expr|ordinal|alias, ... [WITH ROLLUP|CUBE] | ROLLUP(...) | CUBE(...) | GROUPING SETS (...)]
+    [HAVING condition] [ORDER BY expr|ordinal [ASC|DESC] [NULLS FIRST|LAST], ...]
+    [LIMIT n] [OFFSET n]
+    [{UNION|INTERSECT|EXCEPT|MINUS} [ALL|DISTINCT] select]
+
+source := table | (select) | VALUES (v, ...), ... [AS t(col, ...)]
+
+expr := literals, columns, t.col, struct.field, arr[i], map[key], + - * / % DIV, & | ^ ~,
+        = == != <> < <= > >= <=>, AND OR NOT, IS [NOT] NULL, [NOT] IN (...), [NOT] BETWEEN,
+        [NOT] LIKE | RLIKE | REGEXP | ILIKE, CASE [x] WHEN ... END, CAST(x AS type),
+        (scalar select), function(...) [FILTER (WHERE c)] [OVER (PARTITION BY ... ORDER BY ...
+        [ROWS|RANGE BETWEEN ... AND ...])], every sql.functions name plus IF / IFF / NVL / NVL2 /
+        IFNULL / NULLIF / typeof / named_struct
+"""
+
 _TOKEN = re.compile(r"""
     (?P<ws>\s+|--[^\n]*)
   | (?P<num>\d+\.\d*(?:[eE][-+]?\d+)?|\.\d+(?:[eE][-+]?\d+)?|\d+(?:[eE][-+]?\d+)?)

@@ -128,7 +128,7 @@ def class_methods_page(title: str, classes) -> str:
                 continue
             doc = (inspect.getdoc(fn) or "").split("\n")[0]
             sig = "" if isinstance(fn, property) else str(inspect.signature(fn)).replace("(self, ", "(").replace("(self)", "()")
-            sig = re.sub(r"<function (\w+) at 0x[0-9a-f]+>", r"\1", sig)       # stable across runs
+            sig = re.sub(r"<function ([\w.<>]+) at 0x[0-9a-f]+>", r"\1", sig)   # stable across runs
             lines.append(f"- `{name}{sig}`" + (f" — {doc}" if doc else ""))
         lines.append("")
     return "\n".join(lines)
@@ -170,8 +170,13 @@ def main():
         f.write("\n".join([f"# `orange3_spark_amd.sql.functions` ({len(fns)} functions)", "",
                            "Column functions with `pyspark.sql.functions` names and semantics.", ""]
                           + [f"- `{n}{inspect.signature(getattr(SF, n))}`" for n in fns]) + "\n")
+    from orange3_spark_amd.sql.parser import GRAMMAR
+    with open(os.path.join(DOC, "api", "sql.md"), "w") as f:
+        f.write("# SQL statements (`session.sql`, the Data Frame widget)\n\nParsed by the in-house "
+                "recursive-descent parser (`orange3_spark_amd/sql/parser.py`), executed by `sql/engine.py` "
+                "as the same device operators as the DataFrame API.\n\n```\n" + GRAMMAR + "```\n")
     index += ["- [RDD / SparkContext](api/rdd.md)", "- [`ml.functions`](api/ml_functions.md)",
-              "- [`sql.functions`](api/sql_functions.md)"]
+              "- [`sql.functions`](api/sql_functions.md)", "- [SQL statements](api/sql.md)"]
     with open(os.path.join(DOC, "index.md"), "w") as f:
         f.write("\n".join(index) + "\n")
     print("wrote", DOC)
