@@ -495,6 +495,7 @@ class Parser:
             s.offset = int(float(self.expect("num").val))
         if self.kw("union"):
             s.union_all = bool(self.kw("all"))
+            self.kw("distinct")
             s.union = self.select()
         elif self.idw("intersect") or self.idw("except") or self.idw("minus"):
             op = self.toks[self.i - 1].val.lower()
