@@ -278,6 +278,48 @@ class Expr:
 
     __getitem__ = getItem
 
+    def withField(self, fieldName: str, col: "Expr"):
+        """Struct with field ``fieldName`` added or replaced (Spark ``Column.withField``)."""
+        val = col if isinstance(col, Expr) else lit(col)
+
+        def f(df):
+            from .dataframe import Row
+            c, v = self.eval(df), _host_values(val.eval(df), len(df))
+            out = np.empty(len(c), dtype=object)
+            for i, (s_, x) in enumerate(zip(c.values, v)):
+                if s_ is None:
+                    out[i] = None
+                    continue
+                names = list(s_.__fields__) if hasattr(s_, "__fields__") else list(s_.keys())
+                vals = list(s_) if hasattr(s_, "__fields__") else [s_[k] for k in names]
+                if fieldName in names:
+                    vals[names.index(fieldName)] = x
+                else:
+                    names.append(fieldName)
+                    vals.append(x)
+                out[i] = Row._make(names, vals)
+            return C.ArrayColumn(out)
+        return Expr(f, f"update_fields({self._name}, WithField({fieldName}))", self.refs + val.refs)
+
+    def dropFields(self, *fieldNames: str):
+        """Struct without the named fields (Spark ``Column.dropFields``)."""
+        def f(df):
+            from .dataframe import Row
+            c = self.eval(df)
+            out = np.empty(len(c), dtype=object)
+            for i, s_ in enumerate(c.values):
+                if s_ is None:
+                    out[i] = None
+                    continue
+                names = list(s_.__fields__) if hasattr(s_, "__fields__") else list(s_.keys())
+                vals = list(s_) if hasattr(s_, "__fields__") else [s_[k] for k in names]
+                keep = [(n, v) for n, v in zip(names, vals) if n not in fieldNames]
+                if not keep:
+                    raise ValueError("cannot drop all fields of a struct")
+                out[i] = Row._make([n for n, _ in keep], [v for _, v in keep])
+            return C.ArrayColumn(out)
+        return Expr(f, f"update_fields({self._name}, dropField())", self.refs)
+
     def getField(self, name: str):
         """Field of a struct column (``Row`` / dict values), e.g. ``window.start``."""
         def f(df):

@@ -307,3 +307,12 @@ def test_struct_fields_and_window_group_keys(s):
     got = sorted(tuple(r) for r in s.sql("SELECT w.start AS st, sum(v) AS sv FROM (SELECT window(ts, '10 minutes') "
                                          "AS w, v FROM tw_struct) GROUP BY w.start").collect())
     assert got == [("2024-01-01 00:00:00", 3.0), ("2024-01-01 00:10:00", 3.0)]
+
+
+def test_struct_with_and_drop_fields(s):
+    d = s.createDataFrame(pd.DataFrame({"a": [1, 2], "b": ["x", "y"]}))
+    st = d.select(F.struct("a", "b").alias("s"))
+    r = st.select(F.col("s").withField("c", F.col("s").getField("a") * 10).alias("s2")).collect()
+    assert [(x.s2.a, x.s2.b, x.s2.c) for x in r] == [(1, "x", 10), (2, "y", 20)]
+    r = st.select(F.col("s").withField("a", F.lit(0)).dropFields("b").alias("s3")).collect()
+    assert [tuple(x.s3.__fields__) for x in r] == [("a",), ("a",)] and [x.s3.a for x in r] == [0, 0]
