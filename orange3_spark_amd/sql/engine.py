@@ -179,8 +179,9 @@ def _insert(session, name, cols, src, overwrite) -> DataFrame:
     for c in missing:                                    # unlisted columns get NULL
         new = new.withColumn(c, E.lit(None))
     types = dict(target.dtypes)
-    new = new.select(*[E.col(c).cast(types[c]).alias(c) if types[c] not in ("string",) else E.col(c)
-                       for c in target.columns])
+    scalar = {"tinyint", "smallint", "int", "bigint", "float", "double", "boolean"}
+    new = new.select(*[E.col(c).cast(types[c]).alias(c) if types[c] in scalar else E.col(c)
+                       for c in target.columns])                  # numeric targets keep their type
     cat.saveAsTable(new, name, "overwrite" if overwrite else "append")
     return session.emptyDataFrame()
 
