@@ -187,7 +187,8 @@ def _insert(session, name, cols, src, overwrite) -> DataFrame:
 
 
 def _values_frame(session, rows, names=None) -> DataFrame:
-    """Inline table (VALUES ...): built on rank 0, rows spread like createDataFrame."""
+    """Inline table (VALUES ...): every rank parses the same literal rows and createDataFrame
+    keeps this rank's slice, like any local collection."""
     width = len(rows[0]) if rows else 0
     names = list(names) if names else [f"col{i + 1}" for i in range(width)]
     return session.createDataFrame([tuple(r) for r in rows], names)
