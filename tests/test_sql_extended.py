@@ -207,3 +207,10 @@ def test_set_truncate_rename_drop_view(s):
     s.sql("DROP VIEW IF EXISTS tv2")
     with pytest.raises(KeyError):
         s.sql("DROP VIEW tv2")
+
+
+def test_union_distinct(s):
+    t = _t()
+    got = _rows(s.sql("SELECT k FROM t UNION DISTINCT SELECT k FROM t"))
+    assert got == sorted((k,) for k in set(t.k))
+    assert s.sql("SELECT k FROM t UNION ALL SELECT k FROM t").count() == 2 * len(t)
