@@ -178,7 +178,7 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
 
     def __getitem__(self, item):
         if isinstance(item, str):
-            return E.bound_col(item, self._col(item))
+            return E.bound_col(item, self._col(item), self)
         if isinstance(item, int):
             return E.col(self.columns[item])
         if isinstance(item, (list, tuple)):
@@ -192,10 +192,10 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
             raise AttributeError(name)
         cols = self.__dict__.get("_cols", {})
         if name in cols:
-            return E.bound_col(name, cols[name])
+            return E.bound_col(name, cols[name], self)
         raise AttributeError(name)
 
-    def _col_bound(self, name: str, src) -> C.Column:
+    def _col_bound(self, name: str, src, frame=None) -> C.Column:
         """Resolve ``other[name]`` on this frame: the column object itself when this frame holds
         it, the renamed copy a condition join made of it (``_prov``), else by name."""
         if src is not None:

@@ -469,20 +469,23 @@ def qualified_col(qual: str, name: str) -> Expr:
     return e
 
 
-def bound_col(name: str, src) -> Expr:
+def bound_col(name: str, src, frame=None) -> Expr:
     """``df[name]`` / ``df.name``: a column reference that also remembers WHICH column object
-    it came from (Spark's attribute id), so a join condition such as
-    ``a.id == b.id`` can tell the two sides apart.  Frames without side information
-    resolve it by name like :func:`col`."""
+    it came from (Spark's attribute id) and which frame it was taken from (Spark's dataset
+    id), so a join condition such as ``a.id == b.id`` can tell the two sides apart even
+    when ``b`` is derived from ``a`` and shares its column objects (self joins).  Frames
+    without side information resolve it by name like :func:`col`."""
     import weakref
     ref = weakref.ref(src)
+    fref = weakref.ref(frame) if frame is not None else (lambda: None)
 
     def f(df):
         g = getattr(type(df), "_col_bound", None)
-        return g(df, name, ref()) if g is not None else df._col(name)
+        return g(df, name, ref(), fref()) if g is not None else df._col(name)
     e = Expr(f, name, (name,))
     e._colname = name
     e._src = ref
+    e._frame = fref
     return e
 
 

@@ -5,7 +5,13 @@ their rank.
 Condition joins (``a.join(b, (a.id == b.uid) & (a.t < b.t), how)``) take the equality
 conjuncts between the two sides as hash keys (vectorised sort + searchsorted) and evaluate
 the rest of the condition on the candidate pairs; with no equality conjunct the candidates
-are the cross product, walked in bounded blocks of left rows (Spark's nested-loop join)."""
+are the cross product, walked in bounded blocks of left rows (Spark's nested-loop join).
+
+Intentional difference from Spark: a right-side column whose name clashes with a left-side
+column is kept under ``<name>_r`` (Spark keeps both under the same name and requires
+qualified access).  Positional results are identical; ``other[c]`` / ``b.c`` references and
+qualified names (``col("b.t")``) still resolve to the renamed column through the join's
+provenance map, so only code that looks the duplicate up by its bare name sees the suffix."""
 from __future__ import annotations
 
 from collections import OrderedDict
@@ -269,7 +275,24 @@ class _Sides:
             return name
         return next(k for k, v in f._cols.items() if v is obj)
 
-    def resolve(self, name: str, src=None, qual: str | None = None) -> tuple[int, str]:
+    def _key_of(self, s: int, src) -> str | None:
+        f = self.orig[s]
+        for k, v in f._cols.items():
+            if v is src:
+                return k
+        return None
+
+    def resolve(self, name: str, src=None, qual: str | None = None, frame=None) -> tuple[int, str]:
+        if frame is not None:
+            # the frame the reference was taken from (Spark's dataset id) decides the side,
+            # also when both sides share the column object (df.join(df.withColumn(..)))
+            for s in (0, 1):
+                if self.orig[s] is frame:
+                    k = self._key_of(s, src) if src is not None else None
+                    if k is not None:
+                        return s, k
+                    if self._has(s, name):
+                        return s, self._key(s, name)
         if src is not None:
             for s in (0, 1):
                 f = self.orig[s]
@@ -304,7 +327,25 @@ class _Sides:
         if name is None:
             return None
         ref = getattr(e, "_src", None)
-        return self.resolve(name, None if ref is None else ref(), getattr(e, "_qual", None))
+        fref = getattr(e, "_frame", None)
+        return self.resolve(name, None if ref is None else ref(), getattr(e, "_qual", None),
+                            None if fref is None else fref())
+
+    def split_shared(self, e1, e2) -> tuple[str, str] | None:
+        """``x.id == y.id`` whose operands both resolved to one side because the two frames
+        share the column object: as Spark does for a trivially-true self-join equality,
+        take the left operand from the left side and the right operand from the right
+        side (None when the objects are not present on both sides)."""
+        r1, r2 = getattr(e1, "_src", None), getattr(e2, "_src", None)
+        if r1 is None or r2 is None:
+            return None
+        k1, k2 = self._key_of(0, r1()), self._key_of(1, r2())
+        if k1 is not None and k2 is not None:
+            return k1, k2
+        k1, k2 = self._key_of(0, r2()), self._key_of(1, r1())
+        if k1 is not None and k2 is not None:
+            return k1, k2
+        return None
 
 
 class _PairFrame(DataFrame):
@@ -324,8 +365,8 @@ class _PairFrame(DataFrame):
     def _col(self, name):
         return self._take_side(*self._sides.resolve(name))
 
-    def _col_bound(self, name, src):
-        return self._take_side(*self._sides.resolve(name, src))
+    def _col_bound(self, name, src, frame=None):
+        return self._take_side(*self._sides.resolve(name, src, None, frame))
 
     def _col_qualified(self, qual, name):
         return self._take_side(*self._sides.resolve(name, None, qual))
@@ -348,6 +389,15 @@ def _split_condition(cond, sides: _Sides):
             a, b = sides.side_of(t[1]), sides.side_of(t[2])
             if a is not None and b is not None and a[0] != b[0]:
                 keys.append((a[1], b[1]) if a[0] == 0 else (b[1], a[1]))
+                continue
+            if a is not None and b is not None and a[1] == b[1]:
+                # both operands on one side through a shared column object: never let the
+                # always-true residual x == x turn the join into a cross product
+                pair = sides.split_shared(t[1], t[2])
+                if pair is None:
+                    raise ValueError(f"join condition {c} compares column '{a[1]}' with itself; the sides "
+                                     "share it -- alias the frames (df.alias('a')) and use qualified names")
+                keys.append(pair)
                 continue
         rest.append(c)
     residual = None

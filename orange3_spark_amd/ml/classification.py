@@ -18,7 +18,7 @@ from .base import Estimator, Model
 from .linalg import DenseMatrix, DenseVector, Vectors
 from .param import (HasAggregationDepth, HasElasticNetParam, HasFeaturesCol, HasFitIntercept, HasLabelCol,
                     HasMaxBlockSizeInMB, HasMaxIter, HasPredictionCol, HasProbabilityCol, HasRawPredictionCol,
-                    HasRegParam, HasStandardization, HasStepSize, HasThreshold, HasThresholds, HasTol,
+                    HasRegParam, HasSeed, HasStandardization, HasStepSize, HasThreshold, HasThresholds, HasTol,
                     HasWeightCol, TypeConverters, add_accessors, keyword_only, shared)
 from ..runtime.checkpoint import for_estimator
 from .util import MLReadable, MLWritable, apply_metadata, mat_col, read_data, register, vec_col, write_data
@@ -55,20 +55,22 @@ def _svc_summary(model, df, res=None):
 class _LogisticRegressionParams(HasFeaturesCol, HasLabelCol, HasPredictionCol, HasProbabilityCol,
                                 HasRawPredictionCol, HasMaxIter, HasRegParam, HasElasticNetParam, HasTol,
                                 HasFitIntercept, HasThreshold, HasThresholds, HasStandardization, HasWeightCol,
-                                HasAggregationDepth, HasStepSize, HasMaxBlockSizeInMB):
+                                HasAggregationDepth, HasStepSize, HasMaxBlockSizeInMB, HasSeed):
     family = shared("family", "The name of family which is a description of the label distribution to be used in "
                               "the model. Supported options: auto, binomial, multinomial", TypeConverters.toString)
     solver = shared("solver", "The solver algorithm for optimization. Supported options: auto, l-bfgs, sgd "
-                              "(sgd = full-pass gradient descent with stepSize/sqrt(t) steps).",
+                              "(sgd = mini-batch gradient descent with stepSize/sqrt(t) steps, mllib "
+                              "GradientDescent semantics).",
                     TypeConverters.toString)
-    miniBatchFraction = shared("miniBatchFraction", "Fraction of rows used per SGD iteration, in (0, 1].",
-                               TypeConverters.toFloat)
+    miniBatchFraction = shared("miniBatchFraction", "Fraction of rows used per SGD iteration, in (0, 1]; each "
+                                                    "iteration draws its own Bernoulli sample keyed on (seed, "
+                                                    "iteration, row).", TypeConverters.toFloat)
 
     def __init__(self):
         super().__init__()
         self._setDefault(maxIter=100, regParam=0.0, tol=1e-6, threshold=0.5, family="auto", solver="auto",
                          stepSize=1.0, miniBatchFraction=1.0, elasticNetParam=0.0, fitIntercept=True,
-                         standardization=True)
+                         standardization=True, seed=42)
 
 
 @add_accessors
@@ -84,7 +86,7 @@ class LogisticRegression(Estimator, _LogisticRegressionParams, MLWritable, MLRea
                  regParam=0.0, elasticNetParam=0.0, tol=1e-6, fitIntercept=True, threshold=0.5, thresholds=None,
                  probabilityCol="probability", rawPredictionCol="rawPrediction", standardization=True,
                  weightCol=None, aggregationDepth=2, family="auto", solver="auto", stepSize=1.0,
-                 miniBatchFraction=1.0, maxBlockSizeInMB=0.0):
+                 miniBatchFraction=1.0, maxBlockSizeInMB=0.0, seed=42):
         super().__init__()
         self._set(**self._input_kwargs)
 
@@ -93,7 +95,7 @@ class LogisticRegression(Estimator, _LogisticRegressionParams, MLWritable, MLRea
                   regParam=0.0, elasticNetParam=0.0, tol=1e-6, fitIntercept=True, threshold=0.5, thresholds=None,
                   probabilityCol="probability", rawPredictionCol="rawPrediction", standardization=True,
                   weightCol=None, aggregationDepth=2, family="auto", solver="auto", stepSize=1.0,
-                  miniBatchFraction=1.0, maxBlockSizeInMB=0.0):
+                  miniBatchFraction=1.0, maxBlockSizeInMB=0.0, seed=42):
         return self._set(**self._input_kwargs)
 
     def _fit(self, df):
@@ -119,13 +121,15 @@ class LogisticRegression(Estimator, _LogisticRegressionParams, MLWritable, MLRea
         res = GLM.fit_glm(data, "logistic", g(self.regParam), g(self.elasticNetParam), g(self.fitIntercept),
                           g(self.standardization), g(self.maxIter), g(self.tol),
                           "sgd" if solver == "sgd" else "auto", g(self.stepSize), g(self.miniBatchFraction),
-                          ckpt=for_estimator(self, df))
+                          g(self.seed), ckpt=for_estimator(self, df))
         m = LogisticRegressionModel._from(res.coef[None, :], np.array([res.intercept]), False, 2)._with_parent(self)
         m.summary = _lr_summary(m, df, True, res)
+        m._fit_setup_seconds = getattr(res, "setup_seconds", 0.0)
         return m
 
     def trainer(self, df):
-        """Device-resident SGD stepper for this estimator's params (used by bench.py)."""
+        """Device-resident SGD stepper for this estimator's params (the engine of
+        ``fit(solver='sgd')``, exposed for step-level tests and tools)."""
         g = self.getOrDefault
         feat = U.features_column(df, g(self.featuresCol))
         y = U.numeric_column(df, g(self.labelCol), torch.float32)
@@ -135,7 +139,8 @@ class LogisticRegression(Estimator, _LogisticRegressionParams, MLWritable, MLRea
             _, var, *_ = data.moments()
             std = np.sqrt(var)
         return GLM.DeviceSGD(data, "logistic", g(self.regParam), g(self.fitIntercept), g(self.stepSize),
-                             g(self.standardization), std)
+                             g(self.standardization), std, elastic_net=g(self.elasticNetParam),
+                             mini_batch_fraction=g(self.miniBatchFraction), seed=g(self.seed))
 
 
 @register("org.apache.spark.ml.classification.LogisticRegressionModel")

@@ -51,7 +51,12 @@ def _worker(payload: bytes, rank: int, world: int, port: int, use_gpu: bool, q) 
 class TorchDistributor:
     """Distributed PyTorch training on the local MI355X GPUs (or CPU processes with gloo)."""
 
-    def __init__(self, num_processes: int = 1, local_mode: bool = True, use_gpu: bool = True, _ssl_conf=None):
+    def __init__(self, num_processes: int = 1, local_mode: bool = True, use_gpu: bool = True, _ssl_conf=None,
+                 timeout: float | None = None):
+        """``timeout`` (seconds, None = no deadline): like Spark's barrier-task timeout, a
+        run whose ranks have not all reported by then is torn down -- every rank is
+        terminated, survivors are killed -- and RuntimeError names the silent ranks."""
+        self.timeout = None if timeout is None else float(timeout)
         if int(num_processes) < 1:
             raise ValueError("num_processes must be >= 1")
         if not local_mode:
@@ -86,11 +91,18 @@ class TorchDistributor:
                  for r in range(self.num_processes)]
         for p in procs:
             p.start()
+        import time
         results, error = {}, None
+        deadline = None if self.timeout is None else time.monotonic() + self.timeout
         try:
             while len(results) < len(procs) and error is None:
+                if deadline is not None and time.monotonic() > deadline:
+                    silent = [r for r in range(len(procs)) if r not in results]
+                    error = f"timed out after {self.timeout:g} s; ranks {silent} never reported"
+                    break
+                wait = 5.0 if deadline is None else max(0.05, min(5.0, deadline - time.monotonic()))
                 try:
-                    rank, status, data = q.get(timeout=5)
+                    rank, status, data = q.get(timeout=wait)
                 except Exception:  # noqa: BLE001 - queue.Empty: check for ranks that died silently
                     dead = [r for r, p in enumerate(procs) if p.exitcode not in (None, 0) and r not in results]
                     if dead:
@@ -103,7 +115,11 @@ class TorchDistributor:
             for p in procs:
                 if error is not None and p.is_alive():
                     p.terminate()
-                p.join(60)
+            for p in procs:
+                p.join(10 if error is not None else 60)
+                if p.is_alive():                 # ignored SIGTERM / still stuck in a collective
+                    p.kill()
+                    p.join(10)
         if error is not None:
             raise RuntimeError(f"TorchDistributor: {error}")
         return cloudpickle.loads(results[0])

@@ -77,6 +77,10 @@ class GlmData:
         # for glm_grad's, tools/bench_glm_roles.py)
         self.mixed = self.kernel and os.environ.get("O3S_GLM_MIXED", "1") == "1" \
             and (self.sw is None or self.sw.shape[0] == self.y.shape[0])
+        self._row0 = int(feat.row0) if isinstance(feat, LineageVectorColumn) else None
+        self._setup_workspace()
+
+    def _setup_workspace(self):
         if self.mixed:
             cus = N.num_cus(self.device)
             # 16-row tiles, 4 waves per block: never more blocks than one tile per wave
@@ -93,7 +97,45 @@ class GlmData:
             self.ws = G.GlmWorkspace(self.device, self.ld, grid=res_grid)
             self.overlap = (torch.cuda.Stream(self.device), G.GlmWorkspace(self.device, self.ld, grid=lin_grid))
 
+    def global_row0(self) -> int:
+        """Global index of this rank's first row (row-sharded frames: exclusive prefix sum
+        of the local row counts in rank order) -- the key of the mini-batch sampler."""
+        if self._row0 is None:
+            counts = self.comm.all_gather_object(int(self.n_local))
+            self._row0 = int(sum(counts[: self.comm.rank]))
+        return self._row0
+
+    def require_mixed(self) -> None:
+        """Mini-batch sampling lives in the mixed kernel: switch to it if disabled."""
+        if self.kernel and not self.mixed:
+            self.mixed, self.overlap = True, None
+            self._setup_workspace()
+
     # ---------------------------------------------------------------- moments
+    def stats(self):
+        """Fused summarizer + first-gradient pass (``ops.glm.glm_stats_mixed``), all-reduced,
+        as host fp64 ``(s1, s2, syx, W, sum w y, sum w y^2)`` over the first ``d`` columns;
+        None when this data has no fused pass (CPU dense rows use the torch reference)."""
+        spec, r0, nl = self.lineage if self.lineage else (None, 0, 0)
+        if self.kernel:
+            if not self.mixed:
+                return None
+            st = G.glm_stats_mixed(self.X, self.y, self.sw, nl, spec.d if spec else self.d,
+                                   spec.seed if spec else 0, r0)
+            if st is None:
+                return None
+            dpad = self.ws.dpad
+        else:
+            st = G.glm_stats_torch(self.X, self.y, self.sw, nl, spec.d if spec else self.d,
+                                   spec.seed if spec else 0, r0).to(self.device)
+            dpad = G.layout(self.ld)[0]
+        self.comm.all_reduce(st)
+        h = st.cpu().numpy()
+        d = self.d
+        self.passes += 1
+        return (h[:d], h[dpad:dpad + d], h[2 * dpad:2 * dpad + d], float(h[3 * dpad]), float(h[3 * dpad + 1]),
+                float(h[3 * dpad + 2]))
+
     def moments(self):
         """Global weighted (mean, variance (unbiased), weight sum, label moments)."""
         d = self.d
@@ -131,18 +173,26 @@ class GlmData:
         return mean[:self.d], var[:self.d], W, ymean, yvar
 
     # ---------------------------------------------------------------- one pass
-    def pass_device(self, coef_eff: torch.Tensor, intercept: float | None, loss: int) -> torch.Tensor:
+    def pass_device(self, coef_eff: torch.Tensor, intercept: float | None, loss: int,
+                    t_dev: torch.Tensor | None = None, sample: tuple | None = None) -> torch.Tensor:
         """Local pass; returns device fp64 [grad (dpad) | sum r | loss | wsum] (not reduced).
 
         Resident and lineage rows accumulate into the workspace's result buffer (valid
         until the next pass).  ``intercept=None``: ``coef_eff`` is the fp32 [dpad + 1]
-        device operand (coefficients + intercept).
+        device operand (coefficients + intercept).  ``sample=(seed, fraction)`` with
+        fraction < 1: mini-batch of iteration ``t_dev[0] + 1`` (in-kernel row mask).
         """
         ws = self.ws
+        if sample is not None and sample[1] < 1.0:
+            self.require_mixed()
+            ws = self.ws
         if self.mixed:
             spec, r0, nl = self.lineage if self.lineage else (None, 0, 0)
+            sseed, frac = sample if sample is not None else (0, 1.0)
             G.glm_grad_mixed(self.X, self.y, self.sw, nl, spec.d if spec else self.d,
-                             spec.seed if spec else 0, r0, coef_eff, intercept, loss, ws)
+                             spec.seed if spec else 0, r0, coef_eff, intercept, loss, ws,
+                             res_row0=self.global_row0() if frac < 1.0 else 0, t_dev=t_dev,
+                             sample_seed=sseed, fraction=frac)
             self.passes += 1
             return ws.out
         if self.overlap is not None:
@@ -176,16 +226,22 @@ class GlmData:
         self.passes += 1
         return ws.out
 
-    def pass_torch(self, coef_eff: torch.Tensor, intercept: float, loss: int) -> torch.Tensor:
+    def pass_torch(self, coef_eff: torch.Tensor, intercept: float, loss: int, it: int = 1,
+                   sample: tuple | None = None) -> torch.Tensor:
         dpad = self.ld
         acc = torch.zeros(dpad + 3, dtype=torch.float64, device=self.device)
         c = coef_eff.to(self.device, torch.float64)[: self.ld]
         n = self.X.shape[0]
+        sampled = sample is not None and sample[1] < 1.0
+        g0 = self.global_row0() if sampled else 0
         for a in range(0, n, self.chunk):
             b = min(n, a + self.chunk)
             Xc = self.X[a:b].to(torch.float64)
             yc = self.y[a:b].to(torch.float64)
             wc = None if self.sw is None else self.sw[a:b].to(torch.float64)
+            if sampled:
+                keep = G.sample_mask(sample[0], it, torch.arange(g0 + a, g0 + b), sample[1]).to(self.device)
+                wc = keep.to(torch.float64) if wc is None else wc * keep
             acc += G.glm_grad_torch(Xc, yc, wc, c, intercept, loss)
         self.passes += 1
         return acc
@@ -248,10 +304,25 @@ class SparseGlmData:
         yvar = max((ys2 - W * ymean * ymean) / max(W - 1.0, 1e-300), 0.0)
         return mean, var, W, ymean, yvar
 
+    sample_state = None          # (seed, fraction, iteration) while a mini-batch SGD fit runs
+    _row0 = None
+
+    def global_row0(self) -> int:
+        if self._row0 is None:
+            counts = self.comm.all_gather_object(int(self.n_local))
+            self._row0 = int(sum(counts[: self.comm.rank]))
+        return self._row0
+
     @traced("glm.pass")
     def loss_grad(self, coef_eff: np.ndarray, intercept: float, loss: int):
         ct = torch.from_numpy(np.ascontiguousarray(coef_eff, dtype=np.float64))
-        out = self.rows.loss_grad(ct, intercept, loss, self.y, self.sw)
+        sw = self.sw
+        st = self.sample_state
+        if st is not None and st[1] < 1.0:
+            g0 = self.global_row0()
+            keep = G.sample_mask(st[0], st[2], torch.arange(g0, g0 + self.n_local), st[1]).to(self.device)
+            sw = keep.to(torch.float64) if sw is None else sw.to(torch.float64) * keep
+        out = self.rows.loss_grad(ct, intercept, loss, self.y, sw)
         self.comm.all_reduce(out)
         self.passes += 1
         o = out.cpu().numpy()
@@ -275,6 +346,7 @@ class GlmResult:
     converged: bool = False
     seconds: float = 0.0
     passes: int = 0
+    setup_seconds: float = 0.0
 
 
 class GlmObjective:
@@ -314,9 +386,95 @@ class GlmObjective:
         return f, gx
 
 
+def _initial_intercept(loss: str, fit_intercept: bool, ymean: float, init_intercept=None) -> float:
+    if not fit_intercept:
+        return 0.0
+    if init_intercept is not None:
+        return float(init_intercept)
+    if loss == "logistic" and 0 < ymean < 1:
+        return math.log(ymean / (1 - ymean))
+    if loss == "squared":
+        return float(ymean)
+    return 0.0
+
+
+def _first_step_out(loss: str, b0: float, s1, syx, W: float, wy: float, wyy: float):
+    """[grad | sum r | loss | W] of the pass at the initial iterate (all coefficients 0,
+    every margin = b0) from the fused stats, or None when it is not a closed form."""
+    if loss == "logistic":
+        p = 1.0 / (1.0 + math.exp(-b0))
+        sp = max(b0, 0.0) + math.log1p(math.exp(-abs(b0)))
+        return p * s1 - syx, p * W - wy, sp * W - b0 * wy
+    if loss == "hinge":
+        if abs(b0) >= 1.0:
+            return None
+        # every row active: r = -(2y - 1) w
+        return s1 - 2.0 * syx, W - 2.0 * wy, W - b0 * (2.0 * wy - W)
+    return b0 * s1 - syx, b0 * W - wy, 0.5 * (b0 * b0 * W - 2.0 * b0 * wy + wyy)
+
+
+def fit_sgd(data: GlmData, loss: str, reg=0.0, alpha=0.0, fit_intercept=True, standardization=True,
+            max_iter=100, tol=1e-6, step_size=1.0, mini_batch_fraction=1.0, seed=0, init_intercept=None,
+            ckpt=None, check_every: int = 10) -> GlmResult:
+    """``solver='sgd'`` fit on the device (mllib GradientDescent semantics: step
+    stepSize/sqrt(t), per-iteration Bernoulli mini-batch of ``mini_batch_fraction`` keyed
+    on (seed, t, global row), L2 shrink + L1 soft-threshold updater).
+
+    The summarizer pass is fused with the first iteration's gradient (one pass over the
+    rows instead of two, ``GlmData.stats``); every later iteration is one fused gradient
+    pass + one all-reduce + an on-device update, graph-replayed, with no host sync except
+    a convergence probe every ``check_every`` iterations when ``tol > 0``."""
+    t0 = time.time()
+    frac = float(mini_batch_fraction)
+    G.sample_threshold(frac)                        # validates the fraction
+    last = ckpt.latest() if ckpt is not None else None
+    st = data.stats() if (frac >= 1.0 and last is None and max_iter > 0) else None
+    if st is not None:
+        s1, s2, syx, W, wy, wyy = st
+        mean = s1 / max(W, 1e-300)
+        var = np.maximum((s2 - W * mean * mean) / max(W - 1.0, 1e-300), 0.0)
+        ymean = wy / max(W, 1e-300)
+    else:
+        mean, var, W, ymean, _ = data.moments()
+    std = np.sqrt(var)
+    b0 = _initial_intercept(loss, fit_intercept, ymean, init_intercept)
+    sgd = DeviceSGD(data, loss, reg, fit_intercept, step_size, standardization, std, elastic_net=alpha,
+                    mini_batch_fraction=frac, seed=seed, init_intercept=b0)
+    setup_s = time.time() - t0
+    done = 0
+    if last is not None and last[1]["x"].shape[0] == data.d + (1 if fit_intercept else 0):
+        done = int(last[0])
+        sgd.set_state(last[1]["x"], done)
+    elif st is not None:
+        first = _first_step_out(loss, b0, s1, syx, W, wy, wyy)
+        if first is not None:
+            sgd.apply_first_step(*first, W)
+    converged = False
+    while sgd.t < max_iter:
+        sgd.step()
+        if (tol > 0 or ckpt is not None) and sgd.t % check_every == 0:
+            h = sgd.loss_hist[max(0, sgd.t - 2):sgd.t].cpu().numpy()
+            if ckpt is not None and ckpt.due(sgd.t):
+                ckpt.save(sgd.t, {"x": sgd.state()})
+            if tol > 0 and len(h) == 2 and abs(h[0] - h[1]) / max(abs(h[1]), 1e-12) < tol:
+                converged = True
+                break
+    if ckpt is not None:
+        ckpt.clear()
+    res = sgd.result()
+    res.converged = converged
+    res.seconds = time.time() - t0
+    res.setup_seconds = setup_s
+    res.passes = data.passes
+    return res
+
+
 def fit_glm(data: GlmData, loss: str, reg=0.0, alpha=0.0, fit_intercept=True, standardization=True,
             max_iter=100, tol=1e-6, solver="auto", step_size=1.0, mini_batch_fraction=1.0, seed=0,
             init_intercept=None, ckpt=None) -> GlmResult:
+    if solver in ("sgd", "gd") and isinstance(data, GlmData):
+        return fit_sgd(data, loss, reg, alpha, fit_intercept, standardization, max_iter, tol, step_size,
+                       mini_batch_fraction, seed, init_intercept, ckpt)
     t0 = time.time()
     mean, var, W, ymean, yvar = data.moments()
     std = np.sqrt(var)
@@ -359,29 +517,43 @@ def fit_glm(data: GlmData, loss: str, reg=0.0, alpha=0.0, fit_intercept=True, st
 
 
 def _sgd(obj: GlmObjective, x0, max_iter, step, frac, seed, tol) -> GlmResult:
-    """Host-driven minibatch SGD (Spark mllib GradientDescent: step/sqrt(t) schedule)."""
+    """Host-driven minibatch SGD for CSR rows (Spark mllib GradientDescent: step/sqrt(t)
+    schedule, per-iteration Bernoulli sample of ``frac`` keyed on (seed, t, global row) --
+    the same draw as the device path)."""
     x = x0.copy()
     hist = []
     for t in range(1, max_iter + 1):
+        obj.data.sample_state = (int(seed), float(frac), t)
         f, g = obj.smooth(x)
         hist.append(f)
         x = x - (step / math.sqrt(t)) * g
         if len(hist) > 1 and abs(hist[-2] - hist[-1]) / max(abs(hist[-1]), 1e-12) < tol * 1e-3:
             break
+    obj.data.sample_state = None
     return GlmResult(x, 0.0, hist, len(hist), False)
 
 
 class DeviceSGD:
     """Device-resident gradient-descent stepper (no host sync per step).
 
-    One ``step()`` = one fused pass over every local row (resident + lineage), one
-    all-reduce of a (D+3) fp64 vector, and an on-device update
-    b~ <- b~ - eta_t (grad/W + l2 * b~), eta_t = stepSize / sqrt(t).  This is the
-    ``solver='sgd'`` path of LogisticRegression/LinearSVC and what bench.py times.
+    One ``step()`` = one fused pass over every local row (resident + lineage; with
+    ``mini_batch_fraction < 1`` an in-kernel Bernoulli mask keyed on (seed, t, global row)),
+    one all-reduce of a (D+3) fp64 vector, and an on-device update
+    b~ <- prox_l1(b~ - eta_t (grad/W + l2 * b~)), eta_t = stepSize / sqrt(t), where W is
+    the (sampled) weight sum -- mllib GradientDescent with its Squared-L2 / L1 updaters.
+    This is the ``solver='sgd'`` path of LogisticRegression / LinearSVC / LinearRegression.
+
+    Launch structure: after two eager steps a step is captured into HIP graphs.  With one
+    rank the whole step (pass, update) is one graph; with several ranks the pass and the
+    update are two graphs around the RCCL all-reduce, which runs eagerly on the same stream
+    (stream-ordered, no host sync) -- the collective is never captured, so graph replay
+    never depends on RCCL's capture support.
     """
 
     def __init__(self, data: GlmData, loss: str = "logistic", reg: float = 0.0, fit_intercept=True,
-                 step_size: float = 1.0, standardization: bool = True, std: np.ndarray | None = None):
+                 step_size: float = 1.0, standardization: bool = True, std: np.ndarray | None = None,
+                 elastic_net: float = 0.0, mini_batch_fraction: float = 1.0, seed: int = 0,
+                 init_intercept: float = 0.0):
         self.data, self.loss = data, LOSS_ID[loss]
         dev = data.device
         dpad = data.ws.dpad if data.kernel else data.ld
@@ -389,93 +561,152 @@ class DeviceSGD:
         inv = np.ones(data.d) if std is None else np.where(std > 0, 1.0 / np.where(std > 0, std, 1.0), 0.0)
         self.inv_std = torch.zeros(dpad, dtype=torch.float64, device=dev)
         self.inv_std[: data.d] = torch.from_numpy(inv).to(dev)
-        self.l2 = float(reg) if standardization else 0.0
-        self.l2v = (float(reg) * self.inv_std ** 2) if not standardization else None
+        a = float(elastic_net)
+        l2, l1 = float(reg) * (1.0 - a), float(reg) * a
+        # penalties on the standardised coefficients b~ (standardization=true) or on b
+        self.l2 = l2 if standardization else 0.0
+        self.l2v = (l2 * self.inv_std ** 2) if not standardization else None
+        self.l1 = l1 if standardization else 0.0
+        self.l1v = (l1 * self.inv_std) if (not standardization and l1 > 0) else None
         self.bt = torch.zeros(dpad, dtype=torch.float64, device=dev)      # standardised coefficients
-        self.b = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.b = torch.full((1,), float(init_intercept) if fit_intercept else 0.0, dtype=torch.float64, device=dev)
         # kernel operand: effective fp32 coefficients followed by the intercept
         self.coef_eff = torch.zeros(dpad + 1, dtype=torch.float32, device=dev)
+        self.coef_eff[dpad] = float(self.b[0])
         self.fi = fit_intercept
         self.step_size = float(step_size)
+        self.fraction = float(mini_batch_fraction)
+        G.sample_threshold(self.fraction)
+        self.sample = (int(seed), self.fraction) if self.fraction < 1.0 else None
         self.t = 0
         self.loss_hist = torch.zeros(1024, dtype=torch.float64, device=dev)
         self.t_dev = torch.zeros(1, dtype=torch.int64, device=dev)      # device step counter
-        self._graph = None
+        self._graphs = None
         self._graph_failed = False
         self._eager_steps = 0
-        self.W = float(data.comm.sum_scalar(float(data.n_local if data.sw is None else float(data.sw.sum()))))
+        self._first_buf = None
+        self.passes = 0
+
+    # ---------------------------------------------------------------- state
+    def state(self) -> np.ndarray:
+        """[b~ (d) | intercept] on the host (checkpoint format of fit_glm)."""
+        x = self.bt[: self.data.d].cpu().numpy()
+        return np.concatenate([x, self.b.cpu().numpy()]) if self.fi else x
+
+    def set_state(self, x: np.ndarray, t: int) -> None:
+        d = self.data.d
+        self.bt.zero_()
+        self.bt[:d] = torch.from_numpy(np.asarray(x[:d], dtype=np.float64)).to(self.bt.device)
+        if self.fi:
+            self.b.fill_(float(x[d]))
+        self.coef_eff[: self.dpad].copy_((self.bt * self.inv_std).to(torch.float32))
+        self.coef_eff[self.dpad:].copy_(self.b.to(torch.float32))
+        self.t = int(t)
+        self.t_dev.fill_(int(t))
+        self._ensure_hist()
+        self._graphs = None
+
+    def _ensure_hist(self):
+        if self.t > self.loss_hist.shape[0]:
+            n = self.loss_hist.shape[0]
+            while n < self.t:
+                n *= 2
+            self.loss_hist = torch.cat([self.loss_hist, torch.zeros(n - self.loss_hist.shape[0],
+                                                                     dtype=torch.float64, device=self.loss_hist.device)])
+            self._graphs = None
+
+    # ---------------------------------------------------------------- steps
+    def apply_first_step(self, grad: np.ndarray, sum_r: float, loss_sum: float, W: float) -> None:
+        """Iteration 1 from an already-reduced pass result at the initial iterate (the fused
+        summarizer pass, fit_sgd): only the update runs."""
+        out = torch.zeros(self.dpad + 3, dtype=torch.float64)
+        out[: self.data.d] = torch.from_numpy(np.asarray(grad, dtype=np.float64))
+        out[self.dpad:] = torch.tensor([sum_r, loss_sum, W], dtype=torch.float64)
+        self._first_buf = out.to(self.bt.device)
+        self.t += 1
+        self._ensure_hist()
+        self._update(self._first_buf)
 
     @traced("sgd.step")
     def step(self):
-        """One step, entirely stream-ordered on the device: pass -> all-reduce -> update.
-
-        GPU: after two eager steps the step is captured into a HIP graph (torch.cuda.CUDAGraph
-        over the raw kernel launches; the step counter, step size and loss slot live on the
-        device, so the captured step has no host arguments) and later steps replay it -- the
-        launch sequence of a step costs one graph launch instead of ~4 kernel launches plus
-        Python.  O3S_SGD_GRAPH=0 disables it; with several ranks it is opt-in
-        (O3S_SGD_GRAPH=all: the RCCL all-reduce is captured too)."""
+        """One iteration, stream-ordered on the device: pass -> all-reduce -> update."""
         self.t += 1
+        self._ensure_hist()
         d = self.data
+        self.passes += 1
+        if d.kernel and self._graphs is not None:
+            gp, gu = self._graphs
+            gp.replay()
+            if gu is not None:
+                d.comm.all_reduce(self.data.ws.out)
+                gu.replay()
+            d.passes += 1
+            return
+        out = self._pass()
+        d.comm.all_reduce(out)
+        self._update(out)
         if d.kernel:
-            if self._graph is not None and self.t <= self.loss_hist.shape[0]:
-                self._graph.replay()
-                return
-            if self.t > self.loss_hist.shape[0]:
-                self.loss_hist = torch.cat([self.loss_hist, torch.zeros_like(self.loss_hist)])
-                self._graph = None
-            self._kernel_step()
             self._eager_steps += 1
             self._maybe_capture()
+
+    def _pass(self):
+        if self.data.kernel:
+            return self.data.pass_device(self.coef_eff, None, self.loss, t_dev=self.t_dev, sample=self.sample)
+        return self.data.pass_torch(self.coef_eff[: self.dpad], float(self.b.item()), self.loss, it=self.t,
+                                    sample=self.sample)
+
+    def _update(self, out: torch.Tensor):
+        if self.data.kernel:
+            N.check(N.kernels().o3s_glm_sgd_update_dev(
+                out.data_ptr(), self.dpad, self.bt.data_ptr(), self.b.data_ptr(), self.inv_std.data_ptr(),
+                N.ptr(self.l2v), self.l2, N.ptr(self.l1v), self.l1, self.step_size, int(self.fi),
+                self.coef_eff.data_ptr(), self.loss_hist.data_ptr(), int(self.loss_hist.shape[0]),
+                self.t_dev.data_ptr(), torch.cuda.current_stream(self.data.device).cuda_stream), "glm_sgd_update")
             return
         eta = self.step_size / math.sqrt(self.t)
-        if self.t > self.loss_hist.shape[0]:
-            self.loss_hist = torch.cat([self.loss_hist, torch.zeros_like(self.loss_hist)])
-        slot = self.loss_hist[self.t - 1:self.t]
-        out = self._pass()
-        d.comm.all_reduce(out)
         W = out[self.dpad + 2]
-        g = out[: self.dpad] * self.inv_std / W
+        invW = torch.where(W > 0, 1.0 / W, torch.zeros_like(W))
+        g = out[: self.dpad] * self.inv_std * invW
         g = g + (self.l2v if self.l2v is not None else self.l2) * self.bt
-        self.bt -= eta * g
+        v = self.bt - eta * g
+        if self.l1v is not None or self.l1 > 0:
+            sh = eta * (self.l1v if self.l1v is not None else self.l1)
+            v = torch.sign(v) * torch.clamp(v.abs() - sh, min=0.0)
+        self.bt.copy_(v)
         if self.fi:
-            self.b -= eta * out[self.dpad] / W
+            self.b -= eta * out[self.dpad] * invW
         self.coef_eff[: self.dpad].copy_((self.bt * self.inv_std).to(torch.float32))
         self.coef_eff[self.dpad:].copy_(self.b.to(torch.float32))
-        slot.copy_(out[self.dpad + 1:self.dpad + 2] / W)
-
-    def _kernel_step(self):
-        d = self.data
-        out = self._pass()
-        d.comm.all_reduce(out)
-        N.check(N.kernels().o3s_glm_sgd_update_dev(
-            out.data_ptr(), self.dpad, self.bt.data_ptr(), self.b.data_ptr(), self.inv_std.data_ptr(),
-            N.ptr(self.l2v), self.l2, self.step_size, int(self.fi), self.coef_eff.data_ptr(),
-            self.loss_hist.data_ptr(), int(self.loss_hist.shape[0]), self.t_dev.data_ptr(),
-            torch.cuda.current_stream(d.device).cuda_stream), "glm_sgd_update")
+        self.loss_hist[self.t - 1:self.t].copy_(out[self.dpad + 1:self.dpad + 2] * invW)
+        self.t_dev.fill_(self.t)
 
     def _maybe_capture(self):
         from ..runtime import faults
         mode = os.environ.get("O3S_SGD_GRAPH", "1")
-        if self._graph is not None or self._graph_failed or mode == "0" or self._eager_steps < 2:
-            return
-        if self.data.comm.world_size > 1 and mode != "all":
+        if self._graphs is not None or self._graph_failed or mode == "0" or self._eager_steps < 2:
             return
         if faults.launch_blocking():
             return
+        d = self.data
         try:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._kernel_step()
-            self._graph = g
+            if d.comm.world_size == 1:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    out = self._pass()
+                    self._update(out)
+                self._graphs = (g, None)
+            else:
+                gp, gu = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gp):
+                    out = self._pass()
+                with torch.cuda.graph(gu):
+                    self._update(out)
+                self._graphs = (gp, gu)
+            d.passes -= 1                    # the capture recorded, it did not run
         except Exception as e:  # noqa: BLE001 - fall back to eager launches
             log.warning("SGD step graph capture failed (%s); continuing eagerly", e)
             self._graph_failed = True
-
-    def _pass(self):
-        if self.data.kernel:
-            return self.data.pass_device(self.coef_eff, None, self.loss)
-        return self.data.pass_torch(self.coef_eff[: self.dpad], float(self.b.item()), self.loss)
+            self._graphs = None
 
     def result(self) -> GlmResult:
         coef = (self.bt * self.inv_std)[: self.data.d].cpu().numpy()

@@ -31,7 +31,8 @@ _SIGS: dict[str, list] = {
     "o3s_glm_grad": [c_i32, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_u32, c_i64,
                      c_vp, c_f32, c_vp, c_i32, c_vp, c_i32, c_vp],
     "o3s_glm_grad_mixed": [c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_u32, c_i64, c_i64,
-                           c_vp, c_i32, c_vp, c_i32, c_i32, c_vp],
+                           c_vp, c_i32, c_vp, c_i32, c_i32, c_i64, c_vp, c_u32, c_u32, c_vp],
+    "o3s_glm_stats_mixed": [c_vp, c_i64, c_i64, c_vp, c_vp, c_u32, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp],
     "o3s_bin_features": [c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp],
     "o3s_u8_transpose": [c_vp, c_i64, c_i32, c_vp, c_vp],
     "o3s_slab_range_sum": [c_vp, c_i32, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp],
@@ -45,8 +46,8 @@ _SIGS: dict[str, list] = {
     "o3s_tree_partition": [c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
                            c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_glm_sgd_update": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_f64, c_f64, c_i32, c_vp, c_vp, c_vp],
-    "o3s_glm_sgd_update_dev": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_f64, c_f64, c_i32, c_vp, c_vp, c_i64, c_vp,
-                               c_vp],
+    "o3s_glm_sgd_update_dev": [c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_f64, c_vp, c_f64, c_f64, c_i32, c_vp, c_vp,
+                               c_i64, c_vp, c_vp],
     "o3s_synth_glm": [c_vp, c_i64, c_i64, c_vp, c_u32, c_i64, c_vp, c_f32, c_i32, c_vp],
     "o3s_glm_margin": [c_vp, c_i64, c_i64, c_vp, c_f32, c_vp, c_i32, c_vp],
     "o3s_glm_colstats": [c_i32, c_vp, c_i64, c_i64, c_vp, c_u32, c_i64, c_vp, c_i32, c_vp, c_vp],

@@ -426,11 +426,26 @@ __device__ __forceinline__ void row_reduce_8x2(float (&v)[2], int c) {
 // their lineage (raw bytes b, x = b*kSynthScale + kSynthShift, the affine map folded into
 // the dot product and a per-lane residual sum rs).  Labels / weights of both roles come
 // from the materialised label column (y, sw already offset to the role's first row).
+// Mini-batch sampling (miniBatchFraction < 1, mllib GradientDescent's per-iteration
+// `data.sample(false, fraction, seed + i)`): row r of iteration t is kept iff
+// row_key(sample_key(seed, t), global r) >> 8 < fraction * 2^24.  The mask only zeroes a
+// row's weight (its residual, loss and weight-sum terms), so it costs one hash per row,
+// needs no compaction pass, and the kept set is independent of the sharding.
+struct RowSampler {
+  uint32_t key, thr;   // thr >= 2^24: every row kept (sampling off)
+  int64_t grow0;       // global index of the role's row 0
+  __device__ __forceinline__ bool on() const { return thr < (1u << 24); }
+  __device__ __forceinline__ bool keep(int64_t row) const { return (row_key(key, grow0 + row) >> 8) < thr; }
+};
+__host__ __device__ __forceinline__ uint32_t sample_key(uint32_t seed, uint32_t iter) {
+  return fmix32(seed ^ fmix32(iter * 0x9E3779B1u + 0x7F4A7C15u));
+}
+
 template <int LPR, int CPL, int UNROLL, int LOSS, int SRC>
 __device__ __forceinline__ void mixed_tile(
     int64_t base, int64_t n, const uint16_t* __restrict__ X, int64_t ld, int nch,
     const float* __restrict__ y, const float* __restrict__ sw, uint32_t seed, int64_t row0,
-    const float (&w)[CPL][8], float wshift, float intercept, int g, int c,
+    const float (&w)[CPL][8], float wshift, float intercept, int g, int c, const RowSampler smp,
     float (&acc)[CPL][8], float& rs, float& acc_r, float& acc_loss, float& acc_w) {
   constexpr int G = kWave / LPR;
   using RR = RowReduce<LPR, UNROLL>;
@@ -476,6 +491,7 @@ __device__ __forceinline__ void mixed_tile(
     const float wv = sw ? sw[rowc] : 1.f;
     yy[j] = ok ? yv : 0.f;
     ww[j] = ok ? wv : 0.f;
+    if (smp.on() && !smp.keep(row)) ww[j] = 0.f;
   }
   float dot[UNROLL];
 #pragma unroll
@@ -553,7 +569,8 @@ template <int LPR, int CPL, int UNROLL, int LOSS, int MW, int LW, int UR>
 __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
     const uint16_t* __restrict__ X, int64_t ld, int64_t n_res, const float* __restrict__ y,
     const float* __restrict__ sw, const float* __restrict__ coef, const float* __restrict__ bptr,
-    uint32_t seed, int64_t row0, int64_t n_lin, float* __restrict__ partial, int pstride) {
+    uint32_t seed, int64_t row0, int64_t n_lin, float* __restrict__ partial, int pstride,
+    int64_t res_row0, const int64_t* __restrict__ t_dev, uint32_t sseed, uint32_t sthr) {
   constexpr int G = kWave / LPR;
   constexpr int RT = G * UNROLL;
   constexpr int DP = LPR * CPL * 8;
@@ -565,6 +582,9 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
   const float intercept = *bptr;
   const float* y_lin = y + n_res;
   const float* sw_lin = sw ? sw + n_res : nullptr;
+  // iteration t of a device-side SGD loop = t_dev + 1 (the update kernel advances it)
+  const uint32_t skey = sthr < (1u << 24) ? sample_key(sseed, (uint32_t)((t_dev ? t_dev[0] : 0) + 1)) : 0u;
+  const RowSampler smp_res{skey, sthr, res_row0}, smp_lin{skey, sthr, row0};
 
   float w[CPL][8], acc[CPL][8];
   float wshift = 0.f, rs = 0.f;
@@ -591,10 +611,12 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
       for (int64_t s = gw; s < S; s += nw) {
         if (rem + Tl >= S)
           mixed_tile<LPR, CPL, UNROLL, LOSS, 1>(L * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
-                                                wshift, intercept, g, c, acc, rs, acc_r, acc_loss, acc_w);
+                                                wshift, intercept, g, c, smp_lin, acc, rs, acc_r, acc_loss,
+                                                acc_w);
         else
           mixed_tile<LPR, CPL, UNROLL, LOSS, 0>((s - L) * RT, n_res, X, ld, nch, y, sw, seed, row0, w,
-                                                wshift, intercept, g, c, acc, rs, acc_r, acc_loss, acc_w);
+                                                wshift, intercept, g, c, smp_res, acc, rs, acc_r, acc_loss,
+                                                acc_w);
         rem += r0;
         L += q0;
         if (rem >= S) { rem -= S; ++L; }
@@ -606,14 +628,14 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
       const int64_t nlw = (int64_t)gridDim.x * LW;
       for (int64_t t = (int64_t)blockIdx.x * LW + wid; t < Tl; t += nlw)
         mixed_tile<LPR, CPL, UNROLL, LOSS, 1>(t * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
-                                              wshift, intercept, g, c, acc, rs, acc_r, acc_loss, acc_w);
+                                              wshift, intercept, g, c, smp_lin, acc, rs, acc_r, acc_loss, acc_w);
     } else {
       constexpr int RTR = G * UR;
       const int64_t Tr = (n_res + RTR - 1) / RTR;
       const int64_t nrw = (int64_t)gridDim.x * (kWavesPerBlock - LW);
       for (int64_t t = (int64_t)blockIdx.x * (kWavesPerBlock - LW) + (wid - LW); t < Tr; t += nrw)
         mixed_tile<LPR, CPL, UR, LOSS, 0>(t * RTR, n_res, X, ld, nch, y, sw, seed, row0, w, wshift,
-                                          intercept, g, c, acc, rs, acc_r, acc_loss, acc_w);
+                                          intercept, g, c, smp_res, acc, rs, acc_r, acc_loss, acc_w);
     }
   }
 #pragma unroll
@@ -642,6 +664,144 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
   }
   __syncthreads();
   for (int i = threadIdx.x; i < DP + 3; i += kBlock) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < kWavesPerBlock; ++q) s += red[q][i];
+    partial[(int64_t)blockIdx.x * pstride + i] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Summarizer pass of a gradient-descent fit, fused with its first gradient: per column
+// s1 = sum w x, s2 = sum w x^2 and syx = sum w y x, per row sum w, sum w y, sum w y^2,
+// over the resident rows of X and n_lin lineage rows in ONE interleaved launch (same
+// tile schedule as glm_grad_mixed_kernel).  At the initial iterate every coefficient is
+// zero, so each row's margin is the intercept b0 and the step-1 gradient of every loss
+// is a combination of s1 and syx (logistic: sigmoid(b0) s1 - syx) -- the fit's first
+// step needs no pass of its own (models/glm.py: DeviceSGD.first_step_from_stats).
+template <int LPR, int CPL, int SRC>
+__device__ __forceinline__ void stats_tile(int64_t base, int64_t n, const uint16_t* __restrict__ X, int64_t ld,
+                                           int nch, const float* __restrict__ y, const float* __restrict__ sw,
+                                           uint32_t seed, int64_t row0, int g, int c, float2_ (&s1)[CPL][4],
+                                           float2_ (&s2)[CPL][4], float2_ (&syx)[CPL][4], float (&rsum)[3]) {
+  constexpr int G = kWave / LPR;
+  constexpr int U = CPL >= 8 ? 1 : 8 / CPL;
+  short8 xv[U][CPL];
+  float yv[U], wv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t row = base + u * G + g;
+    const bool ok = row < n;
+    const int64_t rowc = ok ? row : n - 1;
+    yv[u] = y[rowc];
+    const float w0 = sw ? sw[rowc] : 1.f;
+    wv[u] = ok ? w0 : 0.f;
+    if (SRC == 0) {
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) {
+        const int ch = c + k * LPR;
+        const int chc = ch < nch ? ch : nch - 1;
+        short8 v = __builtin_nontemporal_load(reinterpret_cast<const short8*>(X + rowc * ld + 8 * chc));
+        xv[u][k] = ch < nch ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
+      }
+    } else {
+      const uint32_t fk = feat_key(seed, row0 + rowc);
+#pragma unroll
+      for (int k = 0; k < CPL; ++k) xv[u][k] = synth_chunk(fk, c + k * LPR);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float2_ w2 = {wv[u], wv[u]};
+    const float wy = wv[u] * yv[u];
+    const float2_ wy2 = {wy, wy};
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+      float x[8];
+      unpack8(xv[u][k], x);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float2_ xx = {x[2 * j], x[2 * j + 1]};
+        const float2_ wx = w2 * xx;
+        s1[k][j] += wx;
+        s2[k][j] = __builtin_elementwise_fma(wx, xx, s2[k][j]);
+        syx[k][j] = __builtin_elementwise_fma(wy2, xx, syx[k][j]);
+      }
+    }
+    if (c == 0) {
+      rsum[0] += wv[u];
+      rsum[1] += wy;
+      rsum[2] = fmaf(wy, yv[u], rsum[2]);
+    }
+  }
+}
+
+template <int LPR, int CPL>
+__global__ __launch_bounds__(kBlock, 2) void glm_stats_mixed_kernel(
+    const uint16_t* __restrict__ X, int64_t ld, int64_t n_res, const float* __restrict__ y,
+    const float* __restrict__ sw, uint32_t seed, int64_t row0, int64_t n_lin, float* __restrict__ partial,
+    int pstride) {
+  constexpr int G = kWave / LPR;
+  constexpr int U = CPL >= 8 ? 1 : 8 / CPL;
+  constexpr int RT = G * U;
+  constexpr int DP = LPR * CPL * 8;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  const int g = lane / LPR, c = lane % LPR;
+  const int nch = (int)(ld / 8);
+  const float* y_lin = y + n_res;
+  const float* sw_lin = sw ? sw + n_res : nullptr;
+  float2_ s1[CPL][4], s2[CPL][4], syx[CPL][4];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s1[k][j] = s2[k][j] = syx[k][j] = float2_{0.f, 0.f};
+  float rsum[3] = {0.f, 0.f, 0.f};
+  const int64_t Tr = (n_res + RT - 1) / RT, Tl = (n_lin + RT - 1) / RT, S = Tr + Tl;
+  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
+  if (gw < S) {
+    int64_t L = gw * Tl / S, rem = gw * Tl - L * S;
+    const int64_t q0 = nw * Tl / S, r0 = nw * Tl - q0 * S;
+    for (int64_t s = gw; s < S; s += nw) {
+      if (rem + Tl >= S)
+        stats_tile<LPR, CPL, 1>(L * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, g, c, s1, s2, syx, rsum);
+      else
+        stats_tile<LPR, CPL, 0>((s - L) * RT, n_res, X, ld, nch, y, sw, seed, row0, g, c, s1, s2, syx, rsum);
+      rem += r0;
+      L += q0;
+      if (rem >= S) { rem -= S; ++L; }
+    }
+  }
+  // fold the G row groups of the wave, then the waves through LDS in a fixed order
+  __shared__ float red[kWavesPerBlock][3 * DP + 4];
+#pragma unroll
+  for (int k = 0; k < CPL; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float a = s1[k][j][h], b = s2[k][j][h], e = syx[k][j][h];
+#pragma unroll
+        for (int off = LPR; off < kWave; off <<= 1) {
+          a += __shfl_xor(a, off, kWave);
+          b += __shfl_xor(b, off, kWave);
+          e += __shfl_xor(e, off, kWave);
+        }
+        const int col = 8 * (c + k * LPR) + 2 * j + h;
+        if (lane < LPR) {
+          red[wid][col] = a;
+          red[wid][DP + col] = b;
+          red[wid][2 * DP + col] = e;
+        }
+      }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const float v = wave_sum(rsum[q]);
+    if (lane == 0) red[wid][3 * DP + q] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 3 * DP + 3; i += kBlock) {
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < kWavesPerBlock; ++q) s += red[q][i];
@@ -878,20 +1038,27 @@ __global__ __launch_bounds__(256) void glm_sgd_update_kernel(
 
 // Graph-capturable variant: the step counter lives on the device (t <- t + 1, eta =
 // step_size / sqrt(t), loss recorded at loss_hist[t - 1] while t <= cap), so a captured
-// step has no per-step host arguments and can be replayed from a HIP graph.
+// step has no per-step host arguments and can be replayed from a HIP graph.  An L1 term
+// (elastic net / mllib L1Updater) is applied as the proximal soft-threshold
+// bt <- sign(bt) max(|bt| - eta * l1, 0) after the gradient step.
 __global__ __launch_bounds__(256) void glm_sgd_update_dev_kernel(
     const double* __restrict__ out, int dpad, double* __restrict__ bt, double* __restrict__ b,
-    const double* __restrict__ inv_std, const double* __restrict__ l2v, double l2, double step_size,
-    int fit_intercept, float* __restrict__ coef_eff, double* __restrict__ loss_hist, int64_t cap,
-    int64_t* __restrict__ t_dev) {
+    const double* __restrict__ inv_std, const double* __restrict__ l2v, double l2, const double* __restrict__ l1v,
+    double l1, double step_size, int fit_intercept, float* __restrict__ coef_eff, double* __restrict__ loss_hist,
+    int64_t cap, int64_t* __restrict__ t_dev) {
   const int64_t t = t_dev[0] + 1;
   const double eta = step_size / sqrt((double)t);
   const double W = out[dpad + 2];
   const double invW = W > 0.0 ? 1.0 / W : 0.0;
+  const bool prox = l1v != nullptr || l1 > 0.0;
   for (int i = threadIdx.x; i < dpad; i += blockDim.x) {
     const double inv = inv_std[i];
     const double reg = l2v ? l2v[i] : l2;
-    const double v = bt[i] - eta * (out[i] * inv * invW + reg * bt[i]);
+    double v = bt[i] - eta * (out[i] * inv * invW + reg * bt[i]);
+    if (prox) {
+      const double sh = eta * (l1v ? l1v[i] : l1);
+      v = v > sh ? v - sh : (v < -sh ? v + sh : 0.0);
+    }
     bt[i] = v;
     coef_eff[i] = (float)(v * inv);
   }
@@ -1016,18 +1183,22 @@ O3S_API int o3s_glm_grad(int loss, int src, const void* X, int64_t ld, int64_t n
 template <int L, int C, int MW, int LW, int UR>
 static void launch_mixed(int loss, int grid, hipStream_t st, const uint16_t* X, int64_t ld, int64_t n_res,
                          const float* y, const float* sw, const float* coef, const float* b, uint32_t seed,
-                         int64_t row0, int64_t n_lin, float* partial, int pstride) {
+                         int64_t row0, int64_t n_lin, float* partial, int pstride, int64_t res_row0,
+                         const int64_t* t_dev, uint32_t sseed, uint32_t sthr) {
   constexpr int U = C >= 8 ? 1 : 8 / C;
   constexpr int UR2 = UR > 0 ? UR : U;
   if (loss == LOSS_LOGISTIC)
     hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_LOGISTIC, MW, LW, UR2>), dim3(grid), dim3(kBlock), 0,
-                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride);
+                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride, res_row0, t_dev,
+                       sseed, sthr);
   else if (loss == LOSS_HINGE)
     hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_HINGE, MW, LW, UR2>), dim3(grid), dim3(kBlock), 0,
-                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride);
+                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride, res_row0, t_dev,
+                       sseed, sthr);
   else
     hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_SQUARED, MW, LW, UR2>), dim3(grid), dim3(kBlock), 0,
-                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride);
+                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride, res_row0, t_dev,
+                       sseed, sthr);
 }
 
 // Mixed resident + lineage pass in one launch (see glm_grad_mixed_kernel): n_res rows
@@ -1036,11 +1207,14 @@ static void launch_mixed(int loss, int grid, hipStream_t st, const uint16_t* X, 
 // contract as o3s_glm_grad (out is overwritten).  waves: 3 asks the register allocator
 // for 3 waves/SIMD (see glm_grad_mixed_kernel), anything else 2.  mode: 0 = interleaved
 // roles; 1..3 = that many lineage waves per block (fixed roles); 10 + LW = fixed roles
-// with 4 resident rows in flight per lane.
+// with 4 resident rows in flight per lane.  Mini-batch sampling: res_row0 is the global
+// index of resident row 0, t_dev (may be null = iteration 1) the device step counter,
+// sthr = fraction * 2^24 (>= 2^24: no sampling), sseed the sampling seed.
 O3S_API int o3s_glm_grad_mixed(int loss, const void* X, int64_t ld, int64_t n_res, const float* y,
                                const float* sw, const float* coef, uint32_t seed, int64_t row0,
                                int64_t n_lin, float* partial, int grid, double* out, int waves,
-                               int mode, hipStream_t st) {
+                               int mode, int64_t res_row0, const int64_t* t_dev, uint32_t sseed,
+                               uint32_t sthr, hipStream_t st) {
   const int nch = (int)(ld / 8);
   const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
   if (ld % 8 != 0 || cpl > 16 || grid <= 0 || n_res < 0 || n_lin < 0) return -1;
@@ -1056,25 +1230,25 @@ O3S_API int o3s_glm_grad_mixed(int loss, const void* X, int64_t ld, int64_t n_re
     done = true;                                                                                      \
     if (mode == 0 && waves == 3)                                                                      \
       launch_mixed<L, C, 3, 0, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride);                                                 \
+                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
     else if (mode == 0)                                                                               \
       launch_mixed<L, C, 2, 0, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride);                                                 \
+                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
     else if (mode == 1)                                                                               \
       launch_mixed<L, C, 3, 1, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride);                                                 \
+                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
     else if (mode == 2)                                                                               \
       launch_mixed<L, C, 3, 2, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride);                                                 \
+                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
     else if (mode == 3)                                                                               \
       launch_mixed<L, C, 3, 3, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride);                                                 \
+                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
     else if (mode == 12)                                                                              \
       launch_mixed<L, C, 3, 2, 4>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride);                                                 \
+                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
     else if (mode == 11)                                                                              \
       launch_mixed<L, C, 3, 1, 4>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride);                                                 \
+                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
     else done = false;                                                                                \
   }
   O3S_MX(4, 1) O3S_MX(8, 1) O3S_MX(4, 4) O3S_MX(8, 4) O3S_MX(16, 4) O3S_MX(32, 4)
@@ -1176,11 +1350,44 @@ O3S_API int o3s_glm_sgd_update(const double* out, int dpad, double* bt, double* 
 }
 
 O3S_API int o3s_glm_sgd_update_dev(const double* out, int dpad, double* bt, double* b, const double* inv_std,
-                                   const double* l2v, double l2, double step_size, int fit_intercept,
-                                   float* coef_eff, double* loss_hist, int64_t cap, int64_t* t_dev,
-                                   hipStream_t st) {
+                                   const double* l2v, double l2, const double* l1v, double l1, double step_size,
+                                   int fit_intercept, float* coef_eff, double* loss_hist, int64_t cap,
+                                   int64_t* t_dev, hipStream_t st) {
   hipLaunchKernelGGL(glm_sgd_update_dev_kernel, dim3(1), dim3(256), 0, st, out, dpad, bt, b, inv_std, l2v, l2,
-                     step_size, fit_intercept, coef_eff, loss_hist, cap, t_dev);
+                     l1v, l1, step_size, fit_intercept, coef_eff, loss_hist, cap, t_dev);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+// Fused summarizer + first-gradient pass (glm_stats_mixed_kernel): out (fp64, 3*dpad+3) =
+// [s1 | s2 | syx | sum w | sum w y | sum w y^2]; partial holds grid * (3*dpad+4) floats.
+// Returns -2 when the row layout has no stats instantiation (ld > 2048): the caller then
+// uses o3s_glm_colstats plus a regular first pass.
+O3S_API int o3s_glm_stats_mixed(const void* X, int64_t ld, int64_t n_res, const float* y, const float* sw,
+                                uint32_t seed, int64_t row0, int64_t n_lin, float* partial, int grid, double* out,
+                                hipStream_t st) {
+  const int nch = (int)(ld / 8);
+  const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
+  if (ld % 8 != 0 || cpl > 16 || grid <= 0 || n_res < 0 || n_lin < 0) return -1;
+  const int dpad = lpr * cpl * 8, pstride = 3 * dpad + 4;
+  int lpr_s = lpr, cpl_s = cpl;
+  if (cpl == 1 && lpr >= 16) { lpr_s = lpr / 4; cpl_s = 4; }
+  else if (cpl == 2) { lpr_s = 32; cpl_s = 4; }
+  const uint16_t* Xh = (const uint16_t*)X;
+  bool done = false;
+#define O3S_ST(L, C)                                                                                        \
+  if (!done && lpr_s == L && cpl_s == C) {                                                                  \
+    done = true;                                                                                            \
+    hipLaunchKernelGGL((glm_stats_mixed_kernel<L, C>), dim3(grid), dim3(kBlock), 0, st, Xh, ld, n_res, y, sw, \
+                       seed, row0, n_lin, partial, pstride);                                                \
+  }
+  O3S_ST(4, 1) O3S_ST(8, 1) O3S_ST(4, 4) O3S_ST(8, 4) O3S_ST(16, 4) O3S_ST(32, 4) O3S_ST(64, 4)
+#undef O3S_ST
+  if (!done) return -2;
+  O3S_CHECK_LAUNCH();
+  const int ncols = 3 * dpad + 3;
+  hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 31) / 32), dim3(1024), 0, st, partial, grid, pstride, ncols,
+                     out, 0);
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -239,29 +239,108 @@ MIX_WAVES = int(os.environ.get("O3S_GLM_MIX_WAVES", "3"))
 MIX_MODE = int(os.environ.get("O3S_GLM_MIX_MODE", "0"))
 
 
+def sample_threshold(fraction: float) -> int:
+    """miniBatchFraction -> the kernels' 24-bit keep threshold (>= 2^24: keep every row)."""
+    f = float(fraction)
+    if not 0.0 < f <= 1.0:
+        raise ValueError(f"miniBatchFraction must be in (0, 1], got {fraction}")
+    return 1 << 24 if f >= 1.0 else max(1, int(round(f * (1 << 24))))
+
+
+def sample_key(seed: int, it: int) -> int:
+    """Torch/host twin of csrc/glm.hip ``sample_key`` (per-iteration sampling key)."""
+    t = torch.tensor([(int(it) * 0x9E3779B1 + 0x7F4A7C15) & _MASK], dtype=torch.int64)
+    return int(_fmix32((int(seed) & _MASK) ^ _fmix32(t))[0])
+
+
+def sample_mask(seed: int, it: int, grows: torch.Tensor, fraction: float) -> torch.Tensor:
+    """Rows kept by iteration ``it``'s mini-batch (bool per global row index): the same
+    draw as the GLM kernels' ``RowSampler``, so CPU and GPU paths select identical sets."""
+    thr = sample_threshold(fraction)
+    if thr >= 1 << 24:
+        return torch.ones(grows.shape[0], dtype=torch.bool, device=grows.device)
+    return (row_keys(sample_key(seed, it), grows.to(torch.int64)) >> 8) < thr
+
+
 def glm_grad_mixed(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, n_lin: int, d: int,
                    seed: int, row0: int, coef: torch.Tensor, intercept: float | None, loss: int,
-                   ws: GlmWorkspace) -> torch.Tensor:
+                   ws: GlmWorkspace, res_row0: int = 0, t_dev: torch.Tensor | None = None,
+                   sample_seed: int = 0, fraction: float = 1.0) -> torch.Tensor:
     """Resident rows of ``X`` plus ``n_lin`` lineage rows (global rows ``row0..``) in ONE
     launch (csrc/glm.hip ``glm_grad_mixed_kernel``): memory-bound and VALU-bound tiles
     are interleaved inside every wave so both resources stay busy.  ``y``/``sw`` are the
     materialised label/weight columns of all ``X.shape[0] + n_lin`` rows.  Overwrites
-    ``ws.out``."""
+    ``ws.out``.
+
+    ``fraction < 1`` keeps each row with that probability (mini-batch SGD), keyed on
+    (``sample_seed``, iteration ``t_dev[0] + 1`` -- 1 when ``t_dev`` is None, global row:
+    ``res_row0 + i`` for resident row i, ``row0 + j`` for lineage row j)."""
     ld = X.shape[1]
     nr = X.shape[0]
     if y.shape[0] != nr + n_lin or (sw is not None and sw.shape[0] != nr + n_lin):
         raise ValueError("label / weight columns must cover the resident and lineage rows")
+    thr = sample_threshold(fraction)
     if ws.device.type != "cuda":
         Xl, _ = synth_glm(n_lin, d, seed, row0, "cpu", ld, torch.zeros(ld), 0.0)
-        return glm_grad(torch.cat([X, Xl]), y, sw, coef, intercept, loss)
+        w = sw
+        if thr < 1 << 24:
+            it = int(t_dev[0]) + 1 if t_dev is not None else 1
+            grows = torch.cat([torch.arange(res_row0, res_row0 + nr), torch.arange(row0, row0 + n_lin)])
+            keep = sample_mask(sample_seed, it, grows, fraction).to(torch.float64)
+            w = keep if sw is None else sw.to(torch.float64) * keep
+        return glm_grad(torch.cat([X, Xl]), y, w, coef, intercept, loss)
     if X.dtype != torch.bfloat16 or not X.is_contiguous() or not y.is_contiguous():
         raise TypeError("GPU GLM pass expects a contiguous bf16 feature matrix")
     cf = _coef_buf(coef, ws.dpad, ws.device, intercept=intercept)
     N.check(N.kernels().o3s_glm_grad_mixed(loss, X.data_ptr(), ld, nr, y.data_ptr(), N.ptr(sw),
                                            cf.data_ptr(), seed & _MASK, row0, n_lin, ws.partial.data_ptr(),
-                                           ws.grid, ws.out.data_ptr(), MIX_WAVES, MIX_MODE, N.stream_of(X)),
+                                           ws.grid, ws.out.data_ptr(), MIX_WAVES, MIX_MODE, int(res_row0),
+                                           N.ptr(t_dev), int(sample_seed) & _MASK, thr, N.stream_of(X)),
             "glm_grad_mixed")
     return ws.out
+
+
+def glm_stats_mixed(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, n_lin: int, d: int,
+                    seed: int, row0: int, grid: int | None = None) -> torch.Tensor | None:
+    """Summarizer pass fused with the first gradient (csrc/glm.hip ``glm_stats_mixed_kernel``)
+    over the resident rows of ``X`` and ``n_lin`` lineage rows: fp64 [s1 (dpad) | s2 (dpad) |
+    syx (dpad) | sum w | sum w y | sum w y^2] with s1 = sum w x, s2 = sum w x^2, syx =
+    sum w y x.  Returns None when the layout has no fused instantiation (ld > 2048)."""
+    ld = X.shape[1]
+    nr = X.shape[0]
+    dpad, _ = layout(ld)
+    if y.shape[0] != nr + n_lin or (sw is not None and sw.shape[0] != nr + n_lin):
+        raise ValueError("label / weight columns must cover the resident and lineage rows")
+    if X.device.type != "cuda":
+        return glm_stats_torch(X, y, sw, n_lin, d, seed, row0)
+    grid = grid or N.num_cus(X.device) * 8
+    pstride = 3 * dpad + 4
+    partial = torch.empty(grid * pstride, dtype=torch.float32, device=X.device)
+    out = torch.empty(3 * dpad + 3, dtype=torch.float64, device=X.device)
+    rc = N.kernels().o3s_glm_stats_mixed(X.data_ptr(), ld, nr, y.data_ptr(), N.ptr(sw), seed & _MASK, row0,
+                                         n_lin, partial.data_ptr(), grid, out.data_ptr(), N.stream_of(X))
+    if rc == -2:
+        return None
+    N.check(rc, "glm_stats_mixed")
+    return out
+
+
+def glm_stats_torch(X, y, sw, n_lin=0, d=None, seed=0, row0=0) -> torch.Tensor:
+    """fp64 reference of :func:`glm_stats_mixed`."""
+    ld = X.shape[1]
+    dpad, _ = layout(ld)
+    if n_lin:
+        Xl, _ = synth_glm(n_lin, d or ld, seed, row0, "cpu", ld, torch.zeros(ld), 0.0)
+        X = torch.cat([X.cpu(), Xl])
+    Xd = X.to(torch.float64).cpu()
+    yd = y.to(torch.float64).cpu()
+    w = torch.ones_like(yd) if sw is None else sw.to(torch.float64).cpu()
+    out = torch.zeros(3 * dpad + 3, dtype=torch.float64)
+    out[:ld] = w @ Xd
+    out[dpad:dpad + ld] = w @ (Xd * Xd)
+    out[2 * dpad:2 * dpad + ld] = (w * yd) @ Xd
+    out[3 * dpad:] = torch.stack([w.sum(), (w * yd).sum(), (w * yd * yd).sum()])
+    return out
 
 
 _COEF_CACHE: dict = {}

@@ -8,7 +8,7 @@ import numpy as np
 from ..frame import column as C
 from ..frame import expr as E
 from ..frame.dataframe import DataFrame
-from .parser import AggCall, Select, _AggExpr, _as_agg_expr, parse
+from .parser import AggCall, Select, SetOp, _AggExpr, _as_agg_expr, parse
 
 
 def _strings_df(session, data: dict) -> DataFrame:
@@ -131,6 +131,10 @@ def _explain(stmt, text: str) -> str:
     if stmt[0] != "select":
         return f"== Physical Plan ==\nExecute {stmt[0].upper()}: {text}"
     s = stmt[1]
+    if isinstance(s, SetOp):
+        return (f"== Physical Plan ==\n{s.op.capitalize()}{' All' if s.all else ''} (left: "
+                + _explain(("select", s.left), text).splitlines()[1] + ", right: "
+                + _explain(("select", s.right), text).splitlines()[1] + ")")
     steps = []
     if s.ctes:
         steps.append("WithCTE " + ", ".join(n for n, _ in s.ctes))
@@ -153,8 +157,6 @@ def _explain(stmt, text: str) -> str:
                                           for it in s.items))
     if s.limit is not None:
         steps.append(f"Limit {s.limit}")
-    if s.union is not None:
-        steps.append(f"{s.setop.capitalize()}{' All' if s.union_all else ''} (second query)")
     return "== Physical Plan ==\n" + "\n".join(("+- " if i else "") + st for i, st in enumerate(steps))
 
 
@@ -194,9 +196,11 @@ def _values_frame(session, rows, names=None) -> DataFrame:
     return session.createDataFrame([tuple(r) for r in rows], names)
 
 
-def run_select(session, s: Select) -> DataFrame:
+def run_select(session, s) -> DataFrame:
     if s.ctes:
         return _with_ctes(session, s)
+    if isinstance(s, SetOp):
+        return _run_setop(session, s)
     if s.values is not None:
         df = _values_frame(session, s.values, s.value_names)
     elif s.subquery is not None:
@@ -267,19 +271,31 @@ def run_select(session, s: Select) -> DataFrame:
         df = df.offset(s.offset)
     if s.limit is not None:
         df = df.limit(s.limit)
-    if s.union is not None:
-        other = run_select(session, s.union)
-        if len(other.columns) != len(df.columns):
-            raise ValueError(f"{s.setop.upper()} needs the same number of columns on both sides")
-        other = other.toDF(*df.columns)                 # set operations match columns by position
-        if s.setop == "intersect":
-            df = df.intersectAll(other) if s.union_all else df.intersect(other)
-        elif s.setop == "except":
-            df = df.exceptAll(other) if s.union_all else df.subtract(other)
-        else:
-            df = df.union(other)
-            if not s.union_all:
-                df = df.distinct()
+    return df
+
+
+def _run_setop(session, s: SetOp) -> DataFrame:
+    """Left-associative set operation (columns matched by position, named by the left
+    side); a trailing ORDER BY / LIMIT / OFFSET applies to the combined rows."""
+    df = run_select(session, s.left)
+    other = run_select(session, s.right)
+    if len(other.columns) != len(df.columns):
+        raise ValueError(f"{s.op.upper()} needs the same number of columns on both sides")
+    other = other.toDF(*df.columns)
+    if s.op == "intersect":
+        df = df.intersectAll(other) if s.all else df.intersect(other)
+    elif s.op == "except":
+        df = df.exceptAll(other) if s.all else df.subtract(other)
+    else:
+        df = df.union(other)
+        if not s.all:
+            df = df.distinct()
+    if s.order_by:
+        df = df.orderBy(*[e for e, _ in s.order_by], ascending=[a for _, a in s.order_by])
+    if s.offset is not None:
+        df = df.offset(s.offset)
+    if s.limit is not None:
+        df = df.limit(s.limit)
     return df
 
 

@@ -155,15 +155,29 @@ class Select:
     grouping: str | None = None          # "rollup" | "cube" | "sets"
     grouping_sets: list | None = None    # index tuples into group_by (GROUPING SETS)
     distinct: bool = False
-    union: object = None
-    union_all: bool = False
-    setop: str = "union"                 # union | intersect | except (with ``union`` = right side)
     ctes: list = field(default_factory=list)        # WITH name AS (select), ...
     values: list | None = None           # FROM VALUES (..), (..) [AS t(a, b)]
     value_names: list | None = None
     laterals: list = field(default_factory=list)    # LATERAL VIEW [OUTER] gen(..) t AS c
     sample: tuple | None = None          # TABLESAMPLE (x PERCENT | n ROWS)
     pivot: tuple | None = None           # PIVOT (aggs FOR col IN (values))
+
+
+@dataclass
+class SetOp:
+    """``left {UNION|INTERSECT|EXCEPT} [ALL] right`` -- a node of a query expression.
+
+    Chains are left-associative and INTERSECT binds tighter than UNION / EXCEPT (SQL
+    standard, Spark's grammar); a trailing ORDER BY / LIMIT / OFFSET after the last branch
+    applies to the combined result."""
+    op: str                              # union | intersect | except
+    all: bool
+    left: object                         # Select | SetOp
+    right: object
+    order_by: list = field(default_factory=list)
+    limit: int | None = None
+    offset: int | None = None
+    ctes: list = field(default_factory=list)
 
 
 class Parser:
@@ -369,7 +383,55 @@ class Parser:
             raise SyntaxError(f"unexpected trailing input: {self.peek().val!r}")
         return ("select", sel)
 
-    def select(self) -> Select:
+    def select(self):
+        """query := term ((UNION | EXCEPT | MINUS) [ALL | DISTINCT] term)* [ORDER BY / LIMIT / OFFSET]
+        term := primary (INTERSECT [ALL | DISTINCT] primary)*
+        primary := SELECT ... | '(' query ')'"""
+        node = self._set_term()
+        while True:
+            if self.kw("union"):
+                op = "union"
+            elif self.idw("except") or self.idw("minus"):
+                op = "except"
+            else:
+                break
+            is_all = bool(self.kw("all"))
+            if not is_all:
+                self.kw("distinct")
+            node = SetOp(op, is_all, node, self._set_term())
+        if isinstance(node, SetOp):
+            self._lift_tail(node)
+        return node
+
+    def _set_term(self):
+        node = self._set_primary()
+        while self.idw("intersect"):
+            is_all = bool(self.kw("all"))
+            if not is_all:
+                self.kw("distinct")
+            node = SetOp("intersect", is_all, node, self._set_primary())
+        return node
+
+    def _set_primary(self):
+        if self.peek().kind == "op" and self.peek().val == "(" and self.peek(1).val == "select":
+            self.next()
+            q = self.select()
+            self.expect("op", ")")
+            return q
+        return self._select_core()
+
+    @staticmethod
+    def _lift_tail(node: "SetOp") -> None:
+        """ORDER BY / LIMIT / OFFSET parsed with the rightmost SELECT belong to the whole
+        set operation (a branch needs parentheses to own them)."""
+        last = node
+        while isinstance(last, SetOp):
+            last = last.right
+        if isinstance(last, Select) and (last.order_by or last.limit is not None or last.offset is not None):
+            node.order_by, node.limit, node.offset = last.order_by, last.limit, last.offset
+            last.order_by, last.limit, last.offset = [], None, None
+
+    def _select_core(self) -> Select:
         self.expect("kw", "select")
         distinct = bool(self.kw("distinct"))
         items = [self.select_item()]
@@ -493,16 +555,6 @@ class Parser:
             s.limit = int(float(self.expect("num").val))
         if self.idw("offset"):
             s.offset = int(float(self.expect("num").val))
-        if self.kw("union"):
-            s.union_all = bool(self.kw("all"))
-            self.kw("distinct")
-            s.union = self.select()
-        elif self.idw("intersect") or self.idw("except") or self.idw("minus"):
-            op = self.toks[self.i - 1].val.lower()
-            s.setop = "intersect" if op == "intersect" else "except"
-            s.union_all = bool(self.kw("all"))
-            self.kw("distinct")
-            s.union = self.select()
         return s
 
     def _values_rows(self) -> list:

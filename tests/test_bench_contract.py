@@ -51,6 +51,24 @@ def test_bench_single_and_four_ranks_agree():
     assert r4["n_gpus"] == 4 and r4["config"]["parallelism"] == "dp4" and r4["config"]["global_batch"] == 24000
     assert abs(r4["first_loss"] - r1["first_loss"]) < 1e-9
     assert abs(r4["final_loss"] - r1["final_loss"]) < 1e-7 * abs(r1["final_loss"])
+    assert r1["hbm_only_rows_per_s"] > 0 and 0 <= r1["fit_setup_share"] <= 1
+
+
+@pytest.mark.timeout(300)
+def test_bench_self_launches_n_ranks():
+    """The plain driver command ``python bench.py --gpus 4`` (no launcher around it)
+    starts 4 ranks itself and reports n_gpus 4 with the 1-rank losses."""
+    args = ["--steps", "2", "--warmup", "1", "--rows", "16000", "--features", "16", "--no-hbm-only"]
+    one = subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                         timeout=240)
+    assert one.returncode == 0, one.stderr[-2000:]
+    r1 = _json_line(one.stdout)
+    four = subprocess.run([sys.executable, "bench.py", "--gpus", "4", *args], cwd=ROOT, env=_env(),
+                          capture_output=True, text=True, timeout=240)
+    assert four.returncode == 0, four.stderr[-3000:]
+    r4 = _json_line(four.stdout)
+    assert r4["n_gpus"] == 4 and r4["config"]["parallelism"] == "dp4"
+    assert abs(r4["final_loss"] - r1["final_loss"]) < 1e-7 * abs(r1["final_loss"])
 
 
 @pytest.mark.gpu

@@ -207,3 +207,31 @@ def test_gpu_condition_join_matches_oracle(how):
     for case in CASES:
         cond, pred = CASES[case]
         assert _rows(a.join(b, cond(a, b), how)) == _oracle(pa, pb, pred, how), case
+
+
+def test_self_join_with_shared_column_objects(s):
+    """``df.join(df.withColumn(..), df.id == df2.id)`` and ``x.id == y.id`` after alias: the
+    frames share column objects, but each reference names the frame it was taken from, so
+    the equality is a join key (not a trivially-true residual -> cross product)."""
+    pa = pd.DataFrame({"id": [1.0, 2.0, 3.0, 2.0], "t": [0.1, 0.2, 0.3, 0.4]})
+    df = s.createDataFrame(pa)
+    df2 = df.withColumn("z", F.col("t") * 2)
+    out = df.join(df2, df.id == df2.id)
+    want = sum(1 for i in pa.id for j in pa.id if i == j)
+    assert out.count() == want == 6
+    x, y = df.alias("x"), df.alias("y")
+    assert x.join(y, x.id == y.id).count() == 6
+    r = x.join(y, (x.id == y.id) & (x.t < y.t)).collect()
+    assert len(r) == 1
+    # residual predicates also take the side from the frame the reference came from
+    assert df.join(df2, (df.id == df2.id) & (df2.z > 0.5)).count() == sum(
+        1 for i, _ in pa.itertuples(index=False, name=None) for j, tj in pa.itertuples(index=False, name=None)
+        if i == j and tj * 2 > 0.5)
+
+
+def test_self_join_unresolvable_equality_raises(s):
+    pa = pd.DataFrame({"id": [1.0, 2.0], "t": [0.1, 0.2]})
+    df = s.createDataFrame(pa)
+    other = df.select("t", F.col("id").alias("id2"))
+    with pytest.raises((ValueError, KeyError)):
+        df.join(other, F.col("id") == F.col("id")).count()

@@ -184,3 +184,77 @@ def test_gpu_multinomial_fit_kernel_matches_chunked(gpu, monkeypatch):
     B0, b0, r0 = GLM.fit_multinomial(comm, X, y, None, K, reg=0.01, max_iter=50)
     assert abs(r1.f - r0.f) <= 1e-6 * abs(r0.f)
     assert abs(B1 - B0).max() < 1e-3 and abs(b1 - b0).max() < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,weighted", [(256, False), (256, True), (20, False), (100, True), (600, False),
+                                        (2048, False)])
+def test_gpu_stats_mixed_matches_fp64(gpu, d, weighted):
+    """Fused summarizer + first-gradient pass (glm_stats_mixed_kernel) vs fp64 torch over
+    the materialised resident + lineage rows."""
+    n_res, n_lin, seed = 30011, 20007, 17
+    ld = G.padded_width(d)
+    wt, bt = G.synth_truth(seed, d, ld)
+    Xr, yr = G.synth_glm(n_res, d, seed + 1, device=gpu, ld=ld)
+    Xl, yl = G.synth_glm(n_lin, d, seed, row0=n_res, device=gpu, ld=ld, wtrue=wt, btrue=bt)
+    yall = torch.cat([yr, yl])
+    sw = (torch.rand(n_res + n_lin, generator=torch.Generator().manual_seed(3)) + 0.5).to(gpu) if weighted else None
+    out = G.glm_stats_mixed(Xr, yall, sw, n_lin, d, seed, n_res)
+    assert out is not None
+    out = out.cpu()
+    ref = G.glm_stats_torch(torch.cat([Xr, Xl]).cpu(), yall.cpu(), None if sw is None else sw.cpu())
+    dpad, _ = G.layout(ld)
+    for k in range(3):
+        a, b = out[k * dpad:k * dpad + ld], ref[k * dpad:k * dpad + ld]
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-5 * (1 + b.abs().max().item())), (k, (a - b).abs().max())
+    assert torch.allclose(out[3 * dpad:], ref[3 * dpad:], rtol=1e-6)
+    again = G.glm_stats_mixed(Xr, yall, sw, n_lin, d, seed, n_res).cpu()
+    assert torch.equal(out, again)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frac", [0.3, 0.05])
+def test_gpu_grad_mixed_minibatch_matches_cpu_mask(gpu, frac):
+    """In-kernel Bernoulli row mask == the torch twin's mask (same rows kept): the sampled
+    pass equals the fp64 pass with the mask as row weights, for resident and lineage rows,
+    and the iteration key comes from the device step counter."""
+    n_res, n_lin, d, seed = 40009, 20011, 256, 23
+    Xr, yr = G.synth_glm(n_res, d, seed + 1, device=gpu)
+    Xl, yl = G.synth_glm(n_lin, d, seed, row0=5_000_000 + n_res, device=gpu)
+    yall = torch.cat([yr, yl])
+    coef = torch.randn(d, generator=torch.Generator().manual_seed(2)).to(gpu) * 0.05
+    ws = G.GlmWorkspace(gpu, d, grid=512)
+    t_dev = torch.tensor([4], dtype=torch.int64, device=gpu)          # iteration 5
+    out = G.glm_grad_mixed(Xr, yall, None, n_lin, d, seed, 5_000_000 + n_res, coef, 0.1, 0, ws,
+                           res_row0=5_000_000, t_dev=t_dev, sample_seed=99, fraction=frac).clone().cpu()
+    grows = torch.arange(5_000_000, 5_000_000 + n_res + n_lin)
+    keep = G.sample_mask(99, 5, grows, frac).double()
+    ref = G.glm_grad_torch(torch.cat([Xr, Xl]).cpu(), yall.cpu(), keep, coef.double().cpu(), 0.1, 0)
+    assert abs(out[d + 2].item() - keep.sum().item()) < 0.5           # identical kept set
+    assert torch.allclose(out[:d], ref[:d], rtol=1e-3, atol=0.05)
+    assert torch.allclose(out[d:], ref[d:], rtol=1e-3, atol=0.5)
+
+
+@pytest.mark.gpu
+def test_gpu_sgd_fit_matches_cpu(gpu):
+    """LogisticRegression(solver='sgd').fit on the GPU (fused stats pass, graph-replayed
+    steps, mini-batches) == the CPU fp64 path on the same bf16 rows."""
+    import numpy as np
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.frame import column as Cc
+    from orange3_spark_amd.frame.dataframe import DataFrame
+    from orange3_spark_amd.ml.classification import LogisticRegression
+    from collections import OrderedDict
+    X, y = G.synth_glm(60_000, 64, seed=31, device=gpu)
+    sg = Session(SessionConf().setAppName("g"), device=gpu)
+    sc = Session(SessionConf().set("o3s.device", "cpu"))
+    dg = DataFrame(sg, OrderedDict(features=Cc.VectorColumn(X, 64), label=Cc.NumericColumn(y)), X.shape[0])
+    dc = DataFrame(sc, OrderedDict(features=Cc.VectorColumn(X.cpu().double(), 64),
+                                   label=Cc.NumericColumn(y.cpu().double())), X.shape[0])
+    for frac in (1.0, 0.2):
+        kw = dict(solver="sgd", maxIter=12, tol=0.0, miniBatchFraction=frac, seed=5, regParam=0.01)
+        a = LogisticRegression(**kw).fit(dg)
+        b = LogisticRegression(**kw).fit(dc)
+        assert np.allclose(a.coefficients.toArray(), b.coefficients.toArray(), rtol=2e-3, atol=2e-4)
+        assert abs(a.intercept - b.intercept) < 2e-4
+        assert a.summary.totalIterations == 12

@@ -79,7 +79,7 @@ def test_sgd_graph_replay_equals_eager(monkeypatch, resident_fraction):
         return t, t.result()
     te, eager = run("0")
     tg, graph = run("1")
-    assert te._graph is None and tg._graph is not None
+    assert te._graphs is None and tg._graphs is not None
     assert eager.history == graph.history and len(graph.history) == 12
     assert np.array_equal(eager.coef, graph.coef) and eager.intercept == graph.intercept
     # the replay is cheaper per step than the eager launch sequence on a small problem

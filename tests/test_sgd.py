@@ -1,0 +1,177 @@
+"""``solver='sgd'`` (mllib GradientDescent semantics) through ``LogisticRegression.fit``:
+fused summarizer + first step, per-iteration Bernoulli mini-batches keyed on
+(seed, iteration, global row), L2 / L1 updaters, and sharding independence (gloo world 2).
+The oracle is a plain fp64 numpy implementation of the same iteration."""
+import math
+import os
+import socket
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from orange3_spark_amd import Session, SessionConf
+from orange3_spark_amd.ml.classification import LinearSVC, LogisticRegression
+from orange3_spark_amd.ml.feature import VectorAssembler
+from orange3_spark_amd.ops import glm as G
+
+
+@pytest.fixture(scope="module")
+def session():
+    return Session(SessionConf().set("o3s.device", "cpu"))
+
+
+def _table(n=800, d=6, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, d)) * rng.uniform(0.5, 3, size=d) + rng.normal(size=d)
+    w = rng.normal(size=d)
+    y = (rng.uniform(size=n) < 1 / (1 + np.exp(-(X @ w * 0.4 - 0.2)))).astype(float)
+    pdf = pd.DataFrame(X, columns=[f"f{i}" for i in range(d)])
+    pdf["label"] = y
+    return pdf, X, y
+
+
+def _df(session, pdf):
+    cols = [c for c in pdf.columns if c != "label"]
+    return VectorAssembler(inputCols=cols, outputCol="features").transform(session.createDataFrame(pdf))
+
+
+def _reference(X, y, iters, step, reg=0.0, alpha=0.0, frac=1.0, seed=0, loss="logistic"):
+    """mllib-style GD on standardised coefficients (fp64 numpy)."""
+    n, d = X.shape
+    W = float(n)
+    mean = X.mean(0)
+    std = np.sqrt(np.maximum(((X * X).sum(0) - W * mean ** 2) / (W - 1), 0))
+    inv = np.where(std > 0, 1 / np.where(std > 0, std, 1), 0)
+    ym = y.mean()
+    b = math.log(ym / (1 - ym)) if loss == "logistic" else 0.0
+    bt = np.zeros(d)
+    l2, l1 = reg * (1 - alpha), reg * alpha
+    for t in range(1, iters + 1):
+        keep = G.sample_mask(seed, t, torch.arange(n), frac).numpy().astype(float)
+        m = X @ (bt * inv) + b
+        if loss == "logistic":
+            r = (1 / (1 + np.exp(-m)) - y) * keep
+        else:
+            s = 2 * y - 1
+            r = np.where(1 - s * m > 0, -s, 0.0) * keep
+        Wt = keep.sum()
+        eta = step / math.sqrt(t)
+        g = (X.T @ r) * inv / Wt + l2 * bt
+        v = bt - eta * g
+        if l1 > 0:
+            v = np.sign(v) * np.maximum(np.abs(v) - eta * l1, 0)
+        bt = v
+        b -= eta * r.sum() / Wt
+    return bt * inv, b
+
+
+def test_sgd_fit_matches_reference(session):
+    pdf, X, y = _table()
+    m = LogisticRegression(solver="sgd", maxIter=15, stepSize=0.8, tol=0.0).fit(_df(session, pdf))
+    coef, b = _reference(X, y, 15, 0.8)
+    assert np.allclose(m.coefficients.toArray(), coef, rtol=2e-6, atol=1e-9)
+    assert m.intercept == pytest.approx(b, rel=2e-6)
+    assert m.summary.totalIterations == 15
+    # the summarizer pass is fused with iteration 1: 15 passes in total, not 16
+    assert len(m.summary.objectiveHistory) == 15
+
+
+def test_sgd_fused_first_step_equals_trainer(session):
+    pdf, X, y = _table(seed=4)
+    df = _df(session, pdf)
+    t = LogisticRegression(solver="sgd", stepSize=0.5, fitIntercept=False).trainer(df)
+    for _ in range(6):
+        t.step()
+    m = LogisticRegression(solver="sgd", stepSize=0.5, fitIntercept=False, maxIter=6, tol=0.0).fit(df)
+    assert np.allclose(m.coefficients.toArray(), t.result().coef, rtol=1e-10, atol=1e-13)
+
+
+def test_minibatch_fraction_is_honoured_and_deterministic(session):
+    pdf, X, y = _table(seed=1)
+    df = _df(session, pdf)
+    full = LogisticRegression(solver="sgd", maxIter=8, tol=0.0).fit(df).coefficients.toArray()
+    a = LogisticRegression(solver="sgd", maxIter=8, tol=0.0, miniBatchFraction=0.1, seed=3).fit(df)
+    b = LogisticRegression(solver="sgd", maxIter=8, tol=0.0, miniBatchFraction=0.1, seed=3).fit(df)
+    c = LogisticRegression(solver="sgd", maxIter=8, tol=0.0, miniBatchFraction=0.1, seed=4).fit(df)
+    a, b, c = (m.coefficients.toArray() for m in (a, b, c))
+    assert np.array_equal(a, b)
+    assert not np.allclose(a, full, atol=1e-6) and not np.allclose(a, c, atol=1e-6)
+    ref, _ = _reference(X, y, 8, 1.0, frac=0.1, seed=3)
+    assert np.allclose(a, ref, rtol=2e-6, atol=1e-9)
+
+
+def test_sample_mask_rate_and_iteration_keys():
+    rows = torch.arange(200_000)
+    m1 = G.sample_mask(7, 1, rows, 0.25)
+    m2 = G.sample_mask(7, 2, rows, 0.25)
+    assert abs(m1.float().mean().item() - 0.25) < 0.01
+    assert (m1 != m2).float().mean().item() > 0.3          # iterations draw fresh samples
+    assert G.sample_mask(7, 1, rows, 1.0).all()
+    with pytest.raises(ValueError):
+        G.sample_threshold(0.0)
+
+
+def test_sgd_elastic_net_l1_sparsity(session):
+    pdf, X, y = _table(seed=2, d=10)
+    m = LogisticRegression(solver="sgd", maxIter=40, regParam=0.2, elasticNetParam=1.0, tol=0.0).fit(
+        _df(session, pdf))
+    coef, _ = _reference(X, y, 40, 1.0, reg=0.2, alpha=1.0)
+    got = m.coefficients.toArray()
+    assert np.sum(got == 0) >= 2
+    assert np.allclose(got, coef, rtol=2e-6, atol=1e-9)
+
+
+def test_linearsvc_sgd(session):
+    pdf, X, y = _table(seed=5)
+    m = LinearSVC(solver="sgd", maxIter=10, tol=0.0).fit(_df(session, pdf))
+    coef, b = _reference(X, y, 10, 1.0, loss="hinge")
+    assert np.allclose(m.coefficients.toArray(), coef, rtol=2e-6, atol=1e-9)
+    assert m.intercept == pytest.approx(b, rel=2e-6, abs=1e-9)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _work(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    conf = SessionConf().set("o3s.device", "cpu").set("spark.master", "spmd" if world > 1 else "local")
+    s = Session(conf)
+    pdf, _, _ = _table(n=1001, seed=9)
+    df = _df(s, pdf)
+    res = {}
+    for frac in (1.0, 0.1):
+        m = LogisticRegression(solver="sgd", maxIter=7, tol=0.0, miniBatchFraction=frac, seed=11).fit(df)
+        res[frac] = np.concatenate([m.coefficients.toArray(), [m.intercept]])
+    if rank == 0:
+        torch.save(res, os.path.join(out_dir, f"sgd{world}.pt"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_minibatch_independent_of_sharding(tmp_path):
+    _work(0, 1, _free_port(), str(tmp_path))
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_work, args=(r, 2, port, str(tmp_path))) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    a = torch.load(tmp_path / "sgd1.pt", weights_only=False)
+    b = torch.load(tmp_path / "sgd2.pt", weights_only=False)
+    assert np.allclose(a[1.0], b[1.0], rtol=1e-10, atol=1e-13)
+    assert np.allclose(a[0.1], b[0.1], rtol=1e-10, atol=1e-13)
+    assert not np.allclose(a[0.1], a[1.0], atol=1e-6)

@@ -214,3 +214,36 @@ def test_union_distinct(s):
     got = _rows(s.sql("SELECT k FROM t UNION DISTINCT SELECT k FROM t"))
     assert got == sorted((k,) for k in set(t.k))
     assert s.sql("SELECT k FROM t UNION ALL SELECT k FROM t").count() == 2 * len(t)
+
+
+def test_set_operation_chains_are_left_associative(s):
+    """A EXCEPT B EXCEPT C == (A EXCEPT B) EXCEPT C; mixed chains evaluate left to right;
+    INTERSECT binds tighter; a trailing ORDER BY / LIMIT applies to the combined result
+    (pandas/python-set oracle)."""
+    import pandas as pd
+    s.createDataFrame(pd.DataFrame({"x": [1, 2, 3, 3]})).createOrReplaceTempView("sa")
+    s.createDataFrame(pd.DataFrame({"x": [1, 2]})).createOrReplaceTempView("sb")
+    s.createDataFrame(pd.DataFrame({"x": [1, 4]})).createOrReplaceTempView("sc")
+
+    def xs(q):
+        return sorted(r.x for r in s.sql(q).collect())
+    assert xs("SELECT x FROM sa EXCEPT SELECT x FROM sb EXCEPT SELECT x FROM sc") == [3]
+    assert xs("SELECT x FROM sa MINUS SELECT x FROM sc") == [2, 3]
+    # (A UNION ALL B) UNION C: the final UNION DISTINCT removes A's duplicates too
+    assert xs("SELECT x FROM sa UNION ALL SELECT x FROM sb UNION SELECT x FROM sc") == [1, 2, 3, 4]
+    # (A UNION B) UNION ALL C keeps C's duplicate of 1
+    assert xs("SELECT x FROM sa UNION SELECT x FROM sb UNION ALL SELECT x FROM sc") == [1, 1, 2, 3, 4]
+    # A UNION (B INTERSECT C): INTERSECT first
+    assert xs("SELECT x FROM sa UNION SELECT x FROM sb INTERSECT SELECT x FROM sc") == [1, 2, 3]
+    assert xs("SELECT x FROM sb INTERSECT SELECT x FROM sc UNION SELECT x FROM sa") == [1, 2, 3]
+    # parentheses override
+    assert xs("SELECT x FROM sa EXCEPT (SELECT x FROM sb EXCEPT SELECT x FROM sc)") == [1, 3]
+    # ORDER BY / LIMIT after the last branch order / cut the whole union
+    got = [r.x for r in s.sql("SELECT x FROM sa UNION ALL SELECT x FROM sc ORDER BY x DESC LIMIT 3").collect()]
+    assert got == [4, 3, 3]
+    got = [r.x for r in s.sql("SELECT x FROM sc UNION ALL SELECT x FROM sa ORDER BY x LIMIT 2").collect()]
+    assert got == [1, 1]
+    assert xs("SELECT x FROM sa INTERSECT ALL SELECT x FROM sa EXCEPT ALL SELECT x FROM sb") == [3, 3]
+    # set operation inside a subquery / CTE
+    assert xs("SELECT x FROM (SELECT x FROM sa EXCEPT SELECT x FROM sb) q WHERE x > 0") == [3]
+    assert xs("WITH q AS (SELECT x FROM sb UNION SELECT x FROM sc) SELECT x FROM q") == [1, 2, 4]

@@ -36,6 +36,24 @@ def test_failure_reports_rank_traceback():
         TorchDistributor(num_processes=2, use_gpu=False).run(bad)
 
 
+def test_timeout_tears_down_hung_rank():
+    """A rank that never reports (sleeping, as if stuck in a collective) hits the deadline:
+    every rank is terminated and the error names the silent rank."""
+    import time
+
+    def hang():
+        import os
+        import time as _t
+        if os.environ["RANK"] == "1":
+            _t.sleep(600)
+        return 0
+
+    t0 = time.monotonic()
+    with pytest.raises(RuntimeError, match=r"timed out .*ranks \[1\]"):
+        TorchDistributor(num_processes=2, use_gpu=False, timeout=8).run(hang)
+    assert time.monotonic() - t0 < 60
+
+
 def test_script_mode(tmp_path):
     out = tmp_path / "done"
     script = tmp_path / "train.py"
