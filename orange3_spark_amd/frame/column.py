@@ -382,6 +382,18 @@ class DeviceTokensColumn(ArrayColumn):
         return sum(t.element_size() * t.numel() for t in (self.doc_offs, self.tok_start, self.tok_end, self.data))
 
 
+def _h2d(arr: np.ndarray, device) -> torch.Tensor:
+    """Host array -> device tensor.  Large arrays go through a pinned staging buffer and an
+    async DMA on the current stream (a pageable copy runs at a fraction of the link rate and
+    blocks the host); torch's caching host allocator keeps the buffer alive until the copy
+    has run."""
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    dev = torch.device(device)
+    if dev.type == "cuda" and t.nbytes >= (1 << 20):
+        return t.pin_memory().to(dev, non_blocking=True)
+    return t.to(dev)
+
+
 def from_numpy(arr: np.ndarray, device) -> Column:
     """Column from a host numpy array (numeric -> device tensor; other -> host strings)."""
     arr = np.asarray(arr)
@@ -389,8 +401,8 @@ def from_numpy(arr: np.ndarray, device) -> Column:
         if arr.dtype.kind == "u":
             arr = arr.astype(np.int64)
         if arr.ndim == 2:
-            return VectorColumn(torch.from_numpy(np.ascontiguousarray(arr)).to(device))
-        return NumericColumn(torch.from_numpy(np.ascontiguousarray(arr)).to(device))
+            return VectorColumn(_h2d(arr, device))
+        return NumericColumn(_h2d(arr, device))
     vals = arr.astype(object)
     if len(vals) and all(isinstance(v, (list, tuple, np.ndarray)) or v is None for v in vals):
         first = next((v for v in vals if v is not None), None)

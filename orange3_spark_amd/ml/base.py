@@ -24,14 +24,38 @@ def _is_param_map(p) -> bool:
     return isinstance(p, dict)
 
 
+def _pool_of(dataset):
+    """The executor pool holding ``dataset`` when it is a driver-side handle (runtime/executors.py)."""
+    from ..runtime.executors import remote_pool_of
+    return remote_pool_of(dataset)
+
+
+def _exec_fit(est, dataset, params):
+    return est.fit(dataset, params)
+
+
+def _exec_transform(tr, dataset, params):
+    return tr.transform(dataset, params)
+
+
+def _exec_evaluate(ev, dataset, params):
+    return ev.evaluate(dataset, params)
+
+
 class Transformer(Params, ABC):
-    """Abstract: transforms one DataFrame into another."""
+    """Abstract: transforms one DataFrame into another.
+
+    Called with an executor-pool handle (driver process of a multi-GPU session), the
+    stage is shipped to the executors and the result stays there as a handle."""
 
     def transform(self, dataset, params=None):
         if params is None:
             params = {}
         if not _is_param_map(params):
             raise TypeError(f"Params must be a param map but got {type(params)}.")
+        pool = _pool_of(dataset)
+        if pool is not None:
+            return pool.apply(_exec_transform, self, dataset, params)
         with trace(f"{type(self).__name__}.transform"):
             if params:
                 return self.copy(params)._transform(dataset)
@@ -52,6 +76,9 @@ class Estimator(Params, ABC):
             return [self.fit(dataset, p) for p in params]
         if not _is_param_map(params):
             raise TypeError(f"Params must be either a param map or a list/tuple of param maps, but got {type(params)}.")
+        pool = _pool_of(dataset)
+        if pool is not None:                  # driver of an executor pool: fit on every executor
+            return pool.apply(_exec_fit, self, dataset, params)
         import time
         from ..parallel.comm import COMM_STATS
         c0 = {k: tuple(v) for k, v in COMM_STATS.items()}
@@ -108,6 +135,9 @@ class Evaluator(Params, ABC):
     def evaluate(self, dataset, params=None):
         if params is None:
             params = {}
+        pool = _pool_of(dataset)
+        if pool is not None:
+            return pool.apply(_exec_evaluate, self, dataset, params)
         with trace(f"{type(self).__name__}.evaluate"):
             if params:
                 return self.copy(params)._evaluate(dataset)

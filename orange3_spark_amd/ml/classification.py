@@ -102,7 +102,7 @@ class LogisticRegression(Estimator, _LogisticRegressionParams, MLWritable, MLRea
         g = self.getOrDefault
         comm = df.comm
         feat = U.features_column(df, g(self.featuresCol))
-        y = U.numeric_column(df, g(self.labelCol), torch.float64)
+        y = U.numeric_column(df, g(self.labelCol), None)      # storage dtype: no 1B-row copy
         sw = U.weights_or_none(df, self)
         k = U.num_classes(comm, y)
         fam = g(self.family).lower()
@@ -282,7 +282,7 @@ class LinearSVC(Estimator, _LinearSVCParams, MLWritable, MLReadable):
     def _fit(self, df):
         g = self.getOrDefault
         comm = df.comm
-        y = U.numeric_column(df, g(self.labelCol), torch.float64)
+        y = U.numeric_column(df, g(self.labelCol), None)
         k = U.num_classes(comm, y)
         if k > 2:
             raise ValueError(f"LinearSVC only supports binary classification. {k} classes detected in labelCol")

@@ -51,14 +51,18 @@ def linear_margin(X, w: np.ndarray, b: float) -> torch.Tensor:
 
 
 def numeric_column(df, name: str, dtype=torch.float64) -> torch.Tensor:
+    """The column's values as a tensor of ``dtype`` (None: floating columns keep their
+    storage dtype -- no full-length copy of a 1B-row label column)."""
     c = df.column_data(name)
     if isinstance(c, C.NumericColumn):
         d = c.data
         if c.valid is not None and not bool(c.valid.all()):
             raise ValueError(f"column {name} contains null values")
+        if dtype is None:
+            return d if d.is_floating_point() else d.to(torch.float64)
         return d.to(dtype)
     if isinstance(c, C.StringColumn):
-        return c.cast("double").data.to(dtype)
+        return c.cast("double").data.to(dtype or torch.float64)
     raise TypeError(f"Column {name} must be numeric but was {c.dtype.simpleString()}.")
 
 

@@ -194,6 +194,13 @@ class PrefixSpan:
         self.maxLocalProjDBSize, self.sequenceCol = maxLocalProjDBSize, sequenceCol
 
     def findFrequentSequentialPatterns(self, dataset):
+        from ..runtime.executors import remote_pool_of
+        pool = remote_pool_of(dataset)
+        if pool is not None:                 # driver of an executor pool: run on the executors
+            return pool.call(self, "findFrequentSequentialPatterns", (dataset,))
+        return self._find_patterns(dataset)
+
+    def _find_patterns(self, dataset):
         vals = dataset.column_data(self.sequenceCol).values
         parts = dataset.comm.all_gather_object([list(v) for v in vals])
         seqs = [[frozenset(e) for e in s] for p in parts for s in p]

@@ -10,6 +10,8 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
+from ..runtime.executors import ship
+
 from ..frame import column as C
 from ..frame.dataframe import DataFrame
 from . import common as U
@@ -47,6 +49,7 @@ def chi_square_pvalues(comm, X: torch.Tensor, y: torch.Tensor, return_all=False)
 
 class ChiSquareTest:
     @staticmethod
+    @ship
     def test(dataset, featuresCol, labelCol, flatten=False):
         X = U.dense_features(dataset, featuresCol, torch.float64)
         y = U.numeric_column(dataset, labelCol)
@@ -64,6 +67,7 @@ class ChiSquareTest:
 
 class Correlation:
     @staticmethod
+    @ship
     def corr(dataset, column, method="pearson"):
         X = U.dense_features(dataset, column, torch.float64)
         comm = dataset.comm
@@ -119,6 +123,7 @@ class Summarizer:
         return SummaryBuilder(metrics)
 
     @staticmethod
+    @ship
     def compute(dataset, featuresCol, metrics, weightCol=None):
         X = U.dense_features(dataset, featuresCol, torch.float64)
         w = torch.ones(X.shape[0], dtype=torch.float64, device=X.device) if weightCol is None else \
@@ -154,6 +159,7 @@ class Summarizer:
 
 class KolmogorovSmirnovTest:
     @staticmethod
+    @ship
     def test(dataset, sampleCol, distName="norm", *params):
         from scipy import stats
         x = U.numeric_column(dataset, sampleCol)
@@ -179,6 +185,7 @@ class ANOVATest:
     """ANOVA F-test of continuous features against a categorical label (Spark >= 3.1)."""
 
     @staticmethod
+    @ship
     def test(dataset, featuresCol, labelCol, flatten=False):
         from ._feature_extra import anova_f
         X = U.dense_features(dataset, featuresCol, torch.float64)
@@ -191,6 +198,7 @@ class FValueTest:
     """F-value regression test of continuous features against a continuous label."""
 
     @staticmethod
+    @ship
     def test(dataset, featuresCol, labelCol, flatten=False):
         from ._feature_extra import f_regression
         X = U.dense_features(dataset, featuresCol, torch.float64)

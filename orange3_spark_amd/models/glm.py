@@ -680,6 +680,12 @@ class DeviceSGD:
         self.loss_hist[self.t - 1:self.t].copy_(out[self.dpad + 1:self.dpad + 2] * invW)
         self.t_dev.fill_(self.t)
 
+    # Steps whose pass streams more than this many bytes per rank are not captured: their
+    # GPU time (>= ~40 us) already hides the host's launch sequence (the host runs ahead,
+    # nothing in a step syncs), while capturing + instantiating costs ~12 ms of idle GPU
+    # once per fit at 1B x 256 (rocprofv3 timeline, profiles/bench_fit_timeline_r3.json).
+    GRAPH_MAX_BYTES = int(os.environ.get("O3S_SGD_GRAPH_MAX_BYTES", str(256 << 20)))
+
     def _maybe_capture(self):
         from ..runtime import faults
         mode = os.environ.get("O3S_SGD_GRAPH", "1")
@@ -688,6 +694,8 @@ class DeviceSGD:
         if faults.launch_blocking():
             return
         d = self.data
+        if mode != "force" and d.n_local * d.ld * 2 > self.GRAPH_MAX_BYTES:
+            return
         try:
             if d.comm.world_size == 1:
                 g = torch.cuda.CUDAGraph()

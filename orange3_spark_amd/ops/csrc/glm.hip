@@ -441,7 +441,7 @@ __host__ __device__ __forceinline__ uint32_t sample_key(uint32_t seed, uint32_t 
   return fmix32(seed ^ fmix32(iter * 0x9E3779B1u + 0x7F4A7C15u));
 }
 
-template <int LPR, int CPL, int UNROLL, int LOSS, int SRC>
+template <int LPR, int CPL, int UNROLL, int LOSS, int SRC, bool SMP>
 __device__ __forceinline__ void mixed_tile(
     int64_t base, int64_t n, const uint16_t* __restrict__ X, int64_t ld, int nch,
     const float* __restrict__ y, const float* __restrict__ sw, uint32_t seed, int64_t row0,
@@ -491,7 +491,9 @@ __device__ __forceinline__ void mixed_tile(
     const float wv = sw ? sw[rowc] : 1.f;
     yy[j] = ok ? yv : 0.f;
     ww[j] = ok ? wv : 0.f;
-    if (smp.on() && !smp.keep(row)) ww[j] = 0.f;
+    if constexpr (SMP) {
+      if (!smp.keep(row)) ww[j] = 0.f;
+    }
   }
   float dot[UNROLL];
 #pragma unroll
@@ -565,7 +567,7 @@ __device__ __forceinline__ void mixed_tile(
 // LW > 0: fixed roles -- waves 0..LW-1 of each block regenerate lineage tiles, the
 // other 4 - LW stream resident tiles with UR rows per lane in flight, so the load
 // pipeline never pauses for hash work (each role strides over its own tiles).
-template <int LPR, int CPL, int UNROLL, int LOSS, int MW, int LW, int UR>
+template <int LPR, int CPL, int UNROLL, int LOSS, int MW, int LW, int UR, bool SMP>
 __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
     const uint16_t* __restrict__ X, int64_t ld, int64_t n_res, const float* __restrict__ y,
     const float* __restrict__ sw, const float* __restrict__ coef, const float* __restrict__ bptr,
@@ -583,7 +585,8 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
   const float* y_lin = y + n_res;
   const float* sw_lin = sw ? sw + n_res : nullptr;
   // iteration t of a device-side SGD loop = t_dev + 1 (the update kernel advances it)
-  const uint32_t skey = sthr < (1u << 24) ? sample_key(sseed, (uint32_t)((t_dev ? t_dev[0] : 0) + 1)) : 0u;
+  // (SMP = false: the sampler is compiled out -- no hash, no extra registers)
+  const uint32_t skey = SMP ? sample_key(sseed, (uint32_t)((t_dev ? t_dev[0] : 0) + 1)) : 0u;
   const RowSampler smp_res{skey, sthr, res_row0}, smp_lin{skey, sthr, row0};
 
   float w[CPL][8], acc[CPL][8];
@@ -610,11 +613,11 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
       const int64_t q0 = nw * Tl / S, r0 = nw * Tl - q0 * S;
       for (int64_t s = gw; s < S; s += nw) {
         if (rem + Tl >= S)
-          mixed_tile<LPR, CPL, UNROLL, LOSS, 1>(L * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
+          mixed_tile<LPR, CPL, UNROLL, LOSS, 1, SMP>(L * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
                                                 wshift, intercept, g, c, smp_lin, acc, rs, acc_r, acc_loss,
                                                 acc_w);
         else
-          mixed_tile<LPR, CPL, UNROLL, LOSS, 0>((s - L) * RT, n_res, X, ld, nch, y, sw, seed, row0, w,
+          mixed_tile<LPR, CPL, UNROLL, LOSS, 0, SMP>((s - L) * RT, n_res, X, ld, nch, y, sw, seed, row0, w,
                                                 wshift, intercept, g, c, smp_res, acc, rs, acc_r, acc_loss,
                                                 acc_w);
         rem += r0;
@@ -627,14 +630,14 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
       const int64_t Tl = (n_lin + RT - 1) / RT;
       const int64_t nlw = (int64_t)gridDim.x * LW;
       for (int64_t t = (int64_t)blockIdx.x * LW + wid; t < Tl; t += nlw)
-        mixed_tile<LPR, CPL, UNROLL, LOSS, 1>(t * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
+        mixed_tile<LPR, CPL, UNROLL, LOSS, 1, SMP>(t * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
                                               wshift, intercept, g, c, smp_lin, acc, rs, acc_r, acc_loss, acc_w);
     } else {
       constexpr int RTR = G * UR;
       const int64_t Tr = (n_res + RTR - 1) / RTR;
       const int64_t nrw = (int64_t)gridDim.x * (kWavesPerBlock - LW);
       for (int64_t t = (int64_t)blockIdx.x * (kWavesPerBlock - LW) + (wid - LW); t < Tr; t += nrw)
-        mixed_tile<LPR, CPL, UR, LOSS, 0>(t * RTR, n_res, X, ld, nch, y, sw, seed, row0, w, wshift,
+        mixed_tile<LPR, CPL, UR, LOSS, 0, SMP>(t * RTR, n_res, X, ld, nch, y, sw, seed, row0, w, wshift,
                                           intercept, g, c, smp_res, acc, rs, acc_r, acc_loss, acc_w);
     }
   }
@@ -687,6 +690,7 @@ __device__ __forceinline__ void stats_tile(int64_t base, int64_t n, const uint16
   constexpr int G = kWave / LPR;
   constexpr int U = CPL >= 8 ? 1 : 8 / CPL;
   short8 xv[U][CPL];
+  uint32_t fk[U];
   float yv[U], wv[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -705,9 +709,7 @@ __device__ __forceinline__ void stats_tile(int64_t base, int64_t n, const uint16
         xv[u][k] = ch < nch ? v : short8{0, 0, 0, 0, 0, 0, 0, 0};
       }
     } else {
-      const uint32_t fk = feat_key(seed, row0 + rowc);
-#pragma unroll
-      for (int k = 0; k < CPL; ++k) xv[u][k] = synth_chunk(fk, c + k * LPR);
+      fk[u] = feat_key(seed, row0 + rowc);
     }
   }
 #pragma unroll
@@ -718,7 +720,19 @@ __device__ __forceinline__ void stats_tile(int64_t base, int64_t n, const uint16
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
       float x[8];
-      unpack8(xv[u][k], x);
+      if (SRC == 0) {
+        unpack8(xv[u][k], x);
+      } else {
+        // lineage rows: the feature bytes straight from the hash (x = b/128 - 255/256 is
+        // exact), no bf16 round trip
+        const int ch = c + k * LPR;
+        const uint32_t h0 = synth_word(fk[u], 2 * ch), h1 = synth_word(fk[u], 2 * ch + 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x[j] = fmaf(synth_byte(h0, j), kSynthScale, kSynthShift);
+          x[4 + j] = fmaf(synth_byte(h1, j), kSynthScale, kSynthShift);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float2_ xx = {x[2 * j], x[2 * j + 1]};
@@ -1180,7 +1194,7 @@ O3S_API int o3s_glm_grad(int loss, int src, const void* X, int64_t ld, int64_t n
   return 0;
 }
 
-template <int L, int C, int MW, int LW, int UR>
+template <int L, int C, int MW, int LW, int UR, bool SMP = false>
 static void launch_mixed(int loss, int grid, hipStream_t st, const uint16_t* X, int64_t ld, int64_t n_res,
                          const float* y, const float* sw, const float* coef, const float* b, uint32_t seed,
                          int64_t row0, int64_t n_lin, float* partial, int pstride, int64_t res_row0,
@@ -1188,15 +1202,15 @@ static void launch_mixed(int loss, int grid, hipStream_t st, const uint16_t* X, 
   constexpr int U = C >= 8 ? 1 : 8 / C;
   constexpr int UR2 = UR > 0 ? UR : U;
   if (loss == LOSS_LOGISTIC)
-    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_LOGISTIC, MW, LW, UR2>), dim3(grid), dim3(kBlock), 0,
+    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_LOGISTIC, MW, LW, UR2, SMP>), dim3(grid), dim3(kBlock), 0,
                        st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride, res_row0, t_dev,
                        sseed, sthr);
   else if (loss == LOSS_HINGE)
-    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_HINGE, MW, LW, UR2>), dim3(grid), dim3(kBlock), 0,
+    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_HINGE, MW, LW, UR2, SMP>), dim3(grid), dim3(kBlock), 0,
                        st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride, res_row0, t_dev,
                        sseed, sthr);
   else
-    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_SQUARED, MW, LW, UR2>), dim3(grid), dim3(kBlock), 0,
+    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_SQUARED, MW, LW, UR2, SMP>), dim3(grid), dim3(kBlock), 0,
                        st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride, res_row0, t_dev,
                        sseed, sthr);
 }
@@ -1224,16 +1238,25 @@ O3S_API int o3s_glm_grad_mixed(int loss, const void* X, int64_t ld, int64_t n_re
   else if (cpl == 2) { lpr_s = 32; cpl_s = 4; }
   const uint16_t* Xh = (const uint16_t*)X;
   const float* b = coef + dpad;
+  const bool smp = sthr < (1u << 24);     // sampling: interleaved-role layouts (mode 0) only
   bool done = false;
 #define O3S_MX(L, C)                                                                                  \
   if (!done && lpr_s == L && cpl_s == C) {                                                            \
     done = true;                                                                                      \
-    if (mode == 0 && waves == 3)                                                                      \
+    if (mode == 0 && waves == 3 && smp)                                                               \
+      launch_mixed<L, C, 3, 0, 0, true>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0,    \
+                                        n_lin, partial, pstride, res_row0, t_dev, sseed, sthr);       \
+    else if (mode == 0 && waves == 3)                                                                 \
       launch_mixed<L, C, 3, 0, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
                                   partial, pstride, res_row0, t_dev, sseed, sthr);                   \
+    else if (mode == 0 && smp)                                                                        \
+      launch_mixed<L, C, 2, 0, 0, true>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0,    \
+                                        n_lin, partial, pstride, res_row0, t_dev, sseed, sthr);       \
     else if (mode == 0)                                                                               \
       launch_mixed<L, C, 2, 0, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
                                   partial, pstride, res_row0, t_dev, sseed, sthr);                   \
+    else if (smp)                                                                                     \
+      done = false;                                                                                   \
     else if (mode == 1)                                                                               \
       launch_mixed<L, C, 3, 1, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
                                   partial, pstride, res_row0, t_dev, sseed, sthr);                   \

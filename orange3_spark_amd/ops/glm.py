@@ -294,7 +294,8 @@ def glm_grad_mixed(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, n_
     cf = _coef_buf(coef, ws.dpad, ws.device, intercept=intercept)
     N.check(N.kernels().o3s_glm_grad_mixed(loss, X.data_ptr(), ld, nr, y.data_ptr(), N.ptr(sw),
                                            cf.data_ptr(), seed & _MASK, row0, n_lin, ws.partial.data_ptr(),
-                                           ws.grid, ws.out.data_ptr(), MIX_WAVES, MIX_MODE, int(res_row0),
+                                           ws.grid, ws.out.data_ptr(), MIX_WAVES,
+                                           MIX_MODE if thr >= 1 << 24 else 0, int(res_row0),
                                            N.ptr(t_dev), int(sample_seed) & _MASK, thr, N.stream_of(X)),
             "glm_grad_mixed")
     return ws.out

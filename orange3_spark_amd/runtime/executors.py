@@ -1,0 +1,716 @@
+"""Driver + executor-pool runtime: one Orange (driver) process drives N GPU worker processes.
+
+Reference: the Context widget sizes the cluster (``spark.executor.instances=8``,
+orangecontrib/spark/widgets/data/spark_context.py:41-42,76) and every ``fit`` then runs on
+all executors (orangecontrib/spark/base/spark_ml_estimator.py:19-25).  Spark does this with
+a JVM driver, Py4J and YARN executors; the MI355X design is:
+
+* ``Session(conf)`` with ``spark.executor.instances = N > 1`` (outside an SPMD launch)
+  becomes a :class:`DriverSession`: the GUI / script process never touches a GPU; it
+  ``spawn``-s N fresh worker processes (never ``exec``), worker r owns ``cuda:r`` and
+  joins an N-rank RCCL group over xGMI (gloo on CPU).  Each worker holds an ordinary SPMD
+  :class:`~orange3_spark_amd.session.Session` and 1/N of every DataFrame's rows.
+* Every driver-side call is a **command** broadcast to all workers over a pipe; the
+  workers execute it in lock step (so collectives inside line up) and rank 0 returns the
+  result.  Results that are engine objects (DataFrames, column expressions, grouped data,
+  readers, catalogs, RDDs, training summaries, ...) stay on the workers and come back as
+  handles (:class:`RemoteObject` / :class:`RemoteDataFrame`, ``isinstance(h, DataFrame)``
+  holds); plain values (counts, rows, pandas frames, fitted models with their host
+  parameters) come back by value, device tensors moved to host memory.
+* Estimator / Transformer / Evaluator calls on a handle ship the (pickled) stage to the
+  workers (``ml/base.py`` hooks), so a fitted model arrives in the driver as a normal local
+  model object -- widgets, ``model.coefficients`` and ``model.save`` work unchanged.
+* ``createDataFrame(pandas)`` scatters: worker r receives only its row slice (host memory
+  per worker ~ 1/N of the table) and copies it to its GPU through pinned memory.
+* Handles are reference counted: when the driver drops the last handle, the workers free
+  the object at the next command.  A command that fails on some ranks while others are
+  stuck in a collective tears the pool down after a grace period (the session reports
+  itself stopped) instead of hanging the GUI.
+"""
+from __future__ import annotations
+
+import io
+import itertools
+import logging
+import os
+import pickle
+import socket
+import threading
+import time
+import traceback
+import weakref
+
+log = logging.getLogger(__name__)
+
+_REMOTE_MODULES = ("orange3_spark_amd.frame", "orange3_spark_amd.sql", "orange3_spark_amd.rdd",
+                   "orange3_spark_amd.catalog", "orange3_spark_amd.io", "orange3_spark_amd.session",
+                   "orange3_spark_amd.synthetic", "orange3_spark_amd.ml._summary")
+_VALUE_MODULES = ("orange3_spark_amd.frame.types",)
+
+
+class ExecutorError(RuntimeError):
+    """A command failed on one or more executors (carries each failing rank's traceback)."""
+
+
+class ExecutorLost(ExecutorError):
+    """An executor died or a command did not finish on every rank: the pool is torn down."""
+
+
+def _is_remote_kept(obj) -> bool:
+    """Engine objects that stay on the workers (handles) rather than travel by value."""
+    t = type(obj)
+    mod = getattr(t, "__module__", "") or ""
+    if not mod.startswith(_REMOTE_MODULES) or mod.startswith(_VALUE_MODULES):
+        return False
+    return not isinstance(obj, tuple)          # Row (a tuple subclass) travels by value
+
+
+# =====================================================================================
+# worker side
+# =====================================================================================
+class _Null:
+    def write(self, b):
+        return len(b)
+
+
+def _worker_pickler(objs: dict, ids: dict, counter, buf):
+    """Pickler that keeps engine objects on this worker (registered under the next id of a
+    counter every rank advances identically) and moves device tensors to host memory."""
+    import cloudpickle
+    import torch
+
+    class P(cloudpickle.Pickler):
+        def persistent_id(self, obj):
+            if _is_remote_kept(obj):
+                k = ids.get(id(obj))
+                if k is None or objs.get(k) is not obj:
+                    k = next(counter)
+                    objs[k] = obj
+                    ids[id(obj)] = k
+                return ("ref", k, type(obj).__name__, _is_frame(obj))
+            return None
+
+        def reducer_override(self, obj):
+            if isinstance(obj, torch.Tensor) and obj.device.type != "cpu":
+                return obj.detach().cpu().__reduce_ex__(pickle.HIGHEST_PROTOCOL)
+            if isinstance(obj, torch.device) and obj.type != "cpu":
+                return (torch.device, ("cpu",))
+            return super().reducer_override(obj)
+    return P(buf, protocol=pickle.HIGHEST_PROTOCOL)
+
+
+def _is_frame(obj) -> bool:
+    from ..frame.dataframe import DataFrame
+    return isinstance(obj, DataFrame)
+
+
+def _worker_unpickler(objs: dict, data: bytes):
+    class U(pickle.Unpickler):
+        def persistent_load(self, pid):
+            return objs[pid[1]]
+    return U(io.BytesIO(data)).load()
+
+
+def _worker_entry(argv=None) -> int:
+    """``python -m orange3_spark_amd.runtime.executors --connect HOST:PORT --rank R ...``:
+    an executor process.  Started with subprocess (a fresh interpreter: the driver's main
+    module is never re-imported, the driver never forks a process holding GPU state);
+    authenticates to the driver's listener, receives the session conf, serves commands."""
+    import argparse
+    from multiprocessing.connection import Client
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--connect", required=True)
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--dist-port", type=int, required=True)
+    ap.add_argument("--gpu", type=int, default=1)
+    ap.add_argument("--gloo", type=int, default=0)
+    a = ap.parse_args(argv)
+    host, port = a.connect.rsplit(":", 1)
+    key = bytes.fromhex(os.environ.pop("O3S_EXECUTOR_AUTHKEY"))
+    conn = Client((host, int(port)), authkey=key)
+    conn.send_bytes(pickle.dumps(("hello", a.rank)))
+    conf_pairs = pickle.loads(conn.recv_bytes())
+    _worker_main(a.rank, a.world, a.dist_port, conf_pairs, conn, bool(a.gpu), bool(a.gloo))
+    return 0
+
+
+def _worker_main(rank: int, world: int, port: int, conf_pairs, conn, use_gpu: bool, gloo: bool):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if gloo:
+        os.environ["O3S_DIST_BACKEND"] = "gloo"
+    if not use_gpu:
+        os.environ["HIP_VISIBLE_DEVICES"] = ""
+        os.environ["CUDA_VISIBLE_DEVICES"] = ""
+    try:
+        from ..conf import SessionConf
+        from ..session import Session
+        conf = SessionConf(False, conf_pairs).set("spark.master", "spmd")
+        if not use_gpu:
+            conf.set("o3s.device", "cpu")
+        s = Session(conf)
+        Session._active = s
+    except BaseException:  # noqa: BLE001 - reported to the driver
+        conn.send_bytes(pickle.dumps(("error", rank, traceback.format_exc())))
+        return
+    conn.send_bytes(pickle.dumps(("ready", rank, str(s.device))))
+    objs: dict = {0: s}
+    ids: dict = {id(s): 0}
+    counter = itertools.count(1)
+    while True:
+        try:
+            msg = conn.recv_bytes()
+        except (EOFError, OSError):
+            break
+        try:
+            garbage = pickle.loads(msg[8:_hdr_len(msg)])
+        except Exception:  # noqa: BLE001
+            garbage = []
+        for k in garbage:
+            o = objs.pop(k, None)
+            if o is not None and ids.get(id(o)) == k:
+                ids.pop(id(o), None)
+        body = msg[_hdr_len(msg):]
+        try:
+            cmd = _worker_unpickler(objs, body)
+            kind = cmd[0]
+            if kind == "stop":
+                conn.send_bytes(pickle.dumps(("ok", rank, None)))
+                break
+            result = _execute(s, cmd, objs)
+            buf = io.BytesIO() if rank == 0 else _Null()
+            _worker_pickler(objs, ids, counter, buf).dump(result)
+            conn.send_bytes(pickle.dumps(("ok", rank, buf.getvalue() if rank == 0 else None)))
+        except BaseException:  # noqa: BLE001 - every failure goes back to the driver
+            conn.send_bytes(pickle.dumps(("error", rank, traceback.format_exc())))
+    try:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        pass
+
+
+def _hdr_len(msg: bytes) -> int:
+    return 8 + int.from_bytes(msg[:8], "little")
+
+
+def _execute(s, cmd, objs=None):
+    kind = cmd[0]
+    if kind == "getattr":
+        _, target, name = cmd
+        v = getattr(target, name)
+        if callable(v) and not isinstance(v, type) and hasattr(v, "__self__") and not _is_remote_kept(v):
+            return _BoundMethod(name)
+        return v
+    if kind == "call":
+        _, target, name, args, kwargs = cmd
+        return getattr(target, name)(*args, **kwargs)
+    if kind == "apply":                       # fn(*args, **kwargs) with a shipped callable
+        _, fn, args, kwargs = cmd
+        return fn(*args, **kwargs)
+    if kind == "scatter_df":
+        _, part, schema = cmd
+        return s.createDataFrame(part, schema, _local=True)
+    if kind == "info":
+        import torch
+        return {"device": str(s.device), "backend": s.comm.backend, "world": s.comm.world_size,
+                "gpu": torch.cuda.get_device_name(s.device) if s.device.type == "cuda" else None,
+                "objects": len(objs) if objs is not None else None}
+    raise ValueError(f"unknown executor command {kind!r}")
+
+
+class _BoundMethod:
+    """Marker: the attribute is a method of the remote object (call it through the pool)."""
+
+    def __init__(self, name):
+        self.name = name
+
+
+# =====================================================================================
+# driver side
+# =====================================================================================
+def _free_port() -> int:
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    p = sk.getsockname()[1]
+    sk.close()
+    return p
+
+
+class _Proc:
+    """subprocess.Popen with the multiprocessing.Process surface the pool uses."""
+
+    def __init__(self, popen):
+        self.p = popen
+
+    def is_alive(self) -> bool:
+        return self.p.poll() is None
+
+    @property
+    def exitcode(self):
+        return self.p.poll()
+
+    def terminate(self):
+        if self.is_alive():
+            self.p.terminate()
+
+    def kill(self):
+        if self.is_alive():
+            self.p.kill()
+
+    def join(self, timeout=None):
+        import subprocess
+        try:
+            self.p.wait(timeout)
+        except subprocess.TimeoutExpired:
+            pass
+
+
+class ExecutorPool:
+    """N worker processes in one RCCL (or gloo) group, driven by this process."""
+
+    _pools: "weakref.WeakSet[ExecutorPool]" = weakref.WeakSet()
+
+    def __init__(self, n: int, conf_pairs, use_gpu: bool | None = None, start_timeout: float = 600.0,
+                 command_timeout: float | None = None, error_grace: float = 20.0):
+        import secrets
+        import subprocess
+        import sys
+        from multiprocessing.connection import Listener
+        import torch
+        self.n = int(n)
+        if self.n < 1:
+            raise ValueError("an executor pool needs at least one executor")
+        pairs = list(conf_pairs)
+        dev_pref = dict(pairs).get("o3s.device", "auto").lower()
+        ngpu = torch.cuda.device_count()          # counting does not initialise HIP here
+        if use_gpu is None:
+            use_gpu = dev_pref != "cpu" and ngpu > 0
+        gloo = os.environ.get("O3S_DIST_BACKEND") == "gloo"
+        if use_gpu and ngpu < self.n and not gloo:
+            raise RuntimeError(f"spark.executor.instances={self.n} needs {self.n} GPUs, {ngpu} visible "
+                               "(O3S_DIST_BACKEND=gloo shares GPUs between executors for testing)")
+        self.use_gpu = bool(use_gpu)
+        self.command_timeout = command_timeout
+        self.error_grace = float(error_grace)
+        self._lock = threading.RLock()
+        self._garbage: list = []
+        self._proxies: dict = {}
+        self._methods: set = set()
+        self.alive = False
+        self._conns, self._procs = [None] * self.n, []
+        key = secrets.token_bytes(32)
+        listener = Listener(("127.0.0.1", 0), authkey=key)
+        host, lport = listener.address
+        dist_port = _free_port()
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        # executors import what the driver can import (its sys.path: user modules whose
+        # functions / classes are shipped by reference, like Spark's --py-files)
+        paths = [root] + [p for p in sys.path if p and os.path.isdir(p)]
+        paths += [p for p in os.environ.get("PYTHONPATH", "").split(os.pathsep) if p]
+        env = dict(os.environ, O3S_EXECUTOR_AUTHKEY=key.hex(), HSA_ENABLE_IPC_MODE_LEGACY="0",
+                   PYTHONPATH=os.pathsep.join(dict.fromkeys(paths)))
+        env.pop("WORLD_SIZE", None)
+        for r in range(self.n):
+            cmd = [sys.executable, "-m", "orange3_spark_amd.runtime.executors", "--connect", f"{host}:{lport}",
+                   "--rank", str(r), "--world", str(self.n), "--dist-port", str(dist_port),
+                   "--gpu", str(int(self.use_gpu)), "--gloo", str(int(gloo))]
+            self._procs.append(_Proc(subprocess.Popen(cmd, env=env)))
+        try:
+            self._accept(listener, pairs, start_timeout)
+        finally:
+            listener.close()
+        self.devices = [None] * self.n
+        replies = self._gather(start_timeout, what="start")
+        errs = [(r, d) for st, r, d in replies if st != "ready"]
+        if errs:
+            self._teardown()
+            raise ExecutorLost("executor start failed:\n" + "\n".join(f"[rank {r}] {d}" for r, d in errs))
+        for _, r, dev in replies:
+            self.devices[r] = dev
+        self.alive = True
+        ExecutorPool._pools.add(self)
+
+    def _accept(self, listener, pairs, timeout: float):
+        """Accept the N executors' authenticated connections (in a helper thread, so a
+        worker that dies before connecting is noticed) and send each the session conf."""
+        got: list = []
+        err: list = []
+
+        def run():
+            try:
+                for _ in range(self.n):
+                    c = listener.accept()
+                    hello = pickle.loads(c.recv_bytes())
+                    got.append((hello[1], c))
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+        th = threading.Thread(target=run, daemon=True)
+        th.start()
+        deadline = time.monotonic() + timeout
+        while th.is_alive():
+            th.join(0.2)
+            dead = [r for r, p in enumerate(self._procs) if not p.is_alive()]
+            if dead or time.monotonic() > deadline:
+                self._teardown()
+                raise ExecutorLost(f"executor(s) {dead or 'all'} failed to connect "
+                                   f"(exit codes {[self._procs[r].exitcode for r in dead]})")
+        if err or len(got) != self.n:
+            self._teardown()
+            raise ExecutorLost(f"executor handshake failed: {err}")
+        for r, c in got:
+            self._conns[r] = c
+            c.send_bytes(pickle.dumps(pairs))
+
+    # ---------------------------------------------------------------- transport
+    def _gather(self, timeout: float | None, what: str):
+        """One reply per rank.  After the first error, the others get ``error_grace``
+        seconds; ranks that neither reply nor die in time mean the group is wedged (a
+        collective waiting for a failed peer): the pool is torn down."""
+        from multiprocessing.connection import wait
+        pending = dict(enumerate(self._conns))
+        out, first_err = [], None
+        deadline = None if timeout is None else time.monotonic() + timeout
+        while pending:
+            now = time.monotonic()
+            limit = deadline
+            if first_err is not None:
+                g = first_err + self.error_grace
+                limit = g if limit is None else min(limit, g)
+            if limit is not None and now > limit:
+                self._teardown()
+                raise ExecutorLost(f"executors {sorted(pending)} did not finish '{what}'"
+                                   + (f"; errors: {self._fmt(out)}" if out else "") + " -- the pool was shut down")
+            ready = wait(list(pending.values()), timeout=1.0 if limit is None else max(0.01, min(1.0, limit - now)))
+            for c in ready:
+                r = next(k for k, v in pending.items() if v is c)
+                try:
+                    msg = pickle.loads(c.recv_bytes())
+                except (EOFError, OSError):
+                    self._teardown()
+                    raise ExecutorLost(f"executor {r} died during '{what}' (exit code "
+                                       f"{self._procs[r].exitcode})") from None
+                pending.pop(r)
+                out.append(msg)
+                if msg[0] == "error" and first_err is None:
+                    first_err = time.monotonic()
+            for r in list(pending):
+                if not self._procs[r].is_alive():
+                    self._teardown()
+                    raise ExecutorLost(f"executor {r} exited with code {self._procs[r].exitcode} during '{what}'")
+        return out
+
+    @staticmethod
+    def _fmt(replies):
+        return "\n".join(f"[rank {r}] {d}" for st, r, d in replies if st == "error")
+
+    def _driver_pickle(self, cmd) -> bytes:
+        import cloudpickle
+        pool = self
+
+        class P(cloudpickle.Pickler):
+            def persistent_id(self, obj):
+                if isinstance(obj, RemoteObject):
+                    if obj._pool is not pool:
+                        raise ValueError("a handle of another executor pool cannot be used here")
+                    return ("ref", obj._id)
+                return None
+        buf = io.BytesIO()
+        P(buf, protocol=pickle.HIGHEST_PROTOCOL).dump(cmd)
+        return buf.getvalue()
+
+    def _driver_unpickle(self, data: bytes):
+        pool = self
+
+        class U(pickle.Unpickler):
+            def persistent_load(self, pid):
+                _, k, tname, is_frame = pid
+                return pool._proxy(k, tname, is_frame)
+        return U(io.BytesIO(data)).load()
+
+    def _proxy(self, k, tname, is_frame):
+        ref = self._proxies.get(k)
+        obj = ref() if ref is not None else None
+        if obj is None:
+            obj = (RemoteDataFrame if is_frame else RemoteObject)(self, k, tname)
+            self._proxies[k] = weakref.ref(obj)
+            weakref.finalize(obj, self._release, k)
+        return obj
+
+    def _release(self, k):
+        self._garbage.append(k)
+
+    def command(self, cmd, per_rank=None, what: str | None = None):
+        """Run ``cmd`` on every executor (``per_rank[r]`` replaces it on rank r) and return
+        rank 0's result."""
+        with self._lock:
+            if not self.alive:
+                raise ExecutorLost("the executor pool is shut down")
+            garbage, self._garbage = self._garbage, []
+            for k in garbage:
+                self._proxies.pop(k, None)
+            hdr = pickle.dumps(garbage)
+            head = len(hdr).to_bytes(8, "little") + hdr
+            body = self._driver_pickle(cmd) if per_rank is None else None
+            for r, c in enumerate(self._conns):
+                b = body if per_rank is None else self._driver_pickle(per_rank[r])
+                try:
+                    c.send_bytes(head + b)
+                except (BrokenPipeError, OSError):
+                    self._teardown()
+                    raise ExecutorLost(f"executor {r} is gone") from None
+            replies = self._gather(self.command_timeout, what or str(cmd[0]))
+            errs = [m for m in replies if m[0] == "error"]
+            if errs:
+                raise ExecutorError("command failed on executor(s):\n" + self._fmt(replies))
+            data = next(d for st, r, d in replies if r == 0)
+            return self._driver_unpickle(data)
+
+    # ---------------------------------------------------------------- API used by proxies
+    def getattr(self, obj: "RemoteObject", name: str):
+        key = (obj._tname, name)
+        if key in self._methods:                 # known method: no round trip until it is called
+            return RemoteMethod(obj, name)
+        v = self.command(("getattr", obj, name), what=f"{obj._tname}.{name}")
+        if isinstance(v, _BoundMethod):
+            self._methods.add(key)
+            return RemoteMethod(obj, name)
+        return v
+
+    def call(self, obj, name: str, args=(), kwargs=None):
+        return self.command(("call", obj, name, tuple(args), dict(kwargs or {})),
+                            what=f"{getattr(obj, '_tname', type(obj).__name__)}.{name}")
+
+    def apply(self, fn, *args, **kwargs):
+        return self.command(("apply", fn, args, kwargs), what=getattr(fn, "__name__", "apply"))
+
+    def scatter_dataframe(self, pdf, schema=None):
+        """Row slice r of a host pandas frame -> executor r (only that slice is sent)."""
+        n = len(pdf)
+        parts = [pdf.iloc[(n * r) // self.n:(n * (r + 1)) // self.n] for r in range(self.n)]
+        return self.command(None, per_rank=[("scatter_df", p, schema) for p in parts], what="createDataFrame")
+
+    def info(self):
+        return self.command(("info",))
+
+    # ---------------------------------------------------------------- lifecycle
+    def shutdown(self, timeout: float = 30.0):
+        with self._lock:
+            if not self.alive:
+                return
+            self.alive = False
+            hdr = pickle.dumps([])
+            for c in self._conns:
+                try:
+                    c.send_bytes(len(hdr).to_bytes(8, "little") + hdr + pickle.dumps(("stop",)))
+                except (BrokenPipeError, OSError):
+                    pass
+            for p in self._procs:
+                p.join(timeout)
+            self._teardown()
+
+    def _teardown(self):
+        self.alive = False
+        for p in self._procs:
+            if p.is_alive():
+                p.terminate()
+        for p in self._procs:
+            p.join(10)
+            if p.is_alive():
+                p.kill()
+                p.join(5)
+        for c in self._conns:
+            try:
+                if c is not None:
+                    c.close()
+            except OSError:
+                pass
+
+    def __del__(self):
+        try:
+            self._teardown()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def _shutdown_all():
+    for p in list(ExecutorPool._pools):
+        try:
+            p.shutdown(timeout=10)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+import atexit  # noqa: E402
+
+atexit.register(_shutdown_all)
+
+
+# =====================================================================================
+# handles
+# =====================================================================================
+_BINOPS = ("__add__", "__radd__", "__sub__", "__rsub__", "__mul__", "__rmul__", "__truediv__", "__rtruediv__",
+           "__floordiv__", "__mod__", "__rmod__", "__pow__", "__rpow__", "__lt__", "__le__", "__gt__", "__ge__",
+           "__and__", "__rand__", "__or__", "__ror__", "__eq__", "__ne__", "__getitem__", "__contains__")
+_UNOPS = ("__neg__", "__invert__", "__abs__")
+
+
+class RemoteObject:
+    """Driver-side handle of an object that lives on every executor (same id on each)."""
+
+    __slots__ = ("_pool", "_id", "_tname", "__weakref__")
+
+    def __init__(self, pool: ExecutorPool, k: int, tname: str):
+        object.__setattr__(self, "_pool", pool)
+        object.__setattr__(self, "_id", k)
+        object.__setattr__(self, "_tname", tname)
+
+    def __getattr__(self, name):
+        if name.startswith("__") and name.endswith("__"):
+            raise AttributeError(name)
+        return self._pool.getattr(self, name)
+
+    def __setattr__(self, name, value):
+        self._pool.call(_Setattr(), "set", (self, name, value))
+
+    def __call__(self, *args, **kwargs):
+        return self._pool.call(self, "__call__", args, kwargs)
+
+    def __repr__(self):
+        return f"<remote {self._tname} #{self._id} on {self._pool.n} executors>"
+
+    def __hash__(self):
+        return hash((id(self._pool), self._id))
+
+    def __bool__(self):
+        return True
+
+    def __iter__(self):
+        return iter(self._pool.apply(_to_list, self))
+
+    def __len__(self):
+        return int(self._pool.apply(_global_len, self))
+
+    def __reduce__(self):
+        raise TypeError("executor handles cannot be pickled outside their pool")
+
+
+def _make_op(name):
+    def op(self, *args):
+        return self._pool.call(self, name, args)
+    op.__name__ = name
+    return op
+
+
+for _n in _BINOPS + _UNOPS:
+    setattr(RemoteObject, _n, _make_op(_n))
+
+
+class _Setattr:
+    """Shipped helper: setattr on the executor-side object."""
+
+    @staticmethod
+    def set(obj, name, value):
+        setattr(obj, name, value)
+
+
+def _to_list(obj):
+    return list(obj)
+
+
+def _global_len(obj):
+    cnt = getattr(obj, "count", None)
+    if callable(cnt):
+        try:
+            v = cnt()
+            if isinstance(v, int):
+                return v
+        except TypeError:
+            pass
+    return len(obj)
+
+
+class RemoteMethod:
+    __slots__ = ("_obj", "_name")
+
+    def __init__(self, obj, name):
+        self._obj, self._name = obj, name
+
+    def __call__(self, *args, **kwargs):
+        return self._obj._pool.call(self._obj, self._name, args, kwargs)
+
+    def __repr__(self):
+        return f"<remote method {self._obj._tname}.{self._name}>"
+
+
+def _dataframe_class():
+    from ..frame.dataframe import DataFrame
+    return DataFrame
+
+
+class RemoteDataFrame(RemoteObject):
+    """Handle of a row-sharded DataFrame held by the executors.  ``isinstance(h, DataFrame)``
+    is true (``__class__`` reports DataFrame) so widget channels typed DataFrame accept it;
+    every DataFrame method runs on the executors."""
+
+    __slots__ = ()
+
+    @property
+    def __class__(self):
+        return _dataframe_class()
+
+    @property
+    def pool(self):
+        return self._pool
+
+    def __repr__(self):
+        try:
+            cols = self._pool.getattr(self, "columns")
+        except Exception:  # noqa: BLE001
+            cols = "?"
+        return f"DataFrame[{cols}] (on {self._pool.n} executors)"
+
+
+def is_remote(obj) -> bool:
+    return type(obj) in (RemoteObject, RemoteDataFrame)
+
+
+def remote_pool_of(*objs):
+    """The executor pool of the first handle among ``objs`` (recursing into lists/dicts)."""
+    for o in objs:
+        if type(o) in (RemoteObject, RemoteDataFrame):
+            return o._pool
+        if isinstance(o, (list, tuple)):
+            p = remote_pool_of(*o)
+            if p is not None:
+                return p
+        if isinstance(o, dict):
+            p = remote_pool_of(*o.values())
+            if p is not None:
+                return p
+    return None
+
+
+def ship(fn):
+    """Decorator for free functions taking DataFrames (stat tests, correlation, ...): called
+    with executor handles, the function itself runs on the executors."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        pool = remote_pool_of(args, kwargs)
+        if pool is not None:
+            return pool.apply(fn, *args, **kwargs)
+        return fn(*args, **kwargs)
+    return wrapper
+
+
+if __name__ == "__main__":
+    # run the entry from the package module (not this __main__ copy), so every class the
+    # executor pickles back (_BoundMethod, ...) is the driver's class
+    import sys as _sys
+    from orange3_spark_amd.runtime import executors as _executors
+    _sys.exit(_executors._worker_entry())

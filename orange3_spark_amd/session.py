@@ -32,9 +32,26 @@ log = logging.getLogger("orange3_spark_amd")
 __version__ = "0.1.0"
 
 
+def _wants_pool(conf) -> bool:
+    """``spark.executor.instances = N > 1`` outside an SPMD launch -> driver + N executors."""
+    import os
+    if conf is None or os.environ.get("WORLD_SIZE") not in (None, "", "1"):
+        return False
+    try:
+        n = int(float(conf.get("spark.executor.instances", "1")))
+    except (TypeError, ValueError):
+        return False
+    return n > 1 and conf.master().lower() != "spmd"
+
+
 class Session:
     _active: "Session | None" = None
-    _lock = threading.Lock()
+    _lock = threading.RLock()
+
+    def __new__(cls, conf: SessionConf | None = None, comm=None, device=None):
+        if cls is Session and comm is None and device is None and _wants_pool(conf):
+            return object.__new__(DriverSession)
+        return object.__new__(cls)
 
     def __init__(self, conf: SessionConf | None = None, comm=None, device=None):
         self.conf = conf.copy() if conf is not None else SessionConf()
@@ -46,9 +63,10 @@ class Session:
                 if (world > 1 or master == "spmd") else LocalComm(self.device)
         self.comm = comm
         if self.conf.get("spark.master", "").lower() == "spmd":
-            want = int(self.conf.get("spark.executor.instances", str(self.comm.world_size)))
+            want = int(float(self.conf.get("spark.executor.instances", str(self.comm.world_size))))
             if want not in (1, self.comm.world_size):
-                log.warning("spark.executor.instances=%s but WORLD_SIZE=%s", want, self.comm.world_size)
+                raise ValueError(f"spark.executor.instances={want} but this SPMD launch has "
+                                 f"WORLD_SIZE={self.comm.world_size} ranks")
         from .catalog import Catalog
         self.catalog = Catalog(self)
         self._stopped = False
@@ -172,14 +190,20 @@ class Session:
         r, w = self.comm.rank, self.comm.world_size
         return (n * r) // w, (n * (r + 1)) // w
 
-    def createDataFrame(self, data, schema=None, samplingRatio=None, verifySchema=True) -> DataFrame:
+    def createDataFrame(self, data, schema=None, samplingRatio=None, verifySchema=True, _local=False,
+                        scatter_from: int | None = None) -> DataFrame:
         """Create a row-sharded DataFrame from host data.
 
         Accepts a pandas DataFrame, a pyarrow Table, a list of Rows/tuples/dicts, a
         2-D numpy array, a dict of column arrays, or an Orange-style Table (anything
-        with ``domain``/``X``).  Every rank is given the same host data (SPMD) and
-        keeps its contiguous slice.
+        with ``domain``/``X``).  SPMD: by default every rank is given the same host data and
+        keeps its contiguous slice; ``scatter_from=r`` means only rank r holds the table
+        (the others pass None) and each rank receives just its slice (host memory per rank
+        ~ 1/N).  ``_local``: the data already is this rank's slice (executor scatter).
+        Numeric columns reach the GPU through pinned staging buffers.
         """
+        if scatter_from is not None and self.comm.world_size > 1:
+            return self._scatter_create(data, schema, int(scatter_from))
         from .io import arrow_to_columns
         from .utils import data_utils
         import pandas as pd
@@ -195,7 +219,7 @@ class Session:
             data = data_utils.orange_to_pandas(data)
         if pa is not None and isinstance(data, pa.Table):
             n = data.num_rows
-            lo, hi = self._shard_bounds(n)
+            lo, hi = (0, n) if _local else self._shard_bounds(n)
             cols = arrow_to_columns(data.slice(lo, hi - lo), self)
             return DataFrame(self, cols, hi - lo)
         if isinstance(data, dict):
@@ -214,7 +238,7 @@ class Session:
             data = data.copy()
             data.columns = names
         n = len(data)
-        lo, hi = self._shard_bounds(n)
+        lo, hi = (0, n) if _local else self._shard_bounds(n)
         part = data.iloc[lo:hi]
         cols = OrderedDict()
         for k in part.columns:
@@ -226,6 +250,30 @@ class Session:
                 if f.name in df.columns and isinstance(f.dataType, NumericType):
                     df = df.withColumn(f.name, df[f.name].cast(f.dataType))
         return df
+
+    def _scatter_create(self, data, schema, src: int) -> DataFrame:
+        """Rank ``src`` splits its host table into per-rank row slices and sends slice r to
+        rank r (one object all-to-all); no rank but ``src`` ever holds the whole table."""
+        from .utils import data_utils
+        import pandas as pd
+        w = self.comm.world_size
+        parts = [None] * w
+        if self.comm.rank == src:
+            if hasattr(data, "domain") and hasattr(data, "X"):
+                data = data_utils.orange_to_pandas(data)
+            elif isinstance(data, dict):
+                data = pd.DataFrame(data)
+            elif isinstance(data, (list, tuple)):
+                data = _rows_to_pandas(list(data), _schema_names(schema))
+            elif isinstance(data, np.ndarray):
+                data = pd.DataFrame(data if data.ndim == 2 else data[:, None])
+            n = len(data)
+            parts = [data.iloc[(n * r) // w:(n * (r + 1)) // w] for r in range(w)]
+        send = parts if self.comm.rank == src else [None] * w
+        got = self.comm.all_to_all_object(send)
+        part = got[src]
+        del parts, send, got, data
+        return self.createDataFrame(part, schema, _local=True)
 
     def range(self, start: int, end: int | None = None, step: int = 1, numPartitions=None) -> DataFrame:
         if end is None:
@@ -268,6 +316,136 @@ class Session:
     def __repr__(self):
         return (f"Session(app={self.appName!r}, device={self.device}, rank={self.rank}/"
                 f"{self.world_size}, backend={self.comm.backend})")
+
+
+class DriverSession(Session):
+    """Driver of an executor pool (runtime/executors.py): this process keeps no rows and
+    never touches a GPU; ``spark.executor.instances`` worker processes (one per MI355X, an
+    RCCL group over xGMI) hold the data and run every operation.  DataFrames are handles
+    (``RemoteDataFrame``); fits return ordinary local models.  Reference: the Context
+    widget's executor sizing (orangecontrib/spark/widgets/data/spark_context.py:41-42,76)."""
+
+    def __init__(self, conf: SessionConf | None = None, comm=None, device=None):
+        from .runtime.executors import ExecutorPool
+        self.conf = conf.copy() if conf is not None else SessionConf()
+        self.device = torch.device("cpu")
+        self.comm = LocalComm(self.device)
+        n = int(float(self.conf.get("spark.executor.instances", "1")))
+        timeout = self.conf.get("o3s.executor.timeout", None)
+        self.pool = ExecutorPool(n, self.conf.getAll(),
+                                 command_timeout=float(timeout) if timeout not in (None, "", "0") else None,
+                                 error_grace=float(self.conf.get("o3s.executor.errorGrace", "20")))
+        self._remote = self.pool._proxy(0, "Session", False)
+        self.catalog = self._remote.catalog
+        self._stopped = False
+        self.version = __version__
+
+    # --- lifecycle ------------------------------------------------------------------
+    def stop(self) -> None:
+        if not self._stopped:
+            self.pool.shutdown()
+        super().stop()
+
+    @property
+    def executors(self) -> int:
+        return self.pool.n
+
+    @property
+    def world_size(self) -> int:
+        return self.pool.n
+
+    @property
+    def defaultParallelism(self) -> int:
+        return self.pool.n
+
+    def executor_info(self) -> dict:
+        d = self.pool.info()
+        d["devices"] = list(self.pool.devices)
+        return d
+
+    def __repr__(self):
+        devs = self.pool.devices
+        span = devs[0] if len(set(devs)) == 1 else f"{devs[0]}..{devs[-1]}"
+        return (f"Session(app={self.appName!r}, executors={self.pool.n} [{span}], driver=cpu, "
+                f"alive={self.pool.alive})")
+
+    # --- data sources (all executed on the executors) ---------------------------------
+    def createDataFrame(self, data, schema=None, samplingRatio=None, verifySchema=True, **_):
+        """Host data -> executors: executor r receives only its row slice (scatter)."""
+        from .rdd import RDD  # noqa: F401 - type check below
+        from .runtime.executors import is_remote
+        from .utils import data_utils
+        import pandas as pd
+        if is_remote(data):                       # an executor RDD / frame
+            return self._remote.createDataFrame(data, schema)
+        if hasattr(data, "domain") and hasattr(data, "X"):
+            data = data_utils.orange_to_pandas(data)
+        try:
+            import pyarrow as pa
+            if isinstance(data, pa.Table):
+                data = data.to_pandas()
+        except ImportError:  # pragma: no cover
+            pass
+        names = _schema_names(schema)
+        if isinstance(data, dict):
+            data = pd.DataFrame(data)
+        if isinstance(data, np.ndarray):
+            data = pd.DataFrame(data if data.ndim == 2 else data[:, None],
+                                columns=names or [f"_{i + 1}" for i in range(data.shape[1] if data.ndim == 2 else 1)])
+            names = None
+        if isinstance(data, (list, tuple)):
+            data = _rows_to_pandas(list(data), names)
+            names = None
+        if not isinstance(data, pd.DataFrame):
+            raise TypeError(f"cannot create a DataFrame from {type(data).__name__}")
+        return self.pool.scatter_dataframe(data, schema)
+
+    def range(self, start, end=None, step=1, numPartitions=None):
+        return self._remote.range(start, end, step, numPartitions)
+
+    def emptyDataFrame(self):
+        return self._remote.emptyDataFrame()
+
+    def table(self, name):
+        return self._remote.table(name)
+
+    def sql(self, query):
+        return self._remote.sql(query)
+
+    def tableNames(self, dbName=None):
+        return self._remote.tableNames(dbName)
+
+    def tables(self, dbName=None):
+        return self._remote.tables(dbName)
+
+    @property
+    def read(self):
+        return self._remote.read
+
+    @property
+    def synthetic(self):
+        return self._remote.synthetic
+
+    @property
+    def sparkContext(self):
+        return self._remote.sparkContext
+
+    @property
+    def udf(self):
+        return self._remote.udf
+
+    def parallelize(self, c, numSlices=None):
+        return self._remote.parallelize(c, numSlices)
+
+    def setCheckpointDir(self, dirName):
+        super().setCheckpointDir(dirName)
+        self._remote.setCheckpointDir(dirName)
+
+    def health_check(self, timeout_s: float = 30.0) -> dict:
+        return self._remote.health_check(timeout_s)
+
+    def local_view(self):
+        raise RuntimeError("the driver of an executor pool holds no rows (use the executors' session)")
 
 
 SparkSession = Session

@@ -49,9 +49,9 @@ def test_timeout_tears_down_hung_rank():
         return 0
 
     t0 = time.monotonic()
-    with pytest.raises(RuntimeError, match=r"timed out .*ranks \[1\]"):
-        TorchDistributor(num_processes=2, use_gpu=False, timeout=8).run(hang)
-    assert time.monotonic() - t0 < 60
+    with pytest.raises(RuntimeError, match=r"timed out .*ranks \[(0, )?1\]"):
+        TorchDistributor(num_processes=2, use_gpu=False, timeout=30).run(hang)
+    assert time.monotonic() - t0 < 120
 
 
 def test_script_mode(tmp_path):
