@@ -151,6 +151,9 @@ class VectorAssembler(Transformer, HasInputCols, HasOutputCol, HasHandleInvalid,
         cols = self.getOrDefault(self.inputCols)
         n = len(df)
         dev = df.device
+        fused = self._transform_fused(df, cols, n)
+        if fused is not None:
+            return fused
         mats = [_as_matrix(df.column_data(c), n, dev) for c in cols]
         mat = torch.cat(mats, dim=1) if mats else torch.zeros((n, 0), dtype=torch.float64, device=dev)
         hi = self.getOrDefault(self.handleInvalid)
@@ -163,6 +166,38 @@ class VectorAssembler(Transformer, HasInputCols, HasOutputCol, HasHandleInvalid,
                 df = df._mask(~bad)
                 mat = mat[~bad]
         return df.withColumnData(self.getOrDefault(self.outputCol), to_vector_column(df.session, mat))
+
+    def _transform_fused(self, df, cols, n):
+        """GPU, bf16 feature storage: ONE gather kernel (ops/assemble.py) reads every input
+        column once (any numeric dtype, null masks, vector columns) and writes the padded
+        bf16 matrix once, flagging invalid rows in the same pass; None -> torch path."""
+        from ..ops import assemble as A
+        from ..synthetic import LineageVectorColumn
+        if df.device.type != "cuda" or df.session.vector_dtype() != torch.bfloat16 or not cols or n == 0 \
+                or len(cols) > A.MAX_SOURCES:
+            return None
+        srcs = []
+        for c in cols:
+            col = df.column_data(c)
+            if isinstance(col, C.NumericColumn) and A.supported(col.data) and col.data.dim() == 1:
+                srcs.append((col.data.contiguous(), col.valid, 1))
+            elif isinstance(col, C.VectorColumn) and not isinstance(col, (C.SparseVectorColumn, LineageVectorColumn)) \
+                    and A.supported(col.data) and col.data.dim() == 2:
+                srcs.append((col.data, None, int(col.size)))
+            else:
+                return None
+        out, bad, nbad, D = A.assemble_bf16(srcs, n, df.device)
+        nb = int(nbad.item())
+        if nb:
+            hi = self.getOrDefault(self.handleInvalid)
+            if hi == "error":
+                raise ValueError("Encountered null while assembling a row with handleInvalid = \"error\". "
+                                 "Consider removing nulls from dataset or using handleInvalid = \"keep\" or \"skip\".")
+            if hi == "skip":
+                keep = bad == 0
+                df = df._mask(keep)
+                out = out[keep]
+        return df.withColumnData(self.getOrDefault(self.outputCol), C.VectorColumn(out, D))
 
 
 @register("org.apache.spark.ml.feature.VectorSlicer")

@@ -1,0 +1,143 @@
+// VectorAssembler in one pass (gfx950): k numeric / vector columns of any dtype, with
+// null masks, gathered straight into the padded row-major feature matrix the GLM / tree /
+// k-means kernels consume (bf16 [n, ld], ld % 8 == 0, zero padded; or fp32).
+//
+// Reference: the Dataset Builder widget's commit, VectorAssembler(inputCols=features,
+// outputCol='features').transform(df) (orangecontrib/spark/widgets/ml/spark_ml_dataset.py:
+// 575-576) -- the first compute step of the tutorial chain.  The torch composition it
+// replaces (per-column fp64 casts, a concat, an isnan pass, a padded bf16 copy) moved
+// ~5 passes and 8 B/element of scratch; here every input byte is read once and every
+// output byte written once.
+//
+// Mapping: a 256-thread block owns 64 consecutive rows; lane r of each wave is row
+// row0 + r, and the block's 4 waves take the row's 16-B output chunks round robin.  All
+// 64 lanes of a wave work on the same output chunk, so the per-column source lookup
+// (column map in LDS) and the dtype switch are wave-uniform, and the reads of a columnar
+// source are 64 consecutive elements (coalesced).  The 64 rows x ld block of output is
+// written by the block within a short window, so L2 merges the 16-B row segments into
+// full lines before write-back.
+//
+// handleInvalid: a row is invalid if any of its values is null (mask) or NaN; the kernel
+// writes a per-row flag and adds the block's count to *nbad (one integer atomic per
+// block).  Invalid values are stored as NaN ("keep" semantics); the caller raises
+// ("error") or compacts ("skip") using the count.
+#include <hip/hip_fp16.h>
+
+#include "common.h"
+
+using namespace o3s;
+
+namespace {
+
+enum { DT_F64 = 0, DT_F32 = 1, DT_BF16 = 2, DT_F16 = 3, DT_I64 = 4, DT_I32 = 5, DT_I16 = 6, DT_I8 = 7, DT_U8 = 8,
+       DT_BOOL = 9 };
+
+struct AsmSrc {
+  const void* ptr;          // column data: [n] (width 1) or row-major [n, stride] (vector)
+  const uint8_t* valid;     // optional per-row validity (1 = valid), null = all valid
+  int64_t stride;           // elements between consecutive rows (1 for a scalar column)
+  int32_t width;            // values contributed per row
+  int32_t dtype;
+};
+
+constexpr int kRows = 64;
+constexpr int kThreads = 256;
+constexpr int kMaxSrc = 512;
+
+__device__ __forceinline__ float load_as_float(const AsmSrc& s, int64_t row, int e) {
+  const int64_t i = row * s.stride + e;
+  switch (s.dtype) {
+    case DT_F64: return (float)reinterpret_cast<const double*>(s.ptr)[i];
+    case DT_F32: return reinterpret_cast<const float*>(s.ptr)[i];
+    case DT_BF16: return bf16_to_f32(reinterpret_cast<const uint16_t*>(s.ptr)[i]);
+    case DT_F16: return __half2float(reinterpret_cast<const __half*>(s.ptr)[i]);
+    case DT_I64: return (float)reinterpret_cast<const int64_t*>(s.ptr)[i];
+    case DT_I32: return (float)reinterpret_cast<const int32_t*>(s.ptr)[i];
+    case DT_I16: return (float)reinterpret_cast<const int16_t*>(s.ptr)[i];
+    case DT_I8: return (float)reinterpret_cast<const int8_t*>(s.ptr)[i];
+    default: return (float)reinterpret_cast<const uint8_t*>(s.ptr)[i];     // u8 / bool
+  }
+}
+
+// colmap[j] = (source index, element within source) for output column j < D; j >= D: pad.
+template <int OUT>   // 0: bf16 out, 1: fp32 out
+__global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmSrc* __restrict__ srcs, int nsrc,
+                                                            const int2* __restrict__ colmap, int D, int ld,
+                                                            int64_t n, void* __restrict__ out,
+                                                            uint8_t* __restrict__ bad, int* __restrict__ nbad) {
+  __shared__ AsmSrc s_src[kMaxSrc];
+  __shared__ uint8_t s_bad[kRows];
+  for (int i = threadIdx.x; i < nsrc; i += kThreads) s_src[i] = srcs[i];
+  if (threadIdx.x < kRows) s_bad[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  const int nch = ld / 8;
+  const int64_t nblk = (n + kRows - 1) / kRows;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t row = blk * kRows + lane;
+    const bool ok = row < n;
+    const int64_t rowc = ok ? row : n - 1;
+    bool rbad = false;
+    for (int ch = wid; ch < nch; ch += kThreads / kWave) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int j = 8 * ch + q;
+        float x = 0.f;
+        if (j < D) {                                  // wave-uniform
+          const int2 m = colmap[j];
+          const AsmSrc& s = s_src[m.x];
+          x = load_as_float(s, rowc, m.y);
+          const bool valid = s.valid == nullptr || s.valid[rowc] != 0;
+          if (!valid) x = __builtin_nanf("");
+          rbad |= !(x == x);
+        }
+        v[q] = x;
+      }
+      if (ok) {
+        if (OUT == 0) {
+          short8 o;
+#pragma unroll
+          for (int q = 0; q < 8; ++q) o[q] = (short)f32_to_bf16(v[q]);
+          *reinterpret_cast<short8*>(reinterpret_cast<uint16_t*>(out) + row * ld + 8 * ch) = o;
+        } else {
+          float* po = reinterpret_cast<float*>(out) + row * ld + 8 * ch;
+          *reinterpret_cast<float4_*>(po) = float4_{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<float4_*>(po + 4) = float4_{v[4], v[5], v[6], v[7]};
+        }
+      }
+    }
+    if (ok && rbad) s_bad[lane] = 1;                  // benign race: every writer stores 1
+    __syncthreads();
+    if (wid == 0) {
+      const int b = (ok && s_bad[lane]) ? 1 : 0;
+      if (ok && bad) bad[row] = (uint8_t)b;
+      const int cnt = wave_sum_i(b);
+      if (lane == 0 && cnt) atomicAdd(nbad, cnt);
+      s_bad[lane] = 0;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+// srcs: device array of nsrc AsmSrc; colmap: device int2[D]; out: [n, ld] (bf16 when
+// out_f32 == 0, else fp32), ld % 8 == 0, ld >= D; bad: optional uint8[n]; nbad: int (zeroed
+// by the caller).
+O3S_API int o3s_assemble(const void* srcs, int nsrc, const void* colmap, int D, int ld, int64_t n, void* out,
+                         int out_f32, void* bad, void* nbad, int grid, hipStream_t st) {
+  if (nsrc <= 0 || nsrc > kMaxSrc || ld % 8 != 0 || ld < D || n < 0 || grid <= 0) return -1;
+  if (n == 0) return 0;
+  if (out_f32)
+    hipLaunchKernelGGL(assemble_kernel<1>, dim3(grid), dim3(kThreads), 0, st, (const AsmSrc*)srcs, nsrc,
+                       (const int2*)colmap, D, ld, n, out, (uint8_t*)bad, (int*)nbad);
+  else
+    hipLaunchKernelGGL(assemble_kernel<0>, dim3(grid), dim3(kThreads), 0, st, (const AsmSrc*)srcs, nsrc,
+                       (const int2*)colmap, D, ld, n, out, (uint8_t*)bad, (int*)nbad);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+O3S_API int o3s_assemble_src_size() { return (int)sizeof(AsmSrc); }

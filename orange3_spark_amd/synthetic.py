@@ -177,6 +177,32 @@ class SyntheticData:
         df.synthetic_spec = spec
         return df
 
+    def table(self, numRows: int, numFeatures: int, seed: int = 42, dtype=torch.float32,
+              prefix: str = "f") -> DataFrame:
+        """A wide columnar table (what a parquet / Hive table read gives): one numeric column
+        per feature (``f0..f{d-1}``, ``dtype``) and a float ``label`` -- the same rows as
+        :meth:`classification` (so the assembled features equal its feature vectors), but
+        stored column by column, for the DatasetBuilder -> VectorAssembler path."""
+        s = self.session
+        d = G.padded_width(numFeatures)
+        wt, bt = G.synth_truth(seed, numFeatures, d)
+        lo, hi = self._bounds(numRows)
+        n = hi - lo
+        dev = s.device
+        cols = [torch.empty(n, dtype=dtype, device=dev) for _ in range(numFeatures)]
+        y = torch.empty(n, dtype=torch.float32, device=dev)
+        step = 1 << 23 if dev.type == "cuda" else 1 << 16
+        for a in range(0, n, step):
+            b = min(n, a + step)
+            Xc, yc = G.synth_glm(b - a, d, seed, lo + a, dev, d, wt, bt)
+            for j in range(numFeatures):
+                cols[j][a:b] = Xc[:, j]
+            y[a:b] = yc
+            del Xc
+        out = OrderedDict((f"{prefix}{j}", C.NumericColumn(cols[j])) for j in range(numFeatures))
+        out["label"] = C.NumericColumn(y)
+        return DataFrame(s, out, n)
+
     def blobs(self, numRows: int, numFeatures: int, k: int, seed: int = 42, spread: float = 1.0,
               dtype=torch.float32) -> DataFrame:
         """Gaussian blobs around k centres (KMeans config): ``features`` f32 [n, d]."""

@@ -233,3 +233,54 @@ def test_spmd_scatter_ingest_keeps_host_memory_per_rank(tmp_path):
     assert r0["local"] == r1["local"] == 500_000 and r0["count"] == 1_000_000
     assert r1["peak"] < 0.75 * table, r1["peak"]          # ~half the table (+ framing)
     assert r0["sum"] == pytest.approx(float(np.random.default_rng(1).normal(size=1_000_000).sum()), rel=1e-9)
+
+
+@pytest.mark.gpu
+def test_gpu_pool_fits_and_transforms(monkeypatch):
+    """Two executors sharing cuda:0 (gloo; RCCL needs a GPU per rank): the headline
+    estimators fit through handles, the returned local models (host tensors) transform
+    executor frames again, and the results match a single-process GPU session."""
+    monkeypatch.setenv("O3S_DIST_BACKEND", "gloo")
+    from orange3_spark_amd.ml.classification import GBTClassifier, LogisticRegression
+    from orange3_spark_amd.ml.clustering import KMeans
+    from orange3_spark_amd.ml.evaluation import BinaryClassificationEvaluator
+    from orange3_spark_amd.ml.recommendation import ALS
+
+    def run(s):
+        out = {}
+        df = s.synthetic.classification(200_000, 64, seed=3)
+        lr = LogisticRegression(maxIter=10).fit(df)
+        out["lr"] = lr.coefficients.toArray()
+        out["auc"] = BinaryClassificationEvaluator().evaluate(lr.transform(df))
+        sgd = LogisticRegression(solver="sgd", maxIter=5, tol=0.0).fit(df)
+        out["sgd"] = sgd.coefficients.toArray()
+        blobs = s.synthetic.blobs(50_000, 16, k=8, seed=2)
+        km = KMeans(k=8, seed=1, maxIter=5).fit(blobs)
+        out["km"] = km.summary.trainingCost
+        out["km_pred"] = km.transform(blobs).select("prediction").toPandas()["prediction"].to_numpy()[:100]
+        trees = s.synthetic.trees(60_000, 8, seed=4)
+        gbt = GBTClassifier(maxIter=3, maxDepth=4, seed=1).fit(trees)
+        out["gbt_auc"] = BinaryClassificationEvaluator().evaluate(gbt.transform(trees))
+        r = s.synthetic.ratings(500, 300, 20_000, rank=4, seed=5)
+        als = ALS(rank=4, maxIter=3, seed=1).fit(r)
+        out["als"] = als.transform(r).select("prediction").toPandas()["prediction"].to_numpy()[:50]
+        return out
+
+    monkeypatch.delenv("O3S_DIST_BACKEND")
+    local = Session(SessionConf().setAppName("local"))
+    try:
+        a = run(local)
+    finally:
+        local.stop()
+    monkeypatch.setenv("O3S_DIST_BACKEND", "gloo")
+    pool = Session(SessionConf().set("spark.executor.instances", "2"))
+    try:
+        assert type(pool).__name__ == "DriverSession" and all(d.startswith("cuda") for d in pool.pool.devices)
+        b = run(pool)
+    finally:
+        pool.stop()
+    assert np.allclose(a["lr"], b["lr"], atol=1e-4) and abs(a["auc"] - b["auc"]) < 1e-4
+    assert np.allclose(a["sgd"], b["sgd"], rtol=1e-4, atol=1e-6)
+    assert a["km"] == pytest.approx(b["km"], rel=1e-6) and (a["km_pred"] == b["km_pred"]).all()
+    assert abs(a["gbt_auc"] - b["gbt_auc"]) < 1e-3
+    assert np.allclose(a["als"], b["als"], atol=1e-3)

@@ -175,3 +175,59 @@ def test_gpu_tokenizer_and_hashingtf_match_host():
     # downstream host consumers still work on the lazily decoded lists
     sw = F.StopWordsRemover(inputCol="words", outputCol="clean").transform(tok)
     assert sw.count() == len(texts)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("handle", ["keep", "skip", "error"])
+def test_gpu_vector_assembler_fused_kernel_matches_torch(handle):
+    """The one-pass assemble kernel (any dtype, null masks, vector inputs, padded bf16 out)
+    == the torch composition on the same columns, for every handleInvalid mode."""
+    import numpy as np
+    import torch
+    from collections import OrderedDict
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.frame import column as C
+    from orange3_spark_amd.frame.dataframe import DataFrame
+    from orange3_spark_amd.ml.feature import VectorAssembler
+    dev = torch.device("cuda", 0)
+    s = Session(SessionConf().setAppName("asm"), device=dev)
+    g = torch.Generator().manual_seed(1)
+    n = 100_003
+    f64 = torch.randn(n, generator=g, dtype=torch.float64)
+    f32 = torch.randn(n, generator=g)
+    i64 = torch.randint(-5, 5, (n,), generator=g)
+    i32 = torch.randint(0, 100, (n,), generator=g, dtype=torch.int32)
+    bo = torch.rand(n, generator=g) > 0.5
+    vec = torch.randn((n, 12), generator=g).to(torch.bfloat16)
+    vec_pad = torch.zeros((n, 16), dtype=torch.bfloat16)
+    vec_pad[:, :12] = vec
+    valid = torch.ones(n, dtype=torch.bool)
+    if handle != "keep" or True:
+        valid[::997] = False
+    f64[5] = float("nan")
+    cols = OrderedDict(a=C.NumericColumn(f64.to(dev)), b=C.NumericColumn(f32.to(dev), valid.to(dev)),
+                       c=C.NumericColumn(i64.to(dev)), d=C.NumericColumn(i32.to(dev)), e=C.NumericColumn(bo.to(dev)),
+                       v=C.VectorColumn(vec_pad.to(dev), 12), lab=C.NumericColumn(torch.arange(n, dtype=torch.float64).to(dev)))
+    df = DataFrame(s, cols, n)
+    va = VectorAssembler(inputCols=["a", "b", "c", "d", "e", "v"], outputCol="f", handleInvalid=handle)
+    ref_rows = torch.stack([f64, torch.where(valid, f32.double(), torch.full_like(f64, float("nan"))), i64.double(),
+                            i32.double(), bo.double()], 1)
+    ref = torch.cat([ref_rows, vec.double()], 1)
+    bad = torch.isnan(ref).any(1)
+    if handle == "error":
+        with pytest.raises(ValueError, match="handleInvalid"):
+            va.transform(df)
+        return
+    out = va.transform(df)
+    col = out.column_data("f")
+    assert col.size == 17 and col.data.dtype == torch.bfloat16 and col.data.shape[1] == 24
+    got = col.data.cpu()
+    want = ref[~bad] if handle == "skip" else ref
+    assert got.shape[0] == want.shape[0]
+    assert torch.equal(got[:, 17:], torch.zeros_like(got[:, 17:]))          # zero padding
+    w = want.to(torch.bfloat16)
+    same = (got[:, :17] == w) | (torch.isnan(got[:, :17].float()) & torch.isnan(w.float()))
+    assert bool(same.all())
+    if handle == "skip":
+        kept = out.column_data("lab").data.cpu().long()
+        assert torch.equal(kept, torch.nonzero(~bad).squeeze(1))
