@@ -41,6 +41,18 @@ class OWScript(SharedSession, Widget):
         del self.libraryListSource[index]
         self.currentScriptIndex = max(0, min(self.currentScriptIndex, len(self.libraryListSource) - 1))
 
+    def select_script(self, index):
+        """Show library entry ``index`` in the editor (discarding unsaved edits)."""
+        if 0 <= index < len(self.libraryListSource):
+            self.currentScriptIndex = index
+            self.scriptText = None
+
+    def update_script(self, index, script):
+        """Store the editor text into library entry ``index``."""
+        if 0 <= index < len(self.libraryListSource):
+            self.libraryListSource[index] = dict(self.libraryListSource[index], script=script)
+            self.scriptText = None
+
     def current_script(self) -> str:
         if self.scriptText is not None:
             return self.scriptText

@@ -55,6 +55,23 @@ class OWDatasetBuilder(Widget):
     def set_metas(self, names):
         self._move(names, self.meta_attrs)
 
+    def move_to_available(self, names):
+        """Return columns from any role list to the available list (canvas "< Available")."""
+        self._move(names, self.available_attrs)
+
+    def move_feature(self, name, delta: int):
+        """Reorder the features list (canvas Up / Down): the assembled vector follows it."""
+        if name in self.used_attrs:
+            i = self.used_attrs.index(name)
+            j = max(0, min(len(self.used_attrs) - 1, i + int(delta)))
+            self.used_attrs.insert(j, self.used_attrs.pop(i))
+
+    def filtered_available(self, pattern: str = "") -> list:
+        """Available columns whose name contains every whitespace-separated word of
+        ``pattern`` (case-insensitive) -- the reference's filter line edit (:537-567)."""
+        words = [w.lower() for w in (pattern or "").split()]
+        return [c for c in self.available_attrs if all(w in c.lower() for w in words)]
+
     def update_domain_role_hints(self):
         if self.in_df is not None:
             self.domain_role_hints[tuple(self.in_df.columns)] = {

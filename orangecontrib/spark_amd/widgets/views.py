@@ -146,8 +146,16 @@ def qt_view(core_cls, orange=None):
 
     # -- controls ---------------------------------------------------------------------
     def _build_controls(self):
+        from .custom_views import BUILDERS
+        covered = set()
+        self._custom_refresh = None
+        builder = BUILDERS.get(core_cls.__name__)
+        if builder is not None:                # hand-written list / editor controls
+            covered, self._custom_refresh = builder(self, orange)
         box = orange.gui.widgetBox(self.controlArea, "Settings")
         for k, st in core_settings.items():
+            if k in covered:
+                continue
             if isinstance(st.default, bool):
                 orange.gui.checkBox(box, self, k, k, callback=lambda k=k: self._sync(k))
             elif st.default is None or isinstance(st.default, (str, int, float)):
@@ -167,6 +175,8 @@ def qt_view(core_cls, orange=None):
         setattr(self.core, k, getattr(self, k))
 
     def _refresh_editors(self):
+        if self._custom_refresh is not None:
+            self._custom_refresh()
         if self._param_box is None:
             return
         lay = self._param_box.layout()
@@ -210,6 +220,8 @@ def qt_view(core_cls, orange=None):
         self.bridge.flush()
         for k in core_settings:               # the action may update settings (saved params)
             setattr(self, k, getattr(self.core, k))
+        if self._custom_refresh is not None:
+            self._custom_refresh()
         self._show_result()
 
     def on_exception(self, ex):

@@ -63,9 +63,19 @@ def _plain(v):
 
 
 def resolve(qualified_name: str) -> type:
+    """Headless widget class of a workflow node.  Accepts the reference's names
+    (REFERENCE_WIDGETS), the Qt view names Orange registers (``...OWSessionContextView``:
+    the view's ``core_class``, or the name without ``View`` when Orange is absent and no
+    view was generated) and headless class names."""
     qn = REFERENCE_WIDGETS.get(qualified_name, qualified_name)
     mod, _, cls = qn.rpartition(".")
-    return getattr(importlib.import_module(mod), cls)
+    m = importlib.import_module(mod)
+    obj = getattr(m, cls, None)
+    if obj is None and cls.endswith("View"):
+        obj = getattr(m, cls[:-4], None)
+    if obj is None:
+        raise ImportError(f"cannot resolve widget {qualified_name}")
+    return getattr(obj, "core_class", obj)
 
 
 @dataclass

@@ -71,6 +71,101 @@ class _QW:
         pass
 
 
+class _Signal:
+    def __init__(self):
+        self.fns = []
+
+    def connect(self, f):
+        self.fns.append(f)
+
+    def emit(self, *a):
+        for f in self.fns:
+            f(*a)
+
+
+class _Item:
+    def __init__(self, t):
+        self._t = t
+
+    def text(self):
+        return self._t
+
+
+class _QList(_QW):
+    """QListWidget stand-in: items, selection, current row."""
+
+    def __init__(self, *a):
+        super().__init__()
+        self.sel, self.row = [], -1
+        self.currentRowChanged = _Signal()
+
+    def clear(self):
+        self.items, self.sel = [], []
+
+    def setSelectionMode(self, m):
+        self.mode = m
+
+    def selectedItems(self):
+        return [_Item(self.items[i]) for i in self.sel if i < len(self.items)]
+
+    def select(self, *names):                 # test helper: the user's selection
+        self.sel = [self.items.index(n) for n in names]
+
+    def setCurrentRow(self, r):
+        self.row = r
+
+    def click_row(self, r):                   # test helper: user clicks a row
+        self.row = r
+        self.currentRowChanged.emit(r)
+
+
+class _QCombo(_QW):
+    def __init__(self, *a):
+        super().__init__()
+        self.currentTextChanged = _Signal()
+
+    def clear(self):
+        self.items = []
+
+    def currentText(self):
+        return self.text
+
+    def choose(self, t):                      # test helper
+        self.text = t
+        self.currentTextChanged.emit(t)
+
+
+class _QEdit(_QW):
+    def __init__(self, text=""):
+        super().__init__(text)
+        self.textChanged = _Signal()
+
+    def toPlainText(self):
+        return self.text
+
+    def setPlainText(self, t):
+        self.text = t
+
+    def type(self, t):                        # test helper: the user edits the text
+        self.text = t
+        self.textChanged.emit()
+
+
+class _QLine(_QW):
+    def __init__(self, text=""):
+        super().__init__(text)
+        self.textChanged = _Signal()
+
+    def text_(self):
+        return self.text
+
+
+class _QButton(_QW):
+    def __init__(self, text=""):
+        super().__init__(text)
+        self.clicked = _Signal()
+
+
 class _OWWidget:
     def __init__(self, *a, **kw):
         self.controlArea, self.mainArea = _QW(), _QW()
@@ -105,6 +200,8 @@ def _fake_gui():
     def widgetBox(parent, title):
         b = _QW(title)
         made.append(("box", title))
+        if hasattr(parent, "layout"):
+            parent.layout().addWidget(b)          # Orange adds the box to its parent
         return b
 
     def checkBox(box, w, attr, label, callback=None):
@@ -118,11 +215,37 @@ def _fake_gui():
     return SimpleNamespace(widgetBox=widgetBox, checkBox=checkBox, lineEdit=lineEdit, button=button, made=made)
 
 
+class _FakeLineEdit:
+    """QLineEdit: text() is a method in Qt."""
+
+    def __init__(self, text=""):
+        self._text = text
+        self.textChanged = _Signal()
+
+    def setPlaceholderText(self, t):
+        self.ph = t
+
+    def setToolTip(self, t):
+        self.tip = t
+
+    def deleteLater(self):
+        pass
+
+    def text(self):
+        return self._text
+
+    def setText(self, t):
+        self._text = t
+        self.textChanged.emit(t)
+
+
 @pytest.fixture()
 def orange():
     return SimpleNamespace(widget=SimpleNamespace(OWWidget=_OWWidget, Input=_Sig, Output=_Sig),
                            settings=SimpleNamespace(Setting=_Setting), gui=_fake_gui(),
-                           qt=SimpleNamespace(QTextBrowser=_QW, QLabel=_QW, QComboBox=_QW, QLineEdit=_QW),
+                           qt=SimpleNamespace(QTextBrowser=_QEdit, QLabel=_QW, QComboBox=_QCombo, QLineEdit=_FakeLineEdit,
+                                              QListWidget=_QList, QPushButton=_QButton, QPlainTextEdit=_QEdit,
+                                              QAbstractItemView=SimpleNamespace(ExtendedSelection=3)),
                            concurrent=None)
 
 
@@ -192,3 +315,133 @@ def test_evaluation_view_shows_metric_table_and_errors(orange, session):
     assert "rmse" in w.result_view.html
     w.core.error("boom")
     assert w.shown["error"] == "boom"
+
+
+
+def _click(view, label):
+    for box in _all_widgets(view):
+        if isinstance(box, _QButton) and box.text == label:
+            box.clicked.emit()
+            return
+    raise KeyError(label)
+
+
+def _all_widgets(view):
+    out = []
+    for root in (view.controlArea, view.mainArea):
+        stack = [root]
+        while stack:
+            w = stack.pop()
+            out.append(w)
+            stack.extend(w.layout().items if hasattr(w, "layout") else [])
+    return out
+
+
+def test_dataset_builder_view_assigns_roles_through_its_controls(orange, session, monkeypatch):
+    """Role assignment from the canvas: select columns in the list views, press the move
+    buttons, reorder, filter -- then Commit assembles exactly those features."""
+    import orangecontrib.spark_amd.widgets.custom_views as CV
+    from orangecontrib.spark_amd.widgets.ml.owdatasetbuilder import OWDatasetBuilder
+    made = []
+    orig = CV.build_dataset_builder
+
+    def spy(view, o):
+        r = orig(view, o)
+        made.append(view)
+        return r
+    monkeypatch.setitem(CV.BUILDERS, "OWDatasetBuilder", spy)
+    V = qt_view(OWDatasetBuilder, orange)
+    w = V()
+    lists = w.builder_lists
+    df = session.createDataFrame(pd.DataFrame({"x1": [1.0, 2.0, 3.0], "x2": [4.0, 5.0, 6.0], "x3": [7.0, 8.0, 9.0],
+                                               "y": [0, 1, 0], "note": ["a", "b", "c"]}))
+    w.set_dataframe(df)
+    assert lists["available"].items == ["x1", "x2", "x3", "y", "note"]
+    lists["filter"].setText("x")                         # filter narrows the available list
+    assert lists["available"].items == ["x1", "x2", "x3"]
+    lists["available"].select("x1", "x3")
+    _click(w, "Features >")
+    lists["filter"].setText("")
+    lists["available"].select("y")
+    _click(w, "Label >")
+    lists["available"].select("note")
+    _click(w, "Meta >")
+    lists["available"].select("x2")
+    _click(w, "Features >")
+    lists["features"].select("x2")
+    _click(w, "Up")                                      # features now x1, x2, x3
+    assert lists["features"].items == ["x1", "x2", "x3"] and lists["label"].items == ["y"]
+    assert lists["metas"].items == ["note"] and lists["available"].items == []
+    lists["features"].select("x3")
+    _click(w, "< Available")
+    assert lists["available"].items == ["x3"]
+    w.run_action()
+    out = V.Outputs.dataframe.sent[-1]
+    rows = out.select("features", "label").collect()
+    assert [list(r.features.toArray()) for r in rows] == [[1.0, 4.0], [2.0, 5.0], [3.0, 6.0]]
+    assert [r.label for r in rows] == [0.0, 1.0, 0.0]
+    assert "note" in out.columns
+    # the role hints were persisted into the widget setting (workflow save)
+    assert w.domain_role_hints
+
+
+def test_catalog_table_view_combo_boxes(orange, session, tmp_path):
+    from orangecontrib.spark_amd.widgets.data.owtable import OWCatalogTable
+    session.sql("CREATE DATABASE IF NOT EXISTS sales")
+    session.createDataFrame(pd.DataFrame({"a": [1, 2]})).write.mode("overwrite").saveAsTable("sales.q1")
+    session.createDataFrame(pd.DataFrame({"a": [3, 4, 5]})).write.mode("overwrite").saveAsTable("sales.q2")
+    V = qt_view(OWCatalogTable, orange)
+    w = V()
+    c = w.table_controls
+    w._refresh_editors()
+    assert "default" in c["databases"].items and "sales" in c["databases"].items
+    c["databases"].choose("sales")                       # database combo -> table combo refilled
+    assert set(c["tables"].items) == {"q1", "q2"} and w.database == "sales"
+    c["tables"].choose("q2")
+    assert w.table == "q2"
+    w.run_action()                                       # Submit
+    assert V.Outputs.dataframe.sent[-1].count() == 3
+    assert not any(m[:2] == ("line", "table") for m in orange.gui.made)   # combo, not a line edit
+
+
+def test_script_view_library_editor_and_console(orange, session):
+    from orangecontrib.spark_amd.widgets.data.owscript import OWScript
+    V = qt_view(OWScript, orange)
+    w = V()
+    sc = w.script_controls
+    w._refresh_editors()
+    assert sc["library"].items == ["Hello session"] and "out_object = in_object" in sc["editor"].text
+    sc["editor"].type("out_object = 6 * 7\nprint('answer', out_object)")
+    _click(w, "+")                                        # save as a new library entry
+    assert sc["library"].items == ["Hello session", "Script 2"] and w.core.currentScriptIndex == 1
+    w.run_action()
+    assert V.Outputs.out_object.sent[-1] == 42
+    assert "answer 42" in sc["console"].text
+    sc["library"].click_row(0)                            # back to the first script
+    assert sc["editor"].text.startswith("out_object = in_object")
+    sc["editor"].type("out_object = 'changed'")
+    _click(w, "Update")
+    assert w.core.libraryListSource[0]["script"] == "out_object = 'changed'"
+    _click(w, "-")
+    assert sc["library"].items == ["Script 2"]
+
+
+def test_tutorial_names_are_the_classes_orange_registers(orange):
+    """Every node of the shipped tutorial names a Qt view class that export_views creates
+    in that module (what Orange's discovery registers), and the headless runner resolves
+    it to the widget's core."""
+    import importlib
+    import os
+    import xml.etree.ElementTree as ET
+    from orangecontrib.spark_amd.workflow import resolve
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    ows = os.path.join(root, "orangecontrib", "spark_amd", "tutorials", "spark_ml.ows")
+    names = [n.get("qualified_name") for n in ET.parse(ows).getroot().iter("node")]
+    assert len(names) == 8
+    for qn in names:
+        mod, _, cls = qn.rpartition(".")
+        assert cls.endswith("View")
+        g = dict(vars(importlib.import_module(mod)))
+        views = {v.__qualname__: v for v in export_views(g, orange)}
+        assert cls in views, qn
+        assert resolve(qn) is views[cls].core_class
