@@ -29,9 +29,11 @@ def _pa():
 
 
 def vector_arrow_type():
+    """Spark VectorUDT sqlType: struct<type: tinyint NOT NULL, size: int, indices:
+    array<int>, values: array<double>> (type 0 = sparse, 1 = dense)."""
     pa, _ = _pa()
-    return pa.struct([("type", pa.int8()), ("size", pa.int32()), ("indices", pa.list_(pa.int32())),
-                      ("values", pa.list_(pa.float64()))])
+    return pa.struct([pa.field("type", pa.int8(), False), ("size", pa.int32()), ("indices", pa.list_(pa.field("element", pa.int32(), False))),
+                      ("values", pa.list_(pa.field("element", pa.float64(), False)))])
 
 
 def vectors_to_arrow(rows) -> "pa.Array":

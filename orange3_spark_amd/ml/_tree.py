@@ -194,35 +194,70 @@ class _TreeModelMixin:
         X = U.dense_features(df, self.getOrDefault(self.featuresCol))
         return X.float() if X.is_cuda else X.to(torch.float64)
 
-    # persistence: Spark ensemble layout (data/ = treeID + nodeData, treesMetadata/)
+    # persistence, Spark's layouts: ensembles (RF / GBT) write data/ = (treeID, nodeData)
+    # rows + treesMetadata/ = (treeID, metadata JSON, weights); a single decision tree
+    # writes its NodeData rows flat in data/ (DecisionTreeModelReadWrite)
     def _save_data(self, path):
+        import json as _json
         import pyarrow as pa
-        from .util import save_metadata
-        recs = []
-        for tid, t in enumerate(self._ens.trees):
-            for r in _node_records(t):
-                recs.append({"treeID": tid, "nodeData": r})
-        write_data(path, pa.Table.from_pylist(recs, schema=_ens_schema()))
-        tm = [{"treeID": i, "metadata": "{}", "weights": float(w)} for i, w in enumerate(self._ens.weights)]
-        write_data(path, pa.Table.from_pylist(tm), subdir="treesMetadata")
-        _ = save_metadata
+        from .util import SPARK_VERSION
+        trees = self._ens.trees
+        if self._ens.kind == "dt":
+            write_data(path, pa.Table.from_pylist(_node_records(trees[0]), schema=pa.schema(list(_node_type()))),
+                       non_null=_NODE_NON_NULL)
+            return
+        recs = [{"treeID": tid, "nodeData": r} for tid, t in enumerate(trees) for r in _node_records(t)]
+        write_data(path, pa.Table.from_pylist(recs, schema=_ens_schema()), non_null=("treeID",))
+        member = ("org.apache.spark.ml.regression.DecisionTreeRegressionModel"
+                  if self._ens.kind == "gbt" or self._ens.num_classes == 0
+                  else "org.apache.spark.ml.classification.DecisionTreeClassificationModel")
+        tm = [{"treeID": i, "weights": float(w),
+               "metadata": _json.dumps({"class": member, "timestamp": 0, "sparkVersion": SPARK_VERSION,
+                                        "uid": f"{self.uid}_tree{i}", "paramMap": {}, "defaultParamMap": {}},
+                                       separators=(",", ":"))}
+              for i, w in enumerate(self._ens.weights)]
+        tmt = pa.table({"treeID": pa.array([r["treeID"] for r in tm], pa.int32()),
+                        "metadata": pa.array([r["metadata"] for r in tm], pa.string()),
+                        "weights": pa.array([r["weights"] for r in tm], pa.float64())})
+        write_data(path, tmt, subdir="treesMetadata", non_null=("treeID", "weights"))
 
     def _extra_metadata(self):
-        return {"numFeatures": self.numFeatures, "numClasses": self._ens.num_classes,
-                "numTrees": len(self._ens.trees), "ensembleKind": self._ens.kind}
+        meta = {"numFeatures": self.numFeatures}
+        if self._ens.kind != "dt":
+            meta["numTrees"] = len(self._ens.trees)
+        if self._ens.num_classes and self._ens.kind != "gbt":
+            meta["numClasses"] = self._ens.num_classes
+        return meta
 
     @classmethod
     def _load_impl(cls, path, meta):
-        data = read_data(path).to_pylist()
-        tm = sorted(read_data(path, "treesMetadata").to_pylist(), key=lambda r: r["treeID"])
-        by_tree = {}
-        for r in data:
-            by_tree.setdefault(r["treeID"], []).append(r["nodeData"])
+        table = read_data(path)
         F = meta.get("numFeatures", 0)
-        trees = [_tree_from_records(by_tree[i], F) for i in sorted(by_tree)]
+        name = meta["class"].rsplit(".", 1)[-1]
+        kind = "gbt" if name.startswith("GBT") else ("dt" if name.startswith("DecisionTree") else "rf")
+        kind = meta.get("ensembleKind", kind)
+        regression = kind == "gbt" or "Regression" in name
+        if "treeID" in table.column_names:
+            data = table.to_pylist()
+            tm = sorted(read_data(path, "treesMetadata").to_pylist(), key=lambda r: r["treeID"])
+            by_tree = {}
+            for r in data:
+                by_tree.setdefault(r["treeID"], []).append(r["nodeData"])
+            nodes = [x["nodeData"] for x in data]
+            weights = [r["weights"] for r in tm]
+        else:                                 # single tree: flat NodeData rows
+            nodes = table.to_pylist()
+            by_tree = {0: nodes}
+            weights = [1.0]
+        trees = [_tree_from_records(by_tree[i], F, regression) for i in sorted(by_tree)]
+        if "numClasses" in meta:
+            ncls = meta["numClasses"]
+        elif name == "GBTClassificationModel":
+            ncls = 2
+        else:
+            ncls = 0 if regression else max(len(x["impurityStats"]) for x in nodes)
         m = cls()
-        m._ens = TR.Ensemble(trees, [r["weights"] for r in tm], meta.get("ensembleKind", "rf"),
-                             meta.get("numClasses", 0))
+        m._ens = TR.Ensemble(trees, weights, kind, ncls)
         m.numFeatures = F
         apply_metadata(m, meta)
         return m
@@ -249,9 +284,14 @@ def _node_records(t: TR.Tree) -> list:
     def visit(nid):
         my = len(recs)
         v = t.value[nid]
+        c = float(t.count[nid])
+        if len(v) > 1:                       # classification: class counts (gini / entropy)
+            stats = [float(x) for x in v * c]
+        else:                                # regression (variance): [count, sum, sum of squares]
+            mu = float(v[0])
+            stats = [c, c * mu, c * (float(t.impurity[nid]) + mu * mu)]
         rec = {"id": my, "prediction": float(np.argmax(v)) if len(v) > 1 else float(v[0]),
-               "impurity": float(t.impurity[nid]), "impurityStats": [float(x) for x in (v * t.count[nid]
-                                                                                      if len(v) > 1 else v)],
+               "impurity": float(t.impurity[nid]), "impurityStats": stats,
                "rawCount": int(round(t.count[nid])), "gain": float(t.gain[nid]) if not _is_leaf(t, nid) else -1.0,
                "leftChild": -1, "rightChild": -1,
                "split": {"featureIndex": -1, "leftCategoriesOrThreshold": [], "numCategories": -1}}
@@ -266,7 +306,10 @@ def _node_records(t: TR.Tree) -> list:
     return recs
 
 
-def _tree_from_records(recs, F) -> TR.Tree:
+def _tree_from_records(recs, F, regression: bool = False) -> TR.Tree:
+    """Spark NodeData rows -> Tree.  ``regression``: variance trees (GBT members and the
+    regressors), whose impurityStats are [count, sum, sum of squares] and whose node value is
+    ``prediction``; otherwise impurityStats are class counts."""
     by_id = {r["id"]: r for r in recs}
     depth = 0
 
@@ -279,7 +322,7 @@ def _tree_from_records(recs, F) -> TR.Tree:
             d(r["rightChild"], k + 1)
     d(0, 0)
     size = 2 ** (depth + 1)
-    S = max(1, max(len(r["impurityStats"]) for r in recs))
+    S = 1 if regression else max(1, max(len(r["impurityStats"]) for r in recs))
     feat = -np.ones(size, dtype=np.int64)
     thr = np.zeros(size)
     val = np.zeros((size, S))
@@ -306,14 +349,25 @@ def _tree_from_records(recs, F) -> TR.Tree:
     return TR.Tree(feat, thr, np.zeros(size, dtype=np.int64), val, imp, gain, cnt, F)
 
 
+_NODE_NON_NULL = ("id", "prediction", "impurity", "rawCount", "gain", "leftChild", "rightChild")
+
+
+def _node_type():
+    """Spark's NodeData case class (primitive fields NOT NULL) with its SplitData struct."""
+    import pyarrow as pa
+    split = pa.struct([pa.field("featureIndex", pa.int32(), False),
+                       ("leftCategoriesOrThreshold", pa.list_(pa.field("element", pa.float64(), False))),
+                       pa.field("numCategories", pa.int32(), False)])
+    return pa.struct([pa.field("id", pa.int32(), False), pa.field("prediction", pa.float64(), False),
+                      pa.field("impurity", pa.float64(), False), ("impurityStats", pa.list_(pa.field("element", pa.float64(), False))),
+                      pa.field("rawCount", pa.int64(), False), pa.field("gain", pa.float64(), False),
+                      pa.field("leftChild", pa.int32(), False), pa.field("rightChild", pa.int32(), False),
+                      ("split", split)])
+
+
 def _ens_schema():
     import pyarrow as pa
-    split = pa.struct([("featureIndex", pa.int32()), ("leftCategoriesOrThreshold", pa.list_(pa.float64())),
-                       ("numCategories", pa.int32())])
-    node = pa.struct([("id", pa.int32()), ("prediction", pa.float64()), ("impurity", pa.float64()),
-                      ("impurityStats", pa.list_(pa.float64())), ("rawCount", pa.int64()), ("gain", pa.float64()),
-                      ("leftChild", pa.int32()), ("rightChild", pa.int32()), ("split", split)])
-    return pa.schema([("treeID", pa.int32()), ("nodeData", node)])
+    return pa.schema([pa.field("treeID", pa.int32(), False), ("nodeData", _node_type())])
 
 
 class _TreeClassifierModel(_TreeModelMixin, U.ProbabilisticClassifierMixin, Model, MLWritable, MLReadable):

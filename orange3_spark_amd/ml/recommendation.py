@@ -186,14 +186,17 @@ class ALSModel(Model, _ALSModelParams, MLWritable, MLReadable):
                 from .util import _is_rank0
                 if _is_rank0():
                     import pyarrow as pa
-                    import pyarrow.parquet as pq
+                    from .util import write_data
+                    # Spark ALSModel: userFactors/ and itemFactors/ = (id int NOT NULL,
+                    # features array<float NOT NULL>), written as Spark's parquet parts
+                    elem = pa.list_(pa.field("element", pa.float32(), False))
                     for name, ids, F in (("userFactors", self._uid_t, self._U), ("itemFactors", self._iid_t, self._V)):
-                        d = os.path.join(path, name)
-                        os.makedirs(d, exist_ok=True)
-                        t = pa.table({"id": pa.array(ids.cpu().numpy().astype(np.int32)),
-                                      "features": pa.array(F.float().cpu().numpy().tolist(),
-                                                           type=pa.list_(pa.float32()))})
-                        pq.write_table(t, os.path.join(d, "part-00000.snappy.parquet"))
+                        Fh = F.float().cpu().numpy()
+                        feats = pa.ListArray.from_arrays(pa.array(np.arange(0, Fh.size + 1, max(Fh.shape[1], 1),
+                                                                            dtype=np.int32)[:Fh.shape[0] + 1]),
+                                                         pa.array(Fh.reshape(-1)), type=elem)
+                        t = pa.table({"id": pa.array(ids.cpu().numpy().astype(np.int32)), "features": feats})
+                        write_data(path, t, subdir=name, non_null=("id",))
         return _W(self)
 
     @classmethod

@@ -45,7 +45,16 @@ def jvm_name(obj_or_cls) -> str:
     return _PY2JVM.get(cls) or f"orange3_spark_amd.{cls.__module__.split('.')[-1]}.{cls.__name__}"
 
 
+_ML_MODULES = ("feature", "classification", "regression", "clustering", "recommendation", "evaluation", "fpm",
+               "tuning", "base")
+
+
 def py_class(jvm: str) -> type:
+    if jvm in _JVM2PY:
+        return _JVM2PY[jvm]
+    import importlib
+    for m in _ML_MODULES:                  # registration happens at import: load every ML module once
+        importlib.import_module(f"orange3_spark_amd.ml.{m}")
     if jvm in _JVM2PY:
         return _JVM2PY[jvm]
     # accept our own fallback names
@@ -161,17 +170,65 @@ def _from_json(instance, name, v):
     return v
 
 
-def write_data(path: str, columns: dict, subdir: str = "data") -> None:
-    """Write one row-set of model data as a Spark-style parquet part file."""
-    if not _is_rank0():
-        return
+_VEC_FIELDS = ("type", "size", "indices", "values")
+_MAT_FIELDS = ("type", "numRows", "numCols", "colPtrs", "rowIndices", "values", "isTransposed")
+_SPARK_SCALARS = {"int8": "byte", "int16": "short", "int32": "integer", "int64": "long", "float": "float",
+                  "double": "double", "bool": "boolean", "string": "string", "large_string": "string",
+                  "binary": "binary"}
+
+
+def spark_type_json(t):
+    """Spark SQL type JSON of an arrow type; VectorUDT / MatrixUDT structs are annotated
+    as Spark does in the parquet footer (that is how Spark restores Vector columns)."""
     import pyarrow as pa
+    if pa.types.is_struct(t):
+        names = tuple(t.field(i).name for i in range(t.num_fields))
+        sql = {"type": "struct", "fields": [spark_field_json(t.field(i)) for i in range(t.num_fields)]}
+        if names == _VEC_FIELDS:
+            return {"type": "udt", "class": "org.apache.spark.ml.linalg.VectorUDT",
+                    "pyClass": "pyspark.ml.linalg.VectorUDT", "sqlType": sql}
+        if names == _MAT_FIELDS:
+            return {"type": "udt", "class": "org.apache.spark.ml.linalg.MatrixUDT",
+                    "pyClass": "pyspark.ml.linalg.MatrixUDT", "sqlType": sql}
+        return sql
+    if pa.types.is_list(t) or pa.types.is_large_list(t):
+        return {"type": "array", "elementType": spark_type_json(t.value_type),
+                "containsNull": bool(t.value_field.nullable)}
+    name = str(t)
+    if name in _SPARK_SCALARS:
+        return _SPARK_SCALARS[name]
+    raise TypeError(f"no Spark SQL type for arrow type {t}")
+
+
+def spark_field_json(f) -> dict:
+    return {"name": f.name, "type": spark_type_json(f.type), "nullable": bool(f.nullable), "metadata": {}}
+
+
+def write_table(path: str, table, subdir: str = "data") -> None:
+    """One Spark-style parquet part file under ``path/subdir`` (+ ``_SUCCESS``), with the
+    footer metadata Spark writes: ``org.apache.spark.sql.parquet.row.metadata`` (the Spark
+    schema JSON, including the Vector/Matrix UDT annotations) and the writer version."""
     import pyarrow.parquet as pq
     d = os.path.join(path, subdir)
     os.makedirs(d, exist_ok=True)
-    table = pa.table(columns) if not isinstance(columns, pa.Table) else columns
+    row_meta = json.dumps({"type": "struct", "fields": [spark_field_json(f) for f in table.schema]},
+                          separators=(",", ":"))
+    table = table.replace_schema_metadata({"org.apache.spark.version": SPARK_VERSION,
+                                           "org.apache.spark.sql.parquet.row.metadata": row_meta})
     pq.write_table(table, os.path.join(d, f"part-00000-{uuid.uuid4()}-c000.snappy.parquet"), compression="snappy")
     open(os.path.join(d, "_SUCCESS"), "w").close()
+
+
+def write_data(path: str, columns, subdir: str = "data", non_null=()) -> None:
+    """Write one row-set of model data as a Spark-style parquet part file.  ``non_null``:
+    top-level columns Spark declares NOT NULL (primitive case-class fields)."""
+    if not _is_rank0():
+        return
+    import pyarrow as pa
+    table = pa.table(columns) if not isinstance(columns, pa.Table) else columns
+    if non_null:
+        table = table.cast(pa.schema([f.with_nullable(f.name not in non_null) for f in table.schema]))
+    write_table(path, table, subdir)
 
 
 def read_data(path: str, subdir: str = "data"):
@@ -199,10 +256,13 @@ def vector_from_struct(s):
 
 
 def matrix_arrow_type():
+    """Spark MatrixUDT sqlType (type 0 = sparse CSC, 1 = dense; values column-major unless
+    isTransposed)."""
     import pyarrow as pa
-    return pa.struct([("type", pa.int8()), ("numRows", pa.int32()), ("numCols", pa.int32()),
-                      ("colPtrs", pa.list_(pa.int32())), ("rowIndices", pa.list_(pa.int32())),
-                      ("values", pa.list_(pa.float64())), ("isTransposed", pa.bool_())])
+    return pa.struct([pa.field("type", pa.int8(), False), pa.field("numRows", pa.int32(), False),
+                      pa.field("numCols", pa.int32(), False), ("colPtrs", pa.list_(pa.field("element", pa.int32(), False))),
+                      ("rowIndices", pa.list_(pa.field("element", pa.int32(), False))), ("values", pa.list_(pa.field("element", pa.float64(), False))),
+                      pa.field("isTransposed", pa.bool_(), False)])
 
 
 def matrix_struct(m) -> dict:

@@ -1,0 +1,216 @@
+#!/usr/bin/env python
+"""Write tests/fixtures/spark_models/: model directories laid out byte-for-byte the way
+Spark 3.5 ``MLWriter``s write them, built by hand from Spark's documented schemas -- NOT
+with this framework's writers -- so the loaders are pinned to Spark's format rather than
+to their own output.
+
+Layout per model (Spark ``DefaultParamsWriter`` + model writers):
+  metadata/part-00000   one JSON line: class, timestamp, sparkVersion, uid, paramMap,
+                        defaultParamMap (+ model extras: numFeatures/numTrees, rank, ...)
+  data/part-*.parquet   Spark's case-class schema; vectors / matrices are the VectorUDT /
+                        MatrixUDT sqlType structs; the parquet footer carries Spark's
+                        ``org.apache.spark.sql.parquet.row.metadata`` schema JSON with the
+                        UDT annotations (that is how Spark restores Vector columns)
+
+Models: LogisticRegressionModel (binomial), KMeansModel, GBTClassificationModel (two
+variance-impurity regression stumps + tree weights), ALSModel (user / item factor tables)
+and a PipelineModel (VectorAssembler -> LogisticRegressionModel).
+"""
+import json
+import os
+import shutil
+
+import pyarrow as pa
+import pyarrow.parquet as pq
+
+ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "fixtures", "spark_models")
+TS = 1700000000000
+VERSION = "3.5.1"
+
+# ---------------------------------------------------------------- Spark SQL types (JSON)
+VEC_SQL = {"type": "struct", "fields": [
+    {"name": "type", "type": "byte", "nullable": False, "metadata": {}},
+    {"name": "size", "type": "integer", "nullable": True, "metadata": {}},
+    {"name": "indices", "type": {"type": "array", "elementType": "integer", "containsNull": False},
+     "nullable": True, "metadata": {}},
+    {"name": "values", "type": {"type": "array", "elementType": "double", "containsNull": False},
+     "nullable": True, "metadata": {}}]}
+MAT_SQL = {"type": "struct", "fields": [
+    {"name": "type", "type": "byte", "nullable": False, "metadata": {}},
+    {"name": "numRows", "type": "integer", "nullable": False, "metadata": {}},
+    {"name": "numCols", "type": "integer", "nullable": False, "metadata": {}},
+    {"name": "colPtrs", "type": {"type": "array", "elementType": "integer", "containsNull": False},
+     "nullable": True, "metadata": {}},
+    {"name": "rowIndices", "type": {"type": "array", "elementType": "integer", "containsNull": False},
+     "nullable": True, "metadata": {}},
+    {"name": "values", "type": {"type": "array", "elementType": "double", "containsNull": False},
+     "nullable": True, "metadata": {}},
+    {"name": "isTransposed", "type": "boolean", "nullable": False, "metadata": {}}]}
+VEC_UDT = {"type": "udt", "class": "org.apache.spark.ml.linalg.VectorUDT", "pyClass": "pyspark.ml.linalg.VectorUDT",
+           "sqlType": VEC_SQL}
+MAT_UDT = {"type": "udt", "class": "org.apache.spark.ml.linalg.MatrixUDT", "pyClass": "pyspark.ml.linalg.MatrixUDT",
+           "sqlType": MAT_SQL}
+
+VEC_ARROW = pa.struct([pa.field("type", pa.int8(), False), ("size", pa.int32()), ("indices", pa.list_(pa.field("element", pa.int32(), False))),
+                       ("values", pa.list_(pa.field("element", pa.float64(), False)))])
+MAT_ARROW = pa.struct([pa.field("type", pa.int8(), False), pa.field("numRows", pa.int32(), False),
+                       pa.field("numCols", pa.int32(), False), ("colPtrs", pa.list_(pa.field("element", pa.int32(), False))),
+                       ("rowIndices", pa.list_(pa.field("element", pa.int32(), False))), ("values", pa.list_(pa.field("element", pa.float64(), False))),
+                       pa.field("isTransposed", pa.bool_(), False)])
+
+
+def field(name, typ, nullable=True):
+    return {"name": name, "type": typ, "nullable": nullable, "metadata": {}}
+
+
+def write_meta(path, cls, uid, params, defaults, **extra):
+    d = os.path.join(path, "metadata")
+    os.makedirs(d, exist_ok=True)
+    meta = {"class": cls, "timestamp": TS, "sparkVersion": VERSION, "uid": uid, "paramMap": params,
+            "defaultParamMap": defaults}
+    meta.update(extra)
+    with open(os.path.join(d, "part-00000"), "w") as f:
+        f.write(json.dumps(meta, separators=(",", ":")) + "\n")
+    open(os.path.join(d, "_SUCCESS"), "w").close()
+
+
+def write_parquet(path, sub, table: pa.Table, spark_fields):
+    d = os.path.join(path, sub)
+    os.makedirs(d, exist_ok=True)
+    row_meta = json.dumps({"type": "struct", "fields": spark_fields}, separators=(",", ":"))
+    table = table.replace_schema_metadata({"org.apache.spark.version": VERSION,
+                                           "org.apache.spark.sql.parquet.row.metadata": row_meta})
+    pq.write_table(table, os.path.join(d, "part-00000-0b3a7e3c-5f1e-4c7e-9d1e-2a1b3c4d5e6f-c000.snappy.parquet"),
+                   compression="snappy")
+    open(os.path.join(d, "_SUCCESS"), "w").close()
+
+
+LR_DEFAULTS = {"aggregationDepth": 2, "elasticNetParam": 0.0, "family": "auto", "featuresCol": "features",
+               "fitIntercept": True, "labelCol": "label", "maxBlockSizeInMB": 0.0, "maxIter": 100,
+               "predictionCol": "prediction", "probabilityCol": "probability", "rawPredictionCol": "rawPrediction",
+               "regParam": 0.0, "standardization": True, "threshold": 0.5, "tol": 1e-06}
+
+
+def logistic(path, uid="LogisticRegression_4d3a1b2c5e6f"):
+    write_meta(path, "org.apache.spark.ml.classification.LogisticRegressionModel", uid,
+               {"maxIter": 25, "regParam": 0.01}, LR_DEFAULTS)
+    t = pa.table({
+        "numClasses": pa.array([2], pa.int32()),
+        "numFeatures": pa.array([3], pa.int32()),
+        "interceptVector": pa.array([{"type": 1, "size": None, "indices": None, "values": [0.3]}], VEC_ARROW),
+        "coefficientMatrix": pa.array([{"type": 1, "numRows": 1, "numCols": 3, "colPtrs": None, "rowIndices": None,
+                                        "values": [0.5, -1.25, 2.0], "isTransposed": True}], MAT_ARROW),
+        "isMultinomial": pa.array([False], pa.bool_())})
+    write_parquet(path, "data", t, [field("numClasses", "integer", False), field("numFeatures", "integer", False),
+                                    field("interceptVector", VEC_UDT), field("coefficientMatrix", MAT_UDT),
+                                    field("isMultinomial", "boolean", False)])
+
+
+def kmeans(path):
+    write_meta(path, "org.apache.spark.ml.clustering.KMeansModel", "KMeans_8a7b6c5d4e3f",
+               {"k": 2, "seed": 7},
+               {"distanceMeasure": "euclidean", "featuresCol": "features", "initMode": "k-means||", "initSteps": 2,
+                "k": 2, "maxBlockSizeInMB": 0.0, "maxIter": 20, "predictionCol": "prediction",
+                "seed": -1689246527, "solver": "auto", "tol": 0.0001})
+    t = pa.table({"clusterIdx": pa.array([0, 1], pa.int32()),
+                  "clusterCenter": pa.array([{"type": 1, "size": None, "indices": None, "values": [0.0, 0.0]},
+                                             {"type": 1, "size": None, "indices": None, "values": [5.0, 5.0]}],
+                                            VEC_ARROW)})
+    write_parquet(path, "data", t, [field("clusterIdx", "integer", False), field("clusterCenter", VEC_UDT)])
+
+
+SPLIT = pa.struct([pa.field("featureIndex", pa.int32(), False), ("leftCategoriesOrThreshold", pa.list_(pa.field("element", pa.float64(), False))),
+                   pa.field("numCategories", pa.int32(), False)])
+NODE = pa.struct([pa.field("id", pa.int32(), False), pa.field("prediction", pa.float64(), False),
+                  pa.field("impurity", pa.float64(), False), ("impurityStats", pa.list_(pa.field("element", pa.float64(), False))),
+                  pa.field("rawCount", pa.int64(), False), pa.field("gain", pa.float64(), False),
+                  pa.field("leftChild", pa.int32(), False), pa.field("rightChild", pa.int32(), False),
+                  ("split", SPLIT)])
+SPLIT_SQL = {"type": "struct", "fields": [
+    field("featureIndex", "integer", False),
+    field("leftCategoriesOrThreshold", {"type": "array", "elementType": "double", "containsNull": False}),
+    field("numCategories", "integer", False)]}
+NODE_SQL = {"type": "struct", "fields": [
+    field("id", "integer", False), field("prediction", "double", False), field("impurity", "double", False),
+    field("impurityStats", {"type": "array", "elementType": "double", "containsNull": False}),
+    field("rawCount", "long", False), field("gain", "double", False), field("leftChild", "integer", False),
+    field("rightChild", "integer", False), field("split", SPLIT_SQL)]}
+
+
+def _stump(feature, thr, left, right, n_left, n_right):
+    """Variance-impurity regression stump as Spark NodeData rows (preorder ids)."""
+    def stats(n, mean, var):
+        return [float(n), n * mean, n * (var + mean * mean)]
+    n = n_left + n_right
+    mean = (n_left * left + n_right * right) / n
+    var = (n_left * left * left + n_right * right * right) / n - mean * mean
+    leaf_split = {"featureIndex": -1, "leftCategoriesOrThreshold": [], "numCategories": -1}
+    return [
+        {"id": 0, "prediction": mean, "impurity": var, "impurityStats": stats(n, mean, var), "rawCount": n,
+         "gain": var, "leftChild": 1, "rightChild": 2,
+         "split": {"featureIndex": feature, "leftCategoriesOrThreshold": [thr], "numCategories": -1}},
+        {"id": 1, "prediction": left, "impurity": 0.0, "impurityStats": stats(n_left, left, 0.0), "rawCount": n_left,
+         "gain": -1.0, "leftChild": -1, "rightChild": -1, "split": leaf_split},
+        {"id": 2, "prediction": right, "impurity": 0.0, "impurityStats": stats(n_right, right, 0.0),
+         "rawCount": n_right, "gain": -1.0, "leftChild": -1, "rightChild": -1, "split": leaf_split}]
+
+
+def gbt(path):
+    uid = "GBTClassifier_1a2b3c4d5e6f"
+    defaults = {"cacheNodeIds": False, "checkpointInterval": 10, "featureSubsetStrategy": "all",
+                "featuresCol": "features", "impurity": "variance", "labelCol": "label", "leafCol": "",
+                "lossType": "logistic", "maxBins": 32, "maxDepth": 5, "maxIter": 20, "maxMemoryInMB": 256,
+                "minInfoGain": 0.0, "minInstancesPerNode": 1, "minWeightFractionPerNode": 0.0,
+                "predictionCol": "prediction", "probabilityCol": "probability", "rawPredictionCol": "rawPrediction",
+                "seed": -1287390502, "stepSize": 0.1, "subsamplingRate": 1.0, "validationTol": 0.01}
+    write_meta(path, "org.apache.spark.ml.classification.GBTClassificationModel", uid, {"maxIter": 2, "maxDepth": 1},
+               defaults, numFeatures=2, numTrees=2)
+    rows = [{"treeID": 0, "nodeData": r} for r in _stump(0, 0.5, -0.6, 0.8, 40, 60)] + \
+        [{"treeID": 1, "nodeData": r} for r in _stump(1, 1.0, 0.2, -0.3, 70, 30)]
+    t = pa.Table.from_pylist(rows, schema=pa.schema([pa.field("treeID", pa.int32(), False), ("nodeData", NODE)]))
+    write_parquet(path, "data", t, [field("treeID", "integer", False), field("nodeData", NODE_SQL)])
+    tree_meta = [json.dumps({"class": "org.apache.spark.ml.regression.DecisionTreeRegressionModel",
+                             "timestamp": TS, "sparkVersion": VERSION, "uid": f"dtr_{i}",
+                             "paramMap": {"maxDepth": 1, "impurity": "variance"}, "defaultParamMap": {}},
+                            separators=(",", ":")) for i in range(2)]
+    tm = pa.table({"treeID": pa.array([0, 1], pa.int32()), "metadata": pa.array(tree_meta, pa.string()),
+                   "weights": pa.array([1.0, 0.1], pa.float64())})
+    write_parquet(path, "treesMetadata", tm, [field("treeID", "integer", False), field("metadata", "string"),
+                                              field("weights", "double", False)])
+
+
+def als(path):
+    # ALSModel holds only ALSModelParams (Spark copies the estimator's values of those)
+    write_meta(path, "org.apache.spark.ml.recommendation.ALSModel", "ALS_9f8e7d6c5b4a",
+               {"userCol": "user", "itemCol": "item", "coldStartStrategy": "nan"},
+               {"blockSize": 4096, "coldStartStrategy": "nan", "itemCol": "item", "predictionCol": "prediction",
+                "userCol": "user"},
+               rank=2)
+    arr = {"type": "array", "elementType": "float", "containsNull": False}
+    for name, ids, feats in (("userFactors", [10, 20], [[1.0, 0.5], [0.0, 2.0]]),
+                             ("itemFactors", [1, 2, 3], [[1.0, 1.0], [2.0, -1.0], [0.5, 0.25]])):
+        t = pa.table({"id": pa.array(ids, pa.int32()), "features": pa.array(feats, pa.list_(pa.field("element", pa.float32(), False)))})
+        write_parquet(path, name, t, [field("id", "integer", False), field("features", arr)])
+
+
+def pipeline(path):
+    uids = ["VectorAssembler_5c4b3a2d1e0f", "LogisticRegression_4d3a1b2c5e6f"]
+    write_meta(path, "org.apache.spark.ml.PipelineModel", "PipelineModel_0a1b2c3d4e5f", {"stageUids": uids}, {},
+               language="Python")
+    write_meta(os.path.join(path, "stages", f"0_{uids[0]}"), "org.apache.spark.ml.feature.VectorAssembler", uids[0],
+               {"inputCols": ["a", "b", "c"], "outputCol": "features"},
+               {"handleInvalid": "error", "outputCol": f"{uids[0]}__output"})
+    logistic(os.path.join(path, "stages", f"1_{uids[1]}"), uids[1])
+
+
+def main():
+    if os.path.exists(ROOT):
+        shutil.rmtree(ROOT)
+    for name, fn in (("logistic_regression", logistic), ("kmeans", kmeans), ("gbt_classifier", gbt), ("als", als),
+                     ("pipeline", pipeline)):
+        fn(os.path.join(ROOT, name))
+    print(ROOT)
+
+
+if __name__ == "__main__":
+    main()
