@@ -69,8 +69,11 @@ def _is_remote_kept(obj) -> bool:
 # worker side
 # =====================================================================================
 class _Null:
+    """Sink for the pickles of ranks != 0 (they only register objects): protocol 5 may
+    hand large buffers over as PickleBuffer objects, which have no len()."""
+
     def write(self, b):
-        return len(b)
+        return memoryview(b).nbytes
 
 
 def _worker_pickler(objs: dict, ids: dict, counter, buf):
