@@ -48,29 +48,30 @@ class _ALSParams(_ALSModelParams, HasMaxIter, HasRegParam, HasCheckpointInterval
     intermediateStorageLevel = shared("intermediateStorageLevel", "StorageLevel for intermediate datasets. "
                                       "Cannot be 'NONE'.", TypeConverters.toString)
     finalStorageLevel = shared("finalStorageLevel", "StorageLevel for ALS model factors.", TypeConverters.toString)
-    cgIters = shared("cgIters", "conjugate-gradient steps per half-iteration for large problems (warm-started; "
-                                "small problems are solved exactly).", TypeConverters.toInt)
+    cgIters = shared("cgIters", "0 (default): every row's normal equations are solved exactly, as Spark does; "
+                                "> 0: that many warm-started conjugate-gradient steps per half-iteration on large "
+                                "problems (an approximation; small problems are always exact).", TypeConverters.toInt)
 
     def __init__(self):
         super().__init__()
         self._setDefault(rank=10, maxIter=10, regParam=0.1, numUserBlocks=10, numItemBlocks=10,
                          implicitPrefs=False, alpha=1.0, ratingCol="rating", nonnegative=False,
                          checkpointInterval=10, intermediateStorageLevel="MEMORY_AND_DISK",
-                         finalStorageLevel="MEMORY_AND_DISK", cgIters=3, seed=0)
+                         finalStorageLevel="MEMORY_AND_DISK", cgIters=0, seed=0)
 
 
 @register("org.apache.spark.ml.recommendation.ALS")
 class ALS(Estimator, _ALSParams, MLWritable, MLReadable):
     """Alternating Least Squares matrix factorization (explicit or implicit feedback).
     Ratings are exchanged with all-to-all into user and item blocks; the other side's
-    factors are all-gathered each half-iteration; per-row systems are solved with
-    kernel-driven conjugate gradient (exact dense solve for small problems)."""
+    factors are all-gathered each half-iteration; every row's normal equations are solved
+    exactly by the als_exact gfx950 kernels (cgIters > 0: opt-in conjugate gradient)."""
 
     @keyword_only
     def __init__(self, *, rank=10, maxIter=10, regParam=0.1, numUserBlocks=10, numItemBlocks=10,
                  implicitPrefs=False, alpha=1.0, userCol="user", itemCol="item", seed=None, ratingCol="rating",
                  nonnegative=False, checkpointInterval=10, intermediateStorageLevel="MEMORY_AND_DISK",
-                 finalStorageLevel="MEMORY_AND_DISK", coldStartStrategy="nan", blockSize=4096, cgIters=3):
+                 finalStorageLevel="MEMORY_AND_DISK", coldStartStrategy="nan", blockSize=4096, cgIters=0):
         super().__init__()
         self._set(**self._input_kwargs)
 

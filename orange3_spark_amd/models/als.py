@@ -11,9 +11,11 @@ all-reduce of normal equations would be ~330 GB; the factor all-gather is 25.6 G
 Each half-iteration solves, for every local row u,
     (YtY[implicit] + sum_j w_j y_j y_j^T + lambda n_u I) x_u = sum_j b_j y_j
 (Spark's formulation: implicit w = alpha|r|, b = (1 + alpha|r|)[r > 0], n_u = #positive;
-explicit w = 1, b = r, n_u = #ratings) by warm-started conjugate gradient whose matvec is
-the ``als_pass`` HIP kernel plus one batched GEMM for YtY; small problems take an exact
-batched dense solve (bitwise-independent of the CG settings, used by the tests).
+explicit w = 1, b = r, n_u = #ratings) EXACTLY by default, like Spark's per-row Cholesky:
+the ``als_exact`` gfx950 kernels (Woodbury against the eigendecomposition of YtY for rows
+with <= 32 ratings, register Gram + LDS Cholesky for longer rows; ops/als.py).  With
+``cg_iters > 0`` (ALS ``cgIters``) large problems instead run that many warm-started
+conjugate-gradient steps whose matvec is the ``als_pass`` kernel (opt-in approximation).
 """
 from __future__ import annotations
 
@@ -130,28 +132,30 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
     w, b, lam = csr.cache[key]
     nnz = int(csr.cols.numel())
     if exact is None:
-        exact = nnz * R * R <= (1 << 26)
+        exact = cg_iters <= 0 or nnz * R * R <= (1 << 26)
+    if exact:
+        # Spark's per-row exact solve: gfx950 kernels (Woodbury for short rows, register
+        # Gram + LDS Cholesky for long ones), the fp64 torch path elsewhere
+        out = X0 if row_range is not None else torch.empty((n, R), dtype=torch.float32, device=dev)
+        with trace("als.exact_solve"):
+            if A.exact_kernel_ok(Ffull) and out.is_contiguous():
+                A.exact_solve(csr.indptr, csr.cols, w, b, Ffull, FtF if implicit else None, lam, implicit, out,
+                              row_range)
+            else:
+                A.exact_solve_torch(csr.indptr, csr.cols, w, b, Ffull, FtF if implicit else None, lam, out,
+                                    row_range)
+        if nonneg:
+            sl = out if row_range is None else out[row_range[0]:row_range[1]]
+            sl.clamp_(min=0)
+        return out
     indptr = csr.indptr
     if row_range is not None:
-        assert not exact, "row-range solves are CG only"
         a, e = row_range
         indptr, lam, X0, n = csr.indptr[a:e + 1], lam[a:e], X0[a:e], e - a
     if row_range is None and not exact and not nonneg and DENSE_MIN_AVG and A.gram_ok(Ffull) and nnz >= DENSE_MIN_AVG * max(n, 1):
         # many ratings per row (the item side): exact solves, Gram on MFMA + batched Cholesky
         with trace("als.dense_solve"):
             return A.dense_solve(csr.indptr, csr.cols, w, b, Ffull, FtF if implicit else None, lam)
-    if exact:
-        rows = torch.repeat_interleave(torch.arange(n, device=dev), csr.indptr[1:] - csr.indptr[:-1])
-        rhs = A.pass_(1, csr.indptr, csr.cols, b, Ffull, None)
-        Fg = Ffull[csr.cols.long()].to(torch.float64)
-        outer = Fg[:, :, None] * Fg[:, None, :] * w.to(torch.float64)[:, None, None]
-        M = torch.zeros((n, R, R), dtype=torch.float64, device=dev).index_add_(0, rows, outer)
-        if implicit and FtF is not None:
-            M = M + FtF.to(torch.float64)[None]
-        M = M + torch.diag_embed(lam.to(torch.float64)[:, None].expand(n, R))
-        M = M + 1e-12 * torch.eye(R, dtype=torch.float64, device=dev)[None]
-        x = torch.linalg.solve(M, rhs.to(torch.float64)[:, :, None]).squeeze(-1).float()
-        return x.clamp_min(0) if nonneg else x
 
     def Amul(v):
         out = A.pass_(0, indptr, csr.cols, w, Ffull, v)
@@ -260,7 +264,7 @@ class AlsResult:
 
 def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tensor, rank: int = 10,
             max_iter: int = 10, reg: float = 0.1, implicit: bool = False, alpha: float = 1.0, seed: int = 0,
-            nonneg: bool = False, cg_iters: int = 3, exact: bool | None = None, keep_full: bool = True,
+            nonneg: bool = False, cg_iters: int = 0, exact: bool | None = None, keep_full: bool = True,
             ckpt=None) -> AlsResult:
     t0 = time.time()
     dev = ratings.device
@@ -284,8 +288,8 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
         start, st, _ = last              # resume: this rank's factor shards (runtime/checkpoint.py)
         X = torch.from_numpy(st["X"]).to(dev, X.dtype)
         Y = torch.from_numpy(st["Y"]).to(dev, Y.dtype)
-    chunked = comm.world_size > 1 and not (exact if exact is not None else
-                                            max(by_user.cols.numel(), by_item.cols.numel()) * rank * rank <= (1 << 26))
+    small = max(by_user.cols.numel(), by_item.cols.numel()) * rank * rank <= (1 << 26)
+    chunked = comm.world_size > 1 and not small
     if chunked:
         # factor tables in "slot" layout: every all-gather lands in place (no staging copy,
         # no concatenation) and chunk c of every rank is gathered while chunk c+1 solves
@@ -307,7 +311,7 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
                 YtY = YtY.float()
             if chunked:
                 _gather_slots(comm, X, Xf, Ls, lambda a, e: solve_side(
-                    by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, False, row_range=(a, e)))
+                    by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact, row_range=(a, e)))
             else:
                 X = solve_side(by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact)
                 del Yf
@@ -319,7 +323,7 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
                 XtX = XtX.float()
             if chunked:
                 _gather_slots(comm, Y, Yf, Li, lambda a, e: solve_side(
-                    by_item, Xf, Y, reg, implicit, alpha, XtX, cg_iters, nonneg, False, row_range=(a, e)))
+                    by_item, Xf, Y, reg, implicit, alpha, XtX, cg_iters, nonneg, exact, row_range=(a, e)))
             else:
                 Y = solve_side(by_item, Xf, Y, reg, implicit, alpha, XtX, cg_iters, nonneg, exact)
                 del Xf

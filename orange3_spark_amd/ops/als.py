@@ -113,3 +113,68 @@ def dense_solve(indptr, cols, w, b, F, FtF, lam, batch_bytes: int = 1 << 30) -> 
             xs[bad] = torch.linalg.solve(Ad, bv[:m][bad].double()[:, :, None])[:, :, 0].float()
         x[r0:r0 + m] = xs
     return x
+
+
+EXACT_RANKS = (32, 64, 96, 128)
+
+
+def exact_kernel_ok(F: torch.Tensor) -> bool:
+    return F.is_cuda and F.dtype == torch.float32 and F.shape[1] in EXACT_RANKS and F.is_contiguous()
+
+
+def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor, row_range=None) -> torch.Tensor:
+    """Exact per-row solves (csrc/als_exact.hip) written into ``out`` (rows of this CSR,
+    or rows [a, b) of it).  Rows with <= 32 ratings and lam_u > 0 take the Woodbury kernel
+    (an n x n Cholesky against the eigendecomposition of G), the others the dense kernel
+    (register Gram + LDS Cholesky).  G = Y^T Y (implicit only)."""
+    dev = F.device
+    R = F.shape[1]
+    n_all = indptr.numel() - 1
+    a, e = (0, n_all) if row_range is None else row_range
+    cnt = (indptr[a + 1:e + 1] - indptr[a:e])
+    small_m = (cnt <= N.kernels().o3s_als_exact_max_small()) & (lam[a:e] > 0)
+    idx = torch.arange(a, e, device=dev, dtype=torch.int32)
+    small = idx[small_m].contiguous()
+    dense = idx[~small_m].contiguous()
+    Q = QT = eig = Gf = None
+    if implicit:
+        Gd = G.to(torch.float64)
+        ev, V = torch.linalg.eigh(0.5 * (Gd + Gd.T))
+        eig = ev.clamp_min(0.0).float().contiguous()
+        Q = V.float().contiguous()
+        QT = V.T.float().contiguous()
+        Gf = G.float().contiguous()
+    N.check(N.kernels().o3s_als_exact(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
+                                      b.data_ptr(), F.data_ptr(), N.ptr(Gf), N.ptr(Q), N.ptr(QT), N.ptr(eig),
+                                      lam.data_ptr(), small.data_ptr(), int(small.numel()), dense.data_ptr(),
+                                      int(dense.numel()), out.data_ptr(), N.stream_of(out)), "als_exact")
+    return out
+
+
+def exact_solve_torch(indptr, cols, w, b, F, G, lam, out, row_range=None, chunk_rows: int = 4096):
+    """fp64 reference of :func:`exact_solve` (also the CPU path): forms each row's
+    A_u = G + sum w y y^T + lam_u I and solves it, in bounded row chunks."""
+    dev = F.device
+    R = F.shape[1]
+    n_all = indptr.numel() - 1
+    a0, e0 = (0, n_all) if row_range is None else row_range
+    eye = torch.eye(R, dtype=torch.float64, device=dev)
+    for a in range(a0, e0, chunk_rows):
+        e = min(e0, a + chunk_rows)
+        lo, hi = int(indptr[a]), int(indptr[e])
+        m = e - a
+        rows = torch.repeat_interleave(torch.arange(m, device=dev), indptr[a + 1:e + 1] - indptr[a:e])
+        M = torch.zeros((m, R, R), dtype=torch.float64, device=dev)
+        rhs = torch.zeros((m, R), dtype=torch.float64, device=dev)
+        step = max(1, (1 << 25) // (R * R))          # bounded outer-product temporaries
+        for s0 in range(lo, hi, step):
+            s1 = min(hi, s0 + step)
+            Fg = F[cols[s0:s1].long()].to(torch.float64)
+            rr = rows[s0 - lo:s1 - lo]
+            M.index_add_(0, rr, Fg[:, :, None] * Fg[:, None, :] * w[s0:s1].to(torch.float64)[:, None, None])
+            rhs.index_add_(0, rr, Fg * b[s0:s1].to(torch.float64)[:, None])
+        if G is not None:
+            M = M + G.to(torch.float64)[None]
+        M = M + lam[a:e].to(torch.float64)[:, None, None] * eye[None] + 1e-12 * eye[None]
+        out[a:e] = torch.linalg.solve(M, rhs[:, :, None]).squeeze(-1).to(out.dtype)
+    return out

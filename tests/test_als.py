@@ -180,3 +180,68 @@ def test_gpu_init_factors_kernel_matches_torch(rank, nonneg):
     ref = AE.init_factors(1000, 3001, rank, 12345 ^ 0x5A5A, torch.device("cpu"), nonneg)
     got = AE.init_factors(1000, 3001, rank, 12345 ^ 0x5A5A, torch.device("cuda"), nonneg).cpu()
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+
+
+def _exact_case(R, implicit, seed=0, n_rows=700, n_other=900, dev="cuda"):
+    """A CSR with rows of 0, 1, a few, exactly 32, 33 and ~200 ratings (both kernels,
+    every routing edge), implicit zero-rating entries, random factors."""
+    g = torch.Generator().manual_seed(seed)
+    lens = torch.randint(0, 40, (n_rows,), generator=g)
+    lens[:6] = torch.tensor([0, 1, 5, 32, 33, 200])
+    lens[6:40] = torch.randint(60, 260, (34,), generator=g)
+    indptr = torch.zeros(n_rows + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(lens, 0)
+    nnz = int(indptr[-1])
+    cols = torch.randint(0, n_other, (nnz,), generator=g, dtype=torch.int32)
+    vals = torch.randn(nnz, generator=g) * 2
+    if implicit:
+        vals[::17] = 0.0
+    F = torch.randn((n_other, R), generator=g) / R ** 0.5
+    w, b, pos = AE._weights(vals, implicit, 2.0)
+    rows = torch.repeat_interleave(torch.arange(n_rows), lens)
+    nu = torch.zeros(n_rows).index_add_(0, rows, pos.float())
+    lam = (0.05 * nu).float()
+    G = (F.double().T @ F.double()).float() if implicit else None
+    to = (lambda t: None if t is None else t.to(dev))
+    return [to(x) for x in (indptr, cols, w, b, F, G, lam)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [32, 64, 128])
+@pytest.mark.parametrize("implicit", [False, True])
+def test_gpu_exact_kernels_match_fp64_solve(R, implicit):
+    """als_wood_kernel (<= 32 ratings) and als_dense_kernel (longer rows) == fp64
+    torch.linalg.solve of each row's normal equations (rank up to 128)."""
+    from orange3_spark_amd.ops import als as A
+    indptr, cols, w, b, F, G, lam = _exact_case(R, implicit)
+    n = indptr.numel() - 1
+    got = torch.full((n, R), float("nan"), device=F.device)
+    A.exact_solve(indptr, cols, w, b, F, G, lam, implicit, got)
+    ref = torch.empty((n, R), dtype=torch.float64, device=F.device)
+    A.exact_solve_torch(indptr, cols, w, b, F, G, lam, ref)
+    assert not torch.isnan(got).any()
+    err = (got.double() - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-6)
+    assert float(err.max()) < 2e-3, float(err.max())
+    # a row range (the chunked multi-rank path) writes only its rows
+    part = torch.zeros((n, R), device=F.device)
+    A.exact_solve(indptr, cols, w, b, F, G, lam, implicit, part, row_range=(100, 300))
+    assert torch.equal(part[100:300], got[100:300]) and not part[:100].any() and not part[300:].any()
+
+
+@pytest.mark.gpu
+def test_gpu_exact_als_rank128_fit_matches_fp64():
+    """ALS rank 128 (implicit), exact solves by default: the GPU fit after 2 iterations ==
+    the fp64 torch exact path on the CPU from the same initial factors."""
+    g = torch.Generator().manual_seed(3)
+    n = 60_000
+    users = torch.randint(0, 3000, (n,), generator=g)
+    items = torch.randint(0, 800, (n,), generator=g)
+    r = (torch.rand(n, generator=g) * 5).round()
+    from orange3_spark_amd.parallel.comm import LocalComm
+    gpu = AE.fit_als(LocalComm("cuda"), users.cuda(), items.cuda(), r.cuda(), rank=128, max_iter=2, reg=0.1,
+                     implicit=True, alpha=1.0, seed=1)
+    cpu = AE.fit_als(LocalComm("cpu"), users, items, r, rank=128, max_iter=2, reg=0.1, implicit=True, alpha=1.0,
+                     seed=1)
+    for a, b in ((gpu.U, cpu.U), (gpu.V, cpu.V)):
+        err = (a.cpu().double() - b.double()).norm() / b.double().norm()
+        assert float(err) < 5e-3, float(err)

@@ -1,7 +1,16 @@
 """BASELINE config 2: KMeans k=1024 on 100M x 128 fp32, 1 MI355X.
 
 Times Lloyd iterations (assign MFMA kernel + slab update kernel + all-reduce + centre
-update) after a fixed initialisation; prints one JSON line (samples/s per iteration).
+update); prints one JSON line (samples/s per iteration).
+
+``--data blobs`` (well-separated Gaussian clusters) vs ``--data uniform`` (U[-1,1]^d: no
+cluster structure, so many rows sit near a Voronoi boundary); ``--init offset`` (true
+centres + 0.5, blobs only) vs ``--init kmeans||`` (Spark's default k-means|| init, timed
+separately).  The JSON reports ``flagged_fraction`` -- the share of rows whose one-MFMA
+bf16 screen could not certify the argmin and were re-solved by the split-precision kernel
+-- and the assign rate as ``bf16_screen_tflops`` (screen mode: 2 N K D / t with ONE bf16
+MFMA per k-step, not an fp32 rate) or ``split_fp32_equiv_tflops`` (split mode: three bf16
+MFMAs emulate fp32).
 """
 import argparse
 import json
@@ -25,12 +34,34 @@ def main():
     ap.add_argument("--torch-baseline", action="store_true", help="also time a torch (rocBLAS GEMM) assign")
     ap.add_argument("--mode", default="auto", choices=["auto", "screen", "split"],
                     help="assign path: one-MFMA screen + near-tie re-solve, or split precision everywhere")
+    ap.add_argument("--data", default="blobs", choices=["blobs", "uniform"])
+    ap.add_argument("--init", default=None, choices=["offset", "kmeans||"],
+                    help="default: offset for blobs, kmeans|| for uniform")
     a = ap.parse_args()
+    init = a.init or ("offset" if a.data == "blobs" else "kmeans||")
+    if init == "offset" and a.data != "blobs":
+        raise SystemExit("--init offset needs --data blobs (true centres)")
     s = Session.getOrCreate()
-    df = s.synthetic.blobs(a.rows, a.d, k=a.k, seed=3, spread=1.0)
-    X = df.column_data("features").data
-    C = df.true_centers.float() + 0.5
     comm = s.comm
+    if a.data == "blobs":
+        df = s.synthetic.blobs(a.rows, a.d, k=a.k, seed=3, spread=1.0)
+        X = df.column_data("features").data
+    else:
+        X = torch.empty((a.rows, a.d), dtype=torch.float32, device=s.device)
+        g = torch.Generator(device=s.device).manual_seed(3)
+        for r0 in range(0, a.rows, 1 << 24):
+            r1 = min(a.rows, r0 + (1 << 24))
+            X[r0:r1].uniform_(-1.0, 1.0, generator=g)
+    t_init = None
+    if init == "offset":
+        C = df.true_centers.float() + 0.5
+    else:
+        from orange3_spark_amd.models.kmeans import kmeans_parallel_init
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        C = kmeans_parallel_init(comm, X, a.k, 2, 7).float()
+        torch.cuda.synchronize()
+        t_init = time.perf_counter() - t1
     ws = K.UpdateWorkspace(X.device, (a.k + 31) // 32 * 32, a.d)
     torch.cuda.synchronize()
 
@@ -65,10 +96,13 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
     flop = 2.0 * a.rows * a.k * a.d
+    flagged = st.get("flagged")
+    rate_key = "split_fp32_equiv_tflops" if (a.mode == "split" or flagged == a.rows) else "bf16_screen_tflops"
     out = {"metric": "KMeans Lloyd iteration samples/s (k=1024, 100M x 128 fp32)", "value": a.rows / dt,
            "unit": "samples/s", "ms_per_iter": dt * 1e3, "assign_ms": t_assign * 1e3, "update_ms": t_upd * 1e3,
-           "assign_tflops_fp32_equiv": flop / t_assign / 1e12, "rows": a.rows, "d": a.d, "k": a.k, "cost": cost,
-           "assign_mode": a.mode, "near_tie_rows_resolved": st.get("flagged")}
+           rate_key: flop / t_assign / 1e12, "rows": a.rows, "d": a.d, "k": a.k, "cost": cost,
+           "data": a.data, "init": init, "init_s": t_init, "assign_mode": a.mode,
+           "near_tie_rows_resolved": flagged, "flagged_fraction": None if flagged is None else flagged / a.rows}
     if a.torch_baseline:
         t1 = time.perf_counter()
         K.assign_torch(X[: 10_000_000], C, chunk=1 << 20)
