@@ -211,11 +211,16 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
   if (!CLS && f == 0) y2part[wid * RS + rs] = wy2;
   __syncthreads();
   // fixed-order block reduction -> slab[item][f][b][s] (features of this group only);
-  // REG stat 2 (w*y^2) is a node total: stored in (feature 0, bin 0), zero elsewhere
+  // REG stat 2 (w*y^2) is a node total: stored in (feature 0, bin 0), zero elsewhere.
+  // Feature fastest across lanes: the 64 lanes of a wave read one (bin, stat) row of the
+  // image -- 64 consecutive floats, one per bank.  (Mapping (bin, stat) fastest put every
+  // lane of a wave on the same bank: 64 floats apart -- the kernel's measured LDS bank
+  // conflicts, profiles/pmc_kmeans_gbt.json.)  The slab row is then written with a stride
+  // of B*S floats per lane; the block writes the whole row, so L2 merges the lines.
   float* out = slab + (int64_t)blockIdx.x * slab_stride;
   const int cells = FP * B * S;
   for (int i = threadIdx.x; i < cells; i += kHistThreads) {
-    const int ff = i / (B * S), rem = i % (B * S);
+    const int ff = i % FP, rem = i / FP;
     const int bb = rem / S, ss = rem % S;
     if (fg0 + ff >= F) continue;
     float acc = 0.f;
