@@ -299,6 +299,11 @@ __global__ __launch_bounds__(Dense<R>::NTH) void als_dense_kernel(
           for (int q = 0; q < c; ++q) v -= a[q] * L[c][q];
           a[c] = v / L[c][c];
         }
+        // a clamped pivot (singular row, e.g. no ratings and lam = 0) breaks that identity:
+        // store the diagonal itself so the solves never divide by zero
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          if (i == k0 + c) a[c] = L[c][c];
 #pragma unroll
         for (int c = 0; c < 8; ++c) sA[i * LDA + k0 + c] = a[c];
       }
