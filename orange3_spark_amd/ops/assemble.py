@@ -4,6 +4,8 @@ invalid flags and their count (handleInvalid).  CPU tensors are handled by the c
 torch path (ml/feature.py)."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -20,9 +22,22 @@ def supported(t: torch.Tensor) -> bool:
     return t.is_cuda and t.dtype in _DT and (t.dim() == 1 or (t.dim() == 2 and t.stride(1) == 1))
 
 
-def assemble_bf16(sources, n: int, device):
+WINDOW = int(os.environ.get("O3S_ASM_WINDOW", "64"))
+
+
+def _cols_ok(sources) -> bool:
+    """Fast-path eligibility (assemble_cols_kernel): plain contiguous [n] float / double
+    columns, all of one dtype."""
+    dt = sources[0][0].dtype
+    return dt in (torch.float32, torch.float64) and all(
+        t.dtype == dt and t.dim() == 1 and t.stride(0) == 1 and int(w) == 1 for t, _, w in sources)
+
+
+def assemble_bf16(sources, n: int, device, path: str = "auto", window: int | None = None):
     """``sources``: list of (tensor [n] or [n, >= width] row-major, valid bool [n] or None,
-    width).  Returns (bf16 [n, ld] zero padded, uint8 invalid flags [n], invalid count)."""
+    width).  Returns (bf16 [n, ld] zero padded, uint8 invalid flags [n], invalid count).
+    ``path``: "auto" (column-window kernel when every source is a plain float / double
+    column, else the generic gather), "cols" or "generic"."""
     if not sources or len(sources) > MAX_SOURCES:
         raise ValueError(f"assemble needs 1..{MAX_SOURCES} source columns")
     recs = np.zeros(len(sources), dtype=_SRC)
@@ -47,6 +62,16 @@ def assemble_bf16(sources, n: int, device):
     out = torch.empty((n, ld), dtype=torch.bfloat16, device=device)
     bad = torch.empty(n, dtype=torch.uint8, device=device)
     nbad = torch.zeros(1, dtype=torch.int32, device=device)
+    cols = path == "cols" or (path == "auto" and _cols_ok(sources))
+    if cols:
+        if not _cols_ok(sources):
+            raise ValueError("the column-window assembler needs plain float / double columns of one dtype")
+        w = int(window or WINDOW)
+        grid = max(1, min(N.num_cus(torch.device(device)) * (6 if w == 64 else 3) * 4, -(-n // 128)))
+        N.check(lib.o3s_assemble_cols(src_d.data_ptr(), _DT[sources[0][0].dtype], D, ld, n, out.data_ptr(), 0, w,
+                                      bad.data_ptr(), nbad.data_ptr(), grid, N.stream_of(out)), "assemble_cols")
+        del keep
+        return out, bad, nbad, D
     grid = max(1, min(N.num_cus(torch.device(device)) * 8, -(-n // 64)))
     N.check(lib.o3s_assemble(src_d.data_ptr(), len(sources), map_d.data_ptr(), D, ld, n, out.data_ptr(), 0,
                              bad.data_ptr(), nbad.data_ptr(), grid, N.stream_of(out)), "assemble")

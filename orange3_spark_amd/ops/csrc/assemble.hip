@@ -23,6 +23,8 @@
 // ("error") or compacts ("skip") using the count.
 #include <hip/hip_fp16.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 using namespace o3s;
@@ -121,6 +123,126 @@ __global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmSrc* __rest
   }
 }
 
+// Fast path: every source a plain [n] column of one dtype T (the common wide table of
+// float / double columns).  A block owns kCRows = 128 rows and walks the output in
+// windows of kCW = 64 or 128 columns (LDS tile 17 / 33 KB for bf16 out):
+//   load:  wave w takes columns w, w + 4, ...; lane l reads rows l and l + 64 of 8 columns
+//          per batch (16 independent loads in flight, each wave load a 256-B contiguous
+//          run of one column), converts and writes them transposed into an LDS tile whose
+//          row stride is an odd number of dwords (65 / 129), so the 64 lanes -- 64 rows --
+//          land on 64 different banks;
+//   store: the tile goes out row-major, 16 B per lane, each row's window one contiguous
+//          256-B (bf16) / 512-B (fp32) run.
+// Every input byte is read once as part of a long sequential run and every output line is
+// written whole -- the generic kernel above reads 64 elements of 8 different sources per
+// wave step and writes 16-B pieces of 64 rows 512 B apart.
+constexpr int kCRows = 128;
+constexpr int kCBatch = 8;
+typedef unsigned int uint4_ __attribute__((ext_vector_type(4)));
+
+template <typename T>
+__device__ __forceinline__ float to_f(T v) { return (float)v; }
+
+template <typename T, int OUT, int kCW>
+__global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* __restrict__ srcs, int D, int ld,
+                                                                 int64_t n, void* __restrict__ out,
+                                                                 uint8_t* __restrict__ bad, int* __restrict__ nbad) {
+  constexpr int PAD = OUT == 0 ? 2 : 1;
+  constexpr int LS = kCW + PAD;                       // tile row stride (elements): 65 / 129 dwords
+  using OT = typename std::conditional<OUT == 0, uint16_t, float>::type;
+  __shared__ OT tile[kCRows * LS];
+  __shared__ const T* s_ptr[kMaxSrc];
+  __shared__ const uint8_t* s_val[kMaxSrc];
+  __shared__ uint8_t s_bad[kCRows];
+  for (int i = threadIdx.x; i < D; i += kThreads) {
+    s_ptr[i] = reinterpret_cast<const T*>(srcs[i].ptr);
+    s_val[i] = srcs[i].valid;
+  }
+  if (threadIdx.x < kCRows) s_bad[threadIdx.x] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  const int64_t nblk = (n + kCRows - 1) / kCRows;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t row0 = blk * kCRows;
+    const int64_t ra = row0 + lane < n ? row0 + lane : n - 1;
+    const int64_t rb = row0 + lane + 64 < n ? row0 + lane + 64 : n - 1;
+    bool bada = false, badb = false;
+    for (int c0 = 0; c0 < ld; c0 += kCW) {
+      const int cw = ld - c0 < kCW ? ld - c0 : kCW;
+      for (int jb = wid; jb < cw; jb += 4 * kCBatch) {
+        T va[kCBatch], vb[kCBatch];
+#pragma unroll
+        for (int q = 0; q < kCBatch; ++q) {
+          const int j = c0 + jb + 4 * q;                // wave-uniform
+          if (jb + 4 * q < cw && j < D) {
+            va[q] = s_ptr[j][ra];
+            vb[q] = s_ptr[j][rb];
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < kCBatch; ++q) {
+          const int jl = jb + 4 * q, j = c0 + jl;
+          if (jl >= cw) break;
+          float a = 0.f, b = 0.f;
+          if (j < D) {
+            a = to_f(va[q]);
+            b = to_f(vb[q]);
+            const uint8_t* vm = s_val[j];
+            if (vm != nullptr) {
+              if (!vm[ra]) a = __builtin_nanf("");
+              if (!vm[rb]) b = __builtin_nanf("");
+            }
+            bada |= !(a == a);
+            badb |= !(b == b);
+          }
+          if constexpr (OUT == 0) {
+            tile[lane * LS + jl] = f32_to_bf16(a);
+            tile[(lane + 64) * LS + jl] = f32_to_bf16(b);
+          } else {
+            tile[lane * LS + jl] = a;
+            tile[(lane + 64) * LS + jl] = b;
+          }
+        }
+      }
+      __syncthreads();
+      const int cpr = cw / 8;                          // 16-B (bf16) / 32-B (fp32) chunks per row
+      for (int e = threadIdx.x; e < kCRows * cpr; e += kThreads) {
+        const int r = e / cpr, k = e - r * cpr;
+        const int64_t row = row0 + r;
+        if (row < n) {
+          if constexpr (OUT == 0) {
+            const uint32_t* t = reinterpret_cast<const uint32_t*>(&tile[r * LS + 8 * k]);
+            uint4_ o;
+            o.x = t[0]; o.y = t[1]; o.z = t[2]; o.w = t[3];
+            *reinterpret_cast<uint4_*>(reinterpret_cast<uint16_t*>(out) + row * ld + c0 + 8 * k) = o;
+          } else {
+            const float* t = &tile[r * LS + 8 * k];
+            float* po = reinterpret_cast<float*>(out) + row * ld + c0 + 8 * k;
+            *reinterpret_cast<float4_*>(po) = float4_{t[0], t[1], t[2], t[3]};
+            *reinterpret_cast<float4_*>(po + 4) = float4_{t[4], t[5], t[6], t[7]};
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (bada && row0 + lane < n) s_bad[lane] = 1;      // benign race: every writer stores 1
+    if (badb && row0 + lane + 64 < n) s_bad[lane + 64] = 1;
+    __syncthreads();
+    if (wid < 2) {
+      const int r = wid * 64 + lane;
+      const bool ok = row0 + r < n;
+      const int b = (ok && s_bad[r]) ? 1 : 0;
+      if (ok && bad) bad[row0 + r] = (uint8_t)b;
+      const int cnt = wave_sum_i(b);
+      if (lane == 0 && cnt) atomicAdd(nbad, cnt);
+    }
+    __syncthreads();
+    if (threadIdx.x < kCRows) s_bad[threadIdx.x] = 0;
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 // srcs: device array of nsrc AsmSrc; colmap: device int2[D]; out: [n, ld] (bf16 when
@@ -141,3 +263,27 @@ O3S_API int o3s_assemble(const void* srcs, int nsrc, const void* colmap, int D, 
 }
 
 O3S_API int o3s_assemble_src_size() { return (int)sizeof(AsmSrc); }
+
+// Fast path (see assemble_cols_kernel): srcs[j] is output column j for j < D, every source a
+// contiguous [n] column of dtype src_dtype (DT_F32 or DT_F64), ld % 8 == 0, D <= 512.
+O3S_API int o3s_assemble_cols(const void* srcs, int src_dtype, int D, int ld, int64_t n, void* out, int out_f32,
+                              int window, void* bad, void* nbad, int grid, hipStream_t st) {
+  if (D <= 0 || D > kMaxSrc || ld % 8 != 0 || ld < D || n < 0 || grid <= 0) return -1;
+  if (src_dtype != DT_F32 && src_dtype != DT_F64) return -2;
+  if (window != 64 && window != 128) return -3;
+  if (n == 0) return 0;
+#define O3S_ASM_COLS(T, O, W)                                                                            \
+  hipLaunchKernelGGL((assemble_cols_kernel<T, O, W>), dim3(grid), dim3(kThreads), 0, st, (const AsmSrc*)srcs, \
+                     D, ld, n, out, (uint8_t*)bad, (int*)nbad)
+#define O3S_ASM_COLS_W(T, O) \
+  if (window == 64) O3S_ASM_COLS(T, O, 64); else O3S_ASM_COLS(T, O, 128)
+  if (src_dtype == DT_F32) {
+    if (out_f32) { O3S_ASM_COLS_W(float, 1); } else { O3S_ASM_COLS_W(float, 0); }
+  } else {
+    if (out_f32) { O3S_ASM_COLS_W(double, 1); } else { O3S_ASM_COLS_W(double, 0); }
+  }
+#undef O3S_ASM_COLS_W
+#undef O3S_ASM_COLS
+  O3S_CHECK_LAUNCH();
+  return 0;
+}

@@ -231,3 +231,34 @@ def test_gpu_vector_assembler_fused_kernel_matches_torch(handle):
     if handle == "skip":
         kept = out.column_data("lab").data.cpu().long()
         assert torch.equal(kept, torch.nonzero(~bad).squeeze(1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["float32", "float64"])
+@pytest.mark.parametrize("window", [64, 128])
+def test_gpu_assemble_column_window_kernel(dtype, window):
+    """assemble_cols_kernel (plain float / double columns, LDS-transposed windows) ==
+    the generic gather kernel == a torch reference: several windows with a partial last
+    one, a partial last row block, null masks and NaNs flagged per row."""
+    import torch
+    from orange3_spark_amd.ops import assemble as AS
+    dev = torch.device("cuda", 0)
+    dt = getattr(torch, dtype)
+    g = torch.Generator().manual_seed(3)
+    n, D = 1000 * 128 + 77, 203
+    cols = [torch.randn(n, generator=g, dtype=dt) * 3 for _ in range(D)]
+    cols[7][11] = float("nan")
+    valid = torch.ones(n, dtype=torch.bool)
+    valid[::331] = False
+    srcs = [(c.to(dev), valid.to(dev) if j == 100 else None, 1) for j, c in enumerate(cols)]
+    out, bad, nbad, d = AS.assemble_bf16(srcs, n, dev, path="cols", window=window)
+    gen, gbad, gnbad, _ = AS.assemble_bf16(srcs, n, dev, path="generic")
+    ref = torch.stack([c.float() for c in cols], 1)
+    ref[:, 100] = torch.where(valid, ref[:, 100], torch.full_like(ref[:, 100], float("nan")))
+    assert d == D and out.shape == gen.shape and out.shape[1] % 8 == 0
+    assert torch.equal(out.view(torch.int16), gen.view(torch.int16))
+    torch.testing.assert_close(out[:, :D].float().cpu(), ref.to(torch.bfloat16).float(), equal_nan=True)
+    assert not out[:, D:].any()
+    rb = torch.isnan(ref).any(1)
+    assert torch.equal(bad.cpu().bool(), rb) and torch.equal(gbad, bad)
+    assert int(nbad) == int(rb.sum()) == int(gnbad)
