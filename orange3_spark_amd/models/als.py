@@ -336,6 +336,7 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
         ckpt.clear()                     # finished: a later fit must not resume from this run
     Uf = comm.all_gather_v(X) if (keep_full and comm.world_size > 1) else X
     Vf = comm.all_gather_v(Y) if (keep_full and comm.world_size > 1) else Y
+    A.EIG_CACHE.clear()                  # drops the rotated factor table
     return AlsResult(uid, iid, Uf, Vf, time.time() - t0, its)
 
 

@@ -122,11 +122,44 @@ def exact_kernel_ok(F: torch.Tensor) -> bool:
     return F.is_cuda and F.dtype == torch.float32 and F.shape[1] in EXACT_RANKS and F.is_contiguous()
 
 
+class _EigCache:
+    """Eigendecomposition of G and the rotated table F Q for the Woodbury rows, kept for
+    the calls of one half-iteration (the chunked path solves its rows in several calls
+    against the same F and G).  Keyed on the tensors themselves (weak references plus
+    their version counters), so an in-place update or a new table recomputes."""
+
+    def __init__(self):
+        self.key = None
+        self.val = None
+
+    def get(self, F, G, need_fq: bool):
+        import weakref
+        key = (F._version, G._version, tuple(F.shape))
+        if (self.key is not None and self.key[0]() is F and self.key[1]() is G and self.key[2] == key
+                and (self.val[2] is not None or not need_fq)):
+            return self.val
+        Gd = G.to(torch.float64)
+        ev, V = torch.linalg.eigh(0.5 * (Gd + Gd.T))
+        eig = ev.clamp_min(0.0).float().contiguous()
+        Q = V.float().contiguous()
+        FQ = torch.mm(F, Q) if need_fq else None
+        self.key = (weakref.ref(F), weakref.ref(G), key)
+        self.val = (eig, Q, FQ)
+        return self.val
+
+    def clear(self):
+        self.key = self.val = None
+
+
+EIG_CACHE = _EigCache()
+
+
 def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor, row_range=None) -> torch.Tensor:
     """Exact per-row solves (csrc/als_exact.hip) written into ``out`` (rows of this CSR,
     or rows [a, b) of it).  Rows with <= 32 ratings and lam_u > 0 take the Woodbury kernel
-    (an n x n Cholesky against the eigendecomposition of G), the others the dense kernel
-    (register Gram + LDS Cholesky).  G = Y^T Y (implicit only)."""
+    (an n x n Cholesky against the eigendecomposition G = Q diag(e) Q^T, gathering rows of
+    the rotated table F Q; x = Q y afterwards as one GEMM over those rows), the others the
+    dense kernel (register Gram + LDS Cholesky).  G = Y^T Y (implicit only)."""
     dev = F.device
     R = F.shape[1]
     n_all = indptr.numel() - 1
@@ -136,18 +169,28 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
     idx = torch.arange(a, e, device=dev, dtype=torch.int32)
     small = idx[small_m].contiguous()
     dense = idx[~small_m].contiguous()
-    Q = QT = eig = Gf = None
-    if implicit:
-        Gd = G.to(torch.float64)
-        ev, V = torch.linalg.eigh(0.5 * (Gd + Gd.T))
-        eig = ev.clamp_min(0.0).float().contiguous()
-        Q = V.float().contiguous()
-        QT = V.T.float().contiguous()
-        Gf = G.float().contiguous()
-    N.check(N.kernels().o3s_als_exact(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
-                                      b.data_ptr(), F.data_ptr(), N.ptr(Gf), N.ptr(Q), N.ptr(QT), N.ptr(eig),
-                                      lam.data_ptr(), small.data_ptr(), int(small.numel()), dense.data_ptr(),
-                                      int(dense.numel()), out.data_ptr(), N.stream_of(out)), "als_exact")
+    ns, nd = int(small.numel()), int(dense.numel())
+    lib = N.kernels()
+    st = N.stream_of(out)
+    if ns:
+        if implicit:
+            eig, Q, P = EIG_CACHE.get(F, G, True)
+        else:
+            eig, Q, P = torch.zeros(R, dtype=torch.float32, device=dev), None, F
+        N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), P.data_ptr(),
+                                 eig.data_ptr(), lam.data_ptr(), small.data_ptr(), ns, out.data_ptr(), st),
+                "als_wood")
+        if implicit:                          # x = Q y for the Woodbury rows (row form: y Q^T)
+            if ns == e - a:
+                out[a:e] = torch.mm(out[a:e], Q.T)
+            else:
+                il = small.long()
+                out.index_copy_(0, il, torch.mm(out.index_select(0, il), Q.T))
+    if nd:
+        Gf = G.float().contiguous() if implicit else None
+        N.check(lib.o3s_als_dense(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                  F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), nd, out.data_ptr(), st),
+                "als_dense")
     return out
 
 

@@ -67,7 +67,7 @@ def assemble_bf16(sources, n: int, device, path: str = "auto", window: int | Non
         if not _cols_ok(sources):
             raise ValueError("the column-window assembler needs plain float / double columns of one dtype")
         w = int(window or WINDOW)
-        grid = max(1, min(N.num_cus(torch.device(device)) * (6 if w == 64 else 3) * 4, -(-n // 128)))
+        grid = max(1, min(N.num_cus(torch.device(device)) * (4 if w == 128 else 8) * 2, -(-n // 128)))
         N.check(lib.o3s_assemble_cols(src_d.data_ptr(), _DT[sources[0][0].dtype], D, ld, n, out.data_ptr(), 0, w,
                                       bad.data_ptr(), nbad.data_ptr(), grid, N.stream_of(out)), "assemble_cols")
         del keep

@@ -10,18 +10,23 @@
 //
 // * als_wood_kernel (n_u <= 32, lam_u > 0; the user side of the ALS config averages 20
 //   ratings): with G = Q diag(e) Q^T (one eigendecomposition per half-iteration, host) and
-//   P = Y_u Q (n x R), Woodbury gives
+//   P = Y_u Q (n x R: rows of the table F Q, rotated once per half-iteration by one GEMM),
+//   Woodbury gives
 //       x_u = Q D P^T z,   D = diag(1 / (e + lam_u)),   S z = W^{-1} c,
 //       S = W^{-1} + P D P^T   (n x n, SPD)
 //   so the only factorisation is an n x n Cholesky -- no 128-step pivot chain per row.
 //   One wave per row: P lives in registers (lane l holds columns l, l + 64 as float2 ->
 //   v_pk_fma), S in LDS (lane i owns row i), triangular solves broadcast with readlane.
-//   Cost ~ n R^2 FMA per row (the P transform), the same as forming the Gram matrix.
-// * als_dense_kernel (longer rows: the item side, ~200 ratings): one block per row; the
-//   Gram matrix accumulates in registers (8 x 8 tile per thread) from factor rows staged
-//   through LDS, then A sits in LDS for a blocked right-looking Cholesky (8-wide panels:
-//   wave 0 factors the diagonal block and the panel, all threads do the trailing update
-//   over the lower triangle), followed by the two triangular solves.
+//   Per row: a gather of n factor rows and n^2 R / 2 FMA -- no rank x rank work at all
+//   (the rotation back, x = Q y, is one GEMM over all Woodbury rows on the host side).
+// * als_dense_kernel (longer rows: the item side, ~200 ratings): one block per row, thread
+//   (i, j) of an (R/8)^2 grid owns the 8 x 8 tile A_ij (lower triangle) in registers for
+//   the whole solve: the Gram matrix accumulates there (packed FMA over factor rows staged
+//   through LDS), then a blocked right-looking Cholesky runs on the tiles -- per 8-wide
+//   panel the diagonal owner factors and inverts its tile, the panel owners form
+//   L_ip = A_ip inv(L_pp)^T and publish it through LDS, every trailing owner subtracts
+//   L_ip L_jp^T -- and the two triangular solves walk the same tiles.  A never touches
+//   LDS; the per-row LDS is the staging buffer, one panel and the 8 x 8 inverses.
 //
 // Both write x_u straight into the factor table.  fp32 throughout (the Gram / S sums are
 // short: n_u terms).
@@ -38,18 +43,16 @@ __device__ __forceinline__ float rl(float v, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
 
-template <int R, bool IMPL>
+template <int R>
 __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
-    const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ Q,
-    const float* __restrict__ QT, const float* __restrict__ eig, const float* __restrict__ lam,
-    const int32_t* __restrict__ rows, int64_t nlist, float* __restrict__ X) {
+    const float* __restrict__ b, const float* __restrict__ P, const float* __restrict__ eig,
+    const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nlist, float* __restrict__ X) {
   static_assert(R % 32 == 0 && R <= 128, "rank must be a multiple of 32, at most 128");
   constexpr int RV = (R + 63) / 64;              // columns per lane (1 or 2)
-  __shared__ float sY[kWW][kNW][R];              // staged factor rows (IMPL)
   __shared__ float sS[kWW][kNW][kNW + 1];        // S, then its Cholesky factor (lower)
-  __shared__ float sv[kWW][R];                   // y = D u, for x = Q y
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t li = (int64_t)blockIdx.x * kWW + wv;
   if (li >= nlist) return;                       // wave-uniform; the kernel has no block barrier
   const int64_t u = rows[li];
@@ -65,61 +68,27 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
     winv = wi > 0.f ? 1.f / wi : 1e30f;
     t = wi > 0.f ? bi * winv : 0.f;
   }
-  float dinv[RV];
-#pragma unroll
-  for (int k = 0; k < RV; ++k) {
-    const int d = lane + 64 * k;
-    dinv[k] = d < R ? 1.f / ((IMPL ? eig[d] : 0.f) + lu) : 0.f;
-  }
-
-  // P = Y_u Q (implicit) or Y_u (explicit), rows of P in registers: acc[i] = (P[i][lane],
-  // P[i][lane + 64]).  Every loop over rows is unrolled to kNW with a uniform guard, so
-  // acc stays in registers (a runtime index would move it to scratch).
   const bool c0ok = lane < R, c1ok = RV > 1 && lane + 64 < R;
+  const float2_ dd = {c0ok ? 1.f / (eig[lane] + lu) : 0.f, c1ok ? 1.f / (eig[lane + 64] + lu) : 0.f};
+
+  // rows of P = Y_u Q gathered from the pre-rotated table (F Q, one GEMM per
+  // half-iteration; F itself when explicit): acc[i] = (P[i][lane], P[i][lane + 64]).
+  // Every loop over rows is unrolled to kNW with a uniform guard, so acc stays in
+  // registers (a runtime index would move it to scratch) and all n row loads are in
+  // flight together.
   float2_ acc[kNW];
 #pragma unroll
-  for (int i = 0; i < kNW; ++i) acc[i] = float2_{0.f, 0.f};
-  if (IMPL) {
-    for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < kNW; ++i) {
+    acc[i] = float2_{0.f, 0.f};
+    if (i < n) {
       const int64_t c = cols[p0 + i];
-      if (c0ok) sY[wv][i][lane] = F[c * R + lane];
-      if (c1ok) sY[wv][i][lane + 64] = F[c * R + lane + 64];
-    }
-    for (int kk = 0; kk < R; kk += 4) {
-      float2_ q[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        q[s].x = c0ok ? Q[(kk + s) * R + lane] : 0.f;
-        q[s].y = c1ok ? Q[(kk + s) * R + lane + 64] : 0.f;
-      }
-#pragma unroll
-      for (int ib = 0; ib < kNW; ib += 8) {
-        if (ib < n) {                            // uniform: rows in blocks of 8
-#pragma unroll
-          for (int i = ib; i < ib + 8; ++i) {
-            const float4_ y = *reinterpret_cast<const float4_*>(&sY[wv][i][kk]);
-            acc[i] = __builtin_elementwise_fma(float2_{y.x, y.x}, q[0], acc[i]);
-            acc[i] = __builtin_elementwise_fma(float2_{y.y, y.y}, q[1], acc[i]);
-            acc[i] = __builtin_elementwise_fma(float2_{y.z, y.z}, q[2], acc[i]);
-            acc[i] = __builtin_elementwise_fma(float2_{y.w, y.w}, q[3], acc[i]);
-          }
-        }
-      }
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < kNW; ++i) {
-      if (i < n) {
-        const int64_t c = cols[p0 + i];
-        acc[i].x = c0ok ? F[c * R + lane] : 0.f;
-        acc[i].y = c1ok ? F[c * R + lane + 64] : 0.f;
-      }
+      acc[i].x = c0ok ? P[c * R + lane] : 0.f;
+      acc[i].y = c1ok ? P[c * R + lane + 64] : 0.f;
     }
   }
 
   // S = diag(W^{-1}) + P D P^T (lower triangle): per-lane partial over its columns, DPP
   // wave sum per entry
-  const float2_ dd = {dinv[0], RV > 1 ? dinv[RV - 1] : 0.f};
 #pragma unroll
   for (int i = 0; i < kNW; ++i) {
     if (i < n) {
@@ -158,7 +127,8 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
     if (lane == k) v = zk;
     else if (lane < k) v -= S[k][lane] * zk;
   }
-  // y = D P^T z
+  // y = D P^T z: the solution in the eigenbasis (implicit; the host rotates x = Q y for all
+  // Woodbury rows with one GEMM) or x itself (explicit, Q = I)
   float2_ uu = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < kNW; ++i) {
@@ -169,54 +139,46 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
   }
   uu = uu * dd;
   float* xo = X + u * R;
-  if (!IMPL) {
-    if (c0ok) xo[lane] = uu.x;
-    if (c1ok) xo[lane + 64] = uu.y;
-    return;
-  }
-  // x = Q y
-  if (c0ok) sv[wv][lane] = uu.x;
-  if (c1ok) sv[wv][lane + 64] = uu.y;
-  float2_ xx = {0.f, 0.f};
-  for (int j = 0; j < R; ++j) {
-    const float yj = sv[wv][j];
-    const float2_ qt = {c0ok ? QT[j * R + lane] : 0.f, c1ok ? QT[j * R + lane + 64] : 0.f};
-    xx = __builtin_elementwise_fma(float2_{yj, yj}, qt, xx);
-  }
-  if (c0ok) xo[lane] = xx.x;
-  if (c1ok) xo[lane + 64] = xx.y;
+  if (c0ok) xo[lane] = uu.x;
+  if (c1ok) xo[lane + 64] = uu.y;
 }
 
 template <int R>
 struct Dense {
   static constexpr int NT = R / 8;                       // 8 x 8 tiles per side
   static constexpr int NTH = NT * NT < 64 ? 64 : NT * NT;
-  static constexpr int LDA = R + 4;                      // 16-B aligned rows, bank spread
   static constexpr int CH = 16;                          // ratings staged per round
+  static constexpr int PS = 68;                          // panel tile stride (floats): 16-B aligned, banks spread
 };
 
+// element (r, c) of a register tile held as 8 rows x 4 float2 (pairs of columns)
+#define T_(a, r, c) a[r][(c) >> 1][(c)&1]
+
 template <int R, bool IMPL>
-__global__ __launch_bounds__(Dense<R>::NTH) void als_dense_kernel(
+__global__ __launch_bounds__(Dense<R>::NTH, 3) void als_dense_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
     const float* __restrict__ lam, const int32_t* __restrict__ rows, float* __restrict__ X) {
   using D = Dense<R>;
-  constexpr int NT = D::NT, NTH = D::NTH, LDA = D::LDA, CH = D::CH;
-  __shared__ float sA[R * LDA];
+  constexpr int NT = D::NT, NTH = D::NTH, CH = D::CH, PS = D::PS;
   __shared__ float sY[CH][R];
   __shared__ float sW[CH], sB[CH];
-  __shared__ float sr[R];
+  __shared__ float sPT[NT][PS];     // current panel: L_ip transposed (column k at [8k .. 8k+7])
+  __shared__ float sI[NT][64];      // inv(L_pp), row-major, every p (kept for the solves)
+  __shared__ float sr[R];           // rhs -> y -> x
   const int tid = threadIdx.x;
   const int64_t u = rows[blockIdx.x];
   const int64_t p0 = indptr[u], p1 = indptr[u + 1];
   const float lu = lam[u];
   const bool act = tid < NT * NT;
-  const int ti = tid / NT, tj = tid % NT;
-  float acc[8][8];
+  const int ti = act ? tid / NT : NT, tj = act ? tid % NT : NT;   // idle threads own no tile
+  float2_ acc[8][4];
 #pragma unroll
   for (int r = 0; r < 8; ++r)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) acc[r][c] = 0.f;
+    for (int h = 0; h < 4; ++h) acc[r][h] = float2_{0.f, 0.f};
+
+  // ---- Gram sum_c w_c y_c y_c^T: tile (ti, tj) in registers, packed FMA ----
   float rhs = 0.f;
   for (int64_t c0 = p0; c0 < p1; c0 += CH) {
     const int m = (int)(p1 - c0 < CH ? p1 - c0 : CH);
@@ -229,171 +191,234 @@ __global__ __launch_bounds__(Dense<R>::NTH) void als_dense_kernel(
       sB[tid] = b[c0 + tid];
     }
     __syncthreads();
-    if (act) {
+    if (act && ti >= tj) {
       for (int c = 0; c < m; ++c) {
         const float wc = sW[c];
-        float a[8], bb[8];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          a[r] = sY[c][8 * ti + r];
-          bb[r] = wc * sY[c][8 * tj + r];
-        }
+        const float4_ a0 = *reinterpret_cast<const float4_*>(&sY[c][8 * ti]);
+        const float4_ a1 = *reinterpret_cast<const float4_*>(&sY[c][8 * ti + 4]);
+        const float4_ b0 = *reinterpret_cast<const float4_*>(&sY[c][8 * tj]);
+        const float4_ b1 = *reinterpret_cast<const float4_*>(&sY[c][8 * tj + 4]);
+        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float2_ bp[4] = {float2_{b0.x, b0.y} * wc, float2_{b0.z, b0.w} * wc, float2_{b1.x, b1.y} * wc,
+                               float2_{b1.z, b1.w} * wc};
 #pragma unroll
         for (int r = 0; r < 8; ++r)
 #pragma unroll
-          for (int q = 0; q < 8; ++q) acc[r][q] = fmaf(a[r], bb[q], acc[r][q]);
+          for (int h = 0; h < 4; ++h) acc[r][h] = __builtin_elementwise_fma(float2_{av[r], av[r]}, bp[h], acc[r][h]);
       }
     }
     if (tid < R)
       for (int c = 0; c < m; ++c) rhs = fmaf(sB[c], sY[c][tid], rhs);
     __syncthreads();
   }
-  if (act) {
+  if (act && ti >= tj) {
 #pragma unroll
     for (int r = 0; r < 8; ++r)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int i = 8 * ti + r, j = 8 * tj + q;
-        sA[i * LDA + j] = acc[r][q] + (IMPL ? G[i * R + j] : 0.f) + (i == j ? lu : 0.f);
+      for (int c = 0; c < 8; ++c) {
+        float v = T_(acc, r, c);
+        if (IMPL) v += G[(8 * ti + r) * R + 8 * tj + c];
+        if (ti == tj && r == c) v += lu;
+        T_(acc, r, c) = v;
       }
   }
   if (tid < R) sr[tid] = rhs;
-  __syncthreads();
 
-  const int lane = tid & 63;
+  // ---- blocked right-looking Cholesky over the register tiles ----
   for (int p = 0; p < NT; ++p) {
-    const int k0 = 8 * p;
-    if (tid < 64) {
-      // diagonal 8 x 8 factor, computed redundantly by every lane of wave 0
-      float L[8][8];
-#pragma unroll
-      for (int r = 0; r < 8; ++r)
-#pragma unroll
-        for (int c = 0; c < 8; ++c) L[r][c] = c <= r ? sA[(k0 + r) * LDA + k0 + c] : 0.f;
+    if (ti == p && tj == p) {
+      // factor the diagonal tile in place (lower), then invert the factor into sI[p]
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        float s = L[c][c];
+        float s = T_(acc, c, c);
 #pragma unroll
-        for (int q = 0; q < c; ++q) s -= L[c][q] * L[c][q];
-        const float dc = sqrtf(fmaxf(s, 1e-30f));
-        L[c][c] = dc;
+        for (int k = 0; k < c; ++k) s -= T_(acc, c, k) * T_(acc, c, k);
+        const float d = sqrtf(fmaxf(s, 1e-30f));
+        const float id = 1.f / d;
+        T_(acc, c, c) = d;
 #pragma unroll
         for (int r = c + 1; r < 8; ++r) {
-          float v = L[r][c];
+          float v = T_(acc, r, c);
 #pragma unroll
-          for (int q = 0; q < c; ++q) v -= L[r][q] * L[c][q];
-          L[r][c] = v / dc;
+          for (int k = 0; k < c; ++k) v -= T_(acc, r, k) * T_(acc, c, k);
+          T_(acc, r, c) = v * id;
         }
       }
-      // panel rows (TRSM l = a L^-T).  For a row r of the diagonal block the same
-      // recursion reproduces L[r][0..r] (its c = r step gives (A_rr - sum L_rq^2) / L_rr =
-      // L_rr); what it writes right of the diagonal is upper triangle, never read.
-      for (int i = k0 + lane; i < R; i += 64) {
-        float a[8];
+      // inv(L_pp) column by column (one column live in registers), rows into sI[p]
 #pragma unroll
-        for (int c = 0; c < 8; ++c) a[c] = sA[i * LDA + k0 + c];
+      for (int c = 0; c < 8; ++c) {
+        float col[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) col[r] = 0.f;
+        col[c] = 1.f / T_(acc, c, c);
+#pragma unroll
+        for (int r = c + 1; r < 8; ++r) {
+          float v = 0.f;
+#pragma unroll
+          for (int k = c; k < r; ++k) v += T_(acc, r, k) * col[k];
+          col[r] = -v / T_(acc, r, r);
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) sI[p][8 * r + c] = col[r];
+      }
+    }
+    __syncthreads();
+    if (tj == p && ti > p && ti < NT) {
+      // panel: L_ip = A_ip inv(L_pp)^T row by row in place, published transposed
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        float t[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          float v = a[c];
+          const float4_ i0 = *reinterpret_cast<const float4_*>(&sI[p][8 * c]);
+          const float4_ i1 = *reinterpret_cast<const float4_*>(&sI[p][8 * c + 4]);
+          const float iv[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
+          float v = 0.f;
 #pragma unroll
-          for (int q = 0; q < c; ++q) v -= a[q] * L[c][q];
-          a[c] = v / L[c][c];
+          for (int k = 0; k <= c; ++k) v = fmaf(T_(acc, r, k), iv[k], v);
+          t[c] = v;
         }
-        // a clamped pivot (singular row, e.g. no ratings and lam = 0) breaks that identity:
-        // store the diagonal itself so the solves never divide by zero
 #pragma unroll
-        for (int c = 0; c < 8; ++c)
-          if (i == k0 + c) a[c] = L[c][c];
+        for (int c = 0; c < 8; ++c) T_(acc, r, c) = t[c];
+      }
 #pragma unroll
-        for (int c = 0; c < 8; ++c) sA[i * LDA + k0 + c] = a[c];
+      for (int k = 0; k < 8; ++k) {
+        *reinterpret_cast<float4_*>(&sPT[ti][8 * k]) =
+            float4_{T_(acc, 0, k), T_(acc, 1, k), T_(acc, 2, k), T_(acc, 3, k)};
+        *reinterpret_cast<float4_*>(&sPT[ti][8 * k + 4]) =
+            float4_{T_(acc, 4, k), T_(acc, 5, k), T_(acc, 6, k), T_(acc, 7, k)};
       }
     }
     __syncthreads();
-    // trailing update of the lower triangle: A_ij -= L_i,panel . L_j,panel
-    const int T = R - k0 - 8;
-    const int ntri = T * (T + 1) / 2;
-    for (int e = tid; e < ntri; e += NTH) {
-      int ii = (int)((sqrtf(8.f * (float)e + 1.f) - 1.f) * 0.5f);
-      while (ii * (ii + 1) / 2 > e) --ii;
-      while ((ii + 1) * (ii + 2) / 2 <= e) ++ii;
-      const int jj = e - ii * (ii + 1) / 2;
-      const int i = k0 + 8 + ii, j = k0 + 8 + jj;
-      const float4_ a0 = *reinterpret_cast<const float4_*>(&sA[i * LDA + k0]);
-      const float4_ a1 = *reinterpret_cast<const float4_*>(&sA[i * LDA + k0 + 4]);
-      const float4_ b0 = *reinterpret_cast<const float4_*>(&sA[j * LDA + k0]);
-      const float4_ b1 = *reinterpret_cast<const float4_*>(&sA[j * LDA + k0 + 4]);
-      float s = a0.x * b0.x + a0.y * b0.y + a0.z * b0.z + a0.w * b0.w + a1.x * b1.x + a1.y * b1.y +
-                a1.z * b1.z + a1.w * b1.w;
-      sA[i * LDA + j] -= s;
-    }
-    __syncthreads();
-  }
-  // triangular solves on wave 0 (lane holds rows lane, lane + 64)
-  if (tid < 64) {
-    constexpr int RV = (R + 63) / 64;
-    float v[RV];
+    if (tj > p && ti >= tj && ti < NT) {
+      // trailing update A_ij -= L_ip L_jp^T (k not unrolled: 16 operand registers live)
+#pragma unroll 1
+      for (int k = 0; k < 8; ++k) {
+        const float4_ a0 = *reinterpret_cast<const float4_*>(&sPT[ti][8 * k]);
+        const float4_ a1 = *reinterpret_cast<const float4_*>(&sPT[ti][8 * k + 4]);
+        const float4_ b0 = *reinterpret_cast<const float4_*>(&sPT[tj][8 * k]);
+        const float4_ b1 = *reinterpret_cast<const float4_*>(&sPT[tj][8 * k + 4]);
+        const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float2_ bp[4] = {float2_{b0.x, b0.y}, float2_{b0.z, b0.w}, float2_{b1.x, b1.y}, float2_{b1.z, b1.w}};
 #pragma unroll
-    for (int k = 0; k < RV; ++k) v[k] = lane + 64 * k < R ? sr[lane + 64 * k] : 0.f;
-    for (int k = 0; k < R; ++k) {
-      const float zk = rl(k < 64 ? v[0] : v[RV - 1], k & 63) / sA[k * LDA + k];
+        for (int r = 0; r < 8; ++r)
 #pragma unroll
-      for (int q = 0; q < RV; ++q) {
-        const int i = lane + 64 * q;
-        if (i == k) v[q] = zk;
-        else if (i > k && i < R) v[q] -= sA[i * LDA + k] * zk;
+          for (int h = 0; h < 4; ++h)
+            acc[r][h] = __builtin_elementwise_fma(float2_{-av[r], -av[r]}, bp[h], acc[r][h]);
       }
     }
-    for (int k = R - 1; k >= 0; --k) {
-      const float xk = rl(k < 64 ? v[0] : v[RV - 1], k & 63) / sA[k * LDA + k];
-#pragma unroll
-      for (int q = 0; q < RV; ++q) {
-        const int i = lane + 64 * q;
-        if (i == k) v[q] = xk;
-        else if (i < k) v[q] -= sA[k * LDA + i] * xk;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < RV; ++q)
-      if (lane + 64 * q < R) X[u * R + lane + 64 * q] = v[q];
   }
-}
 
-template <int R, bool IMPL>
-void launch_exact(const int64_t* indptr, const int32_t* cols, const float* w, const float* b, const float* F,
-                  const float* G, const float* Q, const float* QT, const float* eig, const float* lam,
-                  const int32_t* small, int64_t nsmall, const int32_t* dense, int64_t ndense, float* X,
-                  hipStream_t st) {
-  if (nsmall > 0)
-    hipLaunchKernelGGL((als_wood_kernel<R, IMPL>), dim3((unsigned)((nsmall + kWW - 1) / kWW)), dim3(kWW * 64), 0, st,
-                       indptr, cols, w, b, F, Q, QT, eig, lam, small, nsmall, X);
-  if (ndense > 0)
-    hipLaunchKernelGGL((als_dense_kernel<R, IMPL>), dim3((unsigned)ndense), dim3(Dense<R>::NTH), 0, st, indptr, cols,
-                       w, b, F, G, lam, dense, X);
+  // ---- L y = rhs (forward, right-looking over block rows) ----
+  __syncthreads();
+  for (int p = 0; p < NT; ++p) {
+    if (ti == p && tj == p) {
+      float rv[8], y[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) rv[k] = sr[8 * p + k];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k <= r; ++k) v = fmaf(sI[p][8 * r + k], rv[k], v);
+        y[r] = v;
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) sr[8 * p + r] = y[r];
+    }
+    __syncthreads();
+    if (tj == p && ti > p && ti < NT) {
+      float yv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) yv[k] = sr[8 * p + k];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v = fmaf(T_(acc, r, k), yv[k], v);
+        sr[8 * ti + r] -= v;
+      }
+    }
+    __syncthreads();
+  }
+  // ---- L^T x = y (backward) ----
+  for (int p = NT - 1; p >= 0; --p) {
+    if (ti == p && tj == p) {
+      float rv[8], x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) rv[k] = sr[8 * p + k];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float v = 0.f;
+#pragma unroll
+        for (int r = c; r < 8; ++r) v = fmaf(sI[p][8 * r + c], rv[r], v);
+        x[c] = v;
+      }
+#pragma unroll
+      for (int c = 0; c < 8; ++c) sr[8 * p + c] = x[c];
+    }
+    __syncthreads();
+    if (ti == p && tj < p) {
+      float xv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) xv[k] = sr[8 * p + k];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v = fmaf(T_(acc, r, c), xv[r], v);
+        sr[8 * tj + c] -= v;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < R) X[u * R + tid] = sr[tid];
 }
+#undef T_
 
 }  // namespace
 
-// Exact per-row solves of one ALS half-iteration.  small / dense: row indices (int32) for
-// the Woodbury (n_u <= 32, lam_u > 0) and the dense-Cholesky kernels; implicit: G = Y^T Y
-// (fp32 R x R) with its eigendecomposition G = Q diag(eig) Q^T (Q row-major, QT = Q^T).
-// X (fp32 [rows, R]) receives x_u for every listed row.
-O3S_API int o3s_als_exact(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
-                          const float* b, const float* F, const float* G, const float* Q, const float* QT,
-                          const float* eig, const float* lam, const int32_t* small, int64_t nsmall,
-                          const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
-  if (nsmall < 0 || ndense < 0 || (nsmall > 0 && implicit && (!Q || !QT || !eig)) || (implicit && ndense > 0 && !G))
-    return -1;
-#define O3S_EX(RR)                                                                                          \
+// Woodbury solves (rows with n_u <= 32 ratings and lam_u > 0).  P: the factor table
+// rotated into the eigenbasis of G (F Q, implicit) or F itself (explicit, eig = 0);
+// eig: the eigenvalues of G (zeros when explicit).  X row u receives y_u = D P_u^T z
+// (implicit: the caller applies x = Q y) or x_u (explicit).
+O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
+                         const float* P, const float* eig, const float* lam, const int32_t* small, int64_t nsmall,
+                         float* X, hipStream_t st) {
+  if (nsmall < 0 || !eig || !P) return -1;
+  if (nsmall == 0) return 0;
+  const dim3 grid((unsigned)((nsmall + kWW - 1) / kWW));
+#define O3S_WD(RR)                                                                                          \
   if (R == RR) {                                                                                            \
-    if (implicit)                                                                                           \
-      launch_exact<RR, true>(indptr, cols, w, b, F, G, Q, QT, eig, lam, small, nsmall, dense, ndense, X, st); \
-    else                                                                                                    \
-      launch_exact<RR, false>(indptr, cols, w, b, F, G, Q, QT, eig, lam, small, nsmall, dense, ndense, X, st); \
+    hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, eig, lam, \
+                       small, nsmall, X);                                                                   \
     O3S_CHECK_LAUNCH();                                                                                     \
     return 0;                                                                                               \
   }
-  O3S_EX(32) O3S_EX(64) O3S_EX(96) O3S_EX(128)
-#undef O3S_EX
+  O3S_WD(32) O3S_WD(64) O3S_WD(96) O3S_WD(128)
+#undef O3S_WD
+  return -2;
+}
+
+// Dense solves (any row): register Gram + LDS Cholesky.  implicit: G = Y^T Y (fp32 R x R).
+O3S_API int o3s_als_dense(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
+                          const float* b, const float* F, const float* G, const float* lam, const int32_t* dense,
+                          int64_t ndense, float* X, hipStream_t st) {
+  if (ndense < 0 || (implicit && !G)) return -1;
+  if (ndense == 0) return 0;
+#define O3S_DN(RR)                                                                                            \
+  if (R == RR) {                                                                                              \
+    if (implicit)                                                                                             \
+      hipLaunchKernelGGL((als_dense_kernel<RR, true>), dim3((unsigned)ndense), dim3(Dense<RR>::NTH), 0, st,   \
+                         indptr, cols, w, b, F, G, lam, dense, X);                                            \
+    else                                                                                                      \
+      hipLaunchKernelGGL((als_dense_kernel<RR, false>), dim3((unsigned)ndense), dim3(Dense<RR>::NTH), 0, st,  \
+                         indptr, cols, w, b, F, G, lam, dense, X);                                            \
+    O3S_CHECK_LAUNCH();                                                                                       \
+    return 0;                                                                                                 \
+  }
+  O3S_DN(32) O3S_DN(64) O3S_DN(96) O3S_DN(128)
+#undef O3S_DN
   return -2;
 }
 

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmSrc* __rest
 
 // Fast path: every source a plain [n] column of one dtype T (the common wide table of
 // float / double columns).  A block owns kCRows = 128 rows and walks the output in
-// windows of kCW = 64 or 128 columns (LDS tile 17 / 33 KB for bf16 out):
+// windows of kCW = 32, 64 or 128 columns (LDS tile 8.5 / 17 / 33 KB for bf16 out):
 //   load:  wave w takes columns w, w + 4, ...; lane l reads rows l and l + 64 of 8 columns
 //          per batch (16 independent loads in flight, each wave load a 256-B contiguous
 //          run of one column), converts and writes them transposed into an LDS tile whose
@@ -151,17 +151,13 @@ __global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* _
   constexpr int LS = kCW + PAD;                       // tile row stride (elements): 65 / 129 dwords
   using OT = typename std::conditional<OUT == 0, uint16_t, float>::type;
   __shared__ OT tile[kCRows * LS];
-  __shared__ const T* s_ptr[kMaxSrc];
-  __shared__ const uint8_t* s_val[kMaxSrc];
   __shared__ uint8_t s_bad[kCRows];
-  for (int i = threadIdx.x; i < D; i += kThreads) {
-    s_ptr[i] = reinterpret_cast<const T*>(srcs[i].ptr);
-    s_val[i] = srcs[i].valid;
-  }
   if (threadIdx.x < kCRows) s_bad[threadIdx.x] = 0;
   __syncthreads();
   const int lane = threadIdx.x & (kWave - 1);
-  const int wid = threadIdx.x / kWave;
+  // wave index made provably uniform: the source descriptors are then read with scalar
+  // loads (constant cache) instead of an LDS table, which keeps LDS for the tile alone
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t nblk = (n + kCRows - 1) / kCRows;
   for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
     const int64_t row0 = blk * kCRows;
@@ -176,8 +172,9 @@ __global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* _
         for (int q = 0; q < kCBatch; ++q) {
           const int j = c0 + jb + 4 * q;                // wave-uniform
           if (jb + 4 * q < cw && j < D) {
-            va[q] = s_ptr[j][ra];
-            vb[q] = s_ptr[j][rb];
+            const T* p = reinterpret_cast<const T*>(srcs[j].ptr);
+            va[q] = p[ra];
+            vb[q] = p[rb];
           }
         }
 #pragma unroll
@@ -188,7 +185,7 @@ __global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* _
           if (j < D) {
             a = to_f(va[q]);
             b = to_f(vb[q]);
-            const uint8_t* vm = s_val[j];
+            const uint8_t* vm = srcs[j].valid;
             if (vm != nullptr) {
               if (!vm[ra]) a = __builtin_nanf("");
               if (!vm[rb]) b = __builtin_nanf("");
@@ -270,13 +267,14 @@ O3S_API int o3s_assemble_cols(const void* srcs, int src_dtype, int D, int ld, in
                               int window, void* bad, void* nbad, int grid, hipStream_t st) {
   if (D <= 0 || D > kMaxSrc || ld % 8 != 0 || ld < D || n < 0 || grid <= 0) return -1;
   if (src_dtype != DT_F32 && src_dtype != DT_F64) return -2;
-  if (window != 64 && window != 128) return -3;
+  if (window != 32 && window != 64 && window != 128) return -3;
   if (n == 0) return 0;
 #define O3S_ASM_COLS(T, O, W)                                                                            \
   hipLaunchKernelGGL((assemble_cols_kernel<T, O, W>), dim3(grid), dim3(kThreads), 0, st, (const AsmSrc*)srcs, \
                      D, ld, n, out, (uint8_t*)bad, (int*)nbad)
 #define O3S_ASM_COLS_W(T, O) \
-  if (window == 64) O3S_ASM_COLS(T, O, 64); else O3S_ASM_COLS(T, O, 128)
+  if (window == 32) O3S_ASM_COLS(T, O, 32); else if (window == 64) O3S_ASM_COLS(T, O, 64); \
+  else O3S_ASM_COLS(T, O, 128)
   if (src_dtype == DT_F32) {
     if (out_f32) { O3S_ASM_COLS_W(float, 1); } else { O3S_ASM_COLS_W(float, 0); }
   } else {

@@ -235,7 +235,7 @@ def test_gpu_vector_assembler_fused_kernel_matches_torch(handle):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["float32", "float64"])
-@pytest.mark.parametrize("window", [64, 128])
+@pytest.mark.parametrize("window", [32, 64, 128])
 def test_gpu_assemble_column_window_kernel(dtype, window):
     """assemble_cols_kernel (plain float / double columns, LDS-transposed windows) ==
     the generic gather kernel == a torch reference: several windows with a partial last

@@ -27,7 +27,8 @@ def main():
     cols = [torch.empty(n, dtype=dt, device=dev).uniform_(-1, 1) for _ in range(a.features)]
     srcs = [(c, None, 1) for c in cols]
     res = {"rows": n, "features": a.features, "dtype": a.dtype}
-    for name, kw in (("generic", dict(path="generic")), ("cols_w64", dict(path="cols", window=64)),
+    for name, kw in (("generic", dict(path="generic")), ("cols_w32", dict(path="cols", window=32)),
+                     ("cols_w64", dict(path="cols", window=64)),
                      ("cols_w128", dict(path="cols", window=128))):
         out = AS.assemble_bf16(srcs, n, dev, **kw)
         del out

@@ -30,7 +30,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--users", type=int, default=1_000_000)
     ap.add_argument("--items", type=int, default=100_000)
-    ap.add_argument("--other", type=int, default=1_000_000)
+    ap.add_argument("--other", type=int, default=1_000_000, help="factor rows gathered by the user side")
+    ap.add_argument("--other-item", type=int, default=None, help="factor rows gathered by the item side")
     ap.add_argument("--rank", type=int, default=128)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--explicit", action="store_true")
@@ -39,11 +40,20 @@ def main():
     from orange3_spark_amd.ops import als as A
     dev = torch.device("cuda", 0)
     R, implicit = a.rank, not a.explicit
-    F = torch.randn((a.other, R), device=dev) / R ** 0.5
-    G = (F.double().T @ F.double()).float() if implicit else None
-    res = {"rank": R, "implicit": implicit, "other_rows": a.other}
-    for side, (n, lo, hi) in (("user", (a.users, 1, 40)), ("item", (a.items, 100, 300))):
-        indptr, cols, vals = csr(n, lo, hi, a.other, R, dev, 7 if side == "user" else 8)
+    res = {"rank": R, "implicit": implicit}
+    for side, (n, lo, hi, n_other) in (("user", (a.users, 1, 40, a.other)),
+                                       ("item", (a.items, 100, 300, a.other_item or a.other))):
+        F = torch.randn((n_other, R), device=dev) / R ** 0.5
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        t0.record()
+        G = AE.gram(F).float() if implicit else None
+        if implicit:
+            torch.linalg.eigh(G.double())
+        t1.record()
+        torch.cuda.synchronize()
+        res[side + "_gram_eigh_s"] = t0.elapsed_time(t1) / 1e3
+        indptr, cols, vals = csr(n, lo, hi, n_other, R, dev, 7 if side == "user" else 8)
         w, b, pos = AE._weights(vals, implicit, 1.0)
         rows = torch.repeat_interleave(torch.arange(n, device=dev), indptr[1:] - indptr[:-1])
         lam = (0.1 * torch.zeros(n, device=dev).index_add_(0, rows, pos.float())).contiguous()
@@ -59,9 +69,11 @@ def main():
             torch.cuda.synchronize()
             best = min(best, e0.elapsed_time(e1) / 1e3)
         small = int(((indptr[1:] - indptr[:-1]) <= 32).sum())
-        res[side] = {"rows": n, "ratings": int(indptr[-1]), "woodbury_rows": small, "dense_rows": n - small,
+        res[side] = {"rows": n, "other_rows": n_other, "ratings": int(indptr[-1]), "woodbury_rows": small, "dense_rows": n - small,
                      "s": best, "rows_per_s": n / best, "finite": bool(torch.isfinite(out).all())}
         print(side, res[side], flush=True)
+        del F, out, indptr, cols, vals, w, b, pos, rows, lam
+        torch.cuda.empty_cache()
     print(json.dumps(res))
 
 
