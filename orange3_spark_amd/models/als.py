@@ -57,7 +57,9 @@ def partition(comm, rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, 
     """Route each rating to the rank owning its row block; build CSR sorted by row."""
     W, r = comm.world_size, comm.rank
     if W > 1:
-        owner = (rows * W) // n_rows
+        # the rank r with block_bounds(n_rows, W, r) containing the row:
+        # floor(n r / W) <= x  <=>  r <= ceil((x + 1) W / n) - 1
+        owner = torch.div((rows + 1) * W + n_rows - 1, n_rows, rounding_mode="floor") - 1
         order = torch.argsort(owner, stable=True)
         counts = torch.bincount(owner, minlength=W).tolist()
         packed = torch.stack([rows[order].to(torch.float64), cols[order].to(torch.float64),

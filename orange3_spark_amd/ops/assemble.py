@@ -23,6 +23,7 @@ def supported(t: torch.Tensor) -> bool:
 
 
 WINDOW = int(os.environ.get("O3S_ASM_WINDOW", "64"))
+BATCH = int(os.environ.get("O3S_ASM_BATCH", "8"))
 
 
 def _cols_ok(sources) -> bool:
@@ -33,7 +34,8 @@ def _cols_ok(sources) -> bool:
         t.dtype == dt and t.dim() == 1 and t.stride(0) == 1 and int(w) == 1 for t, _, w in sources)
 
 
-def assemble_bf16(sources, n: int, device, path: str = "auto", window: int | None = None):
+def assemble_bf16(sources, n: int, device, path: str = "auto", window: int | None = None,
+                  batch: int | None = None):
     """``sources``: list of (tensor [n] or [n, >= width] row-major, valid bool [n] or None,
     width).  Returns (bf16 [n, ld] zero padded, uint8 invalid flags [n], invalid count).
     ``path``: "auto" (column-window kernel when every source is a plain float / double
@@ -68,7 +70,7 @@ def assemble_bf16(sources, n: int, device, path: str = "auto", window: int | Non
             raise ValueError("the column-window assembler needs plain float / double columns of one dtype")
         w = int(window or WINDOW)
         grid = max(1, min(N.num_cus(torch.device(device)) * (4 if w == 128 else 8) * 2, -(-n // 128)))
-        N.check(lib.o3s_assemble_cols(src_d.data_ptr(), _DT[sources[0][0].dtype], D, ld, n, out.data_ptr(), 0, w,
+        N.check(lib.o3s_assemble_cols(src_d.data_ptr(), _DT[sources[0][0].dtype], D, ld, n, out.data_ptr(), 0, w, int(batch or BATCH),
                                       bad.data_ptr(), nbad.data_ptr(), grid, N.stream_of(out)), "assemble_cols")
         del keep
         return out, bad, nbad, D

@@ -127,7 +127,7 @@ __global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmSrc* __rest
 // float / double columns).  A block owns kCRows = 128 rows and walks the output in
 // windows of kCW = 32, 64 or 128 columns (LDS tile 8.5 / 17 / 33 KB for bf16 out):
 //   load:  wave w takes columns w, w + 4, ...; lane l reads rows l and l + 64 of 8 columns
-//          per batch (16 independent loads in flight, each wave load a 256-B contiguous
+//          per batch (8 or 16; 16 or 32 independent loads in flight, each wave load a 256-B contiguous
 //          run of one column), converts and writes them transposed into an LDS tile whose
 //          row stride is an odd number of dwords (65 / 129), so the 64 lanes -- 64 rows --
 //          land on 64 different banks;
@@ -137,13 +137,12 @@ __global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmSrc* __rest
 // written whole -- the generic kernel above reads 64 elements of 8 different sources per
 // wave step and writes 16-B pieces of 64 rows 512 B apart.
 constexpr int kCRows = 128;
-constexpr int kCBatch = 8;
 typedef unsigned int uint4_ __attribute__((ext_vector_type(4)));
 
 template <typename T>
 __device__ __forceinline__ float to_f(T v) { return (float)v; }
 
-template <typename T, int OUT, int kCW>
+template <typename T, int OUT, int kCW, int kCBatch>
 __global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* __restrict__ srcs, int D, int ld,
                                                                  int64_t n, void* __restrict__ out,
                                                                  uint8_t* __restrict__ bad, int* __restrict__ nbad) {
@@ -264,14 +263,16 @@ O3S_API int o3s_assemble_src_size() { return (int)sizeof(AsmSrc); }
 // Fast path (see assemble_cols_kernel): srcs[j] is output column j for j < D, every source a
 // contiguous [n] column of dtype src_dtype (DT_F32 or DT_F64), ld % 8 == 0, D <= 512.
 O3S_API int o3s_assemble_cols(const void* srcs, int src_dtype, int D, int ld, int64_t n, void* out, int out_f32,
-                              int window, void* bad, void* nbad, int grid, hipStream_t st) {
+                              int window, int batch, void* bad, void* nbad, int grid, hipStream_t st) {
   if (D <= 0 || D > kMaxSrc || ld % 8 != 0 || ld < D || n < 0 || grid <= 0) return -1;
   if (src_dtype != DT_F32 && src_dtype != DT_F64) return -2;
-  if (window != 32 && window != 64 && window != 128) return -3;
+  if ((window != 32 && window != 64 && window != 128) || (batch != 8 && batch != 16)) return -3;
   if (n == 0) return 0;
-#define O3S_ASM_COLS(T, O, W)                                                                            \
-  hipLaunchKernelGGL((assemble_cols_kernel<T, O, W>), dim3(grid), dim3(kThreads), 0, st, (const AsmSrc*)srcs, \
+#define O3S_ASM_COLS_B(T, O, W, B)                                                                       \
+  hipLaunchKernelGGL((assemble_cols_kernel<T, O, W, B>), dim3(grid), dim3(kThreads), 0, st, (const AsmSrc*)srcs, \
                      D, ld, n, out, (uint8_t*)bad, (int*)nbad)
+#define O3S_ASM_COLS(T, O, W) \
+  if (batch == 8) O3S_ASM_COLS_B(T, O, W, 8); else O3S_ASM_COLS_B(T, O, W, 16)
 #define O3S_ASM_COLS_W(T, O) \
   if (window == 32) O3S_ASM_COLS(T, O, 32); else if (window == 64) O3S_ASM_COLS(T, O, 64); \
   else O3S_ASM_COLS(T, O, 128)
@@ -282,6 +283,7 @@ O3S_API int o3s_assemble_cols(const void* srcs, int src_dtype, int D, int ld, in
   }
 #undef O3S_ASM_COLS_W
 #undef O3S_ASM_COLS
+#undef O3S_ASM_COLS_B
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -125,7 +125,7 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
         frac = _screen_state.get(key, 0.0)
         mode = "split" if frac > SCREEN_MAX_FLAG_FRACTION or not screen_ok(X) else "screen"
         if mode == "split" and frac > 0.0:
-            _screen_state[key] = 0.5 * frac       # re-probe the screen after a few split calls
+            _screen_state[key] = 0.8 * frac       # re-probe the screen after ~6 split calls
     if mode == "screen" and screen_ok(X):
         cnt, rows = _SWS.get(n, X.device)
         cnt.zero_()

@@ -178,6 +178,27 @@ _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp
         "prod": dist.ReduceOp.PRODUCT}
 
 
+# "ring": RCCL's all_gather (rings over xGMI); "mesh": grouped peer-to-peer transfers to
+# every peer at once (TorchComm._all_gather_mesh).  tools/bench_comm.py times both.
+ALLGATHER_ALGO = os.environ.get("O3S_ALLGATHER", "ring")
+
+
+class _Works:
+    """Handle of several outstanding point-to-point transfers (wait() waits for all)."""
+
+    def __init__(self, reqs):
+        self.reqs = list(reqs)
+
+    def wait(self):
+        for q in self.reqs:
+            q.wait()
+        self.reqs = []
+        return True
+
+    def is_completed(self):
+        return all(q.is_completed() for q in self.reqs)
+
+
 class TorchComm(Comm):
     """torch.distributed process group: RCCL (backend "nccl") on GPU, gloo on CPU.
 
@@ -225,7 +246,29 @@ class TorchComm(Comm):
         if self.world_size == 1:
             out.copy_(t)
             return None
+        if ALLGATHER_ALGO == "mesh":
+            return self._all_gather_mesh(out, t.contiguous(), async_op)
         return dist.all_gather_into_tensor(out, t.contiguous(), group=self.group, async_op=async_op)
+
+    def _all_gather_mesh(self, out, t, async_op):
+        """All-gather as W-1 concurrent peer transfers per rank (one grouped batch of
+        isend/irecv): on xGMI every GPU pair has its own link, so each rank's shard leaves
+        on all 7 links at once instead of hopping around a ring.  Rank r's
+        shard lands at out[r k : (r + 1) k] on every rank, like all_gather_into_tensor."""
+        W, r, k = self.world_size, self.rank, t.shape[0]
+        out[r * k:(r + 1) * k].copy_(t)
+        glob = (lambda q: q) if self.group is None else (lambda q: dist.get_global_rank(self.group, q))
+        ops = []
+        for d in range(1, W):
+            to, frm = (r + d) % W, (r - d) % W
+            ops.append(dist.P2POp(dist.isend, t, glob(to), group=self.group))
+            ops.append(dist.P2POp(dist.irecv, out[frm * k:(frm + 1) * k], glob(frm), group=self.group))
+        reqs = dist.batch_isend_irecv(ops)
+        work = _Works(reqs)
+        if async_op:
+            return work
+        work.wait()
+        return None
 
     def reduce_scatter(self, t):
         if self.world_size == 1:

@@ -6,7 +6,8 @@
   all_reduce   2 MB      GBT depth-8 level histogram (bins 32)
   all_reduce   16 MB     GBT level histogram (bins 256)
   all_gather   2.56 GB   ALS item factors 5M x 128 fp32 gathered every half-iteration
-                         (each rank contributes 1/N)
+                         (each rank contributes 1/N); once with RCCL's all_gather (rings)
+                         and once as the full-mesh grouped isend/irecv (O3S_ALLGATHER=mesh)
 
 ``python tools/bench_comm.py --gpus N`` launches N ranks itself (child torch.distributed.run,
 like bench.py); under an existing launcher it runs as one rank.  RCCL over xGMI on GPUs,
@@ -28,7 +29,8 @@ import torch
 
 SIZES = [("all_reduce", 2 << 10, "lr_grad"), ("all_reduce", 528 << 10, "kmeans_sums"),
          ("all_reduce", 2 << 20, "gbt_level_32bins"), ("all_reduce", 16 << 20, "gbt_level_256bins"),
-         ("all_gather", 2_560_000_000, "als_item_factors")]
+         ("all_gather", 2_560_000_000, "als_item_factors"),
+         ("all_gather_mesh", 2_560_000_000, "als_item_factors (peer-to-peer full mesh)")]
 
 
 def _self_launch(n, argv):
@@ -62,7 +64,7 @@ def main(argv=None):
     n = comm.world_size
     res = []
     for op, nbytes, what in SIZES:
-        nb = max(1024, int(nbytes * scale)) if op == "all_gather" else max(256, int(nbytes * min(scale * 64, 1.0)))
+        nb = max(1024, int(nbytes * scale)) if op.startswith("all_gather") else max(256, int(nbytes * min(scale * 64, 1.0)))
         elems = nb // 4
         iters = a.iters if nb < (256 << 20) else max(3, a.iters // 5)
         if op == "all_reduce":
@@ -73,7 +75,10 @@ def main(argv=None):
             shard = max(1, elems // n)
             src = torch.ones(shard, dtype=torch.float32, device=dev)
             out = torch.empty(shard * n, dtype=torch.float32, device=dev)
-            fn = (lambda o=out, x=src: comm.all_gather_into(o, x))
+            if op == "all_gather_mesh" and n > 1:
+                fn = (lambda o=out, x=src: comm._all_gather_mesh(o, x, False))
+            else:
+                fn = (lambda o=out, x=src: comm.all_gather_into(o, x))
             nb = shard * n * 4
             bus = (n - 1) / n if n > 1 else 0.0
         for _ in range(3):

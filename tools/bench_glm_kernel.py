@@ -5,11 +5,14 @@ synthetic-lineage (regenerate-in-kernel) pass.
 """
 import argparse
 import json
+import os
+import sys
 import time
 
 import torch
 
-from orange3_spark_amd.ops import glm as G
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from orange3_spark_amd.ops import glm as G  # noqa: E402
 
 
 def main():
