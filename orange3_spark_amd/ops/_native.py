@@ -54,8 +54,8 @@ _SIGS: dict[str, list] = {
     "o3s_bin_sums": [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp],
     "o3s_glm_softmax": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp],
     "o3s_kmeans_assign": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp],
-    "o3s_kmeans_screen": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, C.c_float, c_vp, c_vp, c_vp,
-                          c_vp, c_i32, c_vp],
+    "o3s_kmeans_screen": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, C.c_float, C.c_float,
+                          C.c_float, C.c_float, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp],
     "o3s_kmeans_update_ws": [c_i32, c_i32, c_i32, C.POINTER(c_i64), C.POINTER(c_i64), C.POINTER(c_i32)],
     "o3s_murmur3_terms": [c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp, c_vp],
     "o3s_als_init": [c_i64, c_i64, c_i32, c_u32, c_i32, c_vp, c_vp],
@@ -79,6 +79,7 @@ _SIGS: dict[str, list] = {
     "o3s_als_wood": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "o3s_als_dense": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "o3s_als_exact_max_small": [],
+    "o3s_als_rotate": [c_i32, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
     "o3s_assemble": [c_vp, c_i32, c_vp, c_i32, c_i32, c_i64, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp],
     "o3s_assemble_src_size": [],
     "o3s_assemble_cols": [c_vp, c_i32, c_i32, c_i32, c_i64, c_vp, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32, c_vp],

@@ -158,8 +158,8 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
     """Exact per-row solves (csrc/als_exact.hip) written into ``out`` (rows of this CSR,
     or rows [a, b) of it).  Rows with <= 32 ratings and lam_u > 0 take the Woodbury kernel
     (an n x n Cholesky against the eigendecomposition G = Q diag(e) Q^T, gathering rows of
-    the rotated table F Q; x = Q y afterwards as one GEMM over those rows), the others the
-    dense kernel (register Gram + LDS Cholesky).  G = Y^T Y (implicit only)."""
+    the rotated table F Q; x = Q y afterwards by als_rotate_kernel), the others the dense
+    kernel (register-tile Gram + blocked Cholesky).  G = Y^T Y (implicit only)."""
     dev = F.device
     R = F.shape[1]
     n_all = indptr.numel() - 1
@@ -180,12 +180,11 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
         N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), P.data_ptr(),
                                  eig.data_ptr(), lam.data_ptr(), small.data_ptr(), ns, out.data_ptr(), st),
                 "als_wood")
-        if implicit:                          # x = Q y for the Woodbury rows (row form: y Q^T)
-            if ns == e - a:
-                out[a:e] = torch.mm(out[a:e], Q.T)
-            else:
-                il = small.long()
-                out.index_copy_(0, il, torch.mm(out.index_select(0, il), Q.T))
+        if implicit:                          # x = Q y for the Woodbury rows (als_rotate_kernel)
+            QT = Q.T.contiguous()
+            grid = max(1, min(N.num_cus(dev) * 2, -(-ns // 32)))
+            N.check(lib.o3s_als_rotate(R, QT.data_ptr(), small.data_ptr(), ns, out.data_ptr(), grid, st),
+                    "als_rotate")
     if nd:
         Gf = G.float().contiguous() if implicit else None
         N.check(lib.o3s_als_dense(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),

@@ -223,19 +223,25 @@ __global__ __launch_bounds__(Dense<R>::NTH, 3) void als_dense_kernel(
       }
   }
   if (tid < R) sr[tid] = rhs;
+  __syncthreads();
 
-  // ---- blocked right-looking Cholesky over the register tiles ----
+  // ---- blocked right-looking Cholesky over the register tiles (the forward solve
+  // L y = rhs rides along: diagonal owners finish y_p, panel owners update r_i) ----
   for (int p = 0; p < NT; ++p) {
     if (ti == p && tj == p) {
-      // factor the diagonal tile in place (lower), then invert the factor into sI[p]
+      // factor the diagonal tile in place (lower; v_rsq, no divisions), invert the factor
+      // into sI[p], and take this block of the forward solve: y_p = inv(L_pp) r_p (r_p
+      // already carries every earlier panel's update)
+      float idv[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         float s = T_(acc, c, c);
 #pragma unroll
         for (int k = 0; k < c; ++k) s -= T_(acc, c, k) * T_(acc, c, k);
-        const float d = sqrtf(fmaxf(s, 1e-30f));
-        const float id = 1.f / d;
-        T_(acc, c, c) = d;
+        s = fmaxf(s, 1e-30f);
+        const float id = __builtin_amdgcn_rsqf(s);
+        idv[c] = id;
+        T_(acc, c, c) = s * id;
 #pragma unroll
         for (int r = c + 1; r < 8; ++r) {
           float v = T_(acc, r, c);
@@ -244,23 +250,34 @@ __global__ __launch_bounds__(Dense<R>::NTH, 3) void als_dense_kernel(
           T_(acc, r, c) = v * id;
         }
       }
+      float rv[8], y[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        rv[k] = sr[8 * p + k];
+        y[k] = 0.f;
+      }
       // inv(L_pp) column by column (one column live in registers), rows into sI[p]
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         float col[8];
 #pragma unroll
         for (int r = 0; r < 8; ++r) col[r] = 0.f;
-        col[c] = 1.f / T_(acc, c, c);
+        col[c] = idv[c];
 #pragma unroll
         for (int r = c + 1; r < 8; ++r) {
           float v = 0.f;
 #pragma unroll
           for (int k = c; k < r; ++k) v += T_(acc, r, k) * col[k];
-          col[r] = -v / T_(acc, r, r);
+          col[r] = -v * idv[r];
         }
 #pragma unroll
-        for (int r = 0; r < 8; ++r) sI[p][8 * r + c] = col[r];
+        for (int r = 0; r < 8; ++r) {
+          sI[p][8 * r + c] = col[r];
+          y[r] = fmaf(col[r], rv[c], y[r]);
+        }
       }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) sr[8 * p + r] = y[r];
     }
     __syncthreads();
     if (tj == p && ti > p && ti < NT) {
@@ -288,6 +305,17 @@ __global__ __launch_bounds__(Dense<R>::NTH, 3) void als_dense_kernel(
         *reinterpret_cast<float4_*>(&sPT[ti][8 * k + 4]) =
             float4_{T_(acc, 4, k), T_(acc, 5, k), T_(acc, 6, k), T_(acc, 7, k)};
       }
+      // forward solve, right-looking: r_i -= L_ip y_p (one writer of r_i per panel)
+      float yv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) yv[k] = sr[8 * p + k];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v = fmaf(T_(acc, r, k), yv[k], v);
+        sr[8 * ti + r] -= v;
+      }
     }
     __syncthreads();
     if (tj > p && ti >= tj && ti < NT) {
@@ -309,38 +337,7 @@ __global__ __launch_bounds__(Dense<R>::NTH, 3) void als_dense_kernel(
     }
   }
 
-  // ---- L y = rhs (forward, right-looking over block rows) ----
   __syncthreads();
-  for (int p = 0; p < NT; ++p) {
-    if (ti == p && tj == p) {
-      float rv[8], y[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) rv[k] = sr[8 * p + k];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        float v = 0.f;
-#pragma unroll
-        for (int k = 0; k <= r; ++k) v = fmaf(sI[p][8 * r + k], rv[k], v);
-        y[r] = v;
-      }
-#pragma unroll
-      for (int r = 0; r < 8; ++r) sr[8 * p + r] = y[r];
-    }
-    __syncthreads();
-    if (tj == p && ti > p && ti < NT) {
-      float yv[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) yv[k] = sr[8 * p + k];
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        float v = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v = fmaf(T_(acc, r, k), yv[k], v);
-        sr[8 * ti + r] -= v;
-      }
-    }
-    __syncthreads();
-  }
   // ---- L^T x = y (backward) ----
   for (int p = NT - 1; p >= 0; --p) {
     if (ti == p && tj == p) {
@@ -376,6 +373,70 @@ __global__ __launch_bounds__(Dense<R>::NTH, 3) void als_dense_kernel(
 }
 #undef T_
 
+// x = Q y for every listed row, in place (the Woodbury rows of an implicit half-iteration
+// come out in the eigenbasis).  Q^T is staged once per block in LDS; each wave rotates 8
+// rows at a time (rows staged in its LDS slice, lane l owns outputs l and l + 64), so
+// every row is computed by the same instruction sequence whatever the row list holds --
+// chunked (multi-rank) and whole-table solves give bit-identical factors.
+constexpr int kRotRows = 8;
+
+template <int R>
+__global__ __launch_bounds__(256) void als_rotate_kernel(const float* __restrict__ QT, const int32_t* __restrict__ rows,
+                                                         int64_t nrows, float* __restrict__ X) {
+  constexpr int RV = (R + 63) / 64;
+  __shared__ float sQ[R * R];                       // sQ[j R + c] = Q[c][j]
+  __shared__ float sYb[4][kRotRows][R];
+  for (int i = threadIdx.x; i < R * R; i += 256) sQ[i] = QT[i];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int64_t base = ((int64_t)blockIdx.x * 4 + wv) * kRotRows; base < nrows;
+       base += (int64_t)gridDim.x * 4 * kRotRows) {
+    int64_t rid[kRotRows];
+#pragma unroll
+    for (int r = 0; r < kRotRows; ++r) {
+      const int64_t i = base + r;
+      rid[r] = i < nrows ? (int64_t)rows[i] : -1;
+#pragma unroll
+      for (int h = 0; h < RV; ++h) {
+        const int c = lane + 64 * h;
+        if (c < R) sYb[wv][r][c] = rid[r] >= 0 ? X[rid[r] * R + c] : 0.f;
+      }
+    }
+    float acc[kRotRows][RV];
+#pragma unroll
+    for (int r = 0; r < kRotRows; ++r)
+#pragma unroll
+      for (int h = 0; h < RV; ++h) acc[r][h] = 0.f;
+    for (int j = 0; j < R; j += 4) {
+      float q[4][RV];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int h = 0; h < RV; ++h) {
+          const int c = lane + 64 * h;
+          q[s4][h] = c < R ? sQ[(j + s4) * R + c] : 0.f;
+        }
+#pragma unroll
+      for (int r = 0; r < kRotRows; ++r) {
+        const float4_ y = *reinterpret_cast<const float4_*>(&sYb[wv][r][j]);
+#pragma unroll
+        for (int h = 0; h < RV; ++h)
+          acc[r][h] = fmaf(y.w, q[3][h], fmaf(y.z, q[2][h], fmaf(y.y, q[1][h], fmaf(y.x, q[0][h], acc[r][h]))));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kRotRows; ++r) {
+      if (rid[r] < 0) continue;
+#pragma unroll
+      for (int h = 0; h < RV; ++h) {
+        const int c = lane + 64 * h;
+        if (c < R) X[rid[r] * R + c] = acc[r][h];
+      }
+    }
+  }
+}
+
 }  // namespace
 
 // Woodbury solves (rows with n_u <= 32 ratings and lam_u > 0).  P: the factor table
@@ -397,6 +458,22 @@ O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, cons
   }
   O3S_WD(32) O3S_WD(64) O3S_WD(96) O3S_WD(128)
 #undef O3S_WD
+  return -2;
+}
+
+// x = Q y in place for the listed rows (QT = Q^T row-major, R x R).
+O3S_API int o3s_als_rotate(int R, const float* QT, const int32_t* rows, int64_t nrows, float* X, int grid,
+                           hipStream_t st) {
+  if (nrows < 0 || !QT || grid <= 0) return -1;
+  if (nrows == 0) return 0;
+#define O3S_RT(RR)                                                                                       \
+  if (R == RR) {                                                                                         \
+    hipLaunchKernelGGL((als_rotate_kernel<RR>), dim3(grid), dim3(256), 0, st, QT, rows, nrows, X);       \
+    O3S_CHECK_LAUNCH();                                                                                  \
+    return 0;                                                                                            \
+  }
+  O3S_RT(32) O3S_RT(64) O3S_RT(96) O3S_RT(128)
+#undef O3S_RT
   return -2;
 }
 

@@ -45,6 +45,21 @@ __device__ __forceinline__ void split_bf16(float v, short& hi, short& lo) {
   lo = (short)f32_to_bf16(v - bf16_to_f32(h));
 }
 
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// x * scale split into two fp16 halves (hi + lo carries ~22 significant bits); the caller
+// picks the power-of-two scale so |x * scale| <= 2^15 (no fp16 overflow)
+__device__ __forceinline__ void split_f16(float v, float scale, short& hi, short& lo) {
+  const float sv = v * scale;
+  const _Float16 h = (_Float16)sv;
+  hi = __builtin_bit_cast(short, h);
+  lo = __builtin_bit_cast(short, (_Float16)(sv - (float)h));
+}
+
+__device__ __forceinline__ float f16_bits_to_f32(uint32_t bits16) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
+}
+
 // KS = D / 16 k-steps, TT = 32-row tiles per wave.  Cpad: centroids padded to 32
 // (padding rows carry cn = +inf).
 template <int KS, int TT>
@@ -247,19 +262,24 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
 }
 
 // ---------------------------------------------------------------------------------
-// kmeans_screen: ONE bf16 MFMA per k-step plus a rigorous error bound.
+// kmeans_screen: ONE fp16 MFMA per k-step plus a rigorous error bound.
 //
-// With xh = bf16(x), ch = bf16(c) the screened distance d~_c = ||c||^2 + (-2 ch).xh
-// differs from cn_c - 2 x.c by at most 2 (|xl.c| + |xh.cl|) + fp32 accumulation
-// <= 2^-6 ||x|| ||c|| (|xl_i| <= 2^-8 |x_i|, Cauchy-Schwarz); E = 2^-5 ||x|| max||c||
-// keeps a 2x margin.  Each lane tracks best, index and SECOND best (one v_med3: the new
+// x and m = -2c are scaled by powers of two (xs, ms: |x xs|, |m ms| <= 2^15, chosen on the
+// host) and rounded to fp16 (11 significant bits, 8x finer than bf16), so the screened
+// distance S d~_c = S ||c||^2 + (m ms)~.(x xs)~ with S = xs ms differs from S (||c||^2 -
+// 2 x.c) by at most S E, where (derivation in ops/kmeans.py::screen_bound)
+//   E = eps_x ||x|| + eps0,   eps_x ~ (2^-8 + 2^-16) max||c||,   eps0: fp16 underflow of
+//   tiny elements and the fp32 ||c||^2 rounding
+// with a 2x margin.  Each lane tracks best, index and SECOND best (one v_med3: the new
 // second is med3(old best, v, old second)); a row whose margin (second - best) exceeds
 // 2E has provably the same arg-min as the exact product and is finished here: its
-// squared distance is recomputed exactly in fp32 from the register-resident split x and
-// the fp32 centre row.  Other rows (near-ties) are appended to a compacted list (one
-// atomic per wave) and re-solved by the split-precision kernel above.  This is 1/3 of
-// the MFMAs of the split kernel; the ||c||^2 bias is folded into the accumulator init
-// (read from LDS), so the epilogue is 4 VALU per distance (cmp, cndmask, min, med3).
+// squared distance is recomputed exactly in fp32 from the register-resident split x
+// (fp16 hi + lo, ~22 bits) and the fp32 centre row.  Other rows (near-ties) are appended
+// to a compacted list (one atomic per wave) and re-solved by the split-precision kernel
+// above.  This is 1/3 of the MFMAs of the split kernel; the S ||c||^2 bias is folded
+// into the accumulator init (read from LDS), so the epilogue is 4 VALU per distance
+// (cmp, cndmask, min, med3).  On structureless data (uniform in a cube) the fp16 bound
+// leaves ~10% of the rows as near ties where the bf16 one flagged nearly all of them.
 //
 // 4 waves (one per SIMD) x TT 32-row tiles per block, 2 blocks per CU: one block's X
 // staging and DMA prologue overlaps the other's MFMA sweep.
@@ -279,9 +299,9 @@ struct ScrLds {
 template <int KS, int TT>
 __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const float* __restrict__ X, int64_t n, int64_t ldx, const uint16_t* __restrict__ Chi,
-    const float* __restrict__ cn, const float* __restrict__ C32, int ldc, int Cpad, float eps_cmax,
-    int32_t* __restrict__ assign, float* __restrict__ mind, int32_t* __restrict__ flag_cnt,
-    int32_t* __restrict__ flag_rows, int Dx) {
+    const float* __restrict__ cn, const float* __restrict__ C32, int ldc, int Cpad, float eps_x, float eps0,
+    float xscale, float sscale, int32_t* __restrict__ assign, float* __restrict__ mind,
+    int32_t* __restrict__ flag_cnt, int32_t* __restrict__ flag_rows, int Dx) {
   using L = ScrLds<KS>;
   constexpr int D = L::D;
   constexpr int G = L::G;
@@ -299,8 +319,8 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
   const int r = lane & 31, h = lane >> 5;
   const int64_t row_base = (int64_t)blockIdx.x * (kScrWaves * 32 * TT) + (int64_t)wid * 32 * TT;
 
-  for (int i = threadIdx.x; i < Cpad; i += kScrThreads) scn[i] = cn[i];
-  // ---- X tiles -> split bf16 fragments (B operand) + ||x||^2.  All XL loads of a tile
+  for (int i = threadIdx.x; i < Cpad; i += kScrThreads) scn[i] = cn[i] * sscale;
+  // ---- X tiles -> split fp16 fragments (hi: B operand) + ||x||^2.  All XL loads of a tile
   // are issued before any is consumed (one HBM round trip per tile), then staged
   // row-contiguously through this wave's LDS slice (slot XOR swizzle: conflict-free
   // transposed reads).
@@ -339,8 +359,8 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         short h0, l0, h1, l1;
-        split_bf16(v[2 * j], h0, l0);
-        split_bf16(v[2 * j + 1], h1, l1);
+        split_f16(v[2 * j], xscale, h0, l0);
+        split_f16(v[2 * j + 1], xscale, h1, l1);
         ph[j] = (uint32_t)(uint16_t)h0 | ((uint32_t)(uint16_t)h1 << 16);
         pl[j] = (uint32_t)(uint16_t)l0 | ((uint32_t)(uint16_t)l1 << 16);
         s = fmaf(v[2 * j], v[2 * j], s);
@@ -414,7 +434,9 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       if (ks + 1 < KS) nh = afrag(ks + 1);
 #pragma unroll
       for (int t = 0; t < TT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t][ks], ks == 0 ? c0 : acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, ah),
+                                                         __builtin_bit_cast(f16x8, bh[t][ks]),
+                                                         ks == 0 ? c0 : acc[t], 0, 0, 0);
     }
   };
   stage(0, 0);
@@ -458,8 +480,9 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const bool take = ob < best[t] || (ob == best[t] && oi < myi);
     const int idx = take ? oi : myi;
     const float bv = fminf(best[t], ob);
-    // exact fp32 squared distance to the chosen centre from x = xh + xl (branch-free:
-    // padded columns hold x = 0 and read c = 0)
+    // exact fp32 squared distance to the chosen centre from x = (xh + xl) / xs
+    // (branch-free: padded columns hold x = 0 and read c = 0)
+    const float ixs = 1.f / xscale;
     const float* cp = C32 + (int64_t)idx * ldc;
     float s = 0.f;
 #pragma unroll
@@ -476,15 +499,15 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t hw = ph[j >> 1], lw = pl[j >> 1];
-        const float xh = __uint_as_float((j & 1) ? (hw & 0xffff0000u) : (hw << 16));
-        const float xl = __uint_as_float((j & 1) ? (lw & 0xffff0000u) : (lw << 16));
-        const float df = (xh + xl) - cv[j];
+        const float xh = f16_bits_to_f32((j & 1) ? (hw >> 16) : (hw & 0xffffu));
+        const float xl = f16_bits_to_f32((j & 1) ? (lw >> 16) : (lw & 0xffffu));
+        const float df = (xh + xl) * ixs - cv[j];
         s = fmaf(df, df, s);
       }
     }
     s += __shfl_xor(s, 32, 64);
     const int64_t row = row_base + t * 32 + r;
-    const float bound = 2.f * eps_cmax * sqrtf(xn[t]);
+    const float bound = 2.f * sscale * (eps_x * sqrtf(xn[t]) + eps0);   // in the scaled units of bv, sec
     const bool ok = row < n && h == 0;
     const bool fl = ok && !(sec - bv > bound);             // near-tie (or NaN): exact re-solve
     if (ok) {
@@ -790,12 +813,14 @@ O3S_API int o3s_kmeans_assign(const float* X, int64_t n, int64_t ldx, int Dx, co
   return 0;
 }
 
-// Screen pass (see kmeans_screen_kernel).  C32: fp32 centres [K][ldc] (ldc % 4 == 0);
-// eps_cmax = 2^-5 * max ||c||; flag_cnt (zeroed by the caller) / flag_rows [n]: near-tie
-// rows for o3s_kmeans_assign(rowlist).  tt: 32-row tiles per wave (1 or 2).
+// Screen pass (see kmeans_screen_kernel).  Ch16: fp16 bits of -2 C ms [Cpad][D]; C32: fp32
+// centres [K][ldc] (ldc % 4 == 0); bound E = eps_x ||x|| + eps0 (unscaled units); xscale =
+// xs, sscale = xs ms; flag_cnt (zeroed by the caller) / flag_rows [n]: near-tie rows for
+// o3s_kmeans_assign(rowlist).  tt: 32-row tiles per wave (1 or 2).
 O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
-                              const float* C32, int ldc, int Cpad, float eps_cmax, int32_t* assign, float* mind,
-                              int32_t* flag_cnt, int32_t* flag_rows, int tt, hipStream_t st) {
+                              const float* C32, int ldc, int Cpad, float eps_x, float eps0, float xscale,
+                              float sscale, int32_t* assign, float* mind, int32_t* flag_cnt, int32_t* flag_rows,
+                              int tt, hipStream_t st) {
   if (n <= 0) return 0;
   const int D = (Dx + 31) / 32 * 32;
   if (Dx % 4 != 0 || D > 160 || ldx % 4 != 0 || ldc % 4 != 0 || Cpad % 32 != 0 || n > 0x7fffffffll) return -1;
@@ -808,7 +833,8 @@ O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, co
     const int64_t grid = (n + rows_per_block - 1) / rows_per_block;                                        \
     if (ScrLds<KS>::BYTES + dyn > 160 * 1024) return -3;                                                   \
     hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, X, n, \
-                       ldx, hi, cn, C32, ldc, Cpad, eps_cmax, assign, mind, flag_cnt, flag_rows, Dx);       \
+                       ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt,     \
+                       flag_rows, Dx);                                                                     \
   }
   switch (D / 16) {
     case 2: if (tt == 2) O3S_KS(2, 2) else O3S_KS(2, 1) break;

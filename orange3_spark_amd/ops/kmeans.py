@@ -6,6 +6,7 @@ fp64 per-cluster (sums [K, D], counts [K]) of this rank's rows (caller all-reduc
 from __future__ import annotations
 
 import ctypes as Ct
+import math
 
 import torch
 
@@ -16,13 +17,15 @@ MAX_KERNEL_D = 160
 
 class Prepared:
     """Centre-side operands of the assign kernels, built once per Lloyd iteration:
-    bf16 hi/lo split of -2*C [Kp, Dp] (zero padded), ||c||^2 [Kp] (+inf padded), the fp32
-    centres [K, D] (exact distance of screened rows) and max ||c|| (screen bound)."""
+    bf16 hi/lo split of -2*C [Kp, Dp] (zero padded; split kernel), fp16 of -2*C*ms with a
+    power-of-two scale ms (screen kernel), ||c||^2 [Kp] (+inf padded), the fp32 centres
+    [K, D] (exact distance of screened rows) and max ||c|| (screen bound)."""
 
-    __slots__ = ("hi", "lo", "cn", "c32", "cmax")
+    __slots__ = ("hi", "lo", "cn", "c32", "cmax", "h16", "ms")
 
-    def __init__(self, hi, lo, cn, c32, cmax):
+    def __init__(self, hi, lo, cn, c32, cmax, h16=None, ms=1.0):
         self.hi, self.lo, self.cn, self.c32, self.cmax = hi, lo, cn, c32, cmax
+        self.h16, self.ms = h16, ms
 
     def __iter__(self):                         # legacy (hi, lo, cn) unpacking
         return iter((self.hi, self.lo, self.cn))
@@ -40,7 +43,46 @@ def prepare_centers(C: torch.Tensor) -> Prepared:
     norms = (Cd * Cd).sum(1)
     cn[:K] = norms.float()
     cmax = float(norms.max().sqrt()) if K else 0.0
-    return Prepared(hi.contiguous(), lo.contiguous(), cn, C.float().contiguous(), cmax)
+    ms = _pow2_scale(float(m2.abs().max()) if K else 0.0)
+    h16 = (m2 * ms).to(torch.float16)
+    return Prepared(hi.contiguous(), lo.contiguous(), cn, C.float().contiguous(), cmax, h16.contiguous(), ms)
+
+
+def _pow2_scale(amax: float, top: float = 2.0 ** 15) -> float:
+    """Largest power of two s with amax * s <= 2^15 (fp16 keeps its 11 bits up there and
+    cannot overflow); 1 for empty / non-finite input."""
+    if not math.isfinite(amax) or amax <= 0.0:
+        return 1.0
+    return 2.0 ** max(-126, min(126, math.floor(math.log2(top / amax))))
+
+
+_XSCALE: dict = {}
+
+
+def x_scale(X: torch.Tensor) -> float:
+    """Power-of-two fp16 scale of the data (max |x| over X: one reduction per data
+    version, cached -- Lloyd iterations reuse it)."""
+    key = (X.data_ptr(), tuple(X.shape), X._version)
+    v = _XSCALE.get(key)
+    if v is None:
+        lo, hi = torch.aminmax(X)
+        v = _pow2_scale(max(-float(lo), float(hi)))
+        _XSCALE.clear()
+        _XSCALE[key] = v
+    return v
+
+
+def screen_bound(P: "Prepared", xs: float, D: int) -> tuple[float, float]:
+    """(eps_x, eps0) of the screen kernel's error bound E = eps_x ||x|| + eps0 on
+    |d~_c - d_c| (unscaled units), with a 2x margin.  With x^ = fp16(x xs)/xs and
+    m^ = fp16(m ms)/ms, m = -2c: |x^ - x| <= 2^-11 |x| + 2^-25/xs (subnormal spacing),
+    likewise for m, so |x^.m^ - x.m| <= 2^-9 ||x|| max||c|| + 2^-24 sqrt(D) max||c|| / xs
+    + 2^-25 sqrt(D) ||x|| / ms; the fp32 accumulation adds <= 2^-17 ||x|| max||c|| and the
+    fp32 ||c||^2 term 2^-24 max||c||^2."""
+    cmax, ms, rd = P.cmax, P.ms, math.sqrt(D)
+    eps_x = 2.0 * (2.0 ** -9 + 2.0 ** -17) * cmax + 2.0 * 2.0 ** -25 * rd / ms
+    eps0 = 2.0 * (2.0 ** -24 * rd * cmax / xs + 2.0 ** -24 * cmax * cmax)
+    return eps_x, eps0
 
 
 def kernel_ok(X: torch.Tensor) -> bool:
@@ -70,9 +112,7 @@ def assign_torch(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 16):
     return a, d
 
 
-# screen-pass bound factor: E = SCREEN_EPS * ||x|| * max||c|| bounds the error of a one-pass
-# bf16 distance (2^-6 derived in csrc/kmeans.hip; 2x margin)
-SCREEN_EPS = 2.0 ** -5
+# screen-pass bound: see screen_bound (fp16 operands, E ~ 2^-8 ||x|| max||c||)
 # fall back to the split-precision kernel for every row once the screen flags this share
 SCREEN_MAX_FLAG_FRACTION = 0.3
 SCREEN_TT = 0                 # 32-row tiles per wave in the screen kernel (0: by D)
@@ -130,10 +170,12 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
         cnt, rows = _SWS.get(n, X.device)
         cnt.zero_()
         tt = SCREEN_TT or (2 if X.shape[1] <= 128 else 1)
-        N.check(lib.o3s_kmeans_screen(X.data_ptr(), n, X.stride(0), X.shape[1], P.hi.data_ptr(), P.cn.data_ptr(),
-                                      P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0],
-                                      Ct.c_float(SCREEN_EPS * P.cmax), a.data_ptr(), d.data_ptr(),
-                                      cnt.data_ptr(), rows.data_ptr(), tt, st), "kmeans_screen")
+        xs = x_scale(X)
+        eps_x, eps0 = screen_bound(P, xs, X.shape[1])
+        N.check(lib.o3s_kmeans_screen(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
+                                      P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
+                                      Ct.c_float(eps0), Ct.c_float(xs), Ct.c_float(xs * P.ms), a.data_ptr(),
+                                      d.data_ptr(), cnt.data_ptr(), rows.data_ptr(), tt, st), "kmeans_screen")
         m = int(cnt.item())                      # the near-tie count sizes the re-solve grid
         _screen_state[key] = m / max(n, 1)
         if stats is not None:
