@@ -149,13 +149,14 @@ struct Dense {
   static constexpr int NTH = NT * NT < 64 ? 64 : NT * NT;
   static constexpr int CH = 16;                          // ratings staged per round
   static constexpr int PS = 68;                          // panel tile stride (floats): 16-B aligned, banks spread
+  static constexpr int MINW = R == 128 ? 3 : 2;          // waves per SIMD the register budget must allow
 };
 
 // element (r, c) of a register tile held as 8 rows x 4 float2 (pairs of columns)
 #define T_(a, r, c) a[r][(c) >> 1][(c)&1]
 
 template <int R, bool IMPL>
-__global__ __launch_bounds__(Dense<R>::NTH, 3) void als_dense_kernel(
+__global__ __launch_bounds__(Dense<R>::NTH, Dense<R>::MINW) void als_dense_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
     const float* __restrict__ lam, const int32_t* __restrict__ rows, float* __restrict__ X) {
@@ -179,18 +180,40 @@ __global__ __launch_bounds__(Dense<R>::NTH, 3) void als_dense_kernel(
     for (int h = 0; h < 4; ++h) acc[r][h] = float2_{0.f, 0.f};
 
   // ---- Gram sum_c w_c y_c y_c^T: tile (ti, tj) in registers, packed FMA ----
-  float rhs = 0.f;
-  for (int64_t c0 = p0; c0 < p1; c0 += CH) {
+  // Staging is software-pipelined: round k + 1's factor rows are loaded into registers
+  // (PF per thread) while round k is multiplied out of LDS, so the gather latency of a
+  // long row is paid once, not once per 16 ratings.
+  constexpr int PF = (CH * R + NTH - 1) / NTH;
+  float pf[PF];
+  float pw = 0.f, pb = 0.f;
+  auto issue = [&](int64_t c0) {
     const int m = (int)(p1 - c0 < CH ? p1 - c0 : CH);
-    for (int e = tid; e < m * R; e += NTH) {
-      const int c = e / R, d = e % R;
-      sY[c][d] = F[(int64_t)cols[c0 + c] * R + d];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int e = tid + q * NTH;
+      const int c = e / R, d = e - c * R;
+      pf[q] = e < m * R ? F[(int64_t)cols[c0 + c] * R + d] : 0.f;
     }
     if (tid < m) {
-      sW[tid] = w[c0 + tid];
-      sB[tid] = b[c0 + tid];
+      pw = w[c0 + tid];
+      pb = b[c0 + tid];
+    }
+  };
+  float rhs = 0.f;
+  if (p0 < p1) issue(p0);
+  for (int64_t c0 = p0; c0 < p1; c0 += CH) {
+    const int m = (int)(p1 - c0 < CH ? p1 - c0 : CH);
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int e = tid + q * NTH;
+      if (e < m * R) sY[e / R][e % R] = pf[q];
+    }
+    if (tid < m) {
+      sW[tid] = pw;
+      sB[tid] = pb;
     }
     __syncthreads();
+    if (c0 + CH < p1) issue(c0 + CH);
     if (act && ti >= tj) {
       for (int c = 0; c < m; ++c) {
         const float wc = sW[c];

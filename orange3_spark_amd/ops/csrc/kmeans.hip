@@ -296,7 +296,7 @@ struct ScrLds {
   static constexpr int BYTES = STAGE_BYTES > X_BYTES ? STAGE_BYTES : X_BYTES;
 };
 
-template <int KS, int TT>
+template <int KS, int TT, bool PAIR>
 __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const float* __restrict__ X, int64_t n, int64_t ldx, const uint16_t* __restrict__ Chi,
     const float* __restrict__ cn, const float* __restrict__ C32, int ldc, int Cpad, float eps_x, float eps0,
@@ -394,13 +394,21 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
   // Running (best, second, index) per row.  The index is kept RELATIVE to the current
   // chunk base (ch*32 + 4h): candidates are then the inline constants (i&3) + 8*(i>>2)
   // and a new chunk costs one subtract -- 4 VALU per distance (cmp, 2 cndmask, med3).
-  float best[TT], second[TT];
-  int bidx[TT];
+  // PAIR also keeps the second's index and the THIRD value (v_med3 again): a row whose
+  // third is clear of the best by the bound has its arg-min among {best, second} and is
+  // settled by two exact distances instead of the split re-solve (8 VALU per distance).
+  float best[TT], second[TT], third[TT];
+  int bidx[TT], sidx[TT];
 #pragma unroll
-  for (int t = 0; t < TT; ++t) { best[t] = INFINITY; second[t] = INFINITY; bidx[t] = 0; }
+  for (int t = 0; t < TT; ++t) {
+    best[t] = INFINITY; second[t] = INFINITY; third[t] = INFINITY; bidx[t] = 0; sidx[t] = 0;
+  }
   auto epilogue = [&](const f32x16 (&a)[TT]) {
 #pragma unroll
-    for (int t = 0; t < TT; ++t) bidx[t] -= 32;          // re-base onto this chunk
+    for (int t = 0; t < TT; ++t) {                       // re-base onto this chunk
+      bidx[t] -= 32;
+      if (PAIR) sidx[t] -= 32;
+    }
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int k = (i & 3) + 8 * (i >> 2);
@@ -408,6 +416,11 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       for (int t = 0; t < TT; ++t) {
         const float dv = a[t][i];
         const bool better = dv < best[t];
+        if (PAIR) {
+          const bool better2 = dv < second[t];
+          third[t] = __builtin_amdgcn_fmed3f(second[t], dv, third[t]);
+          sidx[t] = better ? bidx[t] : (better2 ? k : sidx[t]);
+        }
         second[t] = __builtin_amdgcn_fmed3f(best[t], dv, second[t]);
         bidx[t] = better ? k : bidx[t];
         best[t] = better ? dv : best[t];
@@ -472,19 +485,32 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
 
 #pragma unroll
   for (int t = 0; t < TT; ++t) {
-    // absolute index, then merge the half-waves (disjoint centroid subsets of one row)
+    // absolute indices, then merge the half-waves (disjoint centroid subsets of one row):
+    // the k-th smallest of two sorted triples is min over i + j = k of max(a_i, b_j)
     const int myi = bidx[t] + last_base;
+    const int mys = sidx[t] + last_base;
     const float ob = __shfl_xor(best[t], 32, 64), os = __shfl_xor(second[t], 32, 64);
     const int oi = __shfl_xor(myi, 32, 64);
     const float sec = fminf(fmaxf(best[t], ob), fminf(second[t], os));
     const bool take = ob < best[t] || (ob == best[t] && oi < myi);
     const int idx = take ? oi : myi;
     const float bv = fminf(best[t], ob);
-    // exact fp32 squared distance to the chosen centre from x = (xh + xl) / xs
-    // (branch-free: padded columns hold x = 0 and read c = 0)
+    int idx2 = idx;
+    float thr = INFINITY;
+    if (PAIR) {
+      const float ot = __shfl_xor(third[t], 32, 64);
+      const int osi = __shfl_xor(mys, 32, 64);
+      thr = fminf(fminf(third[t], ot), fminf(fmaxf(second[t], ob), fmaxf(best[t], os)));
+      // the runner-up: the other list's head against the winner list's second
+      idx2 = take ? ((best[t] < os || (best[t] == os && myi < osi)) ? myi : osi)
+                  : ((ob < second[t] || (ob == second[t] && oi < mys)) ? oi : mys);
+    }
+    // exact fp32 squared distances from x = (xh + xl) / xs (branch-free: padded columns
+    // hold x = 0 and read c = 0) -- to the chosen centre, and (PAIR) to the runner-up
     const float ixs = 1.f / xscale;
     const float* cp = C32 + (int64_t)idx * ldc;
-    float s = 0.f;
+    const float* cq = C32 + (int64_t)idx2 * ldc;
+    float s = 0.f, s2 = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int c0 = ks * 16 + 8 * h;
@@ -494,6 +520,15 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       if (!v0) u = make_float4(0.f, 0.f, 0.f, 0.f);
       if (!v1) w = make_float4(0.f, 0.f, 0.f, 0.f);
       const float cv[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+      float cw[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      if (PAIR) {
+        float4 u2 = *reinterpret_cast<const float4*>(cq + (v0 ? c0 : 0));
+        float4 w2 = *reinterpret_cast<const float4*>(cq + (v1 ? c0 + 4 : 0));
+        if (!v0) u2 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (!v1) w2 = make_float4(0.f, 0.f, 0.f, 0.f);
+        cw[0] = u2.x; cw[1] = u2.y; cw[2] = u2.z; cw[3] = u2.w;
+        cw[4] = w2.x; cw[5] = w2.y; cw[6] = w2.z; cw[7] = w2.w;
+      }
       const uint32_t* ph = reinterpret_cast<const uint32_t*>(&bh[t][ks]);
       const uint32_t* pl = reinterpret_cast<const uint32_t*>(&bl[t][ks]);
 #pragma unroll
@@ -501,18 +536,33 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
         const uint32_t hw = ph[j >> 1], lw = pl[j >> 1];
         const float xh = f16_bits_to_f32((j & 1) ? (hw >> 16) : (hw & 0xffffu));
         const float xl = f16_bits_to_f32((j & 1) ? (lw >> 16) : (lw & 0xffffu));
-        const float df = (xh + xl) * ixs - cv[j];
+        const float xv = (xh + xl) * ixs;
+        const float df = xv - cv[j];
         s = fmaf(df, df, s);
+        if (PAIR) {
+          const float dg = xv - cw[j];
+          s2 = fmaf(dg, dg, s2);
+        }
       }
     }
     s += __shfl_xor(s, 32, 64);
+    if (PAIR) s2 += __shfl_xor(s2, 32, 64);
     const int64_t row = row_base + t * 32 + r;
     const float bound = 2.f * sscale * (eps_x * sqrtf(xn[t]) + eps0);   // in the scaled units of bv, sec
     const bool ok = row < n && h == 0;
-    const bool fl = ok && !(sec - bv > bound);             // near-tie (or NaN): exact re-solve
+    bool fl = ok && !(sec - bv > bound);                   // near-tie (or NaN): exact re-solve
+    int pick = idx;
+    float pd = s;
+    if (PAIR && fl && thr - bv > bound) {
+      // every other centre is provably farther than both: the exact pair decides
+      fl = false;
+      const bool second_wins = s2 < s || (s2 == s && idx2 < idx);
+      pick = second_wins ? idx2 : idx;
+      pd = second_wins ? s2 : s;
+    }
     if (ok) {
-      assign[row] = idx;
-      if (mind) mind[row] = s;
+      assign[row] = pick;
+      if (mind) mind[row] = pd;
     }
     const uint64_t m = __ballot(fl);
     if (m) {
@@ -820,7 +870,7 @@ O3S_API int o3s_kmeans_assign(const float* X, int64_t n, int64_t ldx, int Dx, co
 O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
                               const float* C32, int ldc, int Cpad, float eps_x, float eps0, float xscale,
                               float sscale, int32_t* assign, float* mind, int32_t* flag_cnt, int32_t* flag_rows,
-                              int tt, hipStream_t st) {
+                              int tt, int pair, hipStream_t st) {
   if (n <= 0) return 0;
   const int D = (Dx + 31) / 32 * 32;
   if (Dx % 4 != 0 || D > 160 || ldx % 4 != 0 || ldc % 4 != 0 || Cpad % 32 != 0 || n > 0x7fffffffll) return -1;
@@ -829,10 +879,14 @@ O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, co
   const uint16_t* hi = (const uint16_t*)Chi;
 #define O3S_KS(KS, TT)                                                                                     \
   {                                                                                                        \
+    if (pair) O3S_KSP(KS, 1, true) else O3S_KSP(KS, TT, false)   /* PAIR: one tile per wave (registers) */ \
+  }
+#define O3S_KSP(KS, TT, P)                                                                                 \
+  {                                                                                                        \
     const int rows_per_block = kScrWaves * 32 * TT;                                                        \
     const int64_t grid = (n + rows_per_block - 1) / rows_per_block;                                        \
     if (ScrLds<KS>::BYTES + dyn > 160 * 1024) return -3;                                                   \
-    hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, X, n, \
+    hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, X, n, \
                        ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt,     \
                        flag_rows, Dx);                                                                     \
   }
@@ -845,6 +899,7 @@ O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, co
     default: return -2;
   }
 #undef O3S_KS
+#undef O3S_KSP
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -113,10 +113,14 @@ def assign_torch(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 16):
 
 
 # screen-pass bound: see screen_bound (fp16 operands, E ~ 2^-8 ||x|| max||c||)
-# fall back to the split-precision kernel for every row once the screen flags this share
+# auto mode: the plain screen while it flags at most PAIR_FROM of the rows, then the pair
+# screen (top-3 tracking, near ties between two centres settled exactly in-kernel), then
+# the split kernel for every row once even the pair screen flags SCREEN_MAX_FLAG_FRACTION
+PAIR_FROM = 0.03
 SCREEN_MAX_FLAG_FRACTION = 0.3
+SPLIT_REPROBE = 6             # split calls before the pair screen is tried again
 SCREEN_TT = 0                 # 32-row tiles per wave in the screen kernel (0: by D)
-_screen_state: dict = {}      # (data_ptr, shape, Cpad) -> last flagged fraction (decays)
+_screen_state: dict = {}      # (data_ptr, shape, Cpad) -> (mode, flagged fraction, countdown)
 
 
 class _ScreenWs:
@@ -146,9 +150,11 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
     """(cluster int32 [n], squared distance f32 [n]) of every row of X.
 
     GPU: ``mode='screen'`` runs the one-MFMA screen kernel and re-solves only its near-tie
-    rows with the split-precision kernel; ``'split'`` runs the split kernel on every row;
-    ``'auto'`` screens unless the previous call on this X flagged more than
-    ``SCREEN_MAX_FLAG_FRACTION`` of the rows (then it splits directly)."""
+    rows with the split-precision kernel; ``'pair'`` is the screen that also settles
+    two-centre near ties exactly in-kernel; ``'split'`` runs the split kernel on every
+    row; ``'auto'`` moves screen -> pair -> split as the previous call on this X flagged
+    more than ``PAIR_FROM`` / ``SCREEN_MAX_FLAG_FRACTION`` of its rows (and re-probes the
+    pair screen every ``SPLIT_REPROBE`` split calls)."""
     if not kernel_ok(X):
         return assign_torch(X, C)
     P = prepared if isinstance(prepared, Prepared) else prepare_centers(C)
@@ -162,11 +168,17 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
     # push the later Lloyd iterations (k centres) onto the split path
     key = (X.data_ptr(), tuple(X.shape), P.hi.shape[0])
     if mode == "auto":
-        frac = _screen_state.get(key, 0.0)
-        mode = "split" if frac > SCREEN_MAX_FLAG_FRACTION or not screen_ok(X) else "screen"
-        if mode == "split" and frac > 0.0:
-            _screen_state[key] = 0.8 * frac       # re-probe the screen after ~6 split calls
-    if mode == "screen" and screen_ok(X):
+        m, f, cd = _screen_state.get(key, ("screen", 0.0, 0))
+        if not screen_ok(X):
+            mode = "split"
+        elif m == "split" and cd > 0:
+            mode = "split"
+            _screen_state[key] = ("split", f, cd - 1)
+        else:
+            mode = "pair" if m == "split" else m
+    if stats is not None:
+        stats["mode"] = mode
+    if mode in ("screen", "pair") and screen_ok(X):
         cnt, rows = _SWS.get(n, X.device)
         cnt.zero_()
         tt = SCREEN_TT or (2 if X.shape[1] <= 128 else 1)
@@ -175,9 +187,15 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
         N.check(lib.o3s_kmeans_screen(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
                                       P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
                                       Ct.c_float(eps0), Ct.c_float(xs), Ct.c_float(xs * P.ms), a.data_ptr(),
-                                      d.data_ptr(), cnt.data_ptr(), rows.data_ptr(), tt, st), "kmeans_screen")
+                                      d.data_ptr(), cnt.data_ptr(), rows.data_ptr(), tt, int(mode == "pair"), st),
+                "kmeans_screen")
         m = int(cnt.item())                      # the near-tie count sizes the re-solve grid
-        _screen_state[key] = m / max(n, 1)
+        frac = m / max(n, 1)
+        if mode == "screen":
+            _screen_state[key] = ("pair" if frac > PAIR_FROM else "screen", frac, 0)
+        else:
+            _screen_state[key] = (("split", frac, SPLIT_REPROBE) if frac > SCREEN_MAX_FLAG_FRACTION
+                                  else ("pair", frac, 0))
         if stats is not None:
             stats["flagged"] = m
         if m:

@@ -167,10 +167,39 @@ def test_gpu_screen_auto_falls_back_when_most_rows_tie(gpu):
     C = torch.rand(256, 64, generator=g).to(gpu)
     st = {}
     K.assign(X, C, mode="auto", stats=st)
-    if st["flagged"] > 0.3 * X.shape[0]:
+    assert st["mode"] == "screen"
+    if st["flagged"] > K.PAIR_FROM * X.shape[0]:
         st2 = {}
         K.assign(X, C, mode="auto", stats=st2)
-        assert st2["flagged"] == X.shape[0]             # split path taken directly
+        assert st2["mode"] == "pair" and st2["flagged"] <= st["flagged"]
+        if st2["flagged"] > K.SCREEN_MAX_FLAG_FRACTION * X.shape[0]:
+            st3 = {}
+            K.assign(X, C, mode="auto", stats=st3)
+            assert st3["mode"] == "split" and st3["flagged"] == X.shape[0]   # split path taken directly
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,Kc", [(128, 1024), (64, 100), (160, 64), (32, 7)])
+def test_gpu_pair_screen_matches_split(gpu, D, Kc):
+    """The pair screen (top-3 tracking; two-centre near ties settled by exact distances
+    in-kernel) assigns exactly like the split kernel and flags no more rows than the plain
+    screen; duplicated centres (exact ties) resolve to the lower index like the split."""
+    g = torch.Generator(device="cpu").manual_seed(D + Kc)
+    n = 40_009
+    X = (torch.rand(n, D, generator=g) * 2 - 1).to(gpu)
+    C = X[torch.randperm(n, generator=g)[:Kc].to(gpu)].clone() * 0.5
+    P = K.prepare_centers(C)
+    s1, s2 = {}, {}
+    a1, d1 = K.assign(X, C, P, mode="screen", stats=s1)
+    a2, d2 = K.assign(X, C, P, mode="pair", stats=s2)
+    a3, d3 = K.assign(X, C, P, mode="split")
+    assert s2["flagged"] <= s1["flagged"]
+    assert (a2 == a3).float().mean() > 0.9999 and (a1 == a3).float().mean() > 0.9999
+    torch.testing.assert_close(d2, d3, rtol=1e-4, atol=1e-4)
+    C2 = torch.cat([C, C[:1]])
+    b2, _ = K.assign(X[:4096], C2, mode="pair")
+    ref2, _ = K.assign(X[:4096], C2, mode="split")
+    assert torch.equal(b2, ref2)
 
 
 @pytest.mark.gpu
@@ -188,7 +217,9 @@ def test_gpu_fp16_screen_scaling_keeps_exact_argmin(gpu, scale):
     a1, d1 = K.assign(X, C, P, mode="screen", stats=st)
     a3, d3 = K.assign(X, C, P, mode="split")
     assert torch.equal(a1, a3)
-    torch.testing.assert_close(d1, d3, rtol=1e-4, atol=1e-6 * scale * scale)
+    # the split kernel's ||x||^2 + ||c||^2 - 2 x.c cancels to ~1e-7 ||x||^2 where the
+    # screen's direct (x - c)^2 gives 0 (rows that are centres)
+    torch.testing.assert_close(d1, d3, rtol=1e-4, atol=1e-4 * scale * scale)
     assert st["flagged"] < 0.5 * n, st
     assert P.h16.abs().max() <= 2 ** 15 and torch.isfinite(P.h16.float()).all()
 
