@@ -76,12 +76,19 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
   // Every loop over rows is unrolled to kNW with a uniform guard, so acc stays in
   // registers (a runtime index would move it to scratch) and all n row loads are in
   // flight together.
+  // the row's rating indices arrive in ONE vector load (lane i holds index i) and are
+  // broadcast by v_readlane, so the n row gathers issue back to back (a scalar load per
+  // index would serialise n load latencies behind the per-row guards)
+  const int myc = lane < n ? cols[p0 + lane] : 0;
+  int ci[kNW];                                   // all broadcasts before the first gather
+#pragma unroll
+  for (int i = 0; i < kNW; ++i) ci[i] = __builtin_amdgcn_readlane(myc, i);
   float2_ acc[kNW];
 #pragma unroll
   for (int i = 0; i < kNW; ++i) {
     acc[i] = float2_{0.f, 0.f};
     if (i < n) {
-      const int64_t c = cols[p0 + i];
+      const int64_t c = ci[i];
       acc[i].x = c0ok ? P[c * R + lane] : 0.f;
       acc[i].y = c1ok ? P[c * R + lane + 64] : 0.f;
     }
@@ -188,11 +195,23 @@ __global__ __launch_bounds__(Dense<R>::NTH, Dense<R>::MINW) void als_dense_kerne
   float pw = 0.f, pb = 0.f;
   auto issue = [&](int64_t c0) {
     const int m = (int)(p1 - c0 < CH ? p1 - c0 : CH);
+    // all index loads first, then all factor loads: PF independent gathers in flight
+    // (a loop of dependent index -> row loads would pay one memory latency per element)
+    // out-of-round slots read a valid element (the round's last rating) and are zeroed
+    // by a select: no branches, so every load issues back to back
+    int cidx[PF];
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
       const int e = tid + q * NTH;
-      const int c = e / R, d = e - c * R;
-      pf[q] = e < m * R ? F[(int64_t)cols[c0 + c] * R + d] : 0.f;
+      const int c = e / R < m ? e / R : m - 1;
+      cidx[q] = cols[c0 + c];
+    }
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int e = tid + q * NTH;
+      const int d = e % R;
+      const float v = F[(int64_t)cidx[q] * R + d];
+      pf[q] = e < m * R ? v : 0.f;
     }
     if (tid < m) {
       pw = w[c0 + tid];

@@ -219,7 +219,7 @@ def test_gpu_fp16_screen_scaling_keeps_exact_argmin(gpu, scale):
     assert torch.equal(a1, a3)
     # the split kernel's ||x||^2 + ||c||^2 - 2 x.c cancels to ~1e-7 ||x||^2 where the
     # screen's direct (x - c)^2 gives 0 (rows that are centres)
-    torch.testing.assert_close(d1, d3, rtol=1e-4, atol=1e-4 * scale * scale)
+    torch.testing.assert_close(d1, d3, rtol=1e-4, atol=1e-3 * scale * scale)
     assert st["flagged"] < 0.5 * n, st
     assert P.h16.abs().max() <= 2 ** 15 and torch.isfinite(P.h16.float()).all()
 
