@@ -50,7 +50,8 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
     const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nlist, float* __restrict__ X) {
   static_assert(R % 32 == 0 && R <= 128, "rank must be a multiple of 32, at most 128");
   constexpr int RV = (R + 63) / 64;              // columns per lane (1 or 2)
-  __shared__ float sS[kWW][kNW][kNW + 1];        // S, then its Cholesky factor (lower)
+  __shared__ float sS[kWW][kNW][kNW + 1];        // L by columns (Lc[k][i] = L_ik)
+  __shared__ __attribute__((aligned(16))) float sColb[kWW][kNW + 4];   // step k's column, packed
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t li = (int64_t)blockIdx.x * kWW + wv;
@@ -94,8 +95,11 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
     }
   }
 
-  // S = diag(W^{-1}) + P D P^T (lower triangle): per-lane partial over its columns, DPP
-  // wave sum per entry
+  // S = diag(W^{-1}) + P D P^T (lower triangle) straight into registers: lane i keeps row
+  // i (srow[m] = S_im, m <= i); each entry is a DPP wave sum of per-lane partials
+  float srow[kNW];
+#pragma unroll
+  for (int m = 0; m < kNW; ++m) srow[m] = 0.f;
 #pragma unroll
   for (int i = 0; i < kNW; ++i) {
     if (i < n) {
@@ -103,39 +107,56 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
 #pragma unroll
       for (int m = 0; m <= i; ++m) {
         const float sm = wave_sum_dpp(pi.x * acc[m].x + pi.y * acc[m].y);
-        if (lane == 0) S[i][m] = sm;
+        if (lane == i) srow[m] = sm;
       }
     }
   }
-  if (lane < n) S[lane][lane] += winv;
+#pragma unroll
+  for (int m = 0; m < kNW; ++m)
+    if (m == lane) srow[m] += winv;
 
-  // Cholesky of S in LDS (lane i owns row i), right-looking
+  // Cholesky in registers, right-looking, with a SHIFTING row window: after step k lane i
+  // holds S_{i, k+1+j} in srow[j], so the active column is always srow[0] and every
+  // register index is a constant although k runs in an ordinary loop.  Step k: pivot from
+  // lane k (readlane), column k of L published to LDS twice -- packed at [0, n-k-1) for
+  // the rank-1 update (aligned float4 reads) and at Lc[k][i] for the solves.
+  float (*Lc)[kNW + 1] = S;                      // Lc[k][i] = L_ik
+  float* colb = sColb[wv];
   for (int k = 0; k < n; ++k) {
-    const float dk = sqrtf(fmaxf(S[k][k], 1e-30f));
-    const bool own = lane > k && lane < n;
-    float lik = 0.f;
-    if (own) {
-      lik = S[lane][k] / dk;
-      S[lane][k] = lik;
+    const float piv = fmaxf(rl(srow[0], k), 1e-30f);
+    const float id = __builtin_amdgcn_rsqf(piv);
+    const float lik = lane > k ? srow[0] * id : (lane == k ? piv * id : 0.f);
+    if (lane < kNW) Lc[k][lane] = lik;
+    if (lane > k && lane < kNW) colb[lane - k - 1] = lik;
+#pragma unroll
+    for (int j4 = 0; j4 < kNW; j4 += 4) {
+      const float4_ c4 = *reinterpret_cast<const float4_*>(&colb[j4]);
+      const float cj[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = j4 + q;                    // srow[j + 1] = S_{i, k+1+j} before the shift
+        const float nx = j + 1 < kNW ? srow[j + 1] : 0.f;
+        srow[j] = (k + 1 + j <= lane && k + 1 + j < n) ? fmaf(-lik, cj[q], nx) : nx;
+      }
     }
-    if (lane == k) S[k][k] = dk;
-    if (own)
-      for (int j = k + 1; j <= lane; ++j) S[lane][j] -= lik * S[j][k];
   }
-  // S z = W^{-1} c: forward (L y = t), backward (L^T z = y); lane i holds entry i
+  // S z = W^{-1} c: forward L y = t, backward L^T z = y, both reading L by columns from
+  // LDS (lane i holds entry i)
   float v = t;
   for (int k = 0; k < n; ++k) {
-    const float yk = rl(v, k) / S[k][k];
-    if (lane == k) v = yk;
-    else if (lane > k && lane < n) v -= S[lane][k] * yk;
+    const float lik = Lc[k][lane < kNW ? lane : 0];
+    const float yk = rl(v, k) * __builtin_amdgcn_rcpf(Lc[k][k]);
+    v = lane == k ? yk : (lane > k ? fmaf(-lik, yk, v) : v);
   }
   for (int k = n - 1; k >= 0; --k) {
-    const float zk = rl(v, k) / S[k][k];
-    if (lane == k) v = zk;
-    else if (lane < k) v -= S[k][lane] * zk;
+    // L^T row k = L column k: z_k = (y_k - sum_{i > k} L_ik z_i) / L_kk, right-looking:
+    // v_i -= L_ki z_k for i < k (row k of L = entries Lc[i][k])
+    const float lki = Lc[lane < kNW ? lane : 0][k];
+    const float zk = rl(v, k) * __builtin_amdgcn_rcpf(Lc[k][k]);
+    v = lane == k ? zk : (lane < k ? fmaf(-lki, zk, v) : v);
   }
   // y = D P^T z: the solution in the eigenbasis (implicit; the host rotates x = Q y for all
-  // Woodbury rows with one GEMM) or x itself (explicit, Q = I)
+  // Woodbury rows) or x itself (explicit, Q = I)
   float2_ uu = {0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < kNW; ++i) {

@@ -495,6 +495,9 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const bool take = ob < best[t] || (ob == best[t] && oi < myi);
     const int idx = take ? oi : myi;
     const float bv = fminf(best[t], ob);
+    // a row whose distances never compared (all NaN / inf) keeps an out-of-range index:
+    // clamp it for the loads below; the NaN margin flags the row for the exact re-solve
+    const bool idx_ok = idx >= 0 && idx < Cpad;
     int idx2 = idx;
     float thr = INFINITY;
     if (PAIR) {
@@ -508,8 +511,10 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     // exact fp32 squared distances from x = (xh + xl) / xs (branch-free: padded columns
     // hold x = 0 and read c = 0) -- to the chosen centre, and (PAIR) to the runner-up
     const float ixs = 1.f / xscale;
-    const float* cp = C32 + (int64_t)idx * ldc;
-    const float* cq = C32 + (int64_t)idx2 * ldc;
+    const int idc = idx_ok ? idx : 0;
+    const int idc2 = idx2 >= 0 && idx2 < Cpad ? idx2 : idc;
+    const float* cp = C32 + (int64_t)idc * ldc;
+    const float* cq = C32 + (int64_t)idc2 * ldc;
     float s = 0.f, s2 = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -550,14 +555,14 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const int64_t row = row_base + t * 32 + r;
     const float bound = 2.f * sscale * (eps_x * sqrtf(xn[t]) + eps0);   // in the scaled units of bv, sec
     const bool ok = row < n && h == 0;
-    bool fl = ok && !(sec - bv > bound);                   // near-tie (or NaN): exact re-solve
-    int pick = idx;
+    bool fl = ok && (!(sec - bv > bound) || !idx_ok);      // near-tie (or NaN): exact re-solve
+    int pick = idc;
     float pd = s;
-    if (PAIR && fl && thr - bv > bound) {
+    if (PAIR && fl && idx_ok && idc2 == idx2 && thr - bv > bound) {
       // every other centre is provably farther than both: the exact pair decides
       fl = false;
       const bool second_wins = s2 < s || (s2 == s && idx2 < idx);
-      pick = second_wins ? idx2 : idx;
+      pick = second_wins ? idx2 : idc;
       pd = second_wins ? s2 : s;
     }
     if (ok) {

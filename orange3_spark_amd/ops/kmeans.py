@@ -45,7 +45,11 @@ def prepare_centers(C: torch.Tensor) -> Prepared:
     cmax = float(norms.max().sqrt()) if K else 0.0
     ms = _pow2_scale(float(m2.abs().max()) if K else 0.0)
     h16 = (m2 * ms).to(torch.float16)
-    return Prepared(hi.contiguous(), lo.contiguous(), cn, C.float().contiguous(), cmax, h16.contiguous(), ms)
+    # fp32 centres padded to Kp rows (zeros): every index the screen kernel can form is a
+    # valid row
+    c32 = torch.zeros((Kp, D), dtype=torch.float32, device=C.device)
+    c32[:K] = C.float()
+    return Prepared(hi.contiguous(), lo.contiguous(), cn, c32, cmax, h16.contiguous(), ms)
 
 
 def _pow2_scale(amax: float, top: float = 2.0 ** 15) -> float:
@@ -56,19 +60,19 @@ def _pow2_scale(amax: float, top: float = 2.0 ** 15) -> float:
     return 2.0 ** max(-126, min(126, math.floor(math.log2(top / amax))))
 
 
-_XSCALE: dict = {}
+_XSCALE: list = [None, None, 0.0]      # [weakref to X, (shape, version), scale]
 
 
 def x_scale(X: torch.Tensor) -> float:
     """Power-of-two fp16 scale of the data (max |x| over X: one reduction per data
-    version, cached -- Lloyd iterations reuse it)."""
-    key = (X.data_ptr(), tuple(X.shape), X._version)
-    v = _XSCALE.get(key)
-    if v is None:
+    version, cached for the Lloyd iterations on the same tensor).  The cache holds a weak
+    reference to X itself -- never its address, which a later tensor can reuse."""
+    ref, key, v = _XSCALE
+    if ref is None or ref() is not X or key != (tuple(X.shape), X._version):
         lo, hi = torch.aminmax(X)
         v = _pow2_scale(max(-float(lo), float(hi)))
-        _XSCALE.clear()
-        _XSCALE[key] = v
+        import weakref
+        _XSCALE[:] = [weakref.ref(X), (tuple(X.shape), X._version), v]
     return v
 
 
@@ -113,10 +117,13 @@ def assign_torch(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 16):
 
 
 # screen-pass bound: see screen_bound (fp16 operands, E ~ 2^-8 ||x|| max||c||)
-# auto mode: the plain screen while it flags at most PAIR_FROM of the rows, then the pair
-# screen (top-3 tracking, near ties between two centres settled exactly in-kernel), then
-# the split kernel for every row once even the pair screen flags SCREEN_MAX_FLAG_FRACTION
-PAIR_FROM = 0.03
+# auto mode: the plain screen until it flags SCREEN_MAX_FLAG_FRACTION of the rows, then the
+# split kernel for every row (re-probing the screen every SPLIT_REPROBE calls).  The pair
+# screen (top-3 tracking, two-centre near ties settled exactly in-kernel) joins the chain
+# when PAIR_FROM is set: on uniform data it flags ~3x fewer rows than the plain screen but
+# runs one 32-row tile per wave (register budget), which costs what it saves on MI355X
+# (profiles/kmeans_fp16_screen_r3.json), so auto leaves it off by default.
+PAIR_FROM: float | None = None
 SCREEN_MAX_FLAG_FRACTION = 0.3
 SPLIT_REPROBE = 6             # split calls before the pair screen is tried again
 SCREEN_TT = 0                 # 32-row tiles per wave in the screen kernel (0: by D)
@@ -152,9 +159,9 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
     GPU: ``mode='screen'`` runs the one-MFMA screen kernel and re-solves only its near-tie
     rows with the split-precision kernel; ``'pair'`` is the screen that also settles
     two-centre near ties exactly in-kernel; ``'split'`` runs the split kernel on every
-    row; ``'auto'`` moves screen -> pair -> split as the previous call on this X flagged
-    more than ``PAIR_FROM`` / ``SCREEN_MAX_FLAG_FRACTION`` of its rows (and re-probes the
-    pair screen every ``SPLIT_REPROBE`` split calls)."""
+    row; ``'auto'`` moves screen (-> pair when ``PAIR_FROM`` is set) -> split as the
+    previous call on this X flagged more than ``SCREEN_MAX_FLAG_FRACTION`` of its rows, and
+    re-probes the screen every ``SPLIT_REPROBE`` split calls."""
     if not kernel_ok(X):
         return assign_torch(X, C)
     P = prepared if isinstance(prepared, Prepared) else prepare_centers(C)
@@ -175,7 +182,7 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
             mode = "split"
             _screen_state[key] = ("split", f, cd - 1)
         else:
-            mode = "pair" if m == "split" else m
+            mode = ("pair" if PAIR_FROM is not None else "screen") if m == "split" else m
     if stats is not None:
         stats["mode"] = mode
     if mode in ("screen", "pair") and screen_ok(X):
@@ -191,11 +198,12 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
                 "kmeans_screen")
         m = int(cnt.item())                      # the near-tie count sizes the re-solve grid
         frac = m / max(n, 1)
-        if mode == "screen":
-            _screen_state[key] = ("pair" if frac > PAIR_FROM else "screen", frac, 0)
+        if mode == "screen" and PAIR_FROM is not None and frac > PAIR_FROM:
+            _screen_state[key] = ("pair", frac, 0)
+        elif frac > SCREEN_MAX_FLAG_FRACTION:
+            _screen_state[key] = ("split", frac, SPLIT_REPROBE)
         else:
-            _screen_state[key] = (("split", frac, SPLIT_REPROBE) if frac > SCREEN_MAX_FLAG_FRACTION
-                                  else ("pair", frac, 0))
+            _screen_state[key] = (mode, frac, 0)
         if stats is not None:
             stats["flagged"] = m
         if m:

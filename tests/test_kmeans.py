@@ -168,14 +168,10 @@ def test_gpu_screen_auto_falls_back_when_most_rows_tie(gpu):
     st = {}
     K.assign(X, C, mode="auto", stats=st)
     assert st["mode"] == "screen"
-    if st["flagged"] > K.PAIR_FROM * X.shape[0]:
+    if st["flagged"] > K.SCREEN_MAX_FLAG_FRACTION * X.shape[0]:
         st2 = {}
         K.assign(X, C, mode="auto", stats=st2)
-        assert st2["mode"] == "pair" and st2["flagged"] <= st["flagged"]
-        if st2["flagged"] > K.SCREEN_MAX_FLAG_FRACTION * X.shape[0]:
-            st3 = {}
-            K.assign(X, C, mode="auto", stats=st3)
-            assert st3["mode"] == "split" and st3["flagged"] == X.shape[0]   # split path taken directly
+        assert st2["mode"] == "split" and st2["flagged"] == X.shape[0]   # split path taken directly
 
 
 @pytest.mark.gpu
