@@ -124,7 +124,7 @@ def assign_torch(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 16):
 # runs one 32-row tile per wave (register budget), which costs what it saves on MI355X
 # (profiles/kmeans_fp16_screen_r3.json), so auto leaves it off by default.
 PAIR_FROM: float | None = None
-SCREEN_MAX_FLAG_FRACTION = 0.3
+SCREEN_MAX_FLAG_FRACTION = 0.5
 SPLIT_REPROBE = 6             # split calls before the pair screen is tried again
 SCREEN_TT = 0                 # 32-row tiles per wave in the screen kernel (0: by D)
 _screen_state: dict = {}      # (data_ptr, shape, Cpad) -> (mode, flagged fraction, countdown)
