@@ -119,24 +119,31 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
   // holds S_{i, k+1+j} in srow[j], so the active column is always srow[0] and every
   // register index is a constant although k runs in an ordinary loop.  Step k: pivot from
   // lane k (readlane), column k of L published to LDS twice -- packed at [0, n-k-1) for
-  // the rank-1 update (aligned float4 reads) and at Lc[k][i] for the solves.
+  // the rank-1 update (aligned float4 reads) and at Lc[k][i] for the solves.  About
+  // n^2 / 2 FMAs per lane in all.
   float (*Lc)[kNW + 1] = S;                      // Lc[k][i] = L_ik
   float* colb = sColb[wv];
+  if (lane < kNW + 4) colb[lane] = 0.f;          // never-written slots read as 0, not junk
   for (int k = 0; k < n; ++k) {
     const float piv = fmaxf(rl(srow[0], k), 1e-30f);
     const float id = __builtin_amdgcn_rsqf(piv);
     const float lik = lane > k ? srow[0] * id : (lane == k ? piv * id : 0.f);
     if (lane < kNW) Lc[k][lane] = lik;
     if (lane > k && lane < kNW) colb[lane - k - 1] = lik;
+    // rank-1 update + shift.  Entries right of the diagonal (column > lane) and columns
+    // >= n take garbage-free but unused values (lik = 0 above the diagonal), so there is
+    // no per-entry predicate; blocks past column n are skipped whole (uniform branch).
+    const int live = n - k - 1;
 #pragma unroll
     for (int j4 = 0; j4 < kNW; j4 += 4) {
-      const float4_ c4 = *reinterpret_cast<const float4_*>(&colb[j4]);
-      const float cj[4] = {c4.x, c4.y, c4.z, c4.w};
+      if (j4 < live) {
+        const float4_ c4 = *reinterpret_cast<const float4_*>(&colb[j4]);
+        const float cj[4] = {c4.x, c4.y, c4.z, c4.w};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int j = j4 + q;                    // srow[j + 1] = S_{i, k+1+j} before the shift
-        const float nx = j + 1 < kNW ? srow[j + 1] : 0.f;
-        srow[j] = (k + 1 + j <= lane && k + 1 + j < n) ? fmaf(-lik, cj[q], nx) : nx;
+        for (int q = 0; q < 4; ++q) {
+          const int j = j4 + q;                  // srow[j + 1] = S_{i, k+1+j} before the shift
+          srow[j] = fmaf(-lik, cj[q], j + 1 < kNW ? srow[j + 1] : 0.f);
+        }
       }
     }
   }
@@ -174,7 +181,8 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
 template <int R>
 struct Dense {
   static constexpr int NT = R / 8;                       // 8 x 8 tiles per side
-  static constexpr int NTH = NT * NT < 64 ? 64 : NT * NT;
+  static constexpr int NL = NT * (NT + 1) / 2;            // lower-triangle tiles, one per thread
+  static constexpr int NTH = NL <= 64 ? 64 : (NL + 63) / 64 * 64;
   static constexpr int CH = 16;                          // ratings staged per round
   static constexpr int PS = 68;                          // panel tile stride (floats): 16-B aligned, banks spread
   static constexpr int MINW = R == 128 ? 3 : 2;          // waves per SIMD the register budget must allow
@@ -199,8 +207,15 @@ __global__ __launch_bounds__(Dense<R>::NTH, Dense<R>::MINW) void als_dense_kerne
   const int64_t u = rows[blockIdx.x];
   const int64_t p0 = indptr[u], p1 = indptr[u + 1];
   const float lu = lam[u];
-  const bool act = tid < NT * NT;
-  const int ti = act ? tid / NT : NT, tj = act ? tid % NT : NT;   // idle threads own no tile
+  // thread t < NL owns lower tile t = ti (ti + 1) / 2 + tj: the working lanes are packed
+  // into the first waves (no lanes parked on upper tiles); idle threads own no tile
+  const bool act = tid < D::NL;
+  int ti = NT, tj = NT;
+  if (act) {
+    ti = 0;
+    while ((ti + 1) * (ti + 2) / 2 <= tid) ++ti;
+    tj = tid - ti * (ti + 1) / 2;
+  }
   float2_ acc[8][4];
 #pragma unroll
   for (int r = 0; r < 8; ++r)
