@@ -201,7 +201,8 @@ __global__ __launch_bounds__(Dense<R>::NTH, Dense<R>::MINW) void als_dense_kerne
   __shared__ float sY[CH][R];
   __shared__ float sW[CH], sB[CH];
   __shared__ float sPT[NT][PS];     // current panel: L_ip transposed (column k at [8k .. 8k+7])
-  __shared__ float sI[NT][64];      // inv(L_pp), row-major, every p (kept for the solves)
+  __shared__ float sI[NT][64];      // L_pp, row-major (zeros above the diagonal), every p
+  __shared__ float sIdv[NT][8];     // 1 / L_cc of every diagonal tile
   __shared__ float sr[R];           // rhs -> y -> x
   const int tid = threadIdx.x;
   const int64_t u = rows[blockIdx.x];
@@ -328,54 +329,53 @@ __global__ __launch_bounds__(Dense<R>::NTH, Dense<R>::MINW) void als_dense_kerne
           T_(acc, r, c) = v * id;
         }
       }
-      float rv[8], y[8];
+      // publish L_pp (row-major, zeros above the diagonal) and 1 / L_cc; forward
+      // substitution y_p = L_pp^-1 r_p (r_p already carries every earlier panel's update)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        rv[k] = sr[8 * p + k];
-        y[k] = 0.f;
+      for (int r = 0; r < 8; ++r) {
+        float lr[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) lr[c] = c <= r ? T_(acc, r, c) : 0.f;
+        *reinterpret_cast<float4_*>(&sI[p][8 * r]) = float4_{lr[0], lr[1], lr[2], lr[3]};
+        *reinterpret_cast<float4_*>(&sI[p][8 * r + 4]) = float4_{lr[4], lr[5], lr[6], lr[7]};
       }
-      // inv(L_pp) column by column (one column live in registers), rows into sI[p]
+      *reinterpret_cast<float4_*>(&sIdv[p][0]) = float4_{idv[0], idv[1], idv[2], idv[3]};
+      *reinterpret_cast<float4_*>(&sIdv[p][4]) = float4_{idv[4], idv[5], idv[6], idv[7]};
+      float y[8];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        float col[8];
+      for (int r = 0; r < 8; ++r) {
+        float v = sr[8 * p + r];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) col[r] = 0.f;
-        col[c] = idv[c];
-#pragma unroll
-        for (int r = c + 1; r < 8; ++r) {
-          float v = 0.f;
-#pragma unroll
-          for (int k = c; k < r; ++k) v += T_(acc, r, k) * col[k];
-          col[r] = -v * idv[r];
-        }
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          sI[p][8 * r + c] = col[r];
-          y[r] = fmaf(col[r], rv[c], y[r]);
-        }
+        for (int k = 0; k < r; ++k) v = fmaf(-T_(acc, r, k), y[k], v);
+        y[r] = v * idv[r];
       }
 #pragma unroll
       for (int r = 0; r < 8; ++r) sr[8 * p + r] = y[r];
     }
     __syncthreads();
     if (tj == p && ti > p && ti < NT) {
-      // panel: L_ip = A_ip inv(L_pp)^T row by row in place, published transposed
+      // panel: L_ip = A_ip L_pp^-T by forward substitution along each row (the 8 rows are
+      // independent chains), L_pp and 1 / L_cc loaded once into registers
+      float lp[8][8];
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        float t[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const float4_ i0 = *reinterpret_cast<const float4_*>(&sI[p][8 * c]);
-          const float4_ i1 = *reinterpret_cast<const float4_*>(&sI[p][8 * c + 4]);
-          const float iv[8] = {i0.x, i0.y, i0.z, i0.w, i1.x, i1.y, i1.z, i1.w};
-          float v = 0.f;
-#pragma unroll
-          for (int k = 0; k <= c; ++k) v = fmaf(T_(acc, r, k), iv[k], v);
-          t[c] = v;
-        }
-#pragma unroll
-        for (int c = 0; c < 8; ++c) T_(acc, r, c) = t[c];
+        const float4_ l0 = *reinterpret_cast<const float4_*>(&sI[p][8 * r]);
+        const float4_ l1 = *reinterpret_cast<const float4_*>(&sI[p][8 * r + 4]);
+        lp[r][0] = l0.x; lp[r][1] = l0.y; lp[r][2] = l0.z; lp[r][3] = l0.w;
+        lp[r][4] = l1.x; lp[r][5] = l1.y; lp[r][6] = l1.z; lp[r][7] = l1.w;
       }
+      const float4_ d0 = *reinterpret_cast<const float4_*>(&sIdv[p][0]);
+      const float4_ d1 = *reinterpret_cast<const float4_*>(&sIdv[p][4]);
+      const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          float v = T_(acc, r, c);
+#pragma unroll
+          for (int k = 0; k < c; ++k) v = fmaf(-T_(acc, r, k), lp[c][k], v);
+          T_(acc, r, c) = v * dv[c];
+        }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         *reinterpret_cast<float4_*>(&sPT[ti][8 * k]) =
@@ -397,8 +397,9 @@ __global__ __launch_bounds__(Dense<R>::NTH, Dense<R>::MINW) void als_dense_kerne
     }
     __syncthreads();
     if (tj > p && ti >= tj && ti < NT) {
-      // trailing update A_ij -= L_ip L_jp^T (k not unrolled: 16 operand registers live)
-#pragma unroll 1
+      // trailing update A_ij -= L_ip L_jp^T (two k-steps per iteration: the next step's
+      // LDS reads overlap this step's FMAs)
+#pragma unroll 2
       for (int k = 0; k < 8; ++k) {
         const float4_ a0 = *reinterpret_cast<const float4_*>(&sPT[ti][8 * k]);
         const float4_ a1 = *reinterpret_cast<const float4_*>(&sPT[ti][8 * k + 4]);
@@ -419,15 +420,14 @@ __global__ __launch_bounds__(Dense<R>::NTH, Dense<R>::MINW) void als_dense_kerne
   // ---- L^T x = y (backward) ----
   for (int p = NT - 1; p >= 0; --p) {
     if (ti == p && tj == p) {
-      float rv[8], x[8];
+      // back substitution L_pp^T x_p = r_p (L_pp is still in this thread's registers)
+      float x[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) rv[k] = sr[8 * p + k];
+      for (int c = 7; c >= 0; --c) {
+        float v = sr[8 * p + c];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        float v = 0.f;
-#pragma unroll
-        for (int r = c; r < 8; ++r) v = fmaf(sI[p][8 * r + c], rv[r], v);
-        x[c] = v;
+        for (int k = c + 1; k < 8; ++k) v = fmaf(-T_(acc, k, c), x[k], v);
+        x[c] = v * sIdv[p][c];
       }
 #pragma unroll
       for (int c = 0; c < 8; ++c) sr[8 * p + c] = x[c];
