@@ -139,7 +139,8 @@ def main():
     os.makedirs(os.path.join(DOC, "api"), exist_ok=True)
     index = ["# Orange3-Spark-AMD documentation", "",
              "Generated by `tools/make_docs.py` from the widget and ML classes (do not edit by hand).", "",
-             "- [Architecture and kernels](../README.md)", "- [Measured performance](../BASELINE.md)",
+             "- [Architecture and kernels](../README.md)",
+             "- [Runtime: sessions, executors, collectives, kernels](runtime.md)", "- [Measured performance](../BASELINE.md)",
              "- [Design survey of the reference](../SURVEY.md)", "", "## Widgets", ""]
     cur = None
     for cat, mod, cls in widget_classes():
