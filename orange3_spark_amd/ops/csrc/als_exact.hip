@@ -36,8 +36,10 @@ using namespace o3s;
 
 namespace {
 
+typedef float f32x16_ __attribute__((ext_vector_type(16)));
 constexpr int kNW = 32;   // Woodbury path: rows with at most this many ratings
 constexpr int kWW = 2;    // waves (rows) per Woodbury block
+constexpr int kPS = 136;  // LDS row stride of P' (features 0..63 at [0, 64), 64..127 at [68, 132))
 
 __device__ __forceinline__ float rl(float v, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
@@ -50,7 +52,9 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
     const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nlist, float* __restrict__ X) {
   static_assert(R % 32 == 0 && R <= 128, "rank must be a multiple of 32, at most 128");
   constexpr int RV = (R + 63) / 64;              // columns per lane (1 or 2)
-  __shared__ float sS[kWW][kNW][kNW + 1];        // L by columns (Lc[k][i] = L_ik)
+  // per wave: the sqrt(D)-scaled rows P' for the MFMA (32 x kPS floats), later reused for
+  // the S image and L by columns (Lc[k][i] = L_ik)
+  __shared__ __attribute__((aligned(16))) float sP[kWW][kNW * kPS];
   __shared__ __attribute__((aligned(16))) float sColb[kWW][kNW + 4];   // step k's column, packed
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -60,7 +64,7 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
   const int64_t p0 = indptr[u];
   const int n = (int)(indptr[u + 1] - p0);       // <= kNW (host routing)
   const float lu = lam[u];
-  float (*S)[kNW + 1] = sS[wv];
+  float (*S)[kNW + 1] = reinterpret_cast<float (*)[kNW + 1]>(sP[wv]);
 
   // per-rating W^{-1} c (lane i < n holds rating i); w = 0 (r = 0 implicit): no term
   float t = 0.f, winv = 0.f;
@@ -95,22 +99,41 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
     }
   }
 
-  // S = diag(W^{-1}) + P D P^T (lower triangle) straight into registers: lane i keeps row
-  // i (srow[m] = S_im, m <= i); each entry is a DPP wave sum of per-lane partials
-  float srow[kNW];
-#pragma unroll
-  for (int m = 0; m < kNW; ++m) srow[m] = 0.f;
+  // S = P D P^T = P' P'^T with P' = P sqrt(D), on the matrix cores: the rows go through LDS
+  // once (lane l of the MFMA needs row l & 31 of P'), then 64 v_mfma_f32_32x32x2_f32
+  // accumulate the 32 x 32 product in fp32 (feature 64 h + s in k-slot h of step s, the
+  // same value for the A and B operands).  Rows >= n are zero.
+  const float2_ sq = {sqrtf(dd.x), sqrtf(dd.y)};
+  float* sp = sP[wv];
 #pragma unroll
   for (int i = 0; i < kNW; ++i) {
-    if (i < n) {
-      const float2_ pi = acc[i] * dd;
+    sp[i * kPS + lane] = acc[i].x * sq.x;
+    sp[i * kPS + 68 + lane] = acc[i].y * sq.y;
+  }
+  f32x16_ sacc;
 #pragma unroll
-      for (int m = 0; m <= i; ++m) {
-        const float sm = wave_sum_dpp(pi.x * acc[m].x + pi.y * acc[m].y);
-        if (lane == i) srow[m] = sm;
+  for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
+  {
+    const float* rp = sp + (lane & 31) * kPS + (lane >> 5) * 68;
+#pragma unroll
+    for (int s4 = 0; s4 < 64; s4 += 4) {
+      if (s4 < (R < 64 ? R : 64)) {              // steps whose features are all >= R hold zeros
+        const float4_ v = *reinterpret_cast<const float4_*>(rp + s4);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, v.x, sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, v.y, sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, v.z, sacc, 0, 0, 0);
+        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, v.w, sacc, 0, 0, 0);
       }
     }
   }
+  // S image in LDS (C/D map: column lane & 31, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5)),
+  // then every lane takes its row: srow[m] = S_lane,m (the upper part is the symmetric
+  // half, which the Cholesky below never reads)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) S[(r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)][lane & 31] = sacc[r];
+  float srow[kNW];
+#pragma unroll
+  for (int m = 0; m < kNW; ++m) srow[m] = S[lane & 31][m];
 #pragma unroll
   for (int m = 0; m < kNW; ++m)
     if (m == lane) srow[m] += winv;
