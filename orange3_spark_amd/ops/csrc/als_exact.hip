@@ -39,7 +39,7 @@ namespace {
 typedef float f32x16_ __attribute__((ext_vector_type(16)));
 constexpr int kNW = 32;   // Woodbury path: rows with at most this many ratings
 constexpr int kWW = 2;    // waves (rows) per Woodbury block
-constexpr int kPS = 136;  // LDS row stride of P' (features 0..63 at [0, 64), 64..127 at [68, 132))
+constexpr int kPS = 72;   // LDS row stride of a P' half tile (features 32 h + s at [36 h + s])
 
 __device__ __forceinline__ float rl(float v, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
@@ -99,33 +99,35 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
     }
   }
 
-  // S = P D P^T = P' P'^T with P' = P sqrt(D), on the matrix cores: the rows go through LDS
-  // once (lane l of the MFMA needs row l & 31 of P'), then 64 v_mfma_f32_32x32x2_f32
-  // accumulate the 32 x 32 product in fp32 (feature 64 h + s in k-slot h of step s, the
-  // same value for the A and B operands).  Rows >= n are zero.
+  // S = P D P^T = P' P'^T with P' = P sqrt(D), on the matrix cores: each 64-feature half of
+  // the rows goes through a 9 KB LDS tile (lane l of the MFMA needs row l & 31), then 32
+  // v_mfma_f32_32x32x2_f32 per half accumulate the 32 x 32 product in fp32 (feature
+  // 32 h + s in k-slot h of step s -- the same value for the A and B operands), on two
+  // accumulator chains.  Rows >= n are zero.
   const float2_ sq = {sqrtf(dd.x), sqrtf(dd.y)};
   float* sp = sP[wv];
+  f32x16_ sa0, sa1;
 #pragma unroll
-  for (int i = 0; i < kNW; ++i) {
-    sp[i * kPS + lane] = acc[i].x * sq.x;
-    sp[i * kPS + 68 + lane] = acc[i].y * sq.y;
+  for (int r = 0; r < 16; ++r) {
+    sa0[r] = 0.f;
+    sa1[r] = 0.f;
   }
-  f32x16_ sacc;
+  const int wcol = lane < 32 ? lane : lane + 4;
+  const float* rp = sp + (lane & 31) * kPS + (lane >> 5) * 36;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) sacc[r] = 0.f;
-  {
-    const float* rp = sp + (lane & 31) * kPS + (lane >> 5) * 68;
+  for (int hf = 0; hf < RV; ++hf) {
 #pragma unroll
-    for (int s4 = 0; s4 < 64; s4 += 4) {
-      if (s4 < (R < 64 ? R : 64)) {              // steps whose features are all >= R hold zeros
-        const float4_ v = *reinterpret_cast<const float4_*>(rp + s4);
-        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, v.x, sacc, 0, 0, 0);
-        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, v.y, sacc, 0, 0, 0);
-        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, v.z, sacc, 0, 0, 0);
-        sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, v.w, sacc, 0, 0, 0);
-      }
+    for (int i = 0; i < kNW; ++i) sp[i * kPS + wcol] = hf == 0 ? acc[i].x * sq.x : acc[i].y * sq.y;
+#pragma unroll
+    for (int s4 = 0; s4 < 32; s4 += 4) {
+      const float4_ v = *reinterpret_cast<const float4_*>(rp + s4);
+      sa0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.x, v.x, sa0, 0, 0, 0);
+      sa1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, v.y, sa1, 0, 0, 0);
+      sa0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, v.z, sa0, 0, 0, 0);
+      sa1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, v.w, sa1, 0, 0, 0);
     }
   }
+  const f32x16_ sacc = sa0 + sa1;
   // S image in LDS (C/D map: column lane & 31, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5)),
   // then every lane takes its row: srow[m] = S_lane,m (the upper part is the symmetric
   // half, which the Cholesky below never reads)
