@@ -133,12 +133,10 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
   // half, which the Cholesky below never reads)
 #pragma unroll
   for (int r = 0; r < 16; ++r) S[(r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)][lane & 31] = sacc[r];
+  if (lane < kNW) S[lane][lane] += winv;         // W^{-1} on the diagonal, in the image
   float srow[kNW];
 #pragma unroll
   for (int m = 0; m < kNW; ++m) srow[m] = S[lane & 31][m];
-#pragma unroll
-  for (int m = 0; m < kNW; ++m)
-    if (m == lane) srow[m] += winv;
 
   // Cholesky in registers, right-looking, with a SHIFTING row window: after step k lane i
   // holds S_{i, k+1+j} in srow[j], so the active column is always srow[0] and every
