@@ -7,8 +7,8 @@ update); prints one JSON line (samples/s per iteration).
 cluster structure, so many rows sit near a Voronoi boundary); ``--init offset`` (true
 centres + 0.5, blobs only) vs ``--init kmeans||`` (Spark's default k-means|| init, timed
 separately).  The JSON reports ``flagged_fraction`` -- the share of rows whose one-MFMA
-bf16 screen could not certify the argmin and were re-solved by the split-precision kernel
--- and the assign rate as ``bf16_screen_tflops`` (screen mode: 2 N K D / t with ONE bf16
+fp16 screen could not certify the argmin and were re-solved by the split-precision kernel
+-- and the assign rate as ``fp16_screen_tflops`` (screen mode: 2 N K D / t with ONE fp16
 MFMA per k-step, not an fp32 rate) or ``split_fp32_equiv_tflops`` (split mode: three bf16
 MFMAs emulate fp32).
 """
@@ -97,7 +97,7 @@ def main():
     dt = (time.perf_counter() - t0) / a.iters
     flop = 2.0 * a.rows * a.k * a.d
     flagged = st.get("flagged")
-    rate_key = "split_fp32_equiv_tflops" if (a.mode == "split" or flagged == a.rows) else "bf16_screen_tflops"
+    rate_key = "split_fp32_equiv_tflops" if (a.mode == "split" or flagged == a.rows) else "fp16_screen_tflops"
     out = {"metric": "KMeans Lloyd iteration samples/s (k=1024, 100M x 128 fp32)", "value": a.rows / dt,
            "unit": "samples/s", "ms_per_iter": dt * 1e3, "assign_ms": t_assign * 1e3, "update_ms": t_upd * 1e3,
            rate_key: flop / t_assign / 1e12, "rows": a.rows, "d": a.d, "k": a.k, "cost": cost,
