@@ -339,6 +339,7 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
     Uf = comm.all_gather_v(X) if (keep_full and comm.world_size > 1) else X
     Vf = comm.all_gather_v(Y) if (keep_full and comm.world_size > 1) else Y
     A.EIG_CACHE.clear()                  # drops the rotated factor table
+    A.PAD_CACHE.clear()
     return AlsResult(uid, iid, Uf, Vf, time.time() - t0, its)
 
 

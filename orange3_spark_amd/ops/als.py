@@ -119,7 +119,38 @@ EXACT_RANKS = (32, 64, 96, 128)
 
 
 def exact_kernel_ok(F: torch.Tensor) -> bool:
-    return F.is_cuda and F.dtype == torch.float32 and F.shape[1] in EXACT_RANKS and F.is_contiguous()
+    """Any rank up to 128 runs on the kernels: ranks between the compiled sizes are padded
+    with zero factor columns (see :func:`exact_solve`)."""
+    return F.is_cuda and F.dtype == torch.float32 and 0 < F.shape[1] <= EXACT_RANKS[-1] and F.is_contiguous()
+
+
+def _padded_rank(R: int) -> int:
+    return next(r for r in EXACT_RANKS if r >= R)
+
+
+class _PadCache:
+    """Zero-padded copy of a factor table (rank R -> the next compiled size), reused by
+    the calls of one half-iteration; keyed like _EigCache on the tensor and its version."""
+
+    def __init__(self):
+        self.key = None
+        self.val = None
+
+    def get(self, F, Rp):
+        import weakref
+        key = (F._version, tuple(F.shape), Rp)
+        if self.key is not None and self.key[0]() is F and self.key[1] == key:
+            return self.val
+        Fp = torch.zeros((F.shape[0], Rp), dtype=F.dtype, device=F.device)
+        Fp[:, :F.shape[1]] = F
+        self.key, self.val = (weakref.ref(F), key), Fp
+        return Fp
+
+    def clear(self):
+        self.key = self.val = None
+
+
+PAD_CACHE = _PadCache()
 
 
 class _EigCache:
@@ -162,6 +193,23 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
     kernel (register-tile Gram + blocked Cholesky).  G = Y^T Y (implicit only)."""
     dev = F.device
     R = F.shape[1]
+    if R not in EXACT_RANKS:
+        # zero columns for the padded dimensions: the padded system is block diagonal with
+        # a lam_u * I block (implicit: G padded with zeros), so its solution is [x_u, 0]
+        Rp = _padded_rank(R)
+        Fp = PAD_CACHE.get(F, Rp)
+        Gp = None
+        if G is not None:
+            Gp = torch.zeros((Rp, Rp), dtype=G.dtype, device=G.device)
+            Gp[:R, :R] = G
+        a0, e0 = (0, indptr.numel() - 1) if row_range is None else row_range
+        outp = torch.zeros((e0 - a0, Rp), dtype=torch.float32, device=dev)
+        sub = indptr[a0:e0 + 1]
+        exact_solve(sub - sub[0] if a0 else sub, cols[int(sub[0]):int(sub[-1])] if a0 else cols,
+                    w[int(sub[0]):int(sub[-1])] if a0 else w, b[int(sub[0]):int(sub[-1])] if a0 else b,
+                    Fp, Gp, lam[a0:e0].contiguous(), implicit, outp)
+        out[a0:e0] = outp[:, :R]
+        return out
     n_all = indptr.numel() - 1
     a, e = (0, n_all) if row_range is None else row_range
     cnt = (indptr[a + 1:e + 1] - indptr[a:e])

@@ -245,3 +245,26 @@ def test_gpu_exact_als_rank128_fit_matches_fp64():
     for a, b in ((gpu.U, cpu.U), (gpu.V, cpu.V)):
         err = (a.cpu().double() - b.double()).norm() / b.double().norm()
         assert float(err) < 5e-3, float(err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [10, 40])
+@pytest.mark.parametrize("implicit", [False, True])
+def test_gpu_exact_kernels_pad_other_ranks(R, implicit):
+    """Ranks between the compiled kernel sizes (Spark's default rank 10, or 40) run on the
+    kernels with zero-padded factor columns and match the fp64 solve; a row range writes
+    only its rows."""
+    from orange3_spark_amd.ops import als as A
+    indptr, cols, w, b, F, G, lam = _exact_case(R, implicit, seed=3)
+    n = indptr.numel() - 1
+    got = torch.full((n, R), float("nan"), device=F.device)
+    A.exact_solve(indptr, cols, w, b, F, G, lam, implicit, got)
+    ref = torch.empty((n, R), dtype=torch.float64, device=F.device)
+    A.exact_solve_torch(indptr, cols, w, b, F, G, lam, ref)
+    assert not torch.isnan(got).any()
+    err = (got.double() - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-6)
+    assert float(err.max()) < 2e-3, float(err.max())
+    part = torch.zeros((n, R), device=F.device)
+    A.exact_solve(indptr, cols, w, b, F, G, lam, implicit, part, row_range=(100, 300))
+    assert torch.allclose(part[100:300], got[100:300], rtol=1e-5, atol=1e-6)
+    assert not part[:100].any() and not part[300:].any()
