@@ -138,3 +138,81 @@ def test_pipeline_fixture(s, tmp_path):
     assert _meta(str(tmp_path / "pm"))["paramMap"]["stageUids"] == _meta(path)["paramMap"]["stageUids"]
     stage = "stages/1_LogisticRegression_4d3a1b2c5e6f"
     _same_layout(os.path.join(path, stage), str(tmp_path / "pm" / stage))
+
+
+def test_linear_svc_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.classification import LinearSVCModel
+    path = os.path.join(FIX, "linear_svc")
+    m = LinearSVCModel.load(path)
+    assert list(m.coefficients.toArray()) == [1.5, -0.5] and m.intercept == -0.25
+    X = [[1.0, 2.0], [0.0, 1.0], [2.0, 0.0]]
+    out = m.transform(_frame(s, X)).toPandas()
+    for x, raw, pred in zip(X, out["rawPrediction"], out["prediction"]):
+        z = 1.5 * x[0] - 0.5 * x[1] - 0.25
+        assert abs(raw[1] - z) < 1e-12 and abs(raw[0] + z) < 1e-12 and pred == (1.0 if z > 0.0 else 0.0)
+    m.write().overwrite().save(str(tmp_path / "svc"))
+    _same_layout(path, str(tmp_path / "svc"))
+
+
+def test_linear_regression_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.regression import LinearRegressionModel
+    path = os.path.join(FIX, "linear_regression")
+    m = LinearRegressionModel.load(path)
+    assert list(m.coefficients.toArray()) == [3.0, -1.0, 0.5] and m.intercept == 2.0
+    X = [[1.0, 1.0, 1.0], [0.0, 2.0, -2.0]]
+    out = m.transform(_frame(s, X)).toPandas()
+    for x, p in zip(X, out["prediction"]):
+        assert abs(p - (3.0 * x[0] - x[1] + 0.5 * x[2] + 2.0)) < 1e-12
+    m.write().overwrite().save(str(tmp_path / "linreg"))
+    _same_layout(path, str(tmp_path / "linreg"))
+
+
+def test_standard_scaler_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.feature import StandardScalerModel
+    path = os.path.join(FIX, "standard_scaler")
+    m = StandardScalerModel.load(path)
+    assert list(m.std.toArray()) == [2.0, 0.5] and list(m.mean.toArray()) == [1.0, -1.0]
+    assert m.getOrDefault("withMean") is True and m.getOrDefault("withStd") is True
+    out = m.transform(_frame(s, [[3.0, 0.0], [1.0, -1.5]])).toPandas()
+    assert [list(v) for v in out["scaled"]] == [[1.0, 2.0], [0.0, -1.0]]
+    m.write().overwrite().save(str(tmp_path / "ss"))
+    _same_layout(path, str(tmp_path / "ss"))
+
+
+def test_string_indexer_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.feature import StringIndexerModel
+    path = os.path.join(FIX, "string_indexer")
+    m = StringIndexerModel.load(path)
+    assert list(m.labels) == ["red", "green", "blue"]
+    out = m.transform(s.createDataFrame(pd.DataFrame({"color": ["blue", "red", "green", "red"]}))).toPandas()
+    assert list(out["color_idx"]) == [2.0, 0.0, 1.0, 0.0]
+    m.write().overwrite().save(str(tmp_path / "si"))
+    _same_layout(path, str(tmp_path / "si"))
+
+
+def test_random_forest_classifier_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.classification import RandomForestClassificationModel
+    path = os.path.join(FIX, "random_forest_classifier")
+    m = RandomForestClassificationModel.load(path)
+    assert m.getNumTrees == 2 and m.numFeatures == 2 and m.numClasses == 2
+    X = [[0.2, 1.0], [0.9, 3.0], [0.4, 2.5]]
+    out = m.transform(_frame(s, X)).toPandas()
+    for x, p in zip(X, out["probability"]):
+        # Spark averages each tree's normalised leaf class counts
+        t0 = [30 / 40, 10 / 40] if x[0] <= 0.5 else [5 / 60, 55 / 60]
+        t1 = [8 / 40, 32 / 40] if x[1] <= 2.0 else [40 / 60, 20 / 60]
+        assert abs(p[1] - (t0[1] + t1[1]) / 2) < 1e-12
+    m.write().overwrite().save(str(tmp_path / "rf"))
+    _same_layout(path, str(tmp_path / "rf"), subs=("data", "treesMetadata"))
+
+
+def test_decision_tree_classifier_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.classification import DecisionTreeClassificationModel
+    path = os.path.join(FIX, "decision_tree_classifier")
+    m = DecisionTreeClassificationModel.load(path)
+    assert m.numFeatures == 2 and m.numClasses == 2 and m.depth == 1
+    out = m.transform(_frame(s, [[5.0, -1.0], [5.0, 0.0]])).toPandas()
+    assert list(out["prediction"]) == [0.0, 1.0]
+    assert abs(out["probability"][0][0] - 12 / 15) < 1e-12 and abs(out["probability"][1][1] - 21 / 25) < 1e-12
+    m.write().overwrite().save(str(tmp_path / "dt"))
+    _same_layout(path, str(tmp_path / "dt"))

@@ -13,8 +13,11 @@ Layout per model (Spark ``DefaultParamsWriter`` + model writers):
                         UDT annotations (that is how Spark restores Vector columns)
 
 Models: LogisticRegressionModel (binomial), KMeansModel, GBTClassificationModel (two
-variance-impurity regression stumps + tree weights), ALSModel (user / item factor tables)
-and a PipelineModel (VectorAssembler -> LogisticRegressionModel).
+variance-impurity regression stumps + tree weights), ALSModel (user / item factor tables),
+a PipelineModel (VectorAssembler -> LogisticRegressionModel), LinearSVCModel,
+LinearRegressionModel, StandardScalerModel, StringIndexerModel (labelsArray),
+RandomForestClassificationModel (two gini stumps, class-count impurityStats) and
+DecisionTreeClassificationModel (flat NodeData rows).
 """
 import json
 import os
@@ -203,11 +206,115 @@ def pipeline(path):
     logistic(os.path.join(path, "stages", f"1_{uids[1]}"), uids[1])
 
 
+def linear_svc(path):
+    write_meta(path, "org.apache.spark.ml.classification.LinearSVCModel", "LinearSVC_3c2b1a0f9e8d",
+               {"regParam": 0.1, "maxIter": 50},
+               {"aggregationDepth": 2, "featuresCol": "features", "fitIntercept": True, "labelCol": "label",
+                "maxBlockSizeInMB": 0.0, "maxIter": 100, "predictionCol": "prediction",
+                "rawPredictionCol": "rawPrediction", "regParam": 0.0, "standardization": True, "threshold": 0.0,
+                "tol": 1e-06})
+    t = pa.table({"coefficients": pa.array([{"type": 1, "size": None, "indices": None, "values": [1.5, -0.5]}],
+                                           VEC_ARROW),
+                  "intercept": pa.array([-0.25], pa.float64())})
+    write_parquet(path, "data", t, [field("coefficients", VEC_UDT), field("intercept", "double", False)])
+
+
+def linear_regression(path):
+    write_meta(path, "org.apache.spark.ml.regression.LinearRegressionModel", "LinearRegression_7e6d5c4b3a29",
+               {"regParam": 0.0},
+               {"aggregationDepth": 2, "elasticNetParam": 0.0, "epsilon": 1.35, "featuresCol": "features",
+                "fitIntercept": True, "labelCol": "label", "loss": "squaredError", "maxBlockSizeInMB": 0.0,
+                "maxIter": 100, "predictionCol": "prediction", "regParam": 0.0, "solver": "auto",
+                "standardization": True, "tol": 1e-06})
+    t = pa.table({"intercept": pa.array([2.0], pa.float64()),
+                  "coefficients": pa.array([{"type": 1, "size": None, "indices": None, "values": [3.0, -1.0, 0.5]}],
+                                           VEC_ARROW),
+                  "scale": pa.array([1.0], pa.float64())})
+    write_parquet(path, "data", t, [field("intercept", "double", False), field("coefficients", VEC_UDT),
+                                    field("scale", "double", False)])
+
+
+def standard_scaler(path):
+    write_meta(path, "org.apache.spark.ml.feature.StandardScalerModel", "StandardScaler_2a3b4c5d6e7f",
+               {"inputCol": "features", "outputCol": "scaled", "withMean": True},
+               {"withMean": False, "withStd": True, "outputCol": "StandardScaler_2a3b4c5d6e7f__output"})
+    t = pa.table({"std": pa.array([{"type": 1, "size": None, "indices": None, "values": [2.0, 0.5]}], VEC_ARROW),
+                  "mean": pa.array([{"type": 1, "size": None, "indices": None, "values": [1.0, -1.0]}], VEC_ARROW)})
+    write_parquet(path, "data", t, [field("std", VEC_UDT), field("mean", VEC_UDT)])
+
+
+def string_indexer(path):
+    write_meta(path, "org.apache.spark.ml.feature.StringIndexerModel", "StringIndexer_6f5e4d3c2b1a",
+               {"inputCol": "color", "outputCol": "color_idx"},
+               {"handleInvalid": "error", "outputCol": "StringIndexer_6f5e4d3c2b1a__output",
+                "stringOrderType": "frequencyDesc"})
+    t = pa.table({"labelsArray": pa.array([[["red", "green", "blue"]]],
+                                          pa.list_(pa.field("element", pa.list_(pa.field("element", pa.string(), True)), True)))})
+    arr = {"type": "array", "elementType": {"type": "array", "elementType": "string", "containsNull": True},
+           "containsNull": True}
+    write_parquet(path, "data", t, [field("labelsArray", arr)])
+
+
+def _cls_stump(feature, thr, n_left, n_right):
+    """Gini classification stump (2 classes) as Spark NodeData rows: impurityStats are the
+    per-class (weighted) counts, prediction the majority class."""
+    def gini(c):
+        n = sum(c)
+        return 1.0 - sum((x / n) ** 2 for x in c) if n else 0.0
+    tot = [n_left[0] + n_right[0], n_left[1] + n_right[1]]
+    leaf_split = {"featureIndex": -1, "leftCategoriesOrThreshold": [], "numCategories": -1}
+
+    def node(i, c, lc, rc, split, gain):
+        return {"id": i, "prediction": float(c.index(max(c))), "impurity": gini(c),
+                "impurityStats": [float(x) for x in c], "rawCount": int(sum(c)), "gain": gain,
+                "leftChild": lc, "rightChild": rc, "split": split}
+    g = gini(tot) - (sum(n_left) * gini(n_left) + sum(n_right) * gini(n_right)) / sum(tot)
+    return [node(0, tot, 1, 2, {"featureIndex": feature, "leftCategoriesOrThreshold": [thr], "numCategories": -1}, g),
+            node(1, n_left, -1, -1, leaf_split, -1.0), node(2, n_right, -1, -1, leaf_split, -1.0)]
+
+
+RF_DEFAULTS = {"bootstrap": True, "cacheNodeIds": False, "checkpointInterval": 10, "featureSubsetStrategy": "auto",
+               "featuresCol": "features", "impurity": "gini", "labelCol": "label", "leafCol": "", "maxBins": 32,
+               "maxDepth": 5, "maxMemoryInMB": 256, "minInfoGain": 0.0, "minInstancesPerNode": 1,
+               "minWeightFractionPerNode": 0.0, "numTrees": 20, "predictionCol": "prediction",
+               "probabilityCol": "probability", "rawPredictionCol": "rawPrediction", "seed": 207336481,
+               "subsamplingRate": 1.0}
+
+
+def random_forest(path):
+    uid = "RandomForestClassifier_0e1d2c3b4a59"
+    write_meta(path, "org.apache.spark.ml.classification.RandomForestClassificationModel", uid,
+               {"numTrees": 2, "maxDepth": 1}, RF_DEFAULTS, numFeatures=2, numClasses=2, numTrees=2)
+    rows = [{"treeID": 0, "nodeData": r} for r in _cls_stump(0, 0.5, [30, 10], [5, 55])] + \
+        [{"treeID": 1, "nodeData": r} for r in _cls_stump(1, 2.0, [8, 32], [40, 20])]
+    t = pa.Table.from_pylist(rows, schema=pa.schema([pa.field("treeID", pa.int32(), False), ("nodeData", NODE)]))
+    write_parquet(path, "data", t, [field("treeID", "integer", False), field("nodeData", NODE_SQL)])
+    tree_meta = [json.dumps({"class": "org.apache.spark.ml.classification.DecisionTreeClassificationModel",
+                             "timestamp": TS, "sparkVersion": VERSION, "uid": f"dtc_{i}",
+                             "paramMap": {"maxDepth": 1, "impurity": "gini"}, "defaultParamMap": {}},
+                            separators=(",", ":")) for i in range(2)]
+    tm = pa.table({"treeID": pa.array([0, 1], pa.int32()), "metadata": pa.array(tree_meta, pa.string()),
+                   "weights": pa.array([1.0, 1.0], pa.float64())})
+    write_parquet(path, "treesMetadata", tm, [field("treeID", "integer", False), field("metadata", "string"),
+                                              field("weights", "double", False)])
+
+
+def decision_tree(path):
+    defaults = {k: v for k, v in RF_DEFAULTS.items() if k not in ("bootstrap", "featureSubsetStrategy", "numTrees",
+                                                                  "subsamplingRate")}
+    write_meta(path, "org.apache.spark.ml.classification.DecisionTreeClassificationModel",
+               "DecisionTreeClassifier_5a4b3c2d1e0f", {"maxDepth": 1}, defaults, numFeatures=2, numClasses=2)
+    t = pa.Table.from_pylist(_cls_stump(1, -0.5, [12, 3], [4, 21]), schema=pa.schema(list(NODE)))
+    write_parquet(path, "data", t, NODE_SQL["fields"])
+
+
 def main():
     if os.path.exists(ROOT):
         shutil.rmtree(ROOT)
     for name, fn in (("logistic_regression", logistic), ("kmeans", kmeans), ("gbt_classifier", gbt), ("als", als),
-                     ("pipeline", pipeline)):
+                     ("pipeline", pipeline), ("linear_svc", linear_svc), ("linear_regression", linear_regression),
+                     ("standard_scaler", standard_scaler), ("string_indexer", string_indexer),
+                     ("random_forest_classifier", random_forest), ("decision_tree_classifier", decision_tree)):
         fn(os.path.join(ROOT, name))
     print(ROOT)
 
