@@ -19,7 +19,7 @@ from .base import Estimator, Model
 from .linalg import DenseMatrix, DenseVector
 from .param import (HasCheckpointInterval, HasDistanceMeasure, HasFeaturesCol, HasMaxIter, HasPredictionCol,
                     HasProbabilityCol, HasSeed, HasTol, HasWeightCol, Params, TypeConverters, keyword_only, shared)
-from .util import MLReadable, MLWritable, apply_metadata, mat_col, read_data, register, vec_col, write_data
+from .util import MLReadable, MLWritable, apply_metadata, mat_col, prim_list, read_data, register, vec_col, write_data
 
 
 def _float_features(df, name):
@@ -121,7 +121,7 @@ class BisectingKMeansModel(Model, _BisectingKMeansParams, MLWritable, MLReadable
         idx = sorted(self._centers)
         write_data(path, {"index": pa.array(idx, pa.int32()),
                           "center": vec_col([DenseVector(self._centers[i]) for i in idx]),
-                          "children": pa.array([list(self._children.get(i, ())) for i in idx], pa.list_(pa.int32()))})
+                          "children": pa.array([list(self._children.get(i, ())) for i in idx], prim_list(pa.int32()))})
 
     @classmethod
     def _load_impl(cls, path, meta):
@@ -247,7 +247,7 @@ class GaussianMixtureModel(Model, _GaussianMixtureParams, MLWritable, MLReadable
         from ..io import vector_arrow_type
         from .util import matrix_arrow_type, matrix_struct, vector_struct
         write_data(path, {
-            "weights": pa.array([self._w.tolist()], pa.list_(pa.float64())),
+            "weights": pa.array([self._w.tolist()], prim_list(pa.float64())),
             "mus": pa.array([[vector_struct(DenseVector(v)) for v in self._mu]], pa.list_(vector_arrow_type())),
             "sigmas": pa.array([[matrix_struct(DenseMatrix.from_array(c)) for c in self._cov]],
                                pa.list_(matrix_arrow_type())),

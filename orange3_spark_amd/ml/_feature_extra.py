@@ -31,7 +31,7 @@ from .base import Estimator, Model
 from .linalg import DenseVector
 from .param import (HasFeaturesCol, HasHandleInvalid, HasInputCol, HasLabelCol, HasMaxIter, HasOutputCol, HasSeed,
                     HasStepSize, TypeConverters, keyword_only, shared)
-from .util import MLReadable, MLWritable, apply_metadata, read_data, register, write_data
+from .util import MLReadable, MLWritable, apply_metadata, prim_list, read_data, register, write_data
 
 
 # ====================================================== univariate statistics
@@ -581,7 +581,7 @@ class Word2VecModel(Model, _Word2VecParams, MLWritable, MLReadable):
     def _save_data(self, path):
         import pyarrow as pa
         write_data(path, {"word": pa.array(self._words),
-                          "vector": pa.array([list(map(float, v)) for v in self._E], pa.list_(pa.float32()))})
+                          "vector": pa.array([list(map(float, v)) for v in self._E], prim_list(pa.float32()))})
 
     @classmethod
     def _load_impl(cls, path, meta):

@@ -26,7 +26,7 @@ from .linalg import DenseVector
 from .param import (HasAggregationDepth, HasFeaturesCol, HasFitIntercept, HasLabelCol, HasMaxBlockSizeInMB,
                     HasMaxIter, HasPredictionCol, HasRegParam, HasSolver, HasTol, HasWeightCol, TypeConverters,
                     keyword_only, shared)
-from .util import MLReadable, MLWritable, apply_metadata, read_data, register, vec_col, write_data
+from .util import MLReadable, MLWritable, apply_metadata, prim_list, read_data, register, vec_col, write_data
 
 
 # ===================================================================== Isotonic
@@ -115,8 +115,8 @@ class IsotonicRegressionModel(Model, _IsotonicRegressionParams, MLWritable, MLRe
 
     def _save_data(self, path):
         import pyarrow as pa
-        write_data(path, {"boundaries": pa.array([self._bounds.tolist()], pa.list_(pa.float64())),
-                          "predictions": pa.array([self._preds.tolist()], pa.list_(pa.float64())),
+        write_data(path, {"boundaries": pa.array([self._bounds.tolist()], prim_list(pa.float64())),
+                          "predictions": pa.array([self._preds.tolist()], prim_list(pa.float64())),
                           "isotonic": pa.array([bool(self.getOrDefault(self.isotonic))])})
 
     @classmethod

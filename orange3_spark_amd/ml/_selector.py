@@ -8,7 +8,7 @@ from ..frame import column as C
 from . import common as U
 from .base import Model
 from .param import HasFeaturesCol, HasOutputCol
-from .util import MLReadable, MLWritable, apply_metadata, read_data, write_data
+from .util import MLReadable, MLWritable, apply_metadata, prim_list, read_data, write_data
 
 
 def _vec(df, name) -> torch.Tensor:
@@ -27,7 +27,7 @@ class _SelectorModel(Model, HasFeaturesCol, HasOutputCol, MLWritable, MLReadable
 
     def _save_data(self, path):
         import pyarrow as pa
-        write_data(path, {"selectedFeatures": pa.array([self.selectedFeatures], pa.list_(pa.int32()))})
+        write_data(path, {"selectedFeatures": pa.array([self.selectedFeatures], prim_list(pa.int32()))})
 
     @classmethod
     def _load_impl(cls, path, meta):

@@ -29,7 +29,7 @@ from .linalg import DenseMatrix, DenseVector
 from .param import (HasFeaturesCol, HasHandleInvalid, HasInputCol, HasInputCols, HasLabelCol, HasMaxIter,
                     HasNumFeatures, HasOutputCol, HasOutputCols, HasSeed, HasStepSize, HasTol, HasWeightCol,
                     TypeConverters, keyword_only, shared)
-from .util import MLReadable, MLWritable, apply_metadata, read_data, register, vec_col, write_data
+from .util import MLReadable, MLWritable, apply_metadata, prim_list, read_data, register, vec_col, write_data
 
 
 # ----------------------------------------------------------------------------- helpers
@@ -805,7 +805,7 @@ class IDFModel(Model, _InOut, MLWritable, MLReadable):
 
     def _save_data(self, path):
         import pyarrow as pa
-        write_data(path, {"idf": vec_col([self.idf]), "docFreq": pa.array([self.docFreq], pa.list_(pa.int64())),
+        write_data(path, {"idf": vec_col([self.idf]), "docFreq": pa.array([self.docFreq], prim_list(pa.int64())),
                           "numDocs": pa.array([self.numDocs], pa.int64())})
 
     @classmethod
@@ -1214,7 +1214,7 @@ class OneHotEncoderModel(Model, HasInputCol, HasOutputCol, HasInputCols, HasOutp
 
     def _save_data(self, path):
         import pyarrow as pa
-        write_data(path, {"categorySizes": pa.array([self.categorySizes], pa.list_(pa.int32()))})
+        write_data(path, {"categorySizes": pa.array([self.categorySizes], prim_list(pa.int32()))})
 
     @classmethod
     def _load_impl(cls, path, meta):

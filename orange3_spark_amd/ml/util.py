@@ -200,6 +200,14 @@ def spark_type_json(t):
     raise TypeError(f"no Spark SQL type for arrow type {t}")
 
 
+def prim_list(t):
+    """Arrow list type of a Scala primitive array (Array[Int] / Array[Long] /
+    Array[Double] / Array[Float]): Spark writes those with non-null elements
+    (``containsNull: false``)."""
+    import pyarrow as pa
+    return pa.list_(pa.field("element", t, False))
+
+
 def spark_field_json(f) -> dict:
     return {"name": f.name, "type": spark_type_json(f.type), "nullable": bool(f.nullable), "metadata": {}}
 

@@ -216,3 +216,61 @@ def test_decision_tree_classifier_fixture(s, tmp_path):
     assert abs(out["probability"][0][0] - 12 / 15) < 1e-12 and abs(out["probability"][1][1] - 21 / 25) < 1e-12
     m.write().overwrite().save(str(tmp_path / "dt"))
     _same_layout(path, str(tmp_path / "dt"))
+
+
+def test_naive_bayes_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.classification import NaiveBayesModel
+    path = os.path.join(FIX, "naive_bayes")
+    m = NaiveBayesModel.load(path)
+    theta = np.log([[0.5, 0.3, 0.2], [0.1, 0.2, 0.7]])
+    np.testing.assert_allclose(m.theta.toArray(), theta, rtol=0, atol=1e-15)
+    X = [[1.0, 0.0, 2.0], [3.0, 1.0, 0.0]]
+    out = m.transform(_frame(s, X)).toPandas()
+    for x, raw in zip(X, out["rawPrediction"]):
+        ref = np.log([0.4, 0.6]) + theta @ np.asarray(x)
+        np.testing.assert_allclose(np.asarray(raw), ref, rtol=1e-12, atol=1e-12)
+    m.write().overwrite().save(str(tmp_path / "nb"))
+    _same_layout(path, str(tmp_path / "nb"))
+
+
+def test_min_max_scaler_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.feature import MinMaxScalerModel
+    path = os.path.join(FIX, "min_max_scaler")
+    m = MinMaxScalerModel.load(path)
+    out = m.transform(_frame(s, [[1.0, 0.0], [4.0, -2.0]])).toPandas()
+    assert [list(v) for v in out["scaled"]] == [[0.25, 0.5], [1.0, 0.0]]
+    m.write().overwrite().save(str(tmp_path / "mm"))
+    _same_layout(path, str(tmp_path / "mm"))
+
+
+def test_idf_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.feature import IDFModel
+    path = os.path.join(FIX, "idf")
+    m = IDFModel.load(path)
+    assert list(m.idf.toArray()) == [0.5, 1.25, 0.0] and list(m.docFreq) == [3, 1, 4] and m.numDocs == 4
+    df = s.createDataFrame([(Vectors.dense([2.0, 1.0, 5.0]),)], ["tf"])
+    assert list(m.transform(df).toPandas()["tfidf"][0]) == [1.0, 1.25, 0.0]
+    m.write().overwrite().save(str(tmp_path / "idf"))
+    _same_layout(path, str(tmp_path / "idf"))
+
+
+def test_one_hot_encoder_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.feature import OneHotEncoderModel
+    path = os.path.join(FIX, "one_hot_encoder")
+    m = OneHotEncoderModel.load(path)
+    assert list(m.categorySizes) == [3]
+    out = m.transform(s.createDataFrame(pd.DataFrame({"c": [0.0, 1.0, 2.0]}))).toPandas()
+    assert [list(v.toArray()) for v in out["c_vec"]] == [[1.0, 0.0], [0.0, 1.0], [0.0, 0.0]]   # dropLast
+    m.write().overwrite().save(str(tmp_path / "ohe"))
+    _same_layout(path, str(tmp_path / "ohe"))
+
+
+def test_count_vectorizer_fixture(s, tmp_path):
+    from orange3_spark_amd.ml.feature import CountVectorizerModel
+    path = os.path.join(FIX, "count_vectorizer")
+    m = CountVectorizerModel.load(path)
+    assert list(m.vocabulary) == ["a", "b", "c"]
+    df = s.createDataFrame([(["c", "a", "c", "z"],)], ["words"])
+    assert list(m.transform(df).toPandas()["counts"][0].toArray()) == [1.0, 0.0, 2.0]
+    m.write().overwrite().save(str(tmp_path / "cv"))
+    _same_layout(path, str(tmp_path / "cv"))

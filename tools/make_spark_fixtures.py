@@ -16,8 +16,10 @@ Models: LogisticRegressionModel (binomial), KMeansModel, GBTClassificationModel 
 variance-impurity regression stumps + tree weights), ALSModel (user / item factor tables),
 a PipelineModel (VectorAssembler -> LogisticRegressionModel), LinearSVCModel,
 LinearRegressionModel, StandardScalerModel, StringIndexerModel (labelsArray),
-RandomForestClassificationModel (two gini stumps, class-count impurityStats) and
-DecisionTreeClassificationModel (flat NodeData rows).
+RandomForestClassificationModel (two gini stumps, class-count impurityStats),
+DecisionTreeClassificationModel (flat NodeData rows), NaiveBayesModel (multinomial: pi,
+theta and a 0 x 0 sigma), MinMaxScalerModel, IDFModel, OneHotEncoderModel and
+CountVectorizerModel.
 """
 import json
 import os
@@ -308,13 +310,74 @@ def decision_tree(path):
     write_parquet(path, "data", t, NODE_SQL["fields"])
 
 
+def naive_bayes(path):
+    import math as _m
+    write_meta(path, "org.apache.spark.ml.classification.NaiveBayesModel", "NaiveBayes_4b5c6d7e8f90",
+               {"smoothing": 1.0},
+               {"featuresCol": "features", "labelCol": "label", "modelType": "multinomial",
+                "predictionCol": "prediction", "probabilityCol": "probability", "rawPredictionCol": "rawPrediction",
+                "smoothing": 1.0})
+    pi = [_m.log(0.4), _m.log(0.6)]
+    theta = [[_m.log(0.5), _m.log(0.3), _m.log(0.2)], [_m.log(0.1), _m.log(0.2), _m.log(0.7)]]
+    # MatrixUDT is column-major unless isTransposed: store theta (2 x 3) column by column
+    colmaj = [theta[r][c] for c in range(3) for r in range(2)]
+    t = pa.table({"pi": pa.array([{"type": 1, "size": None, "indices": None, "values": pi}], VEC_ARROW),
+                  "theta": pa.array([{"type": 1, "numRows": 2, "numCols": 3, "colPtrs": None, "rowIndices": None,
+                                      "values": colmaj, "isTransposed": False}], MAT_ARROW),
+                  "sigma": pa.array([{"type": 1, "numRows": 0, "numCols": 0, "colPtrs": None, "rowIndices": None,
+                                      "values": [], "isTransposed": False}], MAT_ARROW)})
+    write_parquet(path, "data", t, [field("pi", VEC_UDT), field("theta", MAT_UDT), field("sigma", MAT_UDT)])
+
+
+def min_max_scaler(path):
+    write_meta(path, "org.apache.spark.ml.feature.MinMaxScalerModel", "MinMaxScaler_1f2e3d4c5b6a",
+               {"inputCol": "features", "outputCol": "scaled"},
+               {"max": 1.0, "min": 0.0, "outputCol": "MinMaxScaler_1f2e3d4c5b6a__output"})
+    t = pa.table({"originalMin": pa.array([{"type": 1, "size": None, "indices": None, "values": [0.0, -2.0]}],
+                                          VEC_ARROW),
+                  "originalMax": pa.array([{"type": 1, "size": None, "indices": None, "values": [4.0, 2.0]}],
+                                          VEC_ARROW)})
+    write_parquet(path, "data", t, [field("originalMin", VEC_UDT), field("originalMax", VEC_UDT)])
+
+
+def idf(path):
+    write_meta(path, "org.apache.spark.ml.feature.IDFModel", "IDF_9a8b7c6d5e4f",
+               {"inputCol": "tf", "outputCol": "tfidf"}, {"minDocFreq": 0, "outputCol": "IDF_9a8b7c6d5e4f__output"})
+    t = pa.table({"idf": pa.array([{"type": 1, "size": None, "indices": None, "values": [0.5, 1.25, 0.0]}],
+                                  VEC_ARROW),
+                  "docFreq": pa.array([[3, 1, 4]], pa.list_(pa.field("element", pa.int64(), False))),
+                  "numDocs": pa.array([4], pa.int64())})
+    arr = {"type": "array", "elementType": "long", "containsNull": False}
+    write_parquet(path, "data", t, [field("idf", VEC_UDT), field("docFreq", arr), field("numDocs", "long", False)])
+
+
+def one_hot_encoder(path):
+    write_meta(path, "org.apache.spark.ml.feature.OneHotEncoderModel", "OneHotEncoder_3e4d5c6b7a81",
+               {"inputCols": ["c"], "outputCols": ["c_vec"]}, {"dropLast": True, "handleInvalid": "error"})
+    t = pa.table({"categorySizes": pa.array([[3]], pa.list_(pa.field("element", pa.int32(), False)))})
+    write_parquet(path, "data", t, [field("categorySizes", {"type": "array", "elementType": "integer",
+                                                            "containsNull": False})])
+
+
+def count_vectorizer(path):
+    write_meta(path, "org.apache.spark.ml.feature.CountVectorizerModel", "CountVectorizer_8e7f6a5b4c3d",
+               {"inputCol": "words", "outputCol": "counts"},
+               {"binary": False, "maxDF": 9.223372036854776e18, "minDF": 1.0, "minTF": 1.0,
+                "outputCol": "CountVectorizer_8e7f6a5b4c3d__output", "vocabSize": 262144})
+    t = pa.table({"vocabulary": pa.array([["a", "b", "c"]], pa.list_(pa.field("element", pa.string(), True)))})
+    write_parquet(path, "data", t, [field("vocabulary", {"type": "array", "elementType": "string",
+                                                         "containsNull": True})])
+
+
 def main():
     if os.path.exists(ROOT):
         shutil.rmtree(ROOT)
     for name, fn in (("logistic_regression", logistic), ("kmeans", kmeans), ("gbt_classifier", gbt), ("als", als),
                      ("pipeline", pipeline), ("linear_svc", linear_svc), ("linear_regression", linear_regression),
                      ("standard_scaler", standard_scaler), ("string_indexer", string_indexer),
-                     ("random_forest_classifier", random_forest), ("decision_tree_classifier", decision_tree)):
+                     ("random_forest_classifier", random_forest), ("decision_tree_classifier", decision_tree),
+                     ("naive_bayes", naive_bayes), ("min_max_scaler", min_max_scaler), ("idf", idf),
+                     ("one_hot_encoder", one_hot_encoder), ("count_vectorizer", count_vectorizer)):
         fn(os.path.join(ROOT, name))
     print(ROOT)
 
