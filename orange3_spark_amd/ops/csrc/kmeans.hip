@@ -277,9 +277,14 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
 // (fp16 hi + lo, ~22 bits) and the fp32 centre row.  Other rows (near-ties) are appended
 // to a compacted list (one atomic per wave) and re-solved by the split-precision kernel
 // above.  This is 1/3 of the MFMAs of the split kernel; the S ||c||^2 bias is folded
-// into the accumulator init (read from LDS), so the epilogue is 4 VALU per distance
-// (cmp, cndmask, min, med3).  On structureless data (uniform in a cube) the fp16 bound
-// leaves ~10% of the rows as near ties where the bf16 one flagged nearly all of them.
+// into the accumulator init (read from LDS).  The epilogue is 3 VALU per distance and
+// touches no VCC: the candidate's slot in its chunk (0..15) replaces the low 4 mantissa
+// bits of the distance (v_and_or: a perturbation below 2^-19 of its magnitude, added to
+// the bound), so best = v_min and second = v_med3 carry the index with them; the chunk
+// of the best is recorded once per chunk.  On structureless data (uniform in a cube) the
+// fp16 bound leaves ~10% of the rows as near ties where the bf16 one flagged nearly all.
+// All LDS (staging + ||c||^2) is ONE dynamic __shared__ array, and each stage's body sees
+// its three regions as __restrict__ pointers (see run_stage).
 //
 // 4 waves (one per SIMD) x TT 32-row tiles per block, 2 blocks per CU: one block's X
 // staging and DMA prologue overlaps the other's MFMA sweep.
@@ -313,13 +318,15 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
   static_assert(G % 2 == 0, "chunks are processed in ping-pong pairs");
   constexpr int XS = D / 4;
   constexpr int XL = 32 * XS / kWave;          // float4 loads per lane per 32-row tile
-  __shared__ __attribute__((aligned(16))) uint16_t lds[L::BYTES / 2];
-  extern __shared__ __attribute__((aligned(16))) float scn[];  // [Cpad] ||c||^2
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];   // [L::BYTES staging | Cpad floats]
+  float* const scn = reinterpret_cast<float*>(lds + L::BYTES / 2);  // S ||c||^2 (padding: 2^125)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int64_t row_base = (int64_t)blockIdx.x * (kScrWaves * 32 * TT) + (int64_t)wid * 32 * TT;
 
-  for (int i = threadIdx.x; i < Cpad; i += kScrThreads) scn[i] = cn[i] * sscale;
+  // padded centres (+inf) become 2^125: finite, so a slot code in the low bits never
+  // turns a key into a NaN, and still farther than any real centre
+  for (int i = threadIdx.x; i < Cpad; i += kScrThreads) scn[i] = fminf(cn[i] * sscale, 0x1p125f);
   // ---- X tiles -> split fp16 fragments (hi: B operand) + ||x||^2.  All XL loads of a tile
   // are issued before any is consumed (one HBM round trip per tile), then staged
   // row-contiguously through this wave's LDS slice (slot XOR swizzle: conflict-free
@@ -376,70 +383,90 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
   __syncthreads();                                         // staging area free; scn visible
 
   const int nchunks = Cpad / 32;
-  auto stage = [&](int stg, int buf) {
+  // one stage = G centroid chunks, DMA'd into dbuf (per-thread offsets from a uniform stage base)
+  auto stage = [&](int stg, uint16_t* __restrict__ dbuf) {
+    const uint16_t* sbase = Chi + (int64_t)stg * G * CH_ELEMS;
 #pragma unroll
     for (int k = 0; k < PER_THREAD; ++k) {
       const int P = threadIdx.x + k * kScrThreads;
       const int g = P / PIECES;
-      const int chunk = stg * G + g;
-      if (P >= G * PIECES || chunk >= nchunks) continue;
+      if (P >= G * PIECES || stg * G + g >= nchunks) continue;
       const int Q = P % PIECES;
       const int cr = Q / SLOTS, sw = Q % SLOTS;
       const int sl = sw ^ (cr & 15 & (SLOTS - 1));
-      const uint16_t* src = Chi + ((int64_t)(chunk * 32 + cr)) * D + sl * 8;
-      uint16_t* dst = lds + buf * G * CH_ELEMS + (wid * kWave + k * kScrThreads) * 8;   // wave-uniform
-      __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(sbase + ((g * 32 + cr) * D + sl * 8),
+                                       dbuf + (wid * kWave + k * kScrThreads) * 8, 16, 0, 0);   // wave-uniform dst
     }
   };
-  // Running (best, second, index) per row.  The index is kept RELATIVE to the current
-  // chunk base (ch*32 + 4h): candidates are then the inline constants (i&3) + 8*(i>>2)
-  // and a new chunk costs one subtract -- 4 VALU per distance (cmp, 2 cndmask, med3).
-  // PAIR also keeps the second's index and the THIRD value (v_med3 again): a row whose
-  // third is clear of the best by the bound has its arg-min among {best, second} and is
-  // settled by two exact distances instead of the split re-solve (8 VALU per distance).
+  // Running (best, second) per row.  PAIR keeps explicit indices RELATIVE to the current
+  // chunk base (ch*32 + 4h): candidates are the inline constants (i&3) + 8*(i>>2) and a new
+  // chunk costs one subtract; it also keeps the second's index and the THIRD value
+  // (v_med3 again): a row whose third is clear of the best by the bound has its arg-min
+  // among {best, second} and is settled by two exact distances instead of the split
+  // re-solve (8 VALU per distance).  The plain screen carries the slot in the key's low
+  // mantissa bits (3 VALU per distance, epi_step) and the chunk of the best in bch.
   float best[TT], second[TT], third[TT];
-  int bidx[TT], sidx[TT];
+  int bidx[TT], sidx[TT], bch[TT];
 #pragma unroll
   for (int t = 0; t < TT; ++t) {
-    best[t] = INFINITY; second[t] = INFINITY; third[t] = INFINITY; bidx[t] = 0; sidx[t] = 0;
+    best[t] = INFINITY; second[t] = INFINITY; third[t] = INFINITY; bidx[t] = 0; sidx[t] = 0; bch[t] = 0;
   }
-  auto epilogue = [&](const f32x16 (&a)[TT]) {
+  auto epilogue = [&](const f32x16 (&a)[TT], int ch) {
+    if constexpr (PAIR) {
 #pragma unroll
-    for (int t = 0; t < TT; ++t) {                       // re-base onto this chunk
-      bidx[t] -= 32;
-      if (PAIR) sidx[t] -= 32;
-    }
+      for (int t = 0; t < TT; ++t) {                     // re-base onto this chunk
+        bidx[t] -= 32;
+        sidx[t] -= 32;
+      }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int k = (i & 3) + 8 * (i >> 2);
+      for (int i = 0; i < 16; ++i) {
+        const int k = (i & 3) + 8 * (i >> 2);
 #pragma unroll
-      for (int t = 0; t < TT; ++t) {
-        const float dv = a[t][i];
-        const bool better = dv < best[t];
-        if (PAIR) {
+        for (int t = 0; t < TT; ++t) {
+          const float dv = a[t][i];
+          const bool better = dv < best[t];
           const bool better2 = dv < second[t];
           third[t] = __builtin_amdgcn_fmed3f(second[t], dv, third[t]);
           sidx[t] = better ? bidx[t] : (better2 ? k : sidx[t]);
+          second[t] = __builtin_amdgcn_fmed3f(best[t], dv, second[t]);
+          bidx[t] = better ? k : bidx[t];
+          best[t] = better ? dv : best[t];
         }
-        second[t] = __builtin_amdgcn_fmed3f(best[t], dv, second[t]);
-        bidx[t] = better ? k : bidx[t];
-        best[t] = better ? dv : best[t];
       }
     }
   };
+  // plain screen: one distance of the previous chunk (element e of E = 16 TT, tiles
+  // interleaved) folded into the running (best, second) keys
+  auto epi_step = [&](const f32x16 (&a)[TT], int e) {
+    const int t = e % TT, i = e / TT;
+    const float key = __uint_as_float((__float_as_uint(a[t][i]) & 0xfffffff0u) | (uint32_t)i);
+    second[t] = __builtin_amdgcn_fmed3f(best[t], key, second[t]);
+    // v_min_f32 itself: fminf would canonicalise the (bit-built) key first
+    asm("v_min_f32 %0, %1, %2" : "=v"(best[t]) : "v"(best[t]), "v"(key));
+  };
   // one chunk's MFMAs: accumulators start at ||c||^2 (bias folded into the first MFMA's C)
-  auto sweep = [&](const uint16_t* Lh, int ch, f32x16 (&acc)[TT]) {
+  // One chunk's MFMAs (accumulators start at S ||c||^2, the bias folded into the first
+  // MFMA's C).  EPI: the previous chunk's epilogue (accumulator old, chunk ch_old) is
+  // spread over the k-steps, E/KS distances after each step's MFMAs, so the wave issues
+  // that VALU work while its own MFMAs occupy the matrix pipe.
+  auto sweep = [&](auto epi_tag, const uint16_t* Lh, const float* sc, int ch, f32x16 (&acc)[TT],
+                   const f32x16 (&old)[TT], int ch_old) {
+    constexpr bool EPI = decltype(epi_tag)::value;
+    constexpr int E = 16 * TT;
     const int cbase = ch * 32 + 4 * h;
     f32x16 c0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const float4 c4 = *reinterpret_cast<const float4*>(scn + cbase + 8 * q);
+      const float4 c4 = *reinterpret_cast<const float4*>(sc + cbase + 8 * q);
       c0[4 * q + 0] = c4.x; c0[4 * q + 1] = c4.y; c0[4 * q + 2] = c4.z; c0[4 * q + 3] = c4.w;
     }
     auto afrag = [&](int ks) {
       const int sw = (ks * 2 + h) ^ (r & 15 & (SLOTS - 1));
       return *reinterpret_cast<const bf16x8*>(Lh + r * D + sw * 8);
     };
+    float b0[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) b0[t] = best[t];
     bf16x8 nh = afrag(0);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -450,44 +477,97 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, ah),
                                                          __builtin_bit_cast(f16x8, bh[t][ks]),
                                                          ks == 0 ? c0 : acc[t], 0, 0, 0);
+      if constexpr (EPI) {
+#pragma unroll
+        for (int e = ks * E / KS; e < (ks + 1) * E / KS; ++e) epi_step(old, e);
+      }
+    }
+    if constexpr (EPI) {
+#pragma unroll
+      for (int t = 0; t < TT; ++t) bch[t] = best[t] != b0[t] ? ch_old : bch[t];
     }
   };
-  stage(0, 0);
+  stage(0, lds);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // ping-pong accumulators: the epilogue of one chunk runs beside the next chunk's MFMAs
   f32x16 accA[TT], accB[TT];
   const int nstages = (nchunks + G - 1) / G;
+  using Yes = std::integral_constant<bool, true>;
+  using No = std::integral_constant<bool, false>;
+  if constexpr (!PAIR) {
+    // sentinel 2^126: the first chunk's "previous" epilogue cannot beat a real distance
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+#pragma unroll
+      for (int j = 0; j < 16; ++j) accB[t][j] = 0x1p126f;
+  }
   bool pendA = false, pendB = false;
-  for (int stg = 0; stg < nstages; ++stg) {
-    const int buf = stg & 1;
-    if (stg + 1 < nstages) stage(stg + 1, buf ^ 1);
+  // One stage's body with its three LDS regions as __restrict__ pointers: the scoped
+  // no-alias info lets hipcc's wait insertion see that the chunk / ||c||^2 reads do not
+  // touch the next stage's in-flight DMA (otherwise it drains that DMA, vmcnt(0), before
+  // the first read of every chunk).  G is even, so chunk pairs never straddle stages.
+  auto run_stage = [&](int stg, const uint16_t* __restrict__ cur, uint16_t* __restrict__ nxt,
+                       const float* __restrict__ sc) {
+    if (stg + 1 < nstages) stage(stg + 1, nxt);
 #pragma unroll
     for (int g = 0; g < G; g += 2) {
       const int ch = stg * G + g;
-      if (ch < nchunks) {
-        sweep(lds + (buf * G + g) * CH_ELEMS, ch, accA);
-        if (pendB) epilogue(accB);
-        pendA = true; pendB = false;
-      }
-      if (ch + 1 < nchunks) {
-        sweep(lds + (buf * G + g + 1) * CH_ELEMS, ch + 1, accB);
-        if (pendA) epilogue(accA);
-        pendB = true; pendA = false;
+      if constexpr (PAIR) {
+        if (ch < nchunks) {
+          sweep(No{}, cur + g * CH_ELEMS, sc, ch, accA, accB, 0);
+          if (pendB) epilogue(accB, ch - 1);
+          pendA = true; pendB = false;
+        }
+        if (ch + 1 < nchunks) {
+          sweep(No{}, cur + (g + 1) * CH_ELEMS, sc, ch + 1, accB, accA, 0);
+          if (pendA) epilogue(accA, ch);
+          pendB = true; pendA = false;
+        }
+      } else {
+        if (ch < nchunks) sweep(Yes{}, cur + g * CH_ELEMS, sc, ch, accA, accB, ch - 1);
+        if (ch + 1 < nchunks) sweep(Yes{}, cur + (g + 1) * CH_ELEMS, sc, ch + 1, accB, accA, ch);
       }
     }
+  };
+  for (int stg = 0; stg < nstages; ++stg) {
+    const int buf = stg & 1;
+    run_stage(stg, lds + buf * G * CH_ELEMS, lds + (buf ^ 1) * G * CH_ELEMS, scn);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  if (pendA) epilogue(accA);
-  if (pendB) epilogue(accB);
+  // the last chunk's epilogue (chunk c sits in accA when c is even)
+  if constexpr (PAIR) {
+    if (pendA) epilogue(accA, nchunks - 1);
+    if (pendB) epilogue(accB, nchunks - 1);
+  } else {
+    const bool lastA = ((nchunks - 1) & 1) == 0;
+    float b0[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) b0[t] = best[t];
+    if (lastA) {
+#pragma unroll
+      for (int e = 0; e < 16 * TT; ++e) epi_step(accA, e);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16 * TT; ++e) epi_step(accB, e);
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t) bch[t] = best[t] != b0[t] ? nchunks - 1 : bch[t];
+  }
   const int last_base = (nchunks - 1) * 32 + 4 * h;
 
 #pragma unroll
   for (int t = 0; t < TT; ++t) {
     // absolute indices, then merge the half-waves (disjoint centroid subsets of one row):
     // the k-th smallest of two sorted triples is min over i + j = k of max(a_i, b_j)
-    const int myi = bidx[t] + last_base;
+    int myi;
+    if constexpr (PAIR) {
+      myi = bidx[t] + last_base;
+    } else {
+      const uint32_t slot = __float_as_uint(best[t]) & 15u;
+      myi = bch[t] * 32 + 4 * h + (int)((slot & 3u) + 8u * (slot >> 2));
+    }
     const int mys = sidx[t] + last_base;
     const float ob = __shfl_xor(best[t], 32, 64), os = __shfl_xor(second[t], 32, 64);
     const int oi = __shfl_xor(myi, 32, 64);
@@ -515,13 +595,21 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const int idc2 = idx2 >= 0 && idx2 < Cpad ? idx2 : idc;
     const float* cp = C32 + (int64_t)idc * ldc;
     const float* cq = C32 + (int64_t)idc2 * ldc;
+    // every centre-row load in flight before the first use (one L2 round trip, not KS)
+    float4 cu[KS], cwv[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int c0 = ks * 16 + 8 * h;
+      cu[ks] = *reinterpret_cast<const float4*>(cp + (c0 < Dx ? c0 : 0));
+      cwv[ks] = *reinterpret_cast<const float4*>(cp + (c0 + 4 < Dx ? c0 + 4 : 0));
+    }
     float s = 0.f, s2 = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int c0 = ks * 16 + 8 * h;
       const bool v0 = c0 < Dx, v1 = c0 + 4 < Dx;
-      float4 u = *reinterpret_cast<const float4*>(cp + (v0 ? c0 : 0));
-      float4 w = *reinterpret_cast<const float4*>(cp + (v1 ? c0 + 4 : 0));
+      float4 u = cu[ks];
+      float4 w = cwv[ks];
       if (!v0) u = make_float4(0.f, 0.f, 0.f, 0.f);
       if (!v1) w = make_float4(0.f, 0.f, 0.f, 0.f);
       const float cv[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
@@ -553,7 +641,10 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     s += __shfl_xor(s, 32, 64);
     if (PAIR) s2 += __shfl_xor(s2, 32, 64);
     const int64_t row = row_base + t * 32 + r;
-    const float bound = 2.f * sscale * (eps_x * sqrtf(xn[t]) + eps0);   // in the scaled units of bv, sec
+    // in the scaled units of bv, sec; the plain screen's slot codes move each key by less
+    // than 2^-19 of its magnitude (twice that allowed for)
+    float bound = 2.f * sscale * (eps_x * sqrtf(xn[t]) + eps0);
+    if constexpr (!PAIR) bound += 0x1p-18f * (fabsf(bv) + fabsf(sec));
     const bool ok = row < n && h == 0;
     bool fl = ok && (!(sec - bv > bound) || !idx_ok);      // near-tie (or NaN): exact re-solve
     int pick = idc;
@@ -880,7 +971,7 @@ O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, co
   const int D = (Dx + 31) / 32 * 32;
   if (Dx % 4 != 0 || D > 160 || ldx % 4 != 0 || ldc % 4 != 0 || Cpad % 32 != 0 || n > 0x7fffffffll) return -1;
   if (tt != 1 && tt != 2) return -1;
-  const size_t dyn = sizeof(float) * (size_t)Cpad;
+  const size_t cdyn = sizeof(float) * (size_t)Cpad;
   const uint16_t* hi = (const uint16_t*)Chi;
 #define O3S_KS(KS, TT)                                                                                     \
   {                                                                                                        \
@@ -890,7 +981,8 @@ O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, co
   {                                                                                                        \
     const int rows_per_block = kScrWaves * 32 * TT;                                                        \
     const int64_t grid = (n + rows_per_block - 1) / rows_per_block;                                        \
-    if (ScrLds<KS>::BYTES + dyn > 160 * 1024) return -3;                                                   \
+    const size_t dyn = ScrLds<KS>::BYTES + cdyn;                                                           \
+    if (dyn > 160 * 1024) return -3;                                                                       \
     hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, X, n, \
                        ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt,     \
                        flag_rows, Dx);                                                                     \
