@@ -61,8 +61,12 @@ __device__ __forceinline__ float f16_bits_to_f32(uint32_t bits16) {
 }
 
 // KS = D / 16 k-steps, TT = 32-row tiles per wave.  Cpad: centroids padded to 32
-// (padding rows carry cn = +inf).
-template <int KS, int TT>
+// (padding rows carry cn = +inf).  CNL: ||c||^2 staged in LDS (when Cpad floats fit beside
+// the chunk buffers) and folded into the accumulator init; else read per chunk.  The
+// epilogue keeps explicit indices (exact ties resolve to the lowest index: the screen's
+// slot-coded keys would order exact ties of negative partial distances backwards), which
+// costs little here: three MFMAs per k-step leave the VALU mostly idle.
+template <int KS, int TT, bool CNL>
 __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
     const float* __restrict__ X, int64_t n, int64_t ldx, const uint16_t* __restrict__ Chi,
     const uint16_t* __restrict__ Clo, const float* __restrict__ cn, int Cpad,
@@ -77,8 +81,11 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
   static_assert(PIECES % kWave == 0, "whole waves per DMA instruction");
   constexpr int ROWS_PER_WAVE = 32 * TT;
   constexpr int ROWS_PER_BLOCK = kAssignWaves * ROWS_PER_WAVE;
-  // ONE __shared__ array (guide §5 item 4a): [buf][hi|lo][32][D] bf16, slot-swizzled rows
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * G * 2 * CH_ELEMS];
+  // ONE __shared__ array (guide §5 item 4a): [buf][hi|lo][32][D] bf16, slot-swizzled rows,
+  // then (CNL) Cpad floats of ||c||^2
+  constexpr int STAGE_ELEMS = 2 * G * 2 * CH_ELEMS;
+  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
+  float* const scn = reinterpret_cast<float*>(lds + STAGE_ELEMS);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int64_t row_base = (int64_t)blockIdx.x * ROWS_PER_BLOCK + wid * ROWS_PER_WAVE;
@@ -91,7 +98,10 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
   // XOR-swizzled by row so the 32-row column reads are conflict free.
   // (D > 128: the tile does not fit the stage buffer; load the fragments directly.)
   constexpr int XS = D / 4;                    // 16-B slots per staged row
-  constexpr bool kStageX = kAssignWaves * ROWS_PER_WAVE * D * 4 <= (int)sizeof(lds);
+  constexpr bool kStageX = kAssignWaves * ROWS_PER_WAVE * D * 4 <= STAGE_ELEMS * 2;
+  if constexpr (CNL) {
+    for (int i = threadIdx.x; i < Cpad; i += kAssignThreads) scn[i] = cn[i];
+  }
   float* xt = reinterpret_cast<float*>(lds) + wid * ROWS_PER_WAVE * D;
   bf16x8 bh[TT][KS], bl[TT][KS];
   float xn[TT];
@@ -158,7 +168,7 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
   // so the XOR swizzle is applied to the SOURCE slot (guide §5.4 rule 21).
   const int nchunks = Cpad / 32;
   const int nchunks_ = Cpad / 32;
-  auto stage = [&](int stg, int buf) {
+  auto stage = [&](int stg, uint16_t* __restrict__ dbuf) {
 #pragma unroll
     for (int k = 0; k < PER_THREAD; ++k) {
       const int P = threadIdx.x + k * kAssignThreads;      // linear 16-B piece index in the stage
@@ -171,8 +181,7 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
       const int cr = rem / SLOTS, sw = rem % SLOTS;
       const int sl = sw ^ (cr & 15 & (SLOTS - 1));
       const uint16_t* src = (which ? Clo : Chi) + ((int64_t)(chunk * 32 + cr)) * D + sl * 8;
-      uint16_t* dst = lds + buf * G * 2 * CH_ELEMS + (wid * kWave + k * kAssignThreads) * 8;   // wave-uniform
-      __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, dbuf + (wid * kWave + k * kAssignThreads) * 8, 16, 0, 0);   // wave-uniform
     }
   };
 
@@ -180,7 +189,7 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
   int besti[TT];
 #pragma unroll
   for (int t = 0; t < TT; ++t) { bestv[t] = INFINITY; besti[t] = 0; xnv[t] = xn[t]; }
-  stage(0, 0);
+  stage(0, lds);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // Software pipeline: the MFMAs of chunk ch are issued, then the arg-min epilogue of
@@ -189,61 +198,83 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
   f32x16 accp[TT];
   auto epilogue = [&](const f32x16 (&a)[TT], int chp) {
     const int cbase = chp * 32 + 4 * h;      // acc reg i -> centroid cbase + (i&3) + 8*(i>>2)
+    float cv[16];
+    if constexpr (!CNL) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float4 c4 = *reinterpret_cast<const float4*>(cn + cbase + 8 * q);
-      const float cv[4] = {c4.x, c4.y, c4.z, c4.w};
+      for (int q = 0; q < 4; ++q) {
+        const float4 c4 = *reinterpret_cast<const float4*>(cn + cbase + 8 * q);
+        cv[4 * q + 0] = c4.x; cv[4 * q + 1] = c4.y; cv[4 * q + 2] = c4.z; cv[4 * q + 3] = c4.w;
+      }
+    }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int idx = cbase + 8 * q + j;
+    for (int i = 0; i < 16; ++i) {
+      const int idx = cbase + (i & 3) + 8 * (i >> 2);
 #pragma unroll
-        for (int t = 0; t < TT; ++t) {
-          const float dv = a[t][4 * q + j] + cv[j];
-          const bool better = dv < bestv[t];
-          bestv[t] = better ? dv : bestv[t];
-          besti[t] = better ? idx : besti[t];
-        }
+      for (int t = 0; t < TT; ++t) {
+        const float dv = CNL ? a[t][i] : a[t][i] + cv[i];
+        const bool better = dv < bestv[t];
+        bestv[t] = better ? dv : bestv[t];
+        besti[t] = better ? idx : besti[t];
       }
     }
   };
   const int nstages = (nchunks + G - 1) / G;
-  for (int stg = 0; stg < nstages; ++stg) {
-   const int buf = stg & 1;
-   if (stg + 1 < nstages) stage(stg + 1, buf ^ 1);      // DMA in flight under the MFMAs
-   for (int g = 0; g < G; ++g) {
-    const int ch = stg * G + g;
-    if (ch >= nchunks) break;
-    const uint16_t* Lh = lds + (buf * G + g) * 2 * CH_ELEMS;
-    const uint16_t* Ll = Lh + CH_ELEMS;
-    f32x16 acc[TT];
+  // One stage's body with its LDS regions as __restrict__ pointers: the scoped no-alias
+  // info keeps hipcc from draining the next stage's in-flight DMA (vmcnt(0)) before the
+  // first LDS read of every chunk.
+  auto run_stage = [&](int stg, const uint16_t* __restrict__ cur, uint16_t* __restrict__ nxt,
+                       const float* __restrict__ sc) {
+    if (stg + 1 < nstages) stage(stg + 1, nxt);         // DMA in flight under the MFMAs
+    for (int g = 0; g < G; ++g) {
+      const int ch = stg * G + g;
+      if (ch >= nchunks) break;
+      const uint16_t* Lh = cur + g * 2 * CH_ELEMS;
+      const uint16_t* Ll = Lh + CH_ELEMS;
+      f32x16 acc[TT];
+      if constexpr (CNL) {                             // accumulators start at ||c||^2
+        const int cbase = ch * 32 + 4 * h;
+        f32x16 c0;
 #pragma unroll
-    for (int t = 0; t < TT; ++t)
+        for (int q = 0; q < 4; ++q) {
+          const float4 c4 = *reinterpret_cast<const float4*>(sc + cbase + 8 * q);
+          c0[4 * q + 0] = c4.x; c0[4 * q + 1] = c4.y; c0[4 * q + 2] = c4.z; c0[4 * q + 3] = c4.w;
+        }
 #pragma unroll
-      for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
-    // A fragments are read one k-step ahead of the MFMAs that consume them, so the LDS
-    // latency hides under the previous step's three MFMAs
-    auto afrag = [&](const uint16_t* L, int ks) {
-      const int sw = (ks * 2 + h) ^ (r & 15 & (SLOTS - 1));
-      return *reinterpret_cast<const bf16x8*>(L + r * D + sw * 8);
-    };
-    bf16x8 nh = afrag(Lh, 0), nl = afrag(Ll, 0);
+        for (int t = 0; t < TT; ++t) acc[t] = c0;
+      } else {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8 ah = nh, al = nl;
-      if (ks + 1 < KS) { nh = afrag(Lh, ks + 1); nl = afrag(Ll, ks + 1); }
+        for (int t = 0; t < TT; ++t)
 #pragma unroll
-      for (int t = 0; t < TT; ++t) {
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t][ks], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t][ks], acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t][ks], acc[t], 0, 0, 0);
+          for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
       }
-    }
-    if (ch > 0) epilogue(accp, ch - 1);
+      // A fragments are read one k-step ahead of the MFMAs that consume them, so the LDS
+      // latency hides under the previous step's three MFMAs
+      auto afrag = [&](const uint16_t* L, int ks) {
+        const int sw = (ks * 2 + h) ^ (r & 15 & (SLOTS - 1));
+        return *reinterpret_cast<const bf16x8*>(L + r * D + sw * 8);
+      };
+      bf16x8 nh = afrag(Lh, 0), nl = afrag(Ll, 0);
 #pragma unroll
-    for (int t = 0; t < TT; ++t) accp[t] = acc[t];
-   }
-   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // next stage landed
-   __syncthreads();                                    // ... for every wave; buf free again
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 ah = nh, al = nl;
+        if (ks + 1 < KS) { nh = afrag(Lh, ks + 1); nl = afrag(Ll, ks + 1); }
+#pragma unroll
+        for (int t = 0; t < TT; ++t) {
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh[t][ks], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh[t][ks], acc[t], 0, 0, 0);
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl[t][ks], acc[t], 0, 0, 0);
+        }
+      }
+      if (ch > 0) epilogue(accp, ch - 1);
+#pragma unroll
+      for (int t = 0; t < TT; ++t) accp[t] = acc[t];
+    }
+  };
+  for (int stg = 0; stg < nstages; ++stg) {
+    const int buf = stg & 1;
+    run_stage(stg, lds + buf * G * 2 * CH_ELEMS, lds + (buf ^ 1) * G * 2 * CH_ELEMS, scn);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // next stage landed
+    __syncthreads();                                    // ... for every wave; buf free again
   }
   if (nchunks > 0) epilogue(accp, nchunks - 1);
   // merge the two half-waves (different centroid subsets of the same row)
@@ -945,10 +976,18 @@ O3S_API int o3s_kmeans_assign(const float* X, int64_t n, int64_t ldx, int Dx, co
   const int grid = (int)((n + rows_per_block - 1) / rows_per_block);
   const uint16_t* hi = (const uint16_t*)Chi;
   const uint16_t* lo = (const uint16_t*)Clo;
+  // chunk buffers: 2 buffers x G chunks x (hi + lo) x 32 x D bf16 = 128 KB at every D
+  const size_t stage_bytes = 2 * (D <= 128 ? 4 : 2) * 2 * 32 * (size_t)D * 2;
+  const bool cnl = stage_bytes + sizeof(float) * (size_t)Cpad <= 160 * 1024;
 #define O3S_KA(KS)                                                                                   \
   case KS:                                                                                           \
-    hipLaunchKernelGGL((kmeans_assign_kernel<KS, 1>), dim3(grid), dim3(kAssignThreads), 0, st, X, n, ldx, \
-                       hi, lo, cn, Cpad, assign, mind, Dx, rowlist);                                 \
+    if (cnl)                                                                                         \
+      hipLaunchKernelGGL((kmeans_assign_kernel<KS, 1, true>), dim3(grid), dim3(kAssignThreads),      \
+                         stage_bytes + sizeof(float) * (size_t)Cpad, st, X, n, ldx, hi, lo, cn, Cpad, \
+                         assign, mind, Dx, rowlist);                                                 \
+    else                                                                                             \
+      hipLaunchKernelGGL((kmeans_assign_kernel<KS, 1, false>), dim3(grid), dim3(kAssignThreads),     \
+                         stage_bytes, st, X, n, ldx, hi, lo, cn, Cpad, assign, mind, Dx, rowlist);   \
     break;
   switch (D / 16) {
     O3S_KA(2) O3S_KA(4) O3S_KA(6) O3S_KA(8) O3S_KA(10) O3S_KA(12) O3S_KA(14) O3S_KA(16)
