@@ -124,9 +124,9 @@ __global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmSrc* __rest
 }
 
 // Fast path: every source a plain [n] column of one dtype T (the common wide table of
-// float / double columns).  A block owns kCRows = 128 rows and walks the output in
-// windows of kCW = 32, 64 or 128 columns (LDS tile 8.5 / 17 / 33 KB for bf16 out):
-//   load:  wave w takes columns w, w + 4, ...; lane l reads rows l and l + 64 of 8 columns
+// float / double columns).  A block owns 64 RPL rows (128 or 256) and walks the output in
+// windows of kCW = 32, 64 or 128 columns (LDS tile 8.5 / 17 / 33 KB for bf16 out, 128 rows):
+//   load:  wave w takes columns w, w + 4, ...; lane l reads rows l, l + 64, ... of 8 columns
 //          per batch (8 or 16; 16 or 32 independent loads in flight, each wave load a 256-B contiguous
 //          run of one column), converts and writes them transposed into an LDS tile whose
 //          row stride is an odd number of dwords (65 / 129), so the 64 lanes -- 64 rows --
@@ -136,68 +136,85 @@ __global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmSrc* __rest
 // Every input byte is read once as part of a long sequential run and every output line is
 // written whole -- the generic kernel above reads 64 elements of 8 different sources per
 // wave step and writes 16-B pieces of 64 rows 512 B apart.
-constexpr int kCRows = 128;
 typedef unsigned int uint4_ __attribute__((ext_vector_type(4)));
 
 template <typename T>
 __device__ __forceinline__ float to_f(T v) { return (float)v; }
 
-template <typename T, int OUT, int kCW, int kCBatch>
+// RPL: rows per lane (a block owns 64 RPL rows: each column is read in runs of 256 RPL
+// bytes for fp32; 256-row blocks: 4.8-4.9 TB/s vs 4.2 at 128 at 100M x 256 fp32 -> bf16);
+// V2 (fp32, even RPL): lane l holds row PAIRS 128 p + 2 l + {0, 1}, read as one 8-B load
+// per pair in full blocks -- each wave load is a 512-B run of the column.
+template <typename T, int OUT, int kCW, int kCBatch, int RPL, bool V2 = false>
 __global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* __restrict__ srcs, int D, int ld,
                                                                  int64_t n, void* __restrict__ out,
                                                                  uint8_t* __restrict__ bad, int* __restrict__ nbad) {
+  constexpr int kCRows = 64 * RPL;
   constexpr int PAD = OUT == 0 ? 2 : 1;
   constexpr int LS = kCW + PAD;                       // tile row stride (elements): 65 / 129 dwords
   using OT = typename std::conditional<OUT == 0, uint16_t, float>::type;
   __shared__ OT tile[kCRows * LS];
   __shared__ uint8_t s_bad[kCRows];
-  if (threadIdx.x < kCRows) s_bad[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < kCRows; i += kThreads) s_bad[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & (kWave - 1);
   // wave index made provably uniform: the source descriptors are then read with scalar
   // loads (constant cache) instead of an LDS table, which keeps LDS for the tile alone
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int64_t nblk = (n + kCRows - 1) / kCRows;
-  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+  // XCD-aware walk: workgroups are dealt to the 8 XCDs round robin, so block b of a grid of
+  // G (G % 8 == 0) takes row block it G + (b % 8) G/8 + b/8 in sweep it -- every XCD streams
+  // one contiguous G/8-block range of each column per sweep instead of every 8th block
+  const int64_t G = gridDim.x;
+  const int64_t xoff = (G % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
+  for (int64_t blk = xoff; blk < nblk; blk += G) {
     const int64_t row0 = blk * kCRows;
-    const int64_t ra = row0 + lane < n ? row0 + lane : n - 1;
-    const int64_t rb = row0 + lane + 64 < n ? row0 + lane + 64 : n - 1;
-    bool bada = false, badb = false;
+    const bool full = row0 + kCRows <= n;
+    auto rib = [&](int i) { return V2 ? 128 * (i >> 1) + 2 * lane + (i & 1) : lane + 64 * i; };   // row in block
+    int64_t rr[RPL];
+    bool rbad[RPL];
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+      rr[i] = row0 + rib(i) < n ? row0 + rib(i) : n - 1;
+      rbad[i] = false;
+    }
     for (int c0 = 0; c0 < ld; c0 += kCW) {
       const int cw = ld - c0 < kCW ? ld - c0 : kCW;
       for (int jb = wid; jb < cw; jb += 4 * kCBatch) {
-        T va[kCBatch], vb[kCBatch];
+        T v[kCBatch][RPL];
 #pragma unroll
         for (int q = 0; q < kCBatch; ++q) {
           const int j = c0 + jb + 4 * q;                // wave-uniform
           if (jb + 4 * q < cw && j < D) {
             const T* p = reinterpret_cast<const T*>(srcs[j].ptr);
-            va[q] = p[ra];
-            vb[q] = p[rb];
+            if (V2 && full) {
+#pragma unroll
+              for (int i = 0; i < RPL; i += 2) {
+                const float2 w2 = *reinterpret_cast<const float2*>(p + rr[i]);
+                v[q][i] = w2.x;
+                v[q][i + 1] = w2.y;
+              }
+            } else {
+#pragma unroll
+              for (int i = 0; i < RPL; ++i) v[q][i] = p[rr[i]];
+            }
           }
         }
 #pragma unroll
         for (int q = 0; q < kCBatch; ++q) {
           const int jl = jb + 4 * q, j = c0 + jl;
           if (jl >= cw) break;
-          float a = 0.f, b = 0.f;
-          if (j < D) {
-            a = to_f(va[q]);
-            b = to_f(vb[q]);
-            const uint8_t* vm = srcs[j].valid;
-            if (vm != nullptr) {
-              if (!vm[ra]) a = __builtin_nanf("");
-              if (!vm[rb]) b = __builtin_nanf("");
+          const uint8_t* vm = j < D ? srcs[j].valid : nullptr;
+#pragma unroll
+          for (int i = 0; i < RPL; ++i) {
+            float a = 0.f;
+            if (j < D) {
+              a = to_f(v[q][i]);
+              if (vm != nullptr && !vm[rr[i]]) a = __builtin_nanf("");
+              rbad[i] |= !(a == a);
             }
-            bada |= !(a == a);
-            badb |= !(b == b);
-          }
-          if constexpr (OUT == 0) {
-            tile[lane * LS + jl] = f32_to_bf16(a);
-            tile[(lane + 64) * LS + jl] = f32_to_bf16(b);
-          } else {
-            tile[lane * LS + jl] = a;
-            tile[(lane + 64) * LS + jl] = b;
+            if constexpr (OUT == 0) tile[rib(i) * LS + jl] = f32_to_bf16(a);
+            else tile[rib(i) * LS + jl] = a;
           }
         }
       }
@@ -222,11 +239,12 @@ __global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* _
       }
       __syncthreads();
     }
-    if (bada && row0 + lane < n) s_bad[lane] = 1;      // benign race: every writer stores 1
-    if (badb && row0 + lane + 64 < n) s_bad[lane + 64] = 1;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i)
+      if (rbad[i] && row0 + rib(i) < n) s_bad[rib(i)] = 1;   // benign race: every writer stores 1
     __syncthreads();
-    if (wid < 2) {
-      const int r = wid * 64 + lane;
+    for (int r = threadIdx.x; r < kCRows; r += kThreads) {
+      // whole waves take part (kCRows is a multiple of 64): the wave sum below is uniform
       const bool ok = row0 + r < n;
       const int b = (ok && s_bad[r]) ? 1 : 0;
       if (ok && bad) bad[row0 + r] = (uint8_t)b;
@@ -234,7 +252,7 @@ __global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* _
       if (lane == 0 && cnt) atomicAdd(nbad, cnt);
     }
     __syncthreads();
-    if (threadIdx.x < kCRows) s_bad[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < kCRows; i += kThreads) s_bad[i] = 0;
     __syncthreads();
   }
 }
@@ -262,20 +280,29 @@ O3S_API int o3s_assemble_src_size() { return (int)sizeof(AsmSrc); }
 
 // Fast path (see assemble_cols_kernel): srcs[j] is output column j for j < D, every source a
 // contiguous [n] column of dtype src_dtype (DT_F32 or DT_F64), ld % 8 == 0, D <= 512.
+// mode (window 64, batch 8 only): 0 = 2 rows per lane (128-row blocks), 1 = 4 rows per
+// lane, 2 = 4 rows per lane as 8-B row pairs (fp32 columns 8-B aligned).
 O3S_API int o3s_assemble_cols(const void* srcs, int src_dtype, int D, int ld, int64_t n, void* out, int out_f32,
-                              int window, int batch, void* bad, void* nbad, int grid, hipStream_t st) {
+                              int window, int batch, int mode, void* bad, void* nbad, int grid, hipStream_t st) {
   if (D <= 0 || D > kMaxSrc || ld % 8 != 0 || ld < D || n < 0 || grid <= 0) return -1;
   if (src_dtype != DT_F32 && src_dtype != DT_F64) return -2;
   if ((window != 32 && window != 64 && window != 128) || (batch != 8 && batch != 16)) return -3;
+  if (mode < 0 || mode > 2 || (mode != 0 && (window != 64 || batch != 8))) return -3;
   if (n == 0) return 0;
-#define O3S_ASM_COLS_B(T, O, W, B)                                                                       \
-  hipLaunchKernelGGL((assemble_cols_kernel<T, O, W, B>), dim3(grid), dim3(kThreads), 0, st, (const AsmSrc*)srcs, \
-                     D, ld, n, out, (uint8_t*)bad, (int*)nbad)
+#define O3S_ASM_COLS_B(T, O, W, B, R)                                                                    \
+  hipLaunchKernelGGL((assemble_cols_kernel<T, O, W, B, R>), dim3(grid), dim3(kThreads), 0, st,           \
+                     (const AsmSrc*)srcs, D, ld, n, out, (uint8_t*)bad, (int*)nbad)
 #define O3S_ASM_COLS(T, O, W) \
-  if (batch == 8) O3S_ASM_COLS_B(T, O, W, 8); else O3S_ASM_COLS_B(T, O, W, 16)
-#define O3S_ASM_COLS_W(T, O) \
-  if (window == 32) O3S_ASM_COLS(T, O, 32); else if (window == 64) O3S_ASM_COLS(T, O, 64); \
-  else O3S_ASM_COLS(T, O, 128)
+  if (batch == 8) O3S_ASM_COLS_B(T, O, W, 8, 2); else O3S_ASM_COLS_B(T, O, W, 16, 2)
+#define O3S_ASM_COLS_W(T, O)                                                                             \
+  if (window == 32) O3S_ASM_COLS(T, O, 32);                                                              \
+  else if (window == 64) {                                                                               \
+    if (mode == 0) O3S_ASM_COLS(T, O, 64);                                                               \
+    else if (mode == 1) O3S_ASM_COLS_B(T, O, 64, 8, 4);                                                  \
+    else hipLaunchKernelGGL((assemble_cols_kernel<T, O, 64, 8, 4, std::is_same<T, float>::value>), \
+                            dim3(grid), dim3(kThreads), 0, st, (const AsmSrc*)srcs, D, ld, n, out,        \
+                            (uint8_t*)bad, (int*)nbad);                                                  \
+  } else O3S_ASM_COLS(T, O, 128)
   if (src_dtype == DT_F32) {
     if (out_f32) { O3S_ASM_COLS_W(float, 1); } else { O3S_ASM_COLS_W(float, 0); }
   } else {
