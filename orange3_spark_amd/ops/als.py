@@ -5,6 +5,8 @@ mode 1 (rhs)   : out[u] = sum_j coef_j * F[c_j]
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native as N
@@ -116,6 +118,10 @@ def dense_solve(indptr, cols, w, b, F, FtF, lam, batch_bytes: int = 1 << 30) -> 
 
 
 EXACT_RANKS = (32, 64, 96, 128)
+# dense (long-row) exact solves: "mfma" / "mfma_blk" = als_dense_mfma_kernel (32 x 32 accumulator tiles,
+# Gram and Cholesky updates on v_mfma_f32_32x32x2_f32), "vgpr" = als_dense_kernel (8 x 8
+# register tiles, packed FMA)
+DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "vgpr")
 
 
 def exact_kernel_ok(F: torch.Tensor) -> bool:
@@ -235,8 +241,9 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
                     "als_rotate")
     if nd:
         Gf = G.float().contiguous() if implicit else None
-        N.check(lib.o3s_als_dense(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
-                                  F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), nd, out.data_ptr(), st),
+        fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk}.get(DENSE_KERNEL, lib.o3s_als_dense)
+        N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                   F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), nd, out.data_ptr(), st),
                 "als_dense")
     return out
 

@@ -27,6 +27,10 @@
 //   L_ip = A_ip inv(L_pp)^T and publish it through LDS, every trailing owner subtracts
 //   L_ip L_jp^T -- and the two triangular solves walk the same tiles.  A never touches
 //   LDS; the per-row LDS is the staging buffer, one panel and the 8 x 8 inverses.
+// * als_dense_mfma_kernel (the default for long rows, ops/als.py DENSE_KERNEL): the same
+//   solve on 32 x 32 tiles in MFMA accumulator layout -- Gram, panel products and trailing
+//   updates on v_mfma_f32_32x32x2_f32, one wave per diagonal factorisation (see the
+//   kernel's own comment).
 //
 // Both write x_u straight into the factor table.  fp32 throughout (the Gram / S sums are
 // short: n_u terms).
@@ -538,6 +542,354 @@ __global__ __launch_bounds__(256) void als_rotate_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------------
+// als_dense_mfma_kernel: the dense solve of als_dense_kernel on the matrix cores, for
+// long rows (the item side: ~200 ratings per row at rank 128).  The VALU kernel above is
+// issue-bound -- its 8 x 8 register tiles leave most lanes idle in the panel and diagonal
+// steps, and the Gram costs ~R^2/64 packed FMAs per rating per thread.  Here the system is
+// held as 32 x 32 tiles in MFMA accumulator layout (lane l: column l & 31, rows
+// (v & 3) + 8 (v >> 2) + 4 (l >> 5) in register v), upper triangle only (tile (j, i),
+// j <= i, holds A[32 j.., 32 i..]), dealt round robin to min(4, #tiles) waves:
+//   Gram   S_ji += sum_c w_c y_c[j] y_c[i]^T      v_mfma_f32_32x32x2_f32, two ratings per
+//          instruction (exact fp32 products, the fmaf-chain numerics of the VALU kernel),
+//          both operands one LDS read of the staged factor rows;
+//   per 32-wide panel p (block Cholesky A = U^T U, U_pp = L_pp^T):
+//     A  the owner of (p, p) stages it through LDS and factors it with one wave (lane i
+//        holds row i; column c's multipliers broadcast by v_readlane).  The SAME
+//        right-looking recurrence run on an identity right-hand side (lanes 0-31) and on
+//        the current rhs block (lanes 32-63) yields X_p = L_pp^-1 (column q on lane q) and
+//        y_p = L_pp^-1 r_p at no extra broadcast cost;
+//     B  U_pi = X_p S_pi: 16 MFMAs whose B operand is the owner's own accumulator
+//        register v (the k index pairs rows (v&3)+8(v>>2) and +4 -- any pairing works if
+//        both operands agree), A operand X_p from LDS; U_pi is published as a row panel
+//        and r_i -= U_pi^T y_p (a sum over the tile's own registers + one lane swap);
+//     C  trailing S_ji -= U_pj^T U_pi: 16 MFMAs with both operands read from the panel;
+//   backward U x = y: per p, owners of (p, i > p) form U_pi x_i (row sums through a
+//   per-wave LDS transpose), the diagonal owner applies x_p = X_p^T (y_p - sum).
+// Two block barriers per panel; R = 32 NT, NT <= 4.
+template <int R>
+struct DenseM {
+  static constexpr int NT = R / 32;
+  static constexpr int NL = NT * (NT + 1) / 2;          // upper-triangle tiles
+  static constexpr int W = NL < 4 ? NL : 4;              // waves per block
+  static constexpr int MT = (NL + W - 1) / W;            // tiles per wave
+  static constexpr int NTH = 64 * W;
+  static constexpr int CH = 16;                          // ratings staged per round
+  static constexpr int PNS = R == 32 ? 32 : (R == 96 ? 96 : R - 32);   // panel row stride (floats)
+  static constexpr int TS = 32 * 33;                     // one padded 32 x 32 tile in LDS
+  static constexpr int SA0 = CH * R > 32 * PNS ? CH * R : 32 * PNS;
+  static constexpr int SA = SA0 > W * TS ? SA0 : W * TS; // staging / panel / backward scratch
+  static constexpr int LDS = SA + TS + NT * TS + R + 2 * CH + W * 32;
+};
+
+template <int R, bool IMPL, bool BLK>
+__global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
+    const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
+    const float* __restrict__ lam, const int32_t* __restrict__ rows, float* __restrict__ X) {
+  using D = DenseM<R>;
+  constexpr int NT = D::NT, NL = D::NL, W = D::W, MT = D::MT, NTH = D::NTH, CH = D::CH, PNS = D::PNS,
+                TS = D::TS;
+  __shared__ __attribute__((aligned(16))) float lds[D::LDS];
+  float* const sY = lds;                 // Gram: staged factor rows [CH][R]
+  float* const sPn = lds;                // factor: row panel [32][PNS]
+  float* const sScr = lds;               // backward: per-wave transpose [W][32][33]
+  float* const sD = lds + D::SA;         // diagonal tile staging [32][33]
+  float* const sX = sD + TS;             // X_p = L_pp^-1, every p: [NT][32][33]
+  float* const sr = sX + NT * TS;        // rhs -> y -> x
+  float* const sW = sr + R;
+  float* const sB = sW + CH;
+  float* const sWp = sB + CH;            // backward partial sums [W][32]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, h = lane >> 5, q = lane & 31;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t u = rows[blockIdx.x];
+  const int64_t p0 = indptr[u], p1 = indptr[u + 1];
+  const float lu = lam[u];
+
+  // this wave's tiles: t = wid + s W, upper-triangle order (0,0), (0,1), .., (1,1), ..
+  int tj[MT], ti[MT];
+#pragma unroll
+  for (int s = 0; s < MT; ++s) {
+    int t = wid + s * W, j = 0;
+    if (t < NL) {
+      while (t >= NT - j) { t -= NT - j; ++j; }
+      tj[s] = j;
+      ti[s] = j + t;
+    } else {
+      tj[s] = ti[s] = NT;                  // no tile
+    }
+  }
+  f32x16_ acc[MT];
+#pragma unroll
+  for (int s = 0; s < MT; ++s)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[s][v] = 0.f;
+
+  // ---- Gram on MFMA: rounds of CH ratings staged through LDS, next round in registers ----
+  constexpr int PF = (CH * R + NTH - 1) / NTH;
+  float pf[PF];
+  float pw = 0.f, pb = 0.f;
+  auto issue = [&](int64_t c0) {
+    const int m = (int)(p1 - c0 < CH ? p1 - c0 : CH);
+    int cidx[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      const int e = tid + k * NTH;
+      const int c = e / R < m ? e / R : m - 1;
+      cidx[k] = cols[c0 + c];
+    }
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      const int e = tid + k * NTH;
+      const float v = F[(int64_t)cidx[k] * R + e % R];
+      pf[k] = e < m * R ? v : 0.f;
+    }
+    pw = 0.f;
+    pb = 0.f;
+    if (tid < m) {
+      pw = w[c0 + tid];
+      pb = b[c0 + tid];
+    }
+  };
+  float rhs = 0.f;
+  if (p0 < p1) issue(p0);
+  for (int64_t c0 = p0; c0 < p1; c0 += CH) {
+    const int m = (int)(p1 - c0 < CH ? p1 - c0 : CH);
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      const int e = tid + k * NTH;
+      if (e < CH * R) sY[e] = pf[k];         // rows >= m are zeros
+    }
+    if (tid < CH) {
+      sW[tid] = pw;
+      sB[tid] = pb;
+    }
+    __syncthreads();
+    if (c0 + CH < p1) issue(c0 + CH);
+#pragma unroll 2
+    for (int k = 0; k < (m + 1) >> 1; ++k) {
+      const int c = 2 * k + h;               // ratings 2k (lanes 0-31) and 2k + 1 (lanes 32-63)
+      const float wc = sW[c];
+      const float* yc = sY + c * R + q;
+#pragma unroll
+      for (int s = 0; s < MT; ++s)
+        if (tj[s] < NT) acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(yc[32 * tj[s]], yc[32 * ti[s]] * wc, acc[s], 0, 0, 0);
+    }
+    if (tid < R)
+      for (int c = 0; c < m; ++c) rhs = fmaf(sB[c], sY[c * R + tid], rhs);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int s = 0; s < MT; ++s) {
+    if (tj[s] >= NT) continue;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int r = (v & 3) + 8 * (v >> 2) + 4 * h;
+      float a = acc[s][v];
+      if (IMPL) a += G[(32 * tj[s] + r) * R + 32 * ti[s] + q];
+      if (tj[s] == ti[s] && r == q) a += lu;
+      acc[s][v] = a;
+    }
+  }
+  if (tid < R) sr[tid] = rhs;
+  __syncthreads();
+
+  // ---- block Cholesky A = U^T U with the forward solve U^T y = rhs riding along ----
+  for (int p = 0; p < NT; ++p) {
+    // A: factor the diagonal tile (one wave; lane i and i + 32 hold row i).  The slot is
+    // resolved first so the factorisation is emitted once, not once per tile slot.
+    int ds = -1;
+#pragma unroll
+    for (int s = 0; s < MT; ++s)
+      if (tj[s] == p && ti[s] == p) ds = s;
+    if (ds >= 0) {
+#pragma unroll
+      for (int s = 0; s < MT; ++s)
+        if (s == ds)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) sD[((v & 3) + 8 * (v >> 2) + 4 * h) * 33 + q] = acc[s][v];
+      if constexpr (BLK) {
+        // lanes 0-31: row q of the tile (-> row q of L); lanes 32-63: column q of the
+        // identity (-> column q of X_p = L_pp^-1) -- ONE register array for both, since
+        // the right-looking updates of a row of A and of a column of X are the same FMA
+        // with the lane's own multiplier (L[q][c], resp. x_c) times L[j][c].  Columns go in
+        // blocks of 4: inside a block the multipliers L[j][c] of the block's rows come
+        // from v_readlane, the update of the later columns is deferred to one rank-4 step
+        // whose multipliers arrive as one float4 LDS broadcast per row (8 LDS round trips
+        // per tile instead of 32).  y_p = X_p r_p afterwards, from the X image in LDS.
+        float v[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) v[k] = h ? (k == q ? 1.f : 0.f) : sD[q * 33 + k];
+        float4_* const sC4 = reinterpret_cast<float4_*>(sD);   // free once the rows are loaded
+#pragma unroll
+        for (int c0 = 0; c0 < 32; c0 += 4) {
+#pragma unroll
+          for (int c = c0; c < c0 + 4; ++c) {
+            const float piv = fmaxf(rl(v[c], c), 1e-30f);
+            const float t = v[c] * __builtin_amdgcn_rsqf(piv);   // L[q][c] / x_c
+            v[c] = t;
+#pragma unroll
+            for (int j = c + 1; j < c0 + 4; ++j) v[j] = fmaf(-t, rl(t, j), v[j]);
+          }
+          if (c0 + 4 < 32) {
+            // every lane stores (an exec-masked store makes the compiler keep all 28 rows'
+            // broadcasts live across the block: 234 instead of 64 VGPRs); lanes 32-63 hold
+            // x values and park them in slots 32-63, which are never read
+            sC4[lane] = float4_{v[c0], v[c0 + 1], v[c0 + 2], v[c0 + 3]};
+#pragma unroll
+            for (int j = c0 + 4; j < 32; ++j) {
+              const float4_ l4 = sC4[j];
+              v[j] = fmaf(-v[c0 + 3], l4.w, fmaf(-v[c0 + 2], l4.z, fmaf(-v[c0 + 1], l4.y, fmaf(-v[c0], l4.x, v[j]))));
+              // at most 8 broadcasts in flight: without a fence the scheduler hoists all 28
+              // float4 reads of a block (112 VGPRs) above the first FMA
+              if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
+        float* Xp = sX + p * TS;
+        if (h == 1) {
+#pragma unroll
+          for (int k = 0; k < 32; ++k) Xp[k * 33 + q] = v[k];       // X_p[k][q]
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (h == 0) {
+          float yq = 0.f;
+#pragma unroll
+          for (int j = 0; j < 32; ++j) {
+            yq = fmaf(Xp[q * 33 + j], sr[32 * p + j], yq);
+            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+          }
+          sr[32 * p + q] = yq;                                       // y_p = X_p r_p
+        }
+      } else {
+        float a[32], x[32];
+  #pragma unroll
+        for (int k = 0; k < 32; ++k) {
+          a[k] = sD[q * 33 + k];
+          x[k] = h ? sr[32 * p + k] : (k == q ? 1.f : 0.f);
+        }
+        // column c's multipliers L[j][c] go through a 32-float LDS vector (sD is free once
+        // the rows are in registers; LDS ops of one wave complete in order) and come back as
+        // float4 broadcasts: VGPR operands, no per-element v_readlane into SGPRs
+        float* const sCol = sD;
+  #pragma unroll
+        for (int c = 0; c < 32; ++c) {
+          const float piv = fmaxf(rl(a[c], c), 1e-30f);
+          const float rs = __builtin_amdgcn_rsqf(piv);
+          const float lc = a[c] * rs;          // L[row][c] (rows >= c)
+          const float xc = x[c] * rs;
+          x[c] = xc;
+          sCol[q] = lc;
+  #pragma unroll
+          for (int g = (c + 1) >> 2; g < 8; ++g) {
+            const float4_ l4 = *reinterpret_cast<const float4_*>(&sCol[4 * g]);
+            const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+  #pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int j = 4 * g + e;
+              if (j > c) {
+                a[j] = fmaf(-lc, lv[e], a[j]);
+                x[j] = fmaf(-lv[e], xc, x[j]);
+              }
+            }
+          }
+        }
+        float* Xp = sX + p * TS;
+        if (h == 0) {
+  #pragma unroll
+          for (int k = 0; k < 32; ++k) Xp[k * 33 + q] = x[k];       // X_p[k][q]
+        } else if (q == 0) {
+  #pragma unroll
+          for (int k = 0; k < 32; ++k) sr[32 * p + k] = x[k];       // y_p
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < MT; ++s) {
+      if (tj[s] != p || ti[s] <= p) continue;
+      // B: U_pi = X_p S_pi; publish it; r_i -= U_pi^T y_p
+      const float* Xp = sX + p * TS + q * 33 + 4 * h;
+      f32x16_ z;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) z[v] = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) z = __builtin_amdgcn_mfma_f32_32x32x2f32(Xp[(v & 3) + 8 * (v >> 2)], acc[s][v], z, 0, 0, 0);
+      acc[s] = z;
+      const int off = 32 * (ti[s] - p - 1);
+      float part = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int r = (v & 3) + 8 * (v >> 2) + 4 * h;
+        sPn[r * PNS + off + q] = z[v];
+        part = fmaf(z[v], sr[32 * p + r], part);
+      }
+      part += __shfl_xor(part, 32, 64);
+      if (h == 0) sr[32 * ti[s] + q] -= part;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < MT; ++s) {
+      if (tj[s] >= NT || tj[s] <= p) continue;
+      // C: trailing update S_ji -= U_pj^T U_pi
+      const float* aj = sPn + 32 * (tj[s] - p - 1) + q;
+      const float* bi = sPn + 32 * (ti[s] - p - 1) + q;
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const int k = 2 * st + h;
+        acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(-aj[k * PNS], bi[k * PNS], acc[s], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- backward U x = y ----
+  for (int p = NT - 1; p >= 0; --p) {
+    float prod[16];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) prod[v] = 0.f;
+    bool any = false;
+#pragma unroll
+    for (int s = 0; s < MT; ++s) {
+      if (tj[s] != p || ti[s] <= p) continue;
+      any = true;
+      const float xi = sr[32 * ti[s] + q];
+#pragma unroll
+      for (int v = 0; v < 16; ++v) prod[v] = fmaf(acc[s][v], xi, prod[v]);
+    }
+    float* scr = sScr + wid * TS;
+    if (any) {
+#pragma unroll
+      for (int v = 0; v < 16; ++v) scr[((v & 3) + 8 * (v >> 2) + 4 * h) * 33 + q] = prod[v];
+    }
+    if (h == 0) {
+      float t = 0.f;
+      if (any)
+#pragma unroll
+        for (int k = 0; k < 32; ++k) t += scr[q * 33 + k];
+      sWp[wid * 32 + q] = t;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < MT; ++s) {
+      if (tj[s] != p || ti[s] != p || h != 0) continue;
+      const float* Xp = sX + p * TS + q;
+      float xq = 0.f;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        float tk = sr[32 * p + k];
+#pragma unroll
+        for (int w2 = 0; w2 < W; ++w2) tk -= sWp[w2 * 32 + k];
+        xq = fmaf(Xp[k * 33], tk, xq);
+      }
+      sr[32 * p + q] = xq;
+    }
+    __syncthreads();
+  }
+  if (tid < R) X[u * R + tid] = sr[tid];
+}
+
 }  // namespace
 
 // Woodbury solves (rows with n_u <= 32 ratings and lam_u > 0).  P: the factor table
@@ -598,6 +950,44 @@ O3S_API int o3s_als_dense(int implicit, int R, const int64_t* indptr, const int3
   O3S_DN(32) O3S_DN(64) O3S_DN(96) O3S_DN(128)
 #undef O3S_DN
   return -2;
+}
+
+namespace {
+template <bool BLK>
+int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
+                      const float* b, const float* F, const float* G, const float* lam, const int32_t* dense,
+                      int64_t ndense, float* X, hipStream_t st) {
+  if (ndense < 0 || (implicit && !G)) return -1;
+  if (ndense == 0) return 0;
+#define O3S_DM(RR)                                                                                              \
+  if (R == RR) {                                                                                                \
+    if (implicit)                                                                                               \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK>), dim3((unsigned)ndense), dim3(DenseM<RR>::NTH), \
+                         0, st, indptr, cols, w, b, F, G, lam, dense, X);                                       \
+    else                                                                                                        \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK>), dim3((unsigned)ndense),                       \
+                         dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X);                \
+    O3S_CHECK_LAUNCH();                                                                                         \
+    return 0;                                                                                                   \
+  }
+  O3S_DM(32) O3S_DM(64) O3S_DM(96) O3S_DM(128)
+#undef O3S_DM
+  return -2;
+}
+}  // namespace
+
+// Dense solves on the matrix cores (als_dense_mfma_kernel); same contract as o3s_als_dense.
+// o3s_als_dense_mfma: diagonal tiles factored column by column (32 LDS broadcasts per
+// tile); o3s_als_dense_mfma_blk: 4-column blocks, row and X column sharing one register array.
+O3S_API int o3s_als_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
+                               const float* b, const float* F, const float* G, const float* lam, const int32_t* dense,
+                               int64_t ndense, float* X, hipStream_t st) {
+  return launch_dense_mfma<false>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
+}
+O3S_API int o3s_als_dense_mfma_blk(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
+                                   const float* b, const float* F, const float* G, const float* lam,
+                                   const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
+  return launch_dense_mfma<true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
 }
 
 O3S_API int o3s_als_exact_max_small() { return kNW; }

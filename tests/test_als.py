@@ -268,3 +268,34 @@ def test_gpu_exact_kernels_pad_other_ranks(R, implicit):
     A.exact_solve(indptr, cols, w, b, F, G, lam, implicit, part, row_range=(100, 300))
     assert torch.allclose(part[100:300], got[100:300], rtol=1e-5, atol=1e-6)
     assert not part[:100].any() and not part[300:].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [32, 64, 96, 128])
+@pytest.mark.parametrize("implicit", [False, True])
+@pytest.mark.parametrize("kernel", ["mfma", "mfma_blk", "vgpr"])
+def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
+    """Both dense exact kernels (als_dense_mfma_kernel: 32 x 32 MFMA accumulator tiles;
+    als_dense_kernel: 8 x 8 register tiles) == the fp64 solve on rows routed to the dense
+    path (lam = 0 rows and rows longer than the Woodbury limit), including rows of 0 and 1
+    ratings, an odd count and a row that is not a multiple of the 16-rating staging round."""
+    from orange3_spark_amd.ops import als as A
+    monkeypatch.setattr(A, "DENSE_KERNEL", kernel)
+    indptr, cols, w, b, F, G, lam = _exact_case(R, implicit, seed=11)
+    lam = lam.clone()
+    lam[:40] = 0.05 * (indptr[1:41] - indptr[:40]).float().clamp_min(1.0)   # rows < 40: dense path too
+    n = indptr.numel() - 1
+    dense = torch.arange(0, 40, device=F.device, dtype=torch.int32)
+    got = torch.full((n, R), float("nan"), device=F.device)
+    from orange3_spark_amd.ops import _native as N
+    fn = {"mfma": N.kernels().o3s_als_dense_mfma, "mfma_blk": N.kernels().o3s_als_dense_mfma_blk}.get(
+        kernel, N.kernels().o3s_als_dense)
+    Gf = G.float().contiguous() if implicit else None
+    N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), F.data_ptr(),
+               N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), 40, got.data_ptr(), N.stream_of(got)), "als_dense")
+    ref = torch.empty((n, R), dtype=torch.float64, device=F.device)
+    A.exact_solve_torch(indptr, cols, w, b, F, G, lam, ref)
+    got, ref = got[:40], ref[:40]
+    assert not torch.isnan(got).any()
+    err = (got.double() - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-6)
+    assert float(err.max()) < 2e-3, float(err.max())
