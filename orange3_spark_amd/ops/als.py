@@ -118,10 +118,11 @@ def dense_solve(indptr, cols, w, b, F, FtF, lam, batch_bytes: int = 1 << 30) -> 
 
 
 EXACT_RANKS = (32, 64, 96, 128)
-# dense (long-row) exact solves: "mfma" / "mfma_blk" = als_dense_mfma_kernel (32 x 32 accumulator tiles,
-# Gram and Cholesky updates on v_mfma_f32_32x32x2_f32), "vgpr" = als_dense_kernel (8 x 8
-# register tiles, packed FMA)
-DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "vgpr")
+# dense (long-row) exact solves: "mfma_blk" (default) = als_dense_mfma_kernel with 4-column
+# diagonal blocks and, at R = 96 / 128, the bf16x3 Gram (0.120 s/iter at the rank-of-8 ALS
+# shapes); "mfma" = the same kernel with column-by-column diagonals and the f32 Gram
+# (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144)
+DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_blk")
 
 
 def exact_kernel_ok(F: torch.Tensor) -> bool:

@@ -41,6 +41,7 @@ using namespace o3s;
 namespace {
 
 typedef float f32x16_ __attribute__((ext_vector_type(16)));
+typedef short bf16x8_ __attribute__((ext_vector_type(8)));
 constexpr int kNW = 32;   // Woodbury path: rows with at most this many ratings
 constexpr int kWW = 2;    // waves (rows) per Woodbury block
 constexpr int kPS = 72;   // LDS row stride of a P' half tile (features 32 h + s at [36 h + s])
@@ -578,7 +579,8 @@ struct DenseM {
   static constexpr int PNS = R == 32 ? 32 : (R == 96 ? 96 : R - 32);   // panel row stride (floats)
   static constexpr int TS = 32 * 33;                     // one padded 32 x 32 tile in LDS
   static constexpr int SA0 = CH * R > 32 * PNS ? CH * R : 32 * PNS;
-  static constexpr int SA = SA0 > W * TS ? SA0 : W * TS; // staging / panel / backward scratch
+  static constexpr int SA1 = SA0 > W * TS ? SA0 : W * TS;
+  static constexpr int SA = SA1 > R * 48 ? SA1 : R * 48;   // staging / panel / backward scratch
   static constexpr int LDS = SA + TS + NT * TS + R + 2 * CH + W * 32;
 };
 
@@ -590,6 +592,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
   using D = DenseM<R>;
   constexpr int NT = D::NT, NL = D::NL, W = D::W, MT = D::MT, NTH = D::NTH, CH = D::CH, PNS = D::PNS,
                 TS = D::TS;
+  constexpr bool G3 = BLK && W == 4;     // bf16x3 Gram (16 staging threads per rating)
   __shared__ __attribute__((aligned(16))) float lds[D::LDS];
   float* const sY = lds;                 // Gram: staged factor rows [CH][R]
   float* const sPn = lds;                // factor: row panel [32][PNS]
@@ -626,59 +629,135 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
 #pragma unroll
     for (int v = 0; v < 16; ++v) acc[s][v] = 0.f;
 
-  // ---- Gram on MFMA: rounds of CH ratings staged through LDS, next round in registers ----
-  constexpr int PF = (CH * R + NTH - 1) / NTH;
-  float pf[PF];
-  float pw = 0.f, pb = 0.f;
-  auto issue = [&](int64_t c0) {
-    const int m = (int)(p1 - c0 < CH ? p1 - c0 : CH);
-    int cidx[PF];
+  // ---- Gram ----
+  // G3 (blocked variant, 4-wave blocks): sqrt(w_c) y_c split into bf16 hi + lo, staged
+  // TRANSPOSED ([R][24] bf16, rating fastest, double-buffered) so one 16-B LDS read is an
+  // MFMA fragment; per 16 ratings and tile 3 v_mfma_f32_32x32x16_bf16 (hi.hi + lo.hi +
+  // hi.lo, ~2^-16 relative: the als_gram_kernel numerics) -- 96 MFMA cycles where the f32
+  // path spends 8 x 64.  The staging threads (16 per rating, R/16 elements each) also
+  // accumulate the rhs in fp32.
+  float rhs_t = 0.f;
+  if constexpr (G3) {
+    constexpr int EPT = R / 16, LDT = 24;
+    uint16_t* const sT = reinterpret_cast<uint16_t*>(lds);    // [buf][hi|lo][R][LDT]
+    const int sk = tid >> 4, sseg = tid & 15;
+    float rh[EPT], yv[EPT], wv = 0.f, bv = 0.f;
 #pragma unroll
-    for (int k = 0; k < PF; ++k) {
-      const int e = tid + k * NTH;
-      const int c = e / R < m ? e / R : m - 1;
-      cidx[k] = cols[c0 + c];
-    }
+    for (int e = 0; e < EPT; ++e) rh[e] = 0.f;
+    auto load = [&](int64_t jb) {
+      const int64_t j = jb + sk;
+      const bool ok = j < p1;
+      const int64_t c = ok ? (int64_t)cols[j] : 0;
+      wv = ok ? w[j] : 0.f;
+      bv = ok ? b[j] : 0.f;
+      const float* fp = F + c * R + sseg * EPT;
 #pragma unroll
-    for (int k = 0; k < PF; ++k) {
-      const int e = tid + k * NTH;
-      const float v = F[(int64_t)cidx[k] * R + e % R];
-      pf[k] = e < m * R ? v : 0.f;
-    }
-    pw = 0.f;
-    pb = 0.f;
-    if (tid < m) {
-      pw = w[c0 + tid];
-      pb = b[c0 + tid];
-    }
-  };
-  float rhs = 0.f;
-  if (p0 < p1) issue(p0);
-  for (int64_t c0 = p0; c0 < p1; c0 += CH) {
-    const int m = (int)(p1 - c0 < CH ? p1 - c0 : CH);
+      for (int e = 0; e < EPT; ++e) yv[e] = ok ? fp[e] : 0.f;
+    };
+    auto store = [&](int buf) {
+      const float sq = sqrtf(fmaxf(wv, 0.f));
+      uint16_t* th = sT + buf * 2 * R * LDT;
 #pragma unroll
-    for (int k = 0; k < PF; ++k) {
-      const int e = tid + k * NTH;
-      if (e < CH * R) sY[e] = pf[k];         // rows >= m are zeros
-    }
-    if (tid < CH) {
-      sW[tid] = pw;
-      sB[tid] = pb;
+      for (int e = 0; e < EPT; ++e) {
+        rh[e] = fmaf(bv, yv[e], rh[e]);
+        const float z = sq * yv[e];
+        const uint16_t hi = f32_to_bf16(z);
+        const int r = sseg * EPT + e;
+        th[r * LDT + sk] = hi;
+        th[R * LDT + r * LDT + sk] = f32_to_bf16(z - bf16_to_f32(hi));
+      }
+    };
+    const int nsteps = (int)((p1 - p0 + CH - 1) / CH);
+    if (nsteps > 0) {
+      load(p0);
+      store(0);
     }
     __syncthreads();
-    if (c0 + CH < p1) issue(c0 + CH);
-#pragma unroll 2
-    for (int k = 0; k < (m + 1) >> 1; ++k) {
-      const int c = 2 * k + h;               // ratings 2k (lanes 0-31) and 2k + 1 (lanes 32-63)
-      const float wc = sW[c];
-      const float* yc = sY + c * R + q;
+    for (int st = 0; st < nsteps; ++st) {
+      const int buf = st & 1;
+      const bool more = st + 1 < nsteps;
+      if (more) load(p0 + (int64_t)(st + 1) * CH);
+      const uint16_t* th = sT + buf * 2 * R * LDT + q * LDT + 8 * h;
+      const uint16_t* tl = th + R * LDT;
 #pragma unroll
-      for (int s = 0; s < MT; ++s)
-        if (tj[s] < NT) acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(yc[32 * tj[s]], yc[32 * ti[s]] * wc, acc[s], 0, 0, 0);
+      for (int s = 0; s < MT; ++s) {
+        if (tj[s] >= NT) continue;
+        const bf16x8_ ah = *reinterpret_cast<const bf16x8_*>(th + 32 * tj[s] * LDT);
+        const bf16x8_ al = *reinterpret_cast<const bf16x8_*>(tl + 32 * tj[s] * LDT);
+        const bf16x8_ bh = *reinterpret_cast<const bf16x8_*>(th + 32 * ti[s] * LDT);
+        const bf16x8_ bl = *reinterpret_cast<const bf16x8_*>(tl + 32 * ti[s] * LDT);
+        acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[s], 0, 0, 0);
+        acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[s], 0, 0, 0);
+        acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[s], 0, 0, 0);
+      }
+      if (more) store(buf ^ 1);
+      __syncthreads();
     }
-    if (tid < R)
-      for (int c = 0; c < m; ++c) rhs = fmaf(sB[c], sY[c * R + tid], rhs);
+    // rhs: the 16 staging threads of each element slice hold partial sums over their ratings
+    float* const rpart = lds;                                  // [16][R], staging is done
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) rpart[sk * R + sseg * EPT + e] = rh[e];
     __syncthreads();
+    if (tid < R) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) rhs_t += rpart[k * R + tid];
+    }
+  } else {
+    // f32 path: rounds of CH ratings staged through LDS, next round in registers
+    constexpr int PF = (CH * R + NTH - 1) / NTH;
+    float pf[PF];
+    float pw = 0.f, pb = 0.f;
+    auto issue = [&](int64_t c0) {
+      const int m = (int)(p1 - c0 < CH ? p1 - c0 : CH);
+      int cidx[PF];
+  #pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const int e = tid + k * NTH;
+        const int c = e / R < m ? e / R : m - 1;
+        cidx[k] = cols[c0 + c];
+      }
+  #pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const int e = tid + k * NTH;
+        const float v = F[(int64_t)cidx[k] * R + e % R];
+        pf[k] = e < m * R ? v : 0.f;
+      }
+      pw = 0.f;
+      pb = 0.f;
+      if (tid < m) {
+        pw = w[c0 + tid];
+        pb = b[c0 + tid];
+      }
+    };
+    float rhs = 0.f;
+    if (p0 < p1) issue(p0);
+    for (int64_t c0 = p0; c0 < p1; c0 += CH) {
+      const int m = (int)(p1 - c0 < CH ? p1 - c0 : CH);
+  #pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const int e = tid + k * NTH;
+        if (e < CH * R) sY[e] = pf[k];         // rows >= m are zeros
+      }
+      if (tid < CH) {
+        sW[tid] = pw;
+        sB[tid] = pb;
+      }
+      __syncthreads();
+      if (c0 + CH < p1) issue(c0 + CH);
+  #pragma unroll 2
+      for (int k = 0; k < (m + 1) >> 1; ++k) {
+        const int c = 2 * k + h;               // ratings 2k (lanes 0-31) and 2k + 1 (lanes 32-63)
+        const float wc = sW[c];
+        const float* yc = sY + c * R + q;
+  #pragma unroll
+        for (int s = 0; s < MT; ++s)
+          if (tj[s] < NT) acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(yc[32 * tj[s]], yc[32 * ti[s]] * wc, acc[s], 0, 0, 0);
+      }
+      if (tid < R)
+        for (int c = 0; c < m; ++c) rhs = fmaf(sB[c], sY[c * R + tid], rhs);
+      __syncthreads();
+    }
+    rhs_t = rhs;
   }
 #pragma unroll
   for (int s = 0; s < MT; ++s) {
@@ -692,7 +771,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
       acc[s][v] = a;
     }
   }
-  if (tid < R) sr[tid] = rhs;
+  if (tid < R) sr[tid] = rhs_t;
   __syncthreads();
 
   // ---- block Cholesky A = U^T U with the forward solve U^T y = rhs riding along ----
