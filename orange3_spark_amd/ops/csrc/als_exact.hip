@@ -638,33 +638,59 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
   // accumulate the rhs in fp32.
   float rhs_t = 0.f;
   if constexpr (G3) {
-    constexpr int EPT = R / 16, LDT = 24;
+    // staging map (conflict-free transposed stores): lane = (r_low = dim within a 16-dim
+    // block, kp_low = rating pair 0..3); a thread owns ITEMS (dim block, pair group) items
+    // and writes each item as ONE dword (ratings 2kp, 2kp + 1 of dim r) at dword 12 r + kp:
+    // banks 12 r_low + kp_low (+ 0 mod 64) are all different across the wave.  Its global
+    // loads are 64-B runs of one factor row per 16 lanes.
+    constexpr int LDT = 24, NRB = R / 16, ITEMS = NRB / 2;   // 2 NRB items over 4 waves
     uint16_t* const sT = reinterpret_cast<uint16_t*>(lds);    // [buf][hi|lo][R][LDT]
-    const int sk = tid >> 4, sseg = tid & 15;
-    float rh[EPT], yv[EPT], wv = 0.f, bv = 0.f;
+    const int r_low = lane & 15, kp_low = lane >> 4;
+    float y0[ITEMS], y1[ITEMS], rh[ITEMS];
+    float wv[2][2], bv[2][2];
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) rh[e] = 0.f;
+    for (int i = 0; i < ITEMS; ++i) rh[i] = 0.f;
+    auto item_r = [&](int i) { return 16 * ((wid + 4 * i) % NRB) + r_low; };
+    auto item_kb = [&](int i) { return (wid + 4 * i) / NRB; };
     auto load = [&](int64_t jb) {
-      const int64_t j = jb + sk;
-      const bool ok = j < p1;
-      const int64_t c = ok ? (int64_t)cols[j] : 0;
-      wv = ok ? w[j] : 0.f;
-      bv = ok ? b[j] : 0.f;
-      const float* fp = F + c * R + sseg * EPT;
+      int64_t ci[2][2];
+      bool ok[2][2];
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) yv[e] = ok ? fp[e] : 0.f;
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int par = 0; par < 2; ++par) {
+          const int64_t j = jb + 2 * (4 * kb + kp_low) + par;
+          ok[kb][par] = j < p1;
+          ci[kb][par] = ok[kb][par] ? (int64_t)cols[j] : 0;
+          wv[kb][par] = ok[kb][par] ? w[j] : 0.f;
+          bv[kb][par] = ok[kb][par] ? b[j] : 0.f;
+        }
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const int kb = item_kb(i), r = item_r(i);
+        const float v0 = F[ci[kb][0] * R + r], v1 = F[ci[kb][1] * R + r];
+        y0[i] = ok[kb][0] ? v0 : 0.f;
+        y1[i] = ok[kb][1] ? v1 : 0.f;
+      }
     };
     auto store = [&](int buf) {
-      const float sq = sqrtf(fmaxf(wv, 0.f));
-      uint16_t* th = sT + buf * 2 * R * LDT;
+      uint32_t* const th = reinterpret_cast<uint32_t*>(sT + buf * 2 * R * LDT);
+      uint32_t* const tl = th + R * LDT / 2;
+      float sq[2][2];
 #pragma unroll
-      for (int e = 0; e < EPT; ++e) {
-        rh[e] = fmaf(bv, yv[e], rh[e]);
-        const float z = sq * yv[e];
-        const uint16_t hi = f32_to_bf16(z);
-        const int r = sseg * EPT + e;
-        th[r * LDT + sk] = hi;
-        th[R * LDT + r * LDT + sk] = f32_to_bf16(z - bf16_to_f32(hi));
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int par = 0; par < 2; ++par) sq[kb][par] = sqrtf(fmaxf(wv[kb][par], 0.f));
+#pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const int kb = item_kb(i), r = item_r(i);
+        rh[i] = fmaf(bv[kb][1], y1[i], fmaf(bv[kb][0], y0[i], rh[i]));
+        const float z0 = sq[kb][0] * y0[i], z1 = sq[kb][1] * y1[i];
+        const uint16_t h0 = f32_to_bf16(z0), h1 = f32_to_bf16(z1);
+        const uint16_t l0 = f32_to_bf16(z0 - bf16_to_f32(h0)), l1 = f32_to_bf16(z1 - bf16_to_f32(h1));
+        const int dw = r * (LDT / 2) + 4 * kb + kp_low;
+        th[dw] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+        tl[dw] = (uint32_t)l0 | ((uint32_t)l1 << 16);
       }
     };
     const int nsteps = (int)((p1 - p0 + CH - 1) / CH);
@@ -693,15 +719,17 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
       if (more) store(buf ^ 1);
       __syncthreads();
     }
-    // rhs: the 16 staging threads of each element slice hold partial sums over their ratings
-    float* const rpart = lds;                                  // [16][R], staging is done
+    // rhs: sum the item partials over the 4 rating-pair lanes, then over the 2 pair groups
+    float* const rpart = lds;                                  // [2][R], staging is done
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) rpart[sk * R + sseg * EPT + e] = rh[e];
-    __syncthreads();
-    if (tid < R) {
-#pragma unroll
-      for (int k = 0; k < 16; ++k) rhs_t += rpart[k * R + tid];
+    for (int i = 0; i < ITEMS; ++i) {
+      float t = rh[i];
+      t += __shfl_xor(t, 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      if (kp_low == 0) rpart[item_kb(i) * R + item_r(i)] = t;
     }
+    __syncthreads();
+    if (tid < R) rhs_t = rpart[tid] + rpart[R + tid];
   } else {
     // f32 path: rounds of CH ratings staged through LDS, next round in registers
     constexpr int PF = (CH * R + NTH - 1) / NTH;
