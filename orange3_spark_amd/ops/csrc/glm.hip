@@ -570,9 +570,10 @@ __device__ __forceinline__ void mixed_tile(
 template <int LPR, int CPL, int UNROLL, int LOSS, int MW, int LW, int UR, bool SMP>
 __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
     const uint16_t* __restrict__ X, int64_t ld, int64_t n_res, const float* __restrict__ y,
-    const float* __restrict__ sw, const float* __restrict__ coef, const float* __restrict__ bptr,
-    uint32_t seed, int64_t row0, int64_t n_lin, float* __restrict__ partial, int pstride,
-    int64_t res_row0, const int64_t* __restrict__ t_dev, uint32_t sseed, uint32_t sthr) {
+    const float* __restrict__ sw, const float* __restrict__ y_lin, const float* __restrict__ sw_lin,
+    const float* __restrict__ coef, const float* __restrict__ bptr, uint32_t seed, int64_t row0, int64_t n_lin,
+    float* __restrict__ partial, int pstride, int64_t res_row0, const int64_t* __restrict__ t_dev, uint32_t sseed,
+    uint32_t sthr, int pacc) {
   constexpr int G = kWave / LPR;
   constexpr int RT = G * UNROLL;
   constexpr int DP = LPR * CPL * 8;
@@ -582,8 +583,6 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
   const int g = lane / LPR, c = lane % LPR;
   const int nch = (int)(ld / 8);
   const float intercept = *bptr;
-  const float* y_lin = y + n_res;
-  const float* sw_lin = sw ? sw + n_res : nullptr;
   // iteration t of a device-side SGD loop = t_dev + 1 (the update kernel advances it)
   // (SMP = false: the sampler is compiled out -- no hash, no extra registers)
   const uint32_t skey = SMP ? sample_key(sseed, (uint32_t)((t_dev ? t_dev[0] : 0) + 1)) : 0u;
@@ -670,7 +669,8 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
     float s = 0.f;
 #pragma unroll
     for (int q = 0; q < kWavesPerBlock; ++q) s += red[q][i];
-    partial[(int64_t)blockIdx.x * pstride + i] = s;
+    float* const pp = partial + (int64_t)blockIdx.x * pstride + i;
+    *pp = pacc ? *pp + s : s;           // pacc: later slices of a split pass add in
   }
 }
 
@@ -1196,23 +1196,23 @@ O3S_API int o3s_glm_grad(int loss, int src, const void* X, int64_t ld, int64_t n
 
 template <int L, int C, int MW, int LW, int UR, bool SMP = false>
 static void launch_mixed(int loss, int grid, hipStream_t st, const uint16_t* X, int64_t ld, int64_t n_res,
-                         const float* y, const float* sw, const float* coef, const float* b, uint32_t seed,
-                         int64_t row0, int64_t n_lin, float* partial, int pstride, int64_t res_row0,
-                         const int64_t* t_dev, uint32_t sseed, uint32_t sthr) {
+                         const float* y, const float* sw, const float* y_lin, const float* sw_lin, const float* coef,
+                         const float* b, uint32_t seed, int64_t row0, int64_t n_lin, float* partial, int pstride,
+                         int64_t res_row0, const int64_t* t_dev, uint32_t sseed, uint32_t sthr, int pacc) {
   constexpr int U = C >= 8 ? 1 : 8 / C;
   constexpr int UR2 = UR > 0 ? UR : U;
   if (loss == LOSS_LOGISTIC)
     hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_LOGISTIC, MW, LW, UR2, SMP>), dim3(grid), dim3(kBlock), 0,
-                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride, res_row0, t_dev,
-                       sseed, sthr);
+                       st, X, ld, n_res, y, sw, y_lin, sw_lin, coef, b, seed, row0, n_lin, partial, pstride,
+                       res_row0, t_dev, sseed, sthr, pacc);
   else if (loss == LOSS_HINGE)
     hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_HINGE, MW, LW, UR2, SMP>), dim3(grid), dim3(kBlock), 0,
-                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride, res_row0, t_dev,
-                       sseed, sthr);
+                       st, X, ld, n_res, y, sw, y_lin, sw_lin, coef, b, seed, row0, n_lin, partial, pstride,
+                       res_row0, t_dev, sseed, sthr, pacc);
   else
     hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_SQUARED, MW, LW, UR2, SMP>), dim3(grid), dim3(kBlock), 0,
-                       st, X, ld, n_res, y, sw, coef, b, seed, row0, n_lin, partial, pstride, res_row0, t_dev,
-                       sseed, sthr);
+                       st, X, ld, n_res, y, sw, y_lin, sw_lin, coef, b, seed, row0, n_lin, partial, pstride,
+                       res_row0, t_dev, sseed, sthr, pacc);
 }
 
 // Mixed resident + lineage pass in one launch (see glm_grad_mixed_kernel): n_res rows
@@ -1228,7 +1228,7 @@ O3S_API int o3s_glm_grad_mixed(int loss, const void* X, int64_t ld, int64_t n_re
                                const float* sw, const float* coef, uint32_t seed, int64_t row0,
                                int64_t n_lin, float* partial, int grid, double* out, int waves,
                                int mode, int64_t res_row0, const int64_t* t_dev, uint32_t sseed,
-                               uint32_t sthr, hipStream_t st) {
+                               uint32_t sthr, int splits, hipStream_t st) {
   const int nch = (int)(ld / 8);
   const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
   if (ld % 8 != 0 || cpl > 16 || grid <= 0 || n_res < 0 || n_lin < 0) return -1;
@@ -1239,46 +1239,57 @@ O3S_API int o3s_glm_grad_mixed(int loss, const void* X, int64_t ld, int64_t n_re
   const uint16_t* Xh = (const uint16_t*)X;
   const float* b = coef + dpad;
   const bool smp = sthr < (1u << 24);     // sampling: interleaved-role layouts (mode 0) only
-  bool done = false;
 #define O3S_MX(L, C)                                                                                  \
   if (!done && lpr_s == L && cpl_s == C) {                                                            \
     done = true;                                                                                      \
     if (mode == 0 && waves == 3 && smp)                                                               \
-      launch_mixed<L, C, 3, 0, 0, true>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0,    \
-                                        n_lin, partial, pstride, res_row0, t_dev, sseed, sthr);       \
+      launch_mixed<L, C, 3, 0, 0, true>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0,  \
+                                        NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                    \
     else if (mode == 0 && waves == 3)                                                                 \
-      launch_mixed<L, C, 3, 0, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
+      launch_mixed<L, C, 3, 0, 0>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
     else if (mode == 0 && smp)                                                                        \
-      launch_mixed<L, C, 2, 0, 0, true>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0,    \
-                                        n_lin, partial, pstride, res_row0, t_dev, sseed, sthr);       \
+      launch_mixed<L, C, 2, 0, 0, true>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);       \
     else if (mode == 0)                                                                               \
-      launch_mixed<L, C, 2, 0, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
+      launch_mixed<L, C, 2, 0, 0>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
     else if (smp)                                                                                     \
       done = false;                                                                                   \
     else if (mode == 1)                                                                               \
-      launch_mixed<L, C, 3, 1, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
+      launch_mixed<L, C, 3, 1, 0>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
     else if (mode == 2)                                                                               \
-      launch_mixed<L, C, 3, 2, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
+      launch_mixed<L, C, 3, 2, 0>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
     else if (mode == 3)                                                                               \
-      launch_mixed<L, C, 3, 3, 0>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
+      launch_mixed<L, C, 3, 3, 0>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
     else if (mode == 12)                                                                              \
-      launch_mixed<L, C, 3, 2, 4>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
+      launch_mixed<L, C, 3, 2, 4>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
     else if (mode == 11)                                                                              \
-      launch_mixed<L, C, 3, 1, 4>(loss, grid, st, Xh, ld, n_res, y, sw, coef, b, seed, row0, n_lin,   \
-                                  partial, pstride, res_row0, t_dev, sseed, sthr);                   \
+      launch_mixed<L, C, 3, 1, 4>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
     else done = false;                                                                                \
   }
-  O3S_MX(4, 1) O3S_MX(8, 1) O3S_MX(4, 4) O3S_MX(8, 4) O3S_MX(16, 4) O3S_MX(32, 4)
-  O3S_MX(64, 4) O3S_MX(64, 8) O3S_MX(64, 16)
+  // splits > 1: the pass runs as that many launches over consecutive 1/splits slices of
+  // the resident and of the lineage rows; later slices add their block sums into the
+  // first slice's slabs (slice order fixed: as deterministic as one launch).  A
+  // grid-stride tile walk drifts over a long launch -- waves that started together end up
+  // gigabytes apart, so the resident stream touches a wider address window; restarting
+  // the walk every 1/splits of a 255 GB table measured 44.2 -> 43.7 ms even with a finish
+  // per slice (tools/bench_glm_split_ab.py).
+  const int K = splits < 1 ? 1 : splits;
+  for (int k = 0; k < K; ++k) {
+    const int64_t r_lo = n_res * k / K, r_hi = n_res * (k + 1) / K;
+    const int64_t l_lo = n_lin * k / K, l_hi = n_lin * (k + 1) / K;
+    const uint16_t* XS = Xh + r_lo * ld;
+    const int64_t NR = r_hi - r_lo, NL = l_hi - l_lo, RL0 = row0 + l_lo, RR0 = res_row0 + r_lo;
+    const float* YR = y + r_lo;
+    const float* SWR = sw ? sw + r_lo : nullptr;
+    const float* YL = y + n_res + l_lo;
+    const float* SWL = sw ? sw + n_res + l_lo : nullptr;
+    float* PS = partial;                 // slices after the first add into the same slabs
+    bool done = false;
+    O3S_MX(4, 1) O3S_MX(8, 1) O3S_MX(4, 4) O3S_MX(8, 4) O3S_MX(16, 4) O3S_MX(32, 4)
+    O3S_MX(64, 4) O3S_MX(64, 8) O3S_MX(64, 16)
+    if (!done) return -1;
+    O3S_CHECK_LAUNCH();
+  }
 #undef O3S_MX
-  if (!done) return -1;
-  O3S_CHECK_LAUNCH();
   const int ncols = dpad + 3;
   hipLaunchKernelGGL(glm_finish_kernel, dim3((ncols + 31) / 32), dim3(1024), 0, st, partial, grid,
                      pstride, ncols, out, 0);

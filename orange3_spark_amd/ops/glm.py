@@ -237,6 +237,13 @@ MIX_WAVES = int(os.environ.get("O3S_GLM_MIX_WAVES", "3"))
 # 0 = every wave interleaves both roles; 1..3 = lineage waves per 4-wave block (fixed
 # roles); 11/12 = fixed roles with 4 resident rows in flight per lane
 MIX_MODE = int(os.environ.get("O3S_GLM_MIX_MODE", "0"))
+# rows per launch slice of a mixed pass (csrc/glm.hip o3s_glm_grad_mixed ``splits``): long
+# passes restart their grid-stride walk every this many rows, at most 16 slices
+MIX_SLICE_ROWS = int(os.environ.get("O3S_GLM_MIX_SLICE_ROWS", str(64 << 20)))
+
+
+def mix_splits(n_rows: int) -> int:
+    return max(1, min(16, n_rows // max(1, MIX_SLICE_ROWS)))
 
 
 def sample_threshold(fraction: float) -> int:
@@ -296,7 +303,8 @@ def glm_grad_mixed(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, n_
                                            cf.data_ptr(), seed & _MASK, row0, n_lin, ws.partial.data_ptr(),
                                            ws.grid, ws.out.data_ptr(), MIX_WAVES,
                                            MIX_MODE if thr >= 1 << 24 else 0, int(res_row0),
-                                           N.ptr(t_dev), int(sample_seed) & _MASK, thr, N.stream_of(X)),
+                                           N.ptr(t_dev), int(sample_seed) & _MASK, thr, mix_splits(nr + n_lin),
+                                           N.stream_of(X)),
             "glm_grad_mixed")
     return ws.out
 

@@ -145,6 +145,30 @@ def test_gpu_grad_mixed_modes_agree(gpu, mode, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("slice_rows", [7000, 30000])
+@pytest.mark.parametrize("frac", [1.0, 0.3])
+def test_gpu_grad_mixed_split_launches_agree(gpu, slice_rows, frac, monkeypatch):
+    """A mixed pass run as several launches over row slices (o3s_glm_grad_mixed splits,
+    later slices adding into the first slice's slabs) == one launch up to fp32 block-sum
+    order, with and without mini-batch sampling (global row keys shifted per slice); the
+    split pass is deterministic."""
+    n_res, n_lin, d, seed = 40009, 30011, 256, 21
+    Xr, yr = G.synth_glm(n_res, d, seed + 1, device=gpu)
+    yall = torch.cat([yr, (torch.arange(n_lin, device=gpu) % 3 == 0).float()])
+    coef = torch.randn(d, generator=torch.Generator().manual_seed(2)).to(gpu) * 0.05
+    ws = G.GlmWorkspace(gpu, d, grid=512)
+    kw = dict(res_row0=123, sample_seed=9, fraction=frac)
+    monkeypatch.setattr(G, "MIX_SLICE_ROWS", 1 << 40)
+    ref = G.glm_grad_mixed(Xr, yall, None, n_lin, d, seed, n_res, coef, -0.2, 0, ws, **kw).clone()
+    monkeypatch.setattr(G, "MIX_SLICE_ROWS", slice_rows)
+    assert G.mix_splits(n_res + n_lin) > 1
+    out = G.glm_grad_mixed(Xr, yall, None, n_lin, d, seed, n_res, coef, -0.2, 0, ws, **kw).clone()
+    again = G.glm_grad_mixed(Xr, yall, None, n_lin, d, seed, n_res, coef, -0.2, 0, ws, **kw).clone()
+    assert torch.equal(out, again)
+    assert torch.allclose(out, ref, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("d,K,weighted,pad", [(256, 10, False, 0), (20, 3, True, 12), (100, 32, True, 4),
                                              (64, 2, False, 0), (200, 7, False, 56)])
 def test_gpu_softmax_pass_matches_fp64(gpu, d, K, weighted, pad):
