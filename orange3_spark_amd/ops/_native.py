@@ -32,7 +32,7 @@ _SIGS: dict[str, list] = {
                      c_vp, c_f32, c_vp, c_i32, c_vp, c_i32, c_vp],
     "o3s_glm_grad_mixed": [c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_u32, c_i64, c_i64,
                            c_vp, c_i32, c_vp, c_i32, c_i32, c_i64, c_vp, c_u32, c_u32, c_i32, c_vp],
-    "o3s_glm_stats_mixed": [c_vp, c_i64, c_i64, c_vp, c_vp, c_u32, c_i64, c_i64, c_vp, c_i32, c_vp, c_vp],
+    "o3s_glm_stats_mixed": [c_vp, c_i64, c_i64, c_vp, c_vp, c_u32, c_i64, c_i64, c_vp, c_i32, c_vp, c_i32, c_vp],
     "o3s_bin_features": [c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp],
     "o3s_u8_transpose": [c_vp, c_i64, c_i32, c_vp, c_vp],
     "o3s_slab_range_sum": [c_vp, c_i32, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp],

@@ -750,8 +750,8 @@ __device__ __forceinline__ void stats_tile(int64_t base, int64_t n, const uint16
   }
 }
 
-template <int LPR, int CPL>
-__global__ __launch_bounds__(kBlock, 2) void glm_stats_mixed_kernel(
+template <int LPR, int CPL, int MW>
+__global__ __launch_bounds__(kBlock, MW) void glm_stats_mixed_kernel(
     const uint16_t* __restrict__ X, int64_t ld, int64_t n_res, const float* __restrict__ y,
     const float* __restrict__ sw, uint32_t seed, int64_t row0, int64_t n_lin, float* __restrict__ partial,
     int pstride) {
@@ -1399,7 +1399,7 @@ O3S_API int o3s_glm_sgd_update_dev(const double* out, int dpad, double* bt, doub
 // uses o3s_glm_colstats plus a regular first pass.
 O3S_API int o3s_glm_stats_mixed(const void* X, int64_t ld, int64_t n_res, const float* y, const float* sw,
                                 uint32_t seed, int64_t row0, int64_t n_lin, float* partial, int grid, double* out,
-                                hipStream_t st) {
+                                int waves, hipStream_t st) {
   const int nch = (int)(ld / 8);
   const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
   if (ld % 8 != 0 || cpl > 16 || grid <= 0 || n_res < 0 || n_lin < 0) return -1;
@@ -1412,8 +1412,12 @@ O3S_API int o3s_glm_stats_mixed(const void* X, int64_t ld, int64_t n_res, const 
 #define O3S_ST(L, C)                                                                                        \
   if (!done && lpr_s == L && cpl_s == C) {                                                                  \
     done = true;                                                                                            \
-    hipLaunchKernelGGL((glm_stats_mixed_kernel<L, C>), dim3(grid), dim3(kBlock), 0, st, Xh, ld, n_res, y, sw, \
-                       seed, row0, n_lin, partial, pstride);                                                \
+    if (waves == 3)                                                                                         \
+      hipLaunchKernelGGL((glm_stats_mixed_kernel<L, C, 3>), dim3(grid), dim3(kBlock), 0, st, Xh, ld, n_res, y, \
+                         sw, seed, row0, n_lin, partial, pstride);                                          \
+    else                                                                                                    \
+      hipLaunchKernelGGL((glm_stats_mixed_kernel<L, C, 2>), dim3(grid), dim3(kBlock), 0, st, Xh, ld, n_res, y, \
+                         sw, seed, row0, n_lin, partial, pstride);                                          \
   }
   O3S_ST(4, 1) O3S_ST(8, 1) O3S_ST(4, 4) O3S_ST(8, 4) O3S_ST(16, 4) O3S_ST(32, 4) O3S_ST(64, 4)
 #undef O3S_ST

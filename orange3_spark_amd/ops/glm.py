@@ -237,6 +237,8 @@ MIX_WAVES = int(os.environ.get("O3S_GLM_MIX_WAVES", "3"))
 # 0 = every wave interleaves both roles; 1..3 = lineage waves per 4-wave block (fixed
 # roles); 11/12 = fixed roles with 4 resident rows in flight per lane
 MIX_MODE = int(os.environ.get("O3S_GLM_MIX_MODE", "0"))
+# waves/SIMD the fused summarizer kernel is compiled for (2: no spill, 3: 6-VGPR spill)
+STATS_WAVES = int(os.environ.get("O3S_GLM_STATS_WAVES", "2"))
 # rows per launch slice of a mixed pass (csrc/glm.hip o3s_glm_grad_mixed ``splits``): long
 # passes restart their grid-stride walk every this many rows, at most 16 slices
 MIX_SLICE_ROWS = int(os.environ.get("O3S_GLM_MIX_SLICE_ROWS", str(64 << 20)))
@@ -327,7 +329,7 @@ def glm_stats_mixed(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, n
     partial = torch.empty(grid * pstride, dtype=torch.float32, device=X.device)
     out = torch.empty(3 * dpad + 3, dtype=torch.float64, device=X.device)
     rc = N.kernels().o3s_glm_stats_mixed(X.data_ptr(), ld, nr, y.data_ptr(), N.ptr(sw), seed & _MASK, row0,
-                                         n_lin, partial.data_ptr(), grid, out.data_ptr(), N.stream_of(X))
+                                         n_lin, partial.data_ptr(), grid, out.data_ptr(), STATS_WAVES, N.stream_of(X))
     if rc == -2:
         return None
     N.check(rc, "glm_stats_mixed")
