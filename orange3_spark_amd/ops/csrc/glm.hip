@@ -682,7 +682,9 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
 // zero, so each row's margin is the intercept b0 and the step-1 gradient of every loss
 // is a combination of s1 and syx (logistic: sigmoid(b0) s1 - syx) -- the fit's first
 // step needs no pass of its own (models/glm.py: DeviceSGD.first_step_from_stats).
-template <int LPR, int CPL, int SRC>
+// UNW: a full tile (every row < n) of an unweighted fit -- w = 1 is folded away, which
+// drops the w*x product from every element (the pass is VALU-bound on lineage tiles).
+template <int LPR, int CPL, int SRC, bool UNW>
 __device__ __forceinline__ void stats_tile(int64_t base, int64_t n, const uint16_t* __restrict__ X, int64_t ld,
                                            int nch, const float* __restrict__ y, const float* __restrict__ sw,
                                            uint32_t seed, int64_t row0, int g, int c, float2_ (&s1)[CPL][4],
@@ -698,8 +700,12 @@ __device__ __forceinline__ void stats_tile(int64_t base, int64_t n, const uint16
     const bool ok = row < n;
     const int64_t rowc = ok ? row : n - 1;
     yv[u] = y[rowc];
-    const float w0 = sw ? sw[rowc] : 1.f;
-    wv[u] = ok ? w0 : 0.f;
+    if (UNW) {
+      wv[u] = 1.f;
+    } else {
+      const float w0 = sw ? sw[rowc] : 1.f;
+      wv[u] = ok ? w0 : 0.f;
+    }
     if (SRC == 0) {
 #pragma unroll
       for (int k = 0; k < CPL; ++k) {
@@ -736,7 +742,7 @@ __device__ __forceinline__ void stats_tile(int64_t base, int64_t n, const uint16
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float2_ xx = {x[2 * j], x[2 * j + 1]};
-        const float2_ wx = w2 * xx;
+        const float2_ wx = UNW ? xx : w2 * xx;
         s1[k][j] += wx;
         s2[k][j] = __builtin_elementwise_fma(wx, xx, s2[k][j]);
         syx[k][j] = __builtin_elementwise_fma(wy2, xx, syx[k][j]);
@@ -778,10 +784,19 @@ __global__ __launch_bounds__(kBlock, MW) void glm_stats_mixed_kernel(
     int64_t L = gw * Tl / S, rem = gw * Tl - L * S;
     const int64_t q0 = nw * Tl / S, r0 = nw * Tl - q0 * S;
     for (int64_t s = gw; s < S; s += nw) {
-      if (rem + Tl >= S)
-        stats_tile<LPR, CPL, 1>(L * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, g, c, s1, s2, syx, rsum);
-      else
-        stats_tile<LPR, CPL, 0>((s - L) * RT, n_res, X, ld, nch, y, sw, seed, row0, g, c, s1, s2, syx, rsum);
+      if (rem + Tl >= S) {
+        const int64_t base = L * RT;
+        if (sw == nullptr && base + RT <= n_lin)
+          stats_tile<LPR, CPL, 1, true>(base, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, g, c, s1, s2, syx, rsum);
+        else
+          stats_tile<LPR, CPL, 1, false>(base, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, g, c, s1, s2, syx, rsum);
+      } else {
+        const int64_t base = (s - L) * RT;
+        if (sw == nullptr && base + RT <= n_res)
+          stats_tile<LPR, CPL, 0, true>(base, n_res, X, ld, nch, y, sw, seed, row0, g, c, s1, s2, syx, rsum);
+        else
+          stats_tile<LPR, CPL, 0, false>(base, n_res, X, ld, nch, y, sw, seed, row0, g, c, s1, s2, syx, rsum);
+      }
       rem += r0;
       L += q0;
       if (rem >= S) { rem -= S; ++L; }
