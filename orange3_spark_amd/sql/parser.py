@@ -888,7 +888,8 @@ class Parser:
             return unboundedFollowing
         if self.word("current", "row"):
             return currentRow
-        n = int(float(self.expect("num").val))
+        x = float(self.expect("num").val)
+        n = int(x) if x.is_integer() else x       # RANGE frames take fractional value offsets
         if self.word("preceding"):
             return -n
         if self.word("following"):

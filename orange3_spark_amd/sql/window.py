@@ -11,7 +11,8 @@ partition by the ORDER BY keys and scanning it.  Here (frame/shuffle.py machiner
    key changes; ranks / ntile / percent_rank / cume_dist are index arithmetic,
    lag / lead are shifted gathers masked at segment edges, aggregates use segment
    prefix sums (running / ROWS BETWEEN frames: differences of inclusive prefix sums;
-   RANGE frames with ties: the value at the last peer) or segment reductions
+   RANGE frames with ties: the value at the last peer; RANGE frames with value offsets:
+   edges from a vectorised per-partition binary search) or segment reductions
    (unordered windows); frame min/max use a sparse table (log-step doubling, any frame).
 
 Several window expressions in one ``select`` share the exchange + sort when they use
@@ -59,11 +60,15 @@ class WindowSpec:
     def rowsBetween(self, start: int, end: int):
         return WindowSpec(self._partition, self._order, ("rows", int(start), int(end)))
 
-    def rangeBetween(self, start: int, end: int):
-        if (start, end) not in ((unboundedPreceding, currentRow), (unboundedPreceding, unboundedFollowing),
-                                (currentRow, unboundedFollowing), (currentRow, currentRow)):
-            raise NotImplementedError("rangeBetween supports unbounded / currentRow boundaries")
-        return WindowSpec(self._partition, self._order, ("range", int(start), int(end)))
+    def rangeBetween(self, start, end):
+        """RANGE frame: ``unboundedPreceding`` / ``currentRow`` (the row's peers) /
+        ``unboundedFollowing``, or numeric value offsets -- a row is in the frame when its
+        ORDER BY value lies within ``[v + start, v + end]`` (Spark ``RangeFrame``; needs
+        exactly one numeric ORDER BY expression)."""
+        def norm(x):
+            x = float(x) if not isinstance(x, int) else x
+            return int(x) if float(x).is_integer() else x
+        return WindowSpec(self._partition, self._order, ("range", norm(start), norm(end)))
 
     def _key(self):
         return (tuple(e.name for e in self._partition),
@@ -319,8 +324,64 @@ class _Ctx:
             lo = st if a <= unboundedPreceding else torch.maximum(st, ar + a)
             hi = en if b >= unboundedFollowing else torch.minimum(en, ar + b)
             return lo, hi
-        lo = st if a <= unboundedPreceding else self.peer_first[self.peer]
-        hi = en if b >= unboundedFollowing else self.peer_last[self.peer]
+        if (a <= unboundedPreceding or a == 0) and (b >= unboundedFollowing or b == 0):
+            lo = st if a <= unboundedPreceding else self.peer_first[self.peer]
+            hi = en if b >= unboundedFollowing else self.peer_last[self.peer]
+            return lo, hi
+        return self._range_value_bounds(a, b, st, en)
+
+    def _range_value_bounds(self, a, b, st, en):
+        """RANGE BETWEEN with value offsets (Spark ``RangeFrame``): row j is in row i's frame
+        when s_j lies in [s_i + a, s_i + b], with s the ORDER BY value (negated for DESC, so
+        PRECEDING always runs against the sort direction).  Rows are sorted by s inside each
+        partition with the nulls contiguous at one end, so both edges come from one
+        vectorised binary search per side over the partition's non-null rows.  A null
+        current row's frame is its null peers (the bound v + offset is null)."""
+        if len(self.spec._order) != 1:
+            raise ValueError("a RANGE frame with value offsets needs exactly one ORDER BY expression")
+        e = self.spec._order[0]
+        c = e.eval(self.df)
+        if not isinstance(c, C.NumericColumn):
+            raise TypeError("a RANGE frame with value offsets needs a numeric ORDER BY expression")
+        dev = st.device
+        n = self.n
+        v = c.data.to(torch.float64).to(dev)
+        null = c.null_mask().to(dev) | torch.isnan(v)
+        s = -v if getattr(e, "_desc", False) else v
+        ar = torch.arange(n, device=dev)
+        nseg = self.seg_len.numel()
+        nn_first = torch.full((nseg,), n, dtype=torch.int64, device=dev)
+        nn_last = torch.full((nseg,), -1, dtype=torch.int64, device=dev)
+        if bool((~null).any()):
+            nn_first.scatter_reduce_(0, self.seg[~null], ar[~null], "amin", include_self=True)
+            nn_last.scatter_reduce_(0, self.seg[~null], ar[~null], "amax", include_self=True)
+        f0, f1 = nn_first[self.seg], nn_last[self.seg] + 1
+        steps = max(1, int(n).bit_length() + 1)
+
+        def first_at_least(target, strict):
+            # first j in [f0, f1) with s_j >= target (> target when strict); f1 if none
+            L, R = f0.clone(), f1.clone()
+            for _ in range(steps):
+                act = L < R
+                mid = (L + R) // 2
+                sm = s[mid.clamp(0, max(n - 1, 0))]
+                right = act & ((sm <= target) if strict else (sm < target))
+                L = torch.where(right, mid + 1, L)
+                R = torch.where(act & ~right, mid, R)
+            return L
+
+        if a <= unboundedPreceding:
+            lo = st
+        elif a == 0:
+            lo = self.peer_first[self.peer]
+        else:
+            lo = torch.where(null, self.peer_first[self.peer], first_at_least(s + a, False))
+        if b >= unboundedFollowing:
+            hi = en
+        elif b == 0:
+            hi = self.peer_last[self.peer]
+        else:
+            hi = torch.where(null, self.peer_last[self.peer], first_at_least(s + b, True) - 1)
         return lo, hi
 
     def _agg(self, a: E.Agg):
@@ -383,8 +444,9 @@ class _Ctx:
         length = (hi - lo + 1).clamp(min=1)
         lg = torch.floor(torch.log2(length.to(torch.float64))).to(torch.int64)
         table = torch.stack(levels)                    # [L, n]
-        a_ = table[lg, lo.clamp(min=0)]
-        b_ = table[lg, (hi - (1 << lg) + 1).clamp(min=0)]
+        top = max(self.n - 1, 0)                       # empty frames may sit past the end
+        a_ = table[lg, lo.clamp(0, top)]
+        b_ = table[lg, (hi - (1 << lg) + 1).clamp(0, top)]
         r = op(a_, b_)
         good = torch.isfinite(r) & (hi >= lo)
         return self._dbl(torch.where(good, r, torch.zeros_like(r)), None if bool(good.all()) else good)

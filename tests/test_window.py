@@ -107,3 +107,64 @@ def test_window_with_column_and_global_order(s):
     out = df.withColumn("r", F.dense_rank().over(Window.orderBy(F.col("x").desc()))).toPandas()
     assert out.x.tolist() == [5.0, 3.0, 3.0, 1.0] and out.r.tolist() == [1, 2, 2, 3]
     assert not any(c.startswith("__win") for c in out.columns)
+
+
+def _range_oracle(pdf, a, b, desc, fn):
+    """Brute-force Spark RangeFrame: rows of the same g whose value lies in [v+a, v+b]
+    (DESC: s = -v)."""
+    out = []
+    for _, r in pdf.iterrows():
+        part = pdf[pdf.g == r.g]
+        if pd.isna(r.v):
+            fr = part[part.v.isna()]
+        else:
+            s = -part.v if desc else part.v
+            si = -r.v if desc else r.v
+            fr = part[part.v.notna() & (s >= si + a) & (s <= si + b)]
+        vals = fr.v.dropna()
+        out.append(None if fn != "count" and vals.empty else
+                   {"sum": vals.sum(), "count": len(fr), "max": vals.max() if len(vals) else None,
+                    "avg": vals.mean() if len(vals) else None}[fn])
+    return out
+
+
+@pytest.mark.parametrize("a,b,desc", [(-3, 0, False), (-2, 2, False), (1, 4, False), (-2.5, 1.5, False),
+                                      (-3, 1, True)])
+def test_range_frame_value_offsets(s, a, b, desc):
+    rng = np.random.default_rng(3)
+    n = 240
+    pdf = pd.DataFrame({"g": rng.choice(["a", "b", "c"], n), "v": rng.integers(0, 30, n).astype(float),
+                        "id": np.arange(n)})
+    df = s.createDataFrame(pdf)
+    o = F.col("v").desc() if desc else F.col("v")
+    w = Window.partitionBy("g").orderBy(o).rangeBetween(a, b)
+    got = df.select("id", F.sum("v").over(w).alias("s"), F.count("*").over(w).alias("c"),
+                    F.max("v").over(w).alias("m"), F.avg("v").over(w).alias("av")).toPandas().sort_values("id")
+    for col, fn in (("s", "sum"), ("c", "count"), ("m", "max"), ("av", "avg")):
+        exp = _range_oracle(pdf, a, b, desc, fn)
+        g = got[col].tolist()
+        for x, y in zip(g, exp):
+            if y is None:
+                assert x is None or (isinstance(x, float) and np.isnan(x))
+            else:
+                assert x == pytest.approx(y)
+
+
+def test_range_frame_offsets_nulls_and_sql(s):
+    rows = [("a", v, i) for i, v in enumerate([1.0, 2.0, None, 4.0, 7.0, None, 8.0])]
+    df = s.createDataFrame(rows, ["g", "v", "id"])            # float None -> NaN: sorts last, NaNs are peers
+    w = Window.partitionBy("g").orderBy("v").rangeBetween(-3, 0)
+    got = df.select("id", F.sum("v").over(w).alias("s"), F.count("*").over(w).alias("c")) \
+        .toPandas().sort_values("id")
+    # a NaN row's frame = the NaN rows (its peers)
+    assert got.s.tolist()[:2] == [1.0, 3.0] and got.s.tolist()[3:5] == [7.0, 11.0] and got.s.tolist()[6] == 15.0
+    assert got.c.tolist() == [1, 2, 2, 3, 2, 2, 2]
+    w2 = Window.partitionBy("g").orderBy("v").rangeBetween(Window.unboundedPreceding, 1)
+    got2 = df.select("id", F.count("*").over(w2).alias("c")).toPandas().sort_values("id")
+    assert got2.c.tolist() == [2, 2, 7, 3, 5, 7, 5]      # NaN rows: partition start .. last NaN peer
+    df.createOrReplaceTempView("rt")
+    q = s.sql("SELECT id, SUM(v) OVER (PARTITION BY g ORDER BY v RANGE BETWEEN 3 PRECEDING AND CURRENT ROW) AS s "
+              "FROM rt").toPandas().sort_values("id")
+    assert q.s.tolist()[3:5] == [7.0, 11.0]
+    with pytest.raises(ValueError):
+        df.select(F.sum("v").over(Window.orderBy("v", "id").rangeBetween(-1, 1))).toPandas()
