@@ -36,6 +36,10 @@ _IDS = itertools.count()
 _REGISTRY: "weakref.WeakValueDictionary[str, WindowExpr]" = weakref.WeakValueDictionary()
 _PREFIX = "__win:"
 
+# aggregates evaluated per frame by the group-by finaliser (host): no prefix-sum form
+_HOST_FRAME_AGGS = ("collect_set", "median", "mode", "product", "bool_and", "bool_or", "percentile",
+                    "percentile_exact", "max_by", "min_by")
+
 unboundedPreceding = -(1 << 62)
 unboundedFollowing = 1 << 62
 currentRow = 0
@@ -399,6 +403,13 @@ class _Ctx:
             arr = np.empty(self.n, dtype=object)
             arr[:] = [[v for v in vals[x:y + 1] if v is not None] for x, y in zip(lo_n, hi_n)]
             return C.ArrayColumn(arr)
+        if a.fn in _HOST_FRAME_AGGS or (a.distinct and a.fn in ("count", "sum", "avg")):
+            # order statistics / sets / products: the group-by finaliser on every row's frame
+            from ..frame.groupby import _host_final, _result_column
+            vals = list(c.values) if isinstance(c, C.HostColumn) else c.to_pylist()
+            lo_n, hi_n = lo.cpu().numpy(), hi.cpu().numpy()
+            res = [_host_final(a, list(enumerate(vals[x:y + 1])) if y >= x else []) for x, y in zip(lo_n, hi_n)]
+            return _result_column(a, res)
         if not isinstance(c, C.NumericColumn):
             raise TypeError(f"{a.fn} over a window needs a numeric column")
         d = c.data.to(torch.float64).to(lo.device)
@@ -423,6 +434,24 @@ class _Ctx:
             var = var.clamp(min=0)
             good = cnt > 1
             return self._dbl(var.sqrt() if a.fn == "stddev" else var, None if bool(good.all()) else good)
+        if a.fn in ("stddev_pop", "var_pop", "skewness", "kurtosis"):
+            # population moments from frame power sums (the group-by formulas, groupby._final)
+            n_ = cnt.clamp(min=1)
+            s1, s2 = wsum(dz), wsum(dz * dz)
+            mu = s1 / n_
+            m2 = (s2 / n_ - mu * mu).clamp(min=0)
+            if a.fn in ("stddev_pop", "var_pop"):
+                return self._dbl(m2.sqrt() if a.fn == "stddev_pop" else m2, None if bool(has.all()) else has)
+            s3 = wsum(dz * dz * dz)
+            good = has & (m2 > 0)
+            m2s = torch.where(good, m2, torch.ones_like(m2))
+            if a.fn == "skewness":
+                m3 = s3 / n_ - 3 * mu * s2 / n_ + 2 * mu ** 3
+                r = m3 / m2s ** 1.5
+            else:
+                m4 = wsum(dz ** 4) / n_ - 4 * mu * s3 / n_ + 6 * mu * mu * s2 / n_ - 3 * mu ** 4
+                r = m4 / (m2s * m2s) - 3.0
+            return self._dbl(torch.where(good, r, torch.zeros_like(r)), None if bool(good.all()) else good)
         if a.fn in ("min", "max"):
             return self._minmax(d, ok, lo, hi, a.fn == "max")
         raise NotImplementedError(f"{a.fn} over a window")

@@ -168,3 +168,27 @@ def test_range_frame_offsets_nulls_and_sql(s):
     assert q.s.tolist()[3:5] == [7.0, 11.0]
     with pytest.raises(ValueError):
         df.select(F.sum("v").over(Window.orderBy("v", "id").rangeBetween(-1, 1))).toPandas()
+
+
+def test_window_moment_and_host_aggregates(s):
+    rng = np.random.default_rng(5)
+    n = 90
+    pdf = pd.DataFrame({"g": rng.choice(["a", "b"], n), "v": rng.integers(0, 9, n).astype(float),
+                        "id": np.arange(n)})
+    df = s.createDataFrame(pdf)
+    w = Window.partitionBy("g").orderBy("id").rowsBetween(-4, 0)
+    got = df.select("id", F.var_pop("v").over(w).alias("vp"), F.skewness("v").over(w).alias("sk"),
+                    F.kurtosis("v").over(w).alias("ku"), F.collect_set("v").over(w).alias("cs"),
+                    F.median("v").over(w).alias("md"), F.product("v").over(w).alias("pr")) \
+        .toPandas().sort_values("id").reset_index(drop=True)
+    for i, r in pdf.iterrows():
+        part = pdf[(pdf.g == r.g) & (pdf.id <= r.id)].tail(5).v.to_numpy()
+        mu = part.mean()
+        m2 = ((part - mu) ** 2).mean()
+        assert got.vp[i] == pytest.approx(m2, abs=1e-9)
+        if m2 > 0:
+            assert got.sk[i] == pytest.approx(((part - mu) ** 3).mean() / m2 ** 1.5, abs=1e-7)
+            assert got.ku[i] == pytest.approx(((part - mu) ** 4).mean() / m2 ** 2 - 3, abs=1e-7)
+        assert sorted(got.cs[i]) == sorted(set(part.tolist()))
+        assert got.md[i] == pytest.approx(np.median(part))
+        assert got.pr[i] == pytest.approx(np.prod(part))
