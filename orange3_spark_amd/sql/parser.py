@@ -98,6 +98,42 @@ def tokenize(sql: str) -> list[Tok]:
     return out
 
 
+def _named_windows(toks: list) -> tuple[list, dict]:
+    """``WINDOW w AS (spec)[, w2 AS (spec)]`` clauses: cut out of the token stream and kept
+    by name; ``OVER w`` splices the spec's tokens back in (window_spec).  The WINDOW word
+    followed by ``(`` is the window() time-bucket function, not a clause."""
+    def definition(i):          # toks[i] = name, toks[i+1] = AS, toks[i+2] = "(" -> index after ")"
+        if not (toks[i].kind == "id" and toks[i + 1].kind == "kw" and toks[i + 1].val == "as"
+                and toks[i + 2].kind == "op" and toks[i + 2].val == "("):
+            return None
+        j, depth = i + 2, 0
+        while toks[j].kind != "eof":
+            if toks[j].kind == "op" and toks[j].val in "()":
+                depth += 1 if toks[j].val == "(" else -1
+            j += 1
+            if depth == 0:
+                return j
+        raise SyntaxError("unterminated WINDOW definition")
+
+    out, named, i = [], {}, 0
+    while i < len(toks):
+        t = toks[i]
+        if t.kind == "id" and t.val.lower() == "window" and i + 4 < len(toks) and definition(i + 1):
+            i += 1
+            while True:
+                j = definition(i)
+                named[toks[i].val.lower()] = toks[i + 2:j]
+                i = j
+                if toks[i].kind == "op" and toks[i].val == "," and definition(i + 1):
+                    i += 1
+                    continue
+                break
+            continue
+        out.append(t)
+        i += 1
+    return out, named
+
+
 @dataclass
 class SelectItem:
     expr: object            # Expr | AggCall | "*"
@@ -182,7 +218,7 @@ class SetOp:
 
 class Parser:
     def __init__(self, sql: str):
-        self.toks = tokenize(sql)
+        self.toks, self.windows = _named_windows(tokenize(sql))
         self.i = 0
         self.src = sql
 
@@ -900,6 +936,9 @@ class Parser:
         """``<function> OVER ([PARTITION BY e, ...] [ORDER BY e [ASC|DESC], ...]
         [ROWS|RANGE BETWEEN <bound> AND <bound>])``."""
         from .window import WindowExpr, WindowFunction, WindowSpec
+        t = self.peek()
+        if t.kind == "id" and t.val.lower() in self.windows:          # OVER w (named WINDOW clause)
+            self.toks[self.i:self.i + 1] = list(self.windows[t.val.lower()])
         self.expect("op", "(")
         spec = WindowSpec()
         if self.word("partition", "by"):
@@ -921,7 +960,7 @@ class Parser:
                 spec = spec.rowsBetween(lo, hi) if kind == "rows" else spec.rangeBetween(lo, hi)
         self.expect("op", ")")
         if isinstance(f, AggCall):
-            f = E.Agg(f.fn, f.arg, f.text, f.distinct)
+            f = f.built if f.built is not None else E.Agg(f.fn, f.arg, f.text, f.distinct)
         if not isinstance(f, (E.Agg, WindowFunction)):
             raise SyntaxError("OVER applies to aggregate or window functions")
         return WindowExpr(f, spec, f"{f.name} OVER (...)")

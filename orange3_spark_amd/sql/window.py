@@ -434,6 +434,29 @@ class _Ctx:
             var = var.clamp(min=0)
             good = cnt > 1
             return self._dbl(var.sqrt() if a.fn == "stddev" else var, None if bool(good.all()) else good)
+        if a.fn in ("corr", "covar_pop", "covar_samp"):
+            # co-moments over the frame rows where both columns are valid (groupby._final)
+            cy = a.arg2.eval(self.df)
+            if not isinstance(cy, C.NumericColumn):
+                raise TypeError(f"{a.fn} over a window needs numeric columns")
+            e = cy.data.to(torch.float64).to(lo.device)
+            both = ok & ~cy.null_mask().to(lo.device) & ~torch.isnan(e)
+            x, yv = torch.where(both, d, torch.zeros_like(d)), torch.where(both, e, torch.zeros_like(e))
+            nb = wsum(both.to(torch.float64))
+            n_ = nb.clamp(min=1)
+            sx, sy = wsum(x), wsum(yv)
+            cxy = wsum(x * yv) - sx * sy / n_
+            if a.fn == "covar_pop":
+                good = nb > 0
+                r = cxy / n_
+            elif a.fn == "covar_samp":
+                good = nb > 1
+                r = cxy / (nb - 1).clamp(min=1)
+            else:
+                cxx, cyy = wsum(x * x) - sx * sx / n_, wsum(yv * yv) - sy * sy / n_
+                good = (nb > 0) & (cxx > 0) & (cyy > 0)
+                r = cxy / torch.where(good, (cxx * cyy).sqrt(), torch.ones_like(cxx))
+            return self._dbl(torch.where(good, r, torch.zeros_like(r)), None if bool(good.all()) else good)
         if a.fn in ("stddev_pop", "var_pop", "skewness", "kurtosis"):
             # population moments from frame power sums (the group-by formulas, groupby._final)
             n_ = cnt.clamp(min=1)

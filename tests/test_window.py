@@ -192,3 +192,21 @@ def test_window_moment_and_host_aggregates(s):
         assert sorted(got.cs[i]) == sorted(set(part.tolist()))
         assert got.md[i] == pytest.approx(np.median(part))
         assert got.pr[i] == pytest.approx(np.prod(part))
+
+
+def test_sql_named_window_and_two_column_aggregates(s):
+    rows = [("a", 1.0, 0), ("a", 3.0, 1), ("b", 2.0, 2), ("a", 5.0, 3), ("a", 4.0, 7)]
+    df = s.createDataFrame(rows, ["g", "v", "id"])
+    df.createOrReplaceTempView("nw")
+    q = s.sql("SELECT id, SUM(v) OVER w AS f, row_number() OVER w2 AS r FROM nw "
+              "WINDOW w AS (PARTITION BY g ORDER BY id), w2 AS (ORDER BY v DESC) ORDER BY id").toPandas()
+    assert q.f.tolist() == [1.0, 4.0, 2.0, 9.0, 13.0] and q.r.tolist() == [5, 3, 4, 1, 2]
+    q = s.sql("SELECT id, corr(v, id) OVER (PARTITION BY g) AS c, covar_samp(v, id) OVER (PARTITION BY g "
+              "ORDER BY id) AS cs, count_if(v > 2) OVER (PARTITION BY g) AS ci, any_value(v) OVER "
+              "(PARTITION BY g ORDER BY id) AS av, approx_count_distinct(v) OVER (PARTITION BY g) AS d "
+              "FROM nw ORDER BY id").toPandas()
+    a = np.array([1.0, 3.0, 5.0, 4.0]), np.array([0.0, 1.0, 3.0, 7.0])
+    assert q.c[0] == pytest.approx(np.corrcoef(*a)[0, 1]) and np.isnan(q.c[2])   # one row in g=b
+    assert q.cs[1] == pytest.approx(1.0) and q.cs[4] == pytest.approx(np.cov(*a)[0, 1])
+    assert q.ci.tolist() == [3, 3, 0, 3, 3] and q.av.tolist() == [1.0, 1.0, 2.0, 1.0, 1.0]
+    assert q.d.tolist() == [4, 4, 1, 4, 4]
