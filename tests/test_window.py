@@ -210,3 +210,25 @@ def test_sql_named_window_and_two_column_aggregates(s):
     assert q.cs[1] == pytest.approx(1.0) and q.cs[4] == pytest.approx(np.cov(*a)[0, 1])
     assert q.ci.tolist() == [3, 3, 0, 3, 3] and q.av.tolist() == [1.0, 1.0, 2.0, 1.0, 1.0]
     assert q.d.tolist() == [4, 4, 1, 4, 4]
+
+
+def _range_and_moments(sess):
+    rng = np.random.default_rng(11)
+    n = 3000
+    pdf = pd.DataFrame({"g": rng.choice(["a", "b", "c"], n), "v": rng.integers(0, 200, n).astype(float),
+                        "id": np.arange(n)})
+    df = sess.createDataFrame(pdf)
+    w = Window.partitionBy("g").orderBy(F.col("v").desc()).rangeBetween(-7, 3)
+    w2 = Window.partitionBy("g").orderBy("id").rowsBetween(-20, 5)
+    return df.select("id", F.sum("v").over(w).alias("s"), F.max("v").over(w).alias("m"),
+                     F.count("*").over(w).alias("c"), F.skewness("v").over(w2).alias("sk"),
+                     F.corr("v", "id").over(w2).alias("co")).toPandas().sort_values("id").reset_index(drop=True)
+
+
+@pytest.mark.gpu
+def test_range_frames_and_moments_gpu_match_cpu(s):
+    a = _range_and_moments(s)
+    b = _range_and_moments(Session(SessionConf().set("o3s.device", "cuda")))
+    assert a.c.tolist() == b.c.tolist() and a.m.tolist() == b.m.tolist()
+    for k in ("s", "sk", "co"):
+        assert np.allclose(a[k].to_numpy(float), b[k].to_numpy(float), rtol=1e-9, atol=1e-9, equal_nan=True), k
