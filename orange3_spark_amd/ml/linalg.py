@@ -158,8 +158,65 @@ class DenseMatrix(Matrix):
     def __reduce__(self):
         return (DenseMatrix, (self.numRows, self.numCols, self.values.tolist(), self.isTransposed))
 
+    def toSparse(self) -> "SparseMatrix":
+        return SparseMatrix.from_array(self.toArray())
+
+    def __eq__(self, other):
+        return isinstance(other, Matrix) and np.array_equal(self.toArray(), other.toArray())
+
+
+class SparseMatrix(Matrix):
+    """Compressed sparse column matrix in Spark's layout (``colPtrs`` of length numCols+1,
+    ``rowIndices`` / ``values`` per stored entry; with ``isTransposed`` the arrays are CSR
+    of the matrix, i.e. CSC of its transpose -- pyspark.ml.linalg.SparseMatrix)."""
+
+    def __init__(self, numRows, numCols, colPtrs, rowIndices, values, isTransposed=False):
+        self.numRows, self.numCols = int(numRows), int(numCols)
+        self.colPtrs = np.asarray(colPtrs, dtype=np.int32).reshape(-1)
+        self.rowIndices = np.asarray(rowIndices, dtype=np.int32).reshape(-1)
+        self.values = np.asarray(values, dtype=np.float64).reshape(-1)
+        self.isTransposed = bool(isTransposed)
+        major = self.numRows if self.isTransposed else self.numCols
+        if self.colPtrs.size != major + 1:
+            raise ValueError(f"expected {major + 1} colPtrs, got {self.colPtrs.size}")
+        if self.rowIndices.size != self.values.size or self.colPtrs[-1] != self.values.size:
+            raise ValueError("rowIndices / values / colPtrs[-1] sizes differ")
+
+    @staticmethod
+    def from_array(a: np.ndarray) -> "SparseMatrix":
+        a = np.asarray(a, dtype=np.float64)
+        r, c = np.nonzero(a.T)                     # column-major order of the nonzeros
+        ptr = np.zeros(a.shape[1] + 1, dtype=np.int32)
+        np.add.at(ptr, r + 1, 1)
+        return SparseMatrix(a.shape[0], a.shape[1], np.cumsum(ptr), c, a.T[r, c])
+
+    def toArray(self):
+        minor = self.numCols if self.isTransposed else self.numRows
+        major = self.numRows if self.isTransposed else self.numCols
+        out = np.zeros((major, minor), dtype=np.float64)
+        seg = np.repeat(np.arange(major), np.diff(self.colPtrs))
+        out[seg, self.rowIndices] = self.values
+        return out if self.isTransposed else out.T
+
+    def toDense(self) -> DenseMatrix:
+        return DenseMatrix.from_array(self.toArray())
+
+    def __eq__(self, other):
+        return isinstance(other, Matrix) and np.array_equal(self.toArray(), other.toArray())
+
+    def __repr__(self):
+        return f"SparseMatrix({self.numRows}, {self.numCols}, nnz={self.values.size})"
+
+    def __reduce__(self):
+        return (SparseMatrix, (self.numRows, self.numCols, self.colPtrs.tolist(), self.rowIndices.tolist(),
+                               self.values.tolist(), self.isTransposed))
+
 
 class Matrices:
     @staticmethod
     def dense(numRows, numCols, values):
         return DenseMatrix(numRows, numCols, values)
+
+    @staticmethod
+    def sparse(numRows, numCols, colPtrs, rowIndices, values):
+        return SparseMatrix(numRows, numCols, colPtrs, rowIndices, values)

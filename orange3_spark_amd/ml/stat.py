@@ -16,6 +16,7 @@ from ..frame import column as C
 from ..frame.dataframe import DataFrame
 from . import common as U
 from .linalg import DenseMatrix, DenseVector
+from ._clustering_extra import MultivariateGaussian  # noqa: F401  (pyspark.ml.stat export)
 
 
 def chi_square_pvalues(comm, X: torch.Tensor, y: torch.Tensor, return_all=False):

@@ -65,11 +65,18 @@ def py_class(jvm: str) -> type:
 
 
 def _jsonable(v: Any):
-    from .linalg import DenseMatrix, Vector
+    from .linalg import Matrix, SparseVector, Vector
+    # Spark's JsonVectorConverter / JsonMatrixConverter forms
+    if isinstance(v, SparseVector):
+        return {"type": 0, "size": int(v.size), "indices": np.asarray(v.indices).tolist(),
+                "values": np.asarray(v.values).tolist()}
     if isinstance(v, Vector):
         return {"type": 1, "values": np.asarray(v.toArray()).tolist()}
-    if isinstance(v, DenseMatrix):
-        return {"numRows": v.numRows, "numCols": v.numCols, "values": v.values.tolist()}
+    if isinstance(v, Matrix):
+        d = matrix_struct(v)
+        if d["type"] == 1:
+            d.pop("colPtrs"), d.pop("rowIndices")
+        return {"class": "matrix", **d}
     if isinstance(v, (np.floating,)):
         return float(v)
     if isinstance(v, (np.integer,)):
@@ -162,11 +169,13 @@ def set_uid(instance, uid: str) -> None:
 
 
 def _from_json(instance, name, v):
-    from .linalg import DenseMatrix, DenseVector
-    if isinstance(v, dict) and "values" in v and "type" in v:
-        return DenseVector(v["values"])
+    from .linalg import DenseMatrix, DenseVector, SparseVector
     if isinstance(v, dict) and "numRows" in v:
-        return DenseMatrix(v["numRows"], v["numCols"], v["values"])
+        if v.get("type") == 0:
+            return matrix_from_struct(v)
+        return DenseMatrix(v["numRows"], v["numCols"], v["values"], v.get("isTransposed", False))
+    if isinstance(v, dict) and "values" in v and "type" in v:
+        return SparseVector(v["size"], v["indices"], v["values"]) if v["type"] == 0 else DenseVector(v["values"])
     return v
 
 
@@ -274,8 +283,12 @@ def matrix_arrow_type():
 
 
 def matrix_struct(m) -> dict:
-    """Dense matrix in Spark MatrixUDT form (type 1 = dense, column-major values)."""
-    from .linalg import DenseMatrix
+    """Matrix in Spark MatrixUDT form (type 1 = dense, column-major values; type 0 =
+    sparse CSC with colPtrs / rowIndices)."""
+    from .linalg import DenseMatrix, SparseMatrix
+    if isinstance(m, SparseMatrix):
+        return {"type": 0, "numRows": m.numRows, "numCols": m.numCols, "colPtrs": m.colPtrs.tolist(),
+                "rowIndices": m.rowIndices.tolist(), "values": m.values.tolist(), "isTransposed": m.isTransposed}
     if not isinstance(m, DenseMatrix):
         m = DenseMatrix.from_array(np.asarray(m))
     return {"type": 1, "numRows": m.numRows, "numCols": m.numCols, "colPtrs": None, "rowIndices": None,
@@ -283,7 +296,9 @@ def matrix_struct(m) -> dict:
 
 
 def matrix_from_struct(s):
-    from .linalg import DenseMatrix
+    from .linalg import DenseMatrix, SparseMatrix
+    if s["type"] == 0:
+        return SparseMatrix(s["numRows"], s["numCols"], s["colPtrs"], s["rowIndices"], s["values"], s["isTransposed"])
     return DenseMatrix(s["numRows"], s["numCols"], s["values"], s["isTransposed"])
 
 
