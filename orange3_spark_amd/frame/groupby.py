@@ -196,7 +196,8 @@ def aggregate(df, keys: list, aggs: list):
             continue
         if a.distinct or a.fn in ("collect_list", "collect_set", "first", "last", "percentile", "median", "mode",
                                   "percentile_exact",
-                                  "product", "bool_and", "bool_or", "max_by", "min_by") or \
+                                  "product", "bool_and", "bool_or", "max_by", "min_by", "bit_and", "bit_or",
+                                  "bit_xor") or \
                 not isinstance(vals, C.NumericColumn):
             # host path: (group, value) pairs or per-group python reductions
             py = vals.to_pylist() if not isinstance(vals, C.HostColumn) else list(vals.values)
@@ -379,6 +380,11 @@ def _host_final(a, pairs):
         for v in nn:
             out *= float(v)
         return out
+    if a.fn in ("bit_and", "bit_or", "bit_xor"):
+        import functools
+        import operator
+        op = {"bit_and": operator.and_, "bit_or": operator.or_, "bit_xor": operator.xor}[a.fn]
+        return functools.reduce(op, (int(v) for v in nn))
     if a.fn == "bool_and":
         return all(bool(v) for v in nn)
     if a.fn == "bool_or":
@@ -412,6 +418,9 @@ def _host_final(a, pairs):
 
 
 def _result_column(a, res):
+    if a.fn in ("bit_and", "bit_or", "bit_xor"):
+        valid = torch.tensor([r is not None for r in res]) if any(r is None for r in res) else None
+        return C.NumericColumn(torch.tensor([0 if r is None else r for r in res], dtype=torch.int64), valid)
     if a.fn == "count":
         return C.NumericColumn(torch.tensor(res, dtype=torch.int64))
     if a.fn in ("collect_list", "collect_set") or (a.fn in ("percentile", "percentile_exact")

@@ -1648,3 +1648,138 @@ def min_by(c, ord_):
 
 def first_value(c, ignoreNulls=False): return first(c, ignoreNulls)
 def last_value(c, ignoreNulls=False): return last(c, ignoreNulls)
+
+
+# ---------------------------------------------------------------- Spark 3.4 / 3.5 additions
+def array_agg(c): return Agg("collect_list", _e(c), f"array_agg({_e(c).name})")
+def bit_and(c): return Agg("bit_and", _e(c), f"bit_and({_e(c).name})")
+def bit_or(c): return Agg("bit_or", _e(c), f"bit_or({_e(c).name})")
+def bit_xor(c): return Agg("bit_xor", _e(c), f"bit_xor({_e(c).name})")
+
+
+def bit_count(c):
+    """Set bits of the 64-bit two's-complement value (Spark BitwiseCount)."""
+    return _host_map("bit_count", lambda v: builtins.bin(int(v) & 0xFFFFFFFFFFFFFFFF).count("1"), c, kind="int")
+
+
+date_diff = datediff
+day = dayofmonth
+
+
+def weekday(c): return _date_map("weekday", lambda s: s.dt.dayofweek.astype("float"), c)   # Monday = 0
+
+
+def date_from_unix_date(c):
+    import datetime as _dt
+    return _host_map("date_from_unix_date",
+                     lambda v: (_dt.date(1970, 1, 1) + _dt.timedelta(days=int(v))).isoformat(), c)
+
+
+def make_timestamp(years, months, days, hours, mins, secs):
+    import datetime as _dt
+
+    def mk(y, mo, d, h, mi, s):
+        s = float(s)
+        t = _dt.datetime(int(y), int(mo), int(d), int(h), int(mi), int(s), int(builtins.round((s % 1) * 1e6)))
+        return t.strftime("%Y-%m-%d %H:%M:%S") + (f".{t.microsecond:06d}".rstrip("0") if t.microsecond else "")
+    return _host_map("make_timestamp", mk, years, months, days, hours, mins, secs)
+
+
+def get(c, index):
+    """0-based array element, null when out of range (Spark 3.4 ``get``)."""
+    idx = index if isinstance(index, (E.Expr, str)) else E.lit(int(index))
+    return _host_map("get", lambda v, i: v[int(i)] if 0 <= int(i) < len(v) else None, c, idx, kind="str")
+
+
+def json_array_length(c):
+    def f(s):
+        try:
+            v = _json.loads(str(s))
+        except ValueError:
+            return None
+        return len(v) if isinstance(v, list) else None
+    return _host_map("json_array_length", f, c, kind="int")
+
+
+def json_object_keys(c):
+    def f(s):
+        try:
+            v = _json.loads(str(s))
+        except ValueError:
+            return None
+        return list(v.keys()) if isinstance(v, dict) else None
+    return _host_map("json_object_keys", f, c, kind="array")
+
+
+def map_contains_key(c, key):
+    k = key if isinstance(key, E.Expr) else E.lit(key)
+    return _host_map("map_contains_key", lambda m, kk: kk in m, c, k, kind="bool")
+
+
+def named_struct(*cols):
+    """named_struct(lit(name1), col1, lit(name2), col2, ...)."""
+    if len(cols) % 2:
+        raise ValueError("named_struct expects name, value pairs")
+    names = [n.eval_literal() if hasattr(n, "eval_literal") else str(n) for n in cols[::2]]
+    return struct(*[_e(v).alias(k) for k, v in zip(names, cols[1::2])])
+
+
+def negate(c): return -_e(c)
+
+
+def position(substr, c, start=None):
+    """1-based position of ``substr`` in ``c`` at or after ``start`` (0 when absent)."""
+    st = start if start is not None else E.lit(1)
+    return _host_map("position", lambda sub, s, p: str(s).find(str(sub), builtins.max(int(p) - 1, 0)) + 1,
+                     substr if isinstance(substr, E.Expr) else E.lit(substr), c,
+                     st if isinstance(st, E.Expr) else E.lit(int(st)), kind="int")
+
+
+def regexp_count(c, regexp):
+    return _host_map("regexp_count", lambda s, p: len(re.findall(str(p), str(s))), c,
+                     regexp if isinstance(regexp, E.Expr) else E.lit(regexp), kind="int")
+
+
+def regexp_substr(c, regexp):
+    def f(s, p):
+        m = re.search(str(p), str(s))
+        return m.group(0) if m else None
+    return _host_map("regexp_substr", f, c, regexp if isinstance(regexp, E.Expr) else E.lit(regexp))
+
+
+def replace(src, search, replace=None):  # noqa: A002
+    rep = E.lit("") if replace is None else (replace if isinstance(replace, E.Expr) else E.lit(replace))
+    return _host_map("replace", lambda s, a, b: str(s).replace(str(a), str(b)), src,
+                     search if isinstance(search, E.Expr) else E.lit(search), rep)
+
+
+def substr(c, pos, length_=None):
+    """substr(str, pos[, len]) with column or literal arguments (1-based, like substring)."""
+    p = pos if isinstance(pos, E.Expr) else E.lit(int(pos))
+    n = E.lit(1 << 30) if length_ is None else (length_ if isinstance(length_, E.Expr) else E.lit(int(length_)))
+
+    def f(s, a, b):
+        s, a, b = str(s), int(a), int(b)
+        start = a - 1 if a > 0 else (len(s) + a if a < 0 else 0)
+        lo = builtins.max(start, 0)
+        return s[lo:builtins.max(lo, start + b)] if b > 0 else ""
+    return _host_map("substr", f, c, p, n)
+
+
+def try_subtract(a, b): return _e(a) - _e(b)
+def try_multiply(a, b): return _e(a) * _e(b)
+
+
+def url_encode(c):
+    from urllib.parse import quote_plus
+    return _host_map("url_encode", lambda s: quote_plus(str(s)), c)
+
+
+def url_decode(c):
+    from urllib.parse import unquote_plus
+    return _host_map("url_decode", lambda s: unquote_plus(str(s)), c)
+
+
+def uuid():
+    import uuid as _uuid
+    return Expr(lambda df: _str_out([str(_uuid.uuid4()) for _ in range(len(df))]), "uuid()")

@@ -153,7 +153,8 @@ class AggCall:
 _EXTRA_AGGS = {"first", "last", "collect_list", "collect_set", "stddev_pop", "var_pop", "skewness",
                "kurtosis", "approx_count_distinct", "corr", "covar_pop", "covar_samp", "percentile_approx",
                "percentile", "grouping", "grouping_id", "median", "mode", "product", "count_if", "bool_and",
-               "bool_or", "every", "some", "any_value", "max_by", "min_by"}
+               "bool_or", "every", "some", "any_value", "max_by", "min_by", "bit_and", "bit_or", "bit_xor",
+               "array_agg"}
 _TWO_COLUMN_AGGS = {"corr", "covar_pop", "covar_samp", "max_by", "min_by"}
 
 

@@ -1,0 +1,58 @@
+"""Spark 3.4 / 3.5 sql.functions additions (DataFrame API and SQL), checked against values
+worked out by hand from Spark's documented semantics."""
+import pytest
+
+from orange3_spark_amd import Session, SessionConf
+from orange3_spark_amd.sql import functions as F
+
+
+@pytest.fixture(scope="module")
+def df():
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    d = s.createDataFrame([("a", 5, "x y&z", "[1,2,3]", '{"k":1,"j":2}', "2024-03-06"),
+                           ("a", 3, "abc123def45", "[]", "{}", "2024-03-09"),
+                           ("b", 6, "q", "x", "[1]", "2024-03-10")], ["g", "v", "s", "ja", "jo", "d"])
+    d.createOrReplaceTempView("f35")
+    return d
+
+
+def test_bit_aggregates_and_array_agg(df):
+    r = df.groupBy("g").agg(F.bit_and("v").alias("ba"), F.bit_or("v").alias("bo"), F.bit_xor("v").alias("bx"),
+                            F.array_agg("v").alias("aa")).orderBy("g").toPandas()
+    assert r.ba.tolist() == [1, 6] and r.bo.tolist() == [7, 6] and r.bx.tolist() == [6, 6]
+    assert r.aa.tolist() == [[5, 3], [6]]
+    q = df.sparkSession.sql("SELECT g, bit_xor(v) AS x FROM f35 GROUP BY g ORDER BY g").toPandas() \
+        if hasattr(df, "sparkSession") else None
+    if q is not None:
+        assert q.x.tolist() == [6, 6]
+
+
+def test_scalar_additions(df):
+    r = df.select(F.bit_count("v").alias("bc"), F.weekday("d").alias("wd"), F.day("d").alias("dy"),
+                  F.date_from_unix_date(F.lit(19000)).alias("du"), F.json_array_length("ja").alias("jl"),
+                  F.json_object_keys("jo").alias("jk"), F.regexp_count("s", F.lit(r"\d+")).alias("rc"),
+                  F.regexp_substr("s", F.lit(r"\d+")).alias("rs"),
+                  F.replace("s", F.lit("abc"), F.lit("Z")).alias("rp"), F.substr("s", F.lit(2), F.lit(3)).alias("ss"),
+                  F.url_encode("s").alias("ue"), F.url_decode(F.url_encode("s")).alias("ud"),
+                  F.position(F.lit("c"), "s").alias("po"), F.negate("v").alias("ng"),
+                  F.try_multiply("v", F.lit(2)).alias("tm"), F.try_subtract("v", F.lit(1)).alias("ts"),
+                  F.make_timestamp(F.lit(2024), F.lit(1), F.lit(2), F.lit(3), F.lit(4), F.lit(5.5)).alias("mt"),
+                  F.map_contains_key(F.create_map(F.lit("k"), "v"), "k").alias("mk"),
+                  F.named_struct(F.lit("a"), "v").alias("ns"), F.uuid().alias("u")).toPandas()
+    assert r.bc.tolist() == [2, 2, 2] and r.wd.tolist() == [2, 5, 6] and r.dy.tolist() == [6, 9, 10]
+    assert r.du.tolist() == ["2022-01-08"] * 3
+    assert r.jl.tolist()[:2] == [3, 0] and r.jl.isna().tolist()[2]
+    assert r.jk.tolist()[:2] == [["k", "j"], []]
+    assert r.rc.tolist() == [0, 2, 0] and r.rs.tolist() == [None, "123", None]
+    assert r.rp.tolist() == ["x y&z", "Z123def45", "q"] and r.ss.tolist() == [" y&", "bc1", ""]
+    assert r.ue.tolist()[0] == "x+y%26z" and r.ud.tolist() == ["x y&z", "abc123def45", "q"]
+    assert r.po.tolist() == [0, 3, 0] and r.ng.tolist() == [-5, -3, -6]
+    assert r.tm.tolist() == [10, 6, 12] and r.ts.tolist() == [4, 2, 5]
+    assert r.mt.tolist()[0] == "2024-01-02 03:04:05.5" and r.mk.tolist() == [True] * 3
+    assert [x.a for x in r.ns.tolist()] == [5, 3, 6] and len(set(r.u.tolist())) == 3
+
+
+def test_sql_spellings(df):
+    s = Session.getOrCreate() if not hasattr(df, "sparkSession") else df.sparkSession
+    q = s.sql("SELECT regexp_count(s, '[a-z]') AS c, url_encode(s) AS u, weekday(d) AS w FROM f35").toPandas()
+    assert q.c.tolist() == [3, 6, 1] and q.w.tolist() == [2, 5, 6]
