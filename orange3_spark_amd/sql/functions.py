@@ -754,7 +754,7 @@ def from_json(c, schema, options=None):
     """JSON text -> struct (a Row of the schema's fields) or, without field info, a dict."""
     from ..frame.dataframe import Row
     try:
-        st = T.parse_type(schema) if isinstance(schema, str) else schema
+        st = _ddl_schema(schema)
         names = [f.name for f in st.fields]
     except Exception:  # noqa: BLE001 - schema forms the type parser does not know: keep dicts
         names = None
@@ -1783,3 +1783,68 @@ def url_decode(c):
 def uuid():
     import uuid as _uuid
     return Expr(lambda df: _str_out([str(_uuid.uuid4()) for _ in range(len(df))]), "uuid()")
+
+
+def _csv_cast(v, dt):
+    if v == "":
+        return None
+    name = dt.simpleString() if hasattr(dt, "simpleString") else str(dt)
+    try:
+        if name in ("int", "bigint", "smallint", "tinyint"):
+            return int(v)
+        if name in ("double", "float") or name.startswith("decimal"):
+            return float(v)
+        if name == "boolean":
+            return {"true": True, "false": False}.get(v.strip().lower())
+    except ValueError:
+        return None                      # PERMISSIVE mode: a malformed field becomes null
+    return v
+
+
+def _ddl_schema(schema) -> T.StructType:
+    """StructType, DDL string ("a INT, b STRING") or STRUCT<...> string -> StructType."""
+    if isinstance(schema, T.StructType):
+        return schema
+    text = (schema.eval_literal() if hasattr(schema, "eval_literal") else str(schema)).strip()
+    if text.lower().startswith("struct<") and text.endswith(">"):
+        text = text[7:-1]
+    return T.parse_schema(text)
+
+
+def from_csv(c, schema, options=None):
+    """CSV text -> struct of the DDL schema's fields (Spark ``from_csv``; options ``sep``)."""
+    import csv as _csv
+    from ..frame.dataframe import Row
+    st = _ddl_schema(schema)
+    sep = (options or {}).get("sep", (options or {}).get("delimiter", ","))
+    names, types = [f.name for f in st.fields], [f.dataType for f in st.fields]
+
+    def fc(s):
+        vals = next(_csv.reader([str(s)], delimiter=sep), [])
+        vals = (vals + [""] * len(names))[:len(names)]
+        return Row._make(names, [_csv_cast(v, t) for v, t in zip(vals, types)])
+    return _host_map("from_csv", fc, c, kind="array")
+
+
+def schema_of_csv(csv, options=None):
+    """DDL of a CSV sample (Spark ``schema_of_csv``: columns _c0, _c1, ... with inferred types)."""
+    import csv as _csv
+    text = csv.eval_literal() if hasattr(csv, "eval_literal") else str(csv)
+    sep = (options or {}).get("sep", ",")
+    vals = next(_csv.reader([text], delimiter=sep), [])
+
+    def typ(v):
+        for t, f in (("INT", int), ("DOUBLE", float)):
+            try:
+                f(v)
+                return t
+            except ValueError:
+                pass
+        return "BOOLEAN" if v.lower() in ("true", "false") else "STRING"
+    ddl = "STRUCT<" + ", ".join(f"_c{i}: {typ(v)}" for i, v in enumerate(vals)) + ">"
+    return E.lit(ddl)
+
+
+def years(c):
+    """Partition transform years(ts) (writeTo().partitionedBy); evaluates to the year."""
+    return year(c)

@@ -56,3 +56,14 @@ def test_sql_spellings(df):
     s = Session.getOrCreate() if not hasattr(df, "sparkSession") else df.sparkSession
     q = s.sql("SELECT regexp_count(s, '[a-z]') AS c, url_encode(s) AS u, weekday(d) AS w FROM f35").toPandas()
     assert q.c.tolist() == [3, 6, 1] and q.w.tolist() == [2, 5, 6]
+
+
+def test_from_csv_and_schema_of_csv():
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    d = s.createDataFrame([("1,abc,2.5", '{"a": 3, "b": "z"}'), ("7,,x", "{}")], ["t", "j"])
+    r = d.select(F.from_csv("t", "a INT, b STRING, c DOUBLE").alias("r"),
+                 F.from_json("j", "STRUCT<a: INT, b: STRING>").alias("q")).toPandas()
+    assert [(x.a, x.b, x.c) for x in r.r] == [(1, "abc", 2.5), (7, None, None)]   # malformed field -> null
+    assert [(x.a, x.b) for x in r.q] == [(3, "z"), (None, None)]
+    ddl = d.select(F.schema_of_csv(F.lit("1,abc,2.5")).alias("x")).toPandas().x[0]
+    assert ddl == "STRUCT<_c0: INT, _c1: STRING, _c2: DOUBLE>"
