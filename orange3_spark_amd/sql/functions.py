@@ -1459,9 +1459,17 @@ def _run_lambda(df, f, params: dict, owner: np.ndarray, outer_refs):
     import pandas as pd
     from ..frame.dataframe import DataFrame
     n_el = len(owner)
-    data = {f"__lp{i}": pd.Series(v, dtype=object) if any(isinstance(x, (list, dict, str)) or x is None
-                                                            for x in v) else pd.Series(v)
-            for i, v in enumerate(params.values())}
+    def series(v):
+        nn = [x for x in v if x is not None]
+        if any(isinstance(x, (list, dict, str, bytes)) for x in nn) or not nn:
+            return pd.Series(v, dtype=object)
+        if len(nn) == len(v):
+            return pd.Series(v)
+        # numeric with nulls: nullable column (null-aware coalesce / isNull in the body)
+        if all(isinstance(x, (int, np.integer)) and not isinstance(x, bool) for x in nn):
+            return pd.Series(pd.array(v, dtype="Int64"))
+        return pd.Series(pd.array(v, dtype="Float64"))
+    data = {f"__lp{i}": series(v) for i, v in enumerate(params.values())}
     local = df.session.local_view()
     body = f(*[col(f"__lp{i}") for i in range(len(params))])
     body = _e(body)
@@ -1848,3 +1856,32 @@ def schema_of_csv(csv, options=None):
 def years(c):
     """Partition transform years(ts) (writeTo().partitionedBy); evaluates to the year."""
     return year(c)
+
+
+def map_zip_with(col1, col2, f):
+    """Merge two maps key-wise with ``f(k, v1, v2)`` over the union of their keys (a key
+    missing from one side passes null for that side)."""
+    e1, e2 = _e(col1), _e(col2)
+
+    def ev(df):
+        n = len(df)
+        a, b = _host(e1.eval(df), n), _host(e2.eval(df), n)
+        owner, ks, v1, v2 = [], [], [], []
+        for r, (x, y) in enumerate(zip(a, b)):
+            if x is None or y is None:
+                continue
+            for k in list(x.keys()) + [k for k in y.keys() if k not in x]:
+                owner.append(r)
+                ks.append(k)
+                v1.append(x.get(k))
+                v2.append(y.get(k))
+        owner = np.asarray(owner, dtype=np.int64)
+        res = _run_lambda(df, f, {"k": ks, "v1": v1, "v2": v2}, owner, ()) if len(owner) else []
+        per = [dict() for _ in range(n)]
+        for o, k, y in zip(owner.tolist(), ks, res):
+            per[o][k] = y
+        arr = np.empty(n, dtype=object)
+        for r in range(n):
+            arr[r] = None if a[r] is None or b[r] is None else per[r]
+        return C.ArrayColumn(arr)
+    return Expr(ev, f"map_zip_with({e1.name}, {e2.name}, lambdafunction)", _refs(e1, e2))

@@ -67,3 +67,13 @@ def test_from_csv_and_schema_of_csv():
     assert [(x.a, x.b) for x in r.q] == [(3, "z"), (None, None)]
     ddl = d.select(F.schema_of_csv(F.lit("1,abc,2.5")).alias("x")).toPandas().x[0]
     assert ddl == "STRUCT<_c0: INT, _c1: STRING, _c2: DOUBLE>"
+
+
+def test_map_zip_with():
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    d = s.createDataFrame([(1,)], ["id"]).select(
+        F.create_map(F.lit("a"), F.lit(1), F.lit("b"), F.lit(2)).alias("m1"),
+        F.create_map(F.lit("b"), F.lit(10), F.lit("c"), F.lit(20)).alias("m2"))
+    r = d.select(F.map_zip_with("m1", "m2", lambda k, v1, v2: F.coalesce(v1, F.lit(0)) + F.coalesce(v2, F.lit(0)))
+                 .alias("z")).toPandas().z[0]
+    assert {k: int(v) for k, v in r.items()} == {"a": 1, "b": 12, "c": 20}
