@@ -197,7 +197,7 @@ def aggregate(df, keys: list, aggs: list):
         if a.distinct or a.fn in ("collect_list", "collect_set", "first", "last", "percentile", "median", "mode",
                                   "percentile_exact",
                                   "product", "bool_and", "bool_or", "max_by", "min_by", "bit_and", "bit_or",
-                                  "bit_xor") or \
+                                  "bit_xor", "histogram_numeric") or \
                 not isinstance(vals, C.NumericColumn):
             # host path: (group, value) pairs or per-group python reductions
             py = vals.to_pylist() if not isinstance(vals, C.HostColumn) else list(vals.values)
@@ -380,6 +380,8 @@ def _host_final(a, pairs):
         for v in nn:
             out *= float(v)
         return out
+    if a.fn == "histogram_numeric":
+        return _numeric_histogram(nn, int(a.param))
     if a.fn in ("bit_and", "bit_or", "bit_xor"):
         import functools
         import operator
@@ -417,13 +419,30 @@ def _host_final(a, pairs):
     raise TypeError(f"aggregate {a.fn} not supported on this column type")
 
 
+def _numeric_histogram(vals, nb):
+    """Ben-Haim / Tom-Tov histogram (Spark ``histogram_numeric``): every distinct value a
+    (centre, count) bin, then the two closest adjacent bins merged into their weighted
+    centre until ``nb`` remain.  Returns [Row(x, y)] sorted by x."""
+    from .dataframe import Row
+    if not vals:
+        return None
+    xs, cnt = np.unique(np.asarray(vals, dtype=np.float64), return_counts=True)
+    xs, cnt = xs.tolist(), cnt.astype(np.float64).tolist()
+    while len(xs) > max(nb, 1):
+        i = int(np.argmin(np.diff(xs)))
+        w = cnt[i] + cnt[i + 1]
+        xs[i:i + 2] = [(xs[i] * cnt[i] + xs[i + 1] * cnt[i + 1]) / w]
+        cnt[i:i + 2] = [w]
+    return [Row._make(["x", "y"], [x, y]) for x, y in zip(xs, cnt)]
+
+
 def _result_column(a, res):
     if a.fn in ("bit_and", "bit_or", "bit_xor"):
         valid = torch.tensor([r is not None for r in res]) if any(r is None for r in res) else None
         return C.NumericColumn(torch.tensor([0 if r is None else r for r in res], dtype=torch.int64), valid)
     if a.fn == "count":
         return C.NumericColumn(torch.tensor(res, dtype=torch.int64))
-    if a.fn in ("collect_list", "collect_set") or (a.fn in ("percentile", "percentile_exact")
+    if a.fn in ("collect_list", "collect_set", "histogram_numeric") or (a.fn in ("percentile", "percentile_exact")
                                                     and isinstance(a.param, (list, tuple))):
         arr = np.empty(len(res), dtype=object)
         for i, r in enumerate(res):        # element-wise: equal-length lists must not broadcast

@@ -1885,3 +1885,11 @@ def map_zip_with(col1, col2, f):
             arr[r] = None if a[r] is None or b[r] is None else per[r]
         return C.ArrayColumn(arr)
     return Expr(ev, f"map_zip_with({e1.name}, {e2.name}, lambdafunction)", _refs(e1, e2))
+
+
+def histogram_numeric(c, nBins):
+    """Approximate histogram as an array of (x, y) = (bin centre, count) structs."""
+    n = nBins.eval_literal() if hasattr(nBins, "eval_literal") else int(nBins)
+    a = Agg("histogram_numeric", _e(c), f"histogram_numeric({_e(c).name}, {n})")
+    a.param = int(n)
+    return a

@@ -154,7 +154,7 @@ _EXTRA_AGGS = {"first", "last", "collect_list", "collect_set", "stddev_pop", "va
                "kurtosis", "approx_count_distinct", "corr", "covar_pop", "covar_samp", "percentile_approx",
                "percentile", "grouping", "grouping_id", "median", "mode", "product", "count_if", "bool_and",
                "bool_or", "every", "some", "any_value", "max_by", "min_by", "bit_and", "bit_or", "bit_xor",
-               "array_agg"}
+               "array_agg", "histogram_numeric"}
 _TWO_COLUMN_AGGS = {"corr", "covar_pop", "covar_samp", "max_by", "min_by"}
 
 

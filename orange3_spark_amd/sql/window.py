@@ -38,7 +38,8 @@ _PREFIX = "__win:"
 
 # aggregates evaluated per frame by the group-by finaliser (host): no prefix-sum form
 _HOST_FRAME_AGGS = ("collect_set", "median", "mode", "product", "bool_and", "bool_or", "percentile",
-                    "percentile_exact", "max_by", "min_by", "bit_and", "bit_or", "bit_xor")
+                    "percentile_exact", "max_by", "min_by", "bit_and", "bit_or", "bit_xor",
+                    "histogram_numeric")
 
 unboundedPreceding = -(1 << 62)
 unboundedFollowing = 1 << 62

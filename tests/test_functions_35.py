@@ -77,3 +77,13 @@ def test_map_zip_with():
     r = d.select(F.map_zip_with("m1", "m2", lambda k, v1, v2: F.coalesce(v1, F.lit(0)) + F.coalesce(v2, F.lit(0)))
                  .alias("z")).toPandas().z[0]
     assert {k: int(v) for k, v in r.items()} == {"a": 1, "b": 12, "c": 20}
+
+
+def test_histogram_numeric():
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    d = s.createDataFrame([("a", float(v)) for v in [1, 2, 2, 3, 10, 11, 12, 30]], ["g", "v"])
+    h = d.groupBy("g").agg(F.histogram_numeric("v", 3).alias("h")).toPandas().h[0]
+    assert [(r.x, r.y) for r in h] == [(2.0, 4.0), (11.0, 3.0), (30.0, 1.0)]   # counts sum to the rows
+    d.createOrReplaceTempView("hn35")
+    h2 = s.sql("SELECT histogram_numeric(v, 2) AS h FROM hn35").toPandas().h[0]
+    assert [r.y for r in h2] == [7.0, 1.0] and h2[0].x == pytest.approx(41 / 7)
