@@ -1893,3 +1893,172 @@ def histogram_numeric(c, nBins):
     a = Agg("histogram_numeric", _e(c), f"histogram_numeric({_e(c).name}, {n})")
     a.param = int(n)
     return a
+
+
+# ---------------------------------------------------------------- aliases and small built-ins
+try_sum = sum
+try_avg = avg
+sha = sha1
+to_timestamp_ltz = to_timestamp
+to_timestamp_ntz = to_timestamp
+try_to_timestamp = to_timestamp
+localtimestamp = current_timestamp
+dateadd = date_add
+
+
+def printf(format, *cols):  # noqa: A002
+    fmt = format.eval_literal() if hasattr(format, "eval_literal") else format
+    return format_string(fmt, *cols)
+
+
+def _epoch(name, scale, c):
+    import pandas as pd
+
+    def f(v):
+        t = pd.Timestamp(str(v))
+        t = t.tz_convert("UTC").tz_localize(None) if t.tzinfo is not None else t
+        return int(t.value // scale)
+    return _host_map(name, f, c, kind="int")
+
+
+def unix_date(c): return _epoch("unix_date", 86_400 * 10 ** 9, c)
+def unix_seconds(c): return _epoch("unix_seconds", 10 ** 9, c)
+def unix_millis(c): return _epoch("unix_millis", 10 ** 6, c)
+def unix_micros(c): return _epoch("unix_micros", 10 ** 3, c)
+
+
+def to_unix_timestamp(c, format=None):  # noqa: A002
+    return unix_timestamp(c) if format is None else \
+        unix_timestamp(c, format.eval_literal() if hasattr(format, "eval_literal") else format)
+
+
+def _from_epoch(name, per_second, c):
+    import datetime as _dt
+
+    def f(v):
+        t = _dt.datetime(1970, 1, 1) + _dt.timedelta(microseconds=int(v) * (10 ** 6 // per_second))
+        return t.strftime("%Y-%m-%d %H:%M:%S") + (f".{t.microsecond:06d}".rstrip("0") if t.microsecond else "")
+    return _host_map(name, f, c)
+
+
+def timestamp_millis(c): return _from_epoch("timestamp_millis", 1000, c)
+def timestamp_micros(c): return _from_epoch("timestamp_micros", 10 ** 6, c)
+
+
+def date_part(field, source):
+    """date_part('YEAR' | 'MONTH' | 'DAY' | 'HOUR' | 'MINUTE' | 'SECOND' | 'QUARTER' | 'WEEK' |
+    'DAYOFWEEK' | 'DOY', source)."""
+    f = (field.eval_literal() if hasattr(field, "eval_literal") else str(field)).strip().upper()
+    table = {"YEAR": year, "YEARS": year, "Y": year, "MONTH": month, "MON": month, "MONTHS": month,
+             "DAY": dayofmonth, "D": dayofmonth, "DAYS": dayofmonth, "HOUR": hour, "H": hour, "HOURS": hour,
+             "MINUTE": minute, "MIN": minute, "MINUTES": minute, "SECOND": second, "S": second, "SEC": second,
+             "SECONDS": second, "QUARTER": quarter, "QTR": quarter, "WEEK": weekofyear, "W": weekofyear,
+             "WEEKS": weekofyear, "DAYOFWEEK": dayofweek, "DOW": dayofweek, "DOY": dayofyear}
+    if f not in table:
+        raise ValueError(f"date_part: unsupported field {f!r}")
+    return table[f](source)
+
+
+datepart = date_part
+extract = date_part
+
+
+def convert_timezone(sourceTz, targetTz, sourceTs=None):
+    """convert_timezone([sourceTz, ]targetTz, sourceTs): wall clock in sourceTz -> targetTz."""
+    import pandas as pd
+    if sourceTs is None:
+        sourceTz, targetTz, sourceTs = E.lit("UTC"), sourceTz, targetTz
+
+    def cv(v, a, b):
+        t = pd.Timestamp(str(v))
+        t = t.tz_localize(str(a)) if t.tzinfo is None else t
+        return t.tz_convert(str(b)).tz_localize(None).strftime("%Y-%m-%d %H:%M:%S")
+    return _host_map("convert_timezone", cv, sourceTs, sourceTz, targetTz)
+
+
+def _const(name, value):
+    return Expr(lambda df: _str_out([value] * len(df)), f"{name}()")
+
+
+def current_timezone(): return _const("current_timezone", "UTC")
+def current_user(): return _const("current_user", __import__("getpass").getuser())
+def user(): return current_user()
+def current_catalog(): return _const("current_catalog", "spark_catalog")
+def current_database(): return _const("current_database", "default")
+def current_schema(): return current_database()
+def version(): return _const("version", "3.5.0 orange3-spark-amd")
+
+
+def mask(c, upperChar=None, lowerChar=None, digitChar=None, otherChar=None):
+    """Spark mask(): upper -> 'X', lower -> 'x', digits -> 'n', others kept (or otherChar)."""
+    lit_of = lambda v, d: d if v is None else (v.eval_literal() if hasattr(v, "eval_literal") else v)  # noqa: E731
+    up, lo, dg, ot = lit_of(upperChar, "X"), lit_of(lowerChar, "x"), lit_of(digitChar, "n"), lit_of(otherChar, None)
+
+    def m(s):
+        out = []
+        for ch in str(s):
+            if ch.isupper():
+                out.append(ch if up is None else up)
+            elif ch.islower():
+                out.append(ch if lo is None else lo)
+            elif ch.isdigit():
+                out.append(ch if dg is None else dg)
+            else:
+                out.append(ch if ot is None else ot)
+        return "".join(out)
+    return _host_map("mask", m, c)
+
+
+def find_in_set(str, str_array):  # noqa: A002
+    """1-based index of ``str`` in the comma-separated ``str_array`` (0 if absent or if str has a comma)."""
+    def f(s, arr):
+        s = builtins.str(s)
+        if "," in s:
+            return 0
+        parts = builtins.str(arr).split(",")
+        return parts.index(s) + 1 if s in parts else 0
+    return _host_map("find_in_set", f, str, str_array, kind="int")
+
+
+def elt(*inputs):
+    """elt(n, in1, in2, ...): the n-th input (1-based), null when out of range."""
+    es = [_e(a) for a in inputs]
+
+    def f(df):
+        n = len(df)
+        cols = [_host(e.eval(df), n) for e in es]
+        out = []
+        for r in range(n):
+            k = cols[0][r]
+            out.append(cols[int(k)][r] if k is not None and 1 <= int(k) < len(cols) else None)
+        return _str_out([None if v is None else builtins.str(v) for v in out])
+    return Expr(f, f"elt({', '.join(e.name for e in es)})", _refs(*es))
+
+
+def chr(c):  # noqa: A001
+    """Character of code point n mod 256 (Spark chr / char); '' for negative n."""
+    return _host_map("chr", lambda v: "" if int(v) < 0 else builtins.chr(int(v) % 256), c)
+
+
+char = chr
+
+
+def shiftrightunsigned(c, numBits: int):
+    return _host_map("shiftrightunsigned", lambda v: (int(v) & 0xFFFFFFFFFFFFFFFF) >> int(numBits), c, kind="int")
+
+
+def to_binary(c, format=None):  # noqa: A002
+    """to_binary(str[, 'hex' | 'utf-8' | 'base64']) -> bytes."""
+    fmt = "hex" if format is None else (format.eval_literal() if hasattr(format, "eval_literal") else format).lower()
+
+    def f(s):
+        s = builtins.str(s)
+        try:
+            if fmt == "hex":
+                return _binascii.unhexlify(s if len(s) % 2 == 0 else "0" + s)
+            if fmt == "base64":
+                return _b64.b64decode(s)
+            return s.encode("utf-8")
+        except (ValueError, _binascii.Error):
+            return None
+    return _host_map("to_binary", f, c, kind="array")

@@ -87,3 +87,20 @@ def test_histogram_numeric():
     d.createOrReplaceTempView("hn35")
     h2 = s.sql("SELECT histogram_numeric(v, 2) AS h FROM hn35").toPandas().h[0]
     assert [r.y for r in h2] == [7.0, 1.0] and h2[0].x == pytest.approx(41 / 7)
+
+
+def test_datetime_epoch_and_misc_builtins():
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    d = s.createDataFrame([("2024-03-06 10:20:30", "Ab1-x", 3, "a,b,c", 1709720430123)], ["t", "s", "n", "csv", "ms"])
+    r = d.select(F.unix_seconds("t").alias("us"), F.unix_date("t").alias("ud"), F.unix_millis("t").alias("um"),
+                 F.timestamp_millis("ms").alias("tm"), F.date_part(F.lit("YEAR"), "t").alias("y"),
+                 F.extract(F.lit("hour"), "t").alias("h"),
+                 F.convert_timezone(F.lit("UTC"), F.lit("Asia/Tokyo"), "t").alias("ct"), F.mask("s").alias("m"),
+                 F.find_in_set(F.lit("b"), "csv").alias("fs"), F.elt(F.lit(2), F.lit("x"), F.lit("y")).alias("el"),
+                 F.chr(F.lit(65)).alias("ch"), F.shiftrightunsigned(F.lit(-1), 60).alias("sr"),
+                 F.to_binary(F.lit("4142")).alias("tb"), F.printf(F.lit("%d-%s"), "n", "s").alias("pf")).toPandas()
+    row = r.iloc[0]
+    assert (row.us, row.ud, row.um) == (1709720430, 19788, 1709720430000)
+    assert row.tm == "2024-03-06 10:20:30.123" and (row.y, row.h) == (2024, 10)
+    assert row.ct == "2024-03-06 19:20:30" and row.m == "Xxn-x" and row.fs == 2 and row.el == "y"
+    assert row.ch == "A" and row.sr == 15 and row.tb == b"AB" and row.pf == "3-Ab1-x"
