@@ -972,6 +972,14 @@ class Parser:
         if fn in ("row_number", "rank", "dense_rank", "percent_rank", "cume_dist"):
             self.expect("op", ")")
             return getattr(W, fn)()
+        if fn == "extract" and self.peek().kind in ("id", "kw") and self.peek(1).kind == "kw" \
+                and self.peek(1).val == "from":
+            from . import functions as F                          # EXTRACT(field FROM source)
+            field = self.next().val
+            self.next()
+            src = self.or_expr()
+            self.expect("op", ")")
+            return F.date_part(E.lit(field), src).alias(f"extract({field} FROM {src.name})")
         if fn in ("ntile", "lag", "lead", "first_value", "last_value"):
             args = [self.or_expr()]
             while self.accept("op", ","):

@@ -104,3 +104,11 @@ def test_datetime_epoch_and_misc_builtins():
     assert row.tm == "2024-03-06 10:20:30.123" and (row.y, row.h) == (2024, 10)
     assert row.ct == "2024-03-06 19:20:30" and row.m == "Xxn-x" and row.fs == 2 and row.el == "y"
     assert row.ch == "A" and row.sr == 15 and row.tb == b"AB" and row.pf == "3-Ab1-x"
+
+
+def test_sql_extract_from():
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    s.createDataFrame([("2024-03-06 10:20:30", "a,b")], ["t", "c"]).createOrReplaceTempView("ex35")
+    q = s.sql("SELECT extract(YEAR FROM t) AS y, EXTRACT(minute FROM t) AS m, date_part('MONTH', t) AS mo, "
+              "find_in_set('b', c) AS f FROM ex35").toPandas()
+    assert q.to_dict("list") == {"y": [2024], "m": [20], "mo": [3], "f": [2]}
