@@ -106,7 +106,9 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
-    conf = SessionConf().set("spark.master", "spmd" if world > 1 else "local[*]").setAppName("bench-lr")
+    # one rank = one in-process GPU session (never an executor pool, whatever the node has)
+    conf = SessionConf().set("spark.master", "spmd" if world > 1 else "local[1]").setAppName("bench-lr")
+    conf.set("spark.executor.instances", str(world))
     s = Session(conf)
     comm = s.comm
     on_gpu = s.device.type == "cuda"

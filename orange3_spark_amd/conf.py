@@ -13,7 +13,15 @@ key                            meaning here
 ``spark.master``               ``local`` / ``local[*]`` (one process, GPU 0 or CPU),
                                ``spmd`` (one process per GPU launched by torchrun);
                                ``yarn-client`` and other cluster URLs map to auto
-``spark.executor.instances``   expected GPU count (checked against WORLD_SIZE in SPMD)
+``spark.executor.instances``   executors = GPUs: ``auto`` (default, every visible GPU --
+                               the reference's 8-executor default on an 8-GPU node) or N;
+                               N > 1 outside SPMD spawns a driver + N-executor pool
+                               (runtime/executors.py); checked against WORLD_SIZE in SPMD
+``o3s.executor.*``             pool knobs: ``pool`` (true: a pool even for 1 GPU),
+                               ``timeout`` (per-command watchdog, 21600 s), ``commTimeout``
+                               (executor collectives, 120 s), ``stragglerTimeout`` (600 s),
+                               ``errorGrace`` (20 s), ``residentModelBytes`` (16 MiB),
+                               ``respawn`` (true)
 ``o3s.device``                 ``auto`` | ``cuda`` | ``cpu``
 ``o3s.vector.dtype``           feature-matrix storage: ``auto`` (bf16 on GPU, f64 on
                                CPU) | ``bfloat16`` | ``float32`` | ``float64``
@@ -30,7 +38,7 @@ from collections import OrderedDict
 DEFAULTS = OrderedDict([
     ("spark.app.name", "OrangeSpark-AMD"),
     ("spark.master", "local[*]"),
-    ("spark.executor.instances", "1"),
+    ("spark.executor.instances", "auto"),
     ("spark.executor.cores", "1"),
     ("spark.executor.memory", "288g"),
     ("spark.driver.cores", "4"),
@@ -44,7 +52,8 @@ DEFAULTS = OrderedDict([
     ("o3s.seed", "42"),
     ("o3s.trace", "false"),                 # runtime/tracing.py phase tracer + roctx ranges
     ("o3s.checkpoint.interval", "0"),       # iterations between checkpoints (needs spark.checkpoint.dir)
-    ("o3s.comm.timeout", "1800"),           # seconds before a hung collective raises
+    # o3s.comm.timeout (unset): seconds before a hung collective raises -- 1800 for SPMD
+    # launches (benchmarks), o3s.executor.commTimeout (120) inside an executor pool
 ])
 
 

@@ -141,9 +141,12 @@ class ALSModel(Model, _ALSModelParams, MLWritable, MLReadable):
         from ..session import Session
         s = Session.active() or Session.getOrCreate()
         k = min(k, T.shape[0])
+        if s.comm.world_size > 1:          # factors are replicated: each rank recommends its block
+            lo, hi = s._shard_bounds(Q.shape[0])
+            Q, ids_q = Q[lo:hi], ids_q[lo:hi]
         recs = []
         for a in range(0, Q.shape[0], 1 << 14):
-            sc = Q[a:a + 1 << 14] @ T.T
+            sc = Q[a:a + (1 << 14)] @ T.T
             v, ix = torch.topk(sc, k, dim=1)
             for row_i, (vv, ii) in enumerate(zip(v.cpu().tolist(), ix.cpu().tolist())):
                 recs.append([Row._make([tname, "rating"], [int(ids_t[j]), float(x)]) for j, x in zip(ii, vv)])
@@ -162,15 +165,21 @@ class ALSModel(Model, _ALSModelParams, MLWritable, MLReadable):
         return self._recommend(self._V, self._iid_t, self._U, self._uid_t.cpu().numpy(), numUsers,
                                self.getOrDefault(self.itemCol), self.getOrDefault(self.userCol))
 
+    @staticmethod
+    def _subset_ids(dataset, col):
+        """Distinct ids of ``col`` over ALL ranks (each rank's rows hold an arbitrary part)."""
+        q = U.numeric_column(dataset, col, torch.int64)
+        return ALSE.global_ids(dataset.comm, q)
+
     def recommendForUserSubset(self, dataset, numItems):
-        q = U.numeric_column(dataset, self.getOrDefault(self.userCol), torch.int64)
-        pos, hit = self._lookup(self._uid_t, self._U, torch.unique(q))
+        q = self._subset_ids(dataset, self.getOrDefault(self.userCol)).to(self._uid_t.device)
+        pos, hit = self._lookup(self._uid_t, self._U, q)
         return self._recommend(self._U[pos[hit]], self._uid_t[pos[hit]], self._V, self._iid_t.cpu().numpy(),
                                numItems, self.getOrDefault(self.userCol), self.getOrDefault(self.itemCol))
 
     def recommendForItemSubset(self, dataset, numUsers):
-        q = U.numeric_column(dataset, self.getOrDefault(self.itemCol), torch.int64)
-        pos, hit = self._lookup(self._iid_t, self._V, torch.unique(q))
+        q = self._subset_ids(dataset, self.getOrDefault(self.itemCol)).to(self._iid_t.device)
+        pos, hit = self._lookup(self._iid_t, self._V, q)
         return self._recommend(self._V[pos[hit]], self._iid_t[pos[hit]], self._U, self._uid_t.cpu().numpy(),
                                numUsers, self.getOrDefault(self.itemCol), self.getOrDefault(self.userCol))
 

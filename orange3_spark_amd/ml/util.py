@@ -349,6 +349,12 @@ class MLReader:
         return self
 
     def load(self, path: str):
+        from ..session import DriverSession, Session
+        s = Session.active()
+        if isinstance(s, DriverSession):
+            # driver of an executor pool: the executors read the files (a large model --
+            # ALS factors -- then stays on them as a RemoteModel handle)
+            return s.live_pool.apply(_exec_load, self.cls, os.path.abspath(path))
         meta = load_metadata(path)
         cls = py_class(meta["class"])
         if not issubclass(cls, self.cls) and not issubclass(self.cls, cls):
@@ -358,6 +364,10 @@ class MLReader:
         inst = cls()
         apply_metadata(inst, meta)
         return inst
+
+
+def _exec_load(cls, path):
+    return MLReader(cls).load(path)
 
 
 class MLWritable:

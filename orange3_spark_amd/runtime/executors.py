@@ -24,8 +24,24 @@ a JVM driver, Py4J and YARN executors; the MI355X design is:
   per worker ~ 1/N of the table) and copies it to its GPU through pinned memory.
 * Handles are reference counted: when the driver drops the last handle, the workers free
   the object at the next command.  A command that fails on some ranks while others are
-  stuck in a collective tears the pool down after a grace period (the session reports
-  itself stopped) instead of hanging the GUI.
+  stuck in a collective tears the pool down after a grace period instead of hanging the
+  GUI; a rank that never answers after its peers did (``stragglerTimeout``) or a command
+  that outlives the watchdog (``o3s.executor.timeout``) does the same.
+* **Executor-resident models** (Spark keeps ALS factors as distributed DataFrames, reached
+  through spark_ml_estimator.py:22 and spark_ml_model.py:53): a fitted model whose device
+  state exceeds ``o3s.executor.residentModelBytes`` (16 MiB) stays on the executors and the
+  driver receives a :class:`RemoteModel` -- ``isinstance(h, ALSModel)`` holds, it carries
+  only the class and uid, and ``transform`` / ``recommendFor*`` / ``userFactors`` /
+  ``save`` run on the executors (no factor byte crosses the driver pipes).  Small models
+  (LR, SVC, KMeans, trees) still travel by value.
+* **Lineage recovery** (Spark recomputes lost partitions from lineage): every handle
+  remembers the command that produced it (a *recipe*: the pickled command plus the
+  recipes of the handles it used).  When an executor dies the pool is torn down; the next
+  call on any handle respawns a fresh pool (new subprocesses, never a re-exec) and
+  replays the handle's recipe from its sources -- catalog tables, parquet readers,
+  synthetic generators, ``createDataFrame`` from the driver-held host frame.  Temp-view
+  registrations are replayed too.  A handle whose lineage is not replayable raises
+  :class:`ExecutorLost` asking to re-run the upstream widgets.
 """
 from __future__ import annotations
 
@@ -65,6 +81,61 @@ def _is_remote_kept(obj) -> bool:
     return not isinstance(obj, tuple)          # Row (a tuple subclass) travels by value
 
 
+RESIDENT_MODEL_BYTES = 16 << 20               # default of o3s.executor.residentModelBytes
+
+
+def _model_candidate(obj) -> bool:
+    """A fitted model that may stay on the executors (PipelineModels never do: their large
+    stages are kept one by one, the pipeline itself travels by value)."""
+    mod = getattr(type(obj), "__module__", "") or ""
+    if not mod.startswith("orange3_spark_amd.ml"):
+        return False
+    from ..ml.base import Model, PipelineModel
+    return isinstance(obj, Model) and not isinstance(obj, PipelineModel)
+
+
+def payload_bytes(obj, depth: int = 0, seen=None) -> int:
+    """Bytes of array state (torch tensors, numpy arrays) reachable from ``obj`` through
+    attributes, containers and engine dataclasses (depth-bounded)."""
+    import numpy as np
+    import torch
+    if seen is None:
+        seen = set()
+    if id(obj) in seen or depth > 6:
+        return 0
+    seen.add(id(obj))
+    if isinstance(obj, torch.Tensor):
+        return obj.numel() * obj.element_size()
+    if isinstance(obj, np.ndarray):
+        return int(obj.nbytes)
+    if isinstance(obj, (str, bytes, int, float, bool, type(None))):
+        return 0
+    if isinstance(obj, dict):
+        return sum(payload_bytes(v, depth + 1, seen) for v in list(obj.values())[:4096])
+    if isinstance(obj, (list, tuple, set, frozenset)):
+        return sum(payload_bytes(v, depth + 1, seen) for v in list(obj)[:4096])
+    mod = getattr(type(obj), "__module__", "") or ""
+    if mod.startswith("orange3_spark_amd") and hasattr(obj, "__dict__"):
+        return sum(payload_bytes(v, depth + 1, seen) for k, v in vars(obj).items() if k != "parent")
+    return 0
+
+
+def _resident_decision(session, obj) -> bool:
+    """Keep ``obj`` on the executors?  The largest payload over the ranks decides, so every
+    rank takes the same branch (the handle ids the ranks assign must stay in step)."""
+    limit = float(session.conf.get("o3s.executor.residentModelBytes", str(RESIDENT_MODEL_BYTES)))
+    nb = float(payload_bytes(obj))
+    comm = session.comm
+    if comm.world_size > 1:
+        nb = float(comm.max_scalar(nb))
+    return nb > limit
+
+
+def _model_meta(obj) -> dict:
+    t = type(obj)
+    return {"cls": (t.__module__, t.__qualname__), "uid": getattr(obj, "uid", None)}
+
+
 # =====================================================================================
 # worker side
 # =====================================================================================
@@ -76,22 +147,36 @@ class _Null:
         return memoryview(b).nbytes
 
 
-def _worker_pickler(objs: dict, ids: dict, counter, buf):
+def _worker_pickler(objs: dict, ids: dict, counter, buf, session=None):
     """Pickler that keeps engine objects on this worker (registered under the next id of a
-    counter every rank advances identically) and moves device tensors to host memory."""
+    counter every rank advances identically) and moves device tensors to host memory.
+    Fitted models above the resident threshold are kept too (``kind`` "model")."""
     import cloudpickle
     import torch
+    decided: dict = {}
 
     class P(cloudpickle.Pickler):
         def persistent_id(self, obj):
+            k = ids.get(id(obj))
+            known = k is not None and objs.get(k) is obj
+            kind = None
             if _is_remote_kept(obj):
-                k = ids.get(id(obj))
-                if k is None or objs.get(k) is not obj:
-                    k = next(counter)
-                    objs[k] = obj
-                    ids[id(obj)] = k
-                return ("ref", k, type(obj).__name__, _is_frame(obj))
-            return None
+                kind = "frame" if _is_frame(obj) else "obj"
+            elif _model_candidate(obj):
+                if known:
+                    kind = "model"
+                elif session is not None:
+                    keep = decided.get(id(obj))
+                    if keep is None:
+                        keep = decided[id(obj)] = _resident_decision(session, obj)
+                    kind = "model" if keep else None
+            if kind is None:
+                return None
+            if not known:
+                k = next(counter)
+                objs[k] = obj
+                ids[id(obj)] = k
+            return ("ref", k, type(obj).__name__, kind, _model_meta(obj) if kind == "model" else None)
 
         def reducer_override(self, obj):
             if isinstance(obj, torch.Tensor) and obj.device.type != "cpu":
@@ -107,10 +192,13 @@ def _is_frame(obj) -> bool:
     return isinstance(obj, DataFrame)
 
 
-def _worker_unpickler(objs: dict, data: bytes):
+def _worker_unpickler(objs: dict, data: bytes, slots=()):
+    """Commands name executor objects by slot: ``("slot", i)`` is ``objs[slots[i]]`` (the
+    slot table travels in the message header, so a recorded command can be replayed
+    against the object ids of a respawned pool)."""
     class U(pickle.Unpickler):
         def persistent_load(self, pid):
-            return objs[pid[1]]
+            return objs[slots[pid[1]]] if pid[0] == "slot" else objs[pid[1]]
     return U(io.BytesIO(data)).load()
 
 
@@ -168,23 +256,23 @@ def _worker_main(rank: int, world: int, port: int, conf_pairs, conn, use_gpu: bo
         except (EOFError, OSError):
             break
         try:
-            garbage = pickle.loads(msg[8:_hdr_len(msg)])
+            garbage, slots = pickle.loads(msg[8:_hdr_len(msg)])
         except Exception:  # noqa: BLE001
-            garbage = []
+            garbage, slots = [], ()
         for k in garbage:
             o = objs.pop(k, None)
             if o is not None and ids.get(id(o)) == k:
                 ids.pop(id(o), None)
         body = msg[_hdr_len(msg):]
         try:
-            cmd = _worker_unpickler(objs, body)
+            cmd = _worker_unpickler(objs, body, slots)
             kind = cmd[0]
             if kind == "stop":
                 conn.send_bytes(pickle.dumps(("ok", rank, None)))
                 break
             result = _execute(s, cmd, objs)
             buf = io.BytesIO() if rank == 0 else _Null()
-            _worker_pickler(objs, ids, counter, buf).dump(result)
+            _worker_pickler(objs, ids, counter, buf, s).dump(result)
             conn.send_bytes(pickle.dumps(("ok", rank, buf.getvalue() if rank == 0 else None)))
         except BaseException:  # noqa: BLE001 - every failure goes back to the driver
             conn.send_bytes(pickle.dumps(("error", rank, traceback.format_exc())))
@@ -272,13 +360,50 @@ class _Proc:
             pass
 
 
+class _Recipe:
+    """How a handle was produced (its lineage): replayed on a respawned pool.
+
+    ``kind``: "session" (the executor session, id 0), "cmd" (``body`` = the pickled command
+    whose executor objects are named by slot, ``slots`` = the recipes of those objects) or
+    "scatter" (``body`` = (host pandas frame, schema) of a createDataFrame).  ``index``
+    picks the handle among the command result's handles (unpickle order)."""
+
+    __slots__ = ("kind", "body", "slots", "index", "_replayed", "__weakref__")
+
+    def __init__(self, kind, body=None, slots=(), index=0):
+        self.kind, self.body, self.slots, self.index = kind, body, tuple(slots), index
+        self._replayed = None
+
+    def at(self, index: int) -> "_Recipe":
+        r = _Recipe(self.kind, self.body, self.slots, index)
+        r._replayed = _Shared(self)
+        return r
+
+
+class _Shared:
+    """Sibling recipes (several handles out of one command) share one replay."""
+
+    __slots__ = ("root",)
+
+    def __init__(self, root):
+        self.root = root
+
+
+_SESSION_RECIPE = _Recipe("session")
+# calls whose effect lives in the executors' session state (replayed after a respawn)
+_EFFECTS = frozenset(("createOrReplaceTempView", "createTempView", "createGlobalTempView",
+                      "createOrReplaceGlobalTempView", "registerTempTable", "dropTempView",
+                      "dropGlobalTempView", "setCheckpointDir", "setCurrentDatabase", "register"))
+
+
 class ExecutorPool:
     """N worker processes in one RCCL (or gloo) group, driven by this process."""
 
     _pools: "weakref.WeakSet[ExecutorPool]" = weakref.WeakSet()
 
     def __init__(self, n: int, conf_pairs, use_gpu: bool | None = None, start_timeout: float = 600.0,
-                 command_timeout: float | None = None, error_grace: float = 20.0):
+                 command_timeout: float | None = None, error_grace: float = 20.0,
+                 straggler_timeout: float | None = None):
         import secrets
         import subprocess
         import sys
@@ -299,11 +424,18 @@ class ExecutorPool:
         self.use_gpu = bool(use_gpu)
         self.command_timeout = command_timeout
         self.error_grace = float(error_grace)
+        self.straggler_timeout = straggler_timeout
         self._lock = threading.RLock()
         self._garbage: list = []
         self._proxies: dict = {}
         self._methods: set = set()
         self.alive = False
+        self.lost_reason: str | None = None
+        self._successor: "ExecutorPool | None" = None
+        self._respawn = None                      # set by DriverSession: () -> new pool
+        self.effects: list = []                   # replayable session-state commands
+        self.bytes_sent = 0                       # command bytes driver -> executors (all ranks)
+        self.bytes_received = 0                   # reply bytes executors -> driver
         self._conns, self._procs = [None] * self.n, []
         key = secrets.token_bytes(32)
         listener = Listener(("127.0.0.1", 0), authkey=key)
@@ -337,6 +469,10 @@ class ExecutorPool:
         self.alive = True
         ExecutorPool._pools.add(self)
 
+    @property
+    def pids(self) -> list:
+        return [p.p.pid for p in self._procs]
+
     def _accept(self, listener, pairs, timeout: float):
         """Accept the N executors' authenticated connections (in a helper thread, so a
         worker that dies before connecting is noticed) and send each the session conf."""
@@ -369,13 +505,20 @@ class ExecutorPool:
             c.send_bytes(pickle.dumps(pairs))
 
     # ---------------------------------------------------------------- transport
+    def _lost(self, msg: str):
+        self.lost_reason = msg
+        self._teardown()
+        return ExecutorLost(msg)
+
     def _gather(self, timeout: float | None, what: str):
         """One reply per rank.  After the first error, the others get ``error_grace``
-        seconds; ranks that neither reply nor die in time mean the group is wedged (a
-        collective waiting for a failed peer): the pool is torn down."""
+        seconds; after the first success, ``straggler_timeout`` (ranks of one command run
+        in lock step: a rank still busy long after its peers finished is wedged).  Ranks
+        that neither reply nor die in time mean the group is wedged (e.g. a collective
+        waiting for a failed peer): the pool is torn down."""
         from multiprocessing.connection import wait
         pending = dict(enumerate(self._conns))
-        out, first_err = [], None
+        out, first_err, first_ok = [], None, None
         deadline = None if timeout is None else time.monotonic() + timeout
         while pending:
             now = time.monotonic()
@@ -383,94 +526,213 @@ class ExecutorPool:
             if first_err is not None:
                 g = first_err + self.error_grace
                 limit = g if limit is None else min(limit, g)
+            if first_ok is not None and self.straggler_timeout is not None:
+                g = first_ok + self.straggler_timeout
+                limit = g if limit is None else min(limit, g)
             if limit is not None and now > limit:
-                self._teardown()
-                raise ExecutorLost(f"executors {sorted(pending)} did not finish '{what}'"
-                                   + (f"; errors: {self._fmt(out)}" if out else "") + " -- the pool was shut down")
+                why = "watchdog" if limit == deadline else ("error grace" if first_err is not None else "straggler")
+                raise self._lost(f"executors {sorted(pending)} did not finish '{what}' ({why} timeout)"
+                                 + (f"; errors: {self._fmt(out)}" if out else "") + " -- the pool was shut down")
             ready = wait(list(pending.values()), timeout=1.0 if limit is None else max(0.01, min(1.0, limit - now)))
             for c in ready:
                 r = next(k for k, v in pending.items() if v is c)
                 try:
-                    msg = pickle.loads(c.recv_bytes())
+                    raw = c.recv_bytes()
                 except (EOFError, OSError):
-                    self._teardown()
-                    raise ExecutorLost(f"executor {r} died during '{what}' (exit code "
-                                       f"{self._procs[r].exitcode})") from None
+                    raise self._lost(f"executor {r} died during '{what}' (exit code "
+                                     f"{self._procs[r].exitcode})") from None
+                self.bytes_received += len(raw)
+                msg = pickle.loads(raw)
                 pending.pop(r)
                 out.append(msg)
                 if msg[0] == "error" and first_err is None:
                     first_err = time.monotonic()
+                elif msg[0] != "error" and first_ok is None:
+                    first_ok = time.monotonic()
             for r in list(pending):
                 if not self._procs[r].is_alive():
-                    self._teardown()
-                    raise ExecutorLost(f"executor {r} exited with code {self._procs[r].exitcode} during '{what}'")
+                    raise self._lost(f"executor {r} exited with code {self._procs[r].exitcode} during '{what}'")
         return out
 
     @staticmethod
     def _fmt(replies):
         return "\n".join(f"[rank {r}] {d}" for st, r, d in replies if st == "error")
 
-    def _driver_pickle(self, cmd) -> bytes:
+    def _driver_pickle(self, cmd):
+        """Pickle ``cmd`` naming every handle by slot; returns (bytes, [handles by slot]).
+        A handle of a dead pool is first rebuilt here from its recipe (lineage replay)."""
         import cloudpickle
         pool = self
+        slots: list = []
+        pos: dict = {}
 
         class P(cloudpickle.Pickler):
             def persistent_id(self, obj):
                 if isinstance(obj, RemoteObject):
                     if obj._pool is not pool:
-                        raise ValueError("a handle of another executor pool cannot be used here")
-                    return ("ref", obj._id)
+                        pool._adopt(obj)
+                    i = pos.get(id(obj))
+                    if i is None:
+                        i = pos[id(obj)] = len(slots)
+                        slots.append(obj)
+                    return ("slot", i)
                 return None
         buf = io.BytesIO()
         P(buf, protocol=pickle.HIGHEST_PROTOCOL).dump(cmd)
-        return buf.getvalue()
+        return buf.getvalue(), slots
 
-    def _driver_unpickle(self, data: bytes):
+    def _driver_unpickle(self, data: bytes, recipe: "_Recipe | None", found: list | None = None):
         pool = self
+        seq = itertools.count()
 
         class U(pickle.Unpickler):
             def persistent_load(self, pid):
-                _, k, tname, is_frame = pid
-                return pool._proxy(k, tname, is_frame)
+                _, k, tname, kind, meta = pid
+                i = next(seq)
+                h = pool._proxy(k, tname, kind, meta, None if recipe is None else recipe.at(i))
+                if found is not None:
+                    found.append(h)
+                return h
         return U(io.BytesIO(data)).load()
 
-    def _proxy(self, k, tname, is_frame):
+    def _proxy(self, k, tname, kind, meta=None, recipe=None):
         ref = self._proxies.get(k)
         obj = ref() if ref is not None else None
         if obj is None:
-            obj = (RemoteDataFrame if is_frame else RemoteObject)(self, k, tname)
+            if kind == "model":
+                obj = RemoteModel(self, k, tname, meta)
+            else:
+                obj = (RemoteDataFrame if kind in ("frame", True) else RemoteObject)(self, k, tname)
+            object.__setattr__(obj, "_recipe", recipe)
             self._proxies[k] = weakref.ref(obj)
-            weakref.finalize(obj, self._release, k)
+            object.__setattr__(obj, "_fin", weakref.finalize(obj, self._release, k))
         return obj
 
     def _release(self, k):
         self._garbage.append(k)
 
-    def command(self, cmd, per_rank=None, what: str | None = None):
+    def _send_all(self, bodies, slot_ids):
+        garbage, self._garbage = self._garbage, []
+        for k in garbage:
+            self._proxies.pop(k, None)
+        hdr = pickle.dumps((garbage, slot_ids))
+        head = len(hdr).to_bytes(8, "little") + hdr
+        for r, c in enumerate(self._conns):
+            msg = head + bodies[r]
+            try:
+                c.send_bytes(msg)
+            except (BrokenPipeError, OSError):
+                raise self._lost(f"executor {r} is gone") from None
+            self.bytes_sent += len(msg)
+
+    def _run(self, bodies, slot_ids, what, recipe, found=None):
+        self._send_all(bodies, slot_ids)
+        replies = self._gather(self.command_timeout, what)
+        errs = [m for m in replies if m[0] == "error"]
+        if errs:
+            raise ExecutorError("command failed on executor(s):\n" + self._fmt(replies))
+        data = next(d for st, r, d in replies if r == 0)
+        return self._driver_unpickle(data, recipe, found)
+
+    def command(self, cmd, per_rank=None, what: str | None = None, recipe: "_Recipe | None" = None):
         """Run ``cmd`` on every executor (``per_rank[r]`` replaces it on rank r) and return
-        rank 0's result."""
+        rank 0's result.  On a dead pool the call moves to its respawned successor."""
         with self._lock:
+            if self.alive:
+                dead = [r for r, p in enumerate(self._procs) if not p.is_alive()]
+                if dead:                          # lost between commands (killed, crashed)
+                    self._lost(f"executor(s) {dead} exited (codes {[self._procs[r].exitcode for r in dead]})")
             if not self.alive:
-                raise ExecutorLost("the executor pool is shut down")
-            garbage, self._garbage = self._garbage, []
-            for k in garbage:
-                self._proxies.pop(k, None)
-            hdr = pickle.dumps(garbage)
-            head = len(hdr).to_bytes(8, "little") + hdr
-            body = self._driver_pickle(cmd) if per_rank is None else None
-            for r, c in enumerate(self._conns):
-                b = body if per_rank is None else self._driver_pickle(per_rank[r])
-                try:
-                    c.send_bytes(head + b)
-                except (BrokenPipeError, OSError):
-                    self._teardown()
-                    raise ExecutorLost(f"executor {r} is gone") from None
-            replies = self._gather(self.command_timeout, what or str(cmd[0]))
-            errs = [m for m in replies if m[0] == "error"]
-            if errs:
-                raise ExecutorError("command failed on executor(s):\n" + self._fmt(replies))
-            data = next(d for st, r, d in replies if r == 0)
-            return self._driver_unpickle(data)
+                return self._revive().command(cmd, per_rank, what, recipe)
+            what = what or str((cmd or per_rank[0])[0])
+            if per_rank is None:
+                body, slots = self._driver_pickle(cmd)
+                bodies = [body] * self.n
+                if recipe is None:
+                    recipe = self._recipe_of(body, slots)
+                    if recipe is not None and cmd[0] == "call" and cmd[2] in _EFFECTS:
+                        self.effects.append(recipe)
+            else:
+                packed = [self._driver_pickle(c) for c in per_rank]
+                bodies = [b for b, _ in packed]
+                slots = packed[0][1]
+                if any(sl != slots for _, sl in packed):
+                    raise ValueError("per-rank commands must name the same handles")
+            return self._run(bodies, [h._id for h in slots], what, recipe)
+
+    @staticmethod
+    def _recipe_of(body, slots):
+        subs = []
+        for h in slots:
+            r = h._recipe
+            if r is None:
+                return None
+            subs.append(r)
+        return _Recipe("cmd", body, subs)
+
+    # ---------------------------------------------------------------- lineage recovery
+    def _revive(self) -> "ExecutorPool":
+        """The live pool that replaces this dead one (respawning it if needed)."""
+        p = self
+        while not p.alive and p._successor is not None:
+            p = p._successor
+        if p.alive:
+            return p
+        if p._respawn is None:
+            raise ExecutorLost("the executor pool is shut down"
+                               + (f" ({p.lost_reason})" if p.lost_reason else ""))
+        new = p._respawn(p)
+        p._successor = new
+        return new
+
+    def _adopt(self, h: "RemoteObject") -> None:
+        """Rebind handle ``h`` (of a dead predecessor pool) to an object of this pool,
+        rebuilt by replaying its recipe."""
+        old = h._pool
+        q = old
+        while q is not None and q is not self:
+            q = q._successor
+        if q is None:
+            raise ValueError("a handle of another executor pool cannot be used here")
+        if h._recipe is None:
+            raise ExecutorLost(f"{h._tname} #{h._id} was lost with its executors and its lineage cannot be "
+                               "replayed (it was not built from a table, file, generator or driver data): "
+                               "re-run the upstream widgets")
+        fresh = self._replay(h._recipe)
+        fresh._fin.detach()
+        object.__setattr__(h, "_pool", self)
+        object.__setattr__(h, "_id", fresh._id)
+        self._proxies[fresh._id] = weakref.ref(h)
+        object.__setattr__(h, "_fin", weakref.finalize(h, self._release, fresh._id))
+
+    def _replay(self, rec: "_Recipe") -> "RemoteObject":
+        if rec.kind == "session":
+            return self._proxy(0, "Session", "obj", None, _SESSION_RECIPE)
+        root = rec._replayed.root if isinstance(rec._replayed, _Shared) else rec
+        got = root._replayed if not isinstance(root._replayed, _Shared) else None
+        if got is None or got[0] is not self:
+            found: list = []
+            if root.kind == "scatter":
+                pdf, schema = root.body
+                found.append(self.scatter_dataframe(pdf, schema))
+            else:
+                handles = [self._replay(r) for r in root.slots]
+                self._run([root.body] * self.n, [h._id for h in handles], "replay", root, found)
+                del handles
+            got = root._replayed = (self, found)
+        handles = got[1]
+        if rec.index >= len(handles):
+            raise ExecutorLost("lineage replay produced a different result shape")
+        return handles[rec.index]
+
+    def replay_effects(self, effects) -> None:
+        for rec in effects:
+            try:
+                handles = [self._replay(r) for r in rec.slots]
+                self._run([rec.body] * self.n, [h._id for h in handles], "replay effect", None)
+                self.effects.append(rec)
+            except (ExecutorError, ExecutorLost) as e:
+                log.warning("could not replay a session effect after respawn: %s", e)
 
     # ---------------------------------------------------------------- API used by proxies
     def getattr(self, obj: "RemoteObject", name: str):
@@ -491,10 +753,13 @@ class ExecutorPool:
         return self.command(("apply", fn, args, kwargs), what=getattr(fn, "__name__", "apply"))
 
     def scatter_dataframe(self, pdf, schema=None):
-        """Row slice r of a host pandas frame -> executor r (only that slice is sent)."""
+        """Row slice r of a host pandas frame -> executor r (only that slice is sent).  The
+        driver keeps a reference to the host frame as the handle's lineage (Spark's
+        ``parallelize`` keeps its local collection the same way)."""
         n = len(pdf)
         parts = [pdf.iloc[(n * r) // self.n:(n * (r + 1)) // self.n] for r in range(self.n)]
-        return self.command(None, per_rank=[("scatter_df", p, schema) for p in parts], what="createDataFrame")
+        return self.command(None, per_rank=[("scatter_df", p, schema) for p in parts], what="createDataFrame",
+                            recipe=_Recipe("scatter", (pdf, schema)))
 
     def info(self):
         return self.command(("info",))
@@ -502,10 +767,11 @@ class ExecutorPool:
     # ---------------------------------------------------------------- lifecycle
     def shutdown(self, timeout: float = 30.0):
         with self._lock:
+            self._respawn = None
             if not self.alive:
                 return
             self.alive = False
-            hdr = pickle.dumps([])
+            hdr = pickle.dumps(([], ()))
             for c in self._conns:
                 try:
                     c.send_bytes(len(hdr).to_bytes(8, "little") + hdr + pickle.dumps(("stop",)))
@@ -562,14 +828,18 @@ _UNOPS = ("__neg__", "__invert__", "__abs__")
 
 
 class RemoteObject:
-    """Driver-side handle of an object that lives on every executor (same id on each)."""
+    """Driver-side handle of an object that lives on every executor (same id on each).
+    ``_recipe`` is its lineage (how to rebuild it on a respawned pool), ``_fin`` the
+    finaliser that frees the executor object when the handle dies."""
 
-    __slots__ = ("_pool", "_id", "_tname", "__weakref__")
+    __slots__ = ("_pool", "_id", "_tname", "_recipe", "_fin", "__weakref__")
 
     def __init__(self, pool: ExecutorPool, k: int, tname: str):
         object.__setattr__(self, "_pool", pool)
         object.__setattr__(self, "_id", k)
         object.__setattr__(self, "_tname", tname)
+        object.__setattr__(self, "_recipe", None)
+        object.__setattr__(self, "_fin", None)
 
     def __getattr__(self, name):
         if name.startswith("__") and name.endswith("__"):
@@ -677,14 +947,95 @@ class RemoteDataFrame(RemoteObject):
         return f"DataFrame[{cols}] (on {self._pool.n} executors)"
 
 
+class RemoteModel(RemoteObject):
+    """Handle of a fitted model held by the executors (its device state exceeded
+    ``o3s.executor.residentModelBytes``).  ``isinstance(h, <ModelClass>)`` holds and ``uid``
+    is local; every other attribute / method (``transform``, ``recommendForAllUsers``,
+    ``userFactors``, params) runs on the executors.  ``save`` / ``write().save`` write from
+    the executors: no model byte goes through the driver."""
+
+    __slots__ = ("_cls", "uid")
+
+    def __init__(self, pool: ExecutorPool, k: int, tname: str, meta: dict | None = None):
+        super().__init__(pool, k, tname)
+        meta = meta or {}
+        cls = None
+        if meta.get("cls"):
+            import importlib
+            mod, qual = meta["cls"]
+            cls = importlib.import_module(mod)
+            for part in qual.split("."):
+                cls = getattr(cls, part)
+        object.__setattr__(self, "_cls", cls)
+        object.__setattr__(self, "uid", meta.get("uid"))
+
+    @property
+    def __class__(self):
+        return self._cls or RemoteModel
+
+    @property
+    def pool(self):
+        return self._pool
+
+    def write(self):
+        return _RemoteWriter(self)
+
+    def save(self, path: str) -> None:
+        self.write().save(path)
+
+    def __repr__(self):
+        return f"{self._tname}: uid={self.uid} (resident on {self._pool.n} executors)"
+
+
+class _RemoteWriter:
+    """``MLWriter`` of an executor-resident model: the ranks write (rank 0 the metadata and
+    its data parts), the driver only sends the path."""
+
+    def __init__(self, h):
+        self._h, self._overwrite, self._opts = h, False, {}
+
+    def overwrite(self):
+        self._overwrite = True
+        return self
+
+    def option(self, k, v):
+        self._opts[k] = v
+        return self
+
+    def session(self, s):
+        return self
+
+    def save(self, path: str) -> None:
+        self._h._pool.apply(_exec_save, self._h, os.path.abspath(path), self._overwrite, self._opts)
+
+    def saveImpl(self, path: str) -> None:
+        self._h._pool.apply(_exec_save_impl, self._h, os.path.abspath(path))
+
+
+def _exec_save(model, path, overwrite, opts):
+    w = model.write()
+    if overwrite:
+        w.overwrite()
+    for k, v in opts.items():
+        w.option(k, v)
+    w.save(path)
+
+
+def _exec_save_impl(model, path):
+    model.write().saveImpl(path)
+
+
+_HANDLE_TYPES = (RemoteObject, RemoteDataFrame, RemoteModel)
+
+
 def is_remote(obj) -> bool:
-    return type(obj) in (RemoteObject, RemoteDataFrame)
+    return type(obj) in _HANDLE_TYPES
 
 
 def remote_pool_of(*objs):
     """The executor pool of the first handle among ``objs`` (recursing into lists/dicts)."""
     for o in objs:
-        if type(o) in (RemoteObject, RemoteDataFrame):
+        if type(o) in _HANDLE_TYPES:
             return o._pool
         if isinstance(o, (list, tuple)):
             p = remote_pool_of(*o)

@@ -32,16 +32,32 @@ log = logging.getLogger("orange3_spark_amd")
 __version__ = "0.1.0"
 
 
+def resolve_executors(value) -> int:
+    """``spark.executor.instances``: an integer, or ``auto`` = every visible GPU (at least 1).
+    Counting devices does not initialise HIP (the driver process never touches a GPU)."""
+    v = str(value if value is not None else "auto").strip().lower()
+    if v in ("", "auto", "*", "all"):
+        return max(1, torch.cuda.device_count())
+    return int(float(v))
+
+
 def _wants_pool(conf) -> bool:
-    """``spark.executor.instances = N > 1`` outside an SPMD launch -> driver + N executors."""
+    """``spark.executor.instances = N > 1`` (``auto``: N = visible GPUs) outside an SPMD
+    launch -> driver + N executors; ``o3s.executor.pool = true`` asks for a pool even at
+    N = 1 (the GUI process then never touches the GPU).  ``spark.master`` ``local`` /
+    ``local[1]`` keeps everything in this process."""
     import os
     if conf is None or os.environ.get("WORLD_SIZE") not in (None, "", "1"):
         return False
+    master = conf.master().lower()
+    if master in ("spmd", "local", "local[1]"):
+        return False
     try:
-        n = int(float(conf.get("spark.executor.instances", "1")))
+        n = resolve_executors(conf.get("spark.executor.instances", "auto"))
     except (TypeError, ValueError):
         return False
-    return n > 1 and conf.master().lower() != "spmd"
+    forced = str(conf.get("o3s.executor.pool", "false")).lower() in ("1", "true", "yes")
+    return n > 1 or (forced and n >= 1)
 
 
 class Session:
@@ -63,7 +79,8 @@ class Session:
                 if (world > 1 or master == "spmd") else LocalComm(self.device)
         self.comm = comm
         if self.conf.get("spark.master", "").lower() == "spmd":
-            want = int(float(self.conf.get("spark.executor.instances", str(self.comm.world_size))))
+            inst = self.conf.get("spark.executor.instances", "auto")
+            want = self.comm.world_size if str(inst).lower() in ("auto", "", "*", "all") else int(float(inst))
             if want not in (1, self.comm.world_size):
                 raise ValueError(f"spark.executor.instances={want} but this SPMD launch has "
                                  f"WORLD_SIZE={self.comm.world_size} ranks")
@@ -322,29 +339,101 @@ class DriverSession(Session):
     """Driver of an executor pool (runtime/executors.py): this process keeps no rows and
     never touches a GPU; ``spark.executor.instances`` worker processes (one per MI355X, an
     RCCL group over xGMI) hold the data and run every operation.  DataFrames are handles
-    (``RemoteDataFrame``); fits return ordinary local models.  Reference: the Context
-    widget's executor sizing (orangecontrib/spark/widgets/data/spark_context.py:41-42,76)."""
+    (``RemoteDataFrame``); small fitted models come back by value, large ones stay on the
+    executors (``RemoteModel``).  When an executor dies the pool is respawned on the next
+    call and handles are rebuilt from their lineage (``events`` records it; listeners
+    registered with :meth:`add_listener` -- the Context widget -- are told).  Canvas
+    defaults are hang-free: collectives time out after ``o3s.executor.commTimeout`` (120 s),
+    a rank still busy ``o3s.executor.stragglerTimeout`` (600 s) after its peers answered, or
+    a command running past ``o3s.executor.timeout`` (6 h), tears the pool down instead of
+    blocking the GUI.  Reference: the Context widget's executor sizing
+    (orangecontrib/spark/widgets/data/spark_context.py:41-42,76)."""
 
     def __init__(self, conf: SessionConf | None = None, comm=None, device=None):
-        from .runtime.executors import ExecutorPool
         self.conf = conf.copy() if conf is not None else SessionConf()
         self.device = torch.device("cpu")
         self.comm = LocalComm(self.device)
-        n = int(float(self.conf.get("spark.executor.instances", "1")))
-        timeout = self.conf.get("o3s.executor.timeout", None)
-        self.pool = ExecutorPool(n, self.conf.getAll(),
-                                 command_timeout=float(timeout) if timeout not in (None, "", "0") else None,
-                                 error_grace=float(self.conf.get("o3s.executor.errorGrace", "20")))
-        self._remote = self.pool._proxy(0, "Session", False)
-        self.catalog = self._remote.catalog
+        self.n_executors = resolve_executors(self.conf.get("spark.executor.instances", "auto"))
+        self.events: list = []
+        self._listeners: list = []
         self._stopped = False
         self.version = __version__
+        self._attach(self._spawn())
+
+    def _pool_conf(self):
+        pairs = OrderedDict(self.conf.getAll())
+        pairs["spark.executor.instances"] = str(self.n_executors)
+        if not self.conf.contains("o3s.comm.timeout"):
+            pairs["o3s.comm.timeout"] = self.conf.get("o3s.executor.commTimeout", "120")
+        return list(pairs.items())
+
+    def _spawn(self):
+        from .runtime.executors import ExecutorPool
+
+        def _f(key, default):
+            v = self.conf.get(key, default)
+            return None if v in (None, "", "0", "none", "None") else float(v)
+        pool = ExecutorPool(self.n_executors, self._pool_conf(),
+                            command_timeout=_f("o3s.executor.timeout", "21600"),
+                            error_grace=float(self.conf.get("o3s.executor.errorGrace", "20")),
+                            straggler_timeout=_f("o3s.executor.stragglerTimeout", "600"))
+        pool._respawn = self._respawn
+        return pool
+
+    def _attach(self, pool):
+        from .runtime.executors import _SESSION_RECIPE
+        self.pool = pool
+        self._remote = pool._proxy(0, "Session", "obj", None, _SESSION_RECIPE)
+        self.catalog = self._remote.catalog
+
+    def _respawn(self, dead):
+        """A fresh pool replacing ``dead`` (new subprocesses; never a re-exec of a process
+        that touched a GPU), with the dead pool's session effects replayed."""
+        if self._stopped or str(self.conf.get("o3s.executor.respawn", "true")).lower() in ("0", "false", "no"):
+            from .runtime.executors import ExecutorLost
+            raise ExecutorLost("the executor pool is shut down" + (f" ({dead.lost_reason})" if dead.lost_reason else ""))
+        import time as _t
+        t0 = _t.time()
+        new = self._spawn()
+        ev = {"event": "executors respawned", "reason": dead.lost_reason, "executors": new.n,
+              "devices": list(new.devices), "seconds": None, "time": t0}
+        self._attach(new)
+        new.replay_effects(dead.effects)
+        ev["seconds"] = _t.time() - t0
+        self.events.append(ev)
+        log.warning("executor pool respawned after: %s", dead.lost_reason)
+        for cb in list(self._listeners):
+            try:
+                cb(ev)
+            except Exception:  # noqa: BLE001 - a listener must not break recovery
+                log.exception("executor event listener failed")
+        return new
+
+    def add_listener(self, cb) -> None:
+        """``cb(event_dict)`` on pool events (respawn after an executor loss)."""
+        self._listeners.append(cb)
+
+    def restart_executors(self):
+        """Replace the pool now (what the next call does after an executor loss)."""
+        old = self.pool
+        if old.alive:
+            old.lost_reason = "restart requested"
+            old._teardown()
+        return old._revive()
 
     # --- lifecycle ------------------------------------------------------------------
     def stop(self) -> None:
         if not self._stopped:
+            self._stopped = True
             self.pool.shutdown()
         super().stop()
+
+    @property
+    def live_pool(self):
+        """The current pool, respawned first if the last one was lost."""
+        if not self.pool.alive:
+            self.pool._revive()
+        return self.pool
 
     @property
     def executors(self) -> int:
@@ -359,8 +448,10 @@ class DriverSession(Session):
         return self.pool.n
 
     def executor_info(self) -> dict:
-        d = self.pool.info()
-        d["devices"] = list(self.pool.devices)
+        pool = self.live_pool
+        d = pool.info()
+        d["devices"] = list(pool.devices)
+        d["respawns"] = len(self.events)
         return d
 
     def __repr__(self):
@@ -398,7 +489,7 @@ class DriverSession(Session):
             names = None
         if not isinstance(data, pd.DataFrame):
             raise TypeError(f"cannot create a DataFrame from {type(data).__name__}")
-        return self.pool.scatter_dataframe(data, schema)
+        return self.live_pool.scatter_dataframe(data, schema)
 
     def range(self, start, end=None, step=1, numPartitions=None):
         return self._remote.range(start, end, step, numPartitions)

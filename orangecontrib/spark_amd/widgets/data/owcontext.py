@@ -1,4 +1,9 @@
-"""Context widget: create the shared Session (reference: widgets/data/spark_context.py:13-78)."""
+"""Context widget: create the shared Session (reference: widgets/data/spark_context.py:13-78).
+
+``spark.executor.instances`` defaults to ``auto`` = every visible MI355X (the reference's
+default cluster is 8 executors, spark_context.py:41); the info line lists the executor
+devices, and an executor loss (the pool respawns and rebuilds handles from lineage) is
+reported as a warning on this widget."""
 from collections import OrderedDict
 
 from orange3_spark_amd.conf import DEFAULTS, SessionConf
@@ -41,9 +46,24 @@ class OWSessionContext(SharedSession, Widget):
             self.saved_gui_params[key] = p.get_value()
         self.session = Session.getOrCreate(conf) if Session.active() is None else Session(conf)
         Session._active = self.session
-        self.info(repr(self.session))
+        self.warning()
+        self.info(self.describe(self.session))
+        if hasattr(self.session, "add_listener"):
+            self.session.add_listener(self._on_executor_event)
         self.hide()
         return self.session
+
+    @staticmethod
+    def describe(session) -> str:
+        pool = getattr(session, "pool", None)
+        if pool is None:
+            return f"{session!r} -- 1 in-process device: {session.device}"
+        return f"{session!r} -- {pool.n} executors: {', '.join(str(d) for d in pool.devices)}"
+
+    def _on_executor_event(self, ev):
+        self.warning(f"{ev['event']} ({ev.get('reason')}); DataFrames and models are rebuilt from their "
+                     f"sources on next use -- re-run upstream widgets for anything else")
+        self.info(self.describe(self.session))
 
     def onDeleteWidget(self):
         if self.session is not None:
