@@ -9,17 +9,22 @@ canvas, as in the reference:
   :569-582);
 * Hive Table -- database and table combo boxes filled from the catalog
   (reference widgets/data/spark_table.py:40-70);
-* Python Script -- script library list with add / remove / update, a multi-line editor
-  and a console pane showing the script's output (reference
-  widgets/data/pyspark_script_console.py:206-466).
+* Python Script -- script library list with add / remove / update / import from file /
+  save to file, an auto-indenting editor with a Python syntax highlighter, and a console
+  pane with an input line running statements in the script's namespace (reference
+  widgets/data/pyspark_script_console.py:39-132,206-466).
 
 A builder receives the Qt view (``view.core`` is the headless widget) and the
 ``orange`` namespace (``gui`` helpers and the ``qt`` widgets module); it returns the
 settings its controls cover (no generic editor is made for those) and a ``refresh``
 callable the view runs after every input and action.  Only plain QtWidgets calls are
-used (QListWidget, QComboBox, QPlainTextEdit, QLineEdit, QPushButton, QTextBrowser).
+used (QListWidget, QComboBox, QPlainTextEdit, QLineEdit, QPushButton, QTextBrowser,
+QFileDialog), plus QtGui.QSyntaxHighlighter / QtCore key codes for the script editor when
+the namespace provides ``qtgui`` / ``qtcore``.
 """
 from __future__ import annotations
+
+import os
 
 
 def _list(qt, multi=True):
@@ -171,19 +176,107 @@ def build_catalog_table(view, orange):
 
 
 # ------------------------------------------------------------------------------ script
+def _script_editor(qt, qtcore):
+    """QPlainTextEdit with the reference's auto-indent keys (PythonScriptEditor,
+    pyspark_script_console.py:100-132): Return keeps the indent (+4 after ':', -4 after
+    pass/return), Tab inserts 4 spaces, Backspace in leading blanks removes one step."""
+    if qtcore is None:
+        return qt.QPlainTextEdit()
+    from .script_support import INDENT, backspace_width, indent_after
+    K = qtcore.Qt
+
+    class ScriptEditor(qt.QPlainTextEdit):
+        def _line(self):
+            cur = self.textCursor()
+            return cur, cur.block().text()[:cur.positionInBlock()]
+
+        def keyPressEvent(self, ev):
+            k = ev.key()
+            if k in (K.Key_Return, K.Key_Enter):
+                _, line = self._line()
+                super().keyPressEvent(ev)
+                self.insertPlainText(" " * indent_after(line))
+            elif k == K.Key_Tab:
+                self.insertPlainText(" " * INDENT)
+            elif k == K.Key_Backspace:
+                cur, line = self._line()
+                if cur.hasSelection():
+                    super().keyPressEvent(ev)
+                else:
+                    for _ in range(backspace_width(line)):
+                        cur.deletePreviousChar()
+            else:
+                super().keyPressEvent(ev)
+    return ScriptEditor()
+
+
+def _highlighter(qtgui, document):
+    """QSyntaxHighlighter over script_support.highlight_spans (ref PythonSyntaxHighlighter,
+    pyspark_script_console.py:39-97)."""
+    if qtgui is None or document is None:
+        return None
+    from .script_support import FORMATS, highlight_spans
+
+    class PythonHighlighter(qtgui.QSyntaxHighlighter):
+        def __init__(self, doc):
+            super().__init__(doc)
+            self._fmt = {}
+            for name, (color, bold) in FORMATS.items():
+                f = qtgui.QTextCharFormat()
+                f.setForeground(qtgui.QColor(color.lower()))
+                if bold:
+                    f.setFontWeight(qtgui.QFont.Bold)
+                self._fmt[name] = f
+
+        def highlightBlock(self, text):
+            spans, state = highlight_spans(str(text), max(0, self.previousBlockState()))
+            for start, n, fmt in spans:
+                self.setFormat(start, n, self._fmt[fmt])
+            self.setCurrentBlockState(state)
+    return PythonHighlighter(document)
+
+
+def _console_input(qt, qtcore, core, refresh):
+    """One-line console input: Return runs the line, Up/Down walk the history."""
+    if qtcore is None:
+        line = qt.QLineEdit()
+    else:
+        K = qtcore.Qt
+
+        class ConsoleLine(qt.QLineEdit):
+            def keyPressEvent(self, ev):
+                if ev.key() == K.Key_Up:
+                    self.setText(core.console_history(-1))
+                elif ev.key() == K.Key_Down:
+                    self.setText(core.console_history(+1))
+                else:
+                    super().keyPressEvent(ev)
+        line = ConsoleLine()
+    line.setPlaceholderText(">>> run a line in the script namespace")
+
+    def run():
+        core.console_push(line.text())
+        line.setText("")
+        refresh()
+    line.returnPressed.connect(run)
+    return line
+
+
 def build_script(view, orange):
     qt, gui, core = orange.qt, orange.gui, view.core
+    qtgui, qtcore = getattr(orange, "qtgui", None), getattr(orange, "qtcore", None)
     lib_box = gui.widgetBox(view.controlArea, "Library")
     ll = lib_box.layout()
     library = _list(qt, multi=False)
     ll.addWidget(library)
     edit_box = gui.widgetBox(view.controlArea, "Script")
     el = edit_box.layout()
-    editor = qt.QPlainTextEdit()
+    editor = _script_editor(qt, qtcore)
+    highlighter = _highlighter(qtgui, editor.document() if hasattr(editor, "document") else None)
     el.addWidget(editor)
     console = qt.QTextBrowser()
-    view.mainArea.layout().addWidget(console) if getattr(view, "mainArea", None) is not None else el.addWidget(console)
-    view.script_controls = {"library": library, "editor": editor, "console": console}
+    main = view.mainArea.layout() if getattr(view, "mainArea", None) is not None else el
+    main.addWidget(console)
     state = {"busy": False}
 
     def refresh():
@@ -196,6 +289,11 @@ def build_script(view, orange):
             console.setPlainText(core.console_output)
         finally:
             state["busy"] = False
+
+    entry = _console_input(qt, qtcore, core, refresh)
+    main.addWidget(entry)
+    view.script_controls = {"library": library, "editor": editor, "console": console, "console_input": entry,
+                            "highlighter": highlighter}
 
     def selected(row):
         if state["busy"] or row is None or row < 0:
@@ -227,11 +325,33 @@ def build_script(view, orange):
     def clear_console():
         core.console_output = ""
         refresh()
+
+    def _name(got):
+        return got[0] if isinstance(got, tuple) else got
+
+    def import_file():
+        name = _name(qt.QFileDialog.getOpenFileName(view, "Open Python Script", os.path.expanduser("~/"),
+                                                    "Python files (*.py);;All files (*.*)"))
+        if name:
+            core.import_script(str(name))
+            view.currentScriptIndex = core.currentScriptIndex
+            refresh()
+
+    def save_file():
+        cur = core.libraryListSource[core.currentScriptIndex] if core.libraryListSource else {}
+        name = _name(qt.QFileDialog.getSaveFileName(view, "Save Python Script",
+                                                    cur.get("filename") or os.path.expanduser("~/"),
+                                                    "Python files (*.py);;All files (*.*)"))
+        if name:
+            core.save_script(str(name))
+            refresh()
     library.currentRowChanged.connect(selected)
     editor.textChanged.connect(edited)
     _button(qt, ll, "+", add)
     _button(qt, ll, "-", remove)
     _button(qt, ll, "Update", update)
+    _button(qt, ll, "Import a script from a file", import_file)
+    _button(qt, ll, "Save selected script to a file", save_file)
     _button(qt, el, "Clear console", clear_console)
     return {"libraryListSource", "currentScriptIndex", "scriptText"}, refresh
 

@@ -3,9 +3,17 @@ widgets/data/pyspark_script_console.py:206-466).  A script library is persisted;
 current script runs in a namespace holding ``session``/``spark`` (and the reference's
 ``sc``/``hc`` aliases), ``in_object`` and ``out_object``; ``out_object`` is READ BACK from
 that namespace after execution (the reference sent a stale copy, quirk Q4; the older
-working semantics are trash/OLDpyspark_script_console.py:489-492,641-648)."""
+working semantics are trash/OLDpyspark_script_console.py:489-492,641-648).
+
+Also as in the reference: an interactive console over the SAME namespace (lines run one
+at a time, state persists between lines and with the script, ``out_object`` is read
+back; ``code.InteractiveConsole`` semantics of trash/OLDpyspark_script_console.py:125-286),
+"Import a script from a file" / "Save selected script to a file"
+(pyspark_script_console.py:286-291,368-392,441-461); the Qt view adds the syntax
+highlighter and the auto-indenting editor (script_support.py, ref :39-132)."""
 import contextlib
 import io
+import os
 import traceback
 
 from ..base import SharedSession
@@ -31,6 +39,7 @@ class OWScript(SharedSession, Widget):
         self.out_object = None
         self.console_output = ""
         self.namespace = {}
+        self._console = None
 
     # -- library ---------------------------------------------------------------
     def add_script(self, name, script):
@@ -53,6 +62,34 @@ class OWScript(SharedSession, Widget):
             self.libraryListSource[index] = dict(self.libraryListSource[index], script=script)
             self.scriptText = None
 
+    def import_script(self, path: str) -> int:
+        """Add the file as a new library entry named after it (ref onAddScriptFromFile)."""
+        with open(path, "rb") as f:
+            text = f.read().decode("utf-8", errors="ignore")
+        self.libraryListSource.append({"name": os.path.basename(path), "script": text,
+                                       "filename": os.path.abspath(path)})
+        self.currentScriptIndex = len(self.libraryListSource) - 1
+        self.scriptText = None
+        return self.currentScriptIndex
+
+    def save_script(self, path: str | None = None, index: int | None = None) -> str:
+        """Write the selected script (the editor text when it is the current one) to
+        ``path`` (default: the file it was imported from / saved to); ``.py`` is added when
+        the name has no extension (ref saveScript)."""
+        index = self.currentScriptIndex if index is None else index
+        entry = self.libraryListSource[index] if 0 <= index < len(self.libraryListSource) else {}
+        path = path or entry.get("filename")
+        if not path:
+            raise ValueError("no file name given for the script")
+        if not os.path.splitext(path)[1]:
+            path += ".py"
+        text = self.current_script() if index == self.currentScriptIndex else entry.get("script", "")
+        with open(path, "w", encoding="utf-8") as f:
+            f.write(text)
+        if entry:
+            self.libraryListSource[index] = dict(entry, filename=os.path.abspath(path))
+        return path
+
     def current_script(self) -> str:
         if self.scriptText is not None:
             return self.scriptText
@@ -66,10 +103,46 @@ class OWScript(SharedSession, Widget):
         if self.auto_commit:
             self.commit()
 
-    def commit(self):
+    # -- interactive console -------------------------------------------------------
+    def _bind(self):
         ns = self.namespace
         ns.update(session=self.session, spark=self.session, sc=self.sc, hc=self.session,
                   in_object=self.in_object, out_object=self.out_object)
+        return ns
+
+    @property
+    def console(self):
+        from ..script_support import ScriptConsole, banner
+        if self._console is None:
+            self._console = ScriptConsole(self.namespace, self._console_write, banner(self.session))
+        return self._console
+
+    def _console_write(self, data):
+        self.console_output += data
+
+    def console_push(self, line: str) -> bool:
+        """Run one console line in the widget namespace; True while a block is open."""
+        con = self.console
+        if not con.more:
+            self._bind()
+        more = con.push(line)
+        self.out_object = self.namespace.get("out_object")
+        return more
+
+    def console_paste(self, source: str) -> bool:
+        con = self.console
+        if not con.more:
+            self._bind()
+        more = con.paste(source)
+        self.out_object = self.namespace.get("out_object")
+        return more
+
+    def console_history(self, step: int) -> str:
+        """Previous (step < 0) / next (step > 0) console line."""
+        return self.console.history_prev() if step < 0 else self.console.history_next()
+
+    def commit(self):
+        ns = self._bind()
         buf = io.StringIO()
         self.error()
         with contextlib.redirect_stdout(buf), contextlib.redirect_stderr(buf):

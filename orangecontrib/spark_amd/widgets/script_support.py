@@ -1,0 +1,174 @@
+"""Python-script tooling of the Script widget, Qt-free so it is testable headless.
+
+Reference: orangecontrib/spark/widgets/data/pyspark_script_console.py --
+``PythonSyntaxHighlighter`` (:39-97), ``PythonScriptEditor`` auto-indent (:100-132) and the
+interactive console.  The console follows the reference's older, working
+``PySparkConsole`` (trash/OLDpyspark_script_console.py:125-286): a
+``code.InteractiveConsole`` over the widget namespace, so lines typed there see and set
+``out_object``, with history and multi-line paste.  The Qt view (custom_views.py) wraps
+these in a ``QSyntaxHighlighter`` subclass, a ``QPlainTextEdit`` with the indent keys
+and an input line under the console pane.
+"""
+from __future__ import annotations
+
+import code
+import contextlib
+import keyword
+import re
+import sys
+
+INDENT = 4
+
+# -------------------------------------------------------------------------- highlighter
+# span formats (the Qt view maps them to QTextCharFormat: colour, weight)
+FORMATS = {"keyword": ("blue", True), "def": ("black", True), "string": ("darkGreen", False),
+           "comment": ("lightGray", False), "decorator": ("darkGray", False), "number": ("darkMagenta", False)}
+
+_RULES = [(re.compile(r"\b(?:%s)\b" % "|".join(keyword.kwlist)), "keyword", 0),
+          (re.compile(r"\bdef\s+([A-Za-z_][A-Za-z0-9_]*)\s*\("), "def", 1),
+          (re.compile(r"\bclass\s+([A-Za-z_][A-Za-z0-9_]*)\s*[(:]"), "def", 1),
+          (re.compile(r"\b\d+(?:\.\d*)?(?:[eE][-+]?\d+)?\b"), "number", 0),
+          (re.compile(r"@[A-Za-z_][A-Za-z0-9_.]*"), "decorator", 0)]
+_STRING = re.compile(r"'(?:[^'\\]|\\.)*'|\"(?:[^\"\\]|\\.)*\"")
+_TRIPLE = re.compile(r"'''|\"\"\"")
+
+
+def highlight_spans(text: str, prev_state: int = 0):
+    """Spans ``[(start, length, format)]`` of one line and the block state to carry into
+    the next line (1 = inside a triple-quoted string opened by ``'''`` , 2 = by
+    ``\"\"\"``).  Later spans override earlier ones (QSyntaxHighlighter.setFormat order):
+    rules, then strings, then comments, then triple-quoted strings."""
+    spans = []
+    for rx, fmt, grp in _RULES:
+        for m in rx.finditer(text):
+            spans.append((m.start(grp), m.end(grp) - m.start(grp), fmt))
+    comment_at = None
+    for m in _STRING.finditer(text):
+        spans.append((m.start(), m.end() - m.start(), "string"))
+    # a '#' outside any string starts a comment
+    masked = _STRING.sub(lambda m: " " * (m.end() - m.start()), text)
+    i = masked.find("#")
+    if i >= 0:
+        comment_at = i
+        spans.append((i, len(text) - i, "comment"))
+    state, pos = prev_state, 0
+    if state:                                   # continue an open triple-quoted string
+        close = "'''" if state == 1 else '"""'
+        j = text.find(close)
+        if j < 0:
+            return [(0, len(text), "string")], state
+        spans.append((0, j + 3, "string"))
+        pos, state = j + 3, 0
+    while True:
+        m = _TRIPLE.search(text, pos)
+        if m is None or (comment_at is not None and m.start() > comment_at):
+            break
+        q = m.group(0)
+        j = text.find(q, m.end())
+        if j < 0:
+            spans.append((m.start(), len(text) - m.start(), "string"))
+            return spans, 1 if q == "'''" else 2
+        spans.append((m.start(), j + 3 - m.start(), "string"))
+        pos = j + 3
+    return spans, 0
+
+
+# ------------------------------------------------------------------------------- editor
+def indent_after(line: str) -> int:
+    """Indent (spaces) of the line opened by Return after ``line`` (reference
+    PythonScriptEditor.keyPressEvent: keep the indent, +4 after ':', -4 after ``pass`` /
+    ``return``)."""
+    indent = len(line) - len(line.lstrip(" "))
+    st = line.strip()
+    if st == "pass" or st.startswith("return ") or st == "return" or st in ("break", "continue") \
+            or st.startswith("raise "):
+        return max(0, indent - INDENT)
+    if st.endswith(":") and not st.startswith("#"):
+        return indent + INDENT
+    return indent
+
+
+def backspace_width(line_before_cursor: str) -> int:
+    """Characters one Backspace deletes: a whole indent step inside leading blanks."""
+    if line_before_cursor and not line_before_cursor.strip():
+        return min(INDENT, len(line_before_cursor)) or 1
+    return 1
+
+
+# ------------------------------------------------------------------------------ console
+class ScriptConsole(code.InteractiveConsole):
+    """Interactive interpreter over a shared namespace.  ``push`` runs one line (returns
+    True while a block is incomplete); everything printed goes to ``write``; a transcript
+    with ``>>> `` / ``... `` prompts is kept as the console text."""
+
+    def __init__(self, namespace: dict, write, banner: str | None = None):
+        super().__init__(namespace, filename="<console>")
+        self._write = write
+        self.history: list[str] = []
+        self._hpos = 0
+        self.more = False
+        if banner:
+            self.write(banner if banner.endswith("\n") else banner + "\n")
+
+    @property
+    def prompt(self) -> str:
+        return "... " if self.more else ">>> "
+
+    def write(self, data):
+        self._write(data)
+
+    def push(self, line: str) -> bool:
+        self.write(self.prompt + line + "\n")
+        if line.strip() and (not self.history or self.history[-1] != line):
+            self.history.append(line)
+        self._hpos = len(self.history)
+        out = _Writer(self.write)
+        with contextlib.redirect_stdout(out), contextlib.redirect_stderr(out):
+            try:
+                self.more = bool(super().push(line))
+            except SystemExit:
+                self.resetbuffer()
+                self.more = False
+        return self.more
+
+    def paste(self, source: str) -> bool:
+        """Run pasted source line by line (reference pasteCode).  Unlike a bare REPL, a
+        top-level line after an indented block first closes the block (as a file would run),
+        and a trailing blank line closes a block left open."""
+        for line in source.splitlines():
+            if self.more and line and not line[0].isspace() and not _CONTINUES.match(line):
+                self.push("")
+            self.push(line)
+        if self.more:
+            self.push("")
+        return self.more
+
+    def history_prev(self) -> str:
+        if not self.history:
+            return ""
+        self._hpos = max(0, self._hpos - 1)
+        return self.history[self._hpos]
+
+    def history_next(self) -> str:
+        if not self.history:
+            return ""
+        self._hpos = min(len(self.history), self._hpos + 1)
+        return self.history[self._hpos] if self._hpos < len(self.history) else ""
+
+
+_CONTINUES = re.compile(r"(?:elif|else|except|finally|case)\b|[)\]}]")
+
+
+class _Writer:
+    def __init__(self, write):
+        self.write = write
+
+    def flush(self):
+        pass
+
+
+def banner(session) -> str:
+    v = getattr(session, "version", "?")
+    return (f"Python {sys.version.split()[0]} on {sys.platform}\n"
+            f"orange3-spark-amd {v}: session available as session / spark (sc, hc aliases); "
+            f"in_object, out_object\n")

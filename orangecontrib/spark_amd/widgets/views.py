@@ -73,19 +73,20 @@ def qt_view(core_cls, orange=None):
     """Build the Qt ``OWWidget`` class for headless widget ``core_cls``.
 
     ``orange`` is a namespace with ``widget``, ``settings``, ``gui`` and ``qt`` (the
-    AnyQt.QtWidgets module); by default the real Orange/AnyQt modules are imported.
+    AnyQt.QtWidgets module; optionally ``qtgui`` / ``qtcore`` for the script editor's
+    highlighter and key handling); by default the real Orange/AnyQt modules are imported.
     """
     if orange is None:
         from types import SimpleNamespace
 
-        from AnyQt import QtWidgets
+        from AnyQt import QtCore, QtGui, QtWidgets
         from Orange.widgets import gui, settings, widget
         try:
             from Orange.widgets.utils.concurrent import ConcurrentWidgetMixin
         except ImportError:  # older Orange: run the action on the GUI thread
             ConcurrentWidgetMixin = None
         orange = SimpleNamespace(widget=widget, settings=settings, gui=gui, qt=QtWidgets,
-                                 concurrent=ConcurrentWidgetMixin)
+                                 qtgui=QtGui, qtcore=QtCore, concurrent=ConcurrentWidgetMixin)
     W, S, Qt = orange.widget, orange.settings, orange.qt
     Mixin = getattr(orange, "concurrent", None)
 

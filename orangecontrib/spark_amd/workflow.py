@@ -85,6 +85,7 @@ class Node:
     title: str
     properties: dict = field(default_factory=dict)
     widget: Widget | None = None
+    position: tuple = (0.0, 0.0)
 
 
 @dataclass
@@ -101,14 +102,25 @@ class Workflow:
         self.title, self.description = title, description
         self.nodes: dict[str, Node] = {}
         self.links: list[Link] = []
+        # canvas annotations: ("text", rect(x, y, w, h), text, font_size) or
+        # ("arrow", start(x, y), end(x, y), fill colour)
+        self.annotations: list[tuple] = []
         self.manager = SignalManager()
 
     # -- construction ------------------------------------------------------------
-    def add_node(self, qualified_name, title=None, properties=None, node_id=None) -> Node:
+    def add_node(self, qualified_name, title=None, properties=None, node_id=None, position=None) -> Node:
         nid = str(node_id if node_id is not None else len(self.nodes))
         n = Node(nid, qualified_name, title or qualified_name.rsplit(".", 1)[-1], dict(properties or {}))
+        if position is not None:
+            n.position = tuple(float(v) for v in position)
         self.nodes[nid] = n
         return n
+
+    def add_text(self, rect, text, font_size=16):
+        self.annotations.append(("text", tuple(float(v) for v in rect), str(text), int(font_size)))
+
+    def add_arrow(self, start, end, fill="#C1272D"):
+        self.annotations.append(("arrow", tuple(float(v) for v in start), tuple(float(v) for v in end), str(fill)))
 
     def add_link(self, source, source_channel, sink, sink_channel, enabled=True):
         self.links.append(Link(str(source), source_channel, str(sink), sink_channel, enabled))
@@ -118,7 +130,23 @@ class Workflow:
         root = ET.parse(path).getroot()
         wf = cls(root.get("title", ""), root.get("description", ""))
         for n in root.iter("node"):
-            wf.add_node(n.get("qualified_name"), n.get("title"), node_id=n.get("id"))
+            pos = None
+            try:
+                pos = ast.literal_eval(n.get("position") or "None")
+            except (ValueError, SyntaxError):
+                pass
+            wf.add_node(n.get("qualified_name"), n.get("title"), node_id=n.get("id"),
+                        position=pos if isinstance(pos, tuple) and len(pos) == 2 else None)
+        for a in root.iter("text"):
+            try:
+                wf.add_text(ast.literal_eval(a.get("rect")), a.text or "", int(a.get("font-size", "16")))
+            except (ValueError, SyntaxError, TypeError):
+                pass
+        for a in root.iter("arrow"):
+            try:
+                wf.add_arrow(ast.literal_eval(a.get("start")), ast.literal_eval(a.get("end")), a.get("fill", "#C1272D"))
+            except (ValueError, SyntaxError, TypeError):
+                pass
         for ln in root.iter("link"):
             wf.add_link(ln.get("source_node_id"), ln.get("source_channel"), ln.get("sink_node_id"),
                         ln.get("sink_channel"), ln.get("enabled", "true") == "true")
@@ -140,12 +168,20 @@ class Workflow:
         for n in self.nodes.values():
             ET.SubElement(nodes, "node", {"id": n.id, "name": n.title, "qualified_name": n.qualified_name,
                                           "project_name": "Orange3-Spark-AMD", "title": n.title, "version": "",
-                                          "position": "(0.0, 0.0)"})
+                                          "position": repr(tuple(n.position))})
         links = ET.SubElement(root, "links")
         for i, ln in enumerate(self.links):
             ET.SubElement(links, "link", {"id": str(i), "source_node_id": ln.source, "sink_node_id": ln.sink,
                                           "source_channel": ln.source_channel, "sink_channel": ln.sink_channel,
                                           "enabled": "true" if ln.enabled else "false"})
+        ann = ET.SubElement(root, "annotations")
+        for i, a in enumerate(self.annotations):
+            if a[0] == "text":
+                e = ET.SubElement(ann, "text", {"id": str(i), "rect": repr(a[1]), "font-family": "Helvetica",
+                                                "font-size": str(a[3])})
+                e.text = a[2]
+            else:
+                ET.SubElement(ann, "arrow", {"id": str(i), "start": repr(a[1]), "end": repr(a[2]), "fill": a[3]})
         props = ET.SubElement(root, "node_properties")
         for n in self.nodes.values():
             d = n.widget.settings_dict() if n.widget is not None else n.properties

@@ -221,9 +221,14 @@ class _FakeLineEdit:
     def __init__(self, text=""):
         self._text = text
         self.textChanged = _Signal()
+        self.returnPressed = _Signal()
 
     def setPlaceholderText(self, t):
         self.ph = t
+
+    def enter(self, t):                       # test helper: the user types a line + Return
+        self.setText(t)
+        self.returnPressed.emit()
 
     def setToolTip(self, t):
         self.tip = t
@@ -239,12 +244,26 @@ class _FakeLineEdit:
         self.textChanged.emit(t)
 
 
+class _FileDialog:
+    """QFileDialog static helpers (Qt5: return (filename, selected_filter))."""
+    next_open = next_save = ""
+
+    @staticmethod
+    def getOpenFileName(parent, caption, directory, filt):
+        return (_FileDialog.next_open, filt)
+
+    @staticmethod
+    def getSaveFileName(parent, caption, directory, filt):
+        return (_FileDialog.next_save, filt)
+
+
 @pytest.fixture()
 def orange():
     return SimpleNamespace(widget=SimpleNamespace(OWWidget=_OWWidget, Input=_Sig, Output=_Sig),
                            settings=SimpleNamespace(Setting=_Setting), gui=_fake_gui(),
                            qt=SimpleNamespace(QTextBrowser=_QEdit, QLabel=_QW, QComboBox=_QCombo, QLineEdit=_FakeLineEdit,
                                               QListWidget=_QList, QPushButton=_QButton, QPlainTextEdit=_QEdit,
+                                              QFileDialog=_FileDialog,
                                               QAbstractItemView=SimpleNamespace(ExtendedSelection=3)),
                            concurrent=None)
 
@@ -424,6 +443,28 @@ def test_script_view_library_editor_and_console(orange, session):
     assert w.core.libraryListSource[0]["script"] == "out_object = 'changed'"
     _click(w, "-")
     assert sc["library"].items == ["Script 2"]
+
+
+def test_script_view_console_import_and_save(orange, session, tmp_path):
+    from orangecontrib.spark_amd.widgets.data.owscript import OWScript
+    V = qt_view(OWScript, orange)
+    w = V()
+    sc = w.script_controls
+    w._refresh_editors()
+    sc["console_input"].enter("x = 20")
+    sc["console_input"].enter("out_object = x + 1")
+    assert w.core.out_object == 21 and ">>> out_object = x + 1" in sc["console"].text
+    src = tmp_path / "job.py"
+    src.write_text("out_object = x * 2\n")
+    _FileDialog.next_open = str(src)
+    _click(w, "Import a script from a file")
+    assert sc["library"].items[-1] == "job.py" and sc["editor"].text == "out_object = x * 2\n"
+    w.run_action()                                        # the script sees the console's x
+    assert V.Outputs.out_object.sent[-1] == 40
+    sc["editor"].type("out_object = 'saved'\n")
+    _FileDialog.next_save = str(tmp_path / "copy")
+    _click(w, "Save selected script to a file")
+    assert (tmp_path / "copy.py").read_text() == "out_object = 'saved'\n"
 
 
 def test_tutorial_names_are_the_classes_orange_registers(orange):

@@ -215,3 +215,26 @@ def test_csv_io_roundtrip_fixes_reference_quirks():
     header, rows = load_csvIO(save_csv_IO(t))
     assert header == ["a", "k", "s"]
     assert rows[0][0] == 1.5 and rows[1][2] is None and rows[2][2] == "z"
+
+
+def test_tutorial_has_reference_layout_and_annotations():
+    """The shipped tutorial places its 8 nodes where the reference does
+    (orangecontrib/spark/tutorials/spark_ml.ows:4-11) and carries its instructional
+    annotations (:22-37), so the canvas opens a readable workflow."""
+    import ast
+    import os
+    import xml.etree.ElementTree as ET
+    from orangecontrib.spark_amd.workflow import Workflow
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(root, "orangecontrib", "spark_amd", "tutorials", "spark_ml.ows")
+    tree = ET.parse(path).getroot()
+    pos = [ast.literal_eval(n.get("position")) for n in tree.iter("node")]
+    assert len(pos) == 8 and len(set(pos)) == 8
+    assert dict(zip([n.get("title") for n in tree.iter("node")], pos))["Evaluation"] == (641.0, 397.0)
+    texts = " ".join(t.text for t in tree.iter("text"))
+    for phrase in ("First, create the session", "features and the label column", "obtain a fitted model",
+                   "Apply the fitted model to the testing dataset", "measures"):
+        assert phrase in texts
+    assert len(list(tree.iter("arrow"))) == 7
+    wf = Workflow.load(path)                       # positions / annotations round-trip
+    assert wf.nodes["3"].position == (341.0, 247.0) and len(wf.annotations) == 13
