@@ -437,7 +437,9 @@ def fit_sgd(data: GlmData, loss: str, reg=0.0, alpha=0.0, fit_intercept=True, st
     else:
         mean, var, W, ymean, _ = data.moments()
     std = np.sqrt(var)
-    b0 = _initial_intercept(loss, fit_intercept, ymean, init_intercept)
+    # mllib GradientDescent starts from all-zero weights, intercept included (the L-BFGS
+    # path's log-odds / mean start is a Spark ML LogisticRegression convention, not mllib's)
+    b0 = float(init_intercept) if (fit_intercept and init_intercept is not None) else 0.0
     sgd = DeviceSGD(data, loss, reg, fit_intercept, step_size, standardization, std, elastic_net=alpha,
                     mini_batch_fraction=frac, seed=seed, init_intercept=b0)
     setup_s = time.time() - t0
@@ -695,6 +697,10 @@ class DeviceSGD:
             return
         d = self.data
         if mode != "force" and d.n_local * d.ld * 2 > self.GRAPH_MAX_BYTES:
+            return
+        if d.comm.world_size > 1 and mode != "all":
+            # multi-rank: pass and update graphs around an eager RCCL all-reduce are opt-in
+            # (O3S_SGD_GRAPH=all) until exercised on a multi-GPU RCCL group
             return
         try:
             if d.comm.world_size == 1:

@@ -127,7 +127,22 @@ PAIR_FROM: float | None = None
 SCREEN_MAX_FLAG_FRACTION = 0.5
 SPLIT_REPROBE = 6             # split calls before the pair screen is tried again
 SCREEN_TT = 0                 # 32-row tiles per wave in the screen kernel (0: by D)
-_screen_state: dict = {}      # (data_ptr, shape, Cpad) -> (mode, flagged fraction, countdown)
+_screen_state: dict = {}      # (id(X), shape, Cpad) -> (weakref to X, mode, flagged fraction, countdown)
+
+
+def _state_get(key, X):
+    e = _screen_state.get(key)
+    if e is None or e[0]() is not X:          # a new tensor (maybe at a reused address)
+        return ("screen", 0.0, 0)
+    return e[1:]
+
+
+def _state_set(key, X, *val):
+    import weakref
+    if len(_screen_state) > 64:
+        for k in [k for k, e in _screen_state.items() if e[0]() is None]:
+            del _screen_state[k]
+    _screen_state[key] = (weakref.ref(X),) + val
 
 
 class _ScreenWs:
@@ -173,14 +188,14 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
     # near-tie rates depend on the centre set: keyed by the padded centre count too, so
     # k-means|| candidate passes (thousands of close candidates: mostly near ties) do not
     # push the later Lloyd iterations (k centres) onto the split path
-    key = (X.data_ptr(), tuple(X.shape), P.hi.shape[0])
+    key = (id(X), tuple(X.shape), P.hi.shape[0])
     if mode == "auto":
-        m, f, cd = _screen_state.get(key, ("screen", 0.0, 0))
+        m, f, cd = _state_get(key, X)
         if not screen_ok(X):
             mode = "split"
         elif m == "split" and cd > 0:
             mode = "split"
-            _screen_state[key] = ("split", f, cd - 1)
+            _state_set(key, X, "split", f, cd - 1)
         else:
             mode = ("pair" if PAIR_FROM is not None else "screen") if m == "split" else m
     if stats is not None:
@@ -199,11 +214,11 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
         m = int(cnt.item())                      # the near-tie count sizes the re-solve grid
         frac = m / max(n, 1)
         if mode == "screen" and PAIR_FROM is not None and frac > PAIR_FROM:
-            _screen_state[key] = ("pair", frac, 0)
+            _state_set(key, X, "pair", frac, 0)
         elif frac > SCREEN_MAX_FLAG_FRACTION:
-            _screen_state[key] = ("split", frac, SPLIT_REPROBE)
+            _state_set(key, X, "split", frac, SPLIT_REPROBE)
         else:
-            _screen_state[key] = (mode, frac, 0)
+            _state_set(key, X, mode, frac, 0)
         if stats is not None:
             stats["flagged"] = m
         if m:

@@ -1666,7 +1666,8 @@ def bit_xor(c): return Agg("bit_xor", _e(c), f"bit_xor({_e(c).name})")
 
 
 def bit_count(c):
-    """Set bits of the 64-bit two's-complement value (Spark BitwiseCount)."""
+    """Set bits of the value sign-extended to 64 bits (Spark BitwiseCount evaluates
+    java.lang.Long.bitCount for every integral input type)."""
     return _host_map("bit_count", lambda v: builtins.bin(int(v) & 0xFFFFFFFFFFFFFFFF).count("1"), c, kind="int")
 
 
@@ -1779,8 +1780,10 @@ def try_multiply(a, b): return _e(a) * _e(b)
 
 
 def url_encode(c):
+    """application/x-www-form-urlencoded as java.net.URLEncoder (UTF-8): letters, digits
+    and ``.-*_`` stay, space -> ``+``, everything else (``~`` included) is %XX."""
     from urllib.parse import quote_plus
-    return _host_map("url_encode", lambda s: quote_plus(str(s)), c)
+    return _host_map("url_encode", lambda s: quote_plus(str(s), safe="*").replace("~", "%7E"), c)
 
 
 def url_decode(c):
@@ -2044,7 +2047,18 @@ char = chr
 
 
 def shiftrightunsigned(c, numBits: int):
-    return _host_map("shiftrightunsigned", lambda v: (int(v) & 0xFFFFFFFFFFFFFFFF) >> int(numBits), c, kind="int")
+    """``>>>`` at the column's width (Spark ShiftRightUnsigned: Java ``>>>`` on an int for
+    byte/short/int columns, on a long for bigint), the shift taken mod the width."""
+    e = _e(c)
+
+    def f(df):
+        col = e.eval(df)
+        narrow = isinstance(col, C.NumericColumn) and col.data.dtype in (torch.int8, torch.int16, torch.int32)
+        bits, mask = (32, 0xFFFFFFFF) if narrow else (64, 0xFFFFFFFFFFFFFFFF)
+        k = int(numBits) % bits
+        vals = _host(col, len(df))
+        return _num_out([None if v is None else (int(v) & mask) >> k for v in vals], torch.int64, df.device)
+    return Expr(f, f"shiftrightunsigned({e.name}, {int(numBits)})", _refs(e))
 
 
 def to_binary(c, format=None):  # noqa: A002

@@ -46,6 +46,20 @@ unboundedFollowing = 1 << 62
 currentRow = 0
 
 
+HOST_FRAME_WARN_ROWS = 50_000_000
+
+
+def _warn_frame_volume(lo_n, hi_n, fn):
+    """Host-evaluated frame aggregates cost O(sum of frame sizes) for frames that differ row
+    to row (sliding ROWS frames); warn when that volume is large."""
+    vol = float(np.maximum(hi_n - lo_n + 1, 0).sum())
+    if vol > HOST_FRAME_WARN_ROWS:
+        import logging
+        logging.getLogger(__name__).warning(
+            "window %s over %.3g frame rows is evaluated on the host (O(rows x frame)); "
+            "bound the frame or aggregate with groupBy", fn, vol)
+
+
 class WindowSpec:
     def __init__(self, partition=(), order=(), frame=None):
         self._partition, self._order, self._frame = tuple(partition), tuple(order), frame
@@ -401,16 +415,32 @@ class _Ctx:
         if a.fn == "collect_list":
             vals = c.to_pylist()
             lo_n, hi_n = lo.cpu().numpy(), hi.cpu().numpy()
+            _warn_frame_volume(lo_n, hi_n, a.fn)
+            memo: dict = {}
             arr = np.empty(self.n, dtype=object)
-            arr[:] = [[v for v in vals[x:y + 1] if v is not None] for x, y in zip(lo_n, hi_n)]
+            out = []
+            for x, y in zip(lo_n, hi_n):
+                k = (int(x), int(y))
+                if k not in memo:
+                    memo[k] = [v for v in vals[x:y + 1] if v is not None]
+                out.append(list(memo[k]))
+            arr[:] = out
             return C.ArrayColumn(arr)
         if a.fn in _HOST_FRAME_AGGS or (a.distinct and a.fn in ("count", "sum", "avg")):
             # order statistics / sets / products: the group-by finaliser on every row's frame
             from ..frame.groupby import _host_final, _result_column
             vals = list(c.values) if isinstance(c, C.HostColumn) else c.to_pylist()
             lo_n, hi_n = lo.cpu().numpy(), hi.cpu().numpy()
-            res = [_host_final(a, list(enumerate(vals[x:y + 1])) if y >= x else []) for x, y in zip(lo_n, hi_n)]
-            return _result_column(a, res)
+            _warn_frame_volume(lo_n, hi_n, a.fn)
+            memo: dict = {}                 # rows sharing a frame (peer groups, whole partitions) share one result
+
+            def one(x, y):
+                k = (int(x), int(y))
+                r = memo.get(k, memo)
+                if r is memo:
+                    r = memo[k] = _host_final(a, list(enumerate(vals[x:y + 1])) if y >= x else [])
+                return r
+            return _result_column(a, [one(x, y) for x, y in zip(lo_n, hi_n)])
         if not isinstance(c, C.NumericColumn):
             raise TypeError(f"{a.fn} over a window needs a numeric column")
         d = c.data.to(torch.float64).to(lo.device)

@@ -112,3 +112,17 @@ def test_sql_extract_from():
     q = s.sql("SELECT extract(YEAR FROM t) AS y, EXTRACT(minute FROM t) AS m, date_part('MONTH', t) AS mo, "
               "find_in_set('b', c) AS f FROM ex35").toPandas()
     assert q.to_dict("list") == {"y": [2024], "m": [20], "mo": [3], "f": [2]}
+
+
+def test_shiftrightunsigned_width_and_url_encode_java_safe_set():
+    """>>> shifts an int column as a 32-bit value and a bigint as 64-bit (Spark
+    ShiftRightUnsigned); url_encode keeps java.net.URLEncoder's safe set ('*' stays,
+    '~' is encoded)."""
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.sql import functions as F
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    df = s.createDataFrame({"a": [-1, 8], "t": ["a b~c*d", "é"]})
+    df = df.withColumn("ai", df.a.cast("int"))
+    got = df.select(F.shiftrightunsigned("ai", 28).alias("i"), F.shiftrightunsigned("a", 60).alias("l"),
+                    F.url_encode("t").alias("u")).collect()
+    assert [tuple(r) for r in got] == [(15, 15, "a+b%7Ec*d"), (0, 0, "%C3%A9")]

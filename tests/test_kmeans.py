@@ -231,3 +231,32 @@ def test_screen_scales_and_bound():
     assert P.cmax == 5.0 and P.ms == K._pow2_scale(8.0)
     ex, e0 = K.screen_bound(P, 2.0 ** 10, 2)
     assert 2 ** -8 * 5.0 <= ex < 2 ** -7 * 5.0 and 0 < e0 < 1e-5
+
+
+@pytest.mark.gpu
+def test_gpu_assign_after_address_reuse_with_larger_scale(gpu):
+    """Regression for the round-3 fault (d527171): the fp16 data scale and the screen
+    state were cached by tensor ADDRESS.  Assign on A, free it, allocate B with 1000x larger
+    values at the recycled address, assign again: B's result must match the fp64 argmin
+    (a stale scale overflows fp16 -> negative / garbage indices)."""
+    g = torch.Generator(device="cpu").manual_seed(5)
+    n, D, Kc = 40_000, 64, 96
+    CA = torch.randn(Kc, D, generator=g).to(gpu)
+    A = torch.randn(n, D, generator=g).to(gpu)
+    a0, _ = K.assign(A, CA)
+    ptr = A.data_ptr()
+    del A
+    torch.cuda.synchronize()
+    B = torch.empty(n, D, dtype=torch.float32, device=gpu)          # same size: the caching allocator reuses the block
+    B.copy_(torch.randn(n, D, generator=g).to(gpu) * 1000.0)
+    CB = CA * 1000.0
+    assert B.data_ptr() == ptr, "allocator did not recycle the address (test precondition)"
+    a1, d1 = K.assign(B, CB)
+    assert int(a1.min()) >= 0 and int(a1.max()) < Kc
+    Bd, Cd = B.double(), CB.double()
+    full = torch.cdist(Bd, Cd) ** 2
+    best = full.min(1).values
+    sel = full.gather(1, a1.long()[:, None])[:, 0]
+    assert torch.all(sel <= best * (1 + 1e-5) + 1e-6 * best.max())
+    assert (a1.long() == full.argmin(1)).float().mean() > 0.999
+    torch.testing.assert_close(d1.double(), best, rtol=1e-4, atol=1e-3 * 1000.0 ** 2)

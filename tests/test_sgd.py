@@ -46,7 +46,8 @@ def _reference(X, y, iters, step, reg=0.0, alpha=0.0, frac=1.0, seed=0, loss="lo
     std = np.sqrt(np.maximum(((X * X).sum(0) - W * mean ** 2) / (W - 1), 0))
     inv = np.where(std > 0, 1 / np.where(std > 0, std, 1), 0)
     ym = y.mean()
-    b = math.log(ym / (1 - ym)) if loss == "logistic" else 0.0
+    b = 0.0                                   # mllib GradientDescent: all-zero start
+    _ = ym
     bt = np.zeros(d)
     l2, l1 = reg * (1 - alpha), reg * alpha
     for t in range(1, iters + 1):
