@@ -167,6 +167,9 @@ def main(argv=None):
             "lineage_rows": int(tot_lineage),
             "device": str(s.device) if on_gpu else "cpu",
         },
+        # how the rows reach each pass: HBM-resident, plus (N = 1) rows regenerated in-kernel
+        # from their lineage; "streamed" (pinned host -> HBM) is tools/bench_streamed.py
+        "mode": "resident" if tot_lineage == 0 else "resident+lineage",
         "fit_setup_ms": setup * 1e3,
         "fit_setup_share": setup / elapsed if elapsed > 0 else None,
         "hbm_only_rows_per_s": hbm_rate,

@@ -85,9 +85,19 @@ class Row(tuple):
 
 
 class StorageLevel:
+    """Spark storage levels.  MEMORY_ONLY pins rows in HBM (rows beyond the budget of a
+    synthetic table are recomputed from lineage); MEMORY_AND_DISK keeps the rows of dense
+    vector columns beyond the HBM budget in pinned host memory and streams them through the
+    GPU on every pass (frame/spill.py); DISK_ONLY keeps all of them on the host."""
     NONE = "NONE"
     MEMORY_ONLY = "MEMORY_ONLY"
+    MEMORY_ONLY_2 = "MEMORY_ONLY_2"
     MEMORY_AND_DISK = "MEMORY_AND_DISK"
+    MEMORY_AND_DISK_2 = "MEMORY_AND_DISK_2"
+    MEMORY_AND_DISK_DESER = "MEMORY_AND_DISK_DESER"
+    DISK_ONLY = "DISK_ONLY"
+    DISK_ONLY_2 = "DISK_ONLY_2"
+    OFF_HEAP = "OFF_HEAP"
 
 
 class DataFrame(DataFrameExtras, DataFrameExtras2):
@@ -522,10 +532,29 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
         return self
 
     def persist(self, storageLevel=None) -> "DataFrame":
-        return self.cache()
+        """``MEMORY_AND_DISK`` / ``DISK_ONLY`` (and their variants): rows of dense vector
+        columns beyond the HBM budget (``o3s.storage.hbmBudget`` bytes; default
+        ``o3s.memory.fraction`` of the HBM this frame's vectors and the free memory span)
+        move to pinned host memory and are streamed on every pass; other levels pin in HBM
+        (:meth:`cache`)."""
+        lvl = str(storageLevel if storageLevel is not None else StorageLevel.MEMORY_AND_DISK).upper()
+        self.cache()
+        if "DISK" in lvl or lvl == StorageLevel.OFF_HEAP:
+            from . import spill
+            budget = None
+            if self.session.conf.get("o3s.storage.hbmBudget", None) in (None, "", "auto") \
+                    and self.device.type == "cuda":
+                free, _ = torch.cuda.mem_get_info(self.device)
+                mine = sum(c.data.numel() * c.data.element_size() for c in self._cols.values()
+                           if isinstance(c, C.VectorColumn))
+                budget = int((free + mine) * self.session.conf.memory_fraction())
+            spill.spill_to_budget(self, budget, disk_only=lvl.startswith("DISK_ONLY"))
+        self._level = lvl
+        return self
 
     def unpersist(self, blocking=False) -> "DataFrame":
         self._cached = False
+        self._level = None
         return self
 
     @property
@@ -534,6 +563,9 @@ class DataFrame(DataFrameExtras, DataFrameExtras2):
 
     @property
     def storageLevel(self):
+        lvl = getattr(self, "_level", None)
+        if lvl is not None and self._cached:
+            return lvl
         return StorageLevel.MEMORY_ONLY if self._cached else StorageLevel.NONE
 
     # ------------------------------------------------------------------ gathering

@@ -1,0 +1,264 @@
+"""MEMORY_AND_DISK storage: feature rows beyond the HBM budget live in pinned host memory
+and stream through the GPU on every pass.
+
+Reference: ``df.cache()`` (orangecontrib/spark/widgets/data/spark_df_cache.py:39) and the
+estimators' repeated passes (spark_ml_estimator.py:22).  Spark's default storage level
+spills partitions that do not fit in executor memory and streams them back on each use;
+on MI355X the "memory" tier is 288 GB of HBM3E per GPU and the "disk" tier is pinned host
+DRAM behind PCIe.  Design:
+
+* :class:`SpilledVectorColumn` -- a vector column whose first ``resident_rows`` rows are
+  a device matrix and whose remaining rows are one pinned host matrix.
+* :class:`HostStreamer` -- double-buffered H2D streaming of the host rows in fixed-size
+  chunks on a dedicated copy stream: chunk i+1 is copied while the consumer's kernels run
+  on chunk i; copies and kernels are ordered by HIP events only (no host synchronisation
+  per chunk), and a staging buffer is refilled only after the kernels that read it
+  finished (``free`` event).  Consumers: the GLM pass (models/glm.py) and the KMeans
+  assign/update pass (models/kmeans.py).
+* :func:`spill_to_budget` -- ``DataFrame.persist(MEMORY_AND_DISK)``: moves the rows of
+  device vector columns beyond the HBM budget (``o3s.storage.hbmBudget`` bytes, default
+  the session's ``o3s.memory.fraction`` of free HBM) to pinned host memory.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from . import column as C
+
+CHUNK_BYTES = int(os.environ.get("O3S_SPILL_CHUNK_MB", "512")) << 20
+
+
+class SpilledVectorColumn(C.VectorColumn):
+    """Dense vectors: rows [0, resident) on the device (``data``), rows [resident, n) in
+    pinned host memory (``host``), same dtype and leading dimension."""
+
+    max_materialise_bytes = 32 << 30
+
+    def __init__(self, resident: torch.Tensor, host: torch.Tensor, size: int | None = None):
+        super().__init__(resident, size)
+        if host.dim() != 2 or host.shape[1] != resident.shape[1] or host.dtype != resident.dtype:
+            raise ValueError("host rows must match the resident rows' width and dtype")
+        self.host = host
+
+    def __len__(self):
+        return int(self.data.shape[0] + self.host.shape[0])
+
+    @property
+    def resident_rows(self) -> int:
+        return int(self.data.shape[0])
+
+    @property
+    def spilled_rows(self) -> int:
+        return int(self.host.shape[0])
+
+    def full(self) -> torch.Tensor:
+        nbytes = len(self) * self.ld * self.data.element_size()
+        if nbytes > self.max_materialise_bytes and self.data.is_cuda:
+            raise MemoryError(f"materialising {nbytes / 2**30:.1f} GiB of spilled rows on the device; consume "
+                              "this column with a streaming op (GLM / KMeans fits) or sample / limit first")
+        return torch.cat([self.data, self.host.to(self.data.device)])
+
+    def dense(self):
+        f = self.full()
+        return f if self.size == self.ld else f[:, : self.size]
+
+    def take(self, idx):
+        idx = idx.to(torch.int64)
+        dev = self.data.device
+        out = torch.empty((idx.numel(), self.ld), dtype=self.data.dtype, device=dev)
+        nr = self.resident_rows
+        idx_d = idx.to(dev)
+        on_dev = idx_d < nr
+        if bool(on_dev.any()):
+            out[on_dev] = self.data[idx_d[on_dev]]
+        off = ~on_dev
+        if bool(off.any()):
+            hi = (idx_d[off] - nr).cpu()
+            out[off] = self.host[hi].to(dev)
+        return C.VectorColumn(out, self.size)
+
+    def mask_select(self, mask):
+        return self.take(torch.nonzero(mask.to(self.data.device)).reshape(-1))
+
+    def slice(self, start, end):
+        n = len(self)
+        start, end = max(0, start), min(n, end)
+        nr = self.resident_rows
+        if end <= nr:
+            return C.VectorColumn(self.data[start:end], self.size)
+        if start >= nr:
+            return SpilledVectorColumn(self.data[:0], self.host[start - nr:end - nr], self.size)
+        return SpilledVectorColumn(self.data[start:nr], self.host[: end - nr], self.size)
+
+    def to_numpy(self):
+        a = torch.cat([self.data.detach().cpu(), self.host])[:, : self.size]
+        if a.dtype in (torch.bfloat16, torch.float16):
+            a = a.float()
+        return a.numpy().astype(np.float64)
+
+    def nbytes(self):
+        return (self.data.numel() + self.host.numel()) * self.data.element_size()
+
+    @staticmethod
+    def concat(cols):
+        dev = cols[0].data.device
+        parts = [c.full() if isinstance(c, SpilledVectorColumn) else c.data.to(dev) for c in cols]
+        return C.VectorColumn(torch.cat(parts), cols[0].size)
+
+    def streamer(self, chunk_bytes: int | None = None) -> "HostStreamer":
+        s = getattr(self, "_streamer", None)
+        if s is None or (chunk_bytes is not None and s.chunk_bytes != chunk_bytes):
+            s = self._streamer = HostStreamer(self.host, self.data.device, chunk_bytes)
+        return s
+
+
+class HostStreamer:
+    """Double-buffered host -> device streaming of a pinned [n, ld] matrix in row chunks."""
+
+    def __init__(self, host: torch.Tensor, device, chunk_bytes: int | None = None):
+        self.host = host
+        self.device = torch.device(device)
+        self.chunk_bytes = int(chunk_bytes or CHUNK_BYTES)
+        row_bytes = max(1, host.shape[1] * host.element_size())
+        self.chunk_rows = max(1, self.chunk_bytes // row_bytes)
+        n = int(host.shape[0])
+        self.ranges = [(a, min(n, a + self.chunk_rows)) for a in range(0, n, self.chunk_rows)]
+        self.bytes_streamed = 0
+        if self.device.type == "cuda" and self.ranges:
+            rows = min(self.chunk_rows, n)
+            self.buf = [torch.empty((rows, host.shape[1]), dtype=host.dtype, device=self.device) for _ in range(2)]
+            self.stream = torch.cuda.Stream(self.device)
+            self.ready = [torch.cuda.Event(), torch.cuda.Event()]
+            self.free = [torch.cuda.Event(), torch.cuda.Event()]
+            self._free_recorded = [False, False]
+
+    def __len__(self):
+        return len(self.ranges)
+
+    def _issue_copy(self, i: int):
+        a, b = self.ranges[i]
+        k = i & 1
+        cs = self.stream
+        if self._free_recorded[k]:
+            cs.wait_event(self.free[k])           # the kernels of chunk i-2 are done with buf[k]
+        with torch.cuda.stream(cs):
+            self.buf[k][: b - a].copy_(self.host[a:b], non_blocking=True)
+        self.ready[k].record(cs)
+
+    def run(self, fn) -> None:
+        """``fn(chunk, row_offset)`` for every chunk, in order, on the current stream.
+
+        GPU: copy i+1 is issued before ``fn(i)`` runs (prefetch depth 1, whatever ``fn``
+        does on the host), ``fn``'s kernels wait only for their chunk's copy event, and
+        a staging buffer is refilled only after the kernels that read it finished.  The
+        chunk view is valid until ``fn`` returns (enqueue-wise)."""
+        if not self.ranges:
+            return
+        if self.device.type != "cuda":
+            for a, b in self.ranges:
+                fn(self.host[a:b], a)
+            return
+        main = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(main)                # the consumer's inputs (e.g. coefficients) are ready
+        self._issue_copy(0)
+        for i, (a, b) in enumerate(self.ranges):
+            if i + 1 < len(self.ranges):
+                self._issue_copy(i + 1)
+            k = i & 1
+            main.wait_event(self.ready[k])
+            fn(self.buf[k][: b - a], a)
+            self.free[k].record(main)
+            self._free_recorded[k] = True
+            self.bytes_streamed += (b - a) * self.host.shape[1] * self.host.element_size()
+
+
+def map_rows(col: "SpilledVectorColumn", fn) -> torch.Tensor:
+    """``fn`` (device rows -> per-row tensor) over the resident rows and then every
+    streamed chunk; the pieces are concatenated in row order (e.g. a model's margins)."""
+    outs = [fn(col.data)] if col.resident_rows or not col.spilled_rows else []
+    col.streamer().run(lambda X, off: outs.append(fn(X)))
+    return torch.cat(outs) if len(outs) > 1 else outs[0]
+
+
+class RowBlocks:
+    """The rows of a spilled vector column as a sequence of device blocks -- the resident
+    matrix, then every streamed chunk -- each passed through ``prep`` (dtype / layout /
+    normalisation the consumer needs).  ``run(fn)`` calls ``fn(block, first_row)``."""
+
+    def __init__(self, col: "SpilledVectorColumn", prep=None):
+        self.col = col
+        self.prep = prep or (lambda X: X)
+        self.n = len(col)
+        self.nres = col.resident_rows
+        self.D = col.size
+        self.device = col.data.device
+        self._res = self.prep(col.data[:, : col.size]) if self.nres else None
+
+    @property
+    def shape(self):
+        return (self.n, self.D)
+
+    def run(self, fn) -> None:
+        if self.nres:
+            fn(self._res, 0)
+        if self.col.spilled_rows:
+            self.col.streamer().run(lambda X, off: fn(self.prep(X[:, : self.D]), self.nres + off))
+
+    def rows(self, idx: torch.Tensor) -> torch.Tensor:
+        """Rows at local indices ``idx`` (device tensor, prepared)."""
+        return self.prep(self.col.take(idx).data[:, : self.D])
+
+
+def _pinned_copy(src: torch.Tensor) -> torch.Tensor:
+    """Device rows -> a pinned host matrix, in bounded chunks (no full-size staging)."""
+    out = torch.empty(tuple(src.shape), dtype=src.dtype, pin_memory=src.is_cuda)
+    step = max(1, (256 << 20) // max(1, src.shape[1] * src.element_size()))
+    for a in range(0, src.shape[0], step):
+        out[a:a + step].copy_(src[a:a + step])
+    return out
+
+
+def hbm_budget(session) -> int:
+    v = session.conf.get("o3s.storage.hbmBudget", None)
+    if v not in (None, "", "auto"):
+        return int(float(v))
+    dev = session.device
+    if dev.type != "cuda":
+        return 1 << 62
+    free, _ = torch.cuda.mem_get_info(dev)
+    return int(free * session.conf.memory_fraction())
+
+
+def spill_to_budget(df, budget: int | None = None, disk_only: bool = False) -> int:
+    """Move rows of ``df``'s dense vector columns beyond ``budget`` bytes (largest column
+    first; every column's resident prefix counts against the budget) to pinned host memory,
+    in place.  Returns the bytes moved.  ``disk_only``: every row of those columns."""
+    budget = hbm_budget(df.session) if budget is None else int(budget)
+    vec = [(k, c) for k, c in df._cols.items()
+           if type(c) is C.VectorColumn or isinstance(c, SpilledVectorColumn)]
+    vec.sort(key=lambda kc: -kc[1].nbytes())
+    moved = 0
+    left = 0 if disk_only else budget
+    for k, c in vec:
+        row_bytes = c.ld * c.data.element_size()
+        n = len(c)
+        keep = min(n, max(0, left // max(row_bytes, 1)))
+        if isinstance(c, SpilledVectorColumn):
+            if keep >= c.resident_rows:
+                left -= c.resident_rows * row_bytes
+                continue
+            host = torch.cat([_pinned_copy(c.data[keep:]), c.host])
+            res = c.data[:keep].clone()
+        else:
+            if keep >= n:
+                left -= n * row_bytes
+                continue
+            host = _pinned_copy(c.data[keep:])
+            res = c.data[:keep].clone()
+        moved += (n - keep) * row_bytes - (c.spilled_rows * row_bytes if isinstance(c, SpilledVectorColumn) else 0)
+        df._cols[k] = SpilledVectorColumn(res, host, c.size)
+        left -= keep * row_bytes
+    return moved

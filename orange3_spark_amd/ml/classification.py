@@ -194,15 +194,24 @@ class LogisticRegressionModel(U.ProbabilisticClassifierMixin, Model, _LogisticRe
         return self.summary is not None
 
     def _features_for_predict(self, df, name):
+        from ..frame.spill import SpilledVectorColumn
         c = U.features_column(df, name)
+        if isinstance(c, SpilledVectorColumn) and c.data.is_cuda and c.data.dtype == torch.bfloat16 \
+                and not self._multinomial:
+            return c                 # resident + host-streamed rows -> margin kernel per chunk
         if isinstance(c, C.VectorColumn) and c.data.is_cuda and c.data.dtype == torch.bfloat16 \
-                and not self._multinomial and not isinstance(c, LineageVectorColumn):
+                and not self._multinomial and not isinstance(c, (LineageVectorColumn, SpilledVectorColumn)):
             return c.data            # padded bf16 -> margin kernel
         if isinstance(c, C.SparseVectorColumn) and not self._multinomial:
             return U.linear_features(df, name)     # CSR rows -> sparse margin kernel
         return U.dense_features(df, name)
 
     def _raw(self, X):
+        from ..frame.spill import SpilledVectorColumn, map_rows
+        if isinstance(X, SpilledVectorColumn):
+            w = torch.from_numpy(self._B[0]).float().to(X.data.device)
+            m = map_rows(X, lambda Xc: G.glm_margin(Xc, w, float(self._b[0])).double())
+            return torch.stack([-m, m], dim=1)
         if not self._multinomial:
             if isinstance(X, torch.Tensor) and X.is_cuda and X.dtype == torch.bfloat16:
                 m = G.glm_margin(X, torch.from_numpy(self._B[0]).float().to(X.device), float(self._b[0])).double()

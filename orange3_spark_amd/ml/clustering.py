@@ -64,10 +64,19 @@ class KMeans(Estimator, _KMeansParams, MLWritable, MLReadable):
         return self._set(**self._input_kwargs)
 
     def _fit(self, df):
+        from ..frame.spill import RowBlocks, SpilledVectorColumn
         g = self.getOrDefault
-        X = U.dense_features(df, g(self.featuresCol))
-        X = X.float().contiguous() if X.is_cuda else X.to(torch.float64)
         w = U.weights_or_none(df, self)
+        col = U.features_column(df, g(self.featuresCol))
+        cosine = g(self.distanceMeasure) == "cosine"
+        if isinstance(col, SpilledVectorColumn) and col.spilled_rows and w is None:
+            def prep(X):          # the assign/update kernels' operand (+ cosine normalisation)
+                X = X.float().contiguous() if X.is_cuda else X.to(torch.float64)
+                return X / X.norm(dim=1, keepdim=True).clamp_min(1e-300) if cosine else X
+            X = RowBlocks(col, prep)
+        else:
+            X = U.dense_features(df, g(self.featuresCol))
+            X = X.float().contiguous() if X.is_cuda else X.to(torch.float64)
         from ..runtime.checkpoint import for_estimator
         res = KM.fit_kmeans(df.comm, X, g(self.k), g(self.maxIter), g(self.tol), g(self.seed), g(self.initMode),
                             g(self.initSteps), weights=w, cosine=g(self.distanceMeasure) == "cosine",

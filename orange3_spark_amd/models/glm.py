@@ -42,13 +42,19 @@ class GlmData:
 
     def __init__(self, comm, feat: C.Column, y: torch.Tensor, sw: torch.Tensor | None = None,
                  chunk_rows: int = 1 << 22):
+        from ..frame.spill import SpilledVectorColumn
         self.comm = comm
         self.lineage = None
+        self.spill = None            # HostStreamer of the rows kept in pinned host memory
         if isinstance(feat, C.SparseVectorColumn):
             feat = C.VectorColumn(feat.to_dense(torch.float32), feat.size)
         if isinstance(feat, LineageVectorColumn):
             X = feat.data
             self.lineage = (feat.spec, feat.row0 + feat.resident_rows, feat.lineage_rows)
+        elif isinstance(feat, SpilledVectorColumn):
+            X = feat.data
+            if feat.spilled_rows:
+                self.spill = feat.streamer()
         else:
             X = feat.data
         self.d = int(feat.size)
@@ -58,7 +64,9 @@ class GlmData:
         self.ld = int(X.shape[1])
         self.y = y.to(self.device, torch.float32).contiguous() if self.kernel else y.to(self.device)
         self.sw = None if sw is None else (sw.to(self.device, torch.float32).contiguous() if self.kernel else sw.to(self.device))
-        self.n_local = int(X.shape[0]) + (self.lineage[2] if self.lineage else 0)
+        self.nres = int(X.shape[0])
+        self.n_local = self.nres + (self.lineage[2] if self.lineage else 0) + \
+            (int(self.spill.host.shape[0]) if self.spill is not None else 0)
         self.n = int(comm.sum_scalar(self.n_local))
         self.chunk = chunk_rows
         self.ws = G.GlmWorkspace(self.device, self.ld) if self.kernel else None
@@ -78,7 +86,27 @@ class GlmData:
         self.mixed = self.kernel and os.environ.get("O3S_GLM_MIXED", "1") == "1" \
             and (self.sw is None or self.sw.shape[0] == self.y.shape[0])
         self._row0 = int(feat.row0) if isinstance(feat, LineageVectorColumn) else None
+        if self.spill is not None and self.kernel:
+            self.mixed = True                  # chunks run through the mixed kernel (sampling, weights)
         self._setup_workspace()
+        self.ws_stream = G.GlmWorkspace(self.device, self.ld) if (self.spill is not None and self.kernel) else None
+
+    # ---------------------------------------------------------------- streamed rows
+    def _res(self, t):
+        """The resident rows' slice of a per-row column (labels / weights)."""
+        return None if t is None else (t if self.spill is None else t[: self.nres])
+
+    def _chunk_rows(self, t, off, rows):
+        return None if t is None else t[self.nres + off: self.nres + off + rows]
+
+    @property
+    def mode(self) -> str:
+        """How this rank's rows reach the pass: resident / resident+lineage / resident+streamed."""
+        if self.lineage:
+            return "resident+lineage" if self.nres else "lineage"
+        if self.spill is not None:
+            return "resident+streamed" if self.nres else "streamed"
+        return "resident"
 
     def _setup_workspace(self):
         if self.mixed:
@@ -87,6 +115,8 @@ class GlmData:
             # (a small table would otherwise launch 8K mostly-idle blocks and make the
             # finish kernel sum 8K slab rows -- ~100 us per step on a 4K-row table)
             tiles = -(-int(self.X.shape[0]) // 16) + -(-int(self.lineage[2] if self.lineage else 0) // 16)
+            if self.spill is not None:
+                tiles = max(tiles, -(-int(self.spill.chunk_rows) // 16))
             grid = max(1, min(cus * 32, -(-tiles // 4)))
             self.ws = G.GlmWorkspace(self.device, self.ld,
                                      grid=int(os.environ.get("O3S_GLM_GRID_MIX", str(grid))))
@@ -120,15 +150,25 @@ class GlmData:
         if self.kernel:
             if not self.mixed:
                 return None
-            st = G.glm_stats_mixed(self.X, self.y, self.sw, nl, spec.d if spec else self.d,
+            st = G.glm_stats_mixed(self.X, self._res(self.y), self._res(self.sw), nl, spec.d if spec else self.d,
                                    spec.seed if spec else 0, r0)
             if st is None:
                 return None
             dpad = self.ws.dpad
         else:
-            st = G.glm_stats_torch(self.X, self.y, self.sw, nl, spec.d if spec else self.d,
+            st = G.glm_stats_torch(self.X, self._res(self.y), self._res(self.sw), nl, spec.d if spec else self.d,
                                    spec.seed if spec else 0, r0).to(self.device)
             dpad = G.layout(self.ld)[0]
+        if self.spill is not None:
+            acc = st
+
+            def chunk(Xc, off):
+                yc, wc = self._chunk_rows(self.y, off, Xc.shape[0]), self._chunk_rows(self.sw, off, Xc.shape[0])
+                if self.kernel:
+                    acc.add_(G.glm_stats_mixed(Xc, yc, wc, 0, self.d, 0, 0))
+                else:
+                    acc.add_(G.glm_stats_torch(Xc, yc, wc, 0, self.d, 0, 0).to(self.device))
+            self.spill.run(chunk)
         self.comm.all_reduce(st)
         h = st.cpu().numpy()
         d = self.d
@@ -139,8 +179,13 @@ class GlmData:
     def moments(self):
         """Global weighted (mean, variance (unbiased), weight sum, label moments)."""
         d = self.d
+        def torch_stats(Xc, swc):
+            Xd = Xc.to(torch.float64)
+            w = torch.ones(Xd.shape[0], dtype=torch.float64, device=Xd.device) if swc is None \
+                else swc.to(torch.float64)
+            return torch.cat([w @ Xd, w @ (Xd * Xd), w.sum().reshape(1)])
         if self.kernel:
-            parts = [G.glm_colstats(self.X, self.sw)] if self.X.shape[0] else []
+            parts = [G.glm_colstats(self.X, self._res(self.sw))] if self.X.shape[0] else []
             if self.lineage:
                 spec, r0, nl = self.lineage
                 parts.append(G.glm_colstats_synth(nl, self.ld, spec.d, spec.seed, r0, self.device))
@@ -149,10 +194,12 @@ class GlmData:
             else:
                 st = torch.zeros(2 * self.ld + 1, dtype=torch.float64, device=self.device)
         else:
-            Xd = self.X.to(torch.float64)
-            w = torch.ones(Xd.shape[0], dtype=torch.float64, device=Xd.device) if self.sw is None \
-                else self.sw.to(torch.float64)
-            st = torch.cat([w @ Xd, w @ (Xd * Xd), w.sum().reshape(1)])
+            st = torch_stats(self.X, self._res(self.sw))
+        if self.spill is not None:
+            def chunk(Xc, off):
+                wc = self._chunk_rows(self.sw, off, Xc.shape[0])
+                st.add_(G.glm_colstats(Xc, wc) if self.kernel else torch_stats(Xc, wc).to(st.device))
+            self.spill.run(chunk)
         ld = self.ld
         yw = self.y.to(torch.float64) * (1.0 if self.sw is None else self.sw.to(torch.float64))
         ystats = torch.stack([yw.sum(), (yw * self.y.to(torch.float64)).sum()]).to(st.device)
@@ -189,10 +236,24 @@ class GlmData:
         if self.mixed:
             spec, r0, nl = self.lineage if self.lineage else (None, 0, 0)
             sseed, frac = sample if sample is not None else (0, 1.0)
-            G.glm_grad_mixed(self.X, self.y, self.sw, nl, spec.d if spec else self.d,
-                             spec.seed if spec else 0, r0, coef_eff, intercept, loss, ws,
-                             res_row0=self.global_row0() if frac < 1.0 else 0, t_dev=t_dev,
-                             sample_seed=sseed, fraction=frac)
+            g0 = self.global_row0() if frac < 1.0 else 0
+            if self.nres or nl:
+                G.glm_grad_mixed(self.X, self._res(self.y), self._res(self.sw), nl, spec.d if spec else self.d,
+                                 spec.seed if spec else 0, r0, coef_eff, intercept, loss, ws,
+                                 res_row0=g0, t_dev=t_dev, sample_seed=sseed, fraction=frac)
+            else:
+                ws.out.zero_()
+            if self.spill is not None:
+                cf = G._coef_buf(coef_eff, ws.dpad, self.device, intercept=intercept)
+                wss = self.ws_stream
+
+                def chunk(Xc, off):
+                    rows = Xc.shape[0]
+                    G.glm_grad_mixed(Xc, self._chunk_rows(self.y, off, rows), self._chunk_rows(self.sw, off, rows),
+                                     0, self.d, 0, 0, cf, None, loss, wss, res_row0=g0 + self.nres + off,
+                                     t_dev=t_dev, sample_seed=sseed, fraction=frac)
+                    ws.out.add_(wss.out)
+                self.spill.run(chunk)
             self.passes += 1
             return ws.out
         if self.overlap is not None:
@@ -231,18 +292,24 @@ class GlmData:
         dpad = self.ld
         acc = torch.zeros(dpad + 3, dtype=torch.float64, device=self.device)
         c = coef_eff.to(self.device, torch.float64)[: self.ld]
-        n = self.X.shape[0]
         sampled = sample is not None and sample[1] < 1.0
         g0 = self.global_row0() if sampled else 0
-        for a in range(0, n, self.chunk):
-            b = min(n, a + self.chunk)
-            Xc = self.X[a:b].to(torch.float64)
-            yc = self.y[a:b].to(torch.float64)
-            wc = None if self.sw is None else self.sw[a:b].to(torch.float64)
-            if sampled:
-                keep = G.sample_mask(sample[0], it, torch.arange(g0 + a, g0 + b), sample[1]).to(self.device)
-                wc = keep.to(torch.float64) if wc is None else wc * keep
-            acc += G.glm_grad_torch(Xc, yc, wc, c, intercept, loss)
+
+        def block(X, base):
+            n = X.shape[0]
+            for a in range(0, n, self.chunk):
+                b = min(n, a + self.chunk)
+                Xc = X[a:b].to(self.device, torch.float64)
+                yc = self.y[base + a:base + b].to(torch.float64)
+                wc = None if self.sw is None else self.sw[base + a:base + b].to(torch.float64)
+                if sampled:
+                    keep = G.sample_mask(sample[0], it, torch.arange(g0 + base + a, g0 + base + b),
+                                         sample[1]).to(self.device)
+                    wc = keep.to(torch.float64) if wc is None else wc * keep
+                acc.add_(G.glm_grad_torch(Xc, yc, wc, c, intercept, loss))
+        block(self.X, 0)
+        if self.spill is not None:
+            self.spill.run(lambda Xc, off: block(Xc, self.nres + off))
         self.passes += 1
         return acc
 
@@ -696,6 +763,8 @@ class DeviceSGD:
         if faults.launch_blocking():
             return
         d = self.data
+        if d.spill is not None:               # host-streamed rows: copies + events stay eager
+            return
         if mode != "force" and d.n_local * d.ld * 2 > self.GRAPH_MAX_BYTES:
             return
         if d.comm.world_size > 1 and mode != "all":

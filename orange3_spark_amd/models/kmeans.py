@@ -139,9 +139,125 @@ def random_init(comm, X, k, seed):
     return C
 
 
-def fit_kmeans(comm, X: torch.Tensor, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int = 0,
+# ------------------------------------------------------------------ streamed rows
+def _blocks_init(comm, B, k: int, steps: int, seed: int, init: str) -> torch.Tensor:
+    """k-means|| / random initialisation over RowBlocks (resident + host-streamed rows):
+    the same draws as the resident path (keyed on global rows), one streamed pass per
+    round."""
+    dev = B.device
+    rows_all, n = _global_rows(comm, B.n, dev)
+    off = int(rows_all[0]) if B.n else 0
+    rng = np.random.default_rng(seed)
+    if init == "random":
+        picks = rng.choice(max(n, 1), size=min(k, n), replace=False)
+        C = torch.zeros((k, B.D), dtype=torch.float64, device=dev)
+        for j, r in enumerate(picks.tolist()):
+            if off <= r < off + B.n:
+                C[j] = B.rows(torch.tensor([r - off], device=dev))[0].to(torch.float64)
+        comm.all_reduce(C)
+        return C
+    pick = int(rng.integers(0, max(n, 1)))
+    c0 = torch.zeros(B.D, dtype=torch.float64, device=dev)
+    if off <= pick < off + B.n:
+        c0 = B.rows(torch.tensor([pick - off], device=dev))[0].to(torch.float64).contiguous()
+    comm.all_reduce(c0)
+    centers = c0[None, :]
+    for step in range(steps):
+        with trace("kmeans.init.round"):
+            d = torch.empty(B.n, dtype=torch.float32, device=dev)
+            Cf = centers.float()
+            B.run(lambda X, a: d[a:a + X.shape[0]].copy_(K.assign(X, Cf, mode="split")[1]))
+            cost = d.to(torch.float64).sum()
+            comm.all_reduce(cost)
+            if float(cost) <= 0:
+                break
+            p = (2.0 * k * d.to(torch.float64) / float(cost)).clamp(max=1.0)
+            u = sampling.uniform(rows_all, seed + 1 + step, stream=7)
+            sel = torch.nonzero(u < p).reshape(-1)
+            new = B.rows(sel).to(torch.float64) if sel.numel() else torch.zeros((0, B.D), dtype=torch.float64,
+                                                                               device=dev)
+            new = comm.all_gather_v(new) if comm.world_size > 1 else new
+            centers = torch.cat([centers, new.to(dev)])
+    with trace("kmeans.init.weights"):
+        wts = torch.zeros(centers.shape[0], dtype=torch.float64, device=dev)
+        Cf = centers.float()
+
+        def wfn(X, a):
+            lab, _ = K.assign(X, Cf, mode="split")
+            wts.add_(torch.bincount(lab.long(), minlength=centers.shape[0])[: centers.shape[0]].to(torch.float64))
+        B.run(wfn)
+        comm.all_reduce(wts)
+    with trace("kmeans.init.local"):
+        return _local_kmeanspp(centers, wts, k, seed)
+
+
+def _fit_kmeans_blocks(comm, B, k, max_iter, tol, seed, init, init_steps, initial, cosine, ckpt) -> KMeansResult:
+    """Lloyd iterations over RowBlocks: every block is assigned (split-precision kernel: no
+    per-chunk host sync) and folded into the slab update; the host-streamed chunks' H2D
+    copies overlap the previous chunk's kernels (frame/spill.HostStreamer)."""
+    t0 = time.time()
+    dev, D = B.device, B.D
+    C = initial.to(dev, torch.float64) if initial is not None else _blocks_init(comm, B, k, init_steps, seed, init)
+    Kp = ((k + 31) // 32) * 32
+    ws = K.UpdateWorkspace(dev, Kp, D) if dev.type == "cuda" and D <= 256 else None
+    hist, sizes, it = [], None, 0
+    for it in range(1, max_iter + 1):
+        with trace("kmeans.iter"):
+            Cf = C.float()
+            prep = K.prepare_centers(Cf) if dev.type == "cuda" else None
+            sums = torch.zeros((k, D), dtype=torch.float64, device=dev)
+            cnt = torch.zeros(k, dtype=torch.float64, device=dev)
+            cost = torch.zeros(1, dtype=torch.float64, device=dev)
+
+            def step(X, a0):
+                lab, d = K.assign(X, Cf, prep, mode="split")
+                if ws is not None and K.update_kernel_ok(X):
+                    s_, c_ = K.update(X, lab, ws.K, ws)
+                    sums.add_(s_[:k])
+                    cnt.add_(c_[:k])
+                else:
+                    s_, c_ = K.update_torch(X, lab, k)
+                    sums.add_(s_)
+                    cnt.add_(c_)
+                cost.add_(d.to(torch.float64).sum())
+            B.run(step)
+            buf = torch.cat([sums.reshape(-1), cnt, cost])
+            comm.all_reduce(buf)
+            sums, cnt, c = buf[: k * D].reshape(k, D), buf[k * D: k * D + k], float(buf[-1])
+            hist.append(c)
+            newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp_min(1e-300)[:, None], C)
+            if cosine:
+                newC = newC / newC.norm(dim=1, keepdim=True).clamp_min(1e-300)
+            moved = ((newC - C) ** 2).sum(1).max().item()
+            C = newC
+            sizes = cnt
+            if moved <= tol * tol:
+                break
+    cnt = torch.zeros(k, dtype=torch.float64, device=dev)
+    cost = torch.zeros(1, dtype=torch.float64, device=dev)
+    Cf = C.float()
+
+    def final(X, a0):
+        lab, d = K.assign(X, Cf, mode="split")
+        cnt.add_(torch.bincount(lab.long(), minlength=k)[:k].to(torch.float64))
+        cost.add_(d.to(torch.float64).sum())
+    B.run(final)
+    buf = torch.cat([cnt, cost])
+    comm.all_reduce(buf)
+    _ = sizes
+    return KMeansResult(C.cpu(), float(buf[-1]), it, [int(x) for x in buf[:k].tolist()], hist, time.time() - t0)
+
+
+def fit_kmeans(comm, X, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int = 0,
                init: str = "k-means||", init_steps: int = 2, initial: torch.Tensor | None = None,
                weights: torch.Tensor | None = None, cosine: bool = False, ckpt=None) -> KMeansResult:
+    """``X``: this rank's [n, D] rows, or a ``frame.spill.RowBlocks`` (MEMORY_AND_DISK rows:
+    resident + host-streamed; unweighted)."""
+    from ..frame.spill import RowBlocks
+    if isinstance(X, RowBlocks):
+        if weights is not None:
+            raise ValueError("weighted KMeans over host-streamed rows is not supported; persist with MEMORY_ONLY")
+        return _fit_kmeans_blocks(comm, X, k, max_iter, tol, seed, init, init_steps, initial, cosine, ckpt)
     t0 = time.time()
     if cosine:
         X = X / X.norm(dim=1, keepdim=True).clamp_min(1e-300)
