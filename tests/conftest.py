@@ -7,6 +7,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# spark.executor.instances defaults to "auto" (every visible GPU): a test session built from
+# SessionConf() must stay in-process even on a multi-GPU box; pool tests set it explicitly
+os.environ.setdefault("O3S_CONF_SPARK__EXECUTOR__INSTANCES", "1")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (ROCm GPU); run with -m gpu")

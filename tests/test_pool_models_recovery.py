@@ -185,11 +185,12 @@ def test_executor_instances_auto_counts_gpus_without_initialising(monkeypatch):
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
     init = []
     monkeypatch.setattr(torch.cuda, "init", lambda: init.append(1))
+    auto = lambda: SessionConf().set("spark.executor.instances", "auto")   # noqa: E731 (conftest pins 1)
     assert resolve_executors("auto") == 8 and resolve_executors("3") == 3
-    assert _wants_pool(SessionConf()) and not _wants_pool(SessionConf().set("spark.master", "local[1]"))
+    assert _wants_pool(auto()) and not _wants_pool(auto().set("spark.master", "local[1]"))
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 0)
-    assert resolve_executors("auto") == 1 and not _wants_pool(SessionConf())
-    assert _wants_pool(SessionConf().set("o3s.executor.pool", "true"))
+    assert resolve_executors("auto") == 1 and not _wants_pool(auto())
+    assert _wants_pool(auto().set("o3s.executor.pool", "true"))
     assert not init
 
 
