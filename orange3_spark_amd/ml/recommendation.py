@@ -138,24 +138,23 @@ class ALSModel(Model, _ALSModelParams, MLWritable, MLReadable):
         return out
 
     def _recommend(self, Q, ids_q, T, ids_t, k, qname, tname):
+        """Top-``k`` rows of ``T`` per row of ``Q`` by dot product (Spark
+        recommendForAll*): the score matrix is never materialised -- query x target
+        blocks of bounded size, a running top-k merged per target block -- and the result
+        stays on the device (``RecsColumn``: ids / scores [n, k]; Rows are built only when
+        the column is read on the host).  Factors are replicated, so each rank recommends
+        for its own block of query rows."""
         from ..session import Session
         s = Session.active() or Session.getOrCreate()
-        k = min(k, T.shape[0])
         if s.comm.world_size > 1:          # factors are replicated: each rank recommends its block
             lo, hi = s._shard_bounds(Q.shape[0])
             Q, ids_q = Q[lo:hi], ids_q[lo:hi]
-        recs = []
-        for a in range(0, Q.shape[0], 1 << 14):
-            sc = Q[a:a + (1 << 14)] @ T.T
-            v, ix = torch.topk(sc, k, dim=1)
-            for row_i, (vv, ii) in enumerate(zip(v.cpu().tolist(), ix.cpu().tolist())):
-                recs.append([Row._make([tname, "rating"], [int(ids_t[j]), float(x)]) for j, x in zip(ii, vv)])
+        vals, idx = topk_scores(Q, T, k)
+        ids_t = torch.as_tensor(ids_t).to(idx.device, torch.int64)
         cols = OrderedDict()
         cols[qname] = C.NumericColumn(ids_q.to(torch.int32).to(s.device))
-        arr = np.empty(len(recs), dtype=object)
-        arr[:] = recs
-        cols["recommendations"] = C.ArrayColumn(arr)
-        return DataFrame(s, cols, len(recs))
+        cols["recommendations"] = RecsColumn(ids_t[idx].to(torch.int32), vals.float(), tname)
+        return DataFrame(s, cols, int(Q.shape[0]))
 
     def recommendForAllUsers(self, numItems):
         return self._recommend(self._U, self._uid_t, self._V, self._iid_t.cpu().numpy(), numItems,
@@ -224,6 +223,94 @@ class ALSModel(Model, _ALSModelParams, MLWritable, MLReadable):
         m = cls._from(parts[0], parts[1], parts[2], parts[3], meta.get("rank", parts[1].shape[1]))
         apply_metadata(m, meta)
         return m
+
+
+def topk_scores(Q: torch.Tensor, T: torch.Tensor, k: int, budget: int = 1 << 28):
+    """(values, indices) [nQ, k] of the k largest Q @ T^T entries per row, computed over
+    query x target blocks of at most ``budget`` scores (fp32 GEMM + top-k, merged per
+    target block), so 50M x 5M never materialises."""
+    nQ, nT = int(Q.shape[0]), int(T.shape[0])
+    k = max(0, min(int(k), nT))
+    dev = Q.device
+    vals = torch.empty((nQ, k), dtype=torch.float32, device=dev)
+    idx = torch.empty((nQ, k), dtype=torch.int64, device=dev)
+    if nQ == 0 or k == 0:
+        return vals, idx
+    tc = min(nT, max(k, budget // max(1, min(nQ, 4096))))
+    qc = max(1, min(nQ, budget // tc))
+    Tf = T.float()
+    for a in range(0, nQ, qc):
+        Qa = Q[a:a + qc].float()
+        bv = bi = None
+        for t0 in range(0, nT, tc):
+            sc = Qa @ Tf[t0:t0 + tc].T
+            v, i = torch.topk(sc, min(k, sc.shape[1]), dim=1)
+            i = i + t0
+            if bv is None:
+                bv, bi = v, i
+            else:
+                cv, ci = torch.cat([bv, v], 1), torch.cat([bi, i], 1)
+                bv, pos = torch.topk(cv, k, dim=1)
+                bi = ci.gather(1, pos)
+            del sc
+        vals[a:a + qc], idx[a:a + qc] = bv, bi
+    return vals, idx
+
+
+class RecsColumn(C.ArrayColumn):
+    """array<struct<id, rating>> kept on the device as ids [n, k] (int32) and scores [n, k]
+    (float32); the host ``values`` (lists of Rows, Spark's recommendation layout) are built
+    on first access."""
+
+    def __init__(self, ids: torch.Tensor, scores: torch.Tensor, id_name: str):
+        from ..frame import types as T
+        self.ids, self.scores, self.id_name = ids, scores, id_name
+        self.dtype = T.ArrayType(T.StructType([T.StructField(id_name, T.IntegerType()),
+                                               T.StructField("rating", T.FloatType())]))
+        self._host = None
+
+    def __len__(self):
+        return int(self.ids.shape[0])
+
+    @property
+    def values(self):
+        if self._host is None:
+            ids, sc = self.ids.cpu().tolist(), self.scores.cpu().tolist()
+            names = [self.id_name, "rating"]
+            arr = np.empty(len(ids), dtype=object)
+            arr[:] = [[Row._make(names, [i, float(v)]) for i, v in zip(ri, rv)] for ri, rv in zip(ids, sc)]
+            self._host = arr
+        return self._host
+
+    @values.setter
+    def values(self, v):
+        self._host = v
+
+    def _sub(self, sel):
+        return RecsColumn(self.ids[sel], self.scores[sel], self.id_name)
+
+    def take(self, idx):
+        return self._sub(idx.to(self.ids.device).long())
+
+    def mask_select(self, mask):
+        return self._sub(mask.to(self.ids.device).bool())
+
+    def slice(self, start, end):
+        return RecsColumn(self.ids[start:end], self.scores[start:end], self.id_name)
+
+    def null_mask(self):
+        return torch.zeros(len(self), dtype=torch.bool)
+
+    def nbytes(self):
+        return self.ids.numel() * 4 + self.scores.numel() * 4
+
+    @classmethod
+    def concat(cls, cols):
+        if all(isinstance(c, RecsColumn) and c.ids.shape[1:] == cols[0].ids.shape[1:] for c in cols):
+            dev = cols[0].ids.device
+            return RecsColumn(torch.cat([c.ids.to(dev) for c in cols]), torch.cat([c.scores.to(dev) for c in cols]),
+                              cols[0].id_name)
+        return C.ArrayColumn(np.concatenate([c.values for c in cols]), cols[0].dtype.elementType)
 
 
 def _to(c, dev):

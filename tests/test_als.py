@@ -300,3 +300,28 @@ def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
     assert not torch.isnan(got).any()
     err = (got.double() - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-6)
     assert float(err.max()) < 2e-3, float(err.max())
+
+
+def test_blockwise_topk_recommendations_match_brute_force():
+    """recommendForAll*: blockwise top-k (bounded score blocks, running merge) equals the
+    full score matrix's top-k; the column stays on the device until read."""
+    from orange3_spark_amd.ml.recommendation import RecsColumn, topk_scores
+    g = torch.Generator().manual_seed(0)
+    Q, T = torch.randn(300, 8, generator=g), torch.randn(1000, 8, generator=g)
+    v, i = topk_scores(Q, T, 7, budget=300)              # tiny budget: many query / target blocks
+    rv, ri = torch.topk(Q @ T.T, 7, dim=1)
+    assert torch.allclose(v, rv) and torch.equal(i, ri)
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    rng = np.random.default_rng(2)
+    pdf = pd.DataFrame({"user": rng.integers(0, 50, 2000), "item": rng.integers(0, 80, 2000),
+                        "rating": rng.integers(1, 6, 2000).astype(float)})
+    m = ALS(rank=4, maxIter=3, seed=1).fit(s.createDataFrame(pdf))
+    recs = m.recommendForAllUsers(5)
+    col = recs.column_data("recommendations")
+    assert isinstance(col, RecsColumn) and col.ids.shape == (50, 5)
+    first = recs.orderBy("user").collect()[0]
+    U_, V_ = m._U.double(), m._V.double()
+    u0 = int(torch.searchsorted(m._uid_t, torch.tensor(first.user)))
+    want = torch.topk(U_[u0] @ V_.T, 5).indices
+    assert [r.item for r in first.recommendations] == m._iid_t[want].tolist()
+    assert recs.filter(recs.user < 10).count() == 10
