@@ -129,7 +129,11 @@ class ALSModel(Model, _ALSModelParams, MLWritable, MLReadable):
         i = U.numeric_column(df, g(self.itemCol), torch.int64)
         pu, hu = self._lookup(self._uid_t, self._U, u)
         pi, hi = self._lookup(self._iid_t, self._V, i)
-        pred = (self._U[pu].to(torch.float64) * self._V[pi].to(torch.float64)).sum(1)
+        pred = torch.empty(pu.shape[0], dtype=torch.float64, device=pu.device)
+        step = 1 << 21                        # bounded gathers: 2M rows x rank per chunk
+        for a in range(0, pu.shape[0], step):
+            pred[a:a + step] = (self._U[pu[a:a + step]].to(torch.float64)
+                                * self._V[pi[a:a + step]].to(torch.float64)).sum(1)
         ok = hu & hi
         pred = torch.where(ok, pred, torch.full_like(pred, float("nan")))
         out = df.withColumnData(g(self.predictionCol), C.NumericColumn(pred.float()))

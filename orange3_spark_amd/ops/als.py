@@ -121,8 +121,8 @@ EXACT_RANKS = (32, 64, 96, 128)
 # dense (long-row) exact solves: "mfma_blk" (default) = als_dense_mfma_kernel with 4-column
 # diagonal blocks and, at R = 96 / 128, the bf16x3 Gram (0.120 s/iter at the rank-of-8 ALS
 # shapes); "mfma" = the same kernel with column-by-column diagonals and the f32 Gram
-# (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144);
-# "mfma_pf" = mfma_blk with the rating indices prefetched one Gram step ahead
+# (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144).  Rejected:
+# rating indices prefetched one Gram step ahead of the gathers (0.127 vs 0.122 s)
 DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_blk")
 
 
@@ -243,8 +243,7 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
                     "als_rotate")
     if nd:
         Gf = G.float().contiguous() if implicit else None
-        fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
-              "mfma_pf": lib.o3s_als_dense_mfma_pf}.get(DENSE_KERNEL, lib.o3s_als_dense)
+        fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk}.get(DENSE_KERNEL, lib.o3s_als_dense)
         N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                    F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), nd, out.data_ptr(), st),
                 "als_dense")

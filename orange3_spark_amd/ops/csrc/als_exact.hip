@@ -584,7 +584,7 @@ struct DenseM {
   static constexpr int LDS = SA + TS + NT * TS + R + 2 * CH + W * 32;
 };
 
-template <int R, bool IMPL, bool BLK, bool PF2 = false>
+template <int R, bool IMPL, bool BLK>
 __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
@@ -652,9 +652,9 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
     for (int i = 0; i < ITEMS; ++i) rh[i] = 0.f;
     auto item_r = [&](int i) { return 16 * ((wid + 4 * i) % NRB) + r_low; };
     auto item_kb = [&](int i) { return (wid + 4 * i) / NRB; };
-    // rating indices / weights of a step (ci = -1: past the row's end); PF2 issues them one
-    // step AHEAD of the factor-row gathers that use them, so a step's gathers depend on
-    // registers loaded a step earlier instead of on a global load issued just before
+    // rating indices / weights of a step (ci = -1: past the row's end), then the factor-row
+    // gathers they address.  (Issuing the indices one step ahead of their gathers measured
+    // slower: 0.127 vs 0.122 s per rank-of-8 iteration.)
     struct Idx { int32_t ci[2][2]; float wv[2][2], bv[2][2]; };
     auto load_idx = [&](int64_t jb, Idx& o) {
 #pragma unroll
@@ -711,24 +711,15 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
       }
     };
     const int nsteps = (int)((p1 - p0 + CH - 1) / CH);
-    Idx nxt;
     if (nsteps > 0) {
       load(p0);
-      if (PF2 && nsteps > 1) load_idx(p0 + CH, nxt);
       store(0);
     }
     __syncthreads();
     for (int st = 0; st < nsteps; ++st) {
       const int buf = st & 1;
       const bool more = st + 1 < nsteps;
-      if constexpr (PF2) {
-        if (more) {
-          load_f(nxt);
-          if (st + 2 < nsteps) load_idx(p0 + (int64_t)(st + 2) * CH, nxt);
-        }
-      } else {
-        if (more) load(p0 + (int64_t)(st + 1) * CH);
-      }
+      if (more) load(p0 + (int64_t)(st + 1) * CH);
       const uint16_t* th = sT + buf * 2 * R * LDT + q * LDT + 8 * h;
       const uint16_t* tl = th + R * LDT;
 #pragma unroll
@@ -1086,7 +1077,7 @@ O3S_API int o3s_als_dense(int implicit, int R, const int64_t* indptr, const int3
 }
 
 namespace {
-template <bool BLK, bool PF2 = false>
+template <bool BLK>
 int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
                       const float* b, const float* F, const float* G, const float* lam, const int32_t* dense,
                       int64_t ndense, float* X, hipStream_t st) {
@@ -1095,10 +1086,10 @@ int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t*
 #define O3S_DM(RR)                                                                                              \
   if (R == RR) {                                                                                                \
     if (implicit)                                                                                               \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK, PF2>), dim3((unsigned)ndense), dim3(DenseM<RR>::NTH), \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK>), dim3((unsigned)ndense), dim3(DenseM<RR>::NTH), \
                          0, st, indptr, cols, w, b, F, G, lam, dense, X);                                       \
     else                                                                                                        \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK, PF2>), dim3((unsigned)ndense),                  \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK>), dim3((unsigned)ndense),                       \
                          dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X);                \
     O3S_CHECK_LAUNCH();                                                                                         \
     return 0;                                                                                                   \
@@ -1121,13 +1112,6 @@ O3S_API int o3s_als_dense_mfma_blk(int implicit, int R, const int64_t* indptr, c
                                    const float* b, const float* F, const float* G, const float* lam,
                                    const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
   return launch_dense_mfma<true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
-}
-
-// same with the rating indices prefetched one Gram step ahead of the factor gathers
-O3S_API int o3s_als_dense_mfma_pf(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
-                                  const float* b, const float* F, const float* G, const float* lam,
-                                  const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
-  return launch_dense_mfma<true, true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
 }
 
 O3S_API int o3s_als_exact_max_small() { return kNW; }
