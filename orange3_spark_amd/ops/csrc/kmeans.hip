@@ -332,12 +332,13 @@ struct ScrLds {
   static constexpr int BYTES = STAGE_BYTES > X_BYTES ? STAGE_BYTES : X_BYTES;
 };
 
-template <int KS, int TT, bool PAIR>
+template <int KS, int TT, bool PAIR, bool PS = false>
 __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const float* __restrict__ X, int64_t n, int64_t ldx, const uint16_t* __restrict__ Chi,
     const float* __restrict__ cn, const float* __restrict__ C32, int ldc, int Cpad, float eps_x, float eps0,
     float xscale, float sscale, int32_t* __restrict__ assign, float* __restrict__ mind,
-    int32_t* __restrict__ flag_cnt, int32_t* __restrict__ flag_rows, int Dx) {
+    int32_t* __restrict__ flag_cnt, int32_t* __restrict__ flag_rows, int Dx,
+    const uint4* __restrict__ XP = nullptr, const float* __restrict__ XN = nullptr) {
   using L = ScrLds<KS>;
   constexpr int D = L::D;
   constexpr int G = L::G;
@@ -365,6 +366,29 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
   float* xt = reinterpret_cast<float*>(lds) + wid * 32 * D;
   bf16x8 bh[TT][KS], bl[TT][KS];
   float xn[TT];
+  if constexpr (PS) {
+    // pre-split rows (kmeans_presplit_kernel, once per data version): per row and
+    // (k-step, half) group 16 B of scaled fp16 hi then 16 B of lo, loaded straight into the
+    // MFMA B fragments -- no fp32 staging, no conversion VALU in the prologue
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+      const int64_t row = row_base + t * 32 + r;
+      const int64_t rowc = row < n ? row : n - 1;
+      const uint4* src = XP + rowc * (D / 4);
+      uint4 hv[KS], lv[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        hv[ks] = src[(ks * 2 + h) * 2];
+        lv[ks] = src[(ks * 2 + h) * 2 + 1];
+      }
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bh[t][ks] = __builtin_bit_cast(bf16x8, hv[ks]);
+        bl[t][ks] = __builtin_bit_cast(bf16x8, lv[ks]);
+      }
+      xn[t] = XN[rowc];
+    }
+  } else {
 #pragma unroll
   for (int t = 0; t < TT; ++t) {
     float4 xv[XL];
@@ -410,6 +434,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     }
     xn[t] = s + __shfl_xor(s, 32, 64);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slice reads done before the next tile
+  }
   }
   __syncthreads();                                         // staging area free; scn visible
 
@@ -1002,10 +1027,68 @@ O3S_API int o3s_kmeans_assign(const float* X, int64_t n, int64_t ldx, int Dx, co
 // centres [K][ldc] (ldc % 4 == 0); bound E = eps_x ||x|| + eps0 (unscaled units); xscale =
 // xs, sscale = xs ms; flag_cnt (zeroed by the caller) / flag_rows [n]: near-tie rows for
 // o3s_kmeans_assign(rowlist).  tt: 32-row tiles per wave (1 or 2).
+namespace {
+// X (fp32 [n][ldx], Dx valid columns) -> the screen kernel's pre-split rows: per row D/8
+// groups (group g = 2 ks + h: dims 8 g .. 8 g + 7) of 16 B scaled-fp16 hi + 16 B lo (the
+// split_f16 of the kernel's prologue, zero past Dx), and ||x||^2 in fp32.  One lane per
+// group; the row norm is a shuffle reduction over the row's lanes.
+template <int D>
+__global__ __launch_bounds__(256) void kmeans_presplit_kernel(const float* __restrict__ X, int64_t n, int64_t ldx,
+                                                              int Dx, float xscale, uint4* __restrict__ XP,
+                                                              float* __restrict__ XN) {
+  constexpr int G = D / 8;                     // groups per row (power of two up to 64 lanes)
+  const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t row = tid / G;
+  const int g = (int)(tid % G);
+  float s = 0.f;
+  if (row < n) {
+    uint32_t ph[4], pl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c0 = 8 * g + 2 * j;
+      const float v0 = c0 < Dx ? X[row * ldx + c0] : 0.f;
+      const float v1 = c0 + 1 < Dx ? X[row * ldx + c0 + 1] : 0.f;
+      short h0, l0, h1, l1;
+      split_f16(v0, xscale, h0, l0);
+      split_f16(v1, xscale, h1, l1);
+      ph[j] = (uint32_t)(uint16_t)h0 | ((uint32_t)(uint16_t)h1 << 16);
+      pl[j] = (uint32_t)(uint16_t)l0 | ((uint32_t)(uint16_t)l1 << 16);
+      s = fmaf(v0, v0, s);
+      s = fmaf(v1, v1, s);
+    }
+    XP[(row * G + g) * 2] = make_uint4(ph[0], ph[1], ph[2], ph[3]);
+    XP[(row * G + g) * 2 + 1] = make_uint4(pl[0], pl[1], pl[2], pl[3]);
+  }
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) s += __shfl_xor(s, o, 64);
+  if (row < n && g == 0) XN[row] = s;
+}
+}  // namespace
+
+// Pre-split rows for the screen kernel (see kmeans_presplit_kernel): XP [n][D / 8][2] x 16 B,
+// XN [n] fp32; D = Dx rounded up to 32 (<= 128).
+O3S_API int o3s_kmeans_presplit(const float* X, int64_t n, int64_t ldx, int Dx, float xscale, void* XP, float* XN,
+                                hipStream_t st) {
+  if (n <= 0) return 0;
+  const int D = (Dx + 31) / 32 * 32;
+  if (Dx % 4 != 0 || D > 128) return -1;
+  const int64_t threads = n * (D / 8);
+  const dim3 grid((unsigned)((threads + 255) / 256));
+  switch (D) {
+    case 32: hipLaunchKernelGGL((kmeans_presplit_kernel<32>), grid, dim3(256), 0, st, X, n, ldx, Dx, xscale, (uint4*)XP, XN); break;
+    case 64: hipLaunchKernelGGL((kmeans_presplit_kernel<64>), grid, dim3(256), 0, st, X, n, ldx, Dx, xscale, (uint4*)XP, XN); break;
+    case 96: hipLaunchKernelGGL((kmeans_presplit_kernel<96>), grid, dim3(256), 0, st, X, n, ldx, Dx, xscale, (uint4*)XP, XN); break;
+    case 128: hipLaunchKernelGGL((kmeans_presplit_kernel<128>), grid, dim3(256), 0, st, X, n, ldx, Dx, xscale, (uint4*)XP, XN); break;
+    default: return -2;
+  }
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
 O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
                               const float* C32, int ldc, int Cpad, float eps_x, float eps0, float xscale,
                               float sscale, int32_t* assign, float* mind, int32_t* flag_cnt, int32_t* flag_rows,
-                              int tt, int pair, hipStream_t st) {
+                              int tt, int pair, const void* XP, const float* XN, hipStream_t st) {
   if (n <= 0) return 0;
   const int D = (Dx + 31) / 32 * 32;
   if (Dx % 4 != 0 || D > 160 || ldx % 4 != 0 || ldc % 4 != 0 || Cpad % 32 != 0 || n > 0x7fffffffll) return -1;
@@ -1022,9 +1105,14 @@ O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, co
     const int64_t grid = (n + rows_per_block - 1) / rows_per_block;                                        \
     const size_t dyn = ScrLds<KS>::BYTES + cdyn;                                                           \
     if (dyn > 160 * 1024) return -3;                                                                       \
-    hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, X, n, \
-                       ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt,     \
-                       flag_rows, Dx);                                                                     \
+    if (XP && !P)                                                                                          \
+      hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, \
+                         X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt, \
+                         flag_rows, Dx, (const uint4*)XP, XN);                                             \
+    else                                                                                                   \
+      hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, X, n, \
+                         ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt,   \
+                         flag_rows, Dx, nullptr, nullptr);                                                 \
   }
   switch (D / 16) {
     case 2: if (tt == 2) O3S_KS(2, 2) else O3S_KS(2, 1) break;

@@ -76,6 +76,42 @@ def x_scale(X: torch.Tensor) -> float:
     return v
 
 
+# Pre-split data for the screen kernel (kmeans_presplit_kernel): the scaled fp16 hi / lo
+# halves of every row (D * 4 bytes per row, as much as X itself) and ||x||^2, built once per
+# data version and reused by every Lloyd iteration -- the kernel's prologue then loads its
+# MFMA fragments instead of converting fp32 rows.  PRESPLIT: None = auto (when X is at least
+# PRESPLIT_MIN_ROWS rows and the copy fits in half of the free HBM), True / False forces.
+PRESPLIT: bool | None = None
+PRESPLIT_MIN_ROWS = 1 << 20
+_XSPLIT: list = [None, None, None]     # [weakref to X, (shape, version, xs), (XP, XN)]
+
+
+def presplit(X: torch.Tensor, xs: float):
+    """(XP, XN) for the screen kernel, cached per (X, version, scale); None when off."""
+    import weakref
+    D = (X.shape[1] + 31) // 32 * 32
+    if D > 128 or PRESPLIT is False or X.shape[0] == 0:
+        return None
+    ref, key, val = _XSPLIT
+    k = (tuple(X.shape), X._version, xs)
+    if ref is not None and ref() is X and key == k:
+        return val
+    _XSPLIT[:] = [None, None, None]
+    need = X.shape[0] * (D * 4 + 4)
+    if PRESPLIT is None:
+        if X.shape[0] < PRESPLIT_MIN_ROWS:
+            return None
+        free, _ = torch.cuda.mem_get_info(X.device)
+        if need > free // 2:
+            return None
+    XP = torch.empty((X.shape[0], D), dtype=torch.int32, device=X.device)
+    XN = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
+    N.check(N.kernels().o3s_kmeans_presplit(X.data_ptr(), X.shape[0], X.stride(0), X.shape[1], Ct.c_float(xs),
+                                            XP.data_ptr(), XN.data_ptr(), N.stream_of(X)), "kmeans_presplit")
+    _XSPLIT[:] = [weakref.ref(X), k, (XP, XN)]
+    return XP, XN
+
+
 def screen_bound(P: "Prepared", xs: float, D: int) -> tuple[float, float]:
     """(eps_x, eps0) of the screen kernel's error bound E = eps_x ||x|| + eps0 on
     |d~_c - d_c| (unscaled units), with a 2x margin.  With x^ = fp16(x xs)/xs and
@@ -206,10 +242,12 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
         tt = SCREEN_TT or (2 if X.shape[1] <= 128 else 1)
         xs = x_scale(X)
         eps_x, eps0 = screen_bound(P, xs, X.shape[1])
+        ps = presplit(X, xs) if mode == "screen" else None
         N.check(lib.o3s_kmeans_screen(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
                                       P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
                                       Ct.c_float(eps0), Ct.c_float(xs), Ct.c_float(xs * P.ms), a.data_ptr(),
-                                      d.data_ptr(), cnt.data_ptr(), rows.data_ptr(), tt, int(mode == "pair"), st),
+                                      d.data_ptr(), cnt.data_ptr(), rows.data_ptr(), tt, int(mode == "pair"),
+                                      N.ptr(ps[0]) if ps else None, N.ptr(ps[1]) if ps else None, st),
                 "kmeans_screen")
         m = int(cnt.item())                      # the near-tie count sizes the re-solve grid
         frac = m / max(n, 1)

@@ -260,3 +260,26 @@ def test_gpu_assign_after_address_reuse_with_larger_scale(gpu):
     assert torch.all(sel <= best * (1 + 1e-5) + 1e-6 * best.max())
     assert (a1.long() == full.argmin(1)).float().mean() > 0.999
     torch.testing.assert_close(d1.double(), best, rtol=1e-4, atol=1e-3 * 1000.0 ** 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D", [32, 64, 100, 128])
+def test_gpu_presplit_screen_matches_plain_screen(gpu, D, monkeypatch):
+    """The pre-split screen (fp16 hi / lo rows built once per data version and loaded as
+    MFMA fragments) assigns exactly like the plain screen and its exact distances agree."""
+    g = torch.Generator(device="cpu").manual_seed(D)
+    X = (torch.randn(50_001, D, generator=g) * 2).to(gpu)
+    C = X[torch.randperm(50_001, generator=g)[:256].to(gpu)].clone() + 0.01
+    P = K.prepare_centers(C)
+    monkeypatch.setattr(K, "PRESPLIT", False)
+    a0, d0 = K.assign(X, C, P, mode="screen")
+    monkeypatch.setattr(K, "PRESPLIT", True)
+    a1, d1 = K.assign(X, C, P, mode="screen")
+    assert K._XSPLIT[0] is not None and K._XSPLIT[0]() is X
+    assert torch.equal(a0, a1)
+    torch.testing.assert_close(d0, d1, rtol=1e-6, atol=1e-5)
+    ra, _ = K.assign(X, C, P, mode="split")
+    assert (a1 == ra).float().mean() > 0.999
+    X.mul_(2.0)                                          # new data version: the cache must rebuild
+    a2, _ = K.assign(X, C * 2.0, K.prepare_centers(C * 2.0), mode="screen")
+    assert torch.equal(a2, a0)

@@ -37,7 +37,10 @@ def main():
     ap.add_argument("--data", default="blobs", choices=["blobs", "uniform"])
     ap.add_argument("--init", default=None, choices=["offset", "kmeans||"],
                     help="default: offset for blobs, kmeans|| for uniform")
+    ap.add_argument("--presplit", default="auto", choices=["auto", "on", "off"],
+                    help="screen kernel over pre-split fp16 rows (ops.kmeans.PRESPLIT)")
     a = ap.parse_args()
+    K.PRESPLIT = {"auto": None, "on": True, "off": False}[a.presplit]
     init = a.init or ("offset" if a.data == "blobs" else "kmeans||")
     if init == "offset" and a.data != "blobs":
         raise SystemExit("--init offset needs --data blobs (true centres)")
