@@ -214,3 +214,33 @@ def test_context_widget_lists_devices_and_reports_respawn(tmp_path):
         s.stop()
         SharedSession._session = None
         Session._active = None
+
+
+def test_pipeline_with_resident_stage_saves_and_loads_on_executors(tmp_path):
+    """A PipelineModel travels by value while its large stages stay on the executors; saving
+    it writes those stages from the executors and loading under the pool session brings
+    them back as handles."""
+    from orange3_spark_amd.ml.base import Pipeline, PipelineModel
+    from orange3_spark_amd.ml.classification import LogisticRegression, LogisticRegressionModel
+    from orange3_spark_amd.ml.feature import VectorAssembler
+    s = _pool(tmp_path, **{"o3s.executor.residentModelBytes": "1"})
+    prev = Session._active
+    Session._active = s
+    try:
+        rng = np.random.default_rng(3)
+        pdf = pd.DataFrame(rng.normal(size=(300, 3)), columns=list("abc"))
+        pdf["label"] = (pdf.a - pdf.b > 0).astype(float)
+        df = s.createDataFrame(pdf)
+        pm = Pipeline(stages=[VectorAssembler(inputCols=list("abc"), outputCol="features"),
+                              LogisticRegression(maxIter=10)]).fit(df)
+        assert type(pm) is PipelineModel and type(pm.stages[-1]) is RemoteModel
+        assert isinstance(pm.stages[-1], LogisticRegressionModel)
+        before = pm.transform(df).agg({"prediction": "sum"}).collect()[0][0]
+        path = str(tmp_path / "pm")
+        pm.write().overwrite().save(path)
+        back = PipelineModel.load(path)
+        assert type(back.stages[-1]) is RemoteModel
+        assert back.transform(df).agg({"prediction": "sum"}).collect()[0][0] == before
+    finally:
+        Session._active = prev
+        s.stop()
