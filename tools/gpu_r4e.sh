@@ -4,6 +4,15 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_als.py \
+  > gpurun_out/r4e_als_tests.log 2>&1 || { echo "als tests failed"; tail -40 gpurun_out/r4e_als_tests.log; exit 1; }
+tail -1 gpurun_out/r4e_als_tests.log
+for k in mfma_blk mfma_dp mfma_blk mfma_dp; do
+  O3S_ALS_DENSE=$k timeout -k 10 200 python -u tools/bench_als.py --rank-of 8 --users 50000000 --items 5000000 \
+    --ratings 1000000000 --iters 2 > gpurun_out/r4e_als_$k.json 2> gpurun_out/r4e_als_$k.err \
+    || { echo "bench_als $k failed"; tail -20 gpurun_out/r4e_als_$k.err; exit 1; }
+  echo "$k $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/r4e_als_$k.json').read().strip().splitlines()[-1]); print(d['value'])")"
+done
 for other in 1000000 8000000 50000000; do
   timeout -k 10 240 python -u tools/prof_als_exact.py --users 100000 --items 625000 --other 1000000 --other-item $other --reps 2 \
     > gpurun_out/r4e_als_other_$other.log 2>&1 || { echo "prof_als $other failed"; tail -20 gpurun_out/r4e_als_other_$other.log; exit 1; }
