@@ -1,8 +1,14 @@
-"""Cache DataFrame widget: pin the partition in HBM on arrival
-(reference widgets/data/spark_df_cache.py:10-40)."""
-from orange3_spark_amd.frame.dataframe import DataFrame
+"""Cache DataFrame widget: pin the partition on arrival
+(reference widgets/data/spark_df_cache.py:10-40, ``in_df.cache()``).
 
-from ..compat import Widget
+``storageLevel`` (beyond-ref): ``MEMORY_ONLY`` (default: HBM; rows of a synthetic table
+beyond the budget are recomputed from lineage), ``MEMORY_AND_DISK`` (vector rows beyond the
+HBM budget kept in pinned host memory and streamed through every pass) or ``DISK_ONLY``."""
+from orange3_spark_amd.frame.dataframe import DataFrame, StorageLevel
+
+from ..compat import Setting, Widget
+
+LEVELS = ("MEMORY_ONLY", "MEMORY_AND_DISK", "DISK_ONLY")
 
 
 class OWCacheDataFrame(Widget):
@@ -12,10 +18,17 @@ class OWCacheDataFrame(Widget):
     icon = "../icons/cache.svg"
     inputs = [("DataFrame", DataFrame, "get_input")]
     outputs = [("DataFrame", DataFrame)]
+    storageLevel = Setting("MEMORY_ONLY")
 
     def get_input(self, df):
+        self.error()
         if df is not None:
-            df = df.cache()
+            lvl = str(self.storageLevel or "MEMORY_ONLY").strip().upper()
+            if lvl not in LEVELS:
+                self.error(f"storageLevel must be one of {', '.join(LEVELS)}")
+                lvl = StorageLevel.MEMORY_ONLY
+            df = df.cache() if lvl == StorageLevel.MEMORY_ONLY else df.persist(lvl)
+            self.info(f"cached ({lvl})")
         self.send("DataFrame", df)
 
 

@@ -124,3 +124,16 @@ def test_gpu_streamed_lr_and_kmeans_match_resident(monkeypatch):
     # centre SETS (each reference centre has a streamed-fit centre within 1e-3)
     dist = np.sqrt(((A[:, None] - B[None]) ** 2).sum(-1))
     assert dist.min(0).max() < 1e-3 and km.summary.trainingCost == pytest.approx(kref.summary.trainingCost, rel=1e-4)
+
+
+def test_cache_widget_storage_level():
+    from orangecontrib.spark_amd.widgets.data.owcache import OWCacheDataFrame
+    s = _session(budget=500 * 7 * 8)
+    w = OWCacheDataFrame(storageLevel="MEMORY_AND_DISK")
+    df = _lr_frame(s)
+    w.get_input(df)
+    out = w.sent["DataFrame"]
+    assert isinstance(out.column_data("features"), SpilledVectorColumn) and out.storageLevel == "MEMORY_AND_DISK"
+    w2 = OWCacheDataFrame()
+    w2.get_input(_lr_frame(s))
+    assert w2.sent["DataFrame"].is_cached and w2.sent["DataFrame"].storageLevel == "MEMORY_ONLY"

@@ -14,9 +14,9 @@ for k in mfma_blk mfma_dp mfma_blk mfma_dp; do
   echo "$k $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/r4e_als_$k.json').read().strip().splitlines()[-1]); print(d['value'])")"
 done
 for other in 1000000 8000000 50000000; do
-  timeout -k 10 240 python -u tools/prof_als_exact.py --users 100000 --items 625000 --other 1000000 --other-item $other --reps 2 \
+  timeout -k 10 240 python -u tools/prof_als_exact.py --users 2000000 --items 625000 --other $other --other-item $other --reps 2 \
     > gpurun_out/r4e_als_other_$other.log 2>&1 || { echo "prof_als $other failed"; tail -20 gpurun_out/r4e_als_other_$other.log; exit 1; }
-  echo "other=$other $(grep '^item' gpurun_out/r4e_als_other_$other.log)"
+  echo "other=$other $(grep -E '^(user|item)' gpurun_out/r4e_als_other_$other.log | tr '\n' ' ')"
 done
 timeout -k 10 600 bash tools/pmc_als_exact.sh || { echo "pmc als failed"; exit 1; }
 cat gpurun_out/pmc_als/summary_dense.txt
