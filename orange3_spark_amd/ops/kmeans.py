@@ -81,7 +81,7 @@ def x_scale(X: torch.Tensor) -> float:
 # data version and reused by every Lloyd iteration -- the kernel's prologue then loads its
 # MFMA fragments instead of converting fp32 rows.  PRESPLIT: None = auto (when X is at least
 # PRESPLIT_MIN_ROWS rows and the copy fits in half of the free HBM), True / False forces.
-PRESPLIT: bool | None = False
+PRESPLIT: bool | None = None
 PRESPLIT_MIN_ROWS = 1 << 20
 _XSPLIT: list = [None, None, None]     # [weakref to X, (shape, version, xs), (XP, XN)]
 

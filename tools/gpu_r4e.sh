@@ -20,3 +20,13 @@ for other in 1000000 8000000 50000000; do
 done
 timeout -k 10 600 bash tools/pmc_als_exact.sh || { echo "pmc als failed"; exit 1; }
 cat gpurun_out/pmc_als/summary_dense.txt
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_trees.py \
+  > gpurun_out/r4e_tree_tests.log 2>&1 || { echo "tree tests failed"; tail -30 gpurun_out/r4e_tree_tests.log; exit 1; }
+O3S_HIST_WIDE=1 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_trees.py \
+  > gpurun_out/r4e_tree_tests_wide.log 2>&1 || { echo "tree tests (wide) failed"; tail -30 gpurun_out/r4e_tree_tests_wide.log; exit 1; }
+tail -1 gpurun_out/r4e_tree_tests_wide.log
+for wide in 0 1 0 1; do
+  O3S_HIST_WIDE=$wide timeout -k 10 200 python -u tools/bench_gbt.py --trees 3 > gpurun_out/r4e_gbt_w$wide.json 2> gpurun_out/r4e_gbt_w$wide.err \
+    || { echo "bench_gbt $wide failed"; tail -20 gpurun_out/r4e_gbt_w$wide.err; exit 1; }
+  echo "wide=$wide $(python3 -c "import json; d=json.loads(open('gpurun_out/r4e_gbt_w$wide.json').read().strip().splitlines()[-1]); print(d['value'], d['loss'][-1])")"
+done
