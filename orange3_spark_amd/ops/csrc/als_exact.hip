@@ -584,7 +584,7 @@ struct DenseM {
   static constexpr int LDS = SA + TS + NT * TS + R + 2 * CH + W * 32;
 };
 
-template <int R, bool IMPL, bool BLK, bool DP = false>
+template <int R, bool IMPL, bool BLK>
 __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
@@ -726,61 +726,20 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
         acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[s], 0, 0, 0);
       }
     };
-    if constexpr (DP) {
-      // gathers two steps ahead: register sets A / B alternate (loop unrolled by two so
-      // both stay static), so each step's factor rows have two MFMA steps to arrive
-      float ya0[ITEMS], ya1[ITEMS], yb0[ITEMS], yb1[ITEMS], wa[2][2], ba[2][2], wb[2][2], bb[2][2];
-      auto grab = [&](int64_t jb, float (&u0)[ITEMS], float (&u1)[ITEMS], float (&uw)[2][2], float (&ub)[2][2]) {
-        load(jb);
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) { u0[i] = y0[i]; u1[i] = y1[i]; }
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int par = 0; par < 2; ++par) { uw[kb][par] = wv[kb][par]; ub[kb][par] = bv[kb][par]; }
-      };
-      auto put = [&](int buf, const float (&u0)[ITEMS], const float (&u1)[ITEMS], const float (&uw)[2][2],
-                     const float (&ub)[2][2]) {
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) { y0[i] = u0[i]; y1[i] = u1[i]; }
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int par = 0; par < 2; ++par) { wv[kb][par] = uw[kb][par]; bv[kb][par] = ub[kb][par]; }
-        store(buf);
-      };
-      if (nsteps > 0) {
-        load(p0);
-        store(0);
-      }
-      if (nsteps > 1) grab(p0 + CH, ya0, ya1, wa, ba);
-      if (nsteps > 2) grab(p0 + 2 * CH, yb0, yb1, wb, bb);
+    // (gathers issued two steps ahead with two register sets measured no faster: 0.1233 vs
+    // 0.1224 s per rank-of-8 iteration, profiles/kernel_experiments_r4.json)
+    if (nsteps > 0) {
+      load(p0);
+      store(0);
+    }
+    __syncthreads();
+    for (int st = 0; st < nsteps; ++st) {
+      const int buf = st & 1;
+      const bool more = st + 1 < nsteps;
+      if (more) load(p0 + (int64_t)(st + 1) * CH);
+      gram_step(buf);
+      if (more) store(buf ^ 1);
       __syncthreads();
-      for (int st = 0; st < nsteps; st += 2) {
-        gram_step(0);                                    // step st (even): A = st + 1, B = st + 2
-        if (st + 1 < nsteps) put(1, ya0, ya1, wa, ba);
-        if (st + 3 < nsteps) grab(p0 + (int64_t)(st + 3) * CH, ya0, ya1, wa, ba);
-        __syncthreads();
-        if (st + 1 >= nsteps) break;
-        gram_step(1);                                    // step st + 1 (odd): B = st + 2, A = st + 3
-        if (st + 2 < nsteps) put(0, yb0, yb1, wb, bb);
-        if (st + 4 < nsteps) grab(p0 + (int64_t)(st + 4) * CH, yb0, yb1, wb, bb);
-        __syncthreads();
-      }
-    } else {
-      if (nsteps > 0) {
-        load(p0);
-        store(0);
-      }
-      __syncthreads();
-      for (int st = 0; st < nsteps; ++st) {
-        const int buf = st & 1;
-        const bool more = st + 1 < nsteps;
-        if (more) load(p0 + (int64_t)(st + 1) * CH);
-        gram_step(buf);
-        if (more) store(buf ^ 1);
-        __syncthreads();
-      }
     }
     // rhs: sum the item partials over the 4 rating-pair lanes, then over the 2 pair groups
     float* const rpart = lds;                                  // [2][R], staging is done
@@ -1123,7 +1082,7 @@ O3S_API int o3s_als_dense(int implicit, int R, const int64_t* indptr, const int3
 }
 
 namespace {
-template <bool BLK, bool DP = false>
+template <bool BLK>
 int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
                       const float* b, const float* F, const float* G, const float* lam, const int32_t* dense,
                       int64_t ndense, float* X, hipStream_t st) {
@@ -1132,10 +1091,10 @@ int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t*
 #define O3S_DM(RR)                                                                                              \
   if (R == RR) {                                                                                                \
     if (implicit)                                                                                               \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK, DP>), dim3((unsigned)ndense), dim3(DenseM<RR>::NTH), \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK>), dim3((unsigned)ndense), dim3(DenseM<RR>::NTH), \
                          0, st, indptr, cols, w, b, F, G, lam, dense, X);                                       \
     else                                                                                                        \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK, DP>), dim3((unsigned)ndense),                   \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK>), dim3((unsigned)ndense),                       \
                          dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X);                \
     O3S_CHECK_LAUNCH();                                                                                         \
     return 0;                                                                                                   \
@@ -1158,13 +1117,6 @@ O3S_API int o3s_als_dense_mfma_blk(int implicit, int R, const int64_t* indptr, c
                                    const float* b, const float* F, const float* G, const float* lam,
                                    const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
   return launch_dense_mfma<true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
-}
-
-// same with the factor-row gathers issued two Gram steps ahead (two register sets)
-O3S_API int o3s_als_dense_mfma_dp(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
-                                  const float* b, const float* F, const float* G, const float* lam,
-                                  const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
-  return launch_dense_mfma<true, true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
 }
 
 O3S_API int o3s_als_exact_max_small() { return kNW; }

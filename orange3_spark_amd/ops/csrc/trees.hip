@@ -20,8 +20,6 @@
 // CLS (S = #classes: weighted class counts -- gini/entropy).
 #include "common.h"
 
-#include <cstdlib>
-
 
 using namespace o3s;
 
@@ -43,7 +41,7 @@ constexpr int kHistThreads = kHistWaves * kWave;
 // YP: y / w are stored in POSITION order (y[p] belongs to row order[p]; the partition
 // moves them with the rows), so they stream contiguously instead of costing one random
 // cache-line gather each per row -- only the 64-B bins row is gathered.
-template <int FP, bool CLS, bool HW, bool YP, int U, bool WG = false>
+template <int FP, bool CLS, bool HW, bool YP, int U>
 __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
     const uint8_t* __restrict__ bins, int F, int fg0, int B, int S, const int32_t* __restrict__ order,
     const float* __restrict__ y, const float* __restrict__ w, const int64_t* __restrict__ item_lo,
@@ -71,92 +69,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
   const int32_t nl = (int32_t)(hi - lo);
   const float* __restrict__ yl = YP ? y + lo : y;
   const float* __restrict__ wl = (YP && HW) ? w + lo : w;
-  if constexpr (RS == 1 && WG) {
-    // Wide gathers (F % 64 == 0): a 32-row chunk arrives in TWO 16-B loads per lane (lane l:
-    // bytes 16 (l & 3) .. of row (l >> 2) + 16 g, the row id taken from the chunk's order[]
-    // lane by ds_bpermute) instead of 32 one-byte gathers, so 3 chunks (96 rows) are in
-    // flight per wave for 6 vmcnt slots; the chunk is transposed through a 2 KB per-wave LDS
-    // stage (ds_write_b128, then lane f reads byte f of each row: 64 consecutive bytes, no
-    // conflicts) and accumulated exactly as below.
-    constexpr int32_t CH = 32;
-    constexpr int32_t cstep = kHistWaves * CH;
-    const int32_t j0w = wid * CH;
-    uint8_t* const stg = reinterpret_cast<uint8_t*>(hist + kHistWaves * per_wave) + wid * (CH * 64);
-    const int64_t fgb = fg0 + 16 * (lane & 3);
-    struct Chunk { uint4 v0, v1; float y, w; };
-    auto ld_ord = [&](int32_t jb, int32_t& ov) {
-      const int32_t j = jb + j0w + (lane & (CH - 1));
-      ov = ord[j < nl ? j : nl - 1];
-    };
-    auto ld_chunk = [&](int32_t jb, int32_t ov, Chunk& c) {
-      const int32_t r0 = __builtin_amdgcn_ds_bpermute((lane >> 2) << 2, ov);
-      const int32_t r1 = __builtin_amdgcn_ds_bpermute(((lane >> 2) + 16) << 2, ov);
-      c.v0 = *reinterpret_cast<const uint4*>(bins + (int64_t)r0 * F + fgb);
-      c.v1 = *reinterpret_cast<const uint4*>(bins + (int64_t)r1 * F + fgb);
-      const int32_t j = jb + j0w + (lane & (CH - 1));
-      const int32_t jc = j < nl ? j : nl - 1;
-      const float yv = YP ? yl[jc] : y[ov];
-      float wv = HW ? (YP ? wl[jc] : w[ov]) : 1.f;
-      c.y = yv;
-      c.w = j < nl ? wv : 0.f;
-    };
-    auto acc_chunk = [&](const Chunk& c) {
-      *reinterpret_cast<uint4*>(stg + (lane >> 2) * 64 + 16 * (lane & 3)) = c.v0;
-      *reinterpret_cast<uint4*>(stg + ((lane >> 2) + 16) * 64 + 16 * (lane & 3)) = c.v1;
-      // all 32 bins of the chunk back to back (one LDS round trip), then the updates
-      int bos[CH];
-#pragma unroll
-      for (int q = 0; q < CH; ++q) bos[q] = stg[q * 64 + f];
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int q = 0; q < CH; ++q) {
-        const int bo = fok ? bos[q] : 0;
-        const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c.y), q));
-        const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c.w), q));
-        float* cell = my + bo * SL * FP + f;
-        if (CLS) {
-          cell[(int)yq * FP] += wq;
-        } else {
-          const float wy = wq * yq;
-          cell[0] += wq;
-          cell[FP] += wy;
-          wy2 = fmaf(wy, yq, wy2);
-        }
-      }
-    };
-    if (j0w < nl) {
-      Chunk A, B, Cc;
-      int32_t ov;
-      ld_ord(0, ov);
-      ld_chunk(0, ov, A);
-      ld_ord(cstep, ov);
-      ld_chunk(cstep, ov, B);
-      ld_ord(2 * cstep, ov);
-      for (int32_t jb = 0;; jb += 3 * cstep) {
-        __builtin_amdgcn_sched_barrier(0);
-        ld_chunk(jb + 2 * cstep, ov, Cc);
-        __builtin_amdgcn_sched_barrier(0);
-        ld_ord(jb + 3 * cstep, ov);
-        __builtin_amdgcn_sched_barrier(0);
-        acc_chunk(A);
-        if (jb + cstep + j0w >= nl) break;
-        __builtin_amdgcn_sched_barrier(0);
-        ld_chunk(jb + 3 * cstep, ov, A);
-        __builtin_amdgcn_sched_barrier(0);
-        ld_ord(jb + 4 * cstep, ov);
-        __builtin_amdgcn_sched_barrier(0);
-        acc_chunk(B);
-        if (jb + 2 * cstep + j0w >= nl) break;
-        __builtin_amdgcn_sched_barrier(0);
-        ld_chunk(jb + 4 * cstep, ov, B);
-        __builtin_amdgcn_sched_barrier(0);
-        ld_ord(jb + 5 * cstep, ov);
-        __builtin_amdgcn_sched_barrier(0);
-        acc_chunk(Cc);
-        if (jb + 3 * cstep + j0w >= nl) break;
-      }
-    }
-  } else if constexpr (RS == 1) {
+  if constexpr (RS == 1) {
     // One row per wave-instruction (lane = feature).  The per-row metadata comes in
     // 32-row chunks -- lane l loads order[] / y / w of position l of the chunk, ONE
     // vector load each per 32 rows -- and is broadcast per row with v_readlane, so a row
@@ -946,22 +859,13 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
   int fp = 1;
   while (fp < F && fp < 64) fp <<= 1;
   if (fp < 4) fp = 4;
-  int lds = o3s_tree_hist_lds(fp, B, S, cls);
+  const int lds = o3s_tree_hist_lds(fp, B, S, cls);
   if (lds == 0) return -2;
-  // wide 16-B row gathers (tree_hist_kernel WG): whole 64-feature groups only
-  const char* wide_env = getenv("O3S_HIST_WIDE");
-  const bool wide = fp == 64 && F % 64 == 0 && wide_env && wide_env[0] == '1' &&
-                    lds + kHistWaves * 32 * 64 <= 160 * 1024;
-  if (wide) lds += kHistWaves * 32 * 64;
   const int64_t stride = (int64_t)F * B * S;
   for (int fg0 = 0; fg0 < F; fg0 += fp) {
 #define O3S_TH2(FPV, C, W, P)                                                                           \
-  if (FPV == 64 && wide)                                                                                \
-    hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, 8, FPV == 64>), dim3(n_items), dim3(kHistThreads), lds, \
-                       st, bins, F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);             \
-  else                                                                                                  \
-    hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, 8>), dim3(n_items), dim3(kHistThreads), lds, st, bins, \
-                       F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
+  hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, 8>), dim3(n_items), dim3(kHistThreads), lds, st, bins,   \
+                     F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
 #define O3S_TH1(FPV, C, W)                                                                              \
   if (ypos) { O3S_TH2(FPV, C, W, true) } else { O3S_TH2(FPV, C, W, false) }
 #define O3S_TH(FPV)                                                                                     \

@@ -273,7 +273,7 @@ def test_gpu_exact_kernels_pad_other_ranks(R, implicit):
 @pytest.mark.gpu
 @pytest.mark.parametrize("R", [32, 64, 96, 128])
 @pytest.mark.parametrize("implicit", [False, True])
-@pytest.mark.parametrize("kernel", ["mfma", "mfma_blk", "mfma_dp", "vgpr"])
+@pytest.mark.parametrize("kernel", ["mfma", "mfma_blk", "vgpr"])
 def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
     """Both dense exact kernels (als_dense_mfma_kernel: 32 x 32 MFMA accumulator tiles;
     als_dense_kernel: 8 x 8 register tiles) == the fp64 solve on rows routed to the dense
@@ -288,8 +288,7 @@ def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
     dense = torch.arange(0, 40, device=F.device, dtype=torch.int32)
     got = torch.full((n, R), float("nan"), device=F.device)
     from orange3_spark_amd.ops import _native as N
-    fn = {"mfma": N.kernels().o3s_als_dense_mfma, "mfma_blk": N.kernels().o3s_als_dense_mfma_blk,
-          "mfma_dp": N.kernels().o3s_als_dense_mfma_dp}.get(
+    fn = {"mfma": N.kernels().o3s_als_dense_mfma, "mfma_blk": N.kernels().o3s_als_dense_mfma_blk}.get(
         kernel, N.kernels().o3s_als_dense)
     Gf = G.float().contiguous() if implicit else None
     N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), F.data_ptr(),
