@@ -584,11 +584,17 @@ struct DenseM {
   static constexpr int LDS = SA + TS + NT * TS + R + 2 * CH + W * 32;
 };
 
-template <int R, bool IMPL, bool BLK>
+template <int R, bool IMPL, bool BLK, bool TIM = false>
 __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
-    const float* __restrict__ lam, const int32_t* __restrict__ rows, float* __restrict__ X) {
+    const float* __restrict__ lam, const int32_t* __restrict__ rows, float* __restrict__ X,
+    int64_t* __restrict__ timing = nullptr) {
+  // TIM (diagnostic build, o3s_als_dense_mfma_timed): thread 0 stamps the shader clock at
+  // the block-synchronised phase boundaries -> timing[block][0..5] = Gram, diagonal
+  // factors, panel products, trailing updates (wave 0's share), backward, total (cycles)
+  int64_t tm0 = 0, tmA = 0, tmB = 0, tmC = 0, tmG = 0, tmP = 0;
+  if constexpr (TIM) tm0 = tmP = clock64();
   using D = DenseM<R>;
   constexpr int NT = D::NT, NL = D::NL, W = D::W, MT = D::MT, NTH = D::NTH, CH = D::CH, PNS = D::PNS,
                 TS = D::TS;
@@ -823,6 +829,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
   }
   if (tid < R) sr[tid] = rhs_t;
   __syncthreads();
+  if constexpr (TIM) { const int64_t t = clock64(); tmG = t - tm0; tmP = t; }
 
   // ---- block Cholesky A = U^T U with the forward solve U^T y = rhs riding along ----
   for (int p = 0; p < NT; ++p) {
@@ -935,6 +942,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
       }
     }
     __syncthreads();
+    if constexpr (TIM) { const int64_t t = clock64(); tmA += t - tmP; tmP = t; }
 #pragma unroll
     for (int s = 0; s < MT; ++s) {
       if (tj[s] != p || ti[s] <= p) continue;
@@ -958,6 +966,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
       if (h == 0) sr[32 * ti[s] + q] -= part;
     }
     __syncthreads();
+    if constexpr (TIM) { const int64_t t = clock64(); tmB += t - tmP; tmP = t; }
 #pragma unroll
     for (int s = 0; s < MT; ++s) {
       if (tj[s] >= NT || tj[s] <= p) continue;
@@ -970,8 +979,10 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
         acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(-aj[k * PNS], bi[k * PNS], acc[s], 0, 0, 0);
       }
     }
+    if constexpr (TIM) { const int64_t t = clock64(); tmC += t - tmP; tmP = t; }
   }
   __syncthreads();
+  if constexpr (TIM) tmP = clock64();
 
   // ---- backward U x = y ----
   for (int p = NT - 1; p >= 0; --p) {
@@ -1017,6 +1028,13 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
     __syncthreads();
   }
   if (tid < R) X[u * R + tid] = sr[tid];
+  if constexpr (TIM) {
+    if (tid == 0) {
+      const int64_t t = clock64();
+      int64_t* o = timing + (int64_t)blockIdx.x * 6;
+      o[0] = tmG; o[1] = tmA; o[2] = tmB; o[3] = tmC; o[4] = t - tmP; o[5] = t - tm0;
+    }
+  }
 }
 
 }  // namespace
@@ -1117,6 +1135,18 @@ O3S_API int o3s_als_dense_mfma_blk(int implicit, int R, const int64_t* indptr, c
                                    const float* b, const float* F, const float* G, const float* lam,
                                    const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
   return launch_dense_mfma<true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
+}
+
+// Diagnostic: the default dense kernel (BLK, implicit, R = 128) with per-block phase cycle
+// counts in timing [ndense][6] (see the kernel's TIM comment).
+O3S_API int o3s_als_dense_mfma_timed(const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
+                                     const float* F, const float* G, const float* lam, const int32_t* dense,
+                                     int64_t ndense, float* X, int64_t* timing, hipStream_t st) {
+  if (ndense <= 0 || !G || !timing) return -1;
+  hipLaunchKernelGGL((als_dense_mfma_kernel<128, true, true, true>), dim3((unsigned)ndense), dim3(DenseM<128>::NTH),
+                     0, st, indptr, cols, w, b, F, G, lam, dense, X, timing);
+  O3S_CHECK_LAUNCH();
+  return 0;
 }
 
 O3S_API int o3s_als_exact_max_small() { return kNW; }
