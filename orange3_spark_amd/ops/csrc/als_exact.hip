@@ -653,62 +653,60 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
     uint16_t* const sT = reinterpret_cast<uint16_t*>(lds);    // [buf][hi|lo][R][LDT]
     const int r_low = lane & 15, kp_low = lane >> 4;
     float y0[ITEMS], y1[ITEMS], rh[ITEMS];
-    float wv[2][2], bv[2][2];
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) rh[i] = 0.f;
     auto item_r = [&](int i) { return 16 * ((wid + 4 * i) % NRB) + r_low; };
-    auto item_kb = [&](int i) { return (wid + 4 * i) / NRB; };
-    // rating indices / weights of a step (ci = -1: past the row's end), then the factor-row
-    // gathers they address.  (Issuing the indices one step ahead of their gathers measured
-    // slower: 0.127 vs 0.122 s per rank-of-8 iteration.)
-    struct Idx { int32_t ci[2][2]; float wv[2][2], bv[2][2]; };
+    // item i's rating-pair group, as a wave-uniform bool: indexing the [2] arrays with a
+    // runtime subscript puts them in scratch memory
+    auto item_k1 = [&](int i) { return (wid + 4 * i) >= NRB; };
+    // A step's rating indices / weights are loaded with the index clamped to the row's last
+    // rating, so every load is unconditional and in bounds; ratings past the end are zeroed
+    // in store() through their weights (w = b = 0 -> z = 0, no rhs term), not by selecting
+    // on the loaded values -- a select right after a gather makes the compiler wait for it
+    // there, before the step's MFMAs.  The indices run one step ahead of their gathers.
+    struct Idx { int32_t c[2][2]; float w[2][2], b[2][2]; };
     auto load_idx = [&](int64_t jb, Idx& o) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int par = 0; par < 2; ++par) {
           const int64_t j = jb + 2 * (4 * kb + kp_low) + par;
-          const bool ok = j < p1;
-          o.ci[kb][par] = ok ? cols[j] : -1;
-          o.wv[kb][par] = ok ? w[j] : 0.f;
-          o.bv[kb][par] = ok ? b[j] : 0.f;
+          const int64_t jc = j < p1 ? j : p1 - 1;
+          o.c[kb][par] = cols[jc];
+          o.w[kb][par] = w[jc];
+          o.b[kb][par] = b[jc];
         }
     };
     auto load_f = [&](const Idx& o) {
 #pragma unroll
+      for (int i = 0; i < ITEMS; ++i) {
+        const bool k1 = item_k1(i);
+        const int r = item_r(i);
+        const int64_t c0 = k1 ? o.c[1][0] : o.c[0][0], c1 = k1 ? o.c[1][1] : o.c[0][1];
+        y0[i] = F[c0 * R + r];
+        y1[i] = F[c1 * R + r];
+      }
+    };
+    auto store = [&](int buf, const Idx& o, int64_t jb) {
+      uint32_t* const th = reinterpret_cast<uint32_t*>(sT + buf * 2 * R * LDT);
+      uint32_t* const tl = th + R * LDT / 2;
+      float sq[2][2], bv[2][2];
+#pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int par = 0; par < 2; ++par) {
-          wv[kb][par] = o.wv[kb][par];
-          bv[kb][par] = o.bv[kb][par];
+          const bool ok = jb + 2 * (4 * kb + kp_low) + par < p1;
+          sq[kb][par] = ok ? sqrtf(fmaxf(o.w[kb][par], 0.f)) : 0.f;
+          bv[kb][par] = ok ? o.b[kb][par] : 0.f;
         }
 #pragma unroll
       for (int i = 0; i < ITEMS; ++i) {
-        const int kb = item_kb(i), r = item_r(i);
-        const int64_t c0 = o.ci[kb][0] < 0 ? 0 : o.ci[kb][0], c1 = o.ci[kb][1] < 0 ? 0 : o.ci[kb][1];
-        const float v0 = F[c0 * R + r], v1 = F[c1 * R + r];
-        y0[i] = o.ci[kb][0] >= 0 ? v0 : 0.f;
-        y1[i] = o.ci[kb][1] >= 0 ? v1 : 0.f;
-      }
-    };
-    auto load = [&](int64_t jb) {
-      Idx o;
-      load_idx(jb, o);
-      load_f(o);
-    };
-    auto store = [&](int buf) {
-      uint32_t* const th = reinterpret_cast<uint32_t*>(sT + buf * 2 * R * LDT);
-      uint32_t* const tl = th + R * LDT / 2;
-      float sq[2][2];
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int par = 0; par < 2; ++par) sq[kb][par] = sqrtf(fmaxf(wv[kb][par], 0.f));
-#pragma unroll
-      for (int i = 0; i < ITEMS; ++i) {
-        const int kb = item_kb(i), r = item_r(i);
-        rh[i] = fmaf(bv[kb][1], y1[i], fmaf(bv[kb][0], y0[i], rh[i]));
-        const float z0 = sq[kb][0] * y0[i], z1 = sq[kb][1] * y1[i];
+        const bool k1 = item_k1(i);
+        const int kb = k1 ? 1 : 0, r = item_r(i);
+        const float s0 = k1 ? sq[1][0] : sq[0][0], s1 = k1 ? sq[1][1] : sq[0][1];
+        const float b0 = k1 ? bv[1][0] : bv[0][0], b1 = k1 ? bv[1][1] : bv[0][1];
+        rh[i] = fmaf(b1, y1[i], fmaf(b0, y0[i], rh[i]));
+        const float z0 = s0 * y0[i], z1 = s1 * y1[i];
         const uint16_t h0 = f32_to_bf16(z0), h1 = f32_to_bf16(z1);
         const uint16_t l0 = f32_to_bf16(z0 - bf16_to_f32(h0)), l1 = f32_to_bf16(z1 - bf16_to_f32(h1));
         const int dw = r * (LDT / 2) + 4 * kb + kp_low;
@@ -734,17 +732,26 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
     };
     // (gathers issued two steps ahead with two register sets measured no faster: 0.1233 vs
     // 0.1224 s per rank-of-8 iteration, profiles/kernel_experiments_r4.json)
+    Idx nxt;
     if (nsteps > 0) {
-      load(p0);
-      store(0);
+      Idx o;
+      load_idx(p0, o);
+      load_f(o);
+      load_idx(p0 + CH, nxt);
+      store(0, o, p0);
     }
     __syncthreads();
     for (int st = 0; st < nsteps; ++st) {
       const int buf = st & 1;
       const bool more = st + 1 < nsteps;
-      if (more) load(p0 + (int64_t)(st + 1) * CH);
+      const int64_t jn = p0 + (int64_t)(st + 1) * CH;
+      const Idx cur = nxt;                 // step st + 1's indices (loaded a step ago)
+      if (more) {
+        load_f(cur);
+        load_idx(jn + CH, nxt);
+      }
       gram_step(buf);
-      if (more) store(buf ^ 1);
+      if (more) store(buf ^ 1, cur, jn);
       __syncthreads();
     }
     // rhs: sum the item partials over the 4 rating-pair lanes, then over the 2 pair groups
@@ -754,7 +761,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
       float t = rh[i];
       t += __shfl_xor(t, 16, 64);
       t += __shfl_xor(t, 32, 64);
-      if (kp_low == 0) rpart[item_kb(i) * R + item_r(i)] = t;
+      if (kp_low == 0) rpart[(item_k1(i) ? R : 0) + item_r(i)] = t;
     }
     __syncthreads();
     if (tid < R) rhs_t = rpart[tid] + rpart[R + tid];
@@ -772,11 +779,13 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
         const int c = e / R < m ? e / R : m - 1;
         cidx[k] = cols[c0 + c];
       }
+      // rows >= m hold a copy of row m - 1 (finite), not zeros: their weights are 0, and a
+      // select on the loaded value would make the compiler wait for the gather right here
+      // instead of after the round's MFMAs
   #pragma unroll
       for (int k = 0; k < PF; ++k) {
         const int e = tid + k * NTH;
-        const float v = F[(int64_t)cidx[k] * R + e % R];
-        pf[k] = e < m * R ? v : 0.f;
+        pf[k] = F[(int64_t)cidx[k] * R + e % R];
       }
       pw = 0.f;
       pb = 0.f;
@@ -792,7 +801,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
   #pragma unroll
       for (int k = 0; k < PF; ++k) {
         const int e = tid + k * NTH;
-        if (e < CH * R) sY[e] = pf[k];         // rows >= m are zeros
+        if (e < CH * R) sY[e] = pf[k];         // rows >= m: zero weight
       }
       if (tid < CH) {
         sW[tid] = pw;

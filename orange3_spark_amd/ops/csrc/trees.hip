@@ -95,16 +95,16 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
       const int32_t j = jb + j0w + (lane & (CH - 1));
       const int32_t jc = j < nl ? j : nl - 1;
       yv = YP ? yl[jc] : y[ov];
-      wv = HW ? (YP ? wl[jc] : w[ov]) : 1.f;
-      wv = j < nl ? wv : 0.f;
+      wv = HW ? (YP ? wl[jc] : w[ov]) : 1.f;   // rows past the item: zeroed in acc_chunk
     };
     // (Grouping rows so several LDS read-modify-writes share one wait -- duplicates
     // merged first -- measured slower: the extra VALU outweighs the LDS round trips.)
-    auto acc_chunk = [&](const int (&bo)[CH], float yv, float wv) {
+    auto acc_chunk = [&](int32_t jb, const int (&bo)[CH], float yv, float wv) {
 #pragma unroll
       for (int q = 0; q < CH; ++q) {
         const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), q));
-        const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), q));
+        const float wr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), q));
+        const float wq = jb + j0w + q < nl ? wr : 0.f;                   // wave-uniform
         float* cell = my + bo[q] * SL * FP + f;
         if (CLS) {
           cell[(int)yq * FP] += wq;
@@ -117,30 +117,39 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
       }
     };
     if (j0w < nl) {
-      // per step: gathers of chunk c+1 (its order[] arrived during the previous step),
-      // order[] of chunk c+2, then the LDS updates of chunk c.  sched_barrier keeps the
-      // phases in this order (the scheduler would pull loads next to their consumers).
+      // per step: order[] of chunk c+2, then the gathers of chunk c+1, then the LDS updates
+      // of chunk c.  The order[] load goes FIRST: vmcnt retires in issue order, so the
+      // readlanes of chunk c+1's rows (next step) wait only for loads issued before chunk
+      // c+1's gathers, and two chunks of gathers stay in flight.  (Issued after the
+      // gathers, the next step's readlanes drained them with vmcnt(0): one chunk in
+      // flight, its latency exposed once per chunk.)  sched_barrier keeps the phases in
+      // this order (the scheduler would pull loads next to their consumers).  The loop runs
+      // whole chunk PAIRS with no exit between the halves: an exit there let the compiler
+      // sink the first half's gathers past it (they are dead on that path), next to their
+      // consumers.  A pair's second chunk past the item costs clamped, cached loads and a
+      // zero-weight accumulate.
       int bA[CH], bB[CH];
-      int32_t ov;
+      int32_t o1, o2;
       float yA, yB, wA, wB;
-      ld_ord(0, ov);
-      ld_chunk(0, ov, bA, yA, wA);
-      ld_ord(cstep, ov);
-      for (int32_t jb = 0;; jb += 2 * cstep) {
+      const int32_t npair = ((nl - j0w + cstep - 1) / cstep + 1) / 2;
+      ld_ord(0, o1);
+      ld_ord(cstep, o2);
+      __builtin_amdgcn_sched_barrier(0);   // o2 before chunk 0's gathers (see above)
+      ld_chunk(0, o1, bA, yA, wA);
+      for (int32_t pi = 0; pi < npair; ++pi) {
+        const int32_t jb = pi * 2 * cstep;
         __builtin_amdgcn_sched_barrier(0);
-        ld_chunk(jb + cstep, ov, bB, yB, wB);
+        ld_ord(jb + 2 * cstep, o1);
         __builtin_amdgcn_sched_barrier(0);
-        ld_ord(jb + 2 * cstep, ov);
+        ld_chunk(jb + cstep, o2, bB, yB, wB);
         __builtin_amdgcn_sched_barrier(0);
-        acc_chunk(bA, yA, wA);
-        if (jb + cstep + j0w >= nl) break;
+        acc_chunk(jb, bA, yA, wA);
         __builtin_amdgcn_sched_barrier(0);
-        ld_chunk(jb + 2 * cstep, ov, bA, yA, wA);
+        ld_ord(jb + 3 * cstep, o2);
         __builtin_amdgcn_sched_barrier(0);
-        ld_ord(jb + 3 * cstep, ov);
+        ld_chunk(jb + 2 * cstep, o1, bA, yA, wA);
         __builtin_amdgcn_sched_barrier(0);
-        acc_chunk(bB, yB, wB);
-        if (jb + 2 * cstep + j0w >= nl) break;
+        acc_chunk(jb + cstep, bB, yB, wB);
       }
     }
   } else {
@@ -158,7 +167,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
         r[u] = ord[j < nl ? j : nl - 1];
       }
     };
-    auto ld_data = [&](int32_t jb, const int32_t (&r)[U], int (&bo)[U], float (&yo)[U], float (&wo)[U]) {
+    auto ld_data = [&](int32_t jb, const int32_t (&r)[U], uint8_t (&bo)[U], float (&yo)[U], float (&wo)[U]) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t row = r[u];
@@ -174,7 +183,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
         }
       }
     };
-    auto accumulate = [&](int32_t jb, const int (&bo)[U], const float (&yo)[U], const float (&wo)[U]) {
+    auto accumulate = [&](int32_t jb, const uint8_t (&bo)[U], const float (&yo)[U], const float (&wo)[U]) {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const bool ok = fok && (jb + jw + u * RS < nl);
@@ -191,19 +200,29 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
       }
     };
     int32_t rA[U], rB[U];
-    int bA[U], bB[U];
+    uint8_t bA[U], bB[U];   // bytes: an int copy made the compiler widen them at the loop head (a drain)
     float yA[U], yB[U], wA[U], wB[U];
     if (jw < nl) {
+      // order[] of batch k+2 is issued BEFORE batch k+1's gathers, and the loop runs whole
+      // batch pairs (see the RS == 1 path)
+      const int32_t npair = ((nl + step - 1) / step + 1) / 2;
       ld_rows(0, rA);
-      ld_data(0, rA, bA, yA, wA);
       ld_rows(step, rB);
-      for (int32_t j0 = 0; j0 < nl; j0 += 2 * step) {
-        ld_data(j0 + step, rB, bB, yB, wB);
+      __builtin_amdgcn_sched_barrier(0);
+      ld_data(0, rA, bA, yA, wA);
+      for (int32_t pi = 0; pi < npair; ++pi) {
+        const int32_t j0 = pi * 2 * step;
+        __builtin_amdgcn_sched_barrier(0);
         ld_rows(j0 + 2 * step, rA);
+        __builtin_amdgcn_sched_barrier(0);
+        ld_data(j0 + step, rB, bB, yB, wB);
+        __builtin_amdgcn_sched_barrier(0);
         accumulate(j0, bA, yA, wA);
-        if (j0 + step >= nl) break;
-        ld_data(j0 + 2 * step, rA, bA, yA, wA);
+        __builtin_amdgcn_sched_barrier(0);
         ld_rows(j0 + 3 * step, rB);
+        __builtin_amdgcn_sched_barrier(0);
+        ld_data(j0 + 2 * step, rA, bA, yA, wA);
+        __builtin_amdgcn_sched_barrier(0);
         accumulate(j0 + step, bB, yB, wB);
       }
     }
