@@ -30,6 +30,15 @@ class KMeansResult:
     seconds: float = 0.0
 
 
+def _sum_sq(X: torch.Tensor) -> torch.Tensor:
+    """sum ||x||^2 over the rows (fp64 accumulation, bounded row chunks: no fp64 copy of X)."""
+    s = torch.zeros((), dtype=torch.float64, device=X.device)
+    step = max(1, (1 << 26) // max(1, X.shape[1]))
+    for i in range(0, X.shape[0], step):
+        s += torch.linalg.vector_norm(X[i:i + step], 2, dtype=torch.float64) ** 2
+    return s
+
+
 def _global_rows(comm, n_local, device):
     sizes = comm.all_gather_object(int(n_local))
     off = sum(sizes[: comm.rank])
@@ -284,17 +293,26 @@ def fit_kmeans(comm, X, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int
         hist = [float(v) for v in st["hist"]]
     sizes = None
     cost = float("nan")
+    # unweighted: an iteration's cost comes from its cluster sums S_a and counts n_a,
+    #   sum_x ||x - c_a(x)||^2 = sum_x ||x||^2 - sum_a (2 c_a.S_a - n_a ||c_a||^2)
+    # (fp64), so the assign pass needs no per-row distance (the screen kernel then skips the
+    # exact-distance epilogue and half of its row reads)
+    sumsq = _sum_sq(X) if weights is None else None
     for it in range(start + 1, max_iter + 1):
         with trace("kmeans.iter"):
             prep = K.prepare_centers(C.float()) if K.kernel_ok(X) else None
-            a, d = K.assign(X, C.float(), prep)
+            a, d = K.assign(X, C.float(), prep, need_dist=weights is not None)
             if ws is not None:
                 sums, cnt = K.update(X, a, ws.K, ws)
                 sums, cnt = sums[:k], cnt[:k]
             else:
                 sums, cnt = K.update_torch(X, a, k, weights)
-            dd = d.to(torch.float64) if weights is None else d.to(torch.float64) * weights.to(torch.float64)
-            buf = torch.cat([sums.reshape(-1), cnt, dd.sum().reshape(1)])
+            if weights is None:
+                Cd = C.to(sums.device, torch.float64)
+                local = sumsq - (2.0 * (Cd * sums).sum() - (cnt * (Cd * Cd).sum(1)).sum())
+            else:
+                local = (d.to(torch.float64) * weights.to(torch.float64)).sum()
+            buf = torch.cat([sums.reshape(-1), cnt, local.reshape(1)])
             comm.all_reduce(buf)
             sums, cnt, cost = buf[: k * D].reshape(k, D), buf[k * D: k * D + k], float(buf[-1])
             hist.append(cost)

@@ -582,9 +582,16 @@ struct DenseM {
   static constexpr int SA1 = SA0 > W * TS ? SA0 : W * TS;
   static constexpr int SA = SA1 > R * 48 ? SA1 : R * 48;   // staging / panel / backward scratch
   static constexpr int LDS = SA + TS + NT * TS + R + 2 * CH + W * 32;
+  // glds ring layout (GL, R = 128): the factor rows of DEP Gram steps land in LDS by
+  // LDS-DMA (no VGPRs hold in-flight gathers); the ring shares its region with the diagonal
+  // staging / X_p images, which are only used after the Gram.  IC = rating indices staged
+  // per chunk (one refill per IC ratings).
+  static constexpr int DEP = 3, IC = 128;
+  static constexpr int XR = TS + NT * TS > DEP * CH * R ? TS + NT * TS : DEP * CH * R;
+  static constexpr int LDSG = SA + XR + R + 2 * CH + W * 32 + 3 * IC + 2 * DEP * CH;
 };
 
-template <int R, bool IMPL, bool BLK, bool TIM = false>
+template <int R, bool IMPL, bool BLK, bool TIM = false, bool GL = false>
 __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
@@ -599,13 +606,14 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
   constexpr int NT = D::NT, NL = D::NL, W = D::W, MT = D::MT, NTH = D::NTH, CH = D::CH, PNS = D::PNS,
                 TS = D::TS;
   constexpr bool G3 = BLK && W == 4;     // bf16x3 Gram (16 staging threads per rating)
-  __shared__ __attribute__((aligned(16))) float lds[D::LDS];
+  constexpr bool GLP = GL && G3 && R == 128;   // factor-row gathers by LDS-DMA into a ring
+  __shared__ __attribute__((aligned(16))) float lds[GLP ? D::LDSG : D::LDS];
   float* const sY = lds;                 // Gram: staged factor rows [CH][R]
   float* const sPn = lds;                // factor: row panel [32][PNS]
   float* const sScr = lds;               // backward: per-wave transpose [W][32][33]
   float* const sD = lds + D::SA;         // diagonal tile staging [32][33]
   float* const sX = sD + TS;             // X_p = L_pp^-1, every p: [NT][32][33]
-  float* const sr = sX + NT * TS;        // rhs -> y -> x
+  float* const sr = GLP ? lds + D::SA + D::XR : sX + NT * TS;   // rhs -> y -> x
   float* const sW = sr + R;
   float* const sB = sW + CH;
   float* const sWp = sB + CH;            // backward partial sums [W][32]
@@ -732,6 +740,100 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
     };
     // (gathers issued two steps ahead with two register sets measured no faster: 0.1233 vs
     // 0.1224 s per rank-of-8 iteration, profiles/kernel_experiments_r4.json)
+    if constexpr (GLP) {
+      // ---- LDS-DMA ring: the gathers of step s + DEP are issued while step s's MFMAs and
+      // step s + 1's conversion run, so DEP - 1 steps of factor rows (16 KB per block) stay
+      // in flight across the barriers with no VGPR holding them.  Each wave gathers 4 of a
+      // step's 16 rows as 2 global_load_lds_dwordx4 (one row = 32 lanes x 16 B; the DMA image
+      // is lane-linear, rows contiguous).  The rating indices come from an LDS chunk, so no
+      // ordinary global load is consumed while a DMA is outstanding (hipcc would drain the
+      // ring with vmcnt(0) there); only the chunk refill, once per IC ratings, drains it.
+      // Barriers are raw s_barrier + lgkmcnt(0): __syncthreads()' fence would wait vmcnt(0).
+      constexpr int DEP = D::DEP, IC = D::IC;
+      float* const ring = lds + D::SA;                                  // [DEP][CH][R]
+      int32_t* const sCi = reinterpret_cast<int32_t*>(sWp + W * 32);    // index chunk [IC]
+      float* const sWc = reinterpret_cast<float*>(sCi + IC);            // w of the chunk
+      float* const sBc = sWc + IC;                                      // b of the chunk
+      float* const sWs = sBc + IC;                                      // per slot: sqrt(w), 0 past the row
+      float* const sBs = sWs + DEP * CH;                                // per slot: b, 0 past the row
+      auto bar = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      };
+      int64_t cb = -(int64_t)IC - 1;       // first rating of the staged chunk (block-uniform)
+      auto issue = [&](int s) {
+        const int64_t j0 = p0 + (int64_t)s * CH;
+        if (j0 >= cb + IC) {               // chunks start at step boundaries (IC % CH == 0)
+          cb = j0;
+          if (tid < IC) {
+            const int64_t j = j0 + tid < p1 ? j0 + tid : p1 - 1;
+            sCi[tid] = cols[j];
+            sWc[tid] = w[j];
+            sBc[tid] = b[j];
+          }
+          bar();
+        }
+        const int slot = s % DEP, o = (int)(j0 - cb);
+        if (tid < CH) {
+          const bool ok = j0 + tid < p1;
+          sWs[slot * CH + tid] = ok ? sqrtf(fmaxf(sWc[o + tid], 0.f)) : 0.f;
+          sBs[slot * CH + tid] = ok ? sBc[o + tid] : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int rr = 4 * wid + 2 * k;                               // wave-uniform
+          const int64_t c = sCi[o + rr + h];                            // clamped at refill
+          __builtin_amdgcn_global_load_lds(F + c * R + 4 * q, ring + (slot * CH + rr) * R, 16, 0, 0);
+        }
+      };
+      auto convert = [&](const float* __restrict__ rg, const float* __restrict__ ws,
+                         const float* __restrict__ bs, uint16_t* __restrict__ dst) {
+        uint32_t* const th = reinterpret_cast<uint32_t*>(dst);
+        uint32_t* const tl = th + R * LDT / 2;
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+          const int kb = item_k1(i) ? 1 : 0, r = item_r(i);
+          const int c0 = 2 * (4 * kb + kp_low);
+          const float u0 = rg[c0 * R + r], u1 = rg[(c0 + 1) * R + r];
+          const float s0 = ws[c0], s1 = ws[c0 + 1];
+          rh[i] = fmaf(bs[c0 + 1], u1, fmaf(bs[c0], u0, rh[i]));
+          const float z0 = s0 * u0, z1 = s1 * u1;
+          const uint16_t h0 = f32_to_bf16(z0), h1 = f32_to_bf16(z1);
+          const uint16_t l0 = f32_to_bf16(z0 - bf16_to_f32(h0)), l1 = f32_to_bf16(z1 - bf16_to_f32(h1));
+          const int dw = r * (LDT / 2) + 4 * kb + kp_low;
+          th[dw] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+          tl[dw] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+        }
+      };
+      auto conv = [&](int s) {
+        const int slot = s % DEP;
+        convert(ring + slot * CH * R, sWs + slot * CH, sBs + slot * CH, sT + (s & 1) * 2 * R * LDT);
+      };
+      if (nsteps > 0) {
+        issue(0);
+        if (nsteps > 1) issue(1);
+        if (nsteps > 2) issue(2);
+        if (nsteps > 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (nsteps > 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();                                                          // step 0 landed
+        conv(0);
+        if (nsteps > 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        bar();                                                          // step 1 landed, sT[0] ready
+      }
+      for (int st = 0; st < nsteps; ++st) {
+        gram_step(st & 1);
+        if (st + 1 < nsteps) conv(st + 1);
+        if (st + DEP < nsteps) {
+          issue(st + DEP);                 // into the slot step st vacated
+          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");             // step st + 2 landed
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar();
+      }
+    } else {
     Idx nxt;
     if (nsteps > 0) {
       Idx o;
@@ -753,6 +855,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
       gram_step(buf);
       if (more) store(buf ^ 1, cur, jn);
       __syncthreads();
+    }
     }
     // rhs: sum the item partials over the 4 rating-pair lanes, then over the 2 pair groups
     float* const rpart = lds;                                  // [2][R], staging is done
@@ -1109,7 +1212,7 @@ O3S_API int o3s_als_dense(int implicit, int R, const int64_t* indptr, const int3
 }
 
 namespace {
-template <bool BLK>
+template <bool BLK, bool GL = false>
 int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
                       const float* b, const float* F, const float* G, const float* lam, const int32_t* dense,
                       int64_t ndense, float* X, hipStream_t st) {
@@ -1118,11 +1221,11 @@ int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t*
 #define O3S_DM(RR)                                                                                              \
   if (R == RR) {                                                                                                \
     if (implicit)                                                                                               \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK>), dim3((unsigned)ndense), dim3(DenseM<RR>::NTH), \
-                         0, st, indptr, cols, w, b, F, G, lam, dense, X);                                       \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK, false, GL>), dim3((unsigned)ndense),             \
+                         dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X, nullptr);       \
     else                                                                                                        \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK>), dim3((unsigned)ndense),                       \
-                         dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X);                \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK, false, GL>), dim3((unsigned)ndense),            \
+                         dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X, nullptr);       \
     O3S_CHECK_LAUNCH();                                                                                         \
     return 0;                                                                                                   \
   }
@@ -1134,7 +1237,8 @@ int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t*
 
 // Dense solves on the matrix cores (als_dense_mfma_kernel); same contract as o3s_als_dense.
 // o3s_als_dense_mfma: diagonal tiles factored column by column (32 LDS broadcasts per
-// tile); o3s_als_dense_mfma_blk: 4-column blocks, row and X column sharing one register array.
+// tile); o3s_als_dense_mfma_blk: 4-column blocks, row and X column sharing one register array;
+// o3s_als_dense_mfma_gl: _blk with the R = 128 Gram fed by the LDS-DMA gather ring.
 O3S_API int o3s_als_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
                                const float* b, const float* F, const float* G, const float* lam, const int32_t* dense,
                                int64_t ndense, float* X, hipStream_t st) {
@@ -1145,15 +1249,24 @@ O3S_API int o3s_als_dense_mfma_blk(int implicit, int R, const int64_t* indptr, c
                                    const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
   return launch_dense_mfma<true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
 }
+O3S_API int o3s_als_dense_mfma_gl(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
+                                  const float* b, const float* F, const float* G, const float* lam,
+                                  const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
+  return launch_dense_mfma<true, true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
+}
 
-// Diagnostic: the default dense kernel (BLK, implicit, R = 128) with per-block phase cycle
-// counts in timing [ndense][6] (see the kernel's TIM comment).
-O3S_API int o3s_als_dense_mfma_timed(const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
-                                     const float* F, const float* G, const float* lam, const int32_t* dense,
-                                     int64_t ndense, float* X, int64_t* timing, hipStream_t st) {
+// Diagnostic: the dense kernel (BLK, implicit, R = 128; gl != 0: with the LDS-DMA gather
+// ring) with per-block phase cycle counts in timing [ndense][6] (see the kernel's TIM comment).
+O3S_API int o3s_als_dense_mfma_timed(int gl, const int64_t* indptr, const int32_t* cols, const float* w,
+                                     const float* b, const float* F, const float* G, const float* lam,
+                                     const int32_t* dense, int64_t ndense, float* X, int64_t* timing, hipStream_t st) {
   if (ndense <= 0 || !G || !timing) return -1;
-  hipLaunchKernelGGL((als_dense_mfma_kernel<128, true, true, true>), dim3((unsigned)ndense), dim3(DenseM<128>::NTH),
-                     0, st, indptr, cols, w, b, F, G, lam, dense, X, timing);
+  if (gl)
+    hipLaunchKernelGGL((als_dense_mfma_kernel<128, true, true, true, true>), dim3((unsigned)ndense),
+                       dim3(DenseM<128>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X, timing);
+  else
+    hipLaunchKernelGGL((als_dense_mfma_kernel<128, true, true, true>), dim3((unsigned)ndense),
+                       dim3(DenseM<128>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X, timing);
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -332,7 +332,11 @@ struct ScrLds {
   static constexpr int BYTES = STAGE_BYTES > X_BYTES ? STAGE_BYTES : X_BYTES;
 };
 
-template <int KS, int TT, bool PAIR, bool PS = false>
+// NOD (plain screen, mind == nullptr: the Lloyd iterations, whose cost comes from the
+// cluster sums -- models/kmeans.py): no per-row distance, so neither the lo half of x (the
+// pre-split rows' second 16 B: half the prologue's HBM bytes) nor the chosen centre's fp32
+// row (an L2 gather of D floats per row) is read.
+template <int KS, int TT, bool PAIR, bool PS = false, bool NOD = false>
 __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const float* __restrict__ X, int64_t n, int64_t ldx, const uint16_t* __restrict__ Chi,
     const float* __restrict__ cn, const float* __restrict__ C32, int ldc, int Cpad, float eps_x, float eps0,
@@ -379,12 +383,12 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         hv[ks] = src[(ks * 2 + h) * 2];
-        lv[ks] = src[(ks * 2 + h) * 2 + 1];
+        if constexpr (!NOD) lv[ks] = src[(ks * 2 + h) * 2 + 1];
       }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         bh[t][ks] = __builtin_bit_cast(bf16x8, hv[ks]);
-        bl[t][ks] = __builtin_bit_cast(bf16x8, lv[ks]);
+        if constexpr (!NOD) bl[t][ks] = __builtin_bit_cast(bf16x8, lv[ks]);
       }
       xn[t] = XN[rowc];
     }
@@ -430,7 +434,8 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       }
       bh[t][ks] = __builtin_bit_cast(bf16x8, ph);
       bl[t][ks] = __builtin_bit_cast(bf16x8, pl);
-      asm volatile("" : "+v"(bh[t][ks]), "+v"(bl[t][ks]));
+      if constexpr (NOD) asm volatile("" : "+v"(bh[t][ks]));
+      else asm volatile("" : "+v"(bh[t][ks]), "+v"(bl[t][ks]));
     }
     xn[t] = s + __shfl_xor(s, 32, 64);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slice reads done before the next tile
@@ -649,6 +654,8 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const float ixs = 1.f / xscale;
     const int idc = idx_ok ? idx : 0;
     const int idc2 = idx2 >= 0 && idx2 < Cpad ? idx2 : idc;
+    float s = 0.f, s2 = 0.f;
+    if constexpr (!NOD) {
     const float* cp = C32 + (int64_t)idc * ldc;
     const float* cq = C32 + (int64_t)idc2 * ldc;
     // every centre-row load in flight before the first use (one L2 round trip, not KS)
@@ -659,7 +666,6 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       cu[ks] = *reinterpret_cast<const float4*>(cp + (c0 < Dx ? c0 : 0));
       cwv[ks] = *reinterpret_cast<const float4*>(cp + (c0 + 4 < Dx ? c0 + 4 : 0));
     }
-    float s = 0.f, s2 = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int c0 = ks * 16 + 8 * h;
@@ -696,6 +702,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     }
     s += __shfl_xor(s, 32, 64);
     if (PAIR) s2 += __shfl_xor(s2, 32, 64);
+    }
     const int64_t row = row_base + t * 32 + r;
     // in the scaled units of bv, sec; the plain screen's slot codes move each key by less
     // than 2^-19 of its magnitude (twice that allowed for)
@@ -714,7 +721,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     }
     if (ok) {
       assign[row] = pick;
-      if (mind) mind[row] = pd;
+      if (!NOD && mind) mind[row] = pd;
     }
     const uint64_t m = __ballot(fl);
     if (m) {
@@ -1105,10 +1112,18 @@ O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, co
     const int64_t grid = (n + rows_per_block - 1) / rows_per_block;                                        \
     const size_t dyn = ScrLds<KS>::BYTES + cdyn;                                                           \
     if (dyn > 160 * 1024) return -3;                                                                       \
-    if (XP && !P)                                                                                          \
+    if (XP && !P && !mind)                                                                                 \
+      hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, true, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, \
+                         st, X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind,     \
+                         flag_cnt, flag_rows, Dx, (const uint4*)XP, XN);                                   \
+    else if (XP && !P)                                                                                     \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, \
                          X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt, \
                          flag_rows, Dx, (const uint4*)XP, XN);                                             \
+    else if (!P && !mind)                                                                                  \
+      hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, false, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, \
+                         st, X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind,     \
+                         flag_cnt, flag_rows, Dx, nullptr, nullptr);                                       \
     else                                                                                                   \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, X, n, \
                          ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt,   \

@@ -204,8 +204,11 @@ def screen_ok(X: torch.Tensor) -> bool:
     return kernel_ok(X) and X.shape[0] < 2 ** 31
 
 
-def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", stats: dict | None = None):
-    """(cluster int32 [n], squared distance f32 [n]) of every row of X.
+def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", stats: dict | None = None,
+           need_dist: bool = True):
+    """(cluster int32 [n], squared distance f32 [n]) of every row of X.  ``need_dist=False``
+    returns (cluster, None) and lets the screen kernel skip the per-row exact distance (the
+    lo half of the pre-split rows and the chosen centre's fp32 row are then never read).
 
     GPU: ``mode='screen'`` runs the one-MFMA screen kernel and re-solves only its near-tie
     rows with the split-precision kernel; ``'pair'`` is the screen that also settles
@@ -214,11 +217,12 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
     previous call on this X flagged more than ``SCREEN_MAX_FLAG_FRACTION`` of its rows, and
     re-probes the screen every ``SPLIT_REPROBE`` split calls."""
     if not kernel_ok(X):
-        return assign_torch(X, C)
+        a, d = assign_torch(X, C)
+        return a, (d if need_dist else None)
     P = prepared if isinstance(prepared, Prepared) else prepare_centers(C)
     n = X.shape[0]
     a = torch.empty(n, dtype=torch.int32, device=X.device)
-    d = torch.empty(n, dtype=torch.float32, device=X.device)
+    d = torch.empty(n, dtype=torch.float32, device=X.device) if need_dist else None
     lib = N.kernels()
     st = N.stream_of(X)
     # near-tie rates depend on the centre set: keyed by the padded centre count too, so
@@ -246,7 +250,7 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
         N.check(lib.o3s_kmeans_screen(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
                                       P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
                                       Ct.c_float(eps0), Ct.c_float(xs), Ct.c_float(xs * P.ms), a.data_ptr(),
-                                      d.data_ptr(), cnt.data_ptr(), rows.data_ptr(), tt, int(mode == "pair"),
+                                      N.ptr(d), cnt.data_ptr(), rows.data_ptr(), tt, int(mode == "pair"),
                                       N.ptr(ps[0]) if ps else None, N.ptr(ps[1]) if ps else None, st),
                 "kmeans_screen")
         m = int(cnt.item())                      # the near-tie count sizes the re-solve grid
@@ -262,10 +266,10 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
         if m:
             N.check(lib.o3s_kmeans_assign(X.data_ptr(), m, X.stride(0), X.shape[1], P.hi.data_ptr(),
                                           P.lo.data_ptr(), P.cn.data_ptr(), P.hi.shape[0], a.data_ptr(),
-                                          d.data_ptr(), rows.data_ptr(), st), "kmeans_assign(recheck)")
+                                          N.ptr(d), rows.data_ptr(), st), "kmeans_assign(recheck)")
         return a, d
     N.check(lib.o3s_kmeans_assign(X.data_ptr(), n, X.stride(0), X.shape[1], P.hi.data_ptr(), P.lo.data_ptr(),
-                                  P.cn.data_ptr(), P.hi.shape[0], a.data_ptr(), d.data_ptr(), None, st),
+                                  P.cn.data_ptr(), P.hi.shape[0], a.data_ptr(), N.ptr(d), None, st),
             "kmeans_assign")
     if stats is not None:
         stats["flagged"] = n

@@ -189,6 +189,7 @@ def _exact_case(R, implicit, seed=0, n_rows=700, n_other=900, dev="cuda"):
     lens = torch.randint(0, 40, (n_rows,), generator=g)
     lens[:6] = torch.tensor([0, 1, 5, 32, 33, 200])
     lens[6:40] = torch.randint(60, 260, (34,), generator=g)
+    lens[6] = 1000                                  # several index-chunk refills (mfma_gl)
     indptr = torch.zeros(n_rows + 1, dtype=torch.int64)
     indptr[1:] = torch.cumsum(lens, 0)
     nnz = int(indptr[-1])
@@ -273,7 +274,7 @@ def test_gpu_exact_kernels_pad_other_ranks(R, implicit):
 @pytest.mark.gpu
 @pytest.mark.parametrize("R", [32, 64, 96, 128])
 @pytest.mark.parametrize("implicit", [False, True])
-@pytest.mark.parametrize("kernel", ["mfma", "mfma_blk", "vgpr"])
+@pytest.mark.parametrize("kernel", ["mfma", "mfma_blk", "mfma_gl", "vgpr"])
 def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
     """Both dense exact kernels (als_dense_mfma_kernel: 32 x 32 MFMA accumulator tiles;
     als_dense_kernel: 8 x 8 register tiles) == the fp64 solve on rows routed to the dense
@@ -288,8 +289,9 @@ def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
     dense = torch.arange(0, 40, device=F.device, dtype=torch.int32)
     got = torch.full((n, R), float("nan"), device=F.device)
     from orange3_spark_amd.ops import _native as N
-    fn = {"mfma": N.kernels().o3s_als_dense_mfma, "mfma_blk": N.kernels().o3s_als_dense_mfma_blk}.get(
-        kernel, N.kernels().o3s_als_dense)
+    lib = N.kernels()
+    fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
+          "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(kernel, lib.o3s_als_dense)
     Gf = G.float().contiguous() if implicit else None
     N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), F.data_ptr(),
                N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), 40, got.data_ptr(), N.stream_of(got)), "als_dense")

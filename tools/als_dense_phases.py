@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--items", type=int, default=625_000)
     ap.add_argument("--other", type=int, default=8_000_000)
+    ap.add_argument("--gl", type=int, default=1, help="phase-time the LDS-DMA ring variant")
     a = ap.parse_args()
     from orange3_spark_amd.models import als as AE
     from orange3_spark_amd.ops import _native as N
@@ -42,17 +43,22 @@ def main():
     lib = N.kernels()
     st = N.stream_of(out)
 
+    def prod_gl():
+        N.check(lib.o3s_als_dense_mfma_gl(1, R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                          F.data_ptr(), G.data_ptr(), lam.data_ptr(), dense.data_ptr(), a.items,
+                                          out.data_ptr(), st), "dense_gl")
+
     def prod():
         N.check(lib.o3s_als_dense_mfma_blk(1, R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                                            F.data_ptr(), G.data_ptr(), lam.data_ptr(), dense.data_ptr(), a.items,
                                            out.data_ptr(), st), "dense")
 
     def timed():
-        N.check(lib.o3s_als_dense_mfma_timed(indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+        N.check(lib.o3s_als_dense_mfma_timed(int(a.gl), indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                                              F.data_ptr(), G.data_ptr(), lam.data_ptr(), dense.data_ptr(), a.items,
                                              out.data_ptr(), tim.data_ptr(), st), "dense_timed")
     res = {}
-    for name, fn in (("production", prod), ("timed", timed)):
+    for name, fn in (("production_blk", prod), ("production_gl", prod_gl), ("timed", timed)):
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -65,7 +71,8 @@ def main():
     names = ["gram", "diag_factor", "panel_products", "trailing_updates_wave0", "backward", "total"]
     res["cycles_per_block_mean"] = dict(zip(names, [round(x) for x in m]))
     res["share_of_block"] = {k: round(v / m[5], 3) for k, v in zip(names[:5], m[:5])}
-    res["items"], res["other_rows"], res["ratings"] = a.items, a.other, nnz
+    res["items"], res["other_rows"], res["ratings"], res["timed_variant"] = a.items, a.other, nnz, \
+        "mfma_gl" if a.gl else "mfma_blk"
     print(json.dumps(res))
 
 

@@ -39,6 +39,9 @@ def main():
                     help="default: offset for blobs, kmeans|| for uniform")
     ap.add_argument("--presplit", default="auto", choices=["auto", "on", "off"],
                     help="screen kernel over pre-split fp16 rows (ops.kmeans.PRESPLIT)")
+    ap.add_argument("--cost", default="sums", choices=["sums", "rows"],
+                    help="iteration cost from the cluster sums (the fit's path: no per-row distance in the "
+                         "assign pass) or from per-row distances")
     a = ap.parse_args()
     K.PRESPLIT = {"auto": None, "on": True, "off": False}[a.presplit]
     init = a.init or ("offset" if a.data == "blobs" else "kmeans||")
@@ -66,13 +69,21 @@ def main():
         torch.cuda.synchronize()
         t_init = time.perf_counter() - t1
     ws = K.UpdateWorkspace(X.device, (a.k + 31) // 32 * 32, a.d)
+    need = a.cost == "rows"
+    from orange3_spark_amd.models.kmeans import _sum_sq
+    sumsq = _sum_sq(X)
     torch.cuda.synchronize()
 
     def it(C):
         prep = K.prepare_centers(C)
-        asg, d = K.assign(X, C, prep, mode=a.mode)
+        asg, d = K.assign(X, C, prep, mode=a.mode, need_dist=need)
         sums, cnt = K.update(X, asg, ws.K, ws)
-        buf = torch.cat([sums[: a.k].reshape(-1), cnt[: a.k], d.double().sum().reshape(1)])
+        if need:
+            cost = d.double().sum()
+        else:
+            Cd = C.double()
+            cost = sumsq - (2.0 * (Cd * sums[: a.k]).sum() - (cnt[: a.k] * (Cd * Cd).sum(1)).sum())
+        buf = torch.cat([sums[: a.k].reshape(-1), cnt[: a.k], cost.reshape(1)])
         comm.all_reduce(buf)
         cnt = buf[a.k * a.d: a.k * a.d + a.k]
         sums = buf[: a.k * a.d].reshape(a.k, a.d)
@@ -84,7 +95,7 @@ def main():
     prep = K.prepare_centers(C)
     st = {}
     for _ in range(a.iters):
-        asg, d = K.assign(X, C, prep, mode=a.mode, stats=st)
+        asg, d = K.assign(X, C, prep, mode=a.mode, stats=st, need_dist=need)
     torch.cuda.synchronize()
     t_assign = (time.perf_counter() - t_assign) / a.iters
     t_upd = time.perf_counter()
@@ -104,7 +115,7 @@ def main():
     out = {"metric": "KMeans Lloyd iteration samples/s (k=1024, 100M x 128 fp32)", "value": a.rows / dt,
            "unit": "samples/s", "ms_per_iter": dt * 1e3, "assign_ms": t_assign * 1e3, "update_ms": t_upd * 1e3,
            rate_key: flop / t_assign / 1e12, "rows": a.rows, "d": a.d, "k": a.k, "cost": cost,
-           "data": a.data, "init": init, "init_s": t_init, "assign_mode": a.mode,
+           "data": a.data, "cost_from": a.cost, "init": init, "init_s": t_init, "assign_mode": a.mode,
            "near_tie_rows_resolved": flagged, "flagged_fraction": None if flagged is None else flagged / a.rows}
     if a.torch_baseline:
         t1 = time.perf_counter()
