@@ -118,12 +118,14 @@ def dense_solve(indptr, cols, w, b, F, FtF, lam, batch_bytes: int = 1 << 30) -> 
 
 
 EXACT_RANKS = (32, 64, 96, 128)
-# dense (long-row) exact solves: "mfma_blk" (default) = als_dense_mfma_kernel with 4-column
-# diagonal blocks and, at R = 96 / 128, the bf16x3 Gram (0.120 s/iter at the rank-of-8 ALS
-# shapes); "mfma" = the same kernel with column-by-column diagonals and the f32 Gram
-# (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144).  Rejected:
-# rating indices prefetched one Gram step ahead of the gathers (0.127 vs 0.122 s)
-DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_blk")
+# dense (long-row) exact solves: "mfma_gl" (default) = als_dense_mfma_kernel with 4-column
+# diagonal blocks and, at R = 96 / 128, the bf16x3 Gram; at R = 128 its factor rows are
+# gathered by LDS-DMA into a 3-step ring (45.1 vs 46.6 ms for 625K items x 200 ratings;
+# 0.1067 vs 0.1087 s per rank-of-8 iteration, profiles/als_gl_ring_r4.json); "mfma_blk" =
+# the same kernel with register-staged gathers; "mfma" = column-by-column diagonals and
+# the f32 Gram (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144).
+# Rejected: rating indices prefetched one Gram step ahead of the gathers (0.127 vs 0.122 s)
+DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_gl")
 
 
 def exact_kernel_ok(F: torch.Tensor) -> bool:

@@ -35,6 +35,25 @@ namespace {
 constexpr int kHistWaves = 2;
 constexpr int kHistThreads = kHistWaves * kWave;
 
+// bins + row * F computed on the SALU (row and F are wave-uniform): left to the compiler,
+// the multiply was fused with the per-lane feature offset into one v_mad_i64_i32 per row
+// (a multi-pass VALU op) in the histogram's per-row loop.  The result is an SGPR base for
+// the saddr form of the byte gather.
+typedef const uint8_t __attribute__((address_space(1)))* gbytes;   // global (not flat) loads
+__device__ __forceinline__ gbytes scalar_row(const uint8_t* base, int32_t row, int32_t F) {
+  const uint64_t b = (uint64_t)base;
+  uint32_t lo, hi;
+  asm("s_mul_i32 %0, %2, %3\n\ts_mul_hi_i32 %1, %2, %3\n\ts_add_u32 %0, %0, %4\n\ts_addc_u32 %1, %1, %5"
+      : "=&s"(lo), "=&s"(hi)
+      : "s"(row), "s"(F), "s"((uint32_t)b), "s"((uint32_t)(b >> 32))
+      : "scc");
+  // (readfirstlane of the SGPR results: marks them uniform for the divergence analysis,
+  // which treats inline-asm outputs as divergent -- else the base goes through VGPRs)
+  lo = __builtin_amdgcn_readfirstlane(lo);
+  hi = __builtin_amdgcn_readfirstlane(hi);
+  return (gbytes)(((uint64_t)hi << 32) | lo);
+}
+
 // FP: features per row-slot (power of 2, <= 64); RS = 64 / FP row-slots per wave.
 // HW: per-row weights present (a compile-time switch: a runtime null test per row
 // became a branch around every weight load and split the counted vmcnt waits).
@@ -48,7 +67,9 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
     const int64_t* __restrict__ item_hi, float* __restrict__ slab, int64_t slab_stride) {
   constexpr int RS = kWave / FP;
   const int SL = CLS ? S : 2;                                     // stats kept in LDS
-  extern __shared__ __attribute__((aligned(16))) float hist[];   // [wave][rs][B][SL][FP] (+pad)
+  // CLS: [wave][rs][B][S][FP] (+pad); REG: [wave][rs][B][FP][2] -- a cell's (w, w*y) pair
+  // is one 8-B LDS word, updated by one ds_read_b64 / v_pk_add_f32 / ds_write_b64
+  extern __shared__ __attribute__((aligned(16))) float hist[];
   __shared__ float y2part[kHistWaves * RS];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
@@ -90,7 +111,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
 #pragma unroll
       for (int q = 0; q < CH; ++q) {
         const int32_t row = __builtin_amdgcn_readlane(ov, q);
-        bo[q] = (bins + (int64_t)row * F)[fc];
+        bo[q] = scalar_row(bins, row, F)[(uint32_t)fc];
       }
       const int32_t j = jb + j0w + (lane & (CH - 1));
       const int32_t jc = j < nl ? j : nl - 1;
@@ -100,19 +121,28 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
     // (Grouping rows so several LDS read-modify-writes share one wait -- duplicates
     // merged first -- measured slower: the extra VALU outweighs the LDS round trips.)
     auto acc_chunk = [&](int32_t jb, const int (&bo)[CH], float yv, float wv) {
+      if constexpr (CLS) {
 #pragma unroll
-      for (int q = 0; q < CH; ++q) {
-        const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), q));
-        const float wr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), q));
-        const float wq = jb + j0w + q < nl ? wr : 0.f;                   // wave-uniform
-        float* cell = my + bo[q] * SL * FP + f;
-        if (CLS) {
-          cell[(int)yq * FP] += wq;
-        } else {
-          const float wy = wq * yq;
-          cell[0] += wq;
-          cell[FP] += wy;
-          wy2 = fmaf(wy, yq, wy2);
+        for (int q = 0; q < CH; ++q) {
+          const float yq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(yv), q));
+          const float wr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wv), q));
+          const float wq = jb + j0w + q < nl ? wr : 0.f;                 // wave-uniform
+          my[bo[q] * SL * FP + f + (int)yq * FP] += wq;
+        }
+      } else {
+        // per-position work once per chunk, vectorised (lane q = position q): validity,
+        // w and w*y, and the node's w*y^2 partial (lanes < CH); a row then costs two
+        // broadcasts, one LDS address and one packed add
+        const int32_t jl = jb + j0w + (lane & (CH - 1));
+        const float wl0 = jl < nl ? wv : 0.f;
+        const float wyl = wl0 * yv;
+        if (lane < CH) wy2 = fmaf(wyl, yv, wy2);
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl0), q));
+          const float wyq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wyl), q));
+          float2_* cell = reinterpret_cast<float2_*>(my + (bo[q] * FP + f) * 2);
+          *cell += float2_{wq, wyq};
         }
       }
     };
@@ -188,13 +218,12 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
       for (int u = 0; u < U; ++u) {
         const bool ok = fok && (jb + jw + u * RS < nl);
         const float wv = ok ? wo[u] : 0.f;
-        float* cell = my + bo[u] * SL * FP + f;
         if (CLS) {
-          cell[(int)yo[u] * FP] += wv;
+          my[bo[u] * SL * FP + f + (int)yo[u] * FP] += wv;
         } else {
           const float wy = wv * yo[u];
-          cell[0] += wv;
-          cell[FP] += wy;
+          float2_* cell = reinterpret_cast<float2_*>(my + (bo[u] * FP + f) * 2);
+          *cell += float2_{wv, wy};
           wy2 = fmaf(wy, yo[u], wy2);
         }
       }
@@ -227,6 +256,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
       }
     }
   }
+  if constexpr (!CLS && RS == 1) wy2 = group_sum<32>(wy2);         // chunk partials of lanes 0..CH-1
   if (!CLS && f == 0) y2part[wid * RS + rs] = wy2;
   __syncthreads();
   // fixed-order block reduction -> slab[item][f][b][s] (features of this group only);
@@ -245,7 +275,8 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
     float acc = 0.f;
     if (CLS || ss < 2) {
       for (int q = 0; q < kHistWaves; ++q)
-        for (int r = 0; r < RS; ++r) acc += hist[q * per_wave + r * region + (bb * SL + ss) * FP + ff];
+        for (int r = 0; r < RS; ++r)
+          acc += hist[q * per_wave + r * region + (CLS ? (bb * SL + ss) * FP + ff : (bb * FP + ff) * 2 + ss)];
     } else if (fg0 + ff == 0 && bb == 0) {
       for (int q = 0; q < kHistWaves * RS; ++q) acc += y2part[q];
     }

@@ -21,3 +21,9 @@ for c in rows sums rows sums; do
     || { echo "bench_kmeans $c failed"; tail -20 gpurun_out/r4j_km_$c.err; exit 1; }
   grep -v amdgpu.ids gpurun_out/r4j_km_$c.json
 done
+# GBT histogram after the round-3 conflict fix and the round-4 load ordering: kernel stats
+# + PMC passes (kernel trace only), then the histogram micro-benchmark
+timeout -k 10 900 bash tools/pmc_gbt_hist.sh || { echo "gbt pmc failed"; tail -5 gpurun_out/pmc_gbt/*.log; exit 1; }
+cat gpurun_out/pmc_gbt/summary.txt
+timeout -k 10 200 python -u tools/bench_hist.py > gpurun_out/r4j_hist.json 2>/dev/null || { echo "bench_hist failed"; exit 1; }
+cat gpurun_out/r4j_hist.json
