@@ -50,17 +50,58 @@ __device__ __forceinline__ float rl(float v, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
 
-template <int R>
-__global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
+// S z = t for one Woodbury row (lane i holds row i of S in srow, t_i in t; n <= NM):
+// right-looking Cholesky S = L L^T where step k needs only broadcasts -- the pivot and L's
+// column k (L_mk, m > k) come from v_readlane, so the factorisation has no LDS round trip
+// (publishing the column through LDS cost ~880 cycles per step: tools/als_wood_phases.py,
+// profiles/als_wood_phases_r4.json); the forward solve L y = t rides along, column k of L
+// goes to LDS (Lc[k][i] = L_ik) for the backward solve L^T z = y.  Steps k >= n are exact
+// no-ops (rows and columns >= n of S are zero and t_i = 0 there: the clamped pivot gives
+// L_kk = 1e-15, every other L entry and y_k are 0), so NM steps run with no branches.
+// Returns z (lane i holds z_i).
+template <int NM>
+__device__ __forceinline__ float wood_factor_solve(float (&srow)[kNW], float v, float (*Lc)[kNW + 1], int lane) {
+#pragma unroll
+  for (int k = 0; k < NM; ++k) {
+    const float piv = fmaxf(rl(srow[k], k), 1e-30f);
+    const float id = __builtin_amdgcn_rsqf(piv);
+    const float lik = lane > k ? srow[k] * id : (lane == k ? piv * id : 0.f);
+    if (lane < kNW) Lc[k][lane] = lik;
+    const float yk = rl(v, k) * id;
+    v = lane == k ? yk : (lane > k ? fmaf(-lik, yk, v) : v);
+#pragma unroll
+    for (int m = k + 1; m < NM; ++m) srow[m] = fmaf(-lik, rl(lik, m), srow[m]);
+  }
+  // backward, right-looking: z_k = v_k / L_kk, then v_i -= L_ki z_k for i < k (row k of L =
+  // entries Lc[i][k]: lane i's column read, conflict-free at stride kNW + 1); the L entries
+  // and the reciprocal diagonal are loaded up front, off the z chain
+#pragma unroll
+  for (int k = NM - 1; k >= 0; --k) {
+    const float lki = Lc[lane & 31][k];
+    const float zk = rl(v, k) * __builtin_amdgcn_rcpf(Lc[k][k]);
+    v = lane == k ? zk : (lane < k ? fmaf(-lki, zk, v) : v);
+  }
+  return v;
+}
+
+// TIM (diagnostic build, o3s_als_wood_timed): lane 0 stamps the shader clock at the phase
+// boundaries of each row -> timing[row][0..4] = gathers landed, S built (MFMA + LDS image),
+// Cholesky, both solves, output (cycles; the gathers are waited for with vmcnt(0) there)
+// WOCC: waves per SIMD the register budget must allow (3: 168 VGPRs, no spill; 4: 128,
+// a 44-byte spill -- o3s_als_wood_occ selects the build)
+template <int R, bool TIM = false, int WOCC = 3>
+__global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ P, const float* __restrict__ eig,
-    const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nlist, float* __restrict__ X) {
+    const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nlist, float* __restrict__ X,
+    int64_t* __restrict__ timing = nullptr) {
+  int64_t tm[6] = {0, 0, 0, 0, 0, 0};
+  if constexpr (TIM) tm[0] = clock64();
   static_assert(R % 32 == 0 && R <= 128, "rank must be a multiple of 32, at most 128");
   constexpr int RV = (R + 63) / 64;              // columns per lane (1 or 2)
   // per wave: the sqrt(D)-scaled rows P' for the MFMA (32 x kPS floats), later reused for
   // the S image and L by columns (Lc[k][i] = L_ik)
   __shared__ __attribute__((aligned(16))) float sP[kWW][kNW * kPS];
-  __shared__ __attribute__((aligned(16))) float sColb[kWW][kNW + 4];   // step k's column, packed
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t li = (int64_t)blockIdx.x * kWW + wv;
@@ -104,6 +145,10 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
     }
   }
 
+  if constexpr (TIM) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tm[1] = clock64();
+  }
   // S = P D P^T = P' P'^T with P' = P sqrt(D), on the matrix cores: each 64-feature half of
   // the rows goes through a 9 KB LDS tile (lane l of the MFMA needs row l & 31), then 32
   // v_mfma_f32_32x32x2_f32 per half accumulate the 32 x 32 product in fp32 (feature
@@ -142,54 +187,22 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
   float srow[kNW];
 #pragma unroll
   for (int m = 0; m < kNW; ++m) srow[m] = S[lane & 31][m];
+  if constexpr (TIM) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    tm[2] = clock64();
+  }
 
-  // Cholesky in registers, right-looking, with a SHIFTING row window: after step k lane i
-  // holds S_{i, k+1+j} in srow[j], so the active column is always srow[0] and every
-  // register index is a constant although k runs in an ordinary loop.  Step k: pivot from
-  // lane k (readlane), column k of L published to LDS twice -- packed at [0, n-k-1) for
-  // the rank-1 update (aligned float4 reads) and at Lc[k][i] for the solves.  About
-  // n^2 / 2 FMAs per lane in all.
+  // Cholesky + both triangular solves in registers (wood_factor_solve): NM = the row length
+  // rounded up to 8, so the fully unrolled steps keep every register index constant and
+  // carry no per-step branches
   float (*Lc)[kNW + 1] = S;                      // Lc[k][i] = L_ik
-  float* colb = sColb[wv];
-  if (lane < kNW + 4) colb[lane] = 0.f;          // never-written slots read as 0, not junk
-  for (int k = 0; k < n; ++k) {
-    const float piv = fmaxf(rl(srow[0], k), 1e-30f);
-    const float id = __builtin_amdgcn_rsqf(piv);
-    const float lik = lane > k ? srow[0] * id : (lane == k ? piv * id : 0.f);
-    if (lane < kNW) Lc[k][lane] = lik;
-    if (lane > k && lane < kNW) colb[lane - k - 1] = lik;
-    // rank-1 update + shift.  Entries right of the diagonal (column > lane) and columns
-    // >= n take garbage-free but unused values (lik = 0 above the diagonal), so there is
-    // no per-entry predicate; blocks past column n are skipped whole (uniform branch).
-    const int live = n - k - 1;
-#pragma unroll
-    for (int j4 = 0; j4 < kNW; j4 += 4) {
-      if (j4 < live) {
-        const float4_ c4 = *reinterpret_cast<const float4_*>(&colb[j4]);
-        const float cj[4] = {c4.x, c4.y, c4.z, c4.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int j = j4 + q;                  // srow[j + 1] = S_{i, k+1+j} before the shift
-          srow[j] = fmaf(-lik, cj[q], j + 1 < kNW ? srow[j + 1] : 0.f);
-        }
-      }
-    }
-  }
-  // S z = W^{-1} c: forward L y = t, backward L^T z = y, both reading L by columns from
-  // LDS (lane i holds entry i)
   float v = t;
-  for (int k = 0; k < n; ++k) {
-    const float lik = Lc[k][lane < kNW ? lane : 0];
-    const float yk = rl(v, k) * __builtin_amdgcn_rcpf(Lc[k][k]);
-    v = lane == k ? yk : (lane > k ? fmaf(-lik, yk, v) : v);
-  }
-  for (int k = n - 1; k >= 0; --k) {
-    // L^T row k = L column k: z_k = (y_k - sum_{i > k} L_ik z_i) / L_kk, right-looking:
-    // v_i -= L_ki z_k for i < k (row k of L = entries Lc[i][k])
-    const float lki = Lc[lane < kNW ? lane : 0][k];
-    const float zk = rl(v, k) * __builtin_amdgcn_rcpf(Lc[k][k]);
-    v = lane == k ? zk : (lane < k ? fmaf(-lki, zk, v) : v);
-  }
+  if (n <= 8) v = wood_factor_solve<8>(srow, t, Lc, lane);
+  else if (n <= 16) v = wood_factor_solve<16>(srow, t, Lc, lane);
+  else if (n <= 24) v = wood_factor_solve<24>(srow, t, Lc, lane);
+  else v = wood_factor_solve<32>(srow, t, Lc, lane);
+  if constexpr (TIM) tm[3] = clock64();
+  if constexpr (TIM) tm[4] = clock64();
   // y = D P^T z: the solution in the eigenbasis (implicit; the host rotates x = Q y for all
   // Woodbury rows) or x itself (explicit, Q = I)
   float2_ uu = {0.f, 0.f};
@@ -204,6 +217,11 @@ __global__ __launch_bounds__(kWW * 64) void als_wood_kernel(
   float* xo = X + u * R;
   if (c0ok) xo[lane] = uu.x;
   if (c1ok) xo[lane + 64] = uu.y;
+  if constexpr (TIM) {
+    tm[5] = clock64();
+    if (lane == 0)
+      for (int k = 0; k < 5; ++k) timing[li * 5 + k] = tm[k + 1] - tm[k];
+  }
 }
 
 template <int R>
@@ -1155,6 +1173,26 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
 // rotated into the eigenbasis of G (F Q, implicit) or F itself (explicit, eig = 0);
 // eig: the eigenvalues of G (zeros when explicit).  X row u receives y_u = D P_u^T z
 // (implicit: the caller applies x = Q y) or x_u (explicit).
+namespace {
+int g_wood_occ = 3;
+}
+O3S_API int o3s_als_wood_occ(int occ) {
+  if (occ != 3 && occ != 4) return -1;
+  g_wood_occ = occ;
+  return 0;
+}
+
+// Diagnostic: als_wood_kernel<128> with per-row phase cycles in timing [nsmall][5].
+O3S_API int o3s_als_wood_timed(const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
+                               const float* P, const float* eig, const float* lam, const int32_t* small,
+                               int64_t nsmall, float* X, int64_t* timing, hipStream_t st) {
+  if (nsmall <= 0 || !eig || !P || !timing) return -1;
+  hipLaunchKernelGGL((als_wood_kernel<128, true>), dim3((unsigned)((nsmall + kWW - 1) / kWW)), dim3(kWW * 64), 0, st,
+                     indptr, cols, w, b, P, eig, lam, small, nsmall, X, timing);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
 O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
                          const float* P, const float* eig, const float* lam, const int32_t* small, int64_t nsmall,
                          float* X, hipStream_t st) {
@@ -1163,8 +1201,12 @@ O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, cons
   const dim3 grid((unsigned)((nsmall + kWW - 1) / kWW));
 #define O3S_WD(RR)                                                                                          \
   if (R == RR) {                                                                                            \
-    hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, eig, lam, \
-                       small, nsmall, X);                                                                   \
+    if (g_wood_occ == 4)                                                                                    \
+      hipLaunchKernelGGL((als_wood_kernel<RR, false, 4>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, \
+                         eig, lam, small, nsmall, X, nullptr);                                              \
+    else                                                                                                    \
+      hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, eig, lam, \
+                         small, nsmall, X, nullptr);                                                        \
     O3S_CHECK_LAUNCH();                                                                                     \
     return 0;                                                                                               \
   }

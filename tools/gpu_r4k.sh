@@ -20,3 +20,6 @@ for o in 2 3 2 3; do
     || { echo "bench_kmeans occ $o failed"; tail -20 gpurun_out/r4k_km_$o.err; exit 1; }
   echo "occ $o $(python3 -c "import json; d=json.loads(open('gpurun_out/r4k_km_$o.json').read().strip().splitlines()[-1]); print(round(d['ms_per_iter'],2), round(d['assign_ms'],2), d['cost'])")"
 done
+timeout -k 10 200 python -u tools/als_wood_phases.py > gpurun_out/r4k_wood_phases.json 2> gpurun_out/r4k_wood.err \
+  || { echo "wood phases failed"; tail -20 gpurun_out/r4k_wood.err; exit 1; }
+grep -v amdgpu.ids gpurun_out/r4k_wood_phases.json
