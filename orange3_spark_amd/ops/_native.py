@@ -102,7 +102,9 @@ class NativeError(O3SError):
 
 
 def lib_path() -> Path:
-    return _build.KERNEL_LIB
+    # O3S_KERNEL_LIB: an alternative build of the library (A/B timing tools only)
+    alt = os.environ.get("O3S_KERNEL_LIB")
+    return Path(alt) if alt else _build.KERNEL_LIB
 
 
 def _load():

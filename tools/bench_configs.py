@@ -35,6 +35,16 @@ def _mem_gb():
     return round(torch.cuda.max_memory_allocated() / 2**30, 1) if torch.cuda.is_available() else None
 
 
+def _alloc_stats():
+    """Caching-allocator events of the run: retries (an allocation that first failed and
+    flushed the cache) and device mallocs / frees (each a synchronising hipMalloc/hipFree)."""
+    if not torch.cuda.is_available():
+        return None
+    st = torch.cuda.memory_stats()
+    return {"num_alloc_retries": st.get("num_alloc_retries"), "num_device_alloc": st.get("num_device_alloc"),
+            "num_device_free": st.get("num_device_free"), "reserved_gb": round(torch.cuda.memory_reserved() / 2**30, 1)}
+
+
 def run_als(s, a):
     from orange3_spark_amd.ml.recommendation import ALS
     from orange3_spark_amd.runtime.tracing import TRACER
@@ -76,14 +86,21 @@ def run_gbt(s, a):
     t_gen = time.perf_counter() - t0
     print(f"[bench_configs] rows generated in {t_gen:.1f}s", file=sys.stderr, flush=True)
     est = GBTClassifier(maxDepth=a.depth, maxIter=a.trees, stepSize=0.1, seed=0)
-    TRACER.reset()
-    s.comm.barrier()
-    _sync()
-    t1 = time.perf_counter()
-    model = est.fit(df)
-    _sync()
-    s.comm.barrier()
-    fit_s = time.perf_counter() - t1
+    # the fit is timed --repeat times in this process: the first (cold) fit's fresh device
+    # allocations (the 32 GB feature-major copy) are cleared by the driver before first use
+    # (~1.6 s on a box whose memory a previous process used); later fits reuse the caching
+    # allocator's blocks, as in a long-running session.  value = the last (warm) fit.
+    fits = []
+    for _ in range(max(1, a.repeat)):
+        TRACER.reset()
+        s.comm.barrier()
+        _sync()
+        t1 = time.perf_counter()
+        model = est.fit(df)
+        _sync()
+        s.comm.barrier()
+        fits.append(time.perf_counter() - t1)
+    fit_s = fits[-1]
     ph = {k: round(v["total_s"], 4) for k, v in TRACER.summary().items()} if TRACER.enabled else None
     prep = None
     if ph:
@@ -93,10 +110,11 @@ def run_gbt(s, a):
            "dtype": "fp32", "data": "synthetic", "mode": "resident",
            "config": {"model": f"GBTClassifier maxDepth={a.depth} maxBins=32", "rows": a.rows,
                       "features": a.features, "maxIter": a.trees, "parallelism": f"dp{s.comm.world_size}"},
-           "fit_seconds": round(fit_s, 3), "binning_seconds": prep,
+           "fit_seconds": round(fit_s, 3), "fit_seconds_each": [round(x, 3) for x in fits], "binning_seconds": prep,
            "per_tree_excl_binning_s": (round((fit_s - prep) / a.trees, 4) if prep is not None else None),
            "train_loss": [round(x, 5) for x in model.trainingLossHistory][-3:],
-           "datagen_seconds_untimed": round(t_gen, 2), "max_mem_gb": _mem_gb(), "phases_s": ph}
+           "datagen_seconds_untimed": round(t_gen, 2), "max_mem_gb": _mem_gb(), "alloc": _alloc_stats(),
+           "phases_s": ph}
     return out
 
 
@@ -112,6 +130,7 @@ def main(argv=None):
     ap.add_argument("--features", type=int, default=64)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--trees", type=int, default=5)
+    ap.add_argument("--repeat", type=int, default=2, help="GBT: fits timed in one process (value = the last)")
     ap.add_argument("--trace", action="store_true", help="per-phase timings (synchronising tracer)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
