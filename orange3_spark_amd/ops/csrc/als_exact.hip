@@ -609,7 +609,7 @@ struct DenseM {
   static constexpr int LDSG = SA + XR + R + 2 * CH + W * 32 + 3 * IC + 2 * DEP * CH;
 };
 
-template <int R, bool IMPL, bool BLK, bool TIM = false, bool GL = false, bool RLD = false>
+template <int R, bool IMPL, bool BLK, bool TIM = false, bool GL = false>
 __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
@@ -998,15 +998,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
 #pragma unroll
             for (int j = c + 1; j < c0 + 4; ++j) v[j] = fmaf(-t, rl(t, j), v[j]);
           }
-          if (RLD && c0 + 4 < 32) {
-            // (RLD) the block's multipliers L[j][c0..c0+3] straight from lane j by v_readlane:
-            // no LDS write / read-back round trip per column block
-#pragma unroll
-            for (int j = c0 + 4; j < 32; ++j) {
-              const float l0 = rl(v[c0], j), l1 = rl(v[c0 + 1], j), l2 = rl(v[c0 + 2], j), l3 = rl(v[c0 + 3], j);
-              v[j] = fmaf(-v[c0 + 3], l3, fmaf(-v[c0 + 2], l2, fmaf(-v[c0 + 1], l1, fmaf(-v[c0], l0, v[j]))));
-            }
-          } else if (c0 + 4 < 32) {
+          if (c0 + 4 < 32) {
             // every lane stores (an exec-masked store makes the compiler keep all 28 rows'
             // broadcasts live across the block: 234 instead of 64 VGPRs); lanes 32-63 hold
             // x values and park them in slots 32-63, which are never read
@@ -1262,7 +1254,7 @@ O3S_API int o3s_als_dense(int implicit, int R, const int64_t* indptr, const int3
 }
 
 namespace {
-template <bool BLK, bool GL = false, bool RLD = false>
+template <bool BLK, bool GL = false>
 int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
                       const float* b, const float* F, const float* G, const float* lam, const int32_t* dense,
                       int64_t ndense, float* X, hipStream_t st) {
@@ -1271,10 +1263,10 @@ int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t*
 #define O3S_DM(RR)                                                                                              \
   if (R == RR) {                                                                                                \
     if (implicit)                                                                                               \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK, false, GL, RLD>), dim3((unsigned)ndense),        \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK, false, GL>), dim3((unsigned)ndense),             \
                          dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X, nullptr);       \
     else                                                                                                        \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK, false, GL, RLD>), dim3((unsigned)ndense),       \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK, false, GL>), dim3((unsigned)ndense),            \
                          dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X, nullptr);       \
     O3S_CHECK_LAUNCH();                                                                                         \
     return 0;                                                                                                   \
@@ -1303,13 +1295,6 @@ O3S_API int o3s_als_dense_mfma_gl(int implicit, int R, const int64_t* indptr, co
                                   const float* b, const float* F, const float* G, const float* lam,
                                   const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
   return launch_dense_mfma<true, true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
-}
-
-// _gl with the diagonal factor's rank-4 multipliers broadcast by v_readlane (no LDS)
-O3S_API int o3s_als_dense_mfma_glr(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
-                                   const float* b, const float* F, const float* G, const float* lam,
-                                   const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
-  return launch_dense_mfma<true, true, true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
 }
 
 // Diagnostic: the dense kernel (BLK, implicit, R = 128; gl != 0: with the LDS-DMA gather

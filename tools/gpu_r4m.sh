@@ -23,13 +23,3 @@ timeout -k 10 300 python -u tools/bench_kmeans.py > gpurun_out/r4m_km.json 2> gp
 grep -v amdgpu.ids gpurun_out/r4m_km.json
 timeout -k 10 400 python -u tools/bench_kmeans_fit.py --iters 10 > gpurun_out/r4m_km_fit.json 2> gpurun_out/r4m_km_fit.err || { echo "kmeans fit failed"; tail -20 gpurun_out/r4m_km_fit.err; exit 1; }
 grep -v amdgpu.ids gpurun_out/r4m_km_fit.json
-# dense ALS kernel: diagonal factor multipliers by v_readlane (mfma_glr) vs LDS broadcast (mfma_gl)
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_als.py -k "dense_kernels" \
-  > gpurun_out/r4m_glr_tests.log 2>&1 || { echo "glr tests failed"; tail -30 gpurun_out/r4m_glr_tests.log; exit 1; }
-tail -1 gpurun_out/r4m_glr_tests.log
-for v in mfma_gl mfma_glr mfma_gl mfma_glr; do
-  O3S_ALS_DENSE=$v timeout -k 10 200 python -u tools/bench_als.py --rank-of 8 --users 50000000 --items 5000000 \
-    --ratings 1000000000 --iters 2 > gpurun_out/r4m_als_$v.json 2> gpurun_out/r4m_als_$v.err \
-    || { echo "bench_als $v failed"; tail -20 gpurun_out/r4m_als_$v.err; exit 1; }
-  echo "$v $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/r4m_als_$v.json').read().strip().splitlines()[-1]); print(d['value'])")"
-done
