@@ -322,32 +322,30 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
 constexpr int kScrWaves = 4;
 constexpr int kScrThreads = kScrWaves * kWave;
 
-// LEAN (pre-split rows only: no fp32 X staging area): 2 chunks per stage, so a block
-// needs ~36 KB of LDS and 3 blocks fit a CU (with the 168-VGPR budget of OCC = 3).
-template <int KS, bool LEAN = false>
+template <int KS>
 struct ScrLds {
   static constexpr int D = KS * 16;
-  static constexpr int G = LEAN || D > 128 ? 2 : 4;             // centroid chunks per stage
+  static constexpr int G = D <= 128 ? 4 : 2;                    // centroid chunks per stage
   static constexpr int CHUNK_BYTES = 2 * 32 * D;                // hi only
   static constexpr int STAGE_BYTES = 2 * G * CHUNK_BYTES;       // double buffered
-  static constexpr int X_BYTES = LEAN ? 0 : kScrWaves * 32 * D * 4;   // one 32-row tile per wave
+  static constexpr int X_BYTES = kScrWaves * 32 * D * 4;        // one 32-row tile per wave
   static constexpr int BYTES = STAGE_BYTES > X_BYTES ? STAGE_BYTES : X_BYTES;
 };
-int g_screen_occ = 2;      // o3s_kmeans_screen_occ: 3 = the LEAN, 3-blocks-per-CU build (NOD + PS)
 
 // NOD (plain screen, mind == nullptr: the Lloyd iterations, whose cost comes from the
 // cluster sums -- models/kmeans.py): no per-row distance, so neither the lo half of x (the
 // pre-split rows' second 16 B: half the prologue's HBM bytes) nor the chosen centre's fp32
 // row (an L2 gather of D floats per row) is read.
-template <int KS, int TT, bool PAIR, bool PS = false, bool NOD = false, int OCC = 2>
-__global__ __launch_bounds__(kScrThreads, OCC) void kmeans_screen_kernel(
+// (a lean build -- 2-chunk stages, 3 blocks per CU at 168 VGPRs -- measured slower: 44.4 vs
+// 39.2 ms per iteration, profiles/kernel_experiments_r4.json)
+template <int KS, int TT, bool PAIR, bool PS = false, bool NOD = false>
+__global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const float* __restrict__ X, int64_t n, int64_t ldx, const uint16_t* __restrict__ Chi,
     const float* __restrict__ cn, const float* __restrict__ C32, int ldc, int Cpad, float eps_x, float eps0,
     float xscale, float sscale, int32_t* __restrict__ assign, float* __restrict__ mind,
     int32_t* __restrict__ flag_cnt, int32_t* __restrict__ flag_rows, int Dx,
     const uint4* __restrict__ XP = nullptr, const float* __restrict__ XN = nullptr) {
-  static_assert(OCC == 2 || (PS && NOD), "the lean build has no fp32 X staging");
-  using L = ScrLds<KS, (OCC > 2)>;
+  using L = ScrLds<KS>;
   constexpr int D = L::D;
   constexpr int G = L::G;
   constexpr int SLOTS = D / 8;
@@ -1096,13 +1094,6 @@ O3S_API int o3s_kmeans_presplit(const float* X, int64_t n, int64_t ldx, int Dx, 
   return 0;
 }
 
-// Screen-kernel build for the no-distance pre-split pass: 2 (default) or 3 blocks per CU.
-O3S_API int o3s_kmeans_screen_occ(int occ) {
-  if (occ != 2 && occ != 3) return -1;
-  g_screen_occ = occ;
-  return 0;
-}
-
 O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
                               const float* C32, int ldc, int Cpad, float eps_x, float eps0, float xscale,
                               float sscale, int32_t* assign, float* mind, int32_t* flag_cnt, int32_t* flag_rows,
@@ -1123,11 +1114,7 @@ O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, co
     const int64_t grid = (n + rows_per_block - 1) / rows_per_block;                                        \
     const size_t dyn = ScrLds<KS>::BYTES + cdyn;                                                           \
     if (dyn > 160 * 1024) return -3;                                                                       \
-    if (XP && !P && !mind && g_screen_occ == 3) {                                                          \
-      hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, true, true, 3>), dim3((unsigned)grid), dim3(kScrThreads), \
-                         (ScrLds<KS, true>::BYTES + cdyn), st, X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0,   \
-                         xscale, sscale, assign, mind, flag_cnt, flag_rows, Dx, (const uint4*)XP, XN);      \
-    } else if (XP && !P && !mind)                                                                          \
+    if (XP && !P && !mind)                                                                          \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, true, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, \
                          st, X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind,     \
                          flag_cnt, flag_rows, Dx, (const uint4*)XP, XN);                                   \

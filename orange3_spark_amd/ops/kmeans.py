@@ -7,7 +7,6 @@ from __future__ import annotations
 
 import ctypes as Ct
 import math
-import os
 
 import torch
 
@@ -164,8 +163,7 @@ PAIR_FROM: float | None = None
 SCREEN_MAX_FLAG_FRACTION = 0.5
 SPLIT_REPROBE = 6             # split calls before the pair screen is tried again
 SCREEN_TT = 0                 # 32-row tiles per wave in the screen kernel (0: by D)
-# blocks per CU of the no-distance pre-split screen build (2, or 3: 2-chunk stages, 168 VGPRs)
-SCREEN_OCC = int(os.environ.get("O3S_KM_SCREEN_OCC", "2"))
+
 _screen_state: dict = {}      # (id(X), shape, Cpad) -> (weakref to X, mode, flagged fraction, countdown)
 
 
@@ -250,7 +248,6 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
         xs = x_scale(X)
         eps_x, eps0 = screen_bound(P, xs, X.shape[1])
         ps = presplit(X, xs) if mode == "screen" else None
-        lib.o3s_kmeans_screen_occ(SCREEN_OCC)
         N.check(lib.o3s_kmeans_screen(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
                                       P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
                                       Ct.c_float(eps0), Ct.c_float(xs), Ct.c_float(xs * P.ms), a.data_ptr(),
