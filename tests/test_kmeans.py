@@ -283,3 +283,22 @@ def test_gpu_presplit_screen_matches_plain_screen(gpu, D, monkeypatch):
     X.mul_(2.0)                                          # new data version: the cache must rebuild
     a2, _ = K.assign(X, C * 2.0, K.prepare_centers(C * 2.0), mode="screen")
     assert torch.equal(a2, a0)
+
+
+def test_lloyd_cost_from_cluster_sums_equals_direct_cost():
+    """The Lloyd iterations take their cost from the cluster sums (sum ||x||^2 - sum_a
+    (2 c_a.S_a - n_a ||c_a||^2), fp64) so the assign pass needs no per-row distance; the
+    history entry of iteration 1 equals the direct sum of squared distances to the initial
+    centres, and a weighted fit keeps the per-row form."""
+    from orange3_spark_amd.models.kmeans import fit_kmeans
+    from orange3_spark_amd.parallel.comm import LocalComm
+    g = torch.Generator().manual_seed(4)
+    X = torch.randn(3000, 6, generator=g, dtype=torch.float32) * 3 + 1
+    C0 = X[:5].double().clone()
+    res = fit_kmeans(LocalComm("cpu"), X, 5, max_iter=1, tol=0.0, initial=C0)
+    d = torch.cdist(X.double(), C0).pow(2).min(1).values.sum()
+    assert abs(res.history[0] - float(d)) <= 1e-9 * float(d)
+    w = torch.rand(3000, generator=g, dtype=torch.float32)
+    resw = fit_kmeans(LocalComm("cpu"), X, 5, max_iter=1, tol=0.0, initial=C0, weights=w)
+    dw = (torch.cdist(X.double(), C0).pow(2).min(1).values * w.double()).sum()
+    assert abs(resw.history[0] - float(dw)) <= 1e-6 * float(dw)
