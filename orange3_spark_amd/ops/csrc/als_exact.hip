@@ -634,12 +634,9 @@ struct DenseM {
   // LDS-DMA (no VGPRs hold in-flight gathers); the ring shares its region with the diagonal
   // staging / X_p images, which are only used after the Gram.  IC = rating indices staged
   // per chunk (one refill per IC ratings).
-  // The GL staging rows are unpadded (LDT = 16, halves XOR-swizzled by row bit 3), which
-  // frees the LDS for a 4-step ring at 3 blocks per CU.
-  static constexpr int DEP = 4, IC = 128;
-  static constexpr int SAG = SA1 > R * 32 ? SA1 : R * 32;
+  static constexpr int DEP = 3, IC = 128;
   static constexpr int XR = TS + NT * TS > DEP * CH * R ? TS + NT * TS : DEP * CH * R;
-  static constexpr int LDSG = SAG + XR + R + 2 * CH + W * 32 + 3 * IC + 2 * DEP * CH;
+  static constexpr int LDSG = SA + XR + R + 2 * CH + W * 32 + 3 * IC + 2 * DEP * CH;
 };
 
 template <int R, bool IMPL, bool BLK, bool TIM = false, bool GL = false>
@@ -662,9 +659,9 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
   float* const sY = lds;                 // Gram: staged factor rows [CH][R]
   float* const sPn = lds;                // factor: row panel [32][PNS]
   float* const sScr = lds;               // backward: per-wave transpose [W][32][33]
-  float* const sD = lds + (GLP ? D::SAG : D::SA);   // diagonal tile staging [32][33]
+  float* const sD = lds + D::SA;         // diagonal tile staging [32][33]
   float* const sX = sD + TS;             // X_p = L_pp^-1, every p: [NT][32][33]
-  float* const sr = GLP ? lds + D::SAG + D::XR : sX + NT * TS;   // rhs -> y -> x
+  float* const sr = GLP ? lds + D::SA + D::XR : sX + NT * TS;   // rhs -> y -> x
   float* const sW = sr + R;
   float* const sB = sW + CH;
   float* const sWp = sB + CH;            // backward partial sums [W][32]
@@ -708,9 +705,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
     // and writes each item as ONE dword (ratings 2kp, 2kp + 1 of dim r) at dword 12 r + kp:
     // banks 12 r_low + kp_low (+ 0 mod 64) are all different across the wave.  Its global
     // loads are 64-B runs of one factor row per 16 lanes.
-    // LDT: u16 per staged dim row (16 ratings + 8 pad; GL: 16, the two 16-B halves swapped
-    // on rows with bit 3 set -- conflict-free fragment reads and transposed stores)
-    constexpr int LDT = GLP ? 16 : 24, NRB = R / 16, ITEMS = NRB / 2;   // 2 NRB items over 4 waves
+    constexpr int LDT = 24, NRB = R / 16, ITEMS = NRB / 2;   // 2 NRB items over 4 waves
     uint16_t* const sT = reinterpret_cast<uint16_t*>(lds);    // [buf][hi|lo][R][LDT]
     const int r_low = lane & 15, kp_low = lane >> 4;
     float y0[ITEMS], y1[ITEMS], rh[ITEMS];
@@ -777,7 +772,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
     };
     const int nsteps = (int)((p1 - p0 + CH - 1) / CH);
     auto gram_step = [&](int buf) {
-      const uint16_t* th = sT + buf * 2 * R * LDT + q * LDT + 8 * (GLP ? (h ^ ((q >> 3) & 1)) : h);
+      const uint16_t* th = sT + buf * 2 * R * LDT + q * LDT + 8 * h;
       const uint16_t* tl = th + R * LDT;
 #pragma unroll
       for (int s = 0; s < MT; ++s) {
@@ -803,7 +798,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
       // ring with vmcnt(0) there); only the chunk refill, once per IC ratings, drains it.
       // Barriers are raw s_barrier + lgkmcnt(0): __syncthreads()' fence would wait vmcnt(0).
       constexpr int DEP = D::DEP, IC = D::IC;
-      float* const ring = lds + D::SAG;                                 // [DEP][CH][R]
+      float* const ring = lds + D::SA;                                  // [DEP][CH][R]
       int32_t* const sCi = reinterpret_cast<int32_t*>(sWp + W * 32);    // index chunk [IC]
       float* const sWc = reinterpret_cast<float*>(sCi + IC);            // w of the chunk
       float* const sBc = sWc + IC;                                      // b of the chunk
@@ -853,7 +848,7 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
           const float z0 = s0 * u0, z1 = s1 * u1;
           const uint16_t h0 = f32_to_bf16(z0), h1 = f32_to_bf16(z1);
           const uint16_t l0 = f32_to_bf16(z0 - bf16_to_f32(h0)), l1 = f32_to_bf16(z1 - bf16_to_f32(h1));
-          const int dw = r * (LDT / 2) + 4 * (kb ^ ((r >> 3) & 1)) + kp_low;
+          const int dw = r * (LDT / 2) + 4 * kb + kp_low;
           th[dw] = (uint32_t)h0 | ((uint32_t)h1 << 16);
           tl[dw] = (uint32_t)l0 | ((uint32_t)l1 << 16);
         }
@@ -862,32 +857,28 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
         const int slot = s % DEP;
         convert(ring + slot * CH * R, sWs + slot * CH, sBs + slot * CH, sT + (s & 1) * 2 * R * LDT);
       };
-      // wait until at most `steps` whole steps (2 DMA instructions each) are still in flight
-      auto wait_steps = [&](int steps) {
-        static_assert(DEP <= 4, "vmcnt immediates below cover up to 3 steps in flight");
-        if (steps >= 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else if (steps == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else if (steps == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      };
       if (nsteps > 0) {
-        const int pre = nsteps < DEP ? nsteps : DEP;                    // steps 0 .. pre-1 in flight
-#pragma unroll
-        for (int k = 0; k < DEP; ++k)
-          if (k < pre) issue(k);
-        wait_steps(pre - 1);
+        issue(0);
+        if (nsteps > 1) issue(1);
+        if (nsteps > 2) issue(2);
+        if (nsteps > 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else if (nsteps > 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();                                                          // step 0 landed
         conv(0);
-        wait_steps(pre - 2);
+        if (nsteps > 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         bar();                                                          // step 1 landed, sT[0] ready
       }
       for (int st = 0; st < nsteps; ++st) {
         gram_step(st & 1);
         if (st + 1 < nsteps) conv(st + 1);
-        if (st + DEP < nsteps) issue(st + DEP);                         // into the slot step st vacated
-        // step st + 2 landed: the steps issued after it may stay in flight
-        const int last = st + DEP < nsteps ? st + DEP : nsteps - 1;
-        wait_steps(last - (st + 2));
+        if (st + DEP < nsteps) {
+          issue(st + DEP);                 // into the slot step st vacated
+          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");             // step st + 2 landed
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         bar();
       }
     } else {
