@@ -89,7 +89,9 @@ __device__ __forceinline__ float wood_factor_solve(float (&srow)[kNW], float v, 
 // Cholesky, both solves, output (cycles; the gathers are waited for with vmcnt(0) there)
 // WOCC: waves per SIMD the register budget must allow (3: 168 VGPRs, no spill; 4: 128,
 // a 44-byte spill -- o3s_als_wood_occ selects the build)
-template <int R, bool TIM = false, int WOCC = 3>
+// S3: S = P' P'^T as bf16x3 on v_mfma_f32_32x32x16_bf16 (hi.hi + lo.hi + hi.lo, ~2^-16
+// relative, the dense Gram's numerics) instead of exact fp32 products on 32x32x2
+template <int R, bool TIM = false, int WOCC = 3, bool S3 = false>
 __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ P, const float* __restrict__ eig,
@@ -168,6 +170,30 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   for (int hf = 0; hf < RV; ++hf) {
 #pragma unroll
     for (int i = 0; i < kNW; ++i) sp[i * kPS + wcol] = hf == 0 ? acc[i].x * sq.x : acc[i].y * sq.y;
+    if constexpr (S3) {
+      // k-step m: lane l holds features 16 m + 8 (l >> 5) .. + 8 of row l & 31 -- the same
+      // register serves as the A (rows) and the B (columns) operand of S = P' P'^T
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const float* src = sp + (lane & 31) * kPS + 36 * (m >> 1) + 16 * (m & 1) + 8 * (lane >> 5);
+        const float4_ u0 = *reinterpret_cast<const float4_*>(src);
+        const float4_ u1 = *reinterpret_cast<const float4_*>(src + 4);
+        const float uv[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+        uint32_t ph[4], pl[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint16_t h0 = f32_to_bf16(uv[2 * j]), h1 = f32_to_bf16(uv[2 * j + 1]);
+          const uint16_t l0 = f32_to_bf16(uv[2 * j] - bf16_to_f32(h0));
+          const uint16_t l1 = f32_to_bf16(uv[2 * j + 1] - bf16_to_f32(h1));
+          ph[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+          pl[j] = (uint32_t)l0 | ((uint32_t)l1 << 16);
+        }
+        const bf16x8_ hi = __builtin_bit_cast(bf16x8_, ph), lo = __builtin_bit_cast(bf16x8_, pl);
+        sa0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi, hi, sa0, 0, 0, 0);
+        sa1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lo, hi, sa1, 0, 0, 0);
+        sa1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi, lo, sa1, 0, 0, 0);
+      }
+    } else {
 #pragma unroll
     for (int s4 = 0; s4 < 32; s4 += 4) {
       const float4_ v = *reinterpret_cast<const float4_*>(rp + s4);
@@ -175,6 +201,7 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
       sa1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, v.y, sa1, 0, 0, 0);
       sa0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, v.z, sa0, 0, 0, 0);
       sa1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, v.w, sa1, 0, 0, 0);
+    }
     }
   }
   const f32x16_ sacc = sa0 + sa1;
@@ -1204,11 +1231,11 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
 // eig: the eigenvalues of G (zeros when explicit).  X row u receives y_u = D P_u^T z
 // (implicit: the caller applies x = Q y) or x_u (explicit).
 namespace {
-int g_wood_occ = 3;
+int g_wood_s3 = 0;
 }
-O3S_API int o3s_als_wood_occ(int occ) {
-  if (occ != 3 && occ != 4) return -1;
-  g_wood_occ = occ;
+// Woodbury S build: 0 = exact fp32 products (default), 1 = bf16x3 (see S3)
+O3S_API int o3s_als_wood_s3(int on) {
+  g_wood_s3 = on ? 1 : 0;
   return 0;
 }
 
@@ -1231,9 +1258,9 @@ O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, cons
   const dim3 grid((unsigned)((nsmall + kWW - 1) / kWW));
 #define O3S_WD(RR)                                                                                          \
   if (R == RR) {                                                                                            \
-    if (g_wood_occ == 4)                                                                                    \
-      hipLaunchKernelGGL((als_wood_kernel<RR, false, 4>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, \
-                         eig, lam, small, nsmall, X, nullptr);                                              \
+    if (g_wood_s3)                                                                                          \
+      hipLaunchKernelGGL((als_wood_kernel<RR, false, 3, true>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, \
+                         P, eig, lam, small, nsmall, X, nullptr);                                           \
     else                                                                                                    \
       hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, eig, lam, \
                          small, nsmall, X, nullptr);                                                        \

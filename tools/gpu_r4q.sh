@@ -1,0 +1,21 @@
+#!/bin/bash
+# Woodbury S build bf16x3 (opt-in) vs exact fp32: tests, kernel time, rank-of-8 iteration;
+# then the KMeans screen PMC (no-distance vs per-row-distance builds).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+O3S_ALS_WOOD_S3=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_als.py \
+  > gpurun_out/r4q_tests_s3.log 2>&1 || { echo "s3 tests failed"; grep -E "assert|Error" gpurun_out/r4q_tests_s3.log | head -10; tail -5 gpurun_out/r4q_tests_s3.log; }
+tail -1 gpurun_out/r4q_tests_s3.log
+for s3 in 0 1 0 1; do
+  timeout -k 10 200 python -u tools/als_wood_phases.py --s3 $s3 > gpurun_out/r4q_wood_$s3.json 2>/dev/null || { echo "wood $s3 failed"; exit 1; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/r4q_wood_$s3.json').read().strip().splitlines()[-1]); print('s3', $s3, round(d['production_ms'],3))"
+done
+for s3 in 0 1; do
+  O3S_ALS_WOOD_S3=$s3 timeout -k 10 200 python -u tools/bench_als.py --rank-of 8 --users 50000000 --items 5000000 \
+    --ratings 1000000000 --iters 2 > gpurun_out/r4q_als_$s3.json 2> gpurun_out/r4q_als_$s3.err \
+    || { echo "bench_als $s3 failed"; tail -20 gpurun_out/r4q_als_$s3.err; exit 1; }
+  echo "als s3=$s3 $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/r4q_als_$s3.json').read().strip().splitlines()[-1]); print(d['value'])")"
+done
+timeout -k 10 900 bash tools/gpu_r4p.sh
