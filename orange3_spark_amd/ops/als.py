@@ -250,7 +250,8 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
     if nd:
         Gf = G.float().contiguous() if implicit else None
         fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
-              "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(DENSE_KERNEL, lib.o3s_als_dense)
+              "mfma_gl": lib.o3s_als_dense_mfma_gl, "mfma_gd": lib.o3s_als_dense_mfma_gd}.get(
+            DENSE_KERNEL, lib.o3s_als_dense)
         N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                    F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), nd, out.data_ptr(), st),
                 "als_dense")

@@ -666,7 +666,19 @@ struct DenseM {
   static constexpr int LDSG = SA + XR + R + 2 * CH + W * 32 + 3 * IC + 2 * DEP * CH;
 };
 
-template <int R, bool IMPL, bool BLK, bool TIM = false, bool GL = false>
+// upper-triangle tile t of a 4 x 4 tile grid (order (0,0), (0,1), .., (1,1), ..) -> (j, i)
+__host__ __device__ constexpr int ut_j(int t) {
+  int j = 0;
+  while (t >= 4 - j) { t -= 4 - j; ++j; }
+  return j;
+}
+__host__ __device__ constexpr int ut_i(int t) {
+  int j = 0;
+  while (t >= 4 - j) { t -= 4 - j; ++j; }
+  return j + t;
+}
+
+template <int R, bool IMPL, bool BLK, bool TIM = false, bool GL = false, bool GD = false>
 __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
@@ -801,6 +813,38 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
     auto gram_step = [&](int buf) {
       const uint16_t* th = sT + buf * 2 * R * LDT + q * LDT + 8 * h;
       const uint16_t* tl = th + R * LDT;
+      if constexpr (GLP && NT == 4 && W == 4 && GD) {
+        // every row block's hi / lo fragments read once (the A and B operands of a tile are
+        // the same staged rows, and a wave's tiles share blocks), then the wave's tiles
+        // (t = wid + 4 s, compile-time per wave) issued term-major: 2-3 independent MFMA
+        // chains instead of three dependent MFMAs per tile behind each tile's LDS reads
+        bf16x8_ fh[4], fl[4];
+#pragma unroll
+        for (int b2 = 0; b2 < 4; ++b2) {
+          fh[b2] = *reinterpret_cast<const bf16x8_*>(th + 32 * b2 * LDT);
+          fl[b2] = *reinterpret_cast<const bf16x8_*>(tl + 32 * b2 * LDT);
+        }
+        auto tiles = [&](auto wtag) {
+          constexpr int WV = decltype(wtag)::value;
+          constexpr int NS = WV + 8 < 10 ? 3 : 2;
+          constexpr int J[3] = {ut_j(WV), ut_j(WV + 4), ut_j(WV + 8 < 10 ? WV + 8 : 0)};
+          constexpr int I[3] = {ut_i(WV), ut_i(WV + 4), ut_i(WV + 8 < 10 ? WV + 8 : 0)};
+#pragma unroll
+          for (int s2 = 0; s2 < NS; ++s2)
+            acc[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh[J[s2]], fh[I[s2]], acc[s2], 0, 0, 0);
+#pragma unroll
+          for (int s2 = 0; s2 < NS; ++s2)
+            acc[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl[J[s2]], fh[I[s2]], acc[s2], 0, 0, 0);
+#pragma unroll
+          for (int s2 = 0; s2 < NS; ++s2)
+            acc[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh[J[s2]], fl[I[s2]], acc[s2], 0, 0, 0);
+        };
+        if (wid == 0) tiles(std::integral_constant<int, 0>{});
+        else if (wid == 1) tiles(std::integral_constant<int, 1>{});
+        else if (wid == 2) tiles(std::integral_constant<int, 2>{});
+        else tiles(std::integral_constant<int, 3>{});
+        return;
+      }
 #pragma unroll
       for (int s = 0; s < MT; ++s) {
         if (tj[s] >= NT) continue;
@@ -1311,7 +1355,7 @@ O3S_API int o3s_als_dense(int implicit, int R, const int64_t* indptr, const int3
 }
 
 namespace {
-template <bool BLK, bool GL = false>
+template <bool BLK, bool GL = false, bool GD = false>
 int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
                       const float* b, const float* F, const float* G, const float* lam, const int32_t* dense,
                       int64_t ndense, float* X, hipStream_t st) {
@@ -1320,10 +1364,10 @@ int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t*
 #define O3S_DM(RR)                                                                                              \
   if (R == RR) {                                                                                                \
     if (implicit)                                                                                               \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK, false, GL>), dim3((unsigned)ndense),             \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK, false, GL, GD>), dim3((unsigned)ndense),         \
                          dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X, nullptr);       \
     else                                                                                                        \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK, false, GL>), dim3((unsigned)ndense),            \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK, false, GL, GD>), dim3((unsigned)ndense),        \
                          dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X, nullptr);       \
     O3S_CHECK_LAUNCH();                                                                                         \
     return 0;                                                                                                   \
@@ -1352,6 +1396,13 @@ O3S_API int o3s_als_dense_mfma_gl(int implicit, int R, const int64_t* indptr, co
                                   const float* b, const float* F, const float* G, const float* lam,
                                   const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
   return launch_dense_mfma<true, true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
+}
+
+// _gl with the Gram's fragments read once per row block and the tiles' MFMAs interleaved
+O3S_API int o3s_als_dense_mfma_gd(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
+                                  const float* b, const float* F, const float* G, const float* lam,
+                                  const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
+  return launch_dense_mfma<true, true, true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
 }
 
 // Diagnostic: the dense kernel (BLK, implicit, R = 128; gl != 0: with the LDS-DMA gather

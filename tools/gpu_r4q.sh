@@ -18,4 +18,15 @@ for s3 in 0 1; do
     || { echo "bench_als $s3 failed"; tail -20 gpurun_out/r4q_als_$s3.err; exit 1; }
   echo "als s3=$s3 $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/r4q_als_$s3.json').read().strip().splitlines()[-1]); print(d['value'])")"
 done
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_als.py -k dense_kernels \
+  > gpurun_out/r4q_gd_tests.log 2>&1 || { echo "gd tests failed"; tail -30 gpurun_out/r4q_gd_tests.log; exit 1; }
+tail -1 gpurun_out/r4q_gd_tests.log
+timeout -k 10 200 python -u tools/als_dense_phases.py --gl 1 > gpurun_out/r4q_phases.json 2>/dev/null || { echo "phases failed"; exit 1; }
+grep -v amdgpu.ids gpurun_out/r4q_phases.json
+for v in mfma_gl mfma_gd mfma_gl mfma_gd; do
+  O3S_ALS_DENSE=$v timeout -k 10 200 python -u tools/bench_als.py --rank-of 8 --users 50000000 --items 5000000 \
+    --ratings 1000000000 --iters 2 > gpurun_out/r4q_als_$v.json 2> gpurun_out/r4q_als_$v.err \
+    || { echo "bench_als $v failed"; tail -20 gpurun_out/r4q_als_$v.err; exit 1; }
+  echo "$v $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/r4q_als_$v.json').read().strip().splitlines()[-1]); print(d['value'])")"
+done
 timeout -k 10 900 bash tools/gpu_r4p.sh
