@@ -78,13 +78,11 @@ _SIGS: dict[str, list] = {
     "o3s_confusion": [c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp],
     "o3s_score_hist": [c_vp, c_i32, c_i64, c_vp, c_i32, c_vp, c_i32, c_i64, c_f64, c_f64, c_i32, c_vp, c_vp],
     "o3s_als_wood": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
-    "o3s_als_wood_s3": [c_i32],
     "o3s_als_wood_timed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp],
     "o3s_als_dense": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "o3s_als_dense_mfma": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "o3s_als_dense_mfma_blk": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "o3s_als_dense_mfma_gl": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
-    "o3s_als_dense_mfma_gd": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "o3s_als_dense_mfma_timed": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp],
     "o3s_als_exact_max_small": [],
     "o3s_als_rotate": [c_i32, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],

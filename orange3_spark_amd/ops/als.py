@@ -126,9 +126,6 @@ EXACT_RANKS = (32, 64, 96, 128)
 # the f32 Gram (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144).
 # Rejected: rating indices prefetched one Gram step ahead of the gathers (0.127 vs 0.122 s)
 DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_gl")
-# Woodbury S = P D P^T: exact fp32 MFMA products (default) or bf16x3 (O3S_ALS_WOOD_S3=1; a
-# 4-waves-per-SIMD build of the kernel measured 8.6% slower: profiles/als_wood_readlane_cholesky_r4.json)
-WOOD_S3 = os.environ.get("O3S_ALS_WOOD_S3", "0") == "1"
 
 
 def exact_kernel_ok(F: torch.Tensor) -> bool:
@@ -238,7 +235,6 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
             eig, Q, P = EIG_CACHE.get(F, G, True)
         else:
             eig, Q, P = torch.zeros(R, dtype=torch.float32, device=dev), None, F
-        lib.o3s_als_wood_s3(int(WOOD_S3))
         N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), P.data_ptr(),
                                  eig.data_ptr(), lam.data_ptr(), small.data_ptr(), ns, out.data_ptr(), st),
                 "als_wood")
@@ -250,8 +246,7 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
     if nd:
         Gf = G.float().contiguous() if implicit else None
         fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
-              "mfma_gl": lib.o3s_als_dense_mfma_gl, "mfma_gd": lib.o3s_als_dense_mfma_gd}.get(
-            DENSE_KERNEL, lib.o3s_als_dense)
+              "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(DENSE_KERNEL, lib.o3s_als_dense)
         N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                    F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), nd, out.data_ptr(), st),
                 "als_dense")

@@ -89,9 +89,9 @@ __device__ __forceinline__ float wood_factor_solve(float (&srow)[kNW], float v, 
 // Cholesky, both solves, output (cycles; the gathers are waited for with vmcnt(0) there)
 // WOCC: waves per SIMD the register budget must allow (3: 168 VGPRs, no spill; 4: 128,
 // a 44-byte spill -- o3s_als_wood_occ selects the build)
-// S3: S = P' P'^T as bf16x3 on v_mfma_f32_32x32x16_bf16 (hi.hi + lo.hi + hi.lo, ~2^-16
-// relative, the dense Gram's numerics) instead of exact fp32 products on 32x32x2
-template <int R, bool TIM = false, int WOCC = 3, bool S3 = false>
+// (a 4-waves-per-SIMD build spilled and measured 8.6% slower; S = P D P^T as bf16x3 on
+// 32x32x16 MFMAs measured 4% slower: profiles/kernel_experiments_r4.json)
+template <int R, bool TIM = false, int WOCC = 3>
 __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ P, const float* __restrict__ eig,
@@ -170,30 +170,6 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   for (int hf = 0; hf < RV; ++hf) {
 #pragma unroll
     for (int i = 0; i < kNW; ++i) sp[i * kPS + wcol] = hf == 0 ? acc[i].x * sq.x : acc[i].y * sq.y;
-    if constexpr (S3) {
-      // k-step m: lane l holds features 16 m + 8 (l >> 5) .. + 8 of row l & 31 -- the same
-      // register serves as the A (rows) and the B (columns) operand of S = P' P'^T
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const float* src = sp + (lane & 31) * kPS + 36 * (m >> 1) + 16 * (m & 1) + 8 * (lane >> 5);
-        const float4_ u0 = *reinterpret_cast<const float4_*>(src);
-        const float4_ u1 = *reinterpret_cast<const float4_*>(src + 4);
-        const float uv[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-        uint32_t ph[4], pl[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint16_t h0 = f32_to_bf16(uv[2 * j]), h1 = f32_to_bf16(uv[2 * j + 1]);
-          const uint16_t l0 = f32_to_bf16(uv[2 * j] - bf16_to_f32(h0));
-          const uint16_t l1 = f32_to_bf16(uv[2 * j + 1] - bf16_to_f32(h1));
-          ph[j] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-          pl[j] = (uint32_t)l0 | ((uint32_t)l1 << 16);
-        }
-        const bf16x8_ hi = __builtin_bit_cast(bf16x8_, ph), lo = __builtin_bit_cast(bf16x8_, pl);
-        sa0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi, hi, sa0, 0, 0, 0);
-        sa1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lo, hi, sa1, 0, 0, 0);
-        sa1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi, lo, sa1, 0, 0, 0);
-      }
-    } else {
 #pragma unroll
     for (int s4 = 0; s4 < 32; s4 += 4) {
       const float4_ v = *reinterpret_cast<const float4_*>(rp + s4);
@@ -201,7 +177,6 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
       sa1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.y, v.y, sa1, 0, 0, 0);
       sa0 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.z, v.z, sa0, 0, 0, 0);
       sa1 = __builtin_amdgcn_mfma_f32_32x32x2f32(v.w, v.w, sa1, 0, 0, 0);
-    }
     }
   }
   const f32x16_ sacc = sa0 + sa1;
@@ -666,19 +641,7 @@ struct DenseM {
   static constexpr int LDSG = SA + XR + R + 2 * CH + W * 32 + 3 * IC + 2 * DEP * CH;
 };
 
-// upper-triangle tile t of a 4 x 4 tile grid (order (0,0), (0,1), .., (1,1), ..) -> (j, i)
-__host__ __device__ constexpr int ut_j(int t) {
-  int j = 0;
-  while (t >= 4 - j) { t -= 4 - j; ++j; }
-  return j;
-}
-__host__ __device__ constexpr int ut_i(int t) {
-  int j = 0;
-  while (t >= 4 - j) { t -= 4 - j; ++j; }
-  return j + t;
-}
-
-template <int R, bool IMPL, bool BLK, bool TIM = false, bool GL = false, bool GD = false>
+template <int R, bool IMPL, bool BLK, bool TIM = false, bool GL = false>
 __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
@@ -813,38 +776,6 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
     auto gram_step = [&](int buf) {
       const uint16_t* th = sT + buf * 2 * R * LDT + q * LDT + 8 * h;
       const uint16_t* tl = th + R * LDT;
-      if constexpr (GLP && NT == 4 && W == 4 && GD) {
-        // every row block's hi / lo fragments read once (the A and B operands of a tile are
-        // the same staged rows, and a wave's tiles share blocks), then the wave's tiles
-        // (t = wid + 4 s, compile-time per wave) issued term-major: 2-3 independent MFMA
-        // chains instead of three dependent MFMAs per tile behind each tile's LDS reads
-        bf16x8_ fh[4], fl[4];
-#pragma unroll
-        for (int b2 = 0; b2 < 4; ++b2) {
-          fh[b2] = *reinterpret_cast<const bf16x8_*>(th + 32 * b2 * LDT);
-          fl[b2] = *reinterpret_cast<const bf16x8_*>(tl + 32 * b2 * LDT);
-        }
-        auto tiles = [&](auto wtag) {
-          constexpr int WV = decltype(wtag)::value;
-          constexpr int NS = WV + 8 < 10 ? 3 : 2;
-          constexpr int J[3] = {ut_j(WV), ut_j(WV + 4), ut_j(WV + 8 < 10 ? WV + 8 : 0)};
-          constexpr int I[3] = {ut_i(WV), ut_i(WV + 4), ut_i(WV + 8 < 10 ? WV + 8 : 0)};
-#pragma unroll
-          for (int s2 = 0; s2 < NS; ++s2)
-            acc[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh[J[s2]], fh[I[s2]], acc[s2], 0, 0, 0);
-#pragma unroll
-          for (int s2 = 0; s2 < NS; ++s2)
-            acc[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fl[J[s2]], fh[I[s2]], acc[s2], 0, 0, 0);
-#pragma unroll
-          for (int s2 = 0; s2 < NS; ++s2)
-            acc[s2] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fh[J[s2]], fl[I[s2]], acc[s2], 0, 0, 0);
-        };
-        if (wid == 0) tiles(std::integral_constant<int, 0>{});
-        else if (wid == 1) tiles(std::integral_constant<int, 1>{});
-        else if (wid == 2) tiles(std::integral_constant<int, 2>{});
-        else tiles(std::integral_constant<int, 3>{});
-        return;
-      }
 #pragma unroll
       for (int s = 0; s < MT; ++s) {
         if (tj[s] >= NT) continue;
@@ -1274,15 +1205,6 @@ __global__ __launch_bounds__(DenseM<R>::NTH, BLK ? 3 : 1) void als_dense_mfma_ke
 // rotated into the eigenbasis of G (F Q, implicit) or F itself (explicit, eig = 0);
 // eig: the eigenvalues of G (zeros when explicit).  X row u receives y_u = D P_u^T z
 // (implicit: the caller applies x = Q y) or x_u (explicit).
-namespace {
-int g_wood_s3 = 0;
-}
-// Woodbury S build: 0 = exact fp32 products (default), 1 = bf16x3 (see S3)
-O3S_API int o3s_als_wood_s3(int on) {
-  g_wood_s3 = on ? 1 : 0;
-  return 0;
-}
-
 // Diagnostic: als_wood_kernel<128> with per-row phase cycles in timing [nsmall][5].
 O3S_API int o3s_als_wood_timed(const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
                                const float* P, const float* eig, const float* lam, const int32_t* small,
@@ -1302,12 +1224,8 @@ O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, cons
   const dim3 grid((unsigned)((nsmall + kWW - 1) / kWW));
 #define O3S_WD(RR)                                                                                          \
   if (R == RR) {                                                                                            \
-    if (g_wood_s3)                                                                                          \
-      hipLaunchKernelGGL((als_wood_kernel<RR, false, 3, true>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, \
-                         P, eig, lam, small, nsmall, X, nullptr);                                           \
-    else                                                                                                    \
-      hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, eig, lam, \
-                         small, nsmall, X, nullptr);                                                        \
+    hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, eig, lam, \
+                       small, nsmall, X, nullptr);                                                          \
     O3S_CHECK_LAUNCH();                                                                                     \
     return 0;                                                                                               \
   }
@@ -1355,7 +1273,7 @@ O3S_API int o3s_als_dense(int implicit, int R, const int64_t* indptr, const int3
 }
 
 namespace {
-template <bool BLK, bool GL = false, bool GD = false>
+template <bool BLK, bool GL = false>
 int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
                       const float* b, const float* F, const float* G, const float* lam, const int32_t* dense,
                       int64_t ndense, float* X, hipStream_t st) {
@@ -1364,10 +1282,10 @@ int launch_dense_mfma(int implicit, int R, const int64_t* indptr, const int32_t*
 #define O3S_DM(RR)                                                                                              \
   if (R == RR) {                                                                                                \
     if (implicit)                                                                                               \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK, false, GL, GD>), dim3((unsigned)ndense),         \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, true, BLK, false, GL>), dim3((unsigned)ndense),             \
                          dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X, nullptr);       \
     else                                                                                                        \
-      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK, false, GL, GD>), dim3((unsigned)ndense),        \
+      hipLaunchKernelGGL((als_dense_mfma_kernel<RR, false, BLK, false, GL>), dim3((unsigned)ndense),            \
                          dim3(DenseM<RR>::NTH), 0, st, indptr, cols, w, b, F, G, lam, dense, X, nullptr);       \
     O3S_CHECK_LAUNCH();                                                                                         \
     return 0;                                                                                                   \
@@ -1396,13 +1314,6 @@ O3S_API int o3s_als_dense_mfma_gl(int implicit, int R, const int64_t* indptr, co
                                   const float* b, const float* F, const float* G, const float* lam,
                                   const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
   return launch_dense_mfma<true, true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
-}
-
-// _gl with the Gram's fragments read once per row block and the tiles' MFMAs interleaved
-O3S_API int o3s_als_dense_mfma_gd(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
-                                  const float* b, const float* F, const float* G, const float* lam,
-                                  const int32_t* dense, int64_t ndense, float* X, hipStream_t st) {
-  return launch_dense_mfma<true, true, true>(implicit, R, indptr, cols, w, b, F, G, lam, dense, ndense, X, st);
 }
 
 // Diagnostic: the dense kernel (BLK, implicit, R = 128; gl != 0: with the LDS-DMA gather

@@ -274,7 +274,7 @@ def test_gpu_exact_kernels_pad_other_ranks(R, implicit):
 @pytest.mark.gpu
 @pytest.mark.parametrize("R", [32, 64, 96, 128])
 @pytest.mark.parametrize("implicit", [False, True])
-@pytest.mark.parametrize("kernel", ["mfma", "mfma_blk", "mfma_gl", "mfma_gd", "vgpr"])
+@pytest.mark.parametrize("kernel", ["mfma", "mfma_blk", "mfma_gl", "vgpr"])
 def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
     """Both dense exact kernels (als_dense_mfma_kernel: 32 x 32 MFMA accumulator tiles;
     als_dense_kernel: 8 x 8 register tiles) == the fp64 solve on rows routed to the dense
@@ -291,7 +291,7 @@ def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
     from orange3_spark_amd.ops import _native as N
     lib = N.kernels()
     fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
-          "mfma_gl": lib.o3s_als_dense_mfma_gl, "mfma_gd": lib.o3s_als_dense_mfma_gd}.get(kernel, lib.o3s_als_dense)
+          "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(kernel, lib.o3s_als_dense)
     Gf = G.float().contiguous() if implicit else None
     N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), F.data_ptr(),
                N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), 40, got.data_ptr(), N.stream_of(got)), "als_dense")

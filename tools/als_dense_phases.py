@@ -48,11 +48,6 @@ def main():
                                           F.data_ptr(), G.data_ptr(), lam.data_ptr(), dense.data_ptr(), a.items,
                                           out.data_ptr(), st), "dense_gl")
 
-    def prod_gd():
-        N.check(lib.o3s_als_dense_mfma_gd(1, R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
-                                          F.data_ptr(), G.data_ptr(), lam.data_ptr(), dense.data_ptr(), a.items,
-                                          out.data_ptr(), st), "dense_gd")
-
     def prod():
         N.check(lib.o3s_als_dense_mfma_blk(1, R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                                            F.data_ptr(), G.data_ptr(), lam.data_ptr(), dense.data_ptr(), a.items,
@@ -63,8 +58,7 @@ def main():
                                              F.data_ptr(), G.data_ptr(), lam.data_ptr(), dense.data_ptr(), a.items,
                                              out.data_ptr(), tim.data_ptr(), st), "dense_timed")
     res = {}
-    for name, fn in (("production_blk", prod), ("production_gl", prod_gl), ("production_gd", prod_gd),
-                     ("timed", timed)):
+    for name, fn in (("production_blk", prod), ("production_gl", prod_gl), ("timed", timed)):
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -30,3 +30,11 @@ for v in mfma_gl mfma_gd mfma_gl mfma_gd; do
   echo "$v $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/r4q_als_$v.json').read().strip().splitlines()[-1]); print(d['value'])")"
 done
 timeout -k 10 900 bash tools/gpu_r4p.sh
+# verification of the current defaults: the whole GPU suite, smoke(), the N=1 bench
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+  > gpurun_out/r4q_gputests.log 2>&1 || { echo "gpu tests failed"; grep -E "FAILED|Error" gpurun_out/r4q_gputests.log | head -20; tail -20 gpurun_out/r4q_gputests.log; exit 1; }
+tail -1 gpurun_out/r4q_gputests.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4q_smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/r4q_smoke.log; exit 1; }
+tail -1 gpurun_out/r4q_smoke.log
+timeout -k 10 300 python -u bench.py > gpurun_out/r4q_bench.json 2> gpurun_out/r4q_bench.err || { echo "bench failed"; tail -20 gpurun_out/r4q_bench.err; exit 1; }
+grep -v amdgpu.ids gpurun_out/r4q_bench.json
