@@ -17,3 +17,5 @@ for pf in 0 1 0 1; do
     || { echo "bench_als $pf failed"; tail -20 gpurun_out/r4r_als_$pf.err; exit 1; }
   echo "als pf=$pf $(python3 -c "import json,sys; d=json.loads(open('gpurun_out/r4r_als_$pf.json').read().strip().splitlines()[-1]); print(d['value'])")"
 done
+timeout -k 10 420 python -u tools/bench_configs.py --config als --iters 3 --trace --out gpurun_out/r4r_cfg_als_trace.json > gpurun_out/r4r_cfg_als_trace.log 2>&1 || { echo "als cfg failed"; tail -30 gpurun_out/r4r_cfg_als_trace.log; exit 1; }
+cat gpurun_out/r4r_cfg_als_trace.json
