@@ -4,6 +4,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_als.py \
+  > gpurun_out/r4r_tests.log 2>&1 || { echo "tests failed"; grep -E "assert|Error" gpurun_out/r4r_tests.log | head -10; tail -5 gpurun_out/r4r_tests.log; exit 1; }
+tail -1 gpurun_out/r4r_tests.log
 O3S_ALS_WOOD_PF=1 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_als.py \
   > gpurun_out/r4r_tests_pf.log 2>&1 || { echo "pf tests failed"; grep -E "assert|Error" gpurun_out/r4r_tests_pf.log | head -10; tail -5 gpurun_out/r4r_tests_pf.log; exit 1; }
 tail -1 gpurun_out/r4r_tests_pf.log
