@@ -126,8 +126,6 @@ EXACT_RANKS = (32, 64, 96, 128)
 # the f32 Gram (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144).
 # Rejected: rating indices prefetched one Gram step ahead of the gathers (0.127 vs 0.122 s)
 DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_gl")
-# Woodbury rows: persistent waves that prefetch the next row's metadata (O3S_ALS_WOOD_PF=1)
-WOOD_PF = os.environ.get("O3S_ALS_WOOD_PF", "0") == "1"
 
 
 def exact_kernel_ok(F: torch.Tensor) -> bool:
@@ -237,7 +235,6 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
             eig, Q, P = EIG_CACHE.get(F, G, True)
         else:
             eig, Q, P = torch.zeros(R, dtype=torch.float32, device=dev), None, F
-        lib.o3s_als_wood_pf(int(WOOD_PF))
         N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), P.data_ptr(),
                                  eig.data_ptr(), lam.data_ptr(), small.data_ptr(), ns, out.data_ptr(), st),
                 "als_wood")

@@ -87,18 +87,18 @@ __device__ __forceinline__ float wood_factor_solve(float (&srow)[kNW], float v, 
 // TIM (diagnostic build, o3s_als_wood_timed): lane 0 stamps the shader clock at the phase
 // boundaries of each row -> timing[row][0..4] = gathers landed, S built (MFMA + LDS image),
 // Cholesky, both solves, output (cycles; the gathers are waited for with vmcnt(0) there)
+// WOCC: waves per SIMD the register budget must allow (3: 168 VGPRs, no spill).
 // (a 4-waves-per-SIMD build spilled and measured 8.6% slower; S = P D P^T as bf16x3 on
-// 32x32x16 MFMAs measured 4% slower: profiles/kernel_experiments_r4.json)
-// PF: persistent waves -- each wave solves rows li, li + stride, ..., and fetches the next
-// row's metadata chain (rows -> indptr / lam -> cols / w / b: three dependent round trips
-// that otherwise precede every row's factor gathers) while the current row is solved.
-template <int R, bool TIM = false, int WOCC = 3, bool PF = false>
+// 32x32x16 MFMAs measured 4% slower; persistent waves prefetching the next row's metadata
+// measured 14% slower: profiles/kernel_experiments_r4.json)
+template <int R, bool TIM = false, int WOCC = 3>
 __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ P, const float* __restrict__ eig,
     const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nlist, float* __restrict__ X,
     int64_t* __restrict__ timing = nullptr) {
   int64_t tm[6] = {0, 0, 0, 0, 0, 0};
+  if constexpr (TIM) tm[0] = clock64();
   static_assert(R % 32 == 0 && R <= 128, "rank must be a multiple of 32, at most 128");
   constexpr int RV = (R + 63) / 64;              // columns per lane (1 or 2)
   // per wave: the sqrt(D)-scaled rows P' for the MFMA (32 x kPS floats), later reused for
@@ -106,39 +106,23 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   __shared__ __attribute__((aligned(16))) float sP[kWW][kNW * kPS];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  int64_t li = (int64_t)blockIdx.x * kWW + wv;
-  const int64_t stride = (int64_t)gridDim.x * kWW;
+  const int64_t li = (int64_t)blockIdx.x * kWW + wv;
   if (li >= nlist) return;                       // wave-uniform; the kernel has no block barrier
+  const int64_t u = rows[li];
+  const int64_t p0 = indptr[u];
+  const int n = (int)(indptr[u + 1] - p0);       // <= kNW (host routing)
+  const float lu = lam[u];
   float (*S)[kNW + 1] = reinterpret_cast<float (*)[kNW + 1]>(sP[wv]);
-  const bool c0ok = lane < R, c1ok = RV > 1 && lane + 64 < R;
-  const float e0 = c0ok ? eig[lane] : 0.f, e1 = c1ok ? eig[lane + 64] : 0.f;
-  // the first row's metadata
-  int64_t u = rows[li];
-  int64_t p0 = indptr[u];
-  int n = (int)(indptr[u + 1] - p0);             // <= kNW (host routing)
-  float lu = lam[u];
-  int myc = 0;
-  float wi = 0.f, bi = 0.f;
-  if (lane < n) {
-    myc = cols[p0 + lane];
-    wi = w[p0 + lane];
-    bi = b[p0 + lane];
-  }
-  for (;;) {
-  if constexpr (TIM) tm[0] = clock64();
-  const int64_t li_n = li + stride;
-  const bool more = PF && li_n < nlist;          // wave-uniform
-  int64_t u_n = 0, p0_n = 0;
-  int n_n = 0, myc_n = 0;
-  float lu_n = 0.f, wi_n = 0.f, bi_n = 0.f;
 
   // per-rating W^{-1} c (lane i < n holds rating i); w = 0 (r = 0 implicit): no term
   float t = 0.f, winv = 0.f;
   if (lane < n) {
+    const float wi = w[p0 + lane], bi = b[p0 + lane];
     winv = wi > 0.f ? 1.f / wi : 1e30f;
     t = wi > 0.f ? bi * winv : 0.f;
   }
-  const float2_ dd = {c0ok ? 1.f / (e0 + lu) : 0.f, c1ok ? 1.f / (e1 + lu) : 0.f};
+  const bool c0ok = lane < R, c1ok = RV > 1 && lane + 64 < R;
+  const float2_ dd = {c0ok ? 1.f / (eig[lane] + lu) : 0.f, c1ok ? 1.f / (eig[lane + 64] + lu) : 0.f};
 
   // rows of P = Y_u Q gathered from the pre-rotated table (F Q, one GEMM per
   // half-iteration; F itself when explicit): acc[i] = (P[i][lane], P[i][lane + 64]).
@@ -148,6 +132,7 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   // the row's rating indices arrive in ONE vector load (lane i holds index i) and are
   // broadcast by v_readlane, so the n row gathers issue back to back (a scalar load per
   // index would serialise n load latencies behind the per-row guards)
+  const int myc = lane < n ? cols[p0 + lane] : 0;
   int ci[kNW];                                   // all broadcasts before the first gather
 #pragma unroll
   for (int i = 0; i < kNW; ++i) ci[i] = __builtin_amdgcn_readlane(myc, i);
@@ -162,7 +147,6 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
     }
   }
 
-  if (more) u_n = rows[li_n];                    // next row, stage 1 (scalar load)
   if constexpr (TIM) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     tm[1] = clock64();
@@ -205,11 +189,6 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   float srow[kNW];
 #pragma unroll
   for (int m = 0; m < kNW; ++m) srow[m] = S[lane & 31][m];
-  if (more) {                                    // next row, stage 2
-    p0_n = indptr[u_n];
-    n_n = (int)(indptr[u_n + 1] - p0_n);
-    lu_n = lam[u_n];
-  }
   if constexpr (TIM) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     tm[2] = clock64();
@@ -224,11 +203,6 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   else if (n <= 16) v = wood_factor_solve<16>(srow, t, Lc, lane);
   else if (n <= 24) v = wood_factor_solve<24>(srow, t, Lc, lane);
   else v = wood_factor_solve<32>(srow, t, Lc, lane);
-  if (more && lane < n_n) {                      // next row, stage 3 (vector loads)
-    myc_n = cols[p0_n + lane];
-    wi_n = w[p0_n + lane];
-    bi_n = b[p0_n + lane];
-  }
   if constexpr (TIM) tm[3] = clock64();
   if constexpr (TIM) tm[4] = clock64();
   // y = D P^T z: the solution in the eigenbasis (implicit; the host rotates x = Q y for all
@@ -249,16 +223,6 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
     tm[5] = clock64();
     if (lane == 0)
       for (int k = 0; k < 5; ++k) timing[li * 5 + k] = tm[k + 1] - tm[k];
-  }
-  if (!more) break;
-  li = li_n;
-  u = u_n;
-  p0 = p0_n;
-  n = n_n;
-  lu = lu_n;
-  myc = myc_n;
-  wi = wi_n;
-  bi = bi_n;
   }
 }
 
@@ -1252,41 +1216,16 @@ O3S_API int o3s_als_wood_timed(const int64_t* indptr, const int32_t* cols, const
   return 0;
 }
 
-namespace {
-int g_wood_pf = 0;          // o3s_als_wood_pf: persistent, metadata-prefetching Woodbury build
-int wood_persistent_blocks() {
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
-  return cus * 6;           // 12 waves per CU: the 3 waves per SIMD the register budget allows
-}
-}  // namespace
-
-O3S_API int o3s_als_wood_pf(int on) {
-  g_wood_pf = on ? 1 : 0;
-  return 0;
-}
-
 O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
                          const float* P, const float* eig, const float* lam, const int32_t* small, int64_t nsmall,
                          float* X, hipStream_t st) {
   if (nsmall < 0 || !eig || !P) return -1;
   if (nsmall == 0) return 0;
-  const int64_t need = (nsmall + kWW - 1) / kWW;
-  const dim3 grid((unsigned)need);
-  const dim3 pgrid((unsigned)(need < wood_persistent_blocks() ? need : wood_persistent_blocks()));
+  const dim3 grid((unsigned)((nsmall + kWW - 1) / kWW));
 #define O3S_WD(RR)                                                                                          \
   if (R == RR) {                                                                                            \
-    if (g_wood_pf)                                                                                          \
-      hipLaunchKernelGGL((als_wood_kernel<RR, false, 3, true>), pgrid, dim3(kWW * 64), 0, st, indptr, cols, w, \
-                         b, P, eig, lam, small, nsmall, X, nullptr);                                        \
-    else                                                                                                    \
-      hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, eig, lam, \
-                         small, nsmall, X, nullptr);                                                        \
+    hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, eig, lam, \
+                       small, nsmall, X, nullptr);                                                          \
     O3S_CHECK_LAUNCH();                                                                                     \
     return 0;                                                                                               \
   }

@@ -18,7 +18,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--users", type=int, default=2_000_000)
     ap.add_argument("--other", type=int, default=5_000_000)
-    ap.add_argument("--pf", type=int, default=0, help="persistent prefetching build (production kernel)")
     a = ap.parse_args()
     from orange3_spark_amd.models import als as AE
     from orange3_spark_amd.ops import _native as N
@@ -41,7 +40,6 @@ def main():
     out = torch.empty((a.users, R), device=dev)
     tim = torch.zeros((a.users, 5), dtype=torch.int64, device=dev)
     lib = N.kernels()
-    lib.o3s_als_wood_pf(a.pf)
     st = N.stream_of(out)
 
     def prod():
@@ -70,7 +68,6 @@ def main():
     res["share_of_row"] = {k: round(v / tot, 3) for k, v in zip(names, m)}
     res["users"], res["other_rows"], res["ratings"], res["mean_len"] = a.users, a.other, nnz, nnz / a.users
     res["ns_per_row_production"] = res["production_ms"] * 1e6 / a.users
-    res["pf"] = a.pf
     print(json.dumps(res))
 
 
