@@ -236,11 +236,15 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
 
 
 def gram(F: torch.Tensor, chunk: int = 1 << 20) -> torch.Tensor:
-    """F^T F (fp64 [R, R]) as chunked fp32 GEMMs (hipBLASLt) accumulated in fp64.
-
-    One fp64 GEMM over millions of rows runs on the fp64 matrix path (~180 ms for
-    6.25M x 128 on MI355X); fp32 tiles of 1M rows keep the long sum in fp64 at ~1 ms."""
+    """F^T F (fp64 [R, R]).  On the GPU (fp32, R <= 128): ``ftf_kernel`` -- exact fp32
+    products on the matrix cores, each wave summing its own row range, the wave partials
+    added in fp64 in a fixed order.  Elsewhere: chunked fp32 GEMMs accumulated in fp64 (one
+    fp64 GEMM over millions of rows runs on the fp64 matrix path, ~180 ms for 6.25M x 128;
+    hipBLASLt's fp32 GEMM of this shape keeps a few CUs busy: ~1.8 ms per 1M rows)."""
     R = F.shape[1]
+    if (F.is_cuda and F.dtype == torch.float32 and F.dim() == 2 and 0 < R <= 128 and F.stride(1) == 1
+            and F.shape[0] > 0):
+        return A.ftf(F)
     out = torch.zeros((R, R), dtype=torch.float64, device=F.device)
     for a in range(0, F.shape[0], chunk):
         Fc = F[a:a + chunk].float()

@@ -37,6 +37,7 @@ _SIGS: dict[str, list] = {
     "o3s_u8_transpose": [c_vp, c_i64, c_i32, c_vp, c_vp],
     "o3s_slab_range_sum": [c_vp, c_i32, c_i64, c_vp, c_vp, c_i32, c_vp, c_vp],
     "o3s_tree_leaf_apply": [c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp],
+    "o3s_ftf": [c_vp, c_i64, c_i64, c_i32, c_i64, c_vp, c_vp, c_vp],
     "o3s_als_gram": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp],
     "o3s_csr_glm": [c_i32, c_vp, c_vp, c_vp, c_i64, c_vp, c_f32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp],
     "o3s_csc_colsum": [c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],

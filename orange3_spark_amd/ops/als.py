@@ -128,6 +128,28 @@ EXACT_RANKS = (32, 64, 96, 128)
 DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_gl")
 
 
+_FTF_WS: dict = {}
+
+
+def ftf(F: torch.Tensor) -> torch.Tensor:
+    """F^T F (fp64 [R, R]) of a device fp32 table with unit column stride and R <= 128
+    (``ftf_kernel`` + ``ftf_reduce_kernel``: bitwise reproducible for a given shape)."""
+    n, R = F.shape
+    nt = (R + 31) // 32
+    nl = nt * (nt + 1) // 2
+    nwaves = max(4, min(2048, (-(-n // 4096) + 3) // 4 * 4))
+    need = nwaves * nl * 1024
+    ws = _FTF_WS.get(F.device)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(max(need, 2048 * 10 * 1024 if n >= (1 << 22) else need), dtype=torch.float32,
+                         device=F.device)
+        _FTF_WS[F.device] = ws
+    out = torch.empty((R, R), dtype=torch.float64, device=F.device)
+    N.check(N.kernels().o3s_ftf(F.data_ptr(), n, F.stride(0), R, nwaves, ws.data_ptr(), out.data_ptr(),
+                                N.stream_of(F)), "ftf")
+    return out
+
+
 def exact_kernel_ok(F: torch.Tensor) -> bool:
     """Any rank up to 128 runs on the kernels: ranks between the compiled sizes are padded
     with zero factor columns (see :func:`exact_solve`)."""

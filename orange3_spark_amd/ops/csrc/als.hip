@@ -325,7 +325,132 @@ __global__ __launch_bounds__(256) void als_init_kernel(int64_t row0, int64_t n, 
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// F^T F of an [n][ld] fp32 factor table (the implicit-ALS Gram Y^T Y, once per
+// half-iteration over all rows of one side).  Exact fp32 products on
+// v_mfma_f32_32x32x2_f32 with the K index running over rows: each wave owns a contiguous
+// row range and ALL NT (NT + 1) / 2 upper 32 x 32 tiles of the result in its accumulators
+// (NT = 4: 10 tiles, 160 registers), so no operand is shared between waves and no LDS is
+// touched -- per row pair a lane loads one float per 32-column block,
+// F[r + (lane >> 5)][32 cb + (lane & 31)] (coalesced 128-B half-wave runs), which is at once
+// the A operand (rows i of the tile) and the B operand (columns j) of every tile using
+// block cb.  PF row pairs are in flight per wave.  Partials go to slab[wave][tile][16][64]
+// in accumulator order; ftf_reduce_kernel sums them per element in wave order in fp64
+// (bitwise reproducible).  hipBLASLt's GEMM for this shape (K = millions, M = N = 128)
+// ran a handful of 32 x 32 output tiles on a few CUs: ~1.8 ms per 1M rows.
+typedef float f32x16_ __attribute__((ext_vector_type(16)));
+constexpr int kFtfWaves = 4;
+
+template <int NT>
+__global__ __launch_bounds__(kFtfWaves * 64, 2) void ftf_kernel(const float* __restrict__ F, int64_t n, int64_t ld,
+                                                                int R, int64_t rows_per_wave,
+                                                                float* __restrict__ slab) {
+  constexpr int NL = NT * (NT + 1) / 2;
+  constexpr int PF = NT == 4 ? 6 : 8;                    // row pairs in flight (register budget)
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * kFtfWaves + (threadIdx.x >> 6);
+  const int64_t r0 = gw * rows_per_wave;
+  const int64_t r1 = r0 + rows_per_wave < n ? r0 + rows_per_wave : n;
+  const int kr = lane >> 5, c = lane & 31;
+  float cm[NT];                                          // column mask (columns >= R read as 0)
+  int col[NT];
+#pragma unroll
+  for (int cb = 0; cb < NT; ++cb) {
+    cm[cb] = 32 * cb + c < R ? 1.f : 0.f;
+    col[cb] = 32 * cb + c < R ? 32 * cb + c : 0;
+  }
+  f32x16_ acc[NL];
+#pragma unroll
+  for (int t = 0; t < NL; ++t)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[t][v] = 0.f;
+  auto load = [&](int64_t pr, float (&o)[NT]) {         // row pair pr of the range (clamped row)
+    int64_t r = r0 + 2 * pr + kr;
+    r = r < n ? r : n - 1;
+#pragma unroll
+    for (int cb = 0; cb < NT; ++cb) o[cb] = F[r * ld + col[cb]];
+  };
+  auto consume = [&](const float (&o)[NT], float rm) {  // rm: this lane's row weight (0 / 1)
+    float a[NT];
+#pragma unroll
+    for (int cb = 0; cb < NT; ++cb) a[cb] = o[cb] * cm[cb] * rm;
+    int t = 0;
+#pragma unroll
+    for (int i = 0; i < NT; ++i)
+#pragma unroll
+      for (int j = i; j < NT; ++j, ++t) acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], a[j], acc[t], 0, 0, 0);
+  };
+  const int64_t nrows = r1 > r0 ? r1 - r0 : 0;
+  const int64_t full = nrows / 2 / PF * PF;              // whole ring rounds of full pairs
+  float v[PF][NT];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load(u, v[u]);
+  for (int64_t pr = 0; pr < full; pr += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      consume(v[u], 1.f);
+      load(pr + PF + u, v[u]);                           // next round (clamped past the range)
+    }
+  }
+  // tail: the remaining rows one pair at a time, rows past the range weighted 0
+  for (int64_t pr = full; 2 * pr < nrows; ++pr) {
+    float o[NT];
+    load(pr, o);
+    consume(o, r0 + 2 * pr + kr < r1 ? 1.f : 0.f);
+  }
+  float* out = slab + gw * NL * 1024;
+#pragma unroll
+  for (int t = 0; t < NL; ++t)
+#pragma unroll
+    for (int v2 = 0; v2 < 16; ++v2) out[(t * 16 + v2) * 64 + lane] = acc[t][v2];
+}
+
+// out[i][j] (fp64 R x R, both triangles) = sum over waves, in wave order, of the slab
+// element holding (i, j) of the upper tile (i / 32, j / 32) (i <= j; (j, i) otherwise)
+__global__ __launch_bounds__(256) void ftf_reduce_kernel(const float* __restrict__ slab, int64_t nwaves, int NT,
+                                                         int R, double* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= R * R) return;
+  int i = e / R, j = e % R;
+  if (i > j) { const int tmp = i; i = j; j = tmp; }
+  const int ib = i >> 5, jb = j >> 5, ri = i & 31, cj = j & 31;
+  const int t = ib * NT - ib * (ib - 1) / 2 + (jb - ib);  // upper-triangle tile index
+  const int v = (ri & 3) + 4 * (ri >> 3), l = cj + 32 * ((ri >> 2) & 1);
+  const int NL = NT * (NT + 1) / 2;
+  double s = 0.0;
+  for (int64_t g = 0; g < nwaves; ++g) s += (double)slab[(g * NL + t) * 1024 + v * 64 + l];
+  out[e] = s;
+}
+
 }  // namespace
+
+// F^T F (fp64 [R][R]) of an [n][ld] fp32 table, R <= 128.  slab: >= nwaves * NL * 1024
+// floats, NL = NT (NT + 1) / 2, NT = ceil(R / 32); nwaves = a multiple of 4.
+O3S_API int o3s_ftf(const float* F, int64_t n, int64_t ld, int R, int64_t nwaves, float* slab, double* out,
+                    hipStream_t st) {
+  if (n < 0 || R <= 0 || R > 128 || ld < R || nwaves <= 0 || nwaves % kFtfWaves) return -1;
+  const int NT = (R + 31) / 32;
+  int64_t rpw = (n + nwaves - 1) / nwaves;
+  rpw += rpw & 1;                                        // even: whole row pairs per wave
+  const dim3 grid((unsigned)(nwaves / kFtfWaves));
+  if (n > 0) {
+    switch (NT) {
+      case 1: hipLaunchKernelGGL((ftf_kernel<1>), grid, dim3(kFtfWaves * 64), 0, st, F, n, ld, R, rpw, slab); break;
+      case 2: hipLaunchKernelGGL((ftf_kernel<2>), grid, dim3(kFtfWaves * 64), 0, st, F, n, ld, R, rpw, slab); break;
+      case 3: hipLaunchKernelGGL((ftf_kernel<3>), grid, dim3(kFtfWaves * 64), 0, st, F, n, ld, R, rpw, slab); break;
+      default: hipLaunchKernelGGL((ftf_kernel<4>), grid, dim3(kFtfWaves * 64), 0, st, F, n, ld, R, rpw, slab); break;
+    }
+    O3S_CHECK_LAUNCH();
+  } else {
+    if (hipMemsetAsync(slab, 0, sizeof(float) * (size_t)nwaves * (NT * (NT + 1) / 2) * 1024, st) != hipSuccess)
+      return -3;
+  }
+  hipLaunchKernelGGL(ftf_reduce_kernel, dim3((unsigned)((R * R + 255) / 256)), dim3(256), 0, st, slab, nwaves, NT, R,
+                     out);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
 
 // mode 0: CG init (x, av = A-part of A x, rhs -> r, p, rs); mode 1: CG step (p, av = A-part of A p).
 // All [nrows, R] fp32 row-major; pf / rhs may be null where unused.

@@ -326,3 +326,23 @@ def test_blockwise_topk_recommendations_match_brute_force():
     want = torch.topk(U_[u0] @ V_.T, 5).indices
     assert [r.item for r in first.recommendations] == m._iid_t[want].tolist()
     assert recs.filter(recs.user < 10).count() == 10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [10, 32, 64, 96, 128])
+@pytest.mark.parametrize("n", [1, 3, 1001, 300_007])
+def test_gpu_ftf_kernel_matches_fp64(R, n):
+    """ftf_kernel (the implicit-ALS Gram F^T F on the matrix cores, wave partials summed in
+    fp64 in a fixed order) == the fp64 product, for ranks that pad to 32-column blocks, odd
+    row counts, a row stride wider than R, and bitwise repeatable."""
+    from orange3_spark_amd.ops import als as A
+    g = torch.Generator(device="cuda").manual_seed(R + n)
+    base = torch.randn((n, R + 3), generator=g, device="cuda")
+    F = base[:, :R]                                   # stride(0) = R + 3
+    got = A.ftf(F)
+    ref = F.double().T @ F.double()
+    err = (got - ref).abs().max() / ref.abs().max()
+    assert float(err) < 1e-6, float(err)
+    assert torch.equal(got, got.T)
+    assert torch.equal(A.ftf(F), got)
+    assert torch.allclose(AE.gram(F.contiguous()), ref, rtol=1e-6, atol=1e-6 * float(ref.abs().max()))
