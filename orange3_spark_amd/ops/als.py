@@ -126,6 +126,8 @@ EXACT_RANKS = (32, 64, 96, 128)
 # the f32 Gram (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144).
 # Rejected: rating indices prefetched one Gram step ahead of the gathers (0.127 vs 0.122 s)
 DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_gl")
+# x = Q y for the Woodbury rows on the matrix cores (R = 128; O3S_ALS_ROTATE_MFMA=0: packed-FMA kernel)
+ROTATE_MFMA = os.environ.get("O3S_ALS_ROTATE_MFMA", "0") == "1"
 
 
 _FTF_WS: dict = {}
@@ -263,6 +265,7 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
         if implicit:                          # x = Q y for the Woodbury rows (als_rotate_kernel)
             QT = Q.T.contiguous()
             grid = max(1, min(N.num_cus(dev) * 2, -(-ns // 32)))
+            lib.o3s_als_rotate_mfma(int(ROTATE_MFMA))
             N.check(lib.o3s_als_rotate(R, QT.data_ptr(), small.data_ptr(), ns, out.data_ptr(), grid, st),
                     "als_rotate")
     if nd:

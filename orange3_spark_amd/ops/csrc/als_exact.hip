@@ -506,6 +506,68 @@ __global__ __launch_bounds__(Dense<R>::NTH, Dense<R>::MINW) void als_dense_kerne
 // chunked (multi-rank) and whole-table solves give bit-identical factors.
 constexpr int kRotRows = 8;
 
+// x = Q y on the matrix cores (R = 128): a block takes 32 listed rows at a time, stages
+// them in LDS (row stride 130 floats: the MFMA operand reads of 32 rows x 2 columns fall
+// on 64 different banks), and wave w computes output columns [32 w, 32 w + 32) as 64
+// v_mfma_f32_32x32x2_f32 steps (exact fp32 products) with its B operand -- column block w
+// of Q^T, 64 values per lane -- held in registers for the whole launch.  The next tile's
+// rows are loaded into registers while the current tile's MFMAs run.  Every row is computed
+// by the same instruction sequence whatever the list holds (chunked and whole-table solves
+// agree bitwise).  Rows are rewritten in place: a tile's rows are all staged before any is
+// written.
+constexpr int kRotStride = 130;
+__global__ __launch_bounds__(256, 2) void als_rotate_mfma_kernel(const float* __restrict__ QT,
+                                                                 const int32_t* __restrict__ rows, int64_t nrows,
+                                                                 float* __restrict__ X) {
+  __shared__ __attribute__((aligned(16))) float sY[32 * kRotStride];
+  __shared__ int64_t sRid[32];                          // the tile's row ids (-1: past the list)
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane & 31, h = lane >> 5;
+  float bq[64];                                         // B operand: Q^T[2 s + h][32 wid + c]
+#pragma unroll
+  for (int st = 0; st < 64; ++st) bq[st] = QT[(2 * st + h) * 128 + 32 * wid + c];
+  // tile staging: thread t loads row t >> 3, columns 16 (t & 7) .. + 16 (4 float4)
+  const int lr = threadIdx.x >> 3, lc = 16 * (threadIdx.x & 7);
+  const int64_t ntiles = (nrows + 31) / 32;
+  auto load = [&](int64_t tile, float4_ (&o)[4], int64_t& rid) {
+    const int64_t i = tile * 32 + lr;
+    rid = i < nrows ? (int64_t)rows[i] : -1;
+    const int64_t rr = rid >= 0 ? rid : (int64_t)rows[nrows - 1];   // in bounds; never written
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = *reinterpret_cast<const float4_*>(X + rr * 128 + lc + 4 * k);
+  };
+  float4_ nx[4];
+  int64_t nrid = -1;
+  int64_t tile = blockIdx.x;
+  if (tile < ntiles) load(tile, nx, nrid);
+  for (; tile < ntiles; tile += gridDim.x) {
+    // stage this tile (float2 stores: rows start 8-B aligned at stride 130)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float2_* d = reinterpret_cast<float2_*>(sY + lr * kRotStride + lc + 4 * k);
+      d[0] = float2_{nx[k].x, nx[k].y};
+      d[1] = float2_{nx[k].z, nx[k].w};
+    }
+    if ((threadIdx.x & 7) == 0) sRid[lr] = nrid;
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) load(tile + gridDim.x, nx, nrid);
+    f32x16_ acc;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[v] = 0.f;
+    const float* ya = sY + c * kRotStride + h;
+#pragma unroll
+    for (int st = 0; st < 64; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya[2 * st], bq[st], acc, 0, 0, 0);
+    // outputs: register v -> row (v & 3) + 8 (v >> 2) + 4 h of the tile, column 32 wid + c
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int64_t ri = sRid[(v & 3) + 8 * (v >> 2) + 4 * h];
+      if (ri >= 0) X[ri * 128 + 32 * wid + c] = acc[v];
+    }
+    __syncthreads();                                    // sY reused by the next tile
+  }
+}
+
 template <int R>
 __global__ __launch_bounds__(256) void als_rotate_kernel(const float* __restrict__ QT, const int32_t* __restrict__ rows,
                                                          int64_t nrows, float* __restrict__ X) {
@@ -1235,10 +1297,25 @@ O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, cons
 }
 
 // x = Q y in place for the listed rows (QT = Q^T row-major, R x R).
+namespace {
+int g_rotate_mfma = 0;      // o3s_als_rotate_mfma: x = Q y on the matrix cores (R = 128)
+}
+O3S_API int o3s_als_rotate_mfma(int on) {
+  g_rotate_mfma = on ? 1 : 0;
+  return 0;
+}
+
 O3S_API int o3s_als_rotate(int R, const float* QT, const int32_t* rows, int64_t nrows, float* X, int grid,
                            hipStream_t st) {
   if (nrows < 0 || !QT || grid <= 0) return -1;
   if (nrows == 0) return 0;
+  if (R == 128 && g_rotate_mfma) {
+    const int64_t tiles = (nrows + 31) / 32;
+    const int g = (int)(tiles < 4096 ? tiles : 4096);
+    hipLaunchKernelGGL(als_rotate_mfma_kernel, dim3(g), dim3(256), 0, st, QT, rows, nrows, X);
+    O3S_CHECK_LAUNCH();
+    return 0;
+  }
 #define O3S_RT(RR)                                                                                       \
   if (R == RR) {                                                                                         \
     hipLaunchKernelGGL((als_rotate_kernel<RR>), dim3(grid), dim3(256), 0, st, QT, rows, nrows, X);       \
