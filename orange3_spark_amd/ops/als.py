@@ -126,8 +126,9 @@ EXACT_RANKS = (32, 64, 96, 128)
 # the f32 Gram (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144).
 # Rejected: rating indices prefetched one Gram step ahead of the gathers (0.127 vs 0.122 s)
 DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_gl")
-# x = Q y for the Woodbury rows on the matrix cores (R = 128; O3S_ALS_ROTATE_MFMA=0: packed-FMA kernel)
-ROTATE_MFMA = os.environ.get("O3S_ALS_ROTATE_MFMA", "0") == "1"
+# x = Q y for the Woodbury rows on the matrix cores (R = 128: rank-of-8 iteration 0.0903 ->
+# 0.0881 s, profiles/als_rotate_mfma_r4.json; O3S_ALS_ROTATE_MFMA=0: the packed-FMA kernel)
+ROTATE_MFMA = os.environ.get("O3S_ALS_ROTATE_MFMA", "1") == "1"
 
 
 _FTF_WS: dict = {}
