@@ -20,13 +20,14 @@ def main():
     ap.add_argument("--d", type=int, default=128)
     ap.add_argument("--ks", default="2,8,64,1024,4096")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--grid", type=int, default=0, help="update blocks (default 2 per CU)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     X = torch.randn(args.rows, args.d, device=dev)
     out = {"rows": args.rows, "d": args.d, "ms_by_k": {}, "tbps_by_k": {}}
     for k in [int(v) for v in args.ks.split(",")]:
         a = torch.randint(0, k, (args.rows,), device=dev, dtype=torch.int32)
-        ws = K.UpdateWorkspace(dev, k, args.d)
+        ws = K.UpdateWorkspace(dev, k, args.d, grid=args.grid or None)
         K.update(X, a, k, ws)
         torch.cuda.synchronize()
         t = time.perf_counter()

@@ -1,0 +1,6 @@
+#!/bin/bash
+# KMeans update kernel: occupancy variant A/B (100M x 128, k 1024 / 64)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u tools/bench_kmeans_update.py --ks 1024,64 --flush-modes 0,4,0,4 --iters 10 > gpurun_out/r4x_update_g512.log 2>&1 &&
+timeout -k 10 300 python -u tools/bench_kmeans_update.py --ks 1024,64 --flush-modes 0,4,0,4 --iters 10 --grid 768 > gpurun_out/r4x_update_g768.log 2>&1
