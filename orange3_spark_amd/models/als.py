@@ -145,6 +145,19 @@ def _weights(vals: torch.Tensor, implicit: bool, alpha: float):
     return torch.ones_like(vals).float().contiguous(), vals.float().contiguous(), torch.ones_like(vals, dtype=torch.bool)
 
 
+def _row_counts(indptr: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+    """Per CSR row, the number of True entries of ``pos`` (fp32): differences of one
+    prefix sum at the row bounds (no per-rating row-id tensor, no scatter-add)."""
+    n = indptr.numel() - 1
+    if pos.numel() == 0:
+        return torch.zeros(n, dtype=torch.float32, device=pos.device)
+    cs = torch.cumsum(pos, 0, dtype=torch.int32 if pos.numel() < (1 << 31) else torch.int64)
+    ends, starts = indptr[1:], indptr[:-1]
+    hi = torch.where(ends > 0, cs[(ends - 1).clamp_min(0)], torch.zeros((), dtype=cs.dtype, device=cs.device))
+    lo = torch.where(starts > 0, cs[(starts - 1).clamp_min(0)], torch.zeros((), dtype=cs.dtype, device=cs.device))
+    return (hi - lo).to(torch.float32)
+
+
 FUSED_CG = True        # False: CG bookkeeping as separate torch ops (reference path)
 # rows averaging at least this many ratings are solved exactly (MFMA Gram + batched
 # Cholesky, Spark's per-row solve) instead of by warm-started CG; 0 disables.  Off by
@@ -164,12 +177,12 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
     dev = Ffull.device
     key = (implicit, float(alpha), float(reg))
     if key not in csr.cache:          # the ratings do not change between iterations
-        w, b, pos = _weights(csr.vals, implicit, alpha)
-        rows = torch.repeat_interleave(torch.arange(n, device=dev), csr.indptr[1:] - csr.indptr[:-1])
-        nu = torch.zeros(n, dtype=torch.float32, device=dev).index_add_(0, rows, pos.float())
-        csr.cache.clear()
-        csr.cache[key] = (w, b, (reg * nu).to(torch.float32).contiguous())
-        del rows, pos
+        with trace("als.weights"):
+            w, b, pos = _weights(csr.vals, implicit, alpha)
+            nu = _row_counts(csr.indptr, pos)
+            csr.cache.clear()
+            csr.cache[key] = (w, b, (reg * nu).to(torch.float32).contiguous())
+            del pos
     w, b, lam = csr.cache[key]
     nnz = int(csr.cols.numel())
     if exact is None:
@@ -244,7 +257,8 @@ def gram(F: torch.Tensor, chunk: int = 1 << 20) -> torch.Tensor:
     R = F.shape[1]
     if (F.is_cuda and F.dtype == torch.float32 and F.dim() == 2 and 0 < R <= 128 and F.stride(1) == 1
             and F.shape[0] > 0):
-        return A.ftf(F)
+        with trace("als.gram", rows=F.shape[0]):
+            return A.ftf(F)
     out = torch.zeros((R, R), dtype=torch.float64, device=F.device)
     for a in range(0, F.shape[0], chunk):
         Fc = F[a:a + chunk].float()

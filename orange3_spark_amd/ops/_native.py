@@ -88,6 +88,7 @@ _SIGS: dict[str, list] = {
     "o3s_als_exact_max_small": [],
     "o3s_als_rotate_mfma": [c_i32],
     "o3s_als_rotate": [c_i32, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
+    "o3s_als_rotate_to": [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp],
     "o3s_assemble": [c_vp, c_i32, c_vp, c_i32, c_i32, c_i64, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp],
     "o3s_assemble_src_size": [],
     "o3s_assemble_cols": [c_vp, c_i32, c_i32, c_i32, c_i64, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32,

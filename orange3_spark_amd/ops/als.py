@@ -10,6 +10,7 @@ import os
 import torch
 
 from . import _native as N
+from ..runtime.tracing import trace
 
 
 def pass_torch(mode, indptr, cols, coef, F, V):
@@ -204,11 +205,15 @@ class _EigCache:
         if (self.key is not None and self.key[0]() is F and self.key[1]() is G and self.key[2] == key
                 and (self.val[2] is not None or not need_fq)):
             return self.val
-        Gd = G.to(torch.float64)
+        # the rank x rank eigendecomposition runs on the host (LAPACK, fp64): 1.4 ms for
+        # R = 128 against 2.2 ms for torch.linalg.eigh on the GPU, whose first call in a
+        # process also pays ~125 ms of solver start-up (tools/probe_eigh.py,
+        # profiles/als_first_iteration_r4.json)
+        Gd = G.detach().to(device="cpu", dtype=torch.float64)
         ev, V = torch.linalg.eigh(0.5 * (Gd + Gd.T))
-        eig = ev.clamp_min(0.0).float().contiguous()
-        Q = V.float().contiguous()
-        FQ = torch.mm(F, Q) if need_fq else None
+        eig = ev.clamp_min(0.0).float().to(F.device).contiguous()
+        Q = V.float().to(F.device).contiguous()
+        FQ = rotated_table(F, Q) if need_fq else None
         self.key = (weakref.ref(F), weakref.ref(G), key)
         self.val = (eig, Q, FQ)
         return self.val
@@ -218,6 +223,28 @@ class _EigCache:
 
 
 EIG_CACHE = _EigCache()
+
+
+def rotated_table(F: torch.Tensor, Q: torch.Tensor) -> torch.Tensor:
+    """F Q for the Woodbury gathers.  On the GPU: the x = Q y rotation kernel (matrix cores at
+    rank 128) over every row of F with Q in the place of Q^T (row f -> Q^T f = (f Q)^T),
+    written to a new table -- no GEMM library call (hipBLASLt's first call in a process costs
+    ~160 ms of the first ALS iteration, profiles/als_first_iteration_r4.json); elsewhere
+    torch.mm."""
+    R = F.shape[1]
+    if not (F.is_cuda and F.dtype == torch.float32 and F.is_contiguous() and R in EXACT_RANKS
+            and F.shape[0] < (1 << 31)):
+        return torch.mm(F, Q)
+    FQ = torch.empty_like(F)
+    n = F.shape[0]
+    if n:
+        rows = torch.arange(n, dtype=torch.int32, device=F.device)
+        lib = N.kernels()
+        grid = max(1, min(N.num_cus(F.device) * 2, -(-n // 32)))
+        lib.o3s_als_rotate_mfma(int(ROTATE_MFMA))
+        N.check(lib.o3s_als_rotate_to(R, Q.contiguous().data_ptr(), rows.data_ptr(), n, F.data_ptr(),
+                                      FQ.data_ptr(), grid, N.stream_of(FQ)), "als_rotate(F Q)")
+    return FQ
 
 
 def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor, row_range=None) -> torch.Tensor:
@@ -257,25 +284,29 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
     st = N.stream_of(out)
     if ns:
         if implicit:
-            eig, Q, P = EIG_CACHE.get(F, G, True)
+            with trace("als.eig_rotated_table"):
+                eig, Q, P = EIG_CACHE.get(F, G, True)
         else:
             eig, Q, P = torch.zeros(R, dtype=torch.float32, device=dev), None, F
-        N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), P.data_ptr(),
-                                 eig.data_ptr(), lam.data_ptr(), small.data_ptr(), ns, out.data_ptr(), st),
-                "als_wood")
+        with trace("als.woodbury", rows=ns):
+            N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                     P.data_ptr(), eig.data_ptr(), lam.data_ptr(), small.data_ptr(), ns,
+                                     out.data_ptr(), st), "als_wood")
         if implicit:                          # x = Q y for the Woodbury rows (als_rotate_kernel)
-            QT = Q.T.contiguous()
-            grid = max(1, min(N.num_cus(dev) * 2, -(-ns // 32)))
-            lib.o3s_als_rotate_mfma(int(ROTATE_MFMA))
-            N.check(lib.o3s_als_rotate(R, QT.data_ptr(), small.data_ptr(), ns, out.data_ptr(), grid, st),
-                    "als_rotate")
+            with trace("als.rotate", rows=ns):
+                QT = Q.T.contiguous()
+                grid = max(1, min(N.num_cus(dev) * 2, -(-ns // 32)))
+                lib.o3s_als_rotate_mfma(int(ROTATE_MFMA))
+                N.check(lib.o3s_als_rotate(R, QT.data_ptr(), small.data_ptr(), ns, out.data_ptr(), grid, st),
+                        "als_rotate")
     if nd:
-        Gf = G.float().contiguous() if implicit else None
-        fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
-              "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(DENSE_KERNEL, lib.o3s_als_dense)
-        N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
-                   F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), nd, out.data_ptr(), st),
-                "als_dense")
+        with trace("als.dense", rows=nd):
+            Gf = G.float().contiguous() if implicit else None
+            fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
+                  "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(DENSE_KERNEL, lib.o3s_als_dense)
+            N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                       F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), nd, out.data_ptr(), st),
+                    "als_dense")
     return out
 
 

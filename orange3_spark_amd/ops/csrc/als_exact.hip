@@ -516,9 +516,10 @@ constexpr int kRotRows = 8;
 // agree bitwise).  Rows are rewritten in place: a tile's rows are all staged before any is
 // written.
 constexpr int kRotStride = 130;
+// Y: the source rows (Y == X: in place; the rotated table F Q reads F, writes FQ).
 __global__ __launch_bounds__(256, 2) void als_rotate_mfma_kernel(const float* __restrict__ QT,
                                                                  const int32_t* __restrict__ rows, int64_t nrows,
-                                                                 float* __restrict__ X) {
+                                                                 const float* Y, float* X) {
   __shared__ __attribute__((aligned(16))) float sY[32 * kRotStride];
   __shared__ int64_t sRid[32];                          // the tile's row ids (-1: past the list)
   const int lane = threadIdx.x & 63;
@@ -535,7 +536,7 @@ __global__ __launch_bounds__(256, 2) void als_rotate_mfma_kernel(const float* __
     rid = i < nrows ? (int64_t)rows[i] : -1;
     const int64_t rr = rid >= 0 ? rid : (int64_t)rows[nrows - 1];   // in bounds; never written
 #pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = *reinterpret_cast<const float4_*>(X + rr * 128 + lc + 4 * k);
+    for (int k = 0; k < 4; ++k) o[k] = *reinterpret_cast<const float4_*>(Y + rr * 128 + lc + 4 * k);
   };
   float4_ nx[4];
   int64_t nrid = -1;
@@ -570,7 +571,7 @@ __global__ __launch_bounds__(256, 2) void als_rotate_mfma_kernel(const float* __
 
 template <int R>
 __global__ __launch_bounds__(256) void als_rotate_kernel(const float* __restrict__ QT, const int32_t* __restrict__ rows,
-                                                         int64_t nrows, float* __restrict__ X) {
+                                                         int64_t nrows, const float* Y, float* X) {
   constexpr int RV = (R + 63) / 64;
   __shared__ float sQ[R * R];                       // sQ[j R + c] = Q[c][j]
   __shared__ float sYb[4][kRotRows][R];
@@ -588,7 +589,7 @@ __global__ __launch_bounds__(256) void als_rotate_kernel(const float* __restrict
 #pragma unroll
       for (int h = 0; h < RV; ++h) {
         const int c = lane + 64 * h;
-        if (c < R) sYb[wv][r][c] = rid[r] >= 0 ? X[rid[r] * R + c] : 0.f;
+        if (c < R) sYb[wv][r][c] = rid[r] >= 0 ? Y[rid[r] * R + c] : 0.f;
       }
     }
     if constexpr (RV == 2) {
@@ -626,6 +627,8 @@ __global__ __launch_bounds__(256) void als_rotate_kernel(const float* __restrict
     for (int r = 0; r < kRotRows; ++r)
 #pragma unroll
       for (int h = 0; h < RV; ++h) acc[r][h] = 0.f;
+    // (bounded unroll: the fully unrolled loop hoisted every LDS read and spilled at R = 64)
+#pragma unroll 2
     for (int j = 0; j < R; j += 4) {
       float q[4][RV];
 #pragma unroll
@@ -1305,26 +1308,32 @@ O3S_API int o3s_als_rotate_mfma(int on) {
   return 0;
 }
 
-O3S_API int o3s_als_rotate(int R, const float* QT, const int32_t* rows, int64_t nrows, float* X, int grid,
-                           hipStream_t st) {
-  if (nrows < 0 || !QT || grid <= 0) return -1;
+// x = Q y for the listed rows: read from Y, written to X (Y == X: in place).
+O3S_API int o3s_als_rotate_to(int R, const float* QT, const int32_t* rows, int64_t nrows, const float* Y,
+                              float* X, int grid, hipStream_t st) {
+  if (nrows < 0 || !QT || !Y || grid <= 0) return -1;
   if (nrows == 0) return 0;
   if (R == 128 && g_rotate_mfma) {
     const int64_t tiles = (nrows + 31) / 32;
     const int g = (int)(tiles < 4096 ? tiles : 4096);
-    hipLaunchKernelGGL(als_rotate_mfma_kernel, dim3(g), dim3(256), 0, st, QT, rows, nrows, X);
+    hipLaunchKernelGGL(als_rotate_mfma_kernel, dim3(g), dim3(256), 0, st, QT, rows, nrows, Y, X);
     O3S_CHECK_LAUNCH();
     return 0;
   }
 #define O3S_RT(RR)                                                                                       \
   if (R == RR) {                                                                                         \
-    hipLaunchKernelGGL((als_rotate_kernel<RR>), dim3(grid), dim3(256), 0, st, QT, rows, nrows, X);       \
+    hipLaunchKernelGGL((als_rotate_kernel<RR>), dim3(grid), dim3(256), 0, st, QT, rows, nrows, Y, X);    \
     O3S_CHECK_LAUNCH();                                                                                  \
     return 0;                                                                                            \
   }
   O3S_RT(32) O3S_RT(64) O3S_RT(96) O3S_RT(128)
 #undef O3S_RT
   return -2;
+}
+
+O3S_API int o3s_als_rotate(int R, const float* QT, const int32_t* rows, int64_t nrows, float* X, int grid,
+                           hipStream_t st) {
+  return o3s_als_rotate_to(R, QT, rows, nrows, X, X, grid, st);
 }
 
 // Dense solves (any row): register Gram + LDS Cholesky.  implicit: G = Y^T Y (fp32 R x R).

@@ -346,3 +346,35 @@ def test_gpu_ftf_kernel_matches_fp64(R, n):
     assert torch.equal(got, got.T)
     assert torch.equal(A.ftf(F), got)
     assert torch.allclose(AE.gram(F.contiguous()), ref, rtol=1e-6, atol=1e-6 * float(ref.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [32, 64, 96, 128])
+@pytest.mark.parametrize("n", [1, 33, 100_003])
+def test_gpu_rotated_table_matches_fp64(R, n):
+    """F Q for the Woodbury gathers comes from the in-place rotation kernel (Q passed where
+    the x = Q y path passes Q^T): equal to the fp64 product, F itself untouched."""
+    from orange3_spark_amd.ops import als as A
+    g = torch.Generator(device="cuda").manual_seed(R * 7 + n)
+    F = torch.randn((n, R), generator=g, device="cuda")
+    Q = torch.linalg.qr(torch.randn((R, R), generator=g, device="cuda", dtype=torch.float64))[0].float()
+    F0 = F.clone()
+    got = A.rotated_table(F, Q)
+    ref = F.double() @ Q.double()
+    assert torch.equal(F, F0)
+    assert float((got.double() - ref).abs().max()) < 2e-5 * float(ref.abs().max())
+
+
+def test_row_counts_equal_scatter_count():
+    """Per-row positive-rating counts from the prefix sum == the repeat_interleave +
+    index_add form, empty rows (leading, inner, trailing) included."""
+    g = torch.Generator().manual_seed(3)
+    lens = torch.randint(0, 6, (1000,), generator=g)
+    lens[0] = lens[500] = lens[-1] = 0
+    indptr = torch.zeros(1001, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(lens, 0)
+    pos = torch.rand(int(indptr[-1]), generator=g) > 0.3
+    rows = torch.repeat_interleave(torch.arange(1000), lens)
+    ref = torch.zeros(1000).index_add_(0, rows, pos.float())
+    assert torch.equal(AE._row_counts(indptr, pos), ref)
+    assert torch.equal(AE._row_counts(torch.zeros(4, dtype=torch.int64), pos[:0]), torch.zeros(3))

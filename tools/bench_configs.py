@@ -74,6 +74,9 @@ def run_als(s, a):
            "datagen_seconds_untimed": round(t_gen, 2), "max_mem_gb": _mem_gb(),
            "phases_s": ({k: round(v["total_s"], 4) for k, v in TRACER.summary().items()}
                         if TRACER.enabled else None)}
+    if TRACER.enabled:   # the fit's spans in order (iteration 1 vs the steady state)
+        out["events_ms"] = [[n, round(dt * 1e3, 2)] for n, _t, dt, _a, _tid in TRACER._events
+                            if n.startswith("als.") and not n.startswith("als.gather")][:400]
     return out
 
 
