@@ -58,34 +58,45 @@ def global_ids(comm, ids: torch.Tensor) -> torch.Tensor:
     """Sorted unique ids over all ranks (replicated).  Dense id ranges use a presence
     bitmap (one scatter, one max all-reduce of span bytes, one nonzero) instead of a sort of
     every id (1B ids: a 150 ms radix sort)."""
-    ids = ids.to(torch.int64)
+    if ids.dtype not in (torch.int32, torch.int64):
+        ids = ids.to(torch.int64)
     lo, hi = _id_range(comm, ids)
     span = hi - lo + 1
     if hi >= lo and span <= DENSE_ID_SPAN * max(1, ids.numel() * comm.world_size) and span <= (1 << 33):
         mark = torch.zeros(span, dtype=torch.uint8, device=ids.device)
-        mark[ids - lo] = 1
+        mark[_offsets(ids, lo, span)] = 1
         if comm.world_size > 1:
             comm.all_reduce(mark, "max")
         return torch.nonzero(mark).reshape(-1) + lo
-    u = torch.unique(ids)
+    u = torch.unique(ids.to(torch.int64))
     if comm.world_size > 1:
         u = torch.unique(comm.all_gather_v(u))
     return u
 
 
+def _offsets(ids: torch.Tensor, lo: int, span: int) -> torch.Tensor:
+    """ids - lo, in int32 when the ids are int32 and the span fits (no int64 copy of a
+    billion ids), else in int64."""
+    if ids.dtype == torch.int32 and span < (1 << 31) and lo >= -(1 << 31):
+        return ids - lo if lo == 0 or -(1 << 31) <= -lo < (1 << 31) else ids.to(torch.int64) - lo
+    return ids.to(torch.int64) - lo
+
+
 def dense_index(uid: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
-    """Position of every id in the sorted unique table ``uid`` (int64): a lookup table over
-    the id span when it is dense (one scatter + one gather), else a binary search."""
-    ids = ids.to(torch.int64)
+    """Position of every id in the sorted unique table ``uid``: a lookup table over the id
+    span when it is dense (one scatter + one gather; int32 positions when they fit), else a
+    binary search (int64)."""
+    if ids.dtype not in (torch.int32, torch.int64):
+        ids = ids.to(torch.int64)
     if uid.numel() == 0:
-        return torch.zeros_like(ids)
+        return torch.zeros(ids.shape, dtype=torch.int64, device=ids.device)
     lo, hi = int(uid[0]), int(uid[-1])
     span = hi - lo + 1
     if span <= DENSE_ID_SPAN * uid.numel() and span <= (1 << 33):
         lut = torch.empty(span, dtype=torch.int32 if uid.numel() < (1 << 31) else torch.int64, device=uid.device)
         lut[uid - lo] = torch.arange(uid.numel(), dtype=lut.dtype, device=uid.device)
-        return lut[ids - lo].to(torch.int64)
-    return torch.searchsorted(uid, ids)
+        return lut[_offsets(ids, lo, span)]
+    return torch.searchsorted(uid, ids.to(torch.int64))
 
 
 def block_bounds(n: int, world: int, r: int) -> tuple[int, int]:
@@ -98,6 +109,7 @@ def partition(comm, rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, 
     if W > 1:
         # the rank r with block_bounds(n_rows, W, r) containing the row:
         # floor(n r / W) <= x  <=>  r <= ceil((x + 1) W / n) - 1
+        rows = rows.to(torch.int64)
         owner = torch.div((rows + 1) * W + n_rows - 1, n_rows, rounding_mode="floor") - 1
         order = torch.argsort(owner, stable=True)
         counts = torch.bincount(owner, minlength=W).tolist()
@@ -106,13 +118,19 @@ def partition(comm, rows: torch.Tensor, cols: torch.Tensor, vals: torch.Tensor, 
         recv, _ = comm.all_to_all_v(packed, counts)
         rows, cols, vals = recv[:, 0].long(), recv[:, 1].long(), recv[:, 2].float()
     lo, hi = block_bounds(n_rows, W, r)
-    o = torch.argsort(rows, stable=True)
-    rows, cols, vals = rows[o], cols[o], vals[o]
-    cnt = torch.bincount(rows - lo, minlength=hi - lo) if rows.numel() else torch.zeros(hi - lo, dtype=torch.int64,
-                                                                                         device=rows.device)
+    # local row keys in 32 bits when they fit (half the radix passes of int64 keys); the
+    # sorted row ids themselves are never needed -- the counts come from the unsorted keys
+    key = rows - lo
+    if hi - lo < (1 << 31):
+        key = key.to(torch.int32)
+    o = torch.argsort(key, stable=True)
+    cols, vals = cols.to(torch.int32)[o], vals[o]
+    cnt = torch.bincount(key, minlength=hi - lo) if key.numel() else torch.zeros(hi - lo, dtype=torch.int64,
+                                                                                  device=rows.device)
+    del key, o
     indptr = torch.zeros(hi - lo + 1, dtype=torch.int64, device=rows.device)
     indptr[1:] = torch.cumsum(cnt, 0)
-    return Csr(indptr, cols.to(torch.int32).contiguous(), vals.contiguous(), lo, hi - lo)
+    return Csr(indptr, cols.contiguous(), vals.contiguous(), lo, hi - lo)
 
 
 def init_factors(n_lo: int, n: int, rank: int, seed: int, device, nonneg: bool) -> torch.Tensor:

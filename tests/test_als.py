@@ -378,3 +378,19 @@ def test_row_counts_equal_scatter_count():
     ref = torch.zeros(1000).index_add_(0, rows, pos.float())
     assert torch.equal(AE._row_counts(indptr, pos), ref)
     assert torch.equal(AE._row_counts(torch.zeros(4, dtype=torch.int64), pos[:0]), torch.zeros(3))
+
+
+@pytest.mark.parametrize("dt", [torch.int32, torch.int64])
+def test_id_maps_int32_and_int64(dt):
+    """Distinct ids and dense positions are the same for int32 and int64 id columns, on the
+    bitmap / lookup-table path (dense span, including the int32 minimum) and the sorted one."""
+    class _C:
+        world_size = 1
+    lo = -(1 << 31) if dt == torch.int32 else -(1 << 40)
+    for ids in (torch.tensor([3, 1, 2, 9, 1, 3, 5]), torch.tensor([5, -3, 7, 5, -3, 100]),
+                torch.tensor([lo + 5, lo, lo + 3, lo])):
+        ids = ids.to(dt)
+        uid = AE.global_ids(_C(), ids)
+        assert uid.tolist() == sorted(set(ids.tolist()))
+        pos = AE.dense_index(uid, ids)
+        assert uid[pos.long()].tolist() == ids.tolist()
