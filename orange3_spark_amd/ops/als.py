@@ -130,6 +130,9 @@ DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_gl")
 # x = Q y for the Woodbury rows on the matrix cores (R = 128: rank-of-8 iteration 0.0903 ->
 # 0.0881 s, profiles/als_rotate_mfma_r4.json; O3S_ALS_ROTATE_MFMA=0: the packed-FMA kernel)
 ROTATE_MFMA = os.environ.get("O3S_ALS_ROTATE_MFMA", "1") == "1"
+# Woodbury Cholesky in 8-column panels with the trailing updates on the matrix cores
+# (O3S_ALS_WOOD_BLK=0: every rank-1 update by v_readlane broadcasts)
+WOOD_BLK = os.environ.get("O3S_ALS_WOOD_BLK", "1") == "1"
 
 
 _FTF_WS: dict = {}
@@ -289,6 +292,7 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
         else:
             eig, Q, P = torch.zeros(R, dtype=torch.float32, device=dev), None, F
         with trace("als.woodbury", rows=ns):
+            lib.o3s_als_wood_blocked(int(WOOD_BLK))
             N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                                      P.data_ptr(), eig.data_ptr(), lam.data_ptr(), small.data_ptr(), ns,
                                      out.data_ptr(), st), "als_wood")

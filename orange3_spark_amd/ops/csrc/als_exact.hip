@@ -16,7 +16,8 @@
 //       S = W^{-1} + P D P^T   (n x n, SPD)
 //   so the only factorisation is an n x n Cholesky -- no 128-step pivot chain per row.
 //   One wave per row: P lives in registers (lane l holds columns l, l + 64 as float2 ->
-//   v_pk_fma), S in LDS (lane i owns row i), triangular solves broadcast with readlane.
+//   v_pk_fma), S in registers (lane i owns row i), the Cholesky in 8-column panels (readlane
+//   broadcasts inside a panel, the trailing rank-8 update on MFMA), solves by readlane.
 //   Per row: a gather of n factor rows and n^2 R / 2 FMA -- no rank x rank work at all
 //   (the rotation back, x = Q y, is one GEMM over all Woodbury rows on the host side).
 // * als_dense_kernel (longer rows: the item side, ~200 ratings): one block per row, thread
@@ -59,27 +60,61 @@ __device__ __forceinline__ float rl(float v, int lane) {
 // no-ops (rows and columns >= n of S are zero and t_i = 0 there: the clamped pivot gives
 // L_kk = 1e-15, every other L entry and y_k are 0), so NM steps run with no branches.
 // Returns z (lane i holds z_i).
-template <int NM>
+// BLK: 8-column panels -- inside a panel the v_readlane rank-1 updates above, then the
+// trailing columns take the panel's whole rank-8 update P = L21 L21^T from 4
+// v_mfma_f32_32x32x2_f32 (A = B = the panel's L entries, lane l holding row l & 31 and
+// k-slot l >> 5); P is symmetric, so the accumulator's column l & 31 is row l & 31 of P,
+// split between lanes l and l ^ 32 (one ds_bpermute exchange per register).  Per trailing
+// column: 2 VALU ops per panel instead of 16.  Lanes l >= 32 mirror rows l & 31 exactly
+// (the MFMA reads their L entries).
+template <int NM, bool BLK = false>
 __device__ __forceinline__ float wood_factor_solve(float (&srow)[kNW], float v, float (*Lc)[kNW + 1], int lane) {
+  const int r = lane & 31;
+  const int h = lane >> 5;
 #pragma unroll
-  for (int k = 0; k < NM; ++k) {
-    const float piv = fmaxf(rl(srow[k], k), 1e-30f);
-    const float id = __builtin_amdgcn_rsqf(piv);
-    const float lik = lane > k ? srow[k] * id : (lane == k ? piv * id : 0.f);
-    if (lane < kNW) Lc[k][lane] = lik;
-    const float yk = rl(v, k) * id;
-    v = lane == k ? yk : (lane > k ? fmaf(-lik, yk, v) : v);
+  for (int p = 0; p < NM / 8; ++p) {
 #pragma unroll
-    for (int m = k + 1; m < NM; ++m) srow[m] = fmaf(-lik, rl(lik, m), srow[m]);
+    for (int j = 0; j < 8; ++j) {
+      const int k = 8 * p + j;
+      const float piv = fmaxf(rl(srow[k], k), 1e-30f);
+      const float id = __builtin_amdgcn_rsqf(piv);
+      const float lik = r > k ? srow[k] * id : (r == k ? piv * id : 0.f);
+      if (lane < kNW) Lc[k][lane] = lik;
+      const float yk = rl(v, k) * id;
+      v = r == k ? yk : (r > k ? fmaf(-lik, yk, v) : v);
+#pragma unroll
+      for (int m = k + 1; m < (BLK ? 8 * p + 8 : NM); ++m) srow[m] = fmaf(-lik, rl(lik, m), srow[m]);
+    }
+    if constexpr (BLK) {
+      if (8 * p + 8 < NM) {
+        f32x16_ acc;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc[q] = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          const float a = Lc[8 * p + 2 * s2 + h][r];      // the panel's L, back from LDS
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, a, acc, 0, 0, 0);
+        }
+        // register q holds P[r][(q & 3) + 8 (q >> 2) + 4 h]; its partner lane the other half
+#pragma unroll
+        for (int q = 4 * (p + 1); q < 4 * (NM / 8); ++q) {
+          const float mine = acc[q];
+          const float other = __shfl_xor(mine, 32, 64);
+          const int m0 = (q & 3) + 8 * (q >> 2);
+          srow[m0] -= h ? other : mine;
+          srow[m0 + 4] -= h ? mine : other;
+        }
+      }
+    }
   }
   // backward, right-looking: z_k = v_k / L_kk, then v_i -= L_ki z_k for i < k (row k of L =
   // entries Lc[i][k]: lane i's column read, conflict-free at stride kNW + 1); the L entries
   // and the reciprocal diagonal are loaded up front, off the z chain
 #pragma unroll
   for (int k = NM - 1; k >= 0; --k) {
-    const float lki = Lc[lane & 31][k];
+    const float lki = Lc[r][k];
     const float zk = rl(v, k) * __builtin_amdgcn_rcpf(Lc[k][k]);
-    v = lane == k ? zk : (lane < k ? fmaf(-lki, zk, v) : v);
+    v = r == k ? zk : (r < k ? fmaf(-lki, zk, v) : v);
   }
   return v;
 }
@@ -91,7 +126,7 @@ __device__ __forceinline__ float wood_factor_solve(float (&srow)[kNW], float v, 
 // (a 4-waves-per-SIMD build spilled and measured 8.6% slower; S = P D P^T as bf16x3 on
 // 32x32x16 MFMAs measured 4% slower; persistent waves prefetching the next row's metadata
 // measured 14% slower: profiles/kernel_experiments_r4.json)
-template <int R, bool TIM = false, int WOCC = 3>
+template <int R, bool TIM = false, int WOCC = 3, bool BLK = false>
 __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ P, const float* __restrict__ eig,
@@ -199,10 +234,10 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   // carry no per-step branches
   float (*Lc)[kNW + 1] = S;                      // Lc[k][i] = L_ik
   float v = t;
-  if (n <= 8) v = wood_factor_solve<8>(srow, t, Lc, lane);
-  else if (n <= 16) v = wood_factor_solve<16>(srow, t, Lc, lane);
-  else if (n <= 24) v = wood_factor_solve<24>(srow, t, Lc, lane);
-  else v = wood_factor_solve<32>(srow, t, Lc, lane);
+  if (n <= 8) v = wood_factor_solve<8, BLK>(srow, t, Lc, lane);
+  else if (n <= 16) v = wood_factor_solve<16, BLK>(srow, t, Lc, lane);
+  else if (n <= 24) v = wood_factor_solve<24, BLK>(srow, t, Lc, lane);
+  else v = wood_factor_solve<32, BLK>(srow, t, Lc, lane);
   if constexpr (TIM) tm[3] = clock64();
   if constexpr (TIM) tm[4] = clock64();
   // y = D P^T z: the solution in the eigenbasis (implicit; the host rotates x = Q y for all
@@ -1281,6 +1316,14 @@ O3S_API int o3s_als_wood_timed(const int64_t* indptr, const int32_t* cols, const
   return 0;
 }
 
+namespace {
+int g_wood_blk = 1;         // o3s_als_wood_blocked: panel-blocked Woodbury Cholesky (MFMA trailing updates)
+}
+O3S_API int o3s_als_wood_blocked(int on) {
+  g_wood_blk = on ? 1 : 0;
+  return 0;
+}
+
 O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
                          const float* P, const float* eig, const float* lam, const int32_t* small, int64_t nsmall,
                          float* X, hipStream_t st) {
@@ -1289,8 +1332,12 @@ O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, cons
   const dim3 grid((unsigned)((nsmall + kWW - 1) / kWW));
 #define O3S_WD(RR)                                                                                          \
   if (R == RR) {                                                                                            \
-    hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, eig, lam, \
-                       small, nsmall, X, nullptr);                                                          \
+    if (g_wood_blk)                                                                                         \
+      hipLaunchKernelGGL((als_wood_kernel<RR, false, 3, true>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, \
+                         b, P, eig, lam, small, nsmall, X, nullptr);                                        \
+    else                                                                                                    \
+      hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P, eig,    \
+                         lam, small, nsmall, X, nullptr);                                                   \
     O3S_CHECK_LAUNCH();                                                                                     \
     return 0;                                                                                               \
   }
