@@ -79,6 +79,7 @@ _SIGS: dict[str, list] = {
     "o3s_confusion": [c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp],
     "o3s_score_hist": [c_vp, c_i32, c_i64, c_vp, c_i32, c_vp, c_i32, c_i64, c_f64, c_f64, c_i32, c_vp, c_vp],
     "o3s_als_wood_blocked": [c_i32],
+    "o3s_als_wood_kn": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "o3s_als_wood": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "o3s_als_wood_timed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp],
     "o3s_als_dense": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],

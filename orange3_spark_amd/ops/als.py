@@ -133,6 +133,9 @@ ROTATE_MFMA = os.environ.get("O3S_ALS_ROTATE_MFMA", "1") == "1"
 # Woodbury Cholesky in 8-column panels with the trailing updates on the matrix cores
 # (O3S_ALS_WOOD_BLK=0: every rank-1 update by v_readlane broadcasts)
 WOOD_BLK = os.environ.get("O3S_ALS_WOOD_BLK", "1") == "1"
+# rows with <= 16 ratings in their own Woodbury launch (16 x 16 S, half the P registers);
+# O3S_ALS_WOOD_SPLIT=0: one launch for every Woodbury row
+WOOD_SPLIT = os.environ.get("O3S_ALS_WOOD_SPLIT", "1") == "1"
 
 
 _FTF_WS: dict = {}
@@ -293,9 +296,17 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
             eig, Q, P = torch.zeros(R, dtype=torch.float32, device=dev), None, F
         with trace("als.woodbury", rows=ns):
             lib.o3s_als_wood_blocked(int(WOOD_BLK))
-            N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
-                                     P.data_ptr(), eig.data_ptr(), lam.data_ptr(), small.data_ptr(), ns,
-                                     out.data_ptr(), st), "als_wood")
+            if WOOD_SPLIT and WOOD_BLK:
+                short_m = cnt[small_m] <= 16
+                for kn, lst in ((16, small[short_m].contiguous()), (32, small[~short_m].contiguous())):
+                    if lst.numel():
+                        N.check(lib.o3s_als_wood_kn(R, kn, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
+                                                    b.data_ptr(), P.data_ptr(), eig.data_ptr(), lam.data_ptr(),
+                                                    lst.data_ptr(), lst.numel(), out.data_ptr(), st), "als_wood")
+            else:
+                N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                         P.data_ptr(), eig.data_ptr(), lam.data_ptr(), small.data_ptr(), ns,
+                                         out.data_ptr(), st), "als_wood")
         if implicit:                          # x = Q y for the Woodbury rows (als_rotate_kernel)
             with trace("als.rotate", rows=ns):
                 QT = Q.T.contiguous()

@@ -67,8 +67,8 @@ __device__ __forceinline__ float rl(float v, int lane) {
 // split between lanes l and l ^ 32 (one ds_bpermute exchange per register).  Per trailing
 // column: 2 VALU ops per panel instead of 16.  Lanes l >= 32 mirror rows l & 31 exactly
 // (the MFMA reads their L entries).
-template <int NM, bool BLK = false>
-__device__ __forceinline__ float wood_factor_solve(float (&srow)[kNW], float v, float (*Lc)[kNW + 1], int lane) {
+template <int NM, bool BLK = false, int KN = kNW>
+__device__ __forceinline__ float wood_factor_solve(float (&srow)[KN], float v, float (*Lc)[kNW + 1], int lane) {
   const int r = lane & 31;
   const int h = lane >> 5;
 #pragma unroll
@@ -126,7 +126,9 @@ __device__ __forceinline__ float wood_factor_solve(float (&srow)[kNW], float v, 
 // (a 4-waves-per-SIMD build spilled and measured 8.6% slower; S = P D P^T as bf16x3 on
 // 32x32x16 MFMAs measured 4% slower; persistent waves prefetching the next row's metadata
 // measured 14% slower: profiles/kernel_experiments_r4.json)
-template <int R, bool TIM = false, int WOCC = 3, bool BLK = false>
+// KN: the longest row of the launch (32, or 16 for the launch of the short rows: half the
+// P registers, and S on v_mfma_f32_16x16x4_f32 -- a quarter of the matrix-pipe cycles)
+template <int R, bool TIM = false, int WOCC = 3, bool BLK = false, int KN = kNW>
 __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ P, const float* __restrict__ eig,
@@ -138,7 +140,8 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   constexpr int RV = (R + 63) / 64;              // columns per lane (1 or 2)
   // per wave: the sqrt(D)-scaled rows P' for the MFMA (32 x kPS floats), later reused for
   // the S image and L by columns (Lc[k][i] = L_ik)
-  __shared__ __attribute__((aligned(16))) float sP[kWW][kNW * kPS];
+  // (KN = 16: 16 staged rows; the 32 x 33 S / L image, 1056 floats, still fits in 16 x kPS)
+  __shared__ __attribute__((aligned(16))) float sP[kWW][(KN == 16 ? 16 : kNW) * kPS];
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t li = (int64_t)blockIdx.x * kWW + wv;
@@ -168,12 +171,12 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   // broadcast by v_readlane, so the n row gathers issue back to back (a scalar load per
   // index would serialise n load latencies behind the per-row guards)
   const int myc = lane < n ? cols[p0 + lane] : 0;
-  int ci[kNW];                                   // all broadcasts before the first gather
+  int ci[KN];                                    // all broadcasts before the first gather
 #pragma unroll
-  for (int i = 0; i < kNW; ++i) ci[i] = __builtin_amdgcn_readlane(myc, i);
-  float2_ acc[kNW];
+  for (int i = 0; i < KN; ++i) ci[i] = __builtin_amdgcn_readlane(myc, i);
+  float2_ acc[KN];
 #pragma unroll
-  for (int i = 0; i < kNW; ++i) {
+  for (int i = 0; i < KN; ++i) {
     acc[i] = float2_{0.f, 0.f};
     if (i < n) {
       const int64_t c = ci[i];
@@ -193,13 +196,42 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   // accumulator chains.  Rows >= n are zero.
   const float2_ sq = {sqrtf(dd.x), sqrtf(dd.y)};
   float* sp = sP[wv];
+  const int wcol = lane < 32 ? lane : lane + 4;
+  float srow[KN];
+  if constexpr (KN == 16) {
+    // 16 x 16 S: lane l feeds row l & 15, k-slot g = l >> 4 = features 16 g + s of the half
+    // (s = 0..15); rows 16..31 of the image are never read (those lanes' srow is zero, so
+    // their L entries are exact zeros)
+    const int g = lane >> 4;
+    const float* rq = sp + (lane & 15) * kPS + 16 * g + (g >> 1) * 4;
+    float4_ sb0 = {0.f, 0.f, 0.f, 0.f}, sb1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int hf = 0; hf < RV; ++hf) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sp[i * kPS + wcol] = hf == 0 ? acc[i].x * sq.x : acc[i].y * sq.y;
+#pragma unroll
+      for (int s4 = 0; s4 < 16; s4 += 4) {
+        const float4_ x = *reinterpret_cast<const float4_*>(rq + s4);
+        sb0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x.x, x.x, sb0, 0, 0, 0);
+        sb1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x.y, x.y, sb1, 0, 0, 0);
+        sb0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x.z, x.z, sb0, 0, 0, 0);
+        sb1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x.w, x.w, sb1, 0, 0, 0);
+      }
+    }
+    const float4_ sc = sb0 + sb1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) S[4 * g + q][lane & 15] = sc[q];   // column lane & 15, row 4 g + q
+    if (lane < 16) S[lane][lane] += winv;
+    const bool rok = (lane & 31) < 16;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) srow[m] = rok ? S[lane & 31][m] : 0.f;
+  } else {
   f32x16_ sa0, sa1;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     sa0[r] = 0.f;
     sa1[r] = 0.f;
   }
-  const int wcol = lane < 32 ? lane : lane + 4;
   const float* rp = sp + (lane & 31) * kPS + (lane >> 5) * 36;
 #pragma unroll
   for (int hf = 0; hf < RV; ++hf) {
@@ -221,9 +253,9 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
 #pragma unroll
   for (int r = 0; r < 16; ++r) S[(r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)][lane & 31] = sacc[r];
   if (lane < kNW) S[lane][lane] += winv;         // W^{-1} on the diagonal, in the image
-  float srow[kNW];
 #pragma unroll
   for (int m = 0; m < kNW; ++m) srow[m] = S[lane & 31][m];
+  }
   if constexpr (TIM) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     tm[2] = clock64();
@@ -234,17 +266,19 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   // carry no per-step branches
   float (*Lc)[kNW + 1] = S;                      // Lc[k][i] = L_ik
   float v = t;
-  if (n <= 8) v = wood_factor_solve<8, BLK>(srow, t, Lc, lane);
-  else if (n <= 16) v = wood_factor_solve<16, BLK>(srow, t, Lc, lane);
-  else if (n <= 24) v = wood_factor_solve<24, BLK>(srow, t, Lc, lane);
-  else v = wood_factor_solve<32, BLK>(srow, t, Lc, lane);
+  if (n <= 8) v = wood_factor_solve<8, BLK, KN>(srow, t, Lc, lane);
+  else if (KN == 16 || n <= 16) v = wood_factor_solve<16, BLK, KN>(srow, t, Lc, lane);
+  else if constexpr (KN == 32) {
+    if (n <= 24) v = wood_factor_solve<24, BLK, KN>(srow, t, Lc, lane);
+    else v = wood_factor_solve<32, BLK, KN>(srow, t, Lc, lane);
+  }
   if constexpr (TIM) tm[3] = clock64();
   if constexpr (TIM) tm[4] = clock64();
   // y = D P^T z: the solution in the eigenbasis (implicit; the host rotates x = Q y for all
   // Woodbury rows) or x itself (explicit, Q = I)
   float2_ uu = {0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < kNW; ++i) {
+  for (int i = 0; i < KN; ++i) {
     if (i < n) {
       const float zi = rl(v, i);
       uu = __builtin_elementwise_fma(float2_{zi, zi}, acc[i], uu);
@@ -1322,6 +1356,30 @@ int g_wood_blk = 1;         // o3s_als_wood_blocked: panel-blocked Woodbury Chol
 O3S_API int o3s_als_wood_blocked(int on) {
   g_wood_blk = on ? 1 : 0;
   return 0;
+}
+
+// Woodbury rows of at most kn ratings (kn = 16: the short-row build, 16 x 16 S; 32: as
+// o3s_als_wood), panel-blocked Cholesky.
+O3S_API int o3s_als_wood_kn(int R, int kn, const int64_t* indptr, const int32_t* cols, const float* w,
+                            const float* b, const float* P, const float* eig, const float* lam, const int32_t* small,
+                            int64_t nsmall, float* X, hipStream_t st) {
+  if (nsmall < 0 || !eig || !P || (kn != 16 && kn != 32)) return -1;
+  if (nsmall == 0) return 0;
+  const dim3 grid((unsigned)((nsmall + kWW - 1) / kWW));
+#define O3S_WK(RR)                                                                                          \
+  if (R == RR) {                                                                                            \
+    if (kn == 16)                                                                                           \
+      hipLaunchKernelGGL((als_wood_kernel<RR, false, 3, true, 16>), grid, dim3(kWW * 64), 0, st, indptr,    \
+                         cols, w, b, P, eig, lam, small, nsmall, X, nullptr);                               \
+    else                                                                                                    \
+      hipLaunchKernelGGL((als_wood_kernel<RR, false, 3, true>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, \
+                         b, P, eig, lam, small, nsmall, X, nullptr);                                        \
+    O3S_CHECK_LAUNCH();                                                                                     \
+    return 0;                                                                                               \
+  }
+  O3S_WK(32) O3S_WK(64) O3S_WK(96) O3S_WK(128)
+#undef O3S_WK
+  return -2;
 }
 
 O3S_API int o3s_als_wood(int R, const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
