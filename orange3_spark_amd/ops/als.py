@@ -136,6 +136,8 @@ WOOD_BLK = os.environ.get("O3S_ALS_WOOD_BLK", "1") == "1"
 # rows with <= 16 ratings in their own Woodbury launch (16 x 16 S, half the P registers);
 # O3S_ALS_WOOD_SPLIT=0: one launch for every Woodbury row
 WOOD_SPLIT = os.environ.get("O3S_ALS_WOOD_SPLIT", "1") == "1"
+# ... and rows with 17..24 ratings in a 24-row launch (O3S_ALS_WOOD_SPLIT24=0: with the 32-row ones)
+WOOD_SPLIT24 = os.environ.get("O3S_ALS_WOOD_SPLIT24", "1") == "1"
 
 
 _FTF_WS: dict = {}
@@ -297,8 +299,12 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
         with trace("als.woodbury", rows=ns):
             lib.o3s_als_wood_blocked(int(WOOD_BLK))
             if WOOD_SPLIT and WOOD_BLK:
-                short_m = cnt[small_m] <= 16
-                for kn, lst in ((16, small[short_m].contiguous()), (32, small[~short_m].contiguous())):
+                cs = cnt[small_m]
+                if WOOD_SPLIT24:
+                    parts = ((16, cs <= 16), (24, (cs > 16) & (cs <= 24)), (32, cs > 24))
+                else:
+                    parts = ((16, cs <= 16), (32, cs > 16))
+                for kn, lst in ((kn, small[m].contiguous()) for kn, m in parts):
                     if lst.numel():
                         N.check(lib.o3s_als_wood_kn(R, kn, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
                                                     b.data_ptr(), P.data_ptr(), eig.data_ptr(), lam.data_ptr(),

@@ -236,7 +236,8 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
 #pragma unroll
   for (int hf = 0; hf < RV; ++hf) {
 #pragma unroll
-    for (int i = 0; i < kNW; ++i) sp[i * kPS + wcol] = hf == 0 ? acc[i].x * sq.x : acc[i].y * sq.y;
+    for (int i = 0; i < kNW; ++i)
+      sp[i * kPS + wcol] = i >= KN ? 0.f : (hf == 0 ? acc[i < KN ? i : 0].x * sq.x : acc[i < KN ? i : 0].y * sq.y);
 #pragma unroll
     for (int s4 = 0; s4 < 32; s4 += 4) {
       const float4_ v = *reinterpret_cast<const float4_*>(rp + s4);
@@ -254,7 +255,7 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   for (int r = 0; r < 16; ++r) S[(r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)][lane & 31] = sacc[r];
   if (lane < kNW) S[lane][lane] += winv;         // W^{-1} on the diagonal, in the image
 #pragma unroll
-  for (int m = 0; m < kNW; ++m) srow[m] = S[lane & 31][m];
+  for (int m = 0; m < KN; ++m) srow[m] = S[lane & 31][m];
   }
   if constexpr (TIM) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -268,7 +269,9 @@ __global__ __launch_bounds__(kWW * 64, WOCC) void als_wood_kernel(
   float v = t;
   if (n <= 8) v = wood_factor_solve<8, BLK, KN>(srow, t, Lc, lane);
   else if (KN == 16 || n <= 16) v = wood_factor_solve<16, BLK, KN>(srow, t, Lc, lane);
-  else if constexpr (KN == 32) {
+  else if constexpr (KN == 24) {
+    v = wood_factor_solve<24, BLK, KN>(srow, t, Lc, lane);
+  } else if constexpr (KN == 32) {
     if (n <= 24) v = wood_factor_solve<24, BLK, KN>(srow, t, Lc, lane);
     else v = wood_factor_solve<32, BLK, KN>(srow, t, Lc, lane);
   }
@@ -1363,13 +1366,16 @@ O3S_API int o3s_als_wood_blocked(int on) {
 O3S_API int o3s_als_wood_kn(int R, int kn, const int64_t* indptr, const int32_t* cols, const float* w,
                             const float* b, const float* P, const float* eig, const float* lam, const int32_t* small,
                             int64_t nsmall, float* X, hipStream_t st) {
-  if (nsmall < 0 || !eig || !P || (kn != 16 && kn != 32)) return -1;
+  if (nsmall < 0 || !eig || !P || (kn != 16 && kn != 24 && kn != 32)) return -1;
   if (nsmall == 0) return 0;
   const dim3 grid((unsigned)((nsmall + kWW - 1) / kWW));
 #define O3S_WK(RR)                                                                                          \
   if (R == RR) {                                                                                            \
     if (kn == 16)                                                                                           \
       hipLaunchKernelGGL((als_wood_kernel<RR, false, 3, true, 16>), grid, dim3(kWW * 64), 0, st, indptr,    \
+                         cols, w, b, P, eig, lam, small, nsmall, X, nullptr);                               \
+    else if (kn == 24)                                                                                      \
+      hipLaunchKernelGGL((als_wood_kernel<RR, false, 3, true, 24>), grid, dim3(kWW * 64), 0, st, indptr,    \
                          cols, w, b, P, eig, lam, small, nsmall, X, nullptr);                               \
     else                                                                                                    \
       hipLaunchKernelGGL((als_wood_kernel<RR, false, 3, true>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, \
