@@ -214,11 +214,35 @@ class RowBlocks:
 
 def _pinned_copy(src: torch.Tensor) -> torch.Tensor:
     """Device rows -> a pinned host matrix, in bounded chunks (no full-size staging)."""
-    out = torch.empty(tuple(src.shape), dtype=src.dtype, pin_memory=src.is_cuda)
-    step = max(1, (256 << 20) // max(1, src.shape[1] * src.element_size()))
-    for a in range(0, src.shape[0], step):
-        out[a:a + step].copy_(src[a:a + step])
+    return _pinned_cat([src], pin=src.is_cuda)
+
+
+def _pinned_cat(parts, pin: bool = True) -> torch.Tensor:
+    """Row-concatenation of device and/or host matrices into ONE pinned host matrix
+    (``torch.cat`` of pinned tensors returns pageable memory, which would halve the
+    streaming rate), copied in bounded chunks."""
+    parts = [p for p in parts if p is not None]
+    ld, dt = parts[0].shape[1], parts[0].dtype
+    n = sum(int(p.shape[0]) for p in parts)
+    out = torch.empty((n, ld), dtype=dt, pin_memory=pin and torch.cuda.is_available())
+    step = max(1, (256 << 20) // max(1, ld * parts[0].element_size()))
+    off = 0
+    for p in parts:
+        for a in range(0, p.shape[0], step):
+            b = min(p.shape[0], a + step)
+            out[off + a:off + b].copy_(p[a:b])
+        off += int(p.shape[0])
     return out
+
+
+def device_free_bytes(dev) -> int:
+    """Bytes a new device allocation can take now: free HBM plus the caching allocator's
+    reserved-but-unused blocks."""
+    dev = torch.device(dev)
+    if dev.type != "cuda":
+        return 1 << 62
+    free, _ = torch.cuda.mem_get_info(dev)
+    return int(free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev))
 
 
 def hbm_budget(session) -> int:
@@ -242,23 +266,39 @@ def spill_to_budget(df, budget: int | None = None, disk_only: bool = False) -> i
     vec.sort(key=lambda kc: -kc[1].nbytes())
     moved = 0
     left = 0 if disk_only else budget
-    for k, c in vec:
+    while vec:
+        k, c = vec.pop(0)
         row_bytes = c.ld * c.data.element_size()
         n = len(c)
         keep = min(n, max(0, left // max(row_bytes, 1)))
-        if isinstance(c, SpilledVectorColumn):
-            if keep >= c.resident_rows:
-                left -= c.resident_rows * row_bytes
-                continue
-            host = torch.cat([_pinned_copy(c.data[keep:]), c.host])
+        nres = c.resident_rows if isinstance(c, SpilledVectorColumn) else n
+        if keep >= nres:
+            left -= nres * row_bytes
+            continue
+        old_host = c.host if isinstance(c, SpilledVectorColumn) else None
+        size, dev = c.size, c.data.device
+        host = _pinned_cat([c.data[keep:], old_host])
+        moved += (nres - keep) * row_bytes
+        if keep * row_bytes + (64 << 20) <= device_free_bytes(dev):
             res = c.data[:keep].clone()
         else:
-            if keep >= n:
-                left -= n * row_bytes
-                continue
-            host = _pinned_copy(c.data[keep:])
-            res = c.data[:keep].clone()
-        moved += (n - keep) * row_bytes - (c.spilled_rows * row_bytes if isinstance(c, SpilledVectorColumn) else 0)
-        df._cols[k] = SpilledVectorColumn(res, host, c.size)
+            # the new resident prefix does not fit NEXT TO the old column (the auto budget
+            # counts the column's own bytes as available): stage the prefix through pinned
+            # host memory, drop the device column, then re-allocate what is actually free
+            # (less if another frame still shares the old buffer)
+            pre = _pinned_cat([c.data[:keep]])
+            df._cols[k] = SpilledVectorColumn(torch.empty((0, c.ld), dtype=c.data.dtype, device=dev), host, size)
+            del c
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            fit = max(0, (device_free_bytes(dev) - (64 << 20)) // max(row_bytes, 1))
+            k2 = min(keep, fit)
+            res = pre[:k2].to(dev)
+            if k2 < keep:
+                host = _pinned_cat([pre[k2:], host])
+            del pre
+            moved += (keep - k2) * row_bytes
+            keep = k2
+        df._cols[k] = SpilledVectorColumn(res, host, size)
         left -= keep * row_bytes
     return moved

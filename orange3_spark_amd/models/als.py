@@ -62,7 +62,10 @@ def global_ids(comm, ids: torch.Tensor) -> torch.Tensor:
         ids = ids.to(torch.int64)
     lo, hi = _id_range(comm, ids)
     span = hi - lo + 1
-    if hi >= lo and span <= DENSE_ID_SPAN * max(1, ids.numel() * comm.world_size) and span <= (1 << 33):
+    # the path choice picks the collective (max all-reduce vs all_gather_v), so it must be
+    # made from values every rank agrees on: the global id count, not a local estimate
+    n_total = comm.sum_scalar(int(ids.numel())) if comm.world_size > 1 else int(ids.numel())
+    if hi >= lo and span <= DENSE_ID_SPAN * max(1, n_total) and span <= (1 << 33):
         mark = torch.zeros(span, dtype=torch.uint8, device=ids.device)
         mark[_offsets(ids, lo, span)] = 1
         if comm.world_size > 1:

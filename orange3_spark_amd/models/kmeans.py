@@ -30,13 +30,28 @@ class KMeansResult:
     seconds: float = 0.0
 
 
-def _sum_sq(X: torch.Tensor) -> torch.Tensor:
-    """sum ||x||^2 over the rows (fp64 accumulation, bounded row chunks: no fp64 copy of X)."""
+def _sum_sq(X: torch.Tensor, m: torch.Tensor | None = None) -> torch.Tensor:
+    """sum ||x - m||^2 over the rows (fp64 accumulation, bounded row chunks: no fp64 copy
+    of X)."""
     s = torch.zeros((), dtype=torch.float64, device=X.device)
     step = max(1, (1 << 26) // max(1, X.shape[1]))
     for i in range(0, X.shape[0], step):
-        s += torch.linalg.vector_norm(X[i:i + step], 2, dtype=torch.float64) ** 2
+        blk = X[i:i + step]
+        if m is not None:
+            blk = blk.to(torch.float64) - m
+        s += torch.linalg.vector_norm(blk, 2, dtype=torch.float64) ** 2
     return s
+
+
+def _global_mean(comm, X: torch.Tensor) -> torch.Tensor:
+    """Mean row over all ranks (fp64, chunked sums)."""
+    buf = torch.zeros(X.shape[1] + 1, dtype=torch.float64, device=X.device)
+    step = max(1, (1 << 26) // max(1, X.shape[1]))
+    for i in range(0, X.shape[0], step):
+        buf[:-1] += X[i:i + step].sum(0, dtype=torch.float64)
+    buf[-1] = X.shape[0]
+    comm.all_reduce(buf)
+    return buf[:-1] / buf[-1].clamp_min(1.0)
 
 
 def _global_rows(comm, n_local, device):
@@ -294,10 +309,13 @@ def fit_kmeans(comm, X, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int
     sizes = None
     cost = float("nan")
     # unweighted: an iteration's cost comes from its cluster sums S_a and counts n_a,
-    #   sum_x ||x - c_a(x)||^2 = sum_x ||x||^2 - sum_a (2 c_a.S_a - n_a ||c_a||^2)
-    # (fp64), so the assign pass needs no per-row distance (the screen kernel then skips the
-    # exact-distance epilogue and half of its row reads)
-    sumsq = _sum_sq(X) if weights is None else None
+    #   sum_x ||x - c_a(x)||^2 = sum_x ||x'||^2 - sum_a (2 c'_a.S'_a - n_a ||c'_a||^2)
+    # (fp64, every point and centre taken relative to the global mean m: x' = x - m,
+    # S'_a = S_a - n_a m -- about the origin the identity cancels catastrophically for data
+    # far from 0), so the assign pass needs no per-row distance (the screen kernel then
+    # skips the exact-distance epilogue and half of its row reads)
+    mean = _global_mean(comm, X) if weights is None else None
+    sumsq = _sum_sq(X, mean) if weights is None else None
     for it in range(start + 1, max_iter + 1):
         with trace("kmeans.iter"):
             prep = K.prepare_centers(C.float()) if K.kernel_ok(X) else None
@@ -308,13 +326,14 @@ def fit_kmeans(comm, X, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int
             else:
                 sums, cnt = K.update_torch(X, a, k, weights)
             if weights is None:
-                Cd = C.to(sums.device, torch.float64)
-                local = sumsq - (2.0 * (Cd * sums).sum() - (cnt * (Cd * Cd).sum(1)).sum())
+                Cd = C.to(sums.device, torch.float64) - mean
+                Sd = sums.to(torch.float64) - cnt.to(torch.float64)[:, None] * mean
+                local = sumsq - (2.0 * (Cd * Sd).sum() - (cnt * (Cd * Cd).sum(1)).sum())
             else:
                 local = (d.to(torch.float64) * weights.to(torch.float64)).sum()
             buf = torch.cat([sums.reshape(-1), cnt, local.reshape(1)])
             comm.all_reduce(buf)
-            sums, cnt, cost = buf[: k * D].reshape(k, D), buf[k * D: k * D + k], float(buf[-1])
+            sums, cnt, cost = buf[: k * D].reshape(k, D), buf[k * D: k * D + k], max(0.0, float(buf[-1]))
             hist.append(cost)
             newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp_min(1e-300)[:, None], C)
             if cosine:
@@ -333,6 +352,7 @@ def fit_kmeans(comm, X, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int
     cnt = torch.bincount(a.long(), minlength=k)[:k].to(torch.float64)
     buf = torch.cat([cnt, d.to(torch.float64).sum().reshape(1)])
     comm.all_reduce(buf)
+    K.clear_presplit()                   # the split copy of X (as large as X) is not kept past the fit
     return KMeansResult(C.cpu(), float(buf[-1]), it, [int(x) for x in buf[:k].tolist()], hist, time.time() - t0)
 
 
@@ -340,6 +360,7 @@ def predict(X: torch.Tensor, C: torch.Tensor, cosine=False) -> torch.Tensor:
     if cosine:
         X = X / X.norm(dim=1, keepdim=True).clamp_min(1e-300)
     a, _ = K.assign(X.float() if X.is_cuda else X, C.to(X.device).float() if X.is_cuda else C.to(X.device))
+    K.clear_presplit()                   # one-shot transform: do not keep the split copy of X
     return a
 
 

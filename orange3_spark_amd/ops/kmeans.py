@@ -108,8 +108,19 @@ def presplit(X: torch.Tensor, xs: float):
     XN = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
     N.check(N.kernels().o3s_kmeans_presplit(X.data_ptr(), X.shape[0], X.stride(0), X.shape[1], Ct.c_float(xs),
                                             XP.data_ptr(), XN.data_ptr(), N.stream_of(X)), "kmeans_presplit")
-    _XSPLIT[:] = [weakref.ref(X), k, (XP, XN)]
+    # the split copy lives no longer than X itself (and fit_kmeans drops it when it ends)
+    _XSPLIT[:] = [weakref.ref(X, _drop_presplit), k, (XP, XN)]
     return XP, XN
+
+
+def _drop_presplit(ref) -> None:
+    if _XSPLIT[0] is ref:
+        _XSPLIT[:] = [None, None, None]
+
+
+def clear_presplit() -> None:
+    """Free the presplit copy of the last X (as large as X itself)."""
+    _XSPLIT[:] = [None, None, None]
 
 
 def screen_bound(P: "Prepared", xs: float, D: int) -> tuple[float, float]:

@@ -710,20 +710,34 @@ class ExecutorPool:
             return self._proxy(0, "Session", "obj", None, _SESSION_RECIPE)
         root = rec._replayed.root if isinstance(rec._replayed, _Shared) else rec
         got = root._replayed if not isinstance(root._replayed, _Shared) else None
-        if got is None or got[0] is not self:
-            found: list = []
-            if root.kind == "scatter":
-                pdf, schema = root.body
-                found.append(self.scatter_dataframe(pdf, schema))
-            else:
-                handles = [self._replay(r) for r in root.slots]
-                self._run([root.body] * self.n, [h._id for h in handles], "replay", root, found)
-                del handles
-            got = root._replayed = (self, found)
-        handles = got[1]
-        if rec.index >= len(handles):
+        # the cache holds executor ids only (no proxies): a replayed object that no live
+        # handle holds is released like any other, and an id is reused only while a live
+        # proxy of THIS pool still names it (an adopting handle takes over the id)
+        if got is not None and got[0]() is self and rec.index < len(got[1]):
+            live = self._live_proxy(got[1][rec.index])
+            if live is not None:
+                return live
+        found: list = []
+        if root.kind == "scatter":
+            pdf, schema = root.body
+            found.append(self.scatter_dataframe(pdf, schema))
+        else:
+            handles = [self._replay(r) for r in root.slots]
+            self._run([root.body] * self.n, [h._id for h in handles], "replay", root, found)
+            del handles
+        root._replayed = (weakref.ref(self), [h._id for h in found])
+        if rec.index >= len(found):
             raise ExecutorLost("lineage replay produced a different result shape")
-        return handles[rec.index]
+        return found[rec.index]
+
+    def _live_proxy(self, k):
+        """The live proxy naming executor object ``k`` of this pool, or None if it was
+        released (or is queued for release)."""
+        ref = self._proxies.get(k)
+        obj = ref() if ref is not None else None
+        if obj is None or k in self._garbage or getattr(obj, "_id", None) != k:
+            return None
+        return obj
 
     def replay_effects(self, effects) -> None:
         for rec in effects:

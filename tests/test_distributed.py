@@ -54,7 +54,8 @@ def _work(rank, world, port, out_dir):
     pdf = pd.DataFrame({"user": u, "item": i, "rating": r})
     als = ALS(rank=3, maxIter=3, seed=1).fit(s.createDataFrame(pdf))
     res["als_U"] = als._U.numpy()
-    from orange3_spark_amd.models.als import fit_als     # CG path: chunked slot-layout all-gathers at 2 ranks
+    from orange3_spark_amd.models.als import fit_als     # opt-in CG path (below the size gate: unchunked;
+    # the chunked slot-layout path is covered by tests/test_distributed_gates.py)
     t = torch.from_numpy(rows[lo:hi])
     cg = fit_als(s.comm, t[:, 0].long(), t[:, 1].long(), t[:, 2].float(), rank=4, max_iter=3, implicit=True,
                  alpha=2.0, exact=False, cg_iters=3)

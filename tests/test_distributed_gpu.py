@@ -48,13 +48,37 @@ def _work(rank, world, port, out_dir):
     pdf = pd.DataFrame({"user": rng.integers(0, 300, 5000), "item": rng.integers(0, 120, 5000),
                         "rating": rng.normal(size=5000)})
     res["als_U"] = ALS(rank=8, maxIter=3, seed=1).fit(s.createDataFrame(pdf))._U.cpu().numpy()
-    # CG path with chunked slot-layout all-gathers (async, overlapping the next chunk's solve)
+    # opt-in CG path (this shape is below the size gate: the unchunked all_gather_v path)
+    from orange3_spark_amd.models import als as ALSE
     from orange3_spark_amd.models.als import fit_als
     lo, hi = (5000 * rank) // world, (5000 * (rank + 1)) // world
     t = torch.tensor(pdf.to_numpy()[lo:hi], device=s.device)
     cg = fit_als(s.comm, t[:, 0].long(), t[:, 1].long(), t[:, 2].float(), rank=32, max_iter=3, implicit=True,
                  alpha=2.0, exact=False, cg_iters=3)
     res["als_cg"] = np.concatenate([cg.U.cpu().numpy().ravel(), cg.V.cpu().numpy().ravel()])
+    # the DEFAULT exact solver above the size gate (per-rank nnz * R^2 > 2^26): the chunked
+    # slot-layout path -- HIP Woodbury + dense kernels with row_range, writing in place into
+    # factor tables that the async all-gathers fill (counted, so the path provably ran)
+    calls = [0]
+    real = ALSE._gather_slots
+
+    def counted(*a, **k):
+        calls[0] += 1
+        return real(*a, **k)
+    ALSE._gather_slots = counted
+    g2 = np.random.default_rng(7)
+    nr = 240_000
+    uu = g2.integers(0, 20_000, nr)
+    ii = np.minimum((g2.pareto(1.2, nr) * 40).astype(np.int64), 2_999)
+    rr = g2.integers(1, 6, nr).astype(np.float32)
+    lo, hi = (nr * rank) // world, (nr * (rank + 1)) // world
+    dev = s.device
+    for implicit in (True, False):
+        ex = fit_als(s.comm, torch.from_numpy(uu[lo:hi]).to(dev), torch.from_numpy(ii[lo:hi]).to(dev),
+                     torch.from_numpy(rr[lo:hi]).to(dev), rank=32, max_iter=3, reg=0.05, implicit=implicit,
+                     alpha=2.0, seed=3)
+        res[f"als_exact_{int(implicit)}"] = (ex.U.cpu().numpy(), ex.V.cpu().numpy())
+    res["gather_calls"] = calls[0]
     if rank == 0:
         torch.save(res, os.path.join(out_dir, f"g{world}.pt"))
     if world > 1:
@@ -85,3 +109,9 @@ def test_gpu_world2_matches_world1(tmp_path):
     assert np.allclose(a["rf_imp"], b["rf_imp"], atol=1e-6)
     assert np.allclose(a["als_U"], b["als_U"], atol=1e-3)
     assert np.allclose(a["als_cg"], b["als_cg"], atol=1e-4)
+    assert a["gather_calls"] == 0 and b["gather_calls"] == 2 * (1 + 2 * 3)
+    for imp in (0, 1):
+        for x, y in zip(a[f"als_exact_{imp}"], b[f"als_exact_{imp}"]):
+            assert x.shape == y.shape
+            # fp32 kernels on the same factor rows; only YtY's fp64 partial sums differ by shard
+            assert np.abs(x - y).max() <= 1e-4 * max(1.0, np.abs(x).max()), (imp, float(np.abs(x - y).max()))

@@ -302,3 +302,27 @@ def test_lloyd_cost_from_cluster_sums_equals_direct_cost():
     resw = fit_kmeans(LocalComm("cpu"), X, 5, max_iter=1, tol=0.0, initial=C0, weights=w)
     dw = (torch.cdist(X.double(), C0).pow(2).min(1).values * w.double()).sum()
     assert abs(resw.history[0] - float(dw)) <= 1e-6 * float(dw)
+
+
+def test_lloyd_cost_far_from_origin_keeps_its_digits():
+    """Data offset by 1e6 with unit spread: the sums-based cost is taken about the global
+    mean, so the history keeps ~1e-9 relative accuracy instead of cancelling."""
+    from orange3_spark_amd.models.kmeans import fit_kmeans
+    from orange3_spark_amd.parallel.comm import LocalComm
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(4000, 8, generator=g, dtype=torch.float64).float() + 1e6
+    C0 = X[:6].double().clone()
+    res = fit_kmeans(LocalComm("cpu"), X, 6, max_iter=1, tol=0.0, initial=C0)
+    d = torch.cdist(X.double(), C0).pow(2).min(1).values.sum()
+    assert abs(res.history[0] - float(d)) <= 1e-8 * float(d)
+
+
+@pytest.mark.gpu
+def test_gpu_presplit_dropped_after_fit(gpu, monkeypatch):
+    """The presplit copy of X (as large as X) does not outlive the fit."""
+    from orange3_spark_amd.models.kmeans import fit_kmeans
+    from orange3_spark_amd.parallel.comm import LocalComm
+    monkeypatch.setattr(K, "PRESPLIT", True)
+    X = torch.randn(60_000, 64, device=gpu)
+    fit_kmeans(LocalComm(gpu), X, 64, max_iter=3, seed=1)
+    assert K._XSPLIT == [None, None, None]

@@ -132,6 +132,30 @@ def test_executor_loss_respawns_and_replays_lineage(tmp_path):
         s.stop()
 
 
+def test_replay_after_adopted_parent_is_dropped(tmp_path):
+    """Respawn, use h1 (adopted), drop h1, then use h2 = f(h1) built before the kill: the
+    replay must not reuse h1's released executor id, and the replay cache
+    must not keep un-adopted ancestors alive."""
+    import gc
+    s = _pool(tmp_path)
+    try:
+        h1 = s.range(0, 1000)
+        h2 = h1.filter(h1.id % 3 == 0)
+        want = h2.count()
+        _kill(s.pool, 0)
+        assert h1.count() == 1000                     # respawn + adopt h1
+        pool = s.pool
+        del h1
+        gc.collect()
+        assert h2.count() == want                     # replays h1's recipe afresh
+        assert h2.filter(h2.id > 500).count() == len([i for i in range(501, 1000) if i % 3 == 0])
+        gc.collect()
+        live = [k for k, r in pool._proxies.items() if r() is not None]
+        assert len(live) <= 3, live                   # session + h2 (+ a transient), no pinned ancestors
+    finally:
+        s.stop()
+
+
 def _wedge_straggler():
     from orange3_spark_amd.session import Session
     if Session.active().comm.rank == 1:

@@ -52,6 +52,23 @@ def test_persist_memory_and_disk_spills_beyond_budget():
     assert isinstance(c2, SpilledVectorColumn) and c2.resident_rows == 0
 
 
+def test_spill_when_prefix_does_not_fit_next_to_the_column(monkeypatch):
+    """The auto budget counts the column's own bytes as available, so the new resident
+    prefix may not fit beside the old column: the prefix is staged through
+    host memory and re-allocated after the old column is dropped; with less free memory
+    than the budget, the resident part shrinks to what fits instead of raising OOM."""
+    from orange3_spark_amd.frame import spill
+    free = iter([0, 500 * 7 * 8 + (64 << 20)])           # before / after dropping the column
+    monkeypatch.setattr(spill, "device_free_bytes", lambda dev: next(free))
+    s = _session(budget=1000 * 7 * 8)
+    df = _lr_frame(s).persist(StorageLevel.MEMORY_AND_DISK)
+    col = df.column_data("features")
+    assert isinstance(col, SpilledVectorColumn) and len(col) == 3000
+    assert col.resident_rows == 500 and col.spilled_rows == 2500
+    ref = _lr_frame(_session())
+    assert np.allclose(col.to_numpy(), ref.column_data("features").to_numpy())
+
+
 def test_host_streamer_covers_every_row_in_order():
     host = torch.arange(1000 * 4, dtype=torch.float32).reshape(1000, 4)
     st = HostStreamer(host, "cpu", chunk_bytes=4 * 4 * 96)
