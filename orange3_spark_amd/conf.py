@@ -57,6 +57,18 @@ DEFAULTS = OrderedDict([
 ])
 
 
+def env_key(name: str) -> str:
+    """Configuration key of an ``O3S_CONF_<key>`` environment variable: ``__`` separates
+    the key's parts (``.``).  A suffix written all in upper case (the shell convention,
+    ``O3S_CONF_SPARK__EXECUTOR__INSTANCES``) is lower-cased; any other suffix keeps its
+    case, so camelCase keys survive (``O3S_CONF_o3s__executor__commTimeout`` ->
+    ``o3s.executor.commTimeout``)."""
+    k = name[len("O3S_CONF_"):]
+    if k.upper() == k:
+        k = k.lower()
+    return k.replace("__", ".")
+
+
 class SessionConf:
     """Mutable string->string map with SparkConf's method names."""
 
@@ -66,7 +78,7 @@ class SessionConf:
             self._d.update(DEFAULTS)
             for k, v in os.environ.items():
                 if k.startswith("O3S_CONF_"):
-                    self._d[k[9:].lower().replace("__", ".")] = v
+                    self._d[env_key(k)] = v
         if _pairs:
             for k, v in _pairs:
                 self._d[str(k)] = str(v)

@@ -69,15 +69,31 @@ class Transformer(Params, ABC):
 class Estimator(Params, ABC):
     """Abstract: fits a Model to a DataFrame."""
 
-    def fit(self, dataset, params=None):
+    def fit(self, dataset, params=None, *, progress=None, cancelled=None):
+        """pyspark's ``fit(dataset, params=None)``, plus two optional keywords (SURVEY
+        §2.10 Q14): ``progress(percent)`` receives the fit's progress, non-decreasing
+        0..100 (per iteration for the linear models, KMeans and ALS, per tree level /
+        tree for the tree ensembles), and a ``cancelled()`` that returns True stops the
+        fit with ``runtime.progress.FitCancelled`` at the next iteration."""
+        from ..runtime import progress as P
+        if progress is not None or cancelled is not None:
+            with P.progress_scope(progress, cancelled):
+                model = self.fit(dataset, params)
+                P.report(1.0)
+            return model
         if params is None:
             params = {}
         if isinstance(params, (list, tuple)):
-            return [self.fit(dataset, p) for p in params]
+            out = []
+            for i, p in enumerate(params):
+                with P.sub_range(i / len(params), (i + 1) / len(params)):
+                    out.append(self.fit(dataset, p))
+            return out
         if not _is_param_map(params):
             raise TypeError(f"Params must be either a param map or a list/tuple of param maps, but got {type(params)}.")
         pool = _pool_of(dataset)
         if pool is not None:                  # driver of an executor pool: fit on every executor
+            P.report(0.0)
             return pool.apply(_exec_fit, self, dataset, params)
         import time
         from ..parallel.comm import COMM_STATS
@@ -219,7 +235,9 @@ class Pipeline(Estimator, MLWritable, MLReadable):
                     models.append(s)
                     df = s.transform(df)
                 else:
-                    m = s.fit(df)
+                    from ..runtime import progress as P
+                    with P.sub_range(i / (last_est + 1), (i + 1) / (last_est + 1)):
+                        m = s.fit(df)
                     models.append(m)
                     if i < last_est:
                         df = m.transform(df)

@@ -29,6 +29,7 @@ import torch
 from ..ops import als as A
 from ..ops import sampling
 from ..runtime.tracing import trace
+from ..runtime import progress
 
 
 @dataclass
@@ -380,6 +381,7 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
         Yf = torch.zeros((GATHER_CHUNKS * comm.world_size * Li, rank), dtype=Y.dtype, device=dev)
         _gather_slots(comm, Y, Yf, Li, None)
     for it in range(start, max_iter):
+        progress.iteration(it, max_iter)
         with trace("als.iter"):
             ti = time.time()
             if not chunked:

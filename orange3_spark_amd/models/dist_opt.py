@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from . import optim
+from ..runtime import progress
 
 LocalLoss = Callable[[torch.Tensor, int, int], torch.Tensor]
 
@@ -107,6 +108,7 @@ def gradient_descent(obj: Objective, x0: np.ndarray, max_iter: int, step: float,
     mask = None if obj.mask is None else torch.from_numpy(obj.mask).to(dev, dt)
     prev = None
     for it in range(1, max_iter + 1):
+        progress.iteration(it - 1, max_iter)
         parts = obj.parts
         if fraction < 1.0:
             rng = np.random.default_rng([seed, it])

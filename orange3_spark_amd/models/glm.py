@@ -31,6 +31,7 @@ from ..ops import glm as G
 from ..runtime.tracing import traced
 from ..synthetic import LineageVectorColumn
 from . import optim
+from ..runtime import progress
 
 log = logging.getLogger(__name__)
 
@@ -520,6 +521,7 @@ def fit_sgd(data: GlmData, loss: str, reg=0.0, alpha=0.0, fit_intercept=True, st
             sgd.apply_first_step(*first, W)
     converged = False
     while sgd.t < max_iter:
+        progress.iteration(sgd.t, max_iter)
         sgd.step()
         if (tol > 0 or ckpt is not None) and sgd.t % check_every == 0:
             h = sgd.loss_hist[max(0, sgd.t - 2):sgd.t].cpu().numpy()
@@ -592,6 +594,7 @@ def _sgd(obj: GlmObjective, x0, max_iter, step, frac, seed, tol) -> GlmResult:
     x = x0.copy()
     hist = []
     for t in range(1, max_iter + 1):
+        progress.iteration(t - 1, max_iter)
         obj.data.sample_state = (int(seed), float(frac), t)
         f, g = obj.smooth(x)
         hist.append(f)

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from ..ops.gram import rows_t_matmul
+from ..runtime import progress
 
 _DEFAULT_LINK = {"gaussian": "identity", "binomial": "logit", "poisson": "log", "gamma": "inverse"}
 _EPS = 1e-16
@@ -219,6 +220,7 @@ def fit_irls(comm, X: torch.Tensor, y: torch.Tensor, w: torch.Tensor | None, off
     it = 0
     cov = None
     for it in range(1, max_iter + 1):
+        progress.iteration(it - 1, max_iter)
         dmu = 1.0 / link.deriv(mu)                      # d mu / d eta
         z = eta - off + (y - mu) / dmu
         ww = w * dmu * dmu / family.variance(mu)

@@ -18,6 +18,7 @@ import torch
 from ..ops import kmeans as K
 from ..ops import sampling
 from ..runtime.tracing import trace
+from ..runtime import progress
 
 
 @dataclass
@@ -226,6 +227,7 @@ def _fit_kmeans_blocks(comm, B, k, max_iter, tol, seed, init, init_steps, initia
     ws = K.UpdateWorkspace(dev, Kp, D) if dev.type == "cuda" and D <= 256 else None
     hist, sizes, it = [], None, 0
     for it in range(1, max_iter + 1):
+        progress.iteration(it - 1, max_iter)
         with trace("kmeans.iter"):
             Cf = C.float()
             prep = K.prepare_centers(Cf) if dev.type == "cuda" else None
@@ -317,6 +319,7 @@ def fit_kmeans(comm, X, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int
     mean = _global_mean(comm, X) if weights is None else None
     sumsq = _sum_sq(X, mean) if weights is None else None
     for it in range(start + 1, max_iter + 1):
+        progress.iteration(it - 1, max_iter)
         with trace("kmeans.iter"):
             prep = K.prepare_centers(C.float()) if K.kernel_ok(X) else None
             a, d = K.assign(X, C.float(), prep, need_dist=weights is not None)

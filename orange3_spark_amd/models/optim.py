@@ -13,6 +13,8 @@ from typing import Callable
 
 import numpy as np
 
+from ..runtime import progress
+
 Fn = Callable[[np.ndarray], tuple[float, np.ndarray]]
 
 
@@ -99,6 +101,7 @@ def lbfgs(fg: Fn, x0: np.ndarray, max_iter: int = 100, tol: float = 1e-6, m: int
     S, Y = [], []
     res = OptimResult(x, f, 0, hist)
     for it in range(1, max_iter + 1):
+        progress.iteration(it - 1, max_iter)
         # two-loop recursion
         q = g.copy()
         alphas = []
@@ -171,6 +174,7 @@ def owlqn(fg: Fn, x0: np.ndarray, l1: np.ndarray, max_iter: int = 100, tol: floa
     S, Y = [], []
     res = OptimResult(x, F, 0, hist)
     for it in range(1, max_iter + 1):
+        progress.iteration(it - 1, max_iter)
         pg = pseudo_grad(x, g)
         q = pg.copy()
         alphas = []

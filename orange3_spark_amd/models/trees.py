@@ -27,6 +27,7 @@ from ..ops import _native as N
 from ..ops import sampling
 from ..ops import trees as T
 from ..runtime.tracing import trace
+from ..runtime import progress
 
 
 # ----------------------------------------------------------------------------- binning
@@ -293,7 +294,8 @@ class TreeBuilder:
         for a in range(0, len(ws), tb):
             self.ws, self.seeds = ws[a:a + tb], seeds[a:a + tb]
             try:
-                trees += self._grow(None, 1.0)
+                with progress.sub_range(a / len(ws), min(len(ws), a + tb) / len(ws)):
+                    trees += self._grow(None, 1.0)
             finally:
                 self.ws, self.seeds = ws, seeds
         return trees
@@ -350,6 +352,7 @@ class TreeBuilder:
         parent_H = None                                           # [P, F, B, S] fp64, global
         small_right = None                                        # [P] bool (host): right child smaller
         for depth in range(self.max_depth + 1):
+            progress.iteration(depth, self.max_depth + 1)
             k = len(seg_nid)
             if k == 0:
                 break
@@ -550,6 +553,7 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
     best_err, best_m = math.inf, 0
     target = yy.to(torch.float32)                            # tree 0 fits the (scaled) labels
     for m in range(max_iter):
+        progress.iteration(m, max_iter)
         sw = w
         if subsampling_rate < 1.0 and rows is not None:
             sub = subsample_weights(None, rows, subsampling_rate, seed + m, False)
@@ -558,7 +562,8 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
                          min_info_gain, feature_fraction, seed + m, bins_t=bins_t,
                          min_weight_fraction=min_weight_fraction, own_y=True)
         wt = 1.0 if m == 0 else step
-        tree, _ = tb.build(leaf_acc=Fm, leaf_scale=wt)          # Fm += wt * leaf value, per row
+        with progress.sub_range(m / max_iter, (m + 1) / max_iter):
+            tree, _ = tb.build(leaf_acc=Fm, leaf_scale=wt)      # Fm += wt * leaf value, per row
         tu = trace("gbt.update")
         tu.__enter__()
         trees.append(tree)

@@ -126,6 +126,9 @@ EXACT_RANKS = (32, 64, 96, 128)
 # the same kernel with register-staged gathers; "mfma" = column-by-column diagonals and
 # the f32 Gram (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144).
 # Rejected: rating indices prefetched one Gram step ahead of the gathers (0.127 vs 0.122 s)
+# "wave" (default): als_dense_wave_kernel (csrc/als_dense.hip) -- one wave per row, four
+# independent waves per CU, factor rows gathered by an LDS-DMA ring that streams across
+# rows, the rows listed longest first.
 DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_gl")
 # x = Q y for the Woodbury rows on the matrix cores (R = 128: rank-of-8 iteration 0.0903 ->
 # 0.0881 s, profiles/als_rotate_mfma_r4.json; O3S_ALS_ROTATE_MFMA=0: the packed-FMA kernel)
@@ -323,6 +326,16 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
     if nd:
         with trace("als.dense", rows=nd):
             Gf = G.float().contiguous() if implicit else None
+            if DENSE_KERNEL == "wave":
+                # longest rows first: the waves take rows round robin, so the long tail of
+                # popular items spreads over the whole chip instead of finishing last
+                order = torch.argsort(cnt[dense - a], descending=True)
+                rows_sorted = dense[order].contiguous()
+                N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
+                                               b.data_ptr(), F.data_ptr(), N.ptr(Gf), lam.data_ptr(),
+                                               rows_sorted.data_ptr(), nd, out.data_ptr(), N.num_cus(dev), st),
+                        "als_dense_wave")
+                return out
             fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
                   "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(DENSE_KERNEL, lib.o3s_als_dense)
             N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),

@@ -1,0 +1,435 @@
+// Dense exact ALS solves, ONE WAVE PER ROW: the long rows of an exact ALS half-iteration
+// (the item side of the ALS config: ~200 ratings per row at rank 128; every row with more
+// ratings than the Woodbury limit, or lam_u = 0).  Spark solves each row's normal equations
+// with a per-row Cholesky (reached through the Recommendation widget -> ALS.fit,
+// orangecontrib/spark/widgets/ml/spark_ml_recommendation.py:15); this is that solve:
+//
+//   A_u = G + sum_c w_c y_c y_c^T + lam_u I,   b_u = sum_c b_c y_c,   x_u = A_u^{-1} b_u
+//
+// Structure (replaces the one-row-per-4-wave-block kernel, whose serial diagonal phase and
+// two block barriers per panel parked 3 of 4 waves: MFMA busy 0.16):
+// * a 256-thread block = 4 INDEPENDENT waves, one per SIMD (launch bounds (256, 1): the
+//   whole 512-register file per wave); each wave walks its own rows (row gw + k * GW of the
+//   length-sorted list), no block barrier after the prologue;
+// * the factor rows of a row's ratings are gathered by LDS-DMA (global_load_lds_dwordx4,
+//   per-lane source = a factor row, lane-linear image) into a per-wave ring of DEPTH steps
+//   of 16 ratings, with w / b of the step DMA'd beside them; the ring is a continuous
+//   STREAM across rows, so the next row's first steps are in flight while this row
+//   factors.  Rating indices come through the scalar cache (s_load), so no ordinary
+//   vector load is ever consumed while a DMA is outstanding, and the consumer waits with a
+//   counted s_waitcnt vmcnt (the DMAs of later steps stay in flight);
+// * the system is held as the NL = NT (NT + 1) / 2 upper 32 x 32 tiles in MFMA accumulator
+//   layout (lane l: column l & 31, rows (v & 3) + 8 (v >> 2) + 4 (l >> 5) in register v):
+//   160 registers at rank 128;
+//   Gram   per 16 ratings, sqrt(w_c) y_c split into bf16 hi + lo, and per tile three
+//          v_mfma_f32_32x32x16_bf16 (hi.hi + lo.hi + hi.lo: ~2^-16 relative, the numerics
+//          of the previous kernel); A and B fragments are the same registers (lane = dim,
+//          8 k-slots = 8 ratings);
+//   per 32-wide panel p (A = U^T U, U_pp = L_pp^T):
+//     A  the diagonal tile is factored by this wave (lane i holds row i, column c's
+//        multipliers by v_readlane inside 4-column blocks, a float4 LDS broadcast for the
+//        deferred rank-4 update); lanes 32-63 run the same recurrence on the identity,
+//        giving X_p = L_pp^-1, and y_p = X_p r_p;
+//     B  U_pi = X_p S_pi on v_mfma_f32_32x32x2_f32, B operand = the tile's own registers;
+//        r_i -= U_pi^T y_p (a sum over the tile's registers + one lane swap);
+//     C  S_ji -= U_pj^T U_pi with BOTH operands straight from registers (register v of
+//        tile (p, j) is exactly the A fragment that pairs with register v of tile (p, i));
+//   backward U x = y: per p the products U_pi x_i are summed across lanes through one LDS
+//   transpose, x_p = X_p^T t with X_p parked in the diagonal tile's registers.
+// * implicit G: its upper tiles live in LDS once per block, in accumulator order (one
+//   ds_read_b128 per 4 registers).
+#include "common.h"
+
+using namespace o3s;
+
+namespace {
+
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef const int32_t __attribute__((address_space(4)))* sptr_i32;
+typedef const int64_t __attribute__((address_space(4)))* sptr_i64;
+typedef const float __attribute__((address_space(4)))* sptr_f32;
+
+template <int R>
+struct DW {
+  static constexpr int NT = R / 32;
+  static constexpr int NL = NT * (NT + 1) / 2;
+  static constexpr int CH = 16;                         // ratings per step (one k-block of 16)
+  static constexpr int LPR = R / 4;                     // lanes per factor row (16 B each)
+  static constexpr int LPS = R == 96 ? 32 : LPR;        // lane span of a row in one DMA
+  static constexpr int RS = R == 96 ? 128 : R;          // LDS row stride (floats)
+  static constexpr int RPI = 64 / LPS;                  // rows per DMA instruction
+  static constexpr int NI = CH / RPI;                   // row DMAs per step
+  static constexpr int NIS = NI + 1;                    // + the w / b DMA
+  static constexpr int DEPTH = R >= 96 ? 3 : (R == 64 ? 5 : 8);
+  static constexpr int SLOT = CH * RS;                  // floats per ring slot
+  static constexpr int TS = 32 * 33;                    // padded 32 x 32 scratch tile
+  static constexpr int WAVE = DEPTH * SLOT + DEPTH * 32 + TS + R;   // floats per wave
+  static constexpr int GL = NL * 1024;                  // implicit G, accumulator order
+};
+
+__device__ __forceinline__ float rl(float v, int lane) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
+}
+__device__ __forceinline__ constexpr int rowof(int v, int h) { return (v & 3) + 8 * (v >> 2) + 4 * h; }
+template <int NT>
+__device__ __forceinline__ constexpr int tix(int j, int i) { return j * NT - j * (j - 1) / 2 + (i - j); }
+
+// s_waitcnt vmcnt(n * NIS) for a wave-uniform n in [0, 7]: the DMAs of the n later steps
+// stay in flight (loads retire in order, so this is exactly "this step has landed")
+template <int NIS>
+__device__ __forceinline__ void wait_steps(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * NIS) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIS) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NIS) : "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NIS) : "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * NIS) : "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * NIS) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(7 * NIS) : "memory"); break;
+  }
+}
+
+// z = s * y for 8 ratings -> bf16 hi (RNE) and lo = bf16(z - hi), packed as MFMA fragments
+__device__ __forceinline__ void split8(const float (&z)[8], bf16x8_t& hi, bf16x8_t& lo) {
+  u32x4_t H, L;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const f32x2_t a = {z[2 * k], z[2 * k + 1]};
+    const unsigned hu = __builtin_bit_cast(unsigned, __builtin_convertvector(a, bf16x2_t));
+    const f32x2_t hf = {__builtin_bit_cast(float, hu << 16), __builtin_bit_cast(float, hu & 0xffff0000u)};
+    const unsigned lu = __builtin_bit_cast(unsigned, __builtin_convertvector(a - hf, bf16x2_t));
+    H[k] = hu;
+    L[k] = lu;
+  }
+  hi = __builtin_bit_cast(bf16x8_t, H);
+  lo = __builtin_bit_cast(bf16x8_t, L);
+}
+
+template <int R, bool IMPL>
+__global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
+    const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
+    const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nrows, float* __restrict__ X) {
+  using D = DW<R>;
+  constexpr int NT = D::NT, NL = D::NL, CH = D::CH, DEPTH = D::DEPTH, RS = D::RS, LPS = D::LPS,
+                RPI = D::RPI, NI = D::NI, SLOT = D::SLOT;
+  // ONE __shared__ array (a second object beside the DMA ring can make hipcc wait vmcnt(0)
+  // before ring reads)
+  __shared__ __attribute__((aligned(16))) float lds[4 * D::WAVE + (IMPL ? D::GL : 0)];
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // G first: its per-lane reads are one base register + immediate offsets (< 64 KB)
+  float* const sG = lds;                                  // [NL][4][64][4]
+  float* const wl = lds + (IMPL ? D::GL : 0) + wid * D::WAVE;
+  float* const ring = wl;                                 // [DEPTH][CH][RS]
+  float* const swb = wl + DEPTH * SLOT;                   // [DEPTH][w 16 | b 16]
+  float* const scr = swb + DEPTH * 32;                    // [32][33] scratch tile
+  float* const sr = scr + D::TS;                          // [R] rhs -> y -> x
+
+  if constexpr (IMPL) {
+    // G's upper tiles in accumulator order: lane l's registers 4k..4k+3 of tile t at
+    // sG[t][k][l][0..3] (no DMA is in flight yet: a plain __syncthreads is a bare barrier)
+    const int h = lane >> 5, q = lane & 31;
+    for (int t = wid; t < NL; t += 4) {
+      int tj = 0, tt = t;
+      while (tt >= NT - tj) { tt -= NT - tj; ++tj; }
+      const int ti = tj + tt;
+#pragma unroll
+      for (int v = 0; v < 16; ++v)
+        sG[t * 1024 + (v >> 2) * 256 + lane * 4 + (v & 3)] = G[(32 * tj + rowof(v, h)) * R + 32 * ti + q];
+    }
+    __syncthreads();
+  }
+
+  const int64_t GW = (int64_t)gridDim.x * 4;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + wid;
+  const sptr_i32 scol = (const sptr_i32)cols;
+  const sptr_i64 sptrs = (const sptr_i64)indptr;
+  const sptr_i32 srow = (const sptr_i32)rows;
+  const sptr_f32 slam = (const sptr_f32)lam;
+
+  // ---- producer: the stream of 16-rating steps over this wave's rows ----
+  int64_t p_idx = gw - GW, pj = 0, pe = 0;
+  int issued = 0, pslot = 0;
+  auto produce = [&]() {
+    while (pj >= pe) {
+      p_idx += GW;
+      if (p_idx >= nrows) return;
+      const int64_t u = srow[p_idx];
+      pj = sptrs[u];
+      pe = sptrs[u + 1];
+    }
+    const int64_t last = pe - 1;
+    int32_t c[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i)   // readfirstlane: keeps hipcc from turning the per-lane
+      c[i] = __builtin_amdgcn_readfirstlane(scol[pj + i < last ? pj + i : last]);   // select into a vector load
+    float* const dst = ring + pslot * SLOT;
+    const int rr = lane / LPS, lo = lane % LPS;
+#pragma unroll
+    for (int ins = 0; ins < NI; ++ins) {
+      int32_t ci = c[ins * RPI];
+#pragma unroll
+      for (int e = 1; e < RPI; ++e) ci = rr == e ? c[ins * RPI + e] : ci;
+      const float* src = F + (int64_t)ci * R + 4 * lo;
+      if constexpr (R == 96) {
+        if (lo < 24) __builtin_amdgcn_global_load_lds(src, dst + ins * RPI * RS, 16, 0, 0);
+      } else {
+        __builtin_amdgcn_global_load_lds(src, dst + ins * RPI * RS, 16, 0, 0);
+      }
+    }
+    if (lane < 32) {
+      const int64_t jj = pj + (lane & 15) < last ? pj + (lane & 15) : last;
+      __builtin_amdgcn_global_load_lds((lane < 16 ? w : b) + jj, swb + pslot * 32, 4, 0, 0);
+    }
+    pj += CH;
+    ++issued;
+    pslot = pslot + 1 == DEPTH ? 0 : pslot + 1;
+  };
+
+  for (int i = 0; i < DEPTH - 1; ++i) produce();
+  int consumed = 0, cslot = 0;
+
+  for (int64_t idx = gw; idx < nrows; idx += GW) {
+    const int64_t u = srow[idx];
+    const int64_t p0 = sptrs[u], p1 = sptrs[u + 1];
+    const float lu = slam[u];
+    // the lane's coordinates, laundered per row: lane-dependent constants of the solve
+    // (identity columns, diagonal masks, LDS addresses) are then recomputed in the row
+    // instead of being hoisted out of the loop into ~100 registers that spill
+    int q = lane & 31, h = lane >> 5;
+    asm volatile("" : "+v"(q), "+v"(h));
+    // the system starts as G + lam_u I (G from its LDS copy), the Gram accumulates on top
+    f32x16_t acc[NL];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int i = j; i < NT; ++i) {
+        const int t = tix<NT>(j, i);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float4_ g = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (IMPL) g = *reinterpret_cast<const float4_*>(sG + t * 1024 + k * 256 + lane * 4);
+          const float gv[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc[t][4 * k + e] = (i == j && rowof(4 * k + e, h) == q) ? gv[e] + lu : gv[e];
+        }
+      }
+    float rh[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) rh[j] = 0.f;
+
+    // ---- Gram ----
+    for (int64_t j0 = p0; j0 < p1; j0 += CH) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot being refilled is read out
+      produce();
+      wait_steps<D::NIS>(issued - 1 - consumed);
+      const float* sl = ring + cslot * SLOT;
+      const float* wb = swb + cslot * 32;
+      const int nv = (int)(p1 - j0 < CH ? p1 - j0 : CH);
+      const float4_ w0 = *reinterpret_cast<const float4_*>(wb + 8 * h);
+      const float4_ w1 = *reinterpret_cast<const float4_*>(wb + 8 * h + 4);
+      const float4_ b0 = *reinterpret_cast<const float4_*>(wb + 16 + 8 * h);
+      const float4_ b1 = *reinterpret_cast<const float4_*>(wb + 16 + 8 * h + 4);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      float sw[8], bb[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool ok = 8 * h + k < nv;
+        sw[k] = ok ? __builtin_sqrtf(fmaxf(wv[k], 0.f)) : 0.f;
+        bb[k] = ok ? bv[k] : 0.f;
+      }
+      bf16x8_t hi[NT], lo[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        float y[8], z[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y[k] = sl[(8 * h + k) * RS + 32 * j + q];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          rh[j] = fmaf(bb[k], y[k], rh[j]);
+          z[k] = sw[k] * y[k];
+        }
+        split8(z, hi[j], lo[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int i = j; i < NT; ++i) {
+          f32x16_t& a = acc[tix<NT>(j, i)];
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi[j], hi[i], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lo[j], hi[i], a, 0, 0, 0);
+          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi[j], lo[i], a, 0, 0, 0);
+        }
+      ++consumed;
+      cslot = cslot + 1 == DEPTH ? 0 : cslot + 1;
+    }
+
+    // ---- rhs ----
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float t = rh[j] + __shfl_xor(rh[j], 32, 64);
+      if (h == 0) sr[32 * j + q] = t;
+    }
+
+    // ---- blocked Cholesky A = U^T U, forward solve U^T y = rhs riding along ----
+#pragma unroll
+    for (int p = 0; p < NT; ++p) {
+      f32x16_t& dg = acc[tix<NT>(p, p)];
+#pragma unroll
+      for (int v = 0; v < 16; ++v) scr[rowof(v, h) * 33 + q] = dg[v];
+      // A: lanes 0-31 row q of the tile -> row q of L; lanes 32-63 column q of the
+      // identity -> column q of X_p = L_pp^-1 (the same right-looking FMA with the lane's
+      // own multiplier).  4-column blocks: v_readlane inside, one rank-4 update per later
+      // column from a float4 LDS broadcast.
+      float v[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) v[k] = h ? (k == q ? 1.f : 0.f) : scr[q * 33 + k];
+      float4_* const sC4 = reinterpret_cast<float4_*>(scr);
+#pragma unroll
+      for (int c0 = 0; c0 < 32; c0 += 4) {
+#pragma unroll
+        for (int c = c0; c < c0 + 4; ++c) {
+          const float piv = fmaxf(rl(v[c], c), 1e-30f);
+          const float t = v[c] * __builtin_amdgcn_rsqf(piv);
+          v[c] = t;
+#pragma unroll
+          for (int j = c + 1; j < c0 + 4; ++j) v[j] = fmaf(-t, rl(t, j), v[j]);
+        }
+        if (c0 + 4 < 32) {
+          sC4[lane] = float4_{v[c0], v[c0 + 1], v[c0 + 2], v[c0 + 3]};
+#pragma unroll
+          for (int j = c0 + 4; j < 32; ++j) {
+            const float4_ l4 = sC4[j];
+            v[j] = fmaf(-v[c0 + 3], l4.w, fmaf(-v[c0 + 2], l4.z, fmaf(-v[c0 + 1], l4.y, fmaf(-v[c0], l4.x, v[j]))));
+            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      if (h == 1) {
+#pragma unroll
+        for (int k = 0; k < 32; ++k) scr[k * 33 + q] = v[k];        // X_p[k][q]
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (h == 0) {
+        float yq = 0.f;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) yq = fmaf(scr[q * 33 + j], sr[32 * p + j], yq);
+        sr[32 * p + q] = yq;                                        // y_p = X_p r_p
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      float xa[16], yv[16];
+#pragma unroll
+      for (int vv = 0; vv < 16; ++vv) {
+        xa[vv] = scr[q * 33 + rowof(vv, h)];                        // X_p[q][r(v, h)]: A operand
+        yv[vv] = sr[32 * p + rowof(vv, h)];
+      }
+#pragma unroll
+      for (int vv = 0; vv < 16; ++vv) dg[vv] = scr[rowof(vv, h) * 33 + q];   // X_p, C layout
+      // B: U_pi = X_p S_pi; r_i -= U_pi^T y_p
+#pragma unroll
+      for (int i = p + 1; i < NT; ++i) {
+        f32x16_t& s = acc[tix<NT>(p, i)];
+        f32x16_t z;
+#pragma unroll
+        for (int vv = 0; vv < 16; ++vv) z[vv] = 0.f;
+#pragma unroll
+        for (int vv = 0; vv < 16; ++vv) z = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[vv], s[vv], z, 0, 0, 0);
+        s = z;
+        float part = 0.f;
+#pragma unroll
+        for (int vv = 0; vv < 16; ++vv) part = fmaf(z[vv], yv[vv], part);
+        part += __shfl_xor(part, 32, 64);
+        if (h == 0) sr[32 * i + q] -= part;
+      }
+      // C: S_ji -= U_pj^T U_pi, operands straight from the panel tiles' registers
+#pragma unroll
+      for (int j = p + 1; j < NT; ++j)
+#pragma unroll
+        for (int i = j; i < NT; ++i) {
+          const f32x16_t& uj = acc[tix<NT>(p, j)];
+          const f32x16_t& ui = acc[tix<NT>(p, i)];
+          f32x16_t& s = acc[tix<NT>(j, i)];
+#pragma unroll
+          for (int vv = 0; vv < 16; ++vv) s = __builtin_amdgcn_mfma_f32_32x32x2f32(-uj[vv], ui[vv], s, 0, 0, 0);
+        }
+    }
+
+    // ---- backward U x = y ----
+#pragma unroll
+    for (int p = NT - 1; p >= 0; --p) {
+      if (p < NT - 1) {
+        float prod[16];
+#pragma unroll
+        for (int vv = 0; vv < 16; ++vv) prod[vv] = 0.f;
+#pragma unroll
+        for (int i = p + 1; i < NT; ++i) {
+          const float xi = sr[32 * i + q];
+          const f32x16_t& ui = acc[tix<NT>(p, i)];
+#pragma unroll
+          for (int vv = 0; vv < 16; ++vv) prod[vv] = fmaf(ui[vv], xi, prod[vv]);
+        }
+#pragma unroll
+        for (int vv = 0; vv < 16; ++vv) scr[rowof(vv, h) * 33 + q] = prod[vv];
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) s += scr[q * 33 + k];
+        if (h == 0) sr[32 * p + q] -= s;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const f32x16_t& xp = acc[tix<NT>(p, p)];
+      float t = 0.f;
+#pragma unroll
+      for (int vv = 0; vv < 16; ++vv) t = fmaf(xp[vv], sr[32 * p + rowof(vv, h)], t);
+      t += __shfl_xor(t, 32, 64);
+      if (h == 0) sr[32 * p + q] = t;
+    }
+#pragma unroll
+    for (int c = 0; c < R; c += 64)
+      if (c + lane < R) X[u * R + c + lane] = sr[c + lane];
+  }
+  // every DMA this wave issued was waited for by the step that consumed it
+}
+
+template <int R>
+int launch(int implicit, const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
+           const float* F, const float* G, const float* lam, const int32_t* rows, int64_t nrows, float* X,
+           int grid, hipStream_t st) {
+  if (implicit)
+    hipLaunchKernelGGL((als_dense_wave_kernel<R, true>), dim3(grid), dim3(256), 0, st, indptr, cols, w, b, F, G, lam,
+                       rows, nrows, X);
+  else
+    hipLaunchKernelGGL((als_dense_wave_kernel<R, false>), dim3(grid), dim3(256), 0, st, indptr, cols, w, b, F, G,
+                       lam, rows, nrows, X);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+// Dense exact solves of the rows listed in ``rows`` (any length; the caller lists them
+// longest first for balance), one wave per row, ``grid`` blocks of 4 waves (persistent:
+// at most 4 blocks' worth of waves per CU are resident, 1 block per CU).  Same contract
+// as o3s_als_dense_mfma: x_u written into X[u]; implicit: G = Y^T Y (fp32 R x R).
+O3S_API int o3s_als_dense_wave(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
+                               const float* b, const float* F, const float* G, const float* lam, const int32_t* rows,
+                               int64_t nrows, float* X, int grid, hipStream_t st) {
+  if (nrows < 0 || (implicit && !G) || grid <= 0) return -1;
+  if (nrows == 0) return 0;
+  const int64_t need = (nrows + 3) / 4;
+  if (grid > need) grid = (int)need;
+  switch (R) {
+    case 32: return launch<32>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, st);
+    case 64: return launch<64>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, st);
+    case 96: return launch<96>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, st);
+    case 128: return launch<128>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, st);
+    default: return -2;
+  }
+}

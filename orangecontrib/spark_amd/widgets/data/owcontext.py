@@ -23,8 +23,12 @@ class OWSessionContext(SharedSession, Widget):
 
     def __init__(self, **kw):
         super().__init__(**kw)
+        # the reference's order (spark_context.py:31-32,49-58): defaults, then every key the
+        # configuration already holds (O3S_CONF_* environment keys), then saved values
         self.conf = SessionConf()
         params = OrderedDict(DEFAULTS)
+        for k, v in self.conf.getAll():
+            params[k] = v
         for k, v in self.saved_gui_params.items():
             params[k] = v
         self.gui_parameters = OrderedDict((k, GuiParam(label=k, default_value=str(v))) for k, v in params.items())

@@ -11,7 +11,6 @@ back; ``code.InteractiveConsole`` semantics of trash/OLDpyspark_script_console.p
 "Import a script from a file" / "Save selected script to a file"
 (pyspark_script_console.py:286-291,368-392,441-461); the Qt view adds the syntax
 highlighter and the auto-indenting editor (script_support.py, ref :39-132)."""
-import contextlib
 import io
 import os
 import traceback
@@ -145,7 +144,8 @@ class OWScript(SharedSession, Widget):
         ns = self._bind()
         buf = io.StringIO()
         self.error()
-        with contextlib.redirect_stdout(buf), contextlib.redirect_stderr(buf):
+        from ..script_support import capture_output
+        with capture_output(buf):          # this thread's prints only (the view runs it on a worker)
             try:
                 exec(compile(self.current_script(), "<script>", "exec"), ns)
             except Exception:  # noqa: BLE001

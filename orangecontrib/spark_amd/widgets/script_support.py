@@ -16,6 +16,7 @@ import contextlib
 import keyword
 import re
 import sys
+import threading
 
 INDENT = 4
 
@@ -123,7 +124,7 @@ class ScriptConsole(code.InteractiveConsole):
             self.history.append(line)
         self._hpos = len(self.history)
         out = _Writer(self.write)
-        with contextlib.redirect_stdout(out), contextlib.redirect_stderr(out):
+        with capture_output(out):
             try:
                 self.more = bool(super().push(line))
             except SystemExit:
@@ -165,6 +166,60 @@ class _Writer:
 
     def flush(self):
         pass
+
+
+class _PerThreadStream:
+    """Stand-in for ``sys.stdout`` / ``sys.stderr`` that sends a thread's writes to that
+    thread's capture target (if one is set) and everyone else's to the stream it wraps.
+    ``contextlib.redirect_stdout`` swaps the process-global stream, so a script running on
+    a widget's worker thread would capture (and hide) the prints of every other thread
+    for as long as it runs."""
+
+    def __init__(self, base):
+        self._base = base
+        self._local = threading.local()
+
+    def _target(self):
+        t = getattr(self._local, "target", None)
+        return self._base if t is None else t
+
+    def write(self, data):
+        return self._target().write(data)
+
+    def flush(self):
+        f = getattr(self._target(), "flush", None)
+        if f is not None:
+            f()
+
+    def __getattr__(self, name):             # encoding, fileno, isatty, ... of the real stream
+        return getattr(self._base, name)
+
+
+_STREAM_LOCK = threading.Lock()
+
+
+def _wrapped(name: str) -> "_PerThreadStream":
+    with _STREAM_LOCK:
+        cur = getattr(sys, name)
+        if not isinstance(cur, _PerThreadStream):
+            cur = _PerThreadStream(cur)
+            setattr(sys, name, cur)
+        return cur
+
+
+@contextlib.contextmanager
+def capture_output(target):
+    """Send what THIS thread prints (stdout and stderr) to ``target`` (anything with a
+    ``write``) for the duration; other threads' output is untouched."""
+    streams = [_wrapped("stdout"), _wrapped("stderr")]
+    prev = [getattr(st._local, "target", None) for st in streams]
+    for st in streams:
+        st._local.target = target
+    try:
+        yield target
+    finally:
+        for st, p in zip(streams, prev):
+            st._local.target = p
 
 
 def banner(session) -> str:

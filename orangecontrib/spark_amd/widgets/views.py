@@ -15,10 +15,14 @@ and this module wraps each one in a thin Qt shell:
   ``list_values``, a line edit otherwise -- rebuilt when the method combo changes;
 * the widget's action (``apply``/``commit``/``submit``/``create_context``/``execute``)
   runs from an Apply button, on a worker thread when Orange's ``ConcurrentWidgetMixin``
-  exists (reference quirk Q14: ``fit`` froze the GUI); outputs produced on the worker are
-  queued and sent from the GUI thread when the task finishes;
-* ``info``/``warning``/``error`` of the headless widget show up as the view's messages and
-  a ``table()`` (Evaluation) or the output DataFrame preview fills the main area.
+  exists (reference quirk Q14: ``fit`` froze the GUI), with the fit's progress
+  (runtime/progress.py) reported to the task's progress bar and Cancel honoured at the
+  next iteration; outputs AND messages produced on the worker are queued and delivered on
+  the GUI thread when the task finishes (Qt widgets are touched from the GUI thread only);
+* ``info``/``warning``/``error`` of the headless widget show up as the view's
+  ``information``/``warning``/``error`` messages (``OWBaseWidget.info`` is the StateInfo
+  summary, not a message method) and a ``table()`` (Evaluation) or the output DataFrame
+  preview fills the main area.
 
 Each ``ow*.py`` module calls :func:`export_views` at import time; with Orange absent that
 is a no-op, with Orange present it adds ``<Class>View`` next to the headless class with
@@ -41,23 +45,47 @@ def _ident(channel: str) -> str:
 
 
 class _Bridge:
-    """Stands in as the headless widget's signal manager: forwards ``send`` to the Qt
-    output, or queues it while the action runs off the GUI thread."""
+    """Stands in as the headless widget's signal manager: forwards ``send`` and the
+    ``info``/``warning``/``error`` messages to the Qt widget when called on the GUI thread,
+    and queues them (in order) while the action runs on a worker thread -- Qt widgets may
+    only be touched from the GUI thread; :meth:`flush` runs there when the task ends."""
 
     def __init__(self, view):
         self.view = view
         self.pending = []
+        self._lock = threading.Lock()
+
+    @staticmethod
+    def _on_gui_thread() -> bool:
+        return threading.current_thread() is threading.main_thread()
 
     def send(self, _src, channel, value):
-        if threading.current_thread() is threading.main_thread():
+        if self._on_gui_thread():
             self.view._emit(channel, value)
         else:
-            self.pending.append((channel, value))
+            with self._lock:
+                self.pending.append(("send", channel, value))
+
+    def message(self, level, text):
+        if self._on_gui_thread():
+            self.view._show_message(level, text)
+        else:
+            with self._lock:
+                self.pending.append(("message", level, text))
 
     def flush(self):
-        pending, self.pending = self.pending, []
-        for channel, value in pending:
-            self.view._emit(channel, value)
+        with self._lock:
+            pending, self.pending = self.pending, []
+        for kind, a, b in pending:
+            if kind == "send":
+                self.view._emit(a, b)
+            else:
+                self.view._show_message(a, b)
+
+
+# headless message level -> OWBaseWidget method (``OWBaseWidget.info`` is the widget's
+# StateInfo summary object, not a message method)
+_MESSAGE_METHOD = {"info": "information", "warning": "warning", "error": "error"}
 
 
 def _settings_of(core_cls):
@@ -135,11 +163,14 @@ def qt_view(core_cls, orange=None):
 
     def _message_forwarder(self, level):
         def fwd(text=None):
-            self.core.messages[level] = text
-            shown = getattr(self, level, None)
-            if callable(shown):
-                shown(text) if text else shown()
+            self.core.messages[level] = text          # headless state: any thread
+            self.bridge.message(level, text)          # the Qt message: GUI thread only
         return fwd
+
+    def _show_message(self, level, text):
+        shown = getattr(self, _MESSAGE_METHOD[level], None)
+        if callable(shown):
+            shown(text) if text else shown()
 
     def _emit(self, channel, value):
         getattr(self.Outputs, out_attr[channel]).send(value)
@@ -212,7 +243,17 @@ def qt_view(core_cls, orange=None):
             self._sync(k)
         fn = getattr(self.core, action)
         if Mixin is not None:
-            self.start(lambda _state: fn())
+            def task(state):
+                # the fit's per-iteration / per-tree progress goes to the task state (Orange
+                # delivers it to the GUI thread's progress bar); Cancel stops the fit at its
+                # next iteration (runtime/progress.py)
+                from orange3_spark_amd.runtime.progress import progress_scope, report
+                with progress_scope(getattr(state, "set_progress_value", None),
+                                    getattr(state, "is_interruption_requested", None)):
+                    out = fn()
+                    report(1.0)
+                    return out
+            self.start(task)
         else:
             fn()
             self.on_done(None)
@@ -226,6 +267,7 @@ def qt_view(core_cls, orange=None):
         self._show_result()
 
     def on_exception(self, ex):
+        self.bridge.flush()
         self.core.error(f"{type(ex).__name__}: {ex}")
 
     def _show_result(self):
@@ -256,7 +298,8 @@ def qt_view(core_cls, orange=None):
         name=core_cls.name, description=core_cls.description, icon=core_cls.icon, priority=core_cls.priority,
         want_main_area=bool(core_cls.want_main_area or has_table),
         resizing_enabled=core_cls.resizing_enabled, Inputs=Inputs, Outputs=Outputs, core_class=core_cls,
-        __init__=__init__, _message_forwarder=_message_forwarder, _emit=_emit, _build_controls=_build_controls,
+        __init__=__init__, _message_forwarder=_message_forwarder, _show_message=_show_message, _emit=_emit,
+        _build_controls=_build_controls,
         _sync=_sync, _refresh_editors=_refresh_editors, _param_changed=_param_changed, run_action=run_action,
         on_done=on_done, on_exception=on_exception, _show_result=_show_result, onDeleteWidget=onDeleteWidget,
         __module__=core_cls.__module__, __qualname__=core_cls.__name__ + "View"))

@@ -274,7 +274,7 @@ def test_gpu_exact_kernels_pad_other_ranks(R, implicit):
 @pytest.mark.gpu
 @pytest.mark.parametrize("R", [32, 64, 96, 128])
 @pytest.mark.parametrize("implicit", [False, True])
-@pytest.mark.parametrize("kernel", ["mfma", "mfma_blk", "mfma_gl", "vgpr"])
+@pytest.mark.parametrize("kernel", ["wave", "mfma", "mfma_blk", "mfma_gl", "vgpr"])
 def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
     """Both dense exact kernels (als_dense_mfma_kernel: 32 x 32 MFMA accumulator tiles;
     als_dense_kernel: 8 x 8 register tiles) == the fp64 solve on rows routed to the dense
@@ -290,17 +290,71 @@ def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
     got = torch.full((n, R), float("nan"), device=F.device)
     from orange3_spark_amd.ops import _native as N
     lib = N.kernels()
-    fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
-          "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(kernel, lib.o3s_als_dense)
     Gf = G.float().contiguous() if implicit else None
-    N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), F.data_ptr(),
-               N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), 40, got.data_ptr(), N.stream_of(got)), "als_dense")
+    if kernel == "wave":
+        N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
+                                       b.data_ptr(), F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), 40,
+                                       got.data_ptr(), 256, N.stream_of(got)), "als_dense_wave")
+    else:
+        fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
+              "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(kernel, lib.o3s_als_dense)
+        N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), F.data_ptr(),
+                   N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), 40, got.data_ptr(), N.stream_of(got)), "als_dense")
     ref = torch.empty((n, R), dtype=torch.float64, device=F.device)
     A.exact_solve_torch(indptr, cols, w, b, F, G, lam, ref)
     got, ref = got[:40], ref[:40]
     assert not torch.isnan(got).any()
     err = (got.double() - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-6)
     assert float(err.max()) < 2e-3, float(err.max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [32, 64, 96, 128])
+@pytest.mark.parametrize("implicit", [False, True])
+@pytest.mark.parametrize("grid", [1, 3, 256])
+def test_gpu_dense_wave_streams_many_rows_per_wave(R, implicit, grid):
+    """als_dense_wave_kernel with several rows per wave (grid 1 and 3 blocks: 4 / 12 waves
+    walk 600 rows each way; 256: one or two): the LDS-DMA ring streams ACROSS rows (the
+    next row's steps land while this row factors), rows of 0, 1, 15, 16, 17, 33 and up to
+    ~2000 ratings, every row == the fp64 solve, bitwise the same for every grid."""
+    from orange3_spark_amd.ops import _native as N
+    from orange3_spark_amd.ops import als as A
+    g = torch.Generator().manual_seed(R + 7 * implicit)
+    n_rows, n_other = 600, 5000
+    lens = torch.randint(33, 120, (n_rows,), generator=g)
+    lens[:8] = torch.tensor([0, 1, 15, 16, 17, 33, 2000, 517])
+    indptr = torch.zeros(n_rows + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(lens, 0)
+    nnz = int(indptr[-1])
+    cols = torch.randint(0, n_other, (nnz,), generator=g, dtype=torch.int32)
+    vals = torch.randn(nnz, generator=g) * 2
+    if implicit:
+        vals[::13] = 0.0
+    F = torch.randn((n_other, R), generator=g) / R ** 0.5
+    w, b, pos = AE._weights(vals, implicit, 2.0)
+    rows = torch.repeat_interleave(torch.arange(n_rows), lens)
+    nu = torch.zeros(n_rows).index_add_(0, rows, pos.float())
+    lam = (0.05 * nu.clamp_min(1.0)).float()
+    G = (F.double().T @ F.double()).float() if implicit else None
+    dev = "cuda"
+    indptr, cols, w, b, F, lam = (x.to(dev) for x in (indptr, cols, w, b, F, lam))
+    Gf = G.to(dev).contiguous() if implicit else None
+    order = torch.argsort(lens, descending=True).to(torch.int32).to(dev)
+    lib = N.kernels()
+    got = torch.full((n_rows, R), float("nan"), device=dev)
+    N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                   F.data_ptr(), N.ptr(Gf), lam.data_ptr(), order.data_ptr(), n_rows, got.data_ptr(),
+                                   grid, N.stream_of(got)), "als_dense_wave")
+    ref = torch.empty((n_rows, R), dtype=torch.float64, device=dev)
+    A.exact_solve_torch(indptr, cols, w, b, F, None if G is None else G.to(dev), lam, ref)
+    assert not torch.isnan(got).any()
+    err = (got.double() - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-6)
+    assert float(err.max()) < 2e-3, float(err.max())
+    again = torch.full_like(got, float("nan"))
+    N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                   F.data_ptr(), N.ptr(Gf), lam.data_ptr(), order.data_ptr(), n_rows,
+                                   again.data_ptr(), 2, N.stream_of(got)), "als_dense_wave")
+    assert torch.equal(got, again)
 
 
 def test_blockwise_topk_recommendations_match_brute_force():

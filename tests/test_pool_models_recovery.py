@@ -224,7 +224,10 @@ def test_context_widget_lists_devices_and_reports_respawn(tmp_path):
     SharedSession._session = None
     Session._active = None
     ctx = OWSessionContext()
-    assert ctx.gui_parameters["spark.executor.instances"].get_value() == "auto"
+    from orange3_spark_amd.conf import DEFAULTS, SessionConf
+    assert DEFAULTS["spark.executor.instances"] == "auto"
+    # the editor shows the configured value (tests/conftest.py sets O3S_CONF_SPARK__EXECUTOR__INSTANCES)
+    assert ctx.gui_parameters["spark.executor.instances"].get_value() == SessionConf().get("spark.executor.instances")
     ctx.set_param("o3s.device", "cpu").set_param("spark.sql.warehouse.dir", str(tmp_path / "wh"))
     ctx.set_param("spark.executor.instances", "2")
     s = ctx.create_context()

@@ -156,3 +156,41 @@ def test_fit_stats_attached():
     st = m.fitStats
     assert st["seconds"] > 0 and st["rows_local"] == 500 and st["rows_per_s_local"] > 0
     assert isinstance(st["collectives"], dict)
+
+
+def test_fit_progress_per_iteration_and_cancellation():
+    """Estimator.fit(progress=, cancelled=): per-iteration progress for KMeans
+    / ALS / GBT, non-decreasing to 100, nested Pipeline stages mapped onto sub-ranges, and a
+    cancel request stops the fit at the next iteration."""
+    import numpy as np
+    import pandas as pd
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.ml.base import Pipeline
+    from orange3_spark_amd.ml.classification import GBTClassifier
+    from orange3_spark_amd.ml.clustering import KMeans
+    from orange3_spark_amd.ml.recommendation import ALS
+    from orange3_spark_amd.runtime.progress import FitCancelled
+    s = Session(SessionConf().set("o3s.device", "cpu"))
+    blobs = s.synthetic.blobs(2000, 4, k=3, seed=1)
+    seen = []
+    KMeans(k=3, maxIter=8, tol=0.0, seed=1).fit(blobs, progress=seen.append)
+    assert seen[0] == 0.0 and seen[-1] == 100.0 and all(b >= a for a, b in zip(seen, seen[1:])) and len(seen) >= 3
+    assert all(v % 12.5 == 0 for v in seen)            # per Lloyd iteration of 8 (converged early)
+    rng = np.random.default_rng(0)
+    r = s.createDataFrame(pd.DataFrame({"user": rng.integers(0, 40, 500), "item": rng.integers(0, 30, 500),
+                                        "rating": rng.normal(size=500)}))
+    als = []
+    ALS(rank=4, maxIter=5, seed=1).fit(r, progress=als.append)
+    assert als == [0.0, 20.0, 40.0, 60.0, 80.0, 100.0]
+    pipe = []
+    Pipeline(stages=[KMeans(k=3, maxIter=4, tol=0.0, seed=1, predictionCol="c"),
+                     KMeans(k=2, maxIter=4, tol=0.0, seed=1)]).fit(blobs, progress=pipe.append)
+    assert pipe[-1] == 100.0 and all(b >= a for a, b in zip(pipe, pipe[1:]))
+    assert any(0 < v < 50 for v in pipe) and any(50 <= v < 100 for v in pipe)
+    calls = []
+
+    def stop():
+        calls.append(1)
+        return len(calls) > 2
+    with pytest.raises(FitCancelled):
+        GBTClassifier(maxIter=10, maxDepth=3).fit(s.synthetic.trees(1000, 5, seed=2), cancelled=stop)

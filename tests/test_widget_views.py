@@ -3,6 +3,7 @@ widget API (Orange3/Qt are not installed here): signal forwarding, settings sync
 reflective parameter editors, action + output bridging, main-area table."""
 import importlib
 import pkgutil
+import threading
 from types import SimpleNamespace
 
 import pandas as pd
@@ -15,6 +16,12 @@ from orangecontrib.spark_amd.widgets.base import SharedSession
 from orangecontrib.spark_amd.widgets.views import export_views, qt_view
 
 
+def _gui_thread_only(what):
+    """The fake Qt objects refuse to be touched off the GUI (main) thread, as Qt requires."""
+    if threading.current_thread() is not threading.main_thread():
+        raise AssertionError(f"{what} called from worker thread {threading.current_thread().name}")
+
+
 class _Sig:
     def __init__(self, name, typ, multiple=False):
         self.name, self.type, self.multiple = name, typ, multiple
@@ -25,6 +32,7 @@ class _Sig:
         return fn
 
     def send(self, value):
+        _gui_thread_only("Output.send")
         self.sent.append(value)
 
 
@@ -65,6 +73,7 @@ class _QW:
         self.ph = t
 
     def setHtml(self, h):
+        _gui_thread_only("setHtml")
         self.html = h
 
     def deleteLater(self):
@@ -166,26 +175,75 @@ class _QButton(_QW):
         self.clicked = _Signal()
 
 
+class _StateInfo:
+    """``OWBaseWidget.info`` in current Orange: the widget's input/output summary object,
+    NOT a message method (the messages are ``information`` / ``warning`` / ``error``)."""
+
+    def set_input_summary(self, *a, **k):
+        pass
+
+    def set_output_summary(self, *a, **k):
+        pass
+
+
 class _OWWidget:
     def __init__(self, *a, **kw):
         self.controlArea, self.mainArea = _QW(), _QW()
         self.Outputs = type(self).Outputs
         self.shown = {}
+        self.info = _StateInfo()
         for cls in type(self).__mro__:           # Setting -> instance default (Orange's SettingProvider)
             for k, v in vars(cls).items():
                 if isinstance(v, _Setting) and k not in self.__dict__:
                     setattr(self, k, v.default)
 
     def error(self, text=None):
+        _gui_thread_only("error")
         self.shown["error"] = text
 
-    def info(self, text=None):
+    def information(self, text=None):
+        _gui_thread_only("information")
         self.shown["info"] = text
 
     def warning(self, text=None):
+        _gui_thread_only("warning")
         self.shown["warning"] = text
 
     def onDeleteWidget(self):
+        pass
+
+
+class _Concurrent:
+    """Orange's ConcurrentWidgetMixin: ``start(task, *args)`` runs ``task(*args, state)`` on a
+    worker thread; progress set on the state is recorded (Orange forwards it to the GUI
+    thread's progress bar); ``on_done`` / ``on_exception`` run on the GUI thread."""
+
+    def __init__(self):
+        self.progress = []
+        self.progress_threads = set()
+
+    def start(self, task, *args):
+        state = SimpleNamespace(set_progress_value=self._progress, is_interruption_requested=lambda: False)
+        box = {}
+
+        def run():
+            try:
+                box["result"] = task(*args, state)
+            except BaseException as e:  # noqa: BLE001 - handed to on_exception like Orange
+                box["exc"] = e
+        t = threading.Thread(target=run, name="task-worker")
+        t.start()
+        t.join()
+        if "exc" in box:
+            self.on_exception(box["exc"])
+        else:
+            self.on_done(box["result"])
+
+    def _progress(self, p):
+        self.progress.append(p)
+        self.progress_threads.add(threading.current_thread().name)
+
+    def shutdown(self):
         pass
 
 
@@ -266,6 +324,13 @@ def orange():
                                               QFileDialog=_FileDialog,
                                               QAbstractItemView=SimpleNamespace(ExtendedSelection=3)),
                            concurrent=None)
+
+
+@pytest.fixture()
+def orange_mt(orange):
+    """The same stand-ins with Orange's ConcurrentWidgetMixin: actions on a worker thread."""
+    orange.concurrent = _Concurrent
+    return orange
 
 
 @pytest.fixture(scope="module")
@@ -486,3 +551,67 @@ def test_tutorial_names_are_the_classes_orange_registers(orange):
         views = {v.__qualname__: v for v in export_views(g, orange)}
         assert cls in views, qn
         assert resolve(qn) is views[cls].core_class
+
+
+def test_concurrent_fit_reports_progress_and_touches_qt_only_on_gui_thread(orange_mt, session):
+    """Q14 intent (reference spark_ml_estimator.py:19-25 froze the GUI): the Apply action
+    runs the fit on a worker thread, the 20-iteration LR fit's progress rises
+    monotonically to 100 on the task state, and every Qt mutation (outputs, messages,
+    the main-area table) happens on the GUI thread -- the fakes raise otherwise."""
+    from orangecontrib.spark_amd.widgets.ml.owclassification import OWClassification
+    V = qt_view(OWClassification, orange_mt)
+    w = V()
+    df = session.createDataFrame(pd.DataFrame({"features": [[0.0, 1.0], [1.0, 0.3], [0.2, 0.9], [0.8, 0.1]] * 50,
+                                               "label": [1.0, 0.0, 1.0, 0.0] * 50}))
+    w._param_changed("method", "LogisticRegression")
+    w.set_dataframe(df)
+    w._param_changed("maxIter", "20")
+    w._param_changed("tol", "0.0")
+    w.run_action()
+    model = V.Outputs.model.sent[-1]
+    assert type(model).__name__ == "LogisticRegressionModel"
+    p = w.progress
+    assert len(p) >= 10 and p[-1] == 100.0 and all(b >= a for a, b in zip(p, p[1:])), p
+    assert w.progress_threads == {"task-worker"}
+    w.core.info("done on the worker")                    # GUI-thread call: shown at once
+    assert w.shown["info"] == "done on the worker"
+
+
+def test_worker_messages_are_queued_to_the_gui_thread(orange_mt, session):
+    """A message raised by the action on the worker (the Context widget's device list, an
+    estimator's warning) is delivered by the GUI thread when the task ends, through
+    ``information`` (``info`` is the StateInfo summary in current Orange)."""
+    from orangecontrib.spark_amd.widgets.data.owcontext import OWSessionContext
+    V = qt_view(OWSessionContext, orange_mt)
+    w = V()
+    w.core.set_param("o3s.device", "cpu")
+    w.run_action()
+    try:
+        assert "device" in (w.shown.get("info") or "") and isinstance(w.info, _StateInfo)
+    finally:
+        w.core.onDeleteWidget()
+        SharedSession._session = session
+
+
+def test_script_on_worker_captures_only_its_own_prints(orange_mt, session, capsys):
+    """The Script widget's commit runs on the worker: its prints go to the console, a
+    print from another thread while it runs does NOT (no process-global redirect)."""
+    from orangecontrib.spark_amd.widgets.data.owscript import OWScript
+    V = qt_view(OWScript, orange_mt)
+    w = V()
+    sc = w.script_controls
+    w._refresh_editors()
+    other = threading.Event()
+
+    def bystander():
+        print("bystander line")
+        other.set()
+    import orangecontrib.spark_amd.widgets.data.owscript as mod
+    mod._test_hook = bystander
+    sc["editor"].type("import threading, orangecontrib.spark_amd.widgets.data.owscript as m\n"
+                      "t = threading.Thread(target=m._test_hook); t.start(); t.join()\n"
+                      "print('from the script')\nout_object = 5")
+    w.run_action()
+    assert V.Outputs.out_object.sent[-1] == 5 and other.is_set()
+    assert "from the script" in sc["console"].text and "bystander line" not in sc["console"].text
+    assert "bystander line" in capsys.readouterr().out

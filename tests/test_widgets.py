@@ -238,3 +238,27 @@ def test_tutorial_has_reference_layout_and_annotations():
     assert len(list(tree.iter("arrow"))) == 7
     wf = Workflow.load(path)                       # positions / annotations round-trip
     assert wf.nodes["3"].position == (341.0, 247.0) and len(wf.annotations) == 13
+
+
+def test_context_widget_keeps_environment_keys(monkeypatch, warehouse):
+    """Context widget (reference spark_context.py:31-32,52-58): keys the configuration
+    already holds (O3S_CONF_* environment) appear in the editor and reach the session;
+    camelCase keys keep their case."""
+    from orange3_spark_amd.conf import SessionConf, env_key
+    from orangecontrib.spark_amd.widgets.data import owcontext
+    monkeypatch.setenv("O3S_CONF_o3s__executor__commTimeout", "7")
+    monkeypatch.setenv("O3S_CONF_O3S__SEED", "123")
+    assert env_key("O3S_CONF_o3s__executor__commTimeout") == "o3s.executor.commTimeout"
+    assert env_key("O3S_CONF_SPARK__EXECUTOR__INSTANCES") == "spark.executor.instances"
+    assert SessionConf().get("o3s.executor.commTimeout") == "7"
+    ctx = owcontext.OWSessionContext()
+    assert ctx.gui_parameters["o3s.executor.commTimeout"].get_value() == "7"
+    assert ctx.gui_parameters["o3s.seed"].get_value() == "123"
+    ctx.set_param("o3s.device", "cpu").set_param("spark.sql.warehouse.dir", warehouse)
+    s = ctx.create_context()
+    try:
+        assert s.conf.get("o3s.executor.commTimeout") == "7"
+        assert s.conf.get("o3s.seed") == "123"
+        assert ctx.saved_gui_params["o3s.executor.commTimeout"] == "7"
+    finally:
+        ctx.onDeleteWidget()
