@@ -18,6 +18,12 @@ DRAM behind PCIe.  Design:
 * :func:`spill_to_budget` -- ``DataFrame.persist(MEMORY_AND_DISK)``: moves the rows of
   device vector columns beyond the HBM budget (``o3s.storage.hbmBudget`` bytes, default
   the session's ``o3s.memory.fraction`` of free HBM) to pinned host memory.
+* out-of-core ingest (:func:`host_resident`): a table read from parquet / the catalog /
+  pandas / Arrow whose numeric columns exceed the budget keeps them in pinned host memory
+  from the start (nothing is materialised on the device); ``VectorAssembler`` streams
+  them through the assemble kernel in row chunks straight into a SpilledVectorColumn
+  (:func:`assemble_streamed`), whose resident prefix fills the budget; GLM / KMeans / tree
+  fits consume it chunk by chunk (tree binning writes resident uint8 bins per chunk).
 """
 from __future__ import annotations
 
@@ -245,6 +251,35 @@ def device_free_bytes(dev) -> int:
     return int(free + torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev))
 
 
+def ingest_budget(session) -> int | None:
+    """Device bytes the numeric columns of a NEW table may take (out-of-core ingest:
+    read.parquet / catalog tables / createDataFrame): ``o3s.storage.hbmBudget`` when set,
+    else on the GPU the session's ``o3s.memory.fraction`` of the allocatable HBM; None on
+    the CPU with no explicit budget (no limit)."""
+    v = session.conf.get("o3s.storage.hbmBudget", None)
+    if v not in (None, "", "auto"):
+        return int(float(v))
+    if session.device.type != "cuda":
+        return None
+    return int(device_free_bytes(session.device) * session.conf.memory_fraction())
+
+
+def host_resident(session, nbytes: int) -> bool:
+    """True when a new table of ``nbytes`` numeric bytes must stay in pinned host memory
+    (its columns are then streamed to the device by the consumers: VectorAssembler into a
+    SpilledVectorColumn, labels moved on use)."""
+    b = ingest_budget(session)
+    return b is not None and nbytes > b and session.device.type == "cuda"
+
+
+def pinned(t: torch.Tensor) -> torch.Tensor:
+    """A pinned host copy (plain host tensor when no GPU is present)."""
+    t = t.detach()
+    if t.device.type != "cpu":
+        t = t.cpu()
+    return t.pin_memory() if torch.cuda.is_available() else t.contiguous()
+
+
 def hbm_budget(session) -> int:
     v = session.conf.get("o3s.storage.hbmBudget", None)
     if v not in (None, "", "auto"):
@@ -302,3 +337,99 @@ def spill_to_budget(df, budget: int | None = None, disk_only: bool = False) -> i
         df._cols[k] = SpilledVectorColumn(res, host, size)
         left -= keep * row_bytes
     return moved
+
+
+def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes: int | None = None):
+    """VectorAssembler over host-resident (and/or device) columns, in row chunks.
+
+    ``sources``: list of (tensor [n] or [n, w], valid [n] | None, width) -- host tensors
+    are pinned.  Each chunk's inputs are copied to the device on a side stream (chunk c+1
+    is in flight while chunk c is assembled), assembled by the bf16 gather kernel (GPU) or
+    torch (CPU), and placed either in the resident prefix (rows below the budget) or copied
+    back into the pinned host block.  Returns (SpilledVectorColumn | VectorColumn, invalid
+    count)."""
+    from ..ml.feature import _as_matrix
+    from ..ops import assemble as A
+    from ..ops.glm import padded_width
+    dev = session.device
+    vdt = session.vector_dtype()
+    D = sum(int(w) for _, _, w in sources)
+    ld = padded_width(D) if vdt == torch.bfloat16 else D
+    esz = torch.empty((), dtype=vdt).element_size()
+    keep = n if budget is None else max(0, min(n, budget // max(1, ld * esz)))
+    in_row = sum(t.element_size() * (1 if t.dim() == 1 else t.shape[1]) for t, _, _ in sources) or 1
+    rows = max(1024, int(chunk_bytes or CHUNK_BYTES) // in_row)
+    res = torch.empty((keep, ld), dtype=vdt, device=dev)
+    host = torch.empty((n - keep, ld), dtype=vdt, pin_memory=dev.type == "cuda" and torch.cuda.is_available())
+    nbad = 0
+    cuda = dev.type == "cuda"
+    copy = torch.cuda.Stream(dev) if cuda else None
+    main = torch.cuda.current_stream(dev) if cuda else None
+
+    def stage(a, b):
+        out = []
+        ctx = torch.cuda.stream(copy) if cuda else _nullctx()
+        with ctx:
+            for t, valid, w in sources:
+                tt = t[a:b]
+                vv = None if valid is None else valid[a:b]
+                if cuda:
+                    tt = tt.to(dev, non_blocking=True)
+                    vv = None if vv is None else vv.to(dev, non_blocking=True)
+                out.append((tt, vv, w))
+        ev = None
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record(copy)
+        return out, ev
+
+    bounds = [(a, min(n, a + rows)) for a in range(0, n, rows)]
+    nxt = stage(*bounds[0]) if bounds else None
+    for i, (a, b) in enumerate(bounds):
+        cur, ev = nxt
+        if i + 1 < len(bounds):
+            if cuda:
+                copy.wait_stream(main)          # staging buffers of chunk i-1 are done with
+            nxt = stage(*bounds[i + 1])
+        if cuda:
+            main.wait_event(ev)
+            for t, v, _ in cur:
+                t.record_stream(main)
+                if v is not None:
+                    v.record_stream(main)
+        m = b - a
+        if cuda and vdt == torch.bfloat16 and all(A.supported(t) for t, _, _ in cur):
+            out, bad, nb, _ = A.assemble_bf16(cur, m, dev)
+            nbad += int(nb.item())
+        else:
+            mats = []
+            for t, v, w in cur:
+                if t.dim() == 1:
+                    x = t.to(torch.float64)
+                    if v is not None:
+                        x = torch.where(v, x, torch.full_like(x, float("nan")))
+                    mats.append(x[:, None])
+                else:
+                    mats.append(t[:, :int(w)].to(torch.float64))
+            mat = torch.cat(mats, 1)
+            nbad += int(torch.isnan(mat).any(1).sum())
+            out = torch.zeros((m, ld), dtype=vdt, device=mat.device)
+            out[:, :D] = mat.to(vdt)
+        r = max(0, min(b, keep) - a)
+        if r:
+            res[a:a + r].copy_(out[:r])
+        if m - r:
+            host[a + r - keep:b - keep].copy_(out[r:], non_blocking=cuda)
+    if cuda:
+        torch.cuda.synchronize(dev)
+    _ = _as_matrix
+    col = SpilledVectorColumn(res, host, D) if n > keep else C.VectorColumn(res, D)
+    return col, nbad
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

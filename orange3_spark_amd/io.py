@@ -60,8 +60,17 @@ def _is_vector_struct(t) -> bool:
 
 def arrow_to_columns(table, session) -> "OrderedDict[str, C.Column]":
     pa, _ = _pa()
+    from .frame import spill
     out = OrderedDict()
     dev = session.device
+    nb = 0
+    for arr in table.columns:
+        t = arr.type
+        if pa.types.is_integer(t) or pa.types.is_floating(t) or pa.types.is_boolean(t):
+            nb += table.num_rows * max(1, getattr(t, "bit_width", 8) // 8)
+    # out-of-core: a table whose numeric columns exceed the HBM budget keeps them pinned on
+    # the host (VectorAssembler streams them into a SpilledVectorColumn)
+    host = spill.host_resident(session, nb)
     for name, arr in zip(table.column_names, table.columns):
         arr = arr.combine_chunks() if hasattr(arr, "combine_chunks") else arr
         t = arr.type
@@ -83,8 +92,12 @@ def arrow_to_columns(table, session) -> "OrderedDict[str, C.Column]":
                     np_arr = np_arr.astype(np.int64)
                 elif not np_arr.flags.writeable:
                     np_arr = np_arr.copy()               # arrow buffers are read-only
-            col = C.NumericColumn(torch.from_numpy(np.ascontiguousarray(np_arr)).to(dev),
-                                  None if mask is None else torch.from_numpy(~mask).to(dev))
+            if host:
+                col = C.NumericColumn(spill.pinned(torch.from_numpy(np.ascontiguousarray(np_arr))),
+                                      None if mask is None else spill.pinned(torch.from_numpy(~mask)))
+            else:
+                col = C.NumericColumn(torch.from_numpy(np.ascontiguousarray(np_arr)).to(dev),
+                                      None if mask is None else torch.from_numpy(~mask).to(dev))
             out[name] = col
         else:
             out[name] = C.StringColumn(np.array([None if v is None else str(v) for v in arr.to_pylist()], dtype=object))

@@ -95,9 +95,17 @@ class _GBTParams(_EnsembleParams, HasMaxIter, HasStepSize):
 def _prepare(df, est, classification: bool, split_rows: torch.Tensor | None = None):
     """split_rows: optional bool mask of the rows the split candidates come from (GBT with
     a validation indicator: the training rows only, as Spark splits the dataset first)."""
+    from ..frame.spill import RowBlocks, SpilledVectorColumn
     g = est.getOrDefault
-    X = U.dense_features(df, g(est.featuresCol))
-    X = X.float() if X.is_cuda else X.to(torch.float64)
+    col = U.features_column(df, g(est.featuresCol))
+    if isinstance(col, SpilledVectorColumn) and col.spilled_rows and split_rows is None:
+        X = RowBlocks(col)                  # MEMORY_AND_DISK rows: sampled + streamed, never resident
+    else:
+        X = U.dense_features(df, g(est.featuresCol))
+        if not X.is_cuda:
+            X = X.to(torch.float64)
+        elif X.dtype != torch.bfloat16:      # bf16 rows are binned as they are (no fp32 copy)
+            X = X.float()
     y = U.numeric_column(df, g(est.labelCol), torch.float64)
     w = U.weights_or_none(df, est)
     comm = df.comm

@@ -56,6 +56,8 @@ def numeric_column(df, name: str, dtype=torch.float64) -> torch.Tensor:
     c = df.column_data(name)
     if isinstance(c, C.NumericColumn):
         d = c.data
+        if d.device != df.device:            # a host-resident column of an out-of-core table
+            d = d.to(df.device, non_blocking=d.is_pinned())
         if c.valid is not None and not bool(c.valid.all()):
             raise ValueError(f"column {name} contains null values")
         if dtype is None:

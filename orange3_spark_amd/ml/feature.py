@@ -151,6 +151,9 @@ class VectorAssembler(Transformer, HasInputCols, HasOutputCol, HasHandleInvalid,
         cols = self.getOrDefault(self.inputCols)
         n = len(df)
         dev = df.device
+        streamed = self._transform_streamed(df, cols, n)
+        if streamed is not None:
+            return streamed
         fused = self._transform_fused(df, cols, n)
         if fused is not None:
             return fused
@@ -166,6 +169,46 @@ class VectorAssembler(Transformer, HasInputCols, HasOutputCol, HasHandleInvalid,
                 df = df._mask(~bad)
                 mat = mat[~bad]
         return df.withColumnData(self.getOrDefault(self.outputCol), to_vector_column(df.session, mat))
+
+    def _transform_streamed(self, df, cols, n):
+        """Out-of-core assembly (frame/spill.assemble_streamed): when an input column is
+        host-resident (a table larger than the HBM budget) or the assembled matrix would
+        not fit the budget, the rows are assembled chunk by chunk into a
+        SpilledVectorColumn -- resident prefix up to the budget, the rest in pinned host
+        memory; nothing of full length is materialised on the device."""
+        from ..frame import spill
+        from ..synthetic import LineageVectorColumn
+        if not cols or n == 0:
+            return None
+        srcs = []
+        host_in = False
+        for c in cols:
+            col = df.column_data(c)
+            if isinstance(col, C.NumericColumn) and col.data.dim() == 1:
+                srcs.append((col.data, col.valid, 1))
+            elif type(col) is C.VectorColumn and col.data.dim() == 2:
+                srcs.append((col.data, None, int(col.size)))
+            else:
+                return None
+            host_in |= col.data.device != df.device
+        budget = spill.ingest_budget(df.session)
+        explicit = df.session.conf.get("o3s.storage.hbmBudget", None) not in (None, "", "auto")
+        D = sum(w for _, _, w in srcs)
+        esz = torch.empty((), dtype=df.session.vector_dtype()).element_size()
+        too_big = budget is not None and n * D * esz > budget and (explicit or df.device.type == "cuda")
+        if not host_in and not too_big:
+            return None
+        _ = LineageVectorColumn
+        out, nbad = spill.assemble_streamed(srcs, n, df.session, budget)
+        if nbad:
+            hi = self.getOrDefault(self.handleInvalid)
+            if hi == "error":
+                raise ValueError("Encountered null while assembling a row with handleInvalid = \"error\". "
+                                 "Consider removing nulls from dataset or using handleInvalid = \"keep\" or \"skip\".")
+            if hi == "skip":
+                raise ValueError("handleInvalid = \"skip\" needs the table in device memory; the assembled rows "
+                                 "exceed the HBM budget (o3s.storage.hbmBudget) -- use fillna / dropna first")
+        return df.withColumnData(self.getOrDefault(self.outputCol), out)
 
     def _transform_fused(self, df, cols, n):
         """GPU, bf16 feature storage: ONE gather kernel (ops/assemble.py) reads every input
@@ -580,10 +623,10 @@ class HashingTF(_Simple, HasNumFeatures):
         col = df.column_data(name)
         nf = self.getOrDefault(self.numFeatures)
         if isinstance(col, C.DeviceTokensColumn) and col.data.is_cuda:
-            # device tokens: hash the spans in place (murmur3_span_kernel) -> CSR on device
-            bucket = TX.murmur3_span_buckets(col, nf)
-            counts = col.doc_offs[1:] - col.doc_offs[:-1]
-            return _buckets_to_csr(bucket, counts, len(col), nf, self.getOrDefault(self.binary))
+            # device tokens: hash the spans in place and count per document, one wave per
+            # row (hashing_tf_*_kernel) -> CSR on device, no global sort
+            indptr, idx, val = TX.hashing_tf_csr(col, nf, self.getOrDefault(self.binary))
+            return C.SparseVectorColumn(indptr, idx, val, nf)
         vals = col.values
         return _terms_to_csr([None if v is None else [str(t) for t in v] for v in vals],
                              nf, df.device, self.getOrDefault(self.binary))

@@ -31,18 +31,25 @@ from ..runtime import progress
 
 
 # ----------------------------------------------------------------------------- binning
-def find_splits(comm, X: torch.Tensor, max_bins: int, seed: int = 0, sample: int | None = None) -> list:
+def find_splits(comm, X, max_bins: int, seed: int = 0, sample: int | None = None) -> list:
     """Per-feature candidate thresholds from a global sample (Spark findSplitsBySorting:
-    few distinct values -> midpoints, else approximate quantiles)."""
+    few distinct values -> midpoints, else approximate quantiles).  ``X``: a [n, F] tensor,
+    or a ``frame.spill.RowBlocks`` (MEMORY_AND_DISK rows: only the sampled rows are
+    fetched)."""
+    from ..frame.spill import RowBlocks
     n_local = X.shape[0]
     n = comm.sum_scalar(int(n_local))
     want = sample or max(max_bins * max_bins, 10000)
     frac = min(1.0, want / max(n, 1))
     sizes = comm.all_gather_object(int(n_local))
     off = sum(sizes[: comm.rank])
-    rows = torch.arange(off, off + n_local, dtype=torch.int64, device=X.device)
+    dev = X.device
+    rows = torch.arange(off, off + n_local, dtype=torch.int64, device=dev)
     m = sampling.bernoulli_mask(rows, seed + 17, frac)
-    S = X[m].to(torch.float64)
+    if isinstance(X, RowBlocks):
+        S = X.rows(torch.nonzero(m).reshape(-1)).to(torch.float64)
+    else:
+        S = X[m].to(torch.float64)
     S = comm.all_gather_v(S) if comm.world_size > 1 else S
     S = S.cpu().numpy()
     splits = []
@@ -60,32 +67,68 @@ def find_splits(comm, X: torch.Tensor, max_bins: int, seed: int = 0, sample: int
     return splits
 
 
-def bin_features(X: torch.Tensor, splits: list) -> torch.Tensor:
-    """uint8 [n, F]: bin = #thresholds < value (value <= t_0 -> bin 0).
+def _thresholds(splits: list, F: int, device):
+    T_ = max((len(s) for s in splits), default=0) + 1
+    Tp = 1 << max(0, (T_ - 1).bit_length())
+    if Tp > 256 or 4 * F * (Tp + 1) > 160 * 1024:
+        return None, Tp
+    th = np.full((F, Tp), np.inf, dtype=np.float32)
+    for f, s in enumerate(splits):
+        th[f, :len(s)] = np.asarray(s, dtype=np.float32)
+    return torch.from_numpy(th).to(device), Tp
 
-    GPU fp32: one pass of ``bin_features_kernel`` (all thresholds in LDS, branchless
-    search per element); otherwise per-feature ``torch.bucketize``."""
+
+def _bin_block_kernel(X: torch.Tensor, tht, Tp, out: torch.Tensor, out_t: torch.Tensor | None, ldt: int) -> None:
     n, F = X.shape
-    if X.is_cuda and X.dtype == torch.float32 and X.dim() == 2 and X.stride(1) == 1 and n > 0:
-        T_ = max((len(s) for s in splits), default=0) + 1
-        Tp = 1 << max(0, (T_ - 1).bit_length())
-        if Tp <= 256 and 4 * F * (Tp + 1) <= 160 * 1024:
-            th = np.full((F, Tp), np.inf, dtype=np.float32)
-            for f, s in enumerate(splits):
-                th[f, :len(s)] = np.asarray(s, dtype=np.float32)
-            tht = torch.from_numpy(th).to(X.device)
-            out = torch.empty((n, F), dtype=torch.uint8, device=X.device)
-            N.check(N.kernels().o3s_bin_features(X.data_ptr(), n, X.stride(0), F, tht.data_ptr(), Tp,
-                                                 out.data_ptr(), N.stream_of(X)), "bin_features")
-            return out
-    out = torch.empty((n, F), dtype=torch.uint8, device=X.device)
+    N.check(N.kernels().o3s_bin_features2(X.data_ptr(), int(X.dtype == torch.bfloat16), n, X.stride(0), F,
+                                          tht.data_ptr(), Tp, out.data_ptr(), N.ptr(out_t), ldt, N.stream_of(X)),
+            "bin_features")
+
+
+def _bin_block_torch(X: torch.Tensor, splits: list, out: torch.Tensor) -> None:
+    if X.dtype == torch.bfloat16:
+        X = X.float()
     step = 1 << 22
-    for f in range(F):
+    for f in range(X.shape[1]):
         t = torch.as_tensor(splits[f], dtype=X.dtype if X.is_floating_point() else torch.float64, device=X.device)
-        for a in range(0, n, step):
+        for a in range(0, X.shape[0], step):
             col = X[a:a + step, f].contiguous()
             out[a:a + step, f] = torch.bucketize(col.to(t.dtype), t, right=False).to(torch.uint8) if t.numel() \
                 else torch.zeros_like(col, dtype=torch.uint8)
+
+
+def bin_features(X, splits: list) -> torch.Tensor:
+    """uint8 [n, F]: bin = #thresholds < value (value <= t_0 -> bin 0).
+
+    GPU fp32 / bf16: one pass of ``bin_features_kernel`` (all thresholds in LDS, branchless
+    search per element) that also writes the feature-major copy the partition reads
+    (``ops.trees.feature_major`` returns it); otherwise per-feature ``torch.bucketize``.
+    ``X`` may be a ``frame.spill.RowBlocks``: the resident rows and every host-streamed
+    chunk are binned as they arrive into one resident uint8 matrix (the fp/bf16 features
+    never need to fit in device memory together)."""
+    from ..frame.spill import RowBlocks
+    n, F = X.shape
+    dev = X.device
+    out = torch.empty((n, F), dtype=torch.uint8, device=dev)
+    tht, Tp = _thresholds(splits, F, dev) if dev.type == "cuda" else (None, 0)
+    out_t = torch.empty((F, n), dtype=torch.uint8, device=dev) if tht is not None and n > 0 else None
+
+    def block(Xb: torch.Tensor, a: int) -> None:
+        m = Xb.shape[0]
+        if m == 0:
+            return
+        if tht is not None and Xb.dtype in (torch.float32, torch.bfloat16) and Xb.stride(1) == 1:
+            _bin_block_kernel(Xb, tht, Tp, out[a:a + m], out_t[:, a:] if out_t is not None else None, n)
+        else:
+            _bin_block_torch(Xb, splits, out[a:a + m])
+            if out_t is not None:
+                out_t[:, a:a + m] = out[a:a + m].t()
+    if isinstance(X, RowBlocks):
+        X.run(block)
+    else:
+        block(X, 0)
+    if out_t is not None:
+        T.remember_feature_major(out, out_t)
     return out
 
 

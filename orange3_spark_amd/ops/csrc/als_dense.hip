@@ -75,6 +75,12 @@ __device__ __forceinline__ float rl(float v, int lane) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), lane));
 }
 __device__ __forceinline__ constexpr int rowof(int v, int h) { return (v & 3) + 8 * (v >> 2) + 4 * h; }
+
+// Cross-lane hand-off through LDS inside ONE wave: the hardware runs a wave's LDS
+// instructions in order, but the compiler reasons per lane and may move a load past
+// another lane's store (e.g. forward a lane's own conditional store and sink the load into
+// the other branch).  This compiler barrier pins every LDS access on its side.
+__device__ __forceinline__ void lane_sync() { asm volatile("" ::: "memory"); }
 template <int NT>
 __device__ __forceinline__ constexpr int tix(int j, int i) { return j * NT - j * (j - 1) / 2 + (i - j); }
 
@@ -110,11 +116,12 @@ __device__ __forceinline__ void split8(const float (&z)[8], bf16x8_t& hi, bf16x8
   lo = __builtin_bit_cast(bf16x8_t, L);
 }
 
-template <int R, bool IMPL>
+template <int R, bool IMPL, bool DBG = false>
 __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
-    const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nrows, float* __restrict__ X) {
+    const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nrows, float* __restrict__ X,
+    float* __restrict__ dbg) {
   using D = DW<R>;
   constexpr int NT = D::NT, NL = D::NL, CH = D::CH, DEPTH = D::DEPTH, RS = D::RS, LPS = D::LPS,
                 RPI = D::RPI, NI = D::NI, SLOT = D::SLOT;
@@ -170,7 +177,11 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
     for (int i = 0; i < CH; ++i)   // readfirstlane: keeps hipcc from turning the per-lane
       c[i] = __builtin_amdgcn_readfirstlane(scol[pj + i < last ? pj + i : last]);   // select into a vector load
     float* const dst = ring + pslot * SLOT;
-    const int rr = lane / LPS, lo = lane % LPS;
+    // per-lane address terms recomputed per call (hoisted, they sat in spill slots whose
+    // reloads drained the DMA ring with vmcnt(0))
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const int rr = ln / LPS, lo = ln % LPS;
 #pragma unroll
     for (int ins = 0; ins < NI; ++ins) {
       int32_t ci = c[ins * RPI];
@@ -183,9 +194,9 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
         __builtin_amdgcn_global_load_lds(src, dst + ins * RPI * RS, 16, 0, 0);
       }
     }
-    if (lane < 32) {
-      const int64_t jj = pj + (lane & 15) < last ? pj + (lane & 15) : last;
-      __builtin_amdgcn_global_load_lds((lane < 16 ? w : b) + jj, swb + pslot * 32, 4, 0, 0);
+    if (ln < 32) {
+      const int64_t jj = pj + (ln & 15) < last ? pj + (ln & 15) : last;
+      __builtin_amdgcn_global_load_lds((ln < 16 ? w : b) + jj, swb + pslot * 32, 4, 0, 0);
     }
     pj += CH;
     ++issued;
@@ -199,9 +210,9 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
     const int64_t u = srow[idx];
     const int64_t p0 = sptrs[u], p1 = sptrs[u + 1];
     const float lu = slam[u];
-    // the lane's coordinates, laundered per row: lane-dependent constants of the solve
-    // (identity columns, diagonal masks, LDS addresses) are then recomputed in the row
-    // instead of being hoisted out of the loop into ~100 registers that spill
+    // the lane's coordinates, laundered per PHASE: lane-dependent constants (identity
+    // columns, diagonal masks, LDS addresses) are recomputed where they are used instead of
+    // being hoisted across the Gram loop into registers that then spill inside it
     int q = lane & 31, h = lane >> 5;
     asm volatile("" : "+v"(q), "+v"(h));
     // the system starts as G + lam_u I (G from its LDS copy), the Gram accumulates on top
@@ -273,18 +284,29 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
     }
 
     // ---- rhs ----
+    q = lane & 31;
+    h = lane >> 5;
+    asm volatile("" : "+v"(q), "+v"(h));
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const float t = rh[j] + __shfl_xor(rh[j], 32, 64);
       if (h == 0) sr[32 * j + q] = t;
     }
+    lane_sync();
 
+    if (DBG && idx < 64) {                // diagnostic dump: the assembled system (C layout)
+#pragma unroll
+      for (int t = 0; t < NL; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) dbg[((idx * 2) * NL + t) * 1024 + v * 64 + lane] = acc[t][v];
+    }
     // ---- blocked Cholesky A = U^T U, forward solve U^T y = rhs riding along ----
 #pragma unroll
     for (int p = 0; p < NT; ++p) {
       f32x16_t& dg = acc[tix<NT>(p, p)];
 #pragma unroll
       for (int v = 0; v < 16; ++v) scr[rowof(v, h) * 33 + q] = dg[v];
+      lane_sync();
       // A: lanes 0-31 row q of the tile -> row q of L; lanes 32-63 column q of the
       // identity -> column q of X_p = L_pp^-1 (the same right-looking FMA with the lane's
       // own multiplier).  4-column blocks: v_readlane inside, one rank-4 update per later
@@ -305,6 +327,7 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
         }
         if (c0 + 4 < 32) {
           sC4[lane] = float4_{v[c0], v[c0 + 1], v[c0 + 2], v[c0 + 3]};
+          lane_sync();
 #pragma unroll
           for (int j = c0 + 4; j < 32; ++j) {
             const float4_ l4 = sC4[j];
@@ -313,18 +336,19 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
           }
         }
       }
+      lane_sync();                                                   // sC4 reads done
       if (h == 1) {
 #pragma unroll
         for (int k = 0; k < 32; ++k) scr[k * 33 + q] = v[k];        // X_p[k][q]
       }
-      __builtin_amdgcn_sched_barrier(0);
+      lane_sync();
       if (h == 0) {
         float yq = 0.f;
 #pragma unroll
         for (int j = 0; j < 32; ++j) yq = fmaf(scr[q * 33 + j], sr[32 * p + j], yq);
         sr[32 * p + q] = yq;                                        // y_p = X_p r_p
       }
-      __builtin_amdgcn_sched_barrier(0);
+      lane_sync();
       float xa[16], yv[16];
 #pragma unroll
       for (int vv = 0; vv < 16; ++vv) {
@@ -349,6 +373,7 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
         part += __shfl_xor(part, 32, 64);
         if (h == 0) sr[32 * i + q] -= part;
       }
+      lane_sync();
       // C: S_ji -= U_pj^T U_pi, operands straight from the panel tiles' registers
 #pragma unroll
       for (int j = p + 1; j < NT; ++j)
@@ -362,6 +387,13 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
         }
     }
 
+    if (DBG && idx < 64) {                // diagnostic dump: U / X_p tiles and y
+#pragma unroll
+      for (int t = 0; t < NL; ++t)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) dbg[((idx * 2 + 1) * NL + t) * 1024 + v * 64 + lane] = acc[t][v];
+      for (int c = lane; c < R; c += 64) dbg[128 * NL * 1024 + idx * R + c] = sr[c];
+    }
     // ---- backward U x = y ----
 #pragma unroll
     for (int p = NT - 1; p >= 0; --p) {
@@ -376,20 +408,23 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
 #pragma unroll
           for (int vv = 0; vv < 16; ++vv) prod[vv] = fmaf(ui[vv], xi, prod[vv]);
         }
+        lane_sync();
 #pragma unroll
         for (int vv = 0; vv < 16; ++vv) scr[rowof(vv, h) * 33 + q] = prod[vv];
+        lane_sync();
         float s = 0.f;
 #pragma unroll
         for (int k = 0; k < 32; ++k) s += scr[q * 33 + k];
         if (h == 0) sr[32 * p + q] -= s;
       }
-      __builtin_amdgcn_sched_barrier(0);
+      lane_sync();
       const f32x16_t& xp = acc[tix<NT>(p, p)];
       float t = 0.f;
 #pragma unroll
       for (int vv = 0; vv < 16; ++vv) t = fmaf(xp[vv], sr[32 * p + rowof(vv, h)], t);
       t += __shfl_xor(t, 32, 64);
       if (h == 0) sr[32 * p + q] = t;
+      lane_sync();
     }
 #pragma unroll
     for (int c = 0; c < R; c += 64)
@@ -401,13 +436,21 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
 template <int R>
 int launch(int implicit, const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
            const float* F, const float* G, const float* lam, const int32_t* rows, int64_t nrows, float* X,
-           int grid, hipStream_t st) {
-  if (implicit)
+           int grid, float* dbg, hipStream_t st) {
+  if (dbg != nullptr) {
+    if (implicit)
+      hipLaunchKernelGGL((als_dense_wave_kernel<R, true, true>), dim3(grid), dim3(256), 0, st, indptr, cols, w, b, F,
+                         G, lam, rows, nrows, X, dbg);
+    else
+      hipLaunchKernelGGL((als_dense_wave_kernel<R, false, true>), dim3(grid), dim3(256), 0, st, indptr, cols, w, b,
+                         F, G, lam, rows, nrows, X, dbg);
+  } else if (implicit) {
     hipLaunchKernelGGL((als_dense_wave_kernel<R, true>), dim3(grid), dim3(256), 0, st, indptr, cols, w, b, F, G, lam,
-                       rows, nrows, X);
-  else
+                       rows, nrows, X, nullptr);
+  } else {
     hipLaunchKernelGGL((als_dense_wave_kernel<R, false>), dim3(grid), dim3(256), 0, st, indptr, cols, w, b, F, G,
-                       lam, rows, nrows, X);
+                       lam, rows, nrows, X, nullptr);
+  }
   O3S_CHECK_LAUNCH();
   return 0;
 }
@@ -418,18 +461,29 @@ int launch(int implicit, const int64_t* indptr, const int32_t* cols, const float
 // longest first for balance), one wave per row, ``grid`` blocks of 4 waves (persistent:
 // at most 4 blocks' worth of waves per CU are resident, 1 block per CU).  Same contract
 // as o3s_als_dense_mfma: x_u written into X[u]; implicit: G = Y^T Y (fp32 R x R).
-O3S_API int o3s_als_dense_wave(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
-                               const float* b, const float* F, const float* G, const float* lam, const int32_t* rows,
-                               int64_t nrows, float* X, int grid, hipStream_t st) {
+O3S_API int o3s_als_dense_wave_dbg(int implicit, int R, const int64_t* indptr, const int32_t* cols,
+                                   const float* w, const float* b, const float* F, const float* G, const float* lam,
+                                   const int32_t* rows, int64_t nrows, float* X, int grid, float* dbg,
+                                   hipStream_t st) {
   if (nrows < 0 || (implicit && !G) || grid <= 0) return -1;
   if (nrows == 0) return 0;
   const int64_t need = (nrows + 3) / 4;
   if (grid > need) grid = (int)need;
+  if (dbg != nullptr) grid = 1;
   switch (R) {
-    case 32: return launch<32>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, st);
-    case 64: return launch<64>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, st);
-    case 96: return launch<96>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, st);
-    case 128: return launch<128>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, st);
+    case 32: return launch<32>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, dbg, st);
+    case 64: return launch<64>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, dbg, st);
+    case 96: return launch<96>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, dbg, st);
+    case 128: return launch<128>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, dbg, st);
     default: return -2;
   }
+}
+
+// Diagnostic variant: dbg [(64 rows x 2 stages x NL tiles x 1024) + 64 x R] receives, for
+// the first 64 listed rows, the accumulator tiles (raw C layout: [v][lane]) after the
+// system is assembled and after the forward factorisation, plus y (grid forced to 1).
+O3S_API int o3s_als_dense_wave(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
+                               const float* b, const float* F, const float* G, const float* lam, const int32_t* rows,
+                               int64_t nrows, float* X, int grid, hipStream_t st) {
+  return o3s_als_dense_wave_dbg(implicit, R, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, nullptr, st);
 }

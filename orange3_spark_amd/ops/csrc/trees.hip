@@ -505,28 +505,37 @@ __global__ __launch_bounds__(256) void u8_transpose_kernel(const uint8_t* __rest
 // +inf padding to a power of two Tp; the +1 row pad puts consecutive features of one
 // wave on different banks); each element is a branchless log2(Tp)-step search.  One
 // streaming pass: X read once, bins written once (row-major, coalesced bytes).
+// BF16: X holds bf16 bit patterns (the engine's default GPU vector storage), widened
+// exactly in registers -- no fp32 copy of the matrix.  out_t (optional): the same bins
+// feature-major [F][n] in the same pass (the partition's per-row feature reads), instead
+// of a separate transpose of the finished row-major matrix.
 constexpr int kBinRows = 64;
-__global__ __launch_bounds__(256) void bin_features_kernel(const float* __restrict__ X, int64_t n, int64_t ldx,
+template <bool BF16>
+__global__ __launch_bounds__(256) void bin_features_kernel(const void* __restrict__ Xv, int64_t n, int64_t ldx,
                                                            int F, const float* __restrict__ th, int Tp,
-                                                           uint8_t* __restrict__ out) {
+                                                           uint8_t* __restrict__ out, uint8_t* __restrict__ out_t,
+                                                           int64_t ldt) {
   extern __shared__ float sth[];
   const int TS = Tp + 1;
   for (int i = threadIdx.x; i < F * Tp; i += 256) sth[(i / Tp) * TS + i % Tp] = th[i];
   __syncthreads();
-  const int per = kBinRows * F;
   const int64_t nchunks = (n + kBinRows - 1) / kBinRows;
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
     const int64_t r0 = c * kBinRows;
     const int rows = n - r0 < kBinRows ? (int)(n - r0) : kBinRows;
     for (int li = threadIdx.x; li < rows * F; li += 256) {
       const int lr = li / F, f = li - lr * F;
-      const float x = X[(r0 + lr) * ldx + f];
+      float x;
+      if constexpr (BF16)
+        x = bf16_to_f32(reinterpret_cast<const uint16_t*>(Xv)[(r0 + lr) * ldx + f]);
+      else
+        x = reinterpret_cast<const float*>(Xv)[(r0 + lr) * ldx + f];
       const float* a = sth + f * TS;
       int b = 0;
       for (int st = Tp >> 1; st > 0; st >>= 1) b += (a[b + st - 1] < x) ? st : 0;
       out[(r0 + lr) * F + f] = (uint8_t)b;
+      if (out_t != nullptr) out_t[(int64_t)f * ldt + r0 + lr] = (uint8_t)b;
     }
-    (void)per;
   }
 }
 
@@ -837,19 +846,32 @@ O3S_API int o3s_slab_range_sum(const void* in, int in_f64, int64_t C, const int6
   return 0;
 }
 
-// X: [n][F] fp32 (row stride ldx); th: [F][Tp] fp32 sorted, +inf padded, Tp a power of
-// two <= 256 with at least one pad per feature; out: [n][F] uint8.
-O3S_API int o3s_bin_features(const float* X, int64_t n, int64_t ldx, int F, const float* th, int Tp, uint8_t* out,
-                             hipStream_t st) {
+// X: [n][F] fp32 (bf16 != 0: bf16) with row stride ldx; th: [F][Tp] fp32 sorted, +inf
+// padded, Tp a power of two <= 256 with at least one pad per feature; out: [n][F] uint8;
+// out_t (optional): feature f of row r at out_t[f * ldt + r] (ldt >= n: a block of rows of
+// a larger feature-major matrix, out_t pointing at its first row).
+O3S_API int o3s_bin_features2(const void* X, int bf16, int64_t n, int64_t ldx, int F, const float* th, int Tp,
+                              uint8_t* out, uint8_t* out_t, int64_t ldt, hipStream_t st) {
   if (n <= 0) return 0;
   if (Tp < 1 || Tp > 256 || (Tp & (Tp - 1)) || F <= 0) return -1;
   const size_t lds = sizeof(float) * (size_t)F * (Tp + 1);
   if (lds > 160 * 1024) return -2;
   const int64_t nchunks = (n + kBinRows - 1) / kBinRows;
   const unsigned grid = (unsigned)(nchunks < 8192 ? nchunks : 8192);
-  hipLaunchKernelGGL(bin_features_kernel, dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, Tp, out);
+  if (out_t != nullptr && ldt < n) return -3;
+  if (bf16)
+    hipLaunchKernelGGL(bin_features_kernel<true>, dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, Tp, out, out_t,
+                       ldt);
+  else
+    hipLaunchKernelGGL(bin_features_kernel<false>, dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, Tp, out, out_t,
+                       ldt);
   O3S_CHECK_LAUNCH();
   return 0;
+}
+
+O3S_API int o3s_bin_features(const float* X, int64_t n, int64_t ldx, int F, const float* th, int Tp, uint8_t* out,
+                             hipStream_t st) {
+  return o3s_bin_features2(X, 0, n, ldx, F, th, Tp, out, nullptr, n, st);
 }
 
 // in: [n][F] uint8 with F % 4 == 0; out: [F][n].

@@ -154,3 +154,45 @@ def murmur3_span_buckets(tok, num_buckets: int, seed: int = SPARK_SEED) -> torch
                                           ntok, seed, num_buckets, out.data_ptr(), N.stream_of(out)),
             "murmur3_spans")
     return out
+
+
+def hashing_tf_csr(tok, num_buckets: int, binary: bool, seed: int = SPARK_SEED):
+    """Spark HashingTF of a DeviceTokensColumn straight to CSR (indptr int64, indices int32,
+    values fp64), per document on the GPU (csrc/text.hip ``hashing_tf_*_kernel``: one wave
+    per document, bitonic sort + run counting in registers / LDS; no global sort).
+    Documents of more than 4096 tokens are counted by a torch sort of their own buckets."""
+    dev = tok.data.device
+    n = len(tok)
+    ntok = int(tok.tok_start.numel())
+    lib = N.kernels()
+    st = N.stream_of(tok.doc_offs)
+    tmp_idx = torch.empty(max(ntok, 1), dtype=torch.int32, device=dev)
+    tmp_cnt = torch.empty(max(ntok, 1), dtype=torch.int32, device=dev)
+    nnz = torch.zeros(n, dtype=torch.int64, device=dev)
+    args = (tok.doc_offs.data_ptr(), tok.tok_start.data_ptr(), tok.tok_end.data_ptr(), tok.data.data_ptr())
+    N.check(lib.o3s_hashing_tf(0, *args, None, n, seed, num_buckets, tmp_idx.data_ptr(), tmp_cnt.data_ptr(),
+                               nnz.data_ptr(), None, 0, None, None, st), "hashing_tf")
+    big = torch.nonzero(nnz < 0).reshape(-1)
+    if big.numel():
+        huge = big[nnz[big] == -2]
+        large = big[nnz[big] == -1].contiguous()
+        if large.numel():
+            N.check(lib.o3s_hashing_tf(1, *args, large.data_ptr(), large.numel(), seed, num_buckets,
+                                       tmp_idx.data_ptr(), tmp_cnt.data_ptr(), nnz.data_ptr(), None, 0, None, None,
+                                       st), "hashing_tf_large")
+        for d in huge.tolist():                     # > 4096 tokens: rare, one sort each
+            a, b = int(tok.doc_offs[d]), int(tok.doc_offs[d + 1])
+            sub = type(tok)(torch.tensor([0, b - a], device=dev), tok.tok_start[a:b], tok.tok_end[a:b], tok.data)
+            u, c = torch.unique(murmur3_span_buckets(sub, num_buckets, seed), return_counts=True)
+            tmp_idx[a:a + u.numel()] = u.to(torch.int32)
+            tmp_cnt[a:a + u.numel()] = c.to(torch.int32)
+            nnz[d] = u.numel()
+    indptr = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(nnz, 0, out=indptr[1:])
+    total = int(indptr[-1])
+    idx = torch.empty(max(total, 1), dtype=torch.int32, device=dev)
+    val = torch.empty(max(total, 1), dtype=torch.float64, device=dev)
+    N.check(lib.o3s_hashing_tf(2, *args, None, n, seed, num_buckets, tmp_idx.data_ptr(), tmp_cnt.data_ptr(),
+                               nnz.data_ptr(), indptr.data_ptr(), int(bool(binary)), idx.data_ptr(), val.data_ptr(),
+                               st), "hashing_tf_compact")
+    return indptr, idx[:total], val[:total]

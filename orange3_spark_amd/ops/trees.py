@@ -1,6 +1,8 @@
 """Tree histogram op: gfx950 kernel (csrc/trees.hip) with a PyTorch reference."""
 from __future__ import annotations
 
+import weakref
+
 import numpy as np
 import torch
 
@@ -29,11 +31,24 @@ def hist_kernel_ok(bins: torch.Tensor, B: int, S: int, cls: bool) -> bool:
     return N.kernels().o3s_tree_hist_lds(fp, B, S, int(cls)) > 0
 
 
+# row-major bins -> the feature-major copy written in the same pass by the binning kernel
+# (models/trees.bin_features), so feature_major() needs no second pass over the matrix
+_FM: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def remember_feature_major(bins: torch.Tensor, bins_t: torch.Tensor) -> None:
+    _FM[bins] = bins_t
+
+
 def feature_major(bins: torch.Tensor) -> torch.Tensor | None:
     """[F, n] copy of the binned matrix for the partition's per-row feature reads (GPU;
-    LDS-tiled ``u8_transpose_kernel``, F % 4 == 0, else torch's strided copy)."""
+    the binning kernel's own feature-major output when it wrote one, else the LDS-tiled
+    ``u8_transpose_kernel``, F % 4 == 0, or torch's strided copy)."""
     if not bins.is_cuda:
         return None
+    fm = _FM.get(bins)
+    if fm is not None:
+        return fm
     n, F = bins.shape
     if F % 4 != 0 or not bins.is_contiguous():
         return bins.t().contiguous()

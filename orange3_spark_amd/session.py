@@ -258,8 +258,16 @@ class Session:
         lo, hi = (0, n) if _local else self._shard_bounds(n)
         part = data.iloc[lo:hi]
         cols = OrderedDict()
+        from .frame import spill
+        nb = sum(part[k].to_numpy().nbytes for k in part.columns if part[k].dtype.kind in "fiub")
+        host = spill.host_resident(self, nb)          # out-of-core: numeric columns stay pinned on the host
         for k in part.columns:
-            cols[str(k)] = C.from_numpy(part[k].to_numpy(), self.device)
+            arr = part[k].to_numpy()
+            if host and arr.dtype.kind in "fiub" and arr.ndim == 1:
+                a = arr.astype(np.int64) if arr.dtype.kind == "u" else arr
+                cols[str(k)] = C.NumericColumn(spill.pinned(torch.from_numpy(np.ascontiguousarray(a))))
+            else:
+                cols[str(k)] = C.from_numpy(arr, self.device)
         df = DataFrame(self, cols, hi - lo)
         if schema is not None and not isinstance(schema, (list, tuple)) and hasattr(schema, "fields"):
             for f in schema.fields:

@@ -259,19 +259,23 @@ class SyntheticData:
         return df
 
     def trees(self, numRows: int, numFeatures: int, seed: int = 42) -> DataFrame:
-        """Nonlinear binary classification (GBT/RF config): ``features`` f32, ``label``."""
+        """Nonlinear binary classification (GBT/RF config): ``features`` (the session's vector
+        storage dtype: bf16 on the GPU -- the 256-level synthetic values are exact in bf16,
+        so 500M x 64 holds 64 GB instead of 128), ``label``."""
         s = self.session
         lo, hi = self._bounds(numRows)
         dev = s.device
         n = hi - lo
-        X = torch.empty((n, numFeatures), dtype=torch.float32, device=dev)
+        vdt = s.vector_dtype()
+        X = torch.empty((n, numFeatures), dtype=vdt if vdt in (torch.bfloat16, torch.float32) else torch.float32,
+                        device=dev)
         y = torch.empty(n, dtype=torch.float32, device=dev)
         step = 1 << 24
         for a in range(0, n, step):
             b = min(n, a + step)
             rk = G.row_keys(seed, torch.arange(lo + a, lo + b, dtype=torch.int64, device=dev))
             xb = G.synth_features_torch(rk, G.padded_width(numFeatures), numFeatures)[:, :numFeatures].float()
-            X[a:b] = xb
+            X[a:b] = xb.to(X.dtype)
             score = torch.sin(3 * xb[:, 0]) + xb[:, 1] * xb[:, 2] * 2 - (xb[:, 3 % numFeatures] > 0.3).float()
             u = ((G._fmix32(rk ^ 0x7777) >> 8).float() / 16777216.0)
             y[a:b] = (u < torch.sigmoid(2 * score)).float()

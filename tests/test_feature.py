@@ -178,6 +178,33 @@ def test_gpu_tokenizer_and_hashingtf_match_host():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("binary", [False, True])
+def test_gpu_hashingtf_per_document_kernel_edges(binary):
+    """hashing_tf_*_kernel (one wave per document: register bitonic sort <= 64 tokens, LDS
+    sort <= 4096, torch above) == the global (row, bucket) sort, bitwise: documents of 0,
+    1, 63, 64, 65, 127, 4096, 4097 and 6000 tokens, heavy duplicates (small vocabularies)
+    and a tiny numFeatures (many collisions)."""
+    from orange3_spark_amd import Session, SessionConf
+    from orange3_spark_amd.frame import column as C
+    from orange3_spark_amd.ops import text as TX
+    gs = Session(SessionConf().set("o3s.device", "cuda"))
+    rng = np.random.default_rng(7)
+    lens = [0, 1, 63, 64, 65, 127, 4096, 4097, 6000] + list(rng.integers(0, 300, 400))
+    texts = []
+    for i, L in enumerate(lens):
+        vocab = 5 if i % 3 == 0 else 2000
+        texts.append(" ".join(f"t{int(v)}" for v in rng.integers(0, vocab, L)) if L else "")
+    df = gs.createDataFrame(pd.DataFrame({"text": texts}))
+    col = F.Tokenizer(inputCol="text", outputCol="w").transform(df).column_data("w")
+    assert isinstance(col, C.DeviceTokensColumn)
+    for nf in (1 << 18, 37):
+        indptr, idx, val = TX.hashing_tf_csr(col, nf, binary)
+        bucket = TX.murmur3_span_buckets(col, nf)
+        ref = F._buckets_to_csr(bucket, col.doc_offs[1:] - col.doc_offs[:-1], len(col), nf, binary)
+        assert torch.equal(indptr, ref.indptr) and torch.equal(idx, ref.indices) and torch.equal(val, ref.values)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("handle", ["keep", "skip", "error"])
 def test_gpu_vector_assembler_fused_kernel_matches_torch(handle):
     """The one-pass assemble kernel (any dtype, null masks, vector inputs, padded bf16 out)

@@ -23,6 +23,15 @@ def _session(device="cpu", budget=None):
     return Session(conf)
 
 
+def _budgeted_frame(budget, **kw):
+    """An all-resident assembled frame, then an HBM budget set on its session (persist
+    below applies it; assembling UNDER a budget streams straight into spilled rows)."""
+    s = _session()
+    df = _lr_frame(s, **kw)
+    s.conf.set("o3s.storage.hbmBudget", str(budget))
+    return df
+
+
 def _lr_frame(s, n=3000, d=7, seed=0):
     rng = np.random.default_rng(seed)
     X = rng.normal(size=(n, d)) * rng.uniform(0.5, 2, size=d)
@@ -34,8 +43,7 @@ def _lr_frame(s, n=3000, d=7, seed=0):
 
 
 def test_persist_memory_and_disk_spills_beyond_budget():
-    s = _session(budget=1000 * 7 * 8)                        # room for 1000 rows of 7 fp64
-    df = _lr_frame(s).persist(StorageLevel.MEMORY_AND_DISK)
+    df = _budgeted_frame(1000 * 7 * 8).persist(StorageLevel.MEMORY_AND_DISK)   # room for 1000 rows
     col = df.column_data("features")
     assert isinstance(col, SpilledVectorColumn) and len(col) == 3000
     assert col.resident_rows == 1000 and col.spilled_rows == 2000
@@ -47,7 +55,7 @@ def test_persist_memory_and_disk_spills_beyond_budget():
                        ref.column_data("features").to_numpy()[[5, 1500, 2999]])
     assert df.filter(df.label > 0).count() == ref.filter(ref.label > 0).count()
     assert len(df.limit(10).toPandas()) == 10
-    d2 = _lr_frame(_session(budget=1 << 40)).persist(StorageLevel.DISK_ONLY)
+    d2 = _budgeted_frame(1 << 40).persist(StorageLevel.DISK_ONLY)
     c2 = d2.column_data("features")
     assert isinstance(c2, SpilledVectorColumn) and c2.resident_rows == 0
 
@@ -60,8 +68,7 @@ def test_spill_when_prefix_does_not_fit_next_to_the_column(monkeypatch):
     from orange3_spark_amd.frame import spill
     free = iter([0, 500 * 7 * 8 + (64 << 20)])           # before / after dropping the column
     monkeypatch.setattr(spill, "device_free_bytes", lambda dev: next(free))
-    s = _session(budget=1000 * 7 * 8)
-    df = _lr_frame(s).persist(StorageLevel.MEMORY_AND_DISK)
+    df = _budgeted_frame(1000 * 7 * 8).persist(StorageLevel.MEMORY_AND_DISK)
     col = df.column_data("features")
     assert isinstance(col, SpilledVectorColumn) and len(col) == 3000
     assert col.resident_rows == 500 and col.spilled_rows == 2500
@@ -84,7 +91,7 @@ def test_lr_on_streamed_rows_equals_resident(solver, monkeypatch):
     monkeypatch.setattr(spill, "CHUNK_BYTES", 8 * 8 * 300)   # many chunks
     kw = dict(maxIter=25, regParam=0.01, solver=solver, tol=0.0)
     ref = LogisticRegression(**kw).fit(_lr_frame(_session()))
-    df = _lr_frame(_session(budget=700 * 7 * 8)).persist(StorageLevel.MEMORY_AND_DISK)
+    df = _budgeted_frame(700 * 7 * 8).persist(StorageLevel.MEMORY_AND_DISK)
     assert df.column_data("features").spilled_rows == 2300
     m = LogisticRegression(**kw).fit(df)
     assert np.allclose(m.coefficients.toArray(), ref.coefficients.toArray(), rtol=1e-9, atol=1e-12)
@@ -154,3 +161,75 @@ def test_cache_widget_storage_level():
     w2 = OWCacheDataFrame()
     w2.get_input(_lr_frame(s))
     assert w2.sent["DataFrame"].is_cached and w2.sent["DataFrame"].storageLevel == "MEMORY_ONLY"
+
+
+def _write_parquet(tmp_path, n=3000, d=7, seed=0):
+    rng = np.random.default_rng(seed)
+    X = rng.normal(size=(n, d)) * rng.uniform(0.5, 2, size=d)
+    y = (X @ rng.normal(size=d) + rng.normal(scale=0.5, size=n) > 0).astype(float)
+    pdf = pd.DataFrame(X, columns=[f"f{i}" for i in range(d)])
+    pdf["label"] = y
+    path = str(tmp_path / "t.parquet")
+    pdf.to_parquet(path)
+    return path, [f"f{i}" for i in range(d)]
+
+
+def _ooc_fits(s, path, names):
+    from orange3_spark_amd.ml.classification import GBTClassifier
+    df = VectorAssembler(inputCols=names, outputCol="features").transform(s.read.parquet(path))
+    lr = LogisticRegression(maxIter=30, regParam=0.01).fit(df)
+    km = KMeans(k=4, seed=2, maxIter=8).fit(df)
+    gbt = GBTClassifier(maxIter=3, maxDepth=3, seed=1).fit(df)
+    return df, lr.coefficients.toArray(), km.summary.trainingCost, np.array(gbt.trainingLossHistory)
+
+
+def test_out_of_core_parquet_assembles_into_spilled_rows_and_fits(tmp_path):
+    """Out-of-core table (reference spark_table.py:80 + spark_df_cache.py:39):
+    with the HBM budget below the table, VectorAssembler streams the rows into a
+    SpilledVectorColumn (resident prefix = the budget) and LR, KMeans and GBT (tree
+    binning over streamed chunks) give the all-resident results."""
+    path, names = _write_parquet(tmp_path)
+    s = _session(budget=1000 * 7 * 8)
+    df, lr, km, gbt = _ooc_fits(s, path, names)
+    col = df.column_data("features")
+    assert isinstance(col, SpilledVectorColumn) and col.resident_rows == 1000 and col.spilled_rows == 2000
+    ref_df, lr0, km0, gbt0 = _ooc_fits(_session(), path, names)
+    assert not isinstance(ref_df.column_data("features"), SpilledVectorColumn)
+    assert np.allclose(col.to_numpy(), ref_df.column_data("features").to_numpy())
+    assert np.allclose(lr, lr0, atol=1e-7)
+    assert km == pytest.approx(km0, rel=1e-9)
+    assert np.allclose(gbt, gbt0, rtol=1e-9)
+
+
+@pytest.mark.gpu
+def test_gpu_out_of_core_parquet_ingest_stays_under_budget(tmp_path):
+    """GPU: a parquet table 4x the HBM budget is read into pinned host columns (no device
+    bytes), assembled chunk by chunk into a SpilledVectorColumn with the device peak under
+    the budget plus two chunks, and LR / KMeans / GBT match the all-resident fits."""
+    n, d = 400_000, 32
+    path, names = _write_parquet(tmp_path, n=n, d=d, seed=3)
+    budget = n * 64 * 2 // 4                       # a quarter of the assembled bf16 rows
+    s = _session("cuda", budget=budget)
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    raw = s.read.parquet(path)
+    assert raw.column_data("f0").data.device.type == "cpu" and raw.column_data("f0").data.is_pinned()
+    df = VectorAssembler(inputCols=names, outputCol="features").transform(raw)
+    torch.cuda.synchronize()
+    col = df.column_data("features")
+    assert isinstance(col, SpilledVectorColumn) and col.spilled_rows > 0
+    from orange3_spark_amd.frame.spill import CHUNK_BYTES
+    assert torch.cuda.max_memory_allocated() - base <= budget + 3 * CHUNK_BYTES
+    from orange3_spark_amd.ml.classification import GBTClassifier
+    lr = LogisticRegression(maxIter=20, regParam=0.01).fit(df).coefficients.toArray()
+    km = KMeans(k=8, seed=2, maxIter=6).fit(df).summary.trainingCost
+    gbt = np.array(GBTClassifier(maxIter=3, maxDepth=4, seed=1).fit(df).trainingLossHistory)
+    r = _session("cuda")
+    rdf = VectorAssembler(inputCols=names, outputCol="features").transform(r.read.parquet(path))
+    assert not isinstance(rdf.column_data("features"), SpilledVectorColumn)
+    assert torch.equal(torch.cat([col.data.cpu(), col.host]), rdf.column_data("features").data.cpu())
+    assert np.allclose(lr, LogisticRegression(maxIter=20, regParam=0.01).fit(rdf).coefficients.toArray(), atol=1e-5)
+    assert km == pytest.approx(KMeans(k=8, seed=2, maxIter=6).fit(rdf).summary.trainingCost, rel=1e-4)
+    assert np.allclose(gbt, np.array(GBTClassifier(maxIter=3, maxDepth=4, seed=1).fit(rdf).trainingLossHistory),
+                       rtol=1e-5)

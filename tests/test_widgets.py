@@ -246,6 +246,10 @@ def test_context_widget_keeps_environment_keys(monkeypatch, warehouse):
     camelCase keys keep their case."""
     from orange3_spark_amd.conf import SessionConf, env_key
     from orangecontrib.spark_amd.widgets.data import owcontext
+    from orange3_spark_amd import Session
+    from orangecontrib.spark_amd.widgets.base import SharedSession
+    monkeypatch.setattr(Session, "_active", None)
+    monkeypatch.setattr(SharedSession, "_session", None)
     monkeypatch.setenv("O3S_CONF_o3s__executor__commTimeout", "7")
     monkeypatch.setenv("O3S_CONF_O3S__SEED", "123")
     assert env_key("O3S_CONF_o3s__executor__commTimeout") == "o3s.executor.commTimeout"

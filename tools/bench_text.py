@@ -39,6 +39,28 @@ def main():
     res = {"metric": "Tokenizer+HashingTF docs/s (device tokens)", "docs": a.docs, "words_per_doc": a.words,
            "seconds": dt, "docs_per_s": a.docs / dt, "tokens_per_s": a.docs * a.words / dt,
            "nnz": int(out.indptr[-1])}
+    # HashingTF alone on the device token column (per-document CSR kernels), best of 5
+    words = tok.transform(df)
+    col = words.column_data("w")
+    best = float("inf")
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        got = tf.transform(words).column_data("tf")
+        torch.cuda.synchronize()
+        best = min(best, time.perf_counter() - t)
+    ntok = int(col.tok_start.numel())
+    res["hashingtf_seconds"] = best
+    res["hashingtf_tokens_per_s"] = ntok / best
+    # the previous formulation (span buckets + one global sort of (row, bucket) keys)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    bucket = TX.murmur3_span_buckets(col, 1 << 18)
+    ref = F._buckets_to_csr(bucket, col.doc_offs[1:] - col.doc_offs[:-1], len(col), 1 << 18, False)
+    torch.cuda.synchronize()
+    res["global_sort_seconds"] = time.perf_counter() - t
+    res["same_csr_as_global_sort"] = bool(torch.equal(ref.indptr, got.indptr) and torch.equal(ref.indices, got.indices)
+                                          and torch.equal(ref.values, got.values))
     if a.host:
         vals = np.asarray(docs, dtype=object)
         t = time.perf_counter()
