@@ -289,8 +289,25 @@ def gram(F: torch.Tensor, chunk: int = 1 << 20) -> torch.Tensor:
 
 
 # row chunks per half-iteration on several ranks: chunk c's all-gather (RCCL, its own
-# stream) overlaps the solve of chunk c+1; only the last chunk's transfer is exposed
-GATHER_CHUNKS = 4
+# stream) overlaps the solve of chunk c+1; only the last chunk's transfer is exposed.
+# GATHER_CHUNKS = None: from the comm model below (BASELINE.md "ALS at N = 2/4/8: comm
+# budget"); an int forces that many chunks.
+GATHER_CHUNKS: int | None = None
+# all-gather rate each rank RECEIVES at (bytes/s) -- an estimate for RCCL over the 7 xGMI
+# links of an MI355X node until a multi-GPU run measures it (O3S_ALS_GATHER_GBPS overrides)
+GATHER_BPS = float(__import__("os").environ.get("O3S_ALS_GATHER_GBPS", "300")) * 1e9
+GATHER_TAIL_S = 2e-3          # target exposed tail (the last chunk's transfer)
+GATHER_MAX_CHUNKS = 16        # per-chunk fixed costs (launches, collective latency) cap it
+
+
+def gather_chunks(rows: int, rank: int, world: int) -> int:
+    """Chunks for the slot-layout all-gather of a [rows, rank] fp32 table at ``world``
+    ranks: the transfer each rank receives, (W-1)/W of the table at GATHER_BPS, split so
+    the exposed last chunk stays under GATHER_TAIL_S (2..GATHER_MAX_CHUNKS chunks)."""
+    if GATHER_CHUNKS is not None:
+        return max(1, int(GATHER_CHUNKS))
+    t_gather = rows * rank * 4 * (world - 1) / max(world, 1) / GATHER_BPS
+    return int(min(GATHER_MAX_CHUNKS, max(2, math.ceil(t_gather / GATHER_TAIL_S))))
 
 
 def _slot_len(n: int, world: int, chunks: int) -> int:
@@ -374,11 +391,12 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
     if chunked:
         # factor tables in "slot" layout: every all-gather lands in place (no staging copy,
         # no concatenation) and chunk c of every rank is gathered while chunk c+1 solves
-        Ls, Li = _slot_len(nU, comm.world_size, GATHER_CHUNKS), _slot_len(nI, comm.world_size, GATHER_CHUNKS)
+        Cu, Ci = gather_chunks(nU, rank, comm.world_size), gather_chunks(nI, rank, comm.world_size)
+        Ls, Li = _slot_len(nU, comm.world_size, Cu), _slot_len(nI, comm.world_size, Ci)
         by_user.cols = _slot_pos(by_user.cols, nI, comm.world_size, Li).to(torch.int32)
         by_item.cols = _slot_pos(by_item.cols, nU, comm.world_size, Ls).to(torch.int32)
-        Xf = torch.zeros((GATHER_CHUNKS * comm.world_size * Ls, rank), dtype=X.dtype, device=dev)
-        Yf = torch.zeros((GATHER_CHUNKS * comm.world_size * Li, rank), dtype=Y.dtype, device=dev)
+        Xf = torch.zeros((Cu * comm.world_size * Ls, rank), dtype=X.dtype, device=dev)
+        Yf = torch.zeros((Ci * comm.world_size * Li, rank), dtype=Y.dtype, device=dev)
         _gather_slots(comm, Y, Yf, Li, None)
     for it in range(start, max_iter):
         progress.iteration(it, max_iter)

@@ -74,24 +74,40 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
     c0 = c0.contiguous()
     comm.all_reduce(c0)
     centers = c0[None, :]
+    last = None                        # (labels, distances) of the last round's assign
+    n_before = 0                       # candidates the last round assigned against
     for step in range(steps):
         tr = trace("kmeans.init.round")
         tr.__enter__()
-        _, d = K.assign(X, centers.float())
-        cost = d.to(torch.float64).sum()
+        a, d = K.assign(X, centers.float())
+        cost = torch.sum(d, dtype=torch.float64)        # no fp64 copy of d
         comm.all_reduce(cost)
         if float(cost) <= 0:
             tr.__exit__(None, None, None)
             break
-        p = (2.0 * k * d.to(torch.float64) / float(cost)).clamp(max=1.0)
+        last, n_before = (a, d), centers.shape[0]
+        p = (d * (2.0 * k / float(cost))).clamp_(max=1.0)
         u = sampling.uniform(rows, seed + 1 + step, stream=7)
         new = X[u < p].to(torch.float64)
+        del p, u
         new = comm.all_gather_v(new) if comm.world_size > 1 else new
         centers = torch.cat([centers, new.to(dev)])
         tr.__exit__(None, None, None)
-    # weights = number of points closest to each candidate
+    # weights = number of points closest to each candidate.  The last round already holds
+    # every row's nearest candidate among the first n_before: only the candidates that
+    # round added are assigned now, and a row moves to one of them only if it is strictly
+    # nearer (ties keep the lower index, as one argmin over all candidates would)
     with trace("kmeans.init.weights"):
-        a, _ = K.assign(X, centers.float())
+        if last is not None and centers.shape[0] > n_before:
+            a_old, d_old = last
+            a_new, d_new = K.assign(X, centers[n_before:].float())
+            a = torch.where(d_new < d_old, a_new.to(torch.int64) + n_before, a_old.to(torch.int64))
+            del a_new, d_new
+        elif last is not None:
+            a = last[0].to(torch.int64)
+        else:
+            a, _ = K.assign(X, centers.float())
+        del last
         # integer histogram (LDS-privatised): an fp64 index_add_ of ones into a few hundred
         # candidates serialises on global atomics
         wts = torch.bincount(a.long(), minlength=centers.shape[0])[: centers.shape[0]].to(torch.float64)
@@ -100,7 +116,8 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
         return _local_kmeanspp(centers, wts, k, seed)
 
 
-def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: int = 30) -> torch.Tensor:
+def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: int = 30,
+                    kernel: bool = True) -> torch.Tensor:
     """Weighted k-means++ + Lloyd on candidates (Spark LocalKMeans), fp64 on device.
 
     Greedy k-means++ (best of ``2 + ln k`` weighted draws per step).  The whole seeding
@@ -125,20 +142,33 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
         rnd = (U[t, :n] * m).long().clamp_max(m - 1)
         return torch.where(tot > 0, idx, rnd)
 
-    first = draw(0, w, 1)[0]
-    picks = torch.empty(k, dtype=torch.int64, device=dev)
-    picks[0] = first
-    d2 = ((P - P[first]) ** 2).sum(1)
     pn = (P * P).sum(1)
-    for t in range(1, k):
-        cand = draw(t, w * d2, trials)
-        # [trials, m] squared distances as |p|^2 + |c|^2 - 2 c.p: one small fp64 GEMM
-        # instead of a [trials, m, D] difference tensor per step
-        cd = (pn[None, :] + pn[cand][:, None] - 2.0 * (P[cand] @ P.T)).clamp_min_(0.0)
-        pot = (w[None, :] * torch.minimum(d2[None, :], cd)).sum(1)
-        best = pot.argmin()
-        picks[t] = cand[best]
-        d2 = torch.minimum(d2, cd[best])
+    if kernel and P.is_cuda and trials <= 16 and P.shape[1] * trials * 8 + 8 * 1040 <= 150 * 1024:
+        # all k steps in ONE block (kmeanspp_kernel): ~10 kernels per step otherwise
+        from ..ops import _native as N
+        Pc, wc, pc = P.contiguous(), w.to(torch.float64).contiguous(), pn.contiguous()
+        Uc = U.contiguous()
+        d2 = torch.empty(m, dtype=torch.float64, device=dev)
+        cs = torch.empty(m, dtype=torch.float64, device=dev)
+        picks32 = torch.empty(k, dtype=torch.int32, device=dev)
+        N.check(N.kernels().o3s_kmeanspp(Pc.data_ptr(), wc.data_ptr(), pc.data_ptr(), m, P.shape[1], k, trials,
+                                         Uc.data_ptr(), d2.data_ptr(), cs.data_ptr(), picks32.data_ptr(),
+                                         N.stream_of(Pc)), "kmeanspp")
+        picks = picks32.to(torch.int64)
+    else:
+        first = draw(0, w, 1)[0]
+        picks = torch.empty(k, dtype=torch.int64, device=dev)
+        picks[0] = first
+        d2 = ((P - P[first]) ** 2).sum(1)
+        for t in range(1, k):
+            cand = draw(t, w * d2, trials)
+            # [trials, m] squared distances as |p|^2 + |c|^2 - 2 c.p: one small fp64 GEMM
+            # instead of a [trials, m, D] difference tensor per step
+            cd = (pn[None, :] + pn[cand][:, None] - 2.0 * (P[cand] @ P.T)).clamp_min_(0.0)
+            pot = (w[None, :] * torch.minimum(d2[None, :], cd)).sum(1)
+            best = pot.argmin()
+            picks[t] = cand[best]
+            d2 = torch.minimum(d2, cd[best])
     C = P[picks]
     for _ in range(iters):
         dist = (P * P).sum(1, keepdim=True) - 2 * P @ C.T + (C * C).sum(1)[None, :]

@@ -1184,3 +1184,166 @@ O3S_API int o3s_kmeans_update(const float* X, int64_t n, int64_t ldx, int D, con
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+// ---------------------------------------------------------------------------------
+// k-means|| seeding, step 2 (Spark LocalKMeans.kMeansPlusPlus on the weighted candidates):
+// greedy k-means++ -- per step, `trials` weighted draws from w * d2 (inverse CDF over a
+// block prefix sum), each draw's potential sum_i w_i min(d2_i, |p_i - c|^2), the best one
+// kept -- as ONE block that runs all k steps (the previous formulation issued ~10 kernels
+// per step: ~10K launches at k = 1024).  fp64 throughout; distances by the |p|^2 + |c|^2
+// - 2 p.c form of the torch reference (models/kmeans._local_kmeanspp), draws from the
+// same counter-hash uniforms U [k][trials + 1] (so CPU and GPU pick from the same draws).
+namespace {
+constexpr int kPPThreads = 1024;
+
+__device__ double pp_block_sum(double v, double* red) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < kPPThreads / 64; ++i) t += red[i];
+  return t;
+}
+
+// inclusive prefix sum of prob[i] = w[i] * (d2 ? d2[i] : 1) into cs; returns the total
+__device__ double pp_scan(const double* __restrict__ w, const double* __restrict__ d2, int m, double* cs,
+                          double* part) {
+  const int tid = threadIdx.x;
+  const int per = (m + kPPThreads - 1) / kPPThreads;
+  const int a = tid * per, e = min(m, a + per);
+  double s = 0.0;
+  for (int i = a; i < e; ++i) s += d2 ? w[i] * d2[i] : w[i];
+  __syncthreads();
+  part[tid] = s;
+  __syncthreads();
+  // Hillis-Steele over the 1024 thread totals (10 rounds, fixed order: deterministic)
+  for (int off = 1; off < kPPThreads; off <<= 1) {
+    const double add = tid >= off ? part[tid - off] : 0.0;
+    __syncthreads();
+    part[tid] += add;
+    __syncthreads();
+  }
+  double run = tid ? part[tid - 1] : 0.0;
+  for (int i = a; i < e; ++i) {
+    run += d2 ? w[i] * d2[i] : w[i];
+    cs[i] = run;
+  }
+  __syncthreads();
+  return part[kPPThreads - 1];
+}
+
+__device__ int pp_draw(const double* __restrict__ cs, int m, double tot, double u) {
+  if (!(tot > 0.0)) {
+    const long long r = (long long)(u * m);
+    return (int)(r < m - 1 ? r : m - 1);
+  }
+  const double x = u * tot;
+  int lo = 0, hi = m;                      // first i with cs[i] > x (searchsorted right)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (cs[mid] > x) hi = mid; else lo = mid + 1;
+  }
+  return lo < m - 1 ? lo : m - 1;
+}
+
+template <int TRIALS>
+__global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __restrict__ P,
+                                                              const double* __restrict__ w,
+                                                              const double* __restrict__ pn, int m, int D, int k,
+                                                              const double* __restrict__ U,
+                                                              double* __restrict__ d2, double* __restrict__ cs,
+                                                              int* __restrict__ picks) {
+  constexpr int trials = TRIALS;          // compile-time: the per-draw arrays stay in registers
+  extern __shared__ double sm[];          // [trials][D] candidate rows, then part[1024], red[16]
+  double* const sc = sm;
+  double* const part = sc + trials * D;
+  double* const red = part + kPPThreads;
+  __shared__ int cand[16];
+  __shared__ double pots[16];
+  const int tid = threadIdx.x;
+  const int nt = trials + 1;
+  // step 0: one draw from w
+  double tot = pp_scan(w, nullptr, m, cs, part);
+  if (tid == 0) cand[0] = pp_draw(cs, m, tot, U[0]);
+  __syncthreads();
+  const int first = cand[0];
+  if (tid == 0) picks[0] = first;
+  for (int i = tid; i < m; i += kPPThreads) {
+    double s = 0.0;
+    for (int d = 0; d < D; ++d) {
+      const double t = P[(int64_t)i * D + d] - P[(int64_t)first * D + d];
+      s += t * t;
+    }
+    d2[i] = s;
+  }
+  __syncthreads();
+  for (int t = 1; t < k; ++t) {
+    tot = pp_scan(w, d2, m, cs, part);
+    if (tid < trials) cand[tid] = pp_draw(cs, m, tot, U[(int64_t)t * nt + tid]);
+    __syncthreads();
+    for (int e = tid; e < trials * D; e += kPPThreads) sc[e] = P[(int64_t)cand[e / D] * D + e % D];
+    __syncthreads();
+    double acc[trials];
+#pragma unroll
+    for (int j = 0; j < trials; ++j) acc[j] = 0.0;
+    for (int i = tid; i < m; i += kPPThreads) {
+      const double* p = P + (int64_t)i * D;
+      double dot[trials];
+#pragma unroll
+      for (int j = 0; j < trials; ++j) dot[j] = 0.0;
+      for (int d = 0; d < D; ++d) {
+        const double x = p[d];
+#pragma unroll
+        for (int j = 0; j < trials; ++j) dot[j] = fma(x, sc[j * D + d], dot[j]);
+      }
+      const double wi = w[i], di = d2[i];
+#pragma unroll
+      for (int j = 0; j < trials; ++j) {
+        const double c = fmax(pn[i] + pn[cand[j]] - 2.0 * dot[j], 0.0);
+        acc[j] += wi * fmin(di, c);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < trials; ++j) {
+      const double s = pp_block_sum(acc[j], red);
+      if (tid == 0) pots[j] = s;
+    }
+    __syncthreads();
+    int best = 0;
+    for (int j = 1; j < trials; ++j)
+      if (pots[j] < pots[best]) best = j;
+    const int c = cand[best];
+    if (tid == 0) picks[t] = c;
+    // d2 = min(d2, |p - c|^2), the same formula
+    for (int i = tid; i < m; i += kPPThreads) {
+      const double* p = P + (int64_t)i * D;
+      double dot = 0.0;
+      for (int d = 0; d < D; ++d) dot = fma(p[d], sc[best * D + d], dot);
+      const double cc = fmax(pn[i] + pn[c] - 2.0 * dot, 0.0);
+      d2[i] = fmin(d2[i], cc);
+    }
+    __syncthreads();
+  }
+}
+}  // namespace
+
+// P [m][D] fp64 candidates, w [m] weights, pn [m] = |p|^2, U [k][trials + 1] uniforms;
+// ws: d2 [m], cs [m] fp64 scratch; picks [k] int32 out.  trials <= 16.
+O3S_API int o3s_kmeanspp(const double* P, const double* w, const double* pn, int m, int D, int k, int trials,
+                         const double* U, double* d2, double* cs, int* picks, hipStream_t st) {
+  if (m <= 0 || k <= 0 || D <= 0 || trials < 1 || trials > 16) return -1;
+  const size_t lds = sizeof(double) * ((size_t)trials * D + kPPThreads + 16);
+  if (lds > 160 * 1024 - 256) return -2;
+  switch (trials) {
+#define O3S_PP(T) \
+    case T: hipLaunchKernelGGL(kmeanspp_kernel<T>, dim3(1), dim3(kPPThreads), lds, st, P, w, pn, m, D, k, U, d2, cs, picks); break;
+    O3S_PP(1) O3S_PP(2) O3S_PP(3) O3S_PP(4) O3S_PP(5) O3S_PP(6) O3S_PP(7) O3S_PP(8)
+    O3S_PP(9) O3S_PP(10) O3S_PP(11) O3S_PP(12) O3S_PP(13) O3S_PP(14) O3S_PP(15) O3S_PP(16)
+#undef O3S_PP
+    default: return -1;
+  }
+  O3S_CHECK_LAUNCH();
+  return 0;
+}

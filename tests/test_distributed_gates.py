@@ -116,7 +116,7 @@ def _close_rel(a, b, rel):
 
 @pytest.mark.timeout(1800)
 def test_default_multirank_paths_above_size_gates_match_world1(tmp_path):
-    from orange3_spark_amd.models.als import GATHER_CHUNKS
+    from orange3_spark_amd.models.als import gather_chunks
     # the gate of models/als.py (small = max per-rank nnz * R^2 <= 2^26) must be FALSE on
     # every rank at world 4, or this test would not reach the chunked path (the call
     # counters below check that it did)
@@ -142,7 +142,9 @@ def test_default_multirank_paths_above_size_gates_match_world1(tmp_path):
         assert np.allclose(ref["km_centers"], res["km_centers"], atol=1e-9)
         assert np.allclose(ref["sgd_coef"], res["sgd_coef"], atol=1e-6)
         assert np.allclose(ref["sgd_hist"], res["sgd_hist"], rtol=1e-6)
-    assert GATHER_CHUNKS >= 1
+    # the comm model: 2 chunks for small tables, more as the transfer grows, capped
+    assert gather_chunks(12_000, 32, 2) == 2
+    assert gather_chunks(50_000_000, 128, 8) == 16 and 2 < gather_chunks(5_000_000, 128, 8) <= 16
 
 
 def _empty_rank_work(rank, world, port, out_dir):

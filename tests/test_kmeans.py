@@ -326,3 +326,21 @@ def test_gpu_presplit_dropped_after_fit(gpu, monkeypatch):
     X = torch.randn(60_000, 64, device=gpu)
     fit_kmeans(LocalComm(gpu), X, 64, max_iter=3, seed=1)
     assert K._XSPLIT == [None, None, None]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,m,D", [(16, 300, 8), (256, 1500, 64), (1024, 4100, 128)])
+def test_gpu_kmeanspp_kernel_matches_torch_steps(gpu, k, m, D):
+    """kmeanspp_kernel (all greedy k-means++ steps in one block) picks the same candidates
+    as the step-by-step torch formulation from the same draws (fp64; then the shared
+    Lloyd refinement gives the same centres)."""
+    from orange3_spark_amd.models.kmeans import _local_kmeanspp
+    g = torch.Generator(device="cpu").manual_seed(k + m)
+    P = (torch.randn(m, D, generator=g, dtype=torch.float64) * 3).to(gpu)
+    w = torch.randint(1, 50, (m,), generator=g).to(torch.float64).to(gpu)
+    a = _local_kmeanspp(P, w, k, seed=5, iters=0, kernel=True)
+    b = _local_kmeanspp(P, w, k, seed=5, iters=0, kernel=False)
+    assert torch.equal(a, b)
+    a = _local_kmeanspp(P, w, k, seed=5, iters=30, kernel=True)
+    b = _local_kmeanspp(P, w, k, seed=5, iters=30, kernel=False)
+    torch.testing.assert_close(a, b, rtol=1e-9, atol=1e-9)

@@ -24,3 +24,7 @@ O3S_ALS_DENSE=wave timeout -k 10 420 python -u tools/bench_configs.py --config a
 python3 -c "import json; d=json.load(open('gpurun_out/r5d_cfg_als.json')); print('full config', d['value'], d['fit_seconds'], d['iter_seconds'])"
 timeout -k 10 300 python -u tools/bench_text.py > gpurun_out/r5d_text.json 2> gpurun_out/r5d_text.err || { echo "text bench failed"; tail -20 gpurun_out/r5d_text.err; exit 1; }
 cat gpurun_out/r5d_text.json
+timeout -k 10 300 $T tests/test_kmeans.py -k kmeanspp > gpurun_out/r5d_kpp.log 2>&1 || { echo "kmeanspp test failed"; grep -E "FAILED|^E " gpurun_out/r5d_kpp.log | head; exit 1; }
+tail -1 gpurun_out/r5d_kpp.log
+timeout -k 10 300 python -u tools/bench_kmeans_fit.py --iters 10 > gpurun_out/r5d_kmeans_fit.json 2> gpurun_out/r5d_kmeans_fit.err || { echo "kmeans fit failed"; tail -20 gpurun_out/r5d_kmeans_fit.err; exit 1; }
+cat gpurun_out/r5d_kmeans_fit.json
