@@ -189,6 +189,9 @@ class VectorColumn(Column):
 
     @staticmethod
     def concat(cols):
+        if any(hasattr(c, "host") for c in cols):       # an out-of-core (spilled) part
+            from .spill import SpilledVectorColumn
+            return SpilledVectorColumn.concat(cols)
         return VectorColumn(torch.cat([c.data.to(cols[0].data.device) for c in cols]), cols[0].size)
 
 

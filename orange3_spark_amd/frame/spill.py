@@ -110,9 +110,23 @@ class SpilledVectorColumn(C.VectorColumn):
 
     @staticmethod
     def concat(cols):
-        dev = cols[0].data.device
-        parts = [c.full() if isinstance(c, SpilledVectorColumn) else c.data.to(dev) for c in cols]
-        return C.VectorColumn(torch.cat(parts), cols[0].size)
+        """Row concatenation WITHOUT materialising on the device (``DataFrame.union`` of
+        out-of-core frames): the first column's resident rows stay resident, every later row
+        goes to one pinned host matrix (a resident prefix plus a host suffix is the only
+        layout the streaming consumers read).  Width / dtype follow the first column."""
+        first = cols[0]
+        dev, dt, ld, size = first.data.device, first.data.dtype, first.ld, first.size
+        res = first.data
+        tail = [first.host] if isinstance(first, SpilledVectorColumn) else []
+        for c in cols[1:]:
+            tail.append(_fit_ld(c.data, ld, dt, size))
+            if isinstance(c, SpilledVectorColumn):
+                tail.append(_fit_ld(c.host, ld, dt, size))
+        tail = [t for t in tail if t.shape[0]]
+        if not tail:
+            return C.VectorColumn(res, size)
+        host = _pinned_cat(tail, pin=dev.type == "cuda")
+        return SpilledVectorColumn(res, host, size)
 
     def streamer(self, chunk_bytes: int | None = None) -> "HostStreamer":
         s = getattr(self, "_streamer", None)
@@ -216,6 +230,78 @@ class RowBlocks:
     def rows(self, idx: torch.Tensor) -> torch.Tensor:
         """Rows at local indices ``idx`` (device tensor, prepared)."""
         return self.prep(self.col.take(idx).data[:, : self.D])
+
+
+def _fit_ld(t: torch.Tensor, ld: int, dt, size: int) -> torch.Tensor:
+    """``t`` with leading dimension ``ld`` and dtype ``dt`` (columns of one vector size can
+    differ in padding / dtype: fp64 unpadded vs bf16 padded)."""
+    if t.shape[1] == ld and t.dtype == dt:
+        return t
+    out = torch.zeros((t.shape[0], ld), dtype=dt, device=t.device)
+    out[:, :size] = t[:, :size].to(dt)
+    return out
+
+
+def map_blocks(col: "SpilledVectorColumn", fn, chunk_bytes: int | None = None) -> "SpilledVectorColumn":
+    """A row-wise map over an out-of-core vector column into a NEW spilled column with the
+    same resident / host split (feature transformers on frames larger than HBM).  ``fn``:
+    fp64 rows [m, size] -> fp64 rows [m, size]; the output keeps the column's dtype and
+    padding.  Resident rows are mapped in bounded chunks (no fp64 copy of the whole
+    prefix); host rows stream through the device and are written back to pinned memory
+    asynchronously on the consumer stream."""
+    dt, ld, D, dev = col.data.dtype, col.ld, col.size, col.data.device
+    cuda = dev.type == "cuda"
+    step = max(1, int(chunk_bytes or CHUNK_BYTES) // max(1, ld * 8))
+
+    def apply(X):
+        y = fn(X[:, :D].to(torch.float64))
+        if y.shape != (X.shape[0], D):
+            raise ValueError("map_blocks: fn must keep the row count and the vector size")
+        out = torch.zeros((X.shape[0], ld), dtype=dt, device=X.device) if ld != D else None
+        if out is None:
+            return y.to(dt)
+        out[:, :D] = y.to(dt)
+        return out
+
+    res = torch.empty((col.resident_rows, ld), dtype=dt, device=dev)
+    for a in range(0, col.resident_rows, step):
+        b = min(col.resident_rows, a + step)
+        res[a:b] = apply(col.data[a:b])
+    host = torch.empty((col.spilled_rows, ld), dtype=dt, pin_memory=cuda and torch.cuda.is_available())
+
+    def sink(X, off):
+        for a in range(0, X.shape[0], step):
+            b = min(X.shape[0], a + step)
+            host[off + a:off + b].copy_(apply(X[a:b]), non_blocking=cuda)
+    col.streamer(chunk_bytes).run(sink)
+    if cuda:
+        torch.cuda.synchronize(dev)
+    return SpilledVectorColumn(res, host, D)
+
+
+def block_moments(col: "SpilledVectorColumn"):
+    """(sum, sum of squares, count, max |x| (finite), min, max) of every vector slot over
+    the resident rows and every streamed chunk, fp64 -- the column summary the scalers fit
+    on, without materialising the column."""
+    D, dev = col.size, col.data.device
+    z = torch.zeros(D, dtype=torch.float64, device=dev)
+    acc = {"s": z.clone(), "ss": z.clone(), "mx": z.clone(),
+           "lo": torch.full((D,), float("inf"), dtype=torch.float64, device=dev),
+           "hi": torch.full((D,), float("-inf"), dtype=torch.float64, device=dev)}
+    step = max(1, CHUNK_BYTES // max(1, D * 8))
+
+    def add(X, _off=0):
+        for a in range(0, X.shape[0], step):
+            x = X[a:a + step, :D].to(torch.float64)
+            acc["s"] += x.sum(0)
+            acc["ss"] += (x * x).sum(0)
+            acc["mx"] = torch.maximum(acc["mx"], torch.where(torch.isfinite(x), x, torch.zeros_like(x)).abs().max(0).values)
+            acc["lo"] = torch.minimum(acc["lo"], x.min(0).values)
+            acc["hi"] = torch.maximum(acc["hi"], x.max(0).values)
+    if col.resident_rows:
+        add(col.data)
+    col.streamer().run(add)
+    return acc["s"], acc["ss"], float(len(col)), acc["mx"], acc["lo"], acc["hi"]
 
 
 def _pinned_copy(src: torch.Tensor) -> torch.Tensor:
@@ -348,7 +434,6 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
     torch (CPU), and placed either in the resident prefix (rows below the budget) or copied
     back into the pinned host block.  Returns (SpilledVectorColumn | VectorColumn, invalid
     count)."""
-    from ..ml.feature import _as_matrix
     from ..ops import assemble as A
     from ..ops.glm import padded_width
     dev = session.device
@@ -422,7 +507,6 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
             host[a + r - keep:b - keep].copy_(out[r:], non_blocking=cuda)
     if cuda:
         torch.cuda.synchronize(dev)
-    _ = _as_matrix
     col = SpilledVectorColumn(res, host, D) if n > keep else C.VectorColumn(res, D)
     return col, nbad
 

@@ -21,6 +21,7 @@ import numpy as np
 import torch
 
 from ..frame import column as C
+from ..frame.spill import SpilledVectorColumn, block_moments, map_blocks
 from ..ops import glm as G
 from ..ops import text as TX
 from . import common as U
@@ -862,6 +863,24 @@ class IDFModel(Model, _InOut, MLWritable, MLReadable):
 
 # ============================================================================ scalers
 def _col_moments(df, X):
+    """Column summary (mean, unbiased std, min, max, max |x|) of the vector column named
+    ``X`` (or of the matrix ``X``), reduced over ranks.  An out-of-core (spilled) column is
+    summarised block by block (frame/spill.py ``block_moments``)."""
+    if isinstance(X, str):
+        c = df.column_data(X)
+        if isinstance(c, SpilledVectorColumn):
+            s_, ss_, n_, mx_, lo_, hi_ = block_moments(c)
+            dev = s_.device
+            st = torch.cat([s_, ss_, torch.tensor([n_], dtype=torch.float64, device=dev)])
+            d = s_.numel()
+            df.comm.all_reduce(st)
+            mx = mx_.contiguous()
+            df.comm.all_reduce(mx, "max")
+            mins, maxs = lo_.contiguous(), hi_.contiguous()
+            df.comm.all_reduce(mins, "min")
+            df.comm.all_reduce(maxs, "max")
+            return _finish_moments(st[:d], st[d:2 * d], st[2 * d], mins, maxs, mx)
+        X = _vec(df, X)
     n = torch.tensor([float(X.shape[0])], dtype=torch.float64, device=X.device)
     st = torch.cat([X.sum(0), (X * X).sum(0), n,
                     torch.where(torch.isfinite(X), X, torch.zeros_like(X)).abs().max(0).values if X.shape[0]
@@ -875,10 +894,24 @@ def _col_moments(df, X):
     mins, maxs = mins.contiguous(), maxs.contiguous()
     df.comm.all_reduce(mins, "min")
     df.comm.all_reduce(maxs, "max")
-    s, ss, m = st[:d], st[d:2 * d], st[2 * d]
+    return _finish_moments(st[:d], st[d:2 * d], st[2 * d], mins, maxs, mx)
+
+
+def _finish_moments(s, ss, m, mins, maxs, mx):
     mean = s / m
     var = ((ss - m * mean * mean) / (m - 1)).clamp_min(0) if m > 1 else torch.zeros_like(mean)
     return mean, var.sqrt(), mins, maxs, mx
+
+
+def _rowwise(df, in_name, out_name, fn):
+    """``df`` with ``out_name`` = the row-wise fp64 map ``fn`` of vector column ``in_name``.
+    An out-of-core (spilled) input maps block by block into a spilled output of the same
+    resident / host split and dtype (frame/spill.py ``map_blocks``); otherwise fp64 rows,
+    as Spark's double vectors."""
+    c = df.column_data(in_name)
+    if isinstance(c, SpilledVectorColumn):
+        return df.withColumnData(out_name, map_blocks(c, fn))
+    return df.withColumnData(out_name, C.VectorColumn(fn(_vec(df, in_name).to(df.device))))
 
 
 class _ScalerModelBase(Model, _InOut, MLWritable, MLReadable):
@@ -913,7 +946,7 @@ class StandardScaler(Estimator, _InOut, MLWritable, MLReadable):
         self._set(**self._input_kwargs)
 
     def _fit(self, df):
-        mean, std, *_ = _col_moments(df, _vec(df, self.getOrDefault(self.inputCol)))
+        mean, std, *_ = _col_moments(df, self.getOrDefault(self.inputCol))
         m = StandardScalerModel()
         m._mean, m._std = mean.cpu().numpy(), std.cpu().numpy()
         return m._with_parent(self)
@@ -934,13 +967,17 @@ class StandardScalerModel(_ScalerModelBase):
         return DenseVector(self._std)
 
     def _transform(self, df):
-        X = _vec(df, self.getOrDefault(self.inputCol))
-        if self.getOrDefault(self.withMean):
-            X = X - torch.from_numpy(self._mean).to(X.device)
-        if self.getOrDefault(self.withStd):
-            s = torch.from_numpy(self._std).to(X.device)
-            X = torch.where(s > 0, X / torch.where(s > 0, s, torch.ones_like(s)), torch.zeros_like(X))
-        return df.withColumnData(self.getOrDefault(self.outputCol), C.VectorColumn(X))
+        mean = torch.from_numpy(self._mean).to(df.device)
+        s = torch.from_numpy(self._std).to(df.device)
+        with_mean, with_std = self.getOrDefault(self.withMean), self.getOrDefault(self.withStd)
+
+        def f(X):
+            if with_mean:
+                X = X - mean
+            if with_std:
+                X = torch.where(s > 0, X / torch.where(s > 0, s, torch.ones_like(s)), torch.zeros_like(X))
+            return X
+        return _rowwise(df, self.getOrDefault(self.inputCol), self.getOrDefault(self.outputCol), f)
 
 
 @register("org.apache.spark.ml.feature.MinMaxScaler")
@@ -957,7 +994,7 @@ class MinMaxScaler(Estimator, _InOut, MLWritable, MLReadable):
         self._set(**self._input_kwargs)
 
     def _fit(self, df):
-        _, _, mins, maxs, _ = _col_moments(df, _vec(df, self.getOrDefault(self.inputCol)))
+        _, _, mins, maxs, _ = _col_moments(df, self.getOrDefault(self.inputCol))
         m = MinMaxScalerModel()
         m._originalMin, m._originalMax = mins.cpu().numpy(), maxs.cpu().numpy()
         return m._with_parent(self)
@@ -978,13 +1015,15 @@ class MinMaxScalerModel(_ScalerModelBase):
         return DenseVector(self._originalMax)
 
     def _transform(self, df):
-        X = _vec(df, self.getOrDefault(self.inputCol))
-        lo = torch.from_numpy(self._originalMin).to(X.device)
-        rng = torch.from_numpy(self._originalMax - self._originalMin).to(X.device)
+        lo = torch.from_numpy(self._originalMin).to(df.device)
+        rng = torch.from_numpy(self._originalMax - self._originalMin).to(df.device)
         a, b = self.getOrDefault(self.min), self.getOrDefault(self.max)
-        scaled = torch.where(rng != 0, (X - lo) / torch.where(rng != 0, rng, torch.ones_like(rng)),
-                             torch.full_like(X, 0.5))
-        return df.withColumnData(self.getOrDefault(self.outputCol), C.VectorColumn(scaled * (b - a) + a))
+
+        def f(X):
+            scaled = torch.where(rng != 0, (X - lo) / torch.where(rng != 0, rng, torch.ones_like(rng)),
+                                 torch.full_like(X, 0.5))
+            return scaled * (b - a) + a
+        return _rowwise(df, self.getOrDefault(self.inputCol), self.getOrDefault(self.outputCol), f)
 
 
 @register("org.apache.spark.ml.feature.MaxAbsScaler")
@@ -997,7 +1036,7 @@ class MaxAbsScaler(Estimator, _InOut, MLWritable, MLReadable):
         self._set(**self._input_kwargs)
 
     def _fit(self, df):
-        *_, mx = _col_moments(df, _vec(df, self.getOrDefault(self.inputCol)))
+        *_, mx = _col_moments(df, self.getOrDefault(self.inputCol))
         m = MaxAbsScalerModel()
         m._maxAbs = mx.cpu().numpy()
         return m._with_parent(self)
@@ -1012,10 +1051,9 @@ class MaxAbsScalerModel(_ScalerModelBase):
         return DenseVector(self._maxAbs)
 
     def _transform(self, df):
-        X = _vec(df, self.getOrDefault(self.inputCol))
-        m = torch.from_numpy(self._maxAbs).to(X.device)
-        return df.withColumnData(self.getOrDefault(self.outputCol),
-                                 C.VectorColumn(torch.where(m > 0, X / torch.where(m > 0, m, torch.ones_like(m)), X)))
+        m = torch.from_numpy(self._maxAbs).to(df.device)
+        return _rowwise(df, self.getOrDefault(self.inputCol), self.getOrDefault(self.outputCol),
+                        lambda X: torch.where(m > 0, X / torch.where(m > 0, m, torch.ones_like(m)), X))
 
 
 @register("org.apache.spark.ml.feature.RobustScaler")

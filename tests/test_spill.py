@@ -233,3 +233,43 @@ def test_gpu_out_of_core_parquet_ingest_stays_under_budget(tmp_path):
     assert km == pytest.approx(KMeans(k=8, seed=2, maxIter=6).fit(rdf).summary.trainingCost, rel=1e-4)
     assert np.allclose(gbt, np.array(GBTClassifier(maxIter=3, maxDepth=4, seed=1).fit(rdf).trainingLossHistory),
                        rtol=1e-5)
+
+
+def test_scalers_and_union_on_spilled_rows_match_resident(tmp_path):
+    """Feature stages and ``union`` on an out-of-core frame (spilled columns
+    broke most consumers): StandardScaler / MinMaxScaler / MaxAbsScaler fit block by block
+    and transform into a spilled output of the same split; union keeps the first frame's
+    resident rows and moves the rest to host memory -- nothing materialises the column."""
+    from orange3_spark_amd.ml.feature import MaxAbsScaler, MinMaxScaler, StandardScaler
+    path, names = _write_parquet(tmp_path)
+    s = _session(budget=1000 * 7 * 8)
+    df = VectorAssembler(inputCols=names, outputCol="features").transform(s.read.parquet(path))
+    ref = VectorAssembler(inputCols=names, outputCol="features").transform(_session().read.parquet(path))
+    assert isinstance(df.column_data("features"), SpilledVectorColumn)
+
+    def boom(self):
+        raise AssertionError("materialised a spilled column")
+    orig_full = SpilledVectorColumn.full
+    SpilledVectorColumn.full = boom
+    try:
+        outs = []
+        for est in (StandardScaler(withMean=True, inputCol="features", outputCol="s"),
+                    MinMaxScaler(min=-1.0, max=2.0, inputCol="features", outputCol="s"),
+                    MaxAbsScaler(inputCol="features", outputCol="s")):
+            m = est.fit(df)
+            o = m.transform(df).column_data("s")
+            assert isinstance(o, SpilledVectorColumn) and o.resident_rows == 1000 and o.spilled_rows == 2000
+            outs.append((m, o))
+        u = df.union(df)
+        uc = u.column_data("features")
+        assert isinstance(uc, SpilledVectorColumn) and uc.resident_rows == 1000 and len(uc) == 6000
+    finally:
+        SpilledVectorColumn.full = orig_full
+    for (m, o), est in zip(outs, (StandardScaler(withMean=True, inputCol="features", outputCol="s"),
+                                  MinMaxScaler(min=-1.0, max=2.0, inputCol="features", outputCol="s"),
+                                  MaxAbsScaler(inputCol="features", outputCol="s"))):
+        r = est.fit(ref).transform(ref).column_data("s").to_numpy()
+        assert np.allclose(o.to_numpy(), r, atol=1e-12)
+    a = ref.column_data("features").to_numpy()
+    assert np.array_equal(uc.to_numpy(), np.concatenate([a, a]))
+    assert u.count() == 6000
