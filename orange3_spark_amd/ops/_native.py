@@ -78,11 +78,8 @@ _SIGS: dict[str, list] = {
     "o3s_regression_stats": [c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_vp, c_vp, c_vp],
     "o3s_confusion": [c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp],
     "o3s_score_hist": [c_vp, c_i32, c_i64, c_vp, c_i32, c_vp, c_i32, c_i64, c_f64, c_f64, c_i32, c_vp, c_vp],
-    "o3s_als_wood_blocked": [c_i32],
     "o3s_als_wood_kn": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
-    "o3s_als_wood": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "o3s_als_wood_timed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp],
-    "o3s_als_dense": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
     "o3s_hashing_tf": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32,
                        c_vp, c_vp, c_vp],
     "o3s_als_dense_wave_dbg": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp,
@@ -90,12 +87,7 @@ _SIGS: dict[str, list] = {
     "o3s_bin_features2": [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp],
     "o3s_kmeanspp": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_als_dense_wave": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
-    "o3s_als_dense_mfma": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
-    "o3s_als_dense_mfma_blk": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
-    "o3s_als_dense_mfma_gl": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
-    "o3s_als_dense_mfma_timed": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp],
     "o3s_als_exact_max_small": [],
-    "o3s_als_rotate_mfma": [c_i32],
     "o3s_als_rotate": [c_i32, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
     "o3s_als_rotate_to": [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp],
     "o3s_assemble": [c_vp, c_i32, c_vp, c_i32, c_i32, c_i64, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp],

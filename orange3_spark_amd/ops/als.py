@@ -119,28 +119,12 @@ def dense_solve(indptr, cols, w, b, F, FtF, lam, batch_bytes: int = 1 << 30) -> 
 
 
 EXACT_RANKS = (32, 64, 96, 128)
-# dense (long-row) exact solves: "mfma_gl" (default) = als_dense_mfma_kernel with 4-column
-# diagonal blocks and, at R = 96 / 128, the bf16x3 Gram; at R = 128 its factor rows are
-# gathered by LDS-DMA into a 3-step ring (45.1 vs 46.6 ms for 625K items x 200 ratings;
-# 0.1067 vs 0.1087 s per rank-of-8 iteration, profiles/als_gl_ring_r4.json); "mfma_blk" =
-# the same kernel with register-staged gathers; "mfma" = column-by-column diagonals and
-# the f32 Gram (0.156); "vgpr" = als_dense_kernel (8 x 8 register tiles, packed FMA; 0.144).
-# Rejected: rating indices prefetched one Gram step ahead of the gathers (0.127 vs 0.122 s)
-# "wave" (default): als_dense_wave_kernel (csrc/als_dense.hip) -- one wave per row, four
-# independent waves per CU, factor rows gathered by an LDS-DMA ring that streams across
-# rows, the rows listed longest first.
-DENSE_KERNEL = os.environ.get("O3S_ALS_DENSE", "mfma_gl")
-# x = Q y for the Woodbury rows on the matrix cores (R = 128: rank-of-8 iteration 0.0903 ->
-# 0.0881 s, profiles/als_rotate_mfma_r4.json; O3S_ALS_ROTATE_MFMA=0: the packed-FMA kernel)
-ROTATE_MFMA = os.environ.get("O3S_ALS_ROTATE_MFMA", "1") == "1"
-# Woodbury Cholesky in 8-column panels with the trailing updates on the matrix cores
-# (O3S_ALS_WOOD_BLK=0: every rank-1 update by v_readlane broadcasts)
-WOOD_BLK = os.environ.get("O3S_ALS_WOOD_BLK", "1") == "1"
-# rows with <= 16 ratings in their own Woodbury launch (16 x 16 S, half the P registers);
-# O3S_ALS_WOOD_SPLIT=0: one launch for every Woodbury row
-WOOD_SPLIT = os.environ.get("O3S_ALS_WOOD_SPLIT", "1") == "1"
-# ... and rows with 17..24 ratings in a 24-row launch (O3S_ALS_WOOD_SPLIT24=0: with the 32-row ones)
-WOOD_SPLIT24 = os.environ.get("O3S_ALS_WOOD_SPLIT24", "1") == "1"
+# Long rows (more than 32 ratings, or lam_u = 0) take als_dense_wave_kernel
+# (csrc/als_dense.hip): one wave per row, four independent waves per CU, factor rows
+# gathered by an LDS-DMA ring that streams across the rows of a wave, rows listed longest
+# first.  625K items x 200 ratings at rank 128: 34.0 ms against 45.2 ms for the round-4
+# block-per-row kernel (profiles/als_dense_wave_r5.json).  Rows with <= 16 / 17..24 / 25..32
+# ratings take Woodbury launches sized to them (16 x 16 S on 16x16x4 MFMAs for the first).
 
 
 _FTF_WS: dict = {}
@@ -252,7 +236,6 @@ def rotated_table(F: torch.Tensor, Q: torch.Tensor) -> torch.Tensor:
         rows = torch.arange(n, dtype=torch.int32, device=F.device)
         lib = N.kernels()
         grid = max(1, min(N.num_cus(F.device) * 2, -(-n // 32)))
-        lib.o3s_als_rotate_mfma(int(ROTATE_MFMA))
         N.check(lib.o3s_als_rotate_to(R, Q.contiguous().data_ptr(), rows.data_ptr(), n, F.data_ptr(),
                                       FQ.data_ptr(), grid, N.stream_of(FQ)), "als_rotate(F Q)")
     return FQ
@@ -300,47 +283,30 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
         else:
             eig, Q, P = torch.zeros(R, dtype=torch.float32, device=dev), None, F
         with trace("als.woodbury", rows=ns):
-            lib.o3s_als_wood_blocked(int(WOOD_BLK))
-            if WOOD_SPLIT and WOOD_BLK:
-                cs = cnt[small_m]
-                if WOOD_SPLIT24:
-                    parts = ((16, cs <= 16), (24, (cs > 16) & (cs <= 24)), (32, cs > 24))
-                else:
-                    parts = ((16, cs <= 16), (32, cs > 16))
-                for kn, lst in ((kn, small[m].contiguous()) for kn, m in parts):
-                    if lst.numel():
-                        N.check(lib.o3s_als_wood_kn(R, kn, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
-                                                    b.data_ptr(), P.data_ptr(), eig.data_ptr(), lam.data_ptr(),
-                                                    lst.data_ptr(), lst.numel(), out.data_ptr(), st), "als_wood")
-            else:
-                N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
-                                         P.data_ptr(), eig.data_ptr(), lam.data_ptr(), small.data_ptr(), ns,
-                                         out.data_ptr(), st), "als_wood")
+            cs = cnt[small_m]
+            for kn, m_ in ((16, cs <= 16), (24, (cs > 16) & (cs <= 24)), (32, cs > 24)):
+                lst = small[m_].contiguous()
+                if lst.numel():
+                    N.check(lib.o3s_als_wood_kn(R, kn, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
+                                                b.data_ptr(), P.data_ptr(), eig.data_ptr(), lam.data_ptr(),
+                                                lst.data_ptr(), lst.numel(), out.data_ptr(), st), "als_wood")
         if implicit:                          # x = Q y for the Woodbury rows (als_rotate_kernel)
             with trace("als.rotate", rows=ns):
                 QT = Q.T.contiguous()
                 grid = max(1, min(N.num_cus(dev) * 2, -(-ns // 32)))
-                lib.o3s_als_rotate_mfma(int(ROTATE_MFMA))
                 N.check(lib.o3s_als_rotate(R, QT.data_ptr(), small.data_ptr(), ns, out.data_ptr(), grid, st),
                         "als_rotate")
     if nd:
         with trace("als.dense", rows=nd):
             Gf = G.float().contiguous() if implicit else None
-            if DENSE_KERNEL == "wave":
-                # longest rows first: the waves take rows round robin, so the long tail of
-                # popular items spreads over the whole chip instead of finishing last
-                order = torch.argsort(cnt[dense - a], descending=True)
-                rows_sorted = dense[order].contiguous()
-                N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
-                                               b.data_ptr(), F.data_ptr(), N.ptr(Gf), lam.data_ptr(),
-                                               rows_sorted.data_ptr(), nd, out.data_ptr(), N.num_cus(dev), st),
-                        "als_dense_wave")
-                return out
-            fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
-                  "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(DENSE_KERNEL, lib.o3s_als_dense)
-            N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
-                       F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), nd, out.data_ptr(), st),
-                    "als_dense")
+            # longest rows first: the waves take rows round robin, so the long tail of
+            # popular items spreads over the whole chip instead of finishing last
+            order = torch.argsort(cnt[dense - a], descending=True)
+            rows_sorted = dense[order].contiguous()
+            N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
+                                           b.data_ptr(), F.data_ptr(), N.ptr(Gf), lam.data_ptr(),
+                                           rows_sorted.data_ptr(), nd, out.data_ptr(), N.num_cus(dev), st),
+                    "als_dense_wave")
     return out
 
 

@@ -189,7 +189,7 @@ def _exact_case(R, implicit, seed=0, n_rows=700, n_other=900, dev="cuda"):
     lens = torch.randint(0, 40, (n_rows,), generator=g)
     lens[:6] = torch.tensor([0, 1, 5, 32, 33, 200])
     lens[6:40] = torch.randint(60, 260, (34,), generator=g)
-    lens[6] = 1000                                  # several index-chunk refills (mfma_gl)
+    lens[6] = 1000                                  # several index-chunk refills of the gather ring
     indptr = torch.zeros(n_rows + 1, dtype=torch.int64)
     indptr[1:] = torch.cumsum(lens, 0)
     nnz = int(indptr[-1])
@@ -211,7 +211,7 @@ def _exact_case(R, implicit, seed=0, n_rows=700, n_other=900, dev="cuda"):
 @pytest.mark.parametrize("R", [32, 64, 128])
 @pytest.mark.parametrize("implicit", [False, True])
 def test_gpu_exact_kernels_match_fp64_solve(R, implicit):
-    """als_wood_kernel (<= 32 ratings) and als_dense_kernel (longer rows) == fp64
+    """als_wood_kernel (<= 32 ratings) and als_dense_wave_kernel (longer rows) == fp64
     torch.linalg.solve of each row's normal equations (rank up to 128)."""
     from orange3_spark_amd.ops import als as A
     indptr, cols, w, b, F, G, lam = _exact_case(R, implicit)
@@ -274,14 +274,12 @@ def test_gpu_exact_kernels_pad_other_ranks(R, implicit):
 @pytest.mark.gpu
 @pytest.mark.parametrize("R", [32, 64, 96, 128])
 @pytest.mark.parametrize("implicit", [False, True])
-@pytest.mark.parametrize("kernel", ["wave", "mfma", "mfma_blk", "mfma_gl", "vgpr"])
-def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
-    """Both dense exact kernels (als_dense_mfma_kernel: 32 x 32 MFMA accumulator tiles;
-    als_dense_kernel: 8 x 8 register tiles) == the fp64 solve on rows routed to the dense
-    path (lam = 0 rows and rows longer than the Woodbury limit), including rows of 0 and 1
-    ratings, an odd count and a row that is not a multiple of the 16-rating staging round."""
+def test_gpu_dense_kernel_matches_fp64_solve(R, implicit):
+    """The dense exact kernel (als_dense_wave_kernel: one wave per row, 32 x 32 MFMA
+    accumulator tiles) == the fp64 solve on rows routed to the dense path (lam = 0 rows and
+    rows longer than the Woodbury limit), including rows of 0 and 1 ratings, an odd count
+    and a row that is not a multiple of the 16-rating staging round."""
     from orange3_spark_amd.ops import als as A
-    monkeypatch.setattr(A, "DENSE_KERNEL", kernel)
     indptr, cols, w, b, F, G, lam = _exact_case(R, implicit, seed=11)
     lam = lam.clone()
     lam[:40] = 0.05 * (indptr[1:41] - indptr[:40]).float().clamp_min(1.0)   # rows < 40: dense path too
@@ -291,15 +289,9 @@ def test_gpu_dense_kernels_match_fp64_solve(R, implicit, kernel, monkeypatch):
     from orange3_spark_amd.ops import _native as N
     lib = N.kernels()
     Gf = G.float().contiguous() if implicit else None
-    if kernel == "wave":
-        N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
-                                       b.data_ptr(), F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), 40,
-                                       got.data_ptr(), 256, N.stream_of(got)), "als_dense_wave")
-    else:
-        fn = {"mfma": lib.o3s_als_dense_mfma, "mfma_blk": lib.o3s_als_dense_mfma_blk,
-              "mfma_gl": lib.o3s_als_dense_mfma_gl}.get(kernel, lib.o3s_als_dense)
-        N.check(fn(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), F.data_ptr(),
-                   N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), 40, got.data_ptr(), N.stream_of(got)), "als_dense")
+    N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
+                                   b.data_ptr(), F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), 40,
+                                   got.data_ptr(), 256, N.stream_of(got)), "als_dense_wave")
     ref = torch.empty((n, R), dtype=torch.float64, device=F.device)
     A.exact_solve_torch(indptr, cols, w, b, F, G, lam, ref)
     got, ref = got[:40], ref[:40]

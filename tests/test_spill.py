@@ -273,3 +273,29 @@ def test_scalers_and_union_on_spilled_rows_match_resident(tmp_path):
     a = ref.column_data("features").to_numpy()
     assert np.array_equal(uc.to_numpy(), np.concatenate([a, a]))
     assert u.count() == 6000
+
+
+@pytest.mark.gpu
+def test_gpu_scalers_and_union_on_spilled_rows(tmp_path):
+    """GPU: StandardScaler fit/transform and union over a host-resident parquet table
+    assembled into spilled bf16 rows equal the all-resident results (bf16 storage)."""
+    from orange3_spark_amd.ml.feature import StandardScaler
+    n, d = 200_000, 16
+    path, names = _write_parquet(tmp_path, n=n, d=d, seed=4)
+    s = _session("cuda", budget=n * 64 * 2 // 4)
+    df = VectorAssembler(inputCols=names, outputCol="features").transform(s.read.parquet(path))
+    r = _session("cuda")
+    rdf = VectorAssembler(inputCols=names, outputCol="features").transform(r.read.parquet(path))
+    assert isinstance(df.column_data("features"), SpilledVectorColumn)
+    est = StandardScaler(withMean=True, inputCol="features", outputCol="s")
+    m, m0 = est.fit(df), est.fit(rdf)
+    assert np.allclose(m.mean.toArray(), m0.mean.toArray(), atol=1e-9)
+    assert np.allclose(m.std.toArray(), m0.std.toArray(), rtol=1e-9)
+    o = m.transform(df).column_data("s")
+    assert isinstance(o, SpilledVectorColumn)
+    ref = m0.transform(rdf).column_data("s").to_numpy()
+    assert np.allclose(o.to_numpy(), ref, atol=2e-2 * np.abs(ref).max())      # bf16 output storage
+    u = df.union(df).column_data("features")
+    assert isinstance(u, SpilledVectorColumn) and len(u) == 2 * n
+    a = rdf.column_data("features").to_numpy()
+    assert np.array_equal(u.to_numpy(), np.concatenate([a, a]))

@@ -43,9 +43,9 @@ def main():
     st = N.stream_of(out)
 
     def prod():
-        N.check(lib.o3s_als_wood(R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), P.data_ptr(),
-                                 eig.data_ptr(), lam.data_ptr(), small.data_ptr(), a.users, out.data_ptr(), st),
-                "wood")
+        N.check(lib.o3s_als_wood_kn(R, 32, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                    P.data_ptr(), eig.data_ptr(), lam.data_ptr(), small.data_ptr(), a.users,
+                                    out.data_ptr(), st), "wood")
 
     def timed():
         N.check(lib.o3s_als_wood_timed(indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), P.data_ptr(),

@@ -2,8 +2,8 @@
 """Exact ALS solve kernels in isolation (rocprofv3 --pmc target; no torch bitwise ops).
 
 Two CSRs shaped like one rank's halves of the rank-128 benchmark, scaled by --scale:
-  user side: rows with 1..40 ratings (mean ~20) -> als_wood_kernel (<= 32) / als_dense_kernel
-  item side: rows with 100..300 ratings        -> als_dense_kernel
+  user side: rows with 1..40 ratings (mean ~20) -> als_wood_kernel (<= 32) / als_dense_wave_kernel
+  item side: rows with 100..300 ratings        -> als_dense_wave_kernel
 gathering from a --other x R factor table.  Prints per-side seconds and solved rows/s."""
 import argparse
 import json
