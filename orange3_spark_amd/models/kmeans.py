@@ -143,6 +143,8 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
         return torch.where(tot > 0, idx, rnd)
 
     pn = (P * P).sum(1)
+    tr = trace("kmeans.init.local.seed")
+    tr.__enter__()
     if kernel and P.is_cuda and trials <= 16 and P.shape[1] * trials * 8 + 8 * 1040 <= 150 * 1024:
         # all k steps in ONE block (kmeanspp_kernel): ~10 kernels per step otherwise
         from ..ops import _native as N
@@ -170,6 +172,12 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
             picks[t] = cand[best]
             d2 = torch.minimum(d2, cd[best])
     C = P[picks]
+    tr.__exit__(None, None, None)
+    with trace("kmeans.init.local.lloyd"):
+        return _local_lloyd(P, w, C, k, iters)
+
+
+def _local_lloyd(P, w, C, k, iters):
     for _ in range(iters):
         dist = (P * P).sum(1, keepdim=True) - 2 * P @ C.T + (C * C).sum(1)[None, :]
         a = dist.argmin(1)
