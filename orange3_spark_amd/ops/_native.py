@@ -140,8 +140,10 @@ _HOST_SIGS: dict[str, list] = {
     "o3s_host_murmur3": [c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp],
     "o3s_host_tokenize": [c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp],
     "o3s_host_pav": [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_vp],
+    "o3s_host_ascii_lengths": [c_vp, c_i64, c_vp, c_vp],
+    "o3s_host_ascii_pack": [c_vp, c_i64, c_vp, c_vp, c_i32],
 }
-_HOST_RET = {"o3s_host_tokenize": C.c_int64, "o3s_host_pav": C.c_int64}
+_HOST_RET = {"o3s_host_tokenize": C.c_int64, "o3s_host_pav": C.c_int64, "o3s_host_ascii_lengths": C.c_int64}
 
 
 def host():

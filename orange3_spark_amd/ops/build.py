@@ -59,7 +59,10 @@ def _compile(src: Path, obj: Path, device: bool) -> Path:
     if device:
         cmd[1:1] = [f"--offload-arch={ARCH}", "-ffp-contract=fast", "-munsafe-fp-atomics"]
     else:
-        cmd[1:1] = ["-x", "c++"]
+        import sysconfig
+        # host_strings.cpp reads str objects through the CPython headers; the symbols
+        # resolve against the interpreter the library is loaded into (no libpython link)
+        cmd[1:1] = ["-x", "c++", "-I", sysconfig.get_paths()["include"]]
     _run(cmd)
     return obj
 

@@ -7,6 +7,7 @@ and runs MurmurHash3_x86_32 either on the GPU (csrc/text.hip) or in the host C++
 from __future__ import annotations
 
 import ctypes as Ct
+import os
 import re
 
 import numpy as np
@@ -111,6 +112,29 @@ def arrow_strings(values):
     return offs - base, data, valid
 
 
+def pack_strings(values):
+    """(offsets int64 [n+1], bytes uint8, valid bool [n] | None, ascii) of an object array of
+    str / None.  Compact ASCII columns (the common case) are packed by the host runtime
+    (csrc/host_strings.cpp: a length pass, then a threaded copy of each string's bytes,
+    GIL released) -- ascii=True; anything else goes through pyarrow -- ascii=None (unknown:
+    the caller checks the bytes)."""
+    vals = np.asarray(values, dtype=object)
+    n = vals.shape[0]
+    if vals.ndim == 1 and vals.flags.c_contiguous and n:
+        lib = N.host()
+        offs = np.empty(n + 1, dtype=np.int64)
+        valid = np.empty(n, dtype=np.uint8)
+        tot = lib.o3s_host_ascii_lengths(vals.ctypes.data, n, offs.ctypes.data, valid.ctypes.data)
+        if tot >= 0:
+            data = np.empty(max(tot, 1), dtype=np.uint8)
+            lib.o3s_host_ascii_pack(vals.ctypes.data, n, offs.ctypes.data, data.ctypes.data,
+                                    min(16, os.cpu_count() or 1))
+            v = valid.view(bool)
+            return offs, data[:tot], (None if v.all() else v.copy()), True
+    offs, data, valid = arrow_strings(vals)
+    return offs, data, valid, None
+
+
 def device_tokenize(values, device, min_rows: int = 1):
     """Spark Tokenizer on the GPU for an ASCII string column: returns a
     :class:`~orange3_spark_amd.frame.column.DeviceTokensColumn` (tokens stay on the device
@@ -120,12 +144,13 @@ def device_tokenize(values, device, min_rows: int = 1):
     dev = torch.device(device)
     if dev.type != "cuda" or len(values) < min_rows:
         return None
-    offs, data, valid = arrow_strings(values)
-    if data.size and int(data.max()) >= 128:
+    offs, data, valid, ascii_ = pack_strings(values)
+    if not ascii_ and data.size and int(data.max()) >= 128:
         return None
     n = len(offs) - 1
     o = torch.from_numpy(np.ascontiguousarray(offs)).to(dev)
-    b = torch.from_numpy(data.copy() if data.size else np.zeros(1, np.uint8)).to(dev)
+    b = torch.from_numpy(data if data.size and data.flags.writeable else
+                         (data.copy() if data.size else np.zeros(1, np.uint8))).to(dev)
     lib = N.kernels()
     st = N.stream_of(o)
     counts = torch.empty(n, dtype=torch.int64, device=dev)

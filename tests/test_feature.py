@@ -290,3 +290,24 @@ def test_gpu_assemble_column_window_kernel(dtype, window, mode):
     rb = torch.isnan(ref).any(1)
     assert torch.equal(bad.cpu().bool(), rb) and torch.equal(gbad, bad)
     assert int(nbad) == int(rb.sum()) == int(gnbad)
+
+
+def test_native_string_packing_matches_arrow_buffers():
+    """ops/text.py pack_strings (csrc/host_strings.cpp: length pass + threaded byte copy,
+    no pyarrow) gives the Arrow (offsets, bytes, validity) of an ASCII column, and falls
+    back to pyarrow for anything that is not a compact ASCII str."""
+    from orange3_spark_amd.ops import text as TX
+    rng = np.random.default_rng(3)
+    words = np.array(["", "a", "Hello", "x y", "  lead", "tab\tsep"] + [f"w{i}" * (i % 7) for i in range(200)],
+                     dtype=object)
+    vals = words[rng.integers(0, len(words), 50_000)]
+    vals[::97] = None
+    offs, data, valid, ascii_ = TX.pack_strings(vals)
+    o2, d2, v2 = TX.arrow_strings(vals)
+    assert ascii_ is True and np.array_equal(offs, o2) and np.array_equal(data, d2) and np.array_equal(valid, v2)
+    big = np.asarray(["z" * 1000] * 20_000, dtype=object)            # > 8 MB: the threaded copy
+    offs, data, valid, _ = TX.pack_strings(big)
+    assert valid is None and offs[-1] == 20_000_000 and bytes(data[-1000:]) == b"z" * 1000
+    for odd in (["héllo", "a"], ["a", b"b"]):
+        offs, data, valid, ascii_ = TX.pack_strings(np.asarray(odd, dtype=object))
+        assert ascii_ is None
