@@ -1,7 +1,6 @@
 """Tree histogram op: gfx950 kernel (csrc/trees.hip) with a PyTorch reference."""
 from __future__ import annotations
 
-import weakref
 
 import numpy as np
 import torch
@@ -32,12 +31,11 @@ def hist_kernel_ok(bins: torch.Tensor, B: int, S: int, cls: bool) -> bool:
 
 
 # row-major bins -> the feature-major copy written in the same pass by the binning kernel
-# (models/trees.bin_features), so feature_major() needs no second pass over the matrix
-_FM: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
-
-
+# (models/trees.bin_features), so feature_major() needs no second pass over the matrix.
+# Kept as an attribute of the bins tensor itself: it lives exactly as long as the bins (a
+# WeakKeyDictionary keyed by tensors compares keys with Tensor.__eq__ on hash collisions).
 def remember_feature_major(bins: torch.Tensor, bins_t: torch.Tensor) -> None:
-    _FM[bins] = bins_t
+    bins._o3s_feature_major = bins_t
 
 
 def feature_major(bins: torch.Tensor) -> torch.Tensor | None:
@@ -46,7 +44,7 @@ def feature_major(bins: torch.Tensor) -> torch.Tensor | None:
     ``u8_transpose_kernel``, F % 4 == 0, or torch's strided copy)."""
     if not bins.is_cuda:
         return None
-    fm = _FM.get(bins)
+    fm = getattr(bins, "_o3s_feature_major", None)
     if fm is not None:
         return fm
     n, F = bins.shape
