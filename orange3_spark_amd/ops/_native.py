@@ -31,7 +31,7 @@ _SIGS: dict[str, list] = {
     "o3s_glm_grad": [c_i32, c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_u32, c_i64,
                      c_vp, c_f32, c_vp, c_i32, c_vp, c_i32, c_vp],
     "o3s_glm_grad_mixed": [c_i32, c_vp, c_i64, c_i64, c_vp, c_vp, c_vp, c_u32, c_i64, c_i64,
-                           c_vp, c_i32, c_vp, c_i32, c_i32, c_i64, c_vp, c_u32, c_u32, c_i32, c_vp],
+                           c_vp, c_i32, c_vp, c_i32, c_i64, c_vp, c_u32, c_u32, c_i32, c_vp],
     "o3s_glm_stats_mixed": [c_vp, c_i64, c_i64, c_vp, c_vp, c_u32, c_i64, c_i64, c_vp, c_i32, c_vp, c_i32, c_vp],
     "o3s_bin_features": [c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp],
     "o3s_u8_transpose": [c_vp, c_i64, c_i32, c_vp, c_vp],
@@ -92,8 +92,7 @@ _SIGS: dict[str, list] = {
     "o3s_als_rotate_to": [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp],
     "o3s_assemble": [c_vp, c_i32, c_vp, c_i32, c_i32, c_i64, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp],
     "o3s_assemble_src_size": [],
-    "o3s_assemble_cols": [c_vp, c_i32, c_i32, c_i32, c_i64, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_i32,
-                          c_vp],
+    "o3s_assemble_cols": [c_vp, c_i32, c_i32, c_i32, c_i64, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp],
     "o3s_kmeans_update": [c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
 }
 

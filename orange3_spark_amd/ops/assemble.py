@@ -4,7 +4,6 @@ invalid flags and their count (handleInvalid).  CPU tensors are handled by the c
 torch path (ml/feature.py)."""
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
@@ -22,12 +21,6 @@ def supported(t: torch.Tensor) -> bool:
     return t.is_cuda and t.dtype in _DT and (t.dim() == 1 or (t.dim() == 2 and t.stride(1) == 1))
 
 
-WINDOW = int(os.environ.get("O3S_ASM_WINDOW", "64"))
-BATCH = int(os.environ.get("O3S_ASM_BATCH", "8"))
-# window-64 / batch-8 variants: 0 = 128-row blocks, 1 = 256-row blocks (default: 4.8-4.9 TB/s
-# vs 4.2 at 100M x 256 fp32, profiles/assemble_kernel_100Mx256.json), 2 = 256 with 8-B
-# row-pair loads (fp32 columns, 8-B aligned)
-MODE = int(os.environ.get("O3S_ASM_MODE", "1"))
 
 
 def _cols_ok(sources) -> bool:
@@ -38,8 +31,7 @@ def _cols_ok(sources) -> bool:
         t.dtype == dt and t.dim() == 1 and t.stride(0) == 1 and int(w) == 1 for t, _, w in sources)
 
 
-def assemble_bf16(sources, n: int, device, path: str = "auto", window: int | None = None,
-                  batch: int | None = None, mode: int | None = None):
+def assemble_bf16(sources, n: int, device, path: str = "auto"):
     """``sources``: list of (tensor [n] or [n, >= width] row-major, valid bool [n] or None,
     width).  Returns (bf16 [n, ld] zero padded, uint8 invalid flags [n], invalid count).
     ``path``: "auto" (column-window kernel when every source is a plain float / double
@@ -72,16 +64,11 @@ def assemble_bf16(sources, n: int, device, path: str = "auto", window: int | Non
     if cols:
         if not _cols_ok(sources):
             raise ValueError("the column-window assembler needs plain float / double columns of one dtype")
-        w, b = int(window or WINDOW), int(batch or BATCH)
-        m = int(MODE if mode is None else mode) if (w, b) == (64, 8) else 0
-        if m == 2 and any(t.data_ptr() % 8 for t, _, _ in sources):
-            m = 1
-        rows = (128, 256, 256)[m]
-        per_cu = 8 if rows == 128 and w != 128 else 4
+        rows, per_cu = 256, 4                # 256-row blocks (assemble_cols_kernel)
         grid = max(1, min(N.num_cus(torch.device(device)) * per_cu * 2, -(-n // rows)))
         if grid >= 8:
             grid -= grid % 8          # the kernel's XCD-aware block walk wants G % 8 == 0
-        N.check(lib.o3s_assemble_cols(src_d.data_ptr(), _DT[sources[0][0].dtype], D, ld, n, out.data_ptr(), 0, w, b, m,
+        N.check(lib.o3s_assemble_cols(src_d.data_ptr(), _DT[sources[0][0].dtype], D, ld, n, out.data_ptr(), 0,
                                       bad.data_ptr(), nbad.data_ptr(), grid, N.stream_of(out)), "assemble_cols")
         del keep
         return out, bad, nbad, D

@@ -124,13 +124,13 @@ __global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmSrc* __rest
 }
 
 // Fast path: every source a plain [n] column of one dtype T (the common wide table of
-// float / double columns).  A block owns 64 RPL rows (128 or 256) and walks the output in
-// windows of kCW = 32, 64 or 128 columns (LDS tile 8.5 / 17 / 33 KB for bf16 out, 128 rows):
+// float / double columns).  A block owns 256 rows (4 per lane) and walks the output in
+// windows of kCW = 64 columns (LDS tile 33 KB for bf16 out):
 //   load:  wave w takes columns w, w + 4, ...; lane l reads rows l, l + 64, ... of 8 columns
-//          per batch (8 or 16; 16 or 32 independent loads in flight, each wave load a 256-B contiguous
-//          run of one column), converts and writes them transposed into an LDS tile whose
-//          row stride is an odd number of dwords (65 / 129), so the 64 lanes -- 64 rows --
-//          land on 64 different banks;
+//          per batch (32 independent loads in flight, each wave load a 256-B contiguous run
+//          of one column), converts and writes them transposed into an LDS tile whose row
+//          stride is an odd number of dwords, so the 64 lanes -- 64 rows -- land on 64
+//          different banks;
 //   store: the tile goes out row-major, 16 B per lane, each row's window one contiguous
 //          256-B (bf16) / 512-B (fp32) run.
 // Every input byte is read once as part of a long sequential run and every output line is
@@ -141,14 +141,14 @@ typedef unsigned int uint4_ __attribute__((ext_vector_type(4)));
 template <typename T>
 __device__ __forceinline__ float to_f(T v) { return (float)v; }
 
-// RPL: rows per lane (a block owns 64 RPL rows: each column is read in runs of 256 RPL
-// bytes for fp32; 256-row blocks: 4.8-4.9 TB/s vs 4.2 at 128 at 100M x 256 fp32 -> bf16);
-// V2 (fp32, even RPL): lane l holds row PAIRS 128 p + 2 l + {0, 1}, read as one 8-B load
-// per pair in full blocks -- each wave load is a 512-B run of the column.
-template <typename T, int OUT, int kCW, int kCBatch, int RPL, bool V2 = false>
+// 256-row blocks measured 4.8-4.9 TB/s against 4.2 for 128-row blocks at 100M x 256 fp32
+// -> bf16; 32- / 128-column windows, 16-column batches and 8-B row-pair loads were no
+// faster (profiles/assemble_kernel_100Mx256.json) and were removed.
+template <typename T, int OUT>
 __global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* __restrict__ srcs, int D, int ld,
                                                                  int64_t n, void* __restrict__ out,
                                                                  uint8_t* __restrict__ bad, int* __restrict__ nbad) {
+  constexpr int kCW = 64, kCBatch = 8, RPL = 4;
   constexpr int kCRows = 64 * RPL;
   constexpr int PAD = OUT == 0 ? 2 : 1;
   constexpr int LS = kCW + PAD;                       // tile row stride (elements): 65 / 129 dwords
@@ -169,8 +169,7 @@ __global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* _
   const int64_t xoff = (G % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (G / 8) + blockIdx.x / 8 : blockIdx.x;
   for (int64_t blk = xoff; blk < nblk; blk += G) {
     const int64_t row0 = blk * kCRows;
-    const bool full = row0 + kCRows <= n;
-    auto rib = [&](int i) { return V2 ? 128 * (i >> 1) + 2 * lane + (i & 1) : lane + 64 * i; };   // row in block
+    auto rib = [&](int i) { return lane + 64 * i; };   // row in block
     int64_t rr[RPL];
     bool rbad[RPL];
 #pragma unroll
@@ -187,17 +186,8 @@ __global__ __launch_bounds__(kThreads) void assemble_cols_kernel(const AsmSrc* _
           const int j = c0 + jb + 4 * q;                // wave-uniform
           if (jb + 4 * q < cw && j < D) {
             const T* p = reinterpret_cast<const T*>(srcs[j].ptr);
-            if (V2 && full) {
 #pragma unroll
-              for (int i = 0; i < RPL; i += 2) {
-                const float2 w2 = *reinterpret_cast<const float2*>(p + rr[i]);
-                v[q][i] = w2.x;
-                v[q][i + 1] = w2.y;
-              }
-            } else {
-#pragma unroll
-              for (int i = 0; i < RPL; ++i) v[q][i] = p[rr[i]];
-            }
+            for (int i = 0; i < RPL; ++i) v[q][i] = p[rr[i]];
           }
         }
 #pragma unroll
@@ -280,37 +270,20 @@ O3S_API int o3s_assemble_src_size() { return (int)sizeof(AsmSrc); }
 
 // Fast path (see assemble_cols_kernel): srcs[j] is output column j for j < D, every source a
 // contiguous [n] column of dtype src_dtype (DT_F32 or DT_F64), ld % 8 == 0, D <= 512.
-// mode (window 64, batch 8 only): 0 = 2 rows per lane (128-row blocks), 1 = 4 rows per
-// lane, 2 = 4 rows per lane as 8-B row pairs (fp32 columns 8-B aligned).
 O3S_API int o3s_assemble_cols(const void* srcs, int src_dtype, int D, int ld, int64_t n, void* out, int out_f32,
-                              int window, int batch, int mode, void* bad, void* nbad, int grid, hipStream_t st) {
+                              void* bad, void* nbad, int grid, hipStream_t st) {
   if (D <= 0 || D > kMaxSrc || ld % 8 != 0 || ld < D || n < 0 || grid <= 0) return -1;
   if (src_dtype != DT_F32 && src_dtype != DT_F64) return -2;
-  if ((window != 32 && window != 64 && window != 128) || (batch != 8 && batch != 16)) return -3;
-  if (mode < 0 || mode > 2 || (mode != 0 && (window != 64 || batch != 8))) return -3;
   if (n == 0) return 0;
-#define O3S_ASM_COLS_B(T, O, W, B, R)                                                                    \
-  hipLaunchKernelGGL((assemble_cols_kernel<T, O, W, B, R>), dim3(grid), dim3(kThreads), 0, st,           \
-                     (const AsmSrc*)srcs, D, ld, n, out, (uint8_t*)bad, (int*)nbad)
-#define O3S_ASM_COLS(T, O, W) \
-  if (batch == 8) O3S_ASM_COLS_B(T, O, W, 8, 2); else O3S_ASM_COLS_B(T, O, W, 16, 2)
-#define O3S_ASM_COLS_W(T, O)                                                                             \
-  if (window == 32) O3S_ASM_COLS(T, O, 32);                                                              \
-  else if (window == 64) {                                                                               \
-    if (mode == 0) O3S_ASM_COLS(T, O, 64);                                                               \
-    else if (mode == 1) O3S_ASM_COLS_B(T, O, 64, 8, 4);                                                  \
-    else hipLaunchKernelGGL((assemble_cols_kernel<T, O, 64, 8, 4, std::is_same<T, float>::value>), \
-                            dim3(grid), dim3(kThreads), 0, st, (const AsmSrc*)srcs, D, ld, n, out,        \
-                            (uint8_t*)bad, (int*)nbad);                                                  \
-  } else O3S_ASM_COLS(T, O, 128)
+#define O3S_ASM_COLS(T, O)                                                                               \
+  hipLaunchKernelGGL((assemble_cols_kernel<T, O>), dim3(grid), dim3(kThreads), 0, st, (const AsmSrc*)srcs, \
+                     D, ld, n, out, (uint8_t*)bad, (int*)nbad)
   if (src_dtype == DT_F32) {
-    if (out_f32) { O3S_ASM_COLS_W(float, 1); } else { O3S_ASM_COLS_W(float, 0); }
+    if (out_f32) { O3S_ASM_COLS(float, 1); } else { O3S_ASM_COLS(float, 0); }
   } else {
-    if (out_f32) { O3S_ASM_COLS_W(double, 1); } else { O3S_ASM_COLS_W(double, 0); }
+    if (out_f32) { O3S_ASM_COLS(double, 1); } else { O3S_ASM_COLS(double, 0); }
   }
-#undef O3S_ASM_COLS_W
 #undef O3S_ASM_COLS
-#undef O3S_ASM_COLS_B
   O3S_CHECK_LAUNCH();
   return 0;
 }

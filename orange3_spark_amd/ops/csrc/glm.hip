@@ -563,11 +563,9 @@ __device__ __forceinline__ void mixed_tile(
 // y / sw hold n_res + n_lin entries: the resident rows' labels, then the lineage rows'.
 // MW: minimum waves per SIMD the register allocator must allow (2 = no constraint at
 // D = 256, 174 VGPRs; 3 = 168 VGPRs with a 4-register spill outside the tile loop).
-// LW = 0: every wave walks the interleaved tile sequence (both roles per wave).
-// LW > 0: fixed roles -- waves 0..LW-1 of each block regenerate lineage tiles, the
-// other 4 - LW stream resident tiles with UR rows per lane in flight, so the load
-// pipeline never pauses for hash work (each role strides over its own tiles).
-template <int LPR, int CPL, int UNROLL, int LOSS, int MW, int LW, int UR, bool SMP>
+// Every wave walks the interleaved tile sequence (both roles per wave; fixed-role layouts
+// -- some waves regenerating, the others streaming -- measured slower and were removed).
+template <int LPR, int CPL, int UNROLL, int LOSS, int MW, bool SMP>
 __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
     const uint16_t* __restrict__ X, int64_t ld, int64_t n_res, const float* __restrict__ y,
     const float* __restrict__ sw, const float* __restrict__ y_lin, const float* __restrict__ sw_lin,
@@ -602,42 +600,25 @@ __global__ __launch_bounds__(kBlock, MW) void glm_grad_mixed_kernel(
   wshift *= kSynthShift;
   float acc_r = 0.f, acc_loss = 0.f, acc_w = 0.f;
 
-  if constexpr (LW == 0) {
-    const int64_t Tr = (n_res + RT - 1) / RT, Tl = (n_lin + RT - 1) / RT, S = Tr + Tl;
-    const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wid;
-    const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
-    if (gw < S) {
-      // lineage tiles before unit s: L = floor(s Tl / S), rem = s Tl mod S (s Tl < 2^62)
-      int64_t L = gw * Tl / S, rem = gw * Tl - L * S;
-      const int64_t q0 = nw * Tl / S, r0 = nw * Tl - q0 * S;
-      for (int64_t s = gw; s < S; s += nw) {
-        if (rem + Tl >= S)
-          mixed_tile<LPR, CPL, UNROLL, LOSS, 1, SMP>(L * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
-                                                wshift, intercept, g, c, smp_lin, acc, rs, acc_r, acc_loss,
-                                                acc_w);
-        else
-          mixed_tile<LPR, CPL, UNROLL, LOSS, 0, SMP>((s - L) * RT, n_res, X, ld, nch, y, sw, seed, row0, w,
-                                                wshift, intercept, g, c, smp_res, acc, rs, acc_r, acc_loss,
-                                                acc_w);
-        rem += r0;
-        L += q0;
-        if (rem >= S) { rem -= S; ++L; }
-      }
-    }
-  } else {
-    if (wid < LW) {
-      const int64_t Tl = (n_lin + RT - 1) / RT;
-      const int64_t nlw = (int64_t)gridDim.x * LW;
-      for (int64_t t = (int64_t)blockIdx.x * LW + wid; t < Tl; t += nlw)
-        mixed_tile<LPR, CPL, UNROLL, LOSS, 1, SMP>(t * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
-                                              wshift, intercept, g, c, smp_lin, acc, rs, acc_r, acc_loss, acc_w);
-    } else {
-      constexpr int RTR = G * UR;
-      const int64_t Tr = (n_res + RTR - 1) / RTR;
-      const int64_t nrw = (int64_t)gridDim.x * (kWavesPerBlock - LW);
-      for (int64_t t = (int64_t)blockIdx.x * (kWavesPerBlock - LW) + (wid - LW); t < Tr; t += nrw)
-        mixed_tile<LPR, CPL, UR, LOSS, 0, SMP>(t * RTR, n_res, X, ld, nch, y, sw, seed, row0, w, wshift,
-                                          intercept, g, c, smp_res, acc, rs, acc_r, acc_loss, acc_w);
+  const int64_t Tr = (n_res + RT - 1) / RT, Tl = (n_lin + RT - 1) / RT, S = Tr + Tl;
+  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wid;
+  const int64_t nw = (int64_t)gridDim.x * kWavesPerBlock;
+  if (gw < S) {
+    // lineage tiles before unit s: L = floor(s Tl / S), rem = s Tl mod S (s Tl < 2^62)
+    int64_t L = gw * Tl / S, rem = gw * Tl - L * S;
+    const int64_t q0 = nw * Tl / S, r0 = nw * Tl - q0 * S;
+    for (int64_t s = gw; s < S; s += nw) {
+      if (rem + Tl >= S)
+        mixed_tile<LPR, CPL, UNROLL, LOSS, 1, SMP>(L * RT, n_lin, X, ld, nch, y_lin, sw_lin, seed, row0, w,
+                                              wshift, intercept, g, c, smp_lin, acc, rs, acc_r, acc_loss,
+                                              acc_w);
+      else
+        mixed_tile<LPR, CPL, UNROLL, LOSS, 0, SMP>((s - L) * RT, n_res, X, ld, nch, y, sw, seed, row0, w,
+                                              wshift, intercept, g, c, smp_res, acc, rs, acc_r, acc_loss,
+                                              acc_w);
+      rem += r0;
+      L += q0;
+      if (rem >= S) { rem -= S; ++L; }
     }
   }
 #pragma unroll
@@ -1209,23 +1190,22 @@ O3S_API int o3s_glm_grad(int loss, int src, const void* X, int64_t ld, int64_t n
   return 0;
 }
 
-template <int L, int C, int MW, int LW, int UR, bool SMP = false>
+template <int L, int C, int MW, bool SMP = false>
 static void launch_mixed(int loss, int grid, hipStream_t st, const uint16_t* X, int64_t ld, int64_t n_res,
                          const float* y, const float* sw, const float* y_lin, const float* sw_lin, const float* coef,
                          const float* b, uint32_t seed, int64_t row0, int64_t n_lin, float* partial, int pstride,
                          int64_t res_row0, const int64_t* t_dev, uint32_t sseed, uint32_t sthr, int pacc) {
   constexpr int U = C >= 8 ? 1 : 8 / C;
-  constexpr int UR2 = UR > 0 ? UR : U;
   if (loss == LOSS_LOGISTIC)
-    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_LOGISTIC, MW, LW, UR2, SMP>), dim3(grid), dim3(kBlock), 0,
+    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_LOGISTIC, MW, SMP>), dim3(grid), dim3(kBlock), 0,
                        st, X, ld, n_res, y, sw, y_lin, sw_lin, coef, b, seed, row0, n_lin, partial, pstride,
                        res_row0, t_dev, sseed, sthr, pacc);
   else if (loss == LOSS_HINGE)
-    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_HINGE, MW, LW, UR2, SMP>), dim3(grid), dim3(kBlock), 0,
+    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_HINGE, MW, SMP>), dim3(grid), dim3(kBlock), 0,
                        st, X, ld, n_res, y, sw, y_lin, sw_lin, coef, b, seed, row0, n_lin, partial, pstride,
                        res_row0, t_dev, sseed, sthr, pacc);
   else
-    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_SQUARED, MW, LW, UR2, SMP>), dim3(grid), dim3(kBlock), 0,
+    hipLaunchKernelGGL((glm_grad_mixed_kernel<L, C, U, LOSS_SQUARED, MW, SMP>), dim3(grid), dim3(kBlock), 0,
                        st, X, ld, n_res, y, sw, y_lin, sw_lin, coef, b, seed, row0, n_lin, partial, pstride,
                        res_row0, t_dev, sseed, sthr, pacc);
 }
@@ -1234,15 +1214,13 @@ static void launch_mixed(int loss, int grid, hipStream_t st, const uint16_t* X, 
 // of X plus n_lin synthetic rows starting at global row row0; y / sw cover all
 // n_res + n_lin rows.  Same out / coef / partial
 // contract as o3s_glm_grad (out is overwritten).  waves: 3 asks the register allocator
-// for 3 waves/SIMD (see glm_grad_mixed_kernel), anything else 2.  mode: 0 = interleaved
-// roles; 1..3 = that many lineage waves per block (fixed roles); 10 + LW = fixed roles
-// with 4 resident rows in flight per lane.  Mini-batch sampling: res_row0 is the global
+// for 3 waves/SIMD (see glm_grad_mixed_kernel), anything else 2.  Mini-batch sampling: res_row0 is the global
 // index of resident row 0, t_dev (may be null = iteration 1) the device step counter,
 // sthr = fraction * 2^24 (>= 2^24: no sampling), sseed the sampling seed.
 O3S_API int o3s_glm_grad_mixed(int loss, const void* X, int64_t ld, int64_t n_res, const float* y,
                                const float* sw, const float* coef, uint32_t seed, int64_t row0,
                                int64_t n_lin, float* partial, int grid, double* out, int waves,
-                               int mode, int64_t res_row0, const int64_t* t_dev, uint32_t sseed,
+                               int64_t res_row0, const int64_t* t_dev, uint32_t sseed,
                                uint32_t sthr, int splits, hipStream_t st) {
   const int nch = (int)(ld / 8);
   const int lpr = pick_lpr(nch), cpl = pick_cpl(nch);
@@ -1253,32 +1231,22 @@ O3S_API int o3s_glm_grad_mixed(int loss, const void* X, int64_t ld, int64_t n_re
   else if (cpl == 2) { lpr_s = 32; cpl_s = 4; }
   const uint16_t* Xh = (const uint16_t*)X;
   const float* b = coef + dpad;
-  const bool smp = sthr < (1u << 24);     // sampling: interleaved-role layouts (mode 0) only
+  const bool smp = sthr < (1u << 24);
 #define O3S_MX(L, C)                                                                                  \
   if (!done && lpr_s == L && cpl_s == C) {                                                            \
     done = true;                                                                                      \
-    if (mode == 0 && waves == 3 && smp)                                                               \
-      launch_mixed<L, C, 3, 0, 0, true>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0,  \
-                                        NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                    \
-    else if (mode == 0 && waves == 3)                                                                 \
-      launch_mixed<L, C, 3, 0, 0>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
-    else if (mode == 0 && smp)                                                                        \
-      launch_mixed<L, C, 2, 0, 0, true>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);       \
-    else if (mode == 0)                                                                               \
-      launch_mixed<L, C, 2, 0, 0>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
+    if (waves == 3 && smp)                                                                            \
+      launch_mixed<L, C, 3, true>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS,     \
+                                  pstride, RR0, t_dev, sseed, sthr, k > 0);                                     \
+    else if (waves == 3)                                                                              \
+      launch_mixed<L, C, 3>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride,  \
+                            RR0, t_dev, sseed, sthr, k > 0);                                                    \
     else if (smp)                                                                                     \
-      done = false;                                                                                   \
-    else if (mode == 1)                                                                               \
-      launch_mixed<L, C, 3, 1, 0>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
-    else if (mode == 2)                                                                               \
-      launch_mixed<L, C, 3, 2, 0>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
-    else if (mode == 3)                                                                               \
-      launch_mixed<L, C, 3, 3, 0>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
-    else if (mode == 12)                                                                              \
-      launch_mixed<L, C, 3, 2, 4>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
-    else if (mode == 11)                                                                              \
-      launch_mixed<L, C, 3, 1, 4>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride, RR0, t_dev, sseed, sthr, k > 0);                   \
-    else done = false;                                                                                \
+      launch_mixed<L, C, 2, true>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS,     \
+                                  pstride, RR0, t_dev, sseed, sthr, k > 0);                                     \
+    else                                                                                              \
+      launch_mixed<L, C, 2>(loss, grid, st, XS, ld, NR, YR, SWR, YL, SWL, coef, b, seed, RL0, NL, PS, pstride,  \
+                            RR0, t_dev, sseed, sthr, k > 0);                                                    \
   }
   // splits > 1: the pass runs as that many launches over consecutive 1/splits slices of
   // the resident and of the lineage rows; later slices add their block sums into the

@@ -234,9 +234,6 @@ def glm_grad_synth(n: int, ld: int, d: int, seed: int, row0: int, wtrue: torch.T
 
 # waves/SIMD the mixed kernel is register-allocated for (2 or 3; tools/sweep_glm_mixed.sh)
 MIX_WAVES = int(os.environ.get("O3S_GLM_MIX_WAVES", "3"))
-# 0 = every wave interleaves both roles; 1..3 = lineage waves per 4-wave block (fixed
-# roles); 11/12 = fixed roles with 4 resident rows in flight per lane
-MIX_MODE = int(os.environ.get("O3S_GLM_MIX_MODE", "0"))
 # waves/SIMD the fused summarizer kernel is compiled for (2: no spill, 3: 6-VGPR spill)
 STATS_WAVES = int(os.environ.get("O3S_GLM_STATS_WAVES", "2"))
 # rows per launch slice of a mixed pass (csrc/glm.hip o3s_glm_grad_mixed ``splits``): long
@@ -303,8 +300,7 @@ def glm_grad_mixed(X: torch.Tensor, y: torch.Tensor, sw: torch.Tensor | None, n_
     cf = _coef_buf(coef, ws.dpad, ws.device, intercept=intercept)
     N.check(N.kernels().o3s_glm_grad_mixed(loss, X.data_ptr(), ld, nr, y.data_ptr(), N.ptr(sw),
                                            cf.data_ptr(), seed & _MASK, row0, n_lin, ws.partial.data_ptr(),
-                                           ws.grid, ws.out.data_ptr(), MIX_WAVES,
-                                           MIX_MODE if thr >= 1 << 24 else 0, int(res_row0),
+                                           ws.grid, ws.out.data_ptr(), MIX_WAVES, int(res_row0),
                                            N.ptr(t_dev), int(sample_seed) & _MASK, thr, mix_splits(nr + n_lin),
                                            N.stream_of(X)),
             "glm_grad_mixed")

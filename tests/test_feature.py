@@ -262,12 +262,10 @@ def test_gpu_vector_assembler_fused_kernel_matches_torch(handle):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["float32", "float64"])
-@pytest.mark.parametrize("window,mode", [(32, 0), (64, 0), (128, 0), (64, 1), (64, 2)])
-def test_gpu_assemble_column_window_kernel(dtype, window, mode):
+def test_gpu_assemble_column_window_kernel(dtype):
     """assemble_cols_kernel (plain float / double columns, LDS-transposed windows) ==
     the generic gather kernel == a torch reference: several windows with a partial last
-    one, a partial last row block, null masks and NaNs flagged per row; mode: 128 / 256-row
-    blocks, 8-B row-pair loads."""
+    one, a partial last row block, null masks and NaNs flagged per row."""
     import torch
     from orange3_spark_amd.ops import assemble as AS
     dev = torch.device("cuda", 0)
@@ -279,7 +277,7 @@ def test_gpu_assemble_column_window_kernel(dtype, window, mode):
     valid = torch.ones(n, dtype=torch.bool)
     valid[::331] = False
     srcs = [(c.to(dev), valid.to(dev) if j == 100 else None, 1) for j, c in enumerate(cols)]
-    out, bad, nbad, d = AS.assemble_bf16(srcs, n, dev, path="cols", window=window, mode=mode)
+    out, bad, nbad, d = AS.assemble_bf16(srcs, n, dev, path="cols")
     gen, gbad, gnbad, _ = AS.assemble_bf16(srcs, n, dev, path="generic")
     ref = torch.stack([c.float() for c in cols], 1)
     ref[:, 100] = torch.where(valid, ref[:, 100], torch.full_like(ref[:, 100], float("nan")))

@@ -27,13 +27,7 @@ def main():
     cols = [torch.empty(n, dtype=dt, device=dev).uniform_(-1, 1) for _ in range(a.features)]
     srcs = [(c, None, 1) for c in cols]
     res = {"rows": n, "features": a.features, "dtype": a.dtype}
-    for name, kw in (("generic", dict(path="generic")), ("cols_w32", dict(path="cols", window=32)),
-                     ("cols_w64", dict(path="cols", window=64, mode=0)),
-                     ("cols_w128", dict(path="cols", window=128)),
-                     ("cols_w64_b16", dict(path="cols", window=64, batch=16)),
-                     ("cols_w32_b16", dict(path="cols", window=32, batch=16)),
-                     ("cols_w64_rows256", dict(path="cols", window=64, batch=8, mode=1)),
-                     ("cols_w64_rows256_pairs", dict(path="cols", window=64, batch=8, mode=2))):
+    for name, kw in (("generic", dict(path="generic")), ("cols", dict(path="cols"))):
         out = AS.assemble_bf16(srcs, n, dev, **kw)
         del out
         torch.cuda.synchronize()
