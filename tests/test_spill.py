@@ -282,7 +282,8 @@ def test_gpu_scalers_and_union_on_spilled_rows(tmp_path):
     from orange3_spark_amd.ml.feature import StandardScaler
     n, d = 200_000, 16
     path, names = _write_parquet(tmp_path, n=n, d=d, seed=4)
-    s = _session("cuda", budget=n * 64 * 2 // 4)
+    from orange3_spark_amd.ops.glm import padded_width
+    s = _session("cuda", budget=n * padded_width(d) * 2 // 4)     # a quarter of the bf16 rows
     df = VectorAssembler(inputCols=names, outputCol="features").transform(s.read.parquet(path))
     r = _session("cuda")
     rdf = VectorAssembler(inputCols=names, outputCol="features").transform(r.read.parquet(path))
