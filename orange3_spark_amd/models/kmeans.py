@@ -149,13 +149,15 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
         # all k steps in ONE block (kmeanspp_kernel): ~10 kernels per step otherwise
         from ..ops import _native as N
         Pc, wc, pc = P.contiguous(), w.to(torch.float64).contiguous(), pn.contiguous()
+        PT = Pc.t().contiguous()                  # coalesced candidate reads in the kernel
         Uc = U.contiguous()
         d2 = torch.empty(m, dtype=torch.float64, device=dev)
         cs = torch.empty(m, dtype=torch.float64, device=dev)
+        cd = torch.empty((trials, m), dtype=torch.float64, device=dev)
         picks32 = torch.empty(k, dtype=torch.int32, device=dev)
-        N.check(N.kernels().o3s_kmeanspp(Pc.data_ptr(), wc.data_ptr(), pc.data_ptr(), m, P.shape[1], k, trials,
-                                         Uc.data_ptr(), d2.data_ptr(), cs.data_ptr(), picks32.data_ptr(),
-                                         N.stream_of(Pc)), "kmeanspp")
+        N.check(N.kernels().o3s_kmeanspp(Pc.data_ptr(), PT.data_ptr(), wc.data_ptr(), pc.data_ptr(), m, P.shape[1], k,
+                                         trials, Uc.data_ptr(), d2.data_ptr(), cs.data_ptr(), cd.data_ptr(),
+                                         picks32.data_ptr(), N.stream_of(Pc)), "kmeanspp")
         picks = picks32.to(torch.int64)
     else:
         first = draw(0, w, 1)[0]
@@ -178,9 +180,17 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
 
 
 def _local_lloyd(P, w, C, k, iters):
+    # GPU: the candidates are assigned by the split-precision assign kernel (fp32-exact
+    # argmin, no GEMM library call: a process's first hipBLASLt call cost ~0.1 s of a cold
+    # fit, profiles/kmeans_init_phases_r5.json); elsewhere the fp64 distance GEMM
+    Pf = P.float().contiguous() if P.is_cuda else None
+    use_kernel = Pf is not None and K.kernel_ok(Pf)
     for _ in range(iters):
-        dist = (P * P).sum(1, keepdim=True) - 2 * P @ C.T + (C * C).sum(1)[None, :]
-        a = dist.argmin(1)
+        if use_kernel:
+            a = K.assign(Pf, C.float(), mode="split", need_dist=False)[0].long()
+        else:
+            dist = (P * P).sum(1, keepdim=True) - 2 * P @ C.T + (C * C).sum(1)[None, :]
+            a = dist.argmin(1)
         sums = torch.zeros_like(C).index_add_(0, a, P * w[:, None])
         cnt = torch.zeros(k, dtype=P.dtype, device=P.device).index_add_(0, a, w)
         newC = torch.where(cnt[:, None] > 0, sums / cnt.clamp_min(1e-300)[:, None], C)

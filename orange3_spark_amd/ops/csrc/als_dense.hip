@@ -30,10 +30,12 @@
 //        multipliers by v_readlane inside 4-column blocks, a float4 LDS broadcast for the
 //        deferred rank-4 update); lanes 32-63 run the same recurrence on the identity,
 //        giving X_p = L_pp^-1, and y_p = X_p r_p;
-//     B  U_pi = X_p S_pi on v_mfma_f32_32x32x2_f32, B operand = the tile's own registers;
-//        r_i -= U_pi^T y_p (a sum over the tile's registers + one lane swap);
-//     C  S_ji -= U_pj^T U_pi with BOTH operands straight from registers (register v of
-//        tile (p, j) is exactly the A fragment that pairs with register v of tile (p, i));
+//     B  U_pi = X_p S_pi as bf16x3 on v_mfma_f32_32x32x16_bf16 (6 instead of 16
+//        v_mfma_f32_32x32x2_f32: a quarter of the matrix-pipe cycles), B operand = the
+//        tile's own registers split hi / lo; r_i -= U_pi^T y_p (a sum over the tile's
+//        registers + one lane swap);
+//     C  S_ji -= U_pj^T U_pi, bf16x3 with BOTH operands straight from registers (register
+//        v of tile (p, j) pairs with register v of tile (p, i): the same k index);
 //   backward U x = y: per p the products U_pi x_i are summed across lanes through one LDS
 //   transpose, x_p = X_p^T t with X_p parked in the diagonal tile's registers.
 // * implicit G: its upper tiles live in LDS once per block, in accumulator order (one
@@ -114,6 +116,17 @@ __device__ __forceinline__ void split8(const float (&z)[8], bf16x8_t& hi, bf16x8
   }
   hi = __builtin_bit_cast(bf16x8_t, H);
   lo = __builtin_bit_cast(bf16x8_t, L);
+}
+
+// registers 8 m .. 8 m + 7 of an accumulator tile -> bf16 hi / lo MFMA fragments
+__device__ __forceinline__ void split_half(const f32x16_t& t, int m, bf16x8_t& hi, bf16x8_t& lo) {
+  float z[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) z[k] = t[8 * m + k];
+  split8(z, hi, lo);
+}
+__device__ __forceinline__ bf16x8_t neg8(bf16x8_t v) {
+  return __builtin_bit_cast(bf16x8_t, __builtin_bit_cast(u32x4_t, v) ^ 0x80008000u);
 }
 
 template <int R, bool IMPL, bool DBG = false>
@@ -357,7 +370,17 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
       }
 #pragma unroll
       for (int vv = 0; vv < 16; ++vv) dg[vv] = scr[rowof(vv, h) * 33 + q];   // X_p, C layout
-      // B: U_pi = X_p S_pi; r_i -= U_pi^T y_p
+      // B: U_pi = X_p S_pi; r_i -= U_pi^T y_p.  bf16x3 on v_mfma_f32_32x32x16_bf16 (the
+      // Gram's numerics): register v of a tile is k-slot v & 7 of k-block v >> 3 for BOTH
+      // operands (lane half h holds k = rowof(v, h)), so the k pairing is consistent
+      bf16x8_t xh[2], xl[2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        float z8[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) z8[k] = xa[8 * m + k];
+        split8(z8, xh[m], xl[m]);
+      }
 #pragma unroll
       for (int i = p + 1; i < NT; ++i) {
         f32x16_t& s = acc[tix<NT>(p, i)];
@@ -365,7 +388,13 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
 #pragma unroll
         for (int vv = 0; vv < 16; ++vv) z[vv] = 0.f;
 #pragma unroll
-        for (int vv = 0; vv < 16; ++vv) z = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[vv], s[vv], z, 0, 0, 0);
+        for (int m = 0; m < 2; ++m) {
+          bf16x8_t sh, sl;
+          split_half(s, m, sh, sl);
+          z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[m], sh, z, 0, 0, 0);
+          z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xl[m], sh, z, 0, 0, 0);
+          z = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xh[m], sl, z, 0, 0, 0);
+        }
         s = z;
         float part = 0.f;
 #pragma unroll
@@ -374,17 +403,27 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
         if (h == 0) sr[32 * i + q] -= part;
       }
       lane_sync();
-      // C: S_ji -= U_pj^T U_pi, operands straight from the panel tiles' registers
+      // C: S_ji -= U_pj^T U_pi, operands straight from the panel tiles' registers (bf16x3,
+      // -U_pj by flipping the bf16 sign bits)
+      bf16x8_t uh[NT][2], ul[NT][2];
 #pragma unroll
-      for (int j = p + 1; j < NT; ++j)
+      for (int i = p + 1; i < NT; ++i)
 #pragma unroll
-        for (int i = j; i < NT; ++i) {
-          const f32x16_t& uj = acc[tix<NT>(p, j)];
-          const f32x16_t& ui = acc[tix<NT>(p, i)];
-          f32x16_t& s = acc[tix<NT>(j, i)];
+        for (int m = 0; m < 2; ++m) split_half(acc[tix<NT>(p, i)], m, uh[i][m], ul[i][m]);
 #pragma unroll
-          for (int vv = 0; vv < 16; ++vv) s = __builtin_amdgcn_mfma_f32_32x32x2f32(-uj[vv], ui[vv], s, 0, 0, 0);
+      for (int j = p + 1; j < NT; ++j) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const bf16x8_t nh = neg8(uh[j][m]), nl = neg8(ul[j][m]);
+#pragma unroll
+          for (int i = j; i < NT; ++i) {
+            f32x16_t& s = acc[tix<NT>(j, i)];
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(nh, uh[i][m], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(nl, uh[i][m], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(nh, ul[i][m], s, 0, 0, 0);
+          }
         }
+      }
     }
 
     if (DBG && idx < 64) {                // diagnostic dump: U / X_p tiles and y

@@ -1248,13 +1248,19 @@ __device__ int pp_draw(const double* __restrict__ cs, int m, double tot, double 
   return lo < m - 1 ? lo : m - 1;
 }
 
+// PT: the candidates transposed ([D][m]): thread i reads coordinate d of candidate i at
+// PT[d m + i], so a wave's loads are one contiguous 512-B run (the row-major walk read 64
+// rows 1 KB apart per instruction: 0.53 s for k = 1024 over ~4K candidates,
+// profiles/kmeans_init_phases_r5.json).  cd [trials][m]: the trial candidates' distances,
+// kept so the d2 update after the pick needs no second pass over the candidates.
 template <int TRIALS>
 __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __restrict__ P,
+                                                              const double* __restrict__ PT,
                                                               const double* __restrict__ w,
                                                               const double* __restrict__ pn, int m, int D, int k,
                                                               const double* __restrict__ U,
                                                               double* __restrict__ d2, double* __restrict__ cs,
-                                                              int* __restrict__ picks) {
+                                                              double* __restrict__ cd, int* __restrict__ picks) {
   constexpr int trials = TRIALS;          // compile-time: the per-draw arrays stay in registers
   extern __shared__ double sm[];          // [trials][D] candidate rows, then part[1024], red[16]
   double* const sc = sm;
@@ -1270,10 +1276,12 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
   __syncthreads();
   const int first = cand[0];
   if (tid == 0) picks[0] = first;
+  for (int e = tid; e < D; e += kPPThreads) sc[e] = P[(int64_t)first * D + e];
+  __syncthreads();
   for (int i = tid; i < m; i += kPPThreads) {
     double s = 0.0;
     for (int d = 0; d < D; ++d) {
-      const double t = P[(int64_t)i * D + d] - P[(int64_t)first * D + d];
+      const double t = PT[(int64_t)d * m + i] - sc[d];
       s += t * t;
     }
     d2[i] = s;
@@ -1284,24 +1292,27 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
     if (tid < trials) cand[tid] = pp_draw(cs, m, tot, U[(int64_t)t * nt + tid]);
     __syncthreads();
     for (int e = tid; e < trials * D; e += kPPThreads) sc[e] = P[(int64_t)cand[e / D] * D + e % D];
+    double pc[trials];
+#pragma unroll
+    for (int j = 0; j < trials; ++j) pc[j] = pn[cand[j]];
     __syncthreads();
     double acc[trials];
 #pragma unroll
     for (int j = 0; j < trials; ++j) acc[j] = 0.0;
     for (int i = tid; i < m; i += kPPThreads) {
-      const double* p = P + (int64_t)i * D;
       double dot[trials];
 #pragma unroll
       for (int j = 0; j < trials; ++j) dot[j] = 0.0;
       for (int d = 0; d < D; ++d) {
-        const double x = p[d];
+        const double x = PT[(int64_t)d * m + i];
 #pragma unroll
         for (int j = 0; j < trials; ++j) dot[j] = fma(x, sc[j * D + d], dot[j]);
       }
-      const double wi = w[i], di = d2[i];
+      const double wi = w[i], di = d2[i], pi = pn[i];
 #pragma unroll
       for (int j = 0; j < trials; ++j) {
-        const double c = fmax(pn[i] + pn[cand[j]] - 2.0 * dot[j], 0.0);
+        const double c = fmax(pi + pc[j] - 2.0 * dot[j], 0.0);
+        cd[(int64_t)j * m + i] = c;
         acc[j] += wi * fmin(di, c);
       }
     }
@@ -1314,31 +1325,28 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
     int best = 0;
     for (int j = 1; j < trials; ++j)
       if (pots[j] < pots[best]) best = j;
-    const int c = cand[best];
-    if (tid == 0) picks[t] = c;
-    // d2 = min(d2, |p - c|^2), the same formula
-    for (int i = tid; i < m; i += kPPThreads) {
-      const double* p = P + (int64_t)i * D;
-      double dot = 0.0;
-      for (int d = 0; d < D; ++d) dot = fma(p[d], sc[best * D + d], dot);
-      const double cc = fmax(pn[i] + pn[c] - 2.0 * dot, 0.0);
-      d2[i] = fmin(d2[i], cc);
-    }
+    if (tid == 0) picks[t] = cand[best];
+    // d2 = min(d2, |p - c|^2): this thread's own cd entries (same i walk as above)
+    for (int i = tid; i < m; i += kPPThreads) d2[i] = fmin(d2[i], cd[(int64_t)best * m + i]);
     __syncthreads();
   }
 }
 }  // namespace
 
-// P [m][D] fp64 candidates, w [m] weights, pn [m] = |p|^2, U [k][trials + 1] uniforms;
-// ws: d2 [m], cs [m] fp64 scratch; picks [k] int32 out.  trials <= 16.
-O3S_API int o3s_kmeanspp(const double* P, const double* w, const double* pn, int m, int D, int k, int trials,
-                         const double* U, double* d2, double* cs, int* picks, hipStream_t st) {
+// P [m][D] fp64 candidates and PT = P^T [D][m], w [m] weights, pn [m] = |p|^2, U [k][trials
+// + 1] uniforms; ws: d2 [m], cs [m], cd [trials][m] fp64 scratch; picks [k] int32 out.
+// trials <= 16.
+O3S_API int o3s_kmeanspp(const double* P, const double* PT, const double* w, const double* pn, int m, int D, int k,
+                         int trials, const double* U, double* d2, double* cs, double* cd, int* picks, hipStream_t st) {
   if (m <= 0 || k <= 0 || D <= 0 || trials < 1 || trials > 16) return -1;
   const size_t lds = sizeof(double) * ((size_t)trials * D + kPPThreads + 16);
   if (lds > 160 * 1024 - 256) return -2;
   switch (trials) {
-#define O3S_PP(T) \
-    case T: hipLaunchKernelGGL(kmeanspp_kernel<T>, dim3(1), dim3(kPPThreads), lds, st, P, w, pn, m, D, k, U, d2, cs, picks); break;
+#define O3S_PP(T)                                                                                           \
+    case T:                                                                                                 \
+      hipLaunchKernelGGL(kmeanspp_kernel<T>, dim3(1), dim3(kPPThreads), lds, st, P, PT, w, pn, m, D, k, U, d2, cs, \
+                         cd, picks);                                                                        \
+      break;
     O3S_PP(1) O3S_PP(2) O3S_PP(3) O3S_PP(4) O3S_PP(5) O3S_PP(6) O3S_PP(7) O3S_PP(8)
     O3S_PP(9) O3S_PP(10) O3S_PP(11) O3S_PP(12) O3S_PP(13) O3S_PP(14) O3S_PP(15) O3S_PP(16)
 #undef O3S_PP
