@@ -70,7 +70,7 @@ def find_splits(comm, X, max_bins: int, seed: int = 0, sample: int | None = None
 def _thresholds(splits: list, F: int, device):
     T_ = max((len(s) for s in splits), default=0) + 1
     Tp = 1 << max(0, (T_ - 1).bit_length())
-    if Tp > 256 or 4 * F * (Tp + 1) > 160 * 1024:
+    if Tp > 256 or 4 * F * (Tp + 1) + F * 68 > 160 * 1024:      # thresholds + the [F][64] bin tile
         return None, Tp
     th = np.full((F, Tp), np.inf, dtype=np.float32)
     for f, s in enumerate(splits):

@@ -218,8 +218,13 @@ def test_gpu_bin_features_matches_bucketize(gpu, n, F, nb):
     for f in range(F):
         t = torch.as_tensor(splits[f], dtype=torch.float32)
         ref[:, f] = torch.bucketize(X[:, f], t).to(torch.uint8) if t.numel() else 0
-    got = TR.bin_features(X.to(gpu), splits).cpu()
+    got_d = TR.bin_features(X.to(gpu), splits)
+    got = got_d.cpu()
     assert torch.equal(got, ref)
+    from orange3_spark_amd.ops import trees as T
+    fm = getattr(got_d, "_o3s_feature_major", None)       # written by the binning kernel itself
+    assert fm is not None and torch.equal(fm.cpu(), ref.t().contiguous())
+    assert T.feature_major(got_d) is fm
 
 
 def test_tree_models_predict_leaf_and_evaluate(cpu):
