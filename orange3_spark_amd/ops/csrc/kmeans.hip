@@ -1194,7 +1194,8 @@ O3S_API int o3s_kmeans_update(const float* X, int64_t n, int64_t ldx, int D, con
 // - 2 p.c form of the torch reference (models/kmeans._local_kmeanspp), draws from the
 // same counter-hash uniforms U [k][trials + 1] (so CPU and GPU pick from the same draws).
 namespace {
-constexpr int kPPThreads = 1024;
+constexpr int kPPThreads = 512;
+constexpr int kPPU = 16;                   // coordinates loaded per round
 
 __device__ double pp_block_sum(double v, double* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1262,9 +1263,10 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
                                                               double* __restrict__ d2, double* __restrict__ cs,
                                                               double* __restrict__ cd, int* __restrict__ picks) {
   constexpr int trials = TRIALS;          // compile-time: the per-draw arrays stay in registers
-  extern __shared__ double sm[];          // [trials][D] candidate rows, then part[1024], red[16]
+  extern __shared__ double sm[];          // [trials][DP] candidate rows (zero padded), part[kPPThreads], red[16]
+  const int DP = (D + kPPU - 1) / kPPU * kPPU;
   double* const sc = sm;
-  double* const part = sc + trials * D;
+  double* const part = sc + trials * DP;
   double* const red = part + kPPThreads;
   __shared__ int cand[16];
   __shared__ double pots[16];
@@ -1280,9 +1282,12 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
   __syncthreads();
   for (int i = tid; i < m; i += kPPThreads) {
     double s = 0.0;
-    for (int d = 0; d < D; ++d) {
-      const double t = PT[(int64_t)d * m + i] - sc[d];
-      s += t * t;
+    for (int d0 = 0; d0 < D; d0 += kPPU) {
+      double x[kPPU];
+#pragma unroll
+      for (int u = 0; u < kPPU; ++u) x[u] = d0 + u < D ? PT[(int64_t)(d0 + u) * m + i] - sc[d0 + u] : 0.0;
+#pragma unroll
+      for (int u = 0; u < kPPU; ++u) s = fma(x[u], x[u], s);
     }
     d2[i] = s;
   }
@@ -1291,7 +1296,10 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
     tot = pp_scan(w, d2, m, cs, part);
     if (tid < trials) cand[tid] = pp_draw(cs, m, tot, U[(int64_t)t * nt + tid]);
     __syncthreads();
-    for (int e = tid; e < trials * D; e += kPPThreads) sc[e] = P[(int64_t)cand[e / D] * D + e % D];
+    for (int e = tid; e < trials * DP; e += kPPThreads) {
+      const int j = e / DP, d = e - j * DP;
+      sc[e] = d < D ? P[(int64_t)cand[j] * D + d] : 0.0;
+    }
     double pc[trials];
 #pragma unroll
     for (int j = 0; j < trials; ++j) pc[j] = pn[cand[j]];
@@ -1303,10 +1311,16 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
       double dot[trials];
 #pragma unroll
       for (int j = 0; j < trials; ++j) dot[j] = 0.0;
-      for (int d = 0; d < D; ++d) {
-        const double x = PT[(int64_t)d * m + i];
+      // 16 coordinates per round, all loads issued before the FMAs (one L2 round trip per
+      // 16 coordinates instead of one per coordinate)
+      for (int d0 = 0; d0 < D; d0 += kPPU) {
+        double x[kPPU];
 #pragma unroll
-        for (int j = 0; j < trials; ++j) dot[j] = fma(x, sc[j * D + d], dot[j]);
+        for (int u = 0; u < kPPU; ++u) x[u] = d0 + u < D ? PT[(int64_t)(d0 + u) * m + i] : 0.0;
+#pragma unroll
+        for (int u = 0; u < kPPU; ++u)
+#pragma unroll
+          for (int j = 0; j < trials; ++j) dot[j] = fma(x[u], sc[j * DP + d0 + u], dot[j]);
       }
       const double wi = w[i], di = d2[i], pi = pn[i];
 #pragma unroll
@@ -1339,7 +1353,7 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
 O3S_API int o3s_kmeanspp(const double* P, const double* PT, const double* w, const double* pn, int m, int D, int k,
                          int trials, const double* U, double* d2, double* cs, double* cd, int* picks, hipStream_t st) {
   if (m <= 0 || k <= 0 || D <= 0 || trials < 1 || trials > 16) return -1;
-  const size_t lds = sizeof(double) * ((size_t)trials * D + kPPThreads + 16);
+  const size_t lds = sizeof(double) * ((size_t)trials * ((D + kPPU - 1) / kPPU * kPPU) + kPPThreads + 16);
   if (lds > 160 * 1024 - 256) return -2;
   switch (trials) {
 #define O3S_PP(T)                                                                                           \
