@@ -19,11 +19,12 @@ DRAM behind PCIe.  Design:
   device vector columns beyond the HBM budget (``o3s.storage.hbmBudget`` bytes, default
   the session's ``o3s.memory.fraction`` of free HBM) to pinned host memory.
 * out-of-core ingest (:func:`host_resident`): a table read from parquet / the catalog /
-  pandas / Arrow whose numeric columns exceed the budget keeps them in pinned host memory
-  from the start (nothing is materialised on the device); ``VectorAssembler`` streams
-  them through the assemble kernel in row chunks straight into a SpilledVectorColumn
-  (:func:`assemble_streamed`), whose resident prefix fills the budget; GLM / KMeans / tree
-  fits consume it chunk by chunk (tree binning writes resident uint8 bins per chunk).
+  pandas / Arrow whose numeric columns exceed the budget keeps them on the host from the
+  start, zero copy over the Arrow / numpy buffers (nothing is materialised on the device);
+  ``VectorAssembler`` stages them through pinned buffers in row chunks into the assemble
+  kernel, straight into a SpilledVectorColumn (:func:`assemble_streamed`), whose resident
+  prefix fills the budget; GLM / KMeans / tree fits and the scalers consume it chunk by
+  chunk (tree binning writes resident uint8 bins per chunk).
 """
 from __future__ import annotations
 
@@ -351,8 +352,8 @@ def ingest_budget(session) -> int | None:
 
 
 def host_resident(session, nbytes: int) -> bool:
-    """True when a new table of ``nbytes`` numeric bytes must stay in pinned host memory
-    (its columns are then streamed to the device by the consumers: VectorAssembler into a
+    """True when a new table of ``nbytes`` numeric bytes must stay in host memory (its
+    columns are then streamed to the device by the consumers: VectorAssembler into a
     SpilledVectorColumn, labels moved on use)."""
     b = ingest_budget(session)
     return b is not None and nbytes > b and session.device.type == "cuda"
@@ -364,6 +365,18 @@ def pinned(t: torch.Tensor) -> torch.Tensor:
     if t.device.type != "cpu":
         t = t.cpu()
     return t.pin_memory() if torch.cuda.is_available() else t.contiguous()
+
+
+def host_array(a: np.ndarray) -> torch.Tensor:
+    """Zero-copy host tensor over a numpy array (out-of-core ingest: Arrow / pandas column
+    buffers are read-only and stay where they are -- no writable copy, no pinned copy; the
+    consumer stages row chunks through pinned buffers, see :func:`assemble_streamed`).
+    The engine never writes into a source column in place."""
+    import warnings
+    a = np.ascontiguousarray(a)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", UserWarning)       # "non-writable NumPy array"
+        return torch.from_numpy(a)
 
 
 def hbm_budget(session) -> int:
@@ -429,11 +442,13 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
     """VectorAssembler over host-resident (and/or device) columns, in row chunks.
 
     ``sources``: list of (tensor [n] or [n, w], valid [n] | None, width) -- host tensors
-    are pinned.  Each chunk's inputs are copied to the device on a side stream (chunk c+1
-    is in flight while chunk c is assembled), assembled by the bf16 gather kernel (GPU) or
-    torch (CPU), and placed either in the resident prefix (rows below the budget) or copied
-    back into the pinned host block.  Returns (SpilledVectorColumn | VectorColumn, invalid
-    count)."""
+    may be pageable (zero-copy Arrow / numpy buffers).  GPU pipeline per chunk c:
+    the host rows of chunk c+1 are copied into one of two pinned staging sets (CPU, while
+    the GPU works) and sent on a copy stream; chunk c is assembled by the bf16 gather kernel
+    on the current stream once its copy event fired; rows beyond the budget go back to the
+    pinned host block on a third stream (H2D and D2H overlap on the full-duplex link); the
+    invalid-row count stays on the device until the end.  CPU: torch, chunk by chunk.
+    Returns (SpilledVectorColumn | VectorColumn, invalid count)."""
     from ..ops import assemble as A
     from ..ops.glm import padded_width
     dev = session.device
@@ -444,71 +459,103 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
     keep = n if budget is None else max(0, min(n, budget // max(1, ld * esz)))
     in_row = sum(t.element_size() * (1 if t.dim() == 1 else t.shape[1]) for t, _, _ in sources) or 1
     rows = max(1024, int(chunk_bytes or CHUNK_BYTES) // in_row)
-    res = torch.empty((keep, ld), dtype=vdt, device=dev)
-    host = torch.empty((n - keep, ld), dtype=vdt, pin_memory=dev.type == "cuda" and torch.cuda.is_available())
-    nbad = 0
     cuda = dev.type == "cuda"
-    copy = torch.cuda.Stream(dev) if cuda else None
-    main = torch.cuda.current_stream(dev) if cuda else None
+    res = torch.empty((keep, ld), dtype=vdt, device=dev)
+    host = torch.empty((n - keep, ld), dtype=vdt, pin_memory=cuda and torch.cuda.is_available())
+    bounds = [(a, min(n, a + rows)) for a in range(0, n, rows)]
+    if not cuda:
+        nbad = 0
+        for a, b in bounds:
+            out, nb = _assemble_chunk_torch([(t[a:b], None if v is None else v[a:b], w) for t, v, w in sources],
+                                            b - a, D, ld, vdt)
+            nbad += nb
+            r = max(0, min(b, keep) - a)
+            res[a:a + r] = out[:r]
+            host[a + r - keep:b - keep] = out[r:]
+        col = SpilledVectorColumn(res, host, D) if n > keep else C.VectorColumn(res, D)
+        return col, nbad
+    copy, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    main = torch.cuda.current_stream(dev)
+    # two pinned staging sets for the host-side sources (pageable -> pinned on the CPU)
+    def _stage_buf(t):
+        shape = (rows,) + tuple(t.shape[1:])
+        return torch.empty(shape, dtype=t.dtype, pin_memory=True)
+    stg = [[(None if t.is_cuda else _stage_buf(t), None if (v is None or v.is_cuda) else _stage_buf(v))
+            for t, v, _ in sources] for _ in range(2)]
+    sent = [None, None]                         # copy event of the chunk that last used set k
 
-    def stage(a, b):
+    def stage(i):
+        a, b = bounds[i]
+        m = b - a
+        k = i & 1
+        if sent[k] is not None:
+            sent[k].synchronize()               # the H2D of chunk i-2 has drained set k
         out = []
-        ctx = torch.cuda.stream(copy) if cuda else _nullctx()
-        with ctx:
-            for t, valid, w in sources:
-                tt = t[a:b]
-                vv = None if valid is None else valid[a:b]
-                if cuda:
-                    tt = tt.to(dev, non_blocking=True)
-                    vv = None if vv is None else vv.to(dev, non_blocking=True)
-                out.append((tt, vv, w))
-        ev = None
-        if cuda:
-            ev = torch.cuda.Event()
-            ev.record(copy)
+        for (t, v, w), (tb, vb) in zip(sources, stg[k]):
+            tt, vv = t[a:b], None if v is None else v[a:b]
+            if tb is not None:
+                tb[:m].copy_(tt)
+                tt = tb[:m]
+            if vb is not None:
+                vb[:m].copy_(vv)
+                vv = vb[:m]
+            out.append((tt, vv, w))
+        with torch.cuda.stream(copy):
+            out = [(tt.to(dev, non_blocking=True), None if vv is None else vv.to(dev, non_blocking=True), w)
+                   for tt, vv, w in out]
+        ev = torch.cuda.Event()
+        ev.record(copy)
+        sent[k] = ev
         return out, ev
 
-    bounds = [(a, min(n, a + rows)) for a in range(0, n, rows)]
-    nxt = stage(*bounds[0]) if bounds else None
+    nbad_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    nxt = stage(0) if bounds else None
     for i, (a, b) in enumerate(bounds):
         cur, ev = nxt
         if i + 1 < len(bounds):
-            if cuda:
-                copy.wait_stream(main)          # staging buffers of chunk i-1 are done with
-            nxt = stage(*bounds[i + 1])
-        if cuda:
-            main.wait_event(ev)
-            for t, v, _ in cur:
-                t.record_stream(main)
-                if v is not None:
-                    v.record_stream(main)
+            nxt = stage(i + 1)                  # CPU staging + H2D of chunk i+1 overlap chunk i
+        main.wait_event(ev)
+        for t, v, _ in cur:
+            t.record_stream(main)
+            if v is not None:
+                v.record_stream(main)
         m = b - a
-        if cuda and vdt == torch.bfloat16 and all(A.supported(t) for t, _, _ in cur):
-            out, bad, nb, _ = A.assemble_bf16(cur, m, dev)
-            nbad += int(nb.item())
+        if vdt == torch.bfloat16 and all(A.supported(t) for t, _, _ in cur):
+            out, _, nb, _ = A.assemble_bf16(cur, m, dev)
+            nbad_d += nb.to(torch.int64)
         else:
-            mats = []
-            for t, v, w in cur:
-                if t.dim() == 1:
-                    x = t.to(torch.float64)
-                    if v is not None:
-                        x = torch.where(v, x, torch.full_like(x, float("nan")))
-                    mats.append(x[:, None])
-                else:
-                    mats.append(t[:, :int(w)].to(torch.float64))
-            mat = torch.cat(mats, 1)
-            nbad += int(torch.isnan(mat).any(1).sum())
-            out = torch.zeros((m, ld), dtype=vdt, device=mat.device)
-            out[:, :D] = mat.to(vdt)
+            out, nb = _assemble_chunk_torch(cur, m, D, ld, vdt)
+            nbad_d += nb
         r = max(0, min(b, keep) - a)
         if r:
             res[a:a + r].copy_(out[:r])
         if m - r:
-            host[a + r - keep:b - keep].copy_(out[r:], non_blocking=cuda)
-    if cuda:
-        torch.cuda.synchronize(dev)
+            d2h.wait_stream(main)
+            with torch.cuda.stream(d2h):
+                host[a + r - keep:b - keep].copy_(out[r:], non_blocking=True)
+            out.record_stream(d2h)
+    torch.cuda.synchronize(dev)
     col = SpilledVectorColumn(res, host, D) if n > keep else C.VectorColumn(res, D)
-    return col, nbad
+    return col, int(nbad_d.item())
+
+
+def _assemble_chunk_torch(cur, m, D, ld, vdt):
+    """(rows [m, ld] of dtype vdt, invalid count) of one chunk by torch (CPU, or GPU
+    sources the kernel does not take)."""
+    mats = []
+    for t, v, w in cur:
+        if t.dim() == 1:
+            x = t.to(torch.float64)
+            if v is not None:
+                x = torch.where(v, x, torch.full_like(x, float("nan")))
+            mats.append(x[:, None])
+        else:
+            mats.append(t[:, :int(w)].to(torch.float64))
+    mat = torch.cat(mats, 1)
+    nb = int(torch.isnan(mat).any(1).sum()) if not mat.is_cuda else torch.isnan(mat).any(1).sum()
+    out = torch.zeros((m, ld), dtype=vdt, device=mat.device)
+    out[:, :D] = mat.to(vdt)
+    return out, nb
 
 
 class _nullctx:

@@ -68,8 +68,8 @@ def arrow_to_columns(table, session) -> "OrderedDict[str, C.Column]":
         t = arr.type
         if pa.types.is_integer(t) or pa.types.is_floating(t) or pa.types.is_boolean(t):
             nb += table.num_rows * max(1, getattr(t, "bit_width", 8) // 8)
-    # out-of-core: a table whose numeric columns exceed the HBM budget keeps them pinned on
-    # the host (VectorAssembler streams them into a SpilledVectorColumn)
+    # out-of-core: a table whose numeric columns exceed the HBM budget keeps them on the host
+    # (VectorAssembler streams them into a SpilledVectorColumn)
     host = spill.host_resident(session, nb)
     for name, arr in zip(table.column_names, table.columns):
         arr = arr.combine_chunks() if hasattr(arr, "combine_chunks") else arr
@@ -90,11 +90,12 @@ def arrow_to_columns(table, session) -> "OrderedDict[str, C.Column]":
                 np_arr = arr.fill_null(0).to_numpy(zero_copy_only=False)
                 if np_arr.dtype.kind == "u":
                     np_arr = np_arr.astype(np.int64)
-                elif not np_arr.flags.writeable:
+                elif not np_arr.flags.writeable and not host:
                     np_arr = np_arr.copy()               # arrow buffers are read-only
             if host:
-                col = C.NumericColumn(spill.pinned(torch.from_numpy(np.ascontiguousarray(np_arr))),
-                                      None if mask is None else spill.pinned(torch.from_numpy(~mask)))
+                # out-of-core: the Arrow buffers themselves (zero copy); the assembler stages
+                # row chunks through pinned buffers
+                col = C.NumericColumn(spill.host_array(np_arr), None if mask is None else spill.host_array(~mask))
             else:
                 col = C.NumericColumn(torch.from_numpy(np.ascontiguousarray(np_arr)).to(dev),
                                       None if mask is None else torch.from_numpy(~mask).to(dev))

@@ -260,12 +260,12 @@ class Session:
         cols = OrderedDict()
         from .frame import spill
         nb = sum(part[k].to_numpy().nbytes for k in part.columns if part[k].dtype.kind in "fiub")
-        host = spill.host_resident(self, nb)          # out-of-core: numeric columns stay pinned on the host
+        host = spill.host_resident(self, nb)          # out-of-core: numeric columns stay on the host
         for k in part.columns:
             arr = part[k].to_numpy()
             if host and arr.dtype.kind in "fiub" and arr.ndim == 1:
                 a = arr.astype(np.int64) if arr.dtype.kind == "u" else arr
-                cols[str(k)] = C.NumericColumn(spill.pinned(torch.from_numpy(np.ascontiguousarray(a))))
+                cols[str(k)] = C.NumericColumn(spill.host_array(a))
             else:
                 cols[str(k)] = C.from_numpy(arr, self.device)
         df = DataFrame(self, cols, hi - lo)

@@ -214,7 +214,7 @@ def test_gpu_out_of_core_parquet_ingest_stays_under_budget(tmp_path):
     base = torch.cuda.memory_allocated()
     torch.cuda.reset_peak_memory_stats()
     raw = s.read.parquet(path)
-    assert raw.column_data("f0").data.device.type == "cpu" and raw.column_data("f0").data.is_pinned()
+    assert raw.column_data("f0").data.device.type == "cpu"          # zero copy over the Arrow buffer
     df = VectorAssembler(inputCols=names, outputCol="features").transform(raw)
     torch.cuda.synchronize()
     col = df.column_data("features")

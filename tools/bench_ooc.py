@@ -1,12 +1,13 @@
 """Out-of-core ingest rate: a table whose numeric columns exceed the HBM budget.
 
 Phases (each timed on its own, synchronised):
-  pin      -- ``createDataFrame(pyarrow.Table)`` with ``o3s.storage.hbmBudget`` below the
-              table: every numeric column lands in pinned host memory (no device bytes);
-  assemble -- ``VectorAssembler`` streams the pinned columns through the assemble kernel in
-              row chunks (side-stream H2D, chunk c+1 in flight while chunk c assembles) into
-              a SpilledVectorColumn: the resident prefix fills the budget, the rest is copied
-              back to pinned host rows;
+  ingest   -- ``createDataFrame(pyarrow.Table)`` with ``o3s.storage.hbmBudget`` below the
+              table: every numeric column stays on the host, zero copy over the Arrow
+              buffers (no device bytes);
+  assemble -- ``VectorAssembler`` stages row chunks of the columns through two pinned
+              buffer sets (CPU copy of chunk c+1 and its H2D overlap chunk c's kernel),
+              assembles them into a SpilledVectorColumn: the resident prefix fills the
+              budget, the rest goes back to pinned host rows on a third stream;
   h2d      -- the measured pinned host -> device copy bound on this box (one 4 GiB copy).
 
 The assemble phase moves (n x d x 4) bytes host -> device plus the spilled part of the
@@ -76,10 +77,10 @@ def main():
         h2d_gbps = 3 * src.numel() * 4 / (time.perf_counter() - t0) / 1e9
     asm_gbps = in_bytes / t_asm / 1e9
     print(json.dumps({
-        "metric": "out-of-core ingest (pinned host columns -> streamed VectorAssembler)", "rows": a.rows, "d": a.d,
+        "metric": "out-of-core ingest (host columns -> pinned staging -> streamed VectorAssembler)", "rows": a.rows, "d": a.d,
         "input_GB": round(in_bytes / 1e9, 2), "budget_GB": round(budget / 1e9, 2), "columns_on_host": on_host,
         "spilled": spilled, "resident_rows": col.resident_rows if spilled else len(col),
-        "spilled_rows": col.spilled_rows if spilled else 0, "pin_s": round(t_pin, 3), "assemble_s": round(t_asm, 3),
+        "spilled_rows": col.spilled_rows if spilled else 0, "ingest_s": round(t_pin, 3), "assemble_s": round(t_asm, 3),
         "assemble_rows_per_s": a.rows / t_asm, "assemble_input_GBps": round(asm_gbps, 2),
         "d2h_GB": round(d2h / 1e9, 2), "h2d_bound_GBps": None if h2d_gbps is None else round(h2d_gbps, 2),
         "fraction_of_h2d_bound": None if not h2d_gbps else round(asm_gbps / h2d_gbps, 3),
