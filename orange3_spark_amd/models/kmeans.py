@@ -145,7 +145,7 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
     pn = (P * P).sum(1)
     tr = trace("kmeans.init.local.seed")
     tr.__enter__()
-    if kernel and P.is_cuda and trials <= 16 and (P.shape[1] + 15) // 16 * 16 * trials * 8 + 8 * 1040 <= 150 * 1024:
+    if kernel and P.is_cuda and trials <= 16 and (P.shape[1] + 3) // 4 * 4 * trials * 8 + 8 * 1040 <= 150 * 1024:
         # all k steps in ONE block (kmeanspp_kernel): ~10 kernels per step otherwise
         from ..ops import _native as N
         Pc, wc, pc = P.contiguous(), w.to(torch.float64).contiguous(), pn.contiguous()

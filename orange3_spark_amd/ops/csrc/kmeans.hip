@@ -1195,7 +1195,7 @@ O3S_API int o3s_kmeans_update(const float* X, int64_t n, int64_t ldx, int D, con
 // same counter-hash uniforms U [k][trials + 1] (so CPU and GPU pick from the same draws).
 namespace {
 constexpr int kPPThreads = 512;
-constexpr int kPPU = 16;                   // coordinates loaded per round
+constexpr int kPPU = 4;                    // coordinates per load round
 
 __device__ double pp_block_sum(double v, double* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1307,27 +1307,47 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
     double acc[trials];
 #pragma unroll
     for (int j = 0; j < trials; ++j) acc[j] = 0.0;
-    for (int i = tid; i < m; i += kPPThreads) {
-      double dot[trials];
+    constexpr int RB = TRIALS <= 8 ? 4 : 2;
+    // register blocking: RB rows (4, or 2 past 8 trials: no spill) x trials dot products per thread, so each coordinate
+    // round loads RB x kPPU candidate values (coalesced) and trials x kPPU centre values
+    // (LDS broadcasts) for RB x trials x kPPU FMAs
+    for (int i0 = tid; i0 < m; i0 += RB * kPPThreads) {
+      double dot[RB][trials];
 #pragma unroll
-      for (int j = 0; j < trials; ++j) dot[j] = 0.0;
-      // 16 coordinates per round, all loads issued before the FMAs (one L2 round trip per
-      // 16 coordinates instead of one per coordinate)
+      for (int r = 0; r < RB; ++r)
+#pragma unroll
+        for (int j = 0; j < trials; ++j) dot[r][j] = 0.0;
       for (int d0 = 0; d0 < D; d0 += kPPU) {
-        double x[kPPU];
+        double x[RB][kPPU];
 #pragma unroll
-        for (int u = 0; u < kPPU; ++u) x[u] = d0 + u < D ? PT[(int64_t)(d0 + u) * m + i] : 0.0;
+        for (int r = 0; r < RB; ++r) {
+          const int i = i0 + r * kPPThreads;
 #pragma unroll
-        for (int u = 0; u < kPPU; ++u)
+          for (int u = 0; u < kPPU; ++u) x[r][u] = (i < m && d0 + u < D) ? PT[(int64_t)(d0 + u) * m + i] : 0.0;
+        }
 #pragma unroll
-          for (int j = 0; j < trials; ++j) dot[j] = fma(x[u], sc[j * DP + d0 + u], dot[j]);
+        for (int u = 0; u < kPPU; ++u) {
+          double c[trials];
+#pragma unroll
+          for (int j = 0; j < trials; ++j) c[j] = sc[j * DP + d0 + u];
+#pragma unroll
+          for (int r = 0; r < RB; ++r)
+#pragma unroll
+            for (int j = 0; j < trials; ++j) dot[r][j] = fma(x[r][u], c[j], dot[r][j]);
+        }
       }
-      const double wi = w[i], di = d2[i], pi = pn[i];
 #pragma unroll
-      for (int j = 0; j < trials; ++j) {
-        const double c = fmax(pi + pc[j] - 2.0 * dot[j], 0.0);
-        cd[(int64_t)j * m + i] = c;
-        acc[j] += wi * fmin(di, c);
+      for (int r = 0; r < RB; ++r) {
+        const int i = i0 + r * kPPThreads;
+        if (i < m) {
+          const double wi = w[i], di = d2[i], pi = pn[i];
+#pragma unroll
+          for (int j = 0; j < trials; ++j) {
+            const double c = fmax(pi + pc[j] - 2.0 * dot[r][j], 0.0);
+            cd[(int64_t)j * m + i] = c;
+            acc[j] += wi * fmin(di, c);
+          }
+        }
       }
     }
 #pragma unroll
