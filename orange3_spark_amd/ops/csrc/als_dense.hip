@@ -249,12 +249,21 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
 #pragma unroll
     for (int j = 0; j < NT; ++j) rh[j] = 0.f;
 
-    // ---- Gram ----
-    for (int64_t j0 = p0; j0 < p1; j0 += CH) {
+    // ---- Gram, software-pipelined in place: after the MFMAs of tile row j of step s
+    // (tiles (j, j..NT-1)), fragment block j is dead for step s and is rebuilt for step
+    // s+1 (LDS reads, sqrt(w) scaling, hi / lo split, rhs FMAs) in the same basic block as
+    // the remaining MFMAs of step s, so the scheduler can place that VALU work in the MFMA
+    // gaps (one wave per SIMD hides ~5 single-issue instructions per
+    // v_mfma_f32_32x32x16_bf16) without a second fragment set (the registers are full at
+    // rank 128).  The ring slot of step s is read out one iteration earlier, so
+    // produce() still keeps two steps in flight. ----
+    auto advance = [&]() {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot being refilled is read out
       produce();
       wait_steps<D::NIS>(issued - 1 - consumed);
-      const float* sl = ring + cslot * SLOT;
+    };
+    float sw[8], bb[8];
+    auto step_scale = [&](int64_t j0) {            // sqrt(w) and b of the step's 8 ratings per lane half
       const float* wb = swb + cslot * 32;
       const int nv = (int)(p1 - j0 < CH ? p1 - j0 : CH);
       const float4_ w0 = *reinterpret_cast<const float4_*>(wb + 8 * h);
@@ -263,37 +272,57 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
       const float4_ b1 = *reinterpret_cast<const float4_*>(wb + 16 + 8 * h + 4);
       const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-      float sw[8], bb[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const bool ok = 8 * h + k < nv;
-        sw[k] = ok ? __builtin_sqrtf(fmaxf(wv[k], 0.f)) : 0.f;
+        sw[k] = ok ? __builtin_amdgcn_sqrtf(fmaxf(wv[k], 0.f)) : 0.f;   // v_sqrt_f32 (1 ulp; sqrtf expands to ~12 VALU)
         bb[k] = ok ? bv[k] : 0.f;
       }
-      bf16x8_t hi[NT], lo[NT];
+    };
+    bf16x8_t hi[NT], lo[NT];
+    auto load_block = [&](int j) {                 // fragment block j of the step in cslot
+      const float* sl = ring + cslot * SLOT;
+      float y[8], z[8];
 #pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        float y[8], z[8];
+      for (int k = 0; k < 8; ++k) y[k] = sl[(8 * h + k) * RS + 32 * j + q];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) y[k] = sl[(8 * h + k) * RS + 32 * j + q];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          rh[j] = fmaf(bb[k], y[k], rh[j]);
-          z[k] = sw[k] * y[k];
-        }
-        split8(z, hi[j], lo[j]);
+      for (int k = 0; k < 8; ++k) {
+        rh[j] = fmaf(bb[k], y[k], rh[j]);
+        z[k] = sw[k] * y[k];
       }
+      split8(z, hi[j], lo[j]);
+    };
+    auto mfma_row = [&](int j) {                   // tiles (j, j..NT-1) of the current step
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
-#pragma unroll
-        for (int i = j; i < NT; ++i) {
-          f32x16_t& a = acc[tix<NT>(j, i)];
-          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi[j], hi[i], a, 0, 0, 0);
-          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lo[j], hi[i], a, 0, 0, 0);
-          a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi[j], lo[i], a, 0, 0, 0);
-        }
+      for (int i = j; i < NT; ++i) {
+        f32x16_t& a = acc[tix<NT>(j, i)];
+        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi[j], hi[i], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(lo[j], hi[i], a, 0, 0, 0);
+        a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(hi[j], lo[i], a, 0, 0, 0);
+      }
+    };
+    auto next_slot = [&]() {
       ++consumed;
       cslot = cslot + 1 == DEPTH ? 0 : cslot + 1;
+    };
+    if (p1 > p0) {
+      advance();
+      step_scale(p0);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) load_block(j);
+      next_slot();
+      for (int64_t j0 = p0 + CH; j0 < p1; j0 += CH) {
+        advance();
+        step_scale(j0);                 // step s+1's scales ...
+#pragma unroll
+        for (int j = 0; j < NT; ++j) {
+          mfma_row(j);                  // ... step s's tile row j ...
+          load_block(j);                // ... then block j rebuilt for step s+1
+        }
+        next_slot();
+      }
+#pragma unroll
+      for (int j = 0; j < NT; ++j) mfma_row(j);
     }
 
     // ---- rhs ----
