@@ -87,7 +87,7 @@ def arrow_to_columns(table, session) -> "OrderedDict[str, C.Column]":
             if pa.types.is_boolean(t):
                 np_arr = np.array(arr.fill_null(False).to_pylist(), dtype=bool)
             else:
-                np_arr = arr.fill_null(0).to_numpy(zero_copy_only=False)
+                np_arr = (arr.fill_null(0) if arr.null_count else arr).to_numpy(zero_copy_only=False)
                 if np_arr.dtype.kind == "u":
                     np_arr = np_arr.astype(np.int64)
                 elif not np_arr.flags.writeable and not host:

@@ -142,14 +142,18 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
         rnd = (U[t, :n] * m).long().clamp_max(m - 1)
         return torch.where(tot > 0, idx, rnd)
 
-    pn = (P * P).sum(1)
+    # the seeding distances use fp32-rounded coordinates (products and sums in fp64) on both
+    # paths: the kernel then streams half the bytes and keeps the candidates L2-resident;
+    # the centres themselves are the fp64 candidates
+    Pr = P.float().double()
+    pn = (Pr * Pr).sum(1)
     tr = trace("kmeans.init.local.seed")
     tr.__enter__()
-    if kernel and P.is_cuda and trials <= 16 and (P.shape[1] + 3) // 4 * 4 * trials * 8 + 8 * 1040 <= 150 * 1024:
+    if kernel and P.is_cuda and trials <= 16 and (P.shape[1] + 3) // 4 * 4 * trials * 4 + 8 * 528 <= 150 * 1024:
         # all k steps in ONE block (kmeanspp_kernel): ~10 kernels per step otherwise
         from ..ops import _native as N
         Pc, wc, pc = P.contiguous(), w.to(torch.float64).contiguous(), pn.contiguous()
-        PT = Pc.t().contiguous()                  # coalesced candidate reads in the kernel
+        PT = Pc.float().t().contiguous()          # fp32 [D][m]: coalesced, L2-resident candidate reads
         Uc = U.contiguous()
         d2 = torch.empty(m, dtype=torch.float64, device=dev)
         cs = torch.empty(m, dtype=torch.float64, device=dev)
@@ -163,12 +167,12 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
         first = draw(0, w, 1)[0]
         picks = torch.empty(k, dtype=torch.int64, device=dev)
         picks[0] = first
-        d2 = ((P - P[first]) ** 2).sum(1)
+        d2 = ((Pr - Pr[first]) ** 2).sum(1)
         for t in range(1, k):
             cand = draw(t, w * d2, trials)
             # [trials, m] squared distances as |p|^2 + |c|^2 - 2 c.p: one small fp64 GEMM
             # instead of a [trials, m, D] difference tensor per step
-            cd = (pn[None, :] + pn[cand][:, None] - 2.0 * (P[cand] @ P.T)).clamp_min_(0.0)
+            cd = (pn[None, :] + pn[cand][:, None] - 2.0 * (Pr[cand] @ Pr.T)).clamp_min_(0.0)
             pot = (w[None, :] * torch.minimum(d2[None, :], cd)).sum(1)
             best = pot.argmin()
             picks[t] = cand[best]

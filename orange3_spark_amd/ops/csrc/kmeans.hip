@@ -1249,25 +1249,28 @@ __device__ int pp_draw(const double* __restrict__ cs, int m, double tot, double 
   return lo < m - 1 ? lo : m - 1;
 }
 
-// PT: the candidates transposed ([D][m]): thread i reads coordinate d of candidate i at
-// PT[d m + i], so a wave's loads are one contiguous 512-B run (the row-major walk read 64
-// rows 1 KB apart per instruction: 0.53 s for k = 1024 over ~4K candidates,
-// profiles/kmeans_init_phases_r5.json).  cd [trials][m]: the trial candidates' distances,
-// kept so the d2 update after the pick needs no second pass over the candidates.
+// PT: the candidates transposed ([D][m]) and rounded to fp32 (the seeding distances use
+// fp32-rounded coordinates, products and sums in fp64; the torch path rounds the same way):
+// thread i reads coordinate d of candidate i at PT[d m + i], so a wave's loads are one
+// contiguous 256-B run, and the whole matrix (2 MB at 4K candidates x 128) stays in the
+// XCD's L2 across the k steps -- a single workgroup pulls ~10 B/cycle from HBM, so the
+// fp64 row-major walk spent 0.53 s and the fp64 transposed one 0.11 s streaming 4 MB per
+// step (profiles/kmeans_init_phases_r5.json).  cd [trials][m]: the trial candidates'
+// distances, kept so the d2 update after the pick needs no second pass.
 template <int TRIALS>
 __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __restrict__ P,
-                                                              const double* __restrict__ PT,
+                                                              const float* __restrict__ PT,
                                                               const double* __restrict__ w,
                                                               const double* __restrict__ pn, int m, int D, int k,
                                                               const double* __restrict__ U,
                                                               double* __restrict__ d2, double* __restrict__ cs,
                                                               double* __restrict__ cd, int* __restrict__ picks) {
   constexpr int trials = TRIALS;          // compile-time: the per-draw arrays stay in registers
-  extern __shared__ double sm[];          // [trials][DP] candidate rows (zero padded), part[kPPThreads], red[16]
+  extern __shared__ double sm[];          // part[kPPThreads], red[16], then [trials][DP] fp32 candidate rows
   const int DP = (D + kPPU - 1) / kPPU * kPPU;
-  double* const sc = sm;
-  double* const part = sc + trials * DP;
+  double* const part = sm;
   double* const red = part + kPPThreads;
+  float* const sc = reinterpret_cast<float*>(red + 16);
   __shared__ int cand[16];
   __shared__ double pots[16];
   const int tid = threadIdx.x;
@@ -1278,14 +1281,14 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
   __syncthreads();
   const int first = cand[0];
   if (tid == 0) picks[0] = first;
-  for (int e = tid; e < D; e += kPPThreads) sc[e] = P[(int64_t)first * D + e];
+  for (int e = tid; e < D; e += kPPThreads) sc[e] = PT[(int64_t)e * m + first];
   __syncthreads();
   for (int i = tid; i < m; i += kPPThreads) {
     double s = 0.0;
     for (int d0 = 0; d0 < D; d0 += kPPU) {
       double x[kPPU];
 #pragma unroll
-      for (int u = 0; u < kPPU; ++u) x[u] = d0 + u < D ? PT[(int64_t)(d0 + u) * m + i] - sc[d0 + u] : 0.0;
+      for (int u = 0; u < kPPU; ++u) x[u] = d0 + u < D ? (double)PT[(int64_t)(d0 + u) * m + i] - (double)sc[d0 + u] : 0.0;
 #pragma unroll
       for (int u = 0; u < kPPU; ++u) s = fma(x[u], x[u], s);
     }
@@ -1298,7 +1301,7 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
     __syncthreads();
     for (int e = tid; e < trials * DP; e += kPPThreads) {
       const int j = e / DP, d = e - j * DP;
-      sc[e] = d < D ? P[(int64_t)cand[j] * D + d] : 0.0;
+      sc[e] = d < D ? PT[(int64_t)d * m + cand[j]] : 0.f;
     }
     double pc[trials];
 #pragma unroll
@@ -1323,13 +1326,13 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
         for (int r = 0; r < RB; ++r) {
           const int i = i0 + r * kPPThreads;
 #pragma unroll
-          for (int u = 0; u < kPPU; ++u) x[r][u] = (i < m && d0 + u < D) ? PT[(int64_t)(d0 + u) * m + i] : 0.0;
+          for (int u = 0; u < kPPU; ++u) x[r][u] = (i < m && d0 + u < D) ? (double)PT[(int64_t)(d0 + u) * m + i] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < kPPU; ++u) {
           double c[trials];
 #pragma unroll
-          for (int j = 0; j < trials; ++j) c[j] = sc[j * DP + d0 + u];
+          for (int j = 0; j < trials; ++j) c[j] = (double)sc[j * DP + d0 + u];
 #pragma unroll
           for (int r = 0; r < RB; ++r)
 #pragma unroll
@@ -1367,13 +1370,14 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
 }
 }  // namespace
 
-// P [m][D] fp64 candidates and PT = P^T [D][m], w [m] weights, pn [m] = |p|^2, U [k][trials
+// P [m][D] fp64 candidates (unused by the kernel) and PT = fp32(P)^T [D][m], w [m] weights,
+// pn [m] = |fp32(p)|^2 (fp64 sums), U [k][trials
 // + 1] uniforms; ws: d2 [m], cs [m], cd [trials][m] fp64 scratch; picks [k] int32 out.
 // trials <= 16.
-O3S_API int o3s_kmeanspp(const double* P, const double* PT, const double* w, const double* pn, int m, int D, int k,
+O3S_API int o3s_kmeanspp(const double* P, const float* PT, const double* w, const double* pn, int m, int D, int k,
                          int trials, const double* U, double* d2, double* cs, double* cd, int* picks, hipStream_t st) {
   if (m <= 0 || k <= 0 || D <= 0 || trials < 1 || trials > 16) return -1;
-  const size_t lds = sizeof(double) * ((size_t)trials * ((D + kPPU - 1) / kPPU * kPPU) + kPPThreads + 16);
+  const size_t lds = sizeof(double) * (kPPThreads + 16) + sizeof(float) * (size_t)trials * ((D + kPPU - 1) / kPPU * kPPU);
   if (lds > 160 * 1024 - 256) return -2;
   switch (trials) {
 #define O3S_PP(T)                                                                                           \
