@@ -191,7 +191,7 @@ DENSE_MIN_AVG = 0
 
 def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, implicit: bool, alpha: float,
                FtF: torch.Tensor | None, cg_iters: int, nonneg: bool, exact: bool | None = None,
-               row_range: tuple[int, int] | None = None) -> torch.Tensor:
+               row_range: tuple[int, int] | None = None, eig_basis: bool = False) -> torch.Tensor:
     """New factors of the rows of ``csr`` (all of them, or the CG solve of rows [a, b)
     written IN PLACE into ``X0[a:b]``, which is returned -- the chunked path of
     :func:`fit_als`, whose per-chunk results are all-gathered while later chunks solve)."""
@@ -216,8 +216,9 @@ def solve_side(csr: Csr, Ffull: torch.Tensor, X0: torch.Tensor, reg: float, impl
         with trace("als.exact_solve"):
             if A.exact_kernel_ok(Ffull) and out.is_contiguous():
                 A.exact_solve(csr.indptr, csr.cols, w, b, Ffull, FtF if implicit else None, lam, implicit, out,
-                              row_range)
+                              row_range, eig_basis=eig_basis)
             else:
+                assert not eig_basis, "eig_basis needs the exact-solve kernels"
                 A.exact_solve_torch(csr.indptr, csr.cols, w, b, Ffull, FtF if implicit else None, lam, out,
                                     row_range)
         if nonneg:
@@ -286,6 +287,11 @@ def gram(F: torch.Tensor, chunk: int = 1 << 20) -> torch.Tensor:
         Fc = F[a:a + chunk].float()
         out += (Fc.T @ Fc).double()
     return out
+
+
+# implicit exact fits keep the factor tables in the eigenbasis of the previous Gram (see
+# fit_als): False rotates every user-side Woodbury row back each iteration instead
+EIG_BASIS = True
 
 
 # row chunks per half-iteration on several ranks: chunk c's all-gather (RCCL, its own
@@ -388,6 +394,19 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
         Y = torch.from_numpy(st["Y"]).to(dev, Y.dtype)
     small = max(by_user.cols.numel(), by_item.cols.numel()) * rank * rank <= (1 << 26)
     chunked = comm.world_size > 1 and not small
+    # implicit exact solves on the kernels keep both tables in a moving orthonormal basis B
+    # (X B, Y B): the user side returns its rows in the eigenbasis of the item Gram (no
+    # x = Q y rotation of the 50M-row side per iteration), the item side solves in that
+    # basis unchanged, and B accumulates the per-iteration eigenbases (fp64, host); the
+    # tables are rotated back once, when the fit ends (or a checkpoint is written)
+    eigmode = (EIG_BASIS and implicit and not nonneg and dev.type == "cuda" and rank in A.EXACT_RANKS
+               and X.dtype == torch.float32 and (exact is True or (exact is None and cg_iters <= 0)))
+    basis = [None]                       # [R, R] fp64 (host); None = the identity
+
+    def to_orig(T):
+        if basis[0] is None:
+            return T
+        return A.rotated_table(T.contiguous(), basis[0].t().contiguous().float().to(T.device))
     if chunked:
         # factor tables in "slot" layout: every all-gather lands in place (no staging copy,
         # no concatenation) and chunk c of every rank is gathered while chunk c+1 solves
@@ -411,9 +430,15 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
                 YtY = YtY.float()
             if chunked:
                 _gather_slots(comm, X, Xf, Ls, lambda a, e: solve_side(
-                    by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact, row_range=(a, e)))
+                    by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact, row_range=(a, e),
+                    eig_basis=eigmode))
             else:
-                X = solve_side(by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact)
+                X = solve_side(by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact,
+                               eig_basis=eigmode)
+            if eigmode:                  # X now holds X (B Q): the basis moves on by Q
+                q = A.EIG_CACHE.get(Yf, YtY, True)[1].double().cpu()
+                basis[0] = q if basis[0] is None else basis[0] @ q
+            if not chunked:
                 del Yf
                 Xf = comm.all_gather_v(X) if comm.world_size > 1 else X
             XtX = None
@@ -431,9 +456,11 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
                 torch.cuda.synchronize(dev)
             its.append(time.time() - ti)
             if ckpt is not None and ckpt.due(it + 1):
-                ckpt.save(it + 1, {"X": X.cpu().numpy(), "Y": Y.cpu().numpy()})
+                ckpt.save(it + 1, {"X": to_orig(X).cpu().numpy(), "Y": to_orig(Y).cpu().numpy()})
     if ckpt is not None:
         ckpt.clear()                     # finished: a later fit must not resume from this run
+    with trace("als.basis_restore"):
+        X, Y = to_orig(X), to_orig(Y)
     Uf = comm.all_gather_v(X) if (keep_full and comm.world_size > 1) else X
     Vf = comm.all_gather_v(Y) if (keep_full and comm.world_size > 1) else Y
     A.EIG_CACHE.clear()                  # drops the rotated factor table

@@ -241,12 +241,18 @@ def rotated_table(F: torch.Tensor, Q: torch.Tensor) -> torch.Tensor:
     return FQ
 
 
-def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor, row_range=None) -> torch.Tensor:
+def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor, row_range=None,
+                eig_basis: bool = False) -> torch.Tensor:
     """Exact per-row solves (csrc/als_exact.hip) written into ``out`` (rows of this CSR,
     or rows [a, b) of it).  Rows with <= 32 ratings and lam_u > 0 take the Woodbury kernel
     (an n x n Cholesky against the eigendecomposition G = Q diag(e) Q^T, gathering rows of
     the rotated table F Q; x = Q y afterwards by als_rotate_kernel), the others the dense
-    kernel (register-tile Gram + blocked Cholesky).  G = Y^T Y (implicit only)."""
+    kernel (register-tile Gram + blocked Cholesky).  G = Y^T Y (implicit only).
+
+    ``eig_basis`` (implicit, compiled ranks): every row is returned in the eigenbasis Q of
+    G, y = Q^T x -- the Woodbury rows skip the x = Q y rotation and the dense rows solve the
+    rotated system (F Q, diag(eig)) -- so a fit that keeps its tables in that basis
+    (models/als.py fit_als) never rotates the large side's table; Q is EIG_CACHE's."""
     dev = F.device
     R = F.shape[1]
     if R not in EXACT_RANKS:
@@ -276,8 +282,14 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
     ns, nd = int(small.numel()), int(dense.numel())
     lib = N.kernels()
     st = N.stream_of(out)
+    eig_basis = bool(eig_basis and implicit)
+    if eig_basis:
+        with trace("als.eig_rotated_table"):
+            eig, Q, P = EIG_CACHE.get(F, G, True)
     if ns:
-        if implicit:
+        if eig_basis:
+            pass
+        elif implicit:
             with trace("als.eig_rotated_table"):
                 eig, Q, P = EIG_CACHE.get(F, G, True)
         else:
@@ -290,7 +302,7 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
                     N.check(lib.o3s_als_wood_kn(R, kn, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
                                                 b.data_ptr(), P.data_ptr(), eig.data_ptr(), lam.data_ptr(),
                                                 lst.data_ptr(), lst.numel(), out.data_ptr(), st), "als_wood")
-        if implicit:                          # x = Q y for the Woodbury rows (als_rotate_kernel)
+        if implicit and not eig_basis:        # x = Q y for the Woodbury rows (als_rotate_kernel)
             with trace("als.rotate", rows=ns):
                 QT = Q.T.contiguous()
                 grid = max(1, min(N.num_cus(dev) * 2, -(-ns // 32)))
@@ -298,7 +310,10 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
                         "als_rotate")
     if nd:
         with trace("als.dense", rows=nd):
-            Gf = G.float().contiguous() if implicit else None
+            if eig_basis:                     # the rotated system: F Q and diag(eig)
+                F, Gf = P, torch.diag(eig).contiguous()
+            else:
+                Gf = G.float().contiguous() if implicit else None
             # longest rows first: the waves take rows round robin, so the long tail of
             # popular items spreads over the whole chip instead of finishing last
             order = torch.argsort(cnt[dense - a], descending=True)

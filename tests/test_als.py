@@ -249,6 +249,30 @@ def test_gpu_exact_als_rank128_fit_matches_fp64():
 
 
 @pytest.mark.gpu
+def test_gpu_exact_implicit_fit_in_eigenbasis_matches_rotating_each_iteration(monkeypatch):
+    """fit_als keeps both tables in the moving eigenbasis of the Gram (no x = Q y rotation
+    of the user side per iteration; one rotation back at the end): 3 iterations over users
+    with both Woodbury (<= 32 ratings) and dense rows == the fit that rotates every
+    half-iteration, up to fp32 rounding of the rotations."""
+    g = torch.Generator().manual_seed(5)
+    n = 80_000
+    users = torch.randint(0, 3000, (n,), generator=g)
+    items = torch.randint(0, 700, (n,), generator=g)
+    r = (torch.rand(n, generator=g) * 5).round()
+    from orange3_spark_amd.parallel.comm import LocalComm
+    fits = {}
+    for mode in (True, False):
+        monkeypatch.setattr(AE, "EIG_BASIS", mode)
+        fits[mode] = AE.fit_als(LocalComm("cuda"), users.cuda(), items.cuda(), r.cuda(), rank=128, max_iter=3,
+                                reg=0.1, implicit=True, alpha=1.0, seed=2)
+    cnt = torch.bincount(users, minlength=3000)
+    assert bool((cnt > 32).any()) and bool((cnt <= 32).any())
+    for a, b in ((fits[True].U, fits[False].U), (fits[True].V, fits[False].V)):
+        err = (a.double() - b.double()).norm() / b.double().norm()
+        assert float(err) < 1e-4, float(err)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("R", [10, 40])
 @pytest.mark.parametrize("implicit", [False, True])
 def test_gpu_exact_kernels_pad_other_ranks(R, implicit):
