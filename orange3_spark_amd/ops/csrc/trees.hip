@@ -552,6 +552,66 @@ __global__ __launch_bounds__(256) void bin_features_kernel(const void* __restric
   }
 }
 
+// Vector fast path (F % 8 == 0, 16-B aligned rows): a lane bins 8 consecutive features of
+// one row -- one 16-B (bf16) or two 16-B (fp32) loads, eight independent branchless
+// searches, one 8-B store -- instead of one 2-/4-B load and one byte store per element
+// (the scalar kernel above ran the 500M x 64 binning at 75 ms, mostly memory-instruction
+// issue).  The feature-major copy goes through the same LDS tile.
+template <bool BF16>
+__global__ __launch_bounds__(256) void bin_features_vec_kernel(const void* __restrict__ Xv, int64_t n, int64_t ldx,
+                                                               int F, const float* __restrict__ th, int Tp,
+                                                               uint8_t* __restrict__ out, uint8_t* __restrict__ out_t,
+                                                               int64_t ldt) {
+  extern __shared__ float sth[];
+  const int TS = Tp + 1;
+  uint8_t* const tile = reinterpret_cast<uint8_t*>(sth + F * TS);
+  for (int i = threadIdx.x; i < F * Tp; i += 256) sth[(i / Tp) * TS + i % Tp] = th[i];
+  __syncthreads();
+  const int G = F >> 3;                                  // 8-feature groups per row
+  const int64_t nchunks = (n + kBinRows - 1) / kBinRows;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t r0 = c * kBinRows;
+    const int rows = n - r0 < kBinRows ? (int)(n - r0) : kBinRows;
+    for (int li = threadIdx.x; li < rows * G; li += 256) {
+      const int lr = li / G, g = li - lr * G;
+      const int64_t row = r0 + lr;
+      float x[8];
+      if constexpr (BF16) {
+        const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(Xv) + row * ldx + 8 * g);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          x[2 * k] = __uint_as_float(w[k] << 16);
+          x[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+        }
+      } else {
+        const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Xv) + row * ldx + 8 * g);
+        const float4 a = p[0], b = p[1];
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+      }
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float* a = sth + (8 * g + k) * TS;
+        int bk = 0;
+        for (int st = Tp >> 1; st > 0; st >>= 1) bk += (a[bk + st - 1] < x[k]) ? st : 0;
+        if (k < 4) lo |= (uint32_t)bk << (8 * k);
+        else hi |= (uint32_t)bk << (8 * (k - 4));
+        if (out_t != nullptr) tile[(8 * g + k) * kBinTS + lr] = (uint8_t)bk;
+      }
+      *reinterpret_cast<uint2*>(out + row * F + 8 * g) = make_uint2(lo, hi);
+    }
+    if (out_t != nullptr) {
+      __syncthreads();
+      for (int e = threadIdx.x; e < F * kBinRows; e += 256) {
+        const int f = e / kBinRows, lr = e - f * kBinRows;
+        if (lr < rows) out_t[(int64_t)f * ldt + r0 + lr] = tile[f * kBinTS + lr];
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------
 // Leaf apply (boosting): when a segment of `order` becomes a leaf, every row in it gets
 // the leaf's (weighted) value added to its running prediction: acc[order[p]] += val.
@@ -872,7 +932,14 @@ O3S_API int o3s_bin_features2(const void* X, int bf16, int64_t n, int64_t ldx, i
   const int64_t nchunks = (n + kBinRows - 1) / kBinRows;
   const unsigned grid = (unsigned)(nchunks < 8192 ? nchunks : 8192);
   if (out_t != nullptr && ldt < n) return -3;
-  if (bf16)
+  const bool vec = F % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X & 15) == 0;
+  if (vec && bf16)
+    hipLaunchKernelGGL(bin_features_vec_kernel<true>, dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, Tp, out,
+                       out_t, ldt);
+  else if (vec)
+    hipLaunchKernelGGL(bin_features_vec_kernel<false>, dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, Tp, out,
+                       out_t, ldt);
+  else if (bf16)
     hipLaunchKernelGGL(bin_features_kernel<true>, dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, Tp, out, out_t,
                        ldt);
   else

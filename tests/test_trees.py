@@ -207,18 +207,24 @@ def test_gpu_u8_transpose(gpu, n, F):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,F,nb", [(100_003, 64, 32), (5000, 7, 2), (777, 130, 255), (3, 1, 32)])
-def test_gpu_bin_features_matches_bucketize(gpu, n, F, nb):
+@pytest.mark.parametrize("n,F,nb,bf16", [(100_003, 64, 32, False), (100_003, 64, 32, True), (2049, 16, 8, True),
+                                         (5000, 7, 2, False), (777, 130, 255, False), (3, 1, 32, False)])
+def test_gpu_bin_features_matches_bucketize(gpu, n, F, nb, bf16):
+    """bin_features (vector kernel for F % 8 == 0: 8 features per lane; scalar kernel
+    otherwise; fp32 or bf16 rows) == torch.bucketize, and the feature-major copy the
+    kernel writes == the transpose."""
     from orange3_spark_amd.models import trees as TR
     g = torch.Generator().manual_seed(F)
     X = torch.randn(n, F, generator=g)
+    if bf16:
+        X = X.to(torch.bfloat16).float()                          # exactly representable in bf16
     X[:, 0] = torch.round(X[:, 0] * 2) / 2                          # ties on thresholds
     splits = TR.find_splits(Session(SessionConf().set("o3s.device", "cpu")).comm, X, nb, 0)
     ref = torch.empty((n, F), dtype=torch.uint8)
     for f in range(F):
         t = torch.as_tensor(splits[f], dtype=torch.float32)
         ref[:, f] = torch.bucketize(X[:, f], t).to(torch.uint8) if t.numel() else 0
-    got_d = TR.bin_features(X.to(gpu), splits)
+    got_d = TR.bin_features(X.to(gpu).to(torch.bfloat16) if bf16 else X.to(gpu), splits)
     got = got_d.cpu()
     assert torch.equal(got, ref)
     from orange3_spark_amd.ops import trees as T
