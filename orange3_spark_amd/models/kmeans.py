@@ -79,7 +79,7 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
     for step in range(steps):
         tr = trace("kmeans.init.round")
         tr.__enter__()
-        a, d = K.assign(X, centers.float())
+        a, d = K.assign(X, centers.float(), mode="approx")
         cost = torch.sum(d, dtype=torch.float64)        # no fp64 copy of d
         comm.all_reduce(cost)
         if float(cost) <= 0:
@@ -100,13 +100,13 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
     with trace("kmeans.init.weights"):
         if last is not None and centers.shape[0] > n_before:
             a_old, d_old = last
-            a_new, d_new = K.assign(X, centers[n_before:].float())
+            a_new, d_new = K.assign(X, centers[n_before:].float(), mode="approx")
             a = torch.where(d_new < d_old, a_new.to(torch.int64) + n_before, a_old.to(torch.int64))
             del a_new, d_new
         elif last is not None:
             a = last[0].to(torch.int64)
         else:
-            a, _ = K.assign(X, centers.float())
+            a, _ = K.assign(X, centers.float(), mode="approx")
         del last
         # integer histogram (LDS-privatised): an fp64 index_add_ of ones into a few hundred
         # candidates serialises on global atomics

@@ -227,7 +227,9 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
     two-centre near ties exactly in-kernel; ``'split'`` runs the split kernel on every
     row; ``'auto'`` moves screen (-> pair when ``PAIR_FROM`` is set) -> split as the
     previous call on this X flagged more than ``SCREEN_MAX_FLAG_FRACTION`` of its rows, and
-    re-probes the screen every ``SPLIT_REPROBE`` split calls."""
+    re-probes the screen every ``SPLIT_REPROBE`` split calls; ``'approx'`` is the screen
+    without the near-tie re-solve (k-means|| sampling: the chosen centre is within the
+    screen bound of the nearest, its distance exact)."""
     if not kernel_ok(X):
         a, d = assign_torch(X, C)
         return a, (d if need_dist else None)
@@ -250,8 +252,28 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
             _state_set(key, X, "split", f, cd - 1)
         else:
             mode = ("pair" if PAIR_FROM is not None else "screen") if m == "split" else m
+    approx = mode == "approx"
+    if approx:
+        # k-means|| rounds / candidate weights: the screen's pick and its exact fp32 distance
+        # are used as they are (a near tie may go to a centre within the screen bound of the
+        # nearest -- irrelevant to the sampling probabilities), no re-solve, no host sync
+        mode = "screen" if screen_ok(X) else "split"
     if stats is not None:
         stats["mode"] = mode
+    if approx and mode == "screen":
+        cnt, rows = _SWS.get(n, X.device)
+        cnt.zero_()                              # the kernel still lists its near ties (< n rows)
+        xs = x_scale(X)
+        eps_x, eps0 = screen_bound(P, xs, X.shape[1])
+        ps = presplit(X, xs)
+        tt = SCREEN_TT or (2 if X.shape[1] <= 128 else 1)
+        N.check(lib.o3s_kmeans_screen(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
+                                      P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
+                                      Ct.c_float(eps0), Ct.c_float(xs), Ct.c_float(xs * P.ms), a.data_ptr(),
+                                      N.ptr(d), cnt.data_ptr(), rows.data_ptr(), tt, 0,
+                                      N.ptr(ps[0]) if ps else None, N.ptr(ps[1]) if ps else None, st),
+                "kmeans_screen")
+        return a, d
     if mode in ("screen", "pair") and screen_ok(X):
         cnt, rows = _SWS.get(n, X.device)
         cnt.zero_()
