@@ -344,3 +344,23 @@ def test_gpu_kmeanspp_kernel_matches_torch_steps(gpu, k, m, D):
     a = _local_kmeanspp(P, w, k, seed=5, iters=30, kernel=True)
     b = _local_kmeanspp(P, w, k, seed=5, iters=30, kernel=False)
     torch.testing.assert_close(a, b, rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_gpu_approx_assign_is_within_the_screen_bound(gpu):
+    """mode='approx' (k-means|| rounds): the screen's pick without the near-tie re-solve --
+    its distance is the exact distance to the picked centre, never more than the screen
+    bound above the true minimum, and most picks are the exact argmin."""
+    from orange3_spark_amd.ops import kmeans as K
+    g = torch.Generator().manual_seed(11)
+    X = (torch.randn(200_000, 64, generator=g) * 3).to(gpu)
+    C = X[torch.randperm(200_000, generator=g)[:700].to(gpu)] + 0.01
+    a1, d1 = K.assign(X, C, mode="approx")
+    a2, d2 = K.assign(X, C, mode="split")
+    P = K.prepare_centers(C)
+    eps_x, eps0 = K.screen_bound(P, K.x_scale(X), X.shape[1])
+    bound = 2 * (eps_x * X.norm(dim=1) + eps0)
+    dx = ((X - C[a1.long()]) ** 2).sum(1)
+    assert torch.allclose(d1, dx, rtol=1e-4, atol=1e-3)
+    assert bool((d1 <= d2 + bound + 1e-3).all())
+    assert float((a1 == a2).float().mean()) > 0.9
