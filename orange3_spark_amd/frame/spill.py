@@ -484,12 +484,20 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
             for t, v, _ in sources] for _ in range(2)]
     sent = [None, None]                         # copy event of the chunk that last used set k
 
+    import time as _time
+    stats = {"chunks": len(bounds), "host_wait_s": 0.0, "host_copy_s": 0.0, "issue_s": 0.0}
+    LAST_ASSEMBLE_STATS.clear()
+    LAST_ASSEMBLE_STATS.update(stats)
+
     def stage(i):
         a, b = bounds[i]
         m = b - a
         k = i & 1
+        t0 = _time.perf_counter()
         if sent[k] is not None:
             sent[k].synchronize()               # the H2D of chunk i-2 has drained set k
+        t1 = _time.perf_counter()
+        LAST_ASSEMBLE_STATS["host_wait_s"] += t1 - t0
         out, copies = [], []
         for (t, v, w), (tb, vb) in zip(sources, stg[k]):
             tt, vv = t[a:b], None if v is None else v[a:b]
@@ -501,6 +509,7 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
                 vv = vb[:m]
             out.append((tt, vv, w))
         _parallel_copy(copies)                  # pageable -> pinned, on host threads
+        LAST_ASSEMBLE_STATS["host_copy_s"] += _time.perf_counter() - t1
         with torch.cuda.stream(copy):
             out = [(tt.to(dev, non_blocking=True), None if vv is None else vv.to(dev, non_blocking=True), w)
                    for tt, vv, w in out]
@@ -535,12 +544,15 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
             with torch.cuda.stream(d2h):
                 host[a + r - keep:b - keep].copy_(out[r:], non_blocking=True)
             out.record_stream(d2h)
+    t2 = _time.perf_counter()
     torch.cuda.synchronize(dev)
+    LAST_ASSEMBLE_STATS["final_sync_s"] = _time.perf_counter() - t2
     col = SpilledVectorColumn(res, host, D) if n > keep else C.VectorColumn(res, D)
     return col, int(nbad_d.item())
 
 
 _COPY_POOL = None
+LAST_ASSEMBLE_STATS: dict = {}      # host-side time split of the last streamed assembly (GPU)
 
 
 def _parallel_copy(pairs, piece_bytes: int = 8 << 20) -> None:

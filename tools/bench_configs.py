@@ -93,7 +93,7 @@ def run_gbt(s, a):
     # allocations (the 32 GB feature-major copy) are cleared by the driver before first use
     # (~1.6 s on a box whose memory a previous process used); later fits reuse the caching
     # allocator's blocks, as in a long-running session.  value = the last (warm) fit.
-    fits = []
+    fits, phases_each = [], []
     for _ in range(max(1, a.repeat)):
         TRACER.reset()
         s.comm.barrier()
@@ -103,6 +103,8 @@ def run_gbt(s, a):
         _sync()
         s.comm.barrier()
         fits.append(time.perf_counter() - t1)
+        if TRACER.enabled:
+            phases_each.append({k: round(v["total_s"], 4) for k, v in TRACER.summary().items()})
     fit_s = fits[-1]
     ph = {k: round(v["total_s"], 4) for k, v in TRACER.summary().items()} if TRACER.enabled else None
     prep = None
@@ -117,7 +119,7 @@ def run_gbt(s, a):
            "per_tree_excl_binning_s": (round((fit_s - prep) / a.trees, 4) if prep is not None else None),
            "train_loss": [round(x, 5) for x in model.trainingLossHistory][-3:],
            "datagen_seconds_untimed": round(t_gen, 2), "max_mem_gb": _mem_gb(), "alloc": _alloc_stats(),
-           "phases_s": ph}
+           "phases_s": ph, "phases_each_fit_s": phases_each or None}
     return out
 
 

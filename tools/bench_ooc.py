@@ -84,7 +84,10 @@ def main():
         "assemble_rows_per_s": a.rows / t_asm, "assemble_input_GBps": round(asm_gbps, 2),
         "d2h_GB": round(d2h / 1e9, 2), "h2d_bound_GBps": None if h2d_gbps is None else round(h2d_gbps, 2),
         "fraction_of_h2d_bound": None if not h2d_gbps else round(asm_gbps / h2d_gbps, 3),
-        "device_peak_GB": round(peak / 1e9, 2)}), flush=True)
+        "device_peak_GB": round(peak / 1e9, 2),
+        "assemble_host_split_s": {k: round(v, 3) if isinstance(v, float) else v
+                                  for k, v in __import__("orange3_spark_amd.frame.spill", fromlist=["x"]).LAST_ASSEMBLE_STATS.items()}}),
+          flush=True)
 
 
 if __name__ == "__main__":
