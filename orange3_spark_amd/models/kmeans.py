@@ -116,11 +116,17 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
         return _local_kmeanspp(centers, wts, k, seed)
 
 
+# Spark's LocalKMeans.kMeansPlusPlus draws ONE candidate per step (probability ~ w * d^2);
+# True: greedy k-means++ (best of 2 + ln k draws per step, scikit-learn's variant)
+GREEDY_KMEANSPP = False
+
+
 def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: int = 30,
                     kernel: bool = True) -> torch.Tensor:
     """Weighted k-means++ + Lloyd on candidates (Spark LocalKMeans), fp64 on device.
 
-    Greedy k-means++ (best of ``2 + ln k`` weighted draws per step).  The whole seeding
+    k-means++ with one weighted draw per step, as Spark (``GREEDY_KMEANSPP``: best of
+    ``2 + ln k`` draws per step).  The whole seeding
     loop stays on the device -- draws are counter-hash uniforms keyed on (seed, step,
     trial) inverted through the cumulative weights by ``searchsorted`` -- so its k
     sequential steps issue kernels without a single host round trip (the host-side
@@ -130,7 +136,7 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
     if m <= k:
         extra = k - m
         return torch.cat([P, P[:1].expand(extra, -1)]) if extra else P
-    trials = 2 + int(math.log(k))          # greedy k-means++: best of several seeds per step
+    trials = 2 + int(math.log(k)) if GREEDY_KMEANSPP else 1
     keys = torch.arange(k * (trials + 1), dtype=torch.int64, device=dev).view(k, trials + 1)
     U = sampling.uniform(keys.reshape(-1), seed, stream=31).view(k, trials + 1)
 
