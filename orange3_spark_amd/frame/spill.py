@@ -460,8 +460,11 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
     in_row = sum(t.element_size() * (1 if t.dim() == 1 else t.shape[1]) for t, _, _ in sources) or 1
     rows = max(1024, int(chunk_bytes or CHUNK_BYTES) // in_row)
     cuda = dev.type == "cuda"
+    import time as _time
+    _t0 = _time.perf_counter()
     res = torch.empty((keep, ld), dtype=vdt, device=dev)
     host = torch.empty((n - keep, ld), dtype=vdt, pin_memory=cuda and torch.cuda.is_available())
+    _t_alloc = _time.perf_counter() - _t0
     bounds = [(a, min(n, a + rows)) for a in range(0, n, rows)]
     if not cuda:
         nbad = 0
@@ -480,12 +483,12 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
     def _stage_buf(t):
         shape = (rows,) + tuple(t.shape[1:])
         return torch.empty(shape, dtype=t.dtype, pin_memory=True)
+    _t1 = _time.perf_counter()
     stg = [[(None if t.is_cuda else _stage_buf(t), None if (v is None or v.is_cuda) else _stage_buf(v))
             for t, v, _ in sources] for _ in range(2)]
     sent = [None, None]                         # copy event of the chunk that last used set k
-
-    import time as _time
-    stats = {"chunks": len(bounds), "host_wait_s": 0.0, "host_copy_s": 0.0, "issue_s": 0.0}
+    stats = {"chunks": len(bounds), "host_wait_s": 0.0, "host_copy_s": 0.0, "out_alloc_s": _t_alloc,
+             "staging_alloc_s": _time.perf_counter() - _t1}
     LAST_ASSEMBLE_STATS.clear()
     LAST_ASSEMBLE_STATS.update(stats)
 

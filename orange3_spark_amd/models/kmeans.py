@@ -116,17 +116,19 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
         return _local_kmeanspp(centers, wts, k, seed)
 
 
-# Spark's LocalKMeans.kMeansPlusPlus draws ONE candidate per step (probability ~ w * d^2);
-# True: greedy k-means++ (best of 2 + ln k draws per step, scikit-learn's variant)
-GREEDY_KMEANSPP = False
+# greedy k-means++ (best of 2 + ln k draws per step, scikit-learn's variant).  False: one
+# draw per step, as Spark's LocalKMeans.kMeansPlusPlus -- on the 100M x 128, k = 1024
+# blobs its seeding leaves a 1.9x higher cost after 10 Lloyd iterations (25.0e9 vs
+# 13.3e9, profiles/kmeans_init_phases_r5.json), so the greedy variant is the default
+GREEDY_KMEANSPP = True
 
 
 def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: int = 30,
                     kernel: bool = True) -> torch.Tensor:
     """Weighted k-means++ + Lloyd on candidates (Spark LocalKMeans), fp64 on device.
 
-    k-means++ with one weighted draw per step, as Spark (``GREEDY_KMEANSPP``: best of
-    ``2 + ln k`` draws per step).  The whole seeding
+    Greedy k-means++ (best of ``2 + ln k`` weighted draws per step; ``GREEDY_KMEANSPP =
+    False``: one draw per step, as Spark's LocalKMeans).  The whole seeding
     loop stays on the device -- draws are counter-hash uniforms keyed on (seed, step,
     trial) inverted through the cumulative weights by ``searchsorted`` -- so its k
     sequential steps issue kernels without a single host round trip (the host-side
@@ -155,7 +157,7 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
     pn = (Pr * Pr).sum(1)
     tr = trace("kmeans.init.local.seed")
     tr.__enter__()
-    if kernel and P.is_cuda and trials <= 16 and (P.shape[1] + 3) // 4 * 4 * trials * 4 + 8 * 528 <= 150 * 1024:
+    if kernel and P.is_cuda and trials <= 16 and (P.shape[1] + 15) // 16 * 16 * trials * 4 + 8 * 528 <= 150 * 1024:
         # all k steps in ONE block (kmeanspp_kernel): ~10 kernels per step otherwise
         from ..ops import _native as N
         Pc, wc, pc = P.contiguous(), w.to(torch.float64).contiguous(), pn.contiguous()

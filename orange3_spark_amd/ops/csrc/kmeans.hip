@@ -1195,7 +1195,7 @@ O3S_API int o3s_kmeans_update(const float* X, int64_t n, int64_t ldx, int D, con
 // same counter-hash uniforms U [k][trials + 1] (so CPU and GPU pick from the same draws).
 namespace {
 constexpr int kPPThreads = 512;
-constexpr int kPPU = 4;                    // coordinates per load round
+constexpr int kPPU = 16;                   // sc row padding (the largest load round)
 
 __device__ double pp_block_sum(double v, double* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1310,33 +1310,35 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
     double acc[trials];
 #pragma unroll
     for (int j = 0; j < trials; ++j) acc[j] = 0.0;
+    // register blocking: RB rows x trials dot products per thread; each round loads RB x U
+    // fp32 coordinates (coalesced, U = 16 up to 8 trials: the step is a chain of load
+    // rounds -- 2 waves per SIMD hide little of the L2 latency -- so each round carries as
+    // many loads as the registers allow) and the trials' centre values from LDS
     constexpr int RB = TRIALS <= 8 ? 4 : 2;
-    // register blocking: RB rows (4, or 2 past 8 trials: no spill) x trials dot products per thread, so each coordinate
-    // round loads RB x kPPU candidate values (coalesced) and trials x kPPU centre values
-    // (LDS broadcasts) for RB x trials x kPPU FMAs
+    constexpr int U = TRIALS <= 4 ? 16 : (TRIALS <= 8 ? 8 : 4);
     for (int i0 = tid; i0 < m; i0 += RB * kPPThreads) {
       double dot[RB][trials];
 #pragma unroll
       for (int r = 0; r < RB; ++r)
 #pragma unroll
         for (int j = 0; j < trials; ++j) dot[r][j] = 0.0;
-      for (int d0 = 0; d0 < D; d0 += kPPU) {
-        double x[RB][kPPU];
+      for (int d0 = 0; d0 < D; d0 += U) {
+        float x[RB][U];
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
           const int i = i0 + r * kPPThreads;
 #pragma unroll
-          for (int u = 0; u < kPPU; ++u) x[r][u] = (i < m && d0 + u < D) ? (double)PT[(int64_t)(d0 + u) * m + i] : 0.0;
+          for (int u = 0; u < U; ++u) x[r][u] = (i < m && d0 + u < D) ? PT[(int64_t)(d0 + u) * m + i] : 0.f;
         }
 #pragma unroll
-        for (int u = 0; u < kPPU; ++u) {
+        for (int u = 0; u < U; ++u) {
           double c[trials];
 #pragma unroll
           for (int j = 0; j < trials; ++j) c[j] = (double)sc[j * DP + d0 + u];
 #pragma unroll
           for (int r = 0; r < RB; ++r)
 #pragma unroll
-            for (int j = 0; j < trials; ++j) dot[r][j] = fma(x[r][u], c[j], dot[r][j]);
+            for (int j = 0; j < trials; ++j) dot[r][j] = fma((double)x[r][u], c[j], dot[r][j]);
         }
       }
 #pragma unroll
