@@ -72,7 +72,10 @@ def arrow_to_columns(table, session) -> "OrderedDict[str, C.Column]":
     # (VectorAssembler streams them into a SpilledVectorColumn)
     host = spill.host_resident(session, nb)
     for name, arr in zip(table.column_names, table.columns):
-        arr = arr.combine_chunks() if hasattr(arr, "combine_chunks") else arr
+        if hasattr(arr, "num_chunks") and arr.num_chunks == 1:
+            arr = arr.chunk(0)                   # no copy (combine_chunks concatenates into a new buffer)
+        elif hasattr(arr, "combine_chunks"):
+            arr = arr.combine_chunks()
         t = arr.type
         if _is_vector_struct(t):
             out[name] = _vector_struct_to_column(arr.to_pylist(), session)
