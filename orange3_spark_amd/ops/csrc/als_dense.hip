@@ -55,7 +55,9 @@ typedef const int32_t __attribute__((address_space(4)))* sptr_i32;
 typedef const int64_t __attribute__((address_space(4)))* sptr_i64;
 typedef const float __attribute__((address_space(4)))* sptr_f32;
 
-template <int R>
+// DEEP (explicit: no G in LDS): the 40 KB G would take carry a fourth ring step at ranks
+// 96 / 128 (implicit keeps G in LDS: reading it per row from global memory spilled)
+template <int R, bool DEEP = false>
 struct DW {
   static constexpr int NT = R / 32;
   static constexpr int NL = NT * (NT + 1) / 2;
@@ -66,7 +68,7 @@ struct DW {
   static constexpr int RPI = 64 / LPS;                  // rows per DMA instruction
   static constexpr int NI = CH / RPI;                   // row DMAs per step
   static constexpr int NIS = NI + 1;                    // + the w / b DMA
-  static constexpr int DEPTH = R >= 96 ? 3 : (R == 64 ? 5 : 8);
+  static constexpr int DEPTH = R >= 96 ? (DEEP ? 4 : 3) : (R == 64 ? 5 : 8);
   static constexpr int SLOT = CH * RS;                  // floats per ring slot
   static constexpr int TS = 32 * 33;                    // padded 32 x 32 scratch tile
   static constexpr int WAVE = DEPTH * SLOT + DEPTH * 32 + TS + R;   // floats per wave
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
     const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nrows, float* __restrict__ X,
     float* __restrict__ dbg) {
-  using D = DW<R>;
+  using D = DW<R, !IMPL>;
   constexpr int NT = D::NT, NL = D::NL, CH = D::CH, DEPTH = D::DEPTH, RS = D::RS, LPS = D::LPS,
                 RPI = D::RPI, NI = D::NI, SLOT = D::SLOT;
   // ONE __shared__ array (a second object beside the DMA ring can make hipcc wait vmcnt(0)
