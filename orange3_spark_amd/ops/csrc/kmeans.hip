@@ -1264,7 +1264,8 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
                                                               const double* __restrict__ pn, int m, int D, int k,
                                                               const double* __restrict__ U,
                                                               double* __restrict__ d2, double* __restrict__ cs,
-                                                              double* __restrict__ cd, int* __restrict__ picks) {
+                                                              double* __restrict__ cd, int* __restrict__ picks,
+                                                              long long* __restrict__ tim) {
   constexpr int trials = TRIALS;          // compile-time: the per-draw arrays stay in registers
   extern __shared__ double sm[];          // part[kPPThreads], red[16], then [trials][DP] fp32 candidate rows
   const int DP = (D + kPPU - 1) / kPPU * kPPU;
@@ -1295,10 +1296,23 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
     d2[i] = s;
   }
   __syncthreads();
+  // tim (diagnostic, may be null): thread 0's shader-clock totals per phase of the steps:
+  // [scan, draw, candidate rows, distances + potentials, pick, d2 update]
+  long long tacc[6] = {0, 0, 0, 0, 0, 0};
+  long long tp = tim ? (long long)clock64() : 0;
+  auto stamp = [&](int ph) {
+    if (tim) {
+      const long long now = (long long)clock64();
+      tacc[ph] += now - tp;
+      tp = now;
+    }
+  };
   for (int t = 1; t < k; ++t) {
     tot = pp_scan(w, d2, m, cs, part);
+    stamp(0);
     if (tid < trials) cand[tid] = pp_draw(cs, m, tot, U[(int64_t)t * nt + tid]);
     __syncthreads();
+    stamp(1);
     for (int e = tid; e < trials * DP; e += kPPThreads) {
       const int j = e / DP, d = e - j * DP;
       sc[e] = d < D ? PT[(int64_t)d * m + cand[j]] : 0.f;
@@ -1307,6 +1321,7 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
 #pragma unroll
     for (int j = 0; j < trials; ++j) pc[j] = pn[cand[j]];
     __syncthreads();
+    stamp(2);
     double acc[trials];
 #pragma unroll
     for (int j = 0; j < trials; ++j) acc[j] = 0.0;
@@ -1355,12 +1370,14 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
         }
       }
     }
+    stamp(3);
 #pragma unroll
     for (int j = 0; j < trials; ++j) {
       const double s = pp_block_sum(acc[j], red);
       if (tid == 0) pots[j] = s;
     }
     __syncthreads();
+    stamp(4);
     int best = 0;
     for (int j = 1; j < trials; ++j)
       if (pots[j] < pots[best]) best = j;
@@ -1368,7 +1385,10 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
     // d2 = min(d2, |p - c|^2): this thread's own cd entries (same i walk as above)
     for (int i = tid; i < m; i += kPPThreads) d2[i] = fmin(d2[i], cd[(int64_t)best * m + i]);
     __syncthreads();
+    stamp(5);
   }
+  if (tim && tid == 0)
+    for (int ph = 0; ph < 6; ++ph) tim[ph] = tacc[ph];
 }
 }  // namespace
 
@@ -1377,7 +1397,8 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
 // + 1] uniforms; ws: d2 [m], cs [m], cd [trials][m] fp64 scratch; picks [k] int32 out.
 // trials <= 16.
 O3S_API int o3s_kmeanspp(const double* P, const float* PT, const double* w, const double* pn, int m, int D, int k,
-                         int trials, const double* U, double* d2, double* cs, double* cd, int* picks, hipStream_t st) {
+                         int trials, const double* U, double* d2, double* cs, double* cd, int* picks,
+                         long long* tim, hipStream_t st) {
   if (m <= 0 || k <= 0 || D <= 0 || trials < 1 || trials > 16) return -1;
   const size_t lds = sizeof(double) * (kPPThreads + 16) + sizeof(float) * (size_t)trials * ((D + kPPU - 1) / kPPU * kPPU);
   if (lds > 160 * 1024 - 256) return -2;
@@ -1385,7 +1406,7 @@ O3S_API int o3s_kmeanspp(const double* P, const float* PT, const double* w, cons
 #define O3S_PP(T)                                                                                           \
     case T:                                                                                                 \
       hipLaunchKernelGGL(kmeanspp_kernel<T>, dim3(1), dim3(kPPThreads), lds, st, P, PT, w, pn, m, D, k, U, d2, cs, \
-                         cd, picks);                                                                        \
+                         cd, picks, tim);                                                                   \
       break;
     O3S_PP(1) O3S_PP(2) O3S_PP(3) O3S_PP(4) O3S_PP(5) O3S_PP(6) O3S_PP(7) O3S_PP(8)
     O3S_PP(9) O3S_PP(10) O3S_PP(11) O3S_PP(12) O3S_PP(13) O3S_PP(14) O3S_PP(15) O3S_PP(16)
