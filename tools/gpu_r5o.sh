@@ -18,3 +18,5 @@ done
 timeout -k 10 300 python -u tools/prof_als_exact.py --users 1000 --items 625000 --other 1000000 --other-item 6250000 --reps 3 --explicit \
   > gpurun_out/r5o_exp.log 2>&1 || { echo "exp failed"; tail -20 gpurun_out/r5o_exp.log; exit 1; }
 echo "explicit (4-step ring): $(grep '^item' gpurun_out/r5o_exp.log | cut -c1-200)"
+timeout -k 10 120 python -u tools/probe_kmeanspp.py > gpurun_out/r5o_kpp_probe.json 2>&1 || { echo 'kpp probe failed'; tail -20 gpurun_out/r5o_kpp_probe.json; exit 1; }
+cat gpurun_out/r5o_kpp_probe.json
