@@ -1257,7 +1257,7 @@ __device__ int pp_draw(const double* __restrict__ cs, int m, double tot, double 
 // fp64 row-major walk spent 0.53 s and the fp64 transposed one 0.11 s streaming 4 MB per
 // step (profiles/kmeans_init_phases_r5.json).  cd [trials][m]: the trial candidates'
 // distances, kept so the d2 update after the pick needs no second pass.
-template <int TRIALS>
+template <int TRIALS, bool LV>
 __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __restrict__ P,
                                                               const float* __restrict__ PT,
                                                               const double* __restrict__ w,
@@ -1267,18 +1267,29 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
                                                               double* __restrict__ cd, int* __restrict__ picks,
                                                               long long* __restrict__ tim) {
   constexpr int trials = TRIALS;          // compile-time: the per-draw arrays stay in registers
-  extern __shared__ double sm[];          // part[kPPThreads], red[16], then [trials][DP] fp32 candidate rows
+  // LDS: part[kPPThreads], red[16], (LV: w, d2, cs [m] each), then [trials][DP] fp32
+  // candidate rows.  LV keeps the per-step vectors in LDS: the scan, the draws' binary
+  // searches and the d2 update then never wait on L2 round trips
+  extern __shared__ double sm[];
   const int DP = (D + kPPU - 1) / kPPU * kPPU;
   double* const part = sm;
   double* const red = part + kPPThreads;
-  float* const sc = reinterpret_cast<float*>(red + 16);
+  double* const lw = red + 16;
+  double* const wv = LV ? lw : const_cast<double*>(w);
+  double* const d2v = LV ? lw + m : d2;
+  double* const csv = LV ? lw + 2 * m : cs;
+  float* const sc = reinterpret_cast<float*>(LV ? lw + 3 * m : lw);
+  if constexpr (LV) {
+    for (int i = threadIdx.x; i < m; i += kPPThreads) lw[i] = w[i];
+    __syncthreads();
+  }
   __shared__ int cand[16];
   __shared__ double pots[16];
   const int tid = threadIdx.x;
   const int nt = trials + 1;
   // step 0: one draw from w
-  double tot = pp_scan(w, nullptr, m, cs, part);
-  if (tid == 0) cand[0] = pp_draw(cs, m, tot, U[0]);
+  double tot = pp_scan(wv, nullptr, m, csv, part);
+  if (tid == 0) cand[0] = pp_draw(csv, m, tot, U[0]);
   __syncthreads();
   const int first = cand[0];
   if (tid == 0) picks[0] = first;
@@ -1293,7 +1304,7 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
 #pragma unroll
       for (int u = 0; u < kPPU; ++u) s = fma(x[u], x[u], s);
     }
-    d2[i] = s;
+    d2v[i] = s;
   }
   __syncthreads();
   // tim (diagnostic, may be null): thread 0's shader-clock totals per phase of the steps:
@@ -1308,9 +1319,9 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
     }
   };
   for (int t = 1; t < k; ++t) {
-    tot = pp_scan(w, d2, m, cs, part);
+    tot = pp_scan(wv, d2v, m, csv, part);
     stamp(0);
-    if (tid < trials) cand[tid] = pp_draw(cs, m, tot, U[(int64_t)t * nt + tid]);
+    if (tid < trials) cand[tid] = pp_draw(csv, m, tot, U[(int64_t)t * nt + tid]);
     __syncthreads();
     stamp(1);
     for (int e = tid; e < trials * DP; e += kPPThreads) {
@@ -1360,7 +1371,7 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
       for (int r = 0; r < RB; ++r) {
         const int i = i0 + r * kPPThreads;
         if (i < m) {
-          const double wi = w[i], di = d2[i], pi = pn[i];
+          const double wi = wv[i], di = d2v[i], pi = pn[i];
 #pragma unroll
           for (int j = 0; j < trials; ++j) {
             const double c = fmax(pi + pc[j] - 2.0 * dot[r][j], 0.0);
@@ -1383,7 +1394,7 @@ __global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __re
       if (pots[j] < pots[best]) best = j;
     if (tid == 0) picks[t] = cand[best];
     // d2 = min(d2, |p - c|^2): this thread's own cd entries (same i walk as above)
-    for (int i = tid; i < m; i += kPPThreads) d2[i] = fmin(d2[i], cd[(int64_t)best * m + i]);
+    for (int i = tid; i < m; i += kPPThreads) d2v[i] = fmin(d2v[i], cd[(int64_t)best * m + i]);
     __syncthreads();
     stamp(5);
   }
@@ -1400,13 +1411,20 @@ O3S_API int o3s_kmeanspp(const double* P, const float* PT, const double* w, cons
                          int trials, const double* U, double* d2, double* cs, double* cd, int* picks,
                          long long* tim, hipStream_t st) {
   if (m <= 0 || k <= 0 || D <= 0 || trials < 1 || trials > 16) return -1;
-  const size_t lds = sizeof(double) * (kPPThreads + 16) + sizeof(float) * (size_t)trials * ((D + kPPU - 1) / kPPU * kPPU);
-  if (lds > 160 * 1024 - 256) return -2;
+  const size_t base = sizeof(double) * (kPPThreads + 16) + sizeof(float) * (size_t)trials * ((D + kPPU - 1) / kPPU * kPPU);
+  if (base > 160 * 1024 - 256) return -2;
+  const size_t lvb = base + sizeof(double) * 3 * (size_t)m;
+  const bool lv = lvb <= 160 * 1024 - 256;            // the per-step vectors fit in LDS
+  const size_t lds = lv ? lvb : base;
   switch (trials) {
 #define O3S_PP(T)                                                                                           \
     case T:                                                                                                 \
-      hipLaunchKernelGGL(kmeanspp_kernel<T>, dim3(1), dim3(kPPThreads), lds, st, P, PT, w, pn, m, D, k, U, d2, cs, \
-                         cd, picks, tim);                                                                   \
+      if (lv)                                                                                               \
+        hipLaunchKernelGGL((kmeanspp_kernel<T, true>), dim3(1), dim3(kPPThreads), lds, st, P, PT, w, pn, m, D, k, \
+                           U, d2, cs, cd, picks, tim);                                                      \
+      else                                                                                                  \
+        hipLaunchKernelGGL((kmeanspp_kernel<T, false>), dim3(1), dim3(kPPThreads), lds, st, P, PT, w, pn, m, D,  \
+                           k, U, d2, cs, cd, picks, tim);                                                   \
       break;
     O3S_PP(1) O3S_PP(2) O3S_PP(3) O3S_PP(4) O3S_PP(5) O3S_PP(6) O3S_PP(7) O3S_PP(8)
     O3S_PP(9) O3S_PP(10) O3S_PP(11) O3S_PP(12) O3S_PP(13) O3S_PP(14) O3S_PP(15) O3S_PP(16)
