@@ -18,5 +18,11 @@ done
 timeout -k 10 300 python -u tools/prof_als_exact.py --users 1000 --items 625000 --other 1000000 --other-item 6250000 --reps 3 --explicit \
   > gpurun_out/r5o_exp.log 2>&1 || { echo "exp failed"; tail -20 gpurun_out/r5o_exp.log; exit 1; }
 echo "explicit (4-step ring): $(grep '^item' gpurun_out/r5o_exp.log | cut -c1-200)"
+timeout -k 10 300 $T tests/test_kmeans.py > gpurun_out/r5o_kmeans_tests.log 2>&1 \
+  || { echo "kmeans tests failed"; grep -E "FAILED|^E " gpurun_out/r5o_kmeans_tests.log | head -20; exit 1; }
+tail -1 gpurun_out/r5o_kmeans_tests.log
+timeout -k 10 300 python -u tools/bench_kmeans_fit.py --iters 10 --repeat 2 > gpurun_out/r5o_kmeans_blobs.json 2> gpurun_out/r5o_kmeans_blobs.err \
+  || { echo "kmeans blobs failed"; tail -20 gpurun_out/r5o_kmeans_blobs.err; exit 1; }
+cut -c1-700 gpurun_out/r5o_kmeans_blobs.json
 timeout -k 10 120 python -u tools/probe_kmeanspp.py > gpurun_out/r5o_kpp_probe.json 2>&1 || { echo 'kpp probe failed'; tail -20 gpurun_out/r5o_kpp_probe.json; exit 1; }
 cat gpurun_out/r5o_kpp_probe.json
