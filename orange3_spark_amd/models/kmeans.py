@@ -121,8 +121,6 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
 # blobs its seeding leaves a 1.9x higher cost after 10 Lloyd iterations (25.0e9 vs
 # 13.3e9, profiles/kmeans_init_phases_r5.json), so the greedy variant is the default
 GREEDY_KMEANSPP = True
-# diagnostic: an int64 device tensor [6] receives kmeanspp_kernel's per-phase clock totals
-KPP_TIMING = None
 
 
 def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: int = 30,
@@ -159,19 +157,23 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
     pn = (Pr * Pr).sum(1)
     tr = trace("kmeans.init.local.seed")
     tr.__enter__()
-    if kernel and P.is_cuda and trials <= 16 and (P.shape[1] + 15) // 16 * 16 * trials * 4 + 8 * 528 <= 150 * 1024:
-        # all k steps in ONE block (kmeanspp_kernel): ~10 kernels per step otherwise
+    if kernel and P.is_cuda and trials <= 16 and trials * P.shape[1] * 8 <= 64 * 1024:
+        # the k greedy steps as 2 launches each (kpp_dist_kernel over every candidate row,
+        # kpp_pick_kernel in one block): no host round trip inside the loop
         from ..ops import _native as N
-        Pc, wc, pc = P.contiguous(), w.to(torch.float64).contiguous(), pn.contiguous()
-        PT = Pc.float().t().contiguous()          # fp32 [D][m]: coalesced, L2-resident candidate reads
+        wc, pc = w.to(torch.float64).contiguous(), pn.contiguous()
+        PT = P.float().t().contiguous()           # fp32 [D][m]: coalesced candidate reads
         Uc = U.contiguous()
         d2 = torch.empty(m, dtype=torch.float64, device=dev)
         cs = torch.empty(m, dtype=torch.float64, device=dev)
         cd = torch.empty((trials, m), dtype=torch.float64, device=dev)
+        partial = torch.empty((-(-m // 256), 16), dtype=torch.float64, device=dev)
+        cand = torch.empty(16, dtype=torch.int32, device=dev)
         picks32 = torch.empty(k, dtype=torch.int32, device=dev)
-        N.check(N.kernels().o3s_kmeanspp(Pc.data_ptr(), PT.data_ptr(), wc.data_ptr(), pc.data_ptr(), m, P.shape[1], k,
-                                         trials, Uc.data_ptr(), d2.data_ptr(), cs.data_ptr(), cd.data_ptr(),
-                                         picks32.data_ptr(), N.ptr(KPP_TIMING), N.stream_of(Pc)), "kmeanspp")
+        N.check(N.kernels().o3s_kmeanspp(PT.data_ptr(), wc.data_ptr(), pc.data_ptr(), m, P.shape[1], k, trials,
+                                         Uc.data_ptr(), d2.data_ptr(), cs.data_ptr(), cd.data_ptr(),
+                                         partial.data_ptr(), cand.data_ptr(), picks32.data_ptr(), N.stream_of(PT)),
+                "kmeanspp")
         picks = picks32.to(torch.int64)
     else:
         first = draw(0, w, 1)[0]

@@ -1188,14 +1188,23 @@ O3S_API int o3s_kmeans_update(const float* X, int64_t n, int64_t ldx, int D, con
 // ---------------------------------------------------------------------------------
 // k-means|| seeding, step 2 (Spark LocalKMeans.kMeansPlusPlus on the weighted candidates):
 // greedy k-means++ -- per step, `trials` weighted draws from w * d2 (inverse CDF over a
-// block prefix sum), each draw's potential sum_i w_i min(d2_i, |p_i - c|^2), the best one
-// kept -- as ONE block that runs all k steps (the previous formulation issued ~10 kernels
-// per step: ~10K launches at k = 1024).  fp64 throughout; distances by the |p|^2 + |c|^2
-// - 2 p.c form of the torch reference (models/kmeans._local_kmeanspp), draws from the
-// same counter-hash uniforms U [k][trials + 1] (so CPU and GPU pick from the same draws).
+// prefix sum), each draw's potential sum_i w_i min(d2_i, |p_i - c|^2), the best one kept.
+// Distances by the |p|^2 + |c|^2 - 2 p.c form of the torch reference
+// (models/kmeans._local_kmeanspp) over fp32-rounded coordinates, products and sums in fp64;
+// draws from the same counter-hash uniforms U [k][trials + 1].
+//
+// Two launches per step, spread over the GPU: kpp_dist_kernel (one row per thread, every
+// candidate row of the chip at once: the trials' distances cd [trials][m] and per-block
+// partial potentials) and kpp_pick_kernel (one block: the potentials summed over the blocks
+// in a fixed order, the pick, d2 = min(d2, cd[best]), the prefix sum of w * d2 in LDS and
+// the next step's draws).  The host loop in o3s_kmeanspp enqueues all 2k launches.  (A
+// single workgroup running all k steps spent 0.17 s of a 0.33 s k-means|| init at k = 1024,
+// m = 4097 -- 94% of it in the fp64 distance sums one CU can issue:
+// profiles/kmeans_init_phases_r5.json.)
 namespace {
-constexpr int kPPThreads = 512;
-constexpr int kPPU = 16;                   // sc row padding (the largest load round)
+constexpr int kPPThreads = 512;             // kpp_pick_kernel
+constexpr int kPDThreads = 256;             // kpp_dist_kernel
+constexpr int kPPMaxT = 16;
 
 __device__ double pp_block_sum(double v, double* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -1204,44 +1213,18 @@ __device__ double pp_block_sum(double v, double* red) {
   if ((threadIdx.x & 63) == 0) red[w] = v;
   __syncthreads();
   double t = 0.0;
-  for (int i = 0; i < kPPThreads / 64; ++i) t += red[i];
+  for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
   return t;
 }
 
-// inclusive prefix sum of prob[i] = w[i] * (d2 ? d2[i] : 1) into cs; returns the total
-__device__ double pp_scan(const double* __restrict__ w, const double* __restrict__ d2, int m, double* cs,
-                          double* part) {
-  const int tid = threadIdx.x;
-  const int per = (m + kPPThreads - 1) / kPPThreads;
-  const int a = tid * per, e = min(m, a + per);
-  double s = 0.0;
-  for (int i = a; i < e; ++i) s += d2 ? w[i] * d2[i] : w[i];
-  __syncthreads();
-  part[tid] = s;
-  __syncthreads();
-  // Hillis-Steele over the 1024 thread totals (10 rounds, fixed order: deterministic)
-  for (int off = 1; off < kPPThreads; off <<= 1) {
-    const double add = tid >= off ? part[tid - off] : 0.0;
-    __syncthreads();
-    part[tid] += add;
-    __syncthreads();
-  }
-  double run = tid ? part[tid - 1] : 0.0;
-  for (int i = a; i < e; ++i) {
-    run += d2 ? w[i] * d2[i] : w[i];
-    cs[i] = run;
-  }
-  __syncthreads();
-  return part[kPPThreads - 1];
-}
-
-__device__ int pp_draw(const double* __restrict__ cs, int m, double tot, double u) {
+// first index i with cs[i] > u * tot (searchsorted right), clamped; tot <= 0: uniform
+__device__ int pp_draw(const double* cs, int m, double tot, double u) {
   if (!(tot > 0.0)) {
     const long long r = (long long)(u * m);
     return (int)(r < m - 1 ? r : m - 1);
   }
   const double x = u * tot;
-  int lo = 0, hi = m;                      // first i with cs[i] > x (searchsorted right)
+  int lo = 0, hi = m;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     if (cs[mid] > x) hi = mid; else lo = mid + 1;
@@ -1249,187 +1232,173 @@ __device__ int pp_draw(const double* __restrict__ cs, int m, double tot, double 
   return lo < m - 1 ? lo : m - 1;
 }
 
-// PT: the candidates transposed ([D][m]) and rounded to fp32 (the seeding distances use
-// fp32-rounded coordinates, products and sums in fp64; the torch path rounds the same way):
-// thread i reads coordinate d of candidate i at PT[d m + i], so a wave's loads are one
-// contiguous 256-B run, and the whole matrix (2 MB at 4K candidates x 128) stays in the
-// XCD's L2 across the k steps -- a single workgroup pulls ~10 B/cycle from HBM, so the
-// fp64 row-major walk spent 0.53 s and the fp64 transposed one 0.11 s streaming 4 MB per
-// step (profiles/kmeans_init_phases_r5.json).  cd [trials][m]: the trial candidates'
-// distances, kept so the d2 update after the pick needs no second pass.
-template <int TRIALS, bool LV>
-__global__ __launch_bounds__(kPPThreads) void kmeanspp_kernel(const double* __restrict__ P,
-                                                              const float* __restrict__ PT,
-                                                              const double* __restrict__ w,
-                                                              const double* __restrict__ pn, int m, int D, int k,
-                                                              const double* __restrict__ U,
-                                                              double* __restrict__ d2, double* __restrict__ cs,
-                                                              double* __restrict__ cd, int* __restrict__ picks,
-                                                              long long* __restrict__ tim) {
-  constexpr int trials = TRIALS;          // compile-time: the per-draw arrays stay in registers
-  // LDS: part[kPPThreads], red[16], (LV: w, d2, cs [m] each), then [trials][DP] fp32
-  // candidate rows.  LV keeps the per-step vectors in LDS: the scan, the draws' binary
-  // searches and the d2 update then never wait on L2 round trips
-  extern __shared__ double sm[];
-  const int DP = (D + kPPU - 1) / kPPU * kPPU;
-  double* const part = sm;
-  double* const red = part + kPPThreads;
-  double* const lw = red + 16;
-  double* const wv = LV ? lw : const_cast<double*>(w);
-  double* const d2v = LV ? lw + m : d2;
-  double* const csv = LV ? lw + 2 * m : cs;
-  float* const sc = reinterpret_cast<float*>(LV ? lw + 3 * m : lw);
-  if constexpr (LV) {
-    for (int i = threadIdx.x; i < m; i += kPPThreads) lw[i] = w[i];
-    __syncthreads();
+// mode 0: d2[i] = |p_i - p_cand[0]|^2 (the first centre); mode 1: cd[j][i] = distance of
+// row i to trial candidate j and partial[block][j] = sum over the block's rows of
+// w_i min(d2_i, cd[j][i]).  PT: fp32 [D][m]; pn: |p|^2 of the rounded rows (fp64).
+__global__ __launch_bounds__(kPDThreads) void kpp_dist_kernel(const float* __restrict__ PT,
+                                                               const double* __restrict__ w,
+                                                               const double* __restrict__ pn, int m, int D,
+                                                               int trials, const int* __restrict__ cand, int mode,
+                                                               double* __restrict__ d2, double* __restrict__ cd,
+                                                               double* __restrict__ partial) {
+  extern __shared__ double sc[];            // [trials][D] candidate coordinates
+  __shared__ double red[kPDThreads / 64];
+  const int nt = mode == 0 ? 1 : trials;
+  for (int e = threadIdx.x; e < nt * D; e += kPDThreads) {
+    const int j = e / D, d = e - j * D;
+    sc[e] = (double)PT[(int64_t)d * m + cand[j]];
   }
-  __shared__ int cand[16];
-  __shared__ double pots[16];
+  __syncthreads();
+  const int i = blockIdx.x * kPDThreads + threadIdx.x;
+  const bool ok = i < m;
+  const int ic = ok ? i : m - 1;
+  // 8 coordinates per round, loaded before use (one L2 round trip per 8 instead of per 1)
+  constexpr int UD = 8;
+  if (mode == 0) {
+    double s = 0.0;
+    for (int d0 = 0; d0 < D; d0 += UD) {
+      float x[UD];
+#pragma unroll
+      for (int u = 0; u < UD; ++u) x[u] = d0 + u < D ? PT[(int64_t)(d0 + u) * m + ic] : 0.f;
+#pragma unroll
+      for (int u = 0; u < UD; ++u)
+        if (d0 + u < D) {
+          const double t = (double)x[u] - sc[d0 + u];
+          s = fma(t, t, s);
+        }
+    }
+    if (ok) d2[i] = s;
+    return;
+  }
+  double dot[kPPMaxT];
+#pragma unroll
+  for (int j = 0; j < kPPMaxT; ++j) dot[j] = 0.0;
+  for (int d0 = 0; d0 < D; d0 += UD) {
+    float x[UD];
+#pragma unroll
+    for (int u = 0; u < UD; ++u) x[u] = d0 + u < D ? PT[(int64_t)(d0 + u) * m + ic] : 0.f;
+#pragma unroll
+    for (int u = 0; u < UD; ++u) {
+      if (d0 + u < D) {
+        const double xv = (double)x[u];
+#pragma unroll
+        for (int j = 0; j < kPPMaxT; ++j)
+          if (j < nt) dot[j] = fma(xv, sc[j * D + d0 + u], dot[j]);
+      }
+    }
+  }
+  const double wi = ok ? w[i] : 0.0, di = ok ? d2[i] : 0.0, pi = pn[ic];
+#pragma unroll
+  for (int j = 0; j < kPPMaxT; ++j) {
+    if (j < nt) {
+      const double c = fmax(pi + pn[cand[j]] - 2.0 * dot[j], 0.0);
+      if (ok) cd[(int64_t)j * m + i] = c;
+      const double s = pp_block_sum(wi * fmin(di, c), red);
+      if (threadIdx.x == 0) partial[(int64_t)blockIdx.x * kPPMaxT + j] = s;
+    }
+  }
+}
+
+// One block.  mode 0 (t = 1): prefix sum of w * d2, the step-1 draws.  mode 1 (step t):
+// pick = argmin of the trials' potentials (block partials summed in order), picks[t],
+// d2 = min(d2, cd[best]), then (t + 1 < k) the prefix sum and step t+1's draws.  mode 2
+// (t = 0): prefix sum of w alone and the first draw.  LDS: cs [m] (m <= kPPLdsRows) else
+// the global cs.
+constexpr int kPPLdsRows = 16384;
+__global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __restrict__ w, int m, int k, int trials,
+                                                               const double* __restrict__ U, int t, int mode,
+                                                               int nblocks, const double* __restrict__ partial,
+                                                               const double* __restrict__ cd, double* __restrict__ d2,
+                                                               double* __restrict__ csg, int* __restrict__ cand,
+                                                               int* __restrict__ picks) {
+  extern __shared__ double lcs[];
+  __shared__ double part[kPPThreads];
+  __shared__ int s_best;
+  double* const cs = m <= kPPLdsRows ? lcs : csg;
   const int tid = threadIdx.x;
   const int nt = trials + 1;
-  // step 0: one draw from w
-  double tot = pp_scan(wv, nullptr, m, csv, part);
-  if (tid == 0) cand[0] = pp_draw(csv, m, tot, U[0]);
-  __syncthreads();
-  const int first = cand[0];
-  if (tid == 0) picks[0] = first;
-  for (int e = tid; e < D; e += kPPThreads) sc[e] = PT[(int64_t)e * m + first];
-  __syncthreads();
-  for (int i = tid; i < m; i += kPPThreads) {
-    double s = 0.0;
-    for (int d0 = 0; d0 < D; d0 += kPPU) {
-      double x[kPPU];
-#pragma unroll
-      for (int u = 0; u < kPPU; ++u) x[u] = d0 + u < D ? (double)PT[(int64_t)(d0 + u) * m + i] - (double)sc[d0 + u] : 0.0;
-#pragma unroll
-      for (int u = 0; u < kPPU; ++u) s = fma(x[u], x[u], s);
-    }
-    d2v[i] = s;
-  }
-  __syncthreads();
-  // tim (diagnostic, may be null): thread 0's shader-clock totals per phase of the steps:
-  // [scan, draw, candidate rows, distances + potentials, pick, d2 update]
-  long long tacc[6] = {0, 0, 0, 0, 0, 0};
-  long long tp = tim ? (long long)clock64() : 0;
-  auto stamp = [&](int ph) {
-    if (tim) {
-      const long long now = (long long)clock64();
-      tacc[ph] += now - tp;
-      tp = now;
-    }
-  };
-  for (int t = 1; t < k; ++t) {
-    tot = pp_scan(wv, d2v, m, csv, part);
-    stamp(0);
-    if (tid < trials) cand[tid] = pp_draw(csv, m, tot, U[(int64_t)t * nt + tid]);
-    __syncthreads();
-    stamp(1);
-    for (int e = tid; e < trials * DP; e += kPPThreads) {
-      const int j = e / DP, d = e - j * DP;
-      sc[e] = d < D ? PT[(int64_t)d * m + cand[j]] : 0.f;
-    }
-    double pc[trials];
-#pragma unroll
-    for (int j = 0; j < trials; ++j) pc[j] = pn[cand[j]];
-    __syncthreads();
-    stamp(2);
-    double acc[trials];
-#pragma unroll
-    for (int j = 0; j < trials; ++j) acc[j] = 0.0;
-    // register blocking: RB rows x trials dot products per thread; each round loads RB x U
-    // fp32 coordinates (coalesced, U = 16 up to 8 trials: the step is a chain of load
-    // rounds -- 2 waves per SIMD hide little of the L2 latency -- so each round carries as
-    // many loads as the registers allow) and the trials' centre values from LDS
-    constexpr int RB = TRIALS <= 8 ? 4 : 2;
-    constexpr int U = TRIALS <= 4 ? 16 : (TRIALS <= 8 ? 8 : 4);
-    for (int i0 = tid; i0 < m; i0 += RB * kPPThreads) {
-      double dot[RB][trials];
-#pragma unroll
-      for (int r = 0; r < RB; ++r)
-#pragma unroll
-        for (int j = 0; j < trials; ++j) dot[r][j] = 0.0;
-      for (int d0 = 0; d0 < D; d0 += U) {
-        float x[RB][U];
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-          const int i = i0 + r * kPPThreads;
-#pragma unroll
-          for (int u = 0; u < U; ++u) x[r][u] = (i < m && d0 + u < D) ? PT[(int64_t)(d0 + u) * m + i] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          double c[trials];
-#pragma unroll
-          for (int j = 0; j < trials; ++j) c[j] = (double)sc[j * DP + d0 + u];
-#pragma unroll
-          for (int r = 0; r < RB; ++r)
-#pragma unroll
-            for (int j = 0; j < trials; ++j) dot[r][j] = fma((double)x[r][u], c[j], dot[r][j]);
-        }
+  if (mode == 1) {
+    if (tid == 0) {
+      int best = 0;
+      double bp = 0.0;
+      for (int j = 0; j < trials; ++j) {
+        double p = 0.0;
+        for (int b = 0; b < nblocks; ++b) p += partial[(int64_t)b * kPPMaxT + j];
+        if (j == 0 || p < bp) { bp = p; best = j; }
       }
-#pragma unroll
-      for (int r = 0; r < RB; ++r) {
-        const int i = i0 + r * kPPThreads;
-        if (i < m) {
-          const double wi = wv[i], di = d2v[i], pi = pn[i];
-#pragma unroll
-          for (int j = 0; j < trials; ++j) {
-            const double c = fmax(pi + pc[j] - 2.0 * dot[r][j], 0.0);
-            cd[(int64_t)j * m + i] = c;
-            acc[j] += wi * fmin(di, c);
-          }
-        }
-      }
-    }
-    stamp(3);
-#pragma unroll
-    for (int j = 0; j < trials; ++j) {
-      const double s = pp_block_sum(acc[j], red);
-      if (tid == 0) pots[j] = s;
+      s_best = best;
+      picks[t] = cand[best];
     }
     __syncthreads();
-    stamp(4);
-    int best = 0;
-    for (int j = 1; j < trials; ++j)
-      if (pots[j] < pots[best]) best = j;
-    if (tid == 0) picks[t] = cand[best];
-    // d2 = min(d2, |p - c|^2): this thread's own cd entries (same i walk as above)
-    for (int i = tid; i < m; i += kPPThreads) d2v[i] = fmin(d2v[i], cd[(int64_t)best * m + i]);
-    __syncthreads();
-    stamp(5);
+    if (t + 1 >= k) return;                  // last step: d2 is not needed any more
   }
-  if (tim && tid == 0)
-    for (int ph = 0; ph < 6; ++ph) tim[ph] = tacc[ph];
+  const int best = mode == 1 ? s_best : 0;
+  // per-thread contiguous chunk: p_i = w_i * d2_i (d2 updated with the pick first)
+  const int per = (m + kPPThreads - 1) / kPPThreads;
+  const int a = tid * per, e = min(m, a + per);
+  double s = 0.0;
+  for (int i = a; i < e; ++i) {
+    double pi = w[i];
+    if (mode != 2) {
+      double di = d2[i];
+      if (mode == 1) {
+        di = fmin(di, cd[(int64_t)best * m + i]);
+        d2[i] = di;
+      }
+      pi *= di;
+    }
+    s += pi;
+    cs[i] = s;                               // local running sum, offset below
+  }
+  part[tid] = s;
+  __syncthreads();
+  for (int off = 1; off < kPPThreads; off <<= 1) {   // Hillis-Steele, fixed order
+    const double add = tid >= off ? part[tid - off] : 0.0;
+    __syncthreads();
+    part[tid] += add;
+    __syncthreads();
+  }
+  const double base = tid ? part[tid - 1] : 0.0;
+  for (int i = a; i < e; ++i) cs[i] += base;
+  __syncthreads();
+  const double tot = part[kPPThreads - 1];
+  if (mode == 2) {
+    if (tid == 0) {
+      const int first = pp_draw(cs, m, tot, U[0]);
+      cand[0] = first;
+      picks[0] = first;
+    }
+  } else {
+    const int tn = mode == 0 ? 1 : t + 1;    // the step the draws are for
+    if (tid < trials) cand[tid] = pp_draw(cs, m, tot, U[(int64_t)tn * nt + tid]);
+  }
 }
 }  // namespace
 
-// P [m][D] fp64 candidates (unused by the kernel) and PT = fp32(P)^T [D][m], w [m] weights,
-// pn [m] = |fp32(p)|^2 (fp64 sums), U [k][trials
-// + 1] uniforms; ws: d2 [m], cs [m], cd [trials][m] fp64 scratch; picks [k] int32 out.
-// trials <= 16.
-O3S_API int o3s_kmeanspp(const double* P, const float* PT, const double* w, const double* pn, int m, int D, int k,
-                         int trials, const double* U, double* d2, double* cs, double* cd, int* picks,
-                         long long* tim, hipStream_t st) {
-  if (m <= 0 || k <= 0 || D <= 0 || trials < 1 || trials > 16) return -1;
-  const size_t base = sizeof(double) * (kPPThreads + 16) + sizeof(float) * (size_t)trials * ((D + kPPU - 1) / kPPU * kPPU);
-  if (base > 160 * 1024 - 256) return -2;
-  const size_t lvb = base + sizeof(double) * 3 * (size_t)m;
-  const bool lv = lvb <= 160 * 1024 - 256;            // the per-step vectors fit in LDS
-  const size_t lds = lv ? lvb : base;
-  switch (trials) {
-#define O3S_PP(T)                                                                                           \
-    case T:                                                                                                 \
-      if (lv)                                                                                               \
-        hipLaunchKernelGGL((kmeanspp_kernel<T, true>), dim3(1), dim3(kPPThreads), lds, st, P, PT, w, pn, m, D, k, \
-                           U, d2, cs, cd, picks, tim);                                                      \
-      else                                                                                                  \
-        hipLaunchKernelGGL((kmeanspp_kernel<T, false>), dim3(1), dim3(kPPThreads), lds, st, P, PT, w, pn, m, D,  \
-                           k, U, d2, cs, cd, picks, tim);                                                   \
-      break;
-    O3S_PP(1) O3S_PP(2) O3S_PP(3) O3S_PP(4) O3S_PP(5) O3S_PP(6) O3S_PP(7) O3S_PP(8)
-    O3S_PP(9) O3S_PP(10) O3S_PP(11) O3S_PP(12) O3S_PP(13) O3S_PP(14) O3S_PP(15) O3S_PP(16)
-#undef O3S_PP
-    default: return -1;
+// PT = fp32(P)^T [D][m], w [m] weights, pn [m] = |fp32(p)|^2 (fp64 sums), U [k][trials + 1]
+// uniforms; ws: d2 [m], cs [m], cd [trials][m] fp64, partial [ceil(m / 256)][16] fp64,
+// cand [16] int32 scratch; picks [k] int32 out.  trials <= 16.
+O3S_API int o3s_kmeanspp(const float* PT, const double* w, const double* pn, int m, int D, int k, int trials,
+                         const double* U, double* d2, double* cs, double* cd, double* partial, int* cand,
+                         int* picks, hipStream_t st) {
+  if (m <= 0 || k <= 0 || D <= 0 || trials < 1 || trials > kPPMaxT) return -1;
+  const size_t dl = sizeof(double) * (size_t)trials * D;
+  if (dl > 64 * 1024) return -2;
+  const int nb = (m + kPDThreads - 1) / kPDThreads;
+  const size_t pl = m <= kPPLdsRows ? sizeof(double) * (size_t)m : 0;
+  hipLaunchKernelGGL(kpp_pick_kernel, dim3(1), dim3(kPPThreads), pl, st, w, m, k, trials, U, 0, 2, nb, partial, cd, d2,
+                     cs, cand, picks);
+  if (k > 1) {
+    hipLaunchKernelGGL(kpp_dist_kernel, dim3(nb), dim3(kPDThreads), sizeof(double) * D, st, PT, w, pn, m, D, trials,
+                       cand, 0, d2, cd, partial);
+    hipLaunchKernelGGL(kpp_pick_kernel, dim3(1), dim3(kPPThreads), pl, st, w, m, k, trials, U, 1, 0, nb, partial, cd,
+                       d2, cs, cand, picks);
+  }
+  for (int t = 1; t < k; ++t) {
+    hipLaunchKernelGGL(kpp_dist_kernel, dim3(nb), dim3(kPDThreads), dl, st, PT, w, pn, m, D, trials, cand, 1, d2, cd,
+                       partial);
+    hipLaunchKernelGGL(kpp_pick_kernel, dim3(1), dim3(kPPThreads), pl, st, w, m, k, trials, U, t, 1, nb, partial, cd,
+                       d2, cs, cand, picks);
   }
   O3S_CHECK_LAUNCH();
   return 0;
