@@ -1318,14 +1318,26 @@ __global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __re
   const int tid = threadIdx.x;
   const int nt = trials + 1;
   if (mode == 1) {
+    // trial j's potential = its block partials summed in block order: the partials are
+    // loaded by all threads at once (part[] as staging), then summed per trial from LDS
+    double pj = 0.0;
+    for (int b0 = 0; b0 < nblocks; b0 += kPPThreads / kPPMaxT) {
+      const int bb = b0 + tid / kPPMaxT, jj = tid % kPPMaxT;
+      __syncthreads();
+      part[tid] = (bb < nblocks && jj < trials) ? partial[(int64_t)bb * kPPMaxT + jj] : 0.0;
+      __syncthreads();
+      if (tid < trials) {
+        const int nb = min(kPPThreads / kPPMaxT, nblocks - b0);
+        for (int q = 0; q < nb; ++q) pj += part[q * kPPMaxT + tid];
+      }
+    }
+    __syncthreads();
+    if (tid < trials) part[tid] = pj;
+    __syncthreads();
     if (tid == 0) {
       int best = 0;
-      double bp = 0.0;
-      for (int j = 0; j < trials; ++j) {
-        double p = 0.0;
-        for (int b = 0; b < nblocks; ++b) p += partial[(int64_t)b * kPPMaxT + j];
-        if (j == 0 || p < bp) { bp = p; best = j; }
-      }
+      for (int j = 1; j < trials; ++j)
+        if (part[j] < part[best]) best = j;
       s_best = best;
       picks[t] = cand[best];
     }
@@ -1333,11 +1345,9 @@ __global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __re
     if (t + 1 >= k) return;                  // last step: d2 is not needed any more
   }
   const int best = mode == 1 ? s_best : 0;
-  // per-thread contiguous chunk: p_i = w_i * d2_i (d2 updated with the pick first)
-  const int per = (m + kPPThreads - 1) / kPPThreads;
-  const int a = tid * per, e = min(m, a + per);
-  double s = 0.0;
-  for (int i = a; i < e; ++i) {
+  // p_i = w_i * d2_i (d2 updated with the pick first): coalesced pass into cs, then each
+  // thread scans its contiguous chunk of cs
+  for (int i = tid; i < m; i += kPPThreads) {
     double pi = w[i];
     if (mode != 2) {
       double di = d2[i];
@@ -1347,7 +1357,14 @@ __global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __re
       }
       pi *= di;
     }
-    s += pi;
+    cs[i] = pi;
+  }
+  __syncthreads();
+  const int per = (m + kPPThreads - 1) / kPPThreads;
+  const int a = tid * per, e = min(m, a + per);
+  double s = 0.0;
+  for (int i = a; i < e; ++i) {
+    s += cs[i];
     cs[i] = s;                               // local running sum, offset below
   }
   part[tid] = s;
