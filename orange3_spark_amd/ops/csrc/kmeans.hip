@@ -27,6 +27,8 @@
 // registers; a cluster's sum is flushed once per chunk into the block's private slab.
 // (The bucket order is row order, produced by a stable ballot-ranked scatter.)
 // Slabs are summed by kmeans_reduce in a fixed order (bitwise deterministic).
+#include <hip/hip_cooperative_groups.h>
+
 #include "common.h"
 
 using namespace o3s;
@@ -1235,21 +1237,17 @@ __device__ int pp_draw(const double* cs, int m, double tot, double u) {
 // mode 0: d2[i] = |p_i - p_cand[0]|^2 (the first centre); mode 1: cd[j][i] = distance of
 // row i to trial candidate j and partial[block][j] = sum over the block's rows of
 // w_i min(d2_i, cd[j][i]).  PT: fp32 [D][m]; pn: |p|^2 of the rounded rows (fp64).
-__global__ __launch_bounds__(kPDThreads) void kpp_dist_kernel(const float* __restrict__ PT,
-                                                               const double* __restrict__ w,
-                                                               const double* __restrict__ pn, int m, int D,
-                                                               int trials, const int* __restrict__ cand, int mode,
-                                                               double* __restrict__ d2, double* __restrict__ cd,
-                                                               double* __restrict__ partial) {
-  extern __shared__ double sc[];            // [trials][D] candidate coordinates
-  __shared__ double red[kPDThreads / 64];
+__device__ void kpp_dist(const float* __restrict__ PT, const double* __restrict__ w, const double* __restrict__ pn,
+                         int m, int D, int trials, const int* __restrict__ cand, int mode, double* __restrict__ d2,
+                         double* __restrict__ cd, double* __restrict__ partial, int blk, double* sc, double* red) {
+  // sc: [trials][D] candidate coordinates (LDS); red: [kPDThreads / 64]
   const int nt = mode == 0 ? 1 : trials;
   for (int e = threadIdx.x; e < nt * D; e += kPDThreads) {
     const int j = e / D, d = e - j * D;
     sc[e] = (double)PT[(int64_t)d * m + cand[j]];
   }
   __syncthreads();
-  const int i = blockIdx.x * kPDThreads + threadIdx.x;
+  const int i = blk * kPDThreads + threadIdx.x;
   const bool ok = i < m;
   const int ic = ok ? i : m - 1;
   // 8 coordinates per round, loaded before use (one L2 round trip per 8 instead of per 1)
@@ -1294,9 +1292,20 @@ __global__ __launch_bounds__(kPDThreads) void kpp_dist_kernel(const float* __res
       const double c = fmax(pi + pn[cand[j]] - 2.0 * dot[j], 0.0);
       if (ok) cd[(int64_t)j * m + i] = c;
       const double s = pp_block_sum(wi * fmin(di, c), red);
-      if (threadIdx.x == 0) partial[(int64_t)blockIdx.x * kPPMaxT + j] = s;
+      if (threadIdx.x == 0) partial[(int64_t)blk * kPPMaxT + j] = s;
     }
   }
+}
+
+__global__ __launch_bounds__(kPDThreads) void kpp_dist_kernel(const float* __restrict__ PT,
+                                                               const double* __restrict__ w,
+                                                               const double* __restrict__ pn, int m, int D,
+                                                               int trials, const int* __restrict__ cand, int mode,
+                                                               double* __restrict__ d2, double* __restrict__ cd,
+                                                               double* __restrict__ partial) {
+  extern __shared__ double sc[];
+  __shared__ double red[kPDThreads / 64];
+  kpp_dist(PT, w, pn, m, D, trials, cand, mode, d2, cd, partial, blockIdx.x, sc, red);
 }
 
 // One block.  mode 0 (t = 1): prefix sum of w * d2, the step-1 draws.  mode 1 (step t):
@@ -1305,29 +1314,25 @@ __global__ __launch_bounds__(kPDThreads) void kpp_dist_kernel(const float* __res
 // (t = 0): prefix sum of w alone and the first draw.  LDS: cs [m] (m <= kPPLdsRows) else
 // the global cs.
 constexpr int kPPLdsRows = 16384;
-__global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __restrict__ w, int m, int k, int trials,
-                                                               const double* __restrict__ U, int t, int mode,
-                                                               int nblocks, const double* __restrict__ partial,
-                                                               const double* __restrict__ cd, double* __restrict__ d2,
-                                                               double* __restrict__ csg, int* __restrict__ cand,
-                                                               int* __restrict__ picks) {
-  extern __shared__ double lcs[];
-  __shared__ double part[kPPThreads];
-  __shared__ int s_best;
-  double* const cs = m <= kPPLdsRows ? lcs : csg;
+template <int NTH>
+__device__ void kpp_pick(const double* __restrict__ w, int m, int k, int trials, const double* __restrict__ U, int t,
+                         int mode, int nblocks, const double* __restrict__ partial, const double* __restrict__ cd,
+                         double* __restrict__ d2, double* __restrict__ csg, int* __restrict__ cand,
+                         int* __restrict__ picks, double* lcs, double* part, int& s_best) {
+  double* const cs = lcs != nullptr ? lcs : csg;
   const int tid = threadIdx.x;
   const int nt = trials + 1;
   if (mode == 1) {
     // trial j's potential = its block partials summed in block order: the partials are
     // loaded by all threads at once (part[] as staging), then summed per trial from LDS
     double pj = 0.0;
-    for (int b0 = 0; b0 < nblocks; b0 += kPPThreads / kPPMaxT) {
+    for (int b0 = 0; b0 < nblocks; b0 += NTH / kPPMaxT) {
       const int bb = b0 + tid / kPPMaxT, jj = tid % kPPMaxT;
       __syncthreads();
       part[tid] = (bb < nblocks && jj < trials) ? partial[(int64_t)bb * kPPMaxT + jj] : 0.0;
       __syncthreads();
       if (tid < trials) {
-        const int nb = min(kPPThreads / kPPMaxT, nblocks - b0);
+        const int nb = min(NTH / kPPMaxT, nblocks - b0);
         for (int q = 0; q < nb; ++q) pj += part[q * kPPMaxT + tid];
       }
     }
@@ -1347,7 +1352,7 @@ __global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __re
   const int best = mode == 1 ? s_best : 0;
   // p_i = w_i * d2_i (d2 updated with the pick first): coalesced pass into cs, then each
   // thread scans its contiguous chunk of cs
-  for (int i = tid; i < m; i += kPPThreads) {
+  for (int i = tid; i < m; i += NTH) {
     double pi = w[i];
     if (mode != 2) {
       double di = d2[i];
@@ -1360,7 +1365,7 @@ __global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __re
     cs[i] = pi;
   }
   __syncthreads();
-  const int per = (m + kPPThreads - 1) / kPPThreads;
+  const int per = (m + NTH - 1) / NTH;
   const int a = tid * per, e = min(m, a + per);
   double s = 0.0;
   for (int i = a; i < e; ++i) {
@@ -1369,7 +1374,7 @@ __global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __re
   }
   part[tid] = s;
   __syncthreads();
-  for (int off = 1; off < kPPThreads; off <<= 1) {   // Hillis-Steele, fixed order
+  for (int off = 1; off < NTH; off <<= 1) {   // Hillis-Steele, fixed order
     const double add = tid >= off ? part[tid - off] : 0.0;
     __syncthreads();
     part[tid] += add;
@@ -1378,7 +1383,7 @@ __global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __re
   const double base = tid ? part[tid - 1] : 0.0;
   for (int i = a; i < e; ++i) cs[i] += base;
   __syncthreads();
-  const double tot = part[kPPThreads - 1];
+  const double tot = part[NTH - 1];
   if (mode == 2) {
     if (tid == 0) {
       const int first = pp_draw(cs, m, tot, U[0]);
@@ -1388,6 +1393,56 @@ __global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __re
   } else {
     const int tn = mode == 0 ? 1 : t + 1;    // the step the draws are for
     if (tid < trials) cand[tid] = pp_draw(cs, m, tot, U[(int64_t)tn * nt + tid]);
+  }
+}
+
+__global__ __launch_bounds__(kPPThreads) void kpp_pick_kernel(const double* __restrict__ w, int m, int k, int trials,
+                                                               const double* __restrict__ U, int t, int mode,
+                                                               int nblocks, const double* __restrict__ partial,
+                                                               const double* __restrict__ cd, double* __restrict__ d2,
+                                                               double* __restrict__ csg, int* __restrict__ cand,
+                                                               int* __restrict__ picks) {
+  extern __shared__ double lcs[];
+  __shared__ double part[kPPThreads];
+  __shared__ int s_best;
+  kpp_pick<kPPThreads>(w, m, k, trials, U, t, mode, nblocks, partial, cd, d2, csg, cand, picks,
+                       m <= kPPLdsRows ? lcs : nullptr, part, s_best);
+}
+
+// All k steps in ONE cooperative launch: the distance phase on every block, the pick on
+// block 0, separated by grid-wide barriers (two per step) -- the same arithmetic as the
+// two-launch loop without 2k kernel launches.  dyn: [trials][D] candidate coordinates,
+// then (lds_cs) cs [m].
+__global__ __launch_bounds__(kPDThreads) void kpp_coop_kernel(const float* __restrict__ PT,
+                                                               const double* __restrict__ w,
+                                                               const double* __restrict__ pn, int m, int D, int k,
+                                                               int trials, const double* __restrict__ U,
+                                                               double* __restrict__ d2, double* __restrict__ csg,
+                                                               double* __restrict__ cd, double* __restrict__ partial,
+                                                               int* __restrict__ cand, int* __restrict__ picks,
+                                                               int lds_cs) {
+  extern __shared__ double dyn[];
+  __shared__ double red[kPDThreads / 64];
+  __shared__ double part[kPDThreads];
+  __shared__ int s_best;
+  cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+  const int nb = (int)gridDim.x;
+  double* const sc = dyn;
+  double* const lcs = lds_cs ? dyn + (int64_t)trials * D : nullptr;
+  const bool lead = blockIdx.x == 0;
+  if (lead) kpp_pick<kPDThreads>(w, m, k, trials, U, 0, 2, nb, partial, cd, d2, csg, cand, picks, lcs, part, s_best);
+  grid.sync();
+  if (k > 1) {
+    kpp_dist(PT, w, pn, m, D, trials, cand, 0, d2, cd, partial, blockIdx.x, sc, red);
+    grid.sync();
+    if (lead) kpp_pick<kPDThreads>(w, m, k, trials, U, 1, 0, nb, partial, cd, d2, csg, cand, picks, lcs, part, s_best);
+    grid.sync();
+  }
+  for (int t = 1; t < k; ++t) {
+    kpp_dist(PT, w, pn, m, D, trials, cand, 1, d2, cd, partial, blockIdx.x, sc, red);
+    grid.sync();
+    if (lead) kpp_pick<kPDThreads>(w, m, k, trials, U, t, 1, nb, partial, cd, d2, csg, cand, picks, lcs, part, s_best);
+    grid.sync();
   }
 }
 }  // namespace
@@ -1403,6 +1458,18 @@ O3S_API int o3s_kmeanspp(const float* PT, const double* w, const double* pn, int
   if (dl > 64 * 1024) return -2;
   const int nb = (m + kPDThreads - 1) / kPDThreads;
   const size_t pl = m <= kPPLdsRows ? sizeof(double) * (size_t)m : 0;
+  {
+    const int lds_cs = dl + sizeof(double) * (size_t)m <= 96 * 1024 ? 1 : 0;
+    const size_t cl = dl + (lds_cs ? sizeof(double) * (size_t)m : 0);
+    void* args[] = {(void*)&PT, (void*)&w, (void*)&pn, (void*)&m, (void*)&D, (void*)&k, (void*)&trials, (void*)&U,
+                    (void*)&d2, (void*)&cs, (void*)&cd, (void*)&partial, (void*)&cand, (void*)&picks, (void*)&lds_cs};
+    if (hipLaunchCooperativeKernel((const void*)kpp_coop_kernel, dim3(nb), dim3(kPDThreads), args, cl, st) ==
+        hipSuccess) {
+      O3S_CHECK_LAUNCH();
+      return 0;
+    }
+    (void)hipGetLastError();                  // not co-resident: the two-launch loop below
+  }
   hipLaunchKernelGGL(kpp_pick_kernel, dim3(1), dim3(kPPThreads), pl, st, w, m, k, trials, U, 0, 2, nb, partial, cd, d2,
                      cs, cand, picks);
   if (k > 1) {
