@@ -1449,16 +1449,17 @@ __global__ __launch_bounds__(kPDThreads) void kpp_coop_kernel(const float* __res
 
 // PT = fp32(P)^T [D][m], w [m] weights, pn [m] = |fp32(p)|^2 (fp64 sums), U [k][trials + 1]
 // uniforms; ws: d2 [m], cs [m], cd [trials][m] fp64, partial [ceil(m / 256)][16] fp64,
-// cand [16] int32 scratch; picks [k] int32 out.  trials <= 16.
+// cand [16] int32 scratch; picks [k] int32 out.  trials <= 16.  coop: one cooperative launch
+// (falls back to 2 launches per step when the grid cannot be co-resident); 0: the 2k launches.
 O3S_API int o3s_kmeanspp(const float* PT, const double* w, const double* pn, int m, int D, int k, int trials,
                          const double* U, double* d2, double* cs, double* cd, double* partial, int* cand,
-                         int* picks, hipStream_t st) {
+                         int* picks, int coop, hipStream_t st) {
   if (m <= 0 || k <= 0 || D <= 0 || trials < 1 || trials > kPPMaxT) return -1;
   const size_t dl = sizeof(double) * (size_t)trials * D;
   if (dl > 64 * 1024) return -2;
   const int nb = (m + kPDThreads - 1) / kPDThreads;
   const size_t pl = m <= kPPLdsRows ? sizeof(double) * (size_t)m : 0;
-  {
+  if (coop) {
     const int lds_cs = dl + sizeof(double) * (size_t)m <= 96 * 1024 ? 1 : 0;
     const size_t cl = dl + (lds_cs ? sizeof(double) * (size_t)m : 0);
     void* args[] = {(void*)&PT, (void*)&w, (void*)&pn, (void*)&m, (void*)&D, (void*)&k, (void*)&trials, (void*)&U,

@@ -330,11 +330,14 @@ def test_gpu_presplit_dropped_after_fit(gpu, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,m,D", [(16, 300, 8), (256, 1500, 64), (1024, 4100, 128)])
-def test_gpu_kmeanspp_kernel_matches_torch_steps(gpu, k, m, D):
+@pytest.mark.parametrize("coop", [True, False])
+def test_gpu_kmeanspp_kernel_matches_torch_steps(gpu, k, m, D, coop, monkeypatch):
     """kmeanspp_kernel (all greedy k-means++ steps in one block) picks the same candidates
     as the step-by-step torch formulation from the same draws (fp64; then the shared
     Lloyd refinement gives the same centres)."""
+    from orange3_spark_amd.models import kmeans as KMM
     from orange3_spark_amd.models.kmeans import _local_kmeanspp
+    monkeypatch.setattr(KMM, "KPP_COOP", coop)
     g = torch.Generator(device="cpu").manual_seed(k + m)
     P = (torch.randn(m, D, generator=g, dtype=torch.float64) * 3).to(gpu)
     w = torch.randint(1, 50, (m,), generator=g).to(torch.float64).to(gpu)
