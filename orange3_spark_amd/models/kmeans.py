@@ -121,8 +121,6 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
 # blobs its seeding leaves a 1.9x higher cost after 10 Lloyd iterations (25.0e9 vs
 # 13.3e9, profiles/kmeans_init_phases_r5.json), so the greedy variant is the default
 GREEDY_KMEANSPP = True
-# the k-means++ kernel runs all k steps in one cooperative launch (False: 2 launches per step)
-KPP_COOP = True
 
 
 def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: int = 30,
@@ -174,8 +172,7 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
         picks32 = torch.empty(k, dtype=torch.int32, device=dev)
         N.check(N.kernels().o3s_kmeanspp(PT.data_ptr(), wc.data_ptr(), pc.data_ptr(), m, P.shape[1], k, trials,
                                          Uc.data_ptr(), d2.data_ptr(), cs.data_ptr(), cd.data_ptr(),
-                                         partial.data_ptr(), cand.data_ptr(), picks32.data_ptr(), int(KPP_COOP),
-                                         N.stream_of(PT)),
+                                         partial.data_ptr(), cand.data_ptr(), picks32.data_ptr(), N.stream_of(PT)),
                 "kmeanspp")
         picks = picks32.to(torch.int64)
     else:

@@ -330,15 +330,11 @@ def test_gpu_presplit_dropped_after_fit(gpu, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("k,m,D", [(16, 300, 8), (256, 1500, 64), (1024, 4100, 128)])
-@pytest.mark.parametrize("coop", [True, False])
-def test_gpu_kmeanspp_kernel_matches_torch_steps(gpu, k, m, D, coop, monkeypatch):
-    """The k-means++ kernels (one cooperative launch for all k greedy steps, or two
-    launches per step) pick the same candidates as the step-by-step torch formulation from
+def test_gpu_kmeanspp_kernel_matches_torch_steps(gpu, k, m, D):
+    """The k-means++ kernels (two launches per greedy step) pick the same candidates as the step-by-step torch formulation from
     the same draws (fp32-rounded coordinates, fp64 sums; then the shared Lloyd refinement
     gives the same centres)."""
-    from orange3_spark_amd.models import kmeans as KMM
     from orange3_spark_amd.models.kmeans import _local_kmeanspp
-    monkeypatch.setattr(KMM, "KPP_COOP", coop)
     g = torch.Generator(device="cpu").manual_seed(k + m)
     P = (torch.randn(m, D, generator=g, dtype=torch.float64) * 3).to(gpu)
     w = torch.randint(1, 50, (m,), generator=g).to(torch.float64).to(gpu)
