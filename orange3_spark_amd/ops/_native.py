@@ -94,6 +94,7 @@ _SIGS: dict[str, list] = {
     "o3s_assemble_src_size": [],
     "o3s_assemble_cols": [c_vp, c_i32, c_i32, c_i32, c_i64, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp],
     "o3s_kmeans_update": [c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp],
+    "o3s_gather_probe": [c_vp, c_i32, c_vp, c_i64, c_i32, c_vp, c_vp],
 }
 
 
