@@ -82,11 +82,11 @@ _SIGS: dict[str, list] = {
     "o3s_als_wood_timed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp],
     "o3s_hashing_tf": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32,
                        c_vp, c_vp, c_vp],
-    "o3s_als_dense_wave_dbg": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp,
-                               c_vp],
+    "o3s_als_dense_wave_dbg": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp],
     "o3s_bin_features2": [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp, c_i64, c_vp],
     "o3s_kmeanspp": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
-    "o3s_als_dense_wave": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
+    "o3s_als_dense_wave_timed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp],
+    "o3s_als_dense_wave": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
     "o3s_als_exact_max_small": [],
     "o3s_als_rotate": [c_i32, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
     "o3s_als_rotate_to": [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp],

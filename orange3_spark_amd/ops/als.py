@@ -317,11 +317,42 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
             # longest rows first: the waves take rows round robin, so the long tail of
             # popular items spreads over the whole chip instead of finishing last
             order = torch.argsort(cnt[dense - a], descending=True)
-            rows_sorted = dense[order].contiguous()
-            N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
-                                           b.data_ptr(), F.data_ptr(), N.ptr(Gf), lam.data_ptr(),
-                                           rows_sorted.data_ptr(), nd, out.data_ptr(), N.num_cus(dev), st),
-                    "als_dense_wave")
+            dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, dense[order], out)
+    return out
+
+
+def dense_meta(indptr, rows, lam):
+    """The dense kernel's per-row metadata, int32 [n][8] in list order:
+    {p0 lo, p0 hi, n, u, lam_u bits, 0, 0, 0} (csrc/als_dense.hip DMAs it ahead of use)."""
+    rows = rows.long()
+    p0 = indptr[rows]
+    meta = torch.zeros((rows.numel(), 8), dtype=torch.int32, device=rows.device)
+    meta[:, 0:2] = p0.view(torch.int32).view(-1, 2)
+    meta[:, 2] = (indptr[rows + 1] - p0).to(torch.int32)
+    meta[:, 3] = rows.to(torch.int32)
+    meta[:, 4] = lam[rows].float().view(torch.int32)
+    return meta
+
+
+def dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, rows, out, grid=None):
+    """o3s_als_dense_wave over the listed rows (in list order: the caller sorts them longest
+    first); rows without ratings are solved here (x = 0: the right-hand side is 0), so every
+    row the kernel walks has at least one 16-rating step."""
+    R = F.shape[1]
+    cnt = indptr[rows.long() + 1] - indptr[rows.long()]
+    empty = cnt == 0
+    if bool(empty.any()):
+        out[rows[empty].long()] = 0
+        rows = rows[~empty]
+    n = int(rows.numel())
+    if not n:
+        return out
+    meta = dense_meta(indptr, rows, lam)
+    lib = N.kernels()
+    N.check(lib.o3s_als_dense_wave(int(implicit), R, meta.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                   F.data_ptr(), N.ptr(Gf), n, out.data_ptr(),
+                                   N.num_cus(F.device) if grid is None else grid, N.stream_of(out)),
+            "als_dense_wave")
     return out
 
 

@@ -15,9 +15,10 @@
 //   per-lane source = a factor row, lane-linear image) into a per-wave ring of DEPTH steps
 //   of 16 ratings, with w / b of the step DMA'd beside them; the ring is a continuous
 //   STREAM across rows, so the next row's first steps are in flight while this row
-//   factors.  Rating indices come through the scalar cache (s_load), so no ordinary
-//   vector load is ever consumed while a DMA is outstanding, and the consumer waits with a
-//   counted s_waitcnt vmcnt (the DMAs of later steps stay in flight);
+//   factors.  The rating indices of a step are DMA'd into its slot DEPTH steps ahead (an
+//   index cursor walks the stream in front of the producer), so no ordinary vector load
+//   is ever consumed while a DMA is outstanding and no step waits on a scalar-cache miss;
+//   the consumer waits with a counted s_waitcnt vmcnt (later steps stay in flight);
 // * the system is held as the NL = NT (NT + 1) / 2 upper 32 x 32 tiles in MFMA accumulator
 //   layout (lane l: column l & 31, rows (v & 3) + 8 (v >> 2) + 4 (l >> 5) in register v):
 //   160 registers at rank 128;
@@ -51,9 +52,6 @@ typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-typedef const int32_t __attribute__((address_space(4)))* sptr_i32;
-typedef const int64_t __attribute__((address_space(4)))* sptr_i64;
-typedef const float __attribute__((address_space(4)))* sptr_f32;
 
 // DEEP (explicit: no G in LDS): the 40 KB G would take carry a fourth ring step at ranks
 // 96 / 128 (implicit keeps G in LDS: reading it per row from global memory spilled)
@@ -67,11 +65,13 @@ struct DW {
   static constexpr int RS = R == 96 ? 128 : R;          // LDS row stride (floats)
   static constexpr int RPI = 64 / LPS;                  // rows per DMA instruction
   static constexpr int NI = CH / RPI;                   // row DMAs per step
-  static constexpr int NIS = NI + 1;                    // + the w / b DMA
+  static constexpr int NIS = NI + 2;                    // + the w / b / index and metadata DMAs
   static constexpr int DEPTH = R >= 96 ? (DEEP ? 4 : 3) : (R == 64 ? 5 : 8);
   static constexpr int SLOT = CH * RS;                  // floats per ring slot
   static constexpr int TS = 32 * 33;                    // padded 32 x 32 scratch tile
-  static constexpr int WAVE = DEPTH * SLOT + DEPTH * 32 + TS + R;   // floats per wave
+  static constexpr int MAHEAD = DEPTH;                  // row metadata fetched this far ahead
+  static constexpr int MR = 3 * DEPTH + 1;              // ... into a ring of MR rows
+  static constexpr int WAVE = DEPTH * SLOT + DEPTH * 48 + MR * 8 + TS + R;   // floats per wave
   static constexpr int GL = NL * 1024;                  // implicit G, accumulator order
 };
 
@@ -90,17 +90,20 @@ __device__ __forceinline__ constexpr int tix(int j, int i) { return j * NT - j *
 
 // s_waitcnt vmcnt(n * NIS) for a wave-uniform n in [0, 7]: the DMAs of the n later steps
 // stay in flight (loads retire in order, so this is exactly "this step has landed")
+// (the counter holds 63: a larger count is clamped, i.e. waits for more; the kernels never
+// keep more than DEPTH - 1 steps = at most 63 DMAs in flight)
+__device__ __forceinline__ constexpr int vm_cap(int n) { return n < 63 ? n : 63; }
 template <int NIS>
 __device__ __forceinline__ void wait_steps(int n) {
   switch (n) {
     case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 * NIS) : "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NIS) : "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NIS) : "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NIS) : "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(5 * NIS) : "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * NIS) : "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(7 * NIS) : "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vm_cap(1 * NIS)) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vm_cap(2 * NIS)) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vm_cap(3 * NIS)) : "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vm_cap(4 * NIS)) : "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vm_cap(5 * NIS)) : "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vm_cap(6 * NIS)) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(vm_cap(7 * NIS)) : "memory"); break;
   }
 }
 
@@ -131,15 +134,19 @@ __device__ __forceinline__ bf16x8_t neg8(bf16x8_t v) {
   return __builtin_bit_cast(bf16x8_t, __builtin_bit_cast(u32x4_t, v) ^ 0x80008000u);
 }
 
-template <int R, bool IMPL, bool DBG = false>
+// TIM (diagnostic, o3s_als_dense_wave_timed): per-wave shader-clock totals of the row
+// setup, the Gram loop (of which: inside advance(), i.e. producing + waiting for the DMA
+// ring), the factorisation + forward solve (of which per panel: A the diagonal factor, the
+// y_p / X_p hand-off, B the U_pi products, C the trailing update), and the backward solve +
+// store, written to ((long long*)dbg)[wave][9]
+template <int R, bool IMPL, bool DBG = false, bool TIM = false>
 __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
-    const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
-    const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G,
-    const float* __restrict__ lam, const int32_t* __restrict__ rows, int64_t nrows, float* __restrict__ X,
-    float* __restrict__ dbg) {
+    const int32_t* __restrict__ meta, const int32_t* __restrict__ cols, const float* __restrict__ w,
+    const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G, int64_t nrows,
+    float* __restrict__ X, float* __restrict__ dbg) {
   using D = DW<R, !IMPL>;
   constexpr int NT = D::NT, NL = D::NL, CH = D::CH, DEPTH = D::DEPTH, RS = D::RS, LPS = D::LPS,
-                RPI = D::RPI, NI = D::NI, SLOT = D::SLOT;
+                RPI = D::RPI, NI = D::NI, SLOT = D::SLOT, MR = D::MR, MAHEAD = D::MAHEAD;
   // ONE __shared__ array (a second object beside the DMA ring can make hipcc wait vmcnt(0)
   // before ring reads)
   __shared__ __attribute__((aligned(16))) float lds[4 * D::WAVE + (IMPL ? D::GL : 0)];
@@ -149,8 +156,9 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
   float* const sG = lds;                                  // [NL][4][64][4]
   float* const wl = lds + (IMPL ? D::GL : 0) + wid * D::WAVE;
   float* const ring = wl;                                 // [DEPTH][CH][RS]
-  float* const swb = wl + DEPTH * SLOT;                   // [DEPTH][w 16 | b 16]
-  float* const scr = swb + DEPTH * 32;                    // [32][33] scratch tile
+  float* const swb = wl + DEPTH * SLOT;                   // [DEPTH][w 16 | b 16 | idx 16]
+  float* const smeta = swb + DEPTH * 48;                  // [MR][8] row metadata ring
+  float* const scr = smeta + MR * 8;                      // [32][33] scratch tile
   float* const sr = scr + D::TS;                          // [R] rhs -> y -> x
 
   if constexpr (IMPL) {
@@ -170,61 +178,149 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
 
   const int64_t GW = (int64_t)gridDim.x * 4;
   const int64_t gw = (int64_t)blockIdx.x * 4 + wid;
-  const sptr_i32 scol = (const sptr_i32)cols;
-  const sptr_i64 sptrs = (const sptr_i64)indptr;
-  const sptr_i32 srow = (const sptr_i32)rows;
-  const sptr_f32 slam = (const sptr_f32)lam;
+  // this wave's k-th row is row gw + k GW of the (length-sorted) list
+  auto has_row = [&](int k) { return gw + (int64_t)k * GW < nrows; };
 
-  // ---- producer: the stream of 16-rating steps over this wave's rows ----
-  int64_t p_idx = gw - GW, pj = 0, pe = 0;
+  // ---- row metadata {p0, n, u, lam_u} (host-built, list order) reaches LDS by DMA, MAHEAD
+  // rows ahead of the index cursor (one row per step at most, the same rate the cursor can
+  // move), into a ring of MR slots: every walk below reads it there, none through the
+  // scalar cache (a strided / gathered s_load missed once per row per walk) ----
+  auto meta_dma = [&](int k, int slot) {       // lanes 0..7: row k's 8 dwords -> slot
+    int64_t idx = gw + (int64_t)k * GW;
+    idx = idx < nrows ? idx : nrows - 1;
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    if (ln < 8)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const float*>(meta + idx * 8 + ln), smeta + slot * 8, 4, 0, 0);
+  };
+  struct RowMeta {
+    int64_t p0, p1;
+    int64_t u;
+    float lam;
+  };
+  auto meta_read = [&](int slot) {
+    const u32x4_t m = *reinterpret_cast<const u32x4_t*>(smeta + slot * 8);
+    const float lm = smeta[slot * 8 + 4];
+    RowMeta r;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(m[0]), hi = __builtin_amdgcn_readfirstlane(m[1]);
+    r.p0 = (int64_t)(((uint64_t)hi << 32) | lo);
+    r.p1 = r.p0 + (int32_t)__builtin_amdgcn_readfirstlane(m[2]);
+    r.u = (int32_t)__builtin_amdgcn_readfirstlane(m[3]);
+    r.lam = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, lm)));
+    return r;
+  };
+  auto next_mod = [](int s) { return s + 1 == MR ? 0 : s + 1; };
+
+  // ---- producer: the stream of 16-rating steps over this wave's rows.  The rating indices
+  // of a step come from its ring slot, DMA'd there DEPTH steps earlier by an index cursor
+  // walking the same stream ahead (with the w / b DMA of the step that last used the slot):
+  // reading them through the scalar cache instead stalled every step on a miss ----
+  int xk = -1, xms = MR - 1;                   // index cursor: row, its metadata slot
+  int64_t xj = 0, xe = 0;
+  auto cursor_next = [&]() -> bool {           // the cursor's next step; false at stream end
+    while (xj >= xe) {
+      if (!has_row(xk + 1)) return false;
+      ++xk;
+      xms = next_mod(xms);
+      const RowMeta m = meta_read(xms);
+      xj = m.p0;
+      xe = m.p1;
+    }
+    return true;
+  };
+  auto index_src = [&](int ln) {                // lanes 32..47: the cursor step's indices
+    const int64_t jx = xj + (ln & 15) < xe - 1 ? xj + (ln & 15) : xe - 1;
+    return reinterpret_cast<const float*>(cols + jx);
+  };
+  long long tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  long long tp = TIM ? (long long)clock64() : 0;
+  auto stamp = [&](int ph) {
+    if constexpr (TIM) {
+      const long long now = (long long)clock64();
+      tacc[ph] += now - tp;
+      tp = now;
+    }
+  };
+  int mk = 0, mslot = 0;                       // next row whose metadata is fetched, its slot
+  int pk = -1, pms = MR - 1;                   // producer: row, its metadata slot
+  int64_t pj = 0, pe = 0;
   int issued = 0, pslot = 0;
   auto produce = [&]() {
     while (pj >= pe) {
-      p_idx += GW;
-      if (p_idx >= nrows) return;
-      const int64_t u = srow[p_idx];
-      pj = sptrs[u];
-      pe = sptrs[u + 1];
+      if (!has_row(pk + 1)) return;
+      ++pk;
+      pms = next_mod(pms);
+      const RowMeta m = meta_read(pms);
+      pj = m.p0;
+      pe = m.p1;
     }
     const int64_t last = pe - 1;
-    int32_t c[CH];
-#pragma unroll
-    for (int i = 0; i < CH; ++i)   // readfirstlane: keeps hipcc from turning the per-lane
-      c[i] = __builtin_amdgcn_readfirstlane(scol[pj + i < last ? pj + i : last]);   // select into a vector load
     float* const dst = ring + pslot * SLOT;
+    float* const wb = swb + pslot * 48;
     // per-lane address terms recomputed per call (hoisted, they sat in spill slots whose
     // reloads drained the DMA ring with vmcnt(0))
     int ln = lane;
     asm volatile("" : "+v"(ln));
     const int rr = ln / LPS, lo = ln % LPS;
+    const int32_t* const si = reinterpret_cast<const int32_t*>(wb + 32);
+    int32_t ci[NI];
+#pragma unroll
+    for (int ins = 0; ins < NI; ++ins) ci[ins] = si[ins * RPI + rr];
 #pragma unroll
     for (int ins = 0; ins < NI; ++ins) {
-      int32_t ci = c[ins * RPI];
-#pragma unroll
-      for (int e = 1; e < RPI; ++e) ci = rr == e ? c[ins * RPI + e] : ci;
-      const float* src = F + (int64_t)ci * R + 4 * lo;
+      const float* src = F + (int64_t)ci[ins] * R + 4 * lo;
       if constexpr (R == 96) {
         if (lo < 24) __builtin_amdgcn_global_load_lds(src, dst + ins * RPI * RS, 16, 0, 0);
       } else {
         __builtin_amdgcn_global_load_lds(src, dst + ins * RPI * RS, 16, 0, 0);
       }
     }
-    if (ln < 32) {
+    // w / b of this step beside it, the indices of the step DEPTH ahead behind them
+    const bool ahead = cursor_next();
+    if (ln < 32 || (ahead && ln < 48)) {
       const int64_t jj = pj + (ln & 15) < last ? pj + (ln & 15) : last;
-      __builtin_amdgcn_global_load_lds((ln < 16 ? w : b) + jj, swb + pslot * 32, 4, 0, 0);
+      const float* src = ln < 16 ? w + jj : ln < 32 ? b + jj : index_src(ln);
+      __builtin_amdgcn_global_load_lds(src, wb, 4, 0, 0);
+    }
+    if (ahead) xj += CH;
+    // one metadata row per step (every step issues the same NIS DMAs): the next one once
+    // the cursor is within MAHEAD rows of it, else the last one again (same bytes)
+    if (mk <= xk + MAHEAD) {
+      meta_dma(mk, mslot);
+      ++mk;
+      mslot = next_mod(mslot);
+    } else {
+      meta_dma(mk - 1, mslot == 0 ? MR - 1 : mslot - 1);
     }
     pj += CH;
     ++issued;
     pslot = pslot + 1 == DEPTH ? 0 : pslot + 1;
   };
 
+  {
+    // the metadata of the first MAHEAD + DEPTH + 1 rows and the indices of the first DEPTH
+    // steps, synchronously (the index cursor's first DEPTH steps may cross DEPTH rows)
+    for (; mk <= MAHEAD + DEPTH; ++mk) meta_dma(mk, mk);
+    mslot = mk;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    for (int k = 0; k < DEPTH && cursor_next(); ++k) {
+      if (ln >= 32 && ln < 48) __builtin_amdgcn_global_load_lds(index_src(ln), swb + k * 48, 4, 0, 0);
+      xj += CH;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   for (int i = 0; i < DEPTH - 1; ++i) produce();
   int consumed = 0, cslot = 0;
 
-  for (int64_t idx = gw; idx < nrows; idx += GW) {
-    const int64_t u = srow[idx];
-    const int64_t p0 = sptrs[u], p1 = sptrs[u + 1];
-    const float lu = slam[u];
+  int cms = MR - 1;
+  for (int k = 0; has_row(k); ++k) {
+    const int64_t idx = gw + (int64_t)k * GW;
+    cms = next_mod(cms);
+    const RowMeta rm = meta_read(cms);
+    const int64_t u = rm.u, p0 = rm.p0, p1 = rm.p1;
+    const float lu = rm.lam;
     // the lane's coordinates, laundered per PHASE: lane-dependent constants (identity
     // columns, diagonal masks, LDS addresses) are recomputed where they are used instead of
     // being hoisted across the Gram loop into registers that then spill inside it
@@ -250,6 +346,7 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
     float rh[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) rh[j] = 0.f;
+    stamp(0);
 
     // ---- Gram, software-pipelined in place: after the MFMAs of tile row j of step s
     // (tiles (j, j..NT-1)), fragment block j is dead for step s and is rebuilt for step
@@ -260,13 +357,16 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
     // rank 128).  The ring slot of step s is read out one iteration earlier, so
     // produce() still keeps two steps in flight. ----
     auto advance = [&]() {
+      stamp(1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot being refilled is read out
       produce();
+      stamp(4);
       wait_steps<D::NIS>(issued - 1 - consumed);
+      stamp(9);
     };
     float sw[8], bb[8];
     auto step_scale = [&](int64_t j0) {            // sqrt(w) and b of the step's 8 ratings per lane half
-      const float* wb = swb + cslot * 32;
+      const float* wb = swb + cslot * 48;
       const int nv = (int)(p1 - j0 < CH ? p1 - j0 : CH);
       const float4_ w0 = *reinterpret_cast<const float4_*>(wb + 8 * h);
       const float4_ w1 = *reinterpret_cast<const float4_*>(wb + 8 * h + 4);
@@ -327,6 +427,7 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
       for (int j = 0; j < NT; ++j) mfma_row(j);
     }
 
+    stamp(1);
     // ---- rhs ----
     q = lane & 31;
     h = lane >> 5;
@@ -357,7 +458,9 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
       // column from a float4 LDS broadcast.
       float v[32];
 #pragma unroll
-      for (int k = 0; k < 32; ++k) v[k] = h ? (k == q ? 1.f : 0.f) : scr[q * 33 + k];
+      for (int k = 0; k < 32; ++k) v[k] = scr[q * 33 + k];   // every lane loads (a per-lane
+#pragma unroll                                                // conditional load became 32 branches)
+      for (int k = 0; k < 32; ++k) v[k] = h ? (k == q ? 1.f : 0.f) : v[k];
       float4_* const sC4 = reinterpret_cast<float4_*>(scr);
 #pragma unroll
       for (int c0 = 0; c0 < 32; c0 += 4) {
@@ -381,6 +484,7 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
         }
       }
       lane_sync();                                                   // sC4 reads done
+      stamp(5);
       if (h == 1) {
 #pragma unroll
         for (int k = 0; k < 32; ++k) scr[k * 33 + q] = v[k];        // X_p[k][q]
@@ -404,6 +508,7 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
       // B: U_pi = X_p S_pi; r_i -= U_pi^T y_p.  bf16x3 on v_mfma_f32_32x32x16_bf16 (the
       // Gram's numerics): register v of a tile is k-slot v & 7 of k-block v >> 3 for BOTH
       // operands (lane half h holds k = rowof(v, h)), so the k pairing is consistent
+      stamp(6);
       bf16x8_t xh[2], xl[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
@@ -434,6 +539,7 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
         if (h == 0) sr[32 * i + q] -= part;
       }
       lane_sync();
+      stamp(7);
       // C: S_ji -= U_pj^T U_pi, operands straight from the panel tiles' registers (bf16x3,
       // -U_pj by flipping the bf16 sign bits)
       bf16x8_t uh[NT][2], ul[NT][2];
@@ -455,8 +561,10 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
           }
         }
       }
+      stamp(8);
     }
 
+    stamp(2);
     if (DBG && idx < 64) {                // diagnostic dump: U / X_p tiles and y
 #pragma unroll
       for (int t = 0; t < NL; ++t)
@@ -499,27 +607,31 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
 #pragma unroll
     for (int c = 0; c < R; c += 64)
       if (c + lane < R) X[u * R + c + lane] = sr[c + lane];
+    stamp(3);
   }
   // every DMA this wave issued was waited for by the step that consumed it
+  if constexpr (TIM) {
+    if (lane == 0)
+      for (int ph = 0; ph < 10; ++ph) reinterpret_cast<long long*>(dbg)[gw * 10 + ph] = tacc[ph];
+  }
 }
 
 template <int R>
-int launch(int implicit, const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
-           const float* F, const float* G, const float* lam, const int32_t* rows, int64_t nrows, float* X,
-           int grid, float* dbg, hipStream_t st) {
+int launch(int implicit, const int32_t* meta, const int32_t* cols, const float* w, const float* b, const float* F,
+           const float* G, int64_t nrows, float* X, int grid, float* dbg, hipStream_t st) {
   if (dbg != nullptr) {
     if (implicit)
-      hipLaunchKernelGGL((als_dense_wave_kernel<R, true, true>), dim3(grid), dim3(256), 0, st, indptr, cols, w, b, F,
-                         G, lam, rows, nrows, X, dbg);
+      hipLaunchKernelGGL((als_dense_wave_kernel<R, true, true>), dim3(grid), dim3(256), 0, st, meta, cols, w, b, F, G,
+                         nrows, X, dbg);
     else
-      hipLaunchKernelGGL((als_dense_wave_kernel<R, false, true>), dim3(grid), dim3(256), 0, st, indptr, cols, w, b,
-                         F, G, lam, rows, nrows, X, dbg);
+      hipLaunchKernelGGL((als_dense_wave_kernel<R, false, true>), dim3(grid), dim3(256), 0, st, meta, cols, w, b, F,
+                         G, nrows, X, dbg);
   } else if (implicit) {
-    hipLaunchKernelGGL((als_dense_wave_kernel<R, true>), dim3(grid), dim3(256), 0, st, indptr, cols, w, b, F, G, lam,
-                       rows, nrows, X, nullptr);
+    hipLaunchKernelGGL((als_dense_wave_kernel<R, true>), dim3(grid), dim3(256), 0, st, meta, cols, w, b, F, G, nrows,
+                       X, nullptr);
   } else {
-    hipLaunchKernelGGL((als_dense_wave_kernel<R, false>), dim3(grid), dim3(256), 0, st, indptr, cols, w, b, F, G,
-                       lam, rows, nrows, X, nullptr);
+    hipLaunchKernelGGL((als_dense_wave_kernel<R, false>), dim3(grid), dim3(256), 0, st, meta, cols, w, b, F, G, nrows,
+                       X, nullptr);
   }
   O3S_CHECK_LAUNCH();
   return 0;
@@ -527,33 +639,47 @@ int launch(int implicit, const int64_t* indptr, const int32_t* cols, const float
 
 }  // namespace
 
-// Dense exact solves of the rows listed in ``rows`` (any length; the caller lists them
-// longest first for balance), one wave per row, ``grid`` blocks of 4 waves (persistent:
-// at most 4 blocks' worth of waves per CU are resident, 1 block per CU).  Same contract
-// as o3s_als_dense_mfma: x_u written into X[u]; implicit: G = Y^T Y (fp32 R x R).
-O3S_API int o3s_als_dense_wave_dbg(int implicit, int R, const int64_t* indptr, const int32_t* cols,
-                                   const float* w, const float* b, const float* F, const float* G, const float* lam,
-                                   const int32_t* rows, int64_t nrows, float* X, int grid, float* dbg,
-                                   hipStream_t st) {
+// Dense exact solves of ``nrows`` rows, one wave per row, ``grid`` blocks of 4 waves
+// (persistent: 1 block per CU, wave gw takes list rows gw, gw + 4 grid, ...).  meta: int32
+// [nrows][8] in list order (the caller lists rows longest first for balance):
+// {p0 lo, p0 hi, n >= 1, u, lam_u bits, 0, 0, 0} -- row u's ratings are [p0, p0 + n) of
+// cols / w / b; x_u written into X[u]; implicit: G = Y^T Y (fp32 R x R).  Diagnostic: a
+// non-null dbg [(64 rows x 2 stages x NL tiles x 1024) + 64 x R] receives, for the first
+// 64 listed rows, the accumulator tiles (raw C layout: [v][lane]) after the system is
+// assembled and after the forward factorisation, plus y (grid forced to 1).
+O3S_API int o3s_als_dense_wave_dbg(int implicit, int R, const int32_t* meta, const int32_t* cols, const float* w,
+                                   const float* b, const float* F, const float* G, int64_t nrows, float* X, int grid,
+                                   float* dbg, hipStream_t st) {
   if (nrows < 0 || (implicit && !G) || grid <= 0) return -1;
   if (nrows == 0) return 0;
   const int64_t need = (nrows + 3) / 4;
   if (grid > need) grid = (int)need;
   if (dbg != nullptr) grid = 1;
   switch (R) {
-    case 32: return launch<32>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, dbg, st);
-    case 64: return launch<64>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, dbg, st);
-    case 96: return launch<96>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, dbg, st);
-    case 128: return launch<128>(implicit, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, dbg, st);
+    case 32: return launch<32>(implicit, meta, cols, w, b, F, G, nrows, X, grid, dbg, st);
+    case 64: return launch<64>(implicit, meta, cols, w, b, F, G, nrows, X, grid, dbg, st);
+    case 96: return launch<96>(implicit, meta, cols, w, b, F, G, nrows, X, grid, dbg, st);
+    case 128: return launch<128>(implicit, meta, cols, w, b, F, G, nrows, X, grid, dbg, st);
     default: return -2;
   }
 }
 
-// Diagnostic variant: dbg [(64 rows x 2 stages x NL tiles x 1024) + 64 x R] receives, for
-// the first 64 listed rows, the accumulator tiles (raw C layout: [v][lane]) after the
-// system is assembled and after the forward factorisation, plus y (grid forced to 1).
-O3S_API int o3s_als_dense_wave(int implicit, int R, const int64_t* indptr, const int32_t* cols, const float* w,
-                               const float* b, const float* F, const float* G, const float* lam, const int32_t* rows,
-                               int64_t nrows, float* X, int grid, hipStream_t st) {
-  return o3s_als_dense_wave_dbg(implicit, R, indptr, cols, w, b, F, G, lam, rows, nrows, X, grid, nullptr, st);
+// Diagnostic (tools/als_dense_phases.py): als_dense_wave_kernel<128, implicit> with the TIM
+// phase clocks; tim: int64 [grid * 4][10] (row setup, Gram, factor + forward, backward +
+// store, of the Gram loop produce(), of the factorisation A, hand-off, B, C, and of the
+// Gram loop the DMA waits).
+O3S_API int o3s_als_dense_wave_timed(const int32_t* meta, const int32_t* cols, const float* w, const float* b,
+                                     const float* F, const float* G, int64_t nrows, float* X, int grid, long long* tim,
+                                     hipStream_t st) {
+  if (nrows <= 0 || !G || grid <= 0 || !tim) return -1;
+  hipLaunchKernelGGL((als_dense_wave_kernel<128, true, false, true>), dim3(grid), dim3(256), 0, st, meta, cols, w, b,
+                     F, G, nrows, X, reinterpret_cast<float*>(tim));
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
+O3S_API int o3s_als_dense_wave(int implicit, int R, const int32_t* meta, const int32_t* cols, const float* w,
+                               const float* b, const float* F, const float* G, int64_t nrows, float* X, int grid,
+                               hipStream_t st) {
+  return o3s_als_dense_wave_dbg(implicit, R, meta, cols, w, b, F, G, nrows, X, grid, nullptr, st);
 }

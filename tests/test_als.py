@@ -310,12 +310,8 @@ def test_gpu_dense_kernel_matches_fp64_solve(R, implicit):
     n = indptr.numel() - 1
     dense = torch.arange(0, 40, device=F.device, dtype=torch.int32)
     got = torch.full((n, R), float("nan"), device=F.device)
-    from orange3_spark_amd.ops import _native as N
-    lib = N.kernels()
     Gf = G.float().contiguous() if implicit else None
-    N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(),
-                                   b.data_ptr(), F.data_ptr(), N.ptr(Gf), lam.data_ptr(), dense.data_ptr(), 40,
-                                   got.data_ptr(), 256, N.stream_of(got)), "als_dense_wave")
+    A.dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, dense, got, grid=256)
     ref = torch.empty((n, R), dtype=torch.float64, device=F.device)
     A.exact_solve_torch(indptr, cols, w, b, F, G, lam, ref)
     got, ref = got[:40], ref[:40]
@@ -356,21 +352,51 @@ def test_gpu_dense_wave_streams_many_rows_per_wave(R, implicit, grid):
     indptr, cols, w, b, F, lam = (x.to(dev) for x in (indptr, cols, w, b, F, lam))
     Gf = G.to(dev).contiguous() if implicit else None
     order = torch.argsort(lens, descending=True).to(torch.int32).to(dev)
-    lib = N.kernels()
     got = torch.full((n_rows, R), float("nan"), device=dev)
-    N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
-                                   F.data_ptr(), N.ptr(Gf), lam.data_ptr(), order.data_ptr(), n_rows, got.data_ptr(),
-                                   grid, N.stream_of(got)), "als_dense_wave")
+    A.dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, order, got, grid=grid)
     ref = torch.empty((n_rows, R), dtype=torch.float64, device=dev)
     A.exact_solve_torch(indptr, cols, w, b, F, None if G is None else G.to(dev), lam, ref)
     assert not torch.isnan(got).any()
     err = (got.double() - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-6)
     assert float(err.max()) < 2e-3, float(err.max())
     again = torch.full_like(got, float("nan"))
-    N.check(lib.o3s_als_dense_wave(int(implicit), R, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
-                                   F.data_ptr(), N.ptr(Gf), lam.data_ptr(), order.data_ptr(), n_rows,
-                                   again.data_ptr(), 2, N.stream_of(got)), "als_dense_wave")
+    A.dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, order, again, grid=2)
     assert torch.equal(got, again)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [32, 128])
+@pytest.mark.parametrize("grid", [1, 256])
+def test_gpu_dense_wave_short_rows_metadata_ring(R, grid):
+    """Rows of 1..20 ratings (one or two 16-rating steps each, the fastest the index cursor
+    can move through rows) through the dense kernel: its row metadata ring (DMA'd MAHEAD =
+    DEPTH rows ahead of the cursor, MR = 3 DEPTH + 1 slots) must hold every row until the
+    consumer has read it -- every row == the fp64 solve; rows without ratings give 0."""
+    from orange3_spark_amd.ops import als as A
+    g = torch.Generator().manual_seed(R + grid)
+    n_rows, n_other = 1500, 3000
+    lens = torch.randint(1, 21, (n_rows,), generator=g)
+    lens[::97] = 0
+    indptr = torch.zeros(n_rows + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(lens, 0)
+    nnz = int(indptr[-1])
+    cols = torch.randint(0, n_other, (nnz,), generator=g, dtype=torch.int32)
+    vals = torch.rand(nnz, generator=g) * 3
+    F = torch.randn((n_other, R), generator=g) / R ** 0.5
+    w, b, pos = AE._weights(vals, True, 1.5)
+    lam = torch.full((n_rows,), 0.3)
+    G = (F.double().T @ F.double()).float()
+    dev = "cuda"
+    indptr, cols, w, b, F, lam, G = (x.to(dev) for x in (indptr, cols, w, b, F, lam, G))
+    order = torch.randperm(n_rows, generator=g).to(torch.int32).to(dev)
+    got = torch.full((n_rows, R), float("nan"), device=dev)
+    A.dense_wave(True, indptr, cols, w, b, F, G.contiguous(), lam, order, got, grid=grid)
+    ref = torch.empty((n_rows, R), dtype=torch.float64, device=dev)
+    A.exact_solve_torch(indptr, cols, w, b, F, G, lam, ref)
+    assert not torch.isnan(got).any()
+    assert not got[lens.to(dev) == 0].any()
+    err = (got.double() - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-6)
+    assert float(err.max()) < 2e-3, float(err.max())
 
 
 def test_blockwise_topk_recommendations_match_brute_force():

@@ -19,6 +19,7 @@ def rowof(v, h):
 def main():
     from orange3_spark_amd.models import als as AE
     from orange3_spark_amd.ops import _native as N
+    from orange3_spark_amd.ops import als as AO
     out = {}
     for R in (64, 128):
         for implicit in (False, True):
@@ -43,10 +44,11 @@ def main():
             rows = torch.arange(n_rows, dtype=torch.int32, device=dev)
             X = torch.zeros((n_rows, R), device=dev)
             dbg = torch.full((128 * NL * 1024 + 64 * R,), float("nan"), device=dev)
-            N.check(N.kernels().o3s_als_dense_wave_dbg(int(implicit), R, d_[0].data_ptr(), d_[1].data_ptr(),
+            meta = AO.dense_meta(d_[0], rows, d_[5])
+            N.check(N.kernels().o3s_als_dense_wave_dbg(int(implicit), R, meta.data_ptr(), d_[1].data_ptr(),
                                                        d_[2].data_ptr(), d_[3].data_ptr(), d_[4].data_ptr(),
-                                                       N.ptr(Gd), d_[5].data_ptr(), rows.data_ptr(), n_rows,
-                                                       X.data_ptr(), 1, dbg.data_ptr(), N.stream_of(X)), "dbg")
+                                                       N.ptr(Gd), n_rows, X.data_ptr(), 1, dbg.data_ptr(),
+                                                       N.stream_of(X)), "dbg")
             torch.cuda.synchronize()
             D = dbg.cpu().numpy().astype(np.float64)
             res = []
