@@ -28,9 +28,11 @@
 //          8 k-slots = 8 ratings);
 //   per 32-wide panel p (A = U^T U, U_pp = L_pp^T):
 //     A  the diagonal tile is factored by this wave (lane i holds row i, column c's
-//        multipliers by v_readlane inside 4-column blocks, a float4 LDS broadcast for the
-//        deferred rank-4 update); lanes 32-63 run the same recurrence on the identity,
-//        giving X_p = L_pp^-1, and y_p = X_p r_p;
+//        multipliers by v_readlane inside 4-column blocks, the deferred rank-4 update of
+//        the later columns two at a time on v_pk_fma_f32 from a transposed LDS block);
+//        lanes 32-63 run the same recurrence on the identity, giving X_p = L_pp^-1, and
+//        y_p = X_p r_p (solving along the pivots instead, one more v_readlane + FMA per
+//        column on the serial chain, cost more than this pass over X_p);
 //     B  U_pi = X_p S_pi as bf16x3 on v_mfma_f32_32x32x16_bf16 (6 instead of 16
 //        v_mfma_f32_32x32x2_f32: a quarter of the matrix-pipe cycles), B operand = the
 //        tile's own registers split hi / lo; r_i -= U_pi^T y_p (a sum over the tile's
@@ -454,36 +456,49 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
       lane_sync();
       // A: lanes 0-31 row q of the tile -> row q of L; lanes 32-63 column q of the
       // identity -> column q of X_p = L_pp^-1 (the same right-looking FMA with the lane's
-      // own multiplier).  4-column blocks: v_readlane inside, one rank-4 update per later
-      // column from a float4 LDS broadcast.
-      float v[32];
+      // own multiplier).  4-column blocks: v_readlane inside, then one rank-4 update of
+      // the later columns.
+      f32x2_t v2[16];                      // v[k] = v2[k / 2][k % 2]: pairs for v_pk_fma_f32
 #pragma unroll
-      for (int k = 0; k < 32; ++k) v[k] = scr[q * 33 + k];   // every lane loads (a per-lane
-#pragma unroll                                                // conditional load became 32 branches)
-      for (int k = 0; k < 32; ++k) v[k] = h ? (k == q ? 1.f : 0.f) : v[k];
-      float4_* const sC4 = reinterpret_cast<float4_*>(scr);
+      for (int k = 0; k < 32; ++k) v2[k >> 1][k & 1] = scr[q * 33 + k];   // every lane loads (a
+#pragma unroll                                                          // per-lane conditional load
+      for (int k = 0; k < 32; ++k)                                      // became 32 branches)
+        v2[k >> 1][k & 1] = h ? (k == q ? 1.f : 0.f) : v2[k >> 1][k & 1];
+      float* const sT = scr;                 // [4][64]: the block's 4 multipliers of every lane
 #pragma unroll
       for (int c0 = 0; c0 < 32; c0 += 4) {
 #pragma unroll
         for (int c = c0; c < c0 + 4; ++c) {
-          const float piv = fmaxf(rl(v[c], c), 1e-30f);
-          const float t = v[c] * __builtin_amdgcn_rsqf(piv);
-          v[c] = t;
+          const float piv = __builtin_amdgcn_fmed3f(rl(v2[c >> 1][c & 1], c), 1e-30f, 3.0e38f);
+          const float t = v2[c >> 1][c & 1] * __builtin_amdgcn_rsqf(piv);
+          v2[c >> 1][c & 1] = t;
 #pragma unroll
-          for (int j = c + 1; j < c0 + 4; ++j) v[j] = fmaf(-t, rl(t, j), v[j]);
+          for (int j = c + 1; j < c0 + 4; ++j) v2[j >> 1][j & 1] = fmaf(-t, rl(t, j), v2[j >> 1][j & 1]);
         }
         if (c0 + 4 < 32) {
-          sC4[lane] = float4_{v[c0], v[c0 + 1], v[c0 + 2], v[c0 + 3]};
+          // rank-4 update of the later columns, two per v_pk_fma_f32: L[j..j+3][c] of rows
+          // j = 4g.. read as one float4 from the transposed block
+#pragma unroll
+          for (int k = 0; k < 4; ++k) sT[k * 64 + lane] = v2[(c0 + k) >> 1][k & 1];
           lane_sync();
 #pragma unroll
-          for (int j = c0 + 4; j < 32; ++j) {
-            const float4_ l4 = sC4[j];
-            v[j] = fmaf(-v[c0 + 3], l4.w, fmaf(-v[c0 + 2], l4.z, fmaf(-v[c0 + 1], l4.y, fmaf(-v[c0], l4.x, v[j]))));
-            if ((j & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+          for (int g = c0 / 4 + 1; g < 8; ++g) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float4_ l = *reinterpret_cast<const float4_*>(sT + k * 64 + 4 * g);
+              const float m = -v2[(c0 + k) >> 1][k & 1];
+              const f32x2_t mm = {m, m};
+              v2[2 * g] = __builtin_elementwise_fma(mm, f32x2_t{l.x, l.y}, v2[2 * g]);
+              v2[2 * g + 1] = __builtin_elementwise_fma(mm, f32x2_t{l.z, l.w}, v2[2 * g + 1]);
+            }
+            if (g & 1) __builtin_amdgcn_sched_barrier(0);
           }
+          lane_sync();                                               // sT reads done
         }
       }
-      lane_sync();                                                   // sC4 reads done
+      float v[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) v[k] = v2[k >> 1][k & 1];
       stamp(5);
       if (h == 1) {
 #pragma unroll
