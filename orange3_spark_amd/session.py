@@ -93,6 +93,14 @@ class Session:
         if str(self.conf.get("o3s.trace", "false")).lower() in ("1", "true", "yes"):
             from .runtime.tracing import TRACER
             TRACER.enable(sync=str(self.conf.get("o3s.trace.sync", "false")).lower() in ("1", "true"))
+        self.warmup_seconds: dict = {}
+
+    def _warmup(self) -> None:
+        """Tiny fits of each estimator family once per process (``runtime/warmup.py``;
+        conf ``o3s.session.warmup``), so the user's first fit does not pay the one-time
+        kernel-loading costs."""
+        from .runtime.warmup import warmup
+        self.warmup_seconds = warmup(self)
 
     # ------------------------------------------------------------------ lifecycle
     def _pick_device(self) -> torch.device:
@@ -111,6 +119,7 @@ class Session:
         with cls._lock:
             if cls._active is None or cls._active._stopped:
                 cls._active = Session(conf)
+                cls._active._warmup()
             elif conf is not None:
                 for k, v in conf.getAll():
                     cls._active.conf.set(k, v)

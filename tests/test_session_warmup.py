@@ -1,0 +1,54 @@
+"""Session warm-up (runtime/warmup.py): tiny fits of each estimator family at session
+start, once per process, so the first user fit does not pay one-time kernel-loading costs
+(profiles/gbt_cold_fit_r5.json)."""
+import pytest
+import torch
+
+from orange3_spark_amd import Session, SessionConf
+from orange3_spark_amd.runtime import warmup as W
+
+
+@pytest.fixture
+def fresh(monkeypatch):
+    monkeypatch.setattr(W, "_DONE", set())
+    a = Session.active()
+    if a is not None:
+        a.stop()
+    yield
+    a = Session.active()
+    if a is not None:
+        a.stop()
+
+
+def test_auto_is_off_on_cpu(fresh):
+    s = Session.getOrCreate(SessionConf().set("o3s.device", "cpu"))
+    assert s.warmup_seconds == {}
+    assert W._DONE == set()
+
+
+def test_listed_families_run_once_per_process(fresh):
+    s = Session.getOrCreate(SessionConf().set("o3s.device", "cpu").set("o3s.session.warmup", "glm,kmeans"))
+    assert set(s.warmup_seconds) == {"glm", "kmeans"}
+    assert all(v >= 0 for v in s.warmup_seconds.values())
+    s.stop()
+    s2 = Session.getOrCreate(SessionConf().set("o3s.device", "cpu").set("o3s.session.warmup", "glm,kmeans,trees"))
+    assert set(s2.warmup_seconds) == {"trees"}          # glm / kmeans already warm in this process
+
+
+def test_unknown_family_is_an_error(fresh):
+    with pytest.raises(ValueError, match="unknown families"):
+        Session.getOrCreate(SessionConf().set("o3s.device", "cpu").set("o3s.session.warmup", "glm,nope"))
+
+
+def test_false_disables(fresh):
+    s = Session.getOrCreate(SessionConf().set("o3s.device", "cpu").set("o3s.session.warmup", "false"))
+    assert s.warmup_seconds == {}
+
+
+@pytest.mark.gpu
+def test_gpu_auto_warms_every_family(fresh):
+    s = Session.getOrCreate(SessionConf())
+    assert s.device.type == "cuda"
+    assert set(s.warmup_seconds) == set(W.FAMILIES)
+    assert sum(s.warmup_seconds.values()) < 30
+    torch.cuda.synchronize()
