@@ -469,11 +469,17 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
       for (int c0 = 0; c0 < 32; c0 += 4) {
 #pragma unroll
         for (int c = c0; c < c0 + 4; ++c) {
-          const float piv = __builtin_amdgcn_fmed3f(rl(v2[c >> 1][c & 1], c), 1e-30f, 3.0e38f);
-          const float t = v2[c >> 1][c & 1] * __builtin_amdgcn_rsqf(piv);
+          // lane c's entries c..c0+3 of the Schur complement, read together: by symmetry
+          // (bitwise: every lane runs the same FMAs on its row) a_j rs = L_jc, so the
+          // multipliers need no second v_readlane after the pivot's rsqrt
+          float a[4];
+#pragma unroll
+          for (int j = c; j < c0 + 4; ++j) a[j - c0] = rl(v2[j >> 1][j & 1], c);
+          const float rs = __builtin_amdgcn_rsqf(__builtin_amdgcn_fmed3f(a[c - c0], 1e-30f, 3.0e38f));
+          const float t = v2[c >> 1][c & 1] * rs;
           v2[c >> 1][c & 1] = t;
 #pragma unroll
-          for (int j = c + 1; j < c0 + 4; ++j) v2[j >> 1][j & 1] = fmaf(-t, rl(t, j), v2[j >> 1][j & 1]);
+          for (int j = c + 1; j < c0 + 4; ++j) v2[j >> 1][j & 1] = fmaf(-t, a[j - c0] * rs, v2[j >> 1][j & 1]);
         }
         if (c0 + 4 < 32) {
           // rank-4 update of the later columns, two per v_pk_fma_f32: L[j..j+3][c] of rows
