@@ -497,7 +497,6 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
               v2[2 * g] = __builtin_elementwise_fma(mm, f32x2_t{l.x, l.y}, v2[2 * g]);
               v2[2 * g + 1] = __builtin_elementwise_fma(mm, f32x2_t{l.z, l.w}, v2[2 * g + 1]);
             }
-            if (g & 1) __builtin_amdgcn_sched_barrier(0);
           }
           lane_sync();                                               // sT reads done
         }
