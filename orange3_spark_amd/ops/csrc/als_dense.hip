@@ -510,11 +510,14 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
         for (int k = 0; k < 32; ++k) scr[k * 33 + q] = v[k];        // X_p[k][q]
       }
       lane_sync();
-      if (h == 0) {
-        float yq = 0.f;
+      {
+        // both lane halves run it (no exec split; the upper half's sums are dropped), four
+        // partial sums so the FMA chain is 8 deep instead of 32
+        float y4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 32; ++j) yq = fmaf(scr[q * 33 + j], sr[32 * p + j], yq);
-        sr[32 * p + q] = yq;                                        // y_p = X_p r_p
+        for (int j = 0; j < 32; ++j) y4[j & 3] = fmaf(scr[q * 33 + j], sr[32 * p + j], y4[j & 3]);
+        lane_sync();
+        if (h == 0) sr[32 * p + q] = (y4[0] + y4[1]) + (y4[2] + y4[3]);   // y_p = X_p r_p
       }
       lane_sync();
       float xa[16], yv[16];
@@ -610,16 +613,17 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
 #pragma unroll
         for (int vv = 0; vv < 16; ++vv) scr[rowof(vv, h) * 33 + q] = prod[vv];
         lane_sync();
-        float s = 0.f;
+        float s4[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < 32; ++k) s += scr[q * 33 + k];
-        if (h == 0) sr[32 * p + q] -= s;
+        for (int k = 0; k < 32; ++k) s4[k & 3] += scr[q * 33 + k];
+        if (h == 0) sr[32 * p + q] -= (s4[0] + s4[1]) + (s4[2] + s4[3]);
       }
       lane_sync();
       const f32x16_t& xp = acc[tix<NT>(p, p)];
-      float t = 0.f;
+      float t2[2] = {0.f, 0.f};
 #pragma unroll
-      for (int vv = 0; vv < 16; ++vv) t = fmaf(xp[vv], sr[32 * p + rowof(vv, h)], t);
+      for (int vv = 0; vv < 16; ++vv) t2[vv & 1] = fmaf(xp[vv], sr[32 * p + rowof(vv, h)], t2[vv & 1]);
+      float t = t2[0] + t2[1];
       t += __shfl_xor(t, 32, 64);
       if (h == 0) sr[32 * p + q] = t;
       lane_sync();
