@@ -116,14 +116,18 @@ class Session:
 
     @classmethod
     def getOrCreate(cls, conf: SessionConf | None = None) -> "Session":
+        created = False
         with cls._lock:
             if cls._active is None or cls._active._stopped:
                 cls._active = Session(conf)
-                cls._active._warmup()
+                created = True
             elif conf is not None:
                 for k, v in conf.getAll():
                     cls._active.conf.set(k, v)
-            return cls._active
+            s = cls._active
+        if created:            # outside the lock: a warm-up fit may look the session up itself
+            s._warmup()
+        return s
 
     @classmethod
     def active(cls) -> "Session | None":
