@@ -79,7 +79,7 @@ _SIGS: dict[str, list] = {
     "o3s_confusion": [c_vp, c_i32, c_vp, c_i32, c_vp, c_i32, c_i64, c_i32, c_vp, c_vp, c_vp],
     "o3s_score_hist": [c_vp, c_i32, c_i64, c_vp, c_i32, c_vp, c_i32, c_i64, c_f64, c_f64, c_i32, c_vp, c_vp],
     "o3s_als_wood_kn": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp],
-    "o3s_als_wood_timed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp],
+    "o3s_als_wood_timed": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp],
     "o3s_hashing_tf": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp, c_vp, c_vp, c_i32,
                        c_vp, c_vp, c_vp],
     "o3s_als_dense_wave_dbg": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp],

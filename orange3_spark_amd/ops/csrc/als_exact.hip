@@ -455,13 +455,24 @@ __global__ __launch_bounds__(256) void als_rotate_kernel(const float* __restrict
 // rotated into the eigenbasis of G (F Q, implicit) or F itself (explicit, eig = 0);
 // eig: the eigenvalues of G (zeros when explicit).  X row u receives y_u = D P_u^T z
 // (implicit: the caller applies x = Q y) or x_u (explicit).
-// Diagnostic: als_wood_kernel<128> with per-row phase cycles in timing [nsmall][5].
-O3S_API int o3s_als_wood_timed(const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
+// Diagnostic: als_wood_kernel<128, kn> (kn = 16 / 24 / 32, as o3s_als_wood_kn) with
+// per-row phase cycles in timing [nsmall][5].
+O3S_API int o3s_als_wood_timed(int kn, const int64_t* indptr, const int32_t* cols, const float* w, const float* b,
                                const float* P, const float* eig, const float* lam, const int32_t* small,
                                int64_t nsmall, float* X, int64_t* timing, hipStream_t st) {
   if (nsmall <= 0 || !eig || !P || !timing) return -1;
-  hipLaunchKernelGGL((als_wood_kernel<128, kNW, true>), dim3((unsigned)((nsmall + kWW - 1) / kWW)), dim3(kWW * 64), 0, st,
-                     indptr, cols, w, b, P, eig, lam, small, nsmall, X, timing);
+  const dim3 grid((unsigned)((nsmall + kWW - 1) / kWW)), block(kWW * 64);
+  if (kn == 16)
+    hipLaunchKernelGGL((als_wood_kernel<128, 16, true>), grid, block, 0, st, indptr, cols, w, b, P, eig, lam, small,
+                       nsmall, X, timing);
+  else if (kn == 24)
+    hipLaunchKernelGGL((als_wood_kernel<128, 24, true>), grid, block, 0, st, indptr, cols, w, b, P, eig, lam, small,
+                       nsmall, X, timing);
+  else if (kn == 32)
+    hipLaunchKernelGGL((als_wood_kernel<128, kNW, true>), grid, block, 0, st, indptr, cols, w, b, P, eig, lam, small,
+                       nsmall, X, timing);
+  else
+    return -2;
   O3S_CHECK_LAUNCH();
   return 0;
 }

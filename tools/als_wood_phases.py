@@ -18,13 +18,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--users", type=int, default=2_000_000)
     ap.add_argument("--other", type=int, default=5_000_000)
+    ap.add_argument("--kn", type=int, default=32, choices=(16, 24, 32),
+                    help="launch width; rows get kn/2+1..kn ratings (1..16 for kn 16)")
     a = ap.parse_args()
     from orange3_spark_amd.models import als as AE
     from orange3_spark_amd.ops import _native as N
     dev = torch.device("cuda", 0)
     R = 128
     g = torch.Generator(device="cpu").manual_seed(9)
-    lens = torch.randint(1, 33, (a.users,), generator=g)
+    lo_len = 1 if a.kn == 16 else (17 if a.kn == 24 else 25)
+    lens = torch.randint(lo_len, a.kn + 1, (a.users,), generator=g)
     indptr = torch.zeros(a.users + 1, dtype=torch.int64)
     indptr[1:] = torch.cumsum(lens, 0)
     nnz = int(indptr[-1])
@@ -43,12 +46,12 @@ def main():
     st = N.stream_of(out)
 
     def prod():
-        N.check(lib.o3s_als_wood_kn(R, 32, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+        N.check(lib.o3s_als_wood_kn(R, a.kn, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                                     P.data_ptr(), eig.data_ptr(), lam.data_ptr(), small.data_ptr(), a.users,
                                     out.data_ptr(), st), "wood")
 
     def timed():
-        N.check(lib.o3s_als_wood_timed(indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), P.data_ptr(),
+        N.check(lib.o3s_als_wood_timed(a.kn, indptr.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(), P.data_ptr(),
                                        eig.data_ptr(), lam.data_ptr(), small.data_ptr(), a.users, out.data_ptr(),
                                        tim.data_ptr(), st), "wood_timed")
     res = {}
@@ -66,6 +69,7 @@ def main():
     tot = sum(m)
     res["cycles_per_row_mean"] = dict(zip(names, [round(x) for x in m]))
     res["share_of_row"] = {k: round(v / tot, 3) for k, v in zip(names, m)}
+    res["kn"] = a.kn
     res["users"], res["other_rows"], res["ratings"], res["mean_len"] = a.users, a.other, nnz, nnz / a.users
     res["ns_per_row_production"] = res["production_ms"] * 1e6 / a.users
     print(json.dumps(res))
