@@ -490,3 +490,21 @@ def test_id_maps_int32_and_int64(dt):
         assert uid.tolist() == sorted(set(ids.tolist()))
         pos = AE.dense_index(uid, ids)
         assert uid[pos.long()].tolist() == ids.tolist()
+
+
+def test_dense_meta_layout_cpu():
+    """ops/als.py dense_meta: the dense kernel's per-row metadata, int32 [n][8] in list
+    order = {p0 lo, p0 hi, n, u, lam_u bits, 0, 0, 0} (csrc/als_dense.hip DMAs it into an
+    LDS ring ahead of use), including a 64-bit p0 beyond 2^32."""
+    from orange3_spark_amd.ops import als as A
+    indptr = torch.tensor([0, 5, 5, 12, (1 << 33) + 7, (1 << 33) + 40], dtype=torch.int64)
+    lam = torch.tensor([0.5, 0.0, 2.25, 1e-3, 7.0])
+    rows = torch.tensor([4, 0, 2], dtype=torch.int32)
+    m = A.dense_meta(indptr, rows, lam)
+    assert m.dtype == torch.int32 and m.shape == (3, 8)
+    p0 = (m[:, 1].long() << 32) | (m[:, 0].long() & 0xFFFFFFFF)
+    assert p0.tolist() == [(1 << 33) + 7, 0, 5]
+    assert m[:, 2].tolist() == [33, 5, 7]
+    assert m[:, 3].tolist() == [4, 0, 2]
+    assert m[:, 4].view(torch.float32).tolist() == [7.0, 0.5, 2.25]
+    assert not m[:, 5:].any()
