@@ -65,15 +65,22 @@ _FIT = {"trees": _fit_trees, "glm": _fit_glm, "kmeans": _fit_kmeans, "als": _fit
 def warmup(session) -> dict:
     """Run the configured families' tiny fits (once per process); returns seconds per
     family run now."""
+    from .tracing import TRACER
     out = {}
-    for fam in _families(session):
-        if fam in _DONE:
-            continue
-        t = time.perf_counter()
-        _FIT[fam](session)
-        if session.device.type == "cuda":
-            import torch
-            torch.cuda.synchronize(session.device)
-        _DONE.add(fam)
-        out[fam] = round(time.perf_counter() - t, 4)
+    fams = [f for f in _families(session) if f not in _DONE]
+    if not fams:
+        return out
+    was = TRACER.enabled                 # the warm-up fits stay out of the user's trace
+    TRACER.enabled = False
+    try:
+        for fam in fams:
+            t = time.perf_counter()
+            _FIT[fam](session)
+            if session.device.type == "cuda":
+                import torch
+                torch.cuda.synchronize(session.device)
+            _DONE.add(fam)
+            out[fam] = round(time.perf_counter() - t, 4)
+    finally:
+        TRACER.enabled = was
     return out

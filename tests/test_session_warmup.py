@@ -52,3 +52,17 @@ def test_gpu_auto_warms_every_family(fresh):
     assert set(s.warmup_seconds) == set(W.FAMILIES)
     assert sum(s.warmup_seconds.values()) < 30
     torch.cuda.synchronize()
+
+
+def test_warmup_fits_stay_out_of_the_trace(fresh):
+    from orange3_spark_amd.runtime.tracing import TRACER
+    TRACER.reset()
+    s = Session.getOrCreate(SessionConf().set("o3s.device", "cpu").set("o3s.session.warmup", "kmeans")
+                            .set("o3s.trace", "true"))
+    try:
+        assert set(s.warmup_seconds) == {"kmeans"}
+        assert TRACER.enabled
+        assert not any(k.startswith("kmeans") for k in TRACER.summary())
+    finally:
+        TRACER.enable(False)
+        TRACER.reset()
