@@ -17,6 +17,7 @@ family; each family is warmed at most once per process."""
 from __future__ import annotations
 
 import time
+import warnings
 
 FAMILIES = ("trees", "glm", "kmeans", "als")
 _DONE: set = set()
@@ -64,7 +65,7 @@ _FIT = {"trees": _fit_trees, "glm": _fit_glm, "kmeans": _fit_kmeans, "als": _fit
 
 def warmup(session) -> dict:
     """Run the configured families' tiny fits (once per process); returns seconds per
-    family run now."""
+    family run now (None for a family whose fit raised: warned, not fatal)."""
     from .tracing import TRACER
     out = {}
     fams = [f for f in _families(session) if f not in _DONE]
@@ -75,10 +76,16 @@ def warmup(session) -> dict:
     try:
         for fam in fams:
             t = time.perf_counter()
-            _FIT[fam](session)
-            if session.device.type == "cuda":
-                import torch
-                torch.cuda.synchronize(session.device)
+            try:
+                _FIT[fam](session)
+                if session.device.type == "cuda":
+                    import torch
+                    torch.cuda.synchronize(session.device)
+            except Exception as e:        # a warm-up failure must not stop the session
+                warnings.warn(f"o3s.session.warmup: the {fam} warm-up fit failed ({type(e).__name__}: {e}); "
+                              "its first real fit pays the one-time costs instead", RuntimeWarning)
+                out[fam] = None
+                continue
             _DONE.add(fam)
             out[fam] = round(time.perf_counter() - t, 4)
     finally:

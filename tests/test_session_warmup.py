@@ -66,3 +66,13 @@ def test_warmup_fits_stay_out_of_the_trace(fresh):
     finally:
         TRACER.enable(False)
         TRACER.reset()
+
+
+def test_a_failing_warmup_fit_warns_and_the_session_still_starts(fresh, monkeypatch):
+    def boom(s):
+        raise RuntimeError("no kernel")
+    monkeypatch.setitem(W._FIT, "glm", boom)
+    with pytest.warns(RuntimeWarning, match="glm warm-up fit failed"):
+        s = Session.getOrCreate(SessionConf().set("o3s.device", "cpu").set("o3s.session.warmup", "glm"))
+    assert s.warmup_seconds == {"glm": None}
+    assert "glm" not in W._DONE
