@@ -30,6 +30,7 @@ is a no-op, with Orange present it adds ``<Class>View`` next to the headless cla
 """
 from __future__ import annotations
 
+import copy
 import html
 import re
 import threading
@@ -145,7 +146,10 @@ def qt_view(core_cls, orange=None):
 
     core_settings = _settings_of(core_cls)
     for k, st in core_settings.items():
-        ns[k] = S.Setting(st.default)
+        # a copy: the Qt class's setting must not share the headless class's mutable
+        # default (a view instance that edits it in place would change every later
+        # headless widget's default)
+        ns[k] = S.Setting(copy.deepcopy(st.default))
     has_table = callable(getattr(core_cls, "table", None))      # Evaluation's Metric|Value table
     action = next((a for a in _ACTIONS if callable(getattr(core_cls, a, None))), None)
 

@@ -615,3 +615,17 @@ def test_script_on_worker_captures_only_its_own_prints(orange_mt, session, capsy
     assert V.Outputs.out_object.sent[-1] == 5 and other.is_set()
     assert "from the script" in sc["console"].text and "bystander line" not in sc["console"].text
     assert "bystander line" in capsys.readouterr().out
+
+
+def test_view_settings_do_not_share_the_headless_default(orange):
+    """A Qt view's setting default is a copy of the headless widget's: editing a view
+    instance's saved parameters in place must not change later headless widgets (it made
+    the Context widget's editor show a stale saved seed in another test)."""
+    from orangecontrib.spark_amd.widgets.data import owcontext
+    from orangecontrib.spark_amd.widgets.views import qt_view
+    core = owcontext.OWSessionContext.saved_gui_params
+    V = qt_view(owcontext.OWSessionContext, orange)
+    assert V.saved_gui_params.default == core.default
+    assert V.saved_gui_params.default is not core.default
+    V.saved_gui_params.default["o3s.seed"] = "42"
+    assert "o3s.seed" not in core.default
