@@ -19,7 +19,12 @@ ap.add_argument("--k", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--repeat", type=int, default=1, help="fits in this process (the first is cold)")
 ap.add_argument("--data", default="blobs", choices=["blobs", "uniform"])
+ap.add_argument("--pair-from", type=float, default=None,
+                help="ops.kmeans.PAIR_FROM: flagged fraction above which the pair screen is tried")
 a = ap.parse_args()
+if a.pair_from is not None:
+    from orange3_spark_amd.ops import kmeans as _K
+    _K.PAIR_FROM = a.pair_from
 SYNC = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
 s = Session.getOrCreate()
 if a.data == "blobs":
@@ -45,4 +50,5 @@ for rep in range(a.repeat):
     init = sum(v for k, v in ph.items() if k in ("kmeans.init.round", "kmeans.init.weights", "kmeans.init.local"))
     print(json.dumps({"metric": "KMeans.fit seconds (k-means|| init + Lloyd)", "value": dt, "fit": rep,
                       "cold": rep == 0, "data": a.data, "rows": a.rows, "d": a.d, "k": a.k, "iters": m.summary.numIter,
-                      "cost": m.summary.trainingCost, "init_s": round(init, 4), "phases_s": ph}), flush=True)
+                      "cost": m.summary.trainingCost, "init_s": round(init, 4), "pair_from": a.pair_from,
+                      "phases_s": ph}), flush=True)
