@@ -83,6 +83,33 @@ def _hbm_only_rate(df, comm, on_gpu, passes=3):
     return comm.sum_scalar(int(X.shape[0])) * passes / el
 
 
+def _allreduce_us(comm, n, on_gpu, reps=50):
+    """Median wall time (us, max over ranks) of one all-reduce of the step's gradient
+    vector (n fp32: coefficients + intercept + loss + count), synchronised per call."""
+    import statistics
+    buf = torch.zeros(n, dtype=torch.float32, device=comm.device)
+    for _ in range(5):
+        comm.all_reduce(buf)
+    ts = []
+    for _ in range(reps):
+        if on_gpu:
+            torch.cuda.synchronize()
+        t = time.perf_counter()
+        comm.all_reduce(buf)
+        if on_gpu:
+            torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t)
+    return comm.max_scalar(statistics.median(ts)) * 1e6
+
+
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+    except Exception:  # noqa: BLE001
+        return None
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
@@ -93,6 +120,9 @@ def main(argv=None):
     ap.add_argument("--resident-fraction", type=float, default=None,
                     help="share of free HBM the feature cache may use (default: session conf, 0.85)")
     ap.add_argument("--no-hbm-only", action="store_true", help="skip the resident-rows-only rate")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow N > 1 GPU ranks on a non-RCCL backend (O3S_DIST_BACKEND=gloo, ranks sharing a GPU); "
+                         "the JSON is then marked rehearsal and is not a headline")
     a = ap.parse_args(argv)
 
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -113,6 +143,12 @@ def main(argv=None):
     comm = s.comm
     on_gpu = s.device.type == "cuda"
     rows = a.rows if on_gpu else min(a.rows, 200_000)
+    rehearsal = comm.world_size > 1 and on_gpu and comm.backend != "nccl"
+    if rehearsal and not a.rehearsal:
+        # a multi-GPU headline must have run its gradient all-reduce on RCCL over xGMI
+        print(f"bench.py: refusing to report n_gpus={comm.world_size} over backend {comm.backend!r} "
+              "(RCCL expected; pass --rehearsal for a gloo rehearsal run)", file=sys.stderr)
+        return 3
 
     t0 = time.time()
     df = s.synthetic.classification(rows, a.features, seed=2024, resident_fraction=a.resident_fraction)
@@ -127,12 +163,16 @@ def main(argv=None):
         torch.cuda.synchronize()
     data_s = time.time() - t0
 
+    from orange3_spark_amd.parallel.comm import COMM_STATS
+    ar0 = tuple(COMM_STATS.get("all_reduce", (0, 0)))
     t = time.perf_counter()
     model = LogisticRegression(maxIter=a.steps, **kw).fit(df)
     if on_gpu:
         torch.cuda.synchronize()
     comm.barrier()
     elapsed = comm.max_scalar(time.perf_counter() - t)
+    ar1 = tuple(COMM_STATS.get("all_reduce", (0, 0)))
+    ar_us = _allreduce_us(comm, a.features + 3, on_gpu) if comm.world_size > 1 else None
 
     hist = model.summary.objectiveHistory
     setup = comm.max_scalar(float(getattr(model, "_fit_setup_seconds", 0.0)))
@@ -176,6 +216,17 @@ def main(argv=None):
         "data_gen_and_warmup_s": data_s,
         "first_loss": hist[0] if hist else None,
         "final_loss": hist[-1] if hist else None,
+        # the collective layer this number was measured on (MULTICHIP self-verification):
+        # backend "nccl" is RCCL on ROCm; "local" is one rank with no collective at all
+        "backend": comm.backend,
+        "collective_world": comm.world_size,
+        "rccl_version": _rccl_version() if comm.backend == "nccl" else None,
+        "rehearsal": rehearsal,
+        # all-reduces issued inside the timed fit (this rank) and their payload, plus the
+        # latency of one gradient-sized all-reduce measured after the timed region
+        "allreduce_calls_timed": ar1[0] - ar0[0],
+        "allreduce_bytes_timed": ar1[1] - ar0[1],
+        "allreduce_us_per_call": ar_us,
     }
     if comm.rank == 0:
         print(json.dumps(out), flush=True)

@@ -436,6 +436,7 @@ class DecisionTreeClassifier(Estimator, _DecisionTreeParams, HasProbabilityCol, 
                              MLWritable, MLReadable):
     """Decision tree learning algorithm for classification (gini/entropy), level-wise
     with LDS histogram kernels and one histogram all-reduce per level."""
+    _warm_family = "trees"          # runtime/warmup.py lazy warm-up
 
     @keyword_only
     def __init__(self, *, featuresCol="features", labelCol="label", predictionCol="prediction",
@@ -482,6 +483,7 @@ class RandomForestClassifier(Estimator, _RFParams, HasProbabilityCol, HasRawPred
                              MLWritable, MLReadable):
     """Random forest learning algorithm for classification (bootstrap via Poisson row
     weights keyed on (seed, global row), per-node feature subsets)."""
+    _warm_family = "trees"          # runtime/warmup.py lazy warm-up
 
     @keyword_only
     def __init__(self, *, featuresCol="features", labelCol="label", predictionCol="prediction",
@@ -517,6 +519,7 @@ class GBTClassifier(Estimator, _GBTParams, HasProbabilityCol, HasRawPredictionCo
                     MLReadable):
     """Gradient-Boosted Trees (GBTs) learning algorithm for classification (binary, logistic
     loss; Spark semantics: tree 0 on labels, later trees on pseudo-residuals * stepSize)."""
+    _warm_family = "trees"          # runtime/warmup.py lazy warm-up
 
     lossType = shared("lossType", "Loss function which GBT tries to minimize (case-insensitive). Supported "
                                   "options: logistic", TypeConverters.toString)
@@ -563,6 +566,7 @@ class GBTClassificationModel(_TreeClassifierModel, _GBTParams, HasProbabilityCol
 @register("org.apache.spark.ml.regression.DecisionTreeRegressor")
 class DecisionTreeRegressor(Estimator, _DecisionTreeParams, MLWritable, MLReadable):
     """Decision tree learning algorithm for regression (variance impurity)."""
+    _warm_family = "trees"          # runtime/warmup.py lazy warm-up
 
     varianceCol = shared("varianceCol", "column name for the biased sample variance of prediction.",
                          TypeConverters.toString)
@@ -606,6 +610,7 @@ class DecisionTreeRegressionModel(_TreeRegressorModel, _DecisionTreeParams):
 @register("org.apache.spark.ml.regression.RandomForestRegressor")
 class RandomForestRegressor(Estimator, _RFParams, MLWritable, MLReadable):
     """Random forest learning algorithm for regression."""
+    _warm_family = "trees"          # runtime/warmup.py lazy warm-up
 
     @keyword_only
     def __init__(self, *, featuresCol="features", labelCol="label", predictionCol="prediction", maxDepth=5,
@@ -638,6 +643,7 @@ class RandomForestRegressionModel(_TreeRegressorModel, _RFParams):
 @register("org.apache.spark.ml.regression.GBTRegressor")
 class GBTRegressor(Estimator, _GBTParams, MLWritable, MLReadable):
     """Gradient-Boosted Trees (GBTs) learning algorithm for regression (squared/absolute loss)."""
+    _warm_family = "trees"          # runtime/warmup.py lazy warm-up
 
     lossType = shared("lossType", "Loss function which GBT tries to minimize (case-insensitive). Supported "
                                   "options: squared, absolute", TypeConverters.toString)

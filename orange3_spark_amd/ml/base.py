@@ -94,9 +94,13 @@ class Estimator(Params, ABC):
         pool = _pool_of(dataset)
         if pool is not None:                  # driver of an executor pool: fit on every executor
             P.report(0.0)
-            return pool.apply(_exec_fit, self, dataset, params)
+            return pool.apply_watched(_exec_fit, self, dataset, params)
         import time
         from ..parallel.comm import COMM_STATS
+        fam = getattr(self, "_warm_family", None)
+        if fam is not None:                   # first fit of a family in this process (lazy warm-up)
+            from ..runtime.warmup import before_fit
+            before_fit(fam)
         c0 = {k: tuple(v) for k, v in COMM_STATS.items()}
         t0 = time.perf_counter()
         with trace(f"{type(self).__name__}.fit"):

@@ -80,6 +80,7 @@ class LogisticRegression(Estimator, _LogisticRegressionParams, MLWritable, MLRea
     regression, L2 / L1 / elastic-net regularisation.  Binomial training streams bf16
     features through the fused gfx950 gradient kernel with one RCCL all-reduce per pass.
     """
+    _warm_family = "glm"          # runtime/warmup.py lazy warm-up
 
     @keyword_only
     def __init__(self, *, featuresCol="features", labelCol="label", predictionCol="prediction", maxIter=100,
@@ -272,6 +273,7 @@ class _LinearSVCParams(HasFeaturesCol, HasLabelCol, HasPredictionCol, HasRawPred
 class LinearSVC(Estimator, _LinearSVCParams, MLWritable, MLReadable):
     """Linear SVM classifier (hinge loss, L2 regularisation); same fused kernel as
     LogisticRegression with a hinge epilogue (beyond-ref: Spark >= 2.2)."""
+    _warm_family = "glm"          # runtime/warmup.py lazy warm-up
 
     @keyword_only
     def __init__(self, *, featuresCol="features", labelCol="label", predictionCol="prediction", maxIter=100,

@@ -49,6 +49,7 @@ class KMeans(Estimator, _KMeansParams, MLWritable, MLReadable):
     """K-means clustering with a k-means++ like initialization mode (the k-means|| algorithm
     by Bahmani et al).  Assignment is a split-bf16 MFMA GEMM with a fused argmin on gfx950;
     per-cluster sums use deterministic slab reductions and one RCCL all-reduce/iteration."""
+    _warm_family = "kmeans"          # runtime/warmup.py lazy warm-up
 
     @keyword_only
     def __init__(self, *, featuresCol="features", predictionCol="prediction", k=2, initMode="k-means||",

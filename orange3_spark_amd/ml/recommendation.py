@@ -66,6 +66,7 @@ class ALS(Estimator, _ALSParams, MLWritable, MLReadable):
     Ratings are exchanged with all-to-all into user and item blocks; the other side's
     factors are all-gathered each half-iteration; every row's normal equations are solved
     exactly by the als_exact gfx950 kernels (cgIters > 0: opt-in conjugate gradient)."""
+    _warm_family = "als"          # runtime/warmup.py lazy warm-up
 
     @keyword_only
     def __init__(self, *, rank=10, maxIter=10, regParam=0.1, numUserBlocks=10, numItemBlocks=10,

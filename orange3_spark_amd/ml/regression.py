@@ -59,6 +59,7 @@ class LinearRegression(Estimator, _LinearRegressionParams, MLWritable, MLReadabl
     """Linear regression (squared loss; L2 / L1 / elastic net).  ``normal`` solves the
     all-reduced weighted Gram system (X^T W X is one GEMM per rank); ``l-bfgs`` streams
     the fused GLM kernel."""
+    _warm_family = "glm"          # runtime/warmup.py lazy warm-up
 
     @keyword_only
     def __init__(self, *, featuresCol="features", labelCol="label", predictionCol="prediction", maxIter=100,

@@ -165,6 +165,29 @@ def host():
     return _HOST
 
 
+PRELOAD_TAGS = ("glm", "trees", "kmeans", "als", "als_dense", "als_exact", "assemble", "binsum", "eval",
+                "sampling", "sparse", "text", "probe")
+
+
+def preload(tags=PRELOAD_TAGS) -> dict:
+    """Load the gfx950 code objects of the given kernel files on the current device without
+    launching anything (``O3S_PRELOAD`` in ``csrc/common.h``); seconds per file."""
+    import time
+    lib = kernels()
+    out = {}
+    for tag in tags:
+        fn = getattr(lib, f"o3s_preload_{tag}", None)
+        if fn is None:
+            continue
+        fn.restype = C.c_int
+        t = time.perf_counter()
+        rc = fn()
+        if rc != 0:
+            raise NativeError(f"o3s_preload_{tag}: hipError {rc}")
+        out[tag] = round(time.perf_counter() - t, 5)
+    return out
+
+
 def available() -> bool:
     try:
         kernels()

@@ -534,3 +534,5 @@ O3S_API int o3s_als_init(int64_t row0, int64_t n, int R, uint32_t seed, int nonn
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+O3S_PRELOAD(als)

@@ -707,3 +707,5 @@ O3S_API int o3s_als_dense_wave(int implicit, int R, const int32_t* meta, const i
                                hipStream_t st) {
   return o3s_als_dense_wave_dbg(implicit, R, meta, cols, w, b, F, G, nrows, X, grid, nullptr, st);
 }
+
+O3S_PRELOAD(als_dense)

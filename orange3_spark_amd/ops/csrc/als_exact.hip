@@ -533,3 +533,5 @@ O3S_API int o3s_als_rotate(int R, const float* QT, const int32_t* rows, int64_t 
 }
 
 O3S_API int o3s_als_exact_max_small() { return kNW; }
+
+O3S_PRELOAD(als_exact)

@@ -287,3 +287,5 @@ O3S_API int o3s_assemble_cols(const void* srcs, int src_dtype, int D, int ld, in
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+O3S_PRELOAD(assemble)

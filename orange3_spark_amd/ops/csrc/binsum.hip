@@ -124,3 +124,5 @@ O3S_API int o3s_bin_sums(const void* X, int dtype, int64_t n, int64_t ldx, int D
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+O3S_PRELOAD(binsum)

@@ -125,3 +125,16 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 
 #define O3S_CHECK_LAUNCH() \
   do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)
+
+// Code-object preload (runtime/warmup.py, "preload"): every .hip file is its own fatbin, and
+// HIP loads a fatbin's gfx950 code object at the first use of any kernel in it.  Each file
+// ends with O3S_PRELOAD(tag), exporting o3s_preload_<tag>() that looks up a trivial kernel
+// of that file -- which loads the file's whole code object without running anything.
+#define O3S_PRELOAD(tag)                                                                   \
+  namespace {                                                                              \
+  __global__ void o3s_preload_touch_kernel() {}                                            \
+  }                                                                                        \
+  O3S_API int o3s_preload_##tag() {                                                        \
+    hipFuncAttributes a__;                                                                 \
+    return (int)hipFuncGetAttributes(&a__, reinterpret_cast<const void*>(&o3s_preload_touch_kernel)); \
+  }

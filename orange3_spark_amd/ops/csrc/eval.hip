@@ -151,3 +151,5 @@ O3S_API int o3s_score_hist(const void* s, int sdt, int64_t pstride, const void* 
   score_hist_kernel<<<eval_grid(n), kEvalThreads, 0, st>>>(s, sdt, pstride, y, ydt, w, wdt, n, lo, scale, bins, hist);
   return (int)hipGetLastError();
 }
+
+O3S_PRELOAD(eval)

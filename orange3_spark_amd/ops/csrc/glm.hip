@@ -1627,3 +1627,5 @@ O3S_API int o3s_glm_softmax(const void* X, int64_t n, int64_t ldx, int d, const 
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+O3S_PRELOAD(glm)

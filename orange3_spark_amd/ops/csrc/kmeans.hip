@@ -1439,3 +1439,5 @@ O3S_API int o3s_kmeanspp(const float* PT, const double* w, const double* pn, int
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+O3S_PRELOAD(kmeans)

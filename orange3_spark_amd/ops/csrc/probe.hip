@@ -50,3 +50,5 @@ O3S_API int o3s_gather_probe(const float* F, int R, const int32_t* idx, int64_t 
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+O3S_PRELOAD(probe)

@@ -36,3 +36,5 @@ O3S_API int o3s_hash_uniform(const int64_t* rows, int64_t row0, int64_t n, uint3
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+O3S_PRELOAD(sampling)

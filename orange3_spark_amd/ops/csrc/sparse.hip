@@ -162,3 +162,5 @@ O3S_API int o3s_csc_colsum(const int64_t* plo, const int32_t* pcnt, int64_t npie
 
 // CSC piece size used by the host planner.
 O3S_API int o3s_csc_piece() { return kPiece; }
+
+O3S_PRELOAD(sparse)

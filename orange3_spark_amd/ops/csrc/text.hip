@@ -279,3 +279,5 @@ O3S_API int o3s_murmur3_terms(const int64_t* offs, const uint8_t* bytes, int64_t
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+O3S_PRELOAD(text)

@@ -1109,3 +1109,5 @@ O3S_API int o3s_tree_final_level(const uint8_t* bins, int64_t rs, int64_t cs, co
   O3S_CHECK_LAUNCH();
   return 0;
 }
+
+O3S_PRELOAD(trees)

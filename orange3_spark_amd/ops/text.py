@@ -117,8 +117,14 @@ def pack_strings(values):
     str / None.  Compact ASCII columns (the common case) are packed by the host runtime
     (csrc/host_strings.cpp: a length pass, then a threaded copy of each string's bytes,
     GIL released) -- ascii=True; anything else goes through pyarrow -- ascii=None (unknown:
-    the caller checks the bytes)."""
-    vals = np.asarray(values, dtype=object)
+    the caller checks the bytes).
+
+    The native passes read the str objects with the GIL released, so they run over a
+    private snapshot of the column (``np.array(..., copy=True)``: a new array holding its
+    own reference to every object, taken under the GIL).  Another thread that replaces an
+    element of the caller's array meanwhile can then neither free an object the passes
+    read nor make the length pass and the copy pass see different strings."""
+    vals = np.array(values, dtype=object, copy=True)
     n = vals.shape[0]
     if vals.ndim == 1 and vals.flags.c_contiguous and n:
         lib = N.host()

@@ -129,6 +129,11 @@ class Comm:
         self.all_reduce(t, "max")
         return t.item()
 
+    def any_flag(self, flag: bool) -> bool:
+        """Collective OR of one host boolean (a stop decision every rank must take at the
+        same point).  Runs on the host (gloo) group: no device allocation or sync."""
+        return bool(flag)
+
     @property
     def is_driver(self) -> bool:
         return self.rank == 0
@@ -317,6 +322,13 @@ class TorchComm(Comm):
         dist.broadcast_object_list(buf, src=src, group=self._cpu_group or self.group)
         return buf[0]
 
+    def any_flag(self, flag):
+        if self.world_size == 1:
+            return bool(flag)
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self._cpu_group or self.group)
+        return bool(t.item())
+
 
 def env_world() -> tuple[int, int, int]:
     """(rank, local_rank, world_size) from torchrun-style environment variables."""
@@ -380,6 +392,6 @@ def _guard(name, fn):
 
 
 for _n in ("all_reduce", "all_gather", "all_gather_v", "all_gather_into", "reduce_scatter", "broadcast", "all_to_all_v", "barrier",
-           "all_gather_object", "broadcast_object"):
+           "all_gather_object", "broadcast_object", "any_flag"):
     setattr(TorchComm, _n, _guard(_n, TorchComm.__dict__[_n]))
 LocalComm.all_reduce = _guard("all_reduce", LocalComm.__dict__["all_reduce"])

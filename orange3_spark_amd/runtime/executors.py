@@ -243,6 +243,7 @@ def _worker_main(rank: int, world: int, port: int, conf_pairs, conn, use_gpu: bo
             conf.set("o3s.device", "cpu")
         s = Session(conf)
         Session._active = s
+        s._warmup()                           # every rank in lock step (runtime/warmup.py)
     except BaseException:  # noqa: BLE001 - reported to the driver
         conn.send_bytes(pickle.dumps(("error", rank, traceback.format_exc())))
         return
@@ -255,6 +256,8 @@ def _worker_main(rank: int, world: int, port: int, conf_pairs, conn, use_gpu: bo
             msg = conn.recv_bytes()
         except (EOFError, OSError):
             break
+        if msg == _CANCEL:                    # a cancel that arrived after its fit finished
+            continue
         try:
             garbage, slots = pickle.loads(msg[8:_hdr_len(msg)])
         except Exception:  # noqa: BLE001
@@ -270,18 +273,54 @@ def _worker_main(rank: int, world: int, port: int, conf_pairs, conn, use_gpu: bo
             if kind == "stop":
                 conn.send_bytes(pickle.dumps(("ok", rank, None)))
                 break
-            result = _execute(s, cmd, objs)
+            if kind == "watched":             # ("watched", inner, want_progress, want_cancel)
+                with _watch_scope(s, conn, rank, cmd[2], cmd[3]):
+                    result = _execute(s, cmd[1], objs)
+            else:
+                result = _execute(s, cmd, objs)
             buf = io.BytesIO() if rank == 0 else _Null()
             _worker_pickler(objs, ids, counter, buf, s).dump(result)
             conn.send_bytes(pickle.dumps(("ok", rank, buf.getvalue() if rank == 0 else None)))
-        except BaseException:  # noqa: BLE001 - every failure goes back to the driver
-            conn.send_bytes(pickle.dumps(("error", rank, traceback.format_exc())))
+        except BaseException as e:  # noqa: BLE001 - every failure goes back to the driver
+            from .progress import FitCancelled
+            st = "cancelled" if isinstance(e, FitCancelled) else "error"
+            conn.send_bytes(pickle.dumps((st, rank, traceback.format_exc())))
     try:
         import torch.distributed as dist
         if dist.is_initialized():
             dist.destroy_process_group()
     except Exception:  # noqa: BLE001
         pass
+
+
+# driver -> executors side message: stop the running fit (see _watch_scope)
+_CANCEL = b"\xff" * 8 + b"o3s-cancel"
+
+
+def _watch_scope(s, conn, rank: int, want_progress: bool, want_cancel: bool):
+    """Progress / cancel scope of a fit shipped from the driver (``ExecutorPool.fit``).
+
+    Rank 0 relays every percentage to the driver as a ``("progress", 0, p)`` side message
+    (the driver forwards it into the calling thread's sink).  For cancellation each rank
+    polls its pipe for :data:`_CANCEL` at every report site and the ranks OR their flags
+    with one host collective (``Comm.any_flag``), so all of them raise ``FitCancelled`` at
+    the same iteration -- a rank that stopped alone would leave its peers waiting in the
+    next all-reduce.  Report sites run in lock step on every rank (SPMD loops), so the
+    collective lines up."""
+    from . import progress as P
+    seen = [False]
+
+    def relay(p):
+        if rank == 0 and want_progress:
+            conn.send_bytes(pickle.dumps(("progress", 0, float(p))))
+
+    def cancelled():
+        if not seen[0]:
+            while conn.poll(0):
+                if conn.recv_bytes() == _CANCEL:
+                    seen[0] = True
+        return s.comm.any_flag(seen[0])
+    return P.progress_scope(relay, cancelled if want_cancel else None)
 
 
 def _hdr_len(msg: bytes) -> int:
@@ -429,6 +468,7 @@ class ExecutorPool:
         self._garbage: list = []
         self._proxies: dict = {}
         self._methods: set = set()
+        self._watch = None                        # progress / cancel relay of a running fit
         self.alive = False
         self.lost_reason: str | None = None
         self._successor: "ExecutorPool | None" = None
@@ -520,7 +560,15 @@ class ExecutorPool:
         pending = dict(enumerate(self._conns))
         out, first_err, first_ok = [], None, None
         deadline = None if timeout is None else time.monotonic() + timeout
+        watch = self._watch
         while pending:
+            if watch is not None and watch["cancel"] is not None and not watch["sent"] and watch["cancel"]():
+                watch["sent"] = True              # every rank sees it at its next report site
+                for c in self._conns:
+                    try:
+                        c.send_bytes(_CANCEL)
+                    except (BrokenPipeError, OSError):
+                        pass
             now = time.monotonic()
             limit = deadline
             if first_err is not None:
@@ -533,7 +581,8 @@ class ExecutorPool:
                 why = "watchdog" if limit == deadline else ("error grace" if first_err is not None else "straggler")
                 raise self._lost(f"executors {sorted(pending)} did not finish '{what}' ({why} timeout)"
                                  + (f"; errors: {self._fmt(out)}" if out else "") + " -- the pool was shut down")
-            ready = wait(list(pending.values()), timeout=1.0 if limit is None else max(0.01, min(1.0, limit - now)))
+            tick = 0.05 if watch is not None and watch["cancel"] is not None and not watch["sent"] else 1.0
+            ready = wait(list(pending.values()), timeout=tick if limit is None else max(0.01, min(tick, limit - now)))
             for c in ready:
                 r = next(k for k, v in pending.items() if v is c)
                 try:
@@ -543,11 +592,15 @@ class ExecutorPool:
                                      f"{self._procs[r].exitcode})") from None
                 self.bytes_received += len(raw)
                 msg = pickle.loads(raw)
+                if msg[0] == "progress":          # side message of a watched fit (rank 0)
+                    if watch is not None:
+                        watch["progress"](msg[2])
+                    continue
                 pending.pop(r)
                 out.append(msg)
-                if msg[0] == "error" and first_err is None:
+                if msg[0] in ("error", "cancelled") and first_err is None:
                     first_err = time.monotonic()
-                elif msg[0] != "error" and first_ok is None:
+                elif msg[0] not in ("error", "cancelled") and first_ok is None:
                     first_ok = time.monotonic()
             for r in list(pending):
                 if not self._procs[r].is_alive():
@@ -556,7 +609,7 @@ class ExecutorPool:
 
     @staticmethod
     def _fmt(replies):
-        return "\n".join(f"[rank {r}] {d}" for st, r, d in replies if st == "error")
+        return "\n".join(f"[rank {r}] {d}" for st, r, d in replies if st in ("error", "cancelled"))
 
     def _driver_pickle(self, cmd):
         """Pickle ``cmd`` naming every handle by slot; returns (bytes, [handles by slot]).
@@ -628,7 +681,10 @@ class ExecutorPool:
     def _run(self, bodies, slot_ids, what, recipe, found=None):
         self._send_all(bodies, slot_ids)
         replies = self._gather(self.command_timeout, what)
-        errs = [m for m in replies if m[0] == "error"]
+        if replies and all(m[0] == "cancelled" for m in replies):
+            from .progress import FitCancelled
+            raise FitCancelled(f"{what} cancelled on all {self.n} executors")
+        errs = [m for m in replies if m[0] != "ok"]
         if errs:
             raise ExecutorError("command failed on executor(s):\n" + self._fmt(replies))
         data = next(d for st, r, d in replies if r == 0)
@@ -765,6 +821,24 @@ class ExecutorPool:
 
     def apply(self, fn, *args, **kwargs):
         return self.command(("apply", fn, args, kwargs), what=getattr(fn, "__name__", "apply"))
+
+    def apply_watched(self, fn, *args, **kwargs):
+        """``apply`` for a fit, relaying the calling thread's progress sink and cancel
+        request (runtime/progress.py) to the executors: rank 0's percentages come back as
+        side messages while the command runs, and a cancel makes every rank raise
+        ``FitCancelled`` at the same iteration -- the pool stays usable."""
+        from . import progress as P
+        want_p, want_c = P.watching()
+        if not (want_p or want_c):
+            return self.apply(fn, *args, **kwargs)
+        with self._lock:
+            pool = self._revive()                 # a respawned successor runs it if this one died
+            pool._watch = {"progress": P.forward, "cancel": P.cancel_requested if want_c else None, "sent": False}
+            try:
+                return pool.command(("watched", ("apply", fn, args, kwargs), want_p, want_c),
+                                    what=getattr(fn, "__name__", "apply"))
+            finally:
+                pool._watch = None
 
     def scatter_dataframe(self, pdf, schema=None):
         """Row slice r of a host pandas frame -> executor r (only that slice is sent).  The

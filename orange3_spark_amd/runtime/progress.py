@@ -69,6 +69,16 @@ def sub_range(frac_lo: float, frac_hi: float):
         s.last = max(s.last, inner.last)
 
 
+@contextlib.contextmanager
+def detached():
+    """No sink inside (a warm-up fit run on behalf of the engine, not the caller's fit)."""
+    tok = _SINK.set(None)
+    try:
+        yield
+    finally:
+        _SINK.reset(tok)
+
+
 def active() -> bool:
     return _SINK.get() is not None
 
@@ -92,3 +102,35 @@ def iteration(done: int, total: int) -> None:
     """``report(done / total)`` for an iteration counter."""
     if total > 0:
         report(done / total)
+
+
+# ---------------------------------------------------------------- executor-pool relay
+# A fit shipped to an executor pool (runtime/executors.py) runs in other processes: rank 0
+# relays its percentages to the driver, which forwards them into the calling thread's sink
+# (never raising there: the driver is in the middle of a pool command), and a cancel request
+# travels the other way as a flag that the ranks OR together collectively at every report
+# site, so all of them raise FitCancelled at the same iteration.
+
+def watching() -> tuple:
+    """(progress wanted, cancellation wanted) for the current thread's fit."""
+    s = _SINK.get()
+    return (s is not None, s is not None and s.cancelled is not None)
+
+
+def forward(percent: float) -> None:
+    """Feed a relayed percentage (0..100 of the remote fit) into this thread's sink without
+    polling for cancellation."""
+    s = _SINK.get()
+    if s is None:
+        return
+    f = min(1.0, max(0.0, float(percent) / 100.0))
+    p = s.lo + (s.hi - s.lo) * f
+    if p > s.last:
+        s.last = p
+        s.callback(p)
+
+
+def cancel_requested() -> bool:
+    """Has this thread's caller asked to stop?  (Polls without raising.)"""
+    s = _SINK.get()
+    return bool(s is not None and s.cancelled is not None and s.cancelled())

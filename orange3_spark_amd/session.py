@@ -94,11 +94,13 @@ class Session:
             from .runtime.tracing import TRACER
             TRACER.enable(sync=str(self.conf.get("o3s.trace.sync", "false")).lower() in ("1", "true"))
         self.warmup_seconds: dict = {}
+        from .runtime.warmup import plan
+        plan(self.conf.get("o3s.session.warmup", "auto"))     # a bad value fails before publication
 
     def _warmup(self) -> None:
-        """Tiny fits of each estimator family once per process (``runtime/warmup.py``;
-        conf ``o3s.session.warmup``), so the user's first fit does not pay the one-time
-        kernel-loading costs."""
+        """Kernel code-object preload and (conf) tiny fits of the estimator families once
+        per process (``runtime/warmup.py``; conf ``o3s.session.warmup``), so the user's
+        first fit does not pay the one-time kernel-loading costs."""
         from .runtime.warmup import warmup
         self.warmup_seconds = warmup(self)
 

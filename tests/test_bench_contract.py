@@ -49,9 +49,28 @@ def test_bench_single_and_four_ranks_agree():
     assert four.returncode == 0, four.stderr[-3000:]
     r4 = _json_line(four.stdout)
     assert r4["n_gpus"] == 4 and r4["config"]["parallelism"] == "dp4" and r4["config"]["global_batch"] == 24000
+    # the record names its collective layer: gloo over 4 CPU ranks (RCCL on a GPU node),
+    # one gradient all-reduce per iteration inside the timed fit, and its measured latency
+    assert r4["backend"] == "gloo" and r4["collective_world"] == 4 and r4["rehearsal"] is False
+    assert r4["allreduce_calls_timed"] >= 3 and r4["allreduce_bytes_timed"] > 0 and r4["allreduce_us_per_call"] > 0
+    assert r1["backend"] == "local" and r1["allreduce_us_per_call"] is None
     assert abs(r4["first_loss"] - r1["first_loss"]) < 1e-9
     assert abs(r4["final_loss"] - r1["final_loss"]) < 1e-7 * abs(r1["final_loss"])
     assert r1["hbm_only_rows_per_s"] > 0 and 0 <= r1["fit_setup_share"] <= 1
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(300)
+def test_gpu_bench_refuses_a_gloo_headline():
+    """Two GPU ranks on gloo (not RCCL) must not print a headline JSON without --rehearsal."""
+    env = dict(os.environ, OMP_NUM_THREADS="4", O3S_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+                          "--steps", "1", "--warmup", "0", "--rows", "100000", "--no-hbm-only"], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=240)
+    assert two.returncode != 0 and "refusing" in two.stderr
+    assert not [ln for ln in two.stdout.splitlines() if ln.startswith("{")]
 
 
 @pytest.mark.timeout(300)
@@ -88,10 +107,12 @@ def test_gpu_bench_two_ranks_match_one_rank():
     assert r1["config"]["resident_rows"] > 0
     two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
-                          *args], cwd=ROOT, env=dict(env, O3S_DIST_BACKEND="gloo"), capture_output=True, text=True,
-                         timeout=240)
+                          *args, "--rehearsal"], cwd=ROOT, env=dict(env, O3S_DIST_BACKEND="gloo"),
+                         capture_output=True, text=True, timeout=240)
     assert two.returncode == 0, two.stderr[-3000:]
     r2 = _json_line(two.stdout)
+    assert r2["backend"] == "gloo" and r2["rehearsal"] is True and r2["collective_world"] == 2
+    assert r1["backend"] == "local" and r1["rehearsal"] is False and r1["collective_world"] == 1
     assert r2["n_gpus"] == 2 and r2["config"]["global_batch"] == 6000000
     assert r2["config"]["resident_rows"] + r2["config"]["lineage_rows"] == 6000000
     assert abs(r2["first_loss"] - r1["first_loss"]) < 1e-6

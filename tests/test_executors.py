@@ -115,6 +115,34 @@ def test_executor_errors_surface_and_pool_survives(pool_session):
     assert s.pool.alive and df.count() == 60
 
 
+def test_pool_fit_relays_progress_and_cancels_collectively(pool_session):
+    """The multi-GPU canvas path (SURVEY Q14 on a DriverSession): a fit shipped to the
+    executors reports rank 0's per-iteration progress into the caller's sink, and a cancel
+    request stops every rank at the same iteration (FitCancelled on the driver, no
+    watchdog teardown); the next fit on the same pool succeeds."""
+    from orange3_spark_amd.ml.classification import GBTClassifier, LogisticRegression
+    from orange3_spark_amd.ml.feature import VectorAssembler
+    from orange3_spark_amd.runtime.progress import FitCancelled
+    s = pool_session
+    pids = list(s.pool.pids)
+    feats = VectorAssembler(inputCols=list("abcde"), outputCol="features").transform(s.createDataFrame(_pdf(6000)))
+    seen = []
+    lr = LogisticRegression(maxIter=20, tol=0.0, regParam=0.01).fit(feats, progress=seen.append)
+    assert seen[-1] == 100.0 and all(b >= a for a, b in zip(seen, seen[1:]))
+    assert len(seen) >= 15 and any(40 <= v <= 60 for v in seen)      # per iteration, from rank 0
+    gb = []
+    GBTClassifier(maxIter=5, maxDepth=3, seed=1).fit(feats, progress=gb.append)
+    assert gb[-1] == 100.0 and all(b >= a for a, b in zip(gb, gb[1:])) and len(gb) >= 5
+    got = []
+    with pytest.raises(FitCancelled):
+        LogisticRegression(solver="sgd", maxIter=200, tol=0.0, regParam=0.01).fit(
+            feats, progress=got.append, cancelled=lambda: bool(got) and got[-1] >= 50.0)
+    assert 50.0 <= got[-1] <= 50.0 + 2 * 100.0 / 200       # stopped within about one iteration
+    assert s.pool.alive and s.pool.pids == pids             # collective stop: no teardown
+    again = LogisticRegression(maxIter=20, tol=0.0, regParam=0.01).fit(feats)
+    np.testing.assert_allclose(again.coefficients.toArray(), lr.coefficients.toArray(), rtol=1e-9, atol=1e-12)
+
+
 def test_dropped_handles_are_freed_on_executors(pool_session):
     import gc
     s = pool_session

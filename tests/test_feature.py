@@ -309,3 +309,36 @@ def test_native_string_packing_matches_arrow_buffers():
     for odd in (["héllo", "a"], ["a", b"b"]):
         offs, data, valid, ascii_ = TX.pack_strings(np.asarray(odd, dtype=object))
         assert ascii_ is None
+
+
+def test_native_string_packing_while_another_thread_mutates_the_column():
+    """The native passes run with the GIL released (ADVICE/VERDICT r5): a second thread
+    replacing elements of the caller's array (and dropping the old strings) while
+    pack_strings runs must not change what is packed -- the passes work on a private
+    snapshot -- and the result must be one consistent column."""
+    import threading
+    from orange3_spark_amd.ops import text as TX
+    n = 20_000
+    src = np.asarray(["a" * (600 + i % 50) for i in range(n)], dtype=object)      # > 8 MB: threaded copy
+    stop = threading.Event()
+
+    def mutate():
+        k = 0
+        while not stop.is_set():
+            i = k % n
+            src[i] = "b" * (1 + k % 3000)                  # frees the previous str (no other reference)
+            k += 1
+    th = threading.Thread(target=mutate)
+    th.start()
+    try:
+        for _ in range(20):
+            offs, data, valid, ascii_ = TX.pack_strings(src)
+            assert ascii_ is True and valid is None and offs.shape == (n + 1,)
+            lens = np.diff(offs)
+            assert int(offs[-1]) == data.shape[0]
+            for i in range(0, n, 997):                    # every string is wholly one version
+                s = bytes(data[offs[i]:offs[i + 1]])
+                assert s == b"a" * lens[i] or s == b"b" * lens[i]
+    finally:
+        stop.set()
+        th.join()

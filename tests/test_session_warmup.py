@@ -36,7 +36,10 @@ def test_listed_families_run_once_per_process(fresh):
 
 
 def test_unknown_family_is_an_error(fresh):
-    with pytest.raises(ValueError, match="unknown families"):
+    with pytest.raises(ValueError, match="unknown value or families"):
+        Session.getOrCreate(SessionConf().set("o3s.device", "cpu").set("o3s.session.warmup", "glm,nope"))
+    assert Session.active() is None                     # not published with the bad value
+    with pytest.raises(ValueError):
         Session.getOrCreate(SessionConf().set("o3s.device", "cpu").set("o3s.session.warmup", "glm,nope"))
 
 
@@ -46,11 +49,28 @@ def test_false_disables(fresh):
 
 
 @pytest.mark.gpu
-def test_gpu_auto_warms_every_family(fresh):
+def test_gpu_auto_preloads_then_warms_only_the_fitted_family(fresh, monkeypatch):
+    """auto: the session start only loads the kernel code objects (no fit); a family's
+    tiny warm-up fit runs right before its first real fit, once per process, and a
+    session that only fits LR never warms the other families."""
+    monkeypatch.setattr(W, "_PRELOADED", set())
     s = Session.getOrCreate(SessionConf())
     assert s.device.type == "cuda"
-    assert set(s.warmup_seconds) == set(W.FAMILIES)
-    assert sum(s.warmup_seconds.values()) < 30
+    assert set(s.warmup_seconds) == {"preload"} and s.warmup_seconds["preload"] < 1.0
+    from orange3_spark_amd.ml.classification import LogisticRegression
+    df = s.synthetic.classification(50_000, 32, seed=1)
+    LogisticRegression(maxIter=3).fit(df)
+    assert set(s.warmup_seconds) == {"preload", "glm"} and W._DONE == {"glm"}
+    LogisticRegression(maxIter=3).fit(df)
+    assert set(s.warmup_seconds) == {"preload", "glm"}
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_gpu_listed_families_warm_at_session_start(fresh):
+    s = Session.getOrCreate(SessionConf().set("o3s.session.warmup", "true"))
+    assert set(s.warmup_seconds) >= set(W.FAMILIES)
+    assert sum(v for v in s.warmup_seconds.values() if v) < 30
     torch.cuda.synchronize()
 
 

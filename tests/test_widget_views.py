@@ -6,6 +6,7 @@ import pkgutil
 import threading
 from types import SimpleNamespace
 
+import numpy as np
 import pandas as pd
 import pytest
 
@@ -221,9 +222,10 @@ class _Concurrent:
     def __init__(self):
         self.progress = []
         self.progress_threads = set()
+        self.interrupt = lambda: False        # the Cancel button (Orange: TaskState.interruption)
 
     def start(self, task, *args):
-        state = SimpleNamespace(set_progress_value=self._progress, is_interruption_requested=lambda: False)
+        state = SimpleNamespace(set_progress_value=self._progress, is_interruption_requested=lambda: self.interrupt())
         box = {}
 
         def run():
@@ -575,6 +577,49 @@ def test_concurrent_fit_reports_progress_and_touches_qt_only_on_gui_thread(orang
     assert w.progress_threads == {"task-worker"}
     w.core.info("done on the worker")                    # GUI-thread call: shown at once
     assert w.shown["info"] == "done on the worker"
+
+
+@pytest.mark.timeout(300)
+def test_pool_fit_from_the_view_reports_progress_and_cancels(orange_mt):
+    """The 8-GPU canvas deployment in miniature: the Context is a 2-executor pool, the
+    Classification view's Apply runs the fit on a worker thread, rank 0's per-iteration
+    progress reaches the task state, and Cancel stops the fit on every executor at the
+    same iteration -- the widget shows FitCancelled, the pool survives for the next Apply."""
+    from orangecontrib.spark_amd.widgets.ml.owclassification import OWClassification
+    pool = Session(SessionConf().set("spark.executor.instances", "2").set("o3s.device", "cpu"))
+    prev = SharedSession._session
+    SharedSession._session = pool
+    try:
+        V = qt_view(OWClassification, orange_mt)
+        w = V()
+        rng = np.random.default_rng(0)
+        X = rng.normal(size=(4000, 2))
+        df = pool.createDataFrame(pd.DataFrame({"features": list(X), "label": (X[:, 0] > X[:, 1]).astype(float)}))
+        w._param_changed("method", "LogisticRegression")
+        w.set_dataframe(df)
+        w._param_changed("solver", "sgd")
+        w._param_changed("maxIter", "20")
+        w._param_changed("tol", "0.0")
+        w.run_action()
+        assert type(V.Outputs.model.sent[-1]).__name__ == "LogisticRegressionModel"
+        p = list(w.progress)
+        assert len(p) >= 15 and p[-1] == 100.0 and all(b >= a for a, b in zip(p, p[1:])), p
+        pids = list(pool.pool.pids)
+        w.progress.clear()
+        sent = len(V.Outputs.model.sent)
+        w._param_changed("maxIter", "400")
+        w.interrupt = lambda: bool(w.progress) and w.progress[-1] >= 50.0
+        w.run_action()
+        assert "FitCancelled" in (w.shown.get("error") or "")
+        assert len(V.Outputs.model.sent) == sent and w.progress[-1] < 52.0
+        assert pool.pool.alive and pool.pool.pids == pids
+        w.interrupt = lambda: False
+        w._param_changed("maxIter", "5")
+        w.run_action()
+        assert len(V.Outputs.model.sent) == sent + 1
+    finally:
+        SharedSession._session = prev
+        pool.stop()
 
 
 def test_worker_messages_are_queued_to_the_gui_thread(orange_mt, session):
