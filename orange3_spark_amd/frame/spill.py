@@ -548,6 +548,7 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
                 host[a + r - keep:b - keep].copy_(out[r:], non_blocking=True)
             out.record_stream(d2h)
     t2 = _time.perf_counter()
+    LAST_ASSEMBLE_STATS["loop_s"] = t2 - _t0
     torch.cuda.synchronize(dev)
     LAST_ASSEMBLE_STATS["final_sync_s"] = _time.perf_counter() - t2
     col = SpilledVectorColumn(res, host, D) if n > keep else C.VectorColumn(res, D)

@@ -97,15 +97,16 @@ class Estimator(Params, ABC):
             return pool.apply_watched(_exec_fit, self, dataset, params)
         import time
         from ..parallel.comm import COMM_STATS
+        from ..runtime import warmup as W
         fam = getattr(self, "_warm_family", None)
         if fam is not None:                   # first fit of a family in this process (lazy warm-up)
-            from ..runtime.warmup import before_fit
-            before_fit(fam)
-        c0 = {k: tuple(v) for k, v in COMM_STATS.items()}
-        t0 = time.perf_counter()
-        with trace(f"{type(self).__name__}.fit"):
-            model = self.copy(params)._fit(dataset) if params else self._fit(dataset)
-        _attach_fit_stats(model, dataset, time.perf_counter() - t0, c0, COMM_STATS)
+            W.before_fit(fam)
+        with W.user_fit(fam):                 # never alongside a background warm-up fit
+            c0 = {k: tuple(v) for k, v in COMM_STATS.items()}
+            t0 = time.perf_counter()
+            with trace(f"{type(self).__name__}.fit"):
+                model = self.copy(params)._fit(dataset) if params else self._fit(dataset)
+            _attach_fit_stats(model, dataset, time.perf_counter() - t0, c0, COMM_STATS)
         return model
 
     def fitMultiple(self, dataset, paramMaps):

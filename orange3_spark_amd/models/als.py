@@ -402,6 +402,8 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
     eigmode = (EIG_BASIS and implicit and not nonneg and dev.type == "cuda" and rank in A.EXACT_RANKS
                and X.dtype == torch.float32 and (exact is True or (exact is None and cg_iters <= 0)))
     basis = [None]                       # [R, R] fp64 (host); None = the identity
+    if eigmode and comm.world_size > 1:
+        A.EIG_CACHE.comm = comm          # the eigenbasis comes from rank 0
 
     def to_orig(T):
         if basis[0] is None:
@@ -436,7 +438,7 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
                 X = solve_side(by_user, Yf, X, reg, implicit, alpha, YtY, cg_iters, nonneg, exact,
                                eig_basis=eigmode)
             if eigmode:                  # X now holds X (B Q): the basis moves on by Q
-                q = A.EIG_CACHE.get(Yf, YtY, True)[1].double().cpu()
+                q = A.EIG_CACHE.get(Yf, YtY, True, shared=True)[1].double().cpu()
                 basis[0] = q if basis[0] is None else basis[0] @ q
             if not chunked:
                 del Yf

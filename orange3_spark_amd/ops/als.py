@@ -193,8 +193,12 @@ class _EigCache:
     def __init__(self):
         self.key = None
         self.val = None
+        # set by fit_als for multi-rank eigenbasis fits: (eig, Q) then come from rank 0 --
+        # every rank's tables must live in the SAME basis, and LAPACK on different ranks
+        # (different CPUs / BLAS dispatch) may pick different signs or degenerate vectors
+        self.comm = None
 
-    def get(self, F, G, need_fq: bool):
+    def get(self, F, G, need_fq: bool, shared: bool = False):
         import weakref
         key = (F._version, G._version, tuple(F.shape))
         if (self.key is not None and self.key[0]() is F and self.key[1]() is G and self.key[2] == key
@@ -208,6 +212,12 @@ class _EigCache:
         ev, V = torch.linalg.eigh(0.5 * (Gd + Gd.T))
         eig = ev.clamp_min(0.0).float().to(F.device).contiguous()
         Q = V.float().to(F.device).contiguous()
+        comm = self.comm if shared else None
+        if comm is not None and comm.world_size > 1:          # rank 0's basis on every rank
+            R = Q.shape[0]
+            both = torch.cat([eig.reshape(1, R), Q]).contiguous()
+            comm.broadcast(both, src=0)
+            eig, Q = both[0].contiguous(), both[1:].contiguous()
         FQ = rotated_table(F, Q) if need_fq else None
         self.key = (weakref.ref(F), weakref.ref(G), key)
         self.val = (eig, Q, FQ)
@@ -215,6 +225,7 @@ class _EigCache:
 
     def clear(self):
         self.key = self.val = None
+        self.comm = None
 
 
 EIG_CACHE = _EigCache()
@@ -283,9 +294,9 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
     lib = N.kernels()
     st = N.stream_of(out)
     eig_basis = bool(eig_basis and implicit)
-    if eig_basis:
+    if eig_basis:                        # every rank calls this (shared basis, see _EigCache)
         with trace("als.eig_rotated_table"):
-            eig, Q, P = EIG_CACHE.get(F, G, True)
+            eig, Q, P = EIG_CACHE.get(F, G, True, shared=True)
     if ns:
         if eig_basis:
             pass

@@ -17,6 +17,7 @@ through ``self.error``) instead of a hang or a silent wrong answer.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 import threading
 from collections import Counter
@@ -56,7 +57,7 @@ class _Injector:
             self.calls = Counter()
 
     def hit(self, op: str):
-        if not self.plan:
+        if not self.plan or getattr(_QUIET, "on", False):
             return
         with self._lock:
             self.calls[op] += 1
@@ -65,6 +66,19 @@ class _Injector:
 
 
 INJECTOR = _Injector()
+_QUIET = threading.local()               # engine-internal threads (warm-up) are not counted
+
+
+@contextlib.contextmanager
+def quiet():
+    """Injection points reached by this thread inside are neither counted nor fired (the
+    background warm-up's kernels and collectives are not the program under test)."""
+    was = getattr(_QUIET, "on", False)
+    _QUIET.on = True
+    try:
+        yield
+    finally:
+        _QUIET.on = was
 
 
 def launch_blocking() -> bool:

@@ -122,13 +122,26 @@ class Tracer:
 
 
 TRACER = Tracer()
+_OFF = threading.local()                 # per-thread suppression (the background warm-up)
+
+
+@contextlib.contextmanager
+def suppressed():
+    """No phases are recorded from this thread inside (engine-internal work such as the
+    warm-up fits stays out of the user's trace; other threads keep tracing)."""
+    was = getattr(_OFF, "on", False)
+    _OFF.on = True
+    try:
+        yield
+    finally:
+        _OFF.on = was
 
 
 @contextlib.contextmanager
 def trace(name: str, **args):
     """Mark a phase (no-op unless tracing is enabled)."""
     t = TRACER
-    if not t.enabled:
+    if not t.enabled or getattr(_OFF, "on", False):
         yield
         return
     t._sync()
@@ -159,7 +172,7 @@ def traced(name: str | None = None):
         label = name or fn.__qualname__
 
         def wrapper(*a, **k):
-            if not TRACER.enabled:
+            if not TRACER.enabled or getattr(_OFF, "on", False):
                 return fn(*a, **k)
             with trace(label):
                 return fn(*a, **k)
@@ -171,5 +184,5 @@ def traced(name: str | None = None):
 
 
 def mark(name: str):
-    if TRACER.enabled:
+    if TRACER.enabled and not getattr(_OFF, "on", False):
         TRACER.roctx.mark(name)

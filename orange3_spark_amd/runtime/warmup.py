@@ -1,39 +1,48 @@
 """Device warm-up: what a process's first fit would otherwise pay once.
 
 The first fit of an estimator family in a process pays one-time costs that later fits do
-not: the HIP code objects of this framework's kernels (one fatbin per ``csrc/*.hip`` file)
-and of PyTorch's are loaded at their first launch, and first calls set up host-side state.
-On the GBT config (500M x 64, depth 8, 5 trees) that was 0.31 s of a 1.01 s first fit
-(``profiles/gbt_cold_fit_r5.json``).  The reference's estimators run on a JVM whose
-executors are already started and JIT-warm when the Orange canvas fits its first model
-(``orangecontrib/spark/base/spark_ml_estimator.py:22``, cluster started at
-``widgets/data/spark_context.py:76``); here the session pays the equivalent up front.
+not.  Measured on the GBT config (``tools/prof_coldfit.py``, ``profiles/coldstart_r6.json``):
+the cold cost is almost all PyTorch's kernel code objects, loaded at the first launch of
+each op (``index_select`` alone 133 ms, ``max`` / ``sum`` / ``zeros_like`` / ``stack`` /
+``cumsum`` 8-23 ms each); this framework's own 13 fatbins load in 37 ms.  The reference's
+estimators run on a JVM whose executors are already started and JIT-warm when the Orange
+canvas fits its first model (``orangecontrib/spark/base/spark_ml_estimator.py:22``, the
+cluster started at ``widgets/data/spark_context.py:76``); here the session does the
+equivalent without making anyone wait for it.
 
 Conf ``o3s.session.warmup``:
 
-* ``auto`` (default) -- GPU sessions preload the kernel code objects (``preload``: no
-  launch, no collective, so SPMD ranks and executor-pool workers do it too) and warm each
-  estimator family lazily, once per process, right before that family's first fit
-  (``lazy``); a family the graph never fits costs nothing;
-* ``preload`` -- the code objects only;  ``lazy`` -- preload + the per-family lazy warm-up;
-* ``true`` / ``all`` or a comma list of :data:`FAMILIES` -- tiny fits of those families
-  at session start (round-5 behaviour), plus the preload;
+* ``auto`` (default) -- GPU sessions preload this framework's kernel code objects
+  (synchronous, ~40 ms, no launch) and then warm the estimator families in a **background
+  thread**: one tiny fit per family, on a private single-rank session (no collective, so
+  SPMD ranks and executor-pool workers do it too) on its own HIP stream, while the caller
+  goes on loading data.  Session start pays only the preload; a family whose first real
+  fit arrives before its warm-up finished simply pays its own cold cost;
+* ``lazy`` -- preload, then each family's tiny fit right before its first real fit;
+* ``preload`` -- the code objects only;
+* ``true`` / ``all`` or a comma list of :data:`FAMILIES` -- tiny fits of those families at
+  session start, synchronously (plus the preload on GPU);
 * ``false`` -- nothing.
 
-The lazy warm-up is a tiny fit of the same family on a few thousand synthetic rows,
-issued on the ranks in lock step (the fit about to run is collective on every rank
-anyway), so it is safe on SPMD ranks and pool workers.  ``Session.warmup_seconds``
-reports the time per step."""
+A background tiny fit never overlaps a user fit: user fits wait for the tiny fit in
+flight (at most one, ~0.05-0.3 s) and the warm-up thread waits while any user fit runs
+(:func:`user_fit`), so the engine's per-family module caches are never shared between
+the two.  The warm-up thread's kernels, collectives and phases are invisible to fault
+injection, ``COMM_STATS`` and the trace.  ``Session.warmup_seconds`` reports the time per
+step (background steps appear when they finish)."""
 from __future__ import annotations
 
+import contextlib
+import threading
 import time
 import warnings
 
 FAMILIES = ("trees", "glm", "kmeans", "als")
-_DONE: set = set()
+_DONE: set = set()                       # families warm in this process
 _RUNNING: set = set()                    # a family's tiny fit must not warm itself again
-_FAILED: set = set()                     # lazy: a failed warm-up is not retried at every fit
+_FAILED: set = set()                     # a failed warm-up is not retried at every fit
 _PRELOADED: set = set()
+_TL = threading.local()                  # .warming: this thread runs a warm-up fit
 
 
 def plan(value) -> tuple:
@@ -42,7 +51,9 @@ def plan(value) -> tuple:
     v = str(value if value is not None else "auto").strip().lower()
     if v in ("false", "0", "no", "off", "none", ""):
         return ("off", ())
-    if v in ("auto", "lazy"):
+    if v == "auto":
+        return ("background", FAMILIES)
+    if v == "lazy":
         return ("lazy", ())
     if v == "preload":
         return ("preload", ())
@@ -80,6 +91,58 @@ def _fit_als(s):
 _FIT = {"trees": _fit_trees, "glm": _fit_glm, "kmeans": _fit_kmeans, "als": _fit_als}
 
 
+# ---------------------------------------------------------------- user-fit / warm-up gate
+class _Gate:
+    """Readers (user fits, any thread, nested) vs one writer (the background tiny fit)."""
+
+    def __init__(self):
+        self.cond = threading.Condition()
+        self.users = 0
+        self.warming = False
+
+    def user_enter(self):
+        with self.cond:
+            while self.warming:
+                self.cond.wait()
+            self.users += 1
+
+    def user_exit(self):
+        with self.cond:
+            self.users -= 1
+            self.cond.notify_all()
+
+    def warm_enter(self):
+        with self.cond:
+            while self.users or self.warming:
+                self.cond.wait()
+            self.warming = True
+
+    def warm_exit(self):
+        with self.cond:
+            self.warming = False
+            self.cond.notify_all()
+
+
+GATE = _Gate()
+
+
+@contextlib.contextmanager
+def user_fit(family):
+    """Around every local fit (``ml/base.py``): waits for a background tiny fit in flight
+    and keeps new ones out until the fit ends; the family counts as warm afterwards."""
+    if getattr(_TL, "warming", False):   # the warm-up's own fit
+        yield
+        return
+    GATE.user_enter()
+    try:
+        yield
+    finally:
+        GATE.user_exit()
+        if family is not None and family not in _DONE:
+            _DONE.add(family)            # its cold cost is paid: the background skips it
+
+
+# ---------------------------------------------------------------- steps
 def _preload(session, out: dict) -> None:
     dev = session.device
     if dev.type != "cuda" or dev in _PRELOADED:
@@ -95,49 +158,122 @@ def _preload(session, out: dict) -> None:
     out["preload"] = round(time.perf_counter() - t, 4)
 
 
-def _run_family(session, fam: str, out: dict) -> None:
-    from .tracing import TRACER
-    from . import progress
+def _run_family(session, fam: str, out: dict, quiet: bool = False) -> None:
+    from . import faults, progress
+    from .tracing import TRACER, suppressed
     was = TRACER.enabled                 # the warm-up fits stay out of the user's trace
-    TRACER.enabled = False
+    if not quiet:
+        TRACER.enabled = False
     _RUNNING.add(fam)
+    _TL.warming = True
     t = time.perf_counter()
     try:
-        with progress.detached():        # and out of the caller's progress / cancel scope
+        with progress.detached(), suppressed(), (faults.quiet() if quiet else contextlib.nullcontext()):
             _FIT[fam](session)
-        if session.device.type == "cuda":
-            import torch
-            torch.cuda.synchronize(session.device)
+            if session.device.type == "cuda":
+                import torch
+                torch.cuda.current_stream(session.device).synchronize()
         out[fam] = round(time.perf_counter() - t, 4)
         _DONE.add(fam)
     except Exception as e:               # a warm-up failure must not stop the session or fit
         warnings.warn(f"o3s.session.warmup: the {fam} warm-up fit failed ({type(e).__name__}: {e}); "
                       "its first real fit pays the one-time costs instead", RuntimeWarning)
         out[fam] = None
+        _FAILED.add(fam)
     finally:
+        _TL.warming = False
         _RUNNING.discard(fam)
-        TRACER.enabled = was
+        if not quiet:
+            TRACER.enabled = was
+
+
+def _private_session(session):
+    """A single-rank session on the same device for the background fits: its comm is a
+    LocalComm whose collectives bypass the traced / counted wrappers."""
+    from ..parallel.comm import LocalComm
+    from ..session import Session
+
+    class _QuietComm(LocalComm):
+        all_reduce = LocalComm.all_reduce.__wrapped__
+
+    conf = session.conf.copy().set("o3s.session.warmup", "false").set("o3s.trace", "false")
+    return Session(conf, comm=_QuietComm(session.device), device=session.device)
+
+
+_THREAD = None
+_STOP = threading.Event()
+
+
+def _stop_background() -> None:
+    """At interpreter exit: let the tiny fit in flight finish and start no other, before
+    the HIP runtime is torn down under a daemon thread still inside a launch."""
+    _STOP.set()
+    wait_background(60)
+
+
+import atexit  # noqa: E402
+
+atexit.register(_stop_background)
+
+
+def _background(session, fams) -> None:
+    import torch
+    try:
+        priv = _private_session(session)
+        torch.cuda.set_device(session.device)
+        stream = torch.cuda.Stream(session.device)
+    except Exception as e:  # noqa: BLE001
+        warnings.warn(f"o3s.session.warmup: background warm-up not started ({e})", RuntimeWarning)
+        return
+    for fam in fams:
+        if fam in _DONE or fam in _FAILED or _STOP.is_set():
+            continue
+        GATE.warm_enter()
+        try:
+            if fam in _DONE or _STOP.is_set():      # a user fit of this family ran meanwhile
+                continue
+            out: dict = {}
+            with torch.cuda.stream(stream):
+                _run_family(priv, fam, out, quiet=True)
+            session.warmup_seconds.update(out)
+        finally:
+            GATE.warm_exit()
+
+
+def wait_background(timeout: float | None = None) -> bool:
+    """Join the background warm-up (tests, benchmarks); True when it has finished."""
+    th = _THREAD
+    if th is not None:
+        th.join(timeout)
+        return not th.is_alive()
+    return True
 
 
 def warmup(session) -> dict:
-    """Session-start warm-up: the preload (GPU) and, in ``eager`` mode, the listed
-    families' tiny fits.  Returns seconds per step run now."""
+    """Session-start warm-up: the preload (GPU), then the families -- synchronously
+    (``eager``) or on the background thread (``auto``).  Returns seconds per step run now."""
+    global _THREAD
     out: dict = {}
     mode, fams = plan(session.conf.get("o3s.session.warmup", "auto"))
     if mode == "off":
         return out
     _preload(session, out)                # GPU only
-    for fam in fams:                      # listed families: also on CPU (explicit request)
-        if fam not in _DONE:
-            _run_family(session, fam, out)
+    if mode == "eager":                   # listed families: also on CPU (explicit request)
+        for fam in fams:
+            if fam not in _DONE:
+                _run_family(session, fam, out)
+    elif mode == "background" and session.device.type == "cuda":
+        todo = [f for f in fams if f not in _DONE and f not in _FAILED]
+        if todo and (_THREAD is None or not _THREAD.is_alive()):
+            _THREAD = threading.Thread(target=_background, args=(session, todo), name="o3s-warmup", daemon=True)
+            _THREAD.start()
     return out
 
 
 def before_fit(family: str) -> None:
-    """Called by each family's fit entry: warms the family once per process (``lazy``
-    mode) with a tiny fit, so the cold cost lands on a few thousand rows instead of the
-    user's data.  No-op after the first call, on CPU, and when warm-up is off."""
-    if family in _DONE or family in _RUNNING or family in _FAILED:
+    """``lazy`` mode: warm ``family`` once per process with a tiny fit right before its
+    first real fit.  No-op in the other modes, after the first call and on CPU."""
+    if family in _DONE or family in _RUNNING or family in _FAILED or getattr(_TL, "warming", False):
         return
     from ..session import Session
     s = Session.active()
@@ -149,6 +285,4 @@ def before_fit(family: str) -> None:
     out = {}
     _preload(s, out)
     _run_family(s, family, out)
-    if out.get(family) is None:
-        _FAILED.add(family)
     s.warmup_seconds.update(out)

@@ -73,7 +73,14 @@ def _work(rank, world, port, out_dir):
     rr = g2.integers(1, 6, nr).astype(np.float32)
     lo, hi = (nr * rank) // world, (nr * (rank + 1)) // world
     dev = s.device
+    from orange3_spark_amd.parallel.comm import COMM_STATS
+    bc0 = COMM_STATS.get("broadcast", [0, 0])[0]
     for implicit in (True, False):
+        if not implicit:
+            # implicit exact fits keep the tables in the Gram eigenbasis: at world 2 every
+            # half-iteration's (eig, Q) comes from rank 0, so both ranks' rows
+            # live in one basis -- counted here, the equality below checks the result
+            res["eig_broadcasts"] = COMM_STATS.get("broadcast", [0, 0])[0] - bc0
         ex = fit_als(s.comm, torch.from_numpy(uu[lo:hi]).to(dev), torch.from_numpy(ii[lo:hi]).to(dev),
                      torch.from_numpy(rr[lo:hi]).to(dev), rank=32, max_iter=3, reg=0.05, implicit=implicit,
                      alpha=2.0, seed=3)
@@ -110,6 +117,7 @@ def test_gpu_world2_matches_world1(tmp_path):
     assert np.allclose(a["als_U"], b["als_U"], atol=1e-3)
     assert np.allclose(a["als_cg"], b["als_cg"], atol=1e-4)
     assert a["gather_calls"] == 0 and b["gather_calls"] == 2 * (1 + 2 * 3)
+    assert a["eig_broadcasts"] == 0 and b["eig_broadcasts"] >= 3        # one per user half-iteration
     for imp in (0, 1):
         for x, y in zip(a[f"als_exact_{imp}"], b[f"als_exact_{imp}"]):
             assert x.shape == y.shape

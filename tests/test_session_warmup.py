@@ -48,15 +48,97 @@ def test_false_disables(fresh):
     assert s.warmup_seconds == {}
 
 
-@pytest.mark.gpu
-def test_gpu_auto_preloads_then_warms_only_the_fitted_family(fresh, monkeypatch):
-    """auto: the session start only loads the kernel code objects (no fit); a family's
-    tiny warm-up fit runs right before its first real fit, once per process, and a
-    session that only fits LR never warms the other families."""
+def test_user_fits_and_background_warmup_never_overlap():
+    """The gate between user fits (shared, nested, any thread) and the background tiny
+    fit (exclusive): a user fit waits for the tiny fit in flight, and the warm-up waits
+    while any user fit runs."""
+    import threading
+    import time
+    g = W._Gate()
+    order = []
+    g.warm_enter()
+
+    def user():
+        g.user_enter()
+        order.append("user-in")
+        g.user_exit()
+    t = threading.Thread(target=user)
+    t.start()
+    time.sleep(0.05)
+    order.append("warm-out")
+    g.warm_exit()
+    t.join(5)
+    assert order == ["warm-out", "user-in"]
+    g.user_enter()
+    g.user_enter()                                    # nested fits (Pipeline stages)
+    got = []
+    w = threading.Thread(target=lambda: (g.warm_enter(), got.append("warm"), g.warm_exit()))
+    w.start()
+    time.sleep(0.05)
+    assert got == []
+    g.user_exit()
+    time.sleep(0.05)
+    assert got == []
+    g.user_exit()
+    w.join(5)
+    assert got == ["warm"]
+
+
+def test_lazy_and_preload_modes_parse():
+    assert W.plan("auto") == ("background", W.FAMILIES)
+    assert W.plan("lazy") == ("lazy", ()) and W.plan("preload") == ("preload", ())
+    assert W.plan("all") == ("eager", W.FAMILIES) and W.plan("false") == ("off", ())
+
+
+@pytest.fixture
+def fresh_gpu(fresh, monkeypatch):
     monkeypatch.setattr(W, "_PRELOADED", set())
+    monkeypatch.setattr(W, "_FAILED", set())
+    W.wait_background(120)
+    monkeypatch.setattr(W, "_THREAD", None)
+    yield
+    W.wait_background(120)
+
+
+@pytest.mark.gpu
+def test_gpu_auto_preloads_then_warms_in_the_background(fresh_gpu):
+    """auto: the session start only loads the kernel code objects (~40 ms, no fit); the
+    families warm on a background thread (private single-rank session, own stream), so
+    the first real fit of a family is a warm fit."""
+    import time
+    t = time.perf_counter()
     s = Session.getOrCreate(SessionConf())
+    start = time.perf_counter() - t
     assert s.device.type == "cuda"
-    assert set(s.warmup_seconds) == {"preload"} and s.warmup_seconds["preload"] < 1.0
+    assert "preload" in s.warmup_seconds and s.warmup_seconds["preload"] < 1.0 and start < 1.5
+    assert W.wait_background(120)
+    assert set(W.FAMILIES) <= set(s.warmup_seconds) and all(s.warmup_seconds[f] for f in W.FAMILIES)
+    from orange3_spark_amd.ml.classification import LogisticRegression
+    LogisticRegression(maxIter=3).fit(s.synthetic.classification(50_000, 32, seed=1))
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_gpu_user_fit_during_background_warmup(fresh_gpu):
+    """A fit issued right after the session start runs while the background warm-up is
+    still going: it waits for the tiny fit in flight, gives the same model as a fit with
+    the warm-up off, and its family is not warmed again afterwards."""
+    from orange3_spark_amd.ml.clustering import KMeans
+    s = Session.getOrCreate(SessionConf())
+    m1 = KMeans(k=8, maxIter=5, seed=3).fit(s.synthetic.blobs(200_000, 32, 8, seed=2))
+    assert "kmeans" in W._DONE
+    assert W.wait_background(120)
+    assert "kmeans" not in s.warmup_seconds or s.warmup_seconds["kmeans"] is not None
+    s.stop()
+    s2 = Session.getOrCreate(SessionConf().set("o3s.session.warmup", "false"))
+    m2 = KMeans(k=8, maxIter=5, seed=3).fit(s2.synthetic.blobs(200_000, 32, 8, seed=2))
+    assert m1.summary.trainingCost == pytest.approx(m2.summary.trainingCost, rel=1e-9)
+
+
+@pytest.mark.gpu
+def test_gpu_lazy_warms_only_the_fitted_family(fresh_gpu):
+    s = Session.getOrCreate(SessionConf().set("o3s.session.warmup", "lazy"))
+    assert set(s.warmup_seconds) == {"preload"}
     from orange3_spark_amd.ml.classification import LogisticRegression
     df = s.synthetic.classification(50_000, 32, seed=1)
     LogisticRegression(maxIter=3).fit(df)

@@ -7,6 +7,8 @@ and both fit times.  Modes:
   preload   -- only ``ops._native.preload()`` (load every kernel code object, no fits)
   family    -- the lazy per-family warm-up (``o3s.session.warmup=lazy``)
   fits      -- the tiny warm-up fits of the fitted family at session start (round 5)
+  auto      -- the default: preload, then every family warmed on a background thread
+               while the data is generated (no explicit wait)
 Run ``HIP_ENABLE_DEFERRED_LOADING=0`` around ``none`` to see how much of the cold cost is
 code-object loading at all (every fatbin of every library loaded at HIP init).
 """
@@ -23,14 +25,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="none", choices=("none", "preload", "family", "fits"))
+    ap.add_argument("--mode", default="none", choices=("none", "preload", "family", "fits", "auto"))
     ap.add_argument("--family", default="trees", choices=("trees", "glm", "kmeans", "als"))
     ap.add_argument("--rows", type=int, default=100_000_000)
     a = ap.parse_args()
     import torch
     t0 = time.perf_counter()
     from orange3_spark_amd import Session, SessionConf
-    warm = {"none": "false", "preload": "preload", "family": "lazy", "fits": a.family}[a.mode]
+    warm = {"none": "false", "preload": "preload", "family": "lazy", "fits": a.family, "auto": "auto"}[a.mode]
     s = Session.getOrCreate(SessionConf().set("spark.master", "local[1]").set("o3s.session.warmup", warm))
     torch.cuda.synchronize()
     t_session = time.perf_counter() - t0
