@@ -88,7 +88,20 @@ class SpilledVectorColumn(C.VectorColumn):
         return C.VectorColumn(out, self.size)
 
     def mask_select(self, mask):
-        return self.take(torch.nonzero(mask.to(self.data.device)).reshape(-1))
+        """Rows where ``mask`` holds, keeping the layout: the selected resident rows stay a
+        device prefix and the selected host rows a pinned host suffix (nothing of the
+        column's length is materialised on the device -- ``filter`` / handleInvalid
+        "skip" on an out-of-core frame)."""
+        nr = self.resident_rows
+        m = mask.reshape(-1)
+        res = self.data[m[:nr].to(self.data.device)]
+        hm = m[nr:].cpu()
+        host = self.host[hm]
+        if self.host.is_pinned() and not host.is_pinned() and host.numel():
+            host = host.pin_memory()
+        if host.shape[0] == 0:
+            return C.VectorColumn(res, self.size)
+        return SpilledVectorColumn(res, host, self.size)
 
     def slice(self, start, end):
         n = len(self)
@@ -243,16 +256,34 @@ def _fit_ld(t: torch.Tensor, ld: int, dt, size: int) -> torch.Tensor:
     return out
 
 
-def map_blocks(col: "SpilledVectorColumn", fn, chunk_bytes: int | None = None) -> "SpilledVectorColumn":
-    """A row-wise map over an out-of-core vector column into a NEW spilled column with the
-    same resident / host split (feature transformers on frames larger than HBM).  ``fn``:
-    fp64 rows [m, size] -> fp64 rows [m, size]; the output keeps the column's dtype and
-    padding.  Resident rows are mapped in bounded chunks (no fp64 copy of the whole
-    prefix); host rows stream through the device and are written back to pinned memory
-    asynchronously on the consumer stream."""
+def map_blocks(col: "SpilledVectorColumn", fn, chunk_bytes: int | None = None,
+               budget: int | None = None) -> "SpilledVectorColumn":
+    """A row-wise map over an out-of-core vector column into a NEW spilled column
+    (feature transformers on frames larger than HBM).  ``fn``: fp64 rows [m, size] ->
+    fp64 rows [m, size].  Resident rows are mapped in bounded chunks (no fp64 copy of the
+    whole prefix); host rows stream through the device and are written back to pinned
+    memory asynchronously on the consumer stream.
+
+    Output storage: the column's own dtype and padding (bf16 on the GPU).  An out-of-core
+    table is by definition larger than HBM, so its derived columns stay in the compact
+    storage dtype -- fp64 (what a resident transform returns, as Spark's double vectors)
+    would take 4x the HBM and pinned host bytes; the map itself is computed in fp64.
+
+    Output split: the input's resident prefix already holds its share of HBM, so the
+    output's device prefix takes at most ``budget`` bytes (default: what the device can
+    allocate now, less working room for the fp64 chunks, times ``o3s.memory.fraction``);
+    rows beyond it go to the pinned host part like the streamed ones."""
     dt, ld, D, dev = col.data.dtype, col.ld, col.size, col.data.device
     cuda = dev.type == "cuda"
     step = max(1, int(chunk_bytes or CHUNK_BYTES) // max(1, ld * 8))
+    row_bytes = ld * col.data.element_size()
+    if budget is None and cuda:
+        from ..session import Session
+        s = Session.active()
+        frac = s.conf.memory_fraction() if s is not None else 0.85
+        work = 4 * step * ld * 8 + (256 << 20)       # fp64 chunk, its map, the cast, slack
+        budget = int(max(0, device_free_bytes(dev) - work) * frac)
+    keep = col.resident_rows if budget is None else min(col.resident_rows, max(0, int(budget) // max(1, row_bytes)))
 
     def apply(X):
         y = fn(X[:, :D].to(torch.float64))
@@ -264,16 +295,22 @@ def map_blocks(col: "SpilledVectorColumn", fn, chunk_bytes: int | None = None) -
         out[:, :D] = y.to(dt)
         return out
 
-    res = torch.empty((col.resident_rows, ld), dtype=dt, device=dev)
+    res = torch.empty((keep, ld), dtype=dt, device=dev)
+    spill = col.resident_rows - keep                # input-resident rows whose output goes to the host
+    host = torch.empty((spill + col.spilled_rows, ld), dtype=dt, pin_memory=cuda and torch.cuda.is_available())
     for a in range(0, col.resident_rows, step):
         b = min(col.resident_rows, a + step)
-        res[a:b] = apply(col.data[a:b])
-    host = torch.empty((col.spilled_rows, ld), dtype=dt, pin_memory=cuda and torch.cuda.is_available())
+        y = apply(col.data[a:b])
+        r = max(0, min(b, keep) - a)
+        if r:
+            res[a:a + r] = y[:r]
+        if b - a - r:
+            host[a + r - keep:b - keep].copy_(y[r:], non_blocking=cuda)
 
     def sink(X, off):
         for a in range(0, X.shape[0], step):
             b = min(X.shape[0], a + step)
-            host[off + a:off + b].copy_(apply(X[a:b]), non_blocking=cuda)
+            host[spill + off + a:spill + off + b].copy_(apply(X[a:b]), non_blocking=cuda)
     col.streamer(chunk_bytes).run(sink)
     if cuda:
         torch.cuda.synchronize(dev)
@@ -438,7 +475,8 @@ def spill_to_budget(df, budget: int | None = None, disk_only: bool = False) -> i
     return moved
 
 
-def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes: int | None = None):
+def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes: int | None = None,
+                      want_bad: bool = False):
     """VectorAssembler over host-resident (and/or device) columns, in row chunks.
 
     ``sources``: list of (tensor [n] or [n, w], valid [n] | None, width) -- host tensors
@@ -448,7 +486,8 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
     on the current stream once its copy event fired; rows beyond the budget go back to the
     pinned host block on a third stream (H2D and D2H overlap on the full-duplex link); the
     invalid-row count stays on the device until the end.  CPU: torch, chunk by chunk.
-    Returns (SpilledVectorColumn | VectorColumn, invalid count)."""
+    Returns (SpilledVectorColumn | VectorColumn, invalid count), plus the per-row invalid
+    flags (bool [n] on the device) when ``want_bad`` (handleInvalid "skip")."""
     from ..ops import assemble as A
     from ..ops.glm import padded_width
     dev = session.device
@@ -466,17 +505,20 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
     host = torch.empty((n - keep, ld), dtype=vdt, pin_memory=cuda and torch.cuda.is_available())
     _t_alloc = _time.perf_counter() - _t0
     bounds = [(a, min(n, a + rows)) for a in range(0, n, rows)]
+    bad_all = torch.zeros(n, dtype=torch.bool, device=dev) if want_bad else None
     if not cuda:
         nbad = 0
         for a, b in bounds:
             out, nb = _assemble_chunk_torch([(t[a:b], None if v is None else v[a:b], w) for t, v, w in sources],
                                             b - a, D, ld, vdt)
             nbad += nb
+            if want_bad and nb:
+                bad_all[a:b] = torch.isnan(out[:, :D].float()).any(1)
             r = max(0, min(b, keep) - a)
             res[a:a + r] = out[:r]
             host[a + r - keep:b - keep] = out[r:]
         col = SpilledVectorColumn(res, host, D) if n > keep else C.VectorColumn(res, D)
-        return col, nbad
+        return (col, nbad, bad_all) if want_bad else (col, nbad)
     copy, d2h = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     main = torch.cuda.current_stream(dev)
     # two pinned staging sets for the host-side sources (pageable -> pinned on the CPU)
@@ -534,11 +576,15 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
                 v.record_stream(main)
         m = b - a
         if vdt == torch.bfloat16 and all(A.supported(t) for t, _, _ in cur):
-            out, _, nb, _ = A.assemble_bf16(cur, m, dev)
+            out, badf, nb, _ = A.assemble_bf16(cur, m, dev)
             nbad_d += nb.to(torch.int64)
+            if want_bad:
+                bad_all[a:b] = badf.bool()
         else:
             out, nb = _assemble_chunk_torch(cur, m, D, ld, vdt)
             nbad_d += nb
+            if want_bad:
+                bad_all[a:b] = torch.isnan(out[:, :D].float()).any(1)
         r = max(0, min(b, keep) - a)
         if r:
             res[a:a + r].copy_(out[:r])
@@ -552,7 +598,7 @@ def assemble_streamed(sources, n: int, session, budget: int | None, chunk_bytes:
     torch.cuda.synchronize(dev)
     LAST_ASSEMBLE_STATS["final_sync_s"] = _time.perf_counter() - t2
     col = SpilledVectorColumn(res, host, D) if n > keep else C.VectorColumn(res, D)
-    return col, int(nbad_d.item())
+    return (col, int(nbad_d.item()), bad_all) if want_bad else (col, int(nbad_d.item()))
 
 
 _COPY_POOL = None

@@ -200,15 +200,15 @@ class VectorAssembler(Transformer, HasInputCols, HasOutputCol, HasHandleInvalid,
         if not host_in and not too_big:
             return None
         _ = LineageVectorColumn
-        out, nbad = spill.assemble_streamed(srcs, n, df.session, budget)
+        hi = self.getOrDefault(self.handleInvalid)
+        got = spill.assemble_streamed(srcs, n, df.session, budget, want_bad=hi == "skip")
+        out, nbad = got[0], got[1]
         if nbad:
-            hi = self.getOrDefault(self.handleInvalid)
             if hi == "error":
                 raise ValueError("Encountered null while assembling a row with handleInvalid = \"error\". "
                                  "Consider removing nulls from dataset or using handleInvalid = \"keep\" or \"skip\".")
-            if hi == "skip":
-                raise ValueError("handleInvalid = \"skip\" needs the table in device memory; the assembled rows "
-                                 "exceed the HBM budget (o3s.storage.hbmBudget) -- use fillna / dropna first")
+            if hi == "skip":             # drop the flagged rows from every column, layout kept
+                return df.withColumnData(self.getOrDefault(self.outputCol), out)._mask(~got[2])
         return df.withColumnData(self.getOrDefault(self.outputCol), out)
 
     def _transform_fused(self, df, cols, n):

@@ -370,6 +370,19 @@ def fit_als(comm, users: torch.Tensor, items: torch.Tensor, ratings: torch.Tenso
             max_iter: int = 10, reg: float = 0.1, implicit: bool = False, alpha: float = 1.0, seed: int = 0,
             nonneg: bool = False, cg_iters: int = 0, exact: bool | None = None, keep_full: bool = True,
             ckpt=None) -> AlsResult:
+    try:
+        return _fit_als(comm, users, items, ratings, rank, max_iter, reg, implicit, alpha, seed, nonneg, cg_iters,
+                        exact, keep_full, ckpt)
+    finally:
+        # also when the fit stops early (FitCancelled from a progress report, a device
+        # error): the rotated factor table and the padded copy are as large as a factor
+        # table and must not outlive the fit
+        A.EIG_CACHE.clear()
+        A.PAD_CACHE.clear()
+
+
+def _fit_als(comm, users, items, ratings, rank, max_iter, reg, implicit, alpha, seed, nonneg, cg_iters, exact,
+             keep_full, ckpt) -> AlsResult:
     t0 = time.time()
     dev = ratings.device
     with trace("als.setup.ids"):

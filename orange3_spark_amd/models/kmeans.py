@@ -348,6 +348,15 @@ def fit_kmeans(comm, X, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int
         if weights is not None:
             raise ValueError("weighted KMeans over host-streamed rows is not supported; persist with MEMORY_ONLY")
         return _fit_kmeans_blocks(comm, X, k, max_iter, tol, seed, init, init_steps, initial, cosine, ckpt)
+    try:
+        return _fit_kmeans_rows(comm, X, k, max_iter, tol, seed, init, init_steps, initial, weights, cosine, ckpt)
+    finally:
+        # also when the fit stops early (FitCancelled from a progress report, a device
+        # error): the split copy of X is as large as X and must not outlive the fit
+        K.clear_presplit()
+
+
+def _fit_kmeans_rows(comm, X, k, max_iter, tol, seed, init, init_steps, initial, weights, cosine, ckpt):
     t0 = time.time()
     if cosine:
         X = X / X.norm(dim=1, keepdim=True).clamp_min(1e-300)
@@ -419,7 +428,6 @@ def fit_kmeans(comm, X, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int
     cnt = torch.bincount(a.long(), minlength=k)[:k].to(torch.float64)
     buf = torch.cat([cnt, d.to(torch.float64).sum().reshape(1)])
     comm.all_reduce(buf)
-    K.clear_presplit()                   # the split copy of X (as large as X) is not kept past the fit
     return KMeansResult(C.cpu(), float(buf[-1]), it, [int(x) for x in buf[:k].tolist()], hist, time.time() - t0)
 
 

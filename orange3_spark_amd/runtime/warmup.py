@@ -24,10 +24,11 @@ Conf ``o3s.session.warmup``:
   session start, synchronously (plus the preload on GPU);
 * ``false`` -- nothing.
 
-A background tiny fit never overlaps a user fit: user fits wait for the tiny fit in
-flight (at most one, ~0.05-0.3 s) and the warm-up thread waits while any user fit runs
-(:func:`user_fit`), so the engine's per-family module caches are never shared between
-the two.  The warm-up thread's kernels, collectives and phases are invisible to fault
+A background tiny fit never overlaps a user fit: a user fit that arrives while one runs
+preempts it (the tiny fit stops at its next iteration through the progress / cancel
+hook, ``runtime/progress.py``, and is retried later), and the warm-up thread waits while
+any user fit runs (:func:`user_fit`), so the engine's per-family module caches are never
+shared between the two and a user fit waits at most one tiny-fit iteration.  The warm-up thread's kernels, collectives and phases are invisible to fault
 injection, ``COMM_STATS`` and the trace.  ``Session.warmup_seconds`` reports the time per
 step (background steps appear when they finish)."""
 from __future__ import annotations
@@ -98,12 +99,18 @@ class _Gate:
     def __init__(self):
         self.cond = threading.Condition()
         self.users = 0
+        self.waiting = 0                 # user fits blocked on a warm-up (it yields to them)
         self.warming = False
 
     def user_enter(self):
         with self.cond:
-            while self.warming:
-                self.cond.wait()
+            if self.warming:
+                self.waiting += 1
+                try:
+                    while self.warming:
+                        self.cond.wait()
+                finally:
+                    self.waiting -= 1
             self.users += 1
 
     def user_exit(self):
@@ -158,7 +165,10 @@ def _preload(session, out: dict) -> None:
     out["preload"] = round(time.perf_counter() - t, 4)
 
 
-def _run_family(session, fam: str, out: dict, quiet: bool = False) -> None:
+def _run_family(session, fam: str, out: dict, quiet: bool = False) -> bool:
+    """One family's tiny fit.  ``quiet`` (the background thread): invisible to fault
+    injection / counters, and it YIELDS to user fits -- a user fit that starts while it
+    runs makes it stop at its next iteration (FitCancelled); returns False then."""
     from . import faults, progress
     from .tracing import TRACER, suppressed
     was = TRACER.enabled                 # the warm-up fits stay out of the user's trace
@@ -167,19 +177,28 @@ def _run_family(session, fam: str, out: dict, quiet: bool = False) -> None:
     _RUNNING.add(fam)
     _TL.warming = True
     t = time.perf_counter()
+    scope = (progress.progress_scope(lambda _p: None, lambda: GATE.waiting > 0) if quiet
+             else progress.detached())
     try:
-        with progress.detached(), suppressed(), (faults.quiet() if quiet else contextlib.nullcontext()):
+        with scope, suppressed(), (faults.quiet() if quiet else contextlib.nullcontext()):
             _FIT[fam](session)
             if session.device.type == "cuda":
                 import torch
                 torch.cuda.current_stream(session.device).synchronize()
         out[fam] = round(time.perf_counter() - t, 4)
         _DONE.add(fam)
+        return True
+    except progress.FitCancelled:        # preempted by a user fit: retried later
+        if session.device.type == "cuda":
+            import torch
+            torch.cuda.current_stream(session.device).synchronize()
+        return False
     except Exception as e:               # a warm-up failure must not stop the session or fit
         warnings.warn(f"o3s.session.warmup: the {fam} warm-up fit failed ({type(e).__name__}: {e}); "
                       "its first real fit pays the one-time costs instead", RuntimeWarning)
         out[fam] = None
         _FAILED.add(fam)
+        return True
     finally:
         _TL.warming = False
         _RUNNING.discard(fam)
@@ -225,7 +244,10 @@ def _background(session, fams) -> None:
     except Exception as e:  # noqa: BLE001
         warnings.warn(f"o3s.session.warmup: background warm-up not started ({e})", RuntimeWarning)
         return
-    for fam in fams:
+    queue = list(fams)
+    retries = {f: 2 for f in fams}
+    while queue:
+        fam = queue.pop(0)
         if fam in _DONE or fam in _FAILED or _STOP.is_set():
             continue
         GATE.warm_enter()
@@ -234,8 +256,11 @@ def _background(session, fams) -> None:
                 continue
             out: dict = {}
             with torch.cuda.stream(stream):
-                _run_family(priv, fam, out, quiet=True)
+                finished = _run_family(priv, fam, out, quiet=True)
             session.warmup_seconds.update(out)
+            if not finished and retries[fam] > 0:   # preempted: try again after the others
+                retries[fam] -= 1
+                queue.append(fam)
         finally:
             GATE.warm_exit()
 

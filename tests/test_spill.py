@@ -275,6 +275,56 @@ def test_scalers_and_union_on_spilled_rows_match_resident(tmp_path):
     assert u.count() == 6000
 
 
+def _write_parquet_with_nulls(tmp_path, n=3000, d=5, seed=1):
+    rng = np.random.default_rng(seed)
+    pdf = pd.DataFrame(rng.normal(size=(n, d)), columns=[f"f{i}" for i in range(d)])
+    for i in range(d):                        # ~4% of rows get a null somewhere, on both sides of the split
+        pdf.loc[rng.random(n) < 0.01, f"f{i}"] = np.nan
+    pdf["label"] = (rng.random(n) > 0.5).astype(float)
+    path = str(tmp_path / "nulls.parquet")
+    pdf.to_parquet(path)
+    return path, [f"f{i}" for i in range(d)], pdf
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_out_of_core_assembly_skips_invalid_rows_like_resident(tmp_path, device):
+    """handleInvalid="skip" on a table beyond the HBM budget (it raised before,
+    so behaviour depended on the table's size): the flagged rows are dropped from every
+    column, the output keeps the resident-prefix + host layout, and the rows equal the
+    resident run's."""
+    path, names, pdf = _write_parquet_with_nulls(tmp_path)
+    from orange3_spark_amd.ops.glm import padded_width
+    row = padded_width(len(names)) * 2 if device == "cuda" else len(names) * 8
+    s = _session(device, budget=1000 * row)
+    va = VectorAssembler(inputCols=names, outputCol="features", handleInvalid="skip")
+    out = va.transform(s.read.parquet(path))
+    col = out.column_data("features")
+    assert isinstance(col, SpilledVectorColumn) and col.resident_rows < 1000 and col.spilled_rows > 0
+    ref = va.transform(_session(device).read.parquet(path))
+    keep = ~pdf[names].isna().any(axis=1).to_numpy()
+    assert out.count() == ref.count() == int(keep.sum()) < len(pdf)
+    assert np.array_equal(col.to_numpy(), ref.column_data("features").to_numpy())
+    assert np.array_equal(out.select("label").toPandas()["label"].to_numpy(), pdf["label"].to_numpy()[keep])
+
+
+def test_map_blocks_output_prefix_respects_the_budget(tmp_path):
+    """a map over an out-of-core column must not allocate a second device
+    prefix as large as the input's; with a budget below the input's resident prefix, the
+    output's extra rows go to the host part, in row order, with the same values."""
+    from orange3_spark_amd.frame.spill import map_blocks
+    path, names = _write_parquet(tmp_path)
+    s = _session(budget=1000 * 7 * 8)
+    col = VectorAssembler(inputCols=names, outputCol="features").transform(s.read.parquet(path)).column_data("features")
+    assert isinstance(col, SpilledVectorColumn) and col.resident_rows == 1000
+    row_bytes = col.ld * col.data.element_size()
+    full = map_blocks(col, lambda x: 2.0 * x + 1.0)
+    part = map_blocks(col, lambda x: 2.0 * x + 1.0, chunk_bytes=300 * 8 * col.ld, budget=300 * row_bytes)
+    assert full.resident_rows == 1000 and part.resident_rows == 300 and len(part) == len(col) == 3000
+    assert part.spilled_rows == 2700
+    assert np.array_equal(part.to_numpy(), full.to_numpy())
+    assert np.allclose(full.to_numpy(), 2.0 * col.to_numpy() + 1.0)
+
+
 @pytest.mark.gpu
 def test_gpu_scalers_and_union_on_spilled_rows(tmp_path):
     """GPU: StandardScaler fit/transform and union over a host-resident parquet table
