@@ -51,7 +51,7 @@ DEFAULTS = OrderedDict([
     ("o3s.memory.fraction", "0.85"),
     ("o3s.seed", "42"),
     ("o3s.trace", "false"),                 # runtime/tracing.py phase tracer + roctx ranges
-    ("o3s.session.warmup", "auto"),         # runtime/warmup.py: tiny fits at session start (GPU, one rank)
+    ("o3s.session.warmup", "auto"),         # runtime/warmup.py: kernel preload; pool workers warm every family
     ("o3s.checkpoint.interval", "0"),       # iterations between checkpoints (needs spark.checkpoint.dir)
     # o3s.comm.timeout (unset): seconds before a hung collective raises -- 1800 for SPMD
     # launches (benchmarks), o3s.executor.commTimeout (120) inside an executor pool

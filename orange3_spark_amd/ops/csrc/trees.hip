@@ -893,7 +893,178 @@ __global__ __launch_bounds__(256) void forest_weights_kernel(const int64_t* __re
   out[(int64_t)t * n + i] = w ? w[i] * v : v;
 }
 
+// ---------------------------------------------------------------------------------
+// GBT tree epilogue, fused (replaces the last level's routing pass, every level's
+// leaf_apply scatter and the boosting step's gbt_grad_loss pass): ONE sequential pass
+// over the rows in ROW order.  Each row walks the finished tree on its row-major bins
+// (a wave stages its 64 consecutive rows -- 64 x F bytes, coalesced -- in LDS and reads
+// the split features from there), then
+//   * Fm[i] += value(leaf)            (leaf values pre-scaled by the tree weight),
+//   * the loss of the updated Fm       (partials [sum l*wd, sum wd, sum l*wv, sum wv]),
+//   * target[i] = next tree's residual (fp32, may be null),
+//   * (REG) sum of w*y^2 of the leaves at depth D -- the children the last split level
+//     created, whose w and w*y came from their parent's histogram -- with y the residual
+//     this tree was fit to, recomputed from (yy, Fm before the update) exactly as the
+//     previous pass wrote it (first tree: y = yy).
+// The old path gathered every row twice at random (feature-major byte + an fp64
+// read-modify-write of acc[order[p]]); this one streams bins / yy / Fm once.
+// Per-leaf sums are deterministic: per wave, one fixed-order wave reduction per distinct
+// leaf present in the wave's 64 rows, into the wave's own LDS array; blocks combine
+// waves in a fixed order and write one fp32 slab row each (summed in fp64, fixed order).
+constexpr int kLeafThreads = 256;
+constexpr int kLeafWaves = kLeafThreads / kWave;
+
+__device__ __forceinline__ void gbt_point(int loss, double yi, double fi, double& l, double& g) {
+  if (loss == 0) {
+    const double z = -2.0 * yi * fi;
+    const double e = exp(-fabs(z));
+    l = 2.0 * (fmax(z, 0.0) + log1p(e));
+    g = 4.0 * yi * (z >= 0.0 ? 1.0 / (1.0 + e) : e / (1.0 + e));
+  } else if (loss == 1) {
+    const double d = yi - fi;
+    l = d * d;
+    g = 2.0 * d;
+  } else {
+    const double d = yi - fi;
+    l = fabs(d);
+    g = (double)((d > 0.0) - (d < 0.0));
+  }
+}
+
+template <bool STAGE>
+__global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
+    const uint8_t* __restrict__ bins, int64_t n, int F, int Fs, const int32_t* __restrict__ node_fb, int nodes,
+    const double* __restrict__ node_val, int D, const double* __restrict__ yy, double* __restrict__ Fm,
+    const float* __restrict__ wt, const double* __restrict__ wd, const double* __restrict__ wv, int loss,
+    int first, float* __restrict__ target, double* __restrict__ partial, float* __restrict__ y2slab, int L) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  int32_t* tree = reinterpret_cast<int32_t*>(lds);                         // [nodes]
+  float* y2w = reinterpret_cast<float*>(lds + 4 * nodes);                  // [waves][L]
+  uint8_t* stage = lds + 4 * nodes + 4 * kLeafWaves * L;                   // [waves][64][Fs]
+  __shared__ double red[4][kLeafWaves];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < nodes; i += kLeafThreads) tree[i] = node_fb[i];
+  for (int i = threadIdx.x; i < kLeafWaves * L; i += kLeafThreads) y2w[i] = 0.f;
+  __syncthreads();
+  float* my_y2 = y2w + wid * L;
+  uint8_t* my_stage = stage + wid * 64 * Fs;
+  const int leaf0 = 1 << D;                                                // first node id at depth D
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  const int64_t nchunks = (n + 63) / 64;
+  const int64_t wstride = (int64_t)gridDim.x * kLeafWaves;
+  for (int64_t c = (int64_t)blockIdx.x * kLeafWaves + wid; c < nchunks; c += wstride) {
+    const int64_t r0 = c * 64;
+    const int rows = n - r0 < 64 ? (int)(n - r0) : 64;
+    const int64_t i = r0 + (lane < rows ? lane : rows - 1);
+    const bool ok = lane < rows;
+    if constexpr (STAGE) {
+      // the wave's rows are one contiguous run of rows * F bytes: 4-byte coalesced reads
+      // (F % 4 == 0) into rows of Fs bytes (Fs / 4 odd: lanes' rows on distinct banks)
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(bins + r0 * F);
+      const int wpr = F >> 2, wtot = rows * wpr;
+      for (int e = lane; e < wtot; e += 64) {
+        const int rr = e / wpr, q = e - rr * wpr;
+        *reinterpret_cast<uint32_t*>(my_stage + rr * Fs + 4 * q) = src[e];
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    int node = 1;
+    for (int d = 0; d < D; ++d) {
+      const int32_t fb = node < nodes ? tree[node] : -1;
+      if (fb < 0) break;                                                   // a leaf (lane-divergent)
+      const int f = fb & 0xffff, sb = (fb >> 16) & 0x7fff;
+      const int b = STAGE ? (int)my_stage[lane * Fs + f] : (int)bins[i * F + f];
+      node = 2 * node + (b > sb ? 1 : 0);
+    }
+    const double yi = yy[i], fo = Fm[i];
+    const double fn = fo + node_val[node];
+    double l, g;
+    gbt_point(loss, yi, fn, l, g);
+    if (ok) {
+      Fm[i] = fn;
+      if (target) target[i] = (float)g;
+      const double wi = wd ? wd[i] : 1.0;
+      s0 += l * wi;
+      s1 += wi;
+      if (wv) {
+        const double vi = wv[i];
+        s2 += l * vi;
+        s3 += vi;
+      }
+    }
+    if (y2slab) {
+      // the residual this tree was fit to (fp32, as the previous pass wrote it)
+      float yo;
+      if (first) {
+        yo = (float)yi;
+      } else {
+        double lo_, go_;
+        gbt_point(loss, yi, fo, lo_, go_);
+        yo = (float)go_;
+      }
+      const float ww = wt ? wt[i] : 1.f;
+      const float v = ok ? ww * yo * yo : 0.f;
+      int key = (ok && node >= leaf0) ? node - leaf0 : -1;
+      // one fixed-order wave sum per distinct leaf among the wave's rows
+      uint64_t pend = __ballot(key >= 0);
+      while (pend) {
+        const int src = __builtin_ctzll(pend);
+        const int kk = __builtin_amdgcn_readlane(key, src);
+        const bool mine = key == kk;
+        const float sum = wave_sum(mine ? v : 0.f);
+        if (lane == 0) my_y2[kk] += sum;
+        pend &= ~__ballot(mine);
+      }
+    }
+    if constexpr (STAGE) __builtin_amdgcn_wave_barrier();                  // the stage is rewritten next chunk
+  }
+  s0 = wave_sum_d(s0); s1 = wave_sum_d(s1); s2 = wave_sum_d(s2); s3 = wave_sum_d(s3);
+  if (lane == 0) { red[0][wid] = s0; red[1][wid] = s1; red[2][wid] = s2; red[3][wid] = s3; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double a = 0.0;
+    for (int q = 0; q < kLeafWaves; ++q) a += red[threadIdx.x][q];
+    partial[(int64_t)blockIdx.x * 4 + threadIdx.x] = a;
+  }
+  if (y2slab) {
+    for (int k = threadIdx.x; k < L; k += kLeafThreads) {
+      float a = 0.f;
+      for (int q = 0; q < kLeafWaves; ++q) a += y2w[q * L + k];
+      y2slab[(int64_t)blockIdx.x * L + k] = a;
+    }
+  }
+}
+
 }  // namespace
+
+// Fused GBT tree epilogue (gbt_leaf_pass_kernel).  bins: [n][F] uint8; node_fb: int32
+// [nodes] heap-ordered (root 1): feature | split bin << 16 for internal nodes, -1 for
+// leaves / absent; node_val: fp64 [nodes] leaf value * tree weight; D: the tree's max
+// depth (leaves at depth D own y2slab columns node - 2^D, L = 2^D).  yy / Fm / wd / wv
+// fp64 [n] (wd, wv nullable), wt fp32 [n] (nullable), target fp32 [n] (nullable).
+// partial: fp64 [grid][4]; y2slab: fp32 [grid][L] or null (no y^2 sums).
+O3S_API int o3s_gbt_leaf_pass(const uint8_t* bins, int64_t n, int F, const int32_t* node_fb, int nodes,
+                              const double* node_val, int D, const double* yy, double* Fm, const float* wt,
+                              const double* wd, const double* wv, int loss, int first, float* target,
+                              double* partial, float* y2slab, int grid, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (F <= 0 || F > 0xffff || nodes <= 1 || D < 0 || D > 14 || loss < 0 || loss > 2 || grid <= 0) return -1;
+  const int L = y2slab ? (1 << D) : 0;
+  const bool stage = (F % 4) == 0 && F <= 256;
+  const int Fs = stage ? ((F / 4) % 2 == 0 ? F + 4 : F) : 0;
+  const size_t lds = 4 * (size_t)nodes + 4 * (size_t)kLeafWaves * L + (size_t)kLeafWaves * 64 * Fs;
+  if (lds > 64 * 1024) return -2;
+  if (stage)
+    hipLaunchKernelGGL((gbt_leaf_pass_kernel<true>), dim3(grid), dim3(kLeafThreads), lds, st, bins, n, F, Fs, node_fb,
+                       nodes, node_val, D, yy, Fm, wt, wd, wv, loss, first, target, partial, y2slab, L);
+  else
+    hipLaunchKernelGGL((gbt_leaf_pass_kernel<false>), dim3(grid), dim3(kLeafThreads), lds, st, bins, n, F, Fs,
+                       node_fb, nodes, node_val, D, yy, Fm, wt, wd, wv, loss, first, target, partial, y2slab, L);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
 
 // acc[order[p]] += it_val[i] for p in [it_lo[i], it_hi[i]) (items of leaf segments).
 O3S_API int o3s_tree_leaf_apply(const int32_t* order, const int64_t* it_lo, const int64_t* it_hi,

@@ -243,7 +243,7 @@ def _worker_main(rank: int, world: int, port: int, conf_pairs, conn, use_gpu: bo
             conf.set("o3s.device", "cpu")
         s = Session(conf)
         Session._active = s
-        s._warmup()                           # every rank in lock step (runtime/warmup.py)
+        s._warmup(pool_worker=True)           # every family, before the first fit (runtime/warmup.py)
     except BaseException:  # noqa: BLE001 - reported to the driver
         conn.send_bytes(pickle.dumps(("error", rank, traceback.format_exc())))
         return

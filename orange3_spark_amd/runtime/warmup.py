@@ -7,30 +7,30 @@ each op (``index_select`` alone 133 ms, ``max`` / ``sum`` / ``zeros_like`` / ``s
 ``cumsum`` 8-23 ms each); this framework's own 13 fatbins load in 37 ms.  The reference's
 estimators run on a JVM whose executors are already started and JIT-warm when the Orange
 canvas fits its first model (``orangecontrib/spark/base/spark_ml_estimator.py:22``, the
-cluster started at ``widgets/data/spark_context.py:76``); here the session does the
-equivalent without making anyone wait for it.
+cluster started at ``widgets/data/spark_context.py:76``).
 
 Conf ``o3s.session.warmup``:
 
 * ``auto`` (default) -- GPU sessions preload this framework's kernel code objects
-  (synchronous, ~40 ms, no launch) and then warm the estimator families in a **background
-  thread**: one tiny fit per family, on a private single-rank session (no collective, so
-  SPMD ranks and executor-pool workers do it too) on its own HIP stream, while the caller
-  goes on loading data.  Session start pays only the preload; a family whose first real
-  fit arrives before its warm-up finished simply pays its own cold cost;
+  (~40 ms, no launch).  Executor-pool workers (the multi-GPU canvas) additionally warm
+  every family at pool start (``all``, on a private single-rank session: no collective);
+  the Context widget asks for ``all`` too, from its worker thread -- the canvas's first
+  fit is then warm.  A plain script pays a family's cold cost in its first fit instead of
+  tiny fits of families it may never use;
+* ``true`` / ``all`` or a comma list of :data:`FAMILIES` -- preload plus tiny fits of
+  those families at session start, synchronously;
 * ``lazy`` -- preload, then each family's tiny fit right before its first real fit;
-* ``preload`` -- the code objects only;
-* ``true`` / ``all`` or a comma list of :data:`FAMILIES` -- tiny fits of those families at
-  session start, synchronously (plus the preload on GPU);
-* ``false`` -- nothing.
+* ``background`` -- preload, then the families' tiny fits on a background thread
+  (private single-rank session, own HIP stream).  A user fit preempts the tiny fit in
+  flight at its next iteration (progress / cancel hook) and the warm-up waits while user
+  fits run (:func:`user_fit`), so module caches are never shared.  Measured: it only
+  pays when the first fit comes > ~1.5 s after the session start (code-object loading
+  in the background thread still delays the main thread's launches), hence opt-in;
+* ``preload`` -- the code objects only;  ``false`` -- nothing.
 
-A background tiny fit never overlaps a user fit: a user fit that arrives while one runs
-preempts it (the tiny fit stops at its next iteration through the progress / cancel
-hook, ``runtime/progress.py``, and is retried later), and the warm-up thread waits while
-any user fit runs (:func:`user_fit`), so the engine's per-family module caches are never
-shared between the two and a user fit waits at most one tiny-fit iteration.  The warm-up thread's kernels, collectives and phases are invisible to fault
-injection, ``COMM_STATS`` and the trace.  ``Session.warmup_seconds`` reports the time per
-step (background steps appear when they finish)."""
+Warm-up kernels, collectives and phases of a background or private-session fit are
+invisible to fault injection, ``COMM_STATS`` and the trace.  ``Session.warmup_seconds``
+reports the time per step."""
 from __future__ import annotations
 
 import contextlib
@@ -52,19 +52,19 @@ def plan(value) -> tuple:
     v = str(value if value is not None else "auto").strip().lower()
     if v in ("false", "0", "no", "off", "none", ""):
         return ("off", ())
-    if v == "auto":
+    if v in ("auto", "preload"):
+        return ("preload", ())
+    if v == "background":
         return ("background", FAMILIES)
     if v == "lazy":
         return ("lazy", ())
-    if v == "preload":
-        return ("preload", ())
     if v in ("true", "1", "yes", "on", "all"):
         return ("eager", FAMILIES)
     fams = tuple(f.strip() for f in v.split(",") if f.strip())
     bad = [f for f in fams if f not in FAMILIES]
     if bad:
         raise ValueError(f"o3s.session.warmup: unknown value or families {bad} "
-                         f"(auto, lazy, preload, true, false, or a list of {', '.join(FAMILIES)})")
+                         f"(auto, true, lazy, background, preload, false, or a list of {', '.join(FAMILIES)})")
     return ("eager", fams)
 
 
@@ -215,7 +215,8 @@ def _private_session(session):
     class _QuietComm(LocalComm):
         all_reduce = LocalComm.all_reduce.__wrapped__
 
-    conf = session.conf.copy().set("o3s.session.warmup", "false").set("o3s.trace", "false")
+    conf = (session.conf.copy().set("o3s.session.warmup", "false").set("o3s.trace", "false")
+            .set("spark.master", "local[1]").set("spark.executor.instances", "1"))
     return Session(conf, comm=_QuietComm(session.device), device=session.device)
 
 
@@ -274,19 +275,28 @@ def wait_background(timeout: float | None = None) -> bool:
     return True
 
 
-def warmup(session) -> dict:
+def warmup(session, pool_worker: bool = False) -> dict:
     """Session-start warm-up: the preload (GPU), then the families -- synchronously
-    (``eager``) or on the background thread (``auto``).  Returns seconds per step run now."""
+    (``eager``; every family for an executor-pool worker in ``auto`` mode) or on the
+    background thread.  Returns seconds per step run now."""
     global _THREAD
     out: dict = {}
-    mode, fams = plan(session.conf.get("o3s.session.warmup", "auto"))
+    value = session.conf.get("o3s.session.warmup", "auto")
+    mode, fams = plan(value)
+    if pool_worker and str(value).strip().lower() == "auto" and session.device.type == "cuda":
+        mode, fams = "eager", FAMILIES    # the canvas's executors: warm before the first fit
     if mode == "off":
         return out
     _preload(session, out)                # GPU only
+    if mode == "eager" and session.device.type != "cuda" and str(value).strip().lower() in (
+            "true", "1", "yes", "on", "all"):
+        return out                        # "all" (the Context widget's default) warms GPUs only
     if mode == "eager":                   # listed families: also on CPU (explicit request)
+        # several ranks: each warms alone on a private single-rank session (no collective)
+        target = _private_session(session) if session.comm.world_size > 1 else session
         for fam in fams:
             if fam not in _DONE:
-                _run_family(session, fam, out)
+                _run_family(target, fam, out, quiet=target is not session)
     elif mode == "background" and session.device.type == "cuda":
         todo = [f for f in fams if f not in _DONE and f not in _FAILED]
         if todo and (_THREAD is None or not _THREAD.is_alive()):

@@ -97,12 +97,12 @@ class Session:
         from .runtime.warmup import plan
         plan(self.conf.get("o3s.session.warmup", "auto"))     # a bad value fails before publication
 
-    def _warmup(self) -> None:
+    def _warmup(self, pool_worker: bool = False) -> None:
         """Kernel code-object preload and (conf) tiny fits of the estimator families once
         per process (``runtime/warmup.py``; conf ``o3s.session.warmup``), so the user's
         first fit does not pay the one-time kernel-loading costs."""
         from .runtime.warmup import warmup
-        self.warmup_seconds = warmup(self)
+        self.warmup_seconds = warmup(self, pool_worker)
 
     # ------------------------------------------------------------------ lifecycle
     def _pick_device(self) -> torch.device:

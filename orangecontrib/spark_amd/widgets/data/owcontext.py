@@ -29,6 +29,10 @@ class OWSessionContext(SharedSession, Widget):
         params = OrderedDict(DEFAULTS)
         for k, v in self.conf.getAll():
             params[k] = v
+        if params.get("o3s.session.warmup") == DEFAULTS["o3s.session.warmup"]:
+            # the canvas's session is created ahead of its first fit (this widget's action
+            # runs on a worker thread): warm every estimator family then (runtime/warmup.py)
+            params["o3s.session.warmup"] = "all"
         for k, v in self.saved_gui_params.items():
             params[k] = v
         self.gui_parameters = OrderedDict((k, GuiParam(label=k, default_value=str(v))) for k, v in params.items())

@@ -103,6 +103,11 @@ def test_handles_behave_like_dataframes(pool_session):
     assert s.pool.apply(_local_rows, df) == 150
 
 
+def _executor_warmup_seconds():
+    from orange3_spark_amd import Session
+    return dict(Session.active().warmup_seconds)
+
+
 def _local_rows(df):
     return int(df._n)
 
@@ -304,6 +309,10 @@ def test_gpu_pool_fits_and_transforms(monkeypatch):
     pool = Session(SessionConf().set("spark.executor.instances", "2"))
     try:
         assert type(pool).__name__ == "DriverSession" and all(d.startswith("cuda") for d in pool.pool.devices)
+        # the executors warmed every estimator family at pool start (runtime/warmup.py):
+        # the canvas's first fit on the pool is not a cold fit
+        warm = pool.pool.apply(_executor_warmup_seconds)
+        assert {"preload", "trees", "glm", "kmeans", "als"} <= set(warm) and all(warm.values()), warm
         b = run(pool)
     finally:
         pool.stop()

@@ -85,9 +85,17 @@ def test_user_fits_and_background_warmup_never_overlap():
 
 
 def test_lazy_and_preload_modes_parse():
-    assert W.plan("auto") == ("background", W.FAMILIES)
+    assert W.plan("auto") == ("preload", ()) and W.plan("background") == ("background", W.FAMILIES)
     assert W.plan("lazy") == ("lazy", ()) and W.plan("preload") == ("preload", ())
     assert W.plan("all") == ("eager", W.FAMILIES) and W.plan("false") == ("off", ())
+
+
+def test_context_widget_warms_every_family_by_default():
+    """The canvas creates its session ahead of the first fit: the Context widget's editor
+    defaults to o3s.session.warmup=all (a plain script's auto only preloads)."""
+    from orangecontrib.spark_amd.widgets.data.owcontext import OWSessionContext
+    w = OWSessionContext()
+    assert w.gui_parameters["o3s.session.warmup"].get_value() == "all"
 
 
 @pytest.fixture
@@ -101,16 +109,26 @@ def fresh_gpu(fresh, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_gpu_auto_preloads_then_warms_in_the_background(fresh_gpu):
-    """auto: the session start only loads the kernel code objects (~40 ms, no fit); the
-    families warm on a background thread (private single-rank session, own stream), so
-    the first real fit of a family is a warm fit."""
+def test_gpu_auto_only_preloads(fresh_gpu):
+    """auto in a script: the session start loads the kernel code objects (~40 ms, no
+    fit) and warms no family -- a session that only fits LR pays no GBT/ALS/KMeans fits."""
     import time
     t = time.perf_counter()
     s = Session.getOrCreate(SessionConf())
     start = time.perf_counter() - t
     assert s.device.type == "cuda"
-    assert "preload" in s.warmup_seconds and s.warmup_seconds["preload"] < 1.0 and start < 1.5
+    assert set(s.warmup_seconds) == {"preload"} and s.warmup_seconds["preload"] < 0.1 and start < 1.0
+    from orange3_spark_amd.ml.classification import LogisticRegression
+    LogisticRegression(maxIter=3).fit(s.synthetic.classification(50_000, 32, seed=1))
+    assert set(s.warmup_seconds) == {"preload"} and W._DONE == {"glm"}
+    torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_gpu_background_warmup_then_fits(fresh_gpu):
+    """background: the families warm on a thread (private single-rank session, own
+    stream) and finish; a fit afterwards is an ordinary fit."""
+    s = Session.getOrCreate(SessionConf().set("o3s.session.warmup", "background"))
     assert W.wait_background(120)
     assert set(W.FAMILIES) <= set(s.warmup_seconds) and all(s.warmup_seconds[f] for f in W.FAMILIES)
     from orange3_spark_amd.ml.classification import LogisticRegression
@@ -121,10 +139,10 @@ def test_gpu_auto_preloads_then_warms_in_the_background(fresh_gpu):
 @pytest.mark.gpu
 def test_gpu_user_fit_during_background_warmup(fresh_gpu):
     """A fit issued right after the session start runs while the background warm-up is
-    still going: it waits for the tiny fit in flight, gives the same model as a fit with
+    still going: it preempts the tiny fit in flight, gives the same model as a fit with
     the warm-up off, and its family is not warmed again afterwards."""
     from orange3_spark_amd.ml.clustering import KMeans
-    s = Session.getOrCreate(SessionConf())
+    s = Session.getOrCreate(SessionConf().set("o3s.session.warmup", "background"))
     m1 = KMeans(k=8, maxIter=5, seed=3).fit(s.synthetic.blobs(200_000, 32, 8, seed=2))
     assert "kmeans" in W._DONE
     assert W.wait_background(120)
