@@ -292,6 +292,11 @@ class TreeBuilder:
     hist_subtraction = True         # False: scan every node at every level (reference path)
     batch_trees = True              # False: forests grow one tree at a time (reference path)
     final_from_parent = True        # False: the last level is histogrammed like any other (reference path)
+    # GBT (fit_gbt): no per-row work at all while growing -- no leaf_apply of finished
+    # segments, no routing pass at the last level; the caller runs ONE fused row-order
+    # pass afterwards (ops/trees.gbt_leaf_pass) that applies every leaf and returns the
+    # last level's w*y^2 sums for complete_final()
+    defer_leaves = False
 
     def __init__(self, comm, bins: torch.Tensor, splits: list, y: torch.Tensor, w,
                  impurity: str, num_classes: int, max_depth: int = 5, min_instances: float = 1.0,
@@ -314,6 +319,7 @@ class TreeBuilder:
         self.max_depth, self.min_inst, self.min_gain = max_depth, min_instances, min_info_gain
         self.ffrac = feature_fraction
         self.F = bins.shape[1]
+        self.pending_y2 = None           # defer_leaves: (node ids [P, 2], w [P, 2], w*y [P, 2]) of the last level
 
     def build(self, leaf_acc: torch.Tensor | None = None, leaf_scale: float = 1.0):
         """Grow the (single) tree.  Returns (tree, None).
@@ -483,7 +489,7 @@ class TreeBuilder:
             value[seg_tree, seg_nid] = vals_np
             impurity[seg_tree, seg_nid] = imp_np
             count[seg_tree, seg_nid] = w_np
-            if leaf_acc is not None and is_leaf.any():
+            if leaf_acc is not None and is_leaf.any() and not self.defer_leaves:
                 with trace("tree.leaf_apply"):          # finished segments: rows in the pre-split order
                     lf = is_leaf
                     T.leaf_apply(old_order, seg_lo[lf], seg_hi[lf], value[seg_tree[lf], seg_nid[lf], 0] * leaf_scale,
@@ -529,6 +535,18 @@ class TreeBuilder:
         else:
             vals = (child[..., 1] / np.maximum(w_ch, 1e-300))[..., None]
         s_lo, s_hi = seg_lo[idx], seg_hi[idx]
+        if self.defer_leaves:            # rows are routed (and y^2 summed) by the caller's leaf pass
+            for side in (0, 1):
+                nid = 2 * sn + side
+                value[st, nid] = vals[:, side].reshape(P, V)
+                count[st, nid] = w_ch[:, side]
+            if not self.cls:
+                self.pending_y2 = (np.stack([2 * sn, 2 * sn + 1], 1), child[..., 0], child[..., 1])
+            else:
+                imp, _ = _impurity(torch.from_numpy(child), self.kind)
+                for side in (0, 1):
+                    impurity[st, 2 * sn + side] = imp.numpy()[:, side]
+            return
         y2 = T.final_level(self.bins, order, s_lo, s_hi, bf[idx], bb[idx], vals[:, 0, 0] * leaf_scale,
                            vals[:, 1, 0] * leaf_scale, yp, wp, leaf_acc, need_y2=not self.cls,
                            bins_t=self.bins_t) if (leaf_acc is not None or not self.cls) else None
@@ -547,6 +565,19 @@ class TreeBuilder:
             count[st, nid] = w_ch[:, side]
 
 
+    def complete_final(self, tree: "Tree", y2_leaves) -> None:
+        """defer_leaves: the impurities of the last level's children from the leaf pass's
+        per-leaf sums of w*y^2 (fp64 [2^maxDepth], all ranks reduced)."""
+        if self.pending_y2 is None:
+            return
+        nid, w, wy = self.pending_y2
+        y2 = np.asarray(y2_leaves, dtype=np.float64)[nid - (1 << self.max_depth)]
+        stats = np.stack([w, wy, y2], -1)                                  # [P, 2, 3]
+        imp, _ = _impurity(torch.from_numpy(stats), self.kind)
+        tree.impurity[nid] = imp.numpy()
+        self.pending_y2 = None
+
+
 # ----------------------------------------------------------------------------- ensembles
 @dataclass
 class Ensemble:
@@ -563,6 +594,9 @@ def subsample_weights(n_local, rows: torch.Tensor, rate: float, seed: int, boots
     if rate < 1.0:
         return sampling.bernoulli_mask(rows, seed, rate).to(torch.float32)
     return None
+
+
+GBT_FUSED_EPILOGUE = True      # False: per-level leaf_apply + last-level routing + gbt_grad_loss (reference path)
 
 
 def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_iter: int = 20,
@@ -592,6 +626,7 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
         wd = torch.where(vmask, torch.zeros_like(wd0), wd0)
         w = wd.float()
     Fm = torch.zeros_like(yy)
+    fused = GBT_FUSED_EPILOGUE and max_depth <= T.LEAF_PASS_MAX_DEPTH and bins.dtype == torch.uint8
     trees, weights, losses = [], [], []
     best_err, best_m = math.inf, 0
     target = yy.to(torch.float32)                            # tree 0 fits the (scaled) labels
@@ -604,6 +639,7 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
         tb = TreeBuilder(comm, bins, splits, target, sw, "variance", 1, max_depth, min_instances,
                          min_info_gain, feature_fraction, seed + m, bins_t=bins_t,
                          min_weight_fraction=min_weight_fraction, own_y=True)
+        tb.defer_leaves = fused
         wt = 1.0 if m == 0 else step
         with progress.sub_range(m / max_iter, (m + 1) / max_iter):
             tree, _ = tb.build(leaf_acc=Fm, leaf_scale=wt)      # Fm += wt * leaf value, per row
@@ -611,10 +647,27 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
         tu.__enter__()
         trees.append(tree)
         weights.append(wt)
-        # one fused pass: this iteration's (validation) loss and the next tree's residuals
-        target = torch.empty_like(target) if m + 1 < max_iter else None
-        buf = T.gbt_grad_loss(loss, yy, Fm, wd, w_val, target)
-        comm.all_reduce(buf)
+        if fused:
+            # ONE row-order pass: every row walks the tree (Fm += wt * leaf), the loss of the
+            # updated ensemble, the next tree's residuals (into the target buffer: the build
+            # is done with it) and the last level's w*y^2 sums
+            nxt = target if m + 1 < max_iter else None
+            need_y2 = tb.pending_y2 is not None
+            buf, y2 = T.gbt_leaf_pass(bins, tree.feature, tree.split_bin, tree.value, wt, max_depth, loss, yy, Fm,
+                                      sw, wd, w_val, m == 0, nxt, need_y2)
+            if need_y2:
+                both = torch.cat([buf, y2]).contiguous()
+                comm.all_reduce(both)
+                buf = both[:4]
+                tb.complete_final(tree, both[4:].cpu().numpy())
+            else:
+                comm.all_reduce(buf)
+            target = nxt
+        else:
+            # one fused pass: this iteration's (validation) loss and the next tree's residuals
+            target = torch.empty_like(target) if m + 1 < max_iter else None
+            buf = T.gbt_grad_loss(loss, yy, Fm, wd, w_val, target)
+            comm.all_reduce(buf)
         sums = buf.cpu().numpy()
         losses.append(float(sums[0] / max(sums[1], 1e-300)))
         tu.__exit__(None, None, None)

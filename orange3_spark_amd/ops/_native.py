@@ -71,6 +71,8 @@ _SIGS: dict[str, list] = {
     "o3s_tree_sibling": [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_i32, c_vp, c_vp],
     "o3s_tree_part_dest": [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp],
     "o3s_gbt_grad_loss": [c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp, c_vp, c_i32, c_vp],
+    "o3s_gbt_leaf_pass": [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32,
+                          c_vp, c_vp, c_vp, c_i32, c_vp],
     "o3s_tree_split": [c_vp, c_i32, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_f64, c_f64, c_f64, c_vp, c_vp, c_vp],
     "o3s_tree_hist": [c_vp, c_i64, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32,
                       c_vp],

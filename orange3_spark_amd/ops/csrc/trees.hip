@@ -908,9 +908,11 @@ __global__ __launch_bounds__(256) void forest_weights_kernel(const int64_t* __re
 //     previous pass wrote it (first tree: y = yy).
 // The old path gathered every row twice at random (feature-major byte + an fp64
 // read-modify-write of acc[order[p]]); this one streams bins / yy / Fm once.
-// Per-leaf sums are deterministic: per wave, one fixed-order wave reduction per distinct
-// leaf present in the wave's 64 rows, into the wave's own LDS array; blocks combine
-// waves in a fixed order and write one fp32 slab row each (summed in fp64, fixed order).
+// Per-leaf sums are deterministic and stay in registers: lane j of a wave owns the leaves
+// k with k % 64 == j (NS = L / 64 accumulators each); the wave walks its 64 rows in a
+// fixed order, broadcasting (leaf, w*y^2) with v_readlane, and only the owner lane adds
+// -- no LDS round trip, no shuffle reduction.  Each wave writes one fp32 slab row; the
+// rows are summed in fp64 in a fixed order.
 constexpr int kLeafThreads = 256;
 constexpr int kLeafWaves = kLeafThreads / kWave;
 
@@ -931,7 +933,9 @@ __device__ __forceinline__ void gbt_point(int loss, double yi, double fi, double
   }
 }
 
-template <bool STAGE>
+// NS: per-lane leaf accumulators (L = 2^D leaves at depth D, NS = max(1, L / 64); 0 = no
+// y^2 sums).
+template <bool STAGE, int NS>
 __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
     const uint8_t* __restrict__ bins, int64_t n, int F, int Fs, const int32_t* __restrict__ node_fb, int nodes,
     const double* __restrict__ node_val, int D, const double* __restrict__ yy, double* __restrict__ Fm,
@@ -939,16 +943,16 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
     int first, float* __restrict__ target, double* __restrict__ partial, float* __restrict__ y2slab, int L) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   int32_t* tree = reinterpret_cast<int32_t*>(lds);                         // [nodes]
-  float* y2w = reinterpret_cast<float*>(lds + 4 * nodes);                  // [waves][L]
-  uint8_t* stage = lds + 4 * nodes + 4 * kLeafWaves * L;                   // [waves][64][Fs]
+  uint8_t* stage = lds + 4 * ((nodes + 3) & ~3);                           // [waves][64][Fs]
   __shared__ double red[4][kLeafWaves];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < nodes; i += kLeafThreads) tree[i] = node_fb[i];
-  for (int i = threadIdx.x; i < kLeafWaves * L; i += kLeafThreads) y2w[i] = 0.f;
   __syncthreads();
-  float* my_y2 = y2w + wid * L;
   uint8_t* my_stage = stage + wid * 64 * Fs;
   const int leaf0 = 1 << D;                                                // first node id at depth D
+  float acc[NS > 0 ? NS : 1];
+#pragma unroll
+  for (int q = 0; q < (NS > 0 ? NS : 1); ++q) acc[q] = 0.f;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   const int64_t nchunks = (n + 63) / 64;
   const int64_t wstride = (int64_t)gridDim.x * kLeafWaves;
@@ -957,17 +961,21 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
     const int rows = n - r0 < 64 ? (int)(n - r0) : 64;
     const int64_t i = r0 + (lane < rows ? lane : rows - 1);
     const bool ok = lane < rows;
+    const double yi = yy[i], fo = Fm[i];
+    const float ww = wt ? wt[i] : 1.f;
     if constexpr (STAGE) {
-      // the wave's rows are one contiguous run of rows * F bytes: 4-byte coalesced reads
-      // (F % 4 == 0) into rows of Fs bytes (Fs / 4 odd: lanes' rows on distinct banks)
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(bins + r0 * F);
-      const int wpr = F >> 2, wtot = rows * wpr;
-      for (int e = lane; e < wtot; e += 64) {
-        const int rr = e / wpr, q = e - rr * wpr;
-        *reinterpret_cast<uint32_t*>(my_stage + rr * Fs + 4 * q) = src[e];
+      // the wave's rows are one contiguous run of rows * F bytes: 16-byte coalesced reads
+      // (F % 16 == 0) into rows of Fs bytes (Fs / 4 odd: the lanes' rows on distinct banks)
+      const int qpr = F >> 4, qtot = rows * qpr;
+      const uint4* src = reinterpret_cast<const uint4*>(bins + r0 * F);
+      for (int e = lane; e < qtot; e += 64) {
+        const int rr = e / qpr, q = e - rr * qpr;
+        const uint4 v = src[e];
+        uint32_t* d = reinterpret_cast<uint32_t*>(my_stage + rr * Fs + 16 * q);
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
       }
-      __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     int node = 1;
@@ -978,7 +986,6 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
       const int b = STAGE ? (int)my_stage[lane * Fs + f] : (int)bins[i * F + f];
       node = 2 * node + (b > sb ? 1 : 0);
     }
-    const double yi = yy[i], fo = Fm[i];
     const double fn = fo + node_val[node];
     double l, g;
     gbt_point(loss, yi, fn, l, g);
@@ -994,7 +1001,7 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
         s3 += vi;
       }
     }
-    if (y2slab) {
+    if constexpr (NS > 0) {
       // the residual this tree was fit to (fp32, as the previous pass wrote it)
       float yo;
       if (first) {
@@ -1004,18 +1011,17 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
         gbt_point(loss, yi, fo, lo_, go_);
         yo = (float)go_;
       }
-      const float ww = wt ? wt[i] : 1.f;
-      const float v = ok ? ww * yo * yo : 0.f;
-      int key = (ok && node >= leaf0) ? node - leaf0 : -1;
-      // one fixed-order wave sum per distinct leaf among the wave's rows
-      uint64_t pend = __ballot(key >= 0);
-      while (pend) {
-        const int src = __builtin_ctzll(pend);
-        const int kk = __builtin_amdgcn_readlane(key, src);
-        const bool mine = key == kk;
-        const float sum = wave_sum(mine ? v : 0.f);
-        if (lane == 0) my_y2[kk] += sum;
-        pend &= ~__ballot(mine);
+      const float v = ww * yo * yo;
+      const int key = (ok && node >= leaf0) ? node - leaf0 : -1;
+      for (int q = 0; q < rows; ++q) {                                     // fixed row order
+        const int kq = __builtin_amdgcn_readlane(key, q);
+        if (kq < 0) continue;                                             // wave-uniform
+        const float vq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), q));
+        const int slot = kq >> 6;
+        const bool own = lane == (kq & 63);
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+          if (s == slot) acc[s] += own ? vq : 0.f;
       }
     }
     if constexpr (STAGE) __builtin_amdgcn_wave_barrier();                  // the stage is rewritten next chunk
@@ -1028,12 +1034,11 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
     for (int q = 0; q < kLeafWaves; ++q) a += red[threadIdx.x][q];
     partial[(int64_t)blockIdx.x * 4 + threadIdx.x] = a;
   }
-  if (y2slab) {
-    for (int k = threadIdx.x; k < L; k += kLeafThreads) {
-      float a = 0.f;
-      for (int q = 0; q < kLeafWaves; ++q) a += y2w[q * L + k];
-      y2slab[(int64_t)blockIdx.x * L + k] = a;
-    }
+  if constexpr (NS > 0) {
+    float* row = y2slab + ((int64_t)blockIdx.x * kLeafWaves + wid) * L;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      if (s * 64 + lane < L) row[s * 64 + lane] = acc[s];
   }
 }
 
@@ -1042,26 +1047,36 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
 // Fused GBT tree epilogue (gbt_leaf_pass_kernel).  bins: [n][F] uint8; node_fb: int32
 // [nodes] heap-ordered (root 1): feature | split bin << 16 for internal nodes, -1 for
 // leaves / absent; node_val: fp64 [nodes] leaf value * tree weight; D: the tree's max
-// depth (leaves at depth D own y2slab columns node - 2^D, L = 2^D).  yy / Fm / wd / wv
-// fp64 [n] (wd, wv nullable), wt fp32 [n] (nullable), target fp32 [n] (nullable).
-// partial: fp64 [grid][4]; y2slab: fp32 [grid][L] or null (no y^2 sums).
+// depth (<= 10; leaves at depth D own y2slab columns node - 2^D, L = 2^D).  yy / Fm /
+// wd / wv fp64 [n] (wd, wv nullable), wt fp32 [n] (nullable), target fp32 [n] (nullable).
+// partial: fp64 [grid][4]; y2slab: fp32 [grid * 4][L] (one row per wave) or null.
 O3S_API int o3s_gbt_leaf_pass(const uint8_t* bins, int64_t n, int F, const int32_t* node_fb, int nodes,
                               const double* node_val, int D, const double* yy, double* Fm, const float* wt,
                               const double* wd, const double* wv, int loss, int first, float* target,
                               double* partial, float* y2slab, int grid, hipStream_t st) {
   if (n <= 0) return 0;
-  if (F <= 0 || F > 0xffff || nodes <= 1 || D < 0 || D > 14 || loss < 0 || loss > 2 || grid <= 0) return -1;
-  const int L = y2slab ? (1 << D) : 0;
-  const bool stage = (F % 4) == 0 && F <= 256;
+  if (F <= 0 || F > 0xffff || nodes <= 1 || D < 0 || D > 10 || loss < 0 || loss > 2 || grid <= 0) return -1;
+  const int L = 1 << D;
+  const int ns = y2slab ? (L > 64 ? L / 64 : 1) : 0;
+  const bool stage = (F % 16) == 0 && F <= 256 && ((uintptr_t)bins & 15) == 0;
   const int Fs = stage ? ((F / 4) % 2 == 0 ? F + 4 : F) : 0;
-  const size_t lds = 4 * (size_t)nodes + 4 * (size_t)kLeafWaves * L + (size_t)kLeafWaves * 64 * Fs;
+  const size_t lds = 4 * (size_t)((nodes + 3) & ~3) + (size_t)kLeafWaves * 64 * Fs;
   if (lds > 64 * 1024) return -2;
-  if (stage)
-    hipLaunchKernelGGL((gbt_leaf_pass_kernel<true>), dim3(grid), dim3(kLeafThreads), lds, st, bins, n, F, Fs, node_fb,
-                       nodes, node_val, D, yy, Fm, wt, wd, wv, loss, first, target, partial, y2slab, L);
-  else
-    hipLaunchKernelGGL((gbt_leaf_pass_kernel<false>), dim3(grid), dim3(kLeafThreads), lds, st, bins, n, F, Fs,
-                       node_fb, nodes, node_val, D, yy, Fm, wt, wd, wv, loss, first, target, partial, y2slab, L);
+#define O3S_LP(S, NSV)                                                                                     \
+  hipLaunchKernelGGL((gbt_leaf_pass_kernel<S, NSV>), dim3(grid), dim3(kLeafThreads), lds, st, bins, n, F, Fs, \
+                     node_fb, nodes, node_val, D, yy, Fm, wt, wd, wv, loss, first, target, partial, y2slab, L)
+#define O3S_LPS(S)                                                                                          \
+  switch (ns) {                                                                                             \
+    case 0: O3S_LP(S, 0); break;                                                                            \
+    case 1: O3S_LP(S, 1); break;                                                                            \
+    case 2: O3S_LP(S, 2); break;                                                                            \
+    case 4: O3S_LP(S, 4); break;                                                                            \
+    case 8: O3S_LP(S, 8); break;                                                                            \
+    default: O3S_LP(S, 16); break;                                                                          \
+  }
+  if (stage) { O3S_LPS(true) } else { O3S_LPS(false) }
+#undef O3S_LPS
+#undef O3S_LP
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -282,6 +282,82 @@ def gbt_grad_loss(loss: str, yy: torch.Tensor, Fm: torch.Tensor, w: torch.Tensor
     return torch.stack(out)
 
 
+LEAF_PASS_MAX_DEPTH = 10            # 2^D per-leaf y^2 columns per wave fit the kernel's LDS
+
+
+def tree_node_arrays(feature: np.ndarray, split_bin: np.ndarray, value: np.ndarray, scale: float):
+    """Heap-ordered tree -> (node_fb int32 [nodes]: feature | bin << 16 for internal
+    nodes, -1 for leaves / absent; node_val fp64 [nodes]: leaf value * scale)."""
+    fe = np.asarray(feature, dtype=np.int64)
+    fb = np.where(fe >= 0, fe | (np.asarray(split_bin, dtype=np.int64) << 16), -1).astype(np.int32)
+    return fb, np.asarray(value, dtype=np.float64).reshape(len(fe), -1)[:, 0] * float(scale)
+
+
+def gbt_leaf_pass(bins: torch.Tensor, feature, split_bin, value, scale: float, depth: int, loss: str,
+                  yy: torch.Tensor, Fm: torch.Tensor, wt: torch.Tensor | None, wd: torch.Tensor | None,
+                  wv: torch.Tensor | None, first: bool, target: torch.Tensor | None, need_y2: bool):
+    """The GBT tree epilogue in ONE pass over the rows in row order (``gbt_leaf_pass_kernel``):
+    every row walks the finished tree on its bins, ``Fm += scale * value(leaf)``, the loss
+    partials of the updated ensemble [sum l*wd, sum wd, sum l*wv, sum wv] (fp64 [4]) are
+    returned, ``target`` (fp32, optional) receives the next tree's residuals, and with
+    ``need_y2`` the sums of wt*y^2 of the leaves at depth ``depth`` (fp64 [2^depth], y =
+    the residual this tree was fit to: yy for the first tree, else the loss gradient at
+    the pre-update Fm) -- the last level's children impurities.  CPU: torch."""
+    n, F = bins.shape
+    dev = bins.device
+    fb, val = tree_node_arrays(feature, split_bin, value, scale)
+    nodes = len(fb)
+    L = 1 << depth
+    if bins.is_cuda and n > 0:
+        f64 = [None if t is None else t.to(torch.float64).contiguous() for t in (wd, wv)]
+        wt32 = None if wt is None else wt.to(torch.float32).contiguous()
+        if target is not None and (target.dtype != torch.float32 or target.numel() != n or not target.is_contiguous()):
+            raise ValueError("target must be a contiguous fp32 [n] tensor")
+        if not (yy.dtype == torch.float64 and Fm.dtype == torch.float64 and yy.is_contiguous() and Fm.is_contiguous()):
+            raise ValueError("yy / Fm must be contiguous fp64")
+        grid = int(max(1, min(N.num_cus(dev) * 8, (n + 255) // 256)))
+        part = torch.empty((grid, 4), dtype=torch.float64, device=dev)
+        slab = torch.empty((grid * 4, L), dtype=torch.float32, device=dev) if need_y2 else None   # a row per wave
+        fb_d, val_d = N.upload_many(dev, fb, val)
+        lib = N.kernels()
+        N.check(lib.o3s_gbt_leaf_pass(bins.data_ptr(), n, F, fb_d.data_ptr(), nodes, val_d.data_ptr(), depth,
+                                      yy.data_ptr(), Fm.data_ptr(), N.ptr(wt32), N.ptr(f64[0]), N.ptr(f64[1]),
+                                      _GBT_LOSS[loss], int(first), N.ptr(target), part.data_ptr(), N.ptr(slab),
+                                      grid, N.stream_of(Fm)), "gbt_leaf_pass")
+        y2 = None
+        if need_y2:
+            y2 = torch.empty((1, L), dtype=torch.float64, device=dev)
+            lo, cnt = N.upload_many(dev, np.zeros(1, np.int64), np.full(1, grid * 4, np.int64))
+            N.check(lib.o3s_slab_range_sum(slab.data_ptr(), 0, L, lo.data_ptr(), cnt.data_ptr(), 1, y2.data_ptr(),
+                                           N.stream_of(Fm)), "gbt_leaf_pass y2")
+            y2 = y2[0]
+        return part.sum(0), y2
+    # torch reference: walk the tree, update, loss / residual, per-leaf y^2
+    fb_t = torch.from_numpy(fb.astype(np.int64)).to(dev)
+    node = torch.ones(n, dtype=torch.int64, device=dev)
+    for _ in range(depth):
+        code = fb_t[node]
+        inner = code >= 0
+        if not bool(inner.any()):
+            break
+        f = torch.where(inner, code & 0xFFFF, torch.zeros_like(code))
+        sb = (code >> 16) & 0x7FFF
+        b = bins.gather(1, f[:, None]).squeeze(1).to(torch.int64)
+        node = torch.where(inner, 2 * node + (b > sb).to(torch.int64), node)
+    Fo = Fm.clone()
+    Fm += torch.from_numpy(val).to(dev)[node]
+    out = gbt_grad_loss(loss, yy, Fm, wd, wv, target)
+    y2 = None
+    if need_y2:
+        yo = yy.to(torch.float32) if first else gbt_residual(loss, yy.double(), Fo.double()).to(torch.float32)
+        ww = torch.ones_like(yo) if wt is None else wt.to(torch.float32)
+        v = (ww * yo * yo).to(torch.float64)
+        at = node >= L
+        y2 = torch.zeros(L, dtype=torch.float64, device=dev)
+        y2.index_add_(0, (node[at] - L), v[at])
+    return out, y2
+
+
 def best_splits(H: torch.Tensor, nb: torch.Tensor, fmask, kind: str, min_inst: float, min_w: float,
                 min_wfrac: float, min_w_node=None) -> torch.Tensor:
     """Per-node best split of histograms H [k, F, B, S] (fp64, GPU) in ONE launch of

@@ -489,3 +489,54 @@ def test_final_level_from_parent_matches_full_level(cpu):
 @pytest.mark.gpu
 def test_gpu_final_level_from_parent_matches_full_level():
     _final_level_parity(Session(SessionConf().set("o3s.device", "cuda")))
+
+
+def _gbt_fused_parity(session):
+    """fit_gbt's fused row-order epilogue (ops/trees.gbt_leaf_pass: every leaf applied,
+    the loss, the next residuals and the last level's w*y^2 in one pass) == the reference
+    path (per-level leaf_apply + last-level routing + gbt_grad_loss): trees, losses,
+    impurities, predictions -- logistic with validation + subsampling, squared and
+    absolute losses with weights."""
+    from orange3_spark_amd.models import trees as TR
+    rng = np.random.default_rng(21)
+    n = 6000
+    X = rng.uniform(-1, 1, size=(n, 7))
+    yc = ((X[:, 0] > 0.1) ^ (X[:, 2] > -0.3)).astype(float)
+    yr = np.sin(3 * X[:, 0]) + X[:, 1] * X[:, 3] + 0.1 * rng.normal(size=n)
+    w = rng.uniform(0.5, 2.0, size=n)
+    val = rng.random(n) < 0.2
+    dfc = session.createDataFrame(pd.DataFrame({"features": list(X), "label": yc, "w": w, "v": val}))
+    dfr = session.createDataFrame(pd.DataFrame({"features": list(X), "label": yr, "w": w}))
+    makers = [(dfc, lambda: GBTClassifier(maxDepth=5, maxIter=6, subsamplingRate=0.8, seed=3,
+                                          validationIndicatorCol="v", validationTol=0.0)),
+              (dfr, lambda: GBTRegressor(maxDepth=4, maxIter=5, weightCol="w", lossType="squared")),
+              (dfr, lambda: GBTRegressor(maxDepth=6, maxIter=4, weightCol="w", lossType="absolute"))]
+    for df, mk in makers:
+        outs = []
+        for flag in (True, False):
+            TR.GBT_FUSED_EPILOGUE = flag
+            try:
+                m = mk().fit(df)
+            finally:
+                TR.GBT_FUSED_EPILOGUE = True
+            ens = m._ens
+            outs.append((m.transform(df).toPandas()["prediction"].to_numpy(), np.array(ens.losses),
+                         [(t.feature.copy(), t.value.copy(), t.impurity.copy(), t.count.copy()) for t in ens.trees]))
+        np.testing.assert_allclose(outs[0][0], outs[1][0], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(outs[0][1], outs[1][1], rtol=1e-9)
+        assert len(outs[0][2]) == len(outs[1][2])
+        for a, b in zip(outs[0][2], outs[1][2]):
+            assert np.array_equal(a[0], b[0])
+            # impurity = E[y^2] - mean^2 from fp32 w*y^2 partials summed in another grouping:
+            # ~1e-7 absolute noise where the variance cancels to ~0
+            for q in (1, 2, 3):
+                np.testing.assert_allclose(a[q], b[q], rtol=1e-5, atol=1e-6)
+
+
+def test_gbt_fused_epilogue_matches_reference(cpu):
+    _gbt_fused_parity(cpu)
+
+
+@pytest.mark.gpu
+def test_gpu_gbt_fused_epilogue_matches_reference():
+    _gbt_fused_parity(Session(SessionConf().set("o3s.device", "cuda")))
