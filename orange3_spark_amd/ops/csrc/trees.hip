@@ -61,7 +61,7 @@ __device__ __forceinline__ gbytes scalar_row(const uint8_t* base, int32_t row, i
 // moves them with the rows), so they stream contiguously instead of costing one random
 // cache-line gather each per row -- only the 64-B bins row is gathered.
 template <int FP, bool CLS, bool HW, bool YP, int U>
-__global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
+__global__ __launch_bounds__(kHistThreads, 5) void tree_hist_kernel(
     const uint8_t* __restrict__ bins, int F, int fg0, int B, int S, const int32_t* __restrict__ order,
     const float* __restrict__ y, const float* __restrict__ w, const int64_t* __restrict__ item_lo,
     const int64_t* __restrict__ item_hi, float* __restrict__ slab, int64_t slab_stride) {
@@ -69,12 +69,14 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
   const int SL = CLS ? S : 2;                                     // stats kept in LDS
   // CLS: [wave][rs][B][S][FP] (+pad); REG: [wave][rs][B][FP][2] -- a cell's (w, w*y) pair
   // is one 8-B LDS word, updated by one ds_read_b64 / v_pk_add_f32 / ds_write_b64
+  // (no static LDS: at F = 64, B = 32 a block's two 16-KB images are exactly a fifth of
+  // the CU's 160 KB, so five blocks -- ten waves -- are resident; the REG w*y^2 partials
+  // leave through the slab instead of an LDS scratch, see the block reduction)
   extern __shared__ __attribute__((aligned(16))) float hist[];
-  __shared__ float y2part[kHistWaves * RS];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform (SGPR)
   const int rs = lane / FP, f = lane % FP;
-  const int region = B * SL * FP + 16;                            // +16: rs-regions on distinct banks
+  const int region = B * SL * FP + (RS > 1 ? 16 : 0);             // +16: rs-regions on distinct banks
   const int per_wave = RS * region;
   float* my = hist + wid * per_wave + rs * region;
   for (int i = threadIdx.x; i < kHistWaves * per_wave; i += kHistThreads) hist[i] = 0.f;
@@ -256,17 +258,23 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
       }
     }
   }
-  if constexpr (!CLS && RS == 1) wy2 = group_sum<32>(wy2);         // chunk partials of lanes 0..CH-1
-  if (!CLS && f == 0) y2part[wid * RS + rs] = wy2;
+  float* out = slab + (int64_t)blockIdx.x * slab_stride;
+  // REG stat 2 (w*y^2) is a node total: wave q writes its partial (summed over its
+  // row-slots in a fixed order) to (feature 0, bin q); every other stat-2 cell is zero.
+  // Consumers only ever sum stat 2 over feature 0's bins (the split kernel's node total,
+  // the sibling subtraction), so the total is unchanged.
+  if constexpr (!CLS) {
+    if constexpr (RS == 1) wy2 = group_sum<32>(wy2);               // chunk partials of lanes 0..CH-1
+    else wy2 = group_sum<64>(f == 0 ? wy2 : 0.f);                  // lanes f == 0 of every row-slot
+    if (fg0 == 0 && lane == 0) out[(int64_t)wid * S + 2] = wy2;
+  }
   __syncthreads();
-  // fixed-order block reduction -> slab[item][f][b][s] (features of this group only);
-  // REG stat 2 (w*y^2) is a node total: stored in (feature 0, bin 0), zero elsewhere.
+  // fixed-order block reduction -> slab[item][f][b][s] (features of this group only).
   // Feature fastest across lanes: the 64 lanes of a wave read one (bin, stat) row of the
   // image -- 64 consecutive floats, one per bank.  (Mapping (bin, stat) fastest put every
   // lane of a wave on the same bank: 64 floats apart -- the kernel's measured LDS bank
   // conflicts, profiles/pmc_kmeans_gbt.json.)  The slab row is then written with a stride
   // of B*S floats per lane; the block writes the whole row, so L2 merges the lines.
-  float* out = slab + (int64_t)blockIdx.x * slab_stride;
   const int cells = FP * B * S;
   for (int i = threadIdx.x; i < cells; i += kHistThreads) {
     const int ff = i % FP, rem = i / FP;
@@ -277,8 +285,8 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
       for (int q = 0; q < kHistWaves; ++q)
         for (int r = 0; r < RS; ++r)
           acc += hist[q * per_wave + r * region + (CLS ? (bb * SL + ss) * FP + ff : (bb * FP + ff) * 2 + ss)];
-    } else if (fg0 + ff == 0 && bb == 0) {
-      for (int q = 0; q < kHistWaves * RS; ++q) acc += y2part[q];
+    } else if (fg0 + ff == 0 && bb < kHistWaves) {
+      continue;                                                    // a wave's w*y^2 partial
     }
     out[((int64_t)(fg0 + ff) * B + bb) * S + ss] = acc;
   }
@@ -1183,7 +1191,7 @@ O3S_API int o3s_tree_part_dest(const int64_t* it_lo, const int64_t* it_hi, const
 O3S_API int o3s_tree_hist_lds(int fp, int B, int S, int cls) {
   const int RS = 64 / fp;
   const int SL = cls ? S : 2;
-  const int64_t bytes = (int64_t)kHistWaves * RS * (B * SL * fp + 16) * 4;
+  const int64_t bytes = (int64_t)kHistWaves * RS * (B * SL * fp + (RS > 1 ? 16 : 0)) * 4;
   return bytes <= 160 * 1024 ? (int)bytes : 0;
 }
 
