@@ -259,10 +259,10 @@ __global__ __launch_bounds__(kHistThreads, 5) void tree_hist_kernel(
     }
   }
   float* out = slab + (int64_t)blockIdx.x * slab_stride;
-  // REG stat 2 (w*y^2) is a node total: wave q writes its partial (summed over its
-  // row-slots in a fixed order) to (feature 0, bin q); every other stat-2 cell is zero.
-  // Consumers only ever sum stat 2 over feature 0's bins (the split kernel's node total,
-  // the sibling subtraction), so the total is unchanged.
+  // REG stat 2 (w*y^2) is a node total, stored in (feature 0, bin 0), zero elsewhere.
+  // Wave q parks its partial (summed over its row-slots in a fixed order) in the slab cell
+  // (feature 0, bin q) -- global memory, visible to the block after the barrier -- and the
+  // thread that owns (feature 0, bin 0) adds them in wave order and clears the others.
   if constexpr (!CLS) {
     if constexpr (RS == 1) wy2 = group_sum<32>(wy2);               // chunk partials of lanes 0..CH-1
     else wy2 = group_sum<64>(f == 0 ? wy2 : 0.f);                  // lanes f == 0 of every row-slot
@@ -285,8 +285,13 @@ __global__ __launch_bounds__(kHistThreads, 5) void tree_hist_kernel(
       for (int q = 0; q < kHistWaves; ++q)
         for (int r = 0; r < RS; ++r)
           acc += hist[q * per_wave + r * region + (CLS ? (bb * SL + ss) * FP + ff : (bb * FP + ff) * 2 + ss)];
+    } else if (fg0 + ff == 0 && bb == 0) {
+#pragma unroll
+      for (int q = 0; q < kHistWaves; ++q) acc += out[(int64_t)q * S + 2];   // the waves' partials
+#pragma unroll
+      for (int q = 1; q < kHistWaves; ++q) out[(int64_t)q * S + 2] = 0.f;
     } else if (fg0 + ff == 0 && bb < kHistWaves) {
-      continue;                                                    // a wave's w*y^2 partial
+      continue;                                                    // cleared by the (bin 0) owner
     }
     out[((int64_t)(fg0 + ff) * B + bb) * S + ss] = acc;
   }
