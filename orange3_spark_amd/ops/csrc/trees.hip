@@ -921,11 +921,13 @@ __global__ __launch_bounds__(256) void forest_weights_kernel(const int64_t* __re
 //     previous pass wrote it (first tree: y = yy).
 // The old path gathered every row twice at random (feature-major byte + an fp64
 // read-modify-write of acc[order[p]]); this one streams bins / yy / Fm once.
-// Per-leaf sums are deterministic and stay in registers: lane j of a wave owns the leaves
-// k with k % 64 == j (NS = L / 64 accumulators each); the wave walks its 64 rows in a
-// fixed order, broadcasting (leaf, w*y^2) with v_readlane, and only the owner lane adds
-// -- no LDS round trip, no shuffle reduction.  Each wave writes one fp32 slab row; the
-// rows are summed in fp64 in a fixed order.
+// Per-leaf sums: every wave owns an LDS array of the 2^D leaf sums and adds its rows with
+// ONE LDS atomic add per chunk (ds_add_f32, no return); lanes that hit the same leaf in
+// one instruction are serialised by the LDS in lane order, instructions in program order,
+// so a wave's sums are a fixed sequence of fp32 adds (deterministic).  Each wave writes
+// its array as one fp32 slab row; the rows are summed in fp64 in a fixed order.  (A
+// register-owned variant -- the owner lane adds each broadcast row -- cost ~2300
+// instructions per 64 rows: 5.2 ms per 100M rows, profiles/gbt_r6_kernels.json.)
 constexpr int kLeafThreads = 256;
 constexpr int kLeafWaves = kLeafThreads / kWave;
 
@@ -946,9 +948,8 @@ __device__ __forceinline__ void gbt_point(int loss, double yi, double fi, double
   }
 }
 
-// NS: per-lane leaf accumulators (L = 2^D leaves at depth D, NS = max(1, L / 64); 0 = no
-// y^2 sums).
-template <bool STAGE, int NS>
+// Y2: per-leaf w*y^2 sums of the leaves at depth D (L = 2^D).
+template <bool STAGE, bool Y2>
 __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
     const uint8_t* __restrict__ bins, int64_t n, int F, int Fs, const int32_t* __restrict__ node_fb, int nodes,
     const double* __restrict__ node_val, int D, const double* __restrict__ yy, double* __restrict__ Fm,
@@ -956,16 +957,17 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
     int first, float* __restrict__ target, double* __restrict__ partial, float* __restrict__ y2slab, int L) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   int32_t* tree = reinterpret_cast<int32_t*>(lds);                         // [nodes]
-  uint8_t* stage = lds + 4 * ((nodes + 3) & ~3);                           // [waves][64][Fs]
+  float* y2w = reinterpret_cast<float*>(lds + 4 * ((nodes + 3) & ~3));     // [waves][L]
+  uint8_t* stage = reinterpret_cast<uint8_t*>(y2w + (Y2 ? kLeafWaves * L : 0));   // [waves][64][Fs]
   __shared__ double red[4][kLeafWaves];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < nodes; i += kLeafThreads) tree[i] = node_fb[i];
+  if constexpr (Y2)
+    for (int i = threadIdx.x; i < kLeafWaves * L; i += kLeafThreads) y2w[i] = 0.f;
   __syncthreads();
   uint8_t* my_stage = stage + wid * 64 * Fs;
+  float* my_y2 = y2w + wid * L;
   const int leaf0 = 1 << D;                                                // first node id at depth D
-  float acc[NS > 0 ? NS : 1];
-#pragma unroll
-  for (int q = 0; q < (NS > 0 ? NS : 1); ++q) acc[q] = 0.f;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   const int64_t nchunks = (n + 63) / 64;
   const int64_t wstride = (int64_t)gridDim.x * kLeafWaves;
@@ -1014,7 +1016,7 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
         s3 += vi;
       }
     }
-    if constexpr (NS > 0) {
+    if constexpr (Y2) {
       // the residual this tree was fit to (fp32, as the previous pass wrote it)
       float yo;
       if (first) {
@@ -1024,18 +1026,7 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
         gbt_point(loss, yi, fo, lo_, go_);
         yo = (float)go_;
       }
-      const float v = ww * yo * yo;
-      const int key = (ok && node >= leaf0) ? node - leaf0 : -1;
-      for (int q = 0; q < rows; ++q) {                                     // fixed row order
-        const int kq = __builtin_amdgcn_readlane(key, q);
-        if (kq < 0) continue;                                             // wave-uniform
-        const float vq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), q));
-        const int slot = kq >> 6;
-        const bool own = lane == (kq & 63);
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-          if (s == slot) acc[s] += own ? vq : 0.f;
-      }
+      if (ok && node >= leaf0) atomicAdd(my_y2 + (node - leaf0), ww * yo * yo);
     }
     if constexpr (STAGE) __builtin_amdgcn_wave_barrier();                  // the stage is rewritten next chunk
   }
@@ -1047,11 +1038,12 @@ __global__ __launch_bounds__(kLeafThreads) void gbt_leaf_pass_kernel(
     for (int q = 0; q < kLeafWaves; ++q) a += red[threadIdx.x][q];
     partial[(int64_t)blockIdx.x * 4 + threadIdx.x] = a;
   }
-  if constexpr (NS > 0) {
+  if constexpr (Y2) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     float* row = y2slab + ((int64_t)blockIdx.x * kLeafWaves + wid) * L;
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-      if (s * 64 + lane < L) row[s * 64 + lane] = acc[s];
+    for (int k = lane; k < L; k += 64) row[k] = my_y2[k];
   }
 }
 
@@ -1070,25 +1062,19 @@ O3S_API int o3s_gbt_leaf_pass(const uint8_t* bins, int64_t n, int F, const int32
   if (n <= 0) return 0;
   if (F <= 0 || F > 0xffff || nodes <= 1 || D < 0 || D > 10 || loss < 0 || loss > 2 || grid <= 0) return -1;
   const int L = 1 << D;
-  const int ns = y2slab ? (L > 64 ? L / 64 : 1) : 0;
+  const bool y2 = y2slab != nullptr;
   const bool stage = (F % 16) == 0 && F <= 256 && ((uintptr_t)bins & 15) == 0;
   const int Fs = stage ? ((F / 4) % 2 == 0 ? F + 4 : F) : 0;
-  const size_t lds = 4 * (size_t)((nodes + 3) & ~3) + (size_t)kLeafWaves * 64 * Fs;
+  const size_t lds = 4 * (size_t)((nodes + 3) & ~3) + (y2 ? 4 * (size_t)kLeafWaves * L : 0) +
+                     (size_t)kLeafWaves * 64 * Fs;
   if (lds > 64 * 1024) return -2;
-#define O3S_LP(S, NSV)                                                                                     \
-  hipLaunchKernelGGL((gbt_leaf_pass_kernel<S, NSV>), dim3(grid), dim3(kLeafThreads), lds, st, bins, n, F, Fs, \
+#define O3S_LP(S, Y)                                                                                       \
+  hipLaunchKernelGGL((gbt_leaf_pass_kernel<S, Y>), dim3(grid), dim3(kLeafThreads), lds, st, bins, n, F, Fs,   \
                      node_fb, nodes, node_val, D, yy, Fm, wt, wd, wv, loss, first, target, partial, y2slab, L)
-#define O3S_LPS(S)                                                                                          \
-  switch (ns) {                                                                                             \
-    case 0: O3S_LP(S, 0); break;                                                                            \
-    case 1: O3S_LP(S, 1); break;                                                                            \
-    case 2: O3S_LP(S, 2); break;                                                                            \
-    case 4: O3S_LP(S, 4); break;                                                                            \
-    case 8: O3S_LP(S, 8); break;                                                                            \
-    default: O3S_LP(S, 16); break;                                                                          \
-  }
-  if (stage) { O3S_LPS(true) } else { O3S_LPS(false) }
-#undef O3S_LPS
+  if (stage && y2) O3S_LP(true, true);
+  else if (stage) O3S_LP(true, false);
+  else if (y2) O3S_LP(false, true);
+  else O3S_LP(false, false);
 #undef O3S_LP
   O3S_CHECK_LAUNCH();
   return 0;

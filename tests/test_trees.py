@@ -540,3 +540,45 @@ def test_gbt_fused_epilogue_matches_reference(cpu):
 @pytest.mark.gpu
 def test_gpu_gbt_fused_epilogue_matches_reference():
     _gbt_fused_parity(Session(SessionConf().set("o3s.device", "cuda")))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("loss,first", [("logistic", True), ("logistic", False), ("squared", False)])
+def test_gpu_gbt_leaf_pass_matches_torch_and_is_deterministic(gpu, loss, first):
+    """The fused GBT epilogue kernel (gbt_leaf_pass_kernel) against its torch reference on
+    a random depth-6 tree: Fm update, loss partials, next residuals and the per-leaf
+    w*y^2 sums; two launches give bitwise-equal results (per-wave LDS sums)."""
+    from orange3_spark_amd.ops import trees as T
+    g = torch.Generator().manual_seed(5)
+    n, F, D = 200_003, 64, 6
+    bins = torch.randint(0, 32, (n, F), generator=g, dtype=torch.uint8)
+    nodes = 1 << (D + 1)
+    rng = np.random.default_rng(3)
+    feature = -np.ones(nodes, dtype=np.int64)
+    split_bin = np.zeros(nodes, dtype=np.int64)
+    for nid in range(1, 1 << D):                       # a full tree except a few early leaves
+        if nid in (5, 12):
+            continue
+        if nid > 1 and feature[nid // 2] < 0:
+            continue
+        feature[nid] = rng.integers(0, F)
+        split_bin[nid] = rng.integers(0, 31)
+    value = rng.normal(size=(nodes, 1))
+    yy = (torch.randint(0, 2, (n,), generator=g).double() * 2 - 1) if loss == "logistic" else torch.randn(n, generator=g,
+                                                                                                  dtype=torch.float64)
+    Fm0 = torch.randn(n, generator=g, dtype=torch.float64) * 0.3
+    wt = torch.rand(n, generator=g)
+    out = []
+    for dev in ("cpu", gpu, gpu):
+        Fm = Fm0.clone().to(dev)
+        tgt = torch.empty(n, dtype=torch.float32, device=dev)
+        buf, y2 = T.gbt_leaf_pass(bins.to(dev), feature, split_bin, value, 0.5, D, loss, yy.to(dev), Fm, wt.to(dev),
+                                  None, None, first, tgt, True)
+        out.append((Fm.cpu(), buf.cpu(), y2.cpu(), tgt.cpu()))
+    ref, a, b = out
+    torch.testing.assert_close(a[0], ref[0], rtol=0, atol=0)
+    torch.testing.assert_close(a[1], ref[1], rtol=1e-12, atol=1e-9)
+    torch.testing.assert_close(a[2], ref[2], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(a[3], ref[3], rtol=1e-6, atol=1e-7)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
