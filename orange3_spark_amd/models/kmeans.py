@@ -338,6 +338,57 @@ def _fit_kmeans_blocks(comm, B, k, max_iter, tol, seed, init, init_steps, initia
     return KMeansResult(C.cpu(), float(buf[-1]), it, [int(x) for x in buf[:k].tolist()], hist, time.time() - t0)
 
 
+HAMERLY = True                 # False: every Lloyd iteration screens every row (reference path)
+HAMERLY_FULL_FRACTION = 0.5    # more rows than this to recheck: screen them all (contiguous)
+LAST_HAMERLY_STATS: list = []  # per iteration: rows screened / changed (diagnostics)
+
+
+def _hamerly_step(X, C, prep, ws, k, hs):
+    """One Lloyd assignment + cluster-sum step with Hamerly bounds (state ``hs`` carried
+    across iterations): returns this rank's (sums fp64 [k, D], counts fp64 [k], stats)."""
+    n = X.shape[0]
+    dev = X.device
+    full = hs["a"] is None
+    rows = None
+    if not full:
+        # centre shifts (fp64, rounded up to a safe fp32)
+        delta = (C.to(torch.float64) - hs["C"].to(torch.float64)).pow(2).sum(1).sqrt()
+        delta = (delta * (1 + 1e-6) + 1e-30).float()
+        dmax = float(delta.max())
+        bnd, a = hs["bnd"], hs["a"]
+        ub = bnd[:, 0]
+        lb = bnd[:, 1]
+        ub.add_(delta[a.long()])
+        lb.sub_(dmax)
+        need = ub >= lb
+        rows = torch.nonzero(need).reshape(-1).to(torch.int32)
+        full = rows.numel() > HAMERLY_FULL_FRACTION * n
+    if full:
+        a = torch.empty(n, dtype=torch.int32, device=dev) if hs["a"] is None else hs["a"]
+        bnd = torch.empty((n, 2), dtype=torch.float32, device=dev) if hs["bnd"] is None else hs["bnd"]
+        K.assign_bounded(X, prep, a, bnd, None)
+        S, cnt = K.update(X, a, ws.K, ws)
+        S, cnt = S[:k].clone(), cnt[:k].clone()
+        st = {"screened": n, "changed": None}
+    else:
+        a, bnd = hs["a"], hs["bnd"]
+        a_old = a[rows.long()].clone()
+        K.assign_bounded(X, prep, a, bnd, rows)
+        a_new = a[rows.long()]
+        ch = rows[a_new != a_old]
+        S, cnt = hs["S"], hs["n"]
+        if ch.numel():
+            Xc = X[ch.long()]
+            s1, c1 = K.update(Xc, a_new[a_new != a_old].contiguous(), ws.K, ws)
+            s1, c1 = s1[:k].clone(), c1[:k].clone()
+            s0, c0 = K.update(Xc, a_old[a_new != a_old].contiguous(), ws.K, ws)
+            S = S + (s1 - s0[:k])
+            cnt = cnt + (c1 - c0[:k])
+        st = {"screened": int(rows.numel()), "changed": int(ch.numel())}
+    hs.update(a=a, bnd=bnd, S=S, n=cnt, C=C.clone())
+    return S, cnt, st
+
+
 def fit_kmeans(comm, X, k: int, max_iter: int = 20, tol: float = 1e-4, seed: int = 0,
                init: str = "k-means||", init_steps: int = 2, initial: torch.Tensor | None = None,
                weights: torch.Tensor | None = None, cosine: bool = False, ckpt=None) -> KMeansResult:
@@ -391,16 +442,30 @@ def _fit_kmeans_rows(comm, X, k, max_iter, tol, seed, init, init_steps, initial,
     # skips the exact-distance epilogue and half of its row reads)
     mean = _global_mean(comm, X) if weights is None else None
     sumsq = _sum_sq(X, mean) if weights is None else None
+    # Hamerly bounds (unweighted, screen kernel): per row an upper bound on the distance to
+    # its centre and a lower bound on the distance to every other one; after the centres
+    # move by delta, ub += delta[a] and lb -= max delta, and only rows with ub >= lb are
+    # screened again -- the others provably keep their centre (exact Lloyd, not an
+    # approximation).  The cluster sums are then updated by the rows that changed centre
+    # (fp64 running sums, deterministic slab kernel on the changed rows).
+    ham = (HAMERLY and weights is None and ws is not None and K.screen_ok(X) and X.shape[0] > 0
+           and not cosine)
+    hs = {"a": None, "bnd": None, "S": None, "n": None, "C": None}
+    stats_it = []
     for it in range(start + 1, max_iter + 1):
         progress.iteration(it - 1, max_iter)
         with trace("kmeans.iter"):
             prep = K.prepare_centers(C.float()) if K.kernel_ok(X) else None
-            a, d = K.assign(X, C.float(), prep, need_dist=weights is not None)
-            if ws is not None:
-                sums, cnt = K.update(X, a, ws.K, ws)
-                sums, cnt = sums[:k], cnt[:k]
+            if ham:
+                sums, cnt, st_ = _hamerly_step(X, C, prep, ws, k, hs)
+                stats_it.append(st_)
             else:
-                sums, cnt = K.update_torch(X, a, k, weights)
+                a, d = K.assign(X, C.float(), prep, need_dist=weights is not None)
+                if ws is not None:
+                    sums, cnt = K.update(X, a, ws.K, ws)
+                    sums, cnt = sums[:k], cnt[:k]
+                else:
+                    sums, cnt = K.update_torch(X, a, k, weights)
             if weights is None:
                 Cd = C.to(sums.device, torch.float64) - mean
                 Sd = sums.to(torch.float64) - cnt.to(torch.float64)[:, None] * mean
@@ -421,6 +486,7 @@ def _fit_kmeans_rows(comm, X, k, max_iter, tol, seed, init, init_steps, initial,
                 ckpt.save(it, {"C": C.cpu().numpy(), "hist": np.asarray(hist)})
             if moved <= tol * tol:
                 break
+    LAST_HAMERLY_STATS[:] = stats_it
     if ckpt is not None:
         ckpt.clear()                     # finished: a later fit must not resume from this run
     # final cost/sizes w.r.t. the returned centres (Spark reports the last assignment's)

@@ -344,7 +344,8 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const float* __restrict__ cn, const float* __restrict__ C32, int ldc, int Cpad, float eps_x, float eps0,
     float xscale, float sscale, int32_t* __restrict__ assign, float* __restrict__ mind,
     int32_t* __restrict__ flag_cnt, int32_t* __restrict__ flag_rows, int Dx,
-    const uint4* __restrict__ XP = nullptr, const float* __restrict__ XN = nullptr) {
+    const uint4* __restrict__ XP = nullptr, const float* __restrict__ XN = nullptr,
+    const int32_t* __restrict__ rowlist = nullptr, float2* __restrict__ bnd = nullptr) {
   using L = ScrLds<KS>;
   constexpr int D = L::D;
   constexpr int G = L::G;
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
 #pragma unroll
     for (int t = 0; t < TT; ++t) {
       const int64_t row = row_base + t * 32 + r;
-      const int64_t rowc = row < n ? row : n - 1;
+      const int64_t rowc = rowlist ? (int64_t)rowlist[row < n ? row : n - 1] : (row < n ? row : n - 1);
       const uint4* src = XP + rowc * (D / 4);
       uint4 hv[KS], lv[KS];
 #pragma unroll
@@ -403,7 +404,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       const int P = lane + q * kWave;
       const int rr = P / XS, sl = P % XS;
       const int64_t row = row_base + t * 32 + rr;
-      const int64_t rowc = row < n ? row : n - 1;
+      const int64_t rowc = rowlist ? (int64_t)rowlist[row < n ? row : n - 1] : (row < n ? row : n - 1);
       const int slc = 4 * sl < Dx ? sl : 0;
       xv[q] = *reinterpret_cast<const float4*>(X + rowc * ldx + 4 * slc);
       if (4 * sl >= Dx) xv[q] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -705,12 +706,13 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     s += __shfl_xor(s, 32, 64);
     if (PAIR) s2 += __shfl_xor(s2, 32, 64);
     }
-    const int64_t row = row_base + t * 32 + r;
+    const int64_t row_l = row_base + t * 32 + r;                  // position in this launch
+    const bool ok = row_l < n && h == 0;
+    const int64_t row = rowlist ? (int64_t)rowlist[ok ? row_l : 0] : row_l;   // the data row
     // in the scaled units of bv, sec; the plain screen's slot codes move each key by less
     // than 2^-19 of its magnitude (twice that allowed for)
     float bound = 2.f * sscale * (eps_x * sqrtf(xn[t]) + eps0);
     if constexpr (!PAIR) bound += 0x1p-18f * (fabsf(bv) + fabsf(sec));
-    const bool ok = row < n && h == 0;
     bool fl = ok && (!(sec - bv > bound) || !idx_ok);      // near-tie (or NaN): exact re-solve
     int pick = idc;
     float pd = s;
@@ -724,6 +726,22 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     if (ok) {
       assign[row] = pick;
       if (!NOD && mind) mind[row] = pd;
+      if (bnd) {
+        // Hamerly bounds for the next Lloyd iteration (unscaled distances, not squared):
+        // ub >= ||x - c_pick||, lb <= ||x - c|| for every other centre.  Screened partial
+        // distances (||c||^2 - 2 x.c) are within bound / (2 S) of the exact ones (the whole
+        // bound is used), plus fp32 rounding of ||x||^2 + partial.  Near ties: (inf, 0) --
+        // rechecked next time.
+        float2 o = make_float2(INFINITY, 0.f);
+        if (!fl && !PAIR) {
+          const float inv = 1.f / sscale;
+          const float pb = bv * inv, psec = sec * inv, mg = bound * inv;
+          const float slack = 0x1p-20f * (xn[t] + fabsf(pb) + fabsf(psec));
+          o.x = sqrtf(fmaxf(xn[t] + pb + mg + slack, 0.f)) * (1.f + 0x1p-20f);
+          o.y = sqrtf(fmaxf(xn[t] + psec - mg - slack, 0.f)) * (1.f - 0x1p-20f);
+        }
+        bnd[row] = o;
+      }
     }
     const uint64_t m = __ballot(fl);
     if (m) {
@@ -1094,10 +1112,12 @@ O3S_API int o3s_kmeans_presplit(const float* X, int64_t n, int64_t ldx, int Dx, 
   return 0;
 }
 
-O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
-                              const float* C32, int ldc, int Cpad, float eps_x, float eps0, float xscale,
-                              float sscale, int32_t* assign, float* mind, int32_t* flag_cnt, int32_t* flag_rows,
-                              int tt, int pair, const void* XP, const float* XN, hipStream_t st) {
+O3S_API int o3s_kmeans_screen2(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
+                               const float* C32, int ldc, int Cpad, float eps_x, float eps0, float xscale,
+                               float sscale, int32_t* assign, float* mind, int32_t* flag_cnt, int32_t* flag_rows,
+                               int tt, int pair, const void* XP, const float* XN, const int32_t* rowlist,
+                               float* bnd2, hipStream_t st) {
+  float2* bnd = reinterpret_cast<float2*>(bnd2);
   if (n <= 0) return 0;
   const int D = (Dx + 31) / 32 * 32;
   if (Dx % 4 != 0 || D > 160 || ldx % 4 != 0 || ldc % 4 != 0 || Cpad % 32 != 0 || n > 0x7fffffffll) return -1;
@@ -1117,19 +1137,19 @@ O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, co
     if (XP && !P && !mind)                                                                          \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, true, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, \
                          st, X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind,     \
-                         flag_cnt, flag_rows, Dx, (const uint4*)XP, XN);                                   \
+                         flag_cnt, flag_rows, Dx, (const uint4*)XP, XN, rowlist, bnd);                     \
     else if (XP && !P)                                                                                     \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, \
                          X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt, \
-                         flag_rows, Dx, (const uint4*)XP, XN);                                             \
+                         flag_rows, Dx, (const uint4*)XP, XN, rowlist, bnd);                               \
     else if (!P && !mind)                                                                                  \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, false, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, \
                          st, X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind,     \
-                         flag_cnt, flag_rows, Dx, nullptr, nullptr);                                       \
+                         flag_cnt, flag_rows, Dx, nullptr, nullptr, rowlist, bnd);                         \
     else                                                                                                   \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, X, n, \
                          ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt,   \
-                         flag_rows, Dx, nullptr, nullptr);                                                 \
+                         flag_rows, Dx, nullptr, nullptr, rowlist, bnd);                                   \
   }
   switch (D / 16) {
     case 2: if (tt == 2) O3S_KS(2, 2) else O3S_KS(2, 1) break;
@@ -1143,6 +1163,15 @@ O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, co
 #undef O3S_KSP
   O3S_CHECK_LAUNCH();
   return 0;
+}
+
+// The screen without row list / bounds (the original entry point).
+O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
+                              const float* C32, int ldc, int Cpad, float eps_x, float eps0, float xscale,
+                              float sscale, int32_t* assign, float* mind, int32_t* flag_cnt, int32_t* flag_rows,
+                              int tt, int pair, const void* XP, const float* XN, hipStream_t st) {
+  return o3s_kmeans_screen2(X, n, ldx, Dx, Chi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind,
+                            flag_cnt, flag_rows, tt, pair, XP, XN, nullptr, nullptr, st);
 }
 
 O3S_API int o3s_kmeans_update_ws(int Kp, int D, int grid, int64_t* slab_floats, int64_t* cnt_floats,

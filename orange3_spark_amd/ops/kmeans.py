@@ -310,6 +310,44 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
     return a, d
 
 
+def assign_bounded(X: torch.Tensor, P: Prepared, a: torch.Tensor, bnd: torch.Tensor,
+                   rows: torch.Tensor | None = None, stats: dict | None = None) -> None:
+    """The plain screen (+ exact re-solve of its near ties) over ``rows`` of X (int32,
+    ascending; None = every row), writing ``a[row]`` and the Hamerly bounds ``bnd[row]``
+    = (upper bound on ||x - c_a||, lower bound on the distance to every other centre;
+    (inf, 0) for re-solved near ties) -- models/kmeans.py skips rows whose bounds, moved
+    by the centres' shifts, still certify the assignment."""
+    n = X.shape[0] if rows is None else int(rows.numel())
+    if n == 0:
+        return
+    lib = N.kernels()
+    st = N.stream_of(X)
+    cnt, flag = _SWS.get(n, X.device)
+    cnt.zero_()
+    xs = x_scale(X)
+    eps_x, eps0 = screen_bound(P, xs, X.shape[1])
+    ps = presplit(X, xs)
+    tt = SCREEN_TT or (2 if X.shape[1] <= 128 else 1)
+    if rows is not None and (rows.dtype != torch.int32 or not rows.is_contiguous()):
+        raise ValueError("rows must be contiguous int32")
+    if bnd.dtype != torch.float32 or tuple(bnd.shape) != (X.shape[0], 2) or not bnd.is_contiguous():
+        raise ValueError("bnd must be fp32 [n, 2]")
+    N.check(lib.o3s_kmeans_screen2(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
+                                   P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
+                                   Ct.c_float(eps0), Ct.c_float(xs), Ct.c_float(xs * P.ms), a.data_ptr(), None,
+                                   cnt.data_ptr(), flag.data_ptr(), tt, 0, N.ptr(ps[0]) if ps else None,
+                                   N.ptr(ps[1]) if ps else None, N.ptr(rows), bnd.data_ptr(), st),
+            "kmeans_screen(bounds)")
+    m = int(cnt.item())
+    if stats is not None:
+        stats["screened"] = n
+        stats["flagged"] = m
+    if m:
+        N.check(lib.o3s_kmeans_assign(X.data_ptr(), m, X.stride(0), X.shape[1], P.hi.data_ptr(), P.lo.data_ptr(),
+                                      P.cn.data_ptr(), P.hi.shape[0], a.data_ptr(), None, flag.data_ptr(), st),
+                "kmeans_assign(recheck)")
+
+
 class UpdateWorkspace:
     def __init__(self, device, K: int, D: int, grid: int | None = None):
         self.K, self.D = K, D

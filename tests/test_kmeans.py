@@ -364,3 +364,34 @@ def test_gpu_approx_assign_is_within_the_screen_bound(gpu):
     assert torch.allclose(d1, dx, rtol=1e-4, atol=1e-3)
     assert bool((d1 <= d2 + bound + 1e-3).all())
     assert float((a1 == a2).float().mean()) > 0.9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["blobs", "uniform"])
+def test_gpu_hamerly_lloyd_equals_full_screens(gpu, kind, monkeypatch):
+    """Lloyd with Hamerly bounds (models/kmeans.py: only rows whose moved bounds no longer
+    certify their centre are screened again, cluster sums updated by the rows that changed)
+    gives the iterations of the every-row screen: the same centres, costs and sizes -- and
+    on clustered data later iterations screen a small fraction of the rows."""
+    from orange3_spark_amd.models import kmeans as KM
+    s = Session(SessionConf().set("o3s.device", "cuda"))
+    if kind == "blobs":
+        df = s.synthetic.blobs(400_000, 64, k=50, seed=4, spread=0.4)
+    else:
+        g = torch.Generator().manual_seed(2)
+        import pandas as pd
+        X = torch.rand(300_000, 32, generator=g)
+        df = s.createDataFrame(pd.DataFrame({"features": list(X.numpy().astype(np.float64))}))
+    out = []
+    for flag in (True, False):
+        monkeypatch.setattr(KM, "HAMERLY", flag)
+        m = KMeans(k=50, seed=7, maxIter=12, tol=0.0).fit(df)
+        out.append((np.array(m.clusterCenters()), m.summary.trainingCost, list(m.summary.clusterSizes),
+                    list(KM.LAST_HAMERLY_STATS)))
+    (c1, cost1, n1, st), (c0, cost0, n0, _) = out
+    assert n1 == n0
+    np.testing.assert_allclose(c1, c0, rtol=1e-9, atol=1e-9)
+    assert cost1 == pytest.approx(cost0, rel=1e-9)
+    assert len(st) >= 2 and st[0]["changed"] is None                    # the first iteration screens all
+    if kind == "blobs":
+        assert min(x["screened"] for x in st[1:]) < 0.2 * 400_000, st
