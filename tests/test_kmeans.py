@@ -389,9 +389,11 @@ def test_gpu_hamerly_lloyd_equals_full_screens(gpu, kind, monkeypatch):
         out.append((np.array(m.clusterCenters()), m.summary.trainingCost, list(m.summary.clusterSizes),
                     list(KM.LAST_HAMERLY_STATS)))
     (c1, cost1, n1, st), (c0, cost0, n0, _) = out
-    assert n1 == n0
-    np.testing.assert_allclose(c1, c0, rtol=1e-9, atol=1e-9)
-    assert cost1 == pytest.approx(cost0, rel=1e-9)
+    # the running sums add the changed rows' fp32 slab partials instead of re-summing all
+    # rows: centres agree to ~1e-7 relative (a row exactly on a boundary may then flip)
+    assert sum(abs(a - b) for a, b in zip(n1, n0)) <= 2
+    np.testing.assert_allclose(c1, c0, rtol=1e-5, atol=1e-6)
+    assert cost1 == pytest.approx(cost0, rel=1e-6)
     assert len(st) >= 2 and st[0]["changed"] is None                    # the first iteration screens all
     if kind == "blobs":
         assert min(x["screened"] for x in st[1:]) < 0.2 * 400_000, st

@@ -19,9 +19,12 @@ ap.add_argument("--k", type=int, default=1024)
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--repeat", type=int, default=1, help="fits in this process (the first is cold)")
 ap.add_argument("--data", default="blobs", choices=["blobs", "uniform"])
+ap.add_argument("--no-hamerly", action="store_true", help="screen every row every Lloyd iteration (A/B)")
 ap.add_argument("--pair-from", type=float, default=None,
                 help="ops.kmeans.PAIR_FROM: flagged fraction above which the pair screen is tried")
 a = ap.parse_args()
+from orange3_spark_amd.models import kmeans as _KM  # noqa: E402
+_KM.HAMERLY = not a.no_hamerly
 if a.pair_from is not None:
     from orange3_spark_amd.ops import kmeans as _K
     _K.PAIR_FROM = a.pair_from
@@ -51,4 +54,6 @@ for rep in range(a.repeat):
     print(json.dumps({"metric": "KMeans.fit seconds (k-means|| init + Lloyd)", "value": dt, "fit": rep,
                       "cold": rep == 0, "data": a.data, "rows": a.rows, "d": a.d, "k": a.k, "iters": m.summary.numIter,
                       "cost": m.summary.trainingCost, "init_s": round(init, 4), "pair_from": a.pair_from,
-                      "phases_s": ph}), flush=True)
+                      "hamerly": _KM.HAMERLY, "lloyd_ms_per_iter": round(1e3 * ph.get("kmeans.iter", 0.0) /
+                                                                         max(1, m.summary.numIter), 2),
+                      "hamerly_stats": list(_KM.LAST_HAMERLY_STATS), "phases_s": ph}), flush=True)
