@@ -23,11 +23,12 @@ for name, order in (("seq", torch.arange(n, device=dev, dtype=torch.int32)),
         lo, hi = cuts[:-1].contiguous(), cuts[1:].contiguous()
         node = torch.arange(nseg, device=dev)
         for chunk in (1 << 13, 1 << 15):
-            T.node_hist(bins, order, y, None, lo, hi, node, nseg, B, 3, False, chunk=chunk)
+            yp = y[order.long()].contiguous()          # position-ordered labels (the GBT path)
+            T.node_hist(bins, order, yp, None, lo, hi, node, nseg, B, 3, False, chunk=chunk, ypos=True)
             torch.cuda.synchronize()
             t = time.perf_counter()
             for _ in range(3):
-                T.node_hist(bins, order, y, None, lo, hi, node, nseg, B, 3, False, chunk=chunk)
+                T.node_hist(bins, order, yp, None, lo, hi, node, nseg, B, 3, False, chunk=chunk, ypos=True)
             torch.cuda.synchronize()
             res[f"{name}_seg{nseg}_chunk{chunk}"] = round((time.perf_counter() - t) / 3 * 1e3, 3)
-print(json.dumps({"n": n, "F": F, "B": B, "ms": res}))
+print(json.dumps({"n": n, "F": F, "B": B, "pairs": os.environ.get("O3S_HIST_PAIRS", "1"), "ms": res}))
