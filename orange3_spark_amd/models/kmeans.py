@@ -350,26 +350,22 @@ def _hamerly_step(X, C, prep, ws, k, hs):
     dev = X.device
     full = hs["a"] is None
     rows = None
+    need = None
     if not full:
         # centre shifts (fp64, rounded up to a safe fp32)
         delta = (C.to(torch.float64) - hs["C"].to(torch.float64)).pow(2).sum(1).sqrt()
         delta = (delta * (1 + 1e-6) + 1e-30).float()
-        dmax = float(delta.max())
-        bnd, a = hs["bnd"], hs["a"]
-        ub = bnd[:, 0]
-        lb = bnd[:, 1]
-        ub.add_(delta[a.long()])
-        lb.sub_(dmax)
-        need = ub >= lb
-        rows = torch.nonzero(need).reshape(-1).to(torch.int32)
+        dmax = float(delta.max()) * (1 + 1e-6)
+        rows = K.bounds_recheck(hs["a"], hs["bnd"], delta, dmax)
         full = rows.numel() > HAMERLY_FULL_FRACTION * n
+        need = int(rows.numel())
     if full:
         a = torch.empty(n, dtype=torch.int32, device=dev) if hs["a"] is None else hs["a"]
         bnd = torch.empty((n, 2), dtype=torch.float32, device=dev) if hs["bnd"] is None else hs["bnd"]
         K.assign_bounded(X, prep, a, bnd, None)
         S, cnt = K.update(X, a, ws.K, ws)
         S, cnt = S[:k].clone(), cnt[:k].clone()
-        st = {"screened": n, "changed": None}
+        st = {"screened": n, "changed": None, "recheck": None if hs["a"] is None else need}
     else:
         a, bnd = hs["a"], hs["bnd"]
         a_old = a[rows.long()].clone()

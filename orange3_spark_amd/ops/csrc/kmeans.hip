@@ -1165,6 +1165,51 @@ O3S_API int o3s_kmeans_screen2(const float* X, int64_t n, int64_t ldx, int Dx, c
   return 0;
 }
 
+// ---------------------------------------------------------------------------------
+// Hamerly bound update of a Lloyd iteration (models/kmeans.py): per row, the upper bound
+// on the distance to its centre grows by that centre's shift and the lower bound on every
+// other centre shrinks by the largest shift; rows whose bounds no longer certify their
+// centre (ub >= lb) are appended to `rows` (one atomic per wave; the caller sorts them).
+__global__ __launch_bounds__(256) void kmeans_bounds_kernel(const int32_t* __restrict__ a, float2* __restrict__ bnd,
+                                                            int64_t n, const float* __restrict__ delta, float dmax,
+                                                            int32_t* __restrict__ cnt, int32_t* __restrict__ rows) {
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+    const int64_t i = base + threadIdx.x;
+    bool need = false;
+    if (i < n) {
+      float2 b = bnd[i];
+      b.x += delta[a[i]];
+      b.y -= dmax;
+      bnd[i] = b;
+      need = !(b.x < b.y);                           // NaN / inf bounds: recheck
+    }
+    const uint64_t m = __ballot(need);
+    if (m) {
+      const int leader = __ffsll((unsigned long long)m) - 1;
+      int b0 = 0;
+      if (lane == leader) b0 = atomicAdd(cnt, (int)__popcll(m));
+      b0 = __shfl(b0, leader, 64);
+      if (need) rows[b0 + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+    }
+  }
+}
+
+// a: int32 [n] centres; bnd: fp32 [n][2] (ub, lb) updated in place; delta: fp32 [K] centre
+// shifts (rounded up); cnt (zeroed by the caller) / rows [n]: rows to screen again.
+O3S_API int o3s_kmeans_bounds(const int32_t* a, float* bnd, int64_t n, const float* delta, float dmax, int32_t* cnt,
+                              int32_t* rows, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n > 0x7fffffffll) return -1;
+  const int64_t blocks = (n + 255) / 256;
+  const unsigned grid = (unsigned)(blocks < 8192 ? blocks : 8192);
+  hipLaunchKernelGGL(kmeans_bounds_kernel, dim3(grid), dim3(256), 0, st, a, reinterpret_cast<float2*>(bnd), n, delta,
+                     dmax, cnt, rows);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
 // The screen without row list / bounds (the original entry point).
 O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
                               const float* C32, int ldc, int Cpad, float eps_x, float eps0, float xscale,

@@ -20,8 +20,6 @@
 // CLS (S = #classes: weighted class counts -- gini/entropy).
 #include "common.h"
 
-#include <stdlib.h>
-
 
 using namespace o3s;
 
@@ -62,11 +60,7 @@ __device__ __forceinline__ gbytes scalar_row(const uint8_t* base, int32_t row, i
 // YP: y / w are stored in POSITION order (y[p] belongs to row order[p]; the partition
 // moves them with the rows), so they stream contiguously instead of costing one random
 // cache-line gather each per row -- only the 64-B bins row is gathered.
-// PR (REG, one row-slot per wave): rows are taken in PAIRS per LDS round trip.  Both
-// cells are read, then written second-row first: when both rows hit the same bin (same
-// cell), the first row's value carries the second's too and its store lands last, so the
-// cell ends right either way -- two dependent read-modify-writes become one.
-template <int FP, bool CLS, bool HW, bool YP, int U, bool PR = false>
+template <int FP, bool CLS, bool HW, bool YP, int U>
 __global__ __launch_bounds__(kHistThreads, 5) void tree_hist_kernel(
     const uint8_t* __restrict__ bins, int F, int fg0, int B, int S, const int32_t* __restrict__ order,
     const float* __restrict__ y, const float* __restrict__ w, const int64_t* __restrict__ item_lo,
@@ -145,29 +139,12 @@ __global__ __launch_bounds__(kHistThreads, 5) void tree_hist_kernel(
         const float wl0 = jl < nl ? wv : 0.f;
         const float wyl = wl0 * yv;
         if (lane < CH) wy2 = fmaf(wyl, yv, wy2);
-        if constexpr (PR) {
 #pragma unroll
-          for (int q = 0; q < CH; q += 2) {
-            const float2_ v0 = {__int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl0), q)),
-                                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wyl), q))};
-            const float2_ v1 = {__int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl0), q + 1)),
-                                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wyl), q + 1))};
-            float2_* c0 = reinterpret_cast<float2_*>(my + (bo[q] * FP + f) * 2);
-            float2_* c1 = reinterpret_cast<float2_*>(my + (bo[q + 1] * FP + f) * 2);
-            const float2_ o0 = *c0, o1 = *c1;
-            const bool same = bo[q] == bo[q + 1];
-            const float2_ z = {0.f, 0.f};
-            *c1 = o1 + v1;
-            *c0 = o0 + v0 + (same ? v1 : z);                    // same cell: this store is last
-          }
-        } else {
-#pragma unroll
-          for (int q = 0; q < CH; ++q) {
-            const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl0), q));
-            const float wyq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wyl), q));
-            float2_* cell = reinterpret_cast<float2_*>(my + (bo[q] * FP + f) * 2);
-            *cell += float2_{wq, wyq};
-          }
+        for (int q = 0; q < CH; ++q) {
+          const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl0), q));
+          const float wyq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wyl), q));
+          float2_* cell = reinterpret_cast<float2_*>(my + (bo[q] * FP + f) * 2);
+          *cell += float2_{wq, wyq};
         }
       }
     };
@@ -1201,15 +1178,6 @@ O3S_API int o3s_tree_part_dest(const int64_t* it_lo, const int64_t* it_hi, const
   return 0;
 }
 
-// O3S_HIST_PAIRS=0 switches the paired-row histogram update off (A/B timing).
-static bool hist_pairs() {
-  static const int v = [] {
-    const char* e = getenv("O3S_HIST_PAIRS");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return v != 0;
-}
-
 // Shared-memory bytes needed for (F-group width fp, B bins, S stats); 0 if it cannot fit.
 O3S_API int o3s_tree_hist_lds(int fp, int B, int S, int cls) {
   const int RS = 64 / fp;
@@ -1233,12 +1201,8 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
   const int64_t stride = (int64_t)F * B * S;
   for (int fg0 = 0; fg0 < F; fg0 += fp) {
 #define O3S_TH2(FPV, C, W, P)                                                                           \
-  if (FPV == 64 && !C && hist_pairs())                                                                  \
-    hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, 8, true>), dim3(n_items), dim3(kHistThreads), lds, st,  \
-                       bins, F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);                     \
-  else                                                                                                  \
-    hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, 8>), dim3(n_items), dim3(kHistThreads), lds, st, bins, \
-                       F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
+  hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, 8>), dim3(n_items), dim3(kHistThreads), lds, st, bins,   \
+                     F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
 #define O3S_TH1(FPV, C, W)                                                                              \
   if (ypos) { O3S_TH2(FPV, C, W, true) } else { O3S_TH2(FPV, C, W, false) }
 #define O3S_TH(FPV)                                                                                     \

@@ -348,6 +348,23 @@ def assign_bounded(X: torch.Tensor, P: Prepared, a: torch.Tensor, bnd: torch.Ten
                 "kmeans_assign(recheck)")
 
 
+def bounds_recheck(a: torch.Tensor, bnd: torch.Tensor, delta: torch.Tensor, dmax: float) -> torch.Tensor:
+    """Move the Hamerly bounds by the centre shifts (ub += delta[a], lb -= dmax, in place)
+    and return the rows (int32, ascending) whose bounds no longer certify their centre."""
+    n = a.shape[0]
+    if a.is_cuda:
+        cnt, rows = _SWS.get(n, a.device)
+        cnt.zero_()
+        d32 = delta.to(torch.float32).contiguous()
+        N.check(N.kernels().o3s_kmeans_bounds(a.data_ptr(), bnd.data_ptr(), n, d32.data_ptr(), Ct.c_float(dmax),
+                                              cnt.data_ptr(), rows.data_ptr(), N.stream_of(a)), "kmeans_bounds")
+        m = int(cnt.item())
+        return torch.sort(rows[:m])[0] if m else rows[:0]
+    bnd[:, 0] += delta[a.long()].to(bnd.dtype)
+    bnd[:, 1] -= dmax
+    return torch.nonzero(~(bnd[:, 0] < bnd[:, 1])).reshape(-1).to(torch.int32)
+
+
 class UpdateWorkspace:
     def __init__(self, device, K: int, D: int, grid: int | None = None):
         self.K, self.D = K, D
