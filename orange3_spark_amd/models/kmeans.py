@@ -356,9 +356,8 @@ def _hamerly_step(X, C, prep, ws, k, hs):
         delta = (C.to(torch.float64) - hs["C"].to(torch.float64)).pow(2).sum(1).sqrt()
         delta = (delta * (1 + 1e-6) + 1e-30).float()
         dmax = float(delta.max()) * (1 + 1e-6)
-        rows = K.bounds_recheck(hs["a"], hs["bnd"], delta, dmax)
-        full = rows.numel() > HAMERLY_FULL_FRACTION * n
-        need = int(rows.numel())
+        need, rows = K.bounds_recheck(hs["a"], hs["bnd"], delta, dmax, int(HAMERLY_FULL_FRACTION * n))
+        full = rows is None
     if full:
         a = torch.empty(n, dtype=torch.int32, device=dev) if hs["a"] is None else hs["a"]
         bnd = torch.empty((n, 2), dtype=torch.float32, device=dev) if hs["bnd"] is None else hs["bnd"]
@@ -375,9 +374,14 @@ def _hamerly_step(X, C, prep, ws, k, hs):
         S, cnt = hs["S"], hs["n"]
         if ch.numel():
             Xc = X[ch.long()]
-            s1, c1 = K.update(Xc, a_new[a_new != a_old].contiguous(), ws.K, ws)
+            # a grid sized to the changed rows (every block zeroes and sums a [Kp, D] slab)
+            sub = hs.get("ws_sub")
+            g = int(max(1, min(ws.grid, -(-ch.numel() // 16384))))
+            if sub is None or sub.grid != g:
+                sub = hs["ws_sub"] = K.UpdateWorkspace(dev, ws.K, X.shape[1], grid=g)
+            s1, c1 = K.update(Xc, a_new[a_new != a_old].contiguous(), ws.K, sub)
             s1, c1 = s1[:k].clone(), c1[:k].clone()
-            s0, c0 = K.update(Xc, a_old[a_new != a_old].contiguous(), ws.K, ws)
+            s0, c0 = K.update(Xc, a_old[a_new != a_old].contiguous(), ws.K, sub)
             S = S + (s1 - s0[:k])
             cnt = cnt + (c1 - c0[:k])
         st = {"screened": int(rows.numel()), "changed": int(ch.numel())}
@@ -446,7 +450,7 @@ def _fit_kmeans_rows(comm, X, k, max_iter, tol, seed, init, init_steps, initial,
     # (fp64 running sums, deterministic slab kernel on the changed rows).
     ham = (HAMERLY and weights is None and ws is not None and K.screen_ok(X) and X.shape[0] > 0
            and not cosine)
-    hs = {"a": None, "bnd": None, "S": None, "n": None, "C": None}
+    hs = {"a": None, "bnd": None, "S": None, "n": None, "C": None, "ws_sub": None}
     stats_it = []
     for it in range(start + 1, max_iter + 1):
         progress.iteration(it - 1, max_iter)

@@ -139,12 +139,22 @@ __global__ __launch_bounds__(kHistThreads, 5) void tree_hist_kernel(
         const float wl0 = jl < nl ? wv : 0.f;
         const float wyl = wl0 * yv;
         if (lane < CH) wy2 = fmaf(wyl, yv, wy2);
+        if (!HW && jb + j0w + CH <= nl) {
+          // unit weights, a full chunk: w = 1 for every row -- one broadcast per row
 #pragma unroll
-        for (int q = 0; q < CH; ++q) {
-          const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl0), q));
-          const float wyq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wyl), q));
-          float2_* cell = reinterpret_cast<float2_*>(my + (bo[q] * FP + f) * 2);
-          *cell += float2_{wq, wyq};
+          for (int q = 0; q < CH; ++q) {
+            const float wyq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wyl), q));
+            float2_* cell = reinterpret_cast<float2_*>(my + (bo[q] * FP + f) * 2);
+            *cell += float2_{1.f, wyq};
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < CH; ++q) {
+            const float wq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wl0), q));
+            const float wyq = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wyl), q));
+            float2_* cell = reinterpret_cast<float2_*>(my + (bo[q] * FP + f) * 2);
+            *cell += float2_{wq, wyq};
+          }
         }
       }
     };

@@ -348,9 +348,12 @@ def assign_bounded(X: torch.Tensor, P: Prepared, a: torch.Tensor, bnd: torch.Ten
                 "kmeans_assign(recheck)")
 
 
-def bounds_recheck(a: torch.Tensor, bnd: torch.Tensor, delta: torch.Tensor, dmax: float) -> torch.Tensor:
-    """Move the Hamerly bounds by the centre shifts (ub += delta[a], lb -= dmax, in place)
-    and return the rows (int32, ascending) whose bounds no longer certify their centre."""
+def bounds_recheck(a: torch.Tensor, bnd: torch.Tensor, delta: torch.Tensor, dmax: float,
+                   max_rows: int | None = None):
+    """Move the Hamerly bounds by the centre shifts (ub += delta[a], lb -= dmax, in place);
+    returns (count, rows): the rows (int32, ascending) whose bounds no longer certify their
+    centre, or rows = None when there are more than ``max_rows`` of them (the caller then
+    screens every row: no list is sorted)."""
     n = a.shape[0]
     if a.is_cuda:
         cnt, rows = _SWS.get(n, a.device)
@@ -359,13 +362,20 @@ def bounds_recheck(a: torch.Tensor, bnd: torch.Tensor, delta: torch.Tensor, dmax
         N.check(N.kernels().o3s_kmeans_bounds(a.data_ptr(), bnd.data_ptr(), n, d32.data_ptr(), Ct.c_float(dmax),
                                               cnt.data_ptr(), rows.data_ptr(), N.stream_of(a)), "kmeans_bounds")
         m = int(cnt.item())
-        return torch.sort(rows[:m])[0] if m else rows[:0]
+        if max_rows is not None and m > max_rows:
+            return m, None
+        return m, (torch.sort(rows[:m])[0] if m else rows[:0].clone())
     bnd[:, 0] += delta[a.long()].to(bnd.dtype)
     bnd[:, 1] -= dmax
-    return torch.nonzero(~(bnd[:, 0] < bnd[:, 1])).reshape(-1).to(torch.int32)
+    r = torch.nonzero(~(bnd[:, 0] < bnd[:, 1])).reshape(-1).to(torch.int32)
+    m = int(r.numel())
+    return m, (None if max_rows is not None and m > max_rows else r)
 
 
 class UpdateWorkspace:
+    """Slab workspace of the update kernel: ``grid`` blocks, each with a private [Kp, D]
+    fp32 slab (zeroed per call, summed in a fixed order)."""
+
     def __init__(self, device, K: int, D: int, grid: int | None = None):
         self.K, self.D = K, D
         self.grid = grid or N.num_cus(device) * 2
