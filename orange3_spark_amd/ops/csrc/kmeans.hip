@@ -1168,44 +1168,75 @@ O3S_API int o3s_kmeans_screen2(const float* X, int64_t n, int64_t ldx, int Dx, c
 // ---------------------------------------------------------------------------------
 // Hamerly bound update of a Lloyd iteration (models/kmeans.py): per row, the upper bound
 // on the distance to its centre grows by that centre's shift and the lower bound on every
-// other centre shrinks by the largest shift; rows whose bounds no longer certify their
-// centre (ub >= lb) are appended to `rows` (one atomic per wave; the caller sorts them).
-__global__ __launch_bounds__(256) void kmeans_bounds_kernel(const int32_t* __restrict__ a, float2* __restrict__ bnd,
-                                                            int64_t n, const float* __restrict__ delta, float dmax,
-                                                            int32_t* __restrict__ cnt, int32_t* __restrict__ rows) {
-  const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+// other centre shrinks by the largest shift; a row whose bounds no longer certify its
+// centre (ub >= lb, or NaN) must be screened again.  Two passes, no atomics, rows in
+// ascending order: block b owns the contiguous rows [b R, (b + 1) R); pass 0 updates the
+// bounds and counts the block's rows to recheck; pass 1 (only when the caller wants the
+// list) writes them at the block's prefix offset, ranked by ballots in row order.
+constexpr int kBndThreads = 256;
+
+__device__ __forceinline__ bool bnd_recheck(float2 b) { return !(b.x < b.y); }
+
+__global__ __launch_bounds__(kBndThreads) void kmeans_bounds_kernel(
+    const int32_t* __restrict__ a, float2* __restrict__ bnd, int64_t n, int64_t per_block,
+    const float* __restrict__ delta, float dmax, int pass, int32_t* __restrict__ cnt,
+    const int64_t* __restrict__ offs, int32_t* __restrict__ rows) {
+  __shared__ int wtot[kBndThreads / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.x * per_block;
+  const int64_t r1 = r0 + per_block < n ? r0 + per_block : n;
+  int64_t out = pass ? offs[blockIdx.x] : 0;
+  int total = 0;
+  for (int64_t base = r0; base < r1; base += kBndThreads) {
     const int64_t i = base + threadIdx.x;
     bool need = false;
-    if (i < n) {
-      float2 b = bnd[i];
-      b.x += delta[a[i]];
-      b.y -= dmax;
-      bnd[i] = b;
-      need = !(b.x < b.y);                           // NaN / inf bounds: recheck
+    if (i < r1) {
+      float2 bv = bnd[i];
+      if (pass == 0) {
+        bv.x += delta[a[i]];
+        bv.y -= dmax;
+        bnd[i] = bv;
+      }
+      need = bnd_recheck(bv);
     }
     const uint64_t m = __ballot(need);
-    if (m) {
-      const int leader = __ffsll((unsigned long long)m) - 1;
-      int b0 = 0;
-      if (lane == leader) b0 = atomicAdd(cnt, (int)__popcll(m));
-      b0 = __shfl(b0, leader, 64);
-      if (need) rows[b0 + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+    if (pass == 0) {
+      total += __popcll(m);                                  // wave-uniform
+      continue;
+    }
+    if (lane == 0) wtot[wid] = __popcll(m);
+    __syncthreads();
+    int before = 0, all = 0;
+#pragma unroll
+    for (int q = 0; q < kBndThreads / 64; ++q) {
+      before += q < wid ? wtot[q] : 0;
+      all += wtot[q];
+    }
+    if (need) rows[out + before + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
+    out += all;
+    __syncthreads();                                       // wtot reused next chunk
+  }
+  if (pass == 0) {
+    if (lane == 0) wtot[wid] = total;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int q = 0; q < kBndThreads / 64; ++q) t += wtot[q];
+      cnt[blockIdx.x] = t;
     }
   }
 }
 
-// a: int32 [n] centres; bnd: fp32 [n][2] (ub, lb) updated in place; delta: fp32 [K] centre
-// shifts (rounded up); cnt (zeroed by the caller) / rows [n]: rows to screen again.
-O3S_API int o3s_kmeans_bounds(const int32_t* a, float* bnd, int64_t n, const float* delta, float dmax, int32_t* cnt,
-                              int32_t* rows, hipStream_t st) {
+// pass 0: a int32 [n] centres, bnd fp32 [n][2] (ub, lb) moved in place by delta (fp32 [K],
+// rounded up) / dmax; cnt int32 [grid] = rows to recheck per block.  pass 1: offs int64
+// [grid] (exclusive prefix of cnt) -> rows int32 (ascending).  Rows per block: ceil(n / grid).
+O3S_API int o3s_kmeans_bounds(const int32_t* a, float* bnd, int64_t n, const float* delta, float dmax, int pass,
+                              int32_t* cnt, const int64_t* offs, int32_t* rows, int grid, hipStream_t st) {
   if (n <= 0) return 0;
-  if (n > 0x7fffffffll) return -1;
-  const int64_t blocks = (n + 255) / 256;
-  const unsigned grid = (unsigned)(blocks < 8192 ? blocks : 8192);
-  hipLaunchKernelGGL(kmeans_bounds_kernel, dim3(grid), dim3(256), 0, st, a, reinterpret_cast<float2*>(bnd), n, delta,
-                     dmax, cnt, rows);
+  if (n > 0x7fffffffll || grid <= 0 || (pass == 1 && (!offs || !rows))) return -1;
+  const int64_t per_block = (n + grid - 1) / grid;
+  hipLaunchKernelGGL(kmeans_bounds_kernel, dim3(grid), dim3(kBndThreads), 0, st, a, reinterpret_cast<float2*>(bnd),
+                     n, per_block, delta, dmax, pass, cnt, offs, rows);
   O3S_CHECK_LAUNCH();
   return 0;
 }

@@ -356,15 +356,24 @@ def bounds_recheck(a: torch.Tensor, bnd: torch.Tensor, delta: torch.Tensor, dmax
     screens every row: no list is sorted)."""
     n = a.shape[0]
     if a.is_cuda:
-        cnt, rows = _SWS.get(n, a.device)
-        cnt.zero_()
+        dev = a.device
+        grid = int(max(1, min(N.num_cus(dev) * 8, -(-n // 4096))))
+        cnt = torch.empty(grid, dtype=torch.int32, device=dev)
         d32 = delta.to(torch.float32).contiguous()
-        N.check(N.kernels().o3s_kmeans_bounds(a.data_ptr(), bnd.data_ptr(), n, d32.data_ptr(), Ct.c_float(dmax),
-                                              cnt.data_ptr(), rows.data_ptr(), N.stream_of(a)), "kmeans_bounds")
-        m = int(cnt.item())
+        lib, st = N.kernels(), N.stream_of(a)
+        N.check(lib.o3s_kmeans_bounds(a.data_ptr(), bnd.data_ptr(), n, d32.data_ptr(), Ct.c_float(dmax), 0,
+                                      cnt.data_ptr(), None, None, grid, st), "kmeans_bounds")
+        offs = torch.cumsum(cnt.to(torch.int64), 0)
+        m = int(offs[-1])
         if max_rows is not None and m > max_rows:
             return m, None
-        return m, (torch.sort(rows[:m])[0] if m else rows[:0].clone())
+        rows = torch.empty(m, dtype=torch.int32, device=dev)
+        if m:
+            offs = offs - cnt.to(torch.int64)                  # exclusive prefix
+            N.check(lib.o3s_kmeans_bounds(a.data_ptr(), bnd.data_ptr(), n, d32.data_ptr(), Ct.c_float(dmax), 1,
+                                          cnt.data_ptr(), offs.data_ptr(), rows.data_ptr(), grid, st),
+                    "kmeans_bounds(list)")
+        return m, rows
     bnd[:, 0] += delta[a.long()].to(bnd.dtype)
     bnd[:, 1] -= dmax
     r = torch.nonzero(~(bnd[:, 0] < bnd[:, 1])).reshape(-1).to(torch.int32)
