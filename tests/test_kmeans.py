@@ -397,3 +397,26 @@ def test_gpu_hamerly_lloyd_equals_full_screens(gpu, kind, monkeypatch):
     assert len(st) >= 2 and st[0]["changed"] is None                    # the first iteration screens all
     if kind == "blobs":
         assert min(x["screened"] for x in st[1:]) < 0.2 * 400_000, st
+
+
+@pytest.mark.gpu
+def test_gpu_bounds_recheck_matches_torch(gpu):
+    """The Hamerly bound update kernel (two passes, block-prefix compaction): the same
+    moved bounds and the same ascending recheck list as the torch reference."""
+    g = torch.Generator().manual_seed(9)
+    n, Kc = 1_000_003, 77
+    a = torch.randint(0, Kc, (n,), generator=g, dtype=torch.int32)
+    ub = torch.rand(n, generator=g) * 2
+    lb = ub + torch.randn(n, generator=g) * 0.3
+    lb[::1000] = float("nan")
+    bnd = torch.stack([ub, lb], 1).contiguous()
+    delta = torch.rand(Kc, generator=g) * 0.05
+    dmax = float(delta.max())
+    b_ref = bnd.clone()
+    m_ref, r_ref = K.bounds_recheck(a, b_ref, delta, dmax)
+    b_gpu = bnd.to(gpu)
+    m, r = K.bounds_recheck(a.to(gpu), b_gpu, delta.to(gpu), dmax)
+    assert m == m_ref and torch.equal(r.cpu(), r_ref)
+    assert torch.equal(b_gpu.cpu(), b_ref)
+    m2, r2 = K.bounds_recheck(a.to(gpu), bnd.clone().to(gpu), delta.to(gpu), dmax, max_rows=10)
+    assert m2 == m_ref and r2 is None
