@@ -417,6 +417,6 @@ def test_gpu_bounds_recheck_matches_torch(gpu):
     b_gpu = bnd.to(gpu)
     m, r = K.bounds_recheck(a.to(gpu), b_gpu, delta.to(gpu), dmax)
     assert m == m_ref and torch.equal(r.cpu(), r_ref)
-    assert torch.equal(b_gpu.cpu(), b_ref)
+    torch.testing.assert_close(b_gpu.cpu(), b_ref, rtol=0, atol=0, equal_nan=True)
     m2, r2 = K.bounds_recheck(a.to(gpu), bnd.clone().to(gpu), delta.to(gpu), dmax, max_rows=10)
     assert m2 == m_ref and r2 is None
