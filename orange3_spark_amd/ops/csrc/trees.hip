@@ -20,6 +20,8 @@
 // CLS (S = #classes: weighted class counts -- gini/entropy).
 #include "common.h"
 
+#include <stdlib.h>
+
 
 using namespace o3s;
 
@@ -60,8 +62,14 @@ __device__ __forceinline__ gbytes scalar_row(const uint8_t* base, int32_t row, i
 // YP: y / w are stored in POSITION order (y[p] belongs to row order[p]; the partition
 // moves them with the rows), so they stream contiguously instead of costing one random
 // cache-line gather each per row -- only the 64-B bins row is gathered.
-template <int FP, bool CLS, bool HW, bool YP, int U>
-__global__ __launch_bounds__(kHistThreads, 5) void tree_hist_kernel(
+// DMA (one row-slot per wave, F % 16 == 0): the chunk's 32 rows are fetched by two LDS-DMA
+// instructions (global_load_lds_dwordx4: 4 lanes x 16 B per row, 16 rows each) into a
+// per-wave double-buffered stage, and each lane reads its feature's byte from LDS.  The
+// per-row 64-lane byte gathers it replaces kept the texture addresser ~86% busy
+// (TA_TA_BUSY, profiles/gbt_hist_ta_r6.json): the kernel was bound by gather ADDRESSES,
+// not bytes, LDS or VALU.
+template <int FP, bool CLS, bool HW, bool YP, int U, bool DMA = false>
+__global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
     const uint8_t* __restrict__ bins, int F, int fg0, int B, int S, const int32_t* __restrict__ order,
     const float* __restrict__ y, const float* __restrict__ w, const int64_t* __restrict__ item_lo,
     const int64_t* __restrict__ item_hi, float* __restrict__ slab, int64_t slab_stride) {
@@ -109,11 +117,26 @@ __global__ __launch_bounds__(kHistThreads, 5) void tree_hist_kernel(
       const int32_t j = jb + j0w + (lane & (CH - 1));
       ov = ord[j < nl ? j : nl - 1];
     };
+    // DMA stage: per wave two buffers of CH rows x 64 B, after the histogram images
+    uint8_t* const stg = reinterpret_cast<uint8_t*>(hist + kHistWaves * per_wave) + wid * (2 * CH * 64);
+    const int piece = 16 * (lane & 3);
+    const bool pok = fg0 + piece < F;                // 16-B pieces past the row: a valid dummy address
     auto ld_chunk = [&](int32_t jb, int32_t ov, int (&bo)[CH], float& yv, float& wv) {
+      if constexpr (DMA) {
+        const int buf = ((jb / cstep) & 1) * (CH * 64);
 #pragma unroll
-      for (int q = 0; q < CH; ++q) {
-        const int32_t row = __builtin_amdgcn_readlane(ov, q);
-        bo[q] = scalar_row(bins, row, F)[(uint32_t)fc];
+        for (int k = 0; k < CH / 16; ++k) {
+          const int32_t row = __shfl(ov, 16 * k + (lane >> 2), 64);
+          const uint8_t* src = pok ? bins + (int64_t)row * F + fg0 + piece : bins;
+          __builtin_amdgcn_global_load_lds(src, stg + buf + k * 1024, 16, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);         // the DMAs before this chunk's y / w loads
+      } else {
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+          const int32_t row = __builtin_amdgcn_readlane(ov, q);
+          bo[q] = scalar_row(bins, row, F)[(uint32_t)fc];
+        }
       }
       const int32_t j = jb + j0w + (lane & (CH - 1));
       const int32_t jc = j < nl ? j : nl - 1;
@@ -122,7 +145,21 @@ __global__ __launch_bounds__(kHistThreads, 5) void tree_hist_kernel(
     };
     // (Grouping rows so several LDS read-modify-writes share one wait -- duplicates
     // merged first -- measured slower: the extra VALU outweighs the LDS round trips.)
-    auto acc_chunk = [&](int32_t jb, const int (&bo)[CH], float yv, float wv) {
+    auto acc_chunk = [&](int32_t jb, const int (&bo_r)[CH], float yv, float wv) {
+      int bo[CH];
+      if constexpr (DMA) {
+        // this chunk's DMAs have landed once at most the VMEM ops issued after them are
+        // outstanding: its y (+ w), the next chunk's order[] load, its two DMAs and its y
+        // (+ w) -- 4 (+ 2) at the least whatever order the compiler gave y / w and the DMAs
+        if constexpr (HW) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        const int buf = ((jb / cstep) & 1) * (CH * 64);
+#pragma unroll
+        for (int q = 0; q < CH; ++q) bo[q] = stg[buf + q * 64 + f];
+      } else {
+#pragma unroll
+        for (int q = 0; q < CH; ++q) bo[q] = bo_r[q];
+      }
       if constexpr (CLS) {
 #pragma unroll
         for (int q = 0; q < CH; ++q) {
@@ -1188,6 +1225,17 @@ O3S_API int o3s_tree_part_dest(const int64_t* it_lo, const int64_t* it_hi, const
   return 0;
 }
 
+constexpr int kHistDmaBytes = kHistWaves * 2 * 32 * 64;   // two 32-row x 64-B stages per wave
+
+// O3S_HIST_DMA=0: the per-row byte gathers instead of the LDS-DMA row stage (A/B timing)
+static bool hist_dma() {
+  static const bool v = [] {
+    const char* e = getenv("O3S_HIST_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // Shared-memory bytes needed for (F-group width fp, B bins, S stats); 0 if it cannot fit.
 O3S_API int o3s_tree_hist_lds(int fp, int B, int S, int cls) {
   const int RS = 64 / fp;
@@ -1208,11 +1256,18 @@ O3S_API int o3s_tree_hist(const uint8_t* bins, int64_t n, int F, int B, int S, i
   if (fp < 4) fp = 4;
   const int lds = o3s_tree_hist_lds(fp, B, S, cls);
   if (lds == 0) return -2;
+  // the LDS-DMA row stage: 16-B aligned rows and room beside the images
+  const bool dma = fp == 64 && F % 16 == 0 && ((uintptr_t)bins & 15) == 0 && lds + kHistDmaBytes <= 160 * 1024 &&
+                   hist_dma();
   const int64_t stride = (int64_t)F * B * S;
   for (int fg0 = 0; fg0 < F; fg0 += fp) {
 #define O3S_TH2(FPV, C, W, P)                                                                           \
-  hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, 8>), dim3(n_items), dim3(kHistThreads), lds, st, bins,   \
-                     F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
+  if (FPV == 64 && dma)                                                                                 \
+    hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, 8, true>), dim3(n_items), dim3(kHistThreads),        \
+                       lds + kHistDmaBytes, st, bins, F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride); \
+  else                                                                                                  \
+    hipLaunchKernelGGL((tree_hist_kernel<FPV, C, W, P, 8>), dim3(n_items), dim3(kHistThreads), lds, st, bins, \
+                       F, fg0, B, S, order, y, w, item_lo, item_hi, slab, stride);
 #define O3S_TH1(FPV, C, W)                                                                              \
   if (ypos) { O3S_TH2(FPV, C, W, true) } else { O3S_TH2(FPV, C, W, false) }
 #define O3S_TH(FPV)                                                                                     \

@@ -69,7 +69,8 @@ def test_gbt_save_load(cpu, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F,B,S,cls", [(64, 32, 3, False), (10, 16, 3, False), (64, 32, 2, True), (100, 32, 4, True)])
+@pytest.mark.parametrize("F,B,S,cls", [(64, 32, 3, False), (10, 16, 3, False), (64, 32, 2, True), (100, 32, 4, True),
+                                      (80, 32, 3, False), (96, 16, 2, True)])
 def test_gpu_hist_matches_torch(gpu, F, B, S, cls):
     from orange3_spark_amd.ops import trees as T
     g = torch.Generator(device="cpu").manual_seed(F + B)
