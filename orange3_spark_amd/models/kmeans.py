@@ -77,22 +77,19 @@ def kmeans_parallel_init(comm, X: torch.Tensor, k: int, steps: int, seed: int) -
     last = None                        # (labels, distances) of the last round's assign
     n_before = 0                       # candidates the last round assigned against
     for step in range(steps):
-        tr = trace("kmeans.init.round")
-        tr.__enter__()
-        a, d = K.assign(X, centers.float(), mode="approx")
-        cost = torch.sum(d, dtype=torch.float64)        # no fp64 copy of d
-        comm.all_reduce(cost)
-        if float(cost) <= 0:
-            tr.__exit__(None, None, None)
-            break
-        last, n_before = (a, d), centers.shape[0]
-        p = (d * (2.0 * k / float(cost))).clamp_(max=1.0)
-        u = sampling.uniform(rows, seed + 1 + step, stream=7)
-        new = X[u < p].to(torch.float64)
-        del p, u
-        new = comm.all_gather_v(new) if comm.world_size > 1 else new
-        centers = torch.cat([centers, new.to(dev)])
-        tr.__exit__(None, None, None)
+        with trace("kmeans.init.round"):
+            a, d = K.assign(X, centers.float(), mode="approx")
+            cost = torch.sum(d, dtype=torch.float64)        # no fp64 copy of d
+            comm.all_reduce(cost)
+            if float(cost) <= 0:
+                break
+            last, n_before = (a, d), centers.shape[0]
+            p = (d * (2.0 * k / float(cost))).clamp_(max=1.0)
+            u = sampling.uniform(rows, seed + 1 + step, stream=7)
+            new = X[u < p].to(torch.float64)
+            del p, u
+            new = comm.all_gather_v(new) if comm.world_size > 1 else new
+            centers = torch.cat([centers, new.to(dev)])
     # weights = number of points closest to each candidate.  The last round already holds
     # every row's nearest candidate among the first n_before: only the candidates that
     # round added are assigned now, and a row moves to one of them only if it is strictly
@@ -155,42 +152,40 @@ def _local_kmeanspp(P: torch.Tensor, w: torch.Tensor, k: int, seed: int, iters: 
     # the centres themselves are the fp64 candidates
     Pr = P.float().double()
     pn = (Pr * Pr).sum(1)
-    tr = trace("kmeans.init.local.seed")
-    tr.__enter__()
-    if kernel and P.is_cuda and trials <= 16 and trials * P.shape[1] * 8 <= 64 * 1024:
-        # the k greedy steps as 2 launches each (kpp_dist_kernel over every candidate row,
-        # kpp_pick_kernel in one block): no host round trip inside the loop
-        from ..ops import _native as N
-        wc, pc = w.to(torch.float64).contiguous(), pn.contiguous()
-        PT = P.float().t().contiguous()           # fp32 [D][m]: coalesced candidate reads
-        Uc = U.contiguous()
-        d2 = torch.empty(m, dtype=torch.float64, device=dev)
-        cs = torch.empty(m, dtype=torch.float64, device=dev)
-        cd = torch.empty((trials, m), dtype=torch.float64, device=dev)
-        partial = torch.empty((-(-m // 256), 16), dtype=torch.float64, device=dev)
-        cand = torch.empty(16, dtype=torch.int32, device=dev)
-        picks32 = torch.empty(k, dtype=torch.int32, device=dev)
-        N.check(N.kernels().o3s_kmeanspp(PT.data_ptr(), wc.data_ptr(), pc.data_ptr(), m, P.shape[1], k, trials,
-                                         Uc.data_ptr(), d2.data_ptr(), cs.data_ptr(), cd.data_ptr(),
-                                         partial.data_ptr(), cand.data_ptr(), picks32.data_ptr(), N.stream_of(PT)),
-                "kmeanspp")
-        picks = picks32.to(torch.int64)
-    else:
-        first = draw(0, w, 1)[0]
-        picks = torch.empty(k, dtype=torch.int64, device=dev)
-        picks[0] = first
-        d2 = ((Pr - Pr[first]) ** 2).sum(1)
-        for t in range(1, k):
-            cand = draw(t, w * d2, trials)
-            # [trials, m] squared distances as |p|^2 + |c|^2 - 2 c.p: one small fp64 GEMM
-            # instead of a [trials, m, D] difference tensor per step
-            cd = (pn[None, :] + pn[cand][:, None] - 2.0 * (Pr[cand] @ Pr.T)).clamp_min_(0.0)
-            pot = (w[None, :] * torch.minimum(d2[None, :], cd)).sum(1)
-            best = pot.argmin()
-            picks[t] = cand[best]
-            d2 = torch.minimum(d2, cd[best])
-    C = P[picks]
-    tr.__exit__(None, None, None)
+    with trace("kmeans.init.local.seed"):
+        if kernel and P.is_cuda and trials <= 16 and trials * P.shape[1] * 8 <= 64 * 1024:
+            # the k greedy steps as 2 launches each (kpp_dist_kernel over every candidate row,
+            # kpp_pick_kernel in one block): no host round trip inside the loop
+            from ..ops import _native as N
+            wc, pc = w.to(torch.float64).contiguous(), pn.contiguous()
+            PT = P.float().t().contiguous()           # fp32 [D][m]: coalesced candidate reads
+            Uc = U.contiguous()
+            d2 = torch.empty(m, dtype=torch.float64, device=dev)
+            cs = torch.empty(m, dtype=torch.float64, device=dev)
+            cd = torch.empty((trials, m), dtype=torch.float64, device=dev)
+            partial = torch.empty((-(-m // 256), 16), dtype=torch.float64, device=dev)
+            cand = torch.empty(16, dtype=torch.int32, device=dev)
+            picks32 = torch.empty(k, dtype=torch.int32, device=dev)
+            N.check(N.kernels().o3s_kmeanspp(PT.data_ptr(), wc.data_ptr(), pc.data_ptr(), m, P.shape[1], k, trials,
+                                             Uc.data_ptr(), d2.data_ptr(), cs.data_ptr(), cd.data_ptr(),
+                                             partial.data_ptr(), cand.data_ptr(), picks32.data_ptr(), N.stream_of(PT)),
+                    "kmeanspp")
+            picks = picks32.to(torch.int64)
+        else:
+            first = draw(0, w, 1)[0]
+            picks = torch.empty(k, dtype=torch.int64, device=dev)
+            picks[0] = first
+            d2 = ((Pr - Pr[first]) ** 2).sum(1)
+            for t in range(1, k):
+                cand = draw(t, w * d2, trials)
+                # [trials, m] squared distances as |p|^2 + |c|^2 - 2 c.p: one small fp64 GEMM
+                # instead of a [trials, m, D] difference tensor per step
+                cd = (pn[None, :] + pn[cand][:, None] - 2.0 * (Pr[cand] @ Pr.T)).clamp_min_(0.0)
+                pot = (w[None, :] * torch.minimum(d2[None, :], cd)).sum(1)
+                best = pot.argmin()
+                picks[t] = cand[best]
+                d2 = torch.minimum(d2, cd[best])
+        C = P[picks]
     with trace("kmeans.init.local.lloyd"):
         return _local_lloyd(P, w, C, k, iters)
 

@@ -419,37 +419,35 @@ class TreeBuilder:
                     Hs = Hs.to(torch.float64).contiguous()
                     self.comm.all_reduce(Hs)
                     H = T.sibling_hists(Hs, parent_H, small_right, self.cls)
-            tsplit = trace("tree.split")
-            tsplit.__enter__()
-            fm = None
-            if self.ffrac < 1.0:
-                m = max(1, int(math.ceil(self.ffrac * F)))
-                fm = np.zeros((k, F), dtype=bool)
-                for t in np.unique(seg_tree):                     # each tree draws from its own stream:
-                    rows_t = np.nonzero(seg_tree == t)[0]         # m of F features per node, uniformly
-                    keys = rngs[t].random((len(rows_t), F))
-                    pick = np.argpartition(keys, m - 1, axis=1)[:, :m] if m < F else \
-                        np.broadcast_to(np.arange(F), (len(rows_t), F))
-                    fm[rows_t[:, None], pick] = True
-            # min child weight: at the root a fraction of its total weight (Spark
-            # minWeightFractionPerNode), below it the absolute value that gave, per tree
-            mw_frac = self.min_wfrac if depth == 0 else 0.0
-            mw_node = (self.min_wfrac * root_w[seg_tree]) if (depth > 0 and self.min_wfrac > 0.0) else None
-            if H.is_cuda:
-                bundle_t = T.best_splits(H, nb, fm, self.kind, self.min_inst, 0.0, mw_frac, mw_node)
-            else:
-                bundle_t = _split_bundle_torch(H, self.kind, self.cls, nb, bin_ids, fm, self.min_inst, 0.0,
-                                               mw_frac, mw_node)
-            # ONE device->host copy of every per-node decision input
-            bundle = bundle_t.cpu().numpy()
-            bi = bundle[:k].astype(np.int64)
-            bg, imp_np, w_np, wl_np, wr_np = (bundle[q * k:(q + 1) * k] for q in range(1, 6))
-            vals_np = bundle[6 * k:].reshape(k, V)
-            if depth == 0:
-                root_w = w_np.copy()
-            bf, bb = bi // (B - 1), bi % (B - 1)
-            do_split = (bg > self.min_gain) & (bg > 0) & np.isfinite(bg) & (depth < self.max_depth)
-            tsplit.__exit__(None, None, None)
+            with trace("tree.split"):
+                fm = None
+                if self.ffrac < 1.0:
+                    m = max(1, int(math.ceil(self.ffrac * F)))
+                    fm = np.zeros((k, F), dtype=bool)
+                    for t in np.unique(seg_tree):                     # each tree draws from its own stream:
+                        rows_t = np.nonzero(seg_tree == t)[0]         # m of F features per node, uniformly
+                        keys = rngs[t].random((len(rows_t), F))
+                        pick = np.argpartition(keys, m - 1, axis=1)[:, :m] if m < F else \
+                            np.broadcast_to(np.arange(F), (len(rows_t), F))
+                        fm[rows_t[:, None], pick] = True
+                # min child weight: at the root a fraction of its total weight (Spark
+                # minWeightFractionPerNode), below it the absolute value that gave, per tree
+                mw_frac = self.min_wfrac if depth == 0 else 0.0
+                mw_node = (self.min_wfrac * root_w[seg_tree]) if (depth > 0 and self.min_wfrac > 0.0) else None
+                if H.is_cuda:
+                    bundle_t = T.best_splits(H, nb, fm, self.kind, self.min_inst, 0.0, mw_frac, mw_node)
+                else:
+                    bundle_t = _split_bundle_torch(H, self.kind, self.cls, nb, bin_ids, fm, self.min_inst, 0.0,
+                                                   mw_frac, mw_node)
+                # ONE device->host copy of every per-node decision input
+                bundle = bundle_t.cpu().numpy()
+                bi = bundle[:k].astype(np.int64)
+                bg, imp_np, w_np, wl_np, wr_np = (bundle[q * k:(q + 1) * k] for q in range(1, 6))
+                vals_np = bundle[6 * k:].reshape(k, V)
+                if depth == 0:
+                    root_w = w_np.copy()
+                bf, bb = bi // (B - 1), bi % (B - 1)
+                do_split = (bg > self.min_gain) & (bg > 0) & np.isfinite(bg) & (depth < self.max_depth)
             old_order = order
             is_leaf = ~do_split                                # segments that end here
             if do_split.any() and depth == self.max_depth - 1 and self.final_from_parent:
@@ -465,27 +463,25 @@ class TreeBuilder:
             if do_split.any():
                 # the partition is launched first: the tree bookkeeping and the leaf
                 # updates below run on the host while it executes
-                tpart = trace("tree.partition")
-                tpart.__enter__()
-                st, sn = seg_tree[do_split], seg_nid[do_split]
-                s_lo, s_hi = seg_lo[do_split], seg_hi[do_split]
-                pay = (yp,) if wp is None else (yp, wp)
-                if pingpong:
-                    pout = (y_sp,) if wp is None else (y_sp, w_sp)
-                    new_order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
-                                                   bins_t=self.bins_t, out=spare, payload=pay, payload_out=pout)
-                    spare, order = order, new_order
-                    y_sp, yp = yp, y_sp
-                    w_sp, wp = wp, w_sp
-                else:
-                    pout = tuple(t.clone() for t in pay)
-                    order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
-                                               bins_t=self.bins_t, payload=pay, payload_out=pout)
-                    yp, wp = pout[0], (pout[1] if len(pout) > 1 else None)
-                # integer gather (a boolean mask index would sync on the device-side nonzero)
-                parent_H = H.index_select(0, N.upload(np.nonzero(do_split)[0], dev))
-                small_right = (wr_np < wl_np)[do_split]
-                tpart.__exit__(None, None, None)
+                with trace("tree.partition"):
+                    st, sn = seg_tree[do_split], seg_nid[do_split]
+                    s_lo, s_hi = seg_lo[do_split], seg_hi[do_split]
+                    pay = (yp,) if wp is None else (yp, wp)
+                    if pingpong:
+                        pout = (y_sp,) if wp is None else (y_sp, w_sp)
+                        new_order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
+                                                       bins_t=self.bins_t, out=spare, payload=pay, payload_out=pout)
+                        spare, order = order, new_order
+                        y_sp, yp = yp, y_sp
+                        w_sp, wp = wp, w_sp
+                    else:
+                        pout = tuple(t.clone() for t in pay)
+                        order, nleft = T.partition(self.bins, order, s_lo, s_hi, bf[do_split], bb[do_split],
+                                                   bins_t=self.bins_t, payload=pay, payload_out=pout)
+                        yp, wp = pout[0], (pout[1] if len(pout) > 1 else None)
+                    # integer gather (a boolean mask index would sync on the device-side nonzero)
+                    parent_H = H.index_select(0, N.upload(np.nonzero(do_split)[0], dev))
+                    small_right = (wr_np < wl_np)[do_split]
             value[seg_tree, seg_nid] = vals_np
             impurity[seg_tree, seg_nid] = imp_np
             count[seg_tree, seg_nid] = w_np
@@ -496,18 +492,16 @@ class TreeBuilder:
                                  leaf_acc)
             if not do_split.any():
                 break
-            tpart = trace("tree.partition")
-            tpart.__enter__()
-            feature[st, sn] = bf[do_split]
-            split_bin[st, sn] = bb[do_split]
-            threshold[st, sn] = [float(self.splits[f_][b_]) for f_, b_ in zip(bf[do_split], bb[do_split])]
-            gain[st, sn] = bg[do_split]
-            mid = s_lo + nleft.cpu().numpy().astype(np.int64)
-            seg_lo = np.stack([s_lo, mid], 1).reshape(-1)
-            seg_hi = np.stack([mid, s_hi], 1).reshape(-1)
-            seg_tree = np.repeat(st, 2)
-            seg_nid = np.stack([2 * sn, 2 * sn + 1], 1).reshape(-1)
-            tpart.__exit__(None, None, None)
+            with trace("tree.partition"):
+                feature[st, sn] = bf[do_split]
+                split_bin[st, sn] = bb[do_split]
+                threshold[st, sn] = [float(self.splits[f_][b_]) for f_, b_ in zip(bf[do_split], bb[do_split])]
+                gain[st, sn] = bg[do_split]
+                mid = s_lo + nleft.cpu().numpy().astype(np.int64)
+                seg_lo = np.stack([s_lo, mid], 1).reshape(-1)
+                seg_hi = np.stack([mid, s_hi], 1).reshape(-1)
+                seg_tree = np.repeat(st, 2)
+                seg_nid = np.stack([2 * sn, 2 * sn + 1], 1).reshape(-1)
             # empty local segments still participate (other ranks may have rows there)
         return [Tree(feature[t], threshold[t], split_bin[t], value[t], impurity[t], gain[t], count[t], F)
                 for t in range(Tn)]
@@ -643,34 +637,32 @@ def fit_gbt(comm, bins, splits, y: torch.Tensor, w, loss: str = "logistic", max_
         wt = 1.0 if m == 0 else step
         with progress.sub_range(m / max_iter, (m + 1) / max_iter):
             tree, _ = tb.build(leaf_acc=Fm, leaf_scale=wt)      # Fm += wt * leaf value, per row
-        tu = trace("gbt.update")
-        tu.__enter__()
-        trees.append(tree)
-        weights.append(wt)
-        if fused:
-            # ONE row-order pass: every row walks the tree (Fm += wt * leaf), the loss of the
-            # updated ensemble, the next tree's residuals (into the target buffer: the build
-            # is done with it) and the last level's w*y^2 sums
-            nxt = target if m + 1 < max_iter else None
-            need_y2 = tb.pending_y2 is not None
-            buf, y2 = T.gbt_leaf_pass(bins, tree.feature, tree.split_bin, tree.value, wt, max_depth, loss, yy, Fm,
-                                      sw, wd, w_val, m == 0, nxt, need_y2)
-            if need_y2:
-                both = torch.cat([buf, y2]).contiguous()
-                comm.all_reduce(both)
-                buf = both[:4]
-                tb.complete_final(tree, both[4:].cpu().numpy())
+        with trace("gbt.update"):
+            trees.append(tree)
+            weights.append(wt)
+            if fused:
+                # ONE row-order pass: every row walks the tree (Fm += wt * leaf), the loss of the
+                # updated ensemble, the next tree's residuals (into the target buffer: the build
+                # is done with it) and the last level's w*y^2 sums
+                nxt = target if m + 1 < max_iter else None
+                need_y2 = tb.pending_y2 is not None
+                buf, y2 = T.gbt_leaf_pass(bins, tree.feature, tree.split_bin, tree.value, wt, max_depth, loss, yy, Fm,
+                                          sw, wd, w_val, m == 0, nxt, need_y2)
+                if need_y2:
+                    both = torch.cat([buf, y2]).contiguous()
+                    comm.all_reduce(both)
+                    buf = both[:4]
+                    tb.complete_final(tree, both[4:].cpu().numpy())
+                else:
+                    comm.all_reduce(buf)
+                target = nxt
             else:
+                # one fused pass: this iteration's (validation) loss and the next tree's residuals
+                target = torch.empty_like(target) if m + 1 < max_iter else None
+                buf = T.gbt_grad_loss(loss, yy, Fm, wd, w_val, target)
                 comm.all_reduce(buf)
-            target = nxt
-        else:
-            # one fused pass: this iteration's (validation) loss and the next tree's residuals
-            target = torch.empty_like(target) if m + 1 < max_iter else None
-            buf = T.gbt_grad_loss(loss, yy, Fm, wd, w_val, target)
-            comm.all_reduce(buf)
-        sums = buf.cpu().numpy()
-        losses.append(float(sums[0] / max(sums[1], 1e-300)))
-        tu.__exit__(None, None, None)
+            sums = buf.cpu().numpy()
+            losses.append(float(sums[0] / max(sums[1], 1e-300)))
         if validation is not None:
             err = float(sums[2] / max(sums[3], 1e-300))
             if m == 0:

@@ -65,9 +65,9 @@ __device__ __forceinline__ gbytes scalar_row(const uint8_t* base, int32_t row, i
 // DMA (one row-slot per wave, F % 16 == 0): the chunk's 32 rows are fetched by two LDS-DMA
 // instructions (global_load_lds_dwordx4: 4 lanes x 16 B per row, 16 rows each) into a
 // per-wave double-buffered stage, and each lane reads its feature's byte from LDS.  The
-// per-row 64-lane byte gathers it replaces kept the texture addresser ~86% busy
-// (TA_TA_BUSY, profiles/gbt_hist_ta_r6.json): the kernel was bound by gather ADDRESSES,
-// not bytes, LDS or VALU.
+// per-row 64-lane byte gathers it replaces kept the texture addressers ~55% busy
+// (TA_BUSY_avr, profiles/kernel_experiments_r6.json); taking them off buys 3-5% on every
+// layout -- the rest is the dependent LDS read-add-write chain per row.
 template <int FP, bool CLS, bool HW, bool YP, int U, bool DMA = false>
 __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
     const uint8_t* __restrict__ bins, int F, int fg0, int B, int S, const int32_t* __restrict__ order,
