@@ -55,10 +55,9 @@ _SIGS: dict[str, list] = {
     "o3s_bin_sums": [c_vp, c_i32, c_i64, c_i64, c_i32, c_vp, c_i64, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp],
     "o3s_glm_softmax": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_vp, c_i32, c_vp, c_i32, c_vp, c_vp],
     "o3s_kmeans_assign": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp, c_vp, c_vp, c_vp],
-    "o3s_kmeans_screen": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, C.c_float, C.c_float,
-                          C.c_float, C.c_float, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp],
     "o3s_kmeans_screen2": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, C.c_float, C.c_float,
-                           C.c_float, C.c_float, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp],
+                           C.c_float, C.c_float, C.c_float, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp, c_vp,
+                           c_vp, c_vp],
     "o3s_kmeans_presplit": [c_vp, c_i64, c_i64, c_i32, C.c_float, c_vp, c_vp, c_vp],
     "o3s_kmeans_bounds": [c_vp, c_vp, c_i64, c_vp, C.c_float, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp],
     "o3s_kmeans_update_ws": [c_i32, c_i32, c_i32, C.POINTER(c_i64), C.POINTER(c_i64), C.POINTER(c_i32)],

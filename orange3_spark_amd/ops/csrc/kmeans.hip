@@ -56,6 +56,17 @@ __device__ __forceinline__ void split_f16(float v, float scale, short& hi, short
   lo = __builtin_bit_cast(short, (_Float16)(sv - (float)h));
 }
 
+// as split_f16, also returning the scaled rounding error of the hi half (exact in fp32:
+// the hi half is the fp16 rounding of sv, so sv - hi is representable)
+__device__ __forceinline__ float split_f16e(float v, float scale, short& hi, short& lo) {
+  const float sv = v * scale;
+  const _Float16 h = (_Float16)sv;
+  const float d = sv - (float)h;
+  hi = __builtin_bit_cast(short, h);
+  lo = __builtin_bit_cast(short, (_Float16)d);
+  return d;
+}
+
 __device__ __forceinline__ float f16_bits_to_f32(uint32_t bits16) {
   return (float)__builtin_bit_cast(_Float16, (uint16_t)bits16);
 }
@@ -299,16 +310,19 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
 // host) and rounded to fp16 (11 significant bits, 8x finer than bf16), so the screened
 // distance S d~_c = S ||c||^2 + (m ms)~.(x xs)~ with S = xs ms differs from S (||c||^2 -
 // 2 x.c) by at most S E, where (derivation in ops/kmeans.py::screen_bound)
-//   E = eps_x ||x|| + eps0,   eps_x ~ (2^-8 + 2^-16) max||c||,   eps0: fp16 underflow of
-//   tiny elements and the fp32 ||c||^2 rounding
-// with a 2x margin.  Each lane tracks best, index and SECOND best (one v_med3: the new
+//   E = eps_x ||x|| + eps_e' ||dx|| + eps0,   dx = fp16(x xs)/xs - x: the row's ACTUAL
+//   rounding error (its norm comes with ||x||^2 from the prologue / the pre-split rows),
+//   eps_x = max_c ||fp16(m_c ms)/ms - m_c|| (+ fp32 accumulation), eps_e' ~ max||m||
+// -- Cauchy-Schwarz on the actual rounding errors instead of 2^-11 per element: ~5x
+// tighter on data with full mantissas (profiles/kernel_experiments_r6.json)
+// Each lane tracks best, index and SECOND best (one v_med3: the new
 // second is med3(old best, v, old second)); a row whose margin (second - best) exceeds
 // 2E has provably the same arg-min as the exact product and is finished here: its
 // squared distance is recomputed exactly in fp32 from the register-resident split x
 // (fp16 hi + lo, ~22 bits) and the fp32 centre row.  Other rows (near-ties) are appended
 // to a compacted list (one atomic per wave) and re-solved by the split-precision kernel
 // above.  This is 1/3 of the MFMAs of the split kernel; the S ||c||^2 bias is folded
-// into the accumulator init (read from LDS).  The epilogue is 3 VALU per distance and
+// into the accumulator init (read from LDS).  The epilogue is 2.5 VALU per distance and
 // touches no VCC: the candidate's slot in its chunk (0..15) replaces the low 4 mantissa
 // bits of the distance (v_and_or: a perturbation below 2^-19 of its magnitude, added to
 // the bound), so best = v_min and second = v_med3 carry the index with them; the chunk
@@ -342,9 +356,9 @@ template <int KS, int TT, bool PAIR, bool PS = false, bool NOD = false>
 __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const float* __restrict__ X, int64_t n, int64_t ldx, const uint16_t* __restrict__ Chi,
     const float* __restrict__ cn, const float* __restrict__ C32, int ldc, int Cpad, float eps_x, float eps0,
-    float xscale, float sscale, int32_t* __restrict__ assign, float* __restrict__ mind,
+    float eps_e, float xscale, float sscale, int32_t* __restrict__ assign, float* __restrict__ mind,
     int32_t* __restrict__ flag_cnt, int32_t* __restrict__ flag_rows, int Dx,
-    const uint4* __restrict__ XP = nullptr, const float* __restrict__ XN = nullptr,
+    const uint4* __restrict__ XP = nullptr, const float2* __restrict__ XN = nullptr,
     const int32_t* __restrict__ rowlist = nullptr, float2* __restrict__ bnd = nullptr) {
   using L = ScrLds<KS>;
   constexpr int D = L::D;
@@ -372,7 +386,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
   // transposed reads).
   float* xt = reinterpret_cast<float*>(lds) + wid * 32 * D;
   bf16x8 bh[TT][KS], bl[TT][KS];
-  float xn[TT];
+  float xn[TT], xe[TT];                    // ||x||^2 and ||x xs - fp16(x xs)||^2 per row
   if constexpr (PS) {
     // pre-split rows (kmeans_presplit_kernel, once per data version): per row and
     // (k-step, half) group 16 B of scaled fp16 hi then 16 B of lo, loaded straight into the
@@ -393,7 +407,9 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
         bh[t][ks] = __builtin_bit_cast(bf16x8, hv[ks]);
         if constexpr (!NOD) bl[t][ks] = __builtin_bit_cast(bf16x8, lv[ks]);
       }
-      xn[t] = XN[rowc];
+      const float2 ne = XN[rowc];
+      xn[t] = ne.x;
+      xe[t] = ne.y;
     }
   } else {
 #pragma unroll
@@ -416,7 +432,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       *reinterpret_cast<float4*>(xt + rr * D + 4 * (sl ^ (rr & (XS - 1) & 31))) = xv[q];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    float s = 0.f;
+    float s = 0.f, e = 0.f;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int s0 = (ks * 16 + 8 * h) / 4;
@@ -428,12 +444,14 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         short h0, l0, h1, l1;
-        split_f16(v[2 * j], xscale, h0, l0);
-        split_f16(v[2 * j + 1], xscale, h1, l1);
+        const float d0 = split_f16e(v[2 * j], xscale, h0, l0);
+        const float d1 = split_f16e(v[2 * j + 1], xscale, h1, l1);
         ph[j] = (uint32_t)(uint16_t)h0 | ((uint32_t)(uint16_t)h1 << 16);
         pl[j] = (uint32_t)(uint16_t)l0 | ((uint32_t)(uint16_t)l1 << 16);
         s = fmaf(v[2 * j], v[2 * j], s);
         s = fmaf(v[2 * j + 1], v[2 * j + 1], s);
+        e = fmaf(d0, d0, e);
+        e = fmaf(d1, d1, e);
       }
       bh[t][ks] = __builtin_bit_cast(bf16x8, ph);
       bl[t][ks] = __builtin_bit_cast(bf16x8, pl);
@@ -441,6 +459,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       else asm volatile("" : "+v"(bh[t][ks]), "+v"(bl[t][ks]));
     }
     xn[t] = s + __shfl_xor(s, 32, 64);
+    xe[t] = e + __shfl_xor(e, 32, 64);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slice reads done before the next tile
   }
   }
@@ -448,7 +467,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
 
   const int nchunks = Cpad / 32;
   // one stage = G centroid chunks, DMA'd into dbuf (per-thread offsets from a uniform stage base)
-  auto stage = [&](int stg, uint16_t* __restrict__ dbuf) {
+  auto stage = [&](int stg, uint16_t* __restrict__ dbuf) __attribute__((always_inline)) {
     const uint16_t* sbase = Chi + (int64_t)stg * G * CH_ELEMS;
 #pragma unroll
     for (int k = 0; k < PER_THREAD; ++k) {
@@ -475,7 +494,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
   for (int t = 0; t < TT; ++t) {
     best[t] = INFINITY; second[t] = INFINITY; third[t] = INFINITY; bidx[t] = 0; sidx[t] = 0; bch[t] = 0;
   }
-  auto epilogue = [&](const f32x16 (&a)[TT], int ch) {
+  auto epilogue = [&](const f32x16 (&a)[TT], int ch) __attribute__((always_inline)) {
     if constexpr (PAIR) {
 #pragma unroll
       for (int t = 0; t < TT; ++t) {                     // re-base onto this chunk
@@ -499,24 +518,33 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       }
     }
   };
-  // plain screen: one distance of the previous chunk (element e of E = 16 TT, tiles
-  // interleaved) folded into the running (best, second) keys
-  auto epi_step = [&](const f32x16 (&a)[TT], int e) {
-    const int t = e % TT, i = e / TT;
-    const float key = __uint_as_float((__float_as_uint(a[t][i]) & 0xfffffff0u) | (uint32_t)i);
-    second[t] = __builtin_amdgcn_fmed3f(best[t], key, second[t]);
-    // v_min_f32 itself: fminf would canonicalise the (bit-built) key first
-    asm("v_min_f32 %0, %1, %2" : "=v"(best[t]) : "v"(best[t]), "v"(key));
+  // plain screen: two distances of the previous chunk (pair e of E = 8 TT, tiles
+  // interleaved) folded into the running (best, second) keys.  With best <= second, the
+  // second smallest of {best, second, ka, kb} is min(second, med3(best, ka, kb)): 3 VALU
+  // per PAIR (med3, min3, min) plus the two slot codes -- 2.5 VALU per distance where one
+  // distance at a time took 3 (med3, min, slot), which left the SIMD's issue port, not
+  // the matrix core, setting the pace (103 VALU per 16 MFMAs of a chunk).
+  auto epi_step = [&](const f32x16 (&a)[TT], int e) __attribute__((always_inline)) {
+    const int t = e % TT, i = 2 * (e / TT);
+    const float ka = __uint_as_float((__float_as_uint(a[t][i]) & 0xfffffff0u) | (uint32_t)i);
+    const float kb = __uint_as_float((__float_as_uint(a[t][i + 1]) & 0xfffffff0u) | (uint32_t)(i + 1));
+    float m3, b3, s2;
+    // the instructions themselves: fminf / fmed3 would canonicalise the (bit-built) keys
+    asm("v_med3_f32 %0, %1, %2, %3" : "=v"(m3) : "v"(best[t]), "v"(ka), "v"(kb));
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(b3) : "v"(best[t]), "v"(ka), "v"(kb));
+    asm("v_min_f32 %0, %1, %2" : "=v"(s2) : "v"(second[t]), "v"(m3));
+    best[t] = b3;
+    second[t] = s2;
   };
   // one chunk's MFMAs: accumulators start at ||c||^2 (bias folded into the first MFMA's C)
   // One chunk's MFMAs (accumulators start at S ||c||^2, the bias folded into the first
   // MFMA's C).  EPI: the previous chunk's epilogue (accumulator old, chunk ch_old) is
-  // spread over the k-steps, E/KS distances after each step's MFMAs, so the wave issues
+  // spread over the k-steps, E/KS distance pairs after each step's MFMAs, so the wave issues
   // that VALU work while its own MFMAs occupy the matrix pipe.
   auto sweep = [&](auto epi_tag, const uint16_t* Lh, const float* sc, int ch, f32x16 (&acc)[TT],
-                   const f32x16 (&old)[TT], int ch_old) {
+                   const f32x16 (&old)[TT], int ch_old) __attribute__((always_inline)) {
     constexpr bool EPI = decltype(epi_tag)::value;
-    constexpr int E = 16 * TT;
+    constexpr int E = 8 * TT;                                     // distance pairs
     const int cbase = ch * 32 + 4 * h;
     f32x16 c0;
 #pragma unroll
@@ -524,7 +552,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       const float4 c4 = *reinterpret_cast<const float4*>(sc + cbase + 8 * q);
       c0[4 * q + 0] = c4.x; c0[4 * q + 1] = c4.y; c0[4 * q + 2] = c4.z; c0[4 * q + 3] = c4.w;
     }
-    auto afrag = [&](int ks) {
+    auto afrag = [&](int ks) __attribute__((always_inline)) {
       const int sw = (ks * 2 + h) ^ (r & 15 & (SLOTS - 1));
       return *reinterpret_cast<const bf16x8*>(Lh + r * D + sw * 8);
     };
@@ -572,7 +600,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
   // touch the next stage's in-flight DMA (otherwise it drains that DMA, vmcnt(0), before
   // the first read of every chunk).  G is even, so chunk pairs never straddle stages.
   auto run_stage = [&](int stg, const uint16_t* __restrict__ cur, uint16_t* __restrict__ nxt,
-                       const float* __restrict__ sc) {
+                       const float* __restrict__ sc) __attribute__((always_inline)) {
     if (stg + 1 < nstages) stage(stg + 1, nxt);
 #pragma unroll
     for (int g = 0; g < G; g += 2) {
@@ -611,10 +639,10 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     for (int t = 0; t < TT; ++t) b0[t] = best[t];
     if (lastA) {
 #pragma unroll
-      for (int e = 0; e < 16 * TT; ++e) epi_step(accA, e);
+      for (int e = 0; e < 8 * TT; ++e) epi_step(accA, e);
     } else {
 #pragma unroll
-      for (int e = 0; e < 16 * TT; ++e) epi_step(accB, e);
+      for (int e = 0; e < 8 * TT; ++e) epi_step(accB, e);
     }
 #pragma unroll
     for (int t = 0; t < TT; ++t) bch[t] = best[t] != b0[t] ? nchunks - 1 : bch[t];
@@ -711,7 +739,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
     const int64_t row = rowlist ? (int64_t)rowlist[ok ? row_l : 0] : row_l;   // the data row
     // in the scaled units of bv, sec; the plain screen's slot codes move each key by less
     // than 2^-19 of its magnitude (twice that allowed for)
-    float bound = 2.f * sscale * (eps_x * sqrtf(xn[t]) + eps0);
+    float bound = 2.f * (sscale * (eps_x * sqrtf(xn[t]) + eps0) + eps_e * sqrtf(xe[t]));
     if constexpr (!PAIR) bound += 0x1p-18f * (fabsf(bv) + fabsf(sec));
     bool fl = ok && (!(sec - bv > bound) || !idx_ok);      // near-tie (or NaN): exact re-solve
     int pick = idc;
@@ -1051,8 +1079,8 @@ O3S_API int o3s_kmeans_assign(const float* X, int64_t n, int64_t ldx, int Dx, co
 }
 
 // Screen pass (see kmeans_screen_kernel).  Ch16: fp16 bits of -2 C ms [Cpad][D]; C32: fp32
-// centres [K][ldc] (ldc % 4 == 0); bound E = eps_x ||x|| + eps0 (unscaled units); xscale =
-// xs, sscale = xs ms; flag_cnt (zeroed by the caller) / flag_rows [n]: near-tie rows for
+// centres [K][ldc] (ldc % 4 == 0); bound S E = S (eps_x ||x|| + eps0) + eps_e ||dx xs||
+// (eps_e = eps_e' ms: the error norm is kept in the scaled units); xscale = xs, sscale = xs ms; flag_cnt (zeroed by the caller) / flag_rows [n]: near-tie rows for
 // o3s_kmeans_assign(rowlist).  tt: 32-row tiles per wave (1 or 2).
 namespace {
 // X (fp32 [n][ldx], Dx valid columns) -> the screen kernel's pre-split rows: per row D/8
@@ -1062,12 +1090,12 @@ namespace {
 template <int D>
 __global__ __launch_bounds__(256) void kmeans_presplit_kernel(const float* __restrict__ X, int64_t n, int64_t ldx,
                                                               int Dx, float xscale, uint4* __restrict__ XP,
-                                                              float* __restrict__ XN) {
+                                                              float2* __restrict__ XN) {
   constexpr int G = D / 8;                     // groups per row (power of two up to 64 lanes)
   const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t row = tid / G;
   const int g = (int)(tid % G);
-  float s = 0.f;
+  float s = 0.f, e = 0.f;
   if (row < n) {
     uint32_t ph[4], pl[4];
 #pragma unroll
@@ -1076,26 +1104,32 @@ __global__ __launch_bounds__(256) void kmeans_presplit_kernel(const float* __res
       const float v0 = c0 < Dx ? X[row * ldx + c0] : 0.f;
       const float v1 = c0 + 1 < Dx ? X[row * ldx + c0 + 1] : 0.f;
       short h0, l0, h1, l1;
-      split_f16(v0, xscale, h0, l0);
-      split_f16(v1, xscale, h1, l1);
+      const float d0 = split_f16e(v0, xscale, h0, l0);
+      const float d1 = split_f16e(v1, xscale, h1, l1);
       ph[j] = (uint32_t)(uint16_t)h0 | ((uint32_t)(uint16_t)h1 << 16);
       pl[j] = (uint32_t)(uint16_t)l0 | ((uint32_t)(uint16_t)l1 << 16);
       s = fmaf(v0, v0, s);
       s = fmaf(v1, v1, s);
+      e = fmaf(d0, d0, e);
+      e = fmaf(d1, d1, e);
     }
     XP[(row * G + g) * 2] = make_uint4(ph[0], ph[1], ph[2], ph[3]);
     XP[(row * G + g) * 2 + 1] = make_uint4(pl[0], pl[1], pl[2], pl[3]);
   }
 #pragma unroll
-  for (int o = 1; o < G; o <<= 1) s += __shfl_xor(s, o, 64);
-  if (row < n && g == 0) XN[row] = s;
+  for (int o = 1; o < G; o <<= 1) {
+    s += __shfl_xor(s, o, 64);
+    e += __shfl_xor(e, o, 64);
+  }
+  if (row < n && g == 0) XN[row] = make_float2(s, e);
 }
 }  // namespace
 
 // Pre-split rows for the screen kernel (see kmeans_presplit_kernel): XP [n][D / 8][2] x 16 B,
 // XN [n] fp32; D = Dx rounded up to 32 (<= 128).
-O3S_API int o3s_kmeans_presplit(const float* X, int64_t n, int64_t ldx, int Dx, float xscale, void* XP, float* XN,
+O3S_API int o3s_kmeans_presplit(const float* X, int64_t n, int64_t ldx, int Dx, float xscale, void* XP, float* XN2,
                                 hipStream_t st) {
+  float2* XN = reinterpret_cast<float2*>(XN2);
   if (n <= 0) return 0;
   const int D = (Dx + 31) / 32 * 32;
   if (Dx % 4 != 0 || D > 128) return -1;
@@ -1113,11 +1147,12 @@ O3S_API int o3s_kmeans_presplit(const float* X, int64_t n, int64_t ldx, int Dx, 
 }
 
 O3S_API int o3s_kmeans_screen2(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
-                               const float* C32, int ldc, int Cpad, float eps_x, float eps0, float xscale,
-                               float sscale, int32_t* assign, float* mind, int32_t* flag_cnt, int32_t* flag_rows,
-                               int tt, int pair, const void* XP, const float* XN, const int32_t* rowlist,
-                               float* bnd2, hipStream_t st) {
+                               const float* C32, int ldc, int Cpad, float eps_x, float eps0, float eps_e,
+                               float xscale, float sscale, int32_t* assign, float* mind, int32_t* flag_cnt,
+                               int32_t* flag_rows, int tt, int pair, const void* XP, const float* XN2,
+                               const int32_t* rowlist, float* bnd2, hipStream_t st) {
   float2* bnd = reinterpret_cast<float2*>(bnd2);
+  const float2* XN = reinterpret_cast<const float2*>(XN2);
   if (n <= 0) return 0;
   const int D = (Dx + 31) / 32 * 32;
   if (Dx % 4 != 0 || D > 160 || ldx % 4 != 0 || ldc % 4 != 0 || Cpad % 32 != 0 || n > 0x7fffffffll) return -1;
@@ -1136,19 +1171,19 @@ O3S_API int o3s_kmeans_screen2(const float* X, int64_t n, int64_t ldx, int Dx, c
     if (dyn > 160 * 1024) return -3;                                                                       \
     if (XP && !P && !mind)                                                                          \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, true, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, \
-                         st, X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind,     \
+                         st, X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, eps_e, xscale, sscale, assign, mind,     \
                          flag_cnt, flag_rows, Dx, (const uint4*)XP, XN, rowlist, bnd);                     \
     else if (XP && !P)                                                                                     \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, \
-                         X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt, \
+                         X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, eps_e, xscale, sscale, assign, mind, flag_cnt, \
                          flag_rows, Dx, (const uint4*)XP, XN, rowlist, bnd);                               \
     else if (!P && !mind)                                                                                  \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P, false, true>), dim3((unsigned)grid), dim3(kScrThreads), dyn, \
-                         st, X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind,     \
+                         st, X, n, ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, eps_e, xscale, sscale, assign, mind,     \
                          flag_cnt, flag_rows, Dx, nullptr, nullptr, rowlist, bnd);                         \
     else                                                                                                   \
       hipLaunchKernelGGL((kmeans_screen_kernel<KS, TT, P>), dim3((unsigned)grid), dim3(kScrThreads), dyn, st, X, n, \
-                         ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind, flag_cnt,   \
+                         ldx, hi, cn, C32, ldc, Cpad, eps_x, eps0, eps_e, xscale, sscale, assign, mind, flag_cnt,   \
                          flag_rows, Dx, nullptr, nullptr, rowlist, bnd);                                   \
   }
   switch (D / 16) {
@@ -1242,14 +1277,6 @@ O3S_API int o3s_kmeans_bounds(const int32_t* a, float* bnd, int64_t n, const flo
 }
 
 // The screen without row list / bounds (the original entry point).
-O3S_API int o3s_kmeans_screen(const float* X, int64_t n, int64_t ldx, int Dx, const void* Chi, const float* cn,
-                              const float* C32, int ldc, int Cpad, float eps_x, float eps0, float xscale,
-                              float sscale, int32_t* assign, float* mind, int32_t* flag_cnt, int32_t* flag_rows,
-                              int tt, int pair, const void* XP, const float* XN, hipStream_t st) {
-  return o3s_kmeans_screen2(X, n, ldx, Dx, Chi, cn, C32, ldc, Cpad, eps_x, eps0, xscale, sscale, assign, mind,
-                            flag_cnt, flag_rows, tt, pair, XP, XN, nullptr, nullptr, st);
-}
-
 O3S_API int o3s_kmeans_update_ws(int Kp, int D, int grid, int64_t* slab_floats, int64_t* cnt_floats,
                                  int* lds_bytes) {
   const int R = upd_rows(Kp);

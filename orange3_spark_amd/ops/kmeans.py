@@ -19,13 +19,18 @@ class Prepared:
     """Centre-side operands of the assign kernels, built once per Lloyd iteration:
     bf16 hi/lo split of -2*C [Kp, Dp] (zero padded; split kernel), fp16 of -2*C*ms with a
     power-of-two scale ms (screen kernel), ||c||^2 [Kp] (+inf padded), the fp32 centres
-    [K, D] (exact distance of screened rows) and max ||c|| (screen bound)."""
+    [K, D] (exact distance of screened rows), and for the screen bound max ||c||, the largest
+    fp16 rounding error max_c ||m^_c - m_c|| of a centre row (``dm``, m = -2c exact in fp64)
+    and max ||m^_c|| (``mmax``)."""
 
-    __slots__ = ("hi", "lo", "cn", "c32", "cmax", "h16", "ms")
+    __slots__ = ("hi", "lo", "cn", "c32", "cmax", "h16", "ms", "dm", "mmax")
 
-    def __init__(self, hi, lo, cn, c32, cmax, h16=None, ms=1.0):
+    def __init__(self, hi, lo, cn, c32, cmax, h16=None, ms=1.0, dm=None, mmax=None):
         self.hi, self.lo, self.cn, self.c32, self.cmax = hi, lo, cn, c32, cmax
         self.h16, self.ms = h16, ms
+        # without the measured errors: the worst case of fp16 rounding (2^-11 per element)
+        self.dm = 2.0 ** -10 * cmax if dm is None else dm
+        self.mmax = 2.0 * cmax * (1 + 2.0 ** -10) if mmax is None else mmax
 
     def __iter__(self):                         # legacy (hi, lo, cn) unpacking
         return iter((self.hi, self.lo, self.cn))
@@ -42,14 +47,20 @@ def prepare_centers(C: torch.Tensor) -> Prepared:
     cn = torch.full((Kp,), float("inf"), dtype=torch.float32, device=C.device)
     norms = (Cd * Cd).sum(1)
     cn[:K] = norms.float()
-    cmax = float(norms.max().sqrt()) if K else 0.0
-    ms = _pow2_scale(float(m2.abs().max()) if K else 0.0)
+    if not K:
+        return Prepared(hi.contiguous(), lo.contiguous(), cn, torch.zeros((Kp, D), device=C.device), 0.0,
+                        torch.zeros((Kp, Dp), dtype=torch.float16, device=C.device), 1.0, 0.0, 0.0)
+    ms = _pow2_scale(float(m2.abs().max()))
     h16 = (m2 * ms).to(torch.float16)
+    # the bound's centre terms from the rounded operands themselves (fp64): one host copy
+    mh = h16[:K, :D].double() / ms
+    stats = torch.stack([norms.max().sqrt(), (mh + 2.0 * Cd).norm(dim=1).max(), mh.norm(dim=1).max()]).cpu()
+    cmax, dm, mmax = (float(v) for v in stats)
     # fp32 centres padded to Kp rows (zeros): every index the screen kernel can form is a
     # valid row
     c32 = torch.zeros((Kp, D), dtype=torch.float32, device=C.device)
     c32[:K] = C.float()
-    return Prepared(hi.contiguous(), lo.contiguous(), cn, c32, cmax, h16.contiguous(), ms)
+    return Prepared(hi.contiguous(), lo.contiguous(), cn, c32, cmax, h16.contiguous(), ms, dm, mmax)
 
 
 def _pow2_scale(amax: float, top: float = 2.0 ** 15) -> float:
@@ -77,7 +88,8 @@ def x_scale(X: torch.Tensor) -> float:
 
 
 # Pre-split data for the screen kernel (kmeans_presplit_kernel): the scaled fp16 hi / lo
-# halves of every row (D * 4 bytes per row, as much as X itself) and ||x||^2, built once per
+# halves of every row (D * 4 bytes per row, as much as X itself), ||x||^2 and the squared norm
+# of the row's scaled fp16 rounding error (the screen bound's row term), built once per
 # data version and reused by every Lloyd iteration -- the kernel's prologue then loads its
 # MFMA fragments instead of converting fp32 rows.  PRESPLIT: None = auto (when X is at least
 # PRESPLIT_MIN_ROWS rows and the copy fits in half of the free HBM), True / False forces.
@@ -97,7 +109,7 @@ def presplit(X: torch.Tensor, xs: float):
     if ref is not None and ref() is X and key == k:
         return val
     _XSPLIT[:] = [None, None, None]
-    need = X.shape[0] * (D * 4 + 4)
+    need = X.shape[0] * (D * 4 + 8)
     if PRESPLIT is None:
         if X.shape[0] < PRESPLIT_MIN_ROWS:
             return None
@@ -105,7 +117,7 @@ def presplit(X: torch.Tensor, xs: float):
         if need > free // 2:
             return None
     XP = torch.empty((X.shape[0], D), dtype=torch.int32, device=X.device)
-    XN = torch.empty(X.shape[0], dtype=torch.float32, device=X.device)
+    XN = torch.empty((X.shape[0], 2), dtype=torch.float32, device=X.device)
     N.check(N.kernels().o3s_kmeans_presplit(X.data_ptr(), X.shape[0], X.stride(0), X.shape[1], Ct.c_float(xs),
                                             XP.data_ptr(), XN.data_ptr(), N.stream_of(X)), "kmeans_presplit")
     # the split copy lives no longer than X itself (and fit_kmeans drops it when it ends)
@@ -123,17 +135,37 @@ def clear_presplit() -> None:
     _XSPLIT[:] = [None, None, None]
 
 
-def screen_bound(P: "Prepared", xs: float, D: int) -> tuple[float, float]:
-    """(eps_x, eps0) of the screen kernel's error bound E = eps_x ||x|| + eps0 on
-    |d~_c - d_c| (unscaled units), with a 2x margin.  With x^ = fp16(x xs)/xs and
-    m^ = fp16(m ms)/ms, m = -2c: |x^ - x| <= 2^-11 |x| + 2^-25/xs (subnormal spacing),
-    likewise for m, so |x^.m^ - x.m| <= 2^-9 ||x|| max||c|| + 2^-24 sqrt(D) max||c|| / xs
-    + 2^-25 sqrt(D) ||x|| / ms; the fp32 accumulation adds <= 2^-17 ||x|| max||c|| and the
-    fp32 ||c||^2 term 2^-24 max||c||^2."""
-    cmax, ms, rd = P.cmax, P.ms, math.sqrt(D)
-    eps_x = 2.0 * (2.0 ** -9 + 2.0 ** -17) * cmax + 2.0 * 2.0 ** -25 * rd / ms
-    eps0 = 2.0 * (2.0 ** -24 * rd * cmax / xs + 2.0 ** -24 * cmax * cmax)
-    return eps_x, eps0
+def screen_bound(P: "Prepared", xs: float, D: int) -> tuple[float, float, float]:
+    """(eps_x, eps0, eps_e) of the screen kernel's error bound on |d~_c - d_c| (unscaled
+    partial distances d_c = ||c||^2 - 2 x.c):
+
+        E(x) = eps_x ||x|| + eps_e ||dx|| + eps0,     dx = x^ - x
+
+    With x^ = fp16(x xs)/xs, m^ = fp16(m ms)/ms and m = -2c (fp64):
+    x^.m^ - x.m = dx.m^ + x.dm, so by Cauchy-Schwarz on the ACTUAL rounding errors
+    |x^.m^ - x.m| <= ||dx|| max||m^|| + ||x|| max||dm|| -- dm and max||m^|| measured on the
+    rounded centres (``prepare_centers``), ||dx|| per row by the kernel.  The fp32
+    accumulation of S ||c||^2 and the D exact fp16 products adds <= g (||c||^2 + ||x^|| ||m^||)
+    with g = 2 (D + 2) 2^-24 (twice the textbook gamma: no assumption on the matrix core's
+    rounding mode), ||x^|| <= ||x|| + ||dx||; the fp32 ||c||^2 adds 2^-24 ||c||^2; a 2^-10
+    margin covers the bound's own fp32 evaluation.  On data with full mantissas ||dx|| is
+    ~2^-12 ||x|| against the 2^-11 per-element worst case, so E is ~5x below the
+    per-element bound this replaced (E = 2^-8 ||x|| max||c||)."""
+    Dp = (D + 31) // 32 * 32
+    g = 2.0 * (Dp + 2) * 2.0 ** -24
+    mg = 1.0 + 2.0 ** -10
+    eps_x = (P.dm + g * P.mmax) * mg
+    eps_e = P.mmax * (1.0 + g) * mg
+    eps0 = (g + 2.0 ** -23) * P.cmax * P.cmax * mg
+    return eps_x, eps0, eps_e
+
+
+def row_bound(X: torch.Tensor, P: "Prepared", xs: float) -> torch.Tensor:
+    """The screen bound E(x) of every row (fp64, torch: tests and diagnostics)."""
+    eps_x, eps0, eps_e = screen_bound(P, xs, X.shape[1])
+    Xd = X.double()
+    dx = (X * xs).half().double() / xs - Xd
+    return eps_x * Xd.norm(dim=1) + eps_e * dx.norm(dim=1) + eps0
 
 
 def kernel_ok(X: torch.Tensor) -> bool:
@@ -163,7 +195,7 @@ def assign_torch(X: torch.Tensor, C: torch.Tensor, chunk: int = 1 << 16):
     return a, d
 
 
-# screen-pass bound: see screen_bound (fp16 operands, E ~ 2^-8 ||x|| max||c||)
+# screen-pass bound: see screen_bound (fp16 operands, Cauchy-Schwarz on the actual errors)
 # auto mode: the plain screen until it flags SCREEN_MAX_FLAG_FRACTION of the rows, then the
 # split kernel for every row (re-probing the screen every SPLIT_REPROBE calls).  The pair
 # screen (top-3 tracking, two-centre near ties settled exactly in-kernel) joins the chain
@@ -264,14 +296,15 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
         cnt, rows = _SWS.get(n, X.device)
         cnt.zero_()                              # the kernel still lists its near ties (< n rows)
         xs = x_scale(X)
-        eps_x, eps0 = screen_bound(P, xs, X.shape[1])
+        eps_x, eps0, eps_e = screen_bound(P, xs, X.shape[1])
         ps = presplit(X, xs)
         tt = SCREEN_TT or (2 if X.shape[1] <= 128 else 1)
-        N.check(lib.o3s_kmeans_screen(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
-                                      P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
-                                      Ct.c_float(eps0), Ct.c_float(xs), Ct.c_float(xs * P.ms), a.data_ptr(),
-                                      N.ptr(d), cnt.data_ptr(), rows.data_ptr(), tt, 0,
-                                      N.ptr(ps[0]) if ps else None, N.ptr(ps[1]) if ps else None, st),
+        N.check(lib.o3s_kmeans_screen2(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
+                                       P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
+                                       Ct.c_float(eps0), Ct.c_float(eps_e * P.ms), Ct.c_float(xs),
+                                       Ct.c_float(xs * P.ms), a.data_ptr(), N.ptr(d), cnt.data_ptr(), rows.data_ptr(),
+                                       tt, 0, N.ptr(ps[0]) if ps else None, N.ptr(ps[1]) if ps else None, None, None,
+                                       st),
                 "kmeans_screen")
         return a, d
     if mode in ("screen", "pair") and screen_ok(X):
@@ -279,13 +312,14 @@ def assign(X: torch.Tensor, C: torch.Tensor, prepared=None, mode: str = "auto", 
         cnt.zero_()
         tt = SCREEN_TT or (2 if X.shape[1] <= 128 else 1)
         xs = x_scale(X)
-        eps_x, eps0 = screen_bound(P, xs, X.shape[1])
+        eps_x, eps0, eps_e = screen_bound(P, xs, X.shape[1])
         ps = presplit(X, xs) if mode == "screen" else None
-        N.check(lib.o3s_kmeans_screen(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
-                                      P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
-                                      Ct.c_float(eps0), Ct.c_float(xs), Ct.c_float(xs * P.ms), a.data_ptr(),
-                                      N.ptr(d), cnt.data_ptr(), rows.data_ptr(), tt, int(mode == "pair"),
-                                      N.ptr(ps[0]) if ps else None, N.ptr(ps[1]) if ps else None, st),
+        N.check(lib.o3s_kmeans_screen2(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
+                                       P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
+                                       Ct.c_float(eps0), Ct.c_float(eps_e * P.ms), Ct.c_float(xs),
+                                       Ct.c_float(xs * P.ms), a.data_ptr(), N.ptr(d), cnt.data_ptr(), rows.data_ptr(),
+                                       tt, int(mode == "pair"), N.ptr(ps[0]) if ps else None,
+                                       N.ptr(ps[1]) if ps else None, None, None, st),
                 "kmeans_screen")
         m = int(cnt.item())                      # the near-tie count sizes the re-solve grid
         frac = m / max(n, 1)
@@ -325,7 +359,7 @@ def assign_bounded(X: torch.Tensor, P: Prepared, a: torch.Tensor, bnd: torch.Ten
     cnt, flag = _SWS.get(n, X.device)
     cnt.zero_()
     xs = x_scale(X)
-    eps_x, eps0 = screen_bound(P, xs, X.shape[1])
+    eps_x, eps0, eps_e = screen_bound(P, xs, X.shape[1])
     ps = presplit(X, xs)
     tt = SCREEN_TT or (2 if X.shape[1] <= 128 else 1)
     if rows is not None and (rows.dtype != torch.int32 or not rows.is_contiguous()):
@@ -334,7 +368,8 @@ def assign_bounded(X: torch.Tensor, P: Prepared, a: torch.Tensor, bnd: torch.Ten
         raise ValueError("bnd must be fp32 [n, 2]")
     N.check(lib.o3s_kmeans_screen2(X.data_ptr(), n, X.stride(0), X.shape[1], P.h16.data_ptr(), P.cn.data_ptr(),
                                    P.c32.data_ptr(), P.c32.stride(0), P.hi.shape[0], Ct.c_float(eps_x),
-                                   Ct.c_float(eps0), Ct.c_float(xs), Ct.c_float(xs * P.ms), a.data_ptr(), None,
+                                   Ct.c_float(eps0), Ct.c_float(eps_e * P.ms), Ct.c_float(xs), Ct.c_float(xs * P.ms),
+                                   a.data_ptr(), None,
                                    cnt.data_ptr(), flag.data_ptr(), tt, 0, N.ptr(ps[0]) if ps else None,
                                    N.ptr(ps[1]) if ps else None, N.ptr(rows), bnd.data_ptr(), st),
             "kmeans_screen(bounds)")

@@ -229,8 +229,43 @@ def test_screen_scales_and_bound():
         assert a * s <= 2 ** 15 < 2 * a * s
     P = K.prepare_centers(torch.tensor([[3.0, 4.0], [0.0, 1.0]]))
     assert P.cmax == 5.0 and P.ms == K._pow2_scale(8.0)
-    ex, e0 = K.screen_bound(P, 2.0 ** 10, 2)
-    assert 2 ** -8 * 5.0 <= ex < 2 ** -7 * 5.0 and 0 < e0 < 1e-5
+    ex, e0, ee = K.screen_bound(P, 2.0 ** 10, 2)
+    # [3, 4] and [0, 1] times -2 ms are exact in fp16: only the accumulation terms remain
+    assert P.dm == 0.0 and P.mmax == 10.0
+    assert 0 < ex < 1e-4 and 10.0 <= ee < 10.01 and 0 < e0 < 1e-3
+
+
+@pytest.mark.parametrize("kind", ["uniform", "randn", "midpoints", "tiny", "huge", "offset"])
+def test_screen_bound_covers_the_fp16_product_error(kind):
+    """The screen bound (Cauchy-Schwarz on the actual fp16 rounding errors of x and -2c)
+    covers |x^.m^ - x.m| computed exactly in fp64 for every (row, centre) pair -- including
+    values on fp16 rounding midpoints, fp16-subnormal scales and offsets -- and is several
+    times tighter than the per-element worst case on data with full mantissas."""
+    g = torch.Generator().manual_seed(hash(kind) % 1000)
+    n, D, Kc = 3000, 96, 64
+    if kind == "uniform":
+        X = torch.rand(n, D, generator=g)
+    elif kind == "randn":
+        X = torch.randn(n, D, generator=g) * 3
+    elif kind == "midpoints":                 # x xs exactly halfway between fp16 neighbours
+        X = (torch.randint(2 ** 10, 2 ** 11, (n, D), generator=g).float() + 0.5) / 2 ** 11
+    elif kind == "tiny":
+        X = torch.randn(n, D, generator=g) * 1e-30
+    elif kind == "huge":
+        X = torch.randn(n, D, generator=g) * 1e30
+    else:
+        X = torch.randn(n, D, generator=g) + 1e3
+    C = X[torch.randperm(n, generator=g)[:Kc]] * 0.9
+    P = K.prepare_centers(C)
+    xs = K._pow2_scale(float(X.abs().max()))
+    E = K.row_bound(X, P, xs)                                       # [n] fp64
+    xh = (X * xs).half().double() / xs
+    mh = P.h16[:Kc, :D].double() / P.ms
+    err = (xh @ mh.T - X.double() @ (-2.0 * C.double()).T).abs()   # exact products in fp64
+    assert bool((err <= E[:, None]).all()), float((err / E[:, None]).max())
+    if kind in ("uniform", "randn"):
+        worst = 2.0 ** -10 * X.double().norm(dim=1) * float(2 * C.double().norm(dim=1).max())
+        assert float((E / worst).max()) < 0.6
 
 
 @pytest.mark.gpu
@@ -358,8 +393,7 @@ def test_gpu_approx_assign_is_within_the_screen_bound(gpu):
     a1, d1 = K.assign(X, C, mode="approx")
     a2, d2 = K.assign(X, C, mode="split")
     P = K.prepare_centers(C)
-    eps_x, eps0 = K.screen_bound(P, K.x_scale(X), X.shape[1])
-    bound = 2 * (eps_x * X.norm(dim=1) + eps0)
+    bound = 2 * K.row_bound(X, P, K.x_scale(X)).float()
     dx = ((X - C[a1.long()]) ** 2).sum(1)
     assert torch.allclose(d1, dx, rtol=1e-4, atol=1e-3)
     assert bool((d1 <= d2 + bound + 1e-3).all())
