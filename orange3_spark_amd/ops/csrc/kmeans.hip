@@ -334,6 +334,10 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_kernel(
 // 4 waves (one per SIMD) x TT 32-row tiles per block, 2 blocks per CU: one block's X
 // staging and DMA prologue overlaps the other's MFMA sweep.
 constexpr int kScrWaves = 4;
+#ifndef O3S_SCR_FRAG_AHEAD
+#define O3S_SCR_FRAG_AHEAD 1
+#endif
+constexpr bool kScrFragAhead = O3S_SCR_FRAG_AHEAD;
 constexpr int kScrThreads = kScrWaves * kWave;
 
 template <int KS>
@@ -579,6 +583,44 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       for (int t = 0; t < TT; ++t) bch[t] = best[t] != b0[t] ? ch_old : bch[t];
     }
   };
+  // The plain screen's chunk sweep with its centre fragments loaded one chunk AHEAD (all KS
+  // of them, double-buffered in registers): the next chunk's LDS reads are issued at the
+  // top of this chunk's sweep, so no MFMA waits on a fragment read (the one-step-ahead
+  // read of the loop above left a lgkmcnt wait every other k-step).
+  auto load_frags = [&](const uint16_t* Lh, bf16x8 (&F)[KS]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int sw = (ks * 2 + h) ^ (r & 15 & (SLOTS - 1));
+      F[ks] = *reinterpret_cast<const bf16x8*>(Lh + r * D + sw * 8);
+    }
+  };
+  auto sweep_f = [&](const bf16x8 (&F)[KS], const uint16_t* Lnext, bf16x8 (&Fn)[KS], const float* sc, int ch,
+                     f32x16 (&acc)[TT], const f32x16 (&old)[TT], int ch_old) __attribute__((always_inline)) {
+    constexpr int E = 8 * TT;
+    const int cbase = ch * 32 + 4 * h;
+    f32x16 c0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float4 c4 = *reinterpret_cast<const float4*>(sc + cbase + 8 * q);
+      c0[4 * q + 0] = c4.x; c0[4 * q + 1] = c4.y; c0[4 * q + 2] = c4.z; c0[4 * q + 3] = c4.w;
+    }
+    if (Lnext) load_frags(Lnext, Fn);
+    float b0[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) b0[t] = best[t];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, F[ks]),
+                                                         __builtin_bit_cast(f16x8, bh[t][ks]),
+                                                         ks == 0 ? c0 : acc[t], 0, 0, 0);
+#pragma unroll
+      for (int e = ks * E / KS; e < (ks + 1) * E / KS; ++e) epi_step(old, e);
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t) bch[t] = best[t] != b0[t] ? ch_old : bch[t];
+  };
   stage(0, lds);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -595,6 +637,7 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
       for (int j = 0; j < 16; ++j) accB[t][j] = 0x1p126f;
   }
   bool pendA = false, pendB = false;
+  bf16x8 FA[KS], FB[KS];
   // One stage's body with its three LDS regions as __restrict__ pointers: the scoped
   // no-alias info lets hipcc's wait insertion see that the chunk / ||c||^2 reads do not
   // touch the next stage's in-flight DMA (otherwise it drains that DMA, vmcnt(0), before
@@ -616,9 +659,17 @@ __global__ __launch_bounds__(kScrThreads, 2) void kmeans_screen_kernel(
           if (pendA) epilogue(accA, ch);
           pendB = true; pendA = false;
         }
-      } else {
+      } else if constexpr (!(kScrFragAhead && NOD)) {   // (with lo halves held: too many registers)
         if (ch < nchunks) sweep(Yes{}, cur + g * CH_ELEMS, sc, ch, accA, accB, ch - 1);
         if (ch + 1 < nchunks) sweep(Yes{}, cur + (g + 1) * CH_ELEMS, sc, ch + 1, accB, accA, ch);
+      } else {
+        // fragments of chunk g in FA (g even) / FB (g odd); the stage's first chunk loads
+        // its own after the stage barrier, every later one was loaded by its predecessor
+        // (a chunk index past nchunks reads stale LDS that no MFMA uses)
+        if (g == 0) load_frags(cur, FA);
+        if (ch < nchunks) sweep_f(FA, cur + (g + 1) * CH_ELEMS, FB, sc, ch, accA, accB, ch - 1);
+        if (ch + 1 < nchunks)
+          sweep_f(FB, g + 2 < G ? cur + (g + 2) * CH_ELEMS : nullptr, FA, sc, ch + 1, accB, accA, ch);
       }
     }
   };
