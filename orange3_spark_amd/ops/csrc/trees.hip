@@ -616,56 +616,89 @@ __global__ __launch_bounds__(256) void bin_features_kernel(const void* __restric
 // one row -- one 16-B (bf16) or two 16-B (fp32) loads, eight independent branchless
 // searches, one 8-B store -- instead of one 2-/4-B load and one byte store per element
 // (the scalar kernel above ran the 500M x 64 binning at 75 ms, mostly memory-instruction
-// issue).  The feature-major copy goes through the same LDS tile.
-template <bool BF16>
+// issue).  ROWS-row chunks (256 when the LDS tile fits): a thread issues the loads of up to
+// four of its items before the first search, so each block keeps several row loads in
+// flight per barrier; the feature-major copy leaves the [F][ROWS] LDS tile as 4-row dwords
+// (ldt % 4 == 0; one byte per lane otherwise).
+template <bool BF16, int ROWS>
 __global__ __launch_bounds__(256) void bin_features_vec_kernel(const void* __restrict__ Xv, int64_t n, int64_t ldx,
                                                                int F, const float* __restrict__ th, int Tp,
                                                                uint8_t* __restrict__ out, uint8_t* __restrict__ out_t,
                                                                int64_t ldt) {
+  constexpr int TSR = ROWS + 4;                          // tile row stride (bytes, % 4 == 0)
   extern __shared__ float sth[];
   const int TS = Tp + 1;
   uint8_t* const tile = reinterpret_cast<uint8_t*>(sth + F * TS);
   for (int i = threadIdx.x; i < F * Tp; i += 256) sth[(i / Tp) * TS + i % Tp] = th[i];
   __syncthreads();
   const int G = F >> 3;                                  // 8-feature groups per row
-  const int64_t nchunks = (n + kBinRows - 1) / kBinRows;
+  const bool dw = (ldt & 3) == 0 && ((uintptr_t)out_t & 3) == 0;
+  const int64_t nchunks = (n + ROWS - 1) / ROWS;
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    const int64_t r0 = c * kBinRows;
-    const int rows = n - r0 < kBinRows ? (int)(n - r0) : kBinRows;
-    for (int li = threadIdx.x; li < rows * G; li += 256) {
-      const int lr = li / G, g = li - lr * G;
-      const int64_t row = r0 + lr;
-      float x[8];
-      if constexpr (BF16) {
-        const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(Xv) + row * ldx + 8 * g);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const int64_t r0 = c * ROWS;
+    const int rows = n - r0 < ROWS ? (int)(n - r0) : ROWS;
+    const int items = rows * G;
+    for (int li0 = threadIdx.x; li0 < items; li0 += 4 * 256) {
+      float x[4][8];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          x[2 * k] = __uint_as_float(w[k] << 16);
-          x[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+      for (int u = 0; u < 4; ++u) {
+        const int li = li0 + u * 256;
+        const int lr = li / G, g = li - lr * G;
+        const int64_t row = r0 + (li < items ? lr : 0);
+        const int gg = li < items ? g : 0;
+        if constexpr (BF16) {
+          const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(Xv) + row * ldx + 8 * gg);
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            x[u][2 * k] = __uint_as_float(w[k] << 16);
+            x[u][2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+          }
+        } else {
+          const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Xv) + row * ldx + 8 * gg);
+          const float4 a = p[0], b = p[1];
+          x[u][0] = a.x; x[u][1] = a.y; x[u][2] = a.z; x[u][3] = a.w;
+          x[u][4] = b.x; x[u][5] = b.y; x[u][6] = b.z; x[u][7] = b.w;
         }
-      } else {
-        const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(Xv) + row * ldx + 8 * g);
-        const float4 a = p[0], b = p[1];
-        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
       }
-      uint32_t lo = 0, hi = 0;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float* a = sth + (8 * g + k) * TS;
-        int bk = 0;
-        for (int st = Tp >> 1; st > 0; st >>= 1) bk += (a[bk + st - 1] < x[k]) ? st : 0;
-        if (k < 4) lo |= (uint32_t)bk << (8 * k);
-        else hi |= (uint32_t)bk << (8 * (k - 4));
-        if (out_t != nullptr) tile[(8 * g + k) * kBinTS + lr] = (uint8_t)bk;
+      for (int u = 0; u < 4; ++u) {
+        const int li = li0 + u * 256;
+        if (li >= items) break;
+        const int lr = li / G, g = li - lr * G;
+        const int64_t row = r0 + lr;
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float* a = sth + (8 * g + k) * TS;
+          int bk = 0;
+          for (int st = Tp >> 1; st > 0; st >>= 1) bk += (a[bk + st - 1] < x[u][k]) ? st : 0;
+          if (k < 4) lo |= (uint32_t)bk << (8 * k);
+          else hi |= (uint32_t)bk << (8 * (k - 4));
+          if (out_t != nullptr) tile[(8 * g + k) * TSR + lr] = (uint8_t)bk;
+        }
+        *reinterpret_cast<uint2*>(out + row * F + 8 * g) = make_uint2(lo, hi);
       }
-      *reinterpret_cast<uint2*>(out + row * F + 8 * g) = make_uint2(lo, hi);
     }
     if (out_t != nullptr) {
       __syncthreads();
-      for (int e = threadIdx.x; e < F * kBinRows; e += 256) {
-        const int f = e / kBinRows, lr = e - f * kBinRows;
-        if (lr < rows) out_t[(int64_t)f * ldt + r0 + lr] = tile[f * kBinTS + lr];
+      if (dw) {
+        constexpr int Q = ROWS / 4;
+        for (int e = threadIdx.x; e < F * Q; e += 256) {
+          const int f = e / Q, q = e - f * Q;
+          const int lr = 4 * q;
+          if (lr + 3 < rows) {
+            *reinterpret_cast<uint32_t*>(out_t + (int64_t)f * ldt + r0 + lr) =
+                *reinterpret_cast<const uint32_t*>(tile + f * TSR + lr);
+          } else {
+            for (int j = lr; j < rows; ++j) out_t[(int64_t)f * ldt + r0 + j] = tile[f * TSR + j];
+          }
+        }
+      } else {
+        for (int e = threadIdx.x; e < F * ROWS; e += 256) {
+          const int f = e / ROWS, lr = e - f * ROWS;
+          if (lr < rows) out_t[(int64_t)f * ldt + r0 + lr] = tile[f * TSR + lr];
+        }
       }
       __syncthreads();
     }
@@ -1165,12 +1198,23 @@ O3S_API int o3s_bin_features2(const void* X, int bf16, int64_t n, int64_t ldx, i
   const unsigned grid = (unsigned)(nchunks < 8192 ? nchunks : 8192);
   if (out_t != nullptr && ldt < n) return -3;
   const bool vec = F % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X & 15) == 0;
-  if (vec && bf16)
-    hipLaunchKernelGGL(bin_features_vec_kernel<true>, dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, Tp, out,
-                       out_t, ldt);
+  // vector kernel: 256-row chunks when that tile fits beside the thresholds
+  const size_t lds256 = sizeof(float) * (size_t)F * (Tp + 1) + (size_t)F * (256 + 4);
+  const bool big = lds256 <= 64 * 1024;
+  const int64_t nch256 = (n + 255) / 256;
+  const unsigned grid256 = (unsigned)(nch256 < 4096 ? nch256 : 4096);
+  if (vec && big && bf16)
+    hipLaunchKernelGGL((bin_features_vec_kernel<true, 256>), dim3(grid256), dim3(256), lds256, st, X, n, ldx, F, th,
+                       Tp, out, out_t, ldt);
+  else if (vec && big)
+    hipLaunchKernelGGL((bin_features_vec_kernel<false, 256>), dim3(grid256), dim3(256), lds256, st, X, n, ldx, F, th,
+                       Tp, out, out_t, ldt);
+  else if (vec && bf16)
+    hipLaunchKernelGGL((bin_features_vec_kernel<true, kBinRows>), dim3(grid), dim3(256), lds, st, X, n, ldx, F, th,
+                       Tp, out, out_t, ldt);
   else if (vec)
-    hipLaunchKernelGGL(bin_features_vec_kernel<false>, dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, Tp, out,
-                       out_t, ldt);
+    hipLaunchKernelGGL((bin_features_vec_kernel<false, kBinRows>), dim3(grid), dim3(256), lds, st, X, n, ldx, F, th,
+                       Tp, out, out_t, ldt);
   else if (bf16)
     hipLaunchKernelGGL(bin_features_kernel<true>, dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, Tp, out, out_t,
                        ldt);

@@ -209,6 +209,7 @@ def test_gpu_u8_transpose(gpu, n, F):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,F,nb,bf16", [(100_003, 64, 32, False), (100_003, 64, 32, True), (2049, 16, 8, True),
+                                         (100_000, 64, 32, True), (4098, 64, 32, False), (100_000, 128, 255, True),
                                          (5000, 7, 2, False), (777, 130, 255, False), (3, 1, 32, False)])
 def test_gpu_bin_features_matches_bucketize(gpu, n, F, nb, bf16):
     """bin_features (vector kernel for F % 8 == 0: 8 features per lane; scalar kernel
