@@ -31,28 +31,25 @@ class KMeansResult:
     seconds: float = 0.0
 
 
-def _sum_sq(X: torch.Tensor, m: torch.Tensor | None = None) -> torch.Tensor:
-    """sum ||x - m||^2 over the rows (fp64 accumulation, bounded row chunks: no fp64 copy
-    of X)."""
-    s = torch.zeros((), dtype=torch.float64, device=X.device)
-    step = max(1, (1 << 26) // max(1, X.shape[1]))
-    for i in range(0, X.shape[0], step):
-        blk = X[i:i + step]
-        if m is not None:
-            blk = blk.to(torch.float64) - m
-        s += torch.linalg.vector_norm(blk, 2, dtype=torch.float64) ** 2
-    return s
-
-
-def _global_mean(comm, X: torch.Tensor) -> torch.Tensor:
-    """Mean row over all ranks (fp64, chunked sums)."""
-    buf = torch.zeros(X.shape[1] + 1, dtype=torch.float64, device=X.device)
-    step = max(1, (1 << 26) // max(1, X.shape[1]))
-    for i in range(0, X.shape[0], step):
-        buf[:-1] += X[i:i + step].sum(0, dtype=torch.float64)
-    buf[-1] = X.shape[0]
+def _centred_moments(comm, X: torch.Tensor):
+    """(global mean row m fp64, this rank's sum ||x - m||^2) in ONE pass over X: the rows'
+    sums are taken about a shift s (rank 0's first row, shared), then
+    sum ||x - m||^2 = sum ||x - s||^2 - 2 (m - s).sum (x - s) + n ||m - s||^2 exactly, with
+    m - s small -- no cancellation for data far from the origin."""
+    D = X.shape[1]
+    s = torch.zeros(D + 1, dtype=torch.float64, device=X.device)
+    if comm.rank == 0 and X.shape[0]:
+        s[:D] = X[0].to(torch.float64)
+        s[D] = 1.0
+    comm.all_reduce(s)                   # rank 0's row (or zeros when it has no rows)
+    shift = s[:D].float()                # an fp32 row: exactly the kernel's shift
+    s1, s2 = K.moments(X, shift)
+    buf = torch.cat([s1, torch.tensor([float(X.shape[0])], dtype=torch.float64, device=X.device)])
     comm.all_reduce(buf)
-    return buf[:-1] / buf[-1].clamp_min(1.0)
+    n = buf[D].clamp_min(1.0)
+    ms = buf[:D] / n                     # m - s
+    local = s2 - 2.0 * (ms * s1).sum() + float(X.shape[0]) * (ms * ms).sum()
+    return shift.to(torch.float64) + ms, local
 
 
 def _global_rows(comm, n_local, device):
@@ -435,8 +432,10 @@ def _fit_kmeans_rows(comm, X, k, max_iter, tol, seed, init, init_steps, initial,
     # S'_a = S_a - n_a m -- about the origin the identity cancels catastrophically for data
     # far from 0), so the assign pass needs no per-row distance (the screen kernel then
     # skips the exact-distance epilogue and half of its row reads)
-    mean = _global_mean(comm, X) if weights is None else None
-    sumsq = _sum_sq(X, mean) if weights is None else None
+    if weights is None:
+        mean, sumsq = _centred_moments(comm, X)
+    else:
+        mean = sumsq = None
     # Hamerly bounds (unweighted, screen kernel): per row an upper bound on the distance to
     # its centre and a lower bound on the distance to every other one; after the centres
     # move by delta, ub += delta[a] and lb -= max delta, and only rows with ub >= lb are
@@ -485,6 +484,19 @@ def _fit_kmeans_rows(comm, X, k, max_iter, tol, seed, init, init_steps, initial,
     if ckpt is not None:
         ckpt.clear()                     # finished: a later fit must not resume from this run
     # final cost/sizes w.r.t. the returned centres (Spark reports the last assignment's)
+    if ham:
+        # one more bounded step: only the rows whose bounds no longer certify their centre
+        # are screened, the cluster sums follow the rows that moved, and the cost comes
+        # from the sums (the loop's identity) -- no full pass over X
+        with trace("kmeans.final"):
+            sums, cnt, _ = _hamerly_step(X, C, K.prepare_centers(C.float()), ws, k, hs)
+            Cd = C.to(sums.device, torch.float64) - mean
+            Sd = sums.to(torch.float64) - cnt.to(torch.float64)[:, None] * mean
+            local = sumsq - (2.0 * (Cd * Sd).sum() - (cnt * (Cd * Cd).sum(1)).sum())
+            buf = torch.cat([cnt.to(torch.float64), local.reshape(1)])
+            comm.all_reduce(buf)
+            cost = max(0.0, float(buf[-1]))
+        return KMeansResult(C.cpu(), cost, it, [int(round(x)) for x in buf[:k].tolist()], hist, time.time() - t0)
     a, d = K.assign(X, C.float())
     cnt = torch.bincount(a.long(), minlength=k)[:k].to(torch.float64)
     buf = torch.cat([cnt, d.to(torch.float64).sum().reshape(1)])

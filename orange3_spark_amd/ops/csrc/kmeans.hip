@@ -1623,4 +1623,61 @@ O3S_API int o3s_kmeanspp(const float* PT, const double* w, const double* pn, int
   return 0;
 }
 
+// ---------------------------------------------------------------------------------
+// Shifted moments of the rows in ONE pass (the Lloyd cost identity's centring): per block
+// of consecutive rows, fp64 sums of (x - s) per column and of ||x - s||^2, with s a shift
+// near the data (models/kmeans.py: a row of rank 0) so the later centring about the exact
+// mean cancels nothing.  Thread t owns the float4 column group t % G (G = D / 4) of rows
+// t / G, t / G + 256 / G, ...; the block's partial row [D + 1] is written in a fixed order.
+namespace {
+constexpr int kMomThreads = 256;
+__global__ __launch_bounds__(kMomThreads) void kmeans_moments_kernel(const float* __restrict__ X, int64_t n,
+                                                                     int64_t ldx, int D, const float* __restrict__ sh,
+                                                                     int64_t rows_per_block, double* __restrict__ part) {
+  __shared__ double red[kMomThreads][5];
+  const int G = D / 4;
+  const int per = kMomThreads / G;                       // rows per sweep of the block
+  const int t = threadIdx.x;
+  const int cg = t % G, r0 = t / G;
+  const bool active = r0 < per;
+  const int64_t b0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t b1 = b0 + rows_per_block < n ? b0 + rows_per_block : n;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0, q = 0.0;
+  const float4 c = active ? *reinterpret_cast<const float4*>(sh + 4 * cg) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (active) {
+    for (int64_t r = b0 + r0; r < b1; r += per) {
+      const float4 v = *reinterpret_cast<const float4*>(X + r * ldx + 4 * cg);
+      const double d0 = (double)v.x - c.x, d1 = (double)v.y - c.y, d2 = (double)v.z - c.z, d3 = (double)v.w - c.w;
+      s0 += d0; s1 += d1; s2 += d2; s3 += d3;
+      q = fma(d0, d0, fma(d1, d1, fma(d2, d2, fma(d3, d3, q))));
+    }
+  }
+  red[t][0] = s0; red[t][1] = s1; red[t][2] = s2; red[t][3] = s3; red[t][4] = q;
+  __syncthreads();
+  double* out = part + (int64_t)blockIdx.x * (D + 1);
+  if (t < G) {                                           // column group t: its threads t, t + G, ...
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    for (int k = t; k < per * G; k += G) { a0 += red[k][0]; a1 += red[k][1]; a2 += red[k][2]; a3 += red[k][3]; }
+    out[4 * t] = a0; out[4 * t + 1] = a1; out[4 * t + 2] = a2; out[4 * t + 3] = a3;
+  }
+  if (t == 0) {
+    double a = 0.0;
+    for (int k = 0; k < per * G; ++k) a += red[k][4];
+    out[D] = a;
+  }
+}
+}  // namespace
+
+// part: fp64 [grid][D + 1] (column sums of x - sh, then the sum of ||x - sh||^2), rows split
+// into grid contiguous ranges; D % 4 == 0, D <= 1024, 16-B aligned rows and shift.
+O3S_API int o3s_kmeans_moments(const float* X, int64_t n, int64_t ldx, int D, const float* sh, int grid,
+                               double* part, hipStream_t st) {
+  if (D % 4 != 0 || D <= 0 || D > 4 * kMomThreads || ldx % 4 != 0 || grid <= 0) return -1;
+  if (n <= 0) return 0;
+  const int64_t rpb = (n + grid - 1) / grid;
+  hipLaunchKernelGGL(kmeans_moments_kernel, dim3(grid), dim3(kMomThreads), 0, st, X, n, ldx, D, sh, rpb, part);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
 O3S_PRELOAD(kmeans)

@@ -383,6 +383,30 @@ def assign_bounded(X: torch.Tensor, P: Prepared, a: torch.Tensor, bnd: torch.Ten
                 "kmeans_assign(recheck)")
 
 
+def moments(X: torch.Tensor, shift: torch.Tensor):
+    """(sum over rows of (x - shift) [D], sum of ||x - shift||^2), fp64, in ONE pass over X
+    (``kmeans_moments_kernel``: fp64 per-thread sums, per-block partials in a fixed order);
+    torch on CPU / shapes the kernel does not take."""
+    n, D = X.shape
+    sh = shift.to(X.device, torch.float32).contiguous()
+    if not (X.is_cuda and X.dtype == torch.float32 and D % 4 == 0 and D <= 1024 and X.stride(1) == 1
+            and X.stride(0) % 4 == 0 and X.data_ptr() % 16 == 0 and n > 0):
+        s1 = torch.zeros(D, dtype=torch.float64, device=X.device)
+        s2 = torch.zeros((), dtype=torch.float64, device=X.device)
+        step = max(1, (1 << 26) // max(1, D))
+        for i in range(0, n, step):
+            blk = X[i:i + step].to(torch.float64) - sh.to(torch.float64)
+            s1 += blk.sum(0)
+            s2 += (blk * blk).sum()
+        return s1, s2
+    grid = int(max(1, min(N.num_cus(X.device) * 8, -(-n // 4096))))
+    part = torch.empty((grid, D + 1), dtype=torch.float64, device=X.device)
+    N.check(N.kernels().o3s_kmeans_moments(X.data_ptr(), n, X.stride(0), D, sh.data_ptr(), grid, part.data_ptr(),
+                                           N.stream_of(X)), "kmeans_moments")
+    tot = part.sum(0)
+    return tot[:D], tot[D]
+
+
 def bounds_recheck(a: torch.Tensor, bnd: torch.Tensor, delta: torch.Tensor, dmax: float,
                    max_rows: int | None = None):
     """Move the Hamerly bounds by the centre shifts (ub += delta[a], lb -= dmax, in place);

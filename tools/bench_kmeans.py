@@ -70,8 +70,7 @@ def main():
         t_init = time.perf_counter() - t1
     ws = K.UpdateWorkspace(X.device, (a.k + 31) // 32 * 32, a.d)
     need = a.cost == "rows"
-    from orange3_spark_amd.models.kmeans import _sum_sq
-    sumsq = _sum_sq(X)
+    sumsq = K.moments(X, torch.zeros(a.d, device=X.device))[1]
     torch.cuda.synchronize()
 
     def it(C):
