@@ -454,3 +454,32 @@ def test_gpu_bounds_recheck_matches_torch(gpu):
     torch.testing.assert_close(b_gpu.cpu(), b_ref, rtol=0, atol=0, equal_nan=True)
     m2, r2 = K.bounds_recheck(a.to(gpu), bnd.clone().to(gpu), delta.to(gpu), dmax, max_rows=10)
     assert m2 == m_ref and r2 is None
+
+
+def test_centred_moments_far_from_origin():
+    """The one-pass centring (sums about a shared shift row, then the exact recentring
+    identity) equals the two-pass mean / sum ||x - m||^2 on data offset by 1e6."""
+    from orange3_spark_amd.models.kmeans import _centred_moments
+    from orange3_spark_amd.parallel.comm import LocalComm
+    g = torch.Generator().manual_seed(9)
+    X = (torch.randn(5000, 12, generator=g, dtype=torch.float64) + 1e6).float()
+    m, ss = _centred_moments(LocalComm("cpu"), X)
+    Xd = X.double()
+    mr = Xd.mean(0)
+    torch.testing.assert_close(m, mr, rtol=0, atol=1e-9)
+    ref = ((Xd - mr) ** 2).sum()
+    assert abs(float(ss) - float(ref)) <= 1e-9 * float(ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,D", [(100_003, 128), (4097, 96), (5, 4), (70_000, 160)])
+def test_gpu_moments_kernel_matches_fp64(gpu, n, D):
+    """kmeans_moments_kernel (one pass, fp64 sums of x - shift and ||x - shift||^2 in
+    per-block partials) equals the fp64 torch sums."""
+    g = torch.Generator().manual_seed(n + D)
+    X = ((torch.randn(n, D, generator=g) * 3) + 1e4).to(gpu)
+    shift = X[0].clone()
+    s1, s2 = K.moments(X, shift)
+    d = X.double() - shift.double()
+    torch.testing.assert_close(s1, d.sum(0), rtol=1e-12, atol=1e-6)
+    torch.testing.assert_close(s2, (d * d).sum(), rtol=1e-12, atol=1e-6)
