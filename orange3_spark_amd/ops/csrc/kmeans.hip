@@ -1486,7 +1486,36 @@ __global__ __launch_bounds__(kPDThreads) void kpp_dist_kernel(const float* __res
                                                                double* __restrict__ partial) {
   extern __shared__ double sc[];
   __shared__ double red[kPDThreads / 64];
-  kpp_dist(PT, w, pn, m, D, trials, cand, mode, d2, cd, partial, blockIdx.x, sc, red);
+  if (mode == 0 || gridDim.y == 1) {
+    kpp_dist(PT, w, pn, m, D, trials, cand, mode, d2, cd, partial, blockIdx.x, sc, red);
+    return;
+  }
+  // mode 1 on a (row block, trial) grid: one trial per block -- the same FMA sequence per
+  // (row, trial) as the all-trials loop, spread over trials x more blocks (the one-block-
+  // per-256-rows grid kept ~16 CUs busy for ~80 us per greedy step)
+  const int j = blockIdx.y;
+  const int cj = cand[j];
+  for (int d = threadIdx.x; d < D; d += kPDThreads) sc[d] = (double)PT[(int64_t)d * m + cj];
+  __syncthreads();
+  const int blk = blockIdx.x;
+  const int i = blk * kPDThreads + threadIdx.x;
+  const bool ok = i < m;
+  const int ic = ok ? i : m - 1;
+  constexpr int UD = 8;
+  double dot = 0.0;
+  for (int d0 = 0; d0 < D; d0 += UD) {
+    float x[UD];
+#pragma unroll
+    for (int u = 0; u < UD; ++u) x[u] = d0 + u < D ? PT[(int64_t)(d0 + u) * m + ic] : 0.f;
+#pragma unroll
+    for (int u = 0; u < UD; ++u)
+      if (d0 + u < D) dot = fma((double)x[u], sc[d0 + u], dot);
+  }
+  const double wi = ok ? w[i] : 0.0, di = ok ? d2[i] : 0.0, pi = pn[ic];
+  const double c = fmax(pi + pn[cj] - 2.0 * dot, 0.0);
+  if (ok) cd[(int64_t)j * m + i] = c;
+  const double sj = pp_block_sum(wi * fmin(di, c), red);
+  if (threadIdx.x == 0) partial[(int64_t)blk * kPPMaxT + j] = sj;
 }
 
 // One block.  mode 0 (t = 1): prefix sum of w * d2, the step-1 draws.  mode 1 (step t):
@@ -1614,8 +1643,8 @@ O3S_API int o3s_kmeanspp(const float* PT, const double* w, const double* pn, int
                        d2, cs, cand, picks);
   }
   for (int t = 1; t < k; ++t) {
-    hipLaunchKernelGGL(kpp_dist_kernel, dim3(nb), dim3(kPDThreads), dl, st, PT, w, pn, m, D, trials, cand, 1, d2, cd,
-                       partial);
+    hipLaunchKernelGGL(kpp_dist_kernel, dim3(nb, trials), dim3(kPDThreads), sizeof(double) * D, st, PT, w, pn, m, D,
+                       trials, cand, 1, d2, cd, partial);
     hipLaunchKernelGGL(kpp_pick_kernel, dim3(1), dim3(kPPThreads), pl, st, w, m, k, trials, U, t, 1, nb, partial, cd,
                        d2, cs, cand, picks);
   }
