@@ -486,16 +486,16 @@ def _fit_kmeans_rows(comm, X, k, max_iter, tol, seed, init, init_steps, initial,
     # final cost/sizes w.r.t. the returned centres (Spark reports the last assignment's)
     if ham:
         # one more bounded step: only the rows whose bounds no longer certify their centre
-        # are screened, the cluster sums follow the rows that moved, and the cost comes
-        # from the sums (the loop's identity) -- no full pass over X
+        # are screened (the sizes follow the rows that moved), then the cost straight from
+        # the rows and their centres in one streaming pass -- per-row distances, not the
+        # loop's cluster-sum identity (whose fp32 slab sums cost it ~1e-6 relative when the
+        # clusters are tight), and no full screen
         with trace("kmeans.final"):
-            sums, cnt, _ = _hamerly_step(X, C, K.prepare_centers(C.float()), ws, k, hs)
-            Cd = C.to(sums.device, torch.float64) - mean
-            Sd = sums.to(torch.float64) - cnt.to(torch.float64)[:, None] * mean
-            local = sumsq - (2.0 * (Cd * Sd).sum() - (cnt * (Cd * Cd).sum(1)).sum())
+            _, cnt, _ = _hamerly_step(X, C, K.prepare_centers(C.float()), ws, k, hs)
+            local = K.cost(X, hs["a"], C.float())
             buf = torch.cat([cnt.to(torch.float64), local.reshape(1)])
             comm.all_reduce(buf)
-            cost = max(0.0, float(buf[-1]))
+            cost = float(buf[-1])
         return KMeansResult(C.cpu(), cost, it, [int(round(x)) for x in buf[:k].tolist()], hist, time.time() - t0)
     a, d = K.assign(X, C.float())
     cnt = torch.bincount(a.long(), minlength=k)[:k].to(torch.float64)

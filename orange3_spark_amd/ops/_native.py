@@ -60,6 +60,7 @@ _SIGS: dict[str, list] = {
                            c_vp, c_vp],
     "o3s_kmeans_presplit": [c_vp, c_i64, c_i64, c_i32, C.c_float, c_vp, c_vp, c_vp],
     "o3s_kmeans_moments": [c_vp, c_i64, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp],
+    "o3s_kmeans_cost": [c_vp, c_i64, c_i64, c_i32, c_vp, c_vp, c_i32, c_i32, c_vp, c_vp],
     "o3s_kmeans_bounds": [c_vp, c_vp, c_i64, c_vp, C.c_float, c_i32, c_vp, c_vp, c_vp, c_i32, c_vp],
     "o3s_kmeans_update_ws": [c_i32, c_i32, c_i32, C.POINTER(c_i64), C.POINTER(c_i64), C.POINTER(c_i32)],
     "o3s_murmur3_terms": [c_vp, c_vp, c_i64, c_u32, c_i64, c_vp, c_vp, c_vp],

@@ -1709,4 +1709,53 @@ O3S_API int o3s_kmeans_moments(const float* X, int64_t n, int64_t ldx, int D, co
   return 0;
 }
 
+// ---------------------------------------------------------------------------------
+// Training cost of an assignment: sum over rows of ||x - c_a(x)||^2, directly from the rows
+// (one streaming pass; the centre rows are L2-resident gathers).  Thread t owns float4
+// column group t % G of rows t / G, t / G + 256 / G, ... of its block's contiguous range;
+// a row's four squared differences are summed in fp32 (fma), everything above in fp64,
+// the block partial in a fixed order.
+namespace {
+__global__ __launch_bounds__(kMomThreads) void kmeans_cost_kernel(const float* __restrict__ X, int64_t n, int64_t ldx,
+                                                                  int D, const int32_t* __restrict__ a,
+                                                                  const float* __restrict__ C, int ldc,
+                                                                  int64_t rows_per_block, double* __restrict__ part) {
+  __shared__ double red[kMomThreads];
+  const int G = D / 4;
+  const int per = kMomThreads / G;
+  const int t = threadIdx.x;
+  const int cg = t % G, r0 = t / G;
+  const int64_t b0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t b1 = b0 + rows_per_block < n ? b0 + rows_per_block : n;
+  double acc = 0.0;
+  if (r0 < per) {
+    for (int64_t r = b0 + r0; r < b1; r += per) {
+      const float4 x = *reinterpret_cast<const float4*>(X + r * ldx + 4 * cg);
+      const float4 c = *reinterpret_cast<const float4*>(C + (int64_t)a[r] * ldc + 4 * cg);
+      const float d0 = x.x - c.x, d1 = x.y - c.y, d2 = x.z - c.z, d3 = x.w - c.w;
+      acc += (double)fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, d3 * d3)));
+    }
+  }
+  red[t] = acc;
+  __syncthreads();
+  if (t == 0) {
+    double s = 0.0;
+    for (int k = 0; k < kMomThreads; ++k) s += red[k];
+    part[blockIdx.x] = s;
+  }
+}
+}  // namespace
+
+// part: fp64 [grid] partial costs (rows split into grid contiguous ranges); C: fp32 centre
+// rows [.][ldc] indexed by a; D % 4 == 0, 16-B aligned rows.
+O3S_API int o3s_kmeans_cost(const float* X, int64_t n, int64_t ldx, int D, const int32_t* a, const float* C, int ldc,
+                            int grid, double* part, hipStream_t st) {
+  if (D % 4 != 0 || D <= 0 || D > 4 * kMomThreads || ldx % 4 != 0 || ldc % 4 != 0 || grid <= 0) return -1;
+  if (n <= 0) return 0;
+  const int64_t rpb = (n + grid - 1) / grid;
+  hipLaunchKernelGGL(kmeans_cost_kernel, dim3(grid), dim3(kMomThreads), 0, st, X, n, ldx, D, a, C, ldc, rpb, part);
+  O3S_CHECK_LAUNCH();
+  return 0;
+}
+
 O3S_PRELOAD(kmeans)

@@ -407,6 +407,27 @@ def moments(X: torch.Tensor, shift: torch.Tensor):
     return tot[:D], tot[D]
 
 
+def cost(X: torch.Tensor, a: torch.Tensor, C: torch.Tensor) -> torch.Tensor:
+    """sum over rows of ||x - C[a]||^2 (fp64 scalar) in one pass: ``kmeans_cost_kernel``
+    (fp32 per float4 of a row, fp64 above, fixed-order block partials); torch elsewhere."""
+    n, D = X.shape
+    Cf = C.to(X.device, torch.float32).contiguous()
+    if not (X.is_cuda and X.dtype == torch.float32 and D % 4 == 0 and D <= 1024 and X.stride(1) == 1
+            and X.stride(0) % 4 == 0 and X.data_ptr() % 16 == 0 and n > 0 and a.dtype == torch.int32
+            and a.is_contiguous()):
+        tot = torch.zeros((), dtype=torch.float64, device=X.device)
+        step = max(1, (1 << 24) // max(1, D))
+        for i in range(0, n, step):
+            d = X[i:i + step].to(torch.float64) - Cf[a[i:i + step].long()].to(torch.float64)
+            tot += (d * d).sum()
+        return tot
+    grid = int(max(1, min(N.num_cus(X.device) * 8, -(-n // 4096))))
+    part = torch.empty(grid, dtype=torch.float64, device=X.device)
+    N.check(N.kernels().o3s_kmeans_cost(X.data_ptr(), n, X.stride(0), D, a.data_ptr(), Cf.data_ptr(), Cf.stride(0),
+                                        grid, part.data_ptr(), N.stream_of(X)), "kmeans_cost")
+    return part.sum()
+
+
 def bounds_recheck(a: torch.Tensor, bnd: torch.Tensor, delta: torch.Tensor, dmax: float,
                    max_rows: int | None = None):
     """Move the Hamerly bounds by the centre shifts (ub += delta[a], lb -= dmax, in place);

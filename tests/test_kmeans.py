@@ -483,3 +483,16 @@ def test_gpu_moments_kernel_matches_fp64(gpu, n, D):
     d = X.double() - shift.double()
     torch.testing.assert_close(s1, d.sum(0), rtol=1e-12, atol=1e-6)
     torch.testing.assert_close(s2, (d * d).sum(), rtol=1e-12, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,D", [(100_003, 128), (5, 4), (70_000, 160)])
+def test_gpu_cost_kernel_matches_fp64(gpu, n, D):
+    """kmeans_cost_kernel: sum ||x - C[a]||^2 from the rows equals the fp64 torch sum."""
+    g = torch.Generator().manual_seed(n + 3 * D)
+    X = (torch.randn(n, D, generator=g) * 2 + 5).to(gpu)
+    C = (torch.randn(37, D, generator=g) + 5).to(gpu)
+    a = torch.randint(0, 37, (n,), generator=g).to(gpu).to(torch.int32)
+    got = K.cost(X, a, C)
+    ref = ((X.double() - C.double()[a.long()]) ** 2).sum()
+    torch.testing.assert_close(got, ref, rtol=1e-7, atol=0)
