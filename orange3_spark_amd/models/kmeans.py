@@ -335,9 +335,11 @@ HAMERLY_FULL_FRACTION = 0.5    # more rows than this to recheck: screen them all
 LAST_HAMERLY_STATS: list = []  # per iteration: rows screened / changed (diagnostics)
 
 
-def _hamerly_step(X, C, prep, ws, k, hs):
+def _hamerly_step(X, C, prep, ws, k, hs, sums=True):
     """One Lloyd assignment + cluster-sum step with Hamerly bounds (state ``hs`` carried
-    across iterations): returns this rank's (sums fp64 [k, D], counts fp64 [k], stats)."""
+    across iterations): returns this rank's (sums fp64 [k, D], counts fp64 [k], stats).
+    ``sums=False`` (the final assignment): counts only, sums None -- the state is then
+    spent."""
     n = X.shape[0]
     dev = X.device
     full = hs["a"] is None
@@ -354,6 +356,10 @@ def _hamerly_step(X, C, prep, ws, k, hs):
         a = torch.empty(n, dtype=torch.int32, device=dev) if hs["a"] is None else hs["a"]
         bnd = torch.empty((n, 2), dtype=torch.float32, device=dev) if hs["bnd"] is None else hs["bnd"]
         K.assign_bounded(X, prep, a, bnd, None)
+        if not sums:
+            cnt = torch.bincount(a.long(), minlength=k)[:k].to(torch.float64)
+            hs.update(a=a, bnd=bnd)
+            return None, cnt, {"screened": n}
         S, cnt = K.update(X, a, ws.K, ws)
         S, cnt = S[:k].clone(), cnt[:k].clone()
         st = {"screened": n, "changed": None, "recheck": None if hs["a"] is None else need}
@@ -364,6 +370,13 @@ def _hamerly_step(X, C, prep, ws, k, hs):
         a_new = a[rows.long()]
         ch = rows[a_new != a_old]
         S, cnt = hs["S"], hs["n"]
+        if not sums:
+            moved = a_new != a_old
+            cnt = cnt.clone()
+            cnt.index_add_(0, a_new[moved].long(), torch.ones(int(moved.sum()), dtype=cnt.dtype, device=dev))
+            cnt.index_add_(0, a_old[moved].long(), -torch.ones(int(moved.sum()), dtype=cnt.dtype, device=dev))
+            hs.update(a=a, bnd=bnd)
+            return None, cnt, {"screened": int(rows.numel()), "changed": int(ch.numel())}
         if ch.numel():
             Xc = X[ch.long()]
             # a grid sized to the changed rows (every block zeroes and sums a [Kp, D] slab)
@@ -491,7 +504,7 @@ def _fit_kmeans_rows(comm, X, k, max_iter, tol, seed, init, init_steps, initial,
         # loop's cluster-sum identity (whose fp32 slab sums cost it ~1e-6 relative when the
         # clusters are tight), and no full screen
         with trace("kmeans.final"):
-            _, cnt, _ = _hamerly_step(X, C, K.prepare_centers(C.float()), ws, k, hs)
+            _, cnt, _ = _hamerly_step(X, C, K.prepare_centers(C.float()), ws, k, hs, sums=False)
             local = K.cost(X, hs["a"], C.float())
             buf = torch.cat([cnt.to(torch.float64), local.reshape(1)])
             comm.all_reduce(buf)
