@@ -1,3 +1,5 @@
+"""DataFrame op timings on the GPU (20M-row range frame: groupBy / join / sort / window
+-style ops), one JSON line."""
 import sys, time, json, os
 sys.path.insert(0, os.getcwd())
 import torch
