@@ -353,6 +353,7 @@ __global__ __launch_bounds__(kHistThreads, 4) void tree_hist_kernel(
 // a block scan, so the split is stable and deterministic.
 constexpr int kPartThreads = 256;
 constexpr int kPartWaves = kPartThreads / kWave;
+constexpr int kPartU = 4;                          // rows per thread per round (count, scatter)
 
 // bins element (row, feat) at row * rs + feat * cs: the partition reads a feature-major
 // copy (rs = 1, cs = n), so within a segment (rows in ascending order after every stable
@@ -371,10 +372,26 @@ __global__ __launch_bounds__(kPartThreads) void tree_part_count_kernel(
   const int64_t lo = it_lo[blockIdx.x], hi = it_hi[blockIdx.x];
   const int feat = it_feat[blockIdx.x], bin = it_bin[blockIdx.x];
   int cnt = 0;
-  for (int64_t p = lo + threadIdx.x; p < hi; p += kPartThreads) {
-    const bool l = goes_left(bins, rs, cs, order[p], feat, bin);     // the one random gather per row
-    flags[p] = l;                                               // pass 2 reads this sequentially
-    cnt += l;
+  // kPartU rows per thread per round: their order[] loads, then their gathers, issue
+  // together (one dependent load pair per row left the memory pipe mostly idle)
+  for (int64_t p0 = lo + threadIdx.x; p0 < hi; p0 += kPartThreads * kPartU) {
+    int32_t row[kPartU];
+#pragma unroll
+    for (int k = 0; k < kPartU; ++k) {
+      const int64_t p = p0 + (int64_t)k * kPartThreads;
+      row[k] = p < hi ? order[p] : 0;
+    }
+    bool l[kPartU];
+#pragma unroll
+    for (int k = 0; k < kPartU; ++k) l[k] = goes_left(bins, rs, cs, row[k], feat, bin);   // the random gathers
+#pragma unroll
+    for (int k = 0; k < kPartU; ++k) {
+      const int64_t p = p0 + (int64_t)k * kPartThreads;
+      if (p < hi) {
+        flags[p] = l[k];                                        // pass 2 reads this sequentially
+        cnt += l[k];
+      }
+    }
   }
   cnt = wave_sum_i(cnt);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -434,38 +451,60 @@ __global__ __launch_bounds__(kPartThreads) void tree_part_scatter_kernel(
     const int32_t* __restrict__ it_bin, const int64_t* __restrict__ dst_left, const int64_t* __restrict__ dst_right,
     const uint8_t* __restrict__ flags, const float* __restrict__ py, float* __restrict__ py_out,
     const float* __restrict__ pw, float* __restrict__ pw_out) {
-  __shared__ int wl[kPartWaves];
+  // kPartU sub-rounds of kPartThreads positions per round: every load of the round first,
+  // then one barrier for the wave counts of all sub-rounds (instead of one round trip and
+  // two barriers per kPartThreads positions); destinations as before, sub-round by sub-round
+  __shared__ int wl[kPartU][kPartWaves];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t lo = it_lo[blockIdx.x], hi = it_hi[blockIdx.x];
-  const int feat = it_feat[blockIdx.x], bin = it_bin[blockIdx.x];
   int64_t nl = dst_left[blockIdx.x], nr = dst_right[blockIdx.x];
   const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  for (int64_t base = lo; base < hi; base += kPartThreads) {
-    const int64_t p = base + threadIdx.x;
-    const bool ok = p < hi;
-    const int32_t row = ok ? order[p] : 0;
-    const bool left = ok && flags[p];
-    const uint64_t m = __ballot(left);
-    if (lane == 0) wl[wid] = __popcll(m);
-    __syncthreads();
-    int before = 0, total = 0;
+  for (int64_t base = lo; base < hi; base += (int64_t)kPartThreads * kPartU) {
+    int32_t row[kPartU];
+    bool left[kPartU];
+    float yv[kPartU], wv[kPartU];
 #pragma unroll
-    for (int i = 0; i < kPartWaves; ++i) {
-      before += i < wid ? wl[i] : 0;
-      total += wl[i];
+    for (int k = 0; k < kPartU; ++k) {
+      const int64_t p = base + (int64_t)k * kPartThreads + threadIdx.x;
+      const bool ok = p < hi;
+      const int64_t pc = ok ? p : lo;
+      row[k] = order[pc];
+      left[k] = ok && flags[pc];
+      yv[k] = py ? py[pc] : 0.f;
+      wv[k] = pw ? pw[pc] : 0.f;
     }
-    const int rank_l = before + __popcll(m & below);             // lefts before me in this round
-    const int64_t round_base = p - threadIdx.x;
-    const int valid = (int)((hi - round_base) < kPartThreads ? (hi - round_base) : kPartThreads);
-    if (ok) {
-      // rights before me = idx - lefts before; position-ordered payloads move with the row
-      const int64_t d = left ? nl + rank_l : nr + ((int)threadIdx.x - rank_l);
-      out[d] = row;
-      if (py) py_out[d] = py[p];
-      if (pw) pw_out[d] = pw[p];
+    uint64_t m[kPartU];
+#pragma unroll
+    for (int k = 0; k < kPartU; ++k) {
+      m[k] = __ballot(left[k]);
+      if (lane == 0) wl[k][wid] = __popcll(m[k]);
     }
-    nl += total;
-    nr += valid - total;
+    __syncthreads();
+    int64_t accl = 0, accr = 0;                                  // lefts / rights of earlier sub-rounds
+#pragma unroll
+    for (int k = 0; k < kPartU; ++k) {
+      int before = 0, total = 0;
+#pragma unroll
+      for (int i = 0; i < kPartWaves; ++i) {
+        before += i < wid ? wl[k][i] : 0;
+        total += wl[k][i];
+      }
+      const int rank_l = before + __popcll(m[k] & below);       // lefts before me in this sub-round
+      const int64_t round_base = base + (int64_t)k * kPartThreads;
+      const int64_t rem = hi - round_base;
+      const int valid = rem <= 0 ? 0 : (rem < kPartThreads ? (int)rem : kPartThreads);
+      if ((int)threadIdx.x < valid) {
+        // rights before me = idx - lefts before; position-ordered payloads move with the row
+        const int64_t d = left[k] ? nl + accl + rank_l : nr + accr + ((int)threadIdx.x - rank_l);
+        out[d] = row[k];
+        if (py) py_out[d] = yv[k];
+        if (pw) pw_out[d] = wv[k];
+      }
+      accl += total;
+      accr += valid - total;
+    }
+    nl += accl;
+    nr += accr;
     __syncthreads();                                              // wl reused next round
   }
 }
