@@ -1,6 +1,7 @@
 """Tree histogram op: gfx950 kernel (csrc/trees.hip) with a PyTorch reference."""
 from __future__ import annotations
 
+import os
 
 import numpy as np
 import torch
@@ -501,7 +502,10 @@ def sibling_hists(Hs: torch.Tensor, parent: torch.Tensor, small_right, cls: bool
 
 
 _RUN = 64      # slab rows per first-stage partial
-HIST_CHUNK = 1 << 13  # rows per histogram work item (4096: same speed, 16384: +5% per tree)
+# rows per histogram work item: with the LDS-DMA row stage 16384 is best on the 500M x 64
+# depth-8 config (s/tree 0.1253 / 0.1195 / 0.1169 / 0.1173 at 4096 / 8192 / 16384 / 32768,
+# profiles/kernel_experiments_r6.json); O3S_HIST_CHUNK overrides for A/B runs
+HIST_CHUNK = int(os.environ.get("O3S_HIST_CHUNK", str(1 << 14)))
 
 
 class _HistPlan:
