@@ -56,8 +56,11 @@ def feature_major(bins: torch.Tensor) -> torch.Tensor | None:
     return out
 
 
+PART_CHUNK = int(os.environ.get("O3S_PART_CHUNK", str(1 << 14)))   # rows per partition work item
+
+
 def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi: torch.Tensor,
-              s_feat: torch.Tensor, s_bin: torch.Tensor, chunk: int = 1 << 14, bins_t: torch.Tensor | None = None,
+              s_feat: torch.Tensor, s_bin: torch.Tensor, chunk: int | None = None, bins_t: torch.Tensor | None = None,
               out: torch.Tensor | None = None, payload=(), payload_out=()):
     """Stable split of every segment [s_lo, s_hi) of ``order`` into rows with
     bins[row, feat] <= bin (first) and the rest.  Returns (new_order, nleft per segment).
@@ -73,6 +76,7 @@ def partition(bins: torch.Tensor, order: torch.Tensor, s_lo: torch.Tensor, s_hi:
     GPU: two passes of ``tree_part_*_kernel`` over work items (count, then scatter to
     destinations from ``tree_part_dest_kernel``); CPU: the PyTorch reference."""
     payload, payload_out = tuple(payload), tuple(payload_out)
+    chunk = chunk or PART_CHUNK
     if len(payload) != len(payload_out) or len(payload) > 2:
         raise ValueError("payload / payload_out mismatch")
     if not (bins.is_cuda and order.dtype == torch.int32):
