@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as Ct
 import math
+import os
 
 import torch
 
@@ -461,13 +462,16 @@ def bounds_recheck(a: torch.Tensor, bnd: torch.Tensor, delta: torch.Tensor, dmax
     return m, (None if max_rows is not None and m > max_rows else r)
 
 
+UPDATE_BLOCKS_PER_CU = int(os.environ.get("O3S_KM_UPDATE_BLOCKS", "4"))   # update-kernel blocks per CU (A/B: 1 / 2 / 4 / 8 -> 57.7 / 56.2 / 55.3 / 57.7 ms per uniform Lloyd iteration)
+
+
 class UpdateWorkspace:
     """Slab workspace of the update kernel: ``grid`` blocks, each with a private [Kp, D]
     fp32 slab (zeroed per call, summed in a fixed order)."""
 
     def __init__(self, device, K: int, D: int, grid: int | None = None):
         self.K, self.D = K, D
-        self.grid = grid or N.num_cus(device) * 2
+        self.grid = grid or N.num_cus(device) * UPDATE_BLOCKS_PER_CU
         sf, cf, lb = Ct.c_int64(), Ct.c_int64(), Ct.c_int()
         # -3: K too large for the in-LDS counting sort -> update() takes the torch path
         self.ok = N.kernels().o3s_kmeans_update_ws(K, D, self.grid, Ct.byref(sf), Ct.byref(cf), Ct.byref(lb)) == 0
