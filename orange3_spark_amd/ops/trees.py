@@ -298,6 +298,9 @@ def tree_node_arrays(feature: np.ndarray, split_bin: np.ndarray, value: np.ndarr
     return fb, np.asarray(value, dtype=np.float64).reshape(len(fe), -1)[:, 0] * float(scale)
 
 
+LEAF_BLOCKS_PER_CU = int(os.environ.get("O3S_LEAF_BLOCKS", "4"))     # gbt_leaf_pass_kernel grid (A/B 4 / 8 / 16: 12.2 / 12.6 / 13.5 ms per tree)
+
+
 def gbt_leaf_pass(bins: torch.Tensor, feature, split_bin, value, scale: float, depth: int, loss: str,
                   yy: torch.Tensor, Fm: torch.Tensor, wt: torch.Tensor | None, wd: torch.Tensor | None,
                   wv: torch.Tensor | None, first: bool, target: torch.Tensor | None, need_y2: bool):
@@ -320,7 +323,7 @@ def gbt_leaf_pass(bins: torch.Tensor, feature, split_bin, value, scale: float, d
             raise ValueError("target must be a contiguous fp32 [n] tensor")
         if not (yy.dtype == torch.float64 and Fm.dtype == torch.float64 and yy.is_contiguous() and Fm.is_contiguous()):
             raise ValueError("yy / Fm must be contiguous fp64")
-        grid = int(max(1, min(N.num_cus(dev) * 8, (n + 255) // 256)))
+        grid = int(max(1, min(N.num_cus(dev) * LEAF_BLOCKS_PER_CU, (n + 255) // 256)))
         part = torch.empty((grid, 4), dtype=torch.float64, device=dev)
         slab = torch.empty((grid * 4, L), dtype=torch.float32, device=dev) if need_y2 else None   # a row per wave
         fb_d, val_d = N.upload_many(dev, fb, val)
