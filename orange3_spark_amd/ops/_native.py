@@ -93,6 +93,7 @@ _SIGS: dict[str, list] = {
     "o3s_kmeanspp": [c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp],
     "o3s_als_dense_wave_timed": [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp, c_vp],
     "o3s_als_dense_wave": [c_i32, c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
+    "o3s_als_dense_wave_gd": [c_i32, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
     "o3s_als_exact_max_small": [],
     "o3s_als_rotate": [c_i32, c_vp, c_vp, c_i64, c_vp, c_i32, c_vp],
     "o3s_als_rotate_to": [c_i32, c_vp, c_vp, c_i64, c_vp, c_vp, c_i32, c_vp],

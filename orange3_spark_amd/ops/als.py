@@ -119,6 +119,9 @@ def dense_solve(indptr, cols, w, b, F, FtF, lam, batch_bytes: int = 1 << 30) -> 
 
 
 EXACT_RANKS = (32, 64, 96, 128)
+# eigenbasis dense solves with G = diag(eig) passed as a vector (no 40 KB G image in LDS,
+# so a 4-step gather ring at rank 128); O3S_ALS_DENSE_GDIAG=0: the full-G build (A/B)
+DENSE_GDIAG = os.environ.get("O3S_ALS_DENSE_GDIAG", "1") != "0"
 # Long rows (more than 32 ratings, or lam_u = 0) take als_dense_wave_kernel
 # (csrc/als_dense.hip): one wave per row, four independent waves per CU, factor rows
 # gathered by an LDS-DMA ring that streams across the rows of a wave, rows listed longest
@@ -321,14 +324,19 @@ def exact_solve(indptr, cols, w, b, F, G, lam, implicit: bool, out: torch.Tensor
                         "als_rotate")
     if nd:
         with trace("als.dense", rows=nd):
+            gd = None
             if eig_basis:                     # the rotated system: F Q and diag(eig)
-                F, Gf = P, torch.diag(eig).contiguous()
+                F = P
+                if DENSE_GDIAG:
+                    gd, Gf = eig.float().contiguous(), None
+                else:
+                    Gf = torch.diag(eig).contiguous()
             else:
                 Gf = G.float().contiguous() if implicit else None
             # longest rows first: the waves take rows round robin, so the long tail of
             # popular items spreads over the whole chip instead of finishing last
             order = torch.argsort(cnt[dense - a], descending=True)
-            dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, dense[order], out)
+            dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, dense[order], out, gdiag=gd)
     return out
 
 
@@ -345,10 +353,12 @@ def dense_meta(indptr, rows, lam):
     return meta
 
 
-def dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, rows, out, grid=None):
+def dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, rows, out, grid=None, gdiag=None):
     """o3s_als_dense_wave over the listed rows (in list order: the caller sorts them longest
     first); rows without ratings are solved here (x = 0: the right-hand side is 0), so every
-    row the kernel walks has at least one 16-rating step."""
+    row the kernel walks has at least one 16-rating step.  ``gdiag`` (fp32 [R], the
+    eigenbasis solves): G = diag(gdiag) instead of ``Gf`` -- the build without the G image
+    in LDS (``o3s_als_dense_wave_gd``)."""
     R = F.shape[1]
     cnt = indptr[rows.long() + 1] - indptr[rows.long()]
     empty = cnt == 0
@@ -360,6 +370,12 @@ def dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, rows, out, grid=None):
         return out
     meta = dense_meta(indptr, rows, lam)
     lib = N.kernels()
+    if gdiag is not None:
+        N.check(lib.o3s_als_dense_wave_gd(R, meta.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                          F.data_ptr(), gdiag.data_ptr(), n, out.data_ptr(),
+                                          N.num_cus(F.device) if grid is None else grid, N.stream_of(out)),
+                "als_dense_wave_gd")
+        return out
     N.check(lib.o3s_als_dense_wave(int(implicit), R, meta.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                                    F.data_ptr(), N.ptr(Gf), n, out.data_ptr(),
                                    N.num_cus(F.device) if grid is None else grid, N.stream_of(out)),

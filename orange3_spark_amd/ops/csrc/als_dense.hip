@@ -145,13 +145,13 @@ template <int R, bool IMPL, bool DBG = false, bool TIM = false>
 __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
     const int32_t* __restrict__ meta, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ F, const float* __restrict__ G, int64_t nrows,
-    float* __restrict__ X, float* __restrict__ dbg) {
+    float* __restrict__ X, float* __restrict__ dbg, const float* __restrict__ gd = nullptr) {
   using D = DW<R, !IMPL>;
   constexpr int NT = D::NT, NL = D::NL, CH = D::CH, DEPTH = D::DEPTH, RS = D::RS, LPS = D::LPS,
                 RPI = D::RPI, NI = D::NI, SLOT = D::SLOT, MR = D::MR, MAHEAD = D::MAHEAD;
   // ONE __shared__ array (a second object beside the DMA ring can make hipcc wait vmcnt(0)
   // before ring reads)
-  __shared__ __attribute__((aligned(16))) float lds[4 * D::WAVE + (IMPL ? D::GL : 0)];
+  __shared__ __attribute__((aligned(16))) float lds[4 * D::WAVE + (IMPL ? D::GL : R)];
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // G first: its per-lane reads are one base register + immediate offsets (< 64 KB)
@@ -175,6 +175,13 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
       for (int v = 0; v < 16; ++v)
         sG[t * 1024 + (v >> 2) * 256 + lane * 4 + (v & 3)] = G[(32 * tj + rowof(v, h)) * R + 32 * ti + q];
     }
+    __syncthreads();
+  } else {
+    // diagonal G (the eigenbasis solve: G = diag(eig), rotated tables): R floats after the
+    // waves' areas, staged once per block -- a per-row global read of gd would be waited
+    // for with vmcnt(0), draining the DMA ring
+    float* const sGd = lds + 4 * D::WAVE;
+    for (int c = threadIdx.x; c < R; c += 256) sGd[c] = gd != nullptr ? gd[c] : 0.f;
     __syncthreads();
   }
 
@@ -331,7 +338,10 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
     // the system starts as G + lam_u I (G from its LDS copy), the Gram accumulates on top
     f32x16_t acc[NL];
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
+    for (int j = 0; j < NT; ++j) {
+      // !IMPL: lam_u plus the diagonal G (zero when explicit) on the diagonal
+      float dj = lu;
+      if constexpr (!IMPL) dj += lds[4 * D::WAVE + 32 * j + q];
 #pragma unroll
       for (int i = j; i < NT; ++i) {
         const int t = tix<NT>(j, i);
@@ -342,9 +352,10 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
           const float gv[4] = {g.x, g.y, g.z, g.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e)
-            acc[t][4 * k + e] = (i == j && rowof(4 * k + e, h) == q) ? gv[e] + lu : gv[e];
+            acc[t][4 * k + e] = (i == j && rowof(4 * k + e, h) == q) ? (IMPL ? gv[e] + lu : dj) : gv[e];
         }
       }
+    }
     float rh[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) rh[j] = 0.f;
@@ -642,20 +653,20 @@ __global__ __launch_bounds__(256, 1) void als_dense_wave_kernel(
 
 template <int R>
 int launch(int implicit, const int32_t* meta, const int32_t* cols, const float* w, const float* b, const float* F,
-           const float* G, int64_t nrows, float* X, int grid, float* dbg, hipStream_t st) {
+           const float* G, int64_t nrows, float* X, int grid, float* dbg, hipStream_t st, const float* gd = nullptr) {
   if (dbg != nullptr) {
     if (implicit)
       hipLaunchKernelGGL((als_dense_wave_kernel<R, true, true>), dim3(grid), dim3(256), 0, st, meta, cols, w, b, F, G,
-                         nrows, X, dbg);
+                         nrows, X, dbg, nullptr);
     else
       hipLaunchKernelGGL((als_dense_wave_kernel<R, false, true>), dim3(grid), dim3(256), 0, st, meta, cols, w, b, F,
-                         G, nrows, X, dbg);
+                         G, nrows, X, dbg, gd);
   } else if (implicit) {
     hipLaunchKernelGGL((als_dense_wave_kernel<R, true>), dim3(grid), dim3(256), 0, st, meta, cols, w, b, F, G, nrows,
-                       X, nullptr);
+                       X, nullptr, nullptr);
   } else {
     hipLaunchKernelGGL((als_dense_wave_kernel<R, false>), dim3(grid), dim3(256), 0, st, meta, cols, w, b, F, G, nrows,
-                       X, nullptr);
+                       X, nullptr, gd);
   }
   O3S_CHECK_LAUNCH();
   return 0;
@@ -706,6 +717,26 @@ O3S_API int o3s_als_dense_wave(int implicit, int R, const int32_t* meta, const i
                                const float* b, const float* F, const float* G, int64_t nrows, float* X, int grid,
                                hipStream_t st) {
   return o3s_als_dense_wave_dbg(implicit, R, meta, cols, w, b, F, G, nrows, X, grid, nullptr, st);
+}
+
+// Diagonal-G solves (the eigenbasis half-iterations: F = the rotated table F Q, G =
+// diag(gd)): the explicit build (no G image in LDS, so a 4-step gather ring at ranks 96 /
+// 128) with gd[c] + lam_u on the diagonal.  gd: fp32 [R].  Timing parity with the full-G
+// build (profiles/kernel_experiments_r6.json); it spares the R x R diag(eig) and the G
+// image's LDS.
+O3S_API int o3s_als_dense_wave_gd(int R, const int32_t* meta, const int32_t* cols, const float* w, const float* b,
+                                  const float* F, const float* gd, int64_t nrows, float* X, int grid, hipStream_t st) {
+  if (nrows < 0 || !gd || grid <= 0) return -1;
+  if (nrows == 0) return 0;
+  const int64_t need = (nrows + 3) / 4;
+  if (grid > need) grid = (int)need;
+  switch (R) {
+    case 32: return launch<32>(0, meta, cols, w, b, F, nullptr, nrows, X, grid, nullptr, st, gd);
+    case 64: return launch<64>(0, meta, cols, w, b, F, nullptr, nrows, X, grid, nullptr, st, gd);
+    case 96: return launch<96>(0, meta, cols, w, b, F, nullptr, nrows, X, grid, nullptr, st, gd);
+    case 128: return launch<128>(0, meta, cols, w, b, F, nullptr, nrows, X, grid, nullptr, st, gd);
+    default: return -2;
+  }
 }
 
 O3S_PRELOAD(als_dense)

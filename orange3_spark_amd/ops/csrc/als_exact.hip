@@ -29,6 +29,8 @@
 // fp32 throughout (the S sums are short: n_u terms).
 #include "common.h"
 
+#include <stdlib.h>
+
 using namespace o3s;
 
 namespace {
@@ -119,7 +121,8 @@ __device__ __forceinline__ float wood_factor_solve(float (&srow)[KN], float v, f
 // measured 14% slower: profiles/kernel_experiments_r4.json)
 // KN: the longest row of the launch (32, or 16 for the launch of the short rows: half the
 // P registers, and S on v_mfma_f32_16x16x4_f32 -- a quarter of the matrix-pipe cycles)
-template <int R, int KN = kNW, bool TIM = false>
+// WOOD24_16: the 17..24- and 25..32-rating launches build S on 16 x 16 tiles (see the S build)
+template <int R, int KN = kNW, bool TIM = false, bool WOOD24_16 = true>
 __global__ __launch_bounds__(kWW * 64, 3) void als_wood_kernel(
     const int64_t* __restrict__ indptr, const int32_t* __restrict__ cols, const float* __restrict__ w,
     const float* __restrict__ b, const float* __restrict__ P, const float* __restrict__ eig,
@@ -216,6 +219,48 @@ __global__ __launch_bounds__(kWW * 64, 3) void als_wood_kernel(
     const bool rok = (lane & 31) < 16;
 #pragma unroll
     for (int m = 0; m < 16; ++m) srow[m] = rok ? S[lane & 31][m] : 0.f;
+  } else if (WOOD24_16) {
+    // S (24 or 32 rows) as three 16 x 16 tiles (rows 0-15 / 16-31 of the image; rows >= n
+    // are zero): S00, S01, S11 on v_mfma_f32_16x16x4_f32 -- 96 MFMAs of 8 passes instead of
+    // the 32 x 32 tile's 64 of 16: the upper blocks only, a quarter of the matrix-pipe
+    // cycles saved (17..24-rating launch: 7.5 -> 6.8-7.4 ms per 2M rows, tools/als_wood_phases.py)
+    const int g = lane >> 4;
+    const float* rq0 = sp + (lane & 15) * kPS + 16 * g + (g >> 1) * 4;
+    const float* rq1 = rq0 + 16 * kPS;
+    float4_ s00 = {0.f, 0.f, 0.f, 0.f}, s01 = {0.f, 0.f, 0.f, 0.f}, s11 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int hf = 0; hf < RV; ++hf) {
+#pragma unroll
+      for (int i = 0; i < kNW; ++i)
+        sp[i * kPS + wcol] = i >= KN ? 0.f : (hf == 0 ? acc[i < KN ? i : 0].x * sq.x : acc[i < KN ? i : 0].y * sq.y);
+#pragma unroll
+      for (int s4 = 0; s4 < 16; s4 += 4) {
+        const float4_ x0 = *reinterpret_cast<const float4_*>(rq0 + s4);
+        const float4_ x1 = *reinterpret_cast<const float4_*>(rq1 + s4);
+        const float a0[4] = {x0.x, x0.y, x0.z, x0.w}, a1[4] = {x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          s00 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[c], a0[c], s00, 0, 0, 0);
+          s01 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[c], a1[c], s01, 0, 0, 0);
+          s11 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[c], a1[c], s11, 0, 0, 0);
+        }
+      }
+    }
+    // register q of lane l: row 4 (l >> 4) + q, column l & 15 of its tile; S01 also as the
+    // lower block S10 = S01^T
+    const int c = lane & 15;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      S[4 * g + q][c] = s00[q];
+      S[4 * g + q][16 + c] = s01[q];
+      S[16 + c][4 * g + q] = s01[q];
+      S[16 + 4 * g + q][16 + c] = s11[q];
+    }
+    asm volatile("" ::: "memory");
+    if (lane < kNW) S[lane][lane] += winv;
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int m = 0; m < KN; ++m) srow[m] = S[lane & 31][m];
   } else {
   f32x16_ sa0, sa1;
 #pragma unroll
@@ -477,31 +522,52 @@ O3S_API int o3s_als_wood_timed(int kn, const int64_t* indptr, const int32_t* col
   return 0;
 }
 
+// A/B switch, read per call so a benchmark can flip it between launches:
+// O3S_ALS_WOOD24_16=0 -- the 17..32-rating launches build S as one 32 x 32 tile.
+// (Rejected, profiles/kernel_experiments_r6.json: rank-128 rows gathered as float2
+// (features 2 l, 2 l + 1: one load per factor row instead of two) -- neutral.)
+static bool env_on(const char* name) {
+  const char* e = getenv(name);
+  return !(e && e[0] == '0');
+}
+
+template <int RR, int KN, bool S16>
+void wood_launch(dim3 grid, hipStream_t st, const int64_t* indptr, const int32_t* cols, const float* w,
+                 const float* b, const float* P, const float* eig, const float* lam, const int32_t* small,
+                 int64_t nsmall, float* X) {
+  hipLaunchKernelGGL((als_wood_kernel<RR, KN, false, S16>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, b, P,
+                     eig, lam, small, nsmall, X, nullptr);
+}
+
+template <int RR>
+void wood_dispatch(int kn, dim3 grid, hipStream_t st, const int64_t* indptr, const int32_t* cols, const float* w,
+                   const float* b, const float* P, const float* eig, const float* lam, const int32_t* small,
+                   int64_t nsmall, float* X) {
+  const bool s16 = env_on("O3S_ALS_WOOD24_16");
+#define O3S_WL(KN, S) wood_launch<RR, KN, S>(grid, st, indptr, cols, w, b, P, eig, lam, small, nsmall, X)
+  if (kn == 16) O3S_WL(16, true);
+  else if (kn == 24) { if (s16) O3S_WL(24, true); else O3S_WL(24, false); }
+  else { if (s16) O3S_WL(kNW, true); else O3S_WL(kNW, false); }
+#undef O3S_WL
+}
+
 // Woodbury rows of at most kn ratings (kn = 16: the short-row build, 16 x 16 S on
-// v_mfma_f32_16x16x4_f32; 24 / 32: the 32 x 32 S), panel-blocked Cholesky.
+// v_mfma_f32_16x16x4_f32; 24 / 32: S on three 16 x 16 tiles), panel-blocked Cholesky.
 O3S_API int o3s_als_wood_kn(int R, int kn, const int64_t* indptr, const int32_t* cols, const float* w,
                             const float* b, const float* P, const float* eig, const float* lam, const int32_t* small,
                             int64_t nsmall, float* X, hipStream_t st) {
   if (nsmall < 0 || !eig || !P || (kn != 16 && kn != 24 && kn != 32)) return -1;
   if (nsmall == 0) return 0;
   const dim3 grid((unsigned)((nsmall + kWW - 1) / kWW));
-#define O3S_WK(RR)                                                                                          \
-  if (R == RR) {                                                                                            \
-    if (kn == 16)                                                                                           \
-      hipLaunchKernelGGL((als_wood_kernel<RR, 16>), grid, dim3(kWW * 64), 0, st, indptr,    \
-                         cols, w, b, P, eig, lam, small, nsmall, X, nullptr);                               \
-    else if (kn == 24)                                                                                      \
-      hipLaunchKernelGGL((als_wood_kernel<RR, 24>), grid, dim3(kWW * 64), 0, st, indptr,    \
-                         cols, w, b, P, eig, lam, small, nsmall, X, nullptr);                               \
-    else                                                                                                    \
-      hipLaunchKernelGGL((als_wood_kernel<RR>), grid, dim3(kWW * 64), 0, st, indptr, cols, w, \
-                         b, P, eig, lam, small, nsmall, X, nullptr);                                        \
-    O3S_CHECK_LAUNCH();                                                                                     \
-    return 0;                                                                                               \
+  switch (R) {
+    case 32: wood_dispatch<32>(kn, grid, st, indptr, cols, w, b, P, eig, lam, small, nsmall, X); break;
+    case 64: wood_dispatch<64>(kn, grid, st, indptr, cols, w, b, P, eig, lam, small, nsmall, X); break;
+    case 96: wood_dispatch<96>(kn, grid, st, indptr, cols, w, b, P, eig, lam, small, nsmall, X); break;
+    case 128: wood_dispatch<128>(kn, grid, st, indptr, cols, w, b, P, eig, lam, small, nsmall, X); break;
+    default: return -2;
   }
-  O3S_WK(32) O3S_WK(64) O3S_WK(96) O3S_WK(128)
-#undef O3S_WK
-  return -2;
+  O3S_CHECK_LAUNCH();
+  return 0;
 }
 
 // x = Q y for the listed rows: read from Y, written to X (Y == X: in place).

@@ -365,6 +365,44 @@ def test_gpu_dense_wave_streams_many_rows_per_wave(R, implicit, grid):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("R", [32, 64, 96, 128])
+@pytest.mark.parametrize("grid", [1, 256])
+def test_gpu_dense_wave_diagonal_g_matches_fp64(R, grid):
+    """The eigenbasis dense solve with G = diag(g) passed as a vector (o3s_als_dense_wave_gd:
+    no G image in LDS, the deeper gather ring) == the fp64 solve of the same systems, and
+    == the full-G build fed diag(g) up to fp32 rounding; rows of 1..2000 ratings."""
+    from orange3_spark_amd.ops import als as A
+    g = torch.Generator().manual_seed(R + grid + 1)
+    n_rows, n_other = 700, 4000
+    lens = torch.randint(33, 260, (n_rows,), generator=g)
+    lens[:5] = torch.tensor([1, 16, 17, 2000, 33])
+    indptr = torch.zeros(n_rows + 1, dtype=torch.int64)
+    indptr[1:] = torch.cumsum(lens, 0)
+    nnz = int(indptr[-1])
+    cols = torch.randint(0, n_other, (nnz,), generator=g, dtype=torch.int32)
+    vals = torch.rand(nnz, generator=g) * 4
+    vals[::11] = 0.0
+    F = torch.randn((n_other, R), generator=g) / R ** 0.5
+    gdiag = torch.rand(R, generator=g) * n_other / R
+    w, b, pos = AE._weights(vals, True, 1.5)
+    rows = torch.repeat_interleave(torch.arange(n_rows), lens)
+    lam = (0.05 * torch.zeros(n_rows).index_add_(0, rows, pos.float()).clamp_min(1.0)).float()
+    dev = "cuda"
+    indptr, cols, w, b, F, lam, gdiag = (x.to(dev) for x in (indptr, cols, w, b, F, lam, gdiag))
+    order = torch.argsort(lens, descending=True).to(torch.int32).to(dev)
+    got = torch.full((n_rows, R), float("nan"), device=dev)
+    A.dense_wave(True, indptr, cols, w, b, F, None, lam, order, got, grid=grid, gdiag=gdiag.contiguous())
+    ref = torch.empty((n_rows, R), dtype=torch.float64, device=dev)
+    A.exact_solve_torch(indptr, cols, w, b, F, torch.diag(gdiag), lam, ref)
+    assert not torch.isnan(got).any()
+    err = (got.double() - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-6)
+    assert float(err.max()) < 2e-3, float(err.max())
+    full = torch.full_like(got, float("nan"))
+    A.dense_wave(True, indptr, cols, w, b, F, torch.diag(gdiag).contiguous(), lam, order, full, grid=grid)
+    assert float(((full - got).norm(dim=1) / full.norm(dim=1).clamp_min(1e-6)).max()) < 1e-4
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("R", [32, 128])
 @pytest.mark.parametrize("grid", [1, 256])
 def test_gpu_dense_wave_short_rows_metadata_ring(R, grid):

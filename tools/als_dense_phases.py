@@ -51,12 +51,20 @@ def main():
         N.check(lib.o3s_als_dense_wave(1, R, meta.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                                        F.data_ptr(), G.data_ptr(), a.items, out.data_ptr(), grid, st), "dense")
 
+    gd = torch.diagonal(G).contiguous()
+
+    def prod_gd():
+        N.check(lib.o3s_als_dense_wave_gd(R, meta.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                          F.data_ptr(), gd.data_ptr(), a.items, out.data_ptr(), grid, st),
+                "dense_gd")
+
     def timed():
         N.check(lib.o3s_als_dense_wave_timed(meta.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                                              F.data_ptr(), G.data_ptr(), a.items, out.data_ptr(), grid,
                                              tim.data_ptr(), st), "dense_timed")
     res = {"items": a.items, "ratings": nnz, "mean_ratings": round(nnz / a.items, 1), "grid": grid}
-    for name, fn in (("production", prod), ("timed", timed)):
+    runs = (("production", prod), ("production_gdiag", prod_gd))
+    for name, fn in list(runs) * 3 + [("timed", timed)]:     # production A/B alternated (box noise)
         fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -64,7 +72,16 @@ def main():
         fn()
         e1.record()
         torch.cuda.synchronize()
-        res[name + "_ms"] = round(e0.elapsed_time(e1), 3)
+        res.setdefault(name + "_ms", []).append(round(e0.elapsed_time(e1), 3))
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        fn()
+        e1.record()
+        torch.cuda.synchronize()
+        res.setdefault(name + "_ms", []).append(round(e0.elapsed_time(e1), 3))
+    os.environ.pop("O3S_ALS_DENSE_IL", None)
     t = tim.double()
     waves = int((t.sum(1) > 0).sum())
     tot = t.sum(0)

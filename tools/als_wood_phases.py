@@ -55,6 +55,22 @@ def main():
                                        eig.data_ptr(), lam.data_ptr(), small.data_ptr(), a.users, out.data_ptr(),
                                        tim.data_ptr(), st), "wood_timed")
     res = {}
+    # A/B of the build switches (csrc/als_exact.hip), alternated, 5 rounds: min / median ms
+    variants = {"s16": "1", "s32": "0"} if a.kn != 16 else {"s16": "1"}
+    ab = {k: [] for k in variants}
+    for rep in range(5):
+        for k, s16 in variants.items():
+            os.environ["O3S_ALS_WOOD24_16"] = s16
+            prod()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            prod()
+            e1.record()
+            torch.cuda.synchronize()
+            ab[k].append(e0.elapsed_time(e1))
+    os.environ.pop("O3S_ALS_WOOD24_16")
+    res["ab_ms"] = {k: {"min": round(min(v), 3), "median": round(sorted(v)[len(v) // 2], 3)} for k, v in ab.items()}
     for name, fn in (("production", prod), ("timed", timed)):
         fn()
         torch.cuda.synchronize()
