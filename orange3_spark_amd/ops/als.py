@@ -122,6 +122,7 @@ EXACT_RANKS = (32, 64, 96, 128)
 # eigenbasis dense solves with G = diag(eig) passed as a vector (no 40 KB G image in LDS,
 # so a 4-step gather ring at rank 128); O3S_ALS_DENSE_GDIAG=0: the full-G build (A/B)
 DENSE_GDIAG = os.environ.get("O3S_ALS_DENSE_GDIAG", "1") != "0"
+
 # Long rows (more than 32 ratings, or lam_u = 0) take als_dense_wave_kernel
 # (csrc/als_dense.hip): one wave per row, four independent waves per CU, factor rows
 # gathered by an LDS-DMA ring that streams across the rows of a wave, rows listed longest
@@ -370,6 +371,17 @@ def dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, rows, out, grid=None, g
         return out
     meta = dense_meta(indptr, rows, lam)
     lib = N.kernels()
+    if gdiag is not None:
+            gmode, g = 1, gdiag.float().contiguous()
+        elif implicit:
+            gmode, g = 2, pair_g_image(Gf)
+        else:
+            gmode, g = 0, None
+        N.check(lib.o3s_als_dense_pair(gmode, meta.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                       F.data_ptr(), N.ptr(g), n, out.data_ptr(),
+                                       (4 * N.num_cus(F.device)) if grid is None else grid, N.stream_of(out)),
+                "als_dense_pair")
+        return out
     if gdiag is not None:
         N.check(lib.o3s_als_dense_wave_gd(R, meta.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                                           F.data_ptr(), gdiag.data_ptr(), n, out.data_ptr(),
