@@ -372,17 +372,6 @@ def dense_wave(implicit, indptr, cols, w, b, F, Gf, lam, rows, out, grid=None, g
     meta = dense_meta(indptr, rows, lam)
     lib = N.kernels()
     if gdiag is not None:
-            gmode, g = 1, gdiag.float().contiguous()
-        elif implicit:
-            gmode, g = 2, pair_g_image(Gf)
-        else:
-            gmode, g = 0, None
-        N.check(lib.o3s_als_dense_pair(gmode, meta.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
-                                       F.data_ptr(), N.ptr(g), n, out.data_ptr(),
-                                       (4 * N.num_cus(F.device)) if grid is None else grid, N.stream_of(out)),
-                "als_dense_pair")
-        return out
-    if gdiag is not None:
         N.check(lib.o3s_als_dense_wave_gd(R, meta.data_ptr(), cols.data_ptr(), w.data_ptr(), b.data_ptr(),
                                           F.data_ptr(), gdiag.data_ptr(), n, out.data_ptr(),
                                           N.num_cus(F.device) if grid is None else grid, N.stream_of(out)),
