@@ -24,6 +24,7 @@ the namespace provides ``qtgui`` / ``qtcore``.
 """
 from __future__ import annotations
 
+import re
 import os
 
 
@@ -236,14 +237,38 @@ def _highlighter(qtgui, document):
     return PythonHighlighter(document)
 
 
+def complete_line(text: str, matches: list) -> tuple:
+    """Tab in the console input: (new text, listing) -- one match replaces the last token,
+    several extend it by their common prefix and are listed in the console."""
+    import os
+    m = re.search(r"[%\w.]*$", text)
+    tok = m.group(0) if m else ""
+    if not matches:
+        return text, ""
+    if len(matches) == 1:
+        return text[:len(text) - len(tok)] + matches[0], ""
+    common = os.path.commonprefix(matches)
+    return text[:len(text) - len(tok)] + (common if len(common) > len(tok) else tok), "  ".join(matches) + "\n"
+
+
 def _console_input(qt, qtcore, core, refresh):
-    """One-line console input: Return runs the line, Up/Down walk the history."""
+    """One-line console input: Return runs the line, Up/Down walk the history, Tab completes."""
     if qtcore is None:
         line = qt.QLineEdit()
     else:
         K = qtcore.Qt
 
         class ConsoleLine(qt.QLineEdit):
+            def event(self, ev):        # Tab would move the focus before keyPressEvent sees it
+                if getattr(ev, "type", lambda: None)() == qtcore.QEvent.KeyPress and ev.key() == K.Key_Tab:
+                    text, listing = complete_line(self.text(), core.console_complete(self.text()))
+                    self.setText(text)
+                    if listing:
+                        core.console_output += listing
+                        refresh()
+                    return True
+                return super().event(ev)
+
             def keyPressEvent(self, ev):
                 if ev.key() == K.Key_Up:
                     self.setText(core.console_history(-1))

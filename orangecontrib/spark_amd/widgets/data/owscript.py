@@ -7,7 +7,11 @@ working semantics are trash/OLDpyspark_script_console.py:489-492,641-648).
 
 Also as in the reference: an interactive console over the SAME namespace (lines run one
 at a time, state persists between lines and with the script, ``out_object`` is read
-back; ``code.InteractiveConsole`` semantics of trash/OLDpyspark_script_console.py:125-286),
+back; ``code.InteractiveConsole`` semantics of trash/OLDpyspark_script_console.py:125-286)
+with the IPython conveniences of the reference's embedded qtconsole
+(pyspark_script_console.py:20-29,331): line magics (%time, %timeit, %who, %whos, %reset,
+%run, %history, %pwd, %cd, %env, %lsmagic), ``obj?`` / ``obj??`` help, ``!cmd`` and Tab
+completion (script_support.ScriptConsole),
 "Import a script from a file" / "Save selected script to a file"
 (pyspark_script_console.py:286-291,368-392,441-461); the Qt view adds the syntax
 highlighter and the auto-indenting editor (script_support.py, ref :39-132)."""
@@ -135,6 +139,13 @@ class OWScript(SharedSession, Widget):
         more = con.paste(source)
         self.out_object = self.namespace.get("out_object")
         return more
+
+    def console_complete(self, text: str) -> list:
+        """Completions of the last token of ``text`` (namespace names and attributes, line
+        magics) over the widget namespace."""
+        if not self.console.more:
+            self._bind()
+        return self.console.complete(text)
 
     def console_history(self, step: int) -> str:
         """Previous (step < 0) / next (step > 0) console line."""

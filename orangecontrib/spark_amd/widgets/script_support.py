@@ -126,11 +126,188 @@ class ScriptConsole(code.InteractiveConsole):
         out = _Writer(self.write)
         with capture_output(out):
             try:
+                if not self.more and self._special(line):
+                    return self.more
                 self.more = bool(super().push(line))
             except SystemExit:
                 self.resetbuffer()
                 self.more = False
         return self.more
+
+    # ---- IPython conveniences (the reference embeds an IPython kernel, qtconsole:
+    # pyspark_script_console.py:20-29,331; none is importable here, so the usual line
+    # magics, ``obj?`` help, ``!cmd`` and completion are implemented over this namespace) --
+    MAGICS = ("cd", "env", "history", "lsmagic", "pwd", "reset", "run", "time", "timeit", "who", "whos")
+    _HELP = re.compile(r"^\s*([A-Za-z_][\w.]*)\s*(\?\??)\s*$")
+
+    def _special(self, line: str) -> bool:
+        """Run ``line`` if it is a magic, a help request or a shell escape; False if it is
+        plain Python."""
+        s = line.strip()
+        if s.startswith("%"):
+            name, _, arg = s[1:].partition(" ")
+            fn = getattr(self, "_magic_" + name, None)
+            if fn is None:
+                print(f"UsageError: Line magic function `%{name}` not found.")
+            else:
+                try:
+                    fn(arg.strip())
+                except Exception:  # noqa: BLE001
+                    self.showtraceback()
+            return True
+        if s.startswith("!"):
+            import subprocess
+            r = subprocess.run(s[1:], shell=True, capture_output=True, text=True)
+            print((r.stdout + r.stderr).rstrip("\n"))
+            return True
+        m = self._HELP.match(line)
+        if m:
+            self._help(m.group(1), m.group(2) == "??")
+            return True
+        return False
+
+    def _eval(self, expr: str):
+        return eval(expr, self.locals)
+
+    def _help(self, expr: str, source: bool) -> None:
+        import inspect
+        try:
+            obj = self._eval(expr)
+        except Exception as e:  # noqa: BLE001
+            print(f"Object `{expr}` not found ({type(e).__name__}).")
+            return
+        print(f"Type:      {type(obj).__name__}")
+        try:
+            print(f"Signature: {expr}{inspect.signature(obj)}")
+        except (TypeError, ValueError):
+            pass
+        if source:
+            try:
+                print(inspect.getsource(obj))
+                return
+            except (TypeError, OSError):
+                pass
+        doc = inspect.getdoc(obj)
+        print("Docstring:", doc if doc else "<no docstring>")
+
+    def _user_names(self):
+        hidden = {"session", "spark", "sc", "hc", "in_object", "out_object", "__builtins__"}
+        import types
+        return sorted(k for k, v in self.locals.items()
+                      if not k.startswith("_") and k not in hidden and not isinstance(v, types.ModuleType))
+
+    def _magic_time(self, stmt: str) -> None:
+        import time
+        t = time.perf_counter()
+        try:
+            val = eval(compile(stmt, "<magic>", "eval"), self.locals)
+            is_expr = True
+        except SyntaxError:
+            exec(compile(stmt, "<magic>", "exec"), self.locals)
+            is_expr, val = False, None
+        el = time.perf_counter() - t
+        print(f"Wall time: {_fmt_seconds(el)}")
+        if is_expr and val is not None:
+            print(repr(val))
+
+    def _magic_timeit(self, arg: str) -> None:
+        import shlex
+        import timeit
+        toks = shlex.split(arg)
+        number, repeat = 0, 7
+        while toks and toks[0] in ("-n", "-r") and len(toks) > 1:
+            if toks[0] == "-n":
+                number = int(toks[1])
+            else:
+                repeat = int(toks[1])
+            toks = toks[2:]
+        stmt = " ".join(toks)
+        t = timeit.Timer(stmt, globals=self.locals)
+        if number <= 0:
+            number = t.autorange()[0]
+        runs = [x / number for x in t.repeat(repeat=repeat, number=number)]
+        mean = sum(runs) / len(runs)
+        sd = (sum((x - mean) ** 2 for x in runs) / len(runs)) ** 0.5
+        print(f"{_fmt_seconds(mean)} ± {_fmt_seconds(sd)} per loop (mean ± std. dev. of {repeat} runs, "
+              f"{number} loops each)")
+
+    def _magic_who(self, arg: str) -> None:
+        names = self._user_names()
+        print("  ".join(names) if names else "Interactive namespace is empty.")
+
+    def _magic_whos(self, arg: str) -> None:
+        names = self._user_names()
+        if not names:
+            print("Interactive namespace is empty.")
+            return
+        rows = [(n, type(self.locals[n]).__name__, repr(self.locals[n])[:60]) for n in names]
+        w0 = max(8, max(len(r[0]) for r in rows))
+        w1 = max(4, max(len(r[1]) for r in rows))
+        print(f"{'Variable':<{w0}}   {'Type':<{w1}}   Data/Info")
+        print("-" * (w0 + w1 + 16))
+        for n, t, r in rows:
+            print(f"{n:<{w0}}   {t:<{w1}}   {r}")
+
+    def _magic_reset(self, arg: str) -> None:
+        if "-f" not in arg.split():
+            print("Use %reset -f to delete every user variable (session, in_object and out_object stay).")
+            return
+        for n in self._user_names():
+            del self.locals[n]
+
+    def _magic_history(self, arg: str) -> None:
+        n = int(arg.lstrip("-n").strip() or 0) if arg else 0
+        hist = [h for h in self.history if h.strip()][:-1]        # minus this %history line
+        for h in hist[-n:] if n else hist:
+            print(h)
+
+    def _magic_run(self, path: str) -> None:
+        with open(path, "rb") as f:
+            src = f.read().decode("utf-8", errors="replace")
+        self.locals.setdefault("__name__", "__main__")
+        exec(compile(src, path, "exec"), self.locals)
+
+    def _magic_pwd(self, arg: str) -> None:
+        import os
+        print(os.getcwd())
+
+    def _magic_cd(self, arg: str) -> None:
+        import os
+        os.chdir(os.path.expanduser(arg or "~"))
+        print(os.getcwd())
+
+    def _magic_env(self, arg: str) -> None:
+        import os
+        if not arg:
+            for k in sorted(os.environ):
+                print(f"{k}={os.environ[k]}")
+        elif "=" in arg:
+            k, _, v = arg.partition("=")
+            os.environ[k.strip()] = v.strip()
+        else:
+            print(os.environ.get(arg, ""))
+
+    def _magic_lsmagic(self, arg: str) -> None:
+        print("Available line magics:\n" + "  ".join("%" + m for m in self.MAGICS))
+
+    def complete(self, text: str) -> list[str]:
+        """Completions of the last token of ``text`` over the console namespace (names,
+        attributes, keywords, builtins -- rlcompleter -- and the line magics)."""
+        import rlcompleter
+        m = re.search(r"[%\w.]*$", text)
+        tok = m.group(0) if m else ""
+        if tok.startswith("%"):
+            return sorted("%" + k for k in self.MAGICS if k.startswith(tok[1:]))
+        comp = rlcompleter.Completer(self.locals)
+        out, i = [], 0
+        while True:
+            c = comp.complete(tok, i)
+            if c is None:
+                break
+            if c not in out:
+                out.append(c)
+            i += 1
+        return out
 
     def paste(self, source: str) -> bool:
         """Run pasted source line by line (reference pasteCode).  Unlike a bare REPL, a
@@ -158,6 +335,13 @@ class ScriptConsole(code.InteractiveConsole):
 
 
 _CONTINUES = re.compile(r"(?:elif|else|except|finally|case)\b|[)\]}]")
+
+
+def _fmt_seconds(t: float) -> str:
+    for unit, scale in (("s", 1.0), ("ms", 1e-3), ("µs", 1e-6)):
+        if t >= scale:
+            return f"{t / scale:.3g} {unit}"
+    return f"{t / 1e-9:.3g} ns"
 
 
 class _Writer:

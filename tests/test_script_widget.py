@@ -118,3 +118,59 @@ def test_console_class_standalone():
     c.push("2]")
     c.push("print(sum(a))")
     assert "3\n" in "".join(out)
+
+
+def test_console_ipython_conveniences(session, tmp_path):
+    """The reference's console is an embedded IPython kernel (pyspark_script_console.py:
+    20-29,331); without IPython the console still takes line magics, ``obj?`` help, ``!cmd``
+    and Tab completion over the widget namespace."""
+    w = OWScript()
+    w.console_push("%time total = sum(range(1000))")
+    assert "Wall time:" in w.console_output and w.namespace["total"] == 499500
+    w.console_push("%timeit -n 5 -r 2 sum(range(100))")
+    assert "per loop (mean ± std. dev. of 2 runs, 5 loops each)" in w.console_output
+    w.console_push("%who")
+    assert "total" in w.console_output.splitlines()[-1]
+    w.console_push("%whos")
+    assert "Variable" in w.console_output and "int" in w.console_output
+    w.console_push("def twice(v):")
+    w.console_push("    '''Double v.'''")
+    w.console_push("    return 2 * v")
+    w.console_push("")
+    w.console_push("twice?")
+    assert "Signature: twice(v)" in w.console_output and "Double v." in w.console_output
+    w.console_push("twice??")
+    assert "return 2 * v" in w.console_output
+    w.console_push("nothing_here?")
+    assert "Object `nothing_here` not found" in w.console_output
+    w.console_push("!echo shell-says-hi")
+    assert "shell-says-hi" in w.console_output
+    w.console_push("%nosuchmagic")
+    assert "UsageError: Line magic function `%nosuchmagic` not found." in w.console_output
+    p = tmp_path / "snippet.py"
+    p.write_text("out_object = twice(total)\n")
+    w.console_push(f"%run {p}")
+    assert w.out_object == 999000
+    w.console_push("%history -n 2")
+    assert w.console_output.rstrip().endswith(f"%run {p}")
+    # completion: names, attributes, magics
+    assert "twice(" in w.console_complete("print(twi")
+    assert any(c.startswith("total.") for c in w.console_complete("total.bit"))
+    assert w.console_complete("%tim") == ["%time", "%timeit"]
+    # session objects survive %reset -f; user names do not
+    w.console_push("%reset -f")
+    assert "total" not in w.namespace and "twice" not in w.namespace
+    assert w.namespace["session"] is session
+    # plain Python still flows through (a block is never taken for a magic)
+    assert w.console_push("for i in range(2):")
+    assert w.console_push("    out_object = i")
+    assert not w.console_push("")
+    assert w.out_object == 1
+
+
+def test_console_tab_completion_text():
+    from orangecontrib.spark_amd.widgets.custom_views import complete_line
+    assert complete_line("x = ran", ["range("]) == ("x = range(", "")
+    text, listing = complete_line("%ti", ["%time", "%timeit"])
+    assert text == "%time" and listing == "%time  %timeit\n"
+    assert complete_line("zz", []) == ("zz", "")
