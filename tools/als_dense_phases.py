@@ -73,15 +73,6 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         res.setdefault(name + "_ms", []).append(round(e0.elapsed_time(e1), 3))
-        fn()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        fn()
-        e1.record()
-        torch.cuda.synchronize()
-        res.setdefault(name + "_ms", []).append(round(e0.elapsed_time(e1), 3))
-    os.environ.pop("O3S_ALS_DENSE_IL", None)
     t = tim.double()
     waves = int((t.sum(1) > 0).sum())
     tot = t.sum(0)

@@ -31,4 +31,4 @@ for name, order in (("seq", torch.arange(n, device=dev, dtype=torch.int32)),
                 T.node_hist(bins, order, yp, None, lo, hi, node, nseg, B, 3, False, chunk=chunk, ypos=True)
             torch.cuda.synchronize()
             res[f"{name}_seg{nseg}_chunk{chunk}"] = round((time.perf_counter() - t) / 3 * 1e3, 3)
-print(json.dumps({"n": n, "F": F, "B": B, "pairs": os.environ.get("O3S_HIST_PAIRS", "1"), "ms": res}))
+print(json.dumps({"n": n, "F": F, "B": B, "ms": res}))
