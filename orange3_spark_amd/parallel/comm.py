@@ -221,7 +221,9 @@ class TorchComm(Comm):
         self.backend = dist.get_backend(group)
         self._cpu_group = None
         if self.backend != "gloo":
-            self._cpu_group = dist.new_group(backend="gloo")
+            # the same ranks as ``group`` (a subgroup's host collectives must not span the world)
+            ranks = None if group is None else dist.get_process_group_ranks(group)
+            self._cpu_group = dist.new_group(ranks=ranks, backend="gloo")
 
     def all_reduce(self, t, op="sum"):
         if self.world_size > 1:
