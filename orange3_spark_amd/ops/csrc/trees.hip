@@ -659,7 +659,7 @@ __global__ __launch_bounds__(256) void bin_features_kernel(const void* __restric
 // four of its items before the first search, so each block keeps several row loads in
 // flight per barrier; the feature-major copy leaves the [F][ROWS] LDS tile as 4-row dwords
 // (ldt % 4 == 0; one byte per lane otherwise).
-template <bool BF16, int ROWS>
+template <bool BF16, int ROWS, int LVC = 0>
 __global__ __launch_bounds__(256) void bin_features_vec_kernel(const void* __restrict__ Xv, int64_t n, int64_t ldx,
                                                                int F, const float* __restrict__ th, int Tp,
                                                                uint8_t* __restrict__ out, uint8_t* __restrict__ out_t,
@@ -668,9 +668,28 @@ __global__ __launch_bounds__(256) void bin_features_vec_kernel(const void* __res
   extern __shared__ float sth[];
   const int TS = Tp + 1;
   uint8_t* const tile = reinterpret_cast<uint8_t*>(sth + F * TS);
-  for (int i = threadIdx.x; i < F * Tp; i += 256) sth[(i / Tp) * TS + i % Tp] = th[i];
-  __syncthreads();
   const int G = F >> 3;                                  // 8-feature groups per row
+  // LVC > 0 (Tp == 2^LVC): thresholds in search-tree order, per level, the G features of one
+  // k-slice (features 8 g + k) interleaved: level L of feature 8 g + k at sth[k G (Tp - 1) +
+  // G (2^L - 1) + g 2^L + j], j in [0, 2^L) holding threshold (2 j + 1) 2^(LVC - 1 - L) - 1.
+  // A lane walks r = g 2^L + j, r' = 2 r + (t < x), from a per-(k, L) uniform base, and the
+  // eight features' searches run interleaved level by level (eight independent LDS chains, no
+  // loop) -- the runtime-depth search below spent ~6 VALU and a full LDS round trip per level
+  // and feature.  A wave's level-L lookups fall in one block of G 2^L floats (distinct banks
+  // up to level 3 at G = 8; the [F][Tp + 1] table put 75% of the LDS cycles in bank conflicts).
+  if constexpr (LVC > 0) {
+    for (int i = threadIdx.x; i < F * (Tp - 1); i += 256) {
+      const int k = i / (G * (Tp - 1)), rem = i % (G * (Tp - 1));
+      int L = 0;
+      while (G * ((2 << L) - 1) <= rem) ++L;               // rem in level L's block
+      const int off = rem - G * ((1 << L) - 1);
+      const int g = off >> L, j = off & ((1 << L) - 1);
+      sth[i] = th[(8 * g + k) * Tp + (2 * j + 1) * (1 << (LVC - 1 - L)) - 1];
+    }
+  } else {
+    for (int i = threadIdx.x; i < F * Tp; i += 256) sth[(i / Tp) * TS + i % Tp] = th[i];
+  }
+  __syncthreads();
   const bool dw = (ldt & 3) == 0 && ((uintptr_t)out_t & 3) == 0;
   const int64_t nchunks = (n + ROWS - 1) / ROWS;
   for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
@@ -706,12 +725,35 @@ __global__ __launch_bounds__(256) void bin_features_vec_kernel(const void* __res
         if (li >= items) break;
         const int lr = li / G, g = li - lr * G;
         const int64_t row = r0 + lr;
+        int bin[8];
+        if constexpr (LVC > 0) {
+          int g0 = g;
+          asm volatile("" : "+v"(g0));                     // keep g = li - lr G out of the addresses
+#pragma unroll
+          for (int k = 0; k < 8; ++k) bin[k] = g0;
+#pragma unroll
+          for (int L = 0; L < LVC; ++L) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const float t = sth[G * (k * ((1 << LVC) - 1) + (1 << L) - 1) + bin[k]];
+              bin[k] = 2 * bin[k] + (t < x[u][k] ? 1 : 0);
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < 8; ++k) bin[k] &= (1 << LVC) - 1;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float* a = sth + (8 * g + k) * TS;
+            int bk = 0;
+            for (int st = Tp >> 1; st > 0; st >>= 1) bk += (a[bk + st - 1] < x[u][k]) ? st : 0;
+            bin[k] = bk;
+          }
+        }
         uint32_t lo = 0, hi = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float* a = sth + (8 * g + k) * TS;
-          int bk = 0;
-          for (int st = Tp >> 1; st > 0; st >>= 1) bk += (a[bk + st - 1] < x[u][k]) ? st : 0;
+          const int bk = bin[k];
           if (k < 4) lo |= (uint32_t)bk << (8 * k);
           else hi |= (uint32_t)bk << (8 * (k - 4));
           if (out_t != nullptr) tile[(8 * g + k) * TSR + lr] = (uint8_t)bk;
@@ -1223,6 +1265,31 @@ O3S_API int o3s_slab_range_sum(const void* in, int in_f64, int64_t C, const int6
   return 0;
 }
 
+// O3S_BIN_EYT=0: the runtime-depth search over the row-major [F][Tp + 1] table instead of
+// the unrolled search-tree kernel (A/B; read per call)
+static bool bin_eyt() {
+  const char* e = getenv("O3S_BIN_EYT");
+  return !(e && e[0] == '0');
+}
+
+template <bool BF16>
+static void bin_vec256_launch(int LV, unsigned grid, size_t lds, hipStream_t st, const void* X, int64_t n,
+                              int64_t ldx, int F, const float* th, int Tp, uint8_t* out, uint8_t* out_t,
+                              int64_t ldt) {
+#define O3S_BIN_LV(LVC)                                                                                   \
+  hipLaunchKernelGGL((bin_features_vec_kernel<BF16, 256, LVC>), dim3(grid), dim3(256), lds, st, X, n, ldx, F, th, \
+                     Tp, out, out_t, ldt)
+  switch (bin_eyt() ? LV : 0) {
+    case 4: O3S_BIN_LV(4); break;
+    case 5: O3S_BIN_LV(5); break;
+    case 6: O3S_BIN_LV(6); break;
+    case 7: O3S_BIN_LV(7); break;
+    case 8: O3S_BIN_LV(8); break;
+    default: O3S_BIN_LV(0); break;
+  }
+#undef O3S_BIN_LV
+}
+
 // X: [n][F] fp32 (bf16 != 0: bf16) with row stride ldx; th: [F][Tp] fp32 sorted, +inf
 // padded, Tp a power of two <= 256 with at least one pad per feature; out: [n][F] uint8;
 // out_t (optional): feature f of row r at out_t[f * ldt + r] (ldt >= n: a block of rows of
@@ -1242,12 +1309,12 @@ O3S_API int o3s_bin_features2(const void* X, int bf16, int64_t n, int64_t ldx, i
   const bool big = lds256 <= 64 * 1024;
   const int64_t nch256 = (n + 255) / 256;
   const unsigned grid256 = (unsigned)(nch256 < 4096 ? nch256 : 4096);
+  int LV = 0;
+  while ((1 << LV) < Tp) ++LV;
   if (vec && big && bf16)
-    hipLaunchKernelGGL((bin_features_vec_kernel<true, 256>), dim3(grid256), dim3(256), lds256, st, X, n, ldx, F, th,
-                       Tp, out, out_t, ldt);
+    bin_vec256_launch<true>(LV, grid256, lds256, st, X, n, ldx, F, th, Tp, out, out_t, ldt);
   else if (vec && big)
-    hipLaunchKernelGGL((bin_features_vec_kernel<false, 256>), dim3(grid256), dim3(256), lds256, st, X, n, ldx, F, th,
-                       Tp, out, out_t, ldt);
+    bin_vec256_launch<false>(LV, grid256, lds256, st, X, n, ldx, F, th, Tp, out, out_t, ldt);
   else if (vec && bf16)
     hipLaunchKernelGGL((bin_features_vec_kernel<true, kBinRows>), dim3(grid), dim3(256), lds, st, X, n, ldx, F, th,
                        Tp, out, out_t, ldt);

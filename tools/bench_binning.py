@@ -37,18 +37,27 @@ def main():
     out = torch.empty((n, F), dtype=torch.uint8, device=dev)
     out_t = torch.empty((F, n), dtype=torch.uint8, device=dev)
     res = {}
-    for name, ot in (("with_feature_major", out_t), ("row_major_only", None)):
-        TR._bin_block_kernel(X, tht, Tp, out, ot, n)
-        torch.cuda.synchronize()
-        ts = []
-        for _ in range(a.reps):
-            t = time.perf_counter()
+    sig = {}
+    # O3S_BIN_EYT: per-level interleaved search-tree threshold table (1, default) vs [F][Tp + 1] (0)
+    for lay in ("1", "0"):
+        os.environ["O3S_BIN_EYT"] = lay
+        for name, ot in (("with_feature_major", out_t), ("row_major_only", None)):
             TR._bin_block_kernel(X, tht, Tp, out, ot, n)
             torch.cuda.synchronize()
-            ts.append(time.perf_counter() - t)
-        ms = 1e3 * min(ts)
-        gb = n * F * (2 + 1 + (1 if ot is not None else 0)) / 1e9
-        res[name] = {"ms": round(ms, 3), "GB_moved": round(gb, 1), "TBps": round(gb / ms, 2)}
+            if ot is not None:
+                sig[lay] = (int(out[:: 997].sum()), int(out_t[:, :: 997].sum()))
+            ts = []
+            for _ in range(a.reps):
+                t = time.perf_counter()
+                TR._bin_block_kernel(X, tht, Tp, out, ot, n)
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t)
+            ms = 1e3 * min(ts)
+            gb = n * F * (2 + 1 + (1 if ot is not None else 0)) / 1e9
+            res[("tree_layout_" if lay == "1" else "row_layout_") + name] = {
+                "ms": round(ms, 3), "GB_moved": round(gb, 1), "TBps": round(gb / ms, 2)}
+    os.environ.pop("O3S_BIN_EYT")
+    res["same_bins"] = sig.get("1") == sig.get("0")
     print(json.dumps({"rows": n, "features": F, "bins": a.bins, **res}), flush=True)
 
 
