@@ -210,11 +210,15 @@ def test_gpu_u8_transpose(gpu, n, F):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,F,nb,bf16", [(100_003, 64, 32, False), (100_003, 64, 32, True), (2049, 16, 8, True),
                                          (100_000, 64, 32, True), (4098, 64, 32, False), (100_000, 128, 255, True),
-                                         (5000, 7, 2, False), (777, 130, 255, False), (3, 1, 32, False)])
+                                         (5000, 7, 2, False), (777, 130, 255, False), (3, 1, 32, False),
+                                         # the unrolled search-tree kernel at every depth it is built
+                                         # for (16..256 bins) and 1, 2, 3, 5, 8 feature groups
+                                         (50_001, 24, 16, True), (20_000, 8, 64, False), (65_537, 64, 64, True),
+                                         (30_000, 40, 128, True), (10_007, 16, 256, False), (9_999, 40, 32, False)])
 def test_gpu_bin_features_matches_bucketize(gpu, n, F, nb, bf16):
-    """bin_features (vector kernel for F % 8 == 0: 8 features per lane; scalar kernel
-    otherwise; fp32 or bf16 rows) == torch.bucketize, and the feature-major copy the
-    kernel writes == the transpose."""
+    """bin_features (vector kernel for F % 8 == 0: 8 features per lane, unrolled for the
+    bin count when it has 16..256 bins; scalar kernel otherwise; fp32 or bf16 rows) ==
+    torch.bucketize, and the feature-major copy the kernel writes == the transpose."""
     from orange3_spark_amd.models import trees as TR
     g = torch.Generator().manual_seed(F)
     X = torch.randn(n, F, generator=g)
