@@ -186,6 +186,9 @@ _OPS = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp
 # "ring": RCCL's all_gather (rings over xGMI); "mesh": grouped peer-to-peer transfers to
 # every peer at once (TorchComm._all_gather_mesh).  tools/bench_comm.py times both.
 ALLGATHER_ALGO = os.environ.get("O3S_ALLGATHER", "ring")
+# O3S_COMM_STRICT=1: GPU sessions refuse host tensors in tensor collectives instead of
+# staging them through the device (TorchComm._host)
+COMM_STRICT = os.environ.get("O3S_COMM_STRICT", "0") == "1"
 
 
 class _Works:
@@ -225,14 +228,32 @@ class TorchComm(Comm):
             ranks = None if group is None else dist.get_process_group_ranks(group)
             self._cpu_group = dist.new_group(ranks=ranks, backend="gloo")
 
+    def _host(self, t) -> bool:
+        """True when a GPU session's collective got a host tensor.  RCCL takes device
+        tensors only (gloo, the one-GPU multi-rank rehearsal, takes both), so such tensors
+        are staged through the session device and the result goes back to the host;
+        O3S_COMM_STRICT=1 raises instead, to find the call sites."""
+        if self.device.type != "cuda" or t.device.type == "cuda":
+            return False
+        if COMM_STRICT:
+            raise RuntimeError(f"host tensor {tuple(t.shape)} {t.dtype} passed to a device collective")
+        return True
+
     def all_reduce(self, t, op="sum"):
         if self.world_size > 1:
-            dist.all_reduce(t, op=_OPS[op], group=self.group)
+            if self._host(t):
+                d = t.to(self.device)
+                dist.all_reduce(d, op=_OPS[op], group=self.group)
+                t.copy_(d.cpu())
+            else:
+                dist.all_reduce(t, op=_OPS[op], group=self.group)
         return t
 
     def all_gather(self, t):
         if self.world_size == 1:
             return t
+        if self._host(t):
+            return self.all_gather(t.to(self.device)).cpu()
         t = t.contiguous()
         out = torch.empty((self.world_size * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, t, group=self.group)
@@ -252,6 +273,9 @@ class TorchComm(Comm):
     def all_gather_into(self, out, t, async_op=False):
         if self.world_size == 1:
             out.copy_(t)
+            return None
+        if self._host(out) or self._host(t):
+            out.copy_(self.all_gather(t.to(self.device)).to(out.device))
             return None
         if ALLGATHER_ALGO == "mesh":
             return self._all_gather_mesh(out, t.contiguous(), async_op)
@@ -280,6 +304,8 @@ class TorchComm(Comm):
     def reduce_scatter(self, t):
         if self.world_size == 1:
             return t
+        if self._host(t):
+            return self.reduce_scatter(t.to(self.device)).cpu()
         k = t.shape[0] // self.world_size
         out = torch.empty((k,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.reduce_scatter_tensor(out, t.contiguous(), group=self.group)
@@ -287,6 +313,11 @@ class TorchComm(Comm):
 
     def broadcast(self, t, src=0):
         if self.world_size > 1:
+            if self._host(t):
+                d = t.to(self.device)
+                dist.broadcast(d, src=src, group=self.group)
+                t.copy_(d.cpu())
+                return t
             dist.broadcast(t, src=src, group=self.group)
         return t
 
@@ -296,6 +327,11 @@ class TorchComm(Comm):
         counts = torch.tensor(list(send_counts), dtype=torch.int64)
         all_counts = self.all_gather_object(counts.tolist())
         recv_counts = [all_counts[r][self.rank] for r in range(self.world_size)]
+        if self._host(send):
+            out = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype, device=self.device)
+            dist.all_to_all_single(out, send.to(self.device).contiguous(), output_split_sizes=recv_counts,
+                                   input_split_sizes=list(map(int, send_counts)), group=self.group)
+            return out.cpu(), recv_counts
         out = torch.empty((sum(recv_counts),) + tuple(send.shape[1:]), dtype=send.dtype, device=send.device)
         dist.all_to_all_single(out, send.contiguous(), output_split_sizes=recv_counts,
                                input_split_sizes=list(map(int, send_counts)), group=self.group)

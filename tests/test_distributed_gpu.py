@@ -123,3 +123,75 @@ def test_gpu_world2_matches_world1(tmp_path):
             assert x.shape == y.shape
             # fp32 kernels on the same factor rows; only YtY's fp64 partial sums differ by shard
             assert np.abs(x - y).max() <= 1e-4 * max(1.0, np.abs(x).max()), (imp, float(np.abs(x - y).max()))
+
+
+def _host_tensor_work(rank, world, port, out_dir, strict):
+    """Every tensor collective of a GPU session's TorchComm fed HOST tensors: RCCL takes
+    device tensors only, so the comm stages them through the device and hands the result
+    back on the host (gloo here, which would accept either, runs the same staging code)."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), O3S_DIST_BACKEND="gloo")
+    import json
+    import torch.distributed as dist
+    from orange3_spark_amd.parallel import comm as C
+    C.COMM_STRICT = strict
+    comm = C.TorchComm(torch.device("cuda:0"))
+    res = {}
+    if strict:
+        try:
+            comm.all_reduce(torch.ones(2))
+            res["raised"] = False
+        except Exception as e:                                   # noqa: BLE001 -- the comm wraps it
+            res["raised"] = "host tensor" in str(e)
+    else:
+        t = torch.full((3,), float(rank + 1))
+        comm.all_reduce(t)
+        res["all_reduce"] = (t.device.type, t.tolist())
+        g = comm.all_gather(torch.tensor([rank]))
+        res["all_gather"] = (g.device.type, g.tolist())
+        gv = comm.all_gather_v(torch.arange(rank + 1))
+        res["all_gather_v"] = (gv.device.type, gv.tolist())
+        b = torch.tensor([rank + 5.0])
+        comm.broadcast(b, 0)
+        res["broadcast"] = (b.device.type, b.tolist())
+        rs = comm.reduce_scatter(torch.ones(4) * (rank + 1))
+        res["reduce_scatter"] = (rs.device.type, rs.tolist())
+        recv, cnt = comm.all_to_all_v(torch.tensor([10 * rank, 10 * rank + 1]), [1, 1])
+        res["all_to_all_v"] = (recv.device.type, recv.tolist(), cnt)
+        out = torch.empty(2, dtype=torch.int64)
+        comm.all_gather_into(out, torch.tensor([rank]))
+        res["all_gather_into"] = (out.device.type, out.tolist())
+        d = torch.full((2,), float(rank), device="cuda:0")         # device tensors: unchanged path
+        comm.all_reduce(d)
+        res["device"] = (d.device.type, d.tolist())
+    with open(os.path.join(out_dir, f"host{int(strict)}_{rank}.json"), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("strict", [False, True])
+def test_gpu_collectives_stage_host_tensors(tmp_path, strict):
+    import json
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_host_tensor_work, args=(r, 2, port, str(tmp_path), strict)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(200)
+        assert p.exitcode == 0
+    for r in range(2):
+        res = json.load(open(tmp_path / f"host{int(strict)}_{r}.json"))
+        if strict:
+            assert res["raised"] is True
+            continue
+        assert res["all_reduce"] == ["cpu", [3.0, 3.0, 3.0]]
+        assert res["all_gather"] == ["cpu", [0, 1]]
+        assert res["all_gather_v"] == ["cpu", [0, 0, 1]]
+        assert res["broadcast"] == ["cpu", [5.0]]
+        assert res["reduce_scatter"] == ["cpu", [3.0, 3.0]]
+        assert res["all_to_all_v"] == ["cpu", [r, 10 + r], [1, 1]]
+        assert res["all_gather_into"] == ["cpu", [0, 1]]
+        assert res["device"] == ["cuda", [1.0, 1.0]]
